@@ -1,0 +1,210 @@
+/*
+ * sydelta.h — C ABI of the MI355X-native delta hot path (libsydelta.so).
+ *
+ * Drop-in boundary for nijaru/sy v0.0.43 `src/delta` (the re-exports at
+ * src/delta/mod.rs:9-16 plus calculate_block_size at mod.rs:20-23).  Every
+ * entry point names the reference interface it replaces; INTEGRATION.md shows
+ * the Rust `extern "C"` block and the safe wrappers a maintainer adds to sy.
+ *
+ * Conventions
+ *  - Plain pointers and sizes only; no torch / HIP types in signatures.  A
+ *    `void *stream` is a hipStream_t (NULL = the library's own per-call stream).
+ *  - Return value: SYDELTA_OK (0) or a negative SYDELTA_E_* code; the message
+ *    of the last failure on the calling thread is sydelta_last_error().  This
+ *    mirrors the reference's io::Result: I/O failures -> SYDELTA_E_IO
+ *    (File::open/read errors propagated by `?`, checksum.rs:50-59,
+ *    generator.rs:83-84); no panics on data.
+ *  - Re-entrant: callers are tokio spawn_blocking threads (ssh.rs:913), up to
+ *    --parallel (default 10) at once (sync/mod.rs:673).  Device init is
+ *    call_once per device; every call uses its own stream and buffers.
+ *  - Data layout in HBM: byte buffers as given; signatures as SoA
+ *    (weak u32[n], strong u64[n]).  Device buffers passed in must be readable
+ *    up to the end of the 16-byte granule holding their last byte (true for
+ *    hipMalloc and the torch caching allocator).
+ *  - Semantics are bit-exact with the reference for block_size in
+ *    [1, 131072] (the production domain, mod.rs:22).  Above 128 KiB the
+ *    reference's streaming generator diverges from its own in-memory one
+ *    (SURVEY.md App. A R10); the streaming entry rejects such sizes with
+ *    SYDELTA_E_INVAL, the in-memory entry follows generate_delta.
+ */
+#ifndef SYDELTA_H
+#define SYDELTA_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define SYDELTA_ABI_VERSION 1
+
+enum {
+    SYDELTA_OK = 0,
+    SYDELTA_E_NODEV = -1,  /* no usable gfx950 device / HIP runtime error at init */
+    SYDELTA_E_OOM = -2,    /* device or host allocation failed */
+    SYDELTA_E_INVAL = -3,  /* bad argument (block_size 0, NULL pointer, ...) */
+    SYDELTA_E_KERNEL = -4, /* kernel launch / execution error */
+    SYDELTA_E_IO = -5      /* file open/read/write error (path-level API) */
+};
+
+/* checksum.rs:9-21 `struct BlockChecksum {index, offset, size, weak, strong}` */
+typedef struct sydelta_block_checksum {
+    uint64_t index;
+    uint64_t offset;
+    uint64_t size;
+    uint32_t weak;
+    uint32_t reserved; /* zero */
+    uint64_t strong;
+} sydelta_block_checksum;
+
+/* generator.rs:10-15 `enum DeltaOp { Copy{offset,size}, Data(Vec<u8>) }`
+ *   kind = SYDELTA_OP_COPY: a = basis offset, b = size (from the matched checksum)
+ *   kind = SYDELTA_OP_DATA: a = offset of the literal run in the source, b = length;
+ *          the bytes are source[a .. a+b) (every reference literal run is a
+ *          contiguous source slice: literal_buffer is flushed at each Copy). */
+enum { SYDELTA_OP_COPY = 0, SYDELTA_OP_DATA = 1 };
+typedef struct sydelta_op {
+    uint32_t kind;
+    uint32_t reserved;
+    uint64_t a;
+    uint64_t b;
+} sydelta_op;
+
+/* Observability counters (SURVEY.md §5 Metrics): per match call. */
+typedef struct sydelta_match_stats {
+    uint64_t positions;      /* full-window positions scanned (len - bs + 1) */
+    uint64_t weak_hits;      /* positions whose weak hash has candidates (strong hashed) */
+    uint64_t verified_hits;  /* positions whose (weak, strong) matched a block */
+    uint64_t copy_ops;
+    uint64_t data_ops;
+    uint64_t literal_bytes;
+} sydelta_match_stats;
+
+typedef struct sydelta_index sydelta_index; /* device-resident probe table built from a signature */
+typedef struct sydelta_delta sydelta_delta; /* result of a match: op list (host memory) */
+
+int sydelta_abi_version(void);
+const char *sydelta_last_error(void);
+/* Number of visible HIP devices (0 without a GPU; never initialises a device). */
+int sydelta_device_count(int *count);
+
+/* mod.rs:20-23 `calculate_block_size(file_size) -> usize`: sqrt clamped to 512..=131072. */
+uint64_t sydelta_calculate_block_size(uint64_t file_size);
+
+/* ---------------------------------------------------------------------------
+ * Device-resident core.  Buffers live in HBM; results are bit-exact with the
+ * reference on the same bytes.
+ * ------------------------------------------------------------------------- */
+
+/* Signature of a device buffer: compute_checksums' per-block loop
+ * (checksum.rs:46-76): ceil(len/bs) blocks, block i = [i*bs, min(len,(i+1)*bs)),
+ * weak = Adler32::hash (rolling.rs:71-81), strong = XXH3-64 seed 0
+ * (checksum.rs:65-67).  d_weak / d_strong are device arrays of ceil(len/bs). */
+int sydelta_signature_device(int device, const uint8_t *d_buf, uint64_t len, uint64_t block_size,
+                             uint32_t *d_weak, uint64_t *d_strong, void *stream);
+
+/* Build the probe table for a basis signature: the candidate map
+ * `HashMap<u32, Vec<&BlockChecksum>>` of generator.rs:75-81 (candidates in index
+ * order).  weak/strong hold nblocks entries (device pointers if
+ * arrays_on_device, else host).  Block i has offset i*block_size and size
+ * block_size except the last, whose size is last_size (1..block_size). */
+int sydelta_index_create(int device, const uint32_t *weak, const uint64_t *strong, uint64_t nblocks,
+                         uint64_t block_size, uint64_t last_size, int arrays_on_device, void *stream,
+                         sydelta_index **out);
+void sydelta_index_free(sydelta_index *idx);
+
+/* Rolling match of a device-resident source against the index: the greedy
+ * scan of generate_delta (generator.rs:242-379; equal to
+ * generate_delta_streaming, :67-228, for block_size <= 128 KiB).  The op list
+ * is returned in host memory.  len may be 0 (no ops). */
+int sydelta_match_device(sydelta_index *idx, const uint8_t *d_src, uint64_t len, void *stream,
+                         sydelta_delta **out);
+
+uint64_t sydelta_delta_num_ops(const sydelta_delta *d);
+const sydelta_op *sydelta_delta_ops(const sydelta_delta *d);
+uint64_t sydelta_delta_source_size(const sydelta_delta *d); /* Delta::source_size (generator.rs:22) */
+uint64_t sydelta_delta_block_size(const sydelta_delta *d);  /* Delta::block_size (generator.rs:24) */
+/* Literal bytes of op i when the delta was produced from host data (buffer or
+ * path entry points); NULL for Copy ops or device-only sources. */
+const uint8_t *sydelta_delta_literal(const sydelta_delta *d, uint64_t op_index);
+int sydelta_delta_stats(const sydelta_delta *d, sydelta_match_stats *out);
+/* Delta::compression_ratio (generator.rs:30-55). */
+double sydelta_delta_compression_ratio(const sydelta_delta *d);
+void sydelta_delta_free(sydelta_delta *d);
+
+/* ---------------------------------------------------------------------------
+ * Host-buffer entry points (pinned staging + H2D inside).
+ * ------------------------------------------------------------------------- */
+
+/* compute_checksums on an in-memory file image (checksum.rs:31-80).
+ * out must hold ceil(len/bs) entries; *n_out receives the count. */
+int sydelta_compute_checksums_buf(int device, const uint8_t *buf, uint64_t len, uint64_t block_size,
+                                  sydelta_block_checksum *out, uint64_t cap, uint64_t *n_out);
+/* generate_delta on an in-memory source (generator.rs:242-379).  sigs as
+ * produced by compute_checksums (index order, offset = index*block_size). */
+int sydelta_generate_delta_buf(int device, const uint8_t *src, uint64_t len, const sydelta_block_checksum *sigs,
+                               uint64_t nsigs, uint64_t block_size, sydelta_delta **out);
+
+/* ---------------------------------------------------------------------------
+ * Path-level mirror of src/delta's public API (file I/O on the host).
+ * ------------------------------------------------------------------------- */
+
+/* checksum.rs:31 `compute_checksums(path: &Path, block_size: usize) -> io::Result<Vec<BlockChecksum>>`.
+ * *out is allocated by the library (free with sydelta_checksums_free); empty
+ * file -> *n = 0 (checksum.rs:36-38). */
+int sydelta_compute_checksums(const char *path, uint64_t block_size, sydelta_block_checksum **out, uint64_t *n);
+void sydelta_checksums_free(sydelta_block_checksum *p);
+
+/* generator.rs:67 `generate_delta_streaming(source_path, dest_checksums, block_size) -> io::Result<Delta>`. */
+int sydelta_generate_delta_streaming(const char *source_path, const sydelta_block_checksum *sigs, uint64_t nsigs,
+                                     uint64_t block_size, sydelta_delta **out);
+/* generator.rs:242 `generate_delta(source_path, dest_checksums, block_size) -> io::Result<Delta>`. */
+int sydelta_generate_delta(const char *source_path, const sydelta_block_checksum *sigs, uint64_t nsigs,
+                           uint64_t block_size, sydelta_delta **out);
+
+/* applier.rs:22 `apply_delta(old_file, delta, new_file) -> io::Result<DeltaStats>`
+ * (receiver side; host file I/O, no device work).  The delta must carry its
+ * literal bytes (produced by a host-data entry point).  DeltaStats fields:
+ * applier.rs:9-13. */
+typedef struct sydelta_apply_stats {
+    uint64_t operations_count;
+    uint64_t literal_bytes;
+    uint64_t bytes_written;
+} sydelta_apply_stats;
+int sydelta_apply_delta(const char *old_file, const sydelta_delta *d, const char *new_file, sydelta_apply_stats *out);
+
+/* rolling.rs:71-81 `Adler32::hash` (host utility for the re-exported Adler32 type). */
+uint32_t sydelta_adler32_hash(const uint8_t *data, uint64_t len);
+
+/* ---------------------------------------------------------------------------
+ * Batched (many independent files, BASELINE config 4).  Segment table:
+ * file f occupies d_buf[off[f] .. off[f]+len[f]); all files share block_size.
+ * Signature output for file f starts at entry sig_off[f] (= sum of
+ * ceil(len/bs) over earlier files).
+ * ------------------------------------------------------------------------- */
+int sydelta_signature_batch_device(int device, const uint8_t *d_buf, const uint64_t *off, const uint64_t *len,
+                                   uint64_t nfiles, uint64_t block_size, uint32_t *d_weak, uint64_t *d_strong,
+                                   void *stream);
+
+/* ---------------------------------------------------------------------------
+ * Measurement support (used by bench.py; not part of the reference API).
+ * ------------------------------------------------------------------------- */
+/* When on, the library records a HIP event pair around every kernel it
+ * launches (on the stream it launches on) and accumulates per-kernel time. */
+void sydelta_set_profiling(int on);
+/* JSON object {"kernel": {"ms": total, "count": n}, ...}; returns bytes written
+ * (excluding NUL) or the size needed if cap is too small. Clears with reset. */
+size_t sydelta_profile_json(char *buf, size_t cap, int reset);
+/* Deterministic synthetic bytes on the device: counter-based splitmix64 of
+ * (seed, 8-byte word index), little endian (oracle.synth_bytes). */
+int sydelta_synth_fill(uint8_t *d_buf, uint64_t len, uint64_t seed, void *stream);
+/* d_dst = d_src with each byte independently replaced, with probability
+ * rate_ppm / 1e6, by a different uniform byte (BASELINE config 3). */
+int sydelta_synth_mutate(uint8_t *d_dst, const uint8_t *d_src, uint64_t len, uint64_t seed, uint32_t rate_ppm,
+                         void *stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* SYDELTA_H */

@@ -1,0 +1,58 @@
+"""Build libsydelta.so (gfx950 HIP kernels + C ABI) in-tree.
+
+    python -m sy_amd.build            # incremental
+    python -m sy_amd.build --force
+"""
+from __future__ import annotations
+
+import os
+import subprocess
+import sys
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(HERE)
+CSRC = os.path.join(HERE, "csrc")
+LIB = os.path.join(HERE, "libsydelta.so")
+SOURCES = ["sydelta_kernels.hip", "sydelta_api.cpp"]
+HEADERS = ["sydelta_device.hpp", "sydelta_internal.hpp", os.path.join("..", "..", "include", "sydelta.h")]
+ARCH = os.environ.get("SYDELTA_ARCH", "gfx950")
+
+
+def _stale() -> bool:
+    if not os.path.exists(LIB):
+        return True
+    t = os.path.getmtime(LIB)
+    return any(os.path.getmtime(os.path.join(CSRC, f)) > t for f in SOURCES + HEADERS)
+
+
+def build(force: bool = False, verbose: bool = False) -> str:
+    if not force and not _stale():
+        return LIB
+    hipcc = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
+    objs = []
+    jobs = []
+    for src in SOURCES:
+        obj = os.path.join(CSRC, src.rsplit(".", 1)[0] + ".o")
+        cmd = [hipcc, f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-Wall", "-Wno-unused-result",
+               "-I", os.path.join(ROOT, "include"), "-x", "hip", "-c", os.path.join(CSRC, src), "-o", obj]
+        objs.append(obj)
+        jobs.append(subprocess.Popen(cmd, stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True))
+    for j in jobs:
+        out, _ = j.communicate()
+        if j.returncode != 0:
+            raise RuntimeError(f"hipcc failed:\n{out}")
+        if verbose and out:
+            print(out)
+    tmp = LIB + ".tmp"
+    link = [hipcc, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", tmp] + objs
+    r = subprocess.run(link, stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True)
+    if r.returncode != 0:
+        raise RuntimeError(f"link failed:\n{r.stdout}")
+    os.replace(tmp, LIB)
+    for o in objs:
+        os.remove(o)
+    return LIB
+
+
+if __name__ == "__main__":
+    print(build(force="--force" in sys.argv, verbose=True))

@@ -1,0 +1,140 @@
+"""Device-resident entry points (HBM buffers held by torch tensors).
+
+torch is plumbing here: it owns the device memory and the stream; every
+computation is a libsydelta.so kernel.  Used by bench.py and the GPU tests.
+"""
+from __future__ import annotations
+
+import ctypes
+from dataclasses import dataclass
+
+import numpy as np
+import torch
+
+from . import _lib
+from ._lib import check, lib
+
+
+def _stream(stream=None) -> int:
+    s = stream if stream is not None else torch.cuda.current_stream()
+    return int(s.cuda_stream)
+
+
+def _ptr(t: torch.Tensor) -> int:
+    assert t.is_cuda and t.is_contiguous()
+    return t.data_ptr()
+
+
+def signature(buf: torch.Tensor, block_size: int, stream=None):
+    """compute_checksums' per-block loop on a device buffer -> (weak int32[n], strong int64[n])
+    (bit patterns of u32 / u64)."""
+    assert buf.dtype == torch.uint8
+    n = buf.numel()
+    nb = -(-n // block_size) if n else 0
+    weak = torch.empty(max(nb, 1), dtype=torch.int32, device=buf.device)
+    strong = torch.empty(max(nb, 1), dtype=torch.int64, device=buf.device)
+    check(lib.sydelta_signature_device(buf.device.index or 0, _ptr(buf) if n else None, n, block_size,
+                                       _ptr(weak), _ptr(strong), _stream(stream)))
+    return weak[:nb], strong[:nb]
+
+
+def signature_batch(buf: torch.Tensor, offs, lens, block_size: int, stream=None):
+    """Batched signature over many files packed in one device buffer."""
+    offs = np.ascontiguousarray(offs, dtype=np.uint64)
+    lens = np.ascontiguousarray(lens, dtype=np.uint64)
+    total = int(sum(-(-int(l) // block_size) for l in lens))
+    weak = torch.empty(max(total, 1), dtype=torch.int32, device=buf.device)
+    strong = torch.empty(max(total, 1), dtype=torch.int64, device=buf.device)
+    check(lib.sydelta_signature_batch_device(buf.device.index or 0, _ptr(buf), offs.ctypes.data, lens.ctypes.data,
+                                             len(lens), block_size, _ptr(weak), _ptr(strong), _stream(stream)))
+    return weak[:total], strong[:total]
+
+
+class Index:
+    """Device probe table for a basis signature (generator.rs:75-81)."""
+
+    def __init__(self, weak, strong, block_size: int, last_size: int, device: int = 0, stream=None):
+        self.h = ctypes.c_void_p()
+        n = int(weak.numel()) if isinstance(weak, torch.Tensor) else len(weak)
+        self.nblocks, self.block_size, self.last_size = n, block_size, last_size
+        if isinstance(weak, torch.Tensor) and weak.is_cuda:
+            check(lib.sydelta_index_create(device, _ptr(weak) if n else None, _ptr(strong) if n else None, n,
+                                           block_size, last_size, 1, _stream(stream), ctypes.byref(self.h)))
+        else:
+            w = np.ascontiguousarray(np.asarray(weak, dtype=np.uint64).astype(np.uint32))
+            s = np.ascontiguousarray(np.asarray(strong, dtype=np.uint64))
+            check(lib.sydelta_index_create(device, w.ctypes.data if n else None, s.ctypes.data if n else None, n,
+                                           block_size, last_size, 0, None, ctypes.byref(self.h)))
+
+    def close(self):
+        if self.h:
+            lib.sydelta_index_free(self.h)
+            self.h = ctypes.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+@dataclass
+class DeviceDelta:
+    kind: np.ndarray   # 0 Copy, 1 Data
+    a: np.ndarray      # Copy: basis offset; Data: source offset
+    b: np.ndarray      # size / length
+    source_size: int
+    block_size: int
+    stats: dict
+
+    def tuples(self):
+        return [("C" if int(k) == 0 else "D", int(x), int(y)) for k, x, y in zip(self.kind, self.a, self.b)]
+
+
+def match(index: Index, src: torch.Tensor, stream=None, length: int | None = None) -> DeviceDelta:
+    """Greedy rolling match of a device-resident source (generator.rs:242-379)."""
+    n = src.numel() if length is None else length
+    h = ctypes.c_void_p()
+    check(lib.sydelta_match_device(index.h, _ptr(src) if n else None, n, _stream(stream), ctypes.byref(h)))
+    try:
+        nops = int(lib.sydelta_delta_num_ops(h))
+        if nops:
+            p = lib.sydelta_delta_ops(h)
+            raw = np.ctypeslib.as_array(ctypes.cast(p, ctypes.POINTER(ctypes.c_uint64)), shape=(nops * 3,)).copy()
+            raw = raw.reshape(nops, 3)
+            kind = (raw[:, 0] & 0xFFFFFFFF).astype(np.uint8)
+            a, b = raw[:, 1].copy(), raw[:, 2].copy()
+        else:
+            kind = np.zeros(0, np.uint8)
+            a = np.zeros(0, np.uint64)
+            b = np.zeros(0, np.uint64)
+        st = _lib.MatchStatsC()
+        check(lib.sydelta_delta_stats(h, ctypes.byref(st)))
+        stats = {f: int(getattr(st, f)) for f, _ in _lib.MatchStatsC._fields_}
+        return DeviceDelta(kind, a, b, int(lib.sydelta_delta_source_size(h)), int(lib.sydelta_delta_block_size(h)),
+                           stats)
+    finally:
+        lib.sydelta_delta_free(h)
+
+
+def synth_fill(buf: torch.Tensor, seed: int, stream=None) -> None:
+    check(lib.sydelta_synth_fill(_ptr(buf), buf.numel(), seed & 0xFFFFFFFFFFFFFFFF, _stream(stream)))
+
+
+def synth_mutate(dst: torch.Tensor, src: torch.Tensor, seed: int, rate_ppm: int, stream=None) -> None:
+    assert dst.numel() == src.numel()
+    check(lib.sydelta_synth_mutate(_ptr(dst), _ptr(src), src.numel(), seed & 0xFFFFFFFFFFFFFFFF, rate_ppm,
+                                   _stream(stream)))
+
+
+def set_profiling(on: bool) -> None:
+    lib.sydelta_set_profiling(1 if on else 0)
+
+
+def profile(reset: bool = False) -> dict:
+    import json
+
+    n = lib.sydelta_profile_json(None, 0, 0)
+    buf = ctypes.create_string_buffer(n + 1)
+    lib.sydelta_profile_json(buf, n + 1, 1 if reset else 0)
+    return json.loads(buf.value.decode())

@@ -1,0 +1,31 @@
+import os
+import sys
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+if ROOT not in sys.path:
+    sys.path.insert(0, ROOT)
+
+
+def pytest_configure(config):
+    config.addinivalue_line("markers", "gpu: needs a real MI355X (gfx950) GPU")
+    config.addinivalue_line("markers", "slow: long-running parity case")
+
+
+@pytest.fixture(scope="session")
+def oracle_c():
+    from oracle import oracle
+
+    return oracle.C()
+
+
+@pytest.fixture(scope="session")
+def gpu():
+    import torch
+
+    if not torch.cuda.is_available():
+        pytest.fail("GPU test selected but no HIP device is visible")
+    import sy_amd.device as dev  # raises if libsydelta.so is missing
+
+    return dev
