@@ -281,28 +281,29 @@ extern "C" int sydelta_index_create(int device, const uint32_t* weak, const uint
     x->nblocks = nblocks;
     x->bs = block_size;
     x->last_size = nblocks ? last_size : 0;
-    // sizes: filter ~16 bits/key (min 2^12 bits), table 2x keys (min 64 slots)
-    const uint32_t fbits = std::min<uint32_t>(31, std::max<uint32_t>(12, ceil_log2(nblocks ? nblocks : 1) + 4));
-    const uint32_t tbits = std::max<uint32_t>(6, ceil_log2(2 * (nblocks ? nblocks : 1)));
-    const size_t tslots = (size_t)1 << tbits;
+    // sizes: Bloom filter ~16 bits/key in 64-bit words (min 2^7 words); buckets of 4 keys at load <= 0.5
+    const uint64_t nk = nblocks ? nblocks : 1;
+    const uint32_t fwbits = std::min<uint32_t>(28, std::max<uint32_t>(7, ceil_log2(nk) - 2));
+    const uint32_t bbits = std::max<uint32_t>(4, ceil_log2((nk + 1) / 2));
+    const size_t nslots = ((size_t)1 << bbits) * 4;
     const size_t nb = std::max<uint64_t>(nblocks, 1);
     auto al = [](size_t v) { return (v + 255) & ~(size_t)255; };
-    const size_t sz_weak = al(4 * nb), sz_strong = al(8 * nb), sz_filt = al(((size_t)1 << fbits) / 8);
-    const size_t sz_t = al(4 * tslots), sz_order = al(4 * nb), sz_slot = al(4 * nb);
+    const size_t sz_weak = al(4 * nb), sz_strong = al(8 * nb), sz_filt = al(((size_t)1 << fwbits) * 8);
+    const size_t sz_t = al(4 * nslots), sz_order = al(4 * nb), sz_slot = al(4 * nb);
     const size_t total = sz_weak + sz_strong + sz_filt + 4 * sz_t + sz_order + sz_slot;
     HIP_TRY(hipMalloc(&x->d_pool, total));
     uint8_t* p = (uint8_t*)x->d_pool;
     x->d_weak = (uint32_t*)p; p += sz_weak;
     x->d_strong = (uint64_t*)p; p += sz_strong;
-    x->ix.filt = (uint32_t*)p; p += sz_filt;
-    x->ix.fbits = fbits;
+    x->ix.filt = (unsigned long long*)p; p += sz_filt;
+    x->ix.fwbits = fwbits;
     x->ix.keys = (uint32_t*)p; p += sz_t;
     x->ix.cnt = (uint32_t*)p; p += sz_t;
     x->ix.start = (uint32_t*)p; p += sz_t;
     x->ix.fill = (uint32_t*)p; p += sz_t;
     x->ix.order = (uint32_t*)p; p += sz_order;
     x->ix.slot_of = (uint32_t*)p; p += sz_slot;
-    x->ix.tmask = (uint32_t)(tslots - 1);
+    x->ix.bmask = (uint32_t)((1u << bbits) - 1);
     const hipMemcpyKind kind = arrays_on_device ? hipMemcpyDeviceToDevice : hipMemcpyHostToDevice;
     if (nblocks) {
         HIP_TRY(hipMemcpyAsync(x->d_weak, weak, 4 * nblocks, kind, s));
@@ -442,35 +443,30 @@ static int match_impl(sydelta_index* ix, const uint8_t* d_src, uint64_t len, hip
         for (uint64_t seg = 0; seg < npos; seg += seg_max) {
             const uint64_t seg_end = std::min(npos, seg + seg_max);
             const uint64_t seg_pos = seg_end - seg;
-            uint64_t want = std::max<uint64_t>(1 << 16, seg_pos / 256 + (1 << 16));
+            // verified hits: at most one per position; start from ~4 per block of positions
+            uint64_t want = std::max<uint64_t>(1 << 16, seg_pos / n * 4 + (1 << 16));
             want = std::min<uint64_t>(want, seg_pos);
-            unsigned long long counts[2] = {0, 0};
+            unsigned long long counts[3] = {0, 0, 0};
             for (int attempt = 0; attempt < 2; ++attempt) {
                 if (want > cap) {
                     if (hit_buf.p) { (void)hipFreeAsync(hit_buf.p, s); hit_buf.p = nullptr; }
                     cap = want;
-                    // weak hits [cap] + verified [cap] + sort scratch [cap]
-                    HIP_TRY(hipMallocAsync(&hit_buf.p, 3 * cap * sizeof(HitRec), s));
+                    // verified hits [cap] + sort scratch [cap]
+                    HIP_TRY(hipMallocAsync(&hit_buf.p, 2 * cap * sizeof(HitRec), s));
                     hit_buf.s = s;
                 }
-                HIP_TRY(hipMemsetAsync(d_counts, 0, 16, s));
-                HIP_TRY(launch_scan(d_src, len, seg, seg_end, (uint32_t)n, ix->ix, (HitRec*)hit_buf.p, cap, d_counts,
-                                    s, prof));
-                HIP_TRY(hipMemcpyAsync(counts, d_counts, 8, hipMemcpyDeviceToHost, s));
+                HIP_TRY(hipMemsetAsync(d_counts, 0, 32, s));
+                HIP_TRY(launch_scan(d_src, len, seg, seg_end, (uint32_t)n, ix->ix, ix->d_strong, (HitRec*)hit_buf.p,
+                                    cap, d_counts, s, prof));
+                HIP_TRY(hipMemcpyAsync(counts, d_counts, 24, hipMemcpyDeviceToHost, s));
                 HIP_TRY(hipStreamSynchronize(s));
                 if (counts[0] <= cap) break;
-                want = counts[0];  // dense weak hits: grow once and rescan
+                want = counts[0];  // dense hits: grow once and rescan
             }
-            const uint64_t nweak = counts[0];
-            d->stats.weak_hits += nweak;
-            HitRec* d_weak_hits = (HitRec*)hit_buf.p;
-            HitRec* d_ver = d_weak_hits + cap;
+            d->stats.weak_hits += counts[1];
+            HitRec* d_ver = (HitRec*)hit_buf.p;
             HitRec* d_sort = d_ver + cap;
-            HIP_TRY(launch_verify(d_src, seg, (uint32_t)n, d_weak_hits, nweak, ix->ix, ix->d_strong, d_ver,
-                                  d_counts + 1, s, prof));
-            HIP_TRY(hipMemcpyAsync(&counts[1], d_counts + 1, 8, hipMemcpyDeviceToHost, s));
-            HIP_TRY(hipStreamSynchronize(s));
-            const uint64_t nver = counts[1];
+            const uint64_t nver = counts[0];
             d->stats.verified_hits += nver;
             if (nver) {
                 HitRec* sorted = nullptr;

@@ -22,15 +22,15 @@ static_assert(sizeof(HitRec) == 8, "HitRec must be 8 bytes");
 
 // Device-resident probe table over a basis signature (SoA in HBM).
 struct DeviceIndex {
-    uint32_t* filt = nullptr;   // 2^fbits-bit filter over weak values
-    uint32_t fbits = 0;
-    uint32_t* keys = nullptr;   // open addressing, unique weak values, kEmptyKey = free
+    unsigned long long* filt = nullptr;  // blocked Bloom filter: 2^fwbits 64-bit words
+    uint32_t fwbits = 0;
+    uint32_t* keys = nullptr;   // 4-key buckets of unique weak values, kEmptyKey = free
     uint32_t* cnt = nullptr;    // candidates per slot
     uint32_t* start = nullptr;  // exclusive prefix of cnt
     uint32_t* fill = nullptr;   // scratch for the scatter
     uint32_t* order = nullptr;  // block indices grouped by slot
     uint32_t* slot_of = nullptr;
-    uint32_t tmask = 0;
+    uint32_t bmask = 0;         // buckets - 1
 };
 
 // Per-kernel HIP-event timing (enabled by sydelta_set_profiling).
@@ -57,11 +57,8 @@ hipError_t launch_index_build(const uint32_t* d_weak, uint64_t n, DeviceIndex& i
 size_t scan_lds_bytes(uint32_t n, uint32_t* nchunks_out);
 uint64_t scan_tile_positions();
 hipError_t launch_scan(const uint8_t* d_src, uint64_t len, uint64_t pos_begin, uint64_t pos_end, uint32_t n,
-                       const DeviceIndex& ix, HitRec* d_hits, uint64_t hit_cap, unsigned long long* d_count,
-                       hipStream_t s, Profiler* prof);
-hipError_t launch_verify(const uint8_t* d_src, uint64_t pos_begin, uint32_t n, const HitRec* d_hits, uint64_t nhits,
-                         const DeviceIndex& ix, const uint64_t* d_strong, HitRec* d_out,
-                         unsigned long long* d_out_count, hipStream_t s, Profiler* prof);
+                       const DeviceIndex& ix, const uint64_t* d_strong, HitRec* d_out, uint64_t out_cap,
+                       unsigned long long* d_counters, hipStream_t s, Profiler* prof);
 hipError_t launch_sort_hits(HitRec* d_in, HitRec* d_tmp_out, uint64_t nhits, hipStream_t s, HitRec** sorted);
 hipError_t launch_tail(const uint8_t* d_src, uint64_t len, uint64_t last_size, uint32_t want_weak, uint64_t want_strong,
                        int* d_flag, hipStream_t s);

@@ -156,35 +156,59 @@ __global__ __launch_bounds__(256) void k_sig_batch(const uint8_t* __restrict__ b
 }
 
 // ===========================================================================
-// K3: index (probe table) over basis weak values
+// K3: index (probe structure) over basis weak values
 // ===========================================================================
-__device__ __forceinline__ uint32_t filt_hash(uint32_t w) {
-    // multiplicative hash of the packed weak value; top bits index the filter
-    return w * 0x9E3779B1u;
+// Blocked Bloom filter: one 64-bit word per key, 4 bits set, ~16 bits/key
+// (FP ~0.6% on Adler values of random blocks; sized to stay L2-resident at 1 Mi
+// keys).  Exact set: bucketised open addressing, 4 keys per 16-byte bucket,
+// load <= 0.5, so a lookup is almost always one dwordx4 load.  Hash inputs are
+// the two 16-bit Adler halves (A = weak & 0xFFFF, B = weak >> 16), mixed with
+// 24-bit multiplies (full-rate v_mad_u32_u24).
+struct BloomProbe {
+    uint32_t word;
+    uint32_t bits;  // four 6-bit bit positions
+};
+__device__ __forceinline__ uint64_t bloom_mask(uint32_t bits) {
+    return (1ull << (bits & 63)) | (1ull << ((bits >> 6) & 63)) | (1ull << ((bits >> 12) & 63)) |
+           (1ull << ((bits >> 18) & 63));
 }
-__device__ __forceinline__ uint32_t slot_hash(uint32_t w) {
+__device__ __forceinline__ BloomProbe bloom_of(uint32_t am, uint32_t bm, uint32_t fwshift) {
+    const uint32_t h1 = am * 0x2F0B35u + bm * 0x9E3779u;
+    const uint32_t g = am * 0x6B43A9u + bm * 0x1B8735u;
+    const uint32_t g2 = am * 0x1F3D5Bu + bm * 0x5A17C3u;
+    BloomProbe p;
+    p.word = h1 >> fwshift;
+    p.bits = (g >> 26) | (((g >> 20) & 63) << 6) | ((g2 >> 26) << 12) | (((g2 >> 20) & 63) << 18);
+    return p;
+}
+__device__ __forceinline__ uint32_t bucket_hash(uint32_t w) {
     uint32_t h = w ^ (w >> 15);
     h *= 0x2C1B3C6Du;
     h ^= h >> 12;
     return h;
 }
 
-__global__ void k_idx_insert(const uint32_t* __restrict__ weak, uint64_t n, uint32_t* __restrict__ filt,
-                             uint32_t fshift, uint32_t* __restrict__ keys, uint32_t* __restrict__ cnt,
-                             uint32_t tmask, uint32_t* __restrict__ slot_of) {
+__global__ void k_idx_insert(const uint32_t* __restrict__ weak, uint64_t n, unsigned long long* __restrict__ filt,
+                             uint32_t fwshift, uint32_t* __restrict__ keys, uint32_t* __restrict__ cnt,
+                             uint32_t bmask, uint32_t* __restrict__ slot_of) {
     const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
     const uint32_t w = weak[i];
-    const uint32_t fh = filt_hash(w) >> fshift;
-    atomicOr(&filt[fh >> 5], 1u << (fh & 31));
-    uint32_t s = slot_hash(w) & tmask;
+    const BloomProbe bp = bloom_of(w & 0xFFFF, w >> 16, fwshift);
+    atomicOr(&filt[bp.word], (unsigned long long)bloom_mask(bp.bits));
+    uint32_t b = bucket_hash(w) & bmask;
     for (;;) {
-        const uint32_t old = atomicCAS(&keys[s], kEmptyKey, w);
-        if (old == kEmptyKey || old == w) break;
-        s = (s + 1) & tmask;
+        for (uint32_t j = 0; j < 4; ++j) {
+            const uint32_t s = 4 * b + j;
+            const uint32_t old = atomicCAS(&keys[s], kEmptyKey, w);
+            if (old == kEmptyKey || old == w) {
+                atomicAdd(&cnt[s], 1u);
+                slot_of[i] = s;
+                return;
+            }
+        }
+        b = (b + 1) & bmask;
     }
-    atomicAdd(&cnt[s], 1u);
-    slot_of[i] = s;
 }
 
 __global__ void k_idx_scatter(uint64_t n, const uint32_t* __restrict__ slot_of, const uint32_t* __restrict__ start,
@@ -196,18 +220,22 @@ __global__ void k_idx_scatter(uint64_t n, const uint32_t* __restrict__ slot_of, 
     order[start[s] + k] = (uint32_t)i;
 }
 
-__device__ __forceinline__ int64_t table_find(const uint32_t* __restrict__ keys, uint32_t tmask, uint32_t w) {
-    uint32_t s = slot_hash(w) & tmask;
+// Exact lookup: slot of weak value w, or -1.
+__device__ __forceinline__ int64_t table_find(const uint32_t* __restrict__ keys, uint32_t bmask, uint32_t w) {
+    uint32_t b = bucket_hash(w) & bmask;
     for (;;) {
-        const uint32_t k = keys[s];
-        if (k == w) return s;
-        if (k == kEmptyKey) return -1;
-        s = (s + 1) & tmask;
+        const uint4 k = *(const uint4*)(keys + 4 * b);
+        if (k.x == w) return 4 * b;
+        if (k.y == w) return 4 * b + 1;
+        if (k.z == w) return 4 * b + 2;
+        if (k.w == w) return 4 * b + 3;
+        if (k.w == kEmptyKey) return -1;  // buckets fill in order: a free last slot ends the chain
+        b = (b + 1) & bmask;
     }
 }
 
 // ===========================================================================
-// K2: rolling scan
+// K2+K4: rolling scan with in-kernel verification
 // ===========================================================================
 // Tile = kScanThreads threads x kScanRun positions.  Thread k rolls positions
 // [p0, p0+kScanRun), p0 = tile_start + k*kScanRun.  The initial window of every
@@ -217,10 +245,19 @@ __device__ __forceinline__ int64_t table_find(const uint32_t* __restrict__ keys,
 //   a_ex += in - out;  A = a_ex mod M
 //   B'   = B + a_ex + nm*(255-out) + C0  (mod M),  nm = n mod M, C0 = 2M-1-(255 nm mod M)
 // which is congruent to B - n*out + A' - 1.
+// Per position the Bloom word is loaded (kBatch loads in flight per lane);
+// positions that pass go to a per-wave LDS queue (fq).  Draining fq does the
+// exact table lookups 64 at a time; weak hits (generator.rs:124 `get(&weak)` is
+// Some) go to a second per-wave queue (wq).  Draining wq verifies each weak hit
+// with a wave-cooperative XXH3 of its window (the bytes were just streamed by
+// this workgroup, so they come from L2) and the first candidate in index order
+// with equal strong (generator.rs:127-153) becomes a verified hit.
 constexpr int kScanThreads = 256;
 constexpr int kScanRun = 256;                         // positions per thread
 constexpr int kScanTile = kScanThreads * kScanRun;    // 65536 positions per workgroup
-constexpr int kBatch = 16;                            // filter loads in flight per thread
+constexpr int kBatch = 16;                            // Bloom loads in flight per lane
+constexpr int kFQ = 64 * kBatch + 64;                 // filter-pass queue entries per wave
+constexpr int kWQ = 128;                              // weak-hit queue entries per wave
 
 struct ScanArgs {
     const uint8_t* src;
@@ -230,14 +267,18 @@ struct ScanArgs {
     uint32_t n;          // block size
     uint32_t nm;         // n mod M
     uint32_t c0;         // 2M - 1 - (255*nm mod M)
-    uint32_t fshift;     // 32 - filter bits
-    const uint32_t* filt;
+    uint32_t fwshift;    // 32 - log2(filter words)
+    const unsigned long long* filt;
     const uint32_t* keys;
-    uint32_t tmask;
+    uint32_t bmask;
     uint32_t nchunks;    // LDS chunk slots per tile
-    HitRec* hits;        // weak hits (unordered): rel pos + slot
-    uint64_t hit_cap;
-    unsigned long long* hit_count;
+    const uint32_t* start;
+    const uint32_t* cnt;
+    const uint32_t* order;
+    const uint64_t* strong;
+    HitRec* out;         // verified hits (unordered): rel pos + block index
+    uint64_t out_cap;
+    unsigned long long* counters;  // [0] verified hits, [1] weak hits, [2] filter passes
 };
 
 // 64-byte chunk [c0, c0+64) of src, bytes at or beyond len read as 0.
@@ -289,16 +330,92 @@ __device__ __forceinline__ void load64_at(const uint8_t* src, uint64_t len, uint
     for (int i = 0; i < 16; ++i) x[i] = __builtin_amdgcn_alignbyte(d[i + 1], d[i], sh);
 }
 
+__device__ __forceinline__ void lds_fence() { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); }
+
+// Verify every queued weak hit of this wave (wave-uniform loop).
+__device__ __forceinline__ void drain_wq(const ScanArgs& a, const uint2* wq, uint32_t nwq, uint64_t tile_start) {
+    const uint32_t lane = threadIdx.x & 63;
+    for (uint32_t i = 0; i < nwq; ++i) {
+        const uint2 e = wq[i];  // {rel pos in tile, table slot}
+        const uint64_t p = tile_start + e.x;
+        const uint8_t* win = a.src + p;
+        uint64_t st;
+        if (a.n > 240) {
+            uint32_t wk;
+            wave_hash_long(win, a.n, wk, st);
+        } else {
+            st = 0;
+            if (lane == 0) st = xxh3_short(win, a.n);
+            st = shfl64(st, 0);
+        }
+        const uint32_t s0 = a.start[e.y], c = a.cnt[e.y];
+        uint32_t best = 0xFFFFFFFFu;
+        for (uint32_t j = lane; j < c; j += 64) {
+            const uint32_t bi = a.order[s0 + j];
+            if (a.strong[bi] == st) best = min(best, bi);
+        }
+#pragma unroll
+        for (int m = 1; m < 64; m <<= 1) best = min(best, (uint32_t)__shfl_xor((int)best, m, 64));
+        if (lane == 0 && best != 0xFFFFFFFFu) {
+            const unsigned long long k = atomicAdd(&a.counters[0], 1ull);
+            if (k < a.out_cap) {
+                HitRec r;
+                r.pos = (uint32_t)(p - a.pos_begin);
+                r.slot = best;
+                a.out[k] = r;
+            }
+        }
+    }
+}
+
+// Exact lookups for the queued Bloom passes, 64 per round; weak hits go to wq.
+__device__ __forceinline__ uint32_t drain_fq(const ScanArgs& a, const uint2* fq, uint32_t nfq, uint2* wq, uint32_t nwq,
+                                          uint64_t tile_start) {
+    const uint32_t lane = threadIdx.x & 63;
+    for (uint32_t base = 0; base < nfq; base += 64) {
+        const uint32_t i = base + lane;
+        int64_t slot = -1;
+        uint2 e = make_uint2(0, 0);
+        if (i < nfq) {
+            e = fq[i];  // {rel pos in tile, packed weak}
+            slot = table_find(a.keys, a.bmask, e.y);
+        }
+        const bool hit = slot >= 0;
+        const uint64_t m = __ballot(hit);
+        const uint32_t cnt = __popcll(m);
+        if (cnt && lane == 0) atomicAdd(&a.counters[1], (unsigned long long)cnt);
+        if (cnt) {
+            if (nwq + cnt > (uint32_t)kWQ) {  // keep room: verify what is queued
+                lds_fence();
+                drain_wq(a, wq, nwq, tile_start);
+                nwq = 0;
+            }
+            if (hit) {
+                const uint32_t off = nwq + __popcll(m & ((1ull << lane) - 1));
+                wq[off] = make_uint2(e.x, (uint32_t)slot);
+            }
+            nwq += cnt;
+            lds_fence();
+        }
+    }
+    return nwq;
+}
+
 __global__ __launch_bounds__(kScanThreads) void k_scan(ScanArgs a) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     const uint32_t nch = a.nchunks;
     uint32_t* PS = (uint32_t*)smem;                 // nch+1 prefix of chunk byte sums
     uint32_t* PV = PS + (nch + 1);                  // nch+1 prefix of in-chunk weighted sums
-    uint64_t* PJ = (uint64_t*)(smem + (((size_t)(2 * (nch + 1)) * 4 + 15) & ~(size_t)15));  // prefix of c*S_c
+    const size_t pj_off = (((size_t)(2 * (nch + 1)) * 4 + 15) & ~(size_t)15);
+    uint64_t* PJ = (uint64_t*)(smem + pj_off);      // prefix of c*S_c
+    const size_t q_off = (pj_off + (size_t)(nch + 1) * 8 + 15) & ~(size_t)15;
+    const uint32_t tid = threadIdx.x;
+    const uint32_t lane = tid & 63, wid = tid >> 6;
+    uint2* fq = (uint2*)(smem + q_off) + (size_t)wid * (kFQ + kWQ);
+    uint2* wq = fq + kFQ;
     __shared__ uint32_t red_s[kScanThreads / 64], red_v[kScanThreads / 64];
     __shared__ uint64_t red_j[kScanThreads / 64];
 
-    const uint32_t tid = threadIdx.x;
     const uint64_t tile_start = a.pos_begin + (uint64_t)blockIdx.x * kScanTile;
     if (tile_start >= a.pos_end) return;
     const uint32_t n = a.n;
@@ -320,10 +437,8 @@ __global__ __launch_bounds__(kScanThreads) void k_scan(ScanArgs a) {
     uint32_t ts = 0, tv = 0;
     uint64_t tj = 0;
     for (uint32_t c = c_lo; c < c_hi; ++c) { ts += PS[c]; tv += PV[c]; tj += (uint64_t)c * PS[c]; }
-    // block exclusive scan of (ts, tv, tj)
     uint32_t is = ts, iv = tv;
     uint64_t ij = tj;
-    const uint32_t lane = tid & 63, wid = tid >> 6;
 #pragma unroll
     for (int m = 1; m < 64; m <<= 1) {
         const uint32_t os = (uint32_t)__shfl_up((int)is, m, 64);
@@ -339,7 +454,6 @@ __global__ __launch_bounds__(kScanThreads) void k_scan(ScanArgs a) {
     for (uint32_t w = 0; w < wid; ++w) { bs_ += red_s[w]; bv_ += red_v[w]; bj_ += red_j[w]; }
     uint32_t es = bs_ + is - ts, ev = bv_ + iv - tv;
     uint64_t ej = bj_ + ij - tj;
-    // rewrite own run as exclusive prefixes (values are consumed in order)
     for (uint32_t c = c_lo; c < c_hi; ++c) {
         const uint32_t s = PS[c], v = PV[c];
         PS[c] = es; PV[c] = ev; PJ[c] = ej;
@@ -350,44 +464,62 @@ __global__ __launch_bounds__(kScanThreads) void k_scan(ScanArgs a) {
 
     // ---- phase 3: initial window of this thread
     const uint64_t p0 = tile_start + (uint64_t)tid * kScanRun;
-    if (p0 >= a.pos_end) return;
     const uint32_t c0 = tid * (kScanRun / 64);
     const uint32_t m = n >> 6, rem = n & 63;
-    const uint64_t dS = PS[c0 + m] - PS[c0];
-    const uint64_t dV = PV[c0 + m] - PV[c0];
-    const uint64_t dJ = PJ[c0 + m] - PJ[c0];
-    uint64_t A = dS;
-    uint64_t B = (uint64_t)n * dS - 64ull * (dJ - (uint64_t)c0 * dS) - dV;
-    if (rem) {
-        uint32_t x[16];
-        load_chunk(a.src, a.len, p0 + 64ull * m, x);
-        for (uint32_t r = 0; r < rem; ++r) {
-            const uint32_t xb = (x[r >> 2] >> (8 * (r & 3))) & 0xFF;
-            A += xb;
-            B += (uint64_t)(rem - r) * xb;
+    uint32_t a_ex = 0, bm = 0;
+    const bool live = p0 < a.pos_end;
+    if (live) {
+        const uint64_t dS = PS[c0 + m] - PS[c0];
+        const uint64_t dV = PV[c0 + m] - PV[c0];
+        const uint64_t dJ = PJ[c0 + m] - PJ[c0];
+        uint64_t A = dS;
+        uint64_t B = (uint64_t)n * dS - 64ull * (dJ - (uint64_t)c0 * dS) - dV;
+        if (rem) {
+            uint32_t x[16];
+            load_chunk(a.src, a.len, p0 + 64ull * m, x);
+            for (uint32_t r = 0; r < rem; ++r) {
+                const uint32_t xb = (x[r >> 2] >> (8 * (r & 3))) & 0xFF;
+                A += xb;
+                B += (uint64_t)(rem - r) * xb;
+            }
         }
+        a_ex = (uint32_t)(1 + A);
+        bm = (uint32_t)((n + B) % kMod);
     }
-    uint32_t a_ex = (uint32_t)(1 + A);
-    uint32_t bm = (uint32_t)((n + B) % kMod);
     const uint32_t nm = a.nm, cc = a.c0;
-    const uint64_t pend = min(a.pos_end, p0 + (uint64_t)kScanRun);
+    const uint64_t pend = live ? min(a.pos_end, p0 + (uint64_t)kScanRun) : p0;
     const uint32_t npos = (uint32_t)(pend - p0);
+    const uint32_t rel0 = tid * kScanRun;  // position of p0 relative to the tile
+    // wave-uniform trip count so the queue ballots see every lane
+    uint32_t wave_npos = npos;
+#pragma unroll
+    for (int k = 1; k < 64; k <<= 1) wave_npos = max(wave_npos, (uint32_t)__shfl_xor((int)wave_npos, k, 64));
+    uint32_t nfq = 0, nwq = 0;
+    unsigned long long passes = 0;
 
     // ---- phase 4: roll
-    for (uint32_t g = 0; g < (uint32_t)kScanRun; g += 64) {
-        if (g >= npos) break;
+    for (uint32_t g = 0; g < wave_npos; g += 64) {
         uint32_t xo[16], xi[16];
-        load_chunk(a.src, a.len, p0 + g, xo);
-        load64_at(a.src, a.len, p0 + g + n, xi);
+        if (g < npos) {
+            load_chunk(a.src, a.len, p0 + g, xo);
+            load64_at(a.src, a.len, p0 + g + n, xi);
+        } else {
+#pragma unroll
+            for (int i = 0; i < 16; ++i) { xo[i] = 0; xi[i] = 0; }
+        }
 #pragma unroll
         for (int hb = 0; hb < 64; hb += kBatch) {
             uint32_t wv[kBatch];
-            uint32_t fw[kBatch];
+            uint64_t fw[kBatch];
+            uint32_t fb[kBatch];
 #pragma unroll
             for (int t = 0; t < kBatch; ++t) {
                 const int i = hb + t;
                 const uint32_t am = a_ex % kMod;
                 wv[t] = (bm << 16) | am;
+                const BloomProbe bp = bloom_of(am, bm, a.fwshift);
+                fw[t] = a.filt[bp.word];
+                fb[t] = bp.bits;
                 const uint32_t out = (xo[i >> 2] >> (8 * (i & 3))) & 0xFF;
                 const uint32_t in = (xi[i >> 2] >> (8 * (i & 3))) & 0xFF;
                 a_ex = a_ex + in - out;
@@ -395,80 +527,30 @@ __global__ __launch_bounds__(kScanThreads) void k_scan(ScanArgs a) {
             }
 #pragma unroll
             for (int t = 0; t < kBatch; ++t) {
-                const uint32_t fh = filt_hash(wv[t]) >> a.fshift;
-                fw[t] = a.filt[fh >> 5] >> (fh & 31);
-            }
-#pragma unroll
-            for (int t = 0; t < kBatch; ++t) {
                 const uint32_t rel = g + hb + t;
-                bool hit = false;
-                int64_t slot = -1;
-                if ((fw[t] & 1u) && rel < npos) {
-                    slot = table_find(a.keys, a.tmask, wv[t]);
-                    hit = slot >= 0;
+                const uint64_t fmask = bloom_mask(fb[t]);
+                const bool pass = ((fw[t] & fmask) == fmask) && rel < npos;
+                const uint64_t mk = __ballot(pass);
+                if (mk) {
+                    if (pass) fq[nfq + __popcll(mk & ((1ull << lane) - 1))] = make_uint2(rel0 + rel, wv[t]);
+                    nfq += __popcll(mk);
                 }
-                const uint64_t mask = __ballot(hit);
-                if (mask) {
-                    const uint32_t cnt = __popcll(mask);
-                    const int leader = __ffsll((long long)mask) - 1;
-                    unsigned long long base = 0;
-                    if ((int)lane == leader) base = atomicAdd(a.hit_count, (unsigned long long)cnt);
-                    base = __shfl((long long)base, leader, 64);
-                    if (hit) {
-                        const uint64_t mine = base + __popcll(mask & ((1ull << lane) - 1));
-                        if (mine < a.hit_cap) {
-                            HitRec h;
-                            h.pos = (uint32_t)(p0 + rel - a.pos_begin);
-                            h.slot = (uint32_t)slot;
-                            a.hits[mine] = h;
-                        }
-                    }
-                }
+            }
+            if (nfq > (uint32_t)(kFQ - 64 * kBatch)) {
+                lds_fence();
+                passes += nfq;
+                nwq = drain_fq(a, fq, nfq, wq, nwq, tile_start);
+                nfq = 0;
+                lds_fence();
             }
         }
     }
-}
-
-// ===========================================================================
-// K4: verify weak hits — strong hash of the window, first candidate (index
-// order) with equal strong wins (generator.rs:127-153; no size check).
-// One wave per weak hit; verified hits appended as (rel pos, block index).
-// ===========================================================================
-__global__ __launch_bounds__(256) void k_verify(const uint8_t* __restrict__ src, uint64_t pos_begin, uint32_t n,
-                                                const HitRec* __restrict__ hits, uint64_t nhits,
-                                                const uint32_t* __restrict__ start, const uint32_t* __restrict__ cnt,
-                                                const uint32_t* __restrict__ order,
-                                                const uint64_t* __restrict__ strong, HitRec* __restrict__ out,
-                                                unsigned long long* __restrict__ out_count) {
-    const uint64_t w = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
-    if (w >= nhits) return;
-    const uint32_t lane = threadIdx.x & 63;
-    const HitRec h = hits[w];
-    const uint8_t* p = src + pos_begin + h.pos;
-    uint64_t st;
-    if (n > 240) {
-        uint32_t wk;
-        wave_hash_long(p, n, wk, st);
-    } else {
-        st = 0;
-        if (lane == 0) st = xxh3_short(p, n);
-        st = shfl64(st, 0);
-    }
-    const uint32_t s0 = start[h.slot], c = cnt[h.slot];
-    uint32_t best = 0xFFFFFFFFu;
-    for (uint32_t j = lane; j < c; j += 64) {
-        const uint32_t bi = order[s0 + j];
-        if (strong[bi] == st) best = min(best, bi);
-    }
-#pragma unroll
-    for (int m = 1; m < 64; m <<= 1) best = min(best, (uint32_t)__shfl_xor((int)best, m, 64));
-    if (lane == 0 && best != 0xFFFFFFFFu) {
-        const unsigned long long k = atomicAdd(out_count, 1ull);
-        HitRec r;
-        r.pos = h.pos;
-        r.slot = best;
-        out[k] = r;
-    }
+    lds_fence();
+    passes += nfq;
+    nwq = drain_fq(a, fq, nfq, wq, nwq, tile_start);
+    lds_fence();
+    drain_wq(a, wq, nwq, tile_start);
+    if (lane == 0 && passes) atomicAdd(&a.counters[2], passes);
 }
 
 // Tail rule (generator.rs:156-184): at p* = len - last_size (last_size < n), the
@@ -564,21 +646,22 @@ hipError_t launch_signature_batch(const uint8_t* d_buf, const uint64_t* d_off, c
 
 hipError_t launch_index_build(const uint32_t* d_weak, uint64_t n, DeviceIndex& ix, hipStream_t s, Profiler* prof) {
     hipError_t e;
-    if ((e = hipMemsetAsync(ix.filt, 0, ((size_t)1 << ix.fbits) / 8, s))) return e;
-    if ((e = hipMemsetAsync(ix.keys, 0xFF, (size_t)(ix.tmask + 1) * 4, s))) return e;
-    if ((e = hipMemsetAsync(ix.cnt, 0, (size_t)(ix.tmask + 1) * 4, s))) return e;
-    if ((e = hipMemsetAsync(ix.fill, 0, (size_t)(ix.tmask + 1) * 4, s))) return e;
+    const size_t nslots = (size_t)(ix.bmask + 1) * 4;
+    if ((e = hipMemsetAsync(ix.filt, 0, ((size_t)1 << ix.fwbits) * 8, s))) return e;
+    if ((e = hipMemsetAsync(ix.keys, 0xFF, nslots * 4, s))) return e;
+    if ((e = hipMemsetAsync(ix.cnt, 0, nslots * 4, s))) return e;
+    if ((e = hipMemsetAsync(ix.fill, 0, nslots * 4, s))) return e;
     if (n == 0) return hipSuccess;
     {
         ProfScope ps(prof, s, "k_idx_insert");
-        hipLaunchKernelGGL(k_idx_insert, dim3(grid_for(n, 256)), dim3(256), 0, s, d_weak, n, ix.filt, 32 - ix.fbits,
-                           ix.keys, ix.cnt, ix.tmask, ix.slot_of);
+        hipLaunchKernelGGL(k_idx_insert, dim3(grid_for(n, 256)), dim3(256), 0, s, d_weak, n, ix.filt, 32 - ix.fwbits,
+                           ix.keys, ix.cnt, ix.bmask, ix.slot_of);
     }
     size_t tmp = 0;
-    if ((e = hipcub::DeviceScan::ExclusiveSum(nullptr, tmp, ix.cnt, ix.start, (int)(ix.tmask + 1), s))) return e;
+    if ((e = hipcub::DeviceScan::ExclusiveSum(nullptr, tmp, ix.cnt, ix.start, (int)nslots, s))) return e;
     void* d_tmp = nullptr;
     if ((e = hipMallocAsync(&d_tmp, tmp ? tmp : 16, s))) return e;
-    e = hipcub::DeviceScan::ExclusiveSum(d_tmp, tmp, ix.cnt, ix.start, (int)(ix.tmask + 1), s);
+    e = hipcub::DeviceScan::ExclusiveSum(d_tmp, tmp, ix.cnt, ix.start, (int)nslots, s);
     (void)hipFreeAsync(d_tmp, s);
     if (e) return e;
     {
@@ -592,15 +675,16 @@ hipError_t launch_index_build(const uint32_t* d_weak, uint64_t n, DeviceIndex& i
 size_t scan_lds_bytes(uint32_t n, uint32_t* nchunks_out) {
     const uint32_t nch = (uint32_t)((kScanTile + (uint64_t)n + 63) / 64) + 1;
     *nchunks_out = nch;
-    const size_t a = (((size_t)2 * (nch + 1) * 4) + 15) & ~(size_t)15;
-    return a + (size_t)(nch + 1) * 8;
+    const size_t pj_off = (((size_t)2 * (nch + 1) * 4) + 15) & ~(size_t)15;
+    const size_t q_off = (pj_off + (size_t)(nch + 1) * 8 + 15) & ~(size_t)15;
+    return q_off + (size_t)(kScanThreads / 64) * (kFQ + kWQ) * sizeof(uint2);
 }
 
 uint64_t scan_tile_positions() { return kScanTile; }
 
 hipError_t launch_scan(const uint8_t* d_src, uint64_t len, uint64_t pos_begin, uint64_t pos_end, uint32_t n,
-                       const DeviceIndex& ix, HitRec* d_hits, uint64_t hit_cap, unsigned long long* d_count,
-                       hipStream_t s, Profiler* prof) {
+                       const DeviceIndex& ix, const uint64_t* d_strong, HitRec* d_out, uint64_t out_cap,
+                       unsigned long long* d_counters, hipStream_t s, Profiler* prof) {
     ScanArgs a;
     a.src = d_src;
     a.len = len;
@@ -609,27 +693,21 @@ hipError_t launch_scan(const uint8_t* d_src, uint64_t len, uint64_t pos_begin, u
     a.n = n;
     a.nm = n % kMod;
     a.c0 = 2 * kMod - 1 - (uint32_t)((255ull * a.nm) % kMod);
-    a.fshift = 32 - ix.fbits;
+    a.fwshift = 32 - ix.fwbits;
     a.filt = ix.filt;
     a.keys = ix.keys;
-    a.tmask = ix.tmask;
+    a.bmask = ix.bmask;
     const size_t lds = scan_lds_bytes(n, &a.nchunks);
-    a.hits = d_hits;
-    a.hit_cap = hit_cap;
-    a.hit_count = d_count;
+    a.start = ix.start;
+    a.cnt = ix.cnt;
+    a.order = ix.order;
+    a.strong = d_strong;
+    a.out = d_out;
+    a.out_cap = out_cap;
+    a.counters = d_counters;
     const uint64_t tiles = (pos_end - pos_begin + kScanTile - 1) / kScanTile;
     ProfScope ps(prof, s, "k_scan");
     hipLaunchKernelGGL(k_scan, dim3((unsigned)tiles), dim3(kScanThreads), lds, s, a);
-    return hipGetLastError();
-}
-
-hipError_t launch_verify(const uint8_t* d_src, uint64_t pos_begin, uint32_t n, const HitRec* d_hits, uint64_t nhits,
-                         const DeviceIndex& ix, const uint64_t* d_strong, HitRec* d_out, unsigned long long* d_out_count,
-                         hipStream_t s, Profiler* prof) {
-    if (!nhits) return hipSuccess;
-    ProfScope ps(prof, s, "k_verify");
-    hipLaunchKernelGGL(k_verify, dim3(grid_for(nhits * 64, 256)), dim3(256), 0, s, d_src, pos_begin, n, d_hits, nhits,
-                       ix.start, ix.cnt, ix.order, d_strong, d_out, d_out_count);
     return hipGetLastError();
 }
 
