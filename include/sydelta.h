@@ -99,7 +99,7 @@ uint64_t sydelta_calculate_block_size(uint64_t file_size);
 
 /* Signature of a device buffer: compute_checksums' per-block loop
  * (checksum.rs:46-76): ceil(len/bs) blocks, block i = [i*bs, min(len,(i+1)*bs)),
- * weak = Adler32::hash (rolling.rs:71-81), strong = XXH3-64 seed 0
+ * weak = Adler32::hash (rolling.rs:35-45), strong = XXH3-64 seed 0
  * (checksum.rs:65-67).  d_weak / d_strong are device arrays of ceil(len/bs). */
 int sydelta_signature_device(int device, const uint8_t *d_buf, uint64_t len, uint64_t block_size,
                              uint32_t *d_weak, uint64_t *d_strong, void *stream);
@@ -174,7 +174,7 @@ typedef struct sydelta_apply_stats {
 } sydelta_apply_stats;
 int sydelta_apply_delta(const char *old_file, const sydelta_delta *d, const char *new_file, sydelta_apply_stats *out);
 
-/* rolling.rs:71-81 `Adler32::hash` (host utility for the re-exported Adler32 type). */
+/* rolling.rs:35-45 `Adler32::hash` (host utility for the re-exported Adler32 type). */
 uint32_t sydelta_adler32_hash(const uint8_t *data, uint64_t len);
 
 /* ---------------------------------------------------------------------------

@@ -30,7 +30,7 @@ from dataclasses import dataclass
 
 import numpy as np
 
-MOD_ADLER = 65521  # rolling.rs:58
+MOD_ADLER = 65521  # rolling.rs:22
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(HERE, "liboracle.so")
 
@@ -39,7 +39,7 @@ LIB_PATH = os.path.join(HERE, "liboracle.so")
 # rolling.rs
 # --------------------------------------------------------------------------
 def py_adler32(data: bytes) -> int:
-    """Adler32::hash, rolling.rs:71-81."""
+    """Adler32::hash, rolling.rs:35-45."""
     a, b = 1, 0
     for x in data:
         a = (a + x) % MOD_ADLER
@@ -48,7 +48,7 @@ def py_adler32(data: bytes) -> int:
 
 
 class PyAdler32:
-    """struct Adler32, rolling.rs:51-128 (u32 wrap semantics kept)."""
+    """struct Adler32, rolling.rs:16-92 (u32 wrap semantics kept)."""
 
     def __init__(self, block_size: int):  # :62-68
         self.a, self.b, self.block_size = 1, 0, block_size

@@ -9,8 +9,8 @@
  * The reference is Rust; no cargo/rustc exists in this image, so the
  * reference cannot be built.  What is restated here:
  *
- *   oracle_adler32            src/delta/rolling.rs:71-81   (Adler32::hash)
- *   oracle_rolling_*          src/delta/rolling.rs:62-120  (new/update_block/roll/digest)
+ *   oracle_adler32            src/delta/rolling.rs:35-45   (Adler32::hash)
+ *   oracle_rolling_*          src/delta/rolling.rs:26-91   (new/update_block/roll/digest)
  *   oracle_xxh3_64            third-party crate xxhash-rust 0.8.15 (Cargo.lock:4124-4127),
  *                             feature "xxh3": XXH3-64, seed 0, default 192-byte secret.
  *                             Not vendored in the reference; restated from the published
@@ -39,13 +39,13 @@
 #include <unistd.h>
 #include <pthread.h>
 
-#define MOD_ADLER 65521u /* rolling.rs:58 */
+#define MOD_ADLER 65521u /* rolling.rs:22 */
 
 /* ------------------------------------------------------------------ */
 /* Adler-32 (rolling.rs)                                              */
 /* ------------------------------------------------------------------ */
 
-/* rolling.rs:71-81 — per byte a=(a+x)%M, b=(b+a)%M; digest (b<<16)|a. */
+/* rolling.rs:35-45 — per byte a=(a+x)%M, b=(b+a)%M; digest (b<<16)|a. */
 uint32_t oracle_adler32(const uint8_t *data, uint64_t len) {
     uint32_t a = 1, b = 0;
     for (uint64_t i = 0; i < len; i++) {
@@ -57,9 +57,9 @@ uint32_t oracle_adler32(const uint8_t *data, uint64_t len) {
 
 typedef struct { uint32_t a, b; uint64_t block_size; } oracle_rolling;
 
-/* rolling.rs:62-68 */
+/* rolling.rs:26-32 */
 void oracle_rolling_new(oracle_rolling *r, uint64_t block_size) { r->a = 1; r->b = 0; r->block_size = block_size; }
-/* rolling.rs:84-92 */
+/* rolling.rs:48-56 */
 void oracle_rolling_update_block(oracle_rolling *r, const uint8_t *blk, uint64_t len) {
     r->a = 1; r->b = 0;
     for (uint64_t i = 0; i < len; i++) {
@@ -67,14 +67,14 @@ void oracle_rolling_update_block(oracle_rolling *r, const uint8_t *blk, uint64_t
         r->b = (r->b + r->a) % MOD_ADLER;
     }
 }
-/* rolling.rs:102-115 — u32 arithmetic exactly as written (n = block_size as u32). */
+/* rolling.rs:66-79 — u32 arithmetic exactly as written (n = block_size as u32). */
 void oracle_rolling_roll(oracle_rolling *r, uint8_t old_byte, uint8_t new_byte) {
     uint32_t old = old_byte, nw = new_byte, n = (uint32_t)r->block_size;
     r->a = (r->a + MOD_ADLER * 2u - old + nw) % MOD_ADLER;
     uint32_t n_old = (n * old) % MOD_ADLER;
     r->b = (r->b + MOD_ADLER * 3u - n_old + r->a - 1u) % MOD_ADLER;
 }
-/* rolling.rs:118-120 */
+/* rolling.rs:82-84 */
 uint32_t oracle_rolling_digest(const oracle_rolling *r) { return (r->b << 16) | r->a; }
 
 /* ------------------------------------------------------------------ */

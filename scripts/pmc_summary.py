@@ -1,0 +1,58 @@
+"""Summarise rocprofv3 output of scripts/gpu_check.sh into profiles/.
+
+    python scripts/pmc_summary.py gpurun_out/<tag> profiles/<tag>
+
+Writes <dst>_kernel_stats.csv (the --kernel-trace --stats summary, verbatim) and
+<dst>_pmc.json: per kernel, average duration and HBM bytes per launch from the
+FETCH_SIZE / WRITE_SIZE passes, corrected as MI355X_MICROARCH.md §HBM says
+(FETCH_SIZE is in KiB and reports half the bytes of 16-B/lane streaming reads on
+gfx950 -> x1024 x2; WRITE_SIZE in KiB, exact -> x1024).  bench.py reads the
+_pmc.json of the current round to fill roofline.traffic.
+"""
+import collections
+import csv
+import json
+import os
+import shutil
+import sys
+
+
+def per_kernel(path):
+    agg = collections.defaultdict(list)
+    for r in csv.DictReader(open(path)):
+        name = r["Kernel_Name"].split("(")[0].replace("sydelta::", "")
+        agg[name].append(float(r["Counter_Value"]))
+    return {k: sum(v) / len(v) for k, v in agg.items()}
+
+
+def main(src, dst):
+    stats = os.path.join(src, "trace", "run_kernel_stats.csv")
+    shutil.copy(stats, dst + "_kernel_stats.csv")
+    dur = {}
+    for r in csv.DictReader(open(stats)):
+        name = r["Name"].split("(")[0].replace("sydelta::", "")
+        dur[name] = {"calls": int(r["Calls"]), "avg_ms": float(r["AverageNs"]) / 1e6}
+    fetch = per_kernel(os.path.join(src, "pmc_fetch", "run_counter_collection.csv"))
+    write = per_kernel(os.path.join(src, "pmc_write", "run_counter_collection.csv"))
+    out = {}
+    for k in dur:
+        if k.startswith("void rocprim") or k.startswith("__amd"):
+            continue
+        f = fetch.get(k)
+        w = write.get(k)
+        out[k] = dict(dur[k])
+        if f is not None:
+            out[k]["fetch_kib_raw"] = round(f, 3)
+            out[k]["hbm_read_bytes"] = int(f * 1024 * 2)
+        if w is not None:
+            out[k]["hbm_write_bytes"] = int(w * 1024)
+        if f is not None and w is not None:
+            out[k]["traffic_bytes"] = out[k]["hbm_read_bytes"] + out[k]["hbm_write_bytes"]
+    meta = {"source": src, "correction": "FETCH_SIZE KiB x1024 x2 (gfx950 half-count of 16B/lane reads); "
+            "WRITE_SIZE KiB x1024", "kernels": out}
+    json.dump(meta, open(dst + "_pmc.json", "w"), indent=1)
+    print(json.dumps(out, indent=1))
+
+
+if __name__ == "__main__":
+    main(sys.argv[1], sys.argv[2])

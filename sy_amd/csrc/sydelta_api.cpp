@@ -718,7 +718,7 @@ extern "C" int sydelta_apply_delta(const char* old_file, const sydelta_delta* d,
     return rc;
 }
 
-// rolling.rs:71-81
+// rolling.rs:35-45
 extern "C" uint32_t sydelta_adler32_hash(const uint8_t* data, uint64_t len) {
     uint32_t a = 1, b = 0;
     for (uint64_t i = 0; i < len; ++i) {

@@ -1,6 +1,6 @@
 // sydelta_device.hpp — device-side primitives for the delta hot path (gfx950).
 //
-// Adler-32 (src/delta/rolling.rs:71-81) and XXH3-64 seed 0 (crate xxhash-rust
+// Adler-32 (src/delta/rolling.rs:35-45) and XXH3-64 seed 0 (crate xxhash-rust
 // 0.8.15, used at src/delta/checksum.rs:65-67 and generator.rs:128-130) laid
 // out for 64-lane wavefronts:
 //   * XXH3's long-path accumulation is additive inside each 1 KiB block, so a
@@ -15,7 +15,7 @@
 
 namespace sydelta {
 
-constexpr uint32_t kMod = 65521u;  // rolling.rs:58
+constexpr uint32_t kMod = 65521u;  // rolling.rs:22
 
 constexpr uint64_t P32_1 = 0x9E3779B1ull, P32_2 = 0x85EBCA77ull, P32_3 = 0xC2B2AE3Dull;
 constexpr uint64_t P64_1 = 0x9E3779B185EBCA87ull, P64_2 = 0xC2B2AE3D27D4EB4Full;

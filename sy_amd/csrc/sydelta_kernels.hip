@@ -9,7 +9,7 @@
 //   K1" k_sig_scalar  one thread per block of <= 240 bytes (XXH3 short paths).
 //   K3 k_idx_*        device hash table over the basis weak values (generator.rs:75-81).
 //   K2 k_scan         rolling weak hash for every window start of the source + probe of the
-//                     table (generator.rs:116-124, rolling.rs:102-115): Adler state rolled per
+//                     table (generator.rs:116-124, rolling.rs:66-79): Adler state rolled per
 //                     position in closed form, filter bit then exact key probe.
 //   K4 k_verify       XXH3 of each weak-hit window and first-in-index-order strong match
 //                     (generator.rs:127-153).
@@ -241,7 +241,7 @@ __device__ __forceinline__ int64_t table_find(const uint32_t* __restrict__ keys,
 // [p0, p0+kScanRun), p0 = tile_start + k*kScanRun.  The initial window of every
 // thread comes from 64-byte chunk prefix sums over the tile (LDS):
 //   A(p0) = 1 + sum x,  B(p0) = n + sum_i (n-i) x_{p0+i}
-// then per position (rolling.rs:102-115 in closed form, u32, one mod each):
+// then per position (rolling.rs:66-79 in closed form, u32, one mod each):
 //   a_ex += in - out;  A = a_ex mod M
 //   B'   = B + a_ex + nm*(255-out) + C0  (mod M),  nm = n mod M, C0 = 2M-1-(255 nm mod M)
 // which is congruent to B - n*out + A' - 1.

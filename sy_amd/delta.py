@@ -13,7 +13,7 @@ Reference functions and where they are mirrored:
 ``generate_delta``     generator.rs:242  ``generate_delta``
 ``apply_delta``        applier.rs:22     ``apply_delta`` (host file I/O)
 ``calculate_block_size`` mod.rs:20       ``calculate_block_size``
-``Adler32``            rolling.rs:51     ``Adler32``
+``Adler32``            rolling.rs:16     ``Adler32``
 ``BlockChecksum``/``Delta``/``DeltaOp``  dataclasses below
 =======================================  =====================================
 
@@ -90,7 +90,7 @@ class DeltaStats:
 
 
 class Adler32:
-    """rolling.rs:51-128 (host utility; the device computes the same values)."""
+    """rolling.rs:16-92 (host utility; the device computes the same values)."""
 
     def __init__(self, block_size: int):
         self.a, self.b, self.block_size = 1, 0, block_size

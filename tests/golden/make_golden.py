@@ -7,7 +7,7 @@ Expected outputs come from the pure-Python restatement in oracle/oracle.py
 python-xxhash 3.8.1 (libxxhash 0.8.2 — the frozen XXH3 algorithm that crate
 xxhash-rust 0.8.15 implements).  The reference (Rust) cannot be run here, so
 these vectors restate (a) every input/expectation of the reference's own unit
-tests in src/delta (rolling.rs:134-301, checksum.rs:88-146,
+tests in src/delta (rolling.rs:95-266, checksum.rs:88-146,
 generator.rs:388-604, applier.rs:87-234, mod.rs:29-35) and (b) the worked
 examples of SURVEY.md Appendix B, plus seeded random edit cases.
 """
@@ -81,9 +81,9 @@ def main():
     cases = []
     # ---- rolling.rs tests (values are Adler-32 of windows; recorded as signature cases
     # with block size = window so the device path is exercised on the same bytes)
-    cases.append({"kind": "adler", "name": "adler_hello_world", "ref": "rolling.rs:139-144",
+    cases.append({"kind": "adler", "name": "adler_hello_world", "ref": "rolling.rs:99-104",
                   "data": enc(b"hello world"), "expect": zlib.adler32(b"hello world")})
-    cases.append({"kind": "adler", "name": "adler_empty_is_1", "ref": "rolling.rs:201-204",
+    cases.append({"kind": "adler", "name": "adler_empty_is_1", "ref": "rolling.rs:165-168",
                   "data": enc(b""), "expect": 1})
     # ---- checksum.rs tests
     cases.append(sig_case("checksums_51B_bs16", b"Hello, World! This is a test file for checksumming.", 16,

@@ -39,7 +39,7 @@ def test_adler32_pinned(oracle_c):
 
 
 # --------------------------------------------------------------------------
-# rolling.rs:134-301 ported
+# rolling.rs:95-266 ported
 # --------------------------------------------------------------------------
 def test_adler32_basic():  # :138-144
     h = O.py_adler32(b"hello world")
