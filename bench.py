@@ -42,6 +42,9 @@ def parse():
     ap.add_argument("--workload", default="c3", choices=["c3", "c2", "c4"])
     ap.add_argument("--size-gib", type=float, default=4.0)
     ap.add_argument("--block-size", type=int, default=4096)
+    ap.add_argument("--basis-mib", type=int, default=0,
+                    help="c3 only: sign just the first M MiB of the basis (smaller index; "
+                         "exercises the LDS-resident filter); 0 = the whole basis")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     return ap.parse_args()
 
@@ -86,6 +89,24 @@ def cpu_baseline(bs: int):
     }
 
 
+def pmc_traffic(kernel: str, per_launch: int):
+    """HBM bytes per launch of `kernel` from the committed rocprofv3 PMC summary of this
+    round (profiles/*_pmc.json, written by scripts/pmc_summary.py from FETCH_SIZE and
+    WRITE_SIZE passes of this same bench command), scaled to this launch's size."""
+    import glob
+
+    best = None
+    for f in sorted(glob.glob(os.path.join(ROOT, "profiles", "r*_pmc.json"))):
+        try:
+            d = json.load(open(f))
+        except Exception:
+            continue
+        for k, v in d.get("kernels", {}).items():
+            if k == kernel and "traffic_bytes" in v and v.get("bytes_per_launch"):
+                best = v["traffic_bytes"] * per_launch / v["bytes_per_launch"]
+    return int(best) if best else None
+
+
 def main():
     args = parse()
     import numpy as np
@@ -104,6 +125,7 @@ def main():
     n = int(args.size_gib * GIB) // bs * bs
     seed_base = 0x5E1D0002 + 0x1000 * rank
 
+    nb_bytes = min(n, (args.basis_mib << 20) // bs * bs) if args.basis_mib else n
     basis = torch.empty(n, dtype=torch.uint8, device="cuda")
     dev.synth_fill(basis, seed_base)
     new = None
@@ -125,7 +147,7 @@ def main():
             dev.signature(basis, bs, stream=stream)
             return None
         if args.workload == "c3":
-            w, s = dev.signature(basis, bs, stream=stream)
+            w, s = dev.signature(basis[:nb_bytes], bs, stream=stream)
             idx = dev.Index(w, s, bs, bs, device=local, stream=stream)
             d = dev.match(idx, new, stream=stream)
             idx.close()
@@ -164,27 +186,27 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
 
-    bytes_per_step = n if args.workload == "c2" else 2 * n
+    bytes_per_step = n if args.workload == "c2" else (nb_bytes + n if args.workload == "c3" else 2 * n)
     total_bytes = bytes_per_step * args.steps * world
     value = total_bytes / elapsed / GIB
     ms_per_step = elapsed / args.steps * 1e3
 
-    # roofline of the dominant kernel: algorithmic bytes per launch / avg launch time
-    algo = {"k_scan": n, "k_sig_fast": n, "k_sig_batch": n, "k_sig_wave": n}
+    # roofline of the dominant kernel: algorithmic bytes per launch / avg launch time.
+    # Per step the signature kernels read the basis once and the scan reads the source
+    # once; a kernel launched L times per step gets 1/L of that per launch (the scan is
+    # split into segments of 2^31 positions).
+    algo_step = {"k_scan": n, "k_scan_lds": n, "k_sig_fast": nb_bytes if args.workload == "c3" else n, "k_sig_batch": n,
+                 "k_sig_wave": n}
     dom = max(prof, key=lambda k: prof[k]["ms"]) if prof else None
     roof = None
-    if dom:
+    if dom and dom in algo_step:
+        launches_per_step = prof[dom]["count"] / args.steps
         avg_ms = prof[dom]["ms"] / max(1, prof[dom]["count"])
-        per_launch = algo.get(dom)
-        if dom == "k_scan" and args.workload == "c4":
-            per_launch = 1 << 20
-        if dom == "k_sig_batch":
-            per_launch = n
-        if per_launch:
-            ach = per_launch / (avg_ms * 1e-3) / 1e9
-            roof = {"bound": "hbm", "achieved": round(ach, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                    "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": None, "kernel": dom,
-                    "avg_launch_ms": round(avg_ms, 4), "algorithmic_bytes_per_launch": per_launch}
+        per_launch = int(algo_step[dom] / launches_per_step)
+        ach = per_launch / (avg_ms * 1e-3) / 1e9
+        roof = {"bound": "hbm", "achieved": round(ach, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": pmc_traffic(dom, per_launch),
+                "kernel": dom, "avg_launch_ms": round(avg_ms, 4), "algorithmic_bytes_per_launch": per_launch}
     kernels = {k: {"avg_ms": round(v["ms"] / max(1, v["count"]), 4), "launches": v["count"]} for k, v in prof.items()}
 
     if rank == 0:
@@ -212,6 +234,7 @@ def main():
                     "c4": "C4 shape: 1 MiB files (batched signature + per-file match)",
                 }[args.workload],
                 "block_size": bs,
+                "basis_bytes": nb_bytes if args.workload == "c3" else n,
                 "bytes_per_rank_per_step": bytes_per_step,
                 "parallelism": f"file-sharded x{world} (independent pairs per rank, no collective)",
             },

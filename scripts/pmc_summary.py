@@ -1,6 +1,6 @@
 """Summarise rocprofv3 output of scripts/gpu_check.sh into profiles/.
 
-    python scripts/pmc_summary.py gpurun_out/<tag> profiles/<tag>
+    python scripts/pmc_summary.py gpurun_out/<tag> profiles/<tag> [kernel=bytes_per_launch ...]
 
 Writes <dst>_kernel_stats.csv (the --kernel-trace --stats summary, verbatim) and
 <dst>_pmc.json: per kernel, average duration and HBM bytes per launch from the
@@ -17,20 +17,28 @@ import shutil
 import sys
 
 
+def norm(name):
+    return name.split("(")[0].replace("void ", "").replace("sydelta::", "").split("<")[0].strip()
+
+
 def per_kernel(path):
     agg = collections.defaultdict(list)
     for r in csv.DictReader(open(path)):
-        name = r["Kernel_Name"].split("(")[0].replace("sydelta::", "")
+        name = norm(r["Kernel_Name"])
         agg[name].append(float(r["Counter_Value"]))
     return {k: sum(v) / len(v) for k, v in agg.items()}
 
 
-def main(src, dst):
+def main(src, dst, sizes=()):
+    sizes = dict(kv.split("=") for kv in sizes)
     stats = os.path.join(src, "trace", "run_kernel_stats.csv")
     shutil.copy(stats, dst + "_kernel_stats.csv")
     dur = {}
     for r in csv.DictReader(open(stats)):
-        name = r["Name"].split("(")[0].replace("sydelta::", "")
+        name = norm(r["Name"])
+        if name in dur:  # template instances of one kernel: keep the busier one
+            if int(r["Calls"]) * float(r["AverageNs"]) <= dur[name]["calls"] * dur[name]["avg_ms"] * 1e6:
+                continue
         dur[name] = {"calls": int(r["Calls"]), "avg_ms": float(r["AverageNs"]) / 1e6}
     fetch = per_kernel(os.path.join(src, "pmc_fetch", "run_counter_collection.csv"))
     write = per_kernel(os.path.join(src, "pmc_write", "run_counter_collection.csv"))
@@ -48,6 +56,10 @@ def main(src, dst):
             out[k]["hbm_write_bytes"] = int(w * 1024)
         if f is not None and w is not None:
             out[k]["traffic_bytes"] = out[k]["hbm_read_bytes"] + out[k]["hbm_write_bytes"]
+        if k in sizes:
+            out[k]["bytes_per_launch"] = int(sizes[k])
+            if "traffic_bytes" in out[k]:
+                out[k]["traffic_over_algorithmic"] = round(out[k]["traffic_bytes"] / int(sizes[k]), 3)
     meta = {"source": src, "correction": "FETCH_SIZE KiB x1024 x2 (gfx950 half-count of 16B/lane reads); "
             "WRITE_SIZE KiB x1024", "kernels": out}
     json.dump(meta, open(dst + "_pmc.json", "w"), indent=1)
@@ -55,4 +67,4 @@ def main(src, dst):
 
 
 if __name__ == "__main__":
-    main(sys.argv[1], sys.argv[2])
+    main(sys.argv[1], sys.argv[2], sys.argv[3:])

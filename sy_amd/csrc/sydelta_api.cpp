@@ -281,21 +281,26 @@ extern "C" int sydelta_index_create(int device, const uint32_t* weak, const uint
     x->nblocks = nblocks;
     x->bs = block_size;
     x->last_size = nblocks ? last_size : 0;
-    // sizes: Bloom filter ~16 bits/key in 64-bit words (min 2^7 words); buckets of 4 keys at load <= 0.5
+    // sizes: Bloom filter in 32-bit words.  Up to kLdsFilterKeys keys it is at most
+    // 2^13 words (32 KiB) and the LDS-staged scan holds it in LDS (>= 16 bits per key,
+    // 128 bits per key for small bases); above that 16 bits per key in HBM/L2.
+    // Exact table: buckets of 4 keys at load <= 0.5.
     const uint64_t nk = nblocks ? nblocks : 1;
-    const uint32_t fwbits = std::min<uint32_t>(28, std::max<uint32_t>(7, ceil_log2(nk) - 2));
+    const uint32_t lk = ceil_log2(nk);
+    const uint32_t fwbits = nk <= kLdsFilterKeys ? std::min<uint32_t>(13, std::max<uint32_t>(6, lk + 2))
+                                                 : std::min<uint32_t>(28, lk - 1);
     const uint32_t bbits = std::max<uint32_t>(4, ceil_log2((nk + 1) / 2));
     const size_t nslots = ((size_t)1 << bbits) * 4;
     const size_t nb = std::max<uint64_t>(nblocks, 1);
     auto al = [](size_t v) { return (v + 255) & ~(size_t)255; };
-    const size_t sz_weak = al(4 * nb), sz_strong = al(8 * nb), sz_filt = al(((size_t)1 << fwbits) * 8);
+    const size_t sz_weak = al(4 * nb), sz_strong = al(8 * nb), sz_filt = al(((size_t)1 << fwbits) * 4);
     const size_t sz_t = al(4 * nslots), sz_order = al(4 * nb), sz_slot = al(4 * nb);
     const size_t total = sz_weak + sz_strong + sz_filt + 4 * sz_t + sz_order + sz_slot;
     HIP_TRY(hipMalloc(&x->d_pool, total));
     uint8_t* p = (uint8_t*)x->d_pool;
     x->d_weak = (uint32_t*)p; p += sz_weak;
     x->d_strong = (uint64_t*)p; p += sz_strong;
-    x->ix.filt = (unsigned long long*)p; p += sz_filt;
+    x->ix.filt = (uint32_t*)p; p += sz_filt;
     x->ix.fwbits = fwbits;
     x->ix.keys = (uint32_t*)p; p += sz_t;
     x->ix.cnt = (uint32_t*)p; p += sz_t;
@@ -438,6 +443,11 @@ static int match_impl(sydelta_index* ix, const uint8_t* d_src, uint64_t len, hip
         DevBuf cnt_buf;
         HIP_TRY(hipMallocAsync((void**)&d_counts, 64, s));
         cnt_buf.p = d_counts; cnt_buf.s = s;
+        const size_t qcap = scan_queue_entries();
+        uint2* d_q = nullptr;
+        DevBuf q_buf;
+        HIP_TRY(hipMallocAsync((void**)&d_q, qcap * sizeof(uint2), s));
+        q_buf.p = d_q; q_buf.s = s;
         uint64_t cap = 0;
         DevBuf hit_buf;
         for (uint64_t seg = 0; seg < npos; seg += seg_max) {
@@ -446,7 +456,7 @@ static int match_impl(sydelta_index* ix, const uint8_t* d_src, uint64_t len, hip
             // verified hits: at most one per position; start from ~4 per block of positions
             uint64_t want = std::max<uint64_t>(1 << 16, seg_pos / n * 4 + (1 << 16));
             want = std::min<uint64_t>(want, seg_pos);
-            unsigned long long counts[3] = {0, 0, 0};
+            unsigned long long counts[8] = {0, 0, 0, 0, 0, 0, 0, 0};
             for (int attempt = 0; attempt < 2; ++attempt) {
                 if (want > cap) {
                     if (hit_buf.p) { (void)hipFreeAsync(hit_buf.p, s); hit_buf.p = nullptr; }
@@ -455,11 +465,14 @@ static int match_impl(sydelta_index* ix, const uint8_t* d_src, uint64_t len, hip
                     HIP_TRY(hipMallocAsync(&hit_buf.p, 2 * cap * sizeof(HitRec), s));
                     hit_buf.s = s;
                 }
-                HIP_TRY(hipMemsetAsync(d_counts, 0, 32, s));
+                HIP_TRY(hipMemsetAsync(d_counts, 0, 64, s));
                 HIP_TRY(launch_scan(d_src, len, seg, seg_end, (uint32_t)n, ix->ix, ix->d_strong, (HitRec*)hit_buf.p,
-                                    cap, d_counts, s, prof));
-                HIP_TRY(hipMemcpyAsync(counts, d_counts, 24, hipMemcpyDeviceToHost, s));
+                                    cap, d_counts, d_q, qcap, s, prof));
+                HIP_TRY(hipMemcpyAsync(counts, d_counts, 64, hipMemcpyDeviceToHost, s));
                 HIP_TRY(hipStreamSynchronize(s));
+                if (getenv("SYDELTA_PHASE_TIMING"))
+                    fprintf(stderr, "sydelta phase cycles (wave 0, summed over workgroups): stage %llu prefix %llu roll %llu flush %llu\n",
+                            counts[4], counts[5], counts[6], counts[7]);
                 if (counts[0] <= cap) break;
                 want = counts[0];  // dense hits: grow once and rescan
             }

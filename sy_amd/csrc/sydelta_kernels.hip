@@ -158,28 +158,19 @@ __global__ __launch_bounds__(256) void k_sig_batch(const uint8_t* __restrict__ b
 // ===========================================================================
 // K3: index (probe structure) over basis weak values
 // ===========================================================================
-// Blocked Bloom filter: one 64-bit word per key, 4 bits set, ~16 bits/key
-// (FP ~0.6% on Adler values of random blocks; sized to stay L2-resident at 1 Mi
-// keys).  Exact set: bucketised open addressing, 4 keys per 16-byte bucket,
-// load <= 0.5, so a lookup is almost always one dwordx4 load.  Hash inputs are
-// the two 16-bit Adler halves (A = weak & 0xFFFF, B = weak >> 16), mixed with
-// 24-bit multiplies (full-rate v_mad_u32_u24).
-struct BloomProbe {
-    uint32_t word;
-    uint32_t bits;  // four 6-bit bit positions
-};
-__device__ __forceinline__ uint64_t bloom_mask(uint32_t bits) {
-    return (1ull << (bits & 63)) | (1ull << ((bits >> 6) & 63)) | (1ull << ((bits >> 12) & 63)) |
-           (1ull << ((bits >> 18) & 63));
+// Blocked Bloom filter: 32-bit words, 3 bits per key, all in the key's word.
+// One 24-bit multiply and one multiply-add of the two 16-bit Adler halves
+// (A = weak & 0xFFFF, B = weak >> 16) give h; the word is the top bits of h, the
+// bit positions are h[0:5), h[5:10), h[10:15) (v_lshlrev_b32 masks its shift
+// count to 5 bits).
+// Sizing (sydelta_index_create): up to 32 Ki keys the filter is <= 64 KiB and
+// the LDS-staged scan copies it into LDS; above that it stays in HBM/L2 at 16
+// bits per key (~0.5 % false passes on Adler values of random blocks).
+__device__ __forceinline__ uint32_t filt_hash(uint32_t am, uint32_t bm) {
+    return __umul24(am, 0x9E3779u) + __umul24(bm, 0x2F0B35u);
 }
-__device__ __forceinline__ BloomProbe bloom_of(uint32_t am, uint32_t bm, uint32_t fwshift) {
-    const uint32_t h1 = am * 0x2F0B35u + bm * 0x9E3779u;
-    const uint32_t g = am * 0x6B43A9u + bm * 0x1B8735u;
-    const uint32_t g2 = am * 0x1F3D5Bu + bm * 0x5A17C3u;
-    BloomProbe p;
-    p.word = h1 >> fwshift;
-    p.bits = (g >> 26) | (((g >> 20) & 63) << 6) | ((g2 >> 26) << 12) | (((g2 >> 20) & 63) << 18);
-    return p;
+__device__ __forceinline__ uint32_t filt_mask(uint32_t h) {
+    return (1u << (h & 31)) | (1u << ((h >> 5) & 31)) | (1u << ((h >> 10) & 31));
 }
 __device__ __forceinline__ uint32_t bucket_hash(uint32_t w) {
     uint32_t h = w ^ (w >> 15);
@@ -188,14 +179,14 @@ __device__ __forceinline__ uint32_t bucket_hash(uint32_t w) {
     return h;
 }
 
-__global__ void k_idx_insert(const uint32_t* __restrict__ weak, uint64_t n, unsigned long long* __restrict__ filt,
+__global__ void k_idx_insert(const uint32_t* __restrict__ weak, uint64_t n, uint32_t* __restrict__ filt,
                              uint32_t fwshift, uint32_t* __restrict__ keys, uint32_t* __restrict__ cnt,
                              uint32_t bmask, uint32_t* __restrict__ slot_of) {
     const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
     const uint32_t w = weak[i];
-    const BloomProbe bp = bloom_of(w & 0xFFFF, w >> 16, fwshift);
-    atomicOr(&filt[bp.word], (unsigned long long)bloom_mask(bp.bits));
+    const uint32_t h = filt_hash(w & 0xFFFF, w >> 16);
+    atomicOr(&filt[h >> fwshift], filt_mask(h));
     uint32_t b = bucket_hash(w) & bmask;
     for (;;) {
         for (uint32_t j = 0; j < 4; ++j) {
@@ -268,7 +259,7 @@ struct ScanArgs {
     uint32_t nm;         // n mod M
     uint32_t c0;         // 2M - 1 - (255*nm mod M)
     uint32_t fwshift;    // 32 - log2(filter words)
-    const unsigned long long* filt;
+    const uint32_t* filt;
     const uint32_t* keys;
     uint32_t bmask;
     uint32_t nchunks;    // LDS chunk slots per tile
@@ -278,29 +269,52 @@ struct ScanArgs {
     const uint64_t* strong;
     HitRec* out;         // verified hits (unordered): rel pos + block index
     uint64_t out_cap;
-    unsigned long long* counters;  // [0] verified hits, [1] weak hits, [2] filter passes
+    unsigned long long* counters;  // [0] verified hits, [1] weak hits, [2] filter passes, [4..8) phase cycles
+    uint32_t timing;     // accumulate per-phase s_memtime cycles of wave 0 into counters[4..8)
+    uint2* gfq;          // k_scan_lds: per-wave filter-pass queues in HBM/L2, kGFQ entries each
 };
 
-// 64-byte chunk [c0, c0+64) of src, bytes at or beyond len read as 0.
+// 64-byte chunk [c0, c0+64) of src, bytes at or beyond len read as 0.  Past the
+// end only whole 16-byte granules that hold a byte of [0, len) are loaded (the
+// buffer is readable to the end of its last granule, sydelta.h) and masked.
 __device__ __forceinline__ void load_chunk(const uint8_t* src, uint64_t len, uint64_t c0, uint32_t x[16]) {
+    const uint4* q = (const uint4*)(src + c0);
     if (c0 + 64 <= len) {
-        const uint4* q = (const uint4*)(src + c0);
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
             const uint4 v = q[i];
             x[4 * i] = v.x; x[4 * i + 1] = v.y; x[4 * i + 2] = v.z; x[4 * i + 3] = v.w;
         }
-    } else {
+        return;
+    }
 #pragma unroll
-        for (int i = 0; i < 16; ++i) {
-            const uint64_t o = c0 + 4 * i;
-            uint32_t v = 0;
-            if (o + 4 <= len) v = *(const uint32_t*)(src + o);
-            else if (o < len) {
-                for (uint64_t b = o; b < len; ++b) v |= (uint32_t)src[b] << (8 * (b - o));
-            }
-            x[i] = v;
+    for (int i = 0; i < 4; ++i) {
+        uint4 v = make_uint4(0, 0, 0, 0);
+        if (c0 + 16 * i < len) v = q[i];
+        x[4 * i] = v.x; x[4 * i + 1] = v.y; x[4 * i + 2] = v.z; x[4 * i + 3] = v.w;
+    }
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+        const uint64_t o = c0 + 4 * i;
+        const uint32_t keep = o >= len ? 0u : (o + 4 <= len ? 0xFFFFFFFFu : (0xFFFFFFFFu >> (8 * (o + 4 - len))));
+        x[i] &= keep;
+    }
+}
+
+// As load_chunk, with non-temporal loads for the aligned case: the staged tile
+// is read once, so it should not evict the Bloom filter from L2.
+__device__ __forceinline__ void load_chunk_nt(const uint8_t* src, uint64_t len, uint64_t c0, uint32_t x[16]) {
+    if (c0 + 64 <= len) {
+        const uint4* q = (const uint4*)(src + c0);
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            uint4 v;
+            v.x = __builtin_nontemporal_load(&q[i].x); v.y = __builtin_nontemporal_load(&q[i].y);
+            v.z = __builtin_nontemporal_load(&q[i].z); v.w = __builtin_nontemporal_load(&q[i].w);
+            x[4 * i] = v.x; x[4 * i + 1] = v.y; x[4 * i + 2] = v.z; x[4 * i + 3] = v.w;
         }
+    } else {
+        load_chunk(src, len, c0, x);
     }
 }
 
@@ -368,7 +382,9 @@ __device__ __forceinline__ void drain_wq(const ScanArgs& a, const uint2* wq, uin
     }
 }
 
-// Exact lookups for the queued Bloom passes, 64 per round; weak hits go to wq.
+// Exact lookups for the queued Bloom passes, 64 per round; weak hits go to wq
+// (capacity WQ entries, verified in place when full).
+template <int WQ>
 __device__ __forceinline__ uint32_t drain_fq(const ScanArgs& a, const uint2* fq, uint32_t nfq, uint2* wq, uint32_t nwq,
                                           uint64_t tile_start) {
     const uint32_t lane = threadIdx.x & 63;
@@ -378,14 +394,14 @@ __device__ __forceinline__ uint32_t drain_fq(const ScanArgs& a, const uint2* fq,
         uint2 e = make_uint2(0, 0);
         if (i < nfq) {
             e = fq[i];  // {rel pos in tile, packed weak}
-            slot = table_find(a.keys, a.bmask, e.y);
+            if (tile_start + e.x < a.pos_end) slot = table_find(a.keys, a.bmask, e.y);
         }
         const bool hit = slot >= 0;
         const uint64_t m = __ballot(hit);
         const uint32_t cnt = __popcll(m);
         if (cnt && lane == 0) atomicAdd(&a.counters[1], (unsigned long long)cnt);
         if (cnt) {
-            if (nwq + cnt > (uint32_t)kWQ) {  // keep room: verify what is queued
+            if (nwq + cnt > (uint32_t)WQ) {  // keep room: verify what is queued
                 lds_fence();
                 drain_wq(a, wq, nwq, tile_start);
                 nwq = 0;
@@ -510,16 +526,15 @@ __global__ __launch_bounds__(kScanThreads) void k_scan(ScanArgs a) {
 #pragma unroll
         for (int hb = 0; hb < 64; hb += kBatch) {
             uint32_t wv[kBatch];
-            uint64_t fw[kBatch];
-            uint32_t fb[kBatch];
+            uint32_t fw[kBatch];
+            uint32_t fh[kBatch];
 #pragma unroll
             for (int t = 0; t < kBatch; ++t) {
                 const int i = hb + t;
                 const uint32_t am = a_ex % kMod;
                 wv[t] = (bm << 16) | am;
-                const BloomProbe bp = bloom_of(am, bm, a.fwshift);
-                fw[t] = a.filt[bp.word];
-                fb[t] = bp.bits;
+                fh[t] = filt_hash(am, bm);
+                fw[t] = a.filt[fh[t] >> a.fwshift];
                 const uint32_t out = (xo[i >> 2] >> (8 * (i & 3))) & 0xFF;
                 const uint32_t in = (xi[i >> 2] >> (8 * (i & 3))) & 0xFF;
                 a_ex = a_ex + in - out;
@@ -528,7 +543,7 @@ __global__ __launch_bounds__(kScanThreads) void k_scan(ScanArgs a) {
 #pragma unroll
             for (int t = 0; t < kBatch; ++t) {
                 const uint32_t rel = g + hb + t;
-                const uint64_t fmask = bloom_mask(fb[t]);
+                const uint32_t fmask = filt_mask(fh[t]);
                 const bool pass = ((fw[t] & fmask) == fmask) && rel < npos;
                 const uint64_t mk = __ballot(pass);
                 if (mk) {
@@ -539,7 +554,7 @@ __global__ __launch_bounds__(kScanThreads) void k_scan(ScanArgs a) {
             if (nfq > (uint32_t)(kFQ - 64 * kBatch)) {
                 lds_fence();
                 passes += nfq;
-                nwq = drain_fq(a, fq, nfq, wq, nwq, tile_start);
+                nwq = drain_fq<kWQ>(a, fq, nfq, wq, nwq, tile_start);
                 nfq = 0;
                 lds_fence();
             }
@@ -547,10 +562,283 @@ __global__ __launch_bounds__(kScanThreads) void k_scan(ScanArgs a) {
     }
     lds_fence();
     passes += nfq;
-    nwq = drain_fq(a, fq, nfq, wq, nwq, tile_start);
+    nwq = drain_fq<kWQ>(a, fq, nfq, wq, nwq, tile_start);
     lds_fence();
     drain_wq(a, wq, nwq, tile_start);
     if (lane == 0 && passes) atomicAdd(&a.counters[2], passes);
+}
+
+// ===========================================================================
+// K2+K4, LDS-staged: k_scan_lds (window n <= kMaxN2)
+// ===========================================================================
+// Same classification as k_scan, reorganised so that every source byte leaves
+// HBM once per tile and every per-position access is an LDS access:
+//   phase 1  the tile's bytes [T0, T0 + kTile2 + n) are loaded with 16-byte
+//            non-temporal loads into LDS rows of 64 bytes (row stride 68 B, so
+//            the per-thread runs below hit distinct banks), chunk sums on the way;
+//   phase 2  exclusive prefix of the chunk sums;
+//   phase 3  thread t's first window [T0+64t, +n) in closed form;
+//   phase 4  thread t rolls its 64 positions with both Adler halves kept
+//            reduced (rolling.rs:66-79: a' = a+new-old, b' = b-n*old+a'-1, each
+//            brought back to [0, M) with two unsigned min-subtracts), reads one
+//            filter word per position (LDS copy of the filter when the index is
+//            small, else HBM/L2), and only when some lane of the wave has a pass
+//            in the batch queues the passes; exact table lookup and strong
+//            verification (drain2) run from one inlined site.
+// Persistent: workgroup b rolls tiles [b*per, (b+1)*per), contiguous, so a tile's
+// halo (the next tile's first n bytes) is re-read from this XCD's L2; the filter
+// copy and the n*x table are built once per workgroup.  Two workgroups per CU:
+// one's staging (HBM latency) overlaps the other's roll.
+constexpr int kT2 = 256;                 // threads per workgroup (4 waves)
+constexpr int kR2 = 64;                  // positions per thread = one 64-byte row
+constexpr int kTile2 = kT2 * kR2;        // 16384 positions per tile
+constexpr int kB2 = 16;                  // positions per batch (filter reads in flight)
+constexpr int kGFQ = 2048;               // filter-pass queue entries per wave (global memory)
+constexpr int kWQ2 = 128;                // weak-hit queue entries per wave (LDS)
+constexpr uint32_t kMaxN2 = 8192;        // largest window the LDS layout holds
+constexpr int kRowDw = 17;               // LDS row = 16 data dwords + 1 pad
+constexpr int kWgPerCu2 = 2;
+
+struct Lds2 {
+    uint32_t nch;
+    uint32_t ps, pv, pj, ntab, filt, q, total;  // byte offsets
+};
+__host__ __device__ __forceinline__ Lds2 lds2_layout(uint32_t n, uint32_t filt_words) {
+    Lds2 L;
+    L.nch = (kTile2 + n + 63) / 64 + 1;
+    uint32_t o = L.nch * kRowDw * 4;
+    o = (o + 15) & ~15u; L.ps = o; o += (L.nch + 1) * 4;
+    L.pv = o; o += (L.nch + 1) * 4;
+    o = (o + 15) & ~15u; L.pj = o; o += (L.nch + 1) * 8;
+    L.ntab = o; o += 256 * 4;
+    L.filt = o; o += filt_words * 4;
+    o = (o + 15) & ~15u; L.q = o; o += (kT2 / 64) * kWQ2 * 8;
+    L.total = o;
+    return L;
+}
+
+// Exact lookups of the queued filter passes (64 per round; positions at or past
+// pos_end dropped here) and strong verification of the weak hits, verified when
+// wq cannot take another round and, if `final`, at the end.  Returns wq's fill.
+__device__ __forceinline__ uint32_t drain2(const ScanArgs& a, const uint2* fq, uint32_t nfq, uint2* wq, uint32_t nwq,
+                                           uint64_t tile_start, bool final) {
+    const uint32_t lane = threadIdx.x & 63;
+    uint32_t base = 0;
+    __builtin_amdgcn_s_waitcnt(0);  // this wave's queue stores have reached L2
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
+    for (;;) {
+        while (base < nfq && nwq + 64 <= (uint32_t)kWQ2) {
+            const uint32_t i = base + lane;
+            int64_t slot = -1;
+            uint2 e = make_uint2(0, 0);
+            if (i < nfq) {
+                e.x = __builtin_nontemporal_load(&fq[i].x);
+                e.y = __builtin_nontemporal_load(&fq[i].y);
+                if (tile_start + e.x < a.pos_end) slot = table_find(a.keys, a.bmask, e.y);
+            }
+            const bool hit = slot >= 0;
+            const uint64_t m = __ballot(hit);
+            if (m) {
+                const uint32_t cnt = __popcll(m);
+                if (lane == 0) atomicAdd(&a.counters[1], (unsigned long long)cnt);
+                if (hit) wq[nwq + __popcll(m & ((1ull << lane) - 1))] = make_uint2(e.x, (uint32_t)slot);
+                nwq += cnt;
+            }
+            base += 64;
+        }
+        const bool done = base >= nfq;
+        if (done && !final) return nwq;
+        lds_fence();
+        drain_wq(a, wq, nwq, tile_start);
+        nwq = 0;
+        if (done) return 0;
+    }
+}
+
+template <bool kLdsFilter>
+__global__ __launch_bounds__(kT2) void k_scan_lds(ScanArgs a, uint32_t ntiles, uint32_t per) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    const uint32_t n = a.n;
+    const uint32_t fwords = kLdsFilter ? (1u << (32 - a.fwshift)) : 0u;
+    const Lds2 L = lds2_layout(n, fwords);
+    uint32_t* rows = (uint32_t*)smem;
+    uint32_t* PS = (uint32_t*)(smem + L.ps);
+    uint32_t* PV = (uint32_t*)(smem + L.pv);
+    uint64_t* PJ = (uint64_t*)(smem + L.pj);
+    uint32_t* ntab = (uint32_t*)(smem + L.ntab);
+    uint32_t* lfilt = (uint32_t*)(smem + L.filt);
+    const uint32_t tid = threadIdx.x;
+    const uint32_t lane = tid & 63, wid = tid >> 6;
+    uint2* wq = (uint2*)(smem + L.q) + (size_t)wid * kWQ2;
+    uint2* fq = a.gfq + ((size_t)blockIdx.x * (kT2 / 64) + wid) * kGFQ;
+    __shared__ uint32_t red_s[kT2 / 64], red_v[kT2 / 64];
+    __shared__ uint64_t red_j[kT2 / 64];
+
+    const uint32_t t_begin = blockIdx.x * per;
+    const uint32_t t_end = min(ntiles, t_begin + per);
+    if (t_begin >= t_end) return;
+    const uint32_t nch = L.nch;
+
+    // ---- once per workgroup: Bloom filter copy, b-update table
+    if (kLdsFilter) {
+        const uint4* src4 = (const uint4*)a.filt;
+        uint4* dst4 = (uint4*)lfilt;
+#pragma unroll 4
+        for (uint32_t i = tid; i < fwords / 4; i += kT2) dst4[i] = src4[i];
+    }
+    for (uint32_t i = tid; i < 256; i += kT2) ntab[i] = kMod - 1 - (a.nm * i) % kMod;
+    const uint32_t fwshift = a.fwshift;
+    const uint32_t sh = n & 3;
+    const uint32_t rel0 = tid * kR2;
+    unsigned long long passes = 0;
+    unsigned long long tm[4] = {0, 0, 0, 0};
+    unsigned long long tprev = a.timing ? __builtin_amdgcn_s_memtime() : 0;
+#define PHASE_MARK(k)                                                  \
+    if (a.timing) {                                                    \
+        const unsigned long long tnow = __builtin_amdgcn_s_memtime(); \
+        tm[k] += tnow - tprev;                                         \
+        tprev = tnow;                                                  \
+    }
+#pragma unroll 1
+    for (uint32_t tile = t_begin; tile < t_end; ++tile) {
+        const uint64_t tile_start = a.pos_begin + (uint64_t)tile * kTile2;
+
+        // ---- phase 1: tile bytes -> LDS rows, chunk sums (chunks tid, tid + kT2)
+#pragma unroll 1
+        for (uint32_t c = tid; c < nch; c += kT2) {
+            uint32_t x[16];
+            load_chunk_nt(a.src, a.len, tile_start + 64ull * c, x);
+            uint32_t S = 0, V = 0;
+#pragma unroll
+            for (int i = 0; i < 16; ++i) {
+                S = udot4(x[i], 0x01010101u, S);
+                V = udot4(x[i], offw(i), V);
+                rows[c * kRowDw + i] = x[i];
+            }
+            PS[c] = S;
+            PV[c] = V;
+        }
+        __syncthreads();
+        PHASE_MARK(0)
+
+        // ---- phase 2: exclusive prefix over chunks
+        {
+            const uint32_t per_t = (nch + kT2 - 1) / kT2;
+            const uint32_t c_lo = min(nch, tid * per_t), c_hi = min(nch, c_lo + per_t);
+            uint32_t ts = 0, tv = 0;
+            uint64_t tj = 0;
+            for (uint32_t c = c_lo; c < c_hi; ++c) { ts += PS[c]; tv += PV[c]; tj += (uint64_t)c * PS[c]; }
+            uint32_t is = ts, iv = tv;
+            uint64_t ij = tj;
+#pragma unroll
+            for (int m = 1; m < 64; m <<= 1) {
+                const uint32_t os = (uint32_t)__shfl_up((int)is, m, 64);
+                const uint32_t ov = (uint32_t)__shfl_up((int)iv, m, 64);
+                const uint32_t ojl = (uint32_t)__shfl_up((int)(uint32_t)ij, m, 64);
+                const uint32_t ojh = (uint32_t)__shfl_up((int)(uint32_t)(ij >> 32), m, 64);
+                if (lane >= (uint32_t)m) { is += os; iv += ov; ij += ((uint64_t)ojh << 32) | ojl; }
+            }
+            if (lane == 63) { red_s[wid] = is; red_v[wid] = iv; red_j[wid] = ij; }
+            __syncthreads();
+            uint32_t bs_ = 0, bv_ = 0;
+            uint64_t bj_ = 0;
+            for (uint32_t w = 0; w < wid; ++w) { bs_ += red_s[w]; bv_ += red_v[w]; bj_ += red_j[w]; }
+            uint32_t es = bs_ + is - ts, ev = bv_ + iv - tv;
+            uint64_t ej = bj_ + ij - tj;
+            for (uint32_t c = c_lo; c < c_hi; ++c) {
+                const uint32_t s0 = PS[c], v0 = PV[c];
+                PS[c] = es; PV[c] = ev; PJ[c] = ej;
+                es += s0; ev += v0; ej += (uint64_t)c * s0;
+            }
+            if (tid == kT2 - 1) { PS[nch] = bs_ + is; PV[nch] = bv_ + iv; PJ[nch] = bj_ + ij; }
+            __syncthreads();
+        }
+
+        // ---- phase 3: first window of this thread (tile offset 64*tid = start of row tid)
+        uint32_t am, bm;
+        {
+            const uint32_t c0 = tid, m = n >> 6, rem = n & 63;
+            const uint64_t dS = PS[c0 + m] - PS[c0];
+            const uint64_t dV = PV[c0 + m] - PV[c0];
+            const uint64_t dJ = PJ[c0 + m] - PJ[c0];
+            uint64_t A = dS;
+            uint64_t B = (uint64_t)n * dS - 64ull * (dJ - (uint64_t)c0 * dS) - dV;
+            for (uint32_t r = 0; r < rem; ++r) {
+                const uint32_t xr = (rows[(c0 + m) * kRowDw + (r >> 2)] >> (8 * (r & 3))) & 0xFF;
+                A += xr;
+                B += (uint64_t)(rem - r) * xr;
+            }
+            am = (uint32_t)((1 + A) % kMod);
+            bm = (uint32_t)((n + B) % kMod);
+        }
+        PHASE_MARK(1)
+
+        // ---- phase 4: roll 64 positions in batches of kB2.  Positions at or past
+        // pos_end (last tile only) are rolled like the others and dropped by drain2's
+        // bound check, so the hot loop carries no bound test.  The pass queue is
+        // drained at the top of a batch when it could not take a full batch, and by
+        // the extra iteration g == kR2 at the end of the tile: one drain2 site.
+        uint32_t nfq = 0, nwq = 0;
+#pragma unroll 1
+        for (uint32_t g = 0; g <= (uint32_t)kR2; g += kB2) {
+            const bool flush = g == (uint32_t)kR2;
+            if (flush) PHASE_MARK(2)
+            if ((flush && (nfq | nwq)) || nfq > (uint32_t)(kGFQ - 64 * kB2)) {
+                passes += nfq;
+                nwq = drain2(a, fq, nfq, wq, nwq, tile_start, flush);
+                nfq = 0;
+            }
+            if (flush) break;
+            uint32_t xo[4], xi[4];
+#pragma unroll
+            for (int j = 0; j < 4; ++j) xo[j] = rows[tid * kRowDw + (g >> 2) + j];
+            {
+                const uint32_t d0 = (rel0 + g + n) >> 2;
+                uint32_t dw[5];
+#pragma unroll
+                for (int j = 0; j < 5; ++j) {
+                    const uint32_t d = d0 + j;
+                    dw[j] = rows[(d >> 4) * kRowDw + (d & 15)];
+                }
+#pragma unroll
+                for (int j = 0; j < 4; ++j) xi[j] = __builtin_amdgcn_alignbyte(dw[j + 1], dw[j], sh);
+            }
+            uint32_t ct[kB2];
+#pragma unroll
+            for (int t = 0; t < kB2; ++t) ct[t] = ntab[(xo[t >> 2] >> (8 * (t & 3))) & 0xFF];
+            uint32_t wv[kB2], fm[kB2], fw[kB2];
+#pragma unroll
+            for (int t = 0; t < kB2; ++t) {
+                const uint32_t out = (xo[t >> 2] >> (8 * (t & 3))) & 0xFF;
+                const uint32_t in = (xi[t >> 2] >> (8 * (t & 3))) & 0xFF;
+                wv[t] = (bm << 16) | am;
+                const uint32_t h = filt_hash(am, bm);
+                fw[t] = kLdsFilter ? lfilt[h >> fwshift] : a.filt[h >> fwshift];
+                fm[t] = filt_mask(h);
+                uint32_t u = am + in - out;  // (-255, M+255), wrapped when negative
+                u = min(u, u + kMod);
+                am = min(u, u - kMod);
+                uint32_t v = bm + am + ct[t];  // [0, 3M)
+                v = min(v, v - kMod);
+                bm = min(v, v - kMod);
+            }
+#pragma unroll
+            for (int t = 0; t < kB2; ++t) {
+                const bool pass = (fm[t] & ~fw[t]) == 0;
+                const uint64_t mk = __ballot(pass);
+                if (mk) {
+                    if (pass) fq[nfq + __popcll(mk & ((1ull << lane) - 1))] = make_uint2(rel0 + g + t, wv[t]);
+                    nfq += __popcll(mk);
+                }
+            }
+        }
+        __syncthreads();  // rows / prefix arrays are rewritten by the next tile
+        PHASE_MARK(3)
+    }
+#undef PHASE_MARK
+    if (lane == 0 && passes) atomicAdd(&a.counters[2], passes);
+    if (a.timing && tid == 0)
+        for (int k = 0; k < 4; ++k) atomicAdd(&a.counters[4 + k], tm[k]);
 }
 
 // Tail rule (generator.rs:156-184): at p* = len - last_size (last_size < n), the
@@ -647,7 +935,7 @@ hipError_t launch_signature_batch(const uint8_t* d_buf, const uint64_t* d_off, c
 hipError_t launch_index_build(const uint32_t* d_weak, uint64_t n, DeviceIndex& ix, hipStream_t s, Profiler* prof) {
     hipError_t e;
     const size_t nslots = (size_t)(ix.bmask + 1) * 4;
-    if ((e = hipMemsetAsync(ix.filt, 0, ((size_t)1 << ix.fwbits) * 8, s))) return e;
+    if ((e = hipMemsetAsync(ix.filt, 0, ((size_t)1 << ix.fwbits) * 4, s))) return e;
     if ((e = hipMemsetAsync(ix.keys, 0xFF, nslots * 4, s))) return e;
     if ((e = hipMemsetAsync(ix.cnt, 0, nslots * 4, s))) return e;
     if ((e = hipMemsetAsync(ix.fill, 0, nslots * 4, s))) return e;
@@ -682,9 +970,11 @@ size_t scan_lds_bytes(uint32_t n, uint32_t* nchunks_out) {
 
 uint64_t scan_tile_positions() { return kScanTile; }
 
+size_t scan_queue_entries() { return (size_t)kWgPerCu2 * 256 * (kT2 / 64) * kGFQ; }
+
 hipError_t launch_scan(const uint8_t* d_src, uint64_t len, uint64_t pos_begin, uint64_t pos_end, uint32_t n,
                        const DeviceIndex& ix, const uint64_t* d_strong, HitRec* d_out, uint64_t out_cap,
-                       unsigned long long* d_counters, hipStream_t s, Profiler* prof) {
+                       unsigned long long* d_counters, uint2* gfq, size_t gfq_cap, hipStream_t s, Profiler* prof) {
     ScanArgs a;
     a.src = d_src;
     a.len = len;
@@ -705,6 +995,40 @@ hipError_t launch_scan(const uint8_t* d_src, uint64_t len, uint64_t pos_begin, u
     a.out = d_out;
     a.out_cap = out_cap;
     a.counters = d_counters;
+    static const bool timing = getenv("SYDELTA_PHASE_TIMING") != nullptr;
+    a.timing = timing ? 1u : 0u;
+    if (n <= kMaxN2) {
+        const bool lds_filter = (1u << ix.fwbits) <= kLdsFilterWordsMax;
+        const Lds2 L = lds2_layout(n, lds_filter ? (1u << ix.fwbits) : 0u);
+        const uint64_t tiles = (pos_end - pos_begin + kTile2 - 1) / kTile2;
+        // dynamic LDS above 64 KiB must be opted into
+        static std::once_flag attr_once;
+        static hipError_t attr_err = hipSuccess;
+        static int num_cus = 256;
+        std::call_once(attr_once, [] {
+            const int cap = 160 * 1024 / kWgPerCu2 - 512;
+            attr_err = hipFuncSetAttribute((const void*)k_scan_lds<true>, hipFuncAttributeMaxDynamicSharedMemorySize, cap);
+            if (attr_err == hipSuccess)
+                attr_err = hipFuncSetAttribute((const void*)k_scan_lds<false>,
+                                               hipFuncAttributeMaxDynamicSharedMemorySize, cap);
+            int dev = 0, cus = 0;
+            if (hipGetDevice(&dev) == hipSuccess &&
+                hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess && cus > 0)
+                num_cus = cus;
+        });
+        if (attr_err != hipSuccess) return attr_err;
+        if (L.total > 160u * 1024 / kWgPerCu2 - 512) return hipErrorInvalidValue;
+        const uint32_t grid = (uint32_t)std::min<uint64_t>(tiles, (uint64_t)num_cus * kWgPerCu2);
+        const uint32_t per = (uint32_t)((tiles + grid - 1) / grid);
+        if (!gfq || gfq_cap < (size_t)grid * (kT2 / 64) * kGFQ) return hipErrorInvalidValue;
+        a.gfq = gfq;
+        ProfScope ps(prof, s, "k_scan_lds");
+        if (lds_filter)
+            hipLaunchKernelGGL(k_scan_lds<true>, dim3(grid), dim3(kT2), L.total, s, a, (uint32_t)tiles, per);
+        else
+            hipLaunchKernelGGL(k_scan_lds<false>, dim3(grid), dim3(kT2), L.total, s, a, (uint32_t)tiles, per);
+        return hipGetLastError();
+    }
     const uint64_t tiles = (pos_end - pos_begin + kScanTile - 1) / kScanTile;
     ProfScope ps(prof, s, "k_scan");
     hipLaunchKernelGGL(k_scan, dim3((unsigned)tiles), dim3(kScanThreads), lds, s, a);
