@@ -45,7 +45,9 @@ def parse():
     ap.add_argument("--basis-mib", type=int, default=0,
                     help="c3 only: sign just the first M MiB of the basis (smaller index; "
                          "exercises the LDS-resident filter); 0 = the whole basis")
+    ap.add_argument("--files", type=int, default=10000, help="c4: total 1 MiB files over all ranks")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-host-inclusive", action="store_true")
     return ap.parse_args()
 
 
@@ -89,6 +91,97 @@ def cpu_baseline(bs: int):
     }
 
 
+def shard_range(nunits: int, world: int, rank: int):
+    """Contiguous, size-balanced share of `nunits` equal units for `rank` (the LPT
+    split when all units have the same size).  No collective: every rank computes
+    its own range."""
+    per, extra = divmod(nunits, world)
+    lo = rank * per + min(rank, extra)
+    return lo, lo + per + (1 if rank < extra else 0)
+
+
+def max_over_ranks(x: float, device: str) -> float:
+    """The job's time is its slowest rank's (one all-reduce MAX, outside the timed region)."""
+    import torch
+    import torch.distributed as dist
+
+    t = torch.tensor([x], dtype=torch.float64, device=device)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return float(t.item())
+
+
+def c4_files(dev, basis_bytes: int, nfiles: int, first: int):
+    """SURVEY.md §8d C4: basis_i = 1 MiB of synthetic bytes (seed 0x5E1D0004 + i);
+    new_i = basis_i with one byte inserted at a random offset and 16 random byte
+    substitutions.  Files are packed at 16-byte aligned offsets in one buffer each."""
+    import numpy as np
+    import torch
+
+    stride = (basis_bytes + 1 + 15) & ~15
+    basis = torch.empty(max(nfiles, 1) * stride, dtype=torch.uint8, device="cuda")
+    new = torch.empty_like(basis)
+    rng = np.random.default_rng(0x5E1D0004 + first)
+    ins = rng.integers(0, basis_bytes + 1, nfiles)
+    for k in range(nfiles):
+        o = k * stride
+        b = basis[o:o + basis_bytes]
+        dev.synth_fill(b, 0x5E1D0004 + first + k)
+        p = int(ins[k])
+        new[o:o + p] = b[:p]
+        new[o + p] = int(rng.integers(0, 256))
+        new[o + p + 1:o + basis_bytes + 1] = b[p:]
+    sub = (np.arange(nfiles)[:, None] * stride + rng.integers(0, basis_bytes + 1, (nfiles, 16))).reshape(-1)
+    idx = torch.from_numpy(sub.astype(np.int64)).cuda()
+    new[idx] = new[idx] ^ torch.from_numpy(rng.integers(1, 256, sub.size).astype(np.uint8)).cuda()
+    offs = np.arange(nfiles, dtype=np.uint64) * stride
+    return basis, new, (offs, np.full(nfiles, basis_bytes, np.uint64), offs.copy(),
+                        np.full(nfiles, basis_bytes + 1, np.uint64))
+
+
+def host_inclusive(dev, bs: int, size: int, stream_dev: int):
+    """Rate including pinned-host <-> HBM copies: a C3-shaped pair
+    of `size` bytes starts in pinned host memory; the basis goes H2D and is signed
+    while the source's H2D runs on a second stream; then index + match, op list on
+    the host.  Reported beside `value`, never as it."""
+    import torch
+
+    hb = torch.empty(size, dtype=torch.uint8, pin_memory=True)
+    hn = torch.empty(size, dtype=torch.uint8, pin_memory=True)
+    db = torch.empty(size, dtype=torch.uint8, device="cuda")
+    dn = torch.empty(size, dtype=torch.uint8, device="cuda")
+    dev.synth_fill(db, 0x5E1D0012)
+    dev.synth_mutate(dn, db, 0x5E1D0013, 50000)
+    hb.copy_(db)
+    hn.copy_(dn)
+    torch.cuda.synchronize()
+    s1 = torch.cuda.Stream()
+    s2 = torch.cuda.Stream()
+    best = None
+    for _ in range(3):
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        with torch.cuda.stream(s1):
+            db.copy_(hb, non_blocking=True)
+        with torch.cuda.stream(s2):
+            dn.copy_(hn, non_blocking=True)
+        w, s = dev.signature(db, bs, stream=s1)
+        idx = dev.Index(w, s, bs, bs, device=stream_dev, stream=s1)
+        s1.wait_stream(s2)
+        d = dev.match(idx, dn, stream=s1)
+        idx.close()
+        torch.cuda.synchronize()
+        dt = time.perf_counter() - t0
+        best = dt if best is None else min(best, dt)
+    t0 = time.perf_counter()
+    db.copy_(hb)
+    torch.cuda.synchronize()
+    h2d = size / (time.perf_counter() - t0) / 1e9
+    return {"value": round(2 * size / best / GIB, 3), "unit": "GiB/s",
+            "sample": f"{size >> 20} MiB basis + {size >> 20} MiB source (5% byte edits) from pinned host memory, "
+                      f"H2D of the source overlapped with the signature, op list to host; best of 3",
+            "h2d_GBps": round(h2d, 2), "ops": len(d.kind)}
+
+
 def pmc_traffic(kernel: str, per_launch: int):
     """HBM bytes per launch of `kernel` from the committed rocprofv3 PMC summary of this
     round (profiles/*_pmc.json, written by scripts/pmc_summary.py from FETCH_SIZE and
@@ -126,19 +219,23 @@ def main():
     seed_base = 0x5E1D0002 + 0x1000 * rank
 
     nb_bytes = min(n, (args.basis_mib << 20) // bs * bs) if args.basis_mib else n
-    basis = torch.empty(n, dtype=torch.uint8, device="cuda")
-    dev.synth_fill(basis, seed_base)
+    basis = None
+    if args.workload != "c4":
+        basis = torch.empty(n, dtype=torch.uint8, device="cuda")
+        dev.synth_fill(basis, seed_base)
     new = None
     files = None
     if args.workload in ("c3",):
         new = torch.empty(n, dtype=torch.uint8, device="cuda")
         dev.synth_mutate(new, basis, seed_base + 1, 50000)
     if args.workload == "c4":
+        # BASELINE config 4: files [lo, hi) of --files 1 MiB files go to this rank
+        # (equal sizes, so contiguous ranges are the bytes-balanced LPT split).
         fsz = 1 << 20
-        nfiles = n // fsz
-        new = torch.empty(n, dtype=torch.uint8, device="cuda")
-        dev.synth_mutate(new, basis, seed_base + 1, 16)  # ~16 substitutions per MiB file
-        files = (np.arange(nfiles, dtype=np.uint64) * fsz, np.full(nfiles, fsz, np.uint64))
+        lo, hi = shard_range(args.files, world, rank)
+        files = c4_files(dev, basis_bytes=fsz, nfiles=hi - lo, first=lo)
+        basis, new, files = files
+        n = int(files[1].sum())  # basis bytes of this rank
     torch.cuda.synchronize()
     stream = torch.cuda.current_stream()
 
@@ -152,16 +249,15 @@ def main():
             d = dev.match(idx, new, stream=stream)
             idx.close()
             return d
-        # c4: batched signature of all basis files, then one match per file
-        offs, lens = files
-        w, s = dev.signature_batch(basis, offs, lens, bs, stream=stream)
-        per = (1 << 20) // bs
-        last = None
-        for f in range(len(lens)):
-            idx = dev.Index(w[f * per:(f + 1) * per], s[f * per:(f + 1) * per], bs, bs, device=local, stream=stream)
-            last = dev.match(idx, new[f << 20:(f + 1) << 20], stream=stream)
-            idx.close()
-        return last
+        # c4: batched signature of all basis files, per-file index, one batched match
+        boff, blen, soff, slen = files
+        w, s = dev.signature_batch(basis, boff, blen, bs, stream=stream)
+        nblk = (blen + bs - 1) // bs
+        last = blen - (nblk - 1) * bs
+        idx = dev.BatchIndex(w, s, nblk, last, bs, device=local, stream=stream)
+        out, tot = dev.match_batch(idx, new, soff, slen, stream=stream)
+        idx.close()
+        return tot
 
     for _ in range(args.warmup):
         step()
@@ -182,11 +278,14 @@ def main():
     dev.set_profiling(False)
     prof = dev.profile(reset=True)
     if world > 1:
-        t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
+        elapsed = max_over_ranks(elapsed, "cuda")
 
-    bytes_per_step = n if args.workload == "c2" else (nb_bytes + n if args.workload == "c3" else 2 * n)
+    if args.workload == "c2":
+        bytes_per_step = n
+    elif args.workload == "c3":
+        bytes_per_step = nb_bytes + n
+    else:
+        bytes_per_step = int(files[1].sum() + files[3].sum())
     total_bytes = bytes_per_step * args.steps * world
     value = total_bytes / elapsed / GIB
     ms_per_step = elapsed / args.steps * 1e3
@@ -195,8 +294,9 @@ def main():
     # Per step the signature kernels read the basis once and the scan reads the source
     # once; a kernel launched L times per step gets 1/L of that per launch (the scan is
     # split into segments of 2^31 positions).
-    algo_step = {"k_scan": n, "k_scan_lds": n, "k_sig_fast": nb_bytes if args.workload == "c3" else n, "k_sig_batch": n,
-                 "k_sig_wave": n}
+    src_bytes = int(files[3].sum()) if args.workload == "c4" else n
+    algo_step = {"k_scan": src_bytes, "k_scan_lds": src_bytes, "k_sig_fast": nb_bytes if args.workload == "c3" else n,
+                 "k_sig_batch": n, "k_sig_wave": n}
     dom = max(prof, key=lambda k: prof[k]["ms"]) if prof else None
     roof = None
     if dom and dom in algo_step:
@@ -213,6 +313,9 @@ def main():
         cpu = None
         if world == 1 and not args.no_cpu_baseline and args.workload == "c3":
             cpu = cpu_baseline(bs)
+        hinc = None
+        if world == 1 and not args.no_host_inclusive and args.workload == "c3":
+            hinc = host_inclusive(dev, bs, min(n, 1 << 30), local)
         sig_ms = kernels.get("k_sig_fast", {}).get("avg_ms")
         line = {
             "metric": METRIC,
@@ -223,7 +326,7 @@ def main():
             "warmup": args.warmup,
             "ms_per_step": round(ms_per_step, 3),
             "higher_is_better": True,
-            "scaling": "weak",
+            "scaling": "strong" if args.workload == "c4" else "weak",
             "vs_baseline": None,
             "dtype": "u8",
             "data": "synthetic (counter-based splitmix64 bytes; Bernoulli byte substitutions)",
@@ -231,19 +334,22 @@ def main():
                 "workload": {
                     "c3": "C3: signature(4 GiB basis) + rolling match(4 GiB source, 5% random byte edits), bs 4096",
                     "c2": "C2: signature only over 4 GiB, bs 4096",
-                    "c4": "C4 shape: 1 MiB files (batched signature + per-file match)",
+                    "c4": f"C4: {args.files} x 1 MiB files (1-byte insertion + 16 substitutions each), "
+                          f"batched signature + per-file index + batched match, file-sharded over ranks",
                 }[args.workload],
                 "block_size": bs,
                 "basis_bytes": nb_bytes if args.workload == "c3" else n,
                 "bytes_per_rank_per_step": bytes_per_step,
                 "parallelism": f"file-sharded x{world} (independent pairs per rank, no collective)",
+                **({"files": args.files, "files_this_rank": len(files[0])} if args.workload == "c4" else {}),
             },
             "pct_hbm_peak": round(value * GIB / 1e9 / HBM_PEAK_GBS * 100, 2),
             "roofline": roof,
             "cpu_baseline": cpu,
+            "host_inclusive": hinc,
             "kernels": kernels,
             "signature_only_gibps": round(n / (sig_ms * 1e-3) / GIB, 2) if sig_ms else None,
-            "match_stats": last.stats if last is not None else None,
+            "match_stats": (last if isinstance(last, dict) else last.stats) if last is not None else None,
         }
         print(json.dumps(line), flush=True)
     if world > 1:

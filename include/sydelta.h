@@ -83,6 +83,7 @@ typedef struct sydelta_match_stats {
 
 typedef struct sydelta_index sydelta_index; /* device-resident probe table built from a signature */
 typedef struct sydelta_delta sydelta_delta; /* result of a match: op list (host memory) */
+typedef struct sydelta_delta_batch sydelta_delta_batch; /* one delta per file of a batched match */
 
 int sydelta_abi_version(void);
 const char *sydelta_last_error(void);
@@ -186,6 +187,27 @@ uint32_t sydelta_adler32_hash(const uint8_t *data, uint64_t len);
 int sydelta_signature_batch_device(int device, const uint8_t *d_buf, const uint64_t *off, const uint64_t *len,
                                    uint64_t nfiles, uint64_t block_size, uint32_t *d_weak, uint64_t *d_strong,
                                    void *stream);
+
+/* Batched index: nfiles basis signatures concatenated in file order (as
+ * sydelta_signature_batch_device writes them); file f has nblocks[f] blocks, the
+ * last of size last_size[f] (ignored when nblocks[f] == 0).  nblocks/last_size are
+ * host arrays; weak/strong are device arrays if arrays_on_device.  Each file gets
+ * its own candidate map (generator.rs:75-81), as if sy called generate_delta once
+ * per file. */
+int sydelta_index_create_batch(int device, const uint32_t *weak, const uint64_t *strong, const uint64_t *nblocks,
+                               const uint64_t *last_size, uint64_t nfiles, uint64_t block_size, int arrays_on_device,
+                               void *stream, sydelta_index **out);
+/* Batched rolling match: source f = d_buf[src_off[f] .. +src_len[f]) (16-byte
+ * aligned) against basis f of idx, all files in one launch.  Result f is the
+ * delta sy's generate_delta would return for that pair. */
+int sydelta_match_batch_device(sydelta_index *idx, const uint8_t *d_buf, const uint64_t *src_off,
+                               const uint64_t *src_len, uint64_t nfiles, void *stream, sydelta_delta_batch **out);
+uint64_t sydelta_delta_batch_count(const sydelta_delta_batch *b);
+/* Borrowed pointer, valid until sydelta_delta_batch_free. */
+const sydelta_delta *sydelta_delta_batch_get(const sydelta_delta_batch *b, uint64_t i);
+/* Totals over the batch (weak_hits is only counted per batch). */
+int sydelta_delta_batch_stats(const sydelta_delta_batch *b, sydelta_match_stats *out);
+void sydelta_delta_batch_free(sydelta_delta_batch *b);
 
 /* ---------------------------------------------------------------------------
  * Measurement support (used by bench.py; not part of the reference API).

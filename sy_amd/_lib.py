@@ -76,6 +76,12 @@ SIGNATURES = [
     ("sydelta_apply_delta", _i, [ctypes.c_char_p, _vp, ctypes.c_char_p, ctypes.POINTER(DeltaStatsC)]),
     ("sydelta_adler32_hash", _u32, [_vp, _u64]),
     ("sydelta_signature_batch_device", _i, [_i, _vp, _vp, _vp, _u64, _u64, _vp, _vp, _vp]),
+    ("sydelta_index_create_batch", _i, [_i, _vp, _vp, _vp, _vp, _u64, _u64, _i, _vp, _pp]),
+    ("sydelta_match_batch_device", _i, [_vp, _vp, _vp, _vp, _u64, _vp, _pp]),
+    ("sydelta_delta_batch_count", _u64, [_vp]),
+    ("sydelta_delta_batch_get", _vp, [_vp, _u64]),
+    ("sydelta_delta_batch_stats", _i, [_vp, ctypes.POINTER(MatchStatsC)]),
+    ("sydelta_delta_batch_free", None, [_vp]),
     ("sydelta_set_profiling", None, [_i]),
     ("sydelta_profile_json", ctypes.c_size_t, [ctypes.c_char_p, ctypes.c_size_t, _i]),
     ("sydelta_synth_fill", _i, [_vp, _u64, _u64, _vp]),

@@ -238,17 +238,18 @@ extern "C" int sydelta_signature_batch_device(int device, const uint8_t* d_buf, 
 }
 
 // ---------------------------------------------------------------------------
-// index
+// index (one or many basis signatures; arrays concatenated over files)
 // ---------------------------------------------------------------------------
 struct sydelta_index {
     int device = 0;
-    uint64_t nblocks = 0, bs = 0, last_size = 0;
-    uint32_t last_weak = 0;
-    uint64_t last_strong = 0;
-    uint32_t* d_weak = nullptr;   // owned copies
+    uint64_t bs = 0;
+    uint64_t nfiles = 0;
+    std::vector<uint64_t> fblk;       // block prefix, nfiles+1
+    std::vector<uint64_t> last_size;  // per file (0 for an empty signature)
+    uint32_t* d_weak = nullptr;       // owned copies, concatenated
     uint64_t* d_strong = nullptr;
     DeviceIndex ix;
-    void* d_pool = nullptr;       // one allocation for all index arrays
+    void* d_pool = nullptr;           // one allocation for all index arrays
 };
 
 static void index_release(sydelta_index* x) {
@@ -263,69 +264,106 @@ extern "C" void sydelta_index_free(sydelta_index* idx) {
     index_release(idx);
 }
 
-extern "C" int sydelta_index_create(int device, const uint32_t* weak, const uint64_t* strong, uint64_t nblocks,
-                                    uint64_t block_size, uint64_t last_size, int arrays_on_device, void* stream,
-                                    sydelta_index** out) {
+static int index_create_impl(int device, const uint32_t* weak, const uint64_t* strong, const uint64_t* nblk,
+                             const uint64_t* last, uint64_t nfiles, uint64_t block_size, int arrays_on_device,
+                             void* stream, sydelta_index** out) {
     if (!out) return fail(SYDELTA_E_INVAL, "out is NULL");
     *out = nullptr;
     if (block_size == 0) return fail(SYDELTA_E_INVAL, "block_size must be > 0");
+    if (nfiles == 0 || nfiles >= 0xFFFFFFFFull) return fail(SYDELTA_E_INVAL, "bad file count %llu", (unsigned long long)nfiles);
+    std::vector<uint64_t> fblk(nfiles + 1, 0);
+    for (uint64_t f = 0; f < nfiles; ++f) {
+        if (nblk[f] && (last[f] == 0 || last[f] > block_size))
+            return fail(SYDELTA_E_INVAL, "file %llu: last_size must be in [1, block_size]", (unsigned long long)f);
+        fblk[f + 1] = fblk[f] + nblk[f];
+    }
+    const uint64_t nblocks = fblk[nfiles];
     if (nblocks && (!weak || !strong)) return fail(SYDELTA_E_INVAL, "NULL signature arrays");
-    if (nblocks && (last_size == 0 || last_size > block_size))
-        return fail(SYDELTA_E_INVAL, "last_size must be in [1, block_size]");
     if (nblocks >= 0xFFFFFFFFull) return fail(SYDELTA_E_INVAL, "too many blocks (%llu)", (unsigned long long)nblocks);
     if (int r = ensure_device(device)) return r;
     if (device < 0) device = 0;
     hipStream_t s = stream ? (hipStream_t)stream : thread_stream(device);
     std::unique_ptr<sydelta_index, void (*)(sydelta_index*)> x(new sydelta_index(), index_release);
     x->device = device;
-    x->nblocks = nblocks;
     x->bs = block_size;
-    x->last_size = nblocks ? last_size : 0;
-    // sizes: Bloom filter in 32-bit words.  Up to kLdsFilterKeys keys it is at most
-    // 2^13 words (32 KiB) and the LDS-staged scan holds it in LDS (>= 16 bits per key,
-    // 128 bits per key for small bases); above that 16 bits per key in HBM/L2.
-    // Exact table: buckets of 4 keys at load <= 0.5.
-    const uint64_t nk = nblocks ? nblocks : 1;
-    const uint32_t lk = ceil_log2(nk);
-    const uint32_t fwbits = nk <= kLdsFilterKeys ? std::min<uint32_t>(13, std::max<uint32_t>(6, lk + 2))
-                                                 : std::min<uint32_t>(28, lk - 1);
-    const uint32_t bbits = std::max<uint32_t>(4, ceil_log2((nk + 1) / 2));
-    const size_t nslots = ((size_t)1 << bbits) * 4;
+    x->nfiles = nfiles;
+    x->fblk = fblk;
+    x->last_size.resize(nfiles);
+    DeviceIndex& ix = x->ix;
+    ix.nfiles = nfiles;
+    ix.nblocks = nblocks;
+    ix.files.resize(nfiles);
+    // per file: Bloom filter in 32-bit words -- up to kLdsFilterKeys keys at most 2^13
+    // words (32 KiB) that the LDS-staged scan holds in LDS (>= 16 bits per key, 128 bits
+    // per key for small bases), above that 16 bits per key in HBM/L2; exact table in
+    // buckets of 4 keys at load <= 0.5.
+    uint64_t fw = 0, sl = 0;
+    for (uint64_t f = 0; f < nfiles; ++f) {
+        x->last_size[f] = nblk[f] ? last[f] : 0;
+        const uint64_t nk = nblk[f] ? nblk[f] : 1;
+        const uint32_t lk = ceil_log2(nk);
+        const uint32_t fwbits = nk <= kLdsFilterKeys ? std::min<uint32_t>(13, std::max<uint32_t>(6, lk + 2))
+                                                     : std::min<uint32_t>(28, lk - 1);
+        const uint32_t bbits = std::max<uint32_t>(2, ceil_log2((nk + 1) / 2));
+        FileIx& F = ix.files[f];
+        F.filt_off = fw;
+        F.slot_off = sl;
+        F.blk_base = fblk[f];
+        F.fwshift = 32 - fwbits;
+        F.bmask = (1u << bbits) - 1;
+        fw += 1ull << fwbits;
+        sl += 4ull << bbits;
+        ix.max_fwords = std::max<uint32_t>(ix.max_fwords, 1u << fwbits);
+    }
+    ix.fwords = fw;
+    ix.nslots = sl;
     const size_t nb = std::max<uint64_t>(nblocks, 1);
     auto al = [](size_t v) { return (v + 255) & ~(size_t)255; };
-    const size_t sz_weak = al(4 * nb), sz_strong = al(8 * nb), sz_filt = al(((size_t)1 << fwbits) * 4);
-    const size_t sz_t = al(4 * nslots), sz_order = al(4 * nb), sz_slot = al(4 * nb);
-    const size_t total = sz_weak + sz_strong + sz_filt + 4 * sz_t + sz_order + sz_slot;
+    const size_t sz_weak = al(4 * nb), sz_strong = al(8 * nb), sz_filt = al(4 * fw), sz_t = al(4 * sl);
+    const size_t sz_order = al(4 * nb), sz_slot = al(4 * nb), sz_files = al(sizeof(FileIx) * nfiles);
+    const size_t sz_fblk = al(8 * (nfiles + 1));
+    const size_t total = sz_weak + sz_strong + sz_filt + 4 * sz_t + sz_order + sz_slot + sz_files + sz_fblk;
     HIP_TRY(hipMalloc(&x->d_pool, total));
     uint8_t* p = (uint8_t*)x->d_pool;
     x->d_weak = (uint32_t*)p; p += sz_weak;
     x->d_strong = (uint64_t*)p; p += sz_strong;
-    x->ix.filt = (uint32_t*)p; p += sz_filt;
-    x->ix.fwbits = fwbits;
-    x->ix.keys = (uint32_t*)p; p += sz_t;
-    x->ix.cnt = (uint32_t*)p; p += sz_t;
-    x->ix.start = (uint32_t*)p; p += sz_t;
-    x->ix.fill = (uint32_t*)p; p += sz_t;
-    x->ix.order = (uint32_t*)p; p += sz_order;
-    x->ix.slot_of = (uint32_t*)p; p += sz_slot;
-    x->ix.bmask = (uint32_t)((1u << bbits) - 1);
+    ix.filt = (uint32_t*)p; p += sz_filt;
+    ix.keys = (uint32_t*)p; p += sz_t;
+    ix.cnt = (uint32_t*)p; p += sz_t;
+    ix.start = (uint32_t*)p; p += sz_t;
+    ix.fill = (uint32_t*)p; p += sz_t;
+    ix.order = (uint32_t*)p; p += sz_order;
+    ix.slot_of = (uint32_t*)p; p += sz_slot;
+    ix.d_files = (FileIx*)p; p += sz_files;
+    ix.d_fblk = (uint64_t*)p; p += sz_fblk;
     const hipMemcpyKind kind = arrays_on_device ? hipMemcpyDeviceToDevice : hipMemcpyHostToDevice;
     if (nblocks) {
         HIP_TRY(hipMemcpyAsync(x->d_weak, weak, 4 * nblocks, kind, s));
         HIP_TRY(hipMemcpyAsync(x->d_strong, strong, 8 * nblocks, kind, s));
-        if (arrays_on_device) {
-            HIP_TRY(hipMemcpyAsync(&x->last_weak, weak + nblocks - 1, 4, hipMemcpyDeviceToHost, s));
-            HIP_TRY(hipMemcpyAsync(&x->last_strong, strong + nblocks - 1, 8, hipMemcpyDeviceToHost, s));
-        } else {
-            x->last_weak = weak[nblocks - 1];
-            x->last_strong = strong[nblocks - 1];
-        }
     }
+    HIP_TRY(hipMemcpyAsync(ix.d_files, ix.files.data(), sizeof(FileIx) * nfiles, hipMemcpyHostToDevice, s));
+    HIP_TRY(hipMemcpyAsync(ix.d_fblk, x->fblk.data(), 8 * (nfiles + 1), hipMemcpyHostToDevice, s));
     CallProf cp;
-    HIP_TRY(launch_index_build(x->d_weak, nblocks, x->ix, s, cp.get()));
-    HIP_TRY(hipStreamSynchronize(s));
+    HIP_TRY(launch_index_build(x->d_weak, ix, s, cp.get()));
+    HIP_TRY(hipStreamSynchronize(s));  // host tables must outlive the copies
     *out = x.release();
     return SYDELTA_OK;
+}
+
+extern "C" int sydelta_index_create(int device, const uint32_t* weak, const uint64_t* strong, uint64_t nblocks,
+                                    uint64_t block_size, uint64_t last_size, int arrays_on_device, void* stream,
+                                    sydelta_index** out) {
+    const uint64_t last = nblocks ? last_size : 0;
+    return index_create_impl(device, weak, strong, &nblocks, &last, 1, block_size, arrays_on_device, stream, out);
+}
+
+extern "C" int sydelta_index_create_batch(int device, const uint32_t* weak, const uint64_t* strong,
+                                          const uint64_t* nblocks, const uint64_t* last_size, uint64_t nfiles,
+                                          uint64_t block_size, int arrays_on_device, void* stream,
+                                          sydelta_index** out) {
+    if (nfiles && (!nblocks || !last_size)) return fail(SYDELTA_E_INVAL, "NULL file table");
+    return index_create_impl(device, weak, strong, nblocks, last_size, nfiles, block_size, arrays_on_device, stream,
+                             out);
 }
 
 // ---------------------------------------------------------------------------
@@ -337,6 +375,11 @@ struct sydelta_delta {
     sydelta_match_stats stats{};
     std::vector<uint8_t> lit;         // literal bytes (host-data entry points)
     std::vector<uint64_t> lit_off;    // per op: offset into lit, or UINT64_MAX
+};
+
+struct sydelta_delta_batch {
+    std::vector<sydelta_delta> d;
+    sydelta_match_stats total{};
 };
 
 extern "C" uint64_t sydelta_delta_num_ops(const sydelta_delta* d) { return d ? d->ops.size() : 0; }
@@ -365,6 +408,17 @@ extern "C" double sydelta_delta_compression_ratio(const sydelta_delta* d) {
 }
 extern "C" void sydelta_delta_free(sydelta_delta* d) { delete d; }
 
+extern "C" uint64_t sydelta_delta_batch_count(const sydelta_delta_batch* b) { return b ? b->d.size() : 0; }
+extern "C" const sydelta_delta* sydelta_delta_batch_get(const sydelta_delta_batch* b, uint64_t i) {
+    return (b && i < b->d.size()) ? &b->d[i] : nullptr;
+}
+extern "C" int sydelta_delta_batch_stats(const sydelta_delta_batch* b, sydelta_match_stats* out) {
+    if (!b || !out) return fail(SYDELTA_E_INVAL, "NULL argument");
+    *out = b->total;
+    return SYDELTA_OK;
+}
+extern "C" void sydelta_delta_batch_free(sydelta_delta_batch* b) { delete b; }
+
 // ---------------------------------------------------------------------------
 // match
 // ---------------------------------------------------------------------------
@@ -377,10 +431,10 @@ struct DevBuf {
     }
 };
 
-// Greedy op emission (generator.rs:116-221) from position-sorted verified hits.
-void emit_ops(const std::vector<HitRec>& hits, const std::vector<uint64_t>& hit_pos, const sydelta_index* ix,
-              uint64_t len, int tail_match, sydelta_delta* d) {
-    const uint64_t n = ix->bs;
+// Greedy op emission (generator.rs:116-221) of one file from its position-sorted
+// verified hits (pos, global block).
+void emit_ops(const uint64_t* pos, const uint32_t* blk, size_t nhits, uint64_t blk_base, uint64_t nblocks,
+              uint64_t n, uint64_t last_size, uint64_t len, int tail_match, sydelta_delta* d) {
     uint64_t x = 0;
     auto data = [&](uint64_t a, uint64_t b) {
         if (b) {
@@ -389,23 +443,23 @@ void emit_ops(const std::vector<HitRec>& hits, const std::vector<uint64_t>& hit_
             d->stats.literal_bytes += b;
         }
     };
-    auto copy = [&](uint64_t blk) {
-        const uint64_t sz = (blk + 1 == ix->nblocks) ? ix->last_size : n;
-        d->ops.push_back({SYDELTA_OP_COPY, 0, blk * n, sz});
+    auto copy = [&](uint64_t b) {
+        const uint64_t sz = (b + 1 == nblocks) ? last_size : n;
+        d->ops.push_back({SYDELTA_OP_COPY, 0, b * n, sz});
         d->stats.copy_ops++;
     };
-    for (size_t i = 0; i < hits.size(); ++i) {
-        const uint64_t p = hit_pos[i];
+    for (size_t i = 0; i < nhits; ++i) {
+        const uint64_t p = pos[i];
         if (p < x) continue;  // inside the previous Copy: never visited
         data(x, p - x);
-        copy(hits[i].slot);
+        copy(blk[i] - blk_base);
         x = p + n;  // generator.rs:313 / :144
     }
     if (tail_match) {  // generator.rs:324-353: only p* = len - last_size can match
-        const uint64_t pstar = len - ix->last_size;
+        const uint64_t pstar = len - last_size;
         if (pstar >= x) {
             data(x, pstar - x);
-            copy(ix->nblocks - 1);
+            copy(nblocks - 1);
             x = len;
         }
     }
@@ -413,91 +467,169 @@ void emit_ops(const std::vector<HitRec>& hits, const std::vector<uint64_t>& hit_
 }
 }  // namespace
 
-static int match_impl(sydelta_index* ix, const uint8_t* d_src, uint64_t len, hipStream_t s, sydelta_delta* d) {
+// Match source f (d_buf[src_off[f] .. +src_len[f])) against file f of the index,
+// for every f; results in b->d[f].
+static int match_impl(sydelta_index* ix, const uint8_t* d_buf, const uint64_t* src_off, const uint64_t* src_len,
+                      hipStream_t s, sydelta_delta_batch* b) {
     CallProf cp;
     Profiler* prof = cp.get();
     const uint64_t n = ix->bs;
-    d->source_size = len;
-    d->block_size = n;
-    if (len == 0) return SYDELTA_OK;  // generator.rs:262-268
-    if (((uintptr_t)d_src & 15) != 0) return fail(SYDELTA_E_INVAL, "device source must be 16-byte aligned");
-    const uint64_t npos = (len >= n) ? len - n + 1 : 0;
-    d->stats.positions = npos;
-    std::vector<HitRec> all_hits;
-    std::vector<uint64_t> all_pos;
-    // tail check (async; read with the first sync)
-    int tail_flag = 0;
-    int* d_flag = nullptr;
-    DevBuf flag_buf;
-    const bool want_tail = ix->nblocks && ix->last_size < n && len >= ix->last_size;
-    if (want_tail) {
-        HIP_TRY(hipMallocAsync((void**)&d_flag, 16, s));
-        flag_buf.p = d_flag; flag_buf.s = s;
-        HIP_TRY(launch_tail(d_src, len, ix->last_size, ix->last_weak, ix->last_strong, d_flag, s));
-        HIP_TRY(hipMemcpyAsync(&tail_flag, d_flag, sizeof(int), hipMemcpyDeviceToHost, s));
+    const uint64_t nf = ix->nfiles;
+    b->d.assign(nf, sydelta_delta());
+    for (uint64_t f = 0; f < nf; ++f) {
+        b->d[f].source_size = src_len[f];
+        b->d[f].block_size = n;
+        if (src_len[f] && !d_buf) return fail(SYDELTA_E_INVAL, "NULL source buffer");
+        if (src_len[f] && ((uintptr_t)(d_buf + src_off[f]) & 15) != 0)
+            return fail(SYDELTA_E_INVAL, "source %llu must start 16-byte aligned", (unsigned long long)f);
     }
-    if (npos && ix->nblocks) {
-        const uint64_t tile = scan_tile_positions();
-        const uint64_t seg_max = (1ull << 31) / tile * tile;
+    // segments: per file, runs of <= seg_max full-window positions (generator.rs:116-155)
+    const uint64_t tile = scan_tile_positions();
+    const uint64_t seg_max = (1ull << 31) / tile * tile;
+    std::vector<ScanSeg> segs;
+    std::vector<uint32_t> seg_file;
+    uint64_t ntiles = 0, tot_pos = 0;
+    for (uint64_t f = 0; f < nf; ++f) {
+        const uint64_t len = src_len[f];
+        const uint64_t npos = len >= n ? len - n + 1 : 0;
+        b->d[f].stats.positions = npos;
+        tot_pos += npos;
+        if (!npos || ix->fblk[f + 1] == ix->fblk[f]) continue;  // no windows, or empty signature
+        for (uint64_t p0 = 0; p0 < npos; p0 += seg_max) {
+            ScanSeg g{};
+            g.src = src_off[f];
+            g.len = len;
+            g.pos_begin = p0;
+            g.pos_end = std::min(npos, p0 + seg_max);
+            g.tile_base = (uint32_t)ntiles;
+            g.file = (uint32_t)f;
+            ntiles += (g.pos_end - g.pos_begin + tile - 1) / tile;
+            segs.push_back(g);
+            seg_file.push_back((uint32_t)f);
+        }
+    }
+    b->total.positions = tot_pos;
+    if (ntiles >= 0xFFFFFFFFull || segs.size() >= 0x7FFFFFFFull)
+        return fail(SYDELTA_E_INVAL, "batch too large (%llu tiles)", (unsigned long long)ntiles);
+    const bool wide = n > scan_max_window();
+    if (wide && nf != 1) return fail(SYDELTA_E_INVAL, "batched match needs block_size <= %u", scan_max_window());
+    // tail rule jobs (generator.rs:156-184)
+    std::vector<TailJob> tails;
+    std::vector<uint32_t> tail_file;
+    for (uint64_t f = 0; f < nf; ++f) {
+        const uint64_t nb = ix->fblk[f + 1] - ix->fblk[f], ls = ix->last_size[f];
+        if (nb && ls < n && src_len[f] >= ls) {
+            tails.push_back({src_off[f] + src_len[f] - ls, ls, ix->fblk[f + 1] - 1});
+            tail_file.push_back((uint32_t)f);
+        }
+    }
+    std::vector<int> tail_flag(tails.size(), 0);
+    DevBuf tail_buf;
+    if (!tails.empty()) {
+        const size_t bytes = tails.size() * sizeof(TailJob);
+        HIP_TRY(hipMallocAsync(&tail_buf.p, bytes + tails.size() * sizeof(int), s));
+        tail_buf.s = s;
+        int* d_flag = (int*)((uint8_t*)tail_buf.p + bytes);
+        HIP_TRY(hipMemcpyAsync(tail_buf.p, tails.data(), bytes, hipMemcpyHostToDevice, s));
+        HIP_TRY(launch_tail(d_buf, (const TailJob*)tail_buf.p, (uint32_t)tails.size(), ix->d_weak, ix->d_strong, d_flag,
+                            s));
+        HIP_TRY(hipMemcpyAsync(tail_flag.data(), d_flag, tails.size() * sizeof(int), hipMemcpyDeviceToHost, s));
+    }
+    std::vector<uint64_t> hkey;
+    std::vector<uint32_t> hval;
+    if (!segs.empty()) {
         unsigned long long* d_counts = nullptr;
         DevBuf cnt_buf;
         HIP_TRY(hipMallocAsync((void**)&d_counts, 64, s));
         cnt_buf.p = d_counts; cnt_buf.s = s;
-        const size_t qcap = scan_queue_entries();
-        uint2* d_q = nullptr;
-        DevBuf q_buf;
-        HIP_TRY(hipMallocAsync((void**)&d_q, qcap * sizeof(uint2), s));
-        q_buf.p = d_q; q_buf.s = s;
-        uint64_t cap = 0;
+        DevBuf seg_buf, q_buf;
+        size_t qcap = 0;
+        if (!wide) {
+            HIP_TRY(hipMallocAsync(&seg_buf.p, segs.size() * sizeof(ScanSeg), s));
+            seg_buf.s = s;
+            HIP_TRY(hipMemcpyAsync(seg_buf.p, segs.data(), segs.size() * sizeof(ScanSeg), hipMemcpyHostToDevice, s));
+            qcap = scan_queue_entries();
+            HIP_TRY(hipMallocAsync(&q_buf.p, qcap * sizeof(uint2), s));
+            q_buf.s = s;
+        }
+        // verified hits: at most one per position; start from ~4 per block of positions
+        uint64_t want = std::min<uint64_t>(tot_pos, tot_pos / n * 4 + (1 << 16));
+        uint64_t cap = 0, nver = 0;
+        unsigned long long counts[8] = {0, 0, 0, 0, 0, 0, 0, 0};
         DevBuf hit_buf;
-        for (uint64_t seg = 0; seg < npos; seg += seg_max) {
-            const uint64_t seg_end = std::min(npos, seg + seg_max);
-            const uint64_t seg_pos = seg_end - seg;
-            // verified hits: at most one per position; start from ~4 per block of positions
-            uint64_t want = std::max<uint64_t>(1 << 16, seg_pos / n * 4 + (1 << 16));
-            want = std::min<uint64_t>(want, seg_pos);
-            unsigned long long counts[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-            for (int attempt = 0; attempt < 2; ++attempt) {
-                if (want > cap) {
-                    if (hit_buf.p) { (void)hipFreeAsync(hit_buf.p, s); hit_buf.p = nullptr; }
-                    cap = want;
-                    // verified hits [cap] + sort scratch [cap]
-                    HIP_TRY(hipMallocAsync(&hit_buf.p, 2 * cap * sizeof(HitRec), s));
-                    hit_buf.s = s;
-                }
-                HIP_TRY(hipMemsetAsync(d_counts, 0, 64, s));
-                HIP_TRY(launch_scan(d_src, len, seg, seg_end, (uint32_t)n, ix->ix, ix->d_strong, (HitRec*)hit_buf.p,
-                                    cap, d_counts, d_q, qcap, s, prof));
-                HIP_TRY(hipMemcpyAsync(counts, d_counts, 64, hipMemcpyDeviceToHost, s));
-                HIP_TRY(hipStreamSynchronize(s));
-                if (getenv("SYDELTA_PHASE_TIMING"))
-                    fprintf(stderr, "sydelta phase cycles (wave 0, summed over workgroups): stage %llu prefix %llu roll %llu flush %llu\n",
-                            counts[4], counts[5], counts[6], counts[7]);
-                if (counts[0] <= cap) break;
-                want = counts[0];  // dense hits: grow once and rescan
+        for (int attempt = 0; attempt < 2; ++attempt) {
+            if (want > cap) {
+                if (hit_buf.p) { (void)hipFreeAsync(hit_buf.p, s); hit_buf.p = nullptr; }
+                cap = want;
+                // keys [cap] + key scratch [cap] + values [cap] + value scratch [cap]
+                HIP_TRY(hipMallocAsync(&hit_buf.p, cap * 24, s));
+                hit_buf.s = s;
             }
-            d->stats.weak_hits += counts[1];
-            HitRec* d_ver = (HitRec*)hit_buf.p;
-            HitRec* d_sort = d_ver + cap;
-            const uint64_t nver = counts[0];
-            d->stats.verified_hits += nver;
-            if (nver) {
-                HitRec* sorted = nullptr;
-                {
-                    ProfScope ps(prof, s, "sort_hits");
-                    HIP_TRY(launch_sort_hits(d_ver, d_sort, nver, s, &sorted));
-                }
-                const size_t base = all_hits.size();
-                all_hits.resize(base + nver);
-                HIP_TRY(hipMemcpyAsync(all_hits.data() + base, sorted, nver * sizeof(HitRec), hipMemcpyDeviceToHost, s));
-                HIP_TRY(hipStreamSynchronize(s));
-                all_pos.resize(base + nver);
-                for (size_t i = base; i < base + nver; ++i) all_pos[i] = seg + all_hits[i].pos;
+            uint64_t* d_key = (uint64_t*)hit_buf.p;
+            uint32_t* d_val = (uint32_t*)(d_key + 2 * cap);
+            HIP_TRY(hipMemsetAsync(d_counts, 0, 64, s));
+            if (!wide) {
+                HIP_TRY(launch_scan(d_buf, (const ScanSeg*)seg_buf.p, (uint32_t)segs.size(), (uint32_t)ntiles,
+                                    (uint32_t)n, ix->ix, ix->d_strong, d_key, d_val, cap, d_counts,
+                                    (uint2*)q_buf.p, qcap, s, prof));
+            } else {
+                for (size_t g = 0; g < segs.size(); ++g)
+                    HIP_TRY(launch_scan_wide(d_buf + segs[g].src, segs[g].len, segs[g].pos_begin, segs[g].pos_end,
+                                             (uint32_t)g, (uint32_t)n, ix->ix, ix->d_strong, d_key, d_val, cap,
+                                             d_counts, s, prof));
             }
+            HIP_TRY(hipMemcpyAsync(counts, d_counts, 64, hipMemcpyDeviceToHost, s));
+            HIP_TRY(hipStreamSynchronize(s));
+            if (getenv("SYDELTA_PHASE_TIMING"))
+                fprintf(stderr, "sydelta phase cycles (wave 0, summed over workgroups): stage %llu prefix %llu roll %llu flush %llu\n",
+                        counts[4], counts[5], counts[6], counts[7]);
+            if (counts[0] <= cap) break;
+            want = counts[0];  // dense hits: grow once and rescan
+        }
+        nver = counts[0];
+        b->total.weak_hits = counts[1];
+        b->total.verified_hits = nver;
+        if (nver) {
+            uint64_t* d_key = (uint64_t*)hit_buf.p;
+            uint32_t* d_val = (uint32_t*)(d_key + 2 * cap);
+            uint64_t* k_out = nullptr;
+            uint32_t* v_out = nullptr;
+            const int end_bit = kSegShift + (int)ceil_log2(segs.size() + 1);
+            {
+                ProfScope ps(prof, s, "sort_hits");
+                HIP_TRY(launch_sort_hits(d_key, d_val, d_key + cap, d_val + cap, nver, end_bit, s, &k_out, &v_out));
+            }
+            hkey.resize(nver);
+            hval.resize(nver);
+            HIP_TRY(hipMemcpyAsync(hkey.data(), k_out, nver * 8, hipMemcpyDeviceToHost, s));
+            HIP_TRY(hipMemcpyAsync(hval.data(), v_out, nver * 4, hipMemcpyDeviceToHost, s));
         }
     }
     HIP_TRY(hipStreamSynchronize(s));
-    emit_ops(all_hits, all_pos, ix, len, tail_flag, d);
+    // per-file op emission from the (segment, position)-sorted hits
+    std::vector<int> tail_of(nf, 0);
+    for (size_t j = 0; j < tails.size(); ++j) tail_of[tail_file[j]] = tail_flag[j];
+    std::vector<uint64_t> pos;
+    std::vector<uint32_t> blk;
+    size_t h = 0;
+    for (uint64_t f = 0; f < nf; ++f) {
+        pos.clear();
+        blk.clear();
+        while (h < hkey.size() && seg_file[hkey[h] >> kSegShift] == f) {
+            const ScanSeg& g = segs[hkey[h] >> kSegShift];
+            pos.push_back(g.pos_begin + (hkey[h] & 0xFFFFFFFFull));
+            blk.push_back(hval[h]);
+            ++h;
+        }
+        sydelta_delta* d = &b->d[f];
+        d->stats.verified_hits = pos.size();
+        const uint64_t nb = ix->fblk[f + 1] - ix->fblk[f];
+        emit_ops(pos.data(), blk.data(), pos.size(), ix->fblk[f], nb, n, ix->last_size[f], src_len[f], tail_of[f], d);
+        b->total.copy_ops += d->stats.copy_ops;
+        b->total.data_ops += d->stats.data_ops;
+        b->total.literal_bytes += d->stats.literal_bytes;
+    }
+    if (nf == 1) b->d[0].stats.weak_hits = b->total.weak_hits;
     return SYDELTA_OK;
 }
 
@@ -505,12 +637,31 @@ extern "C" int sydelta_match_device(sydelta_index* idx, const uint8_t* d_src, ui
                                     sydelta_delta** out) {
     if (!idx || !out) return fail(SYDELTA_E_INVAL, "NULL argument");
     *out = nullptr;
+    if (idx->nfiles != 1) return fail(SYDELTA_E_INVAL, "index holds %llu files; use sydelta_match_batch_device",
+                                      (unsigned long long)idx->nfiles);
     if (len && !d_src) return fail(SYDELTA_E_INVAL, "NULL source");
     if (int r = ensure_device(idx->device)) return r;
     hipStream_t s = stream ? (hipStream_t)stream : thread_stream(idx->device);
-    std::unique_ptr<sydelta_delta> d(new sydelta_delta());
-    if (int r = match_impl(idx, d_src, len, s, d.get())) return r;
-    *out = d.release();
+    sydelta_delta_batch b;
+    const uint64_t off = 0;
+    if (int r = match_impl(idx, d_src, &off, &len, s, &b)) return r;
+    *out = new sydelta_delta(std::move(b.d[0]));
+    return SYDELTA_OK;
+}
+
+extern "C" int sydelta_match_batch_device(sydelta_index* idx, const uint8_t* d_buf, const uint64_t* src_off,
+                                          const uint64_t* src_len, uint64_t nfiles, void* stream,
+                                          sydelta_delta_batch** out) {
+    if (!idx || !out) return fail(SYDELTA_E_INVAL, "NULL argument");
+    *out = nullptr;
+    if (nfiles != idx->nfiles) return fail(SYDELTA_E_INVAL, "index holds %llu files, %llu sources given",
+                                           (unsigned long long)idx->nfiles, (unsigned long long)nfiles);
+    if (nfiles && (!src_off || !src_len)) return fail(SYDELTA_E_INVAL, "NULL segment table");
+    if (int r = ensure_device(idx->device)) return r;
+    hipStream_t s = stream ? (hipStream_t)stream : thread_stream(idx->device);
+    std::unique_ptr<sydelta_delta_batch> b(new sydelta_delta_batch());
+    if (int r = match_impl(idx, d_buf, src_off, src_len, s, b.get())) return r;
+    *out = b.release();
     return SYDELTA_OK;
 }
 
@@ -598,8 +749,10 @@ static int generate_from_host(int device, const uint8_t* src, uint64_t len, cons
         b.p = d_src; b.s = s;
         HIP_TRY(hipMemcpyAsync(d_src, src, len, hipMemcpyHostToDevice, s));
     }
-    std::unique_ptr<sydelta_delta> d(new sydelta_delta());
-    if (int r = match_impl(ix, d_src, len, s, d.get())) return r;
+    sydelta_delta_batch bt;
+    const uint64_t off = 0;
+    if (int r = match_impl(ix, d_src, &off, &len, s, &bt)) return r;
+    std::unique_ptr<sydelta_delta> d(new sydelta_delta(std::move(bt.d[0])));
     // literal bytes: owned copy of each Data run (DeltaOp::Data(Vec<u8>))
     d->lit_off.assign(d->ops.size(), UINT64_MAX);
     uint64_t tot = 0;

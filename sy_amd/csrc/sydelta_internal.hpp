@@ -13,26 +13,46 @@ constexpr uint32_t kEmptyKey = 0xFFFFFFFFu;  // never a valid weak: A = weak & 0
 constexpr uint64_t kLdsFilterKeys = 16384;   // index sizes whose Bloom filter (<= 32 KiB) the scan keeps in LDS
 constexpr uint32_t kLdsFilterWordsMax = 8192;
 
-// One (weak or verified) hit.  pos = position relative to the segment start,
-// slot = table slot (weak hit) or block index (verified hit).  pos is the low
-// word so a radix sort of the record as a u64 on bits [0,32) orders by position.
-struct HitRec {
-    uint32_t pos;
-    uint32_t slot;
-};
-static_assert(sizeof(HitRec) == 8, "HitRec must be 8 bytes");
+// Verified hits are written as key/value pairs: key = (segment << 32) | position
+// relative to the segment's first position, value = global block index (into the
+// index's concatenated signature).  A radix sort of the keys orders hits by
+// (segment, position); segments are laid out in (file, position) order.
+constexpr int kSegShift = 32;
 
-// Device-resident probe table over a basis signature (SoA in HBM).
+// Probe structures of one file inside a (possibly batched) index.  All arrays
+// of the index are concatenations over its files.
+struct FileIx {
+    uint64_t filt_off;  // first Bloom word of this file
+    uint64_t slot_off;  // first exact-table slot (multiple of 4)
+    uint64_t blk_base;  // first block of this file in the concatenated signature
+    uint32_t fwshift;   // 32 - log2(this file's filter words)
+    uint32_t bmask;     // this file's bucket count - 1
+};
+
+// One range of full-window positions of one source, scanned by one launch.
+struct ScanSeg {
+    uint64_t src;        // byte offset of the source in the scanned buffer
+    uint64_t len;        // source length
+    uint64_t pos_begin;  // first position (relative to the source)
+    uint64_t pos_end;    // one past the last full-window position of this segment
+    uint32_t tile_base;  // first tile of this segment within the launch
+    uint32_t file;       // FileIx of the basis this source is matched against
+};
+
+// Device-resident probe table over one or more basis signatures (SoA in HBM).
 struct DeviceIndex {
-    uint32_t* filt = nullptr;  // blocked Bloom filter: 2^fwbits 32-bit words (filt_hash/filt_mask)
-    uint32_t fwbits = 0;
+    uint32_t* filt = nullptr;   // blocked Bloom filters (filt_hash/filt_mask), per-file 2^k 32-bit words
     uint32_t* keys = nullptr;   // 4-key buckets of unique weak values, kEmptyKey = free
     uint32_t* cnt = nullptr;    // candidates per slot
-    uint32_t* start = nullptr;  // exclusive prefix of cnt
+    uint32_t* start = nullptr;  // exclusive prefix of cnt (global positions into order)
     uint32_t* fill = nullptr;   // scratch for the scatter
-    uint32_t* order = nullptr;  // block indices grouped by slot
+    uint32_t* order = nullptr;  // global block indices grouped by slot, index order within a slot
     uint32_t* slot_of = nullptr;
-    uint32_t bmask = 0;         // buckets - 1
+    FileIx* d_files = nullptr;  // per-file offsets (device copy of files)
+    uint64_t* d_fblk = nullptr; // block prefix over files, nfiles+1 entries
+    std::vector<FileIx> files;  // host copy
+    uint64_t nfiles = 0, nblocks = 0, fwords = 0, nslots = 0;
+    uint32_t max_fwords = 0;    // largest per-file filter (decides LDS residency)
 };
 
 // Per-kernel HIP-event timing (enabled by sydelta_set_profiling).
@@ -55,18 +75,38 @@ hipError_t launch_signature(const uint8_t* d_buf, uint64_t len, uint64_t bs, uin
 hipError_t launch_signature_batch(const uint8_t* d_buf, const uint64_t* d_off, const uint64_t* d_len,
                                   const uint64_t* d_fblk, uint64_t nfiles, uint64_t bs, uint64_t total_blocks,
                                   uint32_t* d_weak, uint64_t* d_strong, hipStream_t s, Profiler* prof);
-hipError_t launch_index_build(const uint32_t* d_weak, uint64_t n, DeviceIndex& ix, hipStream_t s, Profiler* prof);
-size_t scan_lds_bytes(uint32_t n, uint32_t* nchunks_out);
-uint64_t scan_tile_positions();
-// Scratch the scan needs: filter-pass queues, scan_queue_entries() uint2 entries
-// (enough for 2 workgroups per CU on a 256-CU device; launch_scan checks).
+// Build filters + exact tables of every file of ix from the concatenated weak
+// values (ix.nblocks entries; ix.d_fblk / ix.d_files already on the device).
+hipError_t launch_index_build(const uint32_t* d_weak, DeviceIndex& ix, hipStream_t s, Profiler* prof);
+uint64_t scan_tile_positions();  // positions per tile of the LDS-staged scan
+uint32_t scan_max_window();      // largest block size the LDS-staged scan handles
+// Scratch the LDS-staged scan needs: filter-pass queues, scan_queue_entries() uint2
+// entries (2 workgroups per CU on up to 256 CUs; launch_scan checks).
 size_t scan_queue_entries();
-hipError_t launch_scan(const uint8_t* d_src, uint64_t len, uint64_t pos_begin, uint64_t pos_end, uint32_t n,
-                       const DeviceIndex& ix, const uint64_t* d_strong, HitRec* d_out, uint64_t out_cap,
-                       unsigned long long* d_counters, uint2* gfq, size_t gfq_cap, hipStream_t s, Profiler* prof);
-hipError_t launch_sort_hits(HitRec* d_in, HitRec* d_tmp_out, uint64_t nhits, hipStream_t s, HitRec** sorted);
-hipError_t launch_tail(const uint8_t* d_src, uint64_t len, uint64_t last_size, uint32_t want_weak, uint64_t want_strong,
-                       int* d_flag, hipStream_t s);
+// Scan all tiles of segs[0..nsegs) (device copy d_segs; block_size n <= scan_max_window()).
+hipError_t launch_scan(const uint8_t* d_buf, const ScanSeg* d_segs, uint32_t nsegs, uint32_t ntiles, uint32_t n,
+                       const DeviceIndex& ix, const uint64_t* d_strong, uint64_t* d_hit_key, uint32_t* d_hit_val,
+                       uint64_t out_cap, unsigned long long* d_counters, uint2* gfq, size_t gfq_cap, hipStream_t s,
+                       Profiler* prof);
+// Fallback for block sizes above scan_max_window(): one segment, file 0 of ix, hits
+// keyed with seg_id.
+hipError_t launch_scan_wide(const uint8_t* d_src, uint64_t len, uint64_t pos_begin, uint64_t pos_end, uint32_t seg_id,
+                            uint32_t n, const DeviceIndex& ix, const uint64_t* d_strong, uint64_t* d_hit_key,
+                            uint32_t* d_hit_val, uint64_t out_cap, unsigned long long* d_counters, hipStream_t s,
+                            Profiler* prof);
+// Sort nhits (key, value) pairs by key on bits [0, end_bit); sorted output in
+// (*key_out, *val_out) (either the input or the tmp arrays).
+hipError_t launch_sort_hits(uint64_t* key, uint32_t* val, uint64_t* key_tmp, uint32_t* val_tmp, uint64_t nhits,
+                            int end_bit, hipStream_t s, uint64_t** key_out, uint32_t** val_out);
+// Tail rule (generator.rs:156-184) of every listed file: flag[i] = 1 iff the
+// suffix of source i hashes to (weak[blk], strong[blk]) of its last basis block.
+struct TailJob {
+    uint64_t src;        // byte offset of the suffix [len - last_size, len) in the buffer
+    uint64_t last_size;  // 1 .. block_size - 1
+    uint64_t blk;        // global index of the file's last basis block
+};
+hipError_t launch_tail(const uint8_t* d_buf, const TailJob* d_jobs, uint32_t njobs, const uint32_t* d_weak,
+                       const uint64_t* d_strong, int* d_flag, hipStream_t s);
 hipError_t launch_synth_fill(uint8_t* d_buf, uint64_t len, uint64_t seed, hipStream_t s);
 hipError_t launch_synth_mutate(uint8_t* d_dst, const uint8_t* d_src, uint64_t len, uint64_t seed, uint32_t rate_ppm,
                                hipStream_t s);

@@ -179,26 +179,37 @@ __device__ __forceinline__ uint32_t bucket_hash(uint32_t w) {
     return h;
 }
 
-__global__ void k_idx_insert(const uint32_t* __restrict__ weak, uint64_t n, uint32_t* __restrict__ filt,
-                             uint32_t fwshift, uint32_t* __restrict__ keys, uint32_t* __restrict__ cnt,
-                             uint32_t bmask, uint32_t* __restrict__ slot_of) {
+// Block i of the concatenated signature -> its file (fblk = block prefix, nf+1 entries).
+__device__ __forceinline__ uint32_t file_of_block(const uint64_t* __restrict__ fblk, uint32_t nf, uint64_t i) {
+    uint32_t lo = 0, hi = nf;
+    while (hi - lo > 1) {
+        const uint32_t mid = (lo + hi) >> 1;
+        if (fblk[mid] <= i) lo = mid; else hi = mid;
+    }
+    return lo;
+}
+
+__global__ void k_idx_insert(const uint32_t* __restrict__ weak, uint64_t n, const uint64_t* __restrict__ fblk,
+                             uint32_t nf, const FileIx* __restrict__ files, uint32_t* __restrict__ filt,
+                             uint32_t* __restrict__ keys, uint32_t* __restrict__ cnt, uint32_t* __restrict__ slot_of) {
     const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
+    const FileIx F = files[file_of_block(fblk, nf, i)];
     const uint32_t w = weak[i];
     const uint32_t h = filt_hash(w & 0xFFFF, w >> 16);
-    atomicOr(&filt[h >> fwshift], filt_mask(h));
-    uint32_t b = bucket_hash(w) & bmask;
+    atomicOr(&filt[F.filt_off + (h >> F.fwshift)], filt_mask(h));
+    uint32_t b = bucket_hash(w) & F.bmask;
     for (;;) {
         for (uint32_t j = 0; j < 4; ++j) {
-            const uint32_t s = 4 * b + j;
-            const uint32_t old = atomicCAS(&keys[s], kEmptyKey, w);
+            const uint64_t sl = F.slot_off + 4ull * b + j;
+            const uint32_t old = atomicCAS(&keys[sl], kEmptyKey, w);
             if (old == kEmptyKey || old == w) {
-                atomicAdd(&cnt[s], 1u);
-                slot_of[i] = s;
+                atomicAdd(&cnt[sl], 1u);
+                slot_of[i] = (uint32_t)sl;
                 return;
             }
         }
-        b = (b + 1) & bmask;
+        b = (b + 1) & F.bmask;
     }
 }
 
@@ -251,27 +262,48 @@ constexpr int kFQ = 64 * kBatch + 64;                 // filter-pass queue entri
 constexpr int kWQ = 128;                              // weak-hit queue entries per wave
 
 struct ScanArgs {
-    const uint8_t* src;
-    uint64_t len;        // source length L
-    uint64_t pos_begin;  // first position of this segment (multiple of kScanTile)
-    uint64_t pos_end;    // one past the last full-window position of this segment
+    const uint8_t* src;  // scanned buffer (sources at segs[].src)
     uint32_t n;          // block size
     uint32_t nm;         // n mod M
-    uint32_t c0;         // 2M - 1 - (255*nm mod M)
-    uint32_t fwshift;    // 32 - log2(filter words)
+    uint32_t c0;         // 2M - 1 - (255*nm mod M)    (k_scan)
+    uint32_t timing;     // accumulate per-phase s_memtime cycles of wave 0 into counters[4..8)
+    // k_scan_lds: segment table and per-file probe offsets
+    const ScanSeg* segs;
+    uint32_t nsegs;
+    uint32_t ntiles;
+    const FileIx* files;
+    // k_scan (one segment of file 0)
+    uint64_t len;        // source length
+    uint64_t pos_begin;  // first position of the segment (multiple of kScanTile)
+    uint64_t pos_end;    // one past its last full-window position
+    uint32_t seg_id;
+    uint32_t fwshift;    // file 0's filter
+    uint32_t bmask;      // file 0's table
+    uint32_t nchunks;    // LDS chunk slots per tile (k_scan)
+    // probe structures (concatenated over files)
     const uint32_t* filt;
     const uint32_t* keys;
-    uint32_t bmask;
-    uint32_t nchunks;    // LDS chunk slots per tile
     const uint32_t* start;
     const uint32_t* cnt;
     const uint32_t* order;
     const uint64_t* strong;
-    HitRec* out;         // verified hits (unordered): rel pos + block index
+    // outputs
+    uint64_t* hit_key;   // (segment << 32) | position - segment start
+    uint32_t* hit_val;   // global block index
     uint64_t out_cap;
     unsigned long long* counters;  // [0] verified hits, [1] weak hits, [2] filter passes, [4..8) phase cycles
-    uint32_t timing;     // accumulate per-phase s_memtime cycles of wave 0 into counters[4..8)
     uint2* gfq;          // k_scan_lds: per-wave filter-pass queues in HBM/L2, kGFQ entries each
+};
+
+// The segment a tile belongs to, as the drains see it.
+struct SegCtx {
+    const uint8_t* base;  // first byte of the source
+    uint64_t pos_begin;   // segment range, positions relative to the source
+    uint64_t pos_end;
+    const uint32_t* keys; // this file's exact table (slot_off applied)
+    uint64_t slot_off;
+    uint32_t bmask;
+    uint32_t seg_id;
 };
 
 // 64-byte chunk [c0, c0+64) of src, bytes at or beyond len read as 0.  Past the
@@ -346,13 +378,15 @@ __device__ __forceinline__ void load64_at(const uint8_t* src, uint64_t len, uint
 
 __device__ __forceinline__ void lds_fence() { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); }
 
-// Verify every queued weak hit of this wave (wave-uniform loop).
-__device__ __forceinline__ void drain_wq(const ScanArgs& a, const uint2* wq, uint32_t nwq, uint64_t tile_start) {
+// Verify every queued weak hit of this wave (wave-uniform loop): XXH3 of the
+// window, first candidate in index order with equal strong (generator.rs:127-153).
+__device__ __forceinline__ void drain_wq(const ScanArgs& a, const SegCtx& c, const uint2* wq, uint32_t nwq,
+                                         uint64_t tile_start) {
     const uint32_t lane = threadIdx.x & 63;
     for (uint32_t i = 0; i < nwq; ++i) {
-        const uint2 e = wq[i];  // {rel pos in tile, table slot}
+        const uint2 e = wq[i];  // {rel pos in tile, global table slot}
         const uint64_t p = tile_start + e.x;
-        const uint8_t* win = a.src + p;
+        const uint8_t* win = c.base + p;
         uint64_t st;
         if (a.n > 240) {
             uint32_t wk;
@@ -362,9 +396,9 @@ __device__ __forceinline__ void drain_wq(const ScanArgs& a, const uint2* wq, uin
             if (lane == 0) st = xxh3_short(win, a.n);
             st = shfl64(st, 0);
         }
-        const uint32_t s0 = a.start[e.y], c = a.cnt[e.y];
+        const uint32_t s0 = a.start[e.y], cn = a.cnt[e.y];
         uint32_t best = 0xFFFFFFFFu;
-        for (uint32_t j = lane; j < c; j += 64) {
+        for (uint32_t j = lane; j < cn; j += 64) {
             const uint32_t bi = a.order[s0 + j];
             if (a.strong[bi] == st) best = min(best, bi);
         }
@@ -373,10 +407,8 @@ __device__ __forceinline__ void drain_wq(const ScanArgs& a, const uint2* wq, uin
         if (lane == 0 && best != 0xFFFFFFFFu) {
             const unsigned long long k = atomicAdd(&a.counters[0], 1ull);
             if (k < a.out_cap) {
-                HitRec r;
-                r.pos = (uint32_t)(p - a.pos_begin);
-                r.slot = best;
-                a.out[k] = r;
+                a.hit_key[k] = ((uint64_t)c.seg_id << kSegShift) | (uint64_t)(uint32_t)(p - c.pos_begin);
+                a.hit_val[k] = best;
             }
         }
     }
@@ -385,8 +417,8 @@ __device__ __forceinline__ void drain_wq(const ScanArgs& a, const uint2* wq, uin
 // Exact lookups for the queued Bloom passes, 64 per round; weak hits go to wq
 // (capacity WQ entries, verified in place when full).
 template <int WQ>
-__device__ __forceinline__ uint32_t drain_fq(const ScanArgs& a, const uint2* fq, uint32_t nfq, uint2* wq, uint32_t nwq,
-                                          uint64_t tile_start) {
+__device__ __forceinline__ uint32_t drain_fq(const ScanArgs& a, const SegCtx& c, const uint2* fq, uint32_t nfq,
+                                             uint2* wq, uint32_t nwq, uint64_t tile_start) {
     const uint32_t lane = threadIdx.x & 63;
     for (uint32_t base = 0; base < nfq; base += 64) {
         const uint32_t i = base + lane;
@@ -394,7 +426,7 @@ __device__ __forceinline__ uint32_t drain_fq(const ScanArgs& a, const uint2* fq,
         uint2 e = make_uint2(0, 0);
         if (i < nfq) {
             e = fq[i];  // {rel pos in tile, packed weak}
-            if (tile_start + e.x < a.pos_end) slot = table_find(a.keys, a.bmask, e.y);
+            if (tile_start + e.x < c.pos_end) slot = table_find(c.keys, c.bmask, e.y);
         }
         const bool hit = slot >= 0;
         const uint64_t m = __ballot(hit);
@@ -403,12 +435,12 @@ __device__ __forceinline__ uint32_t drain_fq(const ScanArgs& a, const uint2* fq,
         if (cnt) {
             if (nwq + cnt > (uint32_t)WQ) {  // keep room: verify what is queued
                 lds_fence();
-                drain_wq(a, wq, nwq, tile_start);
+                drain_wq(a, c, wq, nwq, tile_start);
                 nwq = 0;
             }
             if (hit) {
                 const uint32_t off = nwq + __popcll(m & ((1ull << lane) - 1));
-                wq[off] = make_uint2(e.x, (uint32_t)slot);
+                wq[off] = make_uint2(e.x, (uint32_t)(c.slot_off + slot));
             }
             nwq += cnt;
             lds_fence();
@@ -435,6 +467,14 @@ __global__ __launch_bounds__(kScanThreads) void k_scan(ScanArgs a) {
     const uint64_t tile_start = a.pos_begin + (uint64_t)blockIdx.x * kScanTile;
     if (tile_start >= a.pos_end) return;
     const uint32_t n = a.n;
+    SegCtx sc;
+    sc.base = a.src;
+    sc.pos_begin = a.pos_begin;
+    sc.pos_end = a.pos_end;
+    sc.keys = a.keys;
+    sc.slot_off = 0;
+    sc.bmask = a.bmask;
+    sc.seg_id = a.seg_id;
 
     // ---- phase 1: chunk sums (coalesced: thread t takes chunks t, t+256, ...)
     for (uint32_t c = tid; c < nch; c += kScanThreads) {
@@ -554,7 +594,7 @@ __global__ __launch_bounds__(kScanThreads) void k_scan(ScanArgs a) {
             if (nfq > (uint32_t)(kFQ - 64 * kBatch)) {
                 lds_fence();
                 passes += nfq;
-                nwq = drain_fq<kWQ>(a, fq, nfq, wq, nwq, tile_start);
+                nwq = drain_fq<kWQ>(a, sc, fq, nfq, wq, nwq, tile_start);
                 nfq = 0;
                 lds_fence();
             }
@@ -562,9 +602,9 @@ __global__ __launch_bounds__(kScanThreads) void k_scan(ScanArgs a) {
     }
     lds_fence();
     passes += nfq;
-    nwq = drain_fq<kWQ>(a, fq, nfq, wq, nwq, tile_start);
+    nwq = drain_fq<kWQ>(a, sc, fq, nfq, wq, nwq, tile_start);
     lds_fence();
-    drain_wq(a, wq, nwq, tile_start);
+    drain_wq(a, sc, wq, nwq, tile_start);
     if (lane == 0 && passes) atomicAdd(&a.counters[2], passes);
 }
 
@@ -620,8 +660,8 @@ __host__ __device__ __forceinline__ Lds2 lds2_layout(uint32_t n, uint32_t filt_w
 // Exact lookups of the queued filter passes (64 per round; positions at or past
 // pos_end dropped here) and strong verification of the weak hits, verified when
 // wq cannot take another round and, if `final`, at the end.  Returns wq's fill.
-__device__ __forceinline__ uint32_t drain2(const ScanArgs& a, const uint2* fq, uint32_t nfq, uint2* wq, uint32_t nwq,
-                                           uint64_t tile_start, bool final) {
+__device__ __forceinline__ uint32_t drain2(const ScanArgs& a, const SegCtx& c, const uint2* fq, uint32_t nfq,
+                                           uint2* wq, uint32_t nwq, uint64_t tile_start, bool final) {
     const uint32_t lane = threadIdx.x & 63;
     uint32_t base = 0;
     __builtin_amdgcn_s_waitcnt(0);  // this wave's queue stores have reached L2
@@ -634,14 +674,14 @@ __device__ __forceinline__ uint32_t drain2(const ScanArgs& a, const uint2* fq, u
             if (i < nfq) {
                 e.x = __builtin_nontemporal_load(&fq[i].x);
                 e.y = __builtin_nontemporal_load(&fq[i].y);
-                if (tile_start + e.x < a.pos_end) slot = table_find(a.keys, a.bmask, e.y);
+                if (tile_start + e.x < c.pos_end) slot = table_find(c.keys, c.bmask, e.y);
             }
             const bool hit = slot >= 0;
             const uint64_t m = __ballot(hit);
             if (m) {
                 const uint32_t cnt = __popcll(m);
                 if (lane == 0) atomicAdd(&a.counters[1], (unsigned long long)cnt);
-                if (hit) wq[nwq + __popcll(m & ((1ull << lane) - 1))] = make_uint2(e.x, (uint32_t)slot);
+                if (hit) wq[nwq + __popcll(m & ((1ull << lane) - 1))] = make_uint2(e.x, (uint32_t)(c.slot_off + slot));
                 nwq += cnt;
             }
             base += 64;
@@ -649,18 +689,17 @@ __device__ __forceinline__ uint32_t drain2(const ScanArgs& a, const uint2* fq, u
         const bool done = base >= nfq;
         if (done && !final) return nwq;
         lds_fence();
-        drain_wq(a, wq, nwq, tile_start);
+        drain_wq(a, c, wq, nwq, tile_start);
         nwq = 0;
         if (done) return 0;
     }
 }
 
 template <bool kLdsFilter>
-__global__ __launch_bounds__(kT2) void k_scan_lds(ScanArgs a, uint32_t ntiles, uint32_t per) {
+__global__ __launch_bounds__(kT2) void k_scan_lds(ScanArgs a, uint32_t per, uint32_t lds_fwords) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     const uint32_t n = a.n;
-    const uint32_t fwords = kLdsFilter ? (1u << (32 - a.fwshift)) : 0u;
-    const Lds2 L = lds2_layout(n, fwords);
+    const Lds2 L = lds2_layout(n, kLdsFilter ? lds_fwords : 0u);
     uint32_t* rows = (uint32_t*)smem;
     uint32_t* PS = (uint32_t*)(smem + L.ps);
     uint32_t* PV = (uint32_t*)(smem + L.pv);
@@ -675,22 +714,19 @@ __global__ __launch_bounds__(kT2) void k_scan_lds(ScanArgs a, uint32_t ntiles, u
     __shared__ uint64_t red_j[kT2 / 64];
 
     const uint32_t t_begin = blockIdx.x * per;
-    const uint32_t t_end = min(ntiles, t_begin + per);
+    const uint32_t t_end = min(a.ntiles, t_begin + per);
     if (t_begin >= t_end) return;
     const uint32_t nch = L.nch;
 
-    // ---- once per workgroup: Bloom filter copy, b-update table
-    if (kLdsFilter) {
-        const uint4* src4 = (const uint4*)a.filt;
-        uint4* dst4 = (uint4*)lfilt;
-#pragma unroll 4
-        for (uint32_t i = tid; i < fwords / 4; i += kT2) dst4[i] = src4[i];
-    }
     for (uint32_t i = tid; i < 256; i += kT2) ntab[i] = kMod - 1 - (a.nm * i) % kMod;
-    const uint32_t fwshift = a.fwshift;
     const uint32_t sh = n & 3;
     const uint32_t rel0 = tid * kR2;
     unsigned long long passes = 0;
+    uint32_t cur_file = 0xFFFFFFFFu;
+    uint32_t fwshift = 0;
+    const uint32_t* gfilt = a.filt;
+    SegCtx sc;
+
     unsigned long long tm[4] = {0, 0, 0, 0};
     unsigned long long tprev = a.timing ? __builtin_amdgcn_s_memtime() : 0;
 #define PHASE_MARK(k)                                                  \
@@ -699,15 +735,47 @@ __global__ __launch_bounds__(kT2) void k_scan_lds(ScanArgs a, uint32_t ntiles, u
         tm[k] += tnow - tprev;                                         \
         tprev = tnow;                                                  \
     }
+    uint32_t si = 0;  // segment of the current tile (tiles are visited in increasing order)
 #pragma unroll 1
     for (uint32_t tile = t_begin; tile < t_end; ++tile) {
-        const uint64_t tile_start = a.pos_begin + (uint64_t)tile * kTile2;
+        // ---- segment of this tile (uniform): first one with tile_base > tile, minus one
+        if (tile == t_begin || (si + 1 < a.nsegs && a.segs[si + 1].tile_base <= tile)) {
+            uint32_t lo = si, hi = a.nsegs;
+            if (tile == t_begin) lo = 0;
+            while (hi - lo > 1) {
+                const uint32_t mid = (lo + hi) >> 1;
+                if (a.segs[mid].tile_base <= tile) lo = mid; else hi = mid;
+            }
+            si = lo;
+            const ScanSeg S = a.segs[si];
+            const FileIx F = a.files[S.file];
+            sc.base = a.src + S.src;
+            sc.pos_begin = S.pos_begin;
+            sc.pos_end = S.pos_end;
+            sc.keys = a.keys + F.slot_off;
+            sc.slot_off = F.slot_off;
+            sc.bmask = F.bmask;
+            sc.seg_id = si;
+            fwshift = F.fwshift;
+            gfilt = a.filt + F.filt_off;
+            if (kLdsFilter && S.file != cur_file) {
+                // the previous tile ended with a barrier; phase 1's barrier publishes the copy
+                const uint4* src4 = (const uint4*)gfilt;
+                uint4* dst4 = (uint4*)lfilt;
+                const uint32_t fwords = 1u << (32 - fwshift);
+#pragma unroll 4
+                for (uint32_t i = tid; i < fwords / 4; i += kT2) dst4[i] = src4[i];
+            }
+            cur_file = S.file;
+        }
+        const uint64_t seg_len = a.segs[si].len;
+        const uint64_t tile_start = sc.pos_begin + (uint64_t)(tile - a.segs[si].tile_base) * kTile2;
 
         // ---- phase 1: tile bytes -> LDS rows, chunk sums (chunks tid, tid + kT2)
 #pragma unroll 1
         for (uint32_t c = tid; c < nch; c += kT2) {
             uint32_t x[16];
-            load_chunk_nt(a.src, a.len, tile_start + 64ull * c, x);
+            load_chunk_nt(sc.base, seg_len, tile_start + 64ull * c, x);
             uint32_t S = 0, V = 0;
 #pragma unroll
             for (int i = 0; i < 16; ++i) {
@@ -785,7 +853,7 @@ __global__ __launch_bounds__(kT2) void k_scan_lds(ScanArgs a, uint32_t ntiles, u
             if (flush) PHASE_MARK(2)
             if ((flush && (nfq | nwq)) || nfq > (uint32_t)(kGFQ - 64 * kB2)) {
                 passes += nfq;
-                nwq = drain2(a, fq, nfq, wq, nwq, tile_start, flush);
+                nwq = drain2(a, sc, fq, nfq, wq, nwq, tile_start, flush);
                 nfq = 0;
             }
             if (flush) break;
@@ -813,7 +881,7 @@ __global__ __launch_bounds__(kT2) void k_scan_lds(ScanArgs a, uint32_t ntiles, u
                 const uint32_t in = (xi[t >> 2] >> (8 * (t & 3))) & 0xFF;
                 wv[t] = (bm << 16) | am;
                 const uint32_t h = filt_hash(am, bm);
-                fw[t] = kLdsFilter ? lfilt[h >> fwshift] : a.filt[h >> fwshift];
+                fw[t] = kLdsFilter ? lfilt[h >> fwshift] : gfilt[h >> fwshift];
                 fm[t] = filt_mask(h);
                 uint32_t u = am + in - out;  // (-255, M+255), wrapped when negative
                 u = min(u, u + kMod);
@@ -842,19 +910,23 @@ __global__ __launch_bounds__(kT2) void k_scan_lds(ScanArgs a, uint32_t ntiles, u
 }
 
 // Tail rule (generator.rs:156-184): at p* = len - last_size (last_size < n), the
-// suffix matches the last basis block iff weak and strong equal.  One wave.
-__global__ void k_tail(const uint8_t* __restrict__ src, uint64_t len, uint64_t last_size, uint32_t want_weak,
-                       uint64_t want_strong, int* __restrict__ flag) {
-    const uint8_t* p = src + (len - last_size);
+// suffix matches the last basis block iff weak and strong are equal.  One wave per
+// job (file).
+__global__ void k_tail(const uint8_t* __restrict__ buf, const TailJob* __restrict__ jobs, uint32_t njobs,
+                       const uint32_t* __restrict__ weak, const uint64_t* __restrict__ strong, int* __restrict__ flag) {
+    const uint32_t j = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+    if (j >= njobs) return;
+    const TailJob J = jobs[j];
+    const uint8_t* p = buf + J.src;
     uint32_t wk;
     uint64_t st;
-    if (last_size > 240) {
-        wave_hash_long(p, last_size, wk, st);
+    if (J.last_size > 240) {
+        wave_hash_long(p, J.last_size, wk, st);
     } else {
         wk = 0; st = 0;
-        if ((threadIdx.x & 63) == 0) { wk = adler_scalar(p, last_size); st = xxh3_short(p, last_size); }
+        if ((threadIdx.x & 63) == 0) { wk = adler_scalar(p, J.last_size); st = xxh3_short(p, J.last_size); }
     }
-    if (threadIdx.x == 0) *flag = (wk == want_weak && st == want_strong) ? 1 : 0;
+    if ((threadIdx.x & 63) == 0) flag[j] = (wk == weak[J.blk] && st == strong[J.blk]) ? 1 : 0;
 }
 
 // ===========================================================================
@@ -932,24 +1004,24 @@ hipError_t launch_signature_batch(const uint8_t* d_buf, const uint64_t* d_off, c
     return hipGetLastError();
 }
 
-hipError_t launch_index_build(const uint32_t* d_weak, uint64_t n, DeviceIndex& ix, hipStream_t s, Profiler* prof) {
+hipError_t launch_index_build(const uint32_t* d_weak, DeviceIndex& ix, hipStream_t s, Profiler* prof) {
     hipError_t e;
-    const size_t nslots = (size_t)(ix.bmask + 1) * 4;
-    if ((e = hipMemsetAsync(ix.filt, 0, ((size_t)1 << ix.fwbits) * 4, s))) return e;
-    if ((e = hipMemsetAsync(ix.keys, 0xFF, nslots * 4, s))) return e;
-    if ((e = hipMemsetAsync(ix.cnt, 0, nslots * 4, s))) return e;
-    if ((e = hipMemsetAsync(ix.fill, 0, nslots * 4, s))) return e;
+    if ((e = hipMemsetAsync(ix.filt, 0, ix.fwords * 4, s))) return e;
+    if ((e = hipMemsetAsync(ix.keys, 0xFF, ix.nslots * 4, s))) return e;
+    if ((e = hipMemsetAsync(ix.cnt, 0, ix.nslots * 4, s))) return e;
+    if ((e = hipMemsetAsync(ix.fill, 0, ix.nslots * 4, s))) return e;
+    const uint64_t n = ix.nblocks;
     if (n == 0) return hipSuccess;
     {
         ProfScope ps(prof, s, "k_idx_insert");
-        hipLaunchKernelGGL(k_idx_insert, dim3(grid_for(n, 256)), dim3(256), 0, s, d_weak, n, ix.filt, 32 - ix.fwbits,
-                           ix.keys, ix.cnt, ix.bmask, ix.slot_of);
+        hipLaunchKernelGGL(k_idx_insert, dim3(grid_for(n, 256)), dim3(256), 0, s, d_weak, n, ix.d_fblk,
+                           (uint32_t)ix.nfiles, ix.d_files, ix.filt, ix.keys, ix.cnt, ix.slot_of);
     }
     size_t tmp = 0;
-    if ((e = hipcub::DeviceScan::ExclusiveSum(nullptr, tmp, ix.cnt, ix.start, (int)nslots, s))) return e;
+    if ((e = hipcub::DeviceScan::ExclusiveSum(nullptr, tmp, ix.cnt, ix.start, (int)ix.nslots, s))) return e;
     void* d_tmp = nullptr;
     if ((e = hipMallocAsync(&d_tmp, tmp ? tmp : 16, s))) return e;
-    e = hipcub::DeviceScan::ExclusiveSum(d_tmp, tmp, ix.cnt, ix.start, (int)nslots, s);
+    e = hipcub::DeviceScan::ExclusiveSum(d_tmp, tmp, ix.cnt, ix.start, (int)ix.nslots, s);
     (void)hipFreeAsync(d_tmp, s);
     if (e) return e;
     {
@@ -968,94 +1040,125 @@ size_t scan_lds_bytes(uint32_t n, uint32_t* nchunks_out) {
     return q_off + (size_t)(kScanThreads / 64) * (kFQ + kWQ) * sizeof(uint2);
 }
 
-uint64_t scan_tile_positions() { return kScanTile; }
-
+uint64_t scan_tile_positions() { return kTile2; }
+uint32_t scan_max_window() { return kMaxN2; }
 size_t scan_queue_entries() { return (size_t)kWgPerCu2 * 256 * (kT2 / 64) * kGFQ; }
 
-hipError_t launch_scan(const uint8_t* d_src, uint64_t len, uint64_t pos_begin, uint64_t pos_end, uint32_t n,
-                       const DeviceIndex& ix, const uint64_t* d_strong, HitRec* d_out, uint64_t out_cap,
-                       unsigned long long* d_counters, uint2* gfq, size_t gfq_cap, hipStream_t s, Profiler* prof) {
-    ScanArgs a;
+hipError_t launch_scan(const uint8_t* d_buf, const ScanSeg* d_segs, uint32_t nsegs, uint32_t ntiles, uint32_t n,
+                       const DeviceIndex& ix, const uint64_t* d_strong, uint64_t* d_hit_key, uint32_t* d_hit_val,
+                       uint64_t out_cap, unsigned long long* d_counters, uint2* gfq, size_t gfq_cap, hipStream_t s,
+                       Profiler* prof) {
+    if (n > kMaxN2 || n == 0) return hipErrorInvalidValue;
+    if (ntiles == 0) return hipSuccess;
+    ScanArgs a{};
+    a.src = d_buf;
+    a.n = n;
+    a.nm = n % kMod;
+    static const bool timing = getenv("SYDELTA_PHASE_TIMING") != nullptr;
+    a.timing = timing ? 1u : 0u;
+    a.segs = d_segs;
+    a.nsegs = nsegs;
+    a.ntiles = ntiles;
+    a.files = ix.d_files;
+    a.filt = ix.filt;
+    a.keys = ix.keys;
+    a.start = ix.start;
+    a.cnt = ix.cnt;
+    a.order = ix.order;
+    a.strong = d_strong;
+    a.hit_key = d_hit_key;
+    a.hit_val = d_hit_val;
+    a.out_cap = out_cap;
+    a.counters = d_counters;
+    const bool lds_filter = ix.max_fwords <= kLdsFilterWordsMax;
+    const uint32_t lds_fwords = lds_filter ? std::max<uint32_t>(ix.max_fwords, 4u) : 0u;
+    const Lds2 L = lds2_layout(n, lds_fwords);
+    // dynamic LDS above 64 KiB must be opted into
+    static std::once_flag attr_once;
+    static hipError_t attr_err = hipSuccess;
+    static int num_cus = 256;
+    std::call_once(attr_once, [] {
+        const int cap = 160 * 1024 / kWgPerCu2 - 512;
+        attr_err = hipFuncSetAttribute((const void*)k_scan_lds<true>, hipFuncAttributeMaxDynamicSharedMemorySize, cap);
+        if (attr_err == hipSuccess)
+            attr_err = hipFuncSetAttribute((const void*)k_scan_lds<false>,
+                                           hipFuncAttributeMaxDynamicSharedMemorySize, cap);
+        int dev = 0, cus = 0;
+        if (hipGetDevice(&dev) == hipSuccess &&
+            hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess && cus > 0)
+            num_cus = cus;
+    });
+    if (attr_err != hipSuccess) return attr_err;
+    if (L.total > 160u * 1024 / kWgPerCu2 - 512) return hipErrorInvalidValue;
+    // persistent: up to 2 workgroups per CU, each on a contiguous range of tiles
+    const uint32_t grid = (uint32_t)std::min<uint64_t>(ntiles, (uint64_t)num_cus * kWgPerCu2);
+    const uint32_t per = (ntiles + grid - 1) / grid;
+    if (!gfq || gfq_cap < (size_t)grid * (kT2 / 64) * kGFQ) return hipErrorInvalidValue;
+    a.gfq = gfq;
+    ProfScope ps(prof, s, "k_scan_lds");
+    if (lds_filter)
+        hipLaunchKernelGGL(k_scan_lds<true>, dim3(grid), dim3(kT2), L.total, s, a, per, lds_fwords);
+    else
+        hipLaunchKernelGGL(k_scan_lds<false>, dim3(grid), dim3(kT2), L.total, s, a, per, 0u);
+    return hipGetLastError();
+}
+
+hipError_t launch_scan_wide(const uint8_t* d_src, uint64_t len, uint64_t pos_begin, uint64_t pos_end, uint32_t seg_id,
+                            uint32_t n, const DeviceIndex& ix, const uint64_t* d_strong, uint64_t* d_hit_key,
+                            uint32_t* d_hit_val, uint64_t out_cap, unsigned long long* d_counters, hipStream_t s,
+                            Profiler* prof) {
+    if (ix.nfiles != 1) return hipErrorInvalidValue;
+    ScanArgs a{};
     a.src = d_src;
     a.len = len;
     a.pos_begin = pos_begin;
     a.pos_end = pos_end;
+    a.seg_id = seg_id;
     a.n = n;
     a.nm = n % kMod;
     a.c0 = 2 * kMod - 1 - (uint32_t)((255ull * a.nm) % kMod);
-    a.fwshift = 32 - ix.fwbits;
+    a.fwshift = ix.files[0].fwshift;
+    a.bmask = ix.files[0].bmask;
     a.filt = ix.filt;
     a.keys = ix.keys;
-    a.bmask = ix.bmask;
     const size_t lds = scan_lds_bytes(n, &a.nchunks);
     a.start = ix.start;
     a.cnt = ix.cnt;
     a.order = ix.order;
     a.strong = d_strong;
-    a.out = d_out;
+    a.hit_key = d_hit_key;
+    a.hit_val = d_hit_val;
     a.out_cap = out_cap;
     a.counters = d_counters;
-    static const bool timing = getenv("SYDELTA_PHASE_TIMING") != nullptr;
-    a.timing = timing ? 1u : 0u;
-    if (n <= kMaxN2) {
-        const bool lds_filter = (1u << ix.fwbits) <= kLdsFilterWordsMax;
-        const Lds2 L = lds2_layout(n, lds_filter ? (1u << ix.fwbits) : 0u);
-        const uint64_t tiles = (pos_end - pos_begin + kTile2 - 1) / kTile2;
-        // dynamic LDS above 64 KiB must be opted into
-        static std::once_flag attr_once;
-        static hipError_t attr_err = hipSuccess;
-        static int num_cus = 256;
-        std::call_once(attr_once, [] {
-            const int cap = 160 * 1024 / kWgPerCu2 - 512;
-            attr_err = hipFuncSetAttribute((const void*)k_scan_lds<true>, hipFuncAttributeMaxDynamicSharedMemorySize, cap);
-            if (attr_err == hipSuccess)
-                attr_err = hipFuncSetAttribute((const void*)k_scan_lds<false>,
-                                               hipFuncAttributeMaxDynamicSharedMemorySize, cap);
-            int dev = 0, cus = 0;
-            if (hipGetDevice(&dev) == hipSuccess &&
-                hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess && cus > 0)
-                num_cus = cus;
-        });
-        if (attr_err != hipSuccess) return attr_err;
-        if (L.total > 160u * 1024 / kWgPerCu2 - 512) return hipErrorInvalidValue;
-        const uint32_t grid = (uint32_t)std::min<uint64_t>(tiles, (uint64_t)num_cus * kWgPerCu2);
-        const uint32_t per = (uint32_t)((tiles + grid - 1) / grid);
-        if (!gfq || gfq_cap < (size_t)grid * (kT2 / 64) * kGFQ) return hipErrorInvalidValue;
-        a.gfq = gfq;
-        ProfScope ps(prof, s, "k_scan_lds");
-        if (lds_filter)
-            hipLaunchKernelGGL(k_scan_lds<true>, dim3(grid), dim3(kT2), L.total, s, a, (uint32_t)tiles, per);
-        else
-            hipLaunchKernelGGL(k_scan_lds<false>, dim3(grid), dim3(kT2), L.total, s, a, (uint32_t)tiles, per);
-        return hipGetLastError();
-    }
     const uint64_t tiles = (pos_end - pos_begin + kScanTile - 1) / kScanTile;
     ProfScope ps(prof, s, "k_scan");
     hipLaunchKernelGGL(k_scan, dim3((unsigned)tiles), dim3(kScanThreads), lds, s, a);
     return hipGetLastError();
 }
 
-hipError_t launch_sort_hits(HitRec* d_in, HitRec* d_tmp_out, uint64_t nhits, hipStream_t s, HitRec** sorted) {
-    // Sort (pos, block) records by pos: view each record as a u64 key (pos in low word).
-    // Radix sort on the low 32 bits only (pos); block index rides along in the high word.
-    *sorted = d_in;
+hipError_t launch_sort_hits(uint64_t* key, uint32_t* val, uint64_t* key_tmp, uint32_t* val_tmp, uint64_t nhits,
+                            int end_bit, hipStream_t s, uint64_t** key_out, uint32_t** val_out) {
+    *key_out = key;
+    *val_out = val;
     if (nhits <= 1) return hipSuccess;
     size_t tmp = 0;
     hipError_t e;
-    uint64_t* kin = (uint64_t*)d_in;
-    uint64_t* kout = (uint64_t*)d_tmp_out;
-    if ((e = hipcub::DeviceRadixSort::SortKeys(nullptr, tmp, kin, kout, (int)nhits, 0, 32, s))) return e;
+    if ((e = hipcub::DeviceRadixSort::SortPairs(nullptr, tmp, key, key_tmp, val, val_tmp, (int)nhits, 0, end_bit, s)))
+        return e;
     void* d_t = nullptr;
     if ((e = hipMallocAsync(&d_t, tmp ? tmp : 16, s))) return e;
-    e = hipcub::DeviceRadixSort::SortKeys(d_t, tmp, kin, kout, (int)nhits, 0, 32, s);
+    e = hipcub::DeviceRadixSort::SortPairs(d_t, tmp, key, key_tmp, val, val_tmp, (int)nhits, 0, end_bit, s);
     (void)hipFreeAsync(d_t, s);
-    *sorted = d_tmp_out;
+    *key_out = key_tmp;
+    *val_out = val_tmp;
     return e;
 }
 
-hipError_t launch_tail(const uint8_t* d_src, uint64_t len, uint64_t last_size, uint32_t want_weak, uint64_t want_strong,
-                       int* d_flag, hipStream_t s) {
-    hipLaunchKernelGGL(k_tail, dim3(1), dim3(64), 0, s, d_src, len, last_size, want_weak, want_strong, d_flag);
+hipError_t launch_tail(const uint8_t* d_buf, const TailJob* d_jobs, uint32_t njobs, const uint32_t* d_weak,
+                       const uint64_t* d_strong, int* d_flag, hipStream_t s) {
+    if (!njobs) return hipSuccess;
+    hipLaunchKernelGGL(k_tail, dim3(grid_for((uint64_t)njobs * 64, 256)), dim3(256), 0, s, d_buf, d_jobs, njobs, d_weak,
+                       d_strong, d_flag);
     return hipGetLastError();
 }
 

@@ -78,6 +78,22 @@ class Index:
             pass
 
 
+class BatchIndex(Index):
+    """Per-file probe tables for a batch of basis signatures (concatenated in file
+    order, as signature_batch returns them)."""
+
+    def __init__(self, weak: torch.Tensor, strong: torch.Tensor, nblocks, last_sizes, block_size: int,
+                 device: int = 0, stream=None):
+        self.h = ctypes.c_void_p()
+        nb = np.ascontiguousarray(nblocks, dtype=np.uint64)
+        ls = np.ascontiguousarray(last_sizes, dtype=np.uint64)
+        self.nfiles, self.block_size = len(nb), block_size
+        n = int(nb.sum())
+        check(lib.sydelta_index_create_batch(device, _ptr(weak) if n else None, _ptr(strong) if n else None,
+                                             nb.ctypes.data, ls.ctypes.data, len(nb), block_size, 1,
+                                             _stream(stream), ctypes.byref(self.h)))
+
+
 @dataclass
 class DeviceDelta:
     kind: np.ndarray   # 0 Copy, 1 Data
@@ -91,28 +107,48 @@ class DeviceDelta:
         return [("C" if int(k) == 0 else "D", int(x), int(y)) for k, x, y in zip(self.kind, self.a, self.b)]
 
 
+def _device_delta(h) -> DeviceDelta:
+    nops = int(lib.sydelta_delta_num_ops(h))
+    if nops:
+        p = lib.sydelta_delta_ops(h)
+        raw = np.ctypeslib.as_array(ctypes.cast(p, ctypes.POINTER(ctypes.c_uint64)), shape=(nops * 3,)).copy()
+        raw = raw.reshape(nops, 3)
+        kind = (raw[:, 0] & 0xFFFFFFFF).astype(np.uint8)
+        a, b = raw[:, 1].copy(), raw[:, 2].copy()
+    else:
+        kind = np.zeros(0, np.uint8)
+        a = np.zeros(0, np.uint64)
+        b = np.zeros(0, np.uint64)
+    st = _lib.MatchStatsC()
+    check(lib.sydelta_delta_stats(h, ctypes.byref(st)))
+    stats = {f: int(getattr(st, f)) for f, _ in _lib.MatchStatsC._fields_}
+    return DeviceDelta(kind, a, b, int(lib.sydelta_delta_source_size(h)), int(lib.sydelta_delta_block_size(h)), stats)
+
+
+def match_batch(index: BatchIndex, buf: torch.Tensor, offs, lens, stream=None):
+    """Batched rolling match: source f = buf[offs[f] : offs[f]+lens[f]] against basis f.
+    Returns (list of DeviceDelta, batch totals)."""
+    offs = np.ascontiguousarray(offs, dtype=np.uint64)
+    lens = np.ascontiguousarray(lens, dtype=np.uint64)
+    h = ctypes.c_void_p()
+    check(lib.sydelta_match_batch_device(index.h, _ptr(buf), offs.ctypes.data, lens.ctypes.data, len(lens),
+                                         _stream(stream), ctypes.byref(h)))
+    try:
+        out = [_device_delta(lib.sydelta_delta_batch_get(h, i)) for i in range(int(lib.sydelta_delta_batch_count(h)))]
+        st = _lib.MatchStatsC()
+        check(lib.sydelta_delta_batch_stats(h, ctypes.byref(st)))
+        return out, {f: int(getattr(st, f)) for f, _ in _lib.MatchStatsC._fields_}
+    finally:
+        lib.sydelta_delta_batch_free(h)
+
+
 def match(index: Index, src: torch.Tensor, stream=None, length: int | None = None) -> DeviceDelta:
     """Greedy rolling match of a device-resident source (generator.rs:242-379)."""
     n = src.numel() if length is None else length
     h = ctypes.c_void_p()
     check(lib.sydelta_match_device(index.h, _ptr(src) if n else None, n, _stream(stream), ctypes.byref(h)))
     try:
-        nops = int(lib.sydelta_delta_num_ops(h))
-        if nops:
-            p = lib.sydelta_delta_ops(h)
-            raw = np.ctypeslib.as_array(ctypes.cast(p, ctypes.POINTER(ctypes.c_uint64)), shape=(nops * 3,)).copy()
-            raw = raw.reshape(nops, 3)
-            kind = (raw[:, 0] & 0xFFFFFFFF).astype(np.uint8)
-            a, b = raw[:, 1].copy(), raw[:, 2].copy()
-        else:
-            kind = np.zeros(0, np.uint8)
-            a = np.zeros(0, np.uint64)
-            b = np.zeros(0, np.uint64)
-        st = _lib.MatchStatsC()
-        check(lib.sydelta_delta_stats(h, ctypes.byref(st)))
-        stats = {f: int(getattr(st, f)) for f, _ in _lib.MatchStatsC._fields_}
-        return DeviceDelta(kind, a, b, int(lib.sydelta_delta_source_size(h)), int(lib.sydelta_delta_block_size(h)),
-                           stats)
+        return _device_delta(h)
     finally:
         lib.sydelta_delta_free(h)
 

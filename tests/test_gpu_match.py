@@ -185,3 +185,79 @@ def test_config3_property_1gib(gpu):
     d2 = gpu.match(idx, basis)  # identical source: all Copy, in order
     assert d2.tuples() == [("C", i * bs, bs) for i in range(n // bs)]
     idx.close()
+
+
+def _batch_device(gpu, pairs, bs):
+    """Batched signature + index + match of (src, basis) pairs packed in two buffers
+    (16-byte aligned file starts)."""
+    import torch
+
+    def pack(parts):
+        offs, pos = [], 0
+        for p in parts:
+            offs.append(pos)
+            pos += (len(p) + 15) & ~15
+        buf = torch.zeros(pos + 16, dtype=torch.uint8, device="cuda")
+        host = bytearray(pos + 16)
+        for o, p in zip(offs, parts):
+            host[o:o + len(p)] = p
+        buf.copy_(torch.frombuffer(host, dtype=torch.uint8).cuda())
+        return buf, np.array(offs, np.uint64), np.array([len(p) for p in parts], np.uint64)
+
+    bbuf, boff, blen = pack([b for _, b in pairs])
+    sbuf, soff, slen = pack([s for s, _ in pairs])
+    w, s = gpu.signature_batch(bbuf, boff, blen, bs)
+    nblk = [-(-int(l) // bs) for l in blen]
+    last = [int(l) - (k - 1) * bs if k else 0 for l, k in zip(blen, nblk)]
+    idx = gpu.BatchIndex(w, s, nblk, last, bs)
+    out, tot = gpu.match_batch(idx, sbuf, soff, slen)
+    idx.close()
+    return out, tot
+
+
+def test_batch_matches_per_file_oracle(gpu, oracle_c):
+    """BASELINE config 4 path: many independent pairs in one launch give, per file,
+    exactly the op list sy's generate_delta would (generator.rs:242-379), including
+    empty sources, empty bases, sources shorter than a block and tail-rule files."""
+    rng = random.Random(4)
+    for bs in (4096, 64, 1000):
+        pairs = []
+        for i in range(120):
+            kind = i % 6
+            if kind == 0:
+                basis = rng.randbytes(rng.randint(0, 3 * bs))
+                src = b""
+            elif kind == 1:
+                basis = b""
+                src = rng.randbytes(rng.randint(0, 3 * bs))
+            elif kind == 2:
+                basis = rng.randbytes(rng.randint(1, 6) * bs + rng.randint(1, bs - 1))
+                src = rng.randbytes(rng.randint(0, bs)) + basis[-(len(basis) % bs):]
+            else:
+                basis = rng.randbytes(rng.randint(bs, 40 * bs))
+                src = _mutate(basis, rng, nops=10)
+            pairs.append((src, basis))
+        out, tot = _batch_device(gpu, pairs, bs)
+        assert len(out) == len(pairs)
+        for i, ((src, basis), d) in enumerate(zip(pairs, out)):
+            assert d.tuples() == _oracle_ops(oracle_c, src, basis, bs), (bs, i)
+            assert d.source_size == len(src)
+        assert tot["copy_ops"] == sum(d.stats["copy_ops"] for d in out)
+
+
+def test_batch_1mib_files_c4_shape(gpu, oracle_c):
+    """C4 shape (1 MiB files, one inserted byte + 16 substitutions each), 64 files."""
+    rng = random.Random(44)
+    pairs = []
+    for f in range(64):
+        basis = O.synth_bytes(1 << 20, 0x5E1D0004 + f).tobytes()
+        src = bytearray(basis)
+        p = rng.randrange(len(src))
+        src[p:p] = bytes([rng.randrange(256)])
+        for _ in range(16):
+            q = rng.randrange(len(src))
+            src[q] ^= 1 + rng.randrange(255)
+        pairs.append((bytes(src), basis))
+    out, _ = _batch_device(gpu, pairs, 4096)
+    for (src, basis), d in zip(pairs, out):
+        assert d.tuples() == _oracle_ops(oracle_c, src, basis, 4096)
