@@ -302,8 +302,10 @@ static int index_create_impl(int device, const uint32_t* weak, const uint64_t* s
         x->last_size[f] = nblk[f] ? last[f] : 0;
         const uint64_t nk = nblk[f] ? nblk[f] : 1;
         const uint32_t lk = ceil_log2(nk);
-        const uint32_t fwbits = nk <= kLdsFilterKeys ? std::min<uint32_t>(13, std::max<uint32_t>(6, lk + 2))
-                                                     : std::min<uint32_t>(28, lk - 1);
+        // <= 4 Ki keys: <= 16 KiB filter (3 scan workgroups per CU); <= 16 Ki keys: 32 KiB (2 per CU)
+        const uint32_t fwbits = nk <= 4096 ? std::min<uint32_t>(12, std::max<uint32_t>(6, lk + 2))
+                                : nk <= kLdsFilterKeys ? 13u
+                                                       : std::min<uint32_t>(28, lk - 1);
         const uint32_t bbits = std::max<uint32_t>(2, ceil_log2((nk + 1) / 2));
         FileIx& F = ix.files[f];
         F.filt_off = fw;
@@ -321,8 +323,8 @@ static int index_create_impl(int device, const uint32_t* weak, const uint64_t* s
     auto al = [](size_t v) { return (v + 255) & ~(size_t)255; };
     const size_t sz_weak = al(4 * nb), sz_strong = al(8 * nb), sz_filt = al(4 * fw), sz_t = al(4 * sl);
     const size_t sz_order = al(4 * nb), sz_slot = al(4 * nb), sz_files = al(sizeof(FileIx) * nfiles);
-    const size_t sz_fblk = al(8 * (nfiles + 1));
-    const size_t total = sz_weak + sz_strong + sz_filt + 4 * sz_t + sz_order + sz_slot + sz_files + sz_fblk;
+    const size_t sz_fblk = al(8 * (nfiles + 1)), sz_cstrong = al(8 * nb);
+    const size_t total = sz_weak + sz_strong + sz_filt + 4 * sz_t + sz_order + sz_slot + sz_files + sz_fblk + sz_cstrong;
     HIP_TRY(hipMalloc(&x->d_pool, total));
     uint8_t* p = (uint8_t*)x->d_pool;
     x->d_weak = (uint32_t*)p; p += sz_weak;
@@ -336,6 +338,7 @@ static int index_create_impl(int device, const uint32_t* weak, const uint64_t* s
     ix.slot_of = (uint32_t*)p; p += sz_slot;
     ix.d_files = (FileIx*)p; p += sz_files;
     ix.d_fblk = (uint64_t*)p; p += sz_fblk;
+    ix.cstrong = (uint64_t*)p; p += sz_cstrong;
     const hipMemcpyKind kind = arrays_on_device ? hipMemcpyDeviceToDevice : hipMemcpyHostToDevice;
     if (nblocks) {
         HIP_TRY(hipMemcpyAsync(x->d_weak, weak, 4 * nblocks, kind, s));
@@ -344,7 +347,7 @@ static int index_create_impl(int device, const uint32_t* weak, const uint64_t* s
     HIP_TRY(hipMemcpyAsync(ix.d_files, ix.files.data(), sizeof(FileIx) * nfiles, hipMemcpyHostToDevice, s));
     HIP_TRY(hipMemcpyAsync(ix.d_fblk, x->fblk.data(), 8 * (nfiles + 1), hipMemcpyHostToDevice, s));
     CallProf cp;
-    HIP_TRY(launch_index_build(x->d_weak, ix, s, cp.get()));
+    HIP_TRY(launch_index_build(x->d_weak, x->d_strong, ix, s, cp.get()));
     HIP_TRY(hipStreamSynchronize(s));  // host tables must outlive the copies
     *out = x.release();
     return SYDELTA_OK;

@@ -232,11 +232,37 @@ __device__ __forceinline__ uint32_t offw(int i) {
     return b | ((b + 1) << 8) | ((b + 2) << 16) | ((b + 3) << 24);
 }
 
-// Wave-cooperative Adler-32 + XXH3-64 of an arbitrary segment [p, p+len),
+// Byte sources for wave_hash_long: global memory, or a scan tile's LDS rows
+// (64-byte rows at a 17-dword stride, sydelta_kernels.hip k_scan_lds).
+struct GlobalBytes {
+    const uint8_t* p;
+    __device__ __forceinline__ void load64(uint64_t off, uint32_t x[16]) const { load64_unaligned(p + off, x); }
+    __device__ __forceinline__ uint32_t byte(uint64_t off) const { return p[off]; }
+};
+struct LdsRowBytes {
+    const uint32_t* rows;  // LDS
+    uint32_t base;         // tile offset of byte 0
+    __device__ __forceinline__ uint32_t dword(uint32_t d) const { return rows[(d >> 4) * 17 + (d & 15)]; }
+    __device__ __forceinline__ void load64(uint64_t off, uint32_t x[16]) const {
+        const uint32_t o = base + (uint32_t)off;
+        const uint32_t d0 = o >> 2, sh = o & 3;
+        uint32_t d[17];
+#pragma unroll
+        for (int i = 0; i < 17; ++i) d[i] = dword(d0 + i);
+#pragma unroll
+        for (int i = 0; i < 16; ++i) x[i] = __builtin_amdgcn_alignbyte(d[i + 1], d[i], sh);
+    }
+    __device__ __forceinline__ uint32_t byte(uint64_t off) const {
+        const uint32_t o = base + (uint32_t)off;
+        return (dword(o >> 2) >> (8 * (o & 3))) & 0xFF;
+    }
+};
+
+// Wave-cooperative Adler-32 + XXH3-64 of an arbitrary segment [0, len) of `src`,
 // len > 240.  Every lane of the wave must call it with the same arguments;
 // every lane returns the same result.
-__device__ __forceinline__ void wave_hash_long(const uint8_t* p, uint64_t len, uint32_t& weak_out,
-                                               uint64_t& strong_out) {
+template <class Src>
+__device__ __forceinline__ void wave_hash_src(const Src& src, uint64_t len, uint32_t& weak_out, uint64_t& strong_out) {
     const uint32_t lane = threadIdx.x & 63;
     const uint64_t nS = (len - 1) / 64;          // stripes consumed by the block loop
     const uint64_t nb_blocks = (len - 1) / 1024; // 1 KiB blocks followed by a scramble
@@ -251,7 +277,7 @@ __device__ __forceinline__ void wave_hash_long(const uint8_t* p, uint64_t len, u
         for (int i = 0; i < 8; ++i) c[i] = 0;
         if (s < nS) {
             uint32_t x[16];
-            load64_unaligned(p + 64 * s, x);
+            src.load64(64 * s, x);
             const uint32_t ks = (uint32_t)(s & 15);
             uint32_t S = 0, V = 0;
 #pragma unroll
@@ -289,7 +315,7 @@ __device__ __forceinline__ void wave_hash_long(const uint8_t* p, uint64_t len, u
     {
         const uint64_t o = 64 * nS + lane;
         if (o < len) {
-            const uint32_t xb = p[o];
+            const uint32_t xb = src.byte(o);
             asum += xb;
             bsum += (len - o) * (uint64_t)xb;
         }
@@ -297,7 +323,7 @@ __device__ __forceinline__ void wave_hash_long(const uint8_t* p, uint64_t len, u
     // last stripe (overlapping), identical in every lane
     {
         uint32_t x[16];
-        load64_unaligned(p + len - 64, x);
+        src.load64(len - 64, x);
 #pragma unroll
         for (int i = 0; i < 8; ++i) {
             const uint64_t v = (uint64_t)x[2 * i] | ((uint64_t)x[2 * i + 1] << 32);
@@ -315,6 +341,11 @@ __device__ __forceinline__ void wave_hash_long(const uint8_t* p, uint64_t len, u
     const uint32_t A = (uint32_t)((1 + asum) % kMod);
     const uint32_t B = (uint32_t)((len + bsum) % kMod);
     weak_out = (B << 16) | A;
+}
+
+__device__ __forceinline__ void wave_hash_long(const uint8_t* p, uint64_t len, uint32_t& weak_out,
+                                               uint64_t& strong_out) {
+    wave_hash_src(GlobalBytes{p}, len, weak_out, strong_out);
 }
 
 // splitmix64 finaliser used by the synthetic-data generator.

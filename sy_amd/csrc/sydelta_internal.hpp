@@ -46,7 +46,8 @@ struct DeviceIndex {
     uint32_t* cnt = nullptr;    // candidates per slot
     uint32_t* start = nullptr;  // exclusive prefix of cnt (global positions into order)
     uint32_t* fill = nullptr;   // scratch for the scatter
-    uint32_t* order = nullptr;  // global block indices grouped by slot, index order within a slot
+    uint32_t* order = nullptr;  // global block indices grouped by slot (any order within a slot)
+    uint64_t* cstrong = nullptr;  // strong hash of order[j]
     uint32_t* slot_of = nullptr;
     FileIx* d_files = nullptr;  // per-file offsets (device copy of files)
     uint64_t* d_fblk = nullptr; // block prefix over files, nfiles+1 entries
@@ -77,7 +78,8 @@ hipError_t launch_signature_batch(const uint8_t* d_buf, const uint64_t* d_off, c
                                   uint32_t* d_weak, uint64_t* d_strong, hipStream_t s, Profiler* prof);
 // Build filters + exact tables of every file of ix from the concatenated weak
 // values (ix.nblocks entries; ix.d_fblk / ix.d_files already on the device).
-hipError_t launch_index_build(const uint32_t* d_weak, DeviceIndex& ix, hipStream_t s, Profiler* prof);
+hipError_t launch_index_build(const uint32_t* d_weak, const uint64_t* d_strong, DeviceIndex& ix, hipStream_t s,
+                              Profiler* prof);
 uint64_t scan_tile_positions();  // positions per tile of the LDS-staged scan
 uint32_t scan_max_window();      // largest block size the LDS-staged scan handles
 // Scratch the LDS-staged scan needs: filter-pass queues, scan_queue_entries() uint2

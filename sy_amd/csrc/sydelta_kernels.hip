@@ -213,6 +213,11 @@ __global__ void k_idx_insert(const uint32_t* __restrict__ weak, uint64_t n, cons
     }
 }
 
+// Candidates grouped by slot.  The order inside a group is arbitrary (atomics):
+// generator.rs:127-133 takes the first candidate in index order whose strong
+// matches, which verification reproduces as the minimum matching block index.
+// cstrong mirrors order with the candidates' strong hashes so a verification
+// reads both in one round trip.
 __global__ void k_idx_scatter(uint64_t n, const uint32_t* __restrict__ slot_of, const uint32_t* __restrict__ start,
                               uint32_t* __restrict__ fill, uint32_t* __restrict__ order) {
     const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -220,6 +225,13 @@ __global__ void k_idx_scatter(uint64_t n, const uint32_t* __restrict__ slot_of, 
     const uint32_t s = slot_of[i];
     const uint32_t k = atomicAdd(&fill[s], 1u);
     order[start[s] + k] = (uint32_t)i;
+}
+
+__global__ void k_idx_cstrong(uint64_t n, const uint32_t* __restrict__ order, const uint64_t* __restrict__ strong,
+                              uint64_t* __restrict__ cstrong) {
+    const uint64_t j = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (j >= n) return;
+    cstrong[j] = strong[order[j]];
 }
 
 // Exact lookup: slot of weak value w, or -1.
@@ -286,7 +298,7 @@ struct ScanArgs {
     const uint32_t* start;
     const uint32_t* cnt;
     const uint32_t* order;
-    const uint64_t* strong;
+    const uint64_t* cstrong;  // strong hash of order[j]
     // outputs
     uint64_t* hit_key;   // (segment << 32) | position - segment start
     uint32_t* hit_val;   // global block index
@@ -380,8 +392,10 @@ __device__ __forceinline__ void lds_fence() { asm volatile("s_waitcnt lgkmcnt(0)
 
 // Verify every queued weak hit of this wave (wave-uniform loop): XXH3 of the
 // window, first candidate in index order with equal strong (generator.rs:127-153).
-__device__ __forceinline__ void drain_wq(const ScanArgs& a, const SegCtx& c, const uint2* wq, uint32_t nwq,
-                                         uint64_t tile_start) {
+// rows != nullptr: the tile's bytes are staged in LDS (k_scan_lds) and the window
+// is hashed from there.
+__device__ __forceinline__ void drain_wq(const ScanArgs& a, const SegCtx& c, uint2* wq, uint32_t nwq,
+                                         uint64_t tile_start, const uint32_t* rows = nullptr) {
     const uint32_t lane = threadIdx.x & 63;
     for (uint32_t i = 0; i < nwq; ++i) {
         const uint2 e = wq[i];  // {rel pos in tile, global table slot}
@@ -390,7 +404,10 @@ __device__ __forceinline__ void drain_wq(const ScanArgs& a, const SegCtx& c, con
         uint64_t st;
         if (a.n > 240) {
             uint32_t wk;
-            wave_hash_long(win, a.n, wk, st);
+            if (rows)
+                wave_hash_src(LdsRowBytes{rows, e.x}, a.n, wk, st);
+            else
+                wave_hash_long(win, a.n, wk, st);
         } else {
             st = 0;
             if (lane == 0) st = xxh3_short(win, a.n);
@@ -400,17 +417,35 @@ __device__ __forceinline__ void drain_wq(const ScanArgs& a, const SegCtx& c, con
         uint32_t best = 0xFFFFFFFFu;
         for (uint32_t j = lane; j < cn; j += 64) {
             const uint32_t bi = a.order[s0 + j];
-            if (a.strong[bi] == st) best = min(best, bi);
+            if (a.cstrong[s0 + j] == st) best = min(best, bi);
         }
 #pragma unroll
         for (int m = 1; m < 64; m <<= 1) best = min(best, (uint32_t)__shfl_xor((int)best, m, 64));
-        if (lane == 0 && best != 0xFFFFFFFFu) {
-            const unsigned long long k = atomicAdd(&a.counters[0], 1ull);
-            if (k < a.out_cap) {
-                a.hit_key[k] = ((uint64_t)c.seg_id << kSegShift) | (uint64_t)(uint32_t)(p - c.pos_begin);
-                a.hit_val[k] = best;
-            }
+        if (lane == 0) wq[i].y = best;  // verified block, or none
+    }
+    // one output reservation per wave: the counter is shared by the whole chip
+    lds_fence();
+    uint32_t nver = 0;
+    for (uint32_t base = 0; base < nwq; base += 64) {
+        const bool v = base + lane < nwq && wq[base + lane].y != 0xFFFFFFFFu;
+        nver += __popcll(__ballot(v));
+    }
+    if (!nver) return;
+    unsigned long long k0 = 0;
+    if (lane == 0) k0 = atomicAdd(&a.counters[0], (unsigned long long)nver);
+    k0 = shfl64(k0, 0);
+    for (uint32_t base = 0; base < nwq; base += 64) {
+        const uint32_t i = base + lane;
+        const uint2 e = i < nwq ? wq[i] : make_uint2(0, 0xFFFFFFFFu);
+        const bool v = e.y != 0xFFFFFFFFu;
+        const uint64_t m = __ballot(v);
+        const unsigned long long k = k0 + __popcll(m & ((1ull << lane) - 1));
+        if (v && k < a.out_cap) {
+            const uint64_t p = tile_start + e.x;
+            a.hit_key[k] = ((uint64_t)c.seg_id << kSegShift) | (uint64_t)(uint32_t)(p - c.pos_begin);
+            a.hit_val[k] = e.y;
         }
+        k0 += __popcll(m);
     }
 }
 
@@ -418,7 +453,8 @@ __device__ __forceinline__ void drain_wq(const ScanArgs& a, const SegCtx& c, con
 // (capacity WQ entries, verified in place when full).
 template <int WQ>
 __device__ __forceinline__ uint32_t drain_fq(const ScanArgs& a, const SegCtx& c, const uint2* fq, uint32_t nfq,
-                                             uint2* wq, uint32_t nwq, uint64_t tile_start) {
+                                             uint2* wq, uint32_t nwq, uint64_t tile_start,
+                                             unsigned long long& weak_hits) {
     const uint32_t lane = threadIdx.x & 63;
     for (uint32_t base = 0; base < nfq; base += 64) {
         const uint32_t i = base + lane;
@@ -431,7 +467,7 @@ __device__ __forceinline__ uint32_t drain_fq(const ScanArgs& a, const SegCtx& c,
         const bool hit = slot >= 0;
         const uint64_t m = __ballot(hit);
         const uint32_t cnt = __popcll(m);
-        if (cnt && lane == 0) atomicAdd(&a.counters[1], (unsigned long long)cnt);
+        weak_hits += cnt;
         if (cnt) {
             if (nwq + cnt > (uint32_t)WQ) {  // keep room: verify what is queued
                 lds_fence();
@@ -551,7 +587,7 @@ __global__ __launch_bounds__(kScanThreads) void k_scan(ScanArgs a) {
 #pragma unroll
     for (int k = 1; k < 64; k <<= 1) wave_npos = max(wave_npos, (uint32_t)__shfl_xor((int)wave_npos, k, 64));
     uint32_t nfq = 0, nwq = 0;
-    unsigned long long passes = 0;
+    unsigned long long passes = 0, weak_hits = 0;
 
     // ---- phase 4: roll
     for (uint32_t g = 0; g < wave_npos; g += 64) {
@@ -594,7 +630,7 @@ __global__ __launch_bounds__(kScanThreads) void k_scan(ScanArgs a) {
             if (nfq > (uint32_t)(kFQ - 64 * kBatch)) {
                 lds_fence();
                 passes += nfq;
-                nwq = drain_fq<kWQ>(a, sc, fq, nfq, wq, nwq, tile_start);
+                nwq = drain_fq<kWQ>(a, sc, fq, nfq, wq, nwq, tile_start, weak_hits);
                 nfq = 0;
                 lds_fence();
             }
@@ -602,10 +638,11 @@ __global__ __launch_bounds__(kScanThreads) void k_scan(ScanArgs a) {
     }
     lds_fence();
     passes += nfq;
-    nwq = drain_fq<kWQ>(a, sc, fq, nfq, wq, nwq, tile_start);
+    nwq = drain_fq<kWQ>(a, sc, fq, nfq, wq, nwq, tile_start, weak_hits);
     lds_fence();
     drain_wq(a, sc, wq, nwq, tile_start);
     if (lane == 0 && passes) atomicAdd(&a.counters[2], passes);
+    if (lane == 0 && weak_hits) atomicAdd(&a.counters[1], weak_hits);
 }
 
 // ===========================================================================
@@ -637,7 +674,7 @@ constexpr int kGFQ = 2048;               // filter-pass queue entries per wave (
 constexpr int kWQ2 = 128;                // weak-hit queue entries per wave (LDS)
 constexpr uint32_t kMaxN2 = 8192;        // largest window the LDS layout holds
 constexpr int kRowDw = 17;               // LDS row = 16 data dwords + 1 pad
-constexpr int kWgPerCu2 = 2;
+constexpr int kWgPerCuMax2 = 4;          // up to 4 workgroups per CU when the LDS layout fits
 
 struct Lds2 {
     uint32_t nch;
@@ -652,51 +689,171 @@ __host__ __device__ __forceinline__ Lds2 lds2_layout(uint32_t n, uint32_t filt_w
     o = (o + 15) & ~15u; L.pj = o; o += (L.nch + 1) * 8;
     L.ntab = o; o += 256 * 4;
     L.filt = o; o += filt_words * 4;
-    o = (o + 15) & ~15u; L.q = o; o += (kT2 / 64) * kWQ2 * 8;
+    o = (o + 15) & ~15u; L.q = o; o += (kT2 / 64) * kWQ2 * 16;
     L.total = o;
     return L;
 }
 
-// Exact lookups of the queued filter passes (64 per round; positions at or past
-// pos_end dropped here) and strong verification of the weak hits, verified when
-// wq cannot take another round and, if `final`, at the end.  Returns wq's fill.
-__device__ __forceinline__ uint32_t drain2(const ScanArgs& a, const SegCtx& c, const uint2* fq, uint32_t nfq,
-                                           uint2* wq, uint32_t nwq, uint64_t tile_start, bool final) {
+// k_scan_lds queues.  Filter passes (HBM, kGFQ per wave): {(tile - t_begin) << 14 |
+// position in tile, weak}; weak hits (LDS, kWQ2 per wave): {segment, position in
+// segment, global table slot, 0}.  Both are drained only when nearly full and at
+// the end of the workgroup's tiles, so no tile waits on the latency chain of a
+// lookup + verification; windows are hashed from global memory (L2-warm).
+static_assert(kTile2 == (1 << 14), "queue entries pack the position in 14 bits");
+
+// Segment holding tile t (tiles of a launch are laid out segment after segment).
+__device__ __forceinline__ uint32_t seg_of_tile(const ScanArgs& a, uint32_t t) {
+    uint32_t lo = 0, hi = a.nsegs;
+    while (hi - lo > 1) {
+        const uint32_t mid = (lo + hi) >> 1;
+        if (a.segs[mid].tile_base <= t) lo = mid; else hi = mid;
+    }
+    return lo;
+}
+
+// Verify the queued weak hits: XXH3 of each window, first candidate in index
+// order with equal strong (generator.rs:127-153); one output reservation per wave.
+// rows != nullptr (tile-flush mode): every queued hit lies in the current tile,
+// whose bytes are staged in LDS and whose segment is *cur; hash from LDS and take
+// the segment from registers.  Otherwise windows are hashed from global memory.
+// The candidate group of up to 64 hits is fetched with one round trip of
+// start/cnt and one of (order, cstrong), lane i serving hit i.
+__device__ __forceinline__ void verify3(const ScanArgs& a, uint4* wq, uint32_t nwq, const uint32_t* rows,
+                                        uint64_t tile_start, const SegCtx* cur) {
     const uint32_t lane = threadIdx.x & 63;
-    uint32_t base = 0;
-    __builtin_amdgcn_s_waitcnt(0);  // this wave's queue stores have reached L2
-    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
-    for (;;) {
-        while (base < nfq && nwq + 64 <= (uint32_t)kWQ2) {
-            const uint32_t i = base + lane;
-            int64_t slot = -1;
-            uint2 e = make_uint2(0, 0);
-            if (i < nfq) {
-                e.x = __builtin_nontemporal_load(&fq[i].x);
-                e.y = __builtin_nontemporal_load(&fq[i].y);
-                if (tile_start + e.x < c.pos_end) slot = table_find(c.keys, c.bmask, e.y);
-            }
-            const bool hit = slot >= 0;
-            const uint64_t m = __ballot(hit);
-            if (m) {
-                const uint32_t cnt = __popcll(m);
-                if (lane == 0) atomicAdd(&a.counters[1], (unsigned long long)cnt);
-                if (hit) wq[nwq + __popcll(m & ((1ull << lane) - 1))] = make_uint2(e.x, (uint32_t)(c.slot_off + slot));
-                nwq += cnt;
-            }
-            base += 64;
+    for (uint32_t base = 0; base < nwq; base += 64) {
+        const uint32_t cnt_here = min(64u, nwq - base);
+        // lane i: candidate group of hit base+i, first candidate
+        uint32_t s0 = 0, cn = 0, b0 = 0xFFFFFFFFu;
+        uint64_t st0 = 0;
+        if (lane < cnt_here) {
+            const uint32_t slot = wq[base + lane].z;
+            s0 = a.start[slot];
+            cn = a.cnt[slot];
+            b0 = a.order[s0];
+            st0 = a.cstrong[s0];
         }
-        const bool done = base >= nfq;
-        if (done && !final) return nwq;
-        lds_fence();
-        drain_wq(a, c, wq, nwq, tile_start);
-        nwq = 0;
-        if (done) return 0;
+        for (uint32_t k = 0; k < cnt_here; ++k) {
+            const uint4 e = wq[base + k];  // {segment, position in segment, global slot, -}
+            uint64_t st;
+            if (a.n > 240) {
+                uint32_t wk;
+                if (rows) {
+                    wave_hash_src(LdsRowBytes{rows, (uint32_t)(cur->pos_begin + e.y - tile_start)}, a.n, wk, st);
+                } else {
+                    const ScanSeg S = a.segs[e.x];
+                    wave_hash_long(a.src + S.src + S.pos_begin + e.y, a.n, wk, st);
+                }
+            } else {
+                const uint8_t* win = rows ? cur->base + cur->pos_begin + e.y
+                                          : a.src + a.segs[e.x].src + a.segs[e.x].pos_begin + e.y;
+                st = 0;
+                if (lane == 0) st = xxh3_short(win, a.n);
+                st = shfl64(st, 0);
+            }
+            const uint32_t kcn = (uint32_t)__shfl((int)cn, k, 64);
+            uint32_t best = 0xFFFFFFFFu;
+            if (kcn == 1) {  // the usual case: the one candidate was fetched above
+                if (shfl64(st0, k) == st) best = (uint32_t)__shfl((int)b0, k, 64);
+            } else {
+                const uint32_t ks0 = (uint32_t)__shfl((int)s0, k, 64);
+                for (uint32_t j = lane; j < kcn; j += 64) {
+                    const uint32_t bi = a.order[ks0 + j];
+                    if (a.cstrong[ks0 + j] == st) best = min(best, bi);
+                }
+#pragma unroll
+                for (int m = 1; m < 64; m <<= 1) best = min(best, (uint32_t)__shfl_xor((int)best, m, 64));
+            }
+            if (lane == 0) wq[base + k].w = best;  // verified block, or none
+        }
+    }
+    lds_fence();
+    uint32_t nver = 0;
+    for (uint32_t base = 0; base < nwq; base += 64) {
+        const bool v = base + lane < nwq && wq[base + lane].w != 0xFFFFFFFFu;
+        nver += __popcll(__ballot(v));
+    }
+    if (!nver) return;
+    unsigned long long k0 = 0;
+    if (lane == 0) k0 = atomicAdd(&a.counters[0], (unsigned long long)nver);
+    k0 = shfl64(k0, 0);
+    for (uint32_t base = 0; base < nwq; base += 64) {
+        const uint32_t i = base + lane;
+        const uint4 e = i < nwq ? wq[i] : make_uint4(0, 0, 0, 0xFFFFFFFFu);
+        const bool v = e.w != 0xFFFFFFFFu;
+        const uint64_t m = __ballot(v);
+        const unsigned long long k = k0 + __popcll(m & ((1ull << lane) - 1));
+        if (v && k < a.out_cap) {
+            a.hit_key[k] = ((uint64_t)e.x << kSegShift) | e.y;
+            a.hit_val[k] = e.w;
+        }
+        k0 += __popcll(m);
     }
 }
 
+// Exact lookups of the queued filter passes, 64 per round (positions at or past
+// the segment end are dropped here); weak hits go to wq and are verified when it
+// cannot take another round, and at the end.
+__device__ __forceinline__ void drain3(const ScanArgs& a, const uint2* fq, uint32_t nfq, uint4* wq, uint32_t t_begin,
+                                       unsigned long long& weak_hits, const uint32_t* rows = nullptr,
+                                       uint64_t tile_start = 0, const SegCtx* cur = nullptr) {
+    const uint32_t lane = threadIdx.x & 63;
+    __builtin_amdgcn_s_waitcnt(0);  // this wave's queue stores have reached L2
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
+    uint32_t nwq = 0;
+    for (uint32_t base = 0; base < nfq; base += 64) {
+        const uint32_t i = base + lane;
+        int64_t slot = -1;
+        uint32_t si = 0, rp = 0, fslot = 0;
+        if (i < nfq) {
+            const uint32_t ex = __builtin_nontemporal_load(&fq[i].x);
+            const uint32_t ew = __builtin_nontemporal_load(&fq[i].y);
+            if (cur) {  // tile-flush mode: every entry is from the current tile
+                const uint64_t p = tile_start + (ex & (kTile2 - 1));
+                si = cur->seg_id;
+                if (p < cur->pos_end) {
+                    slot = table_find(cur->keys, cur->bmask, ew);
+                    fslot = (uint32_t)cur->slot_off;
+                }
+                rp = (uint32_t)(p - cur->pos_begin);
+            } else {
+                const uint32_t t = t_begin + (ex >> 14);
+                si = seg_of_tile(a, t);
+                const ScanSeg S = a.segs[si];
+                const uint64_t p = S.pos_begin + (uint64_t)(t - S.tile_base) * kTile2 + (ex & (kTile2 - 1));
+                if (p < S.pos_end) {
+                    const FileIx F = a.files[S.file];
+                    slot = table_find(a.keys + F.slot_off, F.bmask, ew);
+                    fslot = (uint32_t)F.slot_off;
+                }
+                rp = (uint32_t)(p - S.pos_begin);
+            }
+        }
+        const bool hit = slot >= 0;
+        const uint64_t m = __ballot(hit);
+        if (!m) continue;
+        const uint32_t cnt = __popcll(m);
+        weak_hits += cnt;
+        if (nwq + cnt > (uint32_t)kWQ2) {
+            lds_fence();
+            verify3(a, wq, nwq, rows, tile_start, cur);
+            nwq = 0;
+        }
+        if (hit) wq[nwq + __popcll(m & ((1ull << lane) - 1))] = make_uint4(si, rp, fslot + (uint32_t)slot, 0);
+        nwq += cnt;
+    }
+    lds_fence();
+    verify3(a, wq, nwq, rows, tile_start, cur);
+    lds_fence();
+}
+
 template <bool kLdsFilter>
-__global__ __launch_bounds__(kT2) void k_scan_lds(ScanArgs a, uint32_t per, uint32_t lds_fwords) {
+__global__ __launch_bounds__(kT2, kLdsFilter ? 3 : 4) void k_scan_lds(ScanArgs a, uint32_t per, uint32_t lds_fwords) {
+    // Large indexes (filter in HBM/L2) come with dense Adler false hits (C3: ~1 per
+    // 1000 positions): their verification runs at the end of every tile, hashing the
+    // windows from LDS.  Small indexes have rare hits: queue across tiles, verify
+    // from global memory when the queue fills and at the end.
+    constexpr bool kTileFlush = !kLdsFilter;
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     const uint32_t n = a.n;
     const Lds2 L = lds2_layout(n, kLdsFilter ? lds_fwords : 0u);
@@ -708,7 +865,7 @@ __global__ __launch_bounds__(kT2) void k_scan_lds(ScanArgs a, uint32_t per, uint
     uint32_t* lfilt = (uint32_t*)(smem + L.filt);
     const uint32_t tid = threadIdx.x;
     const uint32_t lane = tid & 63, wid = tid >> 6;
-    uint2* wq = (uint2*)(smem + L.q) + (size_t)wid * kWQ2;
+    uint4* wq = (uint4*)(smem + L.q) + (size_t)wid * kWQ2;
     uint2* fq = a.gfq + ((size_t)blockIdx.x * (kT2 / 64) + wid) * kGFQ;
     __shared__ uint32_t red_s[kT2 / 64], red_v[kT2 / 64];
     __shared__ uint64_t red_j[kT2 / 64];
@@ -721,7 +878,8 @@ __global__ __launch_bounds__(kT2) void k_scan_lds(ScanArgs a, uint32_t per, uint
     for (uint32_t i = tid; i < 256; i += kT2) ntab[i] = kMod - 1 - (a.nm * i) % kMod;
     const uint32_t sh = n & 3;
     const uint32_t rel0 = tid * kR2;
-    unsigned long long passes = 0;
+    unsigned long long passes = 0, weak_hits = 0;
+    uint32_t nfq = 0;
     uint32_t cur_file = 0xFFFFFFFFu;
     uint32_t fwshift = 0;
     const uint32_t* gfilt = a.filt;
@@ -842,21 +1000,18 @@ __global__ __launch_bounds__(kT2) void k_scan_lds(ScanArgs a, uint32_t per, uint
         PHASE_MARK(1)
 
         // ---- phase 4: roll 64 positions in batches of kB2.  Positions at or past
-        // pos_end (last tile only) are rolled like the others and dropped by drain2's
-        // bound check, so the hot loop carries no bound test.  The pass queue is
-        // drained at the top of a batch when it could not take a full batch, and by
-        // the extra iteration g == kR2 at the end of the tile: one drain2 site.
-        uint32_t nfq = 0, nwq = 0;
+        // pos_end (last tile of a segment) are rolled like the others and dropped by
+        // drain3's bound check, so the hot loop carries no bound test.  The pass queue
+        // is drained at the top of a batch when it could not take a full batch.
+        const uint32_t qtile = (tile - t_begin) << 14;
 #pragma unroll 1
-        for (uint32_t g = 0; g <= (uint32_t)kR2; g += kB2) {
-            const bool flush = g == (uint32_t)kR2;
-            if (flush) PHASE_MARK(2)
-            if ((flush && (nfq | nwq)) || nfq > (uint32_t)(kGFQ - 64 * kB2)) {
+        for (uint32_t g = 0; g < (uint32_t)kR2; g += kB2) {
+            if (nfq > (uint32_t)(kGFQ - 64 * kB2)) {
                 passes += nfq;
-                nwq = drain2(a, sc, fq, nfq, wq, nwq, tile_start, flush);
+                drain3(a, fq, nfq, wq, t_begin, weak_hits, kTileFlush ? rows : nullptr, tile_start,
+                       kTileFlush ? &sc : nullptr);
                 nfq = 0;
             }
-            if (flush) break;
             uint32_t xo[4], xi[4];
 #pragma unroll
             for (int j = 0; j < 4; ++j) xo[j] = rows[tid * kRowDw + (g >> 2) + j];
@@ -895,16 +1050,25 @@ __global__ __launch_bounds__(kT2) void k_scan_lds(ScanArgs a, uint32_t per, uint
                 const bool pass = (fm[t] & ~fw[t]) == 0;
                 const uint64_t mk = __ballot(pass);
                 if (mk) {
-                    if (pass) fq[nfq + __popcll(mk & ((1ull << lane) - 1))] = make_uint2(rel0 + g + t, wv[t]);
+                    if (pass) fq[nfq + __popcll(mk & ((1ull << lane) - 1))] = make_uint2(qtile | (rel0 + g + t), wv[t]);
                     nfq += __popcll(mk);
                 }
             }
         }
+        PHASE_MARK(2)
+        if (kTileFlush && nfq) {  // dense weak hits: verify while the tile is in LDS
+            passes += nfq;
+            drain3(a, fq, nfq, wq, t_begin, weak_hits, rows, tile_start, &sc);
+            nfq = 0;
+        }
         __syncthreads();  // rows / prefix arrays are rewritten by the next tile
         PHASE_MARK(3)
     }
+    passes += nfq;
+    drain3(a, fq, nfq, wq, t_begin, weak_hits);
 #undef PHASE_MARK
     if (lane == 0 && passes) atomicAdd(&a.counters[2], passes);
+    if (lane == 0 && weak_hits) atomicAdd(&a.counters[1], weak_hits);
     if (a.timing && tid == 0)
         for (int k = 0; k < 4; ++k) atomicAdd(&a.counters[4 + k], tm[k]);
 }
@@ -1004,7 +1168,8 @@ hipError_t launch_signature_batch(const uint8_t* d_buf, const uint64_t* d_off, c
     return hipGetLastError();
 }
 
-hipError_t launch_index_build(const uint32_t* d_weak, DeviceIndex& ix, hipStream_t s, Profiler* prof) {
+hipError_t launch_index_build(const uint32_t* d_weak, const uint64_t* d_strong, DeviceIndex& ix, hipStream_t s,
+                              Profiler* prof) {
     hipError_t e;
     if ((e = hipMemsetAsync(ix.filt, 0, ix.fwords * 4, s))) return e;
     if ((e = hipMemsetAsync(ix.keys, 0xFF, ix.nslots * 4, s))) return e;
@@ -1029,6 +1194,8 @@ hipError_t launch_index_build(const uint32_t* d_weak, DeviceIndex& ix, hipStream
         hipLaunchKernelGGL(k_idx_scatter, dim3(grid_for(n, 256)), dim3(256), 0, s, n, ix.slot_of, ix.start, ix.fill,
                            ix.order);
     }
+    if ((e = hipGetLastError())) return e;
+    hipLaunchKernelGGL(k_idx_cstrong, dim3(grid_for(n, 256)), dim3(256), 0, s, n, ix.order, d_strong, ix.cstrong);
     return hipGetLastError();
 }
 
@@ -1042,7 +1209,7 @@ size_t scan_lds_bytes(uint32_t n, uint32_t* nchunks_out) {
 
 uint64_t scan_tile_positions() { return kTile2; }
 uint32_t scan_max_window() { return kMaxN2; }
-size_t scan_queue_entries() { return (size_t)kWgPerCu2 * 256 * (kT2 / 64) * kGFQ; }
+size_t scan_queue_entries() { return (size_t)kWgPerCuMax2 * 256 * (kT2 / 64) * kGFQ; }
 
 hipError_t launch_scan(const uint8_t* d_buf, const ScanSeg* d_segs, uint32_t nsegs, uint32_t ntiles, uint32_t n,
                        const DeviceIndex& ix, const uint64_t* d_strong, uint64_t* d_hit_key, uint32_t* d_hit_val,
@@ -1065,7 +1232,7 @@ hipError_t launch_scan(const uint8_t* d_buf, const ScanSeg* d_segs, uint32_t nse
     a.start = ix.start;
     a.cnt = ix.cnt;
     a.order = ix.order;
-    a.strong = d_strong;
+    a.cstrong = ix.cstrong;
     a.hit_key = d_hit_key;
     a.hit_val = d_hit_val;
     a.out_cap = out_cap;
@@ -1078,7 +1245,7 @@ hipError_t launch_scan(const uint8_t* d_buf, const ScanSeg* d_segs, uint32_t nse
     static hipError_t attr_err = hipSuccess;
     static int num_cus = 256;
     std::call_once(attr_once, [] {
-        const int cap = 160 * 1024 / kWgPerCu2 - 512;
+        const int cap = 160 * 1024 / 2 - 512;
         attr_err = hipFuncSetAttribute((const void*)k_scan_lds<true>, hipFuncAttributeMaxDynamicSharedMemorySize, cap);
         if (attr_err == hipSuccess)
             attr_err = hipFuncSetAttribute((const void*)k_scan_lds<false>,
@@ -1089,10 +1256,16 @@ hipError_t launch_scan(const uint8_t* d_buf, const ScanSeg* d_segs, uint32_t nse
             num_cus = cus;
     });
     if (attr_err != hipSuccess) return attr_err;
-    if (L.total > 160u * 1024 / kWgPerCu2 - 512) return hipErrorInvalidValue;
-    // persistent: up to 2 workgroups per CU, each on a contiguous range of tiles
-    const uint32_t grid = (uint32_t)std::min<uint64_t>(ntiles, (uint64_t)num_cus * kWgPerCu2);
+    if (L.total > 160u * 1024 / 2 - 512) return hipErrorInvalidValue;
+    // persistent: 2-4 workgroups per CU, as many as the LDS layout allows (launch
+    // bounds hold the LDS-filter kernel to 3 waves per SIMD, the other to 4), each on a
+    // contiguous range of tiles
+    const uint32_t wg_per_cu = (!lds_filter && L.total <= 160u * 1024 / 4 - 512) ? 4u
+                               : L.total <= 160u * 1024 / 3 - 512           ? 3u
+                                                                            : 2u;
+    const uint32_t grid = (uint32_t)std::min<uint64_t>(ntiles, (uint64_t)num_cus * wg_per_cu);
     const uint32_t per = (ntiles + grid - 1) / grid;
+    if (per >= (1u << 18)) return hipErrorInvalidValue;  // queue entries pack (tile - t_begin) in 18 bits
     if (!gfq || gfq_cap < (size_t)grid * (kT2 / 64) * kGFQ) return hipErrorInvalidValue;
     a.gfq = gfq;
     ProfScope ps(prof, s, "k_scan_lds");
@@ -1125,7 +1298,7 @@ hipError_t launch_scan_wide(const uint8_t* d_src, uint64_t len, uint64_t pos_beg
     a.start = ix.start;
     a.cnt = ix.cnt;
     a.order = ix.order;
-    a.strong = d_strong;
+    a.cstrong = ix.cstrong;
     a.hit_key = d_hit_key;
     a.hit_val = d_hit_val;
     a.out_cap = out_cap;
