@@ -8,7 +8,8 @@
  *
  * Conventions
  *  - Plain pointers and sizes only; no torch / HIP types in signatures.  A
- *    `void *stream` is a hipStream_t (NULL = the library's own per-call stream).
+ *    `void *stream` is a hipStream_t (NULL = the library's per-thread stream, created
+ *    blocking so it is ordered against work on the legacy default stream).
  *  - Return value: SYDELTA_OK (0) or a negative SYDELTA_E_* code; the message
  *    of the last failure on the calling thread is sydelta_last_error().  This
  *    mirrors the reference's io::Result: I/O failures -> SYDELTA_E_IO
@@ -210,6 +211,41 @@ int sydelta_delta_batch_stats(const sydelta_delta_batch *b, sydelta_match_stats 
 void sydelta_delta_batch_free(sydelta_delta_batch *b);
 
 /* ---------------------------------------------------------------------------
+ * Chunk-sharded match of ONE large file over several devices (BASELINE config 5,
+ * SURVEY.md §8e).  Not a reference entry point: it splits generate_delta
+ * (generator.rs:242-379) of one (source, signature) pair at block-aligned chunk
+ * boundaries so each rank classifies its own chunk against the all-gathered
+ * signature (file 0 of idx, global block indices).  The walks are then chained:
+ * chunk 0 is walked from 0; chunk g from the exit of chunk g-1 (which may lie up to
+ * block_size-1 bytes inside chunk g after a Copy); the per-chunk deltas joined with
+ * sydelta_delta_append equal generate_delta's op list for the whole file.
+ *
+ * d_buf holds source bytes [buf_pos, buf_pos + buf_len) in device memory (16-byte
+ * aligned; buf_pos a multiple of 16 and <= pos_begin rounded down to 16).  The chunk
+ * classifies full-window positions [pos_begin, min(pos_end, file_len-block_size+1));
+ * pos_begin is a multiple of block_size.  The buffer must reach byte
+ * min(file_len, pos_end + block_size - 1), or file_len for the chunk holding the
+ * file's last full window (pos_end >= file_len - block_size + 1), which also
+ * applies the tail rule (generator.rs:156-184).  The buffer must stay valid until
+ * sydelta_chunk_free: a walk that jumps into a block classified only by its aligned
+ * window scans that block on demand.
+ * ------------------------------------------------------------------------- */
+typedef struct sydelta_chunk sydelta_chunk;
+int sydelta_chunk_classify(sydelta_index *idx, const uint8_t *d_buf, uint64_t buf_pos, uint64_t buf_len,
+                           uint64_t file_len, uint64_t pos_begin, uint64_t pos_end, void *stream,
+                           sydelta_chunk **out);
+/* Greedy walk from entry (>= pos_begin).  *out: the ops for [entry, *exit_pos); a
+ * non-final chunk ends with its literal run up to its last position (continued by
+ * the next chunk's leading Data op), a final chunk ends at file_len. */
+int sydelta_chunk_walk(sydelta_chunk *c, uint64_t entry, uint64_t *exit_pos, sydelta_delta **out);
+void sydelta_chunk_free(sydelta_chunk *c);
+/* Empty delta (Delta { ops: [], source_size, block_size }) to append chunk deltas to. */
+sydelta_delta *sydelta_delta_new(uint64_t source_size, uint64_t block_size);
+/* dst.ops += src.ops, merging dst's trailing Data op with src's leading Data op when
+ * they are contiguous (literal runs stay maximal, generator.rs:186-197). */
+int sydelta_delta_append(sydelta_delta *dst, const sydelta_delta *src);
+
+/* ---------------------------------------------------------------------------
  * Measurement support (used by bench.py; not part of the reference API).
  * ------------------------------------------------------------------------- */
 /* When on, the library records a HIP event pair around every kernel it
@@ -225,6 +261,16 @@ int sydelta_synth_fill(uint8_t *d_buf, uint64_t len, uint64_t seed, void *stream
  * rate_ppm / 1e6, by a different uniform byte (BASELINE config 3). */
 int sydelta_synth_mutate(uint8_t *d_dst, const uint8_t *d_src, uint64_t len, uint64_t seed, uint32_t rate_ppm,
                          void *stream);
+
+/* Ranged forms for sharded inputs: bytes [first, first + len) of the same streams
+ * (first a multiple of 8 for fill). */
+int sydelta_synth_fill_range(uint8_t *d_buf, uint64_t first, uint64_t len, uint64_t seed, void *stream);
+/* BASELINE config 5 edit model: d_dst = d_src with, in each block_size-aligned block
+ * k (global index) selected with probability rate_ppm / 1e6, one byte at a
+ * pseudo-random offset replaced by a different byte.  d_src/d_dst hold bytes
+ * [first, first + len), first a multiple of block_size. */
+int sydelta_synth_mutate_blocks(uint8_t *d_dst, const uint8_t *d_src, uint64_t first, uint64_t len,
+                                uint64_t block_size, uint64_t seed, uint32_t rate_ppm, void *stream);
 
 #ifdef __cplusplus
 }

@@ -272,18 +272,43 @@ def compression_ratio(ops) -> float:
 # --------------------------------------------------------------------------
 # Synthetic inputs: counter-based splitmix64 (parallel-friendly stand-in for §8d PRNG)
 # --------------------------------------------------------------------------
-def synth_bytes(n: int, seed: int) -> np.ndarray:
-    """Deterministic uniform bytes; identical to sy_amd's device generator
-    (counter-based splitmix64 of (seed, word index), little-endian words)."""
-    nw = (n + 7) // 8
-    idx = np.arange(nw, dtype=np.uint64)
+def splitmix_words(idx: np.ndarray, seed: int) -> np.ndarray:
+    """Counter-based splitmix64 of (seed, idx) (sydelta_device.hpp splitmix_word)."""
+    idx = np.asarray(idx, dtype=np.uint64)
     with np.errstate(over="ignore"):
         z = idx * np.uint64(0x9E3779B97F4A7C15) + np.uint64(seed & 0xFFFFFFFFFFFFFFFF) * np.uint64(0xD1B54A32D192ED03)
         z = z + np.uint64(0x9E3779B97F4A7C15)
         z = (z ^ (z >> np.uint64(30))) * np.uint64(0xBF58476D1CE4E5B9)
         z = (z ^ (z >> np.uint64(27))) * np.uint64(0x94D049BB133111EB)
         z = z ^ (z >> np.uint64(31))
+    return z
+
+
+def synth_bytes(n: int, seed: int, first: int = 0) -> np.ndarray:
+    """Deterministic uniform bytes [first, first + n) of the stream; identical to
+    sy_amd's device generator (counter-based splitmix64 of (seed, word index),
+    little-endian words).  first must be a multiple of 8."""
+    assert first % 8 == 0
+    nw = (n + 7) // 8
+    z = splitmix_words(np.arange(first // 8, first // 8 + nw, dtype=np.uint64), seed)
     return z.view(np.uint8)[:n].copy()
+
+
+def synth_edit_blocks(src: np.ndarray, first: int, bs: int, seed: int, rate_ppm: int) -> np.ndarray:
+    """BASELINE C5 edit model (sydelta_synth_mutate_blocks): in each selected
+    block-aligned block one byte is replaced by a different byte."""
+    out = np.array(src, dtype=np.uint8, copy=True)
+    nb = -(-len(out) // bs)
+    k = np.arange(first // bs, first // bs + nb, dtype=np.uint64)
+    r = splitmix_words(k, seed)
+    thresh = (rate_ppm << 32) // 1000000
+    sel = np.nonzero((r & np.uint64(0xFFFFFFFF)) < np.uint64(thresh))[0]
+    for t in sel:
+        o = int(t) * bs + int(r[t] >> np.uint64(32)) % bs
+        if o < len(out):
+            x = 1 + int(splitmix_words(np.array([k[t]], dtype=np.uint64), ~seed & 0xFFFFFFFFFFFFFFFF)[0]) % 255
+            out[o] ^= x
+    return out
 
 
 # --------------------------------------------------------------------------

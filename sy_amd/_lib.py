@@ -82,10 +82,17 @@ SIGNATURES = [
     ("sydelta_delta_batch_get", _vp, [_vp, _u64]),
     ("sydelta_delta_batch_stats", _i, [_vp, ctypes.POINTER(MatchStatsC)]),
     ("sydelta_delta_batch_free", None, [_vp]),
+    ("sydelta_chunk_classify", _i, [_vp, _vp, _u64, _u64, _u64, _u64, _u64, _vp, _pp]),
+    ("sydelta_chunk_walk", _i, [_vp, _u64, ctypes.POINTER(_u64), _pp]),
+    ("sydelta_chunk_free", None, [_vp]),
+    ("sydelta_delta_new", _vp, [_u64, _u64]),
+    ("sydelta_delta_append", _i, [_vp, _vp]),
     ("sydelta_set_profiling", None, [_i]),
     ("sydelta_profile_json", ctypes.c_size_t, [ctypes.c_char_p, ctypes.c_size_t, _i]),
     ("sydelta_synth_fill", _i, [_vp, _u64, _u64, _vp]),
     ("sydelta_synth_mutate", _i, [_vp, _vp, _u64, _u64, _u32, _vp]),
+    ("sydelta_synth_fill_range", _i, [_vp, _u64, _u64, _u64, _vp]),
+    ("sydelta_synth_mutate_blocks", _i, [_vp, _vp, _u64, _u64, _u64, _u64, _u32, _vp]),
 ]
 
 

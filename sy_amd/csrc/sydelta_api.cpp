@@ -16,6 +16,7 @@
 #include <sys/stat.h>
 
 #include <algorithm>
+#include <array>
 #include <atomic>
 #include <cmath>
 #include <map>
@@ -99,13 +100,15 @@ int ensure_device(int device) {
     return SYDELTA_OK;
 }
 
-// one non-blocking stream per (thread, device): calls on different threads never share a stream
+// one stream per (thread, device): calls on different threads never share a stream
 hipStream_t thread_stream(int device) {
     static thread_local std::map<int, hipStream_t> streams;
     auto it = streams.find(device);
     if (it != streams.end()) return it->second;
     hipStream_t s = nullptr;
-    if (hipStreamCreateWithFlags(&s, hipStreamNonBlocking) != hipSuccess) return nullptr;
+    // blocking: orders against work on the legacy default stream (torch's default
+    // stream), so buffers a caller filled there are complete before our kernels read them
+    if (hipStreamCreateWithFlags(&s, hipStreamDefault) != hipSuccess) return nullptr;
     streams[device] = s;
     return s;
 }
@@ -425,6 +428,15 @@ extern "C" void sydelta_delta_batch_free(sydelta_delta_batch* b) { delete b; }
 // ---------------------------------------------------------------------------
 // match
 // ---------------------------------------------------------------------------
+// Classification + walk.  Every full-window position p of a source is classified
+// (hit: first block in index order with equal weak and strong, or not) by one of
+//   * the aligned probe (k_probe): positions k*n, one wave per window;
+//   * the rolling scan (k_scan_lds / k_scan): every position of a block range.
+// The greedy walk (generator.rs:116-221) then runs on the host over the sorted
+// hits.  When the probe runs, the scan covers only the blocks whose aligned window
+// did not hit: the walk reaches such a block's interior only through an unaligned
+// hit's jump, and when it does the block is scanned on demand (Classifier::walk).
+// The op list is identical whichever subset was classified first.
 namespace {
 struct DevBuf {
     void* p = nullptr;
@@ -432,41 +444,421 @@ struct DevBuf {
     ~DevBuf() {
         if (p) (void)hipFreeAsync(p, s);
     }
+    DevBuf() = default;
+    DevBuf(const DevBuf&) = delete;
+    DevBuf& operator=(const DevBuf&) = delete;
 };
 
-// Greedy op emission (generator.rs:116-221) of one file from its position-sorted
-// verified hits (pos, global block).
-void emit_ops(const uint64_t* pos, const uint32_t* blk, size_t nhits, uint64_t blk_base, uint64_t nblocks,
-              uint64_t n, uint64_t last_size, uint64_t len, int tail_match, sydelta_delta* d) {
-    uint64_t x = 0;
+constexpr uint32_t kNoBlk = 0xFFFFFFFFu;
+constexpr uint64_t kUnknownNone = UINT64_MAX;
+
+// One source being classified: a whole file of a batch, or a chunk of one file.
+struct Src {
+    uint32_t file = 0;          // basis file in the index
+    uint64_t off = 0;           // byte offset of source position 0 from the launch base
+    uint64_t len = 0;           // bytes readable from position 0 (zeros beyond, see load_chunk)
+    uint64_t flen = 0;          // source file length (Delta::source_size)
+    uint64_t p0 = 0, p1 = 0;    // full-window positions to classify, [p0, p1); p0 % n == 0
+    uint64_t kb = 0, nblk = 0;  // blocks kb .. kb+nblk-1 (position k*n) cover [p0, p1)
+    bool probed = false;
+    std::vector<uint32_t> ahit;    // probed: per block, its aligned window's hit or kNoBlk
+    std::vector<uint8_t> scanned;  // probed: per block, all its window starts were scanned
+    std::vector<uint64_t> hpos;    // verified hits found so far, sorted, unique
+    std::vector<uint32_t> hblk;    // their global block indices
+};
+
+// Merge sorted (pos, blk) lists into c's hits (equal positions carry equal blocks).
+void merge_hits(Src& c, const std::vector<uint64_t>& pos, const std::vector<uint32_t>& blk) {
+    if (pos.empty()) return;
+    std::vector<uint64_t> np;
+    std::vector<uint32_t> nb;
+    np.reserve(c.hpos.size() + pos.size());
+    nb.reserve(c.hpos.size() + pos.size());
+    size_t i = 0, j = 0;
+    while (i < c.hpos.size() || j < pos.size()) {
+        if (j == pos.size() || (i < c.hpos.size() && c.hpos[i] < pos[j])) {
+            np.push_back(c.hpos[i]); nb.push_back(c.hblk[i]); ++i;
+        } else if (i == c.hpos.size() || pos[j] < c.hpos[i]) {
+            np.push_back(pos[j]); nb.push_back(blk[j]); ++j;
+        } else {
+            np.push_back(pos[j]); nb.push_back(blk[j]); ++i; ++j;
+        }
+    }
+    c.hpos.swap(np);
+    c.hblk.swap(nb);
+}
+
+// First position of [x, p) whose class is unknown (window starts inside a probed
+// block that was not scanned; its aligned start k*n is known), or kUnknownNone.
+uint64_t first_unknown(const Src& c, uint64_t n, uint64_t x, uint64_t p) {
+    if (!c.probed || x >= p) return kUnknownNone;
+    const uint64_t kend = std::min(c.kb + c.nblk, (p - 1) / n + 1);
+    for (uint64_t k = std::max(c.kb, x / n); k < kend; ++k) {
+        if (c.scanned[k - c.kb]) continue;
+        const uint64_t lo = std::max(x, k * n + 1), hi = std::min(p, k * n + n);
+        if (lo < hi) return lo;
+    }
+    return kUnknownNone;
+}
+
+// The basis file a walk copies from.
+struct BasisInfo {
+    uint64_t blk_base;   // its first global block
+    uint64_t nblocks;
+    uint64_t last_size;  // size of its last block
+};
+
+// Greedy walk (generator.rs:116-221 / 283-379) over c's classified positions from
+// `entry`.  ops get Data(source offset, len) and Copy(basis offset, size); consecutive
+// Copies are never merged (generator.rs:135-140).  A non-final chunk ends with the
+// literal run up to p1 (continued by the next chunk) and *exit = where the walk left
+// [p0, p1).  A final source (its file ends inside it) applies the tail rule
+// (generator.rs:156-184: only p* = len - last_size can match) and the last literal
+// run.  Returns 1 with *need = the first position whose class is unknown.
+int walk_src(const Src& c, uint64_t n, uint64_t entry, const BasisInfo& bi, bool final_src, int tail_match,
+             std::vector<sydelta_op>& ops, uint64_t* exit, uint64_t* need) {
+    ops.clear();
+    uint64_t x = entry, lit = entry;
     auto data = [&](uint64_t a, uint64_t b) {
-        if (b) {
-            d->ops.push_back({SYDELTA_OP_DATA, 0, a, b});
+        if (b > a) ops.push_back({SYDELTA_OP_DATA, 0, a, b - a});
+    };
+    auto copy = [&](uint64_t gblk) {
+        const uint64_t b = gblk - bi.blk_base;
+        ops.push_back({SYDELTA_OP_COPY, 0, b * n, (b + 1 == bi.nblocks) ? bi.last_size : n});
+    };
+    size_t i = std::lower_bound(c.hpos.begin(), c.hpos.end(), x) - c.hpos.begin();
+    const size_t H = c.hpos.size();
+    while (x < c.p1) {
+        while (i < H && c.hpos[i] < x) ++i;
+        const uint64_t p = i < H ? c.hpos[i] : c.p1;
+        const uint64_t u = first_unknown(c, n, x, p);
+        if (u != kUnknownNone) {
+            *need = u;
+            return 1;
+        }
+        if (i == H) {
+            x = c.p1;
+            break;
+        }
+        data(lit, p);
+        copy(c.hblk[i]);
+        x = p + n;  // generator.rs:144 / :313
+        lit = x;
+        ++i;
+    }
+    if (!final_src) {
+        data(lit, c.p1);
+        *exit = std::max(x, c.p1);
+        return 0;
+    }
+    if (tail_match && bi.nblocks) {
+        const uint64_t pstar = c.flen - bi.last_size;
+        if (pstar >= lit) {
+            data(lit, pstar);
+            copy(bi.blk_base + bi.nblocks - 1);
+            lit = c.flen;
+        }
+    }
+    data(lit, c.flen);
+    *exit = c.flen;
+    return 0;
+}
+
+int probe_mode_env() {
+    const char* e = getenv("SYDELTA_PROBE");  // "0" never, "1" always, unset/other: auto
+    if (e && e[0] == '0') return 0;
+    if (e && e[0] == '1') return 1;
+    return -1;
+}
+
+struct Classifier {
+    sydelta_index* ix = nullptr;
+    const uint8_t* base = nullptr;  // launch base (sources at Src::off)
+    hipStream_t s = nullptr;
+    Profiler* prof = nullptr;
+    uint64_t n = 0;
+    std::vector<Src> src;
+    uint64_t weak_hits = 0;
+    DevBuf q_buf;
+    size_t qcap = 0;
+
+    // Aligned probe of every block of every source (mode 1), of none (0), or, in
+    // auto mode (-1), when a 1-in-16 sample finds >= 1/8 of its windows hitting.
+    int probe(int mode);
+    // Scan blocks [ka, kz) of source si for every (si, ka, kz); hits merged, blocks marked.
+    int scan(const std::vector<std::array<uint64_t, 3>>& ranges);
+    int classify(int mode);
+    // Walk source i from entry, scanning on demand what the walk needs.
+    int walk(size_t i, uint64_t entry, const BasisInfo& bi, bool final_src, int tail_match, sydelta_delta* d,
+             uint64_t* exit);
+};
+
+int Classifier::probe(int mode) {
+    if (mode == 0) return SYDELTA_OK;
+    uint64_t total = 0;
+    for (auto& c : src) total += c.nblk;
+    if (!total) return SYDELTA_OK;
+    if (mode < 0 && total < 4096) return SYDELTA_OK;  // small inputs: one scan is cheaper
+    bool fast = n % 64 == 0 && n >= 256;
+    for (auto& c : src) fast = fast && ((uintptr_t)(base + c.off) & 15) == 0;
+    auto run = [&](uint32_t stride, std::vector<uint32_t>& out, std::vector<uint64_t>& pfx) -> int {
+        std::vector<ProbeJob> jobs;
+        pfx.assign(src.size() + 1, 0);
+        uint64_t np = 0;
+        for (size_t i = 0; i < src.size(); ++i) {
+            const Src& c = src[i];
+            pfx[i] = np;
+            const uint64_t cnt = (c.nblk + stride - 1) / stride;
+            if (cnt) jobs.push_back({c.off, c.kb, np, c.file, 0});
+            np += cnt;
+        }
+        pfx[src.size()] = np;
+        out.assign(np, kNoBlk);
+        if (!np) return SYDELTA_OK;
+        DevBuf jb;
+        const size_t jbytes = (jobs.size() * sizeof(ProbeJob) + 255) & ~(size_t)255;
+        HIP_TRY(hipMallocAsync(&jb.p, jbytes + np * 4, s));
+        jb.s = s;
+        uint32_t* d_out = (uint32_t*)((uint8_t*)jb.p + jbytes);
+        HIP_TRY(hipMemcpyAsync(jb.p, jobs.data(), jobs.size() * sizeof(ProbeJob), hipMemcpyHostToDevice, s));
+        HIP_TRY(launch_probe(base, (const ProbeJob*)jb.p, (uint32_t)jobs.size(), np, stride, (uint32_t)n, fast,
+                             ix->ix, d_out, s, prof));
+        HIP_TRY(hipMemcpyAsync(out.data(), d_out, np * 4, hipMemcpyDeviceToHost, s));
+        HIP_TRY(hipStreamSynchronize(s));
+        return SYDELTA_OK;
+    };
+    std::vector<uint32_t> out;
+    std::vector<uint64_t> pfx;
+    if (mode < 0) {
+        const uint32_t S = 16;
+        if (int r = run(S, out, pfx)) return r;
+        uint64_t hits = 0;
+        for (uint32_t v : out) hits += v != kNoBlk;
+        if (hits * 8 < out.size()) return SYDELTA_OK;
+    }
+    if (int r = run(1, out, pfx)) return r;
+    for (size_t i = 0; i < src.size(); ++i) {
+        Src& c = src[i];
+        c.probed = true;
+        c.ahit.assign(out.begin() + pfx[i], out.begin() + pfx[i + 1]);
+        c.scanned.assign(c.nblk, 0);
+        std::vector<uint64_t> pos;
+        std::vector<uint32_t> blk;
+        for (uint64_t k = 0; k < c.nblk; ++k)
+            if (c.ahit[k] != kNoBlk) { pos.push_back((c.kb + k) * n); blk.push_back(c.ahit[k]); }
+        merge_hits(c, pos, blk);
+    }
+    return SYDELTA_OK;
+}
+
+int Classifier::scan(const std::vector<std::array<uint64_t, 3>>& ranges) {
+    const uint64_t tile = scan_tile_positions();
+    const uint64_t seg_max = (1ull << 31) / tile * tile;
+    const bool wide = n > scan_max_window();
+    std::vector<ScanSeg> segs;
+    std::vector<uint32_t> seg_src;
+    uint64_t ntiles = 0, tot_pos = 0;
+    for (auto& r : ranges) {
+        Src& c = src[r[0]];
+        const uint64_t lo = std::max(c.p0, r[1] * n), hi = std::min(c.p1, r[2] * n);
+        if (c.probed)
+            for (uint64_t k = r[1]; k < r[2]; ++k) c.scanned[k - c.kb] = 1;
+        if (lo >= hi) continue;
+        // tiles load 16-byte granules from the segment start: start on one
+        const uint64_t lo16 = wide ? lo : (lo & ~15ull);
+        for (uint64_t q = lo16; q < hi; q += seg_max) {
+            ScanSeg g{};
+            g.src = c.off;
+            g.len = c.len;
+            g.pos_begin = q;
+            g.pos_end = std::min(hi, q + seg_max);
+            g.tile_base = (uint32_t)ntiles;
+            g.file = c.file;
+            ntiles += (g.pos_end - g.pos_begin + tile - 1) / tile;
+            tot_pos += g.pos_end - g.pos_begin;
+            segs.push_back(g);
+            seg_src.push_back((uint32_t)r[0]);
+        }
+    }
+    if (segs.empty()) return SYDELTA_OK;
+    if (ntiles >= 0xFFFFFFFFull || segs.size() >= 0x7FFFFFFFull)
+        return fail(SYDELTA_E_INVAL, "scan too large (%llu tiles)", (unsigned long long)ntiles);
+    if (wide && ix->nfiles != 1) return fail(SYDELTA_E_INVAL, "batched match needs block_size <= %u", scan_max_window());
+    unsigned long long* d_counts = nullptr;
+    DevBuf cnt_buf;
+    HIP_TRY(hipMallocAsync((void**)&d_counts, 64, s));
+    cnt_buf.p = d_counts;
+    cnt_buf.s = s;
+    DevBuf seg_buf;
+    if (!wide) {
+        HIP_TRY(hipMallocAsync(&seg_buf.p, segs.size() * sizeof(ScanSeg), s));
+        seg_buf.s = s;
+        HIP_TRY(hipMemcpyAsync(seg_buf.p, segs.data(), segs.size() * sizeof(ScanSeg), hipMemcpyHostToDevice, s));
+        if (!q_buf.p) {
+            qcap = scan_queue_entries();
+            HIP_TRY(hipMallocAsync(&q_buf.p, qcap * sizeof(uint2), s));
+            q_buf.s = s;
+        }
+    }
+    // verified hits: at most one per position; start from ~4 per block of positions
+    uint64_t want = std::min<uint64_t>(tot_pos, tot_pos / n * 4 + (1 << 16));
+    uint64_t cap = 0;
+    unsigned long long counts[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    DevBuf hit_buf;
+    for (int attempt = 0; attempt < 2; ++attempt) {
+        if (want > cap) {
+            if (hit_buf.p) { (void)hipFreeAsync(hit_buf.p, s); hit_buf.p = nullptr; }
+            cap = want;
+            // keys [cap] + key scratch [cap] + values [cap] + value scratch [cap]
+            HIP_TRY(hipMallocAsync(&hit_buf.p, cap * 24, s));
+            hit_buf.s = s;
+        }
+        uint64_t* d_key = (uint64_t*)hit_buf.p;
+        uint32_t* d_val = (uint32_t*)(d_key + 2 * cap);
+        HIP_TRY(hipMemsetAsync(d_counts, 0, 64, s));
+        if (!wide) {
+            HIP_TRY(launch_scan(base, (const ScanSeg*)seg_buf.p, (uint32_t)segs.size(), (uint32_t)ntiles,
+                                (uint32_t)n, ix->ix, ix->d_strong, d_key, d_val, cap, d_counts, (uint2*)q_buf.p, qcap,
+                                s, prof));
+        } else {
+            for (size_t g = 0; g < segs.size(); ++g)
+                HIP_TRY(launch_scan_wide(base + segs[g].src, segs[g].len, segs[g].pos_begin, segs[g].pos_end,
+                                         (uint32_t)g, (uint32_t)n, ix->ix, ix->d_strong, d_key, d_val, cap, d_counts,
+                                         s, prof));
+        }
+        HIP_TRY(hipMemcpyAsync(counts, d_counts, 64, hipMemcpyDeviceToHost, s));
+        HIP_TRY(hipStreamSynchronize(s));
+        if (getenv("SYDELTA_PHASE_TIMING"))
+            fprintf(stderr, "sydelta phase cycles (wave 0, summed over workgroups): stage %llu prefix %llu roll %llu flush %llu\n",
+                    counts[4], counts[5], counts[6], counts[7]);
+        if (counts[0] <= cap) break;
+        want = counts[0];  // dense hits: grow once and rescan
+    }
+    const uint64_t nver = counts[0];
+    weak_hits += counts[1];
+    if (!nver) return SYDELTA_OK;
+    uint64_t* d_key = (uint64_t*)hit_buf.p;
+    uint32_t* d_val = (uint32_t*)(d_key + 2 * cap);
+    uint64_t* k_out = nullptr;
+    uint32_t* v_out = nullptr;
+    const int end_bit = kSegShift + (int)ceil_log2(segs.size() + 1);
+    {
+        ProfScope ps(prof, s, "sort_hits");
+        HIP_TRY(launch_sort_hits(d_key, d_val, d_key + cap, d_val + cap, nver, end_bit, s, &k_out, &v_out));
+    }
+    std::vector<uint64_t> hkey(nver);
+    std::vector<uint32_t> hval(nver);
+    HIP_TRY(hipMemcpyAsync(hkey.data(), k_out, nver * 8, hipMemcpyDeviceToHost, s));
+    HIP_TRY(hipMemcpyAsync(hval.data(), v_out, nver * 4, hipMemcpyDeviceToHost, s));
+    HIP_TRY(hipStreamSynchronize(s));
+    // (segment, position)-sorted; segments are in (source, position) order
+    std::vector<uint64_t> pos;
+    std::vector<uint32_t> blk;
+    size_t h = 0;
+    while (h < nver) {
+        const uint32_t si = seg_src[hkey[h] >> kSegShift];
+        Src& c = src[si];
+        pos.clear();
+        blk.clear();
+        for (; h < nver && seg_src[hkey[h] >> kSegShift] == si; ++h) {
+            const uint64_t p = segs[hkey[h] >> kSegShift].pos_begin + (hkey[h] & 0xFFFFFFFFull);
+            if (p >= c.p0 && p < c.p1) { pos.push_back(p); blk.push_back(hval[h]); }
+        }
+        merge_hits(c, pos, blk);
+    }
+    return SYDELTA_OK;
+}
+
+int Classifier::classify(int mode) {
+    if (int r = probe(mode)) return r;
+    const uint64_t gap_blocks = std::max<uint64_t>(1, scan_tile_positions() / n);
+    std::vector<std::array<uint64_t, 3>> ranges;
+    for (size_t i = 0; i < src.size(); ++i) {
+        const Src& c = src[i];
+        if (!c.nblk) continue;
+        if (!c.probed) {
+            ranges.push_back({i, c.kb, c.kb + c.nblk});
+            continue;
+        }
+        // runs of blocks whose aligned window did not hit; runs closer than a tile merge
+        uint64_t k = 0;
+        while (k < c.nblk) {
+            if (c.ahit[k] != kNoBlk) { ++k; continue; }
+            uint64_t e = k + 1;
+            for (;;) {
+                while (e < c.nblk && c.ahit[e] == kNoBlk) ++e;
+                uint64_t g = e;
+                while (g < c.nblk && c.ahit[g] != kNoBlk && g - e < gap_blocks) ++g;
+                if (g < c.nblk && c.ahit[g] == kNoBlk && g - e < gap_blocks) { e = g; continue; }
+                break;
+            }
+            ranges.push_back({i, c.kb + k, c.kb + e});
+            k = e;
+        }
+    }
+    return scan(ranges);
+}
+
+int Classifier::walk(size_t i, uint64_t entry, const BasisInfo& bi, bool final_src, int tail_match, sydelta_delta* d,
+                     uint64_t* exit) {
+    Src& c = src[i];
+    std::vector<sydelta_op> ops;
+    for (int round = 0;; ++round) {
+        uint64_t need = 0;
+        if (!walk_src(c, n, entry, bi, final_src, tail_match, ops, exit, &need)) break;
+        // the walk jumped into a block only its aligned window was classified for
+        const uint64_t k = need / n;
+        if (round < 4)
+            { if (int r = scan({{i, k, k + 1}})) return r; }
+        else
+            { if (int r = scan({{i, k, c.kb + c.nblk}})) return r; }
+    }
+    d->ops.insert(d->ops.end(), ops.begin(), ops.end());
+    return SYDELTA_OK;
+}
+
+void finish_stats(sydelta_delta* d) {
+    d->stats.copy_ops = d->stats.data_ops = d->stats.literal_bytes = 0;
+    for (auto& o : d->ops) {
+        if (o.kind == SYDELTA_OP_COPY) {
+            d->stats.copy_ops++;
+        } else {
             d->stats.data_ops++;
-            d->stats.literal_bytes += b;
-        }
-    };
-    auto copy = [&](uint64_t b) {
-        const uint64_t sz = (b + 1 == nblocks) ? last_size : n;
-        d->ops.push_back({SYDELTA_OP_COPY, 0, b * n, sz});
-        d->stats.copy_ops++;
-    };
-    for (size_t i = 0; i < nhits; ++i) {
-        const uint64_t p = pos[i];
-        if (p < x) continue;  // inside the previous Copy: never visited
-        data(x, p - x);
-        copy(blk[i] - blk_base);
-        x = p + n;  // generator.rs:313 / :144
-    }
-    if (tail_match) {  // generator.rs:324-353: only p* = len - last_size can match
-        const uint64_t pstar = len - last_size;
-        if (pstar >= x) {
-            data(x, pstar - x);
-            copy(nblocks - 1);
-            x = len;
+            d->stats.literal_bytes += o.b;
         }
     }
-    data(x, len - x);
+}
+
+// Tail-rule flags (generator.rs:156-184) of the given sources of c (file f's last
+// basis block shorter than n, source at least that long).
+int tail_flags(Classifier& C, const std::vector<size_t>& which, std::vector<int>& flag) {
+    sydelta_index* ix = C.ix;
+    std::vector<TailJob> tails;
+    std::vector<size_t> tail_of;
+    flag.assign(C.src.size(), 0);
+    for (size_t i : which) {
+        const Src& c = C.src[i];
+        const uint64_t f = c.file;
+        const uint64_t nb = ix->fblk[f + 1] - ix->fblk[f], ls = ix->last_size[f];
+        if (nb && ls < C.n && c.flen >= ls && c.len >= c.flen) {
+            tails.push_back({c.off + c.flen - ls, ls, ix->fblk[f + 1] - 1});
+            tail_of.push_back(i);
+        }
+    }
+    if (tails.empty()) return SYDELTA_OK;
+    std::vector<int> tf(tails.size(), 0);
+    DevBuf tail_buf;
+    const size_t bytes = (tails.size() * sizeof(TailJob) + 15) & ~(size_t)15;
+    HIP_TRY(hipMallocAsync(&tail_buf.p, bytes + tails.size() * sizeof(int), C.s));
+    tail_buf.s = C.s;
+    int* d_flag = (int*)((uint8_t*)tail_buf.p + bytes);
+    HIP_TRY(hipMemcpyAsync(tail_buf.p, tails.data(), tails.size() * sizeof(TailJob), hipMemcpyHostToDevice, C.s));
+    HIP_TRY(launch_tail(C.base, (const TailJob*)tail_buf.p, (uint32_t)tails.size(), ix->d_weak, ix->d_strong, d_flag,
+                        C.s));
+    HIP_TRY(hipMemcpyAsync(tf.data(), d_flag, tails.size() * sizeof(int), hipMemcpyDeviceToHost, C.s));
+    HIP_TRY(hipStreamSynchronize(C.s));
+    for (size_t j = 0; j < tails.size(); ++j) flag[tail_of[j]] = tf[j];
+    return SYDELTA_OK;
 }
 }  // namespace
 
@@ -475,164 +867,62 @@ void emit_ops(const uint64_t* pos, const uint32_t* blk, size_t nhits, uint64_t b
 static int match_impl(sydelta_index* ix, const uint8_t* d_buf, const uint64_t* src_off, const uint64_t* src_len,
                       hipStream_t s, sydelta_delta_batch* b) {
     CallProf cp;
-    Profiler* prof = cp.get();
     const uint64_t n = ix->bs;
     const uint64_t nf = ix->nfiles;
     b->d.assign(nf, sydelta_delta());
+    Classifier C;
+    C.ix = ix;
+    C.base = d_buf;
+    C.s = s;
+    C.prof = cp.get();
+    C.n = n;
+    C.src.resize(nf);
+    uint64_t tot_pos = 0;
     for (uint64_t f = 0; f < nf; ++f) {
         b->d[f].source_size = src_len[f];
         b->d[f].block_size = n;
         if (src_len[f] && !d_buf) return fail(SYDELTA_E_INVAL, "NULL source buffer");
         if (src_len[f] && ((uintptr_t)(d_buf + src_off[f]) & 15) != 0)
             return fail(SYDELTA_E_INVAL, "source %llu must start 16-byte aligned", (unsigned long long)f);
-    }
-    // segments: per file, runs of <= seg_max full-window positions (generator.rs:116-155)
-    const uint64_t tile = scan_tile_positions();
-    const uint64_t seg_max = (1ull << 31) / tile * tile;
-    std::vector<ScanSeg> segs;
-    std::vector<uint32_t> seg_file;
-    uint64_t ntiles = 0, tot_pos = 0;
-    for (uint64_t f = 0; f < nf; ++f) {
         const uint64_t len = src_len[f];
         const uint64_t npos = len >= n ? len - n + 1 : 0;
         b->d[f].stats.positions = npos;
         tot_pos += npos;
-        if (!npos || ix->fblk[f + 1] == ix->fblk[f]) continue;  // no windows, or empty signature
-        for (uint64_t p0 = 0; p0 < npos; p0 += seg_max) {
-            ScanSeg g{};
-            g.src = src_off[f];
-            g.len = len;
-            g.pos_begin = p0;
-            g.pos_end = std::min(npos, p0 + seg_max);
-            g.tile_base = (uint32_t)ntiles;
-            g.file = (uint32_t)f;
-            ntiles += (g.pos_end - g.pos_begin + tile - 1) / tile;
-            segs.push_back(g);
-            seg_file.push_back((uint32_t)f);
-        }
+        Src& c = C.src[f];
+        c.file = (uint32_t)f;
+        c.off = src_off[f];
+        c.len = c.flen = len;
+        const bool has_sig = ix->fblk[f + 1] > ix->fblk[f];
+        c.p0 = 0;
+        c.p1 = has_sig ? npos : 0;  // an empty signature matches nothing (generator.rs:121)
+        c.kb = 0;
+        c.nblk = (c.p1 + n - 1) / n;
     }
     b->total.positions = tot_pos;
-    if (ntiles >= 0xFFFFFFFFull || segs.size() >= 0x7FFFFFFFull)
-        return fail(SYDELTA_E_INVAL, "batch too large (%llu tiles)", (unsigned long long)ntiles);
-    const bool wide = n > scan_max_window();
-    if (wide && nf != 1) return fail(SYDELTA_E_INVAL, "batched match needs block_size <= %u", scan_max_window());
-    // tail rule jobs (generator.rs:156-184)
-    std::vector<TailJob> tails;
-    std::vector<uint32_t> tail_file;
+    const int mode = n > scan_max_window() ? 0 : probe_mode_env();
+    if (int r = C.classify(mode)) return r;
+    std::vector<size_t> all(nf);
+    for (size_t f = 0; f < nf; ++f) all[f] = f;
+    std::vector<int> tail;
+    if (int r = tail_flags(C, all, tail)) return r;
     for (uint64_t f = 0; f < nf; ++f) {
-        const uint64_t nb = ix->fblk[f + 1] - ix->fblk[f], ls = ix->last_size[f];
-        if (nb && ls < n && src_len[f] >= ls) {
-            tails.push_back({src_off[f] + src_len[f] - ls, ls, ix->fblk[f + 1] - 1});
-            tail_file.push_back((uint32_t)f);
-        }
-    }
-    std::vector<int> tail_flag(tails.size(), 0);
-    DevBuf tail_buf;
-    if (!tails.empty()) {
-        const size_t bytes = tails.size() * sizeof(TailJob);
-        HIP_TRY(hipMallocAsync(&tail_buf.p, bytes + tails.size() * sizeof(int), s));
-        tail_buf.s = s;
-        int* d_flag = (int*)((uint8_t*)tail_buf.p + bytes);
-        HIP_TRY(hipMemcpyAsync(tail_buf.p, tails.data(), bytes, hipMemcpyHostToDevice, s));
-        HIP_TRY(launch_tail(d_buf, (const TailJob*)tail_buf.p, (uint32_t)tails.size(), ix->d_weak, ix->d_strong, d_flag,
-                            s));
-        HIP_TRY(hipMemcpyAsync(tail_flag.data(), d_flag, tails.size() * sizeof(int), hipMemcpyDeviceToHost, s));
-    }
-    std::vector<uint64_t> hkey;
-    std::vector<uint32_t> hval;
-    if (!segs.empty()) {
-        unsigned long long* d_counts = nullptr;
-        DevBuf cnt_buf;
-        HIP_TRY(hipMallocAsync((void**)&d_counts, 64, s));
-        cnt_buf.p = d_counts; cnt_buf.s = s;
-        DevBuf seg_buf, q_buf;
-        size_t qcap = 0;
-        if (!wide) {
-            HIP_TRY(hipMallocAsync(&seg_buf.p, segs.size() * sizeof(ScanSeg), s));
-            seg_buf.s = s;
-            HIP_TRY(hipMemcpyAsync(seg_buf.p, segs.data(), segs.size() * sizeof(ScanSeg), hipMemcpyHostToDevice, s));
-            qcap = scan_queue_entries();
-            HIP_TRY(hipMallocAsync(&q_buf.p, qcap * sizeof(uint2), s));
-            q_buf.s = s;
-        }
-        // verified hits: at most one per position; start from ~4 per block of positions
-        uint64_t want = std::min<uint64_t>(tot_pos, tot_pos / n * 4 + (1 << 16));
-        uint64_t cap = 0, nver = 0;
-        unsigned long long counts[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-        DevBuf hit_buf;
-        for (int attempt = 0; attempt < 2; ++attempt) {
-            if (want > cap) {
-                if (hit_buf.p) { (void)hipFreeAsync(hit_buf.p, s); hit_buf.p = nullptr; }
-                cap = want;
-                // keys [cap] + key scratch [cap] + values [cap] + value scratch [cap]
-                HIP_TRY(hipMallocAsync(&hit_buf.p, cap * 24, s));
-                hit_buf.s = s;
-            }
-            uint64_t* d_key = (uint64_t*)hit_buf.p;
-            uint32_t* d_val = (uint32_t*)(d_key + 2 * cap);
-            HIP_TRY(hipMemsetAsync(d_counts, 0, 64, s));
-            if (!wide) {
-                HIP_TRY(launch_scan(d_buf, (const ScanSeg*)seg_buf.p, (uint32_t)segs.size(), (uint32_t)ntiles,
-                                    (uint32_t)n, ix->ix, ix->d_strong, d_key, d_val, cap, d_counts,
-                                    (uint2*)q_buf.p, qcap, s, prof));
-            } else {
-                for (size_t g = 0; g < segs.size(); ++g)
-                    HIP_TRY(launch_scan_wide(d_buf + segs[g].src, segs[g].len, segs[g].pos_begin, segs[g].pos_end,
-                                             (uint32_t)g, (uint32_t)n, ix->ix, ix->d_strong, d_key, d_val, cap,
-                                             d_counts, s, prof));
-            }
-            HIP_TRY(hipMemcpyAsync(counts, d_counts, 64, hipMemcpyDeviceToHost, s));
-            HIP_TRY(hipStreamSynchronize(s));
-            if (getenv("SYDELTA_PHASE_TIMING"))
-                fprintf(stderr, "sydelta phase cycles (wave 0, summed over workgroups): stage %llu prefix %llu roll %llu flush %llu\n",
-                        counts[4], counts[5], counts[6], counts[7]);
-            if (counts[0] <= cap) break;
-            want = counts[0];  // dense hits: grow once and rescan
-        }
-        nver = counts[0];
-        b->total.weak_hits = counts[1];
-        b->total.verified_hits = nver;
-        if (nver) {
-            uint64_t* d_key = (uint64_t*)hit_buf.p;
-            uint32_t* d_val = (uint32_t*)(d_key + 2 * cap);
-            uint64_t* k_out = nullptr;
-            uint32_t* v_out = nullptr;
-            const int end_bit = kSegShift + (int)ceil_log2(segs.size() + 1);
-            {
-                ProfScope ps(prof, s, "sort_hits");
-                HIP_TRY(launch_sort_hits(d_key, d_val, d_key + cap, d_val + cap, nver, end_bit, s, &k_out, &v_out));
-            }
-            hkey.resize(nver);
-            hval.resize(nver);
-            HIP_TRY(hipMemcpyAsync(hkey.data(), k_out, nver * 8, hipMemcpyDeviceToHost, s));
-            HIP_TRY(hipMemcpyAsync(hval.data(), v_out, nver * 4, hipMemcpyDeviceToHost, s));
-        }
-    }
-    HIP_TRY(hipStreamSynchronize(s));
-    // per-file op emission from the (segment, position)-sorted hits
-    std::vector<int> tail_of(nf, 0);
-    for (size_t j = 0; j < tails.size(); ++j) tail_of[tail_file[j]] = tail_flag[j];
-    std::vector<uint64_t> pos;
-    std::vector<uint32_t> blk;
-    size_t h = 0;
-    for (uint64_t f = 0; f < nf; ++f) {
-        pos.clear();
-        blk.clear();
-        while (h < hkey.size() && seg_file[hkey[h] >> kSegShift] == f) {
-            const ScanSeg& g = segs[hkey[h] >> kSegShift];
-            pos.push_back(g.pos_begin + (hkey[h] & 0xFFFFFFFFull));
-            blk.push_back(hval[h]);
-            ++h;
-        }
         sydelta_delta* d = &b->d[f];
-        d->stats.verified_hits = pos.size();
-        const uint64_t nb = ix->fblk[f + 1] - ix->fblk[f];
-        emit_ops(pos.data(), blk.data(), pos.size(), ix->fblk[f], nb, n, ix->last_size[f], src_len[f], tail_of[f], d);
+        const BasisInfo bi{ix->fblk[f], ix->fblk[f + 1] - ix->fblk[f], ix->last_size[f]};
+        uint64_t exit = 0;
+        if (int r = C.walk(f, 0, bi, true, tail[f], d, &exit)) return r;
+        d->stats.verified_hits = C.src[f].hpos.size();
+        finish_stats(d);
+        b->total.verified_hits += d->stats.verified_hits;
         b->total.copy_ops += d->stats.copy_ops;
         b->total.data_ops += d->stats.data_ops;
         b->total.literal_bytes += d->stats.literal_bytes;
+        // the walk is done with this source's hit lists
+        std::vector<uint64_t>().swap(C.src[f].hpos);
+        std::vector<uint32_t>().swap(C.src[f].hblk);
+        std::vector<uint32_t>().swap(C.src[f].ahit);
     }
-    if (nf == 1) b->d[0].stats.weak_hits = b->total.weak_hits;
+    b->total.weak_hits = C.weak_hits;
+    if (nf == 1) b->d[0].stats.weak_hits = C.weak_hits;
     return SYDELTA_OK;
 }
 
@@ -911,6 +1201,32 @@ extern "C" int sydelta_synth_fill(uint8_t* d_buf, uint64_t len, uint64_t seed, v
     return SYDELTA_OK;
 }
 
+extern "C" int sydelta_synth_fill_range(uint8_t* d_buf, uint64_t first, uint64_t len, uint64_t seed, void* stream) {
+    if (len && !d_buf) return fail(SYDELTA_E_INVAL, "NULL buffer");
+    if (first % 8) return fail(SYDELTA_E_INVAL, "first must be a multiple of 8");
+    int dev = 0;
+    (void)hipGetDevice(&dev);
+    if (int r = ensure_device(dev)) return r;
+    hipStream_t s = stream ? (hipStream_t)stream : thread_stream(dev);
+    HIP_TRY(launch_synth_fill(d_buf, len, seed, s, first));
+    if (!stream) HIP_TRY(hipStreamSynchronize(s));
+    return SYDELTA_OK;
+}
+
+extern "C" int sydelta_synth_mutate_blocks(uint8_t* d_dst, const uint8_t* d_src, uint64_t first, uint64_t len,
+                                           uint64_t block_size, uint64_t seed, uint32_t rate_ppm, void* stream) {
+    if (len && (!d_dst || !d_src)) return fail(SYDELTA_E_INVAL, "NULL buffer");
+    if (!block_size || first % block_size) return fail(SYDELTA_E_INVAL, "first must be a multiple of block_size");
+    int dev = 0;
+    (void)hipGetDevice(&dev);
+    if (int r = ensure_device(dev)) return r;
+    hipStream_t s = stream ? (hipStream_t)stream : thread_stream(dev);
+    if (len && d_dst != d_src) HIP_TRY(hipMemcpyAsync(d_dst, d_src, len, hipMemcpyDeviceToDevice, s));
+    HIP_TRY(launch_synth_edit_blocks(d_dst, len, block_size, first, seed, rate_ppm, s));
+    if (!stream) HIP_TRY(hipStreamSynchronize(s));
+    return SYDELTA_OK;
+}
+
 extern "C" int sydelta_synth_mutate(uint8_t* d_dst, const uint8_t* d_src, uint64_t len, uint64_t seed,
                                     uint32_t rate_ppm, void* stream) {
     if (len && (!d_dst || !d_src)) return fail(SYDELTA_E_INVAL, "NULL buffer");
@@ -921,4 +1237,137 @@ extern "C" int sydelta_synth_mutate(uint8_t* d_dst, const uint8_t* d_src, uint64
     HIP_TRY(launch_synth_mutate(d_dst, d_src, len, seed, rate_ppm, s));
     if (!stream) HIP_TRY(hipStreamSynchronize(s));
     return SYDELTA_OK;
+}
+
+// ---------------------------------------------------------------------------
+// chunk-sharded match of one file (BASELINE C5)
+// ---------------------------------------------------------------------------
+// Rank g classifies the window starts of its chunk [pos_begin, pos_end) against the
+// all-gathered signature; the walks are then chained: chunk g's walk starts where
+// chunk g-1's left (its exit may lie up to n-1 bytes inside chunk g after a Copy),
+// and the op lists concatenate with sydelta_delta_append.  The result equals the
+// single-device op list because classification is a pure function of the position.
+struct sydelta_chunk {
+    Classifier C;
+    bool final_src = false;
+    int tail_flag = 0;
+    uint64_t file_len = 0;
+    BasisInfo bi{0, 0, 0};
+};
+
+extern "C" int sydelta_chunk_classify(sydelta_index* idx, const uint8_t* d_buf, uint64_t buf_pos, uint64_t buf_len,
+                                      uint64_t file_len, uint64_t pos_begin, uint64_t pos_end, void* stream,
+                                      sydelta_chunk** out) {
+    if (!idx || !out) return fail(SYDELTA_E_INVAL, "NULL argument");
+    *out = nullptr;
+    if (idx->nfiles != 1) return fail(SYDELTA_E_INVAL, "chunked match needs a single-file index");
+    const uint64_t n = idx->bs;
+    if (n > scan_max_window()) return fail(SYDELTA_E_INVAL, "chunked match needs block_size <= %u", scan_max_window());
+    if (pos_begin % n) return fail(SYDELTA_E_INVAL, "pos_begin must be a multiple of block_size");
+    if (pos_end < pos_begin) return fail(SYDELTA_E_INVAL, "pos_end < pos_begin");
+    if ((buf_pos & 15) || ((uintptr_t)d_buf & 15))
+        return fail(SYDELTA_E_INVAL, "d_buf and buf_pos must be 16-byte aligned");
+    if (buf_pos > (pos_begin & ~15ull)) return fail(SYDELTA_E_INVAL, "buffer starts after the chunk");
+    const uint64_t npos = file_len >= n ? file_len - n + 1 : 0;
+    const bool final_src = pos_end >= npos;
+    const uint64_t p1 = std::min(pos_end, npos), p0 = std::min(pos_begin, p1);
+    const uint64_t need_end = final_src ? file_len : std::min(file_len, p1 + n - 1);
+    if ((p1 > p0 || final_src) && buf_pos + buf_len < need_end)
+        return fail(SYDELTA_E_INVAL, "buffer ends at %llu, chunk needs bytes up to %llu",
+                    (unsigned long long)(buf_pos + buf_len), (unsigned long long)need_end);
+    if (buf_len && !d_buf) return fail(SYDELTA_E_INVAL, "NULL buffer");
+    if (int r = ensure_device(idx->device)) return r;
+    hipStream_t s = stream ? (hipStream_t)stream : thread_stream(idx->device);
+    std::unique_ptr<sydelta_chunk> ch(new sydelta_chunk());
+    CallProf cp;
+    Classifier& C = ch->C;
+    C.ix = idx;
+    C.base = d_buf - buf_pos;
+    C.s = s;
+    C.prof = cp.get();
+    C.n = n;
+    C.src.resize(1);
+    Src& c = C.src[0];
+    c.file = 0;
+    c.off = 0;
+    c.len = std::min(file_len, buf_pos + buf_len);
+    c.flen = file_len;
+    const bool has_sig = idx->fblk[1] > 0;
+    c.p0 = p0;
+    c.p1 = has_sig ? p1 : p0;
+    c.kb = p0 / n;
+    c.nblk = c.p1 > c.p0 ? (c.p1 + n - 1) / n - c.kb : 0;
+    ch->final_src = final_src;
+    ch->file_len = file_len;
+    ch->bi = BasisInfo{0, idx->fblk[1], idx->last_size[0]};
+    if (int r = C.classify(probe_mode_env())) return r;
+    if (final_src) {
+        std::vector<int> tf;
+        if (int r = tail_flags(C, {0}, tf)) return r;
+        ch->tail_flag = tf[0];
+    }
+    C.prof = nullptr;
+    *out = ch.release();
+    return SYDELTA_OK;
+}
+
+extern "C" int sydelta_chunk_walk(sydelta_chunk* ch, uint64_t entry, uint64_t* exit_pos, sydelta_delta** out) {
+    if (!ch || !exit_pos || !out) return fail(SYDELTA_E_INVAL, "NULL argument");
+    *out = nullptr;
+    Classifier& C = ch->C;
+    const Src& c = C.src[0];
+    if (entry < c.p0) return fail(SYDELTA_E_INVAL, "entry %llu precedes the chunk", (unsigned long long)entry);
+    if (int r = ensure_device(C.ix->device)) return r;
+    CallProf cp;
+    C.prof = cp.get();
+    std::unique_ptr<sydelta_delta> d(new sydelta_delta());
+    d->source_size = ch->file_len;
+    d->block_size = C.n;
+    d->stats.positions = c.p1 - c.p0;
+    const int r = C.walk(0, entry, ch->bi, ch->final_src, ch->tail_flag, d.get(), exit_pos);
+    C.prof = nullptr;
+    if (r) return r;
+    d->stats.verified_hits = c.hpos.size();
+    d->stats.weak_hits = C.weak_hits;
+    finish_stats(d.get());
+    *out = d.release();
+    return SYDELTA_OK;
+}
+
+extern "C" void sydelta_chunk_free(sydelta_chunk* ch) {
+    if (!ch) return;
+    (void)hipSetDevice(ch->C.ix->device);
+    delete ch;
+}
+
+// Concatenate src's ops onto dst; a Data op that ends where src's first Data op
+// starts is extended (literal runs stay maximal, generator.rs:186-197, 218-221).
+extern "C" int sydelta_delta_append(sydelta_delta* dst, const sydelta_delta* src) {
+    if (!dst || !src) return fail(SYDELTA_E_INVAL, "NULL argument");
+    if (!dst->lit_off.empty() || !src->lit_off.empty())
+        return fail(SYDELTA_E_INVAL, "append is for device deltas (no host literal copies)");
+    size_t j = 0;
+    if (!dst->ops.empty() && !src->ops.empty()) {
+        sydelta_op& a = dst->ops.back();
+        const sydelta_op& b = src->ops.front();
+        if (a.kind == SYDELTA_OP_DATA && b.kind == SYDELTA_OP_DATA && a.a + a.b == b.a) {
+            a.b += b.b;
+            j = 1;
+        }
+    }
+    dst->ops.insert(dst->ops.end(), src->ops.begin() + j, src->ops.end());
+    dst->stats.positions += src->stats.positions;
+    dst->stats.weak_hits += src->stats.weak_hits;
+    dst->stats.verified_hits += src->stats.verified_hits;
+    if (!dst->block_size) dst->block_size = src->block_size;
+    dst->source_size = std::max(dst->source_size, src->source_size);
+    finish_stats(dst);
+    return SYDELTA_OK;
+}
+
+extern "C" sydelta_delta* sydelta_delta_new(uint64_t source_size, uint64_t block_size) {
+    sydelta_delta* d = new sydelta_delta();
+    d->source_size = source_size;
+    d->block_size = block_size;
+    return d;
 }

@@ -100,6 +100,21 @@ hipError_t launch_scan_wide(const uint8_t* d_src, uint64_t len, uint64_t pos_beg
 // (*key_out, *val_out) (either the input or the tmp arrays).
 hipError_t launch_sort_hits(uint64_t* key, uint32_t* val, uint64_t* key_tmp, uint32_t* val_tmp, uint64_t nhits,
                             int end_bit, hipStream_t s, uint64_t** key_out, uint32_t** val_out);
+// Aligned-window probe: probe w of job j (jobs[j].pfx <= w < jobs[j+1].pfx) is the
+// window at position k*n, k = k0 + (w - pfx) * stride, of the source at byte
+// offset src from the launch base; out[w] = global block index of its hit
+// (first candidate in index order with equal weak and strong), or 0xFFFFFFFF.
+struct ProbeJob {
+    uint64_t src;
+    uint64_t k0;
+    uint64_t pfx;
+    uint32_t file;
+    uint32_t pad;
+};
+// fast: n % 64 == 0, n >= 256 and every window 16-byte aligned.
+hipError_t launch_probe(const uint8_t* d_base, const ProbeJob* d_jobs, uint32_t njobs, uint64_t nprobes,
+                        uint32_t stride, uint32_t n, bool fast, const DeviceIndex& ix, uint32_t* d_out, hipStream_t s,
+                        Profiler* prof);
 // Tail rule (generator.rs:156-184) of every listed file: flag[i] = 1 iff the
 // suffix of source i hashes to (weak[blk], strong[blk]) of its last basis block.
 struct TailJob {
@@ -109,7 +124,9 @@ struct TailJob {
 };
 hipError_t launch_tail(const uint8_t* d_buf, const TailJob* d_jobs, uint32_t njobs, const uint32_t* d_weak,
                        const uint64_t* d_strong, int* d_flag, hipStream_t s);
-hipError_t launch_synth_fill(uint8_t* d_buf, uint64_t len, uint64_t seed, hipStream_t s);
+hipError_t launch_synth_fill(uint8_t* d_buf, uint64_t len, uint64_t seed, hipStream_t s, uint64_t first = 0);
+hipError_t launch_synth_edit_blocks(uint8_t* d_dst, uint64_t len, uint64_t bs, uint64_t first, uint64_t seed,
+                                    uint32_t rate_ppm, hipStream_t s);
 hipError_t launch_synth_mutate(uint8_t* d_dst, const uint8_t* d_src, uint64_t len, uint64_t seed, uint32_t rate_ppm,
                                hipStream_t s);
 

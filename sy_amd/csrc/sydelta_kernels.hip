@@ -27,12 +27,12 @@ namespace sydelta {
 // ===========================================================================
 // K1: signature
 // ===========================================================================
-__global__ __launch_bounds__(256) void k_sig_fast(const uint8_t* __restrict__ buf, uint64_t nfull, uint32_t bs,
-                                                  uint32_t* __restrict__ weak, uint64_t* __restrict__ strong) {
+// Adler-32 + XXH3-64 of one window [base, base + bs), bs % 64 == 0, bs >= 256,
+// base 16-byte aligned: lane l owns bytes [16l + 1024j, +16) of every 1 KiB piece j,
+// so each wave-instruction loads 1 KiB contiguously.  Every lane returns the result.
+__device__ __forceinline__ void wave_hash_aligned(const uint8_t* __restrict__ base, uint32_t bs, uint32_t& weak_out,
+                                                  uint64_t& strong_out) {
     const uint32_t lane = threadIdx.x & 63;
-    const uint64_t blk = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
-    if (blk >= nfull) return;
-    const uint8_t* base = buf + blk * (uint64_t)bs;
     const uint32_t q = lane & 3, sl = lane >> 2;
     const uint32_t npieces = (bs + 1023) >> 10;
     const uint32_t ns = bs >> 6;
@@ -83,9 +83,20 @@ __global__ __launch_bounds__(256) void k_sig_fast(const uint8_t* __restrict__ bu
     bpos = wave_sum64(bpos);
     const uint32_t A = (1u + asum) % kMod;
     const uint32_t B = (uint32_t)(((uint64_t)bs + bpos - vsum) % kMod);
-    if (lane == 0) {
-        weak[blk] = (B << 16) | A;
-        strong[blk] = h;
+    weak_out = (B << 16) | A;
+    strong_out = h;
+}
+
+__global__ __launch_bounds__(256) void k_sig_fast(const uint8_t* __restrict__ buf, uint64_t nfull, uint32_t bs,
+                                                  uint32_t* __restrict__ weak, uint64_t* __restrict__ strong) {
+    const uint64_t blk = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+    if (blk >= nfull) return;
+    uint32_t wk;
+    uint64_t st;
+    wave_hash_aligned(buf + blk * (uint64_t)bs, bs, wk, st);
+    if ((threadIdx.x & 63) == 0) {
+        weak[blk] = wk;
+        strong[blk] = st;
     }
 }
 
@@ -246,6 +257,72 @@ __device__ __forceinline__ int64_t table_find(const uint32_t* __restrict__ keys,
         if (k.w == kEmptyKey) return -1;  // buckets fill in order: a free last slot ends the chain
         b = (b + 1) & bmask;
     }
+}
+
+// ===========================================================================
+// K5: aligned-window probe (block-aligned positions k*n of a source)
+// ===========================================================================
+// The greedy walk (generator.rs:116-197) over a source that shares most blocks with
+// the basis moves from one block-aligned hit to the next: positions strictly inside
+// a block whose aligned window hits are never visited unless an unaligned hit jumps
+// there.  k_probe classifies the aligned positions exactly like the scan does
+// (weak -> candidates -> first candidate in index order with equal strong,
+// generator.rs:121-155), one wave per window, so the host scans only the other
+// blocks' windows (sydelta_api.cpp, Classifier).  out[w] = global block index of
+// the hit, or kNoBlock.
+constexpr uint32_t kNoBlock = 0xFFFFFFFFu;
+
+__device__ __forceinline__ uint32_t lookup_first(const FileIx& F, const uint32_t* __restrict__ filt,
+                                                 const uint32_t* __restrict__ keys, const uint32_t* __restrict__ start,
+                                                 const uint32_t* __restrict__ cnt, const uint32_t* __restrict__ order,
+                                                 const uint64_t* __restrict__ cstrong, uint32_t wk, uint64_t st) {
+    // wave-uniform arguments; every lane returns the same block
+    const uint32_t lane = threadIdx.x & 63;
+    const uint32_t h = filt_hash(wk & 0xFFFF, wk >> 16);
+    if ((filt_mask(h) & ~filt[F.filt_off + (h >> F.fwshift)]) != 0) return kNoBlock;
+    const int64_t slot = table_find(keys + F.slot_off, F.bmask, wk);
+    if (slot < 0) return kNoBlock;
+    const uint64_t gs = F.slot_off + (uint64_t)slot;
+    const uint32_t s0 = start[gs], c = cnt[gs];
+    uint32_t best = kNoBlock;
+    for (uint32_t j = lane; j < c; j += 64)
+        if (cstrong[s0 + j] == st) best = min(best, order[s0 + j]);
+#pragma unroll
+    for (int m = 1; m < 64; m <<= 1) best = min(best, (uint32_t)__shfl_xor((int)best, m, 64));
+    return best;
+}
+
+__global__ __launch_bounds__(256) void k_probe(const uint8_t* __restrict__ base, const ProbeJob* __restrict__ jobs,
+                                               uint32_t njobs, uint64_t nprobes, uint32_t stride, uint32_t n,
+                                               uint32_t fast, const FileIx* __restrict__ files,
+                                               const uint32_t* __restrict__ filt, const uint32_t* __restrict__ keys,
+                                               const uint32_t* __restrict__ start, const uint32_t* __restrict__ cnt,
+                                               const uint32_t* __restrict__ order,
+                                               const uint64_t* __restrict__ cstrong, uint32_t* __restrict__ out) {
+    const uint64_t w = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+    if (w >= nprobes) return;
+    uint32_t lo = 0, hi = njobs;  // job holding probe w (wave-uniform)
+    while (hi - lo > 1) {
+        const uint32_t mid = (lo + hi) >> 1;
+        if (jobs[mid].pfx <= w) lo = mid; else hi = mid;
+    }
+    const ProbeJob J = jobs[lo];
+    const uint64_t k = J.k0 + (w - J.pfx) * stride;
+    const uint8_t* p = base + J.src + k * n;
+    uint32_t wk;
+    uint64_t st;
+    if (fast) {
+        wave_hash_aligned(p, n, wk, st);
+    } else if (n > 240) {
+        wave_hash_long(p, n, wk, st);
+    } else {
+        wk = 0; st = 0;
+        if ((threadIdx.x & 63) == 0) { wk = adler_scalar(p, n); st = xxh3_short(p, n); }
+        wk = (uint32_t)__shfl((int)wk, 0, 64);
+        st = shfl64(st, 0);
+    }
+    const uint32_t b = lookup_first(files[J.file], filt, keys, start, cnt, order, cstrong, wk, st);
+    if ((threadIdx.x & 63) == 0) out[w] = b;
 }
 
 // ===========================================================================
@@ -1096,16 +1173,30 @@ __global__ void k_tail(const uint8_t* __restrict__ buf, const TailJob* __restric
 // ===========================================================================
 // Synthetic inputs (bench)
 // ===========================================================================
-__global__ void k_synth_fill(uint8_t* __restrict__ buf, uint64_t len, uint64_t seed) {
+// bytes [8*w0, 8*w0 + len) of the stream
+__global__ void k_synth_fill(uint8_t* __restrict__ buf, uint64_t len, uint64_t seed, uint64_t w0) {
     const uint64_t nw = (len + 7) / 8;
     for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < nw; i += (uint64_t)gridDim.x * blockDim.x) {
-        const uint64_t z = splitmix_word(seed, i);
+        const uint64_t z = splitmix_word(seed, w0 + i);
         if (8 * i + 8 <= len) {
             *(uint64_t*)(buf + 8 * i) = z;
         } else {
             for (uint64_t b = 8 * i; b < len; ++b) buf[b] = (uint8_t)(z >> (8 * (b - 8 * i)));
         }
     }
+}
+
+// Block edits (BASELINE C5): block k (global) is edited iff (r & 0xFFFFFFFF) < thresh,
+// r = splitmix(seed, k); byte (r >> 32) % bs of the block ^= 1 + (splitmix(~seed, k) % 255).
+// One thread per block of [k0, k0 + nb); the copy of the unedited bytes is done by the caller.
+__global__ void k_synth_edit_blocks(uint8_t* __restrict__ dst, uint64_t len, uint64_t bs, uint64_t k0, uint64_t nb,
+                                    uint64_t seed, uint64_t thresh) {
+    const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= nb) return;
+    const uint64_t r = splitmix_word(seed, k0 + t);
+    if ((r & 0xFFFFFFFFull) >= thresh) return;
+    const uint64_t o = t * bs + (r >> 32) % bs;
+    if (o < len) dst[o] ^= (uint8_t)(1 + splitmix_word(~seed, k0 + t) % 255);
 }
 
 // Per byte: r = splitmix(seed, i); if (r & 0xFFFFFFFF) < rate * 2^32 / 1e6: byte ^= 1 + (r >> 32) % 255.
@@ -1196,6 +1287,18 @@ hipError_t launch_index_build(const uint32_t* d_weak, const uint64_t* d_strong, 
     }
     if ((e = hipGetLastError())) return e;
     hipLaunchKernelGGL(k_idx_cstrong, dim3(grid_for(n, 256)), dim3(256), 0, s, n, ix.order, d_strong, ix.cstrong);
+    return hipGetLastError();
+}
+
+hipError_t launch_probe(const uint8_t* d_base, const ProbeJob* d_jobs, uint32_t njobs, uint64_t nprobes,
+                        uint32_t stride, uint32_t n, bool fast, const DeviceIndex& ix, uint32_t* d_out, hipStream_t s,
+                        Profiler* prof) {
+    if (!nprobes) return hipSuccess;
+    if (fast && (n % 64 != 0 || n < 256)) return hipErrorInvalidValue;
+    ProfScope ps(prof, s, "k_probe");
+    hipLaunchKernelGGL(k_probe, dim3(grid_for(nprobes * 64, 256)), dim3(256), 0, s, d_base, d_jobs, njobs, nprobes,
+                       stride, n, fast ? 1u : 0u, ix.d_files, ix.filt, ix.keys, ix.start, ix.cnt, ix.order,
+                       ix.cstrong, d_out);
     return hipGetLastError();
 }
 
@@ -1335,9 +1438,21 @@ hipError_t launch_tail(const uint8_t* d_buf, const TailJob* d_jobs, uint32_t njo
     return hipGetLastError();
 }
 
-hipError_t launch_synth_fill(uint8_t* d_buf, uint64_t len, uint64_t seed, hipStream_t s) {
+hipError_t launch_synth_fill(uint8_t* d_buf, uint64_t len, uint64_t seed, hipStream_t s, uint64_t first) {
     if (!len) return hipSuccess;
-    hipLaunchKernelGGL(k_synth_fill, dim3(4096), dim3(256), 0, s, d_buf, len, seed);
+    if (first % 8) return hipErrorInvalidValue;
+    hipLaunchKernelGGL(k_synth_fill, dim3(4096), dim3(256), 0, s, d_buf, len, seed, first / 8);
+    return hipGetLastError();
+}
+
+hipError_t launch_synth_edit_blocks(uint8_t* d_dst, uint64_t len, uint64_t bs, uint64_t first, uint64_t seed,
+                                    uint32_t rate_ppm, hipStream_t s) {
+    if (!len) return hipSuccess;
+    if (!bs || first % bs) return hipErrorInvalidValue;
+    const uint64_t nb = (len + bs - 1) / bs;
+    const uint64_t thresh = (uint64_t)(((unsigned __int128)rate_ppm << 32) / 1000000u);
+    hipLaunchKernelGGL(k_synth_edit_blocks, dim3(grid_for(nb, 256)), dim3(256), 0, s, d_dst, len, bs, first / bs, nb,
+                       seed, thresh);
     return hipGetLastError();
 }
 

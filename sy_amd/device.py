@@ -153,6 +153,75 @@ def match(index: Index, src: torch.Tensor, stream=None, length: int | None = Non
         lib.sydelta_delta_free(h)
 
 
+class Chunk:
+    """One rank's share of a chunk-sharded match of a single file (BASELINE C5):
+    full-window positions [pos_begin, pos_end) classified against the all-gathered
+    signature held by `index`.  `buf` holds source bytes [buf_pos, buf_pos + numel)."""
+
+    def __init__(self, index: Index, buf: torch.Tensor, buf_pos: int, file_len: int, pos_begin: int, pos_end: int,
+                 stream=None):
+        self.h = ctypes.c_void_p()
+        self.buf = buf  # must outlive the chunk (on-demand rescans read it)
+        check(lib.sydelta_chunk_classify(index.h, _ptr(buf), buf_pos, buf.numel(), file_len, pos_begin, pos_end,
+                                          _stream(stream), ctypes.byref(self.h)))
+
+    def walk(self, entry: int):
+        """Greedy walk from `entry` -> (DeviceDelta of [entry, exit), exit)."""
+        d = ctypes.c_void_p()
+        ex = ctypes.c_uint64()
+        check(lib.sydelta_chunk_walk(self.h, entry, ctypes.byref(ex), ctypes.byref(d)))
+        try:
+            return _device_delta(d), int(ex.value)
+        finally:
+            lib.sydelta_delta_free(d)
+
+    def close(self):
+        if self.h:
+            lib.sydelta_chunk_free(self.h)
+            self.h = ctypes.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+def join_deltas(parts, source_size: int, block_size: int) -> DeviceDelta:
+    """Concatenate chunk deltas in file order, merging a trailing Data op with the
+    next chunk's leading Data op when contiguous (sydelta_delta_append's rule)."""
+    kinds, aa, bb = [], [], []
+    for p in parts:
+        k, a, b = list(p.kind), list(p.a), list(p.b)
+        if kinds and k and kinds[-1] == 1 and k[0] == 1 and int(aa[-1]) + int(bb[-1]) == int(a[0]):
+            bb[-1] = int(bb[-1]) + int(b[0])
+            k, a, b = k[1:], a[1:], b[1:]
+        kinds += k
+        aa += a
+        bb += b
+    kind = np.array(kinds, dtype=np.uint8)
+    stats = {"positions": sum(p.stats["positions"] for p in parts),
+             "weak_hits": sum(p.stats["weak_hits"] for p in parts),
+             "verified_hits": sum(p.stats["verified_hits"] for p in parts),
+             "copy_ops": int((kind == 0).sum()), "data_ops": int((kind == 1).sum()),
+             "literal_bytes": int(sum(int(y) for x, y in zip(kinds, bb) if x == 1))}
+    return DeviceDelta(kind, np.array(aa, dtype=np.uint64), np.array(bb, dtype=np.uint64), source_size, block_size,
+                       stats)
+
+
+def synth_fill_range(buf: torch.Tensor, first: int, seed: int, stream=None) -> None:
+    """Bytes [first, first + numel) of the synth_fill stream (first % 8 == 0)."""
+    check(lib.sydelta_synth_fill_range(_ptr(buf), first, buf.numel(), seed & 0xFFFFFFFFFFFFFFFF, _stream(stream)))
+
+
+def synth_mutate_blocks(dst: torch.Tensor, src: torch.Tensor, first: int, block_size: int, seed: int, rate_ppm: int,
+                        stream=None) -> None:
+    """C5 edit model: one substituted byte in each selected block (oracle.synth_edit_blocks)."""
+    assert dst.numel() == src.numel()
+    check(lib.sydelta_synth_mutate_blocks(_ptr(dst), _ptr(src), first, src.numel(), block_size,
+                                          seed & 0xFFFFFFFFFFFFFFFF, rate_ppm, _stream(stream)))
+
+
 def synth_fill(buf: torch.Tensor, seed: int, stream=None) -> None:
     check(lib.sydelta_synth_fill(_ptr(buf), buf.numel(), seed & 0xFFFFFFFFFFFFFFFF, _stream(stream)))
 

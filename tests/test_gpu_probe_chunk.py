@@ -1,0 +1,219 @@
+"""GPU parity for the aligned-window probe (k_probe + on-demand block scans) and
+the chunk-sharded single-file match (BASELINE C5).
+
+Both must reproduce generator.rs's op list exactly: the probe only changes which
+window starts are classified before the walk (the walk scans a block on demand
+when an unaligned hit jumps into it), and chunking only splits the walk at
+block-aligned boundaries.  The oracle is the C restatement of generator.rs."""
+import os
+import random
+
+import numpy as np
+import pytest
+
+from oracle import oracle as O
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(params=["0", "1"], ids=["scan-only", "probe"])
+def probe_mode(request):
+    old = os.environ.get("SYDELTA_PROBE")
+    os.environ["SYDELTA_PROBE"] = request.param
+    yield request.param
+    if old is None:
+        os.environ.pop("SYDELTA_PROBE", None)
+    else:
+        os.environ["SYDELTA_PROBE"] = old
+
+
+def _to_dev(data: bytes, pad: int = 16):
+    import torch
+
+    t = torch.zeros(len(data) + pad, dtype=torch.uint8, device="cuda")
+    if data:
+        t[:len(data)] = torch.frombuffer(bytearray(data), dtype=torch.uint8).cuda()
+    return t
+
+
+def _index(gpu, basis: bytes, bs: int):
+    b = _to_dev(basis)
+    w, s = gpu.signature(b[:len(basis)], bs)
+    nb = w.numel()
+    last = (len(basis) - (nb - 1) * bs) if nb else 0
+    return gpu.Index(w, s, bs, last)
+
+
+def _oracle_ops(oracle_c, src, basis, bs):
+    w, s, z = oracle_c.compute_checksums(basis, bs)
+    return O.ops_from_arrays(*oracle_c.generate_delta(src, w, s, z, bs))
+
+
+def _shift_edits(basis: bytes, rng, bs: int, pairs: int) -> bytes:
+    """Insertions each followed later by a deletion of the same length: the source
+    is shifted between them (unaligned hits) and realigned after (aligned hits), so
+    a walk leaving a shifted hit jumps into a block whose aligned window hit."""
+    src = bytearray(basis)
+    for _ in range(pairs):
+        a = rng.randrange(0, max(1, len(src) - 4 * bs))
+        k = rng.randint(1, 3)
+        src[a:a] = rng.randbytes(k)
+        b = a + k + rng.randint(bs // 2 + 1, 3 * bs)
+        del src[b:b + k]
+    return bytes(src)
+
+
+def test_probe_random_small(probe_mode, gpu, oracle_c):
+    rng = random.Random(77)
+    for it in range(150):
+        alpha = rng.choice([2, 4, 256])
+        basis = bytes(rng.randrange(alpha) for _ in range(rng.randint(0, 3000)))
+        src = bytearray(basis)
+        for _ in range(rng.randint(0, 5)):
+            op, p = rng.randint(0, 2), rng.randint(0, max(0, len(src) - 1))
+            if op == 0 and src:
+                src[p] = rng.randrange(256)
+            elif op == 1:
+                src[p:p] = bytes(rng.randrange(alpha) for _ in range(rng.randint(1, 9)))
+            else:
+                del src[p:p + rng.randint(1, 9)]
+        src = bytes(src)
+        bs = rng.choice([1, 3, 7, 16, 33, 64, 100, 241, 256, 300, 512])
+        idx = _index(gpu, basis, bs)
+        d = gpu.match(idx, _to_dev(src), length=len(src))
+        idx.close()
+        assert d.tuples() == _oracle_ops(oracle_c, src, basis, bs), (it, bs)
+
+
+@pytest.mark.parametrize("bs", [256, 512, 1000, 4096, 8192])
+def test_probe_shifted_regions(bs, probe_mode, gpu, oracle_c):
+    """Shift/realign edits: exercises the on-demand block scans of the probe path."""
+    rng = random.Random(bs)
+    basis = rng.randbytes(rng.randint(1 << 20, 2 << 20))
+    src = _shift_edits(basis, rng, bs, 60)
+    src = bytearray(src)
+    for _ in range(20):
+        src[rng.randrange(len(src))] ^= 0x77
+    src = bytes(src)
+    idx = _index(gpu, basis, bs)
+    d = gpu.match(idx, _to_dev(src), length=len(src))
+    idx.close()
+    expect = _oracle_ops(oracle_c, src, basis, bs)
+    assert d.tuples() == expect
+    assert O.py_apply_delta(basis, src, d.tuples()) == src
+
+
+@pytest.mark.parametrize("pattern", [b"\x00", b"ABC", b"0123456789" * 7])
+def test_probe_degenerate(pattern, probe_mode, gpu, oracle_c):
+    basis = (pattern * (200000 // len(pattern) + 1))[:200000]
+    for src in (basis, basis[5:] + b"xyz", b"q" + basis[:150000]):
+        for bs in (4096, 1000):
+            idx = _index(gpu, basis, bs)
+            d = gpu.match(idx, _to_dev(src), length=len(src))
+            idx.close()
+            assert d.tuples() == _oracle_ops(oracle_c, src, basis, bs)
+
+
+def test_probe_auto_mode_c1(gpu, oracle_c):
+    """Auto mode on the C1 shape (two small edits in 50 MB): the 1-in-16 sample
+    hits, so the probe path runs; result identical to the oracle."""
+    os.environ.pop("SYDELTA_PROBE", None)
+    n = 52_428_800
+    old = O.synth_bytes(n, 0x5E1D0001)
+    new = old.copy()
+    new[1 << 20:(1 << 20) + 18] = np.frombuffer(b"MODIFIED DATA HERE", np.uint8)
+    new[0:20] = np.frombuffer(b"HEADER DATA AT START", np.uint8)
+    idx = _index(gpu, old.tobytes(), 4096)
+    d = gpu.match(idx, _to_dev(new.tobytes()), length=n)
+    idx.close()
+    assert d.tuples() == _oracle_ops(oracle_c, new, old, 4096)
+    # only the two edited blocks' window starts were scanned
+    assert d.stats["weak_hits"] < 4 * 4096
+
+
+def _chunked(gpu, src: bytes, idx, bs: int, bounds):
+    """Classify chunk g = positions [bounds[g], bounds[g+1]) from its own buffer
+    (chunk bytes + window halo), then chain the walks."""
+    L = len(src)
+    chunks = []
+    for g in range(len(bounds) - 1):
+        p0, p1 = bounds[g], bounds[g + 1]
+        final = g == len(bounds) - 2
+        buf_pos = p0 & ~15
+        end = L if final else min(L, p1 + bs - 1)
+        buf = _to_dev(src[buf_pos:end])
+        chunks.append(gpu.Chunk(idx, buf, buf_pos, L, p0, p1 if not final else max(p1, L)))
+    parts, entry = [], 0
+    for c in chunks:
+        d, entry = c.walk(entry)
+        parts.append(d)
+    for c in chunks:
+        c.close()
+    return gpu.join_deltas(parts, L, bs)
+
+
+@pytest.mark.parametrize("bs", [64, 1000, 4096, 8192])
+@pytest.mark.parametrize("nchunks", [1, 2, 3, 8])
+def test_chunked_equals_whole(bs, nchunks, probe_mode, gpu, oracle_c):
+    rng = random.Random(bs * 31 + nchunks)
+    nblk = rng.randint(40, 300)
+    basis = rng.randbytes(nblk * bs + rng.randint(0, bs - 1))
+    src = _shift_edits(basis, rng, bs, 8)
+    src = bytearray(src)
+    for _ in range(10):
+        src[rng.randrange(len(src))] ^= 0x11
+    src = bytes(src)
+    idx = _index(gpu, basis, bs)
+    npos = max(0, len(src) - bs + 1)
+    nb = -(-npos // bs)
+    cuts = sorted(rng.sample(range(1, max(2, nb)), min(nchunks - 1, max(0, nb - 1))))
+    bounds = [0] + [c * bs for c in cuts] + [npos]
+    d = _chunked(gpu, src, idx, bs, bounds)
+    idx.close()
+    assert d.tuples() == _oracle_ops(oracle_c, src, basis, bs)
+
+
+def test_chunked_copy_crosses_boundary(probe_mode, gpu, oracle_c):
+    """A 1-byte insertion before a chunk boundary: the last Copy of chunk 0 ends
+    inside chunk 1, whose walk must start at that exit, not at its first position."""
+    bs = 4096
+    rng = random.Random(5)
+    basis = rng.randbytes(64 * bs + 123)
+    src = basis[:10 * bs] + b"Z" + basis[10 * bs:]
+    idx = _index(gpu, basis, bs)
+    npos = len(src) - bs + 1
+    for cut in (20, 31, 32, 40):
+        d = _chunked(gpu, src, idx, bs, [0, cut * bs, npos])
+        assert d.tuples() == _oracle_ops(oracle_c, src, basis, bs), cut
+    idx.close()
+
+
+def test_chunk_rejects_bad_layout(gpu):
+    import sy_amd._lib as L
+
+    bs = 4096
+    basis = bytes(range(256)) * 64
+    idx = _index(gpu, basis, bs)
+    buf = _to_dev(basis)
+    with pytest.raises(L.SyDeltaError):
+        gpu.Chunk(idx, buf, 0, len(basis), 100, 2 * bs)  # pos_begin not block-aligned
+    with pytest.raises(L.SyDeltaError):
+        gpu.Chunk(idx, buf[:1000], 0, 10 * bs, 0, 2 * bs)  # buffer too short for the windows
+    idx.close()
+
+
+def test_synth_ranges_match_oracle(gpu):
+    import torch
+
+    n, first, bs = 1 << 20, 3 << 16, 8192
+    t = torch.empty(n, dtype=torch.uint8, device="cuda")
+    gpu.synth_fill_range(t, first, 0x5E1D0005)
+    ref = O.synth_bytes(n, 0x5E1D0005, first)
+    assert np.array_equal(t.cpu().numpy(), ref)
+    u = torch.empty_like(t)
+    gpu.synth_mutate_blocks(u, t, first, bs, 0x5E1D0006, 100000)
+    exp = O.synth_edit_blocks(ref, first, bs, 0x5E1D0006, 100000)
+    got = u.cpu().numpy()
+    assert np.array_equal(got, exp)
+    changed = np.nonzero(got != ref)[0] // bs
+    assert 4 <= len(set(changed.tolist())) <= 30 and len(changed) == len(set(changed.tolist()))
