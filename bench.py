@@ -1,6 +1,6 @@
 """bench.py — device-resident delta signature + rolling match on MI355X.
 
-    python bench.py [--gpus N] [--steps K] [--warmup W] [--workload c3|c2|c4]
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--workload c3|c2|c4|c5]
 
 One *step* = one pass of sy's delta hot path over one batch of synthetic input
 already resident in HBM:
@@ -9,9 +9,14 @@ already resident in HBM:
      substitutions -> op list on the host.  Algorithmic bytes = 4 GiB + 4 GiB.
   c2 (config 2): signature only over 4 GiB.
   c4 (config 4 shape): batch of 1 MiB files (signature + per-file match).
-Multi-GPU (torchrun, one rank per GPU): every rank processes its own independent
-pair (file-sharded, no data-path collective) -> "scaling": "weak"; value = total
-bytes of all ranks / max-over-ranks time.
+  c5 (config 5): ONE file of N x 8 GiB (64 GiB at 8 GPUs), bs 8192, 1% of blocks
+     with one substituted byte; chunk-sharded: each rank signs its 8 GiB of the
+     basis, RCCL all-gathers the signature, builds the full index, classifies its
+     8 GiB of the source and the walks are chained (sy_amd/shard.py).
+Multi-GPU (torchrun, one rank per GPU): c3 -- every rank processes its own
+independent pair (file-sharded, no data-path collective); c4 -- the files are
+split over ranks; c5 -- chunks of one file.  value = total bytes of all ranks /
+max-over-ranks time.
 
 The JSON line carries `roofline` for the dominant kernel (per-launch HIP-event
 time measured inside the timed region, algorithmic bytes per launch, HBM peak
@@ -39,16 +44,26 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=2)
-    ap.add_argument("--workload", default="c3", choices=["c3", "c2", "c4"])
-    ap.add_argument("--size-gib", type=float, default=4.0)
-    ap.add_argument("--block-size", type=int, default=4096)
+    ap.add_argument("--workload", default="c3", choices=["c3", "c2", "c4", "c5"])
+    ap.add_argument("--size-gib", type=float, default=None,
+                    help="bytes per rank: c2/c3 basis and source (default 4), c5 chunk (default 8)")
+    ap.add_argument("--block-size", type=int, default=None, help="default 4096 (c5: 8192)")
+    ap.add_argument("--edit-ppm", type=int, default=None,
+                    help="c3: byte substitution rate (default 50000 = 5%%); c5: edited-block rate (default 10000)")
     ap.add_argument("--basis-mib", type=int, default=0,
                     help="c3 only: sign just the first M MiB of the basis (smaller index; "
                          "exercises the LDS-resident filter); 0 = the whole basis")
     ap.add_argument("--files", type=int, default=10000, help="c4: total 1 MiB files over all ranks")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-host-inclusive", action="store_true")
-    return ap.parse_args()
+    a = ap.parse_args()
+    if a.size_gib is None:
+        a.size_gib = 8.0 if a.workload == "c5" else 4.0
+    if a.block_size is None:
+        a.block_size = 8192 if a.workload == "c5" else 4096
+    if a.edit_ppm is None:
+        a.edit_ppm = 10000 if a.workload == "c5" else 50000
+    return a
 
 
 def cpu_baseline(bs: int):
@@ -222,12 +237,35 @@ def main():
     basis = None
     if args.workload != "c4":
         basis = torch.empty(n, dtype=torch.uint8, device="cuda")
-        dev.synth_fill(basis, seed_base)
+        if args.workload != "c5":
+            dev.synth_fill(basis, seed_base)
     new = None
     files = None
     if args.workload in ("c3",):
         new = torch.empty(n, dtype=torch.uint8, device="cuda")
-        dev.synth_mutate(new, basis, seed_base + 1, 50000)
+        dev.synth_mutate(new, basis, seed_base + 1, args.edit_ppm)
+    c5 = None
+    if args.workload == "c5":
+        # BASELINE config 5: one file of world * n bytes; this rank owns basis bytes
+        # [rank*n, (rank+1)*n) and window starts [rank*n, (rank+1)*n) of the source
+        # (+ the next bs-1 bytes as halo).  Counter-based generators give every rank
+        # the same bytes for the same file offsets.
+        from sy_amd import shard
+
+        file_len = world * n
+        first = rank * n
+        dev.synth_fill_range(basis, first, 0x5E1D0005)
+        p0, p1 = shard.chunk_bounds(file_len, bs, world, rank)
+        buf_end = file_len if rank == world - 1 else min(file_len, p1 + bs - 1)
+        new = torch.empty((buf_end - first + 15) // 16 * 16, dtype=torch.uint8, device="cuda")
+        src_view = new[:buf_end - first]
+        dev.synth_fill_range(src_view, first, 0x5E1D0005)
+        dev.synth_mutate_blocks(src_view, src_view, first, bs, 0x5E1D0006, args.edit_ppm)
+        if world > 1:
+            gather, bcast = shard.torch_collectives(dist, "cuda")
+        else:
+            gather, bcast = (lambda v: [v]), (lambda v, src: v)
+        c5 = dict(file_len=file_len, first=first, p0=p0, p1=p1, gather=gather, bcast=bcast, shard=shard)
     if args.workload == "c4":
         # BASELINE config 4: files [lo, hi) of --files 1 MiB files go to this rank
         # (equal sizes, so contiguous ranges are the bytes-balanced LPT split).
@@ -247,6 +285,20 @@ def main():
             w, s = dev.signature(basis[:nb_bytes], bs, stream=stream)
             idx = dev.Index(w, s, bs, bs, device=local, stream=stream)
             d = dev.match(idx, new, stream=stream)
+            idx.close()
+            return d
+        if args.workload == "c5":
+            w, s = dev.signature(basis, bs, stream=stream)
+            if world > 1:  # the one exchange step: RCCL all-gather of the signature SoA
+                W = torch.empty(world * w.numel(), dtype=w.dtype, device="cuda")
+                S = torch.empty(world * s.numel(), dtype=s.dtype, device="cuda")
+                dist.all_gather_into_tensor(W, w)
+                dist.all_gather_into_tensor(S, s)
+                w, s = W, S
+            idx = dev.Index(w, s, bs, bs, device=local, stream=stream)
+            ch = dev.Chunk(idx, new, c5["first"], c5["file_len"], c5["p0"], c5["p1"], stream=stream)
+            d, entry = c5["shard"].walk_chain(ch, rank, world, c5["p0"], c5["gather"], c5["bcast"])
+            ch.close()
             idx.close()
             return d
         # c4: batched signature of all basis files, per-file index, one batched match
@@ -284,6 +336,8 @@ def main():
         bytes_per_step = n
     elif args.workload == "c3":
         bytes_per_step = nb_bytes + n
+    elif args.workload == "c5":
+        bytes_per_step = 2 * n
     else:
         bytes_per_step = int(files[1].sum() + files[3].sum())
     total_bytes = bytes_per_step * args.steps * world
@@ -296,7 +350,7 @@ def main():
     # split into segments of 2^31 positions).
     src_bytes = int(files[3].sum()) if args.workload == "c4" else n
     algo_step = {"k_scan": src_bytes, "k_scan_lds": src_bytes, "k_sig_fast": nb_bytes if args.workload == "c3" else n,
-                 "k_sig_batch": n, "k_sig_wave": n}
+                 "k_sig_batch": n, "k_sig_wave": n, "k_probe": src_bytes}
     dom = max(prof, key=lambda k: prof[k]["ms"]) if prof else None
     roof = None
     if dom and dom in algo_step:
@@ -329,18 +383,24 @@ def main():
             "scaling": "strong" if args.workload == "c4" else "weak",
             "vs_baseline": None,
             "dtype": "u8",
-            "data": "synthetic (counter-based splitmix64 bytes; Bernoulli byte substitutions)",
+            "data": ("synthetic (counter-based splitmix64 bytes; one substituted byte in 1% of 8 KiB blocks)"
+                     if args.workload == "c5" else
+                     "synthetic (counter-based splitmix64 bytes; Bernoulli byte substitutions)"),
             "config": {
                 "workload": {
                     "c3": "C3: signature(4 GiB basis) + rolling match(4 GiB source, 5% random byte edits), bs 4096",
                     "c2": "C2: signature only over 4 GiB, bs 4096",
                     "c4": f"C4: {args.files} x 1 MiB files (1-byte insertion + 16 substitutions each), "
                           f"batched signature + per-file index + batched match, file-sharded over ranks",
+                    "c5": f"C5: one {world * n / GIB:.0f} GiB file, bs {bs}, {args.edit_ppm / 1e4:g}% of blocks with "
+                          f"one substituted byte; signature + all-gather + index + chunk match, chunk-sharded",
                 }[args.workload],
                 "block_size": bs,
                 "basis_bytes": nb_bytes if args.workload == "c3" else n,
                 "bytes_per_rank_per_step": bytes_per_step,
-                "parallelism": f"file-sharded x{world} (independent pairs per rank, no collective)",
+                "parallelism": (f"chunk-sharded x{world} (RCCL all-gather of the signature, chained walks)"
+                                if args.workload == "c5" else
+                                f"file-sharded x{world} (independent pairs per rank, no collective)"),
                 **({"files": args.files, "files_this_rank": len(files[0])} if args.workload == "c4" else {}),
             },
             "pct_hbm_peak": round(value * GIB / 1e9 / HBM_PEAK_GBS * 100, 2),

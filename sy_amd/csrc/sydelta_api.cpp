@@ -18,6 +18,7 @@
 #include <algorithm>
 #include <array>
 #include <atomic>
+#include <chrono>
 #include <cmath>
 #include <map>
 #include <memory>
@@ -375,6 +376,33 @@ extern "C" int sydelta_index_create_batch(int device, const uint32_t* weak, cons
 // ---------------------------------------------------------------------------
 // delta object
 // ---------------------------------------------------------------------------
+// Recycled op arrays: a walk over a copy-heavy source emits one op per block
+// (1 Mi ops = 24 MiB for 8 GiB at 8 KiB blocks); first-touch page faults of a
+// fresh array cost more than the walk itself, so freed deltas hand their arrays
+// back for the next walk (bounded: 4 arrays).
+namespace {
+std::mutex g_ops_mu;
+std::vector<std::vector<sydelta_op>> g_ops_pool;
+std::vector<sydelta_op> take_ops(size_t want) {
+    std::lock_guard<std::mutex> lk(g_ops_mu);
+    size_t best = g_ops_pool.size();
+    for (size_t i = 0; i < g_ops_pool.size(); ++i)
+        if (best == g_ops_pool.size() || g_ops_pool[i].capacity() > g_ops_pool[best].capacity()) best = i;
+    std::vector<sydelta_op> v;
+    if (best < g_ops_pool.size() && (want == 0 || g_ops_pool[best].capacity() >= want / 2)) {
+        v.swap(g_ops_pool[best]);
+        g_ops_pool.erase(g_ops_pool.begin() + best);
+    }
+    v.clear();
+    return v;
+}
+void give_ops(std::vector<sydelta_op>&& v) {
+    if (v.capacity() < 4096) return;
+    std::lock_guard<std::mutex> lk(g_ops_mu);
+    if (g_ops_pool.size() < 4) g_ops_pool.push_back(std::move(v));
+}
+}  // namespace
+
 struct sydelta_delta {
     std::vector<sydelta_op> ops;
     uint64_t source_size = 0, block_size = 0;
@@ -412,7 +440,11 @@ extern "C" double sydelta_delta_compression_ratio(const sydelta_delta* d) {
     const uint64_t tot = lit + cop;
     return tot == 0 ? 1.0 : (double)lit / (double)tot;
 }
-extern "C" void sydelta_delta_free(sydelta_delta* d) { delete d; }
+extern "C" void sydelta_delta_free(sydelta_delta* d) {
+    if (!d) return;
+    give_ops(std::move(d->ops));
+    delete d;
+}
 
 extern "C" uint64_t sydelta_delta_batch_count(const sydelta_delta_batch* b) { return b ? b->d.size() : 0; }
 extern "C" const sydelta_delta* sydelta_delta_batch_get(const sydelta_delta_batch* b, uint64_t i) {
@@ -462,8 +494,9 @@ struct Src {
     uint64_t kb = 0, nblk = 0;  // blocks kb .. kb+nblk-1 (position k*n) cover [p0, p1)
     bool probed = false;
     std::vector<uint32_t> ahit;    // probed: per block, its aligned window's hit or kNoBlk
+    uint64_t nahit = 0;            // aligned windows that hit
     std::vector<uint8_t> scanned;  // probed: per block, all its window starts were scanned
-    std::vector<uint64_t> hpos;    // verified hits found so far, sorted, unique
+    std::vector<uint64_t> hpos;    // hits found by scans, sorted, unique
     std::vector<uint32_t> hblk;    // their global block indices
 };
 
@@ -517,7 +550,8 @@ struct BasisInfo {
 // run.  Returns 1 with *need = the first position whose class is unknown.
 int walk_src(const Src& c, uint64_t n, uint64_t entry, const BasisInfo& bi, bool final_src, int tail_match,
              std::vector<sydelta_op>& ops, uint64_t* exit, uint64_t* need) {
-    ops.clear();
+    const size_t ops0 = ops.size();  // appended to; rolled back on a need
+    ops.reserve(ops0 + 2 * (c.hpos.size() + c.nahit) + 3);
     uint64_t x = entry, lit = entry;
     auto data = [&](uint64_t a, uint64_t b) {
         if (b > a) ops.push_back({SYDELTA_OP_DATA, 0, a, b - a});
@@ -528,23 +562,32 @@ int walk_src(const Src& c, uint64_t n, uint64_t entry, const BasisInfo& bi, bool
     };
     size_t i = std::lower_bound(c.hpos.begin(), c.hpos.end(), x) - c.hpos.begin();
     const size_t H = c.hpos.size();
+    const uint64_t kend = c.kb + c.nblk;
+    uint64_t ka = c.kb;  // next aligned window that may hit (probed sources)
     while (x < c.p1) {
+        // next hit at or after x: the next scan hit or the next aligned hit
         while (i < H && c.hpos[i] < x) ++i;
-        const uint64_t p = i < H ? c.hpos[i] : c.p1;
+        uint64_t p = i < H ? c.hpos[i] : c.p1;
+        uint32_t pb = i < H ? c.hblk[i] : kNoBlk;
+        if (c.probed) {
+            if (ka * n < x) ka = (x + n - 1) / n;  // after an aligned Copy x == (ka+1)*n: no division
+            while (ka < kend && ka * n < p && c.ahit[ka - c.kb] == kNoBlk) ++ka;
+            if (ka < kend && ka * n < p) { p = ka * n; pb = c.ahit[ka - c.kb]; }
+        }
         const uint64_t u = first_unknown(c, n, x, p);
         if (u != kUnknownNone) {
             *need = u;
+            ops.resize(ops0);
             return 1;
         }
-        if (i == H) {
+        if (pb == kNoBlk) {
             x = c.p1;
             break;
         }
         data(lit, p);
-        copy(c.hblk[i]);
+        copy(pb);
         x = p + n;  // generator.rs:144 / :313
         lit = x;
-        ++i;
     }
     if (!final_src) {
         data(lit, c.p1);
@@ -617,12 +660,15 @@ int Classifier::probe(int mode) {
         if (!np) return SYDELTA_OK;
         DevBuf jb;
         const size_t jbytes = (jobs.size() * sizeof(ProbeJob) + 255) & ~(size_t)255;
-        HIP_TRY(hipMallocAsync(&jb.p, jbytes + np * 4, s));
+        const size_t obytes = (np * 4 + 255) & ~(size_t)255;
+        HIP_TRY(hipMallocAsync(&jb.p, jbytes + 2 * obytes + np * 8, s));
         jb.s = s;
         uint32_t* d_out = (uint32_t*)((uint8_t*)jb.p + jbytes);
+        uint32_t* d_pw = (uint32_t*)((uint8_t*)jb.p + jbytes + obytes);
+        uint64_t* d_pst = (uint64_t*)((uint8_t*)jb.p + jbytes + 2 * obytes);
         HIP_TRY(hipMemcpyAsync(jb.p, jobs.data(), jobs.size() * sizeof(ProbeJob), hipMemcpyHostToDevice, s));
         HIP_TRY(launch_probe(base, (const ProbeJob*)jb.p, (uint32_t)jobs.size(), np, stride, (uint32_t)n, fast,
-                             ix->ix, d_out, s, prof));
+                             ix->ix, d_pw, d_pst, d_out, s, prof));
         HIP_TRY(hipMemcpyAsync(out.data(), d_out, np * 4, hipMemcpyDeviceToHost, s));
         HIP_TRY(hipStreamSynchronize(s));
         return SYDELTA_OK;
@@ -642,11 +688,8 @@ int Classifier::probe(int mode) {
         c.probed = true;
         c.ahit.assign(out.begin() + pfx[i], out.begin() + pfx[i + 1]);
         c.scanned.assign(c.nblk, 0);
-        std::vector<uint64_t> pos;
-        std::vector<uint32_t> blk;
-        for (uint64_t k = 0; k < c.nblk; ++k)
-            if (c.ahit[k] != kNoBlk) { pos.push_back((c.kb + k) * n); blk.push_back(c.ahit[k]); }
-        merge_hits(c, pos, blk);
+        c.nahit = 0;
+        for (uint32_t v : c.ahit) c.nahit += v != kNoBlk;
     }
     return SYDELTA_OK;
 }
@@ -769,8 +812,15 @@ int Classifier::scan(const std::vector<std::array<uint64_t, 3>>& ranges) {
     return SYDELTA_OK;
 }
 
+double ms_since(std::chrono::steady_clock::time_point t0) {
+    return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+}
+
 int Classifier::classify(int mode) {
+    static const bool host_timing = getenv("SYDELTA_HOST_TIMING") != nullptr;
+    const auto t0 = std::chrono::steady_clock::now();
     if (int r = probe(mode)) return r;
+    const double t_probe = ms_since(t0);
     const uint64_t gap_blocks = std::max<uint64_t>(1, scan_tile_positions() / n);
     std::vector<std::array<uint64_t, 3>> ranges;
     for (size_t i = 0; i < src.size(); ++i) {
@@ -796,16 +846,29 @@ int Classifier::classify(int mode) {
             k = e;
         }
     }
-    return scan(ranges);
+    const auto t1 = std::chrono::steady_clock::now();
+    const int r = scan(ranges);
+    if (host_timing)
+        fprintf(stderr, "sydelta classify: probe %.3f ms, ranges %zu (%.3f ms), scan %.3f ms\n", t_probe,
+                ranges.size(), std::chrono::duration<double, std::milli>(t1 - t0).count() - t_probe, ms_since(t1));
+    return r;
 }
 
 int Classifier::walk(size_t i, uint64_t entry, const BasisInfo& bi, bool final_src, int tail_match, sydelta_delta* d,
                      uint64_t* exit) {
     Src& c = src[i];
-    std::vector<sydelta_op> ops;
+    std::vector<sydelta_op>& ops = d->ops;
+    if (ops.empty() && c.nahit + c.hpos.size() >= 4096) ops = take_ops(2 * (c.nahit + c.hpos.size()));
+    static const bool host_timing = getenv("SYDELTA_HOST_TIMING") != nullptr;
     for (int round = 0;; ++round) {
         uint64_t need = 0;
-        if (!walk_src(c, n, entry, bi, final_src, tail_match, ops, exit, &need)) break;
+        const auto t0 = std::chrono::steady_clock::now();
+        const int r = walk_src(c, n, entry, bi, final_src, tail_match, ops, exit, &need);
+        if (host_timing)
+            fprintf(stderr, "sydelta walk round %d: %.3f ms, %zu ops, need=%d\n", round,
+                    std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count(),
+                    ops.size(), r);
+        if (!r) break;
         // the walk jumped into a block only its aligned window was classified for
         const uint64_t k = need / n;
         if (round < 4)
@@ -813,7 +876,6 @@ int Classifier::walk(size_t i, uint64_t entry, const BasisInfo& bi, bool final_s
         else
             { if (int r = scan({{i, k, c.kb + c.nblk}})) return r; }
     }
-    d->ops.insert(d->ops.end(), ops.begin(), ops.end());
     return SYDELTA_OK;
 }
 
@@ -910,7 +972,7 @@ static int match_impl(sydelta_index* ix, const uint8_t* d_buf, const uint64_t* s
         const BasisInfo bi{ix->fblk[f], ix->fblk[f + 1] - ix->fblk[f], ix->last_size[f]};
         uint64_t exit = 0;
         if (int r = C.walk(f, 0, bi, true, tail[f], d, &exit)) return r;
-        d->stats.verified_hits = C.src[f].hpos.size();
+        d->stats.verified_hits = C.src[f].hpos.size() + C.src[f].nahit;
         finish_stats(d);
         b->total.verified_hits += d->stats.verified_hits;
         b->total.copy_ops += d->stats.copy_ops;
@@ -1263,12 +1325,13 @@ extern "C" int sydelta_chunk_classify(sydelta_index* idx, const uint8_t* d_buf, 
     if (idx->nfiles != 1) return fail(SYDELTA_E_INVAL, "chunked match needs a single-file index");
     const uint64_t n = idx->bs;
     if (n > scan_max_window()) return fail(SYDELTA_E_INVAL, "chunked match needs block_size <= %u", scan_max_window());
-    if (pos_begin % n) return fail(SYDELTA_E_INVAL, "pos_begin must be a multiple of block_size");
-    if (pos_end < pos_begin) return fail(SYDELTA_E_INVAL, "pos_end < pos_begin");
+    const uint64_t npos = file_len >= n ? file_len - n + 1 : 0;
+    // a chunk at or past the last window start is empty (it may still own the tail)
+    if (pos_begin < npos && pos_begin % n) return fail(SYDELTA_E_INVAL, "pos_begin must be a multiple of block_size");
+    if (pos_end < pos_begin && pos_begin < npos) return fail(SYDELTA_E_INVAL, "pos_end < pos_begin");
     if ((buf_pos & 15) || ((uintptr_t)d_buf & 15))
         return fail(SYDELTA_E_INVAL, "d_buf and buf_pos must be 16-byte aligned");
-    if (buf_pos > (pos_begin & ~15ull)) return fail(SYDELTA_E_INVAL, "buffer starts after the chunk");
-    const uint64_t npos = file_len >= n ? file_len - n + 1 : 0;
+    if (buf_pos > (std::min(pos_begin, npos) & ~15ull)) return fail(SYDELTA_E_INVAL, "buffer starts after the chunk");
     const bool final_src = pos_end >= npos;
     const uint64_t p1 = std::min(pos_end, npos), p0 = std::min(pos_begin, p1);
     const uint64_t need_end = final_src ? file_len : std::min(file_len, p1 + n - 1);
@@ -1327,7 +1390,7 @@ extern "C" int sydelta_chunk_walk(sydelta_chunk* ch, uint64_t entry, uint64_t* e
     const int r = C.walk(0, entry, ch->bi, ch->final_src, ch->tail_flag, d.get(), exit_pos);
     C.prof = nullptr;
     if (r) return r;
-    d->stats.verified_hits = c.hpos.size();
+    d->stats.verified_hits = c.hpos.size() + c.nahit;
     d->stats.weak_hits = C.weak_hits;
     finish_stats(d.get());
     *out = d.release();

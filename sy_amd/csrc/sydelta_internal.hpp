@@ -112,9 +112,10 @@ struct ProbeJob {
     uint32_t pad;
 };
 // fast: n % 64 == 0, n >= 256 and every window 16-byte aligned.
+// Scratch: d_pw[nprobes], d_pst[nprobes] (the windows' weak / strong).
 hipError_t launch_probe(const uint8_t* d_base, const ProbeJob* d_jobs, uint32_t njobs, uint64_t nprobes,
-                        uint32_t stride, uint32_t n, bool fast, const DeviceIndex& ix, uint32_t* d_out, hipStream_t s,
-                        Profiler* prof);
+                        uint32_t stride, uint32_t n, bool fast, const DeviceIndex& ix, uint32_t* d_pw,
+                        uint64_t* d_pst, uint32_t* d_out, hipStream_t s, Profiler* prof);
 // Tail rule (generator.rs:156-184) of every listed file: flag[i] = 1 iff the
 // suffix of source i hashes to (weak[blk], strong[blk]) of its last basis block.
 struct TailJob {

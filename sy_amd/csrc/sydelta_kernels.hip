@@ -224,18 +224,13 @@ __global__ void k_idx_insert(const uint32_t* __restrict__ weak, uint64_t n, cons
     }
 }
 
-// Candidates grouped by slot.  The order inside a group is arbitrary (atomics):
-// generator.rs:127-133 takes the first candidate in index order whose strong
-// matches, which verification reproduces as the minimum matching block index.
-// cstrong mirrors order with the candidates' strong hashes so a verification
-// reads both in one round trip.
-__global__ void k_idx_scatter(uint64_t n, const uint32_t* __restrict__ slot_of, const uint32_t* __restrict__ start,
-                              uint32_t* __restrict__ fill, uint32_t* __restrict__ order) {
+// Candidates grouped by slot in index order: order = block indices stably sorted
+// by slot (launch_index_build), so the first candidate of a sweep whose strong
+// matches is generator.rs:127-133's choice.  cstrong mirrors order with the
+// candidates' strong hashes so a verification reads both in one round trip.
+__global__ void k_iota(uint32_t* __restrict__ v, uint64_t n) {
     const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= n) return;
-    const uint32_t s = slot_of[i];
-    const uint32_t k = atomicAdd(&fill[s], 1u);
-    order[start[s] + k] = (uint32_t)i;
+    if (i < n) v[i] = (uint32_t)i;
 }
 
 __global__ void k_idx_cstrong(uint64_t n, const uint32_t* __restrict__ order, const uint64_t* __restrict__ strong,
@@ -259,6 +254,22 @@ __device__ __forceinline__ int64_t table_find(const uint32_t* __restrict__ keys,
     }
 }
 
+// Candidates of one slot are stored in index order (launch_index_build sorts them),
+// so generator.rs:127-133's "first candidate whose strong matches" is the first hit
+// of an in-order sweep: 64 candidates per step, stop at the first step with a match.
+// Wave-uniform arguments; every lane returns the block (or kNoBlock).
+__device__ __forceinline__ uint32_t first_strong_match(const uint32_t* __restrict__ order,
+                                                       const uint64_t* __restrict__ cstrong, uint32_t s0, uint32_t cn,
+                                                       uint64_t st) {
+    const uint32_t lane = threadIdx.x & 63;
+    for (uint32_t base = 0; base < cn; base += 64) {
+        const uint32_t j = base + lane;
+        const uint64_t m = __ballot(j < cn && cstrong[s0 + j] == st);
+        if (m) return order[s0 + base + (uint32_t)__builtin_ctzll(m)];
+    }
+    return 0xFFFFFFFFu;
+}
+
 // ===========================================================================
 // K5: aligned-window probe (block-aligned positions k*n of a source)
 // ===========================================================================
@@ -272,41 +283,23 @@ __device__ __forceinline__ int64_t table_find(const uint32_t* __restrict__ keys,
 // the hit, or kNoBlock.
 constexpr uint32_t kNoBlock = 0xFFFFFFFFu;
 
-__device__ __forceinline__ uint32_t lookup_first(const FileIx& F, const uint32_t* __restrict__ filt,
-                                                 const uint32_t* __restrict__ keys, const uint32_t* __restrict__ start,
-                                                 const uint32_t* __restrict__ cnt, const uint32_t* __restrict__ order,
-                                                 const uint64_t* __restrict__ cstrong, uint32_t wk, uint64_t st) {
-    // wave-uniform arguments; every lane returns the same block
-    const uint32_t lane = threadIdx.x & 63;
-    const uint32_t h = filt_hash(wk & 0xFFFF, wk >> 16);
-    if ((filt_mask(h) & ~filt[F.filt_off + (h >> F.fwshift)]) != 0) return kNoBlock;
-    const int64_t slot = table_find(keys + F.slot_off, F.bmask, wk);
-    if (slot < 0) return kNoBlock;
-    const uint64_t gs = F.slot_off + (uint64_t)slot;
-    const uint32_t s0 = start[gs], c = cnt[gs];
-    uint32_t best = kNoBlock;
-    for (uint32_t j = lane; j < c; j += 64)
-        if (cstrong[s0 + j] == st) best = min(best, order[s0 + j]);
-#pragma unroll
-    for (int m = 1; m < 64; m <<= 1) best = min(best, (uint32_t)__shfl_xor((int)best, m, 64));
-    return best;
-}
-
-__global__ __launch_bounds__(256) void k_probe(const uint8_t* __restrict__ base, const ProbeJob* __restrict__ jobs,
-                                               uint32_t njobs, uint64_t nprobes, uint32_t stride, uint32_t n,
-                                               uint32_t fast, const FileIx* __restrict__ files,
-                                               const uint32_t* __restrict__ filt, const uint32_t* __restrict__ keys,
-                                               const uint32_t* __restrict__ start, const uint32_t* __restrict__ cnt,
-                                               const uint32_t* __restrict__ order,
-                                               const uint64_t* __restrict__ cstrong, uint32_t* __restrict__ out) {
-    const uint64_t w = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
-    if (w >= nprobes) return;
-    uint32_t lo = 0, hi = njobs;  // job holding probe w (wave-uniform)
+__device__ __forceinline__ uint32_t probe_job(const ProbeJob* __restrict__ jobs, uint32_t njobs, uint64_t w) {
+    uint32_t lo = 0, hi = njobs;
     while (hi - lo > 1) {
         const uint32_t mid = (lo + hi) >> 1;
         if (jobs[mid].pfx <= w) lo = mid; else hi = mid;
     }
-    const ProbeJob J = jobs[lo];
+    return lo;
+}
+
+// Pass 1: weak + strong of every probed window (one wave per window, the
+// signature kernel's access pattern), into pw / pst.
+__global__ __launch_bounds__(256) void k_probe(const uint8_t* __restrict__ base, const ProbeJob* __restrict__ jobs,
+                                               uint32_t njobs, uint64_t nprobes, uint32_t stride, uint32_t n,
+                                               uint32_t fast, uint32_t* __restrict__ pw, uint64_t* __restrict__ pst) {
+    const uint64_t w = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+    if (w >= nprobes) return;
+    const ProbeJob J = jobs[probe_job(jobs, njobs, w)];
     const uint64_t k = J.k0 + (w - J.pfx) * stride;
     const uint8_t* p = base + J.src + k * n;
     uint32_t wk;
@@ -318,11 +311,42 @@ __global__ __launch_bounds__(256) void k_probe(const uint8_t* __restrict__ base,
     } else {
         wk = 0; st = 0;
         if ((threadIdx.x & 63) == 0) { wk = adler_scalar(p, n); st = xxh3_short(p, n); }
-        wk = (uint32_t)__shfl((int)wk, 0, 64);
-        st = shfl64(st, 0);
     }
-    const uint32_t b = lookup_first(files[J.file], filt, keys, start, cnt, order, cstrong, wk, st);
-    if ((threadIdx.x & 63) == 0) out[w] = b;
+    if ((threadIdx.x & 63) == 0) {
+        pw[w] = wk;
+        pst[w] = st;
+    }
+}
+
+// Pass 2: one thread per window: filter, exact table, first candidate in index
+// order with equal strong (generator.rs:121-155).
+__global__ __launch_bounds__(256) void k_probe_lookup(const ProbeJob* __restrict__ jobs, uint32_t njobs,
+                                                      uint64_t nprobes, const FileIx* __restrict__ files,
+                                                      const uint32_t* __restrict__ filt,
+                                                      const uint32_t* __restrict__ keys,
+                                                      const uint32_t* __restrict__ start,
+                                                      const uint32_t* __restrict__ cnt,
+                                                      const uint32_t* __restrict__ order,
+                                                      const uint64_t* __restrict__ cstrong,
+                                                      const uint32_t* __restrict__ pw, const uint64_t* __restrict__ pst,
+                                                      uint32_t* __restrict__ out) {
+    const uint64_t w = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (w >= nprobes) return;
+    const FileIx F = files[jobs[probe_job(jobs, njobs, w)].file];
+    const uint32_t wk = pw[w];
+    uint32_t best = kNoBlock;
+    const uint32_t h = filt_hash(wk & 0xFFFF, wk >> 16);
+    if ((filt_mask(h) & ~filt[F.filt_off + (h >> F.fwshift)]) == 0) {
+        const int64_t slot = table_find(keys + F.slot_off, F.bmask, wk);
+        if (slot >= 0) {
+            const uint64_t gs = F.slot_off + (uint64_t)slot;
+            const uint32_t s0 = start[gs], c = cnt[gs];
+            const uint64_t st = pst[w];
+            for (uint32_t j = 0; j < c; ++j)
+                if (cstrong[s0 + j] == st) { best = order[s0 + j]; break; }
+        }
+    }
+    out[w] = best;
 }
 
 // ===========================================================================
@@ -490,14 +514,7 @@ __device__ __forceinline__ void drain_wq(const ScanArgs& a, const SegCtx& c, uin
             if (lane == 0) st = xxh3_short(win, a.n);
             st = shfl64(st, 0);
         }
-        const uint32_t s0 = a.start[e.y], cn = a.cnt[e.y];
-        uint32_t best = 0xFFFFFFFFu;
-        for (uint32_t j = lane; j < cn; j += 64) {
-            const uint32_t bi = a.order[s0 + j];
-            if (a.cstrong[s0 + j] == st) best = min(best, bi);
-        }
-#pragma unroll
-        for (int m = 1; m < 64; m <<= 1) best = min(best, (uint32_t)__shfl_xor((int)best, m, 64));
+        const uint32_t best = first_strong_match(a.order, a.cstrong, a.start[e.y], a.cnt[e.y], st);
         if (lane == 0) wq[i].y = best;  // verified block, or none
     }
     // one output reservation per wave: the counter is shared by the whole chip
@@ -833,13 +850,7 @@ __device__ __forceinline__ void verify3(const ScanArgs& a, uint4* wq, uint32_t n
             if (kcn == 1) {  // the usual case: the one candidate was fetched above
                 if (shfl64(st0, k) == st) best = (uint32_t)__shfl((int)b0, k, 64);
             } else {
-                const uint32_t ks0 = (uint32_t)__shfl((int)s0, k, 64);
-                for (uint32_t j = lane; j < kcn; j += 64) {
-                    const uint32_t bi = a.order[ks0 + j];
-                    if (a.cstrong[ks0 + j] == st) best = min(best, bi);
-                }
-#pragma unroll
-                for (int m = 1; m < 64; m <<= 1) best = min(best, (uint32_t)__shfl_xor((int)best, m, 64));
+                best = first_strong_match(a.order, a.cstrong, (uint32_t)__shfl((int)s0, k, 64), kcn, st);
             }
             if (lane == 0) wq[base + k].w = best;  // verified block, or none
         }
@@ -1265,7 +1276,6 @@ hipError_t launch_index_build(const uint32_t* d_weak, const uint64_t* d_strong, 
     if ((e = hipMemsetAsync(ix.filt, 0, ix.fwords * 4, s))) return e;
     if ((e = hipMemsetAsync(ix.keys, 0xFF, ix.nslots * 4, s))) return e;
     if ((e = hipMemsetAsync(ix.cnt, 0, ix.nslots * 4, s))) return e;
-    if ((e = hipMemsetAsync(ix.fill, 0, ix.nslots * 4, s))) return e;
     const uint64_t n = ix.nblocks;
     if (n == 0) return hipSuccess;
     {
@@ -1281,24 +1291,43 @@ hipError_t launch_index_build(const uint32_t* d_weak, const uint64_t* d_strong, 
     (void)hipFreeAsync(d_tmp, s);
     if (e) return e;
     {
-        ProfScope ps(prof, s, "k_idx_scatter");
-        hipLaunchKernelGGL(k_idx_scatter, dim3(grid_for(n, 256)), dim3(256), 0, s, n, ix.slot_of, ix.start, ix.fill,
-                           ix.order);
+        // order = block indices stably sorted by slot (keys slot_of, scratch: fill / cstrong)
+        ProfScope ps(prof, s, "k_idx_order");
+        uint32_t* iota = (uint32_t*)ix.cstrong;              // n u32 (cstrong holds n u64)
+        uint32_t* keys_out = ix.fill;                        // nslots >= n u32
+        hipLaunchKernelGGL(k_iota, dim3(grid_for(n, 256)), dim3(256), 0, s, iota, n);
+        if ((e = hipGetLastError())) return e;
+        int end_bit = 1;
+        while (end_bit < 32 && (1ull << end_bit) < ix.nslots) ++end_bit;
+        size_t tmp2 = 0;
+        if ((e = hipcub::DeviceRadixSort::SortPairs(nullptr, tmp2, ix.slot_of, keys_out, iota, ix.order, (int)n, 0,
+                                                    end_bit, s)))
+            return e;
+        void* d_t2 = nullptr;
+        if ((e = hipMallocAsync(&d_t2, tmp2 ? tmp2 : 16, s))) return e;
+        e = hipcub::DeviceRadixSort::SortPairs(d_t2, tmp2, ix.slot_of, keys_out, iota, ix.order, (int)n, 0, end_bit,
+                                               s);
+        (void)hipFreeAsync(d_t2, s);
+        if (e) return e;
     }
-    if ((e = hipGetLastError())) return e;
     hipLaunchKernelGGL(k_idx_cstrong, dim3(grid_for(n, 256)), dim3(256), 0, s, n, ix.order, d_strong, ix.cstrong);
     return hipGetLastError();
 }
 
 hipError_t launch_probe(const uint8_t* d_base, const ProbeJob* d_jobs, uint32_t njobs, uint64_t nprobes,
-                        uint32_t stride, uint32_t n, bool fast, const DeviceIndex& ix, uint32_t* d_out, hipStream_t s,
-                        Profiler* prof) {
+                        uint32_t stride, uint32_t n, bool fast, const DeviceIndex& ix, uint32_t* d_pw,
+                        uint64_t* d_pst, uint32_t* d_out, hipStream_t s, Profiler* prof) {
     if (!nprobes) return hipSuccess;
     if (fast && (n % 64 != 0 || n < 256)) return hipErrorInvalidValue;
-    ProfScope ps(prof, s, "k_probe");
-    hipLaunchKernelGGL(k_probe, dim3(grid_for(nprobes * 64, 256)), dim3(256), 0, s, d_base, d_jobs, njobs, nprobes,
-                       stride, n, fast ? 1u : 0u, ix.d_files, ix.filt, ix.keys, ix.start, ix.cnt, ix.order,
-                       ix.cstrong, d_out);
+    {
+        ProfScope ps(prof, s, stride > 1 ? "k_probe_sample" : "k_probe");
+        hipLaunchKernelGGL(k_probe, dim3(grid_for(nprobes * 64, 256)), dim3(256), 0, s, d_base, d_jobs, njobs,
+                           nprobes, stride, n, fast ? 1u : 0u, d_pw, d_pst);
+    }
+    if (hipError_t e = hipGetLastError()) return e;
+    ProfScope ps(prof, s, "k_probe_lookup");
+    hipLaunchKernelGGL(k_probe_lookup, dim3(grid_for(nprobes, 256)), dim3(256), 0, s, d_jobs, njobs, nprobes,
+                       ix.d_files, ix.filt, ix.keys, ix.start, ix.cnt, ix.order, ix.cstrong, d_pw, d_pst, d_out);
     return hipGetLastError();
 }
 

@@ -107,14 +107,34 @@ class DeviceDelta:
         return [("C" if int(k) == 0 else "D", int(x), int(y)) for k, x, y in zip(self.kind, self.a, self.b)]
 
 
-def _device_delta(h) -> DeviceDelta:
+_OP_DTYPE = np.dtype([("kind", "<u4"), ("reserved", "<u4"), ("a", "<u8"), ("b", "<u8")])
+
+
+class _DeltaHandle:
+    """Owns a sydelta_delta* whose op array numpy views borrow."""
+
+    def __init__(self, h):
+        self.h = h
+
+    def __del__(self):
+        try:
+            lib.sydelta_delta_free(self.h)
+        except Exception:
+            pass
+
+
+def _device_delta(h, owner=None) -> DeviceDelta:
     nops = int(lib.sydelta_delta_num_ops(h))
     if nops:
         p = lib.sydelta_delta_ops(h)
-        raw = np.ctypeslib.as_array(ctypes.cast(p, ctypes.POINTER(ctypes.c_uint64)), shape=(nops * 3,)).copy()
-        raw = raw.reshape(nops, 3)
-        kind = (raw[:, 0] & 0xFFFFFFFF).astype(np.uint8)
-        a, b = raw[:, 1].copy(), raw[:, 2].copy()
+        if owner is not None:  # zero-copy view of the library's sydelta_op array
+            buf = (ctypes.c_uint8 * (24 * nops)).from_address(ctypes.addressof(p.contents))
+            buf._owner = owner  # the handle is freed when the last view goes away
+            raw = np.frombuffer(buf, dtype=_OP_DTYPE)
+        else:
+            raw = np.frombuffer((ctypes.c_uint8 * (24 * nops)).from_address(ctypes.addressof(p.contents)),
+                                dtype=_OP_DTYPE).copy()
+        kind, a, b = raw["kind"], raw["a"], raw["b"]
     else:
         kind = np.zeros(0, np.uint8)
         a = np.zeros(0, np.uint64)
@@ -147,10 +167,7 @@ def match(index: Index, src: torch.Tensor, stream=None, length: int | None = Non
     n = src.numel() if length is None else length
     h = ctypes.c_void_p()
     check(lib.sydelta_match_device(index.h, _ptr(src) if n else None, n, _stream(stream), ctypes.byref(h)))
-    try:
-        return _device_delta(h)
-    finally:
-        lib.sydelta_delta_free(h)
+    return _device_delta(h, _DeltaHandle(h))
 
 
 class Chunk:
@@ -170,10 +187,7 @@ class Chunk:
         d = ctypes.c_void_p()
         ex = ctypes.c_uint64()
         check(lib.sydelta_chunk_walk(self.h, entry, ctypes.byref(ex), ctypes.byref(d)))
-        try:
-            return _device_delta(d), int(ex.value)
-        finally:
-            lib.sydelta_delta_free(d)
+        return _device_delta(d, _DeltaHandle(d)), int(ex.value)
 
     def close(self):
         if self.h:
