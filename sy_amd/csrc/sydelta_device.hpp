@@ -115,6 +115,66 @@ __device__ __forceinline__ uint64_t wave_sum64(uint64_t v) {
     return v;
 }
 
+// Cross-lane sums without the LDS crossbar (ds_bpermute): DPP within a 16-lane row
+// (quad_perm / row_ror) and the gfx950 permlane16/32 swaps across rows.  A rotation
+// by 4 then 8 inside a row sums the 4 lanes of equal lane&3, like xor 4 / xor 8; a
+// permlane swap of x with itself returns the row pair (or wave halves) as two
+// values whose sum is the xor-16 (xor-32) sum on every lane.
+template <int kCtrl>
+__device__ __forceinline__ uint32_t dpp32(uint32_t v) {
+    return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, kCtrl, 0xF, 0xF, false);
+}
+template <int kCtrl>
+__device__ __forceinline__ uint64_t dpp_add64(uint64_t v) {
+    const uint32_t lo = dpp32<kCtrl>((uint32_t)v), hi = dpp32<kCtrl>((uint32_t)(v >> 32));
+    return v + (((uint64_t)hi << 32) | lo);
+}
+__device__ __forceinline__ uint32_t swap16_sum32(uint32_t v) {
+    const auto r = __builtin_amdgcn_permlane16_swap(v, v, false, false);
+    return r[0] + r[1];
+}
+__device__ __forceinline__ uint32_t swap32_sum32(uint32_t v) {
+    const auto r = __builtin_amdgcn_permlane32_swap(v, v, false, false);
+    return r[0] + r[1];
+}
+__device__ __forceinline__ uint64_t swap16_sum64(uint64_t v) {
+    const auto l = __builtin_amdgcn_permlane16_swap((uint32_t)v, (uint32_t)v, false, false);
+    const auto h = __builtin_amdgcn_permlane16_swap((uint32_t)(v >> 32), (uint32_t)(v >> 32), false, false);
+    return ((((uint64_t)h[0]) << 32) | l[0]) + ((((uint64_t)h[1]) << 32) | l[1]);
+}
+__device__ __forceinline__ uint64_t swap32_sum64(uint64_t v) {
+    const auto l = __builtin_amdgcn_permlane32_swap((uint32_t)v, (uint32_t)v, false, false);
+    const auto h = __builtin_amdgcn_permlane32_swap((uint32_t)(v >> 32), (uint32_t)(v >> 32), false, false);
+    return ((((uint64_t)h[0]) << 32) | l[0]) + ((((uint64_t)h[1]) << 32) | l[1]);
+}
+constexpr int kDppQuadXor1 = 0xB1;  // quad_perm [1,0,3,2]
+constexpr int kDppQuadXor2 = 0x4E;  // quad_perm [2,3,0,1]
+constexpr int kDppRowRor4 = 0x124;
+constexpr int kDppRowRor8 = 0x128;
+// sum over the 16 lanes with the same lane & 3 (= xor 4, 8, 16, 32)
+__device__ __forceinline__ uint64_t sum_q16_64(uint64_t v) {
+    v = dpp_add64<kDppRowRor4>(v);
+    v = dpp_add64<kDppRowRor8>(v);
+    v = swap16_sum64(v);
+    return swap32_sum64(v);
+}
+// sum over the 4 lanes of a quad (= xor 1, 2)
+__device__ __forceinline__ uint64_t sum_quad64(uint64_t v) {
+    v = dpp_add64<kDppQuadXor1>(v);
+    return dpp_add64<kDppQuadXor2>(v);
+}
+__device__ __forceinline__ uint32_t wave_sum32_dpp(uint32_t v) {
+    v += dpp32<kDppQuadXor1>(v);
+    v += dpp32<kDppQuadXor2>(v);
+    v += dpp32<kDppRowRor4>(v);
+    v += dpp32<kDppRowRor8>(v);
+    v = swap16_sum32(v);
+    return swap32_sum32(v);
+}
+__device__ __forceinline__ uint64_t wave_sum64_dpp(uint64_t v) {
+    return sum_q16_64(sum_quad64(v));
+}
+
 // Unaligned little-endian loads for the rare scalar paths.  Every aligned word
 // touched holds at least one byte of [p, p+n), so no access leaves the 16-byte
 // granule of a valid byte (see sydelta.h conventions).

@@ -22,31 +22,50 @@
 
 #include <hipcub/hipcub.hpp>
 
+#include <algorithm>
+
 namespace sydelta {
+
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
 
 // ===========================================================================
 // K1: signature
 // ===========================================================================
-// Adler-32 + XXH3-64 of one window [base, base + bs), bs % 64 == 0, bs >= 256,
-// base 16-byte aligned: lane l owns bytes [16l + 1024j, +16) of every 1 KiB piece j,
-// so each wave-instruction loads 1 KiB contiguously.  Every lane returns the result.
-__device__ __forceinline__ void wave_hash_aligned(const uint8_t* __restrict__ base, uint32_t bs, uint32_t& weak_out,
-                                                  uint64_t& strong_out) {
-    const uint32_t lane = threadIdx.x & 63;
-    const uint32_t q = lane & 3, sl = lane >> 2;
-    const uint32_t npieces = (bs + 1023) >> 10;
-    const uint32_t ns = bs >> 6;
-    uint64_t acc_lo = c_tab.init[2 * q], acc_hi = c_tab.init[2 * q + 1];
-    const uint64_t k0n = c_tab.w[sl + 2 * q], k1n = c_tab.w[sl + 2 * q + 1];
-    const uint64_t k0l = c_tab.last[2 * q], k1l = c_tab.last[2 * q + 1];
-    const uint64_t sk0 = c_tab.w[16 + 2 * q], sk1 = c_tab.w[16 + 2 * q + 1];
-    uint32_t asum = 0, vsum = 0;
-    uint64_t bpos = 0;
-    for (uint32_t j = 0; j < npieces; ++j) {
-        const uint32_t off = (j << 10) + (lane << 4);
-        const bool valid = off < bs;
-        uint4 v = make_uint4(0, 0, 0, 0);
-        if (valid) v = *(const uint4*)(base + off);
+// Row-per-block form (the production signature kernel): each 16-lane row of a wave
+// hashes its own block, so a 1 KiB piece is reduced inside the row (two DPP
+// rotations) and the accumulate/scramble fold (XXH3 long loop) runs in the row with
+// no cross-row traffic.  Lane (slot, q) of a row takes stripes slot, slot+4,
+// slot+8, slot+12 of each piece (accumulator pair q): a load instruction reads
+// 256 contiguous bytes per row.  The next piece's loads are issued before the
+// current piece is hashed.  bs % 64 == 0, bs >= 256, blocks 16-byte aligned.
+struct RowPiece {
+    uint4 v[4];
+};
+__device__ __forceinline__ void load_piece(const uint8_t* __restrict__ p, uint32_t slot, uint32_t q, uint32_t lim,
+                                           RowPiece& r) {
+    // bytes [0, lim) of the piece are valid (lim <= 1024); the rest reads as zero
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        const uint32_t off = ((slot + 4 * k) << 6) + (q << 4);
+        r.v[k] = make_uint4(0, 0, 0, 0);
+        if (off < lim) {
+            const u32x4 x = __builtin_nontemporal_load((const u32x4*)(p + off));
+            r.v[k] = make_uint4(x.x, x.y, x.z, x.w);
+        }
+    }
+}
+
+template <bool kLast>
+__device__ __forceinline__ void hash_piece(const RowPiece& r, uint32_t slot, uint32_t q, uint32_t poff, uint32_t bs,
+                                           const uint64_t (&kk0)[4], const uint64_t (&kk1)[4], uint32_t last_k,
+                                           uint32_t last_slot, uint64_t k0l, uint64_t k1l, uint32_t& asum,
+                                           uint32_t& vsum, uint64_t& bpos, uint64_t& c_lo, uint64_t& c_hi) {
+    c_lo = 0;
+    c_hi = 0;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        const uint4 v = r.v[k];
+        const uint32_t off = poff + ((slot + 4 * k) << 6) + (q << 4);
         uint32_t s = udot4(v.x, 0x01010101u, 0);
         s = udot4(v.y, 0x01010101u, s);
         s = udot4(v.z, 0x01010101u, s);
@@ -57,44 +76,93 @@ __device__ __forceinline__ void wave_hash_aligned(const uint8_t* __restrict__ ba
         u = udot4(v.w, 0x0F0E0D0Cu, u);
         asum += s;
         vsum += u;
-        bpos += (uint64_t)(bs - off) * s;  // s == 0 when !valid
-        const uint32_t st = (j << 4) + sl;
-        const bool last = (st == ns - 1);
-        const uint64_t k0 = last ? k0l : k0n, k1 = last ? k1l : k1n;
+        bpos += (uint64_t)(bs - off) * s;  // s == 0 past the end
+        uint64_t k0 = kk0[k], k1 = kk1[k];
+        if (kLast && k == (int)last_k && slot == last_slot) { k0 = k0l; k1 = k1l; }
         const uint64_t w0 = (uint64_t)v.x | ((uint64_t)v.y << 32);
         const uint64_t w1 = (uint64_t)v.z | ((uint64_t)v.w << 32);
-        uint64_t c_lo = mul32x32(w0 ^ k0) + w1;  // acc[2q]   += mul(word 2q) + data(word 2q+1)
-        uint64_t c_hi = mul32x32(w1 ^ k1) + w0;  // acc[2q+1] += mul(word 2q+1) + data(word 2q)
-        if (!valid) { c_lo = 0; c_hi = 0; }
-        c_lo += shfl_xor64(c_lo, 4);  c_hi += shfl_xor64(c_hi, 4);
-        c_lo += shfl_xor64(c_lo, 8);  c_hi += shfl_xor64(c_hi, 8);
-        c_lo += shfl_xor64(c_lo, 16); c_hi += shfl_xor64(c_hi, 16);
-        c_lo += shfl_xor64(c_lo, 32); c_hi += shfl_xor64(c_hi, 32);
+        uint64_t p_lo = mul32x32(w0 ^ k0) + w1;
+        uint64_t p_hi = mul32x32(w1 ^ k1) + w0;
+        if (kLast && off >= bs) { p_lo = 0; p_hi = 0; }
+        c_lo += p_lo;
+        c_hi += p_hi;
+    }
+    c_lo = dpp_add64<kDppRowRor4>(c_lo);
+    c_lo = dpp_add64<kDppRowRor8>(c_lo);
+    c_hi = dpp_add64<kDppRowRor4>(c_hi);
+    c_hi = dpp_add64<kDppRowRor8>(c_hi);
+}
+
+// Hash of the window [base, base + bs) of this lane's row; the result is valid in
+// the row's first lane (lane & 15 == 0).  All four rows of the wave must call it
+// (DPP inside rows only; rows may pass different windows of the same bs).
+__device__ __forceinline__ void row_hash(const uint8_t* __restrict__ base, uint32_t bs, uint32_t& weak_out,
+                                         uint64_t& strong_out) {
+    const uint32_t lane = threadIdx.x & 63;
+    const uint32_t q = lane & 3, slot = (lane >> 2) & 3;
+    const uint32_t npieces = (bs + 1023) >> 10;
+    const uint32_t ls = (bs >> 6) - 1 - ((npieces - 1) << 4);  // last stripe inside the last piece
+    const uint32_t last_k = ls >> 2, last_slot = ls & 3;
+    uint64_t kk0[4], kk1[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        kk0[k] = c_tab.w[slot + 4 * k + 2 * q];
+        kk1[k] = c_tab.w[slot + 4 * k + 2 * q + 1];
+    }
+    const uint64_t k0l = c_tab.last[2 * q], k1l = c_tab.last[2 * q + 1];
+    const uint64_t sk0 = c_tab.w[16 + 2 * q], sk1 = c_tab.w[16 + 2 * q + 1];
+    uint64_t acc_lo = c_tab.init[2 * q], acc_hi = c_tab.init[2 * q + 1];
+    uint32_t asum = 0, vsum = 0;
+    uint64_t bpos = 0;
+    RowPiece cur, nxt;
+    load_piece(base, slot, q, npieces > 1 ? 1024u : bs, cur);
+    for (uint32_t j = 0; j + 1 < npieces; ++j) {  // full pieces, each followed by a scramble
+        const uint32_t nlim = (j + 2 < npieces) ? 1024u : bs - ((j + 1) << 10);
+        load_piece(base + ((j + 1) << 10), slot, q, nlim, nxt);
+        uint64_t c_lo, c_hi;
+        hash_piece<false>(cur, slot, q, j << 10, bs, kk0, kk1, 0, 0, k0l, k1l, asum, vsum, bpos, c_lo, c_hi);
+        acc_lo = scramble1(acc_lo + c_lo, sk0);
+        acc_hi = scramble1(acc_hi + c_hi, sk1);
+        cur = nxt;
+    }
+    {
+        uint64_t c_lo, c_hi;
+        hash_piece<true>(cur, slot, q, (npieces - 1) << 10, bs, kk0, kk1, last_k, last_slot, k0l, k1l, asum, vsum,
+                         bpos, c_lo, c_hi);
         acc_lo += c_lo;
         acc_hi += c_hi;
-        if (j + 1 < npieces) { acc_lo = scramble1(acc_lo, sk0); acc_hi = scramble1(acc_hi, sk1); }
     }
     uint64_t f = fold64(acc_lo ^ c_tab.merge[2 * q], acc_hi ^ c_tab.merge[2 * q + 1]);
-    f += shfl_xor64(f, 1);
-    f += shfl_xor64(f, 2);
-    const uint64_t h = xxh3_aval((uint64_t)bs * P64_1 + f);
-    asum = wave_sum32(asum);
-    vsum = wave_sum32(vsum);
-    bpos = wave_sum64(bpos);
+    f = sum_quad64(f);
+    // row sums of the Adler partials (16 lanes)
+    asum += dpp32<kDppQuadXor1>(asum);
+    asum += dpp32<kDppQuadXor2>(asum);
+    asum += dpp32<kDppRowRor4>(asum);
+    asum += dpp32<kDppRowRor8>(asum);
+    vsum += dpp32<kDppQuadXor1>(vsum);
+    vsum += dpp32<kDppQuadXor2>(vsum);
+    vsum += dpp32<kDppRowRor4>(vsum);
+    vsum += dpp32<kDppRowRor8>(vsum);
+    bpos = sum_quad64(bpos);
+    bpos = dpp_add64<kDppRowRor4>(bpos);
+    bpos = dpp_add64<kDppRowRor8>(bpos);
     const uint32_t A = (1u + asum) % kMod;
     const uint32_t B = (uint32_t)(((uint64_t)bs + bpos - vsum) % kMod);
     weak_out = (B << 16) | A;
-    strong_out = h;
+    strong_out = xxh3_aval((uint64_t)bs * P64_1 + f);
 }
 
+// K1: four blocks per wave, one per row.
 __global__ __launch_bounds__(256) void k_sig_fast(const uint8_t* __restrict__ buf, uint64_t nfull, uint32_t bs,
                                                   uint32_t* __restrict__ weak, uint64_t* __restrict__ strong) {
-    const uint64_t blk = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
-    if (blk >= nfull) return;
+    const uint32_t lane = threadIdx.x & 63;
+    const uint64_t blk = ((((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6) << 2) + (lane >> 4);
+    if ((blk & ~3ull) >= nfull) return;  // wave-uniform
+    const bool live = blk < nfull;
     uint32_t wk;
     uint64_t st;
-    wave_hash_aligned(buf + blk * (uint64_t)bs, bs, wk, st);
-    if ((threadIdx.x & 63) == 0) {
+    row_hash(buf + (live ? blk : (nfull - 1)) * (uint64_t)bs, bs, wk, st);
+    if ((lane & 15) == 0 && live) {
         weak[blk] = wk;
         strong[blk] = st;
     }
@@ -292,11 +360,10 @@ __device__ __forceinline__ uint32_t probe_job(const ProbeJob* __restrict__ jobs,
     return lo;
 }
 
-// Pass 1: weak + strong of every probed window (one wave per window, the
-// signature kernel's access pattern), into pw / pst.
+// Pass 1, general windows: weak + strong, one wave per window, into pw / pst.
 __global__ __launch_bounds__(256) void k_probe(const uint8_t* __restrict__ base, const ProbeJob* __restrict__ jobs,
                                                uint32_t njobs, uint64_t nprobes, uint32_t stride, uint32_t n,
-                                               uint32_t fast, uint32_t* __restrict__ pw, uint64_t* __restrict__ pst) {
+                                               uint32_t* __restrict__ pw, uint64_t* __restrict__ pst) {
     const uint64_t w = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
     if (w >= nprobes) return;
     const ProbeJob J = jobs[probe_job(jobs, njobs, w)];
@@ -304,15 +371,35 @@ __global__ __launch_bounds__(256) void k_probe(const uint8_t* __restrict__ base,
     const uint8_t* p = base + J.src + k * n;
     uint32_t wk;
     uint64_t st;
-    if (fast) {
-        wave_hash_aligned(p, n, wk, st);
-    } else if (n > 240) {
+    if (n > 240) {
         wave_hash_long(p, n, wk, st);
     } else {
         wk = 0; st = 0;
         if ((threadIdx.x & 63) == 0) { wk = adler_scalar(p, n); st = xxh3_short(p, n); }
     }
     if ((threadIdx.x & 63) == 0) {
+        pw[w] = wk;
+        pst[w] = st;
+    }
+}
+
+// Pass 1, aligned windows (n % 64 == 0, n >= 256, 16-byte aligned): four windows
+// per wave, one per row (row_hash, the signature kernel's layout).
+__global__ __launch_bounds__(256) void k_probe_rows(const uint8_t* __restrict__ base,
+                                                    const ProbeJob* __restrict__ jobs, uint32_t njobs,
+                                                    uint64_t nprobes, uint32_t stride, uint32_t n,
+                                                    uint32_t* __restrict__ pw, uint64_t* __restrict__ pst) {
+    const uint32_t lane = threadIdx.x & 63;
+    const uint64_t w = ((((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6) << 2) + (lane >> 4);
+    if ((w & ~3ull) >= nprobes) return;  // wave-uniform
+    const bool live = w < nprobes;
+    const uint64_t wl = live ? w : nprobes - 1;
+    const ProbeJob J = jobs[probe_job(jobs, njobs, wl)];
+    const uint64_t k = J.k0 + (wl - J.pfx) * stride;
+    uint32_t wk;
+    uint64_t st;
+    row_hash(base + J.src + k * n, n, wk, st);
+    if ((lane & 15) == 0 && live) {
         pw[w] = wk;
         pst[w] = st;
     }
@@ -1235,8 +1322,8 @@ hipError_t launch_signature(const uint8_t* d_buf, uint64_t len, uint64_t bs, uin
     uint64_t done = 0;
     if (nfull && aligned && bs % 64 == 0 && bs >= 256 && bs <= (1u << 31)) {
         ProfScope ps(prof, s, "k_sig_fast");
-        hipLaunchKernelGGL(k_sig_fast, dim3(grid_for(nfull * 64, 256)), dim3(256), 0, s, d_buf, nfull, (uint32_t)bs,
-                           d_weak, d_strong);
+        hipLaunchKernelGGL(k_sig_fast, dim3(grid_for((nfull + 3) / 4 * 64, 256)), dim3(256), 0, s, d_buf, nfull,
+                           (uint32_t)bs, d_weak, d_strong);
         done = nfull;
     } else if (nfull && bs > 240) {
         ProfScope ps(prof, s, "k_sig_wave");
@@ -1321,8 +1408,12 @@ hipError_t launch_probe(const uint8_t* d_base, const ProbeJob* d_jobs, uint32_t 
     if (fast && (n % 64 != 0 || n < 256)) return hipErrorInvalidValue;
     {
         ProfScope ps(prof, s, stride > 1 ? "k_probe_sample" : "k_probe");
-        hipLaunchKernelGGL(k_probe, dim3(grid_for(nprobes * 64, 256)), dim3(256), 0, s, d_base, d_jobs, njobs,
-                           nprobes, stride, n, fast ? 1u : 0u, d_pw, d_pst);
+        if (fast)
+            hipLaunchKernelGGL(k_probe_rows, dim3(grid_for((nprobes + 3) / 4 * 64, 256)), dim3(256), 0, s, d_base,
+                               d_jobs, njobs, nprobes, stride, n, d_pw, d_pst);
+        else
+            hipLaunchKernelGGL(k_probe, dim3(grid_for(nprobes * 64, 256)), dim3(256), 0, s, d_base, d_jobs, njobs,
+                               nprobes, stride, n, d_pw, d_pst);
     }
     if (hipError_t e = hipGetLastError()) return e;
     ProfScope ps(prof, s, "k_probe_lookup");
