@@ -892,6 +892,83 @@ __device__ __forceinline__ uint32_t seg_of_tile(const ScanArgs& a, uint32_t t) {
     return lo;
 }
 
+// XXH3-64 of the window at tile offset o (LDS rows, 17-dword stride) for this lane's
+// row, n % 64 == 0 and n >= 256 (row_hash's layout, strong part only: the weak is
+// already known equal).  Valid in every lane of the row.
+__device__ __forceinline__ uint32_t lds_row_dword(const uint32_t* rows, uint32_t d) {
+    return rows[(d >> 4) * kRowDw + (d & 15)];
+}
+__device__ __forceinline__ uint64_t row_strong_lds(const uint32_t* rows, uint32_t o, uint32_t n) {
+    const uint32_t lane = threadIdx.x & 63;
+    const uint32_t q = lane & 3, slot = (lane >> 2) & 3;
+    const uint32_t npieces = (n + 1023) >> 10;
+    const uint32_t ls = (n >> 6) - 1 - ((npieces - 1) << 4);
+    const uint32_t last_k = ls >> 2, last_slot = ls & 3;
+    const uint32_t sh = o & 3;
+    uint64_t acc_lo = c_tab.init[2 * q], acc_hi = c_tab.init[2 * q + 1];
+    for (uint32_t j = 0; j < npieces; ++j) {
+        uint64_t c_lo = 0, c_hi = 0;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            const uint32_t u = (j << 10) + ((slot + 4 * k) << 6) + (q << 4);
+            const uint32_t d0 = (o + u) >> 2;
+            const uint32_t x0 = lds_row_dword(rows, d0), x1 = lds_row_dword(rows, d0 + 1);
+            const uint32_t x2 = lds_row_dword(rows, d0 + 2), x3 = lds_row_dword(rows, d0 + 3);
+            const uint32_t x4 = lds_row_dword(rows, d0 + 4);
+            const uint32_t v0 = __builtin_amdgcn_alignbyte(x1, x0, sh), v1 = __builtin_amdgcn_alignbyte(x2, x1, sh);
+            const uint32_t v2 = __builtin_amdgcn_alignbyte(x3, x2, sh), v3 = __builtin_amdgcn_alignbyte(x4, x3, sh);
+            const bool lastk = (j + 1 == npieces) && k == (int)last_k && slot == last_slot;
+            const uint64_t k0 = lastk ? c_tab.last[2 * q] : c_tab.w[slot + 4 * k + 2 * q];
+            const uint64_t k1 = lastk ? c_tab.last[2 * q + 1] : c_tab.w[slot + 4 * k + 2 * q + 1];
+            const uint64_t w0 = (uint64_t)v0 | ((uint64_t)v1 << 32);
+            const uint64_t w1 = (uint64_t)v2 | ((uint64_t)v3 << 32);
+            uint64_t p_lo = mul32x32(w0 ^ k0) + w1;
+            uint64_t p_hi = mul32x32(w1 ^ k1) + w0;
+            if (u >= n) { p_lo = 0; p_hi = 0; }
+            c_lo += p_lo;
+            c_hi += p_hi;
+        }
+        c_lo = dpp_add64<kDppRowRor4>(c_lo);
+        c_lo = dpp_add64<kDppRowRor8>(c_lo);
+        c_hi = dpp_add64<kDppRowRor4>(c_hi);
+        c_hi = dpp_add64<kDppRowRor8>(c_hi);
+        acc_lo += c_lo;
+        acc_hi += c_hi;
+        if (j + 1 < npieces) {
+            acc_lo = scramble1(acc_lo, c_tab.w[16 + 2 * q]);
+            acc_hi = scramble1(acc_hi, c_tab.w[16 + 2 * q + 1]);
+        }
+    }
+    const uint64_t f = sum_quad64(fold64(acc_lo ^ c_tab.merge[2 * q], acc_hi ^ c_tab.merge[2 * q + 1]));
+    return xxh3_aval((uint64_t)n * P64_1 + f);
+}
+
+// Tile-flush verification with the windows in LDS, four hits per wave (one per
+// row); candidates in index order (first_strong_match's rule).
+__device__ __forceinline__ void verify_rows_lds(const ScanArgs& a, uint4* wq, uint32_t nwq, const uint32_t* rows,
+                                                uint64_t tile_start, const SegCtx* cur) {
+    const uint32_t lane = threadIdx.x & 63, row = lane >> 4, rl = lane & 15;
+    for (uint32_t t = 0; t < nwq; t += 4) {
+        const uint32_t h = t + row;
+        const bool live = h < nwq;
+        const uint4 e = wq[live ? h : t];
+        const uint32_t o = (uint32_t)(cur->pos_begin + e.y - tile_start);
+        const uint64_t st = row_strong_lds(rows, o, a.n);
+        if (!live) continue;
+        const uint32_t s0 = a.start[e.z], cn = a.cnt[e.z];
+        uint32_t best = 0xFFFFFFFFu;
+        for (uint32_t b = 0; b < cn; b += 16) {  // in index order, 16 candidates per step
+            const uint32_t j = b + rl;
+            const uint64_t m = (__ballot(j < cn && a.cstrong[s0 + j] == st) >> (row << 4)) & 0xFFFFull;
+            if (m) {
+                best = a.order[s0 + b + (uint32_t)__builtin_ctzll(m)];
+                break;
+            }
+        }
+        if (rl == 0) wq[h].w = best;
+    }
+}
+
 // Verify the queued weak hits: XXH3 of each window, first candidate in index
 // order with equal strong (generator.rs:127-153); one output reservation per wave.
 // rows != nullptr (tile-flush mode): every queued hit lies in the current tile,
@@ -899,11 +976,16 @@ __device__ __forceinline__ uint32_t seg_of_tile(const ScanArgs& a, uint32_t t) {
 // the segment from registers.  Otherwise windows are hashed from global memory.
 // The candidate group of up to 64 hits is fetched with one round trip of
 // start/cnt and one of (order, cstrong), lane i serving hit i.
+template <bool kRowVerify>
 __device__ __forceinline__ void verify3(const ScanArgs& a, uint4* wq, uint32_t nwq, const uint32_t* rows,
                                         uint64_t tile_start, const SegCtx* cur) {
     const uint32_t lane = threadIdx.x & 63;
     for (uint32_t base = 0; base < nwq; base += 64) {
         const uint32_t cnt_here = min(64u, nwq - base);
+        if (kRowVerify && rows && a.n % 64 == 0 && a.n >= 256) {
+            verify_rows_lds(a, wq + base, cnt_here, rows, tile_start, cur);
+            continue;
+        }
         // lane i: candidate group of hit base+i, first candidate
         uint32_t s0 = 0, cn = 0, b0 = 0xFFFFFFFFu;
         uint64_t st0 = 0;
@@ -969,6 +1051,7 @@ __device__ __forceinline__ void verify3(const ScanArgs& a, uint4* wq, uint32_t n
 // Exact lookups of the queued filter passes, 64 per round (positions at or past
 // the segment end are dropped here); weak hits go to wq and are verified when it
 // cannot take another round, and at the end.
+template <bool kRowVerify>
 __device__ __forceinline__ void drain3(const ScanArgs& a, const uint2* fq, uint32_t nfq, uint4* wq, uint32_t t_begin,
                                        unsigned long long& weak_hits, const uint32_t* rows = nullptr,
                                        uint64_t tile_start = 0, const SegCtx* cur = nullptr) {
@@ -1011,19 +1094,19 @@ __device__ __forceinline__ void drain3(const ScanArgs& a, const uint2* fq, uint3
         weak_hits += cnt;
         if (nwq + cnt > (uint32_t)kWQ2) {
             lds_fence();
-            verify3(a, wq, nwq, rows, tile_start, cur);
+            verify3<kRowVerify>(a, wq, nwq, rows, tile_start, cur);
             nwq = 0;
         }
         if (hit) wq[nwq + __popcll(m & ((1ull << lane) - 1))] = make_uint4(si, rp, fslot + (uint32_t)slot, 0);
         nwq += cnt;
     }
     lds_fence();
-    verify3(a, wq, nwq, rows, tile_start, cur);
+    verify3<kRowVerify>(a, wq, nwq, rows, tile_start, cur);
     lds_fence();
 }
 
-template <bool kLdsFilter>
-__global__ __launch_bounds__(kT2, kLdsFilter ? 3 : 4) void k_scan_lds(ScanArgs a, uint32_t per, uint32_t lds_fwords) {
+template <bool kLdsFilter, int kWgPerCu = kLdsFilter ? 3 : 4, bool kRowVerify = false>
+__global__ __launch_bounds__(kT2, kWgPerCu) void k_scan_lds(ScanArgs a, uint32_t per, uint32_t lds_fwords) {
     // Large indexes (filter in HBM/L2) come with dense Adler false hits (C3: ~1 per
     // 1000 positions): their verification runs at the end of every tile, hashing the
     // windows from LDS.  Small indexes have rare hits: queue across tiles, verify
@@ -1183,7 +1266,7 @@ __global__ __launch_bounds__(kT2, kLdsFilter ? 3 : 4) void k_scan_lds(ScanArgs a
         for (uint32_t g = 0; g < (uint32_t)kR2; g += kB2) {
             if (nfq > (uint32_t)(kGFQ - 64 * kB2)) {
                 passes += nfq;
-                drain3(a, fq, nfq, wq, t_begin, weak_hits, kTileFlush ? rows : nullptr, tile_start,
+                drain3<kRowVerify>(a, fq, nfq, wq, t_begin, weak_hits, kTileFlush ? rows : nullptr, tile_start,
                        kTileFlush ? &sc : nullptr);
                 nfq = 0;
             }
@@ -1233,14 +1316,14 @@ __global__ __launch_bounds__(kT2, kLdsFilter ? 3 : 4) void k_scan_lds(ScanArgs a
         PHASE_MARK(2)
         if (kTileFlush && nfq) {  // dense weak hits: verify while the tile is in LDS
             passes += nfq;
-            drain3(a, fq, nfq, wq, t_begin, weak_hits, rows, tile_start, &sc);
+            drain3<kRowVerify>(a, fq, nfq, wq, t_begin, weak_hits, rows, tile_start, &sc);
             nfq = 0;
         }
         __syncthreads();  // rows / prefix arrays are rewritten by the next tile
         PHASE_MARK(3)
     }
     passes += nfq;
-    drain3(a, fq, nfq, wq, t_begin, weak_hits);
+    drain3<kRowVerify>(a, fq, nfq, wq, t_begin, weak_hits);
 #undef PHASE_MARK
     if (lane == 0 && passes) atomicAdd(&a.counters[2], passes);
     if (lane == 0 && weak_hits) atomicAdd(&a.counters[1], weak_hits);
@@ -1471,7 +1554,7 @@ hipError_t launch_scan(const uint8_t* d_buf, const ScanSeg* d_segs, uint32_t nse
         const int cap = 160 * 1024 / 2 - 512;
         attr_err = hipFuncSetAttribute((const void*)k_scan_lds<true>, hipFuncAttributeMaxDynamicSharedMemorySize, cap);
         if (attr_err == hipSuccess)
-            attr_err = hipFuncSetAttribute((const void*)k_scan_lds<false>,
+            attr_err = hipFuncSetAttribute((const void*)k_scan_lds<false, 3, true>,
                                            hipFuncAttributeMaxDynamicSharedMemorySize, cap);
         int dev = 0, cus = 0;
         if (hipGetDevice(&dev) == hipSuccess &&
@@ -1483,7 +1566,9 @@ hipError_t launch_scan(const uint8_t* d_buf, const ScanSeg* d_segs, uint32_t nse
     // persistent: 2-4 workgroups per CU, as many as the LDS layout allows (launch
     // bounds hold the LDS-filter kernel to 3 waves per SIMD, the other to 4), each on a
     // contiguous range of tiles
-    const uint32_t wg_per_cu = (!lds_filter && L.total <= 160u * 1024 / 4 - 512) ? 4u
+    // global-filter mode: 3 workgroups per CU (the row-parallel LDS verification
+    // needs ~160 VGPRs; 4 per CU spills); LDS-filter mode: as many as the LDS fits
+    const uint32_t wg_per_cu = !lds_filter ? 3u
                                : L.total <= 160u * 1024 / 3 - 512           ? 3u
                                                                             : 2u;
     const uint32_t grid = (uint32_t)std::min<uint64_t>(ntiles, (uint64_t)num_cus * wg_per_cu);
@@ -1495,7 +1580,7 @@ hipError_t launch_scan(const uint8_t* d_buf, const ScanSeg* d_segs, uint32_t nse
     if (lds_filter)
         hipLaunchKernelGGL(k_scan_lds<true>, dim3(grid), dim3(kT2), L.total, s, a, per, lds_fwords);
     else
-        hipLaunchKernelGGL(k_scan_lds<false>, dim3(grid), dim3(kT2), L.total, s, a, per, 0u);
+        hipLaunchKernelGGL((k_scan_lds<false, 3, true>), dim3(grid), dim3(kT2), L.total, s, a, per, 0u);
     return hipGetLastError();
 }
 
