@@ -315,7 +315,7 @@ static int index_create_impl(int device, const uint32_t* weak, const uint64_t* s
         F.filt_off = fw;
         F.slot_off = sl;
         F.blk_base = fblk[f];
-        F.fwshift = 32 - fwbits;
+        F.fwshift = 33 - fwbits;  // 2^(fwbits-1) 64-bit words
         F.bmask = (1u << bbits) - 1;
         fw += 1ull << fwbits;
         sl += 4ull << bbits;
@@ -729,7 +729,7 @@ int Classifier::scan(const std::vector<std::array<uint64_t, 3>>& ranges) {
     if (wide && ix->nfiles != 1) return fail(SYDELTA_E_INVAL, "batched match needs block_size <= %u", scan_max_window());
     unsigned long long* d_counts = nullptr;
     DevBuf cnt_buf;
-    HIP_TRY(hipMallocAsync((void**)&d_counts, 64, s));
+    HIP_TRY(hipMallocAsync((void**)&d_counts, 128, s));
     cnt_buf.p = d_counts;
     cnt_buf.s = s;
     DevBuf seg_buf;
@@ -746,7 +746,7 @@ int Classifier::scan(const std::vector<std::array<uint64_t, 3>>& ranges) {
     // verified hits: at most one per position; start from ~4 per block of positions
     uint64_t want = std::min<uint64_t>(tot_pos, tot_pos / n * 4 + (1 << 16));
     uint64_t cap = 0;
-    unsigned long long counts[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    unsigned long long counts[16] = {0};
     DevBuf hit_buf;
     for (int attempt = 0; attempt < 2; ++attempt) {
         if (want > cap) {
@@ -758,7 +758,7 @@ int Classifier::scan(const std::vector<std::array<uint64_t, 3>>& ranges) {
         }
         uint64_t* d_key = (uint64_t*)hit_buf.p;
         uint32_t* d_val = (uint32_t*)(d_key + 2 * cap);
-        HIP_TRY(hipMemsetAsync(d_counts, 0, 64, s));
+        HIP_TRY(hipMemsetAsync(d_counts, 0, 128, s));
         if (!wide) {
             HIP_TRY(launch_scan(base, (const ScanSeg*)seg_buf.p, (uint32_t)segs.size(), (uint32_t)ntiles,
                                 (uint32_t)n, ix->ix, ix->d_strong, d_key, d_val, cap, d_counts, (uint2*)q_buf.p, qcap,
@@ -769,11 +769,12 @@ int Classifier::scan(const std::vector<std::array<uint64_t, 3>>& ranges) {
                                          (uint32_t)g, (uint32_t)n, ix->ix, ix->d_strong, d_key, d_val, cap, d_counts,
                                          s, prof));
         }
-        HIP_TRY(hipMemcpyAsync(counts, d_counts, 64, hipMemcpyDeviceToHost, s));
+        HIP_TRY(hipMemcpyAsync(counts, d_counts, 128, hipMemcpyDeviceToHost, s));
         HIP_TRY(hipStreamSynchronize(s));
         if (getenv("SYDELTA_PHASE_TIMING"))
-            fprintf(stderr, "sydelta phase cycles (wave 0, summed over workgroups): stage %llu prefix %llu roll %llu flush %llu\n",
-                    counts[4], counts[5], counts[6], counts[7]);
+            fprintf(stderr, "sydelta phase cycles (wave 0, summed over workgroups): stage %llu prefix %llu roll %llu flush %llu"
+                            " (lookup %llu verify %llu) passes %llu weak %llu\n",
+                    counts[4], counts[5], counts[6], counts[7], counts[8], counts[9], counts[2], counts[1]);
         if (counts[0] <= cap) break;
         want = counts[0];  // dense hits: grow once and rescan
     }

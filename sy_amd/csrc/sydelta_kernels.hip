@@ -237,19 +237,24 @@ __global__ __launch_bounds__(256) void k_sig_batch(const uint8_t* __restrict__ b
 // ===========================================================================
 // K3: index (probe structure) over basis weak values
 // ===========================================================================
-// Blocked Bloom filter: 32-bit words, 3 bits per key, all in the key's word.
-// One 24-bit multiply and one multiply-add of the two 16-bit Adler halves
-// (A = weak & 0xFFFF, B = weak >> 16) give h; the word is the top bits of h, the
-// bit positions are h[0:5), h[5:10), h[10:15) (v_lshlrev_b32 masks its shift
-// count to 5 bits).
-// Sizing (sydelta_index_create): up to 32 Ki keys the filter is <= 64 KiB and
+// Blocked Bloom filter: 64-bit words, 4 bits per key, all in the key's word.
+// h = fmix32(weak) picks the word (top bits); a second multiply of h gives the
+// four 6-bit bit positions.  At 16 bits per key that is ~0.5 % false passes
+// (a 32-bit word with 3 bits: ~1 %, measured 1.4 % with a 24-bit-multiply hash).
+// Sizing (sydelta_index_create): up to 16 Ki keys the filter is <= 32 KiB and
 // the LDS-staged scan copies it into LDS; above that it stays in HBM/L2 at 16
-// bits per key (~0.5 % false passes on Adler values of random blocks).
-__device__ __forceinline__ uint32_t filt_hash(uint32_t am, uint32_t bm) {
-    return __umul24(am, 0x9E3779u) + __umul24(bm, 0x2F0B35u);
+// bits per key.  FileIx::filt_off counts 32-bit units; fwshift = 32 - log2(words).
+__device__ __forceinline__ uint32_t filt_hash(uint32_t w) {
+    uint32_t h = w * 0x9E3779B1u;
+    h ^= h >> 16;
+    h *= 0x85EBCA6Bu;
+    h ^= h >> 13;
+    return h;
 }
-__device__ __forceinline__ uint32_t filt_mask(uint32_t h) {
-    return (1u << (h & 31)) | (1u << ((h >> 5) & 31)) | (1u << ((h >> 10) & 31));
+__device__ __forceinline__ uint64_t filt_mask(uint32_t h) {
+    const uint32_t g = (h ^ (h >> 15)) * 0x2C1B3C6Du;
+    return (1ull << ((g >> 8) & 63)) | (1ull << ((g >> 14) & 63)) | (1ull << ((g >> 20) & 63)) |
+           (1ull << (g >> 26));
 }
 __device__ __forceinline__ uint32_t bucket_hash(uint32_t w) {
     uint32_t h = w ^ (w >> 15);
@@ -275,8 +280,8 @@ __global__ void k_idx_insert(const uint32_t* __restrict__ weak, uint64_t n, cons
     if (i >= n) return;
     const FileIx F = files[file_of_block(fblk, nf, i)];
     const uint32_t w = weak[i];
-    const uint32_t h = filt_hash(w & 0xFFFF, w >> 16);
-    atomicOr(&filt[F.filt_off + (h >> F.fwshift)], filt_mask(h));
+    const uint32_t h = filt_hash(w);
+    atomicOr((unsigned long long*)(filt + F.filt_off) + (h >> F.fwshift), (unsigned long long)filt_mask(h));
     uint32_t b = bucket_hash(w) & F.bmask;
     for (;;) {
         for (uint32_t j = 0; j < 4; ++j) {
@@ -422,8 +427,8 @@ __global__ __launch_bounds__(256) void k_probe_lookup(const ProbeJob* __restrict
     const FileIx F = files[jobs[probe_job(jobs, njobs, w)].file];
     const uint32_t wk = pw[w];
     uint32_t best = kNoBlock;
-    const uint32_t h = filt_hash(wk & 0xFFFF, wk >> 16);
-    if ((filt_mask(h) & ~filt[F.filt_off + (h >> F.fwshift)]) == 0) {
+    const uint32_t h = filt_hash(wk);
+    if ((filt_mask(h) & ~((const uint64_t*)(filt + F.filt_off))[h >> F.fwshift]) == 0) {
         const int64_t slot = table_find(keys + F.slot_off, F.bmask, wk);
         if (slot >= 0) {
             const uint64_t gs = F.slot_off + (uint64_t)slot;
@@ -783,15 +788,15 @@ __global__ __launch_bounds__(kScanThreads) void k_scan(ScanArgs a) {
 #pragma unroll
         for (int hb = 0; hb < 64; hb += kBatch) {
             uint32_t wv[kBatch];
-            uint32_t fw[kBatch];
+            uint64_t fw[kBatch];
             uint32_t fh[kBatch];
 #pragma unroll
             for (int t = 0; t < kBatch; ++t) {
                 const int i = hb + t;
                 const uint32_t am = a_ex % kMod;
                 wv[t] = (bm << 16) | am;
-                fh[t] = filt_hash(am, bm);
-                fw[t] = a.filt[fh[t] >> a.fwshift];
+                fh[t] = filt_hash(wv[t]);
+                fw[t] = ((const uint64_t*)a.filt)[fh[t] >> a.fwshift];
                 const uint32_t out = (xo[i >> 2] >> (8 * (i & 3))) & 0xFF;
                 const uint32_t in = (xi[i >> 2] >> (8 * (i & 3))) & 0xFF;
                 a_ex = a_ex + in - out;
@@ -800,7 +805,7 @@ __global__ __launch_bounds__(kScanThreads) void k_scan(ScanArgs a) {
 #pragma unroll
             for (int t = 0; t < kBatch; ++t) {
                 const uint32_t rel = g + hb + t;
-                const uint32_t fmask = filt_mask(fh[t]);
+                const uint64_t fmask = filt_mask(fh[t]);
                 const bool pass = ((fw[t] & fmask) == fmask) && rel < npos;
                 const uint64_t mk = __ballot(pass);
                 if (mk) {
@@ -850,7 +855,7 @@ __global__ __launch_bounds__(kScanThreads) void k_scan(ScanArgs a) {
 constexpr int kT2 = 256;                 // threads per workgroup (4 waves)
 constexpr int kR2 = 64;                  // positions per thread = one 64-byte row
 constexpr int kTile2 = kT2 * kR2;        // 16384 positions per tile
-constexpr int kB2 = 16;                  // positions per batch (filter reads in flight)
+constexpr int kB2 = 8;                   // positions per batch (filter reads in flight per lane)
 constexpr int kGFQ = 2048;               // filter-pass queue entries per wave (global memory)
 constexpr int kWQ2 = 128;                // weak-hit queue entries per wave (LDS)
 constexpr uint32_t kMaxN2 = 8192;        // largest window the LDS layout holds
@@ -869,7 +874,7 @@ __host__ __device__ __forceinline__ Lds2 lds2_layout(uint32_t n, uint32_t filt_w
     L.pv = o; o += (L.nch + 1) * 4;
     o = (o + 15) & ~15u; L.pj = o; o += (L.nch + 1) * 8;
     L.ntab = o; o += 256 * 4;
-    L.filt = o; o += filt_words * 4;
+    o = (o + 15) & ~15u; L.filt = o; o += filt_words * 4;
     o = (o + 15) & ~15u; L.q = o; o += (kT2 / 64) * kWQ2 * 16;
     L.total = o;
     return L;
@@ -894,11 +899,26 @@ __device__ __forceinline__ uint32_t seg_of_tile(const ScanArgs& a, uint32_t t) {
 
 // XXH3-64 of the window at tile offset o (LDS rows, 17-dword stride) for this lane's
 // row, n % 64 == 0 and n >= 256 (row_hash's layout, strong part only: the weak is
-// already known equal).  Valid in every lane of the row.
-__device__ __forceinline__ uint32_t lds_row_dword(const uint32_t* rows, uint32_t d) {
-    return rows[(d >> 4) * kRowDw + (d & 15)];
+// already known equal).  Valid in every lane of the row.  Keys per lane in K.
+struct RowKeys {
+    uint64_t k0[4], k1[4];  // stripe keys of this lane's stripes slot + 4k, words 2q / 2q+1
+    uint64_t l0, l1;        // last-stripe keys
+    uint64_t s0, s1;        // scramble keys
+};
+__device__ __forceinline__ void row_keys(RowKeys& K) {
+    const uint32_t lane = threadIdx.x & 63;
+    const uint32_t q = lane & 3, slot = (lane >> 2) & 3;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        K.k0[k] = c_tab.w[slot + 4 * k + 2 * q];
+        K.k1[k] = c_tab.w[slot + 4 * k + 2 * q + 1];
+    }
+    K.l0 = c_tab.last[2 * q];
+    K.l1 = c_tab.last[2 * q + 1];
+    K.s0 = c_tab.w[16 + 2 * q];
+    K.s1 = c_tab.w[16 + 2 * q + 1];
 }
-__device__ __forceinline__ uint64_t row_strong_lds(const uint32_t* rows, uint32_t o, uint32_t n) {
+__device__ __forceinline__ uint64_t row_strong_lds(const uint32_t* rows, uint32_t o, uint32_t n, const RowKeys& K) {
     const uint32_t lane = threadIdx.x & 63;
     const uint32_t q = lane & 3, slot = (lane >> 2) & 3;
     const uint32_t npieces = (n + 1023) >> 10;
@@ -911,15 +931,20 @@ __device__ __forceinline__ uint64_t row_strong_lds(const uint32_t* rows, uint32_
 #pragma unroll
         for (int k = 0; k < 4; ++k) {
             const uint32_t u = (j << 10) + ((slot + 4 * k) << 6) + (q << 4);
-            const uint32_t d0 = (o + u) >> 2;
-            const uint32_t x0 = lds_row_dword(rows, d0), x1 = lds_row_dword(rows, d0 + 1);
-            const uint32_t x2 = lds_row_dword(rows, d0 + 2), x3 = lds_row_dword(rows, d0 + 3);
-            const uint32_t x4 = lds_row_dword(rows, d0 + 4);
-            const uint32_t v0 = __builtin_amdgcn_alignbyte(x1, x0, sh), v1 = __builtin_amdgcn_alignbyte(x2, x1, sh);
-            const uint32_t v2 = __builtin_amdgcn_alignbyte(x3, x2, sh), v3 = __builtin_amdgcn_alignbyte(x4, x3, sh);
+            // dword d of the tile sits at row d>>4, column d&15 (17-dword rows): the 5
+            // dwords from d0 are at base + i, plus one past a row end
+            const uint32_t d0 = (o + u) >> 2, c0 = d0 & 15;
+            const uint32_t* p = rows + (d0 >> 4) * kRowDw + c0;
+            uint32_t x[5];
+#pragma unroll
+            for (int i = 0; i < 5; ++i) x[i] = p[i + ((c0 + i) >> 4)];
+            const uint32_t v0 = __builtin_amdgcn_alignbyte(x[1], x[0], sh);
+            const uint32_t v1 = __builtin_amdgcn_alignbyte(x[2], x[1], sh);
+            const uint32_t v2 = __builtin_amdgcn_alignbyte(x[3], x[2], sh);
+            const uint32_t v3 = __builtin_amdgcn_alignbyte(x[4], x[3], sh);
             const bool lastk = (j + 1 == npieces) && k == (int)last_k && slot == last_slot;
-            const uint64_t k0 = lastk ? c_tab.last[2 * q] : c_tab.w[slot + 4 * k + 2 * q];
-            const uint64_t k1 = lastk ? c_tab.last[2 * q + 1] : c_tab.w[slot + 4 * k + 2 * q + 1];
+            const uint64_t k0 = lastk ? K.l0 : K.k0[k];
+            const uint64_t k1 = lastk ? K.l1 : K.k1[k];
             const uint64_t w0 = (uint64_t)v0 | ((uint64_t)v1 << 32);
             const uint64_t w1 = (uint64_t)v2 | ((uint64_t)v3 << 32);
             uint64_t p_lo = mul32x32(w0 ^ k0) + w1;
@@ -935,8 +960,8 @@ __device__ __forceinline__ uint64_t row_strong_lds(const uint32_t* rows, uint32_
         acc_lo += c_lo;
         acc_hi += c_hi;
         if (j + 1 < npieces) {
-            acc_lo = scramble1(acc_lo, c_tab.w[16 + 2 * q]);
-            acc_hi = scramble1(acc_hi, c_tab.w[16 + 2 * q + 1]);
+            acc_lo = scramble1(acc_lo, K.s0);
+            acc_hi = scramble1(acc_hi, K.s1);
         }
     }
     const uint64_t f = sum_quad64(fold64(acc_lo ^ c_tab.merge[2 * q], acc_hi ^ c_tab.merge[2 * q + 1]));
@@ -948,14 +973,16 @@ __device__ __forceinline__ uint64_t row_strong_lds(const uint32_t* rows, uint32_
 __device__ __forceinline__ void verify_rows_lds(const ScanArgs& a, uint4* wq, uint32_t nwq, const uint32_t* rows,
                                                 uint64_t tile_start, const SegCtx* cur) {
     const uint32_t lane = threadIdx.x & 63, row = lane >> 4, rl = lane & 15;
+    RowKeys K;
+    row_keys(K);
     for (uint32_t t = 0; t < nwq; t += 4) {
         const uint32_t h = t + row;
         const bool live = h < nwq;
         const uint4 e = wq[live ? h : t];
+        const uint32_t s0 = a.start[e.z], cn = a.cnt[e.z];  // in flight while hashing
         const uint32_t o = (uint32_t)(cur->pos_begin + e.y - tile_start);
-        const uint64_t st = row_strong_lds(rows, o, a.n);
+        const uint64_t st = row_strong_lds(rows, o, a.n, K);
         if (!live) continue;
-        const uint32_t s0 = a.start[e.z], cn = a.cnt[e.z];
         uint32_t best = 0xFFFFFFFFu;
         for (uint32_t b = 0; b < cn; b += 16) {  // in index order, 16 candidates per step
             const uint32_t j = b + rl;
@@ -1058,6 +1085,8 @@ __device__ __forceinline__ void drain3(const ScanArgs& a, const uint2* fq, uint3
     const uint32_t lane = threadIdx.x & 63;
     __builtin_amdgcn_s_waitcnt(0);  // this wave's queue stores have reached L2
     __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
+    const bool tw = a.timing && threadIdx.x == 0;
+    unsigned long long t_lk = 0, t_vf = 0, t0 = tw ? __builtin_amdgcn_s_memtime() : 0;
     uint32_t nwq = 0;
     for (uint32_t base = 0; base < nfq; base += 64) {
         const uint32_t i = base + lane;
@@ -1101,8 +1130,14 @@ __device__ __forceinline__ void drain3(const ScanArgs& a, const uint2* fq, uint3
         nwq += cnt;
     }
     lds_fence();
+    if (tw) { const unsigned long long t1 = __builtin_amdgcn_s_memtime(); t_lk += t1 - t0; t0 = t1; }
     verify3<kRowVerify>(a, wq, nwq, rows, tile_start, cur);
     lds_fence();
+    if (tw) {
+        t_vf += __builtin_amdgcn_s_memtime() - t0;
+        atomicAdd(&a.counters[8], t_lk);
+        atomicAdd(&a.counters[9], t_vf);
+    }
 }
 
 template <bool kLdsFilter, int kWgPerCu = kLdsFilter ? 3 : 4, bool kRowVerify = false>
@@ -1120,7 +1155,7 @@ __global__ __launch_bounds__(kT2, kWgPerCu) void k_scan_lds(ScanArgs a, uint32_t
     uint32_t* PV = (uint32_t*)(smem + L.pv);
     uint64_t* PJ = (uint64_t*)(smem + L.pj);
     uint32_t* ntab = (uint32_t*)(smem + L.ntab);
-    uint32_t* lfilt = (uint32_t*)(smem + L.filt);
+    uint64_t* lfilt = (uint64_t*)(smem + L.filt);
     const uint32_t tid = threadIdx.x;
     const uint32_t lane = tid & 63, wid = tid >> 6;
     uint4* wq = (uint4*)(smem + L.q) + (size_t)wid * kWQ2;
@@ -1140,7 +1175,7 @@ __global__ __launch_bounds__(kT2, kWgPerCu) void k_scan_lds(ScanArgs a, uint32_t
     uint32_t nfq = 0;
     uint32_t cur_file = 0xFFFFFFFFu;
     uint32_t fwshift = 0;
-    const uint32_t* gfilt = a.filt;
+    const uint64_t* gfilt = (const uint64_t*)a.filt;
     SegCtx sc;
 
     unsigned long long tm[4] = {0, 0, 0, 0};
@@ -1173,14 +1208,14 @@ __global__ __launch_bounds__(kT2, kWgPerCu) void k_scan_lds(ScanArgs a, uint32_t
             sc.bmask = F.bmask;
             sc.seg_id = si;
             fwshift = F.fwshift;
-            gfilt = a.filt + F.filt_off;
+            gfilt = (const uint64_t*)(a.filt + F.filt_off);
             if (kLdsFilter && S.file != cur_file) {
                 // the previous tile ended with a barrier; phase 1's barrier publishes the copy
                 const uint4* src4 = (const uint4*)gfilt;
                 uint4* dst4 = (uint4*)lfilt;
-                const uint32_t fwords = 1u << (32 - fwshift);
+                const uint32_t fwords64 = 1u << (32 - fwshift);
 #pragma unroll 4
-                for (uint32_t i = tid; i < fwords / 4; i += kT2) dst4[i] = src4[i];
+                for (uint32_t i = tid; i < fwords64 / 2; i += kT2) dst4[i] = src4[i];
             }
             cur_file = S.file;
         }
@@ -1287,15 +1322,16 @@ __global__ __launch_bounds__(kT2, kWgPerCu) void k_scan_lds(ScanArgs a, uint32_t
             uint32_t ct[kB2];
 #pragma unroll
             for (int t = 0; t < kB2; ++t) ct[t] = ntab[(xo[t >> 2] >> (8 * (t & 3))) & 0xFF];
-            uint32_t wv[kB2], fm[kB2], fw[kB2];
+            uint32_t wv[kB2], fh[kB2];
+            uint64_t fw[kB2];
 #pragma unroll
             for (int t = 0; t < kB2; ++t) {
                 const uint32_t out = (xo[t >> 2] >> (8 * (t & 3))) & 0xFF;
                 const uint32_t in = (xi[t >> 2] >> (8 * (t & 3))) & 0xFF;
                 wv[t] = (bm << 16) | am;
-                const uint32_t h = filt_hash(am, bm);
+                const uint32_t h = filt_hash(wv[t]);
+                fh[t] = h;
                 fw[t] = kLdsFilter ? lfilt[h >> fwshift] : gfilt[h >> fwshift];
-                fm[t] = filt_mask(h);
                 uint32_t u = am + in - out;  // (-255, M+255), wrapped when negative
                 u = min(u, u + kMod);
                 am = min(u, u - kMod);
@@ -1305,7 +1341,7 @@ __global__ __launch_bounds__(kT2, kWgPerCu) void k_scan_lds(ScanArgs a, uint32_t
             }
 #pragma unroll
             for (int t = 0; t < kB2; ++t) {
-                const bool pass = (fm[t] & ~fw[t]) == 0;
+                const bool pass = (filt_mask(fh[t]) & ~fw[t]) == 0;
                 const uint64_t mk = __ballot(pass);
                 if (mk) {
                     if (pass) fq[nfq + __popcll(mk & ((1ull << lane) - 1))] = make_uint2(qtile | (rel0 + g + t), wv[t]);
