@@ -8,14 +8,16 @@ OUT=$R/gpurun_out/$TAG
 mkdir -p "$OUT"
 export TMPDIR=/tmp
 cd "$R"
-step() { local t=$1; shift; echo "== $* (limit ${t}s)"; timeout -k 10 "$t" "$@"; local rc=$?; echo "== rc=$rc"; return $rc; }
+step() { local t=$1; shift; echo "== $* (limit ${t}s)" >&2; timeout -k 10 "$t" "$@"; local rc=$?; echo "== rc=$rc" >&2; return $rc; }
 [ -n "${SKIP_TESTS:-}" ] || step 900 python -m pytest tests -m gpu -x -q -p no:cacheprovider > "$OUT/pytest.log" 2>&1 || { tail -30 "$OUT/pytest.log"; exit 1; }
 tail -3 "$OUT/pytest.log" 2>/dev/null
 step 600 python bench.py "$@" > "$OUT/bench.json" 2> "$OUT/bench.err" || { cat "$OUT/bench.err" | tail -20; exit 1; }
 cat "$OUT/bench.json"
 cd /tmp
-step 600 rocprofv3 --kernel-trace --stats -d "$OUT/trace" -o run --output-format csv -- python3 "$R/bench.py" --no-cpu-baseline "$@" > "$OUT/prof.log" 2>&1 || { tail -20 "$OUT/prof.log"; exit 1; }
-step 600 rocprofv3 --pmc FETCH_SIZE --kernel-trace -d "$OUT/pmc_fetch" -o run --output-format csv -- python3 "$R/bench.py" --no-cpu-baseline "$@" > "$OUT/pmc1.log" 2>&1 || { tail -20 "$OUT/pmc1.log"; exit 1; }
-step 600 rocprofv3 --pmc WRITE_SIZE --kernel-trace -d "$OUT/pmc_write" -o run --output-format csv -- python3 "$R/bench.py" --no-cpu-baseline "$@" > "$OUT/pmc2.log" 2>&1 || { tail -20 "$OUT/pmc2.log"; exit 1; }
+# profiled runs: the same workload without the CPU baseline and host-inclusive legs,
+# so every launch of a kernel has the bench's size and the averages agree
+step 600 rocprofv3 --kernel-trace --stats -d "$OUT/trace" -o run --output-format csv -- python3 "$R/bench.py" --no-cpu-baseline --no-host-inclusive "$@" > "$OUT/prof.log" 2>&1 || { tail -20 "$OUT/prof.log"; exit 1; }
+step 300 rocprofv3 --pmc FETCH_SIZE --kernel-trace -d "$OUT/pmc_fetch" -o run --output-format csv -- python3 "$R/bench.py" --no-cpu-baseline --no-host-inclusive --steps 2 --warmup 1 "$@" > "$OUT/pmc1.log" 2>&1 || { tail -20 "$OUT/pmc1.log"; exit 1; }
+step 300 rocprofv3 --pmc WRITE_SIZE --kernel-trace -d "$OUT/pmc_write" -o run --output-format csv -- python3 "$R/bench.py" --no-cpu-baseline --no-host-inclusive --steps 2 --warmup 1 "$@" > "$OUT/pmc2.log" 2>&1 || { tail -20 "$OUT/pmc2.log"; exit 1; }
 echo "== done"
 find "$OUT" -name "*.csv" | head -20
