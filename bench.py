@@ -9,6 +9,9 @@ already resident in HBM:
      substitutions -> op list on the host.  Algorithmic bytes = 4 GiB + 4 GiB.
   c2 (config 2): signature only over 4 GiB.
   c4 (config 4 shape): batch of 1 MiB files (signature + per-file match).
+  apply: apply_delta on the device for the C5-shaped pair of
+     one rank (8 GiB, 1% edited 8 KiB blocks): Copy ops gathered from the basis, Data
+     ops from the source; value = reconstructed GiB/s.
   c5 (config 5): ONE file of N x 8 GiB (64 GiB at 8 GPUs), bs 8192, 1% of blocks
      with one substituted byte; chunk-sharded: each rank signs its 8 GiB of the
      basis, RCCL all-gathers the signature, builds the full index, classifies its
@@ -44,7 +47,7 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=2)
-    ap.add_argument("--workload", default="c3", choices=["c3", "c2", "c4", "c5"])
+    ap.add_argument("--workload", default="c3", choices=["c3", "c2", "c4", "c5", "apply"])
     ap.add_argument("--size-gib", type=float, default=None,
                     help="bytes per rank: c2/c3 basis and source (default 4), c5 chunk (default 8)")
     ap.add_argument("--block-size", type=int, default=None, help="default 4096 (c5: 8192)")
@@ -58,11 +61,11 @@ def parse():
     ap.add_argument("--no-host-inclusive", action="store_true")
     a = ap.parse_args()
     if a.size_gib is None:
-        a.size_gib = 8.0 if a.workload == "c5" else 4.0
+        a.size_gib = 8.0 if a.workload in ("c5", "apply") else 4.0
     if a.block_size is None:
-        a.block_size = 8192 if a.workload == "c5" else 4096
+        a.block_size = 8192 if a.workload in ("c5", "apply") else 4096
     if a.edit_ppm is None:
-        a.edit_ppm = 10000 if a.workload == "c5" else 50000
+        a.edit_ppm = 10000 if a.workload in ("c5", "apply") else 50000
     return a
 
 
@@ -245,6 +248,17 @@ def main():
         new = torch.empty(n, dtype=torch.uint8, device="cuda")
         dev.synth_mutate(new, basis, seed_base + 1, args.edit_ppm)
     c5 = None
+    apply_d = None
+    if args.workload == "apply":
+        dev.synth_fill_range(basis, 0, 0x5E1D0005)
+        new = torch.empty(n + 16, dtype=torch.uint8, device="cuda")
+        dev.synth_fill_range(new[:n], 0, 0x5E1D0005)
+        dev.synth_mutate_blocks(new[:n], new[:n], 0, bs, 0x5E1D0006, args.edit_ppm)
+        w, s = dev.signature(basis, bs)
+        idx = dev.Index(w, s, bs, bs, device=local)
+        apply_d = dev.match(idx, new, length=n)
+        idx.close()
+        apply_out = torch.empty(n + 16, dtype=torch.uint8, device="cuda")
     if args.workload == "c5":
         # BASELINE config 5: one file of world * n bytes; this rank owns basis bytes
         # [rank*n, (rank+1)*n) and window starts [rank*n, (rank+1)*n) of the source
@@ -287,6 +301,9 @@ def main():
             d = dev.match(idx, new, stream=stream)
             idx.close()
             return d
+        if args.workload == "apply":
+            _, st = dev.apply_device(basis, apply_d, new, out=apply_out, stream=stream)
+            return st
         if args.workload == "c5":
             w, s = dev.signature(basis, bs, stream=stream)
             if world > 1:  # the one exchange step: RCCL all-gather of the signature SoA
@@ -338,6 +355,8 @@ def main():
         bytes_per_step = nb_bytes + n
     elif args.workload == "c5":
         bytes_per_step = 2 * n
+    elif args.workload == "apply":
+        bytes_per_step = n  # reconstructed bytes
     else:
         bytes_per_step = int(files[1].sum() + files[3].sum())
     total_bytes = bytes_per_step * args.steps * world
@@ -350,7 +369,8 @@ def main():
     # split into segments of 2^31 positions).
     src_bytes = int(files[3].sum()) if args.workload == "c4" else n
     algo_step = {"k_scan": src_bytes, "k_scan_lds": src_bytes, "k_sig_fast": nb_bytes if args.workload == "c3" else n,
-                 "k_sig_batch": n, "k_sig_wave": n, "k_probe": src_bytes}
+                 "k_sig_batch": n, "k_sig_wave": n, "k_probe": src_bytes,
+                 "k_apply": 2 * n}  # apply: every output byte read once and written once
     dom = max(prof, key=lambda k: prof[k]["ms"]) if prof else None
     roof = None
     if dom and dom in algo_step:
@@ -384,7 +404,7 @@ def main():
             "vs_baseline": None,
             "dtype": "u8",
             "data": ("synthetic (counter-based splitmix64 bytes; one substituted byte in 1% of 8 KiB blocks)"
-                     if args.workload == "c5" else
+                     if args.workload in ("c5", "apply") else
                      "synthetic (counter-based splitmix64 bytes; Bernoulli byte substitutions)"),
             "config": {
                 "workload": {
@@ -394,6 +414,8 @@ def main():
                           f"batched signature + per-file index + batched match, file-sharded over ranks",
                     "c5": f"C5: one {world * n / GIB:.0f} GiB file, bs {bs}, {args.edit_ppm / 1e4:g}% of blocks with "
                           f"one substituted byte; signature + all-gather + index + chunk match, chunk-sharded",
+                    "apply": f"apply_delta on the device: {n / GIB:.0f} GiB reconstructed from a bs {bs} delta "
+                             f"({args.edit_ppm / 1e4:g}% of blocks edited), per rank",
                 }[args.workload],
                 "block_size": bs,
                 "basis_bytes": nb_bytes if args.workload == "c3" else n,

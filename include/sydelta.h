@@ -176,6 +176,15 @@ typedef struct sydelta_apply_stats {
 } sydelta_apply_stats;
 int sydelta_apply_delta(const char *old_file, const sydelta_delta *d, const char *new_file, sydelta_apply_stats *out);
 
+/* applier.rs:22-56 `apply_delta` on device-resident bytes: d_out
+ * receives the reconstructed file.  Copy ops read d_basis[offset, +size) (past the end:
+ * SYDELTA_E_IO, as read_exact fails); Data ops of a device delta (sydelta_match_device)
+ * read d_lit[op source offset, +len) -- the source the delta was generated from, or any
+ * buffer laid out the same way.  out_cap must hold the reconstructed size. */
+int sydelta_apply_delta_device(int device, const uint8_t *d_basis, uint64_t basis_len, const sydelta_delta *d,
+                               const uint8_t *d_lit, uint64_t lit_len, uint8_t *d_out, uint64_t out_cap,
+                               void *stream, sydelta_apply_stats *out);
+
 /* rolling.rs:35-45 `Adler32::hash` (host utility for the re-exported Adler32 type). */
 uint32_t sydelta_adler32_hash(const uint8_t *data, uint64_t len);
 
@@ -239,6 +248,9 @@ int sydelta_chunk_classify(sydelta_index *idx, const uint8_t *d_buf, uint64_t bu
  * the next chunk's leading Data op), a final chunk ends at file_len. */
 int sydelta_chunk_walk(sydelta_chunk *c, uint64_t entry, uint64_t *exit_pos, sydelta_delta **out);
 void sydelta_chunk_free(sydelta_chunk *c);
+/* A delta holding a copy of n ops (e.g. one received from the sender, to apply on the
+ * device); NULL if ops is NULL with n > 0. */
+sydelta_delta *sydelta_delta_from_ops(const sydelta_op *ops, uint64_t n, uint64_t source_size, uint64_t block_size);
 /* Empty delta (Delta { ops: [], source_size, block_size }) to append chunk deltas to. */
 sydelta_delta *sydelta_delta_new(uint64_t source_size, uint64_t block_size);
 /* dst.ops += src.ops, merging dst's trailing Data op with src's leading Data op when

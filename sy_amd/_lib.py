@@ -74,6 +74,7 @@ SIGNATURES = [
     ("sydelta_generate_delta_streaming", _i, [ctypes.c_char_p, ctypes.POINTER(BlockChecksumC), _u64, _u64, _pp]),
     ("sydelta_generate_delta", _i, [ctypes.c_char_p, ctypes.POINTER(BlockChecksumC), _u64, _u64, _pp]),
     ("sydelta_apply_delta", _i, [ctypes.c_char_p, _vp, ctypes.c_char_p, ctypes.POINTER(DeltaStatsC)]),
+    ("sydelta_apply_delta_device", _i, [_i, _vp, _u64, _vp, _vp, _u64, _vp, _u64, _vp, ctypes.POINTER(DeltaStatsC)]),
     ("sydelta_adler32_hash", _u32, [_vp, _u64]),
     ("sydelta_signature_batch_device", _i, [_i, _vp, _vp, _vp, _u64, _u64, _vp, _vp, _vp]),
     ("sydelta_index_create_batch", _i, [_i, _vp, _vp, _vp, _vp, _u64, _u64, _i, _vp, _pp]),
@@ -87,6 +88,7 @@ SIGNATURES = [
     ("sydelta_chunk_free", None, [_vp]),
     ("sydelta_delta_new", _vp, [_u64, _u64]),
     ("sydelta_delta_append", _i, [_vp, _vp]),
+    ("sydelta_delta_from_ops", _vp, [_vp, _u64, _u64, _u64]),
     ("sydelta_set_profiling", None, [_i]),
     ("sydelta_profile_json", ctypes.c_size_t, [ctypes.c_char_p, ctypes.c_size_t, _i]),
     ("sydelta_synth_fill", _i, [_vp, _u64, _u64, _vp]),

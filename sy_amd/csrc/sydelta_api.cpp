@@ -1199,6 +1199,71 @@ extern "C" int sydelta_generate_delta_streaming(const char* source_path, const s
 }
 
 // applier.rs:22-56 — receiver side, host I/O only.
+// applier.rs:22-56 on device-resident bytes: Copy{offset, size} reads basis[offset,
+// +size) (read_exact: past the end is an error, applier.rs:36), Data reads its literal
+// bytes from d_lit at the op's source offset (a device delta's Data ops index the
+// source the delta was generated from).
+extern "C" int sydelta_apply_delta_device(int device, const uint8_t* d_basis, uint64_t basis_len,
+                                          const sydelta_delta* d, const uint8_t* d_lit, uint64_t lit_len,
+                                          uint8_t* d_out, uint64_t out_cap, void* stream, sydelta_apply_stats* out) {
+    if (!d) return fail(SYDELTA_E_INVAL, "NULL delta");
+    if (int r = ensure_device(device)) return r;
+    // the piece table is staged in pinned host memory (one per thread, grown on demand)
+    // so its upload runs at PCIe speed
+    struct Pinned {
+        ApplyPiece* p = nullptr;
+        size_t cap = 0;
+        ~Pinned() { if (p) (void)hipHostFree(p); }
+    };
+    static thread_local Pinned pin;
+    uint64_t need = 0;
+    constexpr uint64_t kSlice = 64 * 1024;
+    for (const sydelta_op& o : d->ops) need += (o.b + kSlice - 1) / kSlice;
+    if (need > pin.cap) {
+        if (pin.p) { (void)hipHostFree(pin.p); pin.p = nullptr; pin.cap = 0; }
+        const size_t cap = std::max<size_t>(need, 4096) * 5 / 4;
+        HIP_TRY(hipHostMalloc((void**)&pin.p, cap * sizeof(ApplyPiece), hipHostMallocDefault));
+        pin.cap = cap;
+    }
+    ApplyPiece* pieces = pin.p;
+    size_t np = 0;
+    uint64_t pos = 0, literal = 0;
+    for (size_t i = 0; i < d->ops.size(); ++i) {
+        const sydelta_op& o = d->ops[i];
+        const bool cp = o.kind == SYDELTA_OP_COPY;
+        if (cp && (o.a > basis_len || o.b > basis_len - o.a))
+            return fail(SYDELTA_E_IO, "op %zu: Copy{offset %llu, size %llu} past the end of the basis (%llu bytes): "
+                        "failed to fill whole buffer", i, (unsigned long long)o.a, (unsigned long long)o.b,
+                        (unsigned long long)basis_len);
+        if (!cp && (o.a > lit_len || o.b > lit_len - o.a))
+            return fail(SYDELTA_E_INVAL, "op %zu: Data [%llu, +%llu) outside the literal buffer", i,
+                        (unsigned long long)o.a, (unsigned long long)o.b);
+        for (uint64_t k = 0; k < o.b; k += kSlice)
+            pieces[np++] = {pos + k, o.a + k, (uint32_t)std::min<uint64_t>(kSlice, o.b - k), cp ? 1u : 0u};
+        pos += o.b;
+        if (!cp) literal += o.b;
+    }
+    if (pos > out_cap) return fail(SYDELTA_E_INVAL, "output needs %llu bytes, capacity %llu",
+                                   (unsigned long long)pos, (unsigned long long)out_cap);
+    if (pos && !d_out) return fail(SYDELTA_E_INVAL, "NULL output");
+    hipStream_t s = stream ? (hipStream_t)stream : thread_stream(device < 0 ? 0 : device);
+    CallProf cp;
+    if (np) {
+        DevBuf pb;
+        HIP_TRY(hipMallocAsync(&pb.p, np * sizeof(ApplyPiece), s));
+        pb.s = s;
+        HIP_TRY(hipMemcpyAsync(pb.p, pieces, np * sizeof(ApplyPiece), hipMemcpyHostToDevice, s));
+        HIP_TRY(launch_apply((const ApplyPiece*)pb.p, np, d_basis, d_lit, d_out, s, cp.get()));
+        HIP_TRY(hipStreamSynchronize(s));  // the pinned table is reused by the next call
+    }
+    if (out) {
+        out->operations_count = d->ops.size();
+        out->literal_bytes = literal;
+        out->bytes_written = pos;
+    }
+    return SYDELTA_OK;
+}
+
 extern "C" int sydelta_apply_delta(const char* old_file, const sydelta_delta* d, const char* new_file,
                                    sydelta_apply_stats* out) {
     if (!d || !old_file || !new_file) return fail(SYDELTA_E_INVAL, "NULL argument");
@@ -1427,6 +1492,17 @@ extern "C" int sydelta_delta_append(sydelta_delta* dst, const sydelta_delta* src
     dst->source_size = std::max(dst->source_size, src->source_size);
     finish_stats(dst);
     return SYDELTA_OK;
+}
+
+extern "C" sydelta_delta* sydelta_delta_from_ops(const sydelta_op* ops, uint64_t n, uint64_t source_size,
+                                                 uint64_t block_size) {
+    if (n && !ops) return nullptr;
+    sydelta_delta* d = new sydelta_delta();
+    d->source_size = source_size;
+    d->block_size = block_size;
+    d->ops.assign(ops, ops + n);
+    finish_stats(d);
+    return d;
 }
 
 extern "C" sydelta_delta* sydelta_delta_new(uint64_t source_size, uint64_t block_size) {

@@ -125,6 +125,16 @@ struct TailJob {
 };
 hipError_t launch_tail(const uint8_t* d_buf, const TailJob* d_jobs, uint32_t njobs, const uint32_t* d_weak,
                        const uint64_t* d_strong, int* d_flag, hipStream_t s);
+// One slice (<= 64 KiB) of an op for the device apply: out[dst, dst+len) =
+// (from_basis ? basis : lit)[src, src+len).
+struct ApplyPiece {
+    uint64_t dst;
+    uint64_t src;
+    uint32_t len;
+    uint32_t from_basis;
+};
+hipError_t launch_apply(const ApplyPiece* d_pieces, uint64_t npieces, const uint8_t* d_basis, const uint8_t* d_lit,
+                        uint8_t* d_out, hipStream_t s, Profiler* prof);
 hipError_t launch_synth_fill(uint8_t* d_buf, uint64_t len, uint64_t seed, hipStream_t s, uint64_t first = 0);
 hipError_t launch_synth_edit_blocks(uint8_t* d_dst, uint64_t len, uint64_t bs, uint64_t first, uint64_t seed,
                                     uint32_t rate_ppm, hipStream_t s);

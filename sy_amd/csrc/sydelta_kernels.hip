@@ -1388,6 +1388,51 @@ __global__ void k_tail(const uint8_t* __restrict__ buf, const TailJob* __restric
 }
 
 // ===========================================================================
+// K6: apply_delta on the device (applier.rs:22-56 as a gather-copy)
+// ===========================================================================
+// One workgroup per piece (an op, or a <= 64 KiB slice of one).  Thread t writes the
+// aligned 16-byte destination chunks t, t+256, ...; a chunk wholly inside the piece
+// is assembled from two aligned 16-byte source loads with alignbyte (the source
+// misalignment (src - dst) & 15 is uniform per piece); the partial chunks at the two
+// ends of a piece are written byte by byte, so adjacent pieces never race.
+__device__ __forceinline__ uint32_t funnel(uint32_t hi, uint32_t lo, uint32_t r) {
+    return __builtin_amdgcn_alignbyte(hi, lo, r);
+}
+
+__global__ __launch_bounds__(256) void k_apply(const ApplyPiece* __restrict__ pieces, const uint8_t* __restrict__ basis,
+                                               const uint8_t* __restrict__ lit, uint8_t* __restrict__ out) {
+    const ApplyPiece P = pieces[blockIdx.x];
+    const uint8_t* src = (P.from_basis ? basis : lit) + P.src;
+    uint8_t* dst = out + P.dst;
+    const uint64_t d0 = P.dst, d1 = P.dst + P.len;
+    const uint64_t c_first = d0 & ~15ull, c_end = (d1 + 15) & ~15ull;
+    const uint32_t sh = (uint32_t)((P.src - P.dst) & 15);  // source byte of dst byte x is at x + (src - dst)
+    const uint32_t dq = sh >> 2, r = sh & 3;
+    for (uint64_t c = c_first + 16ull * threadIdx.x; c < c_end; c += 16ull * blockDim.x) {
+        if (c >= d0 && c + 16 <= d1) {
+            const uint8_t* s = src + (c - d0);
+            const uint4* sa = (const uint4*)((uintptr_t)s & ~(uintptr_t)15);
+            const uint4 A = sa[0];
+            uint4 B = make_uint4(0, 0, 0, 0);
+            if (sh) B = sa[1];
+            const uint32_t w[8] = {A.x, A.y, A.z, A.w, B.x, B.y, B.z, B.w};
+            uint4 o;
+            // dword k of the output = bytes [sh + 4k, +4) of A|B
+            switch (dq) {
+                case 0: o = make_uint4(funnel(w[1], w[0], r), funnel(w[2], w[1], r), funnel(w[3], w[2], r), funnel(w[4], w[3], r)); break;
+                case 1: o = make_uint4(funnel(w[2], w[1], r), funnel(w[3], w[2], r), funnel(w[4], w[3], r), funnel(w[5], w[4], r)); break;
+                case 2: o = make_uint4(funnel(w[3], w[2], r), funnel(w[4], w[3], r), funnel(w[5], w[4], r), funnel(w[6], w[5], r)); break;
+                default: o = make_uint4(funnel(w[4], w[3], r), funnel(w[5], w[4], r), funnel(w[6], w[5], r), funnel(w[7], w[6], r)); break;
+            }
+            *(uint4*)(out + c) = o;
+        } else {
+            const uint64_t lo = c < d0 ? d0 : c, hi = (c + 16 < d1) ? c + 16 : d1;
+            for (uint64_t x = lo; x < hi; ++x) dst[x - d0] = src[x - d0];
+        }
+    }
+}
+
+// ===========================================================================
 // Synthetic inputs (bench)
 // ===========================================================================
 // bytes [8*w0, 8*w0 + len) of the stream
@@ -1676,6 +1721,17 @@ hipError_t launch_tail(const uint8_t* d_buf, const TailJob* d_jobs, uint32_t njo
     if (!njobs) return hipSuccess;
     hipLaunchKernelGGL(k_tail, dim3(grid_for((uint64_t)njobs * 64, 256)), dim3(256), 0, s, d_buf, d_jobs, njobs, d_weak,
                        d_strong, d_flag);
+    return hipGetLastError();
+}
+
+hipError_t launch_apply(const ApplyPiece* d_pieces, uint64_t npieces, const uint8_t* d_basis, const uint8_t* d_lit,
+                        uint8_t* d_out, hipStream_t s, Profiler* prof) {
+    if (!npieces) return hipSuccess;
+    ProfScope ps(prof, s, "k_apply");
+    for (uint64_t p0 = 0; p0 < npieces; p0 += 0x7FFFFFFFull) {
+        const uint64_t cnt = std::min<uint64_t>(npieces - p0, 0x7FFFFFFFull);
+        hipLaunchKernelGGL(k_apply, dim3((unsigned)cnt), dim3(256), 0, s, d_pieces + p0, d_basis, d_lit, d_out);
+    }
     return hipGetLastError();
 }
 

@@ -102,6 +102,7 @@ class DeviceDelta:
     source_size: int
     block_size: int
     stats: dict
+    handle: object = None  # the library's sydelta_delta (when the ops are its zero-copy view)
 
     def tuples(self):
         return [("C" if int(k) == 0 else "D", int(x), int(y)) for k, x, y in zip(self.kind, self.a, self.b)]
@@ -142,7 +143,8 @@ def _device_delta(h, owner=None) -> DeviceDelta:
     st = _lib.MatchStatsC()
     check(lib.sydelta_delta_stats(h, ctypes.byref(st)))
     stats = {f: int(getattr(st, f)) for f, _ in _lib.MatchStatsC._fields_}
-    return DeviceDelta(kind, a, b, int(lib.sydelta_delta_source_size(h)), int(lib.sydelta_delta_block_size(h)), stats)
+    return DeviceDelta(kind, a, b, int(lib.sydelta_delta_source_size(h)), int(lib.sydelta_delta_block_size(h)), stats,
+                       owner)
 
 
 def match_batch(index: BatchIndex, buf: torch.Tensor, offs, lens, stream=None):
@@ -234,6 +236,36 @@ def synth_mutate_blocks(dst: torch.Tensor, src: torch.Tensor, first: int, block_
     assert dst.numel() == src.numel()
     check(lib.sydelta_synth_mutate_blocks(_ptr(dst), _ptr(src), first, src.numel(), block_size,
                                           seed & 0xFFFFFFFFFFFFFFFF, rate_ppm, _stream(stream)))
+
+
+def apply_device(basis: torch.Tensor, delta: DeviceDelta, lit: torch.Tensor, out: torch.Tensor | None = None,
+                 stream=None):
+    """apply_delta (applier.rs:22-56) on the device: Copy ops from `basis`, Data ops
+    from `lit` at the op's source offset.  Returns (out tensor, stats dict)."""
+    n = len(delta.kind)
+    total = int(np.asarray(delta.b, dtype=np.uint64).sum()) if n else 0
+    if out is None:
+        out = torch.empty(max(total, 1), dtype=torch.uint8, device=basis.device)
+    own = None
+    if delta.handle is not None:  # the library's own delta: no copy of the ops
+        h = delta.handle.h
+    else:
+        ops = np.zeros(n, dtype=_OP_DTYPE)
+        if n:
+            ops["kind"], ops["a"], ops["b"] = delta.kind, delta.a, delta.b
+        own = h = lib.sydelta_delta_from_ops(ops.ctypes.data if n else None, n, delta.source_size,
+                                             delta.block_size)
+        if not h:
+            raise ValueError("bad op array")
+    st = _lib.DeltaStatsC()
+    try:
+        check(lib.sydelta_apply_delta_device(basis.device.index or 0, _ptr(basis), basis.numel(), h,
+                                             _ptr(lit), lit.numel(), _ptr(out), out.numel(), _stream(stream),
+                                             ctypes.byref(st)))
+    finally:
+        if own:
+            lib.sydelta_delta_free(own)
+    return out[:total], {f: int(getattr(st, f)) for f, _ in _lib.DeltaStatsC._fields_}
 
 
 def synth_fill(buf: torch.Tensor, seed: int, stream=None) -> None:

@@ -217,3 +217,43 @@ def test_synth_ranges_match_oracle(gpu):
     assert np.array_equal(got, exp)
     changed = np.nonzero(got != ref)[0] // bs
     assert 4 <= len(set(changed.tolist())) <= 30 and len(changed) == len(set(changed.tolist()))
+
+
+# ---------------------------------------------------------------------------
+# apply_delta on the device (applier.rs:22-56)
+# ---------------------------------------------------------------------------
+@pytest.mark.parametrize("bs", [7, 64, 1000, 4096, 8192])
+def test_apply_device_round_trip(bs, gpu, oracle_c):
+    """apply(match(basis, src)) == src byte for byte, with unaligned Copy/Data
+    offsets (odd block sizes, shifted regions) and ops longer than a 64 KiB slice."""
+    import torch
+
+    rng = random.Random(bs + 11)
+    basis = rng.randbytes(rng.randint(200 * bs, 300 * bs) + rng.randint(0, bs - 1))
+    src = bytearray(_shift_edits(basis, rng, bs, 6))
+    for _ in range(8):
+        p = rng.randrange(len(src))
+        src[p:p] = rng.randbytes(rng.randint(1, 3 * bs))
+    src = bytes(src)
+    idx = _index(gpu, basis, bs)
+    s_dev = _to_dev(src)
+    d = gpu.match(idx, s_dev, length=len(src))
+    idx.close()
+    assert d.tuples() == _oracle_ops(oracle_c, src, basis, bs)
+    b_dev = _to_dev(basis)
+    out, st = gpu.apply_device(b_dev[:len(basis)], d, s_dev[:len(src)])
+    torch.cuda.synchronize()
+    assert bytes(out.cpu().numpy()) == src
+    assert st["bytes_written"] == len(src) and st["operations_count"] == len(d.kind)
+    assert st["literal_bytes"] == sum(int(b) for k, b in zip(d.kind, d.b) if int(k) == 1)
+
+
+def test_apply_device_rejects_copy_past_end(gpu):
+    import torch
+    import sy_amd._lib as L
+
+    b = torch.zeros(4096, dtype=torch.uint8, device="cuda")
+    bad = gpu.DeviceDelta(np.array([0], np.uint32), np.array([4000], np.uint64), np.array([200], np.uint64),
+                          200, 4096, {})
+    with pytest.raises(L.SyDeltaError):
+        gpu.apply_device(b, bad, b)
