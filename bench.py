@@ -12,6 +12,9 @@ already resident in HBM:
   apply: apply_delta on the device for the C5-shaped pair of
      one rank (8 GiB, 1% edited 8 KiB blocks): Copy ops gathered from the basis, Data
      ops from the source; value = reconstructed GiB/s.
+  json: serde_json text of the C3 delta (one 4 GiB literal run,
+     ~3.6 characters per byte) written on the device; value = delta source GiB/s;
+     cpu_baseline = the same text from libsydelta's host writer on a 256 MiB sample.
   c5 (config 5): ONE file of N x 8 GiB (64 GiB at 8 GPUs), bs 8192, 1% of blocks
      with one substituted byte; chunk-sharded: each rank signs its 8 GiB of the
      basis, RCCL all-gathers the signature, builds the full index, classifies its
@@ -47,7 +50,7 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=2)
-    ap.add_argument("--workload", default="c3", choices=["c3", "c2", "c4", "c5", "apply"])
+    ap.add_argument("--workload", default="c3", choices=["c3", "c2", "c4", "c5", "apply", "json"])
     ap.add_argument("--size-gib", type=float, default=None,
                     help="bytes per rank: c2/c3 basis and source (default 4), c5 chunk (default 8)")
     ap.add_argument("--block-size", type=int, default=None, help="default 4096 (c5: 8192)")
@@ -107,6 +110,19 @@ def cpu_baseline(bs: int):
                    f"single-thread rolling scan of {scan_n >> 20} MiB with 5% byte edits "
                    f"({scan_rate / 2**20:.2f} MiB/s); extrapolated to 4 GiB + 4 GiB"),
     }
+
+
+def cpu_json_baseline(src_dev, bs: int):
+    """libsydelta's host serde_json writer (one thread) on a 256 MiB literal sample of
+    the same source: the text sy's sender builds with serde_json::to_string(&delta)."""
+    from sy_amd import wire
+
+    sample = src_dev[:256 << 20].cpu().numpy()
+    t0 = time.perf_counter()
+    text = wire.delta_to_json([1], [0], [sample.size], sample.size, bs, sample)
+    dt = time.perf_counter() - t0
+    return {"value": round(sample.size / dt / GIB, 4), "unit": "GiB/s", "cores": 1, "kind": "port",
+            "sample": f"host writer, one Data op of {sample.size >> 20} MiB ({len(text) >> 20} MiB of text)"}
 
 
 def shard_range(nunits: int, world: int, rank: int):
@@ -231,6 +247,9 @@ def main():
     if world > 1:
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
     import sy_amd.device as dev
+    import ctypes
+
+    from sy_amd._lib import check, lib
 
     bs = args.block_size
     n = int(args.size_gib * GIB) // bs * bs
@@ -249,6 +268,21 @@ def main():
         dev.synth_mutate(new, basis, seed_base + 1, args.edit_ppm)
     c5 = None
     apply_d = None
+    json_d = None
+    if args.workload == "json":
+        from sy_amd import wire
+
+        dev.synth_fill(basis, seed_base)
+        new = torch.empty(n, dtype=torch.uint8, device="cuda")
+        dev.synth_mutate(new, basis, seed_base + 1, args.edit_ppm)
+        w, s = dev.signature(basis, bs)
+        idx = dev.Index(w, s, bs, bs, device=local)
+        json_d = dev.match(idx, new)
+        idx.close()
+        json_h = wire._delta_handle(json_d.kind, json_d.a, json_d.b, json_d.source_size, bs)
+        json_len = ctypes.c_uint64()
+        check(lib.sydelta_delta_to_json_device(json_h, new.data_ptr(), n, None, 0, ctypes.byref(json_len), None))
+        json_out = torch.empty(json_len.value + 16, dtype=torch.uint8, device="cuda")
     if args.workload == "apply":
         dev.synth_fill_range(basis, 0, 0x5E1D0005)
         new = torch.empty(n + 16, dtype=torch.uint8, device="cuda")
@@ -304,6 +338,11 @@ def main():
         if args.workload == "apply":
             _, st = dev.apply_device(basis, apply_d, new, out=apply_out, stream=stream)
             return st
+        if args.workload == "json":
+            ln = ctypes.c_uint64()
+            check(lib.sydelta_delta_to_json_device(json_h, new.data_ptr(), n, json_out.data_ptr(), json_out.numel(),
+                                                   ctypes.byref(ln), int(stream.cuda_stream)))
+            return {"json_bytes": ln.value, "ops": len(json_d.kind)}
         if args.workload == "c5":
             w, s = dev.signature(basis, bs, stream=stream)
             if world > 1:  # the one exchange step: RCCL all-gather of the signature SoA
@@ -357,6 +396,8 @@ def main():
         bytes_per_step = 2 * n
     elif args.workload == "apply":
         bytes_per_step = n  # reconstructed bytes
+    elif args.workload == "json":
+        bytes_per_step = n  # delta source bytes covered by the text
     else:
         bytes_per_step = int(files[1].sum() + files[3].sum())
     total_bytes = bytes_per_step * args.steps * world
@@ -370,7 +411,8 @@ def main():
     src_bytes = int(files[3].sum()) if args.workload == "c4" else n
     algo_step = {"k_scan": src_bytes, "k_scan_lds": src_bytes, "k_sig_fast": nb_bytes if args.workload == "c3" else n,
                  "k_sig_batch": n, "k_sig_wave": n, "k_probe": src_bytes,
-                 "k_apply": 2 * n}  # apply: every output byte read once and written once
+                 "k_apply": 2 * n,  # apply: every output byte read once and written once
+                 "k_json_write": n}  # json: every literal byte read once (text written: ~3.6x)
     dom = max(prof, key=lambda k: prof[k]["ms"]) if prof else None
     roof = None
     if dom and dom in algo_step:
@@ -387,6 +429,8 @@ def main():
         cpu = None
         if world == 1 and not args.no_cpu_baseline and args.workload == "c3":
             cpu = cpu_baseline(bs)
+        if world == 1 and not args.no_cpu_baseline and args.workload == "json":
+            cpu = cpu_json_baseline(new, bs)
         hinc = None
         if world == 1 and not args.no_host_inclusive and args.workload == "c3":
             hinc = host_inclusive(dev, bs, min(n, 1 << 30), local)
@@ -416,6 +460,7 @@ def main():
                           f"one substituted byte; signature + all-gather + index + chunk match, chunk-sharded",
                     "apply": f"apply_delta on the device: {n / GIB:.0f} GiB reconstructed from a bs {bs} delta "
                              f"({args.edit_ppm / 1e4:g}% of blocks edited), per rank",
+                    "json": f"serde_json text of the C3 delta ({n / GIB:.0f} GiB source, one literal run) on the device",
                 }[args.workload],
                 "block_size": bs,
                 "basis_bytes": nb_bytes if args.workload == "c3" else n,

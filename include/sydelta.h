@@ -258,6 +258,29 @@ sydelta_delta *sydelta_delta_new(uint64_t source_size, uint64_t block_size);
 int sydelta_delta_append(sydelta_delta *dst, const sydelta_delta *src);
 
 /* ---------------------------------------------------------------------------
+ * Wire formats: serde_json's compact text of the types sy
+ * moves between sender and receiver.
+ * ------------------------------------------------------------------------- */
+/* serde_json::to_string(&Vec<BlockChecksum>) (sy-remote.rs:146-147, println without
+ * the newline).  Returns the text length; writes it when buf holds that many bytes. */
+uint64_t sydelta_checksums_to_json(const sydelta_block_checksum *sigs, uint64_t n, char *buf, uint64_t cap);
+/* serde_json::from_str::<Vec<BlockChecksum>> (ssh.rs:967-973).  *out is malloc'ed
+ * (free with sydelta_checksums_free). */
+int sydelta_checksums_from_json(const char *json, uint64_t len, sydelta_block_checksum **out, uint64_t *n);
+/* serde_json::to_string(&Delta) (ssh.rs:1003).  Literal bytes: the delta's own when
+ * lit is NULL (host entry points), else lit[op source offset, +len) (device deltas).
+ * *out_len = text length; the text is written when buf holds it. */
+int sydelta_delta_to_json(const sydelta_delta *d, const uint8_t *lit, uint64_t lit_len, char *buf, uint64_t cap,
+                          uint64_t *out_len);
+/* The same text produced on the device from literal bytes in HBM (d_lit indexed by the
+ * Data ops' source offsets) into d_out; *out_len as above (computed on the device). */
+int sydelta_delta_to_json_device(const sydelta_delta *d, const uint8_t *d_lit, uint64_t lit_len, uint8_t *d_out,
+                                 uint64_t out_cap, uint64_t *out_len, void *stream);
+/* serde_json::from_str::<Delta> (sy-remote.rs:175): a host delta holding its literal
+ * bytes, ready for sydelta_apply_delta. */
+int sydelta_delta_from_json(const char *json, uint64_t len, sydelta_delta **out);
+
+/* ---------------------------------------------------------------------------
  * Measurement support (used by bench.py; not part of the reference API).
  * ------------------------------------------------------------------------- */
 /* When on, the library records a HIP event pair around every kernel it

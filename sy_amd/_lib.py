@@ -89,6 +89,12 @@ SIGNATURES = [
     ("sydelta_delta_new", _vp, [_u64, _u64]),
     ("sydelta_delta_append", _i, [_vp, _vp]),
     ("sydelta_delta_from_ops", _vp, [_vp, _u64, _u64, _u64]),
+    ("sydelta_checksums_to_json", _u64, [_vp, _u64, _vp, _u64]),
+    ("sydelta_checksums_from_json", _i, [_vp, _u64, ctypes.POINTER(ctypes.POINTER(BlockChecksumC)),
+                                         ctypes.POINTER(_u64)]),
+    ("sydelta_delta_to_json", _i, [_vp, _vp, _u64, _vp, _u64, ctypes.POINTER(_u64)]),
+    ("sydelta_delta_to_json_device", _i, [_vp, _vp, _u64, _vp, _u64, ctypes.POINTER(_u64), _vp]),
+    ("sydelta_delta_from_json", _i, [_vp, _u64, _pp]),
     ("sydelta_set_profiling", None, [_i]),
     ("sydelta_profile_json", ctypes.c_size_t, [ctypes.c_char_p, ctypes.c_size_t, _i]),
     ("sydelta_synth_fill", _i, [_vp, _u64, _u64, _vp]),
@@ -99,6 +105,14 @@ SIGNATURES = [
 
 
 def _load() -> ctypes.CDLL:
+    # One HIP runtime per process: torch (the harness's device-memory plumbing) ships
+    # its own libamdhip64 with the same soname as /opt/rocm's.  Loading torch first makes
+    # libsydelta bind to that copy; loaded the other way round, the two runtimes both
+    # initialise and the second finds no device.
+    try:
+        import torch  # noqa: F401
+    except ImportError:
+        pass
     if not os.path.exists(LIB_PATH):
         raise ImportError(
             f"libsydelta.so not found at {LIB_PATH}; build it with `python -m sy_amd.build` "

@@ -27,6 +27,7 @@
 #include <vector>
 
 #include "../../include/sydelta.h"
+#include "sydelta_host.hpp"
 #include "sydelta_internal.hpp"
 
 using namespace sydelta;
@@ -36,7 +37,7 @@ using namespace sydelta;
 // ---------------------------------------------------------------------------
 static thread_local std::string t_err;
 
-static int fail(int code, const char* fmt, ...) {
+int sydelta::fail(int code, const char* fmt, ...) {
     char buf[512];
     va_list ap;
     va_start(ap, fmt);
@@ -46,14 +47,6 @@ static int fail(int code, const char* fmt, ...) {
     return code;
 }
 
-#define HIP_TRY(expr)                                                                                   \
-    do {                                                                                                \
-        hipError_t e_ = (expr);                                                                         \
-        if (e_ != hipSuccess) {                                                                         \
-            int code_ = (e_ == hipErrorOutOfMemory) ? SYDELTA_E_OOM : SYDELTA_E_KERNEL;                 \
-            return fail(code_, "%s: %s (%s:%d)", #expr, hipGetErrorString(e_), __FILE__, __LINE__);   \
-        }                                                                                               \
-    } while (0)
 
 extern "C" const char* sydelta_last_error(void) { return t_err.c_str(); }
 extern "C" int sydelta_abi_version(void) { return SYDELTA_ABI_VERSION; }
@@ -70,7 +63,7 @@ struct DevState {
 std::mutex g_dev_mu;
 std::map<int, std::unique_ptr<DevState>> g_devs;
 
-int ensure_device(int device) {
+int ensure_device_impl(int device) {
     if (device < 0) device = 0;
     DevState* st;
     {
@@ -81,8 +74,10 @@ int ensure_device(int device) {
     }
     std::call_once(st->once, [&] {
         int n = 0;
-        if (hipGetDeviceCount(&n) != hipSuccess || n <= device) {
-            st->msg = "no HIP device " + std::to_string(device);
+        const hipError_t e = hipGetDeviceCount(&n);
+        if (e != hipSuccess || n <= device) {
+            st->msg = "no HIP device " + std::to_string(device) + " (hipGetDeviceCount: " + hipGetErrorString(e) +
+                      ", " + std::to_string(n) + " devices)";
             return;
         }
         hipDeviceProp_t prop;
@@ -102,7 +97,7 @@ int ensure_device(int device) {
 }
 
 // one stream per (thread, device): calls on different threads never share a stream
-hipStream_t thread_stream(int device) {
+hipStream_t thread_stream_impl(int device) {
     static thread_local std::map<int, hipStream_t> streams;
     auto it = streams.find(device);
     if (it != streams.end()) return it->second;
@@ -121,6 +116,9 @@ std::atomic<int> g_prof_on{0};
 std::mutex g_prof_mu;
 std::map<std::string, std::pair<double, uint64_t>> g_prof;
 }  // namespace
+
+int sydelta::ensure_device(int device) { return ensure_device_impl(device); }
+hipStream_t sydelta::thread_stream(int device) { return thread_stream_impl(device); }
 
 namespace sydelta {
 ProfScope::ProfScope(Profiler* p_, hipStream_t s_, const char* n) : p(p_), s(s_), name(n) {
@@ -149,13 +147,7 @@ void Profiler::resolve() {
 }
 }  // namespace sydelta
 
-namespace {
-struct CallProf {
-    Profiler prof;
-    Profiler* get() { return g_prof_on.load() ? &prof : nullptr; }
-    ~CallProf() { prof.resolve(); }
-};
-}  // namespace
+bool sydelta::profiling_on() { return g_prof_on.load() != 0; }
 
 extern "C" void sydelta_set_profiling(int on) { g_prof_on.store(on ? 1 : 0); }
 
@@ -403,13 +395,6 @@ void give_ops(std::vector<sydelta_op>&& v) {
 }
 }  // namespace
 
-struct sydelta_delta {
-    std::vector<sydelta_op> ops;
-    uint64_t source_size = 0, block_size = 0;
-    sydelta_match_stats stats{};
-    std::vector<uint8_t> lit;         // literal bytes (host-data entry points)
-    std::vector<uint64_t> lit_off;    // per op: offset into lit, or UINT64_MAX
-};
 
 struct sydelta_delta_batch {
     std::vector<sydelta_delta> d;
@@ -880,7 +865,7 @@ int Classifier::walk(size_t i, uint64_t entry, const BasisInfo& bi, bool final_s
     return SYDELTA_OK;
 }
 
-void finish_stats(sydelta_delta* d) {
+void finish_stats_impl(sydelta_delta* d) {
     d->stats.copy_ops = d->stats.data_ops = d->stats.literal_bytes = 0;
     for (auto& o : d->ops) {
         if (o.kind == SYDELTA_OP_COPY) {
@@ -924,6 +909,8 @@ int tail_flags(Classifier& C, const std::vector<size_t>& which, std::vector<int>
     return SYDELTA_OK;
 }
 }  // namespace
+
+void sydelta::finish_stats(sydelta_delta* d) { finish_stats_impl(d); }
 
 // Match source f (d_buf[src_off[f] .. +src_len[f])) against file f of the index,
 // for every f; results in b->d[f].

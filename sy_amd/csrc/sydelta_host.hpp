@@ -1,0 +1,48 @@
+// sydelta_host.hpp — host-side definitions shared by the C ABI translation units
+// (sydelta_api.cpp: signature / index / match / apply; sydelta_wire.cpp: wire formats).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include <string>
+#include <vector>
+
+#include "../../include/sydelta.h"
+#include "sydelta_internal.hpp"
+
+// Delta (generator.rs:19-25): ops plus, for host-data entry points, the literal bytes.
+struct sydelta_delta {
+    std::vector<sydelta_op> ops;
+    uint64_t source_size = 0, block_size = 0;
+    sydelta_match_stats stats{};
+    std::vector<uint8_t> lit;         // literal bytes (host-data entry points)
+    std::vector<uint64_t> lit_off;    // per op: offset into lit, or UINT64_MAX
+};
+
+namespace sydelta {
+// Record the calling thread's error text (sydelta_last_error) and return code.
+int fail(int code, const char* fmt, ...);
+// Make `device` current after its one-time gfx950 check.
+int ensure_device(int device);
+// The calling thread's stream for `device`.
+hipStream_t thread_stream(int device);
+// Recount copy/data ops and literal bytes of d.
+void finish_stats(sydelta_delta* d);
+// sydelta_set_profiling state; CallProf collects one call's kernel timings.
+bool profiling_on();
+struct CallProf {
+    Profiler prof;
+    Profiler* get() { return profiling_on() ? &prof : nullptr; }
+    ~CallProf() { prof.resolve(); }
+};
+}  // namespace sydelta
+
+#define HIP_TRY(expr)                                                                                   \
+    do {                                                                                                \
+        hipError_t e_ = (expr);                                                                         \
+        if (e_ != hipSuccess) {                                                                         \
+            int code_ = (e_ == hipErrorOutOfMemory) ? SYDELTA_E_OOM : SYDELTA_E_KERNEL;                 \
+            return ::sydelta::fail(code_, "%s: %s (%s:%d)", #expr, hipGetErrorString(e_), __FILE__,     \
+                                   __LINE__);                                                           \
+        }                                                                                               \
+    } while (0)

@@ -135,6 +135,22 @@ struct ApplyPiece {
 };
 hipError_t launch_apply(const ApplyPiece* d_pieces, uint64_t npieces, const uint8_t* d_basis, const uint8_t* d_lit,
                         uint8_t* d_out, hipStream_t s, Profiler* prof);
+// Delta JSON on the device (K7).  A piece is a Copy op (a = offset, b = size) or a
+// chunk of <= kJsonChunk literal bytes of a Data op (lit[src, src+len)).
+constexpr uint32_t kJsonData = 1, kJsonFirst = 2, kJsonLast = 4, kJsonSep = 8;
+constexpr uint32_t kJsonChunk = 16384;
+constexpr uint32_t kJsonStage = 4 * kJsonChunk + 32;  // LDS text staging per chunk
+struct JsonPiece {
+    uint64_t src;
+    uint64_t a, b;
+    uint32_t len;
+    uint32_t flags;
+};
+hipError_t launch_json_len(const JsonPiece* d_pieces, uint64_t npieces, const uint8_t* d_lit, uint64_t* d_len,
+                           hipStream_t s, Profiler* prof);
+hipError_t launch_json_write(const JsonPiece* d_pieces, uint64_t npieces, const uint8_t* d_lit,
+                             const uint64_t* d_off, uint64_t base, uint8_t* d_out, hipStream_t s, Profiler* prof);
+hipError_t launch_exclusive_sum_u64(const uint64_t* d_in, uint64_t* d_out, uint64_t n, hipStream_t s);
 hipError_t launch_synth_fill(uint8_t* d_buf, uint64_t len, uint64_t seed, hipStream_t s, uint64_t first = 0);
 hipError_t launch_synth_edit_blocks(uint8_t* d_dst, uint64_t len, uint64_t bs, uint64_t first, uint64_t seed,
                                     uint32_t rate_ppm, hipStream_t s);

@@ -23,6 +23,7 @@
 #include <hipcub/hipcub.hpp>
 
 #include <algorithm>
+#include <mutex>
 
 namespace sydelta {
 
@@ -1433,6 +1434,182 @@ __global__ __launch_bounds__(256) void k_apply(const ApplyPiece* __restrict__ pi
 }
 
 // ===========================================================================
+// K7: serde_json text of a Delta on the device (wire format, sydelta_wire.cpp)
+// ===========================================================================
+// Pieces in op order: a Copy op, or a <= 16 KiB chunk of a Data op's literal bytes.
+// Pass 1 sizes every piece's text, an exclusive scan places them, pass 2 writes them.
+// A Data chunk is formatted into LDS (<= 4 characters per byte) at the 16-byte phase of
+// its destination, then leaves with aligned 16-byte stores; the partial granules at its
+// two ends are written byte by byte, so neighbouring pieces never race.
+__device__ __forceinline__ uint32_t dec_digits(uint64_t v) {
+    uint32_t n = 1;
+    while (v >= 10) { v /= 10; ++n; }
+    return n;
+}
+__device__ __forceinline__ uint32_t byte_digits(uint32_t v) { return v >= 100 ? 3u : (v >= 10 ? 2u : 1u); }
+
+__device__ __forceinline__ uint32_t json_copy_len(const JsonPiece& P) {
+    return (P.flags & kJsonSep ? 1u : 0u) + 28u + dec_digits(P.a) + dec_digits(P.b);  // {"Copy":{"offset":,"size":}}
+}
+
+__global__ __launch_bounds__(256) void k_json_len(const JsonPiece* __restrict__ pieces, uint64_t npieces,
+                                                  const uint8_t* __restrict__ lit, uint64_t* __restrict__ len) {
+    // one workgroup per piece; Copy pieces are sized by thread 0
+    __shared__ uint32_t red[4];
+    const JsonPiece P = pieces[blockIdx.x];
+    if (!(P.flags & kJsonData)) {
+        if (threadIdx.x == 0) len[blockIdx.x] = json_copy_len(P);
+        return;
+    }
+    uint32_t c = 0;
+    // 16 bytes per thread per step where the run allows it, bytes at the ragged ends
+    const uint64_t a0 = P.src, a1 = P.src + P.len;
+    const uint64_t v0 = (a0 + 15) & ~15ull, v1 = a1 & ~15ull;
+    if (v0 < v1) {
+        for (uint64_t q = v0 + 16ull * threadIdx.x; q < v1; q += 16ull * blockDim.x) {
+            const uint4 v = *(const uint4*)(lit + q);
+            const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+            for (int k = 0; k < 16; ++k) c += byte_digits((w[k >> 2] >> (8 * (k & 3))) & 0xFF);
+        }
+        for (uint64_t q = a0 + threadIdx.x; q < v0; q += blockDim.x) c += byte_digits(lit[q]);
+        for (uint64_t q = v1 + threadIdx.x; q < a1; q += blockDim.x) c += byte_digits(lit[q]);
+    } else {
+        for (uint64_t q = a0 + threadIdx.x; q < a1; q += blockDim.x) c += byte_digits(lit[q]);
+    }
+    c = wave_sum32_dpp(c);
+    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = c;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        uint32_t t = red[0] + red[1] + red[2] + red[3];
+        t += P.len ? P.len - 1 : 0;                     // commas between bytes of the chunk
+        if (!(P.flags & kJsonLast) && P.len) t += 1;    // comma before the next chunk's first byte
+        if (P.flags & kJsonFirst) t += 9;               // {"Data":[
+        if (P.flags & kJsonLast) t += 2;                // ]}
+        if (P.flags & kJsonSep) t += 1;                 // , before the op
+        len[blockIdx.x] = t;
+    }
+}
+
+__device__ __forceinline__ uint32_t put_dec(char* p, uint64_t v) {
+    char t[20];
+    uint32_t n = 0;
+    do { t[n++] = (char)('0' + v % 10); v /= 10; } while (v);
+    for (uint32_t i = 0; i < n; ++i) p[i] = t[n - 1 - i];
+    return n;
+}
+
+__global__ __launch_bounds__(256) void k_json_write(const JsonPiece* __restrict__ pieces,
+                                                    const uint8_t* __restrict__ lit, const uint64_t* __restrict__ off,
+                                                    uint64_t base, uint8_t* __restrict__ out) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char js[];  // text staging, kJsonStage bytes
+    __shared__ uint32_t wsum[4];
+    const JsonPiece P = pieces[blockIdx.x];
+    const uint64_t dst = base + off[blockIdx.x];
+    if (!(P.flags & kJsonData)) {
+        if (threadIdx.x == 0) {
+            char t[72];
+            uint32_t k = 0;
+            if (P.flags & kJsonSep) t[k++] = ',';
+            const char* h = "{\"Copy\":{\"offset\":";
+            for (uint32_t i = 0; h[i]; ++i) t[k++] = h[i];
+            k += put_dec(t + k, P.a);
+            const char* m = ",\"size\":";
+            for (uint32_t i = 0; m[i]; ++i) t[k++] = m[i];
+            k += put_dec(t + k, P.b);
+            t[k++] = '}';
+            t[k++] = '}';
+            for (uint32_t i = 0; i < k; ++i) out[dst + i] = (uint8_t)t[i];
+        }
+        return;
+    }
+    // thread t formats bytes [t*per, (t+1)*per) of the chunk (per = 64 for a full
+    // chunk), read as dwords where aligned
+    const uint32_t per = (P.len + blockDim.x - 1) / blockDim.x;
+    const uint32_t b0 = min(P.len, threadIdx.x * per), b1 = min(P.len, b0 + per);
+    const uint8_t* lp = lit + P.src;
+    const bool dw = (((uintptr_t)lp + b0) & 3) == 0 && (per & 3) == 0;
+    auto byte_at = [&](uint32_t i) -> uint32_t { return lp[i]; };
+    uint32_t mine = 0;
+    if (dw) {
+        for (uint32_t i = b0; i < b1; i += 4) {
+            const uint32_t x = (i + 4 <= b1) ? *(const uint32_t*)(lp + i) : 0u;
+            if (i + 4 <= b1) {
+#pragma unroll
+                for (int k = 0; k < 4; ++k) mine += byte_digits((x >> (8 * k)) & 0xFF) + 1;
+            } else {
+                for (uint32_t j = i; j < b1; ++j) mine += byte_digits(byte_at(j)) + 1;
+            }
+        }
+    } else {
+        for (uint32_t i = b0; i < b1; ++i) mine += byte_digits(byte_at(i)) + 1;  // digits + comma
+    }
+    // exclusive scan of `mine` over the workgroup
+    const uint32_t lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    uint32_t inc = mine;
+#pragma unroll
+    for (int m = 1; m < 64; m <<= 1) {
+        const uint32_t o = (uint32_t)__shfl_up((int)inc, m, 64);
+        if (lane >= (uint32_t)m) inc += o;
+    }
+    if (lane == 63) wsum[wid] = inc;
+    __syncthreads();
+    uint32_t pre = inc - mine;
+    for (uint32_t w = 0; w < wid; ++w) pre += wsum[w];
+    const uint32_t ph = (uint32_t)(dst & 15);  // LDS byte k <-> global byte (dst & ~15) + k
+    uint32_t head = ph;
+    if (P.flags & kJsonSep) head += 1;
+    if (P.flags & kJsonFirst) head += 9;
+    if (threadIdx.x == 0) {
+        uint32_t k = ph;
+        if (P.flags & kJsonSep) js[k++] = ',';
+        if (P.flags & kJsonFirst) {
+            const char* h = "{\"Data\":[";
+            for (uint32_t i = 0; h[i]; ++i) js[k++] = h[i];
+        }
+    }
+    uint32_t k = head + pre;
+    auto emit = [&](uint32_t v) {
+        if (v >= 100) { js[k++] = (unsigned char)('0' + v / 100); js[k++] = (unsigned char)('0' + (v / 10) % 10); }
+        else if (v >= 10) js[k++] = (unsigned char)('0' + v / 10);
+        js[k++] = (unsigned char)('0' + v % 10);
+        js[k++] = ',';
+    };
+    if (dw) {
+        for (uint32_t i = b0; i < b1; i += 4) {
+            if (i + 4 <= b1) {
+                const uint32_t x = *(const uint32_t*)(lp + i);
+#pragma unroll
+                for (int q = 0; q < 4; ++q) emit((x >> (8 * q)) & 0xFF);
+            } else {
+                for (uint32_t j = i; j < b1; ++j) emit(byte_at(j));
+            }
+        }
+    } else {
+        for (uint32_t i = b0; i < b1; ++i) emit(byte_at(i));
+    }
+    const uint32_t body = wsum[0] + wsum[1] + wsum[2] + wsum[3];  // every byte with a comma
+    uint32_t end = head + body;
+    if ((P.flags & kJsonLast) && P.len) end -= 1;  // no comma after the op's last byte
+    if (P.flags & kJsonLast) {
+        __syncthreads();
+        if (threadIdx.x == 0) { js[end] = ']'; js[end + 1] = '}'; }
+        end += 2;
+    }
+    __syncthreads();
+    // LDS [ph, end) -> out [dst, dst + end - ph)
+    uint8_t* g = out + (dst & ~15ull);
+    for (uint32_t c = 16 * threadIdx.x; c < end; c += 16 * blockDim.x) {
+        if (c >= ph && c + 16 <= end) {
+            *(uint4*)(g + c) = *(const uint4*)(js + c);
+        } else {
+            const uint32_t lo = max(c, ph), hi = min(c + 16, end);
+            for (uint32_t x = lo; x < hi; ++x) g[x] = js[x];
+        }
+    }
+}
+
+// ===========================================================================
 // Synthetic inputs (bench)
 // ===========================================================================
 // bytes [8*w0, 8*w0 + len) of the stream
@@ -1733,6 +1910,45 @@ hipError_t launch_apply(const ApplyPiece* d_pieces, uint64_t npieces, const uint
         hipLaunchKernelGGL(k_apply, dim3((unsigned)cnt), dim3(256), 0, s, d_pieces + p0, d_basis, d_lit, d_out);
     }
     return hipGetLastError();
+}
+
+hipError_t launch_json_len(const JsonPiece* d_pieces, uint64_t npieces, const uint8_t* d_lit, uint64_t* d_len,
+                           hipStream_t s, Profiler* prof) {
+    if (!npieces) return hipSuccess;
+    if (npieces > 0x7FFFFFFFull) return hipErrorInvalidValue;
+    ProfScope ps(prof, s, "k_json_len");
+    hipLaunchKernelGGL(k_json_len, dim3((unsigned)npieces), dim3(256), 0, s, d_pieces, npieces, d_lit, d_len);
+    return hipGetLastError();
+}
+
+hipError_t launch_json_write(const JsonPiece* d_pieces, uint64_t npieces, const uint8_t* d_lit,
+                             const uint64_t* d_off, uint64_t base, uint8_t* d_out, hipStream_t s, Profiler* prof) {
+    if (!npieces) return hipSuccess;
+    if (npieces > 0x7FFFFFFFull) return hipErrorInvalidValue;
+    static std::once_flag once;
+    static hipError_t attr = hipSuccess;
+    std::call_once(once, [] {
+        attr = hipFuncSetAttribute((const void*)k_json_write, hipFuncAttributeMaxDynamicSharedMemorySize, kJsonStage);
+    });
+    if (attr != hipSuccess) return attr;
+    ProfScope ps(prof, s, "k_json_write");
+    hipLaunchKernelGGL(k_json_write, dim3((unsigned)npieces), dim3(256), kJsonStage, s, d_pieces, d_lit, d_off, base,
+                       d_out);
+    return hipGetLastError();
+}
+
+// 64-bit exclusive sum (the text of a multi-GiB literal run overflows 32-bit offsets;
+// hipcub accumulates in the input type, so the input is 64-bit too).
+hipError_t launch_exclusive_sum_u64(const uint64_t* d_in, uint64_t* d_out, uint64_t n, hipStream_t s) {
+    if (!n) return hipSuccess;
+    size_t tmp = 0;
+    hipError_t e;
+    if ((e = hipcub::DeviceScan::ExclusiveSum(nullptr, tmp, d_in, d_out, (int)n, s))) return e;
+    void* d_t = nullptr;
+    if ((e = hipMallocAsync(&d_t, tmp ? tmp : 16, s))) return e;
+    e = hipcub::DeviceScan::ExclusiveSum(d_t, tmp, d_in, d_out, (int)n, s);
+    (void)hipFreeAsync(d_t, s);
+    return e;
 }
 
 hipError_t launch_synth_fill(uint8_t* d_buf, uint64_t len, uint64_t seed, hipStream_t s, uint64_t first) {

@@ -1,0 +1,465 @@
+// sydelta_wire.cpp — the delta path's wire formats.
+//
+// sy moves both sides of the delta as JSON (serde_json, compact):
+//   * `sy-remote checksums` prints serde_json::to_string(&Vec<BlockChecksum>)
+//     (src/bin/sy-remote.rs:146-147); the sender parses it (src/transport/ssh.rs:967-973);
+//   * the sender serialises the Delta (ssh.rs:1003-1008), zstd-compresses it and the
+//     receiver parses it back before apply_delta (sy-remote.rs:153-175).
+// serde's derive output for these types is fixed by their declarations:
+//   BlockChecksum {index, offset, size, weak, strong}            checksum.rs:10-21
+//   Delta {ops, source_size, block_size}                          generator.rs:19-25
+//   DeltaOp::Copy{offset, size} -> {"Copy":{"offset":O,"size":S}}
+//   DeltaOp::Data(Vec<u8>)      -> {"Data":[b0,b1,...]}           generator.rs:10-15
+// integers in decimal, no whitespace.  Host writers and parsers for both, and the
+// device writer of a Delta whose literal bytes are in HBM (sydelta_kernels.hip K7:
+// literal runs dominate the text, ~3.6 characters per byte).
+#include <errno.h>
+#include <stdio.h>
+#include <string.h>
+
+#include <stdlib.h>
+
+#include <algorithm>
+#include <memory>
+
+#include "sydelta_host.hpp"
+#include "sydelta_internal.hpp"
+
+using namespace sydelta;
+
+namespace {
+// decimal text of 0..255 followed by ','; length in kByteLen
+struct ByteText {
+    char s[256][4];
+    uint8_t len[256];
+    ByteText() {
+        for (int b = 0; b < 256; ++b) {
+            len[b] = (uint8_t)snprintf(s[b], 4, "%d", b);
+        }
+    }
+};
+const ByteText kBytes;
+
+inline char* put_u64(char* p, uint64_t v) {
+    char t[20];
+    int n = 0;
+    do {
+        t[n++] = (char)('0' + v % 10);
+        v /= 10;
+    } while (v);
+    while (n) *p++ = t[--n];
+    return p;
+}
+inline void put(std::string& o, const char* lit) { o.append(lit); }
+inline void put_num(std::string& o, uint64_t v) {
+    char t[24];
+    o.append(t, put_u64(t, v) - t);
+}
+
+// Minimal strict-enough JSON reader for the two schemas above (whitespace allowed,
+// unknown object keys skipped like serde's default, integers only).
+struct Reader {
+    const char* p;
+    const char* e;
+    std::string err;
+    void ws() {
+        while (p < e && (*p == ' ' || *p == '\n' || *p == '\r' || *p == '\t')) ++p;
+    }
+    bool eat(char c) {
+        ws();
+        if (p < e && *p == c) { ++p; return true; }
+        return false;
+    }
+    bool expect(char c) {
+        if (eat(c)) return true;
+        err = std::string("expected '") + c + "' at byte " + std::to_string(pos());
+        return false;
+    }
+    size_t pos() const { return (size_t)(p - b0); }
+    const char* b0;
+    bool key(std::string& k) {
+        ws();
+        if (p >= e || *p != '"') { err = "expected a key at byte " + std::to_string(pos()); return false; }
+        ++p;
+        const char* s = p;
+        while (p < e && *p != '"') {
+            if (*p == '\\') { err = "escaped keys are not used by these types"; return false; }
+            ++p;
+        }
+        if (p >= e) { err = "unterminated key"; return false; }
+        k.assign(s, p - s);
+        ++p;
+        return expect(':');
+    }
+    bool u64(uint64_t& v) {
+        ws();
+        if (p >= e || *p < '0' || *p > '9') { err = "expected an unsigned integer at byte " + std::to_string(pos()); return false; }
+        v = 0;
+        while (p < e && *p >= '0' && *p <= '9') {
+            const uint64_t d = (uint64_t)(*p - '0');
+            if (v > (UINT64_MAX - d) / 10) { err = "integer overflow at byte " + std::to_string(pos()); return false; }
+            v = v * 10 + d;
+            ++p;
+        }
+        return true;
+    }
+    // skip any JSON value (for unknown keys)
+    bool skip() {
+        ws();
+        if (p >= e) { err = "unexpected end"; return false; }
+        if (*p == '{' || *p == '[') {
+            const char open = *p, close = open == '{' ? '}' : ']';
+            int depth = 0;
+            bool str = false;
+            for (; p < e; ++p) {
+                if (str) {
+                    if (*p == '\\') ++p;
+                    else if (*p == '"') str = false;
+                    continue;
+                }
+                if (*p == '"') str = true;
+                else if (*p == open) ++depth;
+                else if (*p == close && --depth == 0) { ++p; return true; }
+            }
+            err = "unterminated value";
+            return false;
+        }
+        if (*p == '"') {
+            for (++p; p < e; ++p) {
+                if (*p == '\\') ++p;
+                else if (*p == '"') { ++p; return true; }
+            }
+            err = "unterminated string";
+            return false;
+        }
+        while (p < e && *p != ',' && *p != '}' && *p != ']') ++p;
+        return true;
+    }
+};
+struct DevBuf_wire {
+    void* p = nullptr;
+    hipStream_t s = nullptr;
+    ~DevBuf_wire() {
+        if (p) (void)hipFreeAsync(p, s);
+    }
+};
+}  // namespace
+
+// serde_json::to_string(&Vec<BlockChecksum>)  (sy-remote.rs:147, without println's '\n')
+extern "C" uint64_t sydelta_checksums_to_json(const sydelta_block_checksum* sigs, uint64_t n, char* buf,
+                                              uint64_t cap) {
+    std::string o;
+    o.reserve(n * 96 + 2);
+    o.push_back('[');
+    for (uint64_t i = 0; i < n; ++i) {
+        if (i) o.push_back(',');
+        put(o, "{\"index\":");
+        put_num(o, sigs[i].index);
+        put(o, ",\"offset\":");
+        put_num(o, sigs[i].offset);
+        put(o, ",\"size\":");
+        put_num(o, sigs[i].size);
+        put(o, ",\"weak\":");
+        put_num(o, sigs[i].weak);
+        put(o, ",\"strong\":");
+        put_num(o, sigs[i].strong);
+        o.push_back('}');
+    }
+    o.push_back(']');
+    if (buf && cap >= o.size()) memcpy(buf, o.data(), o.size());
+    return o.size();
+}
+
+// serde_json::from_str::<Vec<BlockChecksum>>  (ssh.rs:967-973)
+extern "C" int sydelta_checksums_from_json(const char* json, uint64_t len, sydelta_block_checksum** out,
+                                           uint64_t* n_out) {
+    if (!json || !out || !n_out) return fail(SYDELTA_E_INVAL, "NULL argument");
+    *out = nullptr;
+    *n_out = 0;
+    Reader r{json, json + len, {}, json};
+    std::vector<sydelta_block_checksum> v;
+    auto bad = [&]() { return fail(SYDELTA_E_INVAL, "checksum JSON: %s", r.err.c_str()); };
+    if (!r.expect('[')) return bad();
+    if (!r.eat(']')) {
+        do {
+            if (!r.expect('{')) return bad();
+            sydelta_block_checksum c{};
+            unsigned seen = 0;
+            if (!r.eat('}')) {
+                do {
+                    std::string k;
+                    if (!r.key(k)) return bad();
+                    uint64_t x = 0;
+                    if (k == "index" || k == "offset" || k == "size" || k == "weak" || k == "strong") {
+                        if (!r.u64(x)) return bad();
+                        if (k == "index") { c.index = x; seen |= 1; }
+                        else if (k == "offset") { c.offset = x; seen |= 2; }
+                        else if (k == "size") { c.size = x; seen |= 4; }
+                        else if (k == "weak") {
+                            if (x > 0xFFFFFFFFull) { r.err = "weak out of u32 range"; return bad(); }
+                            c.weak = (uint32_t)x; seen |= 8;
+                        } else { c.strong = x; seen |= 16; }
+                    } else if (!r.skip()) {
+                        return bad();
+                    }
+                } while (r.eat(','));
+                if (!r.expect('}')) return bad();
+            }
+            if (seen != 31) { r.err = "missing field in checksum " + std::to_string(v.size()); return bad(); }
+            v.push_back(c);
+        } while (r.eat(','));
+        if (!r.expect(']')) return bad();
+    }
+    r.ws();
+    if (r.p != r.e) { r.err = "trailing characters"; return bad(); }
+    if (!v.empty()) {
+        *out = (sydelta_block_checksum*)malloc(v.size() * sizeof(sydelta_block_checksum));
+        if (!*out) return fail(SYDELTA_E_OOM, "out of memory");
+        memcpy(*out, v.data(), v.size() * sizeof(sydelta_block_checksum));
+    }
+    *n_out = v.size();
+    return SYDELTA_OK;
+}
+
+// serde_json::to_string(&Delta)  (ssh.rs:1003).  Literal bytes: the delta's own (host
+// entry points), or `lit` indexed by the Data ops' source offsets (device deltas).
+extern "C" int sydelta_delta_to_json(const sydelta_delta* d, const uint8_t* lit, uint64_t lit_len, char* buf,
+                                     uint64_t cap, uint64_t* out_len) {
+    if (!d || !out_len) return fail(SYDELTA_E_INVAL, "NULL argument");
+    const bool own = !lit;
+    if (own && d->lit_off.size() != d->ops.size())
+        return fail(SYDELTA_E_INVAL, "device delta: pass the source bytes as lit");
+    uint64_t total = 0;
+    std::string o;
+    // size first (cheap), then write straight into buf when it fits
+    auto op_len = [&](const sydelta_op& x, const uint8_t* bytes) -> uint64_t {
+        char t[24];
+        if (x.kind == SYDELTA_OP_COPY)
+            return 28 + (put_u64(t, x.a) - t) + (put_u64(t, x.b) - t);  // {"Copy":{"offset":,"size":}}
+        uint64_t L = 11 + (x.b ? x.b - 1 : 0);                           // {"Data":[]} + commas
+        for (uint64_t i = 0; i < x.b; ++i) L += kBytes.len[bytes[i]];
+        return L;
+    };
+    std::vector<const uint8_t*> src(d->ops.size(), nullptr);
+    for (size_t i = 0; i < d->ops.size(); ++i) {
+        const sydelta_op& x = d->ops[i];
+        if (x.kind == SYDELTA_OP_DATA) {
+            if (own) {
+                src[i] = d->lit.data() + d->lit_off[i];
+            } else {
+                if (x.a > lit_len || x.b > lit_len - x.a)
+                    return fail(SYDELTA_E_INVAL, "op %zu: Data outside the literal buffer", i);
+                src[i] = lit + x.a;
+            }
+        }
+    }
+    char t[24];
+    total = 8;  // {"ops":[
+    for (size_t i = 0; i < d->ops.size(); ++i) total += op_len(d->ops[i], src[i]) + (i ? 1 : 0);
+    total += 16 + (put_u64(t, d->source_size) - t) + 14 + (put_u64(t, d->block_size) - t) + 1;
+    *out_len = total;
+    if (!buf || cap < total) return SYDELTA_OK;
+    char* p = buf;
+    auto lit_s = [&](const char* s) { const size_t l = strlen(s); memcpy(p, s, l); p += l; };
+    lit_s("{\"ops\":[");
+    for (size_t i = 0; i < d->ops.size(); ++i) {
+        const sydelta_op& x = d->ops[i];
+        if (i) *p++ = ',';
+        if (x.kind == SYDELTA_OP_COPY) {
+            lit_s("{\"Copy\":{\"offset\":");
+            p = put_u64(p, x.a);
+            lit_s(",\"size\":");
+            p = put_u64(p, x.b);
+            lit_s("}}");
+        } else {
+            lit_s("{\"Data\":[");
+            const uint8_t* b = src[i];
+            for (uint64_t k = 0; k < x.b; ++k) {
+                if (k) *p++ = ',';
+                memcpy(p, kBytes.s[b[k]], 4);  // 4 bytes available: the text is followed by more text or "]}"
+                p += kBytes.len[b[k]];
+            }
+            lit_s("]}");
+        }
+    }
+    lit_s("],\"source_size\":");
+    p = put_u64(p, d->source_size);
+    lit_s(",\"block_size\":");
+    p = put_u64(p, d->block_size);
+    *p++ = '}';
+    return (uint64_t)(p - buf) == total ? SYDELTA_OK : fail(SYDELTA_E_KERNEL, "delta JSON length mismatch");
+}
+
+// serde_json::from_str::<Delta>  (sy-remote.rs:175): a host delta with its literal bytes,
+// ready for sydelta_apply_delta.
+extern "C" int sydelta_delta_from_json(const char* json, uint64_t len, sydelta_delta** out) {
+    if (!json || !out) return fail(SYDELTA_E_INVAL, "NULL argument");
+    *out = nullptr;
+    Reader r{json, json + len, {}, json};
+    std::unique_ptr<sydelta_delta> d(new sydelta_delta());
+    auto bad = [&]() { return fail(SYDELTA_E_INVAL, "delta JSON: %s", r.err.c_str()); };
+    unsigned seen = 0;
+    if (!r.expect('{')) return bad();
+    if (!r.eat('}')) {
+        do {
+            std::string k;
+            if (!r.key(k)) return bad();
+            if (k == "ops") {
+                seen |= 1;
+                if (!r.expect('[')) return bad();
+                if (!r.eat(']')) {
+                    do {
+                        if (!r.expect('{')) return bad();
+                        std::string tag;
+                        if (!r.key(tag)) return bad();
+                        if (tag == "Copy") {
+                            uint64_t off = 0, size = 0;
+                            unsigned f = 0;
+                            if (!r.expect('{')) return bad();
+                            if (!r.eat('}')) {
+                                do {
+                                    std::string ck;
+                                    if (!r.key(ck)) return bad();
+                                    if (ck == "offset") { if (!r.u64(off)) return bad(); f |= 1; }
+                                    else if (ck == "size") { if (!r.u64(size)) return bad(); f |= 2; }
+                                    else if (!r.skip()) return bad();
+                                } while (r.eat(','));
+                                if (!r.expect('}')) return bad();
+                            }
+                            if (f != 3) { r.err = "Copy needs offset and size"; return bad(); }
+                            d->ops.push_back({SYDELTA_OP_COPY, 0, off, size});
+                            d->lit_off.push_back(UINT64_MAX);
+                        } else if (tag == "Data") {
+                            const uint64_t start = d->lit.size();
+                            if (!r.expect('[')) return bad();
+                            if (!r.eat(']')) {
+                                do {
+                                    uint64_t b = 0;
+                                    if (!r.u64(b)) return bad();
+                                    if (b > 255) { r.err = "Data byte out of range"; return bad(); }
+                                    d->lit.push_back((uint8_t)b);
+                                } while (r.eat(','));
+                                if (!r.expect(']')) return bad();
+                            }
+                            d->ops.push_back({SYDELTA_OP_DATA, 0, start, d->lit.size() - start});
+                            d->lit_off.push_back(start);
+                        } else {
+                            r.err = "unknown DeltaOp variant " + tag;
+                            return bad();
+                        }
+                        if (!r.expect('}')) return bad();
+                    } while (r.eat(','));
+                    if (!r.expect(']')) return bad();
+                }
+            } else if (k == "source_size") {
+                if (!r.u64(d->source_size)) return bad();
+                seen |= 2;
+            } else if (k == "block_size") {
+                if (!r.u64(d->block_size)) return bad();
+                seen |= 4;
+            } else if (!r.skip()) {
+                return bad();
+            }
+        } while (r.eat(','));
+        if (!r.expect('}')) return bad();
+    }
+    r.ws();
+    if (r.p != r.e) { r.err = "trailing characters"; return bad(); }
+    if (seen != 7) { r.err = "missing field (ops, source_size, block_size)"; return bad(); }
+    finish_stats(d.get());
+    *out = d.release();
+    return SYDELTA_OK;
+}
+
+// serde_json::to_string(&Delta) on the device (K7): the literal runs (3.6 characters per
+// byte on average) are formatted in HBM; the op table goes up once, pinned.
+extern "C" int sydelta_delta_to_json_device(const sydelta_delta* d, const uint8_t* d_lit, uint64_t lit_len,
+                                            uint8_t* d_out, uint64_t out_cap, uint64_t* out_len, void* stream) {
+    if (!d || !out_len) return fail(SYDELTA_E_INVAL, "NULL argument");
+    int dev = 0;
+    (void)hipGetDevice(&dev);
+    if (int r = ensure_device(dev)) return r;
+    hipStream_t s = stream ? (hipStream_t)stream : thread_stream(dev);
+    struct Pinned {
+        JsonPiece* p = nullptr;
+        size_t cap = 0;
+        ~Pinned() { if (p) (void)hipHostFree(p); }
+    };
+    static thread_local Pinned pin;
+    size_t need = 0;
+    for (const sydelta_op& o : d->ops) need += o.kind == SYDELTA_OP_COPY ? 1 : std::max<uint64_t>(1, (o.b + kJsonChunk - 1) / kJsonChunk);
+    if (need > pin.cap) {
+        if (pin.p) { (void)hipHostFree(pin.p); pin.p = nullptr; pin.cap = 0; }
+        const size_t cap = std::max<size_t>(need, 1024) * 5 / 4;
+        HIP_TRY(hipHostMalloc((void**)&pin.p, cap * sizeof(JsonPiece), hipHostMallocDefault));
+        pin.cap = cap;
+    }
+    size_t np = 0;
+    for (size_t i = 0; i < d->ops.size(); ++i) {
+        const sydelta_op& o = d->ops[i];
+        const uint32_t sep = i ? kJsonSep : 0u;
+        if (o.kind == SYDELTA_OP_COPY) {
+            pin.p[np++] = {0, o.a, o.b, 0, sep};
+            continue;
+        }
+        if (o.a > lit_len || o.b > lit_len - o.a)
+            return fail(SYDELTA_E_INVAL, "op %zu: Data outside the literal buffer", i);
+        if (o.b && !d_lit) return fail(SYDELTA_E_INVAL, "NULL literal buffer");
+        const uint64_t nch = std::max<uint64_t>(1, (o.b + kJsonChunk - 1) / kJsonChunk);
+        for (uint64_t c = 0; c < nch; ++c) {
+            uint32_t fl = kJsonData;
+            if (c == 0) fl |= kJsonFirst | sep;
+            if (c + 1 == nch) fl |= kJsonLast;
+            const uint64_t off = c * kJsonChunk;
+            pin.p[np++] = {o.a + off, 0, 0, (uint32_t)std::min<uint64_t>(kJsonChunk, o.b - off), fl};
+        }
+    }
+    char tail[96];
+    char* t = tail;
+    t += sprintf(t, "],\"source_size\":%llu,\"block_size\":%llu}", (unsigned long long)d->source_size,
+                 (unsigned long long)d->block_size);
+    const uint64_t tail_len = (uint64_t)(t - tail);
+    static const char kHead[] = "{\"ops\":[";
+    uint64_t body = 0;
+    CallProf cp;
+    DevBuf_wire buf;
+    if (np) {
+        const size_t pb = (np * sizeof(JsonPiece) + 255) & ~(size_t)255;
+        const size_t lb = (np * 8 + 255) & ~(size_t)255;
+        HIP_TRY(hipMallocAsync(&buf.p, pb + lb + np * 8, s));
+        buf.s = s;
+        JsonPiece* d_pieces = (JsonPiece*)buf.p;
+        uint64_t* d_len = (uint64_t*)((uint8_t*)buf.p + pb);
+        uint64_t* d_off = (uint64_t*)((uint8_t*)buf.p + pb + lb);
+        HIP_TRY(hipMemcpyAsync(d_pieces, pin.p, np * sizeof(JsonPiece), hipMemcpyHostToDevice, s));
+        HIP_TRY(launch_json_len(d_pieces, np, d_lit, d_len, s, cp.get()));
+        HIP_TRY(launch_exclusive_sum_u64(d_len, d_off, np, s));
+        uint64_t last_off = 0, last_len = 0;
+        HIP_TRY(hipMemcpyAsync(&last_off, d_off + np - 1, 8, hipMemcpyDeviceToHost, s));
+        HIP_TRY(hipMemcpyAsync(&last_len, d_len + np - 1, 8, hipMemcpyDeviceToHost, s));
+        HIP_TRY(hipStreamSynchronize(s));
+        body = last_off + last_len;
+        // the text of every op is bounded from both sides by its byte count; a body
+        // outside the bounds means a sizing fault: never write with it
+        uint64_t lo = 0, hi = 0;
+        for (size_t i = 0; i < d->ops.size(); ++i) {
+            const sydelta_op& o = d->ops[i];
+            const uint64_t sep = i ? 1 : 0;
+            if (o.kind == SYDELTA_OP_COPY) { lo += sep + 30; hi += sep + 28 + 40; }
+            else { lo += sep + 11 + (o.b ? 2 * o.b - 1 : 0); hi += sep + 11 + (o.b ? 4 * o.b - 1 : 0); }
+        }
+        if (body < lo || body > hi)
+            return fail(SYDELTA_E_KERNEL, "delta JSON sizing out of bounds (%llu not in [%llu, %llu])",
+                        (unsigned long long)body, (unsigned long long)lo, (unsigned long long)hi);
+        *out_len = 8 + body + tail_len;
+        if (d_out && out_cap >= *out_len)
+            HIP_TRY(launch_json_write(d_pieces, np, d_lit, d_off, 8, d_out, s, cp.get()));
+    }
+    *out_len = 8 + body + tail_len;
+    if (d_out && out_cap >= *out_len) {
+        HIP_TRY(hipMemcpyAsync(d_out, kHead, 8, hipMemcpyHostToDevice, s));
+        HIP_TRY(hipMemcpyAsync(d_out + 8 + body, tail, tail_len, hipMemcpyHostToDevice, s));
+    }
+    HIP_TRY(hipStreamSynchronize(s));  // pinned piece table and host strings are reused / go away
+    return SYDELTA_OK;
+}
