@@ -50,7 +50,7 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=2)
-    ap.add_argument("--workload", default="c3", choices=["c3", "c2", "c4", "c5", "apply", "json"])
+    ap.add_argument("--workload", default="c3", choices=["c3", "c2", "c4", "c5", "apply", "json", "local"])
     ap.add_argument("--size-gib", type=float, default=None,
                     help="bytes per rank: c2/c3 basis and source (default 4), c5 chunk (default 8)")
     ap.add_argument("--block-size", type=int, default=None, help="default 4096 (c5: 8192)")
@@ -64,11 +64,11 @@ def parse():
     ap.add_argument("--no-host-inclusive", action="store_true")
     a = ap.parse_args()
     if a.size_gib is None:
-        a.size_gib = 8.0 if a.workload in ("c5", "apply") else 4.0
+        a.size_gib = 8.0 if a.workload in ("c5", "apply", "local") else 4.0
     if a.block_size is None:
-        a.block_size = 8192 if a.workload in ("c5", "apply") else 4096
+        a.block_size = {"c5": 8192, "apply": 8192, "local": 65536}.get(a.workload, 4096)
     if a.edit_ppm is None:
-        a.edit_ppm = 10000 if a.workload in ("c5", "apply") else 50000
+        a.edit_ppm = 10000 if a.workload in ("c5", "apply", "local") else 50000
     return a
 
 
@@ -249,6 +249,7 @@ def main():
     import sy_amd.device as dev
     import ctypes
 
+    from sy_amd import _lib
     from sy_amd._lib import check, lib
 
     bs = args.block_size
@@ -293,6 +294,14 @@ def main():
         apply_d = dev.match(idx, new, length=n)
         idx.close()
         apply_out = torch.empty(n + 16, dtype=torch.uint8, device="cuda")
+    if args.workload == "local":
+        # local transport: the new file (source) against the existing one (dest), both
+        # resident; 1% of 64 KiB blocks carry one substituted byte.
+        dev.synth_fill_range(basis, 0, 0x5E1D0007)
+        new = torch.empty(n, dtype=torch.uint8, device="cuda")
+        dev.synth_fill_range(new, 0, 0x5E1D0007)
+        dev.synth_mutate_blocks(new, new, 0, bs, 0x5E1D0008, args.edit_ppm)
+        local_flags = torch.empty(n // bs, dtype=torch.uint8, device="cuda")
     if args.workload == "c5":
         # BASELINE config 5: one file of world * n bytes; this rank owns basis bytes
         # [rank*n, (rank+1)*n) and window starts [rank*n, (rank+1)*n) of the source
@@ -338,6 +347,14 @@ def main():
         if args.workload == "apply":
             _, st = dev.apply_device(basis, apply_d, new, out=apply_out, stream=stream)
             return st
+        if args.workload == "local":
+            # the local delta decision (ratio.rs) then the block compare (local.rs)
+            r = dev.estimate_change_ratio(new, basis, bs, stream=stream)
+            st = _lib.BlockCompareStatsC()
+            check(lib.sydelta_block_compare_device(local, new.data_ptr(), n, basis.data_ptr(), n, bs,
+                                                   local_flags.data_ptr(), int(stream.cuda_stream), ctypes.byref(st)))
+            return {"changed_blocks": st.changed_blocks, "literal_bytes": st.literal_bytes,
+                    "change_ratio": r["change_ratio"], "use_delta": r["use_delta"]}
         if args.workload == "json":
             ln = ctypes.c_uint64()
             check(lib.sydelta_delta_to_json_device(json_h, new.data_ptr(), n, json_out.data_ptr(), json_out.numel(),
@@ -396,6 +413,8 @@ def main():
         bytes_per_step = 2 * n
     elif args.workload == "apply":
         bytes_per_step = n  # reconstructed bytes
+    elif args.workload == "local":
+        bytes_per_step = 2 * n  # both files compared
     elif args.workload == "json":
         bytes_per_step = n  # delta source bytes covered by the text
     else:
@@ -412,7 +431,8 @@ def main():
     algo_step = {"k_scan": src_bytes, "k_scan_lds": src_bytes, "k_sig_fast": nb_bytes if args.workload == "c3" else n,
                  "k_sig_batch": n, "k_sig_wave": n, "k_probe": src_bytes,
                  "k_apply": 2 * n,  # apply: every output byte read once and written once
-                 "k_json_write": n}  # json: every literal byte read once (text written: ~3.6x)
+                 "k_json_write": n,  # json: every literal byte read once (text written: ~3.6x)
+                 "k_block_cmp": 2 * n}  # local: both files read once
     dom = max(prof, key=lambda k: prof[k]["ms"]) if prof else None
     roof = None
     if dom and dom in algo_step:
@@ -447,8 +467,8 @@ def main():
             "scaling": "strong" if args.workload == "c4" else "weak",
             "vs_baseline": None,
             "dtype": "u8",
-            "data": ("synthetic (counter-based splitmix64 bytes; one substituted byte in 1% of 8 KiB blocks)"
-                     if args.workload in ("c5", "apply") else
+            "data": (f"synthetic (counter-based splitmix64 bytes; one substituted byte in {args.edit_ppm / 1e4:g}% of {bs // 1024} KiB blocks)"
+                     if args.workload in ("c5", "apply", "local") else
                      "synthetic (counter-based splitmix64 bytes; Bernoulli byte substitutions)"),
             "config": {
                 "workload": {
@@ -460,6 +480,8 @@ def main():
                           f"one substituted byte; signature + all-gather + index + chunk match, chunk-sharded",
                     "apply": f"apply_delta on the device: {n / GIB:.0f} GiB reconstructed from a bs {bs} delta "
                              f"({args.edit_ppm / 1e4:g}% of blocks edited), per rank",
+                    "local": f"local transport: change-ratio sample + block compare of two {n / GIB:.0f} GiB files, "
+                             f"bs {bs}, {args.edit_ppm / 1e4:g}% of blocks edited",
                     "json": f"serde_json text of the C3 delta ({n / GIB:.0f} GiB source, one literal run) on the device",
                 }[args.workload],
                 "block_size": bs,

@@ -281,6 +281,36 @@ int sydelta_delta_to_json_device(const sydelta_delta *d, const uint8_t *d_lit, u
 int sydelta_delta_from_json(const char *json, uint64_t len, sydelta_delta **out);
 
 /* ---------------------------------------------------------------------------
+ * Local transport, files already in device memory.
+ * ------------------------------------------------------------------------- */
+typedef struct sydelta_block_compare_stats {
+    uint64_t blocks;          /* ceil(src_len / block_size) */
+    uint64_t changed_blocks;  /* local.rs changed_blocks */
+    uint64_t literal_bytes;   /* bytes of the changed blocks */
+    uint64_t bytes_written;   /* src_len */
+} sydelta_block_compare_stats;
+/* The block-compare loop of src/transport/local.rs:541-619 (:682-760): d_changed[k] = 1
+ * iff block k of the source (length min(bs, src_len - k*bs)) differs from block k of the
+ * destination in length or bytes.  d_changed holds ceil(src_len / block_size) bytes. */
+int sydelta_block_compare_device(int device, const uint8_t *d_src, uint64_t src_len, const uint8_t *d_dst,
+                                 uint64_t dst_len, uint64_t block_size, uint8_t *d_changed, void *stream,
+                                 sydelta_block_compare_stats *out);
+/* ratio.rs:11-45 `ChangeRatioResult`. */
+typedef struct sydelta_change_ratio {
+    double change_ratio;
+    uint64_t blocks_sampled;
+    uint64_t blocks_changed;
+    int32_t use_delta;
+    int32_t reserved;
+    double threshold;
+} sydelta_change_ratio;
+/* ratio.rs:78-192 `estimate_change_ratio` on device-resident bytes (sample_count < 0:
+ * 20, threshold < 0: 0.75, the defaults of :85-86). */
+int sydelta_estimate_change_ratio_device(int device, const uint8_t *d_src, uint64_t src_len, const uint8_t *d_dst,
+                                         uint64_t dst_len, uint64_t block_size, int64_t sample_count,
+                                         double threshold, void *stream, sydelta_change_ratio *out);
+
+/* ---------------------------------------------------------------------------
  * Measurement support (used by bench.py; not part of the reference API).
  * ------------------------------------------------------------------------- */
 /* When on, the library records a HIP event pair around every kernel it

@@ -430,3 +430,54 @@ def C() -> _C:
 
 def ops_from_arrays(kind, a, b):
     return [("C" if int(k) == 0 else "D", int(x), int(y)) for k, x, y in zip(kind, a, b)]
+
+
+# --------------------------------------------------------------------------
+# Local path: block compare + change-ratio sampling
+# --------------------------------------------------------------------------
+def py_block_compare(src: bytes, dst: bytes, bs: int):
+    """local.rs:541-619 (and :682-760): read block k of both files (full reads of a
+    regular file: src_read = min(bs, |src| - k*bs), dst_read likewise, 0 past the end);
+    a block matches iff the reads are equal in length and content.  Returns
+    (changed flags per source block, changed_blocks, literal_bytes, bytes_written)."""
+    flags = []
+    literal = 0
+    off = 0
+    while off < len(src):
+        s = src[off:off + bs]
+        d = dst[off:off + bs]
+        changed = not (len(s) == len(d) and s == d)
+        flags.append(1 if changed else 0)
+        if changed:
+            literal += len(s)
+        off += len(s)
+    return flags, sum(flags), literal, len(src)
+
+
+def py_estimate_change_ratio(src: bytes, dst: bytes, bs: int, sample_count=None, threshold=None):
+    """ratio.rs:78-192 `estimate_change_ratio` on in-memory bytes (regular-file reads
+    are full).  Returns (change_ratio, blocks_sampled, blocks_changed, use_delta,
+    threshold)."""
+    sample_count = 20 if sample_count is None else sample_count
+    threshold = 0.75 if threshold is None else threshold
+    ssize, dsize = len(src), len(dst)
+    total_blocks = -(-dsize // bs)
+    sample_count = min(sample_count, total_blocks)
+    size_diff = abs(ssize - dsize) / dsize if dsize > 0 else 1.0
+    if size_diff > 0.5:
+        r = min(size_diff, 1.0)
+        return r, 0, 0, r <= threshold, threshold
+    step = total_blocks // (sample_count - 1) if sample_count > 1 else 0
+    pos = [min(i * step, max(total_blocks - 1, 0)) if sample_count > 1 else 0 for i in range(sample_count)]
+    changed = 0
+    for k in pos:
+        off = k * bs
+        s = src[off:off + bs]
+        d = dst[off:off + bs]
+        if len(s) != len(d):
+            changed += 1
+            continue
+        if py_xxh3(s) != py_xxh3(d):
+            changed += 1
+    ratio = changed / sample_count if sample_count > 0 else 0.0
+    return ratio, sample_count, changed, ratio <= threshold, threshold

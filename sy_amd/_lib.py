@@ -37,6 +37,17 @@ class MatchStatsC(ctypes.Structure):
                 ("copy_ops", ctypes.c_uint64), ("data_ops", ctypes.c_uint64), ("literal_bytes", ctypes.c_uint64)]
 
 
+class BlockCompareStatsC(ctypes.Structure):
+    _fields_ = [("blocks", ctypes.c_uint64), ("changed_blocks", ctypes.c_uint64), ("literal_bytes", ctypes.c_uint64),
+                ("bytes_written", ctypes.c_uint64)]
+
+
+class ChangeRatioC(ctypes.Structure):
+    _fields_ = [("change_ratio", ctypes.c_double), ("blocks_sampled", ctypes.c_uint64),
+                ("blocks_changed", ctypes.c_uint64), ("use_delta", ctypes.c_int32), ("reserved", ctypes.c_int32),
+                ("threshold", ctypes.c_double)]
+
+
 class DeltaStatsC(ctypes.Structure):
     _fields_ = [("operations_count", ctypes.c_uint64), ("literal_bytes", ctypes.c_uint64),
                 ("bytes_written", ctypes.c_uint64)]
@@ -95,6 +106,9 @@ SIGNATURES = [
     ("sydelta_delta_to_json", _i, [_vp, _vp, _u64, _vp, _u64, ctypes.POINTER(_u64)]),
     ("sydelta_delta_to_json_device", _i, [_vp, _vp, _u64, _vp, _u64, ctypes.POINTER(_u64), _vp]),
     ("sydelta_delta_from_json", _i, [_vp, _u64, _pp]),
+    ("sydelta_block_compare_device", _i, [_i, _vp, _u64, _vp, _u64, _u64, _vp, _vp, ctypes.POINTER(BlockCompareStatsC)]),
+    ("sydelta_estimate_change_ratio_device", _i, [_i, _vp, _u64, _vp, _u64, _u64, ctypes.c_int64, ctypes.c_double,
+                                                  _vp, ctypes.POINTER(ChangeRatioC)]),
     ("sydelta_set_profiling", None, [_i]),
     ("sydelta_profile_json", ctypes.c_size_t, [ctypes.c_char_p, ctypes.c_size_t, _i]),
     ("sydelta_synth_fill", _i, [_vp, _u64, _u64, _vp]),

@@ -151,6 +151,12 @@ hipError_t launch_json_len(const JsonPiece* d_pieces, uint64_t npieces, const ui
 hipError_t launch_json_write(const JsonPiece* d_pieces, uint64_t npieces, const uint8_t* d_lit,
                              const uint64_t* d_off, uint64_t base, uint8_t* d_out, hipStream_t s, Profiler* prof);
 hipError_t launch_exclusive_sum_u64(const uint64_t* d_in, uint64_t* d_out, uint64_t n, hipStream_t s);
+// Local path: changed[k] = block k of src differs from block k of dst (k < ceil(slen/bs)).
+hipError_t launch_block_cmp(const uint8_t* d_src, uint64_t slen, const uint8_t* d_dst, uint64_t dlen, uint64_t bs,
+                            uint8_t* d_changed, hipStream_t s, Profiler* prof);
+// out[i] = XXH3-64 of block pos[i] of buf (clipped at len, empty past the end).
+hipError_t launch_hash_blocks(const uint8_t* d_buf, uint64_t len, uint64_t bs, const uint64_t* d_pos, uint32_t count,
+                              uint64_t* d_out, hipStream_t s);
 hipError_t launch_synth_fill(uint8_t* d_buf, uint64_t len, uint64_t seed, hipStream_t s, uint64_t first = 0);
 hipError_t launch_synth_edit_blocks(uint8_t* d_dst, uint64_t len, uint64_t bs, uint64_t first, uint64_t seed,
                                     uint32_t rate_ppm, hipStream_t s);

@@ -1610,6 +1610,77 @@ __global__ __launch_bounds__(256) void k_json_write(const JsonPiece* __restrict_
 }
 
 // ===========================================================================
+// K8: local-path block compare and change-ratio sampling (local.rs, ratio.rs)
+// ===========================================================================
+// Block k of the source against block k of the destination (local.rs:549-570): the
+// reads match iff their lengths are equal and the bytes are equal.  One workgroup per
+// block; 16-byte loads when both blocks are 16-byte aligned.
+__global__ __launch_bounds__(256) void k_block_cmp(const uint8_t* __restrict__ src, uint64_t slen,
+                                                   const uint8_t* __restrict__ dst, uint64_t dlen, uint64_t bs,
+                                                   uint64_t nblocks, uint8_t* __restrict__ changed) {
+    for (uint64_t k = blockIdx.x; k < nblocks; k += gridDim.x) {
+        const uint64_t off = k * bs;
+        const uint64_t sl = min(bs, slen - off);
+        const uint64_t dl = dlen > off ? min(bs, dlen - off) : 0;
+        int diff = sl != dl;
+        if (!diff) {
+            const uint8_t* a = src + off;
+            const uint8_t* b = dst + off;
+            if ((((uintptr_t)a | (uintptr_t)b) & 15) == 0) {
+                // 16-byte nontemporal loads, 4 per buffer in flight per lane
+                const u32x4* A = (const u32x4*)a;
+                const u32x4* B = (const u32x4*)b;
+                const uint64_t nv = sl >> 4, st = blockDim.x;
+                uint32_t acc = 0;
+                uint64_t i = threadIdx.x;
+                for (; i + 3 * st < nv; i += 4 * st) {
+                    u32x4 x[4], y[4];
+#pragma unroll
+                    for (int u = 0; u < 4; ++u) x[u] = __builtin_nontemporal_load(A + i + u * st);
+#pragma unroll
+                    for (int u = 0; u < 4; ++u) y[u] = __builtin_nontemporal_load(B + i + u * st);
+#pragma unroll
+                    for (int u = 0; u < 4; ++u) {
+                        const u32x4 d = x[u] ^ y[u];
+                        acc |= d.x | d.y | d.z | d.w;
+                    }
+                }
+                for (; i < nv; i += st) {
+                    const u32x4 d = A[i] ^ B[i];
+                    acc |= d.x | d.y | d.z | d.w;
+                }
+                diff = acc != 0;
+                for (uint64_t j = (nv << 4) + threadIdx.x; j < sl && !diff; j += st) diff = a[j] != b[j];
+            } else {
+                for (uint64_t i = threadIdx.x; i < sl && !diff; i += blockDim.x) diff = a[i] != b[i];
+            }
+        }
+        diff = __syncthreads_or(diff);
+        if (threadIdx.x == 0) changed[k] = diff ? 1 : 0;
+    }
+}
+
+// XXH3-64 of block pos[i] of buf (length min(bs, len - off), 0 past the end): one
+// wave per sampled block (ratio.rs:160-165).
+__global__ __launch_bounds__(256) void k_hash_blocks(const uint8_t* __restrict__ buf, uint64_t len, uint64_t bs,
+                                                     const uint64_t* __restrict__ pos, uint32_t count,
+                                                     uint64_t* __restrict__ out) {
+    const uint32_t w = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+    if (w >= count) return;
+    const uint64_t off = pos[w] * bs;
+    const uint64_t n = len > off ? min(bs, len - off) : 0;
+    uint32_t wk;
+    uint64_t st;
+    if (n > 240) {
+        wave_hash_long(buf + off, n, wk, st);
+    } else {
+        st = 0;
+        if ((threadIdx.x & 63) == 0) st = xxh3_short(buf + off, n);
+    }
+    if ((threadIdx.x & 63) == 0) out[w] = st;
+}
+
+// ===========================================================================
 // Synthetic inputs (bench)
 // ===========================================================================
 // bytes [8*w0, 8*w0 + len) of the stream
@@ -1949,6 +2020,24 @@ hipError_t launch_exclusive_sum_u64(const uint64_t* d_in, uint64_t* d_out, uint6
     e = hipcub::DeviceScan::ExclusiveSum(d_t, tmp, d_in, d_out, (int)n, s);
     (void)hipFreeAsync(d_t, s);
     return e;
+}
+
+hipError_t launch_block_cmp(const uint8_t* d_src, uint64_t slen, const uint8_t* d_dst, uint64_t dlen, uint64_t bs,
+                            uint8_t* d_changed, hipStream_t s, Profiler* prof) {
+    const uint64_t nb = (slen + bs - 1) / bs;
+    if (!nb) return hipSuccess;
+    ProfScope ps(prof, s, "k_block_cmp");
+    hipLaunchKernelGGL(k_block_cmp, dim3((unsigned)std::min<uint64_t>(nb, 1u << 20)), dim3(256), 0, s, d_src, slen,
+                       d_dst, dlen, bs, nb, d_changed);
+    return hipGetLastError();
+}
+
+hipError_t launch_hash_blocks(const uint8_t* d_buf, uint64_t len, uint64_t bs, const uint64_t* d_pos, uint32_t count,
+                              uint64_t* d_out, hipStream_t s) {
+    if (!count) return hipSuccess;
+    hipLaunchKernelGGL(k_hash_blocks, dim3(grid_for((uint64_t)count * 64, 256)), dim3(256), 0, s, d_buf, len, bs, d_pos,
+                       count, d_out);
+    return hipGetLastError();
 }
 
 hipError_t launch_synth_fill(uint8_t* d_buf, uint64_t len, uint64_t seed, hipStream_t s, uint64_t first) {

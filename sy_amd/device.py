@@ -268,6 +268,31 @@ def apply_device(basis: torch.Tensor, delta: DeviceDelta, lit: torch.Tensor, out
     return out[:total], {f: int(getattr(st, f)) for f, _ in _lib.DeltaStatsC._fields_}
 
 
+def block_compare(src: torch.Tensor, dst: torch.Tensor, block_size: int, stream=None):
+    """The local transport's block-compare loop (local.rs:541-619) on device bytes.
+    Returns (changed uint8 tensor with one flag per source block, stats dict with
+    blocks / changed_blocks / literal_bytes / bytes_written)."""
+    nb = -(-src.numel() // block_size) if block_size > 0 else 0
+    changed = torch.empty(max(nb, 1), dtype=torch.uint8, device=src.device)
+    st = _lib.BlockCompareStatsC()
+    check(lib.sydelta_block_compare_device(src.device.index or 0, _ptr(src), src.numel(), _ptr(dst), dst.numel(),
+                                           block_size, _ptr(changed), _stream(stream), ctypes.byref(st)))
+    return changed[:nb], {f: int(getattr(st, f)) for f, _ in _lib.BlockCompareStatsC._fields_}
+
+
+def estimate_change_ratio(src: torch.Tensor, dst: torch.Tensor, block_size: int, sample_count: int | None = None,
+                          threshold: float | None = None, stream=None) -> dict:
+    """estimate_change_ratio (ratio.rs:78-192) on device bytes: src is the new file,
+    dst the existing one.  Returns the ChangeRatioResult fields as a dict."""
+    r = _lib.ChangeRatioC()
+    check(lib.sydelta_estimate_change_ratio_device(
+        src.device.index or 0, _ptr(src), src.numel(), _ptr(dst), dst.numel(), block_size,
+        -1 if sample_count is None else sample_count, -1.0 if threshold is None else threshold, _stream(stream),
+        ctypes.byref(r)))
+    return {"change_ratio": r.change_ratio, "blocks_sampled": r.blocks_sampled, "blocks_changed": r.blocks_changed,
+            "use_delta": bool(r.use_delta), "threshold": r.threshold}
+
+
 def synth_fill(buf: torch.Tensor, seed: int, stream=None) -> None:
     check(lib.sydelta_synth_fill(_ptr(buf), buf.numel(), seed & 0xFFFFFFFFFFFFFFFF, _stream(stream)))
 

@@ -1,0 +1,104 @@
+"""Local transport on the device: k_block_cmp against the
+oracle's block-compare loop (local.rs:541-619) and the device change-ratio estimate
+(k_hash_blocks, ratio.rs:78-192) against the oracle, on ratio.rs's own test files and
+on seeded inputs with misaligned buffers, block sizes not a multiple of 16, short
+(<= 240-byte) blocks, unequal lengths and one large case checked by properties."""
+import numpy as np
+import pytest
+
+from oracle import oracle as O
+
+pytestmark = pytest.mark.gpu
+
+MiB = 1 << 20
+BS = 64 * 1024
+
+
+def _dev(b, shift=0):
+    import torch
+
+    t = torch.zeros(len(b) + shift + 1, dtype=torch.uint8, device="cuda")
+    if len(b):
+        t[shift:shift + len(b)] = torch.frombuffer(bytearray(b), dtype=torch.uint8).cuda()
+    return t[shift:shift + len(b)]
+
+
+def _cases():
+    rng = np.random.default_rng(11)
+    base = rng.integers(0, 256, 3 * MiB + 12345, dtype=np.uint8).tobytes()
+    yield "same", base, base, BS
+    edited = bytearray(base)
+    for p in rng.integers(0, len(base), 40):
+        edited[p] ^= 0x5A
+    yield "edits", bytes(edited), base, BS
+    yield "src-longer", base, base[:2 * MiB + 17], BS
+    yield "dst-longer", base[:MiB + 3], base, BS
+    yield "odd-bs", bytes(edited), base, 1000 + 7
+    yield "short-blocks", bytes(edited[:200000]), base[:200000], 240
+    yield "tiny-blocks", bytes(edited[:50000]), base[:50000], 13
+    yield "empty-src", b"", base[:1000], BS
+    yield "empty-dst", base[:1000], b"", BS
+
+
+CASES = list(_cases())
+
+
+@pytest.mark.parametrize("shift", [0, 1, 4])
+@pytest.mark.parametrize("case", CASES, ids=lambda c: c[0])
+def test_block_compare_matches_oracle(case, shift, gpu):
+    name, src, dst, bs = case
+    flags, changed, lit, written = O.py_block_compare(src, dst, bs)
+    got, st = gpu.block_compare(_dev(src, shift), _dev(dst), bs)
+    assert got.cpu().tolist() == flags
+    assert st == {"blocks": len(flags), "changed_blocks": changed, "literal_bytes": lit, "bytes_written": written}
+
+
+@pytest.mark.parametrize("sample_count,threshold", [(None, None), (5, None), (1, 0.5), (0, None), (64, 0.1)])
+@pytest.mark.parametrize("case", CASES, ids=lambda c: c[0])
+def test_change_ratio_matches_oracle(case, sample_count, threshold, gpu):
+    name, src, dst, bs = case
+    r, sampled, changed, use, thr = O.py_estimate_change_ratio(src, dst, bs, sample_count, threshold)
+    got = gpu.estimate_change_ratio(_dev(src, 1), _dev(dst), bs, sample_count, threshold)
+    assert got == {"change_ratio": r, "blocks_sampled": sampled, "blocks_changed": changed, "use_delta": use,
+                   "threshold": thr}
+
+
+@pytest.mark.parametrize("name", ["same", "all_changed", "partial", "threshold", "size"])
+def test_change_ratio_reference_files(name, gpu):
+    # The files of ratio.rs:200-307.
+    src = bytearray(b"\x2a" * MiB)
+    dst = bytes(b"\x2a" * MiB)
+    if name == "all_changed":
+        dst = b"\x63" * MiB
+    elif name == "partial":
+        src[:256 * 1024] = b"\x63" * (256 * 1024)
+    elif name == "threshold":
+        src[:800 * 1024] = b"\x63" * (800 * 1024)
+    elif name == "size":
+        src = bytearray(b"\x2a" * (2 * MiB))
+    got = gpu.estimate_change_ratio(_dev(bytes(src)), _dev(dst), BS)
+    exp = O.py_estimate_change_ratio(bytes(src), dst, BS)
+    assert (got["change_ratio"], got["blocks_sampled"], got["blocks_changed"], got["use_delta"]) == exp[:4]
+    if name == "threshold":
+        assert not got["use_delta"]
+        assert gpu.estimate_change_ratio(_dev(bytes(src)), _dev(dst), BS, threshold=0.90)["use_delta"]
+
+
+def test_block_compare_large_properties(gpu):
+    # 1 GiB: flags equal a torch reduction over the reshaped block view, and exactly
+    # the edited blocks are flagged.
+    import torch
+
+    n, bs = 1 << 30, BS
+    src = torch.empty(n, dtype=torch.uint8, device="cuda")
+    gpu.synth_fill(src, seed=5)
+    dst = src.clone()
+    g = torch.Generator().manual_seed(3)
+    pos = torch.randint(0, n, (500,), generator=g)
+    dst[pos.cuda()] ^= 1
+    got, st = gpu.block_compare(src, dst, bs)
+    exp = torch.zeros(n // bs, dtype=torch.uint8)
+    exp[torch.unique(pos // bs)] = 1
+    assert torch.equal(got.cpu(), exp)
+    assert st["changed_blocks"] == int(exp.sum()) and st["literal_bytes"] == int(exp.sum()) * bs
+    assert st["bytes_written"] == n
