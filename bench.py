@@ -50,7 +50,7 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=2)
-    ap.add_argument("--workload", default="c3", choices=["c3", "c2", "c4", "c5", "apply", "json", "local"])
+    ap.add_argument("--workload", default="c3", choices=["c3", "c2", "c4", "c5", "apply", "json", "local", "xxh3"])
     ap.add_argument("--size-gib", type=float, default=None,
                     help="bytes per rank: c2/c3 basis and source (default 4), c5 chunk (default 8)")
     ap.add_argument("--block-size", type=int, default=None, help="default 4096 (c5: 8192)")
@@ -59,12 +59,16 @@ def parse():
     ap.add_argument("--basis-mib", type=int, default=0,
                     help="c3 only: sign just the first M MiB of the basis (smaller index; "
                          "exercises the LDS-resident filter); 0 = the whole basis")
-    ap.add_argument("--files", type=int, default=10000, help="c4: total 1 MiB files over all ranks")
+    ap.add_argument("--files", type=int, default=None,
+                    help="c4: total 1 MiB files over all ranks (10000); xxh3: files per rank (4096; 1 = one file of "
+                         "--size-gib)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-host-inclusive", action="store_true")
     a = ap.parse_args()
     if a.size_gib is None:
         a.size_gib = 8.0 if a.workload in ("c5", "apply", "local") else 4.0
+    if a.files is None:
+        a.files = 4096 if a.workload == "xxh3" else 10000
     if a.block_size is None:
         a.block_size = {"c5": 8192, "apply": 8192, "local": 65536}.get(a.workload, 4096)
     if a.edit_ppm is None:
@@ -123,6 +127,32 @@ def cpu_json_baseline(src_dev, bs: int):
     dt = time.perf_counter() - t0
     return {"value": round(sample.size / dt / GIB, 4), "unit": "GiB/s", "cores": 1, "kind": "port",
             "sample": f"host writer, one Data op of {sample.size >> 20} MiB ({len(text) >> 20} MiB of text)"}
+
+
+def cpu_xxh3_baseline(buf_dev, offs, lens):
+    """The oracle's hash_file (python-xxhash's XXH3, one thread, 1 MiB updates as in
+    integrity/xxhash3.rs:22-30) over a <= 512 MiB prefix of the same files, repeated
+    for >= 3 s."""
+    import numpy as np
+
+    from oracle import oracle as O
+
+    k = max(1, int(np.searchsorted(np.cumsum(lens), 512 << 20, side="right")))
+    k = min(k, len(lens))
+    end = int(offs[k - 1] + lens[k - 1])
+    host = buf_dev[:end].cpu().numpy().tobytes()
+    t0 = time.perf_counter()
+    reps = 0
+    while True:
+        for o, ln in zip(offs[:k], lens[:k]):
+            O.py_hash_file(host[int(o):int(o + ln)])
+        reps += 1
+        if time.perf_counter() - t0 >= 3.0:
+            break
+    dt = time.perf_counter() - t0
+    nbytes = int(lens[:k].sum()) * reps
+    return {"value": round(nbytes / dt / GIB, 3), "unit": "GiB/s", "cores": 1, "kind": "port",
+            "sample": f"{k} file(s), {int(lens[:k].sum()) >> 20} MiB, hashed {reps}x (python-xxhash XXH3)"}
 
 
 def shard_range(nunits: int, world: int, rank: int):
@@ -302,6 +332,14 @@ def main():
         dev.synth_fill_range(new, 0, 0x5E1D0007)
         dev.synth_mutate_blocks(new, new, 0, bs, 0x5E1D0008, args.edit_ppm)
         local_flags = torch.empty(n // bs, dtype=torch.uint8, device="cuda")
+    if args.workload == "xxh3":
+        # integrity verify (integrity/mod.rs:104): whole-file XXH3-64 of every file
+        if args.files == 1:
+            xxh_offs, xxh_lens = np.zeros(1, np.uint64), np.full(1, n, np.uint64)
+        else:
+            fsz = n // args.files
+            xxh_offs = np.arange(args.files, dtype=np.uint64) * np.uint64(fsz)
+            xxh_lens = np.full(args.files, fsz, dtype=np.uint64)
     if args.workload == "c5":
         # BASELINE config 5: one file of world * n bytes; this rank owns basis bytes
         # [rank*n, (rank+1)*n) and window starts [rank*n, (rank+1)*n) of the source
@@ -347,6 +385,9 @@ def main():
         if args.workload == "apply":
             _, st = dev.apply_device(basis, apply_d, new, out=apply_out, stream=stream)
             return st
+        if args.workload == "xxh3":
+            h = dev.xxh3_batch(basis, xxh_offs, xxh_lens, stream=stream)
+            return {"files": len(h), "hash0": f"{int(h[0]):016x}"}
         if args.workload == "local":
             # the local delta decision (ratio.rs) then the block compare (local.rs)
             r = dev.estimate_change_ratio(new, basis, bs, stream=stream)
@@ -415,6 +456,8 @@ def main():
         bytes_per_step = n  # reconstructed bytes
     elif args.workload == "local":
         bytes_per_step = 2 * n  # both files compared
+    elif args.workload == "xxh3":
+        bytes_per_step = int(xxh_lens.sum())
     elif args.workload == "json":
         bytes_per_step = n  # delta source bytes covered by the text
     else:
@@ -432,7 +475,8 @@ def main():
                  "k_sig_batch": n, "k_sig_wave": n, "k_probe": src_bytes,
                  "k_apply": 2 * n,  # apply: every output byte read once and written once
                  "k_json_write": n,  # json: every literal byte read once (text written: ~3.6x)
-                 "k_block_cmp": 2 * n}  # local: both files read once
+                 "k_block_cmp": 2 * n,  # local: both files read once
+                 "k_xxh_pieces": n}  # xxh3: every file byte read once
     dom = max(prof, key=lambda k: prof[k]["ms"]) if prof else None
     roof = None
     if dom and dom in algo_step:
@@ -451,6 +495,8 @@ def main():
             cpu = cpu_baseline(bs)
         if world == 1 and not args.no_cpu_baseline and args.workload == "json":
             cpu = cpu_json_baseline(new, bs)
+        if world == 1 and not args.no_cpu_baseline and args.workload == "xxh3":
+            cpu = cpu_xxh3_baseline(basis, xxh_offs, xxh_lens)
         hinc = None
         if world == 1 and not args.no_host_inclusive and args.workload == "c3":
             hinc = host_inclusive(dev, bs, min(n, 1 << 30), local)
@@ -480,6 +526,9 @@ def main():
                           f"one substituted byte; signature + all-gather + index + chunk match, chunk-sharded",
                     "apply": f"apply_delta on the device: {n / GIB:.0f} GiB reconstructed from a bs {bs} delta "
                              f"({args.edit_ppm / 1e4:g}% of blocks edited), per rank",
+                    "xxh3": (f"integrity: whole-file XXH3-64 of {args.files} x {n // max(1, args.files) >> 20} MiB "
+                             f"files per rank" if args.files != 1 else
+                             f"integrity: whole-file XXH3-64 of one {n / GIB:.0f} GiB file"),
                     "local": f"local transport: change-ratio sample + block compare of two {n / GIB:.0f} GiB files, "
                              f"bs {bs}, {args.edit_ppm / 1e4:g}% of blocks edited",
                     "json": f"serde_json text of the C3 delta ({n / GIB:.0f} GiB source, one literal run) on the device",

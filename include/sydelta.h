@@ -311,6 +311,18 @@ int sydelta_estimate_change_ratio_device(int device, const uint8_t *d_src, uint6
                                          double threshold, void *stream, sydelta_change_ratio *out);
 
 /* ---------------------------------------------------------------------------
+ * Whole-file XXH3-64, bytes already in device memory.
+ * ------------------------------------------------------------------------- */
+/* XxHash3Hasher::hash_file / hash_data (src/integrity/xxhash3.rs:17-40): *out =
+ * xxh3_64(d_buf[0, len)) with seed 0 (the streaming digest equals the one-shot hash). */
+int sydelta_xxh3_device(int device, const uint8_t *d_buf, uint64_t len, void *stream, uint64_t *out);
+/* The same for nfiles files [offs[f], offs[f] + lens[f]) of d_buf (host arrays), as the
+ * verify loop of integrity/mod.rs:104 hashes them one by one: out[f] (host) = hash.
+ * Every range must lie inside [0, buf_len). */
+int sydelta_xxh3_batch_device(int device, const uint8_t *d_buf, uint64_t buf_len, const uint64_t *offs, const uint64_t *lens,
+                              uint64_t nfiles, void *stream, uint64_t *out);
+
+/* ---------------------------------------------------------------------------
  * Measurement support (used by bench.py; not part of the reference API).
  * ------------------------------------------------------------------------- */
 /* When on, the library records a HIP event pair around every kernel it

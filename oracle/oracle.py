@@ -481,3 +481,18 @@ def py_estimate_change_ratio(src: bytes, dst: bytes, bs: int, sample_count=None,
             changed += 1
     ratio = changed / sample_count if sample_count > 0 else 0.0
     return ratio, sample_count, changed, ratio <= threshold, threshold
+
+
+# --------------------------------------------------------------------------
+# integrity/xxhash3.rs
+# --------------------------------------------------------------------------
+def py_hash_file(data: bytes, chunk: int = 1 << 20) -> int:
+    """XxHash3Hasher::hash_file (integrity/xxhash3.rs:17-33): Xxh3::new(), update with
+    1 MiB reads, digest.  Streamed through python-xxhash's XXH3 state, the independent
+    pin of xxhash-rust 0.8.15's Xxh3 (module docstring)."""
+    import xxhash
+
+    h = xxhash.xxh3_64()
+    for o in range(0, len(data), chunk):
+        h.update(data[o:o + chunk])
+    return h.intdigest()

@@ -109,6 +109,8 @@ SIGNATURES = [
     ("sydelta_block_compare_device", _i, [_i, _vp, _u64, _vp, _u64, _u64, _vp, _vp, ctypes.POINTER(BlockCompareStatsC)]),
     ("sydelta_estimate_change_ratio_device", _i, [_i, _vp, _u64, _vp, _u64, _u64, ctypes.c_int64, ctypes.c_double,
                                                   _vp, ctypes.POINTER(ChangeRatioC)]),
+    ("sydelta_xxh3_device", _i, [_i, _vp, _u64, _vp, _vp]),
+    ("sydelta_xxh3_batch_device", _i, [_i, _vp, _u64, _vp, _vp, _u64, _vp, _vp]),
     ("sydelta_set_profiling", None, [_i]),
     ("sydelta_profile_json", ctypes.c_size_t, [ctypes.c_char_p, ctypes.c_size_t, _i]),
     ("sydelta_synth_fill", _i, [_vp, _u64, _u64, _vp]),

@@ -13,7 +13,7 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 ROOT = os.path.dirname(HERE)
 CSRC = os.path.join(HERE, "csrc")
 LIB = os.path.join(HERE, "libsydelta.so")
-SOURCES = ["sydelta_kernels.hip", "sydelta_api.cpp", "sydelta_wire.cpp", "sydelta_local.cpp"]
+SOURCES = ["sydelta_kernels.hip", "sydelta_api.cpp", "sydelta_wire.cpp", "sydelta_local.cpp", "sydelta_integrity.cpp"]
 HEADERS = ["sydelta_device.hpp", "sydelta_internal.hpp", "sydelta_host.hpp", os.path.join("..", "..", "include", "sydelta.h")]
 ARCH = os.environ.get("SYDELTA_ARCH", "gfx950")
 

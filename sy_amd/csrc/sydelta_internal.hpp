@@ -157,6 +157,15 @@ hipError_t launch_block_cmp(const uint8_t* d_src, uint64_t slen, const uint8_t* 
 // out[i] = XXH3-64 of block pos[i] of buf (clipped at len, empty past the end).
 hipError_t launch_hash_blocks(const uint8_t* d_buf, uint64_t len, uint64_t bs, const uint64_t* d_pos, uint32_t count,
                               uint64_t* d_out, hipStream_t s);
+// Whole-file XXH3-64 of files (d_off[f], d_len[f]) of d_buf: d_pfx = prefix of full
+// 1 KiB block counts ((len-1)/1024 for len > 240, else 0), (d_aoff, d_apfx) the same
+// for the nact files with >= 1 block (d_apfx[nact] = npieces), d_order = files by block
+// count descending, d_C = 8 rows of xxh_chain_records(npieces) u64 of scratch, d_out[f] = hash.
+constexpr uint64_t xxh_chain_records(uint64_t npieces) { return npieces + 3 * 32; }
+hipError_t launch_xxh_files(const uint8_t* d_buf, const uint64_t* d_off, const uint64_t* d_len, const uint64_t* d_pfx,
+                            const uint64_t* d_aoff, const uint64_t* d_apfx, uint64_t nact, const uint32_t* d_order,
+                            uint64_t nfiles, uint64_t npieces, uint64_t* d_C, uint64_t* d_out,
+                            hipStream_t s, Profiler* prof);
 hipError_t launch_synth_fill(uint8_t* d_buf, uint64_t len, uint64_t seed, hipStream_t s, uint64_t first = 0);
 hipError_t launch_synth_edit_blocks(uint8_t* d_dst, uint64_t len, uint64_t bs, uint64_t first, uint64_t seed,
                                     uint32_t rate_ppm, hipStream_t s);

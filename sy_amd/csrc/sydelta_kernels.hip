@@ -1681,6 +1681,196 @@ __global__ __launch_bounds__(256) void k_hash_blocks(const uint8_t* __restrict__
 }
 
 // ===========================================================================
+// K9: whole-file XXH3-64 (integrity/xxhash3.rs:17-40, XxHash3Hasher::hash_file)
+// ===========================================================================
+// XXH3's long path is acc <- scramble(acc + C_k) over the 1 KiB blocks k of the file,
+// where C_k (the 16 stripes' accumulator increments) does not depend on acc.  Phase A
+// computes every C_k in parallel (HBM-bound); phase B runs the serial scramble chain,
+// eight lanes per file and eight files per wave, then the tail stripes and the merge.
+
+// 16 bytes at an arbitrary address, as two little-endian u64 (bytes [a, a+16) valid).
+__device__ __forceinline__ void load16u(const uint8_t* a, uint64_t& w0, uint64_t& w1) {
+    const uintptr_t u = (uintptr_t)a;
+    if ((u & 15) == 0) {
+        const u32x4 x = __builtin_nontemporal_load((const u32x4*)a);
+        w0 = (uint64_t)x.x | ((uint64_t)x.y << 32);
+        w1 = (uint64_t)x.z | ((uint64_t)x.w << 32);
+        return;
+    }
+    const uint32_t sh = (uint32_t)(u & 3);
+    const uint32_t* q = (const uint32_t*)(u & ~(uintptr_t)3);
+    const uint32_t d0 = q[0], d1 = q[1], d2 = q[2], d3 = q[3], d4 = sh ? q[4] : 0u;
+    const uint32_t x0 = __builtin_amdgcn_alignbyte(d1, d0, sh), x1 = __builtin_amdgcn_alignbyte(d2, d1, sh);
+    const uint32_t x2 = __builtin_amdgcn_alignbyte(d3, d2, sh), x3 = __builtin_amdgcn_alignbyte(d4, d3, sh);
+    w0 = (uint64_t)x0 | ((uint64_t)x1 << 32);
+    w1 = (uint64_t)x2 | ((uint64_t)x3 << 32);
+}
+
+// Phase A: one 16-lane row per kPieceRows consecutive full 1 KiB blocks (global block e
+// of file f is block e - fpfx[f] of the file); lane (slot, q) takes stripes slot + 4k
+// and accumulator pair (2q, 2q+1).  The file table here lists only files with at
+// least one full block.  C is SoA, C[i * cstride + e] = increment of acc[i] by block e,
+// so a chain lane's addends are contiguous (16-byte loads cover two steps).
+constexpr int kPieceRows = 4;
+__global__ __launch_bounds__(256) void k_xxh_pieces(const uint8_t* __restrict__ buf, const uint64_t* __restrict__ foff,
+                                                    const uint64_t* __restrict__ fpfx, uint64_t nfiles,
+                                                    uint64_t npieces, uint64_t cstride, uint64_t* __restrict__ C) {
+    const uint32_t lane = threadIdx.x & 63, q = lane & 3, slot = (lane >> 2) & 3;
+    const uint64_t row = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 4;
+    const uint64_t ebase = row * kPieceRows;
+    // File of the wave's first block by a 64-way search (fpfx[nfiles] = npieces), then
+    // each block steps forward: every listed file has >= 1 block, so the wave's
+    // 4 * kPieceRows consecutive blocks span at most that many files.
+    const uint64_t e0 = min(__shfl(ebase, 0), npieces - 1);
+    uint64_t lo = 0, hi = nfiles;
+    while (hi - lo > 1) {
+        const uint64_t step = (hi - lo + 63) >> 6;
+        const uint64_t c = lo + lane * step;
+        const uint64_t m = __ballot(c < hi && fpfx[c] <= e0);
+        const uint64_t nlo = lo + (63 - __builtin_clzll(m)) * step;
+        hi = min(hi, nlo + step);
+        lo = nlo;
+    }
+    uint64_t w0[kPieceRows][4], w1[kPieceRows][4];
+#pragma unroll
+    for (int r = 0; r < kPieceRows; ++r) {
+        const uint64_t e = min(ebase + r, npieces - 1);
+        while (fpfx[lo + 1] <= e) ++lo;
+        const uint8_t* p = buf + foff[lo] + ((e - fpfx[lo]) << 10);
+#pragma unroll
+        for (int k = 0; k < 4; ++k) load16u(p + ((slot + 4 * k) << 6) + (q << 4), w0[r][k], w1[r][k]);
+    }
+#pragma unroll
+    for (int r = 0; r < kPieceRows; ++r) {
+        uint64_t c_lo = 0, c_hi = 0;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            const uint32_t st = slot + 4 * k;
+            c_lo += mul32x32(w0[r][k] ^ c_tab.w[st + 2 * q]) + w1[r][k];
+            c_hi += mul32x32(w1[r][k] ^ c_tab.w[st + 2 * q + 1]) + w0[r][k];
+        }
+        c_lo = dpp_add64<kDppRowRor4>(c_lo);
+        c_lo = dpp_add64<kDppRowRor8>(c_lo);
+        c_hi = dpp_add64<kDppRowRor4>(c_hi);
+        c_hi = dpp_add64<kDppRowRor8>(c_hi);
+        const uint64_t e = ebase + r;
+        if (e < npieces && slot == 0) {
+            C[(uint64_t)(2 * q) * cstride + e] = c_lo;
+            C[(uint64_t)(2 * q + 1) * cstride + e] = c_hi;
+        }
+    }
+}
+
+// The chain is carried as y_k = acc_k + C_k (the value block k's scramble sees):
+// y_{k+1} = scramble(y_k) + C_{k+1}, acc after the last block = scramble(y_{nb-1}).
+// scramble(y) = (y ^ (y >> 47) ^ key) * PRIME32_1: y >> 47 touches only the low word,
+// and "* P + c" is one 32x32+64 mad on the low word plus a 32-bit add on the high word,
+// so the dependent path per block is shift -> xor3 -> mad -> add.
+// (Inline asm pins that shape; left alone the compiler folds the high-word product into
+// a second mad behind the first.)  The chain value is kept as two words.
+struct Y2 {
+    uint32_t lo, hi;
+};
+__device__ __forceinline__ Y2 chain_step(Y2 y, uint64_t c, uint32_t klo, uint32_t khi) {
+    uint32_t t;  // y.lo ^ key.lo does not wait for the high word
+    asm("v_xor_b32 %0, %1, %2" : "=v"(t) : "v"(y.lo), "v"(klo));
+    const uint32_t tl = t ^ (y.hi >> 15);
+    uint32_t th;
+    asm("v_mul_lo_u32 %0, %1, %2" : "=v"(th) : "v"(y.hi ^ khi), "s"((uint32_t)P32_1));
+    uint64_t m, cc;
+    asm("v_mad_u64_u32 %0, %1, %2, %3, %4" : "=v"(m), "=s"(cc) : "v"(tl), "s"((uint32_t)P32_1), "v"(c));
+    Y2 r;
+    r.lo = (uint32_t)m;
+    asm("v_add_u32 %0, %1, %2" : "=v"(r.hi) : "v"((uint32_t)(m >> 32)), "v"(th));
+    return r;
+}
+
+constexpr int kChainBatch = 32;
+static_assert(xxh_chain_records(0) == 3 * kChainBatch, "C row slack must cover the batch prefetch");
+
+// Phase B: lanes 8g..8g+7 of a wave hash file order[8 * blockIdx.x + g]; lane i keeps
+// acc[i].  Files are ordered by size so the eight chains of a wave have similar lengths.
+__global__ __launch_bounds__(64) void k_xxh_chain(const uint8_t* __restrict__ buf, const uint64_t* __restrict__ foff,
+                                                  const uint64_t* __restrict__ flen, const uint64_t* __restrict__ fpfx,
+                                                  const uint32_t* __restrict__ order, uint64_t nfiles,
+                                                  uint64_t cstride, const uint64_t* __restrict__ C,
+                                                  uint64_t* __restrict__ out) {
+    const uint32_t lane = threadIdx.x & 63, g = lane >> 3, i = lane & 7;
+    const uint64_t slot = (uint64_t)blockIdx.x * 8 + g;
+    const bool act = slot < nfiles;
+    const uint32_t f = act ? order[slot] : 0;
+    const uint64_t len = act ? flen[f] : 0;
+    const uint8_t* p = buf + foff[f];
+    const uint64_t nb = len > 240 ? (len - 1) >> 10 : 0;
+    const uint64_t steps = nb ? nb - 1 : 0;  // y -> y transitions
+    const uint64_t* Ci = C + (uint64_t)i * cstride + (act ? fpfx[f] : 0);
+    // step range over the wave
+    uint64_t nmin = act ? steps : ~0ull, nmax = steps;
+    for (int m = 8; m < 64; m <<= 1) {
+        nmin = min(nmin, (uint64_t)__shfl_xor((unsigned long long)nmin, m));
+        nmax = max(nmax, (uint64_t)__shfl_xor((unsigned long long)nmax, m));
+    }
+    const uint64_t key = c_tab.w[16 + i];
+    const uint32_t klo = (uint32_t)key, khi = (uint32_t)(key >> 32);
+    const uint64_t y0 = c_tab.init[i] + Ci[0];  // another file's record (or slack) when nb == 0: unused
+    Y2 y{(uint32_t)y0, (uint32_t)(y0 >> 32)};
+    const uint64_t* Cn = Ci + 1;          // the addend of step k is C_{k+1}
+    // Two register batches: the chain consumes one while the other is in flight.  C rows
+    // have 3 * kChainBatch entries of slack, so batch loads never need a bound check.
+    uint64_t ba[kChainBatch], bb[kChainBatch];
+#pragma unroll
+    for (int j = 0; j < kChainBatch; ++j) ba[j] = Cn[j];
+    uint64_t k = 0;
+    for (; k + 2 * kChainBatch <= nmin; k += 2 * kChainBatch) {  // every chain of the wave runs
+#pragma unroll
+        for (int j = 0; j < kChainBatch; ++j) bb[j] = Cn[k + kChainBatch + j];
+#pragma unroll
+        for (int j = 0; j < kChainBatch; ++j) y = chain_step(y, ba[j], klo, khi);
+#pragma unroll
+        for (int j = 0; j < kChainBatch; ++j) ba[j] = Cn[k + 2 * kChainBatch + j];
+#pragma unroll
+        for (int j = 0; j < kChainBatch; ++j) y = chain_step(y, bb[j], klo, khi);
+    }
+    for (; k < nmax; k += 2 * kChainBatch) {  // ragged ends
+#pragma unroll
+        for (int j = 0; j < kChainBatch; ++j) bb[j] = Cn[k + kChainBatch + j];
+#pragma unroll
+        for (int j = 0; j < kChainBatch; ++j)
+            if (k + j < steps) y = chain_step(y, ba[j], klo, khi);
+#pragma unroll
+        for (int j = 0; j < kChainBatch; ++j) ba[j] = Cn[k + 2 * kChainBatch + j];
+#pragma unroll
+        for (int j = 0; j < kChainBatch; ++j)
+            if (k + kChainBatch + j < steps) y = chain_step(y, bb[j], klo, khi);
+    }
+    y = chain_step(y, 0, klo, khi);
+    uint64_t acc = nb ? ((uint64_t)y.hi << 32 | y.lo) : c_tab.init[i];
+    if (!act) return;
+    if (len <= 240) {
+        if (i == 0) out[f] = xxh3_short(p, len);
+        return;
+    }
+    // stripes of the last (partial) block, then the last stripe (keys at secret + 121)
+    const uint64_t tb = nb << 10;
+    const uint64_t ns = ((len - 1) - tb) >> 6;
+    for (uint64_t s = 0; s < ns; ++s) {
+        const uint8_t* st = p + tb + (s << 6);
+        const uint64_t v = ld64u(st + 8 * i), vx = ld64u(st + 8 * (i ^ 1));
+        acc += vx + mul32x32(v ^ c_tab.w[s + i]);
+    }
+    {
+        const uint8_t* st = p + len - 64;
+        const uint64_t v = ld64u(st + 8 * i), vx = ld64u(st + 8 * (i ^ 1));
+        acc += vx + mul32x32(v ^ c_tab.last[i]);
+    }
+    const uint64_t partner = shfl_xor64(acc, 1);
+    uint64_t r = (i & 1) ? 0 : fold64(acc ^ c_tab.merge[i], partner ^ c_tab.merge[i + 1]);
+    r += shfl_xor64(r, 2);
+    r += shfl_xor64(r, 4);
+    if (i == 0) out[f] = xxh3_aval(len * P64_1 + r);
+}
+
+// ===========================================================================
 // Synthetic inputs (bench)
 // ===========================================================================
 // bytes [8*w0, 8*w0 + len) of the stream
@@ -2037,6 +2227,24 @@ hipError_t launch_hash_blocks(const uint8_t* d_buf, uint64_t len, uint64_t bs, c
     if (!count) return hipSuccess;
     hipLaunchKernelGGL(k_hash_blocks, dim3(grid_for((uint64_t)count * 64, 256)), dim3(256), 0, s, d_buf, len, bs, d_pos,
                        count, d_out);
+    return hipGetLastError();
+}
+
+hipError_t launch_xxh_files(const uint8_t* d_buf, const uint64_t* d_off, const uint64_t* d_len, const uint64_t* d_pfx,
+                            const uint64_t* d_aoff, const uint64_t* d_apfx, uint64_t nact, const uint32_t* d_order,
+                            uint64_t nfiles, uint64_t npieces, uint64_t* d_C, uint64_t* d_out,
+                            hipStream_t s, Profiler* prof) {
+    if (!nfiles) return hipSuccess;
+    const uint64_t cstride = xxh_chain_records(npieces);
+    if (npieces) {
+        ProfScope ps(prof, s, "k_xxh_pieces");
+        hipLaunchKernelGGL(k_xxh_pieces, dim3(grid_for((npieces + kPieceRows - 1) / kPieceRows * 16, 256)), dim3(256),
+                           0, s, d_buf, d_aoff, d_apfx, nact, npieces, cstride, d_C);
+        if (hipError_t e = hipGetLastError()) return e;
+    }
+    ProfScope ps(prof, s, "k_xxh_chain");
+    hipLaunchKernelGGL(k_xxh_chain, dim3((unsigned)((nfiles + 7) / 8)), dim3(64), 0, s, d_buf, d_off, d_len, d_pfx,
+                       d_order, nfiles, cstride, d_C, d_out);
     return hipGetLastError();
 }
 

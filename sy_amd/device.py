@@ -293,6 +293,27 @@ def estimate_change_ratio(src: torch.Tensor, dst: torch.Tensor, block_size: int,
             "use_delta": bool(r.use_delta), "threshold": r.threshold}
 
 
+def xxh3(buf: torch.Tensor, stream=None) -> int:
+    """XxHash3Hasher::hash_file / hash_data (integrity/xxhash3.rs:17-40) of device bytes."""
+    out = ctypes.c_uint64()
+    check(lib.sydelta_xxh3_device(buf.device.index or 0, _ptr(buf), buf.numel(), _stream(stream), ctypes.byref(out)))
+    return out.value
+
+
+def xxh3_batch(buf: torch.Tensor, offs, lens, stream=None) -> np.ndarray:
+    """Whole-file XXH3-64 of files [offs[f], offs[f] + lens[f]) of `buf`."""
+    o = np.ascontiguousarray(offs, dtype=np.uint64)
+    ln = np.ascontiguousarray(lens, dtype=np.uint64)
+    if o.shape != ln.shape:
+        raise ValueError("offs and lens differ in length")
+    if len(ln) and int((o + ln).max()) > buf.numel():
+        raise ValueError("file range outside the buffer")
+    out = np.zeros(len(ln), dtype=np.uint64)
+    check(lib.sydelta_xxh3_batch_device(buf.device.index or 0, _ptr(buf), buf.numel(), o.ctypes.data, ln.ctypes.data, len(ln),
+                                        _stream(stream), out.ctypes.data))
+    return out
+
+
 def synth_fill(buf: torch.Tensor, seed: int, stream=None) -> None:
     check(lib.sydelta_synth_fill(_ptr(buf), buf.numel(), seed & 0xFFFFFFFFFFFFFFFF, _stream(stream)))
 
