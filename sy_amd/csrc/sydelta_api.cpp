@@ -23,6 +23,7 @@
 #include <map>
 #include <memory>
 #include <mutex>
+#include <thread>
 #include <string>
 #include <vector>
 
@@ -371,27 +372,33 @@ extern "C" int sydelta_index_create_batch(int device, const uint32_t* weak, cons
 // Recycled op arrays: a walk over a copy-heavy source emits one op per block
 // (1 Mi ops = 24 MiB for 8 GiB at 8 KiB blocks); first-touch page faults of a
 // fresh array cost more than the walk itself, so freed deltas hand their arrays
-// back for the next walk (bounded: 4 arrays).
+// back for the next walk (bounded: 16 arrays; a parallel walk takes one per segment).
 namespace {
 std::mutex g_ops_mu;
-std::vector<std::vector<sydelta_op>> g_ops_pool;
-std::vector<sydelta_op> take_ops(size_t want) {
+std::vector<OpVec> g_ops_pool;
+OpVec take_ops(size_t want) {
+    // best fit: the smallest pooled array holding `want`, else the largest one when it
+    // holds at least half (it grows once)
     std::lock_guard<std::mutex> lk(g_ops_mu);
-    size_t best = g_ops_pool.size();
-    for (size_t i = 0; i < g_ops_pool.size(); ++i)
-        if (best == g_ops_pool.size() || g_ops_pool[i].capacity() > g_ops_pool[best].capacity()) best = i;
-    std::vector<sydelta_op> v;
-    if (best < g_ops_pool.size() && (want == 0 || g_ops_pool[best].capacity() >= want / 2)) {
+    size_t best = g_ops_pool.size(), big = g_ops_pool.size();
+    for (size_t i = 0; i < g_ops_pool.size(); ++i) {
+        const size_t c = g_ops_pool[i].capacity();
+        if (c >= want && (best == g_ops_pool.size() || c < g_ops_pool[best].capacity())) best = i;
+        if (big == g_ops_pool.size() || c > g_ops_pool[big].capacity()) big = i;
+    }
+    if (best == g_ops_pool.size() && big < g_ops_pool.size() && g_ops_pool[big].capacity() >= want / 2) best = big;
+    OpVec v;
+    if (best < g_ops_pool.size()) {
         v.swap(g_ops_pool[best]);
         g_ops_pool.erase(g_ops_pool.begin() + best);
     }
     v.clear();
     return v;
 }
-void give_ops(std::vector<sydelta_op>&& v) {
+void give_ops(OpVec&& v) {
     if (v.capacity() < 4096) return;
     std::lock_guard<std::mutex> lk(g_ops_mu);
-    if (g_ops_pool.size() < 4) g_ops_pool.push_back(std::move(v));
+    if (g_ops_pool.size() < 16) g_ops_pool.push_back(std::move(v));
 }
 }  // namespace
 
@@ -527,16 +534,20 @@ struct BasisInfo {
 };
 
 // Greedy walk (generator.rs:116-221 / 283-379) over c's classified positions from
-// `entry`.  ops get Data(source offset, len) and Copy(basis offset, size); consecutive
+// `entry` up to `end` (c.p1, or a split point of a parallel walk).  ops get Data(source offset, len) and Copy(basis offset, size); consecutive
 // Copies are never merged (generator.rs:135-140).  A non-final chunk ends with the
 // literal run up to p1 (continued by the next chunk) and *exit = where the walk left
 // [p0, p1).  A final source (its file ends inside it) applies the tail rule
 // (generator.rs:156-184: only p* = len - last_size can match) and the last literal
 // run.  Returns 1 with *need = the first position whose class is unknown.
-int walk_src(const Src& c, uint64_t n, uint64_t entry, const BasisInfo& bi, bool final_src, int tail_match,
-             std::vector<sydelta_op>& ops, uint64_t* exit, uint64_t* need) {
+int walk_src(const Src& c, uint64_t n, uint64_t entry, uint64_t end, const BasisInfo& bi, bool final_src,
+             int tail_match, OpVec& ops, uint64_t* exit, uint64_t* need) {
     const size_t ops0 = ops.size();  // appended to; rolled back on a need
-    ops.reserve(ops0 + 2 * (c.hpos.size() + c.nahit) + 3);
+    {
+        const uint64_t span = c.p1 > c.p0 ? c.p1 - c.p0 : 1;
+        const double frac = end > entry ? double(end - entry) / double(span) : 0.0;
+        ops.reserve(ops0 + (size_t)(2.0 * double(c.hpos.size() + c.nahit) * std::min(1.0, frac)) + 16);
+    }
     uint64_t x = entry, lit = entry;
     auto data = [&](uint64_t a, uint64_t b) {
         if (b > a) ops.push_back({SYDELTA_OP_DATA, 0, a, b - a});
@@ -549,11 +560,12 @@ int walk_src(const Src& c, uint64_t n, uint64_t entry, const BasisInfo& bi, bool
     const size_t H = c.hpos.size();
     const uint64_t kend = c.kb + c.nblk;
     uint64_t ka = c.kb;  // next aligned window that may hit (probed sources)
-    while (x < c.p1) {
-        // next hit at or after x: the next scan hit or the next aligned hit
+    while (x < end) {
+        // next hit at or after x and before end: the next scan hit or the next aligned hit
         while (i < H && c.hpos[i] < x) ++i;
-        uint64_t p = i < H ? c.hpos[i] : c.p1;
-        uint32_t pb = i < H ? c.hblk[i] : kNoBlk;
+        uint64_t p = end;
+        uint32_t pb = kNoBlk;
+        if (i < H && c.hpos[i] < end) { p = c.hpos[i]; pb = c.hblk[i]; }
         if (c.probed) {
             if (ka * n < x) ka = (x + n - 1) / n;  // after an aligned Copy x == (ka+1)*n: no division
             while (ka < kend && ka * n < p && c.ahit[ka - c.kb] == kNoBlk) ++ka;
@@ -566,7 +578,7 @@ int walk_src(const Src& c, uint64_t n, uint64_t entry, const BasisInfo& bi, bool
             return 1;
         }
         if (pb == kNoBlk) {
-            x = c.p1;
+            x = end;
             break;
         }
         data(lit, p);
@@ -575,8 +587,8 @@ int walk_src(const Src& c, uint64_t n, uint64_t entry, const BasisInfo& bi, bool
         lit = x;
     }
     if (!final_src) {
-        data(lit, c.p1);
-        *exit = std::max(x, c.p1);
+        data(lit, end);
+        *exit = std::max(x, end);
         return 0;
     }
     if (tail_match && bi.nblocks) {
@@ -619,6 +631,12 @@ struct Classifier {
     // Walk source i from entry, scanning on demand what the walk needs.
     int walk(size_t i, uint64_t entry, const BasisInfo& bi, bool final_src, int tail_match, sydelta_delta* d,
              uint64_t* exit);
+    // The same walk split at block-aligned points over threads, each segment walked
+    // speculatively from its split point; a segment whose true entry (the previous
+    // segment's exit) differs is walked again from it.  Returns 0 (done, d->ops set),
+    // 1 (a segment reached an unclassified block: walk sequentially), 2 (too small).
+    int walk_parallel(size_t i, uint64_t entry, const BasisInfo& bi, bool final_src, int tail_match,
+                      sydelta_delta* d, uint64_t* exit);
 };
 
 int Classifier::probe(int mode) {
@@ -843,13 +861,20 @@ int Classifier::classify(int mode) {
 int Classifier::walk(size_t i, uint64_t entry, const BasisInfo& bi, bool final_src, int tail_match, sydelta_delta* d,
                      uint64_t* exit) {
     Src& c = src[i];
-    std::vector<sydelta_op>& ops = d->ops;
-    if (ops.empty() && c.nahit + c.hpos.size() >= 4096) ops = take_ops(2 * (c.nahit + c.hpos.size()));
+    OpVec& ops = d->ops;
     static const bool host_timing = getenv("SYDELTA_HOST_TIMING") != nullptr;
+    if (ops.empty()) {
+        const auto t0 = std::chrono::steady_clock::now();
+        const int r = walk_parallel(i, entry, bi, final_src, tail_match, d, exit);
+        if (host_timing && r != 2)
+            fprintf(stderr, "sydelta parallel walk: %.3f ms, %zu ops, rc=%d\n", ms_since(t0), ops.size(), r);
+        if (r != 1 && r != 2) return r;  // done, or an error
+    }
+    if (ops.empty() && c.nahit + c.hpos.size() >= 4096) ops = take_ops(2 * (c.nahit + c.hpos.size()));
     for (int round = 0;; ++round) {
         uint64_t need = 0;
         const auto t0 = std::chrono::steady_clock::now();
-        const int r = walk_src(c, n, entry, bi, final_src, tail_match, ops, exit, &need);
+        const int r = walk_src(c, n, entry, c.p1, bi, final_src, tail_match, ops, exit, &need);
         if (host_timing)
             fprintf(stderr, "sydelta walk round %d: %.3f ms, %zu ops, need=%d\n", round,
                     std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count(),
@@ -863,6 +888,111 @@ int Classifier::walk(size_t i, uint64_t entry, const BasisInfo& bi, bool final_s
             { if (int r = scan({{i, k, c.kb + c.nblk}})) return r; }
     }
     return SYDELTA_OK;
+}
+
+int walk_threads() {
+    const char* e = getenv("SYDELTA_WALK_THREADS");
+    if (e && *e) return std::max(1, atoi(e));
+    const unsigned hw = std::thread::hardware_concurrency();
+    return (int)std::min(8u, std::max(1u, hw));
+}
+
+uint64_t walk_par_min() {
+    const char* e = getenv("SYDELTA_WALK_PAR_MIN");  // hits below which the walk stays serial
+    return (e && *e) ? strtoull(e, nullptr, 10) : (1ull << 16);
+}
+
+int Classifier::walk_parallel(size_t i, uint64_t entry, const BasisInfo& bi, bool final_src, int tail_match,
+                              sydelta_delta* d, uint64_t* exit) {
+    const Src& c = src[i];
+    const uint64_t nh = c.nahit + c.hpos.size();
+    const int T0 = walk_threads();
+    if (T0 < 2 || nh < walk_par_min() || c.p1 <= entry || (c.p1 - entry) / n < 2 * (uint64_t)T0) return 2;
+    // split points: multiples of n strictly inside (entry, p1)
+    std::vector<uint64_t> st{entry};
+    for (int t = 1; t < T0; ++t) {
+        const uint64_t q = (entry + (c.p1 - entry) / T0 * t) / n * n;
+        if (q > st.back() && q < c.p1) st.push_back(q);
+    }
+    const int T = (int)st.size();
+    st.push_back(c.p1);
+    std::vector<OpVec> part(T);
+    std::vector<uint64_t> ex(T, 0), need(T, 0);
+    std::vector<int> rc(T, 0);
+    static const bool host_timing = getenv("SYDELTA_HOST_TIMING") != nullptr;
+    const auto t0 = std::chrono::steady_clock::now();
+    OpVec joined = take_ops(nh);  // before the segments' arrays, so they do not take it
+    for (int t = 0; t < T; ++t) part[t] = take_ops(2 * nh / T + 64);
+    struct Give {
+        std::vector<OpVec>& v;
+        ~Give() {
+            for (auto& x : v) give_ops(std::move(x));
+        }
+    } give{part};
+    std::vector<double> tseg(T, 0.0);
+    auto seg = [&](int t, uint64_t from) {
+        const auto ts = std::chrono::steady_clock::now();
+        part[t].clear();
+        const bool fin = final_src && t == T - 1;
+        rc[t] = walk_src(c, n, from, st[t + 1], bi, fin, tail_match, part[t], &ex[t], &need[t]);
+        tseg[t] = ms_since(ts);
+    };
+    {
+        std::vector<std::thread> th;
+        for (int t = 1; t < T; ++t) th.emplace_back(seg, t, st[t]);
+        seg(0, entry);
+        for (auto& x : th) x.join();
+    }
+    const double t_walk = ms_since(t0);
+    if (rc[0]) return 1;
+    // chain: segment t's true entry is segment t-1's exit
+    for (int t = 1; t < T; ++t) {
+        if (ex[t - 1] != st[t]) seg(t, ex[t - 1]);
+        if (rc[t]) return 1;
+    }
+    // join, merging a Data op that ends where the next segment's first Data op starts
+    std::vector<size_t> at(T + 1, 0), skip(T, 0);
+    bool last_data = false;  // the joined list so far ends with a Data op ending at last_end
+    uint64_t last_end = 0;
+    for (int t = 0; t < T; ++t) {
+        const OpVec& v = part[t];
+        if (!v.empty() && last_data && v[0].kind == SYDELTA_OP_DATA && last_end == v[0].a) {
+            skip[t] = 1;
+            last_end += v[0].b;
+        }
+        at[t + 1] = at[t] + v.size() - skip[t];
+        if (v.size() > skip[t]) {
+            last_data = v.back().kind == SYDELTA_OP_DATA;
+            last_end = v.back().a + v.back().b;
+        }
+    }
+    const double t_chain = ms_since(t0);
+    OpVec& ops = d->ops;
+    ops.swap(joined);
+    give_ops(std::move(joined));
+    const size_t cap0 = ops.capacity();
+    ops.resize(at[T]);
+    {
+        std::vector<std::thread> th;
+        auto put = [&](int t) {
+            if (part[t].size() > skip[t])
+                memcpy(ops.data() + at[t], part[t].data() + skip[t], (part[t].size() - skip[t]) * sizeof(sydelta_op));
+        };
+        for (int t = 1; t < T; ++t) th.emplace_back(put, t);
+        put(0);
+        for (auto& x : th) x.join();
+    }
+    // merged lengths: the op before each skipped one absorbs it
+    for (int t = 1; t < T; ++t)
+        if (skip[t]) ops[at[t] - 1].b += part[t][0].b;  // the op before segment t absorbs its first
+    *exit = ex[T - 1];
+    if (host_timing)
+        fprintf(stderr,
+                "sydelta parallel walk: %d segments, walk %.3f ms (segment max %.3f min %.3f), chain %.3f ms, "
+                "join %.3f ms (cap %zu)\n",
+                T, t_walk, *std::max_element(tseg.begin(), tseg.end()), *std::min_element(tseg.begin(), tseg.end()),
+                t_chain - t_walk, ms_since(t0) - t_chain, cap0);
+    return 0;
 }
 
 void finish_stats_impl(sydelta_delta* d) {

@@ -257,3 +257,57 @@ def test_apply_device_rejects_copy_past_end(gpu):
                           200, 4096, {})
     with pytest.raises(L.SyDeltaError):
         gpu.apply_device(b, bad, b)
+
+
+@pytest.fixture(params=[2, 3, 8], ids=lambda t: f"walk{t}")
+def par_walk(request, monkeypatch):
+    """Force the parallel speculative walk (Classifier::walk_parallel) at any size."""
+    monkeypatch.setenv("SYDELTA_WALK_THREADS", str(request.param))
+    monkeypatch.setenv("SYDELTA_WALK_PAR_MIN", "1")
+    return request.param
+
+
+@pytest.mark.parametrize("bs", [64, 1000, 4096])
+def test_parallel_walk_equals_oracle(bs, par_walk, probe_mode, gpu, oracle_c):
+    """Split points land inside literal runs, inside unaligned-copy stretches (exits
+    differ from the speculative entries: segments re-walked) and between aligned
+    copies; the joined op list must equal the sequential one."""
+    rng = random.Random(bs + 7 * par_walk)
+    basis = rng.randbytes(rng.randint(200, 400) * bs + rng.randint(0, bs - 1))
+    src = _shift_edits(basis, rng, bs, 12)
+    src = bytearray(src)
+    a = rng.randrange(len(src) // 2)
+    src[a:a + 5 * bs] = rng.randbytes(5 * bs)  # a long literal run
+    for _ in range(15):
+        src[rng.randrange(len(src))] ^= 0x3C
+    src = bytes(src)
+    idx = _index(gpu, basis, bs)
+    d = gpu.match(idx, _to_dev(src), length=len(src))
+    idx.close()
+    assert d.tuples() == _oracle_ops(oracle_c, src, basis, bs)
+
+
+def test_parallel_walk_all_literal_and_identical(par_walk, gpu, oracle_c):
+    bs = 512
+    rng = random.Random(3)
+    basis = rng.randbytes(300 * bs + 17)
+    for src in (rng.randbytes(len(basis)), basis, basis[:-100] + rng.randbytes(100)):
+        idx = _index(gpu, basis, bs)
+        d = gpu.match(idx, _to_dev(src), length=len(src))
+        idx.close()
+        assert d.tuples() == _oracle_ops(oracle_c, src, basis, bs)
+
+
+@pytest.mark.parametrize("nchunks", [2, 3])
+def test_parallel_walk_in_chunks(nchunks, par_walk, gpu, oracle_c):
+    bs = 1000
+    rng = random.Random(nchunks)
+    basis = rng.randbytes(250 * bs + 321)
+    src = _shift_edits(basis, rng, bs, 6)
+    idx = _index(gpu, basis, bs)
+    npos = len(src) - bs + 1
+    nb = -(-npos // bs)
+    cuts = sorted(rng.sample(range(1, nb), nchunks - 1))
+    d = _chunked(gpu, src, idx, bs, [0] + [c * bs for c in cuts] + [npos])
+    idx.close()
+    assert d.tuples() == _oracle_ops(oracle_c, src, basis, bs)
