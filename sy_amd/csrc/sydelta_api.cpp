@@ -1343,7 +1343,9 @@ extern "C" int sydelta_apply_delta_device(int device, const uint8_t* d_basis, ui
         pin.cap = cap;
     }
     ApplyPiece* pieces = pin.p;
-    size_t np = 0;
+    static const bool host_timing = getenv("SYDELTA_HOST_TIMING") != nullptr;
+    const auto t0 = std::chrono::steady_clock::now();
+    // validate every op first (the output is not touched on an error)
     uint64_t pos = 0, literal = 0;
     for (size_t i = 0; i < d->ops.size(); ++i) {
         const sydelta_op& o = d->ops[i];
@@ -1355,8 +1357,6 @@ extern "C" int sydelta_apply_delta_device(int device, const uint8_t* d_basis, ui
         if (!cp && (o.a > lit_len || o.b > lit_len - o.a))
             return fail(SYDELTA_E_INVAL, "op %zu: Data [%llu, +%llu) outside the literal buffer", i,
                         (unsigned long long)o.a, (unsigned long long)o.b);
-        for (uint64_t k = 0; k < o.b; k += kSlice)
-            pieces[np++] = {pos + k, o.a + k, (uint32_t)std::min<uint64_t>(kSlice, o.b - k), cp ? 1u : 0u};
         pos += o.b;
         if (!cp) literal += o.b;
     }
@@ -1365,13 +1365,53 @@ extern "C" int sydelta_apply_delta_device(int device, const uint8_t* d_basis, ui
     if (pos && !d_out) return fail(SYDELTA_E_INVAL, "NULL output");
     hipStream_t s = stream ? (hipStream_t)stream : thread_stream(device < 0 ? 0 : device);
     CallProf cp;
-    if (np) {
+    if (need) {
+        // Pipelined: the host fills batch j of the piece table while batch j-1 is
+        // uploaded on a copy stream and batch j-2 is copied by k_apply on `s`.
+        constexpr size_t kBatches = 8;
+        // per thread and device, never destroyed (like thread_stream)
+        static thread_local std::map<int, std::pair<hipStream_t, std::vector<hipEvent_t>>> copy_streams;
+        auto& cs = copy_streams[device < 0 ? 0 : device];
+        if (!cs.first) HIP_TRY(hipStreamCreateWithFlags(&cs.first, hipStreamNonBlocking));
+        while (cs.second.size() < kBatches) {
+            hipEvent_t e;
+            HIP_TRY(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+            cs.second.push_back(e);
+        }
+        hipStream_t cstream = cs.first;
+        const std::vector<hipEvent_t>& ev = cs.second;
         DevBuf pb;
-        HIP_TRY(hipMallocAsync(&pb.p, np * sizeof(ApplyPiece), s));
+        HIP_TRY(hipMallocAsync(&pb.p, need * sizeof(ApplyPiece), s));
         pb.s = s;
-        HIP_TRY(hipMemcpyAsync(pb.p, pieces, np * sizeof(ApplyPiece), hipMemcpyHostToDevice, s));
-        HIP_TRY(launch_apply((const ApplyPiece*)pb.p, np, d_basis, d_lit, d_out, s, cp.get()));
+        HIP_TRY(hipEventRecord(ev[0], s));  // the table allocation is ordered before the uploads
+        HIP_TRY(hipStreamWaitEvent(cstream, ev[0], 0));
+        ApplyPiece* dp = (ApplyPiece*)pb.p;
+        const size_t per = std::max<size_t>(1, (d->ops.size() + kBatches - 1) / kBatches);
+        size_t np = 0, j = 0;
+        uint64_t at = 0;
+        for (size_t i0 = 0; i0 < d->ops.size(); i0 += per, ++j) {
+            const size_t i1 = std::min(d->ops.size(), i0 + per);
+            const size_t b0 = np;
+            for (size_t i = i0; i < i1; ++i) {
+                const sydelta_op& o = d->ops[i];
+                const bool cpy = o.kind == SYDELTA_OP_COPY;
+                const uint32_t cpf = cpy ? 1u : 0u;
+                for (uint64_t k = 0; k < o.b; k += kSlice)
+                    pieces[np++] = {at + k, o.a + k, (uint32_t)std::min<uint64_t>(kSlice, o.b - k), cpf};
+                at += o.b;
+            }
+            if (np == b0) continue;
+            HIP_TRY(hipMemcpyAsync(dp + b0, pieces + b0, (np - b0) * sizeof(ApplyPiece), hipMemcpyHostToDevice,
+                                   cstream));
+            HIP_TRY(hipEventRecord(ev[j], cstream));
+            HIP_TRY(hipStreamWaitEvent(s, ev[j], 0));
+            HIP_TRY(launch_apply(dp + b0, np - b0, d_basis, d_lit, d_out, s, cp.get()));
+        }
+        const double t_enq = ms_since(t0);
         HIP_TRY(hipStreamSynchronize(s));  // the pinned table is reused by the next call
+        if (host_timing)
+            fprintf(stderr, "sydelta apply: %zu pieces, validate+build+enqueue %.3f ms, total %.3f ms\n", np,
+                    t_enq, ms_since(t0));
     }
     if (out) {
         out->operations_count = d->ops.size();

@@ -243,8 +243,8 @@ def apply_device(basis: torch.Tensor, delta: DeviceDelta, lit: torch.Tensor, out
     """apply_delta (applier.rs:22-56) on the device: Copy ops from `basis`, Data ops
     from `lit` at the op's source offset.  Returns (out tensor, stats dict)."""
     n = len(delta.kind)
-    total = int(np.asarray(delta.b, dtype=np.uint64).sum()) if n else 0
     if out is None:
+        total = int(np.asarray(delta.b, dtype=np.uint64).sum()) if n else 0
         out = torch.empty(max(total, 1), dtype=torch.uint8, device=basis.device)
     own = None
     if delta.handle is not None:  # the library's own delta: no copy of the ops
@@ -265,7 +265,7 @@ def apply_device(basis: torch.Tensor, delta: DeviceDelta, lit: torch.Tensor, out
     finally:
         if own:
             lib.sydelta_delta_free(own)
-    return out[:total], {f: int(getattr(st, f)) for f, _ in _lib.DeltaStatsC._fields_}
+    return out[:st.bytes_written], {f: int(getattr(st, f)) for f, _ in _lib.DeltaStatsC._fields_}
 
 
 def block_compare(src: torch.Tensor, dst: torch.Tensor, block_size: int, stream=None):

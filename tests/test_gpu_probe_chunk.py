@@ -257,6 +257,15 @@ def test_apply_device_rejects_copy_past_end(gpu):
                           200, 4096, {})
     with pytest.raises(L.SyDeltaError):
         gpu.apply_device(b, bad, b)
+    # the bad Copy after many good ones (the whole op list is checked before any copy)
+    k = np.zeros(100, np.uint32)
+    a = np.zeros(100, np.uint64)
+    ln = np.full(100, 40, np.uint64)
+    a[77] = 4090
+    late = gpu.DeviceDelta(k, a, ln, 4000, 4096, {})
+    out = torch.zeros(8192, dtype=torch.uint8, device="cuda")
+    with pytest.raises(L.SyDeltaError, match="past the end of the basis"):
+        gpu.apply_device(b, late, b, out=out)
 
 
 @pytest.fixture(params=[2, 3, 8], ids=lambda t: f"walk{t}")
