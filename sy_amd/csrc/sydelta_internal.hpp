@@ -138,7 +138,7 @@ hipError_t launch_apply(const ApplyPiece* d_pieces, uint64_t npieces, const uint
 // Delta JSON on the device (K7).  A piece is a Copy op (a = offset, b = size) or a
 // chunk of <= kJsonChunk literal bytes of a Data op (lit[src, src+len)).
 constexpr uint32_t kJsonData = 1, kJsonFirst = 2, kJsonLast = 4, kJsonSep = 8;
-constexpr uint32_t kJsonChunk = 16384;
+constexpr uint32_t kJsonChunk = 4096;
 constexpr uint32_t kJsonStage = 4 * kJsonChunk + 32;  // LDS text staging per chunk
 struct JsonPiece {
     uint64_t src;

@@ -1436,7 +1436,7 @@ __global__ __launch_bounds__(256) void k_apply(const ApplyPiece* __restrict__ pi
 // ===========================================================================
 // K7: serde_json text of a Delta on the device (wire format, sydelta_wire.cpp)
 // ===========================================================================
-// Pieces in op order: a Copy op, or a <= 16 KiB chunk of a Data op's literal bytes.
+// Pieces in op order: a Copy op, or a <= 4 KiB chunk of a Data op's literal bytes.
 // Pass 1 sizes every piece's text, an exclusive scan places them, pass 2 writes them.
 // A Data chunk is formatted into LDS (<= 4 characters per byte) at the 16-byte phase of
 // its destination, then leaves with aligned 16-byte stores; the partial granules at its
@@ -1454,40 +1454,57 @@ __device__ __forceinline__ uint32_t json_copy_len(const JsonPiece& P) {
 
 __global__ __launch_bounds__(256) void k_json_len(const JsonPiece* __restrict__ pieces, uint64_t npieces,
                                                   const uint8_t* __restrict__ lit, uint64_t* __restrict__ len) {
-    // one workgroup per piece; Copy pieces are sized by thread 0
-    __shared__ uint32_t red[4];
-    const JsonPiece P = pieces[blockIdx.x];
+    // one wave per piece (lane l sizes literal bytes [64l, 64l + 64) of a Data chunk);
+    // Copy pieces are sized by lane 0
+    const uint64_t pi = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+    const uint32_t lane = threadIdx.x & 63;
+    if (pi >= npieces) return;
+    const JsonPiece P = pieces[pi];
     if (!(P.flags & kJsonData)) {
-        if (threadIdx.x == 0) len[blockIdx.x] = json_copy_len(P);
+        if (lane == 0) len[pi] = json_copy_len(P);
         return;
     }
+    static_assert(kJsonChunk == 64 * 64, "one lane per 64 literal bytes");
+    const uint32_t b0 = 64 * lane;
+    const uint32_t cnt = b0 < P.len ? min(64u, P.len - b0) : 0u;
+    const uint8_t* lp = lit + P.src + b0;
     uint32_t c = 0;
-    // 16 bytes per thread per step where the run allows it, bytes at the ragged ends
-    const uint64_t a0 = P.src, a1 = P.src + P.len;
-    const uint64_t v0 = (a0 + 15) & ~15ull, v1 = a1 & ~15ull;
-    if (v0 < v1) {
-        for (uint64_t q = v0 + 16ull * threadIdx.x; q < v1; q += 16ull * blockDim.x) {
-            const uint4 v = *(const uint4*)(lit + q);
-            const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+    if (cnt == 64 && ((uintptr_t)lp & 15) == 0) {
+        uint4 v[4];
 #pragma unroll
-            for (int k = 0; k < 16; ++k) c += byte_digits((w[k >> 2] >> (8 * (k & 3))) & 0xFF);
+        for (int k = 0; k < 4; ++k) v[k] = ((const uint4*)lp)[k];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            const uint32_t w[4] = {v[k].x, v[k].y, v[k].z, v[k].w};
+#pragma unroll
+            for (int j = 0; j < 16; ++j) c += byte_digits((w[j >> 2] >> (8 * (j & 3))) & 0xFF);
         }
-        for (uint64_t q = a0 + threadIdx.x; q < v0; q += blockDim.x) c += byte_digits(lit[q]);
-        for (uint64_t q = v1 + threadIdx.x; q < a1; q += blockDim.x) c += byte_digits(lit[q]);
+    } else if (cnt == 64) {  // unaligned: the 17 dwords holding the 64 bytes
+        const uintptr_t u = (uintptr_t)lp;
+        const uint32_t sh = (uint32_t)(u & 3);
+        const uint32_t* q = (const uint32_t*)(u & ~(uintptr_t)3);
+        uint32_t d[17];
+#pragma unroll
+        for (int k = 0; k < 16; ++k) d[k] = q[k];
+        d[16] = sh ? q[16] : 0u;
+#pragma unroll
+        for (int k = 0; k < 16; ++k) {
+            const uint32_t x = __builtin_amdgcn_alignbyte(d[k + 1], d[k], sh);
+#pragma unroll
+            for (int j = 0; j < 4; ++j) c += byte_digits((x >> (8 * j)) & 0xFF);
+        }
     } else {
-        for (uint64_t q = a0 + threadIdx.x; q < a1; q += blockDim.x) c += byte_digits(lit[q]);
+        for (uint32_t j = 0; j < cnt; ++j) c += byte_digits(lp[j]);
     }
     c = wave_sum32_dpp(c);
-    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = c;
-    __syncthreads();
-    if (threadIdx.x == 0) {
-        uint32_t t = red[0] + red[1] + red[2] + red[3];
+    if (lane == 0) {
+        uint32_t t = c;
         t += P.len ? P.len - 1 : 0;                     // commas between bytes of the chunk
         if (!(P.flags & kJsonLast) && P.len) t += 1;    // comma before the next chunk's first byte
         if (P.flags & kJsonFirst) t += 9;               // {"Data":[
         if (P.flags & kJsonLast) t += 2;                // ]}
         if (P.flags & kJsonSep) t += 1;                 // , before the op
-        len[blockIdx.x] = t;
+        len[pi] = t;
     }
 }
 
@@ -1523,26 +1540,32 @@ __global__ __launch_bounds__(256) void k_json_write(const JsonPiece* __restrict_
         }
         return;
     }
-    // thread t formats bytes [t*per, (t+1)*per) of the chunk (per = 64 for a full
-    // chunk), read as dwords where aligned
-    const uint32_t per = (P.len + blockDim.x - 1) / blockDim.x;
-    const uint32_t b0 = min(P.len, threadIdx.x * per), b1 = min(P.len, b0 + per);
-    const uint8_t* lp = lit + P.src;
-    const bool dw = (((uintptr_t)lp + b0) & 3) == 0 && (per & 3) == 0;
-    auto byte_at = [&](uint32_t i) -> uint32_t { return lp[i]; };
-    uint32_t mine = 0;
-    if (dw) {
-        for (uint32_t i = b0; i < b1; i += 4) {
-            const uint32_t x = (i + 4 <= b1) ? *(const uint32_t*)(lp + i) : 0u;
-            if (i + 4 <= b1) {
-#pragma unroll
-                for (int k = 0; k < 4; ++k) mine += byte_digits((x >> (8 * k)) & 0xFF) + 1;
-            } else {
-                for (uint32_t j = i; j < b1; ++j) mine += byte_digits(byte_at(j)) + 1;
-            }
+    // thread t formats bytes [16t, 16t + 16) of the chunk (kJsonChunk = 16 * 256)
+    const uint32_t b0 = 16 * threadIdx.x;
+    const uint32_t cnt = b0 < P.len ? min(16u, P.len - b0) : 0u;
+    const uint8_t* lp = lit + P.src + b0;
+    uint32_t w[4] = {0, 0, 0, 0};
+    if (cnt == 16) {
+        const uintptr_t u = (uintptr_t)lp;
+        if ((u & 15) == 0) {
+            const uint4 v = *(const uint4*)lp;
+            w[0] = v.x; w[1] = v.y; w[2] = v.z; w[3] = v.w;
+        } else {  // dwords holding the 16 bytes (never past the granule of a valid byte)
+            const uint32_t sh = (uint32_t)(u & 3);
+            const uint32_t* q = (const uint32_t*)(u & ~(uintptr_t)3);
+            const uint32_t d0 = q[0], d1 = q[1], d2 = q[2], d3 = q[3], d4 = sh ? q[4] : 0u;
+            w[0] = __builtin_amdgcn_alignbyte(d1, d0, sh); w[1] = __builtin_amdgcn_alignbyte(d2, d1, sh);
+            w[2] = __builtin_amdgcn_alignbyte(d3, d2, sh); w[3] = __builtin_amdgcn_alignbyte(d4, d3, sh);
         }
     } else {
-        for (uint32_t i = b0; i < b1; ++i) mine += byte_digits(byte_at(i)) + 1;  // digits + comma
+        for (uint32_t j = 0; j < cnt; ++j) w[j >> 2] |= (uint32_t)lp[j] << (8 * (j & 3));
+    }
+    // text of each byte + its comma: 2-4 characters, branch-free
+    uint32_t mine = 0;
+#pragma unroll
+    for (int j = 0; j < 16; ++j) {
+        const uint32_t v = (w[j >> 2] >> (8 * (j & 3))) & 0xFF;
+        mine += (j < (int)cnt) ? 2u + (v >= 10) + (v >= 100) : 0u;
     }
     // exclusive scan of `mine` over the workgroup
     const uint32_t lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
@@ -1555,7 +1578,7 @@ __global__ __launch_bounds__(256) void k_json_write(const JsonPiece* __restrict_
     if (lane == 63) wsum[wid] = inc;
     __syncthreads();
     uint32_t pre = inc - mine;
-    for (uint32_t w = 0; w < wid; ++w) pre += wsum[w];
+    for (uint32_t q = 0; q < wid; ++q) pre += wsum[q];
     const uint32_t ph = (uint32_t)(dst & 15);  // LDS byte k <-> global byte (dst & ~15) + k
     uint32_t head = ph;
     if (P.flags & kJsonSep) head += 1;
@@ -1569,26 +1592,25 @@ __global__ __launch_bounds__(256) void k_json_write(const JsonPiece* __restrict_
         }
     }
     uint32_t k = head + pre;
-    auto emit = [&](uint32_t v) {
-        if (v >= 100) { js[k++] = (unsigned char)('0' + v / 100); js[k++] = (unsigned char)('0' + (v / 10) % 10); }
-        else if (v >= 10) js[k++] = (unsigned char)('0' + v / 10);
-        js[k++] = (unsigned char)('0' + v % 10);
-        js[k++] = ',';
-    };
-    if (dw) {
-        for (uint32_t i = b0; i < b1; i += 4) {
-            if (i + 4 <= b1) {
-                const uint32_t x = *(const uint32_t*)(lp + i);
 #pragma unroll
-                for (int q = 0; q < 4; ++q) emit((x >> (8 * q)) & 0xFF);
-            } else {
-                for (uint32_t j = i; j < b1; ++j) emit(byte_at(j));
-            }
+    for (int j = 0; j < 16; ++j) {
+        const uint32_t v = (w[j >> 2] >> (8 * (j & 3))) & 0xFF;
+        const uint32_t h = v / 100, t = (v / 10) % 10, o = v % 10;
+        const uint32_t nd = 1 + (v >= 10) + (v >= 100);
+        // characters: [h] [t] o ','  (leading digits only when present)
+        const uint32_t c0 = nd == 3 ? '0' + h : (nd == 2 ? '0' + t : '0' + o);
+        const uint32_t c1 = nd == 3 ? '0' + t : (nd == 2 ? '0' + o : ',');
+        const uint32_t c2 = nd == 3 ? '0' + o : ',';
+        if (j < (int)cnt) {
+            js[k] = (unsigned char)c0;
+            js[k + 1] = (unsigned char)c1;
+            if (nd >= 2) js[k + 2] = (unsigned char)c2;
+            if (nd == 3) js[k + 3] = ',';
+            k += nd + 1;
         }
-    } else {
-        for (uint32_t i = b0; i < b1; ++i) emit(byte_at(i));
     }
     const uint32_t body = wsum[0] + wsum[1] + wsum[2] + wsum[3];  // every byte with a comma
+    static_assert(kJsonChunk == 16 * 256, "one thread per 16 literal bytes");
     uint32_t end = head + body;
     if ((P.flags & kJsonLast) && P.len) end -= 1;  // no comma after the op's last byte
     if (P.flags & kJsonLast) {
@@ -2178,7 +2200,8 @@ hipError_t launch_json_len(const JsonPiece* d_pieces, uint64_t npieces, const ui
     if (!npieces) return hipSuccess;
     if (npieces > 0x7FFFFFFFull) return hipErrorInvalidValue;
     ProfScope ps(prof, s, "k_json_len");
-    hipLaunchKernelGGL(k_json_len, dim3((unsigned)npieces), dim3(256), 0, s, d_pieces, npieces, d_lit, d_len);
+    hipLaunchKernelGGL(k_json_len, dim3(grid_for(npieces * 64, 256)), dim3(256), 0, s, d_pieces, npieces, d_lit,
+                       d_len);
     return hipGetLastError();
 }
 

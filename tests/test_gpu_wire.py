@@ -23,7 +23,7 @@ def _cases():
         if rng.random() < 0.5:
             kind.append(0); a.append(rng.randrange(1 << 40)); b.append(rng.choice([4096, 8192, 17]))
         else:
-            n = rng.choice([1, 2, 99, 16383, 16384, 16385, 40000])
+            n = rng.choice([1, 2, 99, 4095, 4096, 4097, 16383, 16384, 16385, 40000])
             kind.append(1); a.append(pos); b.append(n)
             pos += n
     yield "mixed", kind, a, b, src
