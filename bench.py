@@ -155,6 +155,60 @@ def cpu_xxh3_baseline(buf_dev, offs, lens):
             "sample": f"{k} file(s), {int(lens[:k].sum()) >> 20} MiB, hashed {reps}x (python-xxhash XXH3)"}
 
 
+def cpu_apply_baseline(basis_dev, new_dev, delta, sample_bytes: int = 1 << 30):
+    """The C oracle's apply_delta (applier.rs:22-56 in memory, one thread) on the ops
+    that rebuild the first `sample_bytes` of the same output, repeated for >= 3 s."""
+    import numpy as np
+
+    from oracle import oracle as O
+
+    kind = np.asarray(delta.kind, dtype=np.uint8)
+    a = np.ascontiguousarray(delta.a, dtype=np.uint64)
+    b = np.ascontiguousarray(delta.b, dtype=np.uint64)
+    k = int(np.searchsorted(np.cumsum(b), sample_bytes, side="right"))
+    kind, a, b = np.ascontiguousarray(kind[:k]), a[:k], b[:k]
+    basis_end = int((a + b)[kind == 0].max()) if (kind == 0).any() else 0
+    lit_end = int((a + b)[kind != 0].max()) if (kind != 0).any() else 0
+    basis = basis_dev[:basis_end].cpu().numpy()
+    lit = new_dev[:lit_end].cpu().numpy()
+    total = int(b.sum())
+    out = np.empty(max(total, 1), np.uint8)
+    L = O.C().L
+    reps = 0
+    t0 = time.perf_counter()
+    while True:
+        got = L.oracle_apply_delta(basis.ctypes.data, basis.size, lit.ctypes.data, kind.ctypes.data, a.ctypes.data,
+                                   b.ctypes.data, k, out.ctypes.data, out.size)
+        if got != total:
+            raise RuntimeError("oracle apply failed")
+        reps += 1
+        if time.perf_counter() - t0 >= 3.0:
+            break
+    dt = time.perf_counter() - t0
+    return {"value": round(total * reps / dt / GIB, 3), "unit": "GiB/s", "cores": 1, "kind": "port",
+            "sample": f"{k} ops rebuilding {total >> 20} MiB, applied {reps}x (C oracle, in memory)"}
+
+
+def cpu_local_baseline(src_dev, dst_dev, bs: int, sample_bytes: int = 1 << 30):
+    """The oracle's block-compare loop (local.rs:549-619, one thread) over the first
+    `sample_bytes` of both files, repeated for >= 3 s; bytes compared = 2 x sample."""
+    from oracle import oracle as O
+
+    n = min(sample_bytes, src_dev.numel())
+    src = src_dev[:n].cpu().numpy().tobytes()
+    dst = dst_dev[:n].cpu().numpy().tobytes()
+    reps = 0
+    t0 = time.perf_counter()
+    while True:
+        O.py_block_compare(src, dst, bs)
+        reps += 1
+        if time.perf_counter() - t0 >= 3.0:
+            break
+    dt = time.perf_counter() - t0
+    return {"value": round(2 * n * reps / dt / GIB, 3), "unit": "GiB/s", "cores": 1, "kind": "port",
+            "sample": f"{n >> 20} MiB of each file in {bs >> 10} KiB blocks, compared {reps}x (bytes compared = 2x)"}
+
+
 def shard_range(nunits: int, world: int, rank: int):
     """Contiguous, size-balanced share of `nunits` equal units for `rank` (the LPT
     split when all units have the same size).  No collective: every rank computes
@@ -497,6 +551,10 @@ def main():
             cpu = cpu_json_baseline(new, bs)
         if world == 1 and not args.no_cpu_baseline and args.workload == "xxh3":
             cpu = cpu_xxh3_baseline(basis, xxh_offs, xxh_lens)
+        if world == 1 and not args.no_cpu_baseline and args.workload == "apply":
+            cpu = cpu_apply_baseline(basis, new, apply_d)
+        if world == 1 and not args.no_cpu_baseline and args.workload == "local":
+            cpu = cpu_local_baseline(new, basis, bs)
         hinc = None
         if world == 1 and not args.no_host_inclusive and args.workload == "c3":
             hinc = host_inclusive(dev, bs, min(n, 1 << 30), local)

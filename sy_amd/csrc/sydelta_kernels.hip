@@ -1508,11 +1508,13 @@ __global__ __launch_bounds__(256) void k_json_len(const JsonPiece* __restrict__ 
     }
 }
 
-__device__ __forceinline__ uint32_t put_dec(char* p, uint64_t v) {
-    char t[20];
-    uint32_t n = 0;
-    do { t[n++] = (char)('0' + v % 10); v /= 10; } while (v);
-    for (uint32_t i = 0; i < n; ++i) p[i] = t[n - 1 - i];
+// Decimal digits of v at p (no terminator); returns their count.
+__device__ __forceinline__ uint32_t put_dec(uint8_t* p, uint64_t v) {
+    const uint32_t n = dec_digits(v);
+    for (uint32_t i = n; i-- > 0;) {
+        p[i] = (uint8_t)('0' + v % 10);
+        v /= 10;
+    }
     return n;
 }
 
@@ -1524,19 +1526,18 @@ __global__ __launch_bounds__(256) void k_json_write(const JsonPiece* __restrict_
     const JsonPiece P = pieces[blockIdx.x];
     const uint64_t dst = base + off[blockIdx.x];
     if (!(P.flags & kJsonData)) {
-        if (threadIdx.x == 0) {
-            char t[72];
+        if (threadIdx.x == 0) {  // {"Copy":{"offset":A,"size":B}} straight to global memory
+            uint8_t* o = out + dst;
             uint32_t k = 0;
-            if (P.flags & kJsonSep) t[k++] = ',';
+            if (P.flags & kJsonSep) o[k++] = ',';
             const char* h = "{\"Copy\":{\"offset\":";
-            for (uint32_t i = 0; h[i]; ++i) t[k++] = h[i];
-            k += put_dec(t + k, P.a);
+            for (uint32_t i = 0; h[i]; ++i) o[k++] = h[i];
+            k += put_dec(o + k, P.a);
             const char* m = ",\"size\":";
-            for (uint32_t i = 0; m[i]; ++i) t[k++] = m[i];
-            k += put_dec(t + k, P.b);
-            t[k++] = '}';
-            t[k++] = '}';
-            for (uint32_t i = 0; i < k; ++i) out[dst + i] = (uint8_t)t[i];
+            for (uint32_t i = 0; m[i]; ++i) o[k++] = m[i];
+            k += put_dec(o + k, P.b);
+            o[k++] = '}';
+            o[k++] = '}';
         }
         return;
     }
@@ -1558,7 +1559,9 @@ __global__ __launch_bounds__(256) void k_json_write(const JsonPiece* __restrict_
             w[2] = __builtin_amdgcn_alignbyte(d3, d2, sh); w[3] = __builtin_amdgcn_alignbyte(d4, d3, sh);
         }
     } else {
-        for (uint32_t j = 0; j < cnt; ++j) w[j >> 2] |= (uint32_t)lp[j] << (8 * (j & 3));
+#pragma unroll
+        for (int j = 0; j < 16; ++j)
+            if (j < (int)cnt) w[j >> 2] |= (uint32_t)lp[j] << (8 * (j & 3));
     }
     // text of each byte + its comma: 2-4 characters, branch-free
     uint32_t mine = 0;
