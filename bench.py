@@ -475,8 +475,12 @@ def main():
         nblk = (blen + bs - 1) // bs
         last = blen - (nblk - 1) * bs
         idx = dev.BatchIndex(w, s, nblk, last, bs, device=local, stream=stream)
-        out, tot = dev.match_batch(idx, new, soff, slen, stream=stream)
+        # the per-file op lists stay in the library's batch (host memory), as the
+        # Rust caller would read them through the accessors
+        res = dev.match_batch_handle(idx, new, soff, slen, stream=stream)
         idx.close()
+        tot = res.stats
+        res.close()
         return tot
 
     for _ in range(args.warmup):

@@ -220,6 +220,46 @@ extern "C" int sydelta_signature_batch_device(int device, const uint8_t* d_buf, 
     for (uint64_t f = 0; f < nfiles; ++f) fblk[f + 1] = fblk[f] + (len[f] + block_size - 1) / block_size;
     const uint64_t total = fblk[nfiles];
     if (!total) return SYDELTA_OK;
+    bool fast = block_size % 64 == 0 && block_size >= 256 && block_size <= (1ull << 31);
+    for (uint64_t f = 0; f < nfiles && fast; ++f) fast = !len[f] || ((uintptr_t)(d_buf + off[f]) & 15) == 0;
+    if (fast) {
+        // one table: aoff | agb | apfx (nact + 1) | loff | llen | lidx
+        std::vector<uint64_t> t;
+        t.reserve(6 * nfiles + 1);
+        std::vector<uint64_t> aoff, agb, apfx{0}, loff, llen, lidx;
+        for (uint64_t f = 0; f < nfiles; ++f) {
+            const uint64_t nfull = len[f] / block_size;
+            if (nfull) {
+                aoff.push_back(off[f]);
+                agb.push_back(fblk[f]);
+                apfx.push_back(apfx.back() + nfull);
+            }
+            if (len[f] % block_size) {
+                loff.push_back(off[f] + nfull * block_size);
+                llen.push_back(len[f] % block_size);
+                lidx.push_back(fblk[f] + nfull);
+            }
+        }
+        const uint64_t nact = aoff.size(), npart = loff.size();
+        for (auto* v : {&aoff, &agb, &apfx, &loff, &llen, &lidx}) t.insert(t.end(), v->begin(), v->end());
+        uint64_t* d_t = nullptr;
+        HIP_TRY(hipMallocAsync((void**)&d_t, 8 * t.size(), s));
+        HIP_TRY(hipMemcpyAsync(d_t, t.data(), 8 * t.size(), hipMemcpyHostToDevice, s));
+        const uint64_t* p = d_t;
+        const uint64_t* d_aoff = p; p += nact;
+        const uint64_t* d_agb = p; p += nact;
+        const uint64_t* d_apfx = p; p += nact + 1;
+        const uint64_t* d_loff = p; p += npart;
+        const uint64_t* d_llen = p; p += npart;
+        const uint64_t* d_lidx = p;
+        CallProf cp;
+        hipError_t e = launch_signature_batch_fast(d_buf, d_aoff, d_agb, d_apfx, nact, apfx.back(), d_loff, d_llen,
+                                                   d_lidx, npart, block_size, d_weak, d_strong, s, cp.get());
+        (void)hipFreeAsync(d_t, s);
+        HIP_TRY(e);
+        HIP_TRY(hipStreamSynchronize(s));  // the host table must outlive the copy
+        return SYDELTA_OK;
+    }
     uint64_t* d_meta = nullptr;
     HIP_TRY(hipMallocAsync((void**)&d_meta, sizeof(uint64_t) * (3 * nfiles + 1), s));
     HIP_TRY(hipMemcpyAsync(d_meta, off, 8 * nfiles, hipMemcpyHostToDevice, s));
@@ -604,6 +644,10 @@ int walk_src(const Src& c, uint64_t n, uint64_t entry, uint64_t end, const Basis
     return 0;
 }
 
+double ms_since(std::chrono::steady_clock::time_point t0);
+int walk_threads();
+uint64_t walk_par_min();
+
 int probe_mode_env() {
     const char* e = getenv("SYDELTA_PROBE");  // "0" never, "1" always, unset/other: auto
     if (e && e[0] == '0') return 0;
@@ -686,18 +730,29 @@ int Classifier::probe(int mode) {
         if (hits * 8 < out.size()) return SYDELTA_OK;
     }
     if (int r = run(1, out, pfx)) return r;
-    for (size_t i = 0; i < src.size(); ++i) {
-        Src& c = src[i];
-        c.probed = true;
-        c.ahit.assign(out.begin() + pfx[i], out.begin() + pfx[i + 1]);
-        c.scanned.assign(c.nblk, 0);
-        c.nahit = 0;
-        for (uint32_t v : c.ahit) c.nahit += v != kNoBlk;
-    }
+    auto fill = [&](size_t i0, size_t i1) {
+        for (size_t i = i0; i < i1; ++i) {
+            Src& c = src[i];
+            c.probed = true;
+            c.ahit.assign(out.begin() + pfx[i], out.begin() + pfx[i + 1]);
+            c.scanned.assign(c.nblk, 0);
+            c.nahit = 0;
+            for (uint32_t v : c.ahit) c.nahit += v != kNoBlk;
+        }
+    };
+    const size_t ns = src.size();
+    const int nthr = ns >= 256 ? walk_threads() : 1;
+    std::vector<std::thread> th;
+    for (int t = 1; t < nthr; ++t) th.emplace_back(fill, ns * t / nthr, ns * (t + 1) / nthr);
+    fill(0, ns / nthr);
+    for (auto& x : th) x.join();
     return SYDELTA_OK;
 }
 
 int Classifier::scan(const std::vector<std::array<uint64_t, 3>>& ranges) {
+    static const bool host_timing = getenv("SYDELTA_HOST_TIMING") != nullptr;
+    const auto t0 = std::chrono::steady_clock::now();
+    double t_kern = 0, t_d2h = 0;
     const uint64_t tile = scan_tile_positions();
     const uint64_t seg_max = (1ull << 31) / tile * tile;
     const bool wide = n > scan_max_window();
@@ -783,6 +838,7 @@ int Classifier::scan(const std::vector<std::array<uint64_t, 3>>& ranges) {
     }
     const uint64_t nver = counts[0];
     weak_hits += counts[1];
+    t_kern = ms_since(t0);
     if (!nver) return SYDELTA_OK;
     uint64_t* d_key = (uint64_t*)hit_buf.p;
     uint32_t* d_val = (uint32_t*)(d_key + 2 * cap);
@@ -798,21 +854,49 @@ int Classifier::scan(const std::vector<std::array<uint64_t, 3>>& ranges) {
     HIP_TRY(hipMemcpyAsync(hkey.data(), k_out, nver * 8, hipMemcpyDeviceToHost, s));
     HIP_TRY(hipMemcpyAsync(hval.data(), v_out, nver * 4, hipMemcpyDeviceToHost, s));
     HIP_TRY(hipStreamSynchronize(s));
-    // (segment, position)-sorted; segments are in (source, position) order
-    std::vector<uint64_t> pos;
-    std::vector<uint32_t> blk;
-    size_t h = 0;
-    while (h < nver) {
-        const uint32_t si = seg_src[hkey[h] >> kSegShift];
-        Src& c = src[si];
-        pos.clear();
-        blk.clear();
-        for (; h < nver && seg_src[hkey[h] >> kSegShift] == si; ++h) {
-            const uint64_t p = segs[hkey[h] >> kSegShift].pos_begin + (hkey[h] & 0xFFFFFFFFull);
-            if (p >= c.p0 && p < c.p1) { pos.push_back(p); blk.push_back(hval[h]); }
+    t_d2h = ms_since(t0);
+    // (segment, position)-sorted; segments are in (source, position) order, so each
+    // source's hits are one run; runs are merged into their sources on host threads
+    auto merge_range = [&](size_t h, size_t hend) {
+        std::vector<uint64_t> pos;
+        std::vector<uint32_t> blk;
+        while (h < hend) {
+            const uint32_t si = seg_src[hkey[h] >> kSegShift];
+            Src& c = src[si];
+            pos.clear();
+            blk.clear();
+            for (; h < hend && seg_src[hkey[h] >> kSegShift] == si; ++h) {
+                const uint64_t p = segs[hkey[h] >> kSegShift].pos_begin + (hkey[h] & 0xFFFFFFFFull);
+                if (p >= c.p0 && p < c.p1) { pos.push_back(p); blk.push_back(hval[h]); }
+            }
+            if (c.hpos.empty()) {
+                c.hpos.swap(pos);
+                c.hblk.swap(blk);
+            } else {
+                merge_hits(c, pos, blk);
+            }
         }
-        merge_hits(c, pos, blk);
+    };
+    const int nthr = nver >= (1u << 16) ? walk_threads() : 1;
+    if (nthr > 1) {
+        // split points at source boundaries
+        std::vector<size_t> cut{0};
+        for (int t = 1; t < nthr; ++t) {
+            size_t h = std::max(cut.back(), nver * t / nthr);
+            while (h < nver && h > 0 && seg_src[hkey[h] >> kSegShift] == seg_src[hkey[h - 1] >> kSegShift]) ++h;
+            cut.push_back(h);
+        }
+        cut.push_back(nver);
+        std::vector<std::thread> th;
+        for (int t = 1; t < nthr; ++t) th.emplace_back(merge_range, cut[t], cut[t + 1]);
+        merge_range(cut[0], cut[1]);
+        for (auto& x : th) x.join();
+    } else {
+        merge_range(0, nver);
     }
+    if (host_timing && src.size() > 1)
+        fprintf(stderr, "sydelta scan: %zu segments, %llu hits: setup+kernel %.3f ms, sort+D2H %.3f ms, merge %.3f ms\n",
+                segs.size(), (unsigned long long)nver, t_kern, t_d2h - t_kern, ms_since(t0) - t_d2h);
     return SYDELTA_OK;
 }
 
@@ -875,7 +959,7 @@ int Classifier::walk(size_t i, uint64_t entry, const BasisInfo& bi, bool final_s
         uint64_t need = 0;
         const auto t0 = std::chrono::steady_clock::now();
         const int r = walk_src(c, n, entry, c.p1, bi, final_src, tail_match, ops, exit, &need);
-        if (host_timing)
+        if (host_timing && src.size() == 1)
             fprintf(stderr, "sydelta walk round %d: %.3f ms, %zu ops, need=%d\n", round,
                     std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count(),
                     ops.size(), r);
@@ -1079,30 +1163,67 @@ static int match_impl(sydelta_index* ix, const uint8_t* d_buf, const uint64_t* s
         c.nblk = (c.p1 + n - 1) / n;
     }
     b->total.positions = tot_pos;
+    static const bool host_timing = getenv("SYDELTA_HOST_TIMING") != nullptr;
+    const auto t0 = std::chrono::steady_clock::now();
     const int mode = n > scan_max_window() ? 0 : probe_mode_env();
     if (int r = C.classify(mode)) return r;
+    const double t_cls = ms_since(t0);
     std::vector<size_t> all(nf);
     for (size_t f = 0; f < nf; ++f) all[f] = f;
     std::vector<int> tail;
     if (int r = tail_flags(C, all, tail)) return r;
+    const double t_tail = ms_since(t0);
+    // Many sources: walk them on host threads first (a walk is pure host work over the
+    // classified hits); a source whose walk reaches an unscanned block, and every source
+    // of a small batch, is walked below through Classifier::walk (on-demand scans).
+    std::vector<uint8_t> walked(nf, 0);
+    const int nthr = walk_threads();
+    if (nf >= 64 && nthr > 1) {
+        std::atomic<uint64_t> next{0};
+        auto worker = [&]() {
+            for (;;) {
+                const uint64_t f0 = next.fetch_add(32);
+                if (f0 >= nf) break;
+                for (uint64_t f = f0; f < std::min<uint64_t>(nf, f0 + 32); ++f) {
+                    const Src& c = C.src[f];
+                    if (c.nahit + c.hpos.size() >= walk_par_min()) continue;  // large: parallel walk below
+                    const BasisInfo bi{ix->fblk[f], ix->fblk[f + 1] - ix->fblk[f], ix->last_size[f]};
+                    uint64_t exit = 0, need = 0;
+                    sydelta_delta* d = &b->d[f];
+                    if (walk_src(c, n, 0, c.p1, bi, true, tail[f], d->ops, &exit, &need) == 0) {
+                        walked[f] = 1;
+                        d->stats.verified_hits = c.hpos.size() + c.nahit;
+                        finish_stats(d);
+                    }
+                }
+            }
+        };
+        std::vector<std::thread> th;
+        for (int t = 1; t < nthr; ++t) th.emplace_back(worker);
+        worker();
+        for (auto& x : th) x.join();
+    }
+    const double t_par = ms_since(t0);
     for (uint64_t f = 0; f < nf; ++f) {
         sydelta_delta* d = &b->d[f];
         const BasisInfo bi{ix->fblk[f], ix->fblk[f + 1] - ix->fblk[f], ix->last_size[f]};
         uint64_t exit = 0;
-        if (int r = C.walk(f, 0, bi, true, tail[f], d, &exit)) return r;
-        d->stats.verified_hits = C.src[f].hpos.size() + C.src[f].nahit;
-        finish_stats(d);
+        if (!walked[f]) {
+            if (int r = C.walk(f, 0, bi, true, tail[f], d, &exit)) return r;
+            d->stats.verified_hits = C.src[f].hpos.size() + C.src[f].nahit;
+            finish_stats(d);
+        }
         b->total.verified_hits += d->stats.verified_hits;
         b->total.copy_ops += d->stats.copy_ops;
         b->total.data_ops += d->stats.data_ops;
         b->total.literal_bytes += d->stats.literal_bytes;
-        // the walk is done with this source's hit lists
-        std::vector<uint64_t>().swap(C.src[f].hpos);
-        std::vector<uint32_t>().swap(C.src[f].hblk);
-        std::vector<uint32_t>().swap(C.src[f].ahit);
     }
     b->total.weak_hits = C.weak_hits;
     if (nf == 1) b->d[0].stats.weak_hits = C.weak_hits;
+    if (host_timing && nf > 1)
+        fprintf(stderr,
+                "sydelta match batch: %llu files, classify %.3f ms, tail %.3f ms, threaded walks %.3f ms, rest %.3f ms\n",
+                (unsigned long long)nf, t_cls, t_tail - t_cls, t_par - t_tail, ms_since(t0) - t_par);
     return SYDELTA_OK;
 }
 

@@ -166,6 +166,14 @@ hipError_t launch_xxh_files(const uint8_t* d_buf, const uint64_t* d_off, const u
                             const uint64_t* d_aoff, const uint64_t* d_apfx, uint64_t nact, const uint32_t* d_order,
                             uint64_t nfiles, uint64_t npieces, uint64_t* d_C, uint64_t* d_out,
                             hipStream_t s, Profiler* prof);
+// Batched signature when bs % 64 == 0, bs >= 256 and every file starts 16-byte aligned:
+// full blocks of the nact files with >= 1 (aoff, agb = first global block, apfx = prefix
+// of full-block counts, apfx[nact] = nfull) by the row kernel, then npart listed
+// segments (loff, llen, output slot lidx) one wave each.
+hipError_t launch_signature_batch_fast(const uint8_t* d_buf, const uint64_t* d_aoff, const uint64_t* d_agb,
+                                       const uint64_t* d_apfx, uint64_t nact, uint64_t nfull, const uint64_t* d_loff,
+                                       const uint64_t* d_llen, const uint64_t* d_lidx, uint64_t npart, uint64_t bs,
+                                       uint32_t* d_weak, uint64_t* d_strong, hipStream_t s, Profiler* prof);
 hipError_t launch_synth_fill(uint8_t* d_buf, uint64_t len, uint64_t seed, hipStream_t s, uint64_t first = 0);
 hipError_t launch_synth_edit_blocks(uint8_t* d_dst, uint64_t len, uint64_t bs, uint64_t first, uint64_t seed,
                                     uint32_t rate_ppm, hipStream_t s);

@@ -201,6 +201,65 @@ __global__ __launch_bounds__(256) void k_sig_scalar(const uint8_t* __restrict__ 
     strong[blk] = xxh3_short(buf + off, sz);
 }
 
+// Batched signature, full blocks of 16-byte aligned files with bs % 64 == 0: the K1
+// row layout (one 16-lane row per block, 4 blocks per wave) over a list of files with
+// >= 1 full block: file j starts at aoff[j], its blocks are global blocks agb[j] + k,
+// apfx = prefix of full-block counts (apfx[nact] = nfull).  The wave finds its first
+// block's file by a 64-way search; its four blocks span at most four listed files.
+__global__ __launch_bounds__(256) void k_sig_fast_batch(const uint8_t* __restrict__ buf,
+                                                        const uint64_t* __restrict__ aoff,
+                                                        const uint64_t* __restrict__ agb,
+                                                        const uint64_t* __restrict__ apfx, uint64_t nact,
+                                                        uint64_t nfull, uint32_t bs, uint32_t* __restrict__ weak,
+                                                        uint64_t* __restrict__ strong) {
+    const uint32_t lane = threadIdx.x & 63;
+    const uint64_t w0 = (((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6) << 2;
+    if (w0 >= nfull) return;  // wave-uniform
+    const uint64_t e = min(w0 + (lane >> 4), nfull - 1);
+    uint64_t lo = 0, hi = nact;
+    while (hi - lo > 1) {
+        const uint64_t step = (hi - lo + 63) >> 6;
+        const uint64_t c = lo + lane * step;
+        const uint64_t m = __ballot(c < hi && apfx[c] <= w0);
+        const uint64_t nlo = lo + (63 - __builtin_clzll(m)) * step;
+        hi = min(hi, nlo + step);
+        lo = nlo;
+    }
+    while (apfx[lo + 1] <= e) ++lo;
+    const uint64_t k = e - apfx[lo];
+    uint32_t wk;
+    uint64_t st;
+    row_hash(buf + aoff[lo] + k * (uint64_t)bs, bs, wk, st);
+    if ((lane & 15) == 0 && w0 + (lane >> 4) < nfull) {
+        weak[agb[lo] + k] = wk;
+        strong[agb[lo] + k] = st;
+    }
+}
+
+// Signature of listed segments (partial last blocks): segment i = [loff[i], +llen[i]),
+// output slot lidx[i]; one wave per segment.
+__global__ __launch_bounds__(256) void k_sig_list(const uint8_t* __restrict__ buf, const uint64_t* __restrict__ loff,
+                                                  const uint64_t* __restrict__ llen, const uint64_t* __restrict__ lidx,
+                                                  uint64_t n, uint32_t* __restrict__ weak,
+                                                  uint64_t* __restrict__ strong) {
+    const uint64_t w = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+    if (w >= n) return;
+    const uint8_t* p = buf + loff[w];
+    const uint64_t sz = llen[w];
+    uint32_t wk;
+    uint64_t st;
+    if (sz > 240) {
+        wave_hash_long(p, sz, wk, st);
+    } else {
+        wk = 0; st = 0;
+        if ((threadIdx.x & 63) == 0) { wk = adler_scalar(p, sz); st = xxh3_short(p, sz); }
+    }
+    if ((threadIdx.x & 63) == 0) {
+        weak[lidx[w]] = wk;
+        strong[lidx[w]] = st;
+    }
+}
+
 // Batched signature (many files, shared block size): one wave per block via a
 // block -> file map built on the host side of the launch (file start block prefix).
 __global__ __launch_bounds__(256) void k_sig_batch(const uint8_t* __restrict__ buf, const uint64_t* __restrict__ foff,
@@ -1981,6 +2040,24 @@ hipError_t launch_signature_batch(const uint8_t* d_buf, const uint64_t* d_off, c
     ProfScope ps(prof, s, "k_sig_batch");
     hipLaunchKernelGGL(k_sig_batch, dim3(grid_for(total_blocks * 64, 256)), dim3(256), 0, s, d_buf, d_off, d_len,
                        d_fblk, nfiles, bs, total_blocks, d_weak, d_strong);
+    return hipGetLastError();
+}
+
+hipError_t launch_signature_batch_fast(const uint8_t* d_buf, const uint64_t* d_aoff, const uint64_t* d_agb,
+                                       const uint64_t* d_apfx, uint64_t nact, uint64_t nfull, const uint64_t* d_loff,
+                                       const uint64_t* d_llen, const uint64_t* d_lidx, uint64_t npart, uint64_t bs,
+                                       uint32_t* d_weak, uint64_t* d_strong, hipStream_t s, Profiler* prof) {
+    if (nfull) {
+        ProfScope ps(prof, s, "k_sig_fast_batch");
+        hipLaunchKernelGGL(k_sig_fast_batch, dim3(grid_for((nfull + 3) / 4 * 64, 256)), dim3(256), 0, s, d_buf, d_aoff,
+                           d_agb, d_apfx, nact, nfull, (uint32_t)bs, d_weak, d_strong);
+        if (hipError_t e = hipGetLastError()) return e;
+    }
+    if (npart) {
+        ProfScope ps(prof, s, "k_sig_list");
+        hipLaunchKernelGGL(k_sig_list, dim3(grid_for(npart * 64, 256)), dim3(256), 0, s, d_buf, d_loff, d_llen, d_lidx,
+                           npart, d_weak, d_strong);
+    }
     return hipGetLastError();
 }
 

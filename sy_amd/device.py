@@ -42,7 +42,7 @@ def signature_batch(buf: torch.Tensor, offs, lens, block_size: int, stream=None)
     """Batched signature over many files packed in one device buffer."""
     offs = np.ascontiguousarray(offs, dtype=np.uint64)
     lens = np.ascontiguousarray(lens, dtype=np.uint64)
-    total = int(sum(-(-int(l) // block_size) for l in lens))
+    total = int(((lens + np.uint64(block_size - 1)) // np.uint64(block_size)).sum()) if len(lens) else 0
     weak = torch.empty(max(total, 1), dtype=torch.int32, device=buf.device)
     strong = torch.empty(max(total, 1), dtype=torch.int64, device=buf.device)
     check(lib.sydelta_signature_batch_device(buf.device.index or 0, _ptr(buf), offs.ctypes.data, lens.ctypes.data,
@@ -147,21 +147,54 @@ def _device_delta(h, owner=None) -> DeviceDelta:
                        owner)
 
 
-def match_batch(index: BatchIndex, buf: torch.Tensor, offs, lens, stream=None):
-    """Batched rolling match: source f = buf[offs[f] : offs[f]+lens[f]] against basis f.
-    Returns (list of DeviceDelta, batch totals)."""
+class DeltaBatch:
+    """The library's per-file deltas of one batched match (sydelta_delta_batch), kept
+    in host memory until freed; `delta(f)` / `deltas()` copy them out on demand."""
+
+    def __init__(self, h):
+        self.h = h
+        self.count = int(lib.sydelta_delta_batch_count(h))
+        st = _lib.MatchStatsC()
+        check(lib.sydelta_delta_batch_stats(h, ctypes.byref(st)))
+        self.stats = {f: int(getattr(st, f)) for f, _ in _lib.MatchStatsC._fields_}
+
+    def delta(self, f: int) -> DeviceDelta:
+        return _device_delta(lib.sydelta_delta_batch_get(self.h, f))
+
+    def deltas(self) -> list:
+        return [self.delta(f) for f in range(self.count)]
+
+    def close(self):
+        if self.h:
+            lib.sydelta_delta_batch_free(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+def match_batch_handle(index: BatchIndex, buf: torch.Tensor, offs, lens, stream=None) -> DeltaBatch:
+    """Batched rolling match: source f = buf[offs[f] : offs[f]+lens[f]] against basis f,
+    results left in the library (DeltaBatch)."""
     offs = np.ascontiguousarray(offs, dtype=np.uint64)
     lens = np.ascontiguousarray(lens, dtype=np.uint64)
     h = ctypes.c_void_p()
     check(lib.sydelta_match_batch_device(index.h, _ptr(buf), offs.ctypes.data, lens.ctypes.data, len(lens),
                                          _stream(stream), ctypes.byref(h)))
+    return DeltaBatch(h)
+
+
+def match_batch(index: BatchIndex, buf: torch.Tensor, offs, lens, stream=None):
+    """Batched rolling match: source f = buf[offs[f] : offs[f]+lens[f]] against basis f.
+    Returns (list of DeviceDelta, batch totals)."""
+    b = match_batch_handle(index, buf, offs, lens, stream)
     try:
-        out = [_device_delta(lib.sydelta_delta_batch_get(h, i)) for i in range(int(lib.sydelta_delta_batch_count(h)))]
-        st = _lib.MatchStatsC()
-        check(lib.sydelta_delta_batch_stats(h, ctypes.byref(st)))
-        return out, {f: int(getattr(st, f)) for f, _ in _lib.MatchStatsC._fields_}
+        return b.deltas(), b.stats
     finally:
-        lib.sydelta_delta_batch_free(h)
+        b.close()
 
 
 def match(index: Index, src: torch.Tensor, stream=None, length: int | None = None) -> DeviceDelta:

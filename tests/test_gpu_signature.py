@@ -113,20 +113,25 @@ def test_signature_4gib_sampled(gpu, oracle_c):
     torch.cuda.empty_cache()
 
 
-def test_signature_batch_matches_per_file(gpu, oracle_c):
+@pytest.mark.parametrize("nfiles,align", [(40, 16), (40, 1), (3000, 16)])
+def test_signature_batch_matches_per_file(nfiles, align, gpu, oracle_c):
+    """Row kernel (bs % 64 == 0, 16-byte aligned files: k_sig_fast_batch + k_sig_list
+    for partial blocks), the generic wave kernel otherwise; runs of empty and short
+    files between long ones; 3000 files exercise the 64-way file search."""
     import torch
 
-    rng = random.Random(11)
-    files = [rng.randbytes(rng.choice([0, 1, 100, 4095, 4096, 4097, 20000, 1 << 17])) for _ in range(40)]
+    rng = random.Random(11 + nfiles + align)
+    sizes = [0, 0, 0, 1, 100, 255, 4095, 4096, 4097, 8192, 20000, 1 << 17]
+    files = [rng.randbytes(rng.choice(sizes if nfiles < 100 else sizes[:9])) for _ in range(nfiles)]
     offs, pos = [], 0
     for f in files:
         offs.append(pos)
-        pos += (len(f) + 15) // 16 * 16
+        pos += (len(f) + align - 1) // align * align
     packed = bytearray(pos + 16)
     for o, f in zip(offs, files):
         packed[o:o + len(f)] = f
     buf = torch.frombuffer(packed, dtype=torch.uint8).cuda()
-    for bs in (4096, 1000):
+    for bs in (4096, 1000, 256, 8192):
         w, s = gpu.signature_batch(buf, offs, [len(f) for f in files], bs)
         w = w.cpu().numpy().view(np.uint32).tolist()
         s = s.cpu().numpy().view(np.uint64).tolist()
@@ -134,6 +139,6 @@ def test_signature_batch_matches_per_file(gpu, oracle_c):
         for f in files:
             ew, es, _ = oracle_c.compute_checksums(f, bs)
             m = len(ew)
-            assert w[k:k + m] == ew.tolist() and s[k:k + m] == es.tolist()
+            assert w[k:k + m] == ew.tolist() and s[k:k + m] == es.tolist(), (bs, k)
             k += m
         assert k == len(w)
