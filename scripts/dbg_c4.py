@@ -23,17 +23,19 @@ def step(T):
     idx = dev.BatchIndex(w, s, nblk, last, bs)
     torch.cuda.synchronize(); T["index"] += time.perf_counter() - t; t = time.perf_counter()
     res = dev.match_batch_handle(idx, new, soff, slen)
-    T["match"] += time.perf_counter() - t; t = time.perf_counter()
+    dt = time.perf_counter() - t; T["match"] += dt; T["match_last"] = dt; t = time.perf_counter()
+    import sys
+    print(f"  python match {1e3 * T['match_last']:.2f}" if 'match_last' in T else "", file=sys.stderr)
     idx.close()
     res.close()
     T["free"] += time.perf_counter() - t
 
 
-T = dict(sig=0.0, index=0.0, match=0.0, free=0.0)
+T = dict(sig=0.0, index=0.0, match=0.0, free=0.0, match_last=0.0)
 step(T)
 dev.set_profiling(True)
 dev.profile(reset=True)
-T = dict(sig=0.0, index=0.0, match=0.0, free=0.0)
+T = dict(sig=0.0, index=0.0, match=0.0, free=0.0, match_last=0.0)
 for _ in range(3):
     step(T)
 prof = dev.profile(reset=True)
