@@ -554,6 +554,7 @@ struct Src {
     std::vector<uint8_t> scanned;  // probed: per block, all its window starts were scanned
     std::vector<uint64_t> hpos;    // hits found by scans, sorted, unique
     std::vector<uint32_t> hblk;    // their global block indices
+    std::vector<uint64_t> ppos;    // probed: per block, its phase-probed window start or kUnknownNone
 };
 
 // Merge sorted (pos, blk) lists into c's hits (equal positions carry equal blocks).
@@ -584,7 +585,10 @@ uint64_t first_unknown(const Src& c, uint64_t n, uint64_t x, uint64_t p) {
     const uint64_t kend = std::min(c.kb + c.nblk, (p - 1) / n + 1);
     for (uint64_t k = std::max(c.kb, x / n); k < kend; ++k) {
         if (c.scanned[k - c.kb]) continue;
-        const uint64_t lo = std::max(x, k * n + 1), hi = std::min(p, k * n + n);
+        uint64_t lo = std::max(x, k * n + 1);
+        const uint64_t hi = std::min(p, k * n + n);
+        // a phase-probed window start inside the block is classified too
+        if (lo < hi && !c.ppos.empty() && c.ppos[k - c.kb] == lo) ++lo;
         if (lo < hi) return lo;
     }
     return kUnknownNone;
@@ -672,6 +676,13 @@ double ms_since(std::chrono::steady_clock::time_point t0);
 int walk_threads();
 uint64_t walk_par_min();
 
+bool phase_probe_on() {
+    // "1": probe long miss runs at their phase (opt-in: on the C4 shape the unaligned
+    // window probes and the extra hit merges cost more host time than the scan they save)
+    const char* e = getenv("SYDELTA_PHASE_PROBE");
+    return e && e[0] == '1';
+}
+
 int probe_mode_env() {
     const char* e = getenv("SYDELTA_PROBE");  // "0" never, "1" always, unset/other: auto
     if (e && e[0] == '0') return 0;
@@ -696,6 +707,12 @@ struct Classifier {
     // Scan blocks [ka, kz) of source si for every (si, ka, kz); hits merged, blocks marked.
     int scan(const std::vector<std::array<uint64_t, 3>>& ranges);
     int classify(int mode);
+    // Probe window starts k*n + phi for blocks [k0, k0 + cnt) of source si, for every
+    // job {si, k0 (local block), cnt, phi}: hits are merged into the sources' hit lists,
+    // every probed start is recorded in ppos, and the blocks that missed are appended
+    // to `missed` as scan ranges.
+    int phase_probe(const std::vector<std::array<uint64_t, 4>>& jobs,
+                    std::vector<std::array<uint64_t, 3>>& missed);
     // Walk source i from entry, scanning on demand what the walk needs.
     int walk(size_t i, uint64_t entry, const BasisInfo& bi, bool final_src, int tail_match, sydelta_delta* d,
              uint64_t* exit);
@@ -928,13 +945,34 @@ double ms_since(std::chrono::steady_clock::time_point t0) {
     return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
 }
 
+// Scan ranges of one source, merged when closer than a scan tile (aligned-hit blocks
+// between them are scanned too: cheaper than another tile).
+void merge_ranges(std::vector<std::array<uint64_t, 3>>& r, uint64_t gap_blocks) {
+    std::vector<std::array<uint64_t, 3>> out;
+    for (auto& x : r) {
+        if (!out.empty() && out.back()[0] == x[0] && x[1] >= out.back()[2] && x[1] - out.back()[2] < gap_blocks)
+            out.back()[2] = std::max(out.back()[2], x[2]);
+        else
+            out.push_back(x);
+    }
+    r.swap(out);
+}
+
 int Classifier::classify(int mode) {
     static const bool host_timing = getenv("SYDELTA_HOST_TIMING") != nullptr;
     const auto t0 = std::chrono::steady_clock::now();
     if (int r = probe(mode)) return r;
     const double t_probe = ms_since(t0);
     const uint64_t gap_blocks = std::max<uint64_t>(1, scan_tile_positions() / n);
+    // Runs of blocks whose aligned window missed.  A short run is scanned.  A long run
+    // (an insertion or deletion shifts everything after it) gets its first block scanned;
+    // its first hit there gives the phase phi the walk will continue at, so the run's
+    // other blocks are probed at k*n + phi (one window each) and only the blocks whose
+    // phase window misses are scanned.  Anything the walk still needs is scanned on
+    // demand (Classifier::walk), so the op list does not depend on these guesses.
+    constexpr uint64_t kPhaseRun = 8;
     std::vector<std::array<uint64_t, 3>> ranges;
+    std::vector<std::array<uint64_t, 3>> runs;  // long runs: source, first, end (local blocks)
     for (size_t i = 0; i < src.size(); ++i) {
         const Src& c = src[i];
         if (!c.nblk) continue;
@@ -942,28 +980,116 @@ int Classifier::classify(int mode) {
             ranges.push_back({i, c.kb, c.kb + c.nblk});
             continue;
         }
-        // runs of blocks whose aligned window did not hit; runs closer than a tile merge
         uint64_t k = 0;
         while (k < c.nblk) {
             if (c.ahit[k] != kNoBlk) { ++k; continue; }
             uint64_t e = k + 1;
-            for (;;) {
-                while (e < c.nblk && c.ahit[e] == kNoBlk) ++e;
-                uint64_t g = e;
-                while (g < c.nblk && c.ahit[g] != kNoBlk && g - e < gap_blocks) ++g;
-                if (g < c.nblk && c.ahit[g] == kNoBlk && g - e < gap_blocks) { e = g; continue; }
-                break;
+            while (e < c.nblk && c.ahit[e] == kNoBlk) ++e;
+            if (e - k >= kPhaseRun && phase_probe_on()) {
+                ranges.push_back({i, c.kb + k, c.kb + k + 2});
+                runs.push_back({i, k, e});
+            } else {
+                ranges.push_back({i, c.kb + k, c.kb + e});
             }
-            ranges.push_back({i, c.kb + k, c.kb + e});
             k = e;
         }
     }
+    merge_ranges(ranges, gap_blocks);
     const auto t1 = std::chrono::steady_clock::now();
-    const int r = scan(ranges);
+    int r = scan(ranges);
+    const double t_scan1 = ms_since(t1);
+    if (r || runs.empty()) {
+        if (host_timing)
+            fprintf(stderr, "sydelta classify: probe %.3f ms, ranges %zu (%.3f ms), scan %.3f ms\n", t_probe,
+                    ranges.size(), std::chrono::duration<double, std::milli>(t1 - t0).count() - t_probe, t_scan1);
+        return r;
+    }
+    // phase of each long run: the first hit in its first two blocks (the block holding
+    // an insertion has no hit; the next one hits at the shifted phase)
+    std::vector<std::array<uint64_t, 4>> jobs;
+    std::vector<std::array<uint64_t, 3>> rest;
+    for (auto& run : runs) {
+        const Src& c = src[run[0]];
+        const uint64_t k = run[1], e = run[2];
+        const uint64_t b0 = (c.kb + k) * n;
+        auto it = std::lower_bound(c.hpos.begin(), c.hpos.end(), b0);
+        if (it == c.hpos.end() || *it >= b0 + 2 * n) {
+            rest.push_back({run[0], c.kb + k + 2, c.kb + e});
+            continue;
+        }
+        const uint64_t phi = (*it - b0) % n;
+        // blocks k+2 .. whose phase window starts inside [p0, p1) (k, k+1 are scanned)
+        uint64_t last = e;
+        while (last > k + 2 && (c.kb + last - 1) * n + phi >= c.p1) --last;
+        if (last > k + 2) jobs.push_back({run[0], k + 2, last - (k + 2), phi});
+        if (last < e) rest.push_back({run[0], c.kb + std::max(last, k + 2), c.kb + e});
+    }
+    const auto t2 = std::chrono::steady_clock::now();
+    if ((r = phase_probe(jobs, rest))) return r;
+    const double t_phase = ms_since(t2);
+    std::sort(rest.begin(), rest.end());
+    merge_ranges(rest, gap_blocks);
+    const auto t3 = std::chrono::steady_clock::now();
+    r = scan(rest);
     if (host_timing)
-        fprintf(stderr, "sydelta classify: probe %.3f ms, ranges %zu (%.3f ms), scan %.3f ms\n", t_probe,
-                ranges.size(), std::chrono::duration<double, std::milli>(t1 - t0).count() - t_probe, ms_since(t1));
+        fprintf(stderr, "sydelta classify: probe %.3f ms, ranges %zu (%.3f ms), scan %.3f ms, phase probe %zu runs "
+                "%.3f ms, scan of %zu missed ranges %.3f ms\n", t_probe, ranges.size(),
+                std::chrono::duration<double, std::milli>(t1 - t0).count() - t_probe, t_scan1, jobs.size(), t_phase,
+                rest.size(), ms_since(t3));
     return r;
+}
+
+int Classifier::phase_probe(const std::vector<std::array<uint64_t, 4>>& jobs,
+                            std::vector<std::array<uint64_t, 3>>& missed) {
+    if (jobs.empty()) return SYDELTA_OK;
+    std::vector<ProbeJob> pj;
+    pj.reserve(jobs.size());
+    uint64_t np = 0;
+    bool fast = n % 64 == 0 && n >= 256;
+    for (auto& j : jobs) {
+        const Src& c = src[j[0]];
+        pj.push_back({c.off + j[3], c.kb + j[1], np, c.file, 0});
+        fast = fast && ((uintptr_t)(base + c.off + j[3]) & 15) == 0;
+        np += j[2];
+    }
+    DevBuf jb;
+    const size_t jbytes = (pj.size() * sizeof(ProbeJob) + 255) & ~(size_t)255;
+    const size_t obytes = (np * 4 + 255) & ~(size_t)255;
+    HIP_TRY(hipMallocAsync(&jb.p, jbytes + 2 * obytes + np * 8, s));
+    jb.s = s;
+    uint32_t* d_out = (uint32_t*)((uint8_t*)jb.p + jbytes);
+    uint32_t* d_pw = (uint32_t*)((uint8_t*)jb.p + jbytes + obytes);
+    uint64_t* d_pst = (uint64_t*)((uint8_t*)jb.p + jbytes + 2 * obytes);
+    HIP_TRY(hipMemcpyAsync(jb.p, pj.data(), pj.size() * sizeof(ProbeJob), hipMemcpyHostToDevice, s));
+    HIP_TRY(launch_probe(base, (const ProbeJob*)jb.p, (uint32_t)pj.size(), np, 1, (uint32_t)n, fast, ix->ix, d_pw,
+                         d_pst, d_out, s, prof));
+    std::vector<uint32_t> out(np);
+    HIP_TRY(hipMemcpyAsync(out.data(), d_out, np * 4, hipMemcpyDeviceToHost, s));
+    HIP_TRY(hipStreamSynchronize(s));
+    uint64_t w = 0;
+    std::vector<uint64_t> pos;
+    std::vector<uint32_t> blk;
+    for (auto& j : jobs) {
+        Src& c = src[j[0]];
+        if (c.ppos.empty()) c.ppos.assign(c.nblk, kUnknownNone);
+        pos.clear();
+        blk.clear();
+        for (uint64_t t = 0; t < j[2]; ++t, ++w) {
+            const uint64_t k = j[1] + t;  // local block
+            const uint64_t q = (c.kb + k) * n + j[3];
+            c.ppos[k] = q;
+            if (out[w] != kNoBlk) {
+                pos.push_back(q);
+                blk.push_back(out[w]);
+            } else if (!missed.empty() && missed.back()[0] == j[0] && missed.back()[2] == c.kb + k) {
+                missed.back()[2] = c.kb + k + 1;
+            } else {
+                missed.push_back({j[0], c.kb + k, c.kb + k + 1});
+            }
+        }
+        merge_hits(c, pos, blk);
+    }
+    return SYDELTA_OK;
 }
 
 int Classifier::walk(size_t i, uint64_t entry, const BasisInfo& bi, bool final_src, int tail_match, sydelta_delta* d,

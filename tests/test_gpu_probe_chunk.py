@@ -320,3 +320,75 @@ def test_parallel_walk_in_chunks(nchunks, par_walk, gpu, oracle_c):
     d = _chunked(gpu, src, idx, bs, [0] + [c * bs for c in cuts] + [npos])
     idx.close()
     assert d.tuples() == _oracle_ops(oracle_c, src, basis, bs)
+
+
+@pytest.mark.parametrize("phase", ["0", "1"], ids=["scan-runs", "phase-probe"])
+@pytest.mark.parametrize("bs", [256, 1000, 4096])
+def test_phase_probe_shifted_runs(bs, phase, gpu, oracle_c, monkeypatch):
+    """Long runs of aligned misses (C4 shape: one insertion, then substitutions and a
+    second insertion/deletion inside the shifted region): the phase probe classifies
+    one window per block at the run's phase; the op list equals the oracle's."""
+    monkeypatch.setenv("SYDELTA_PROBE", "1")
+    monkeypatch.setenv("SYDELTA_PHASE_PROBE", phase)
+    rng = random.Random(bs * 3 + int(phase))
+    for case in range(6):
+        basis = rng.randbytes(rng.randint(60, 200) * bs + rng.randint(0, bs - 1))
+        src = bytearray(basis)
+        a = rng.randrange(len(src) // 4)
+        src[a:a] = rng.randbytes(rng.randint(1, 3))                    # phase shift
+        for _ in range(rng.randint(0, 12)):                            # substitutions
+            src[rng.randrange(a, len(src))] ^= 0x5A
+        if case % 2:
+            b = rng.randrange(a + 20 * bs, len(src) - 2 * bs)          # second shift in the run
+            if rng.random() < 0.5:
+                src[b:b] = rng.randbytes(rng.randint(1, 5))
+            else:
+                del src[b:b + rng.randint(1, 5)]
+        if case == 5:
+            src[-3 * bs:] = rng.randbytes(3 * bs)                      # literal tail
+        src = bytes(src)
+        idx = _index(gpu, basis, bs)
+        d = gpu.match(idx, _to_dev(src), length=len(src))
+        idx.close()
+        assert d.tuples() == _oracle_ops(oracle_c, src, basis, bs), case
+
+
+def test_phase_probe_batch_c4_shape(gpu, oracle_c, monkeypatch):
+    """Batched match of 64 files with one insertion + 16 substitutions each (BASELINE
+    C4's edit shape, 64 KiB files): every file's op list equals the oracle's."""
+    import torch
+
+    monkeypatch.setenv("SYDELTA_PROBE", "1")
+    bs = 4096
+    rng = random.Random(44)
+    bases, news = [], []
+    for f in range(64):
+        b = rng.randbytes(64 * 1024)
+        s = bytearray(b)
+        p = rng.randrange(len(s) + 1)
+        s[p:p] = bytes([rng.randrange(256)])
+        for _ in range(16):
+            s[rng.randrange(len(s))] ^= rng.randrange(1, 256)
+        bases.append(b)
+        news.append(bytes(s))
+
+    def pack(files):
+        offs, pos = [], 0
+        for f in files:
+            offs.append(pos)
+            pos += (len(f) + 15) // 16 * 16
+        buf = bytearray(pos + 16)
+        for o, f in zip(offs, files):
+            buf[o:o + len(f)] = f
+        return torch.frombuffer(buf, dtype=torch.uint8).cuda(), offs, [len(f) for f in files]
+
+    bbuf, boff, blen = pack(bases)
+    sbuf, soff, slen = pack(news)
+    w, s = gpu.signature_batch(bbuf, boff, blen, bs)
+    nblk = [-(-x // bs) for x in blen]
+    last = [x - (k - 1) * bs for x, k in zip(blen, nblk)]
+    idx = gpu.BatchIndex(w, s, nblk, last, bs)
+    ds, _ = gpu.match_batch(idx, sbuf, soff, slen)
+    idx.close()
+    for f in range(64):
+        assert ds[f].tuples() == _oracle_ops(oracle_c, news[f], bases[f], bs), f
