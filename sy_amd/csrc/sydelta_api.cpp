@@ -555,11 +555,17 @@ struct Src {
     std::vector<uint64_t> hpos;    // hits found by scans, sorted, unique
     std::vector<uint32_t> hblk;    // their global block indices
     std::vector<uint64_t> ppos;    // probed: per block, its phase-probed window start or kUnknownNone
+    std::vector<uint32_t> phit;    // ... and that window's hit or kNoBlk
 };
 
 // Merge sorted (pos, blk) lists into c's hits (equal positions carry equal blocks).
 void merge_hits(Src& c, const std::vector<uint64_t>& pos, const std::vector<uint32_t>& blk) {
     if (pos.empty()) return;
+    if (c.hpos.empty() || pos.front() > c.hpos.back()) {  // later positions: append
+        c.hpos.insert(c.hpos.end(), pos.begin(), pos.end());
+        c.hblk.insert(c.hblk.end(), blk.begin(), blk.end());
+        return;
+    }
     std::vector<uint64_t> np;
     std::vector<uint32_t> nb;
     np.reserve(c.hpos.size() + pos.size());
@@ -628,6 +634,8 @@ int walk_src(const Src& c, uint64_t n, uint64_t entry, uint64_t end, const Basis
     const size_t H = c.hpos.size();
     const uint64_t kend = c.kb + c.nblk;
     uint64_t ka = c.kb;  // next aligned window that may hit (probed sources)
+    uint64_t kp = c.kb;  // next block whose phase-probed window may hit
+    const bool has_phase = c.probed && !c.ppos.empty();
     while (x < end) {
         // next hit at or after x and before end: the next scan hit or the next aligned hit
         while (i < H && c.hpos[i] < x) ++i;
@@ -638,6 +646,16 @@ int walk_src(const Src& c, uint64_t n, uint64_t entry, uint64_t end, const Basis
             if (ka * n < x) ka = (x + n - 1) / n;  // after an aligned Copy x == (ka+1)*n: no division
             while (ka < kend && ka * n < p && c.ahit[ka - c.kb] == kNoBlk) ++ka;
             if (ka < kend && ka * n < p) { p = ka * n; pb = c.ahit[ka - c.kb]; }
+            if (has_phase) {  // phase-probed hits (one window per block, inside it)
+                if (kp * n + n <= x) kp = x / n;
+                while (kp < kend && kp * n < p &&
+                       (c.ppos[kp - c.kb] < x || c.ppos[kp - c.kb] == kUnknownNone || c.phit[kp - c.kb] == kNoBlk))
+                    ++kp;
+                if (kp < kend && c.ppos[kp - c.kb] < p && c.ppos[kp - c.kb] >= x && c.phit[kp - c.kb] != kNoBlk) {
+                    p = c.ppos[kp - c.kb];
+                    pb = c.phit[kp - c.kb];
+                }
+            }
         }
         const uint64_t u = first_unknown(c, n, x, p);
         if (u != kUnknownNone) {
@@ -1067,27 +1085,22 @@ int Classifier::phase_probe(const std::vector<std::array<uint64_t, 4>>& jobs,
     HIP_TRY(hipMemcpyAsync(out.data(), d_out, np * 4, hipMemcpyDeviceToHost, s));
     HIP_TRY(hipStreamSynchronize(s));
     uint64_t w = 0;
-    std::vector<uint64_t> pos;
-    std::vector<uint32_t> blk;
     for (auto& j : jobs) {
         Src& c = src[j[0]];
-        if (c.ppos.empty()) c.ppos.assign(c.nblk, kUnknownNone);
-        pos.clear();
-        blk.clear();
+        if (c.ppos.empty()) {
+            c.ppos.assign(c.nblk, kUnknownNone);
+            c.phit.assign(c.nblk, kNoBlk);
+        }
         for (uint64_t t = 0; t < j[2]; ++t, ++w) {
             const uint64_t k = j[1] + t;  // local block
-            const uint64_t q = (c.kb + k) * n + j[3];
-            c.ppos[k] = q;
-            if (out[w] != kNoBlk) {
-                pos.push_back(q);
-                blk.push_back(out[w]);
-            } else if (!missed.empty() && missed.back()[0] == j[0] && missed.back()[2] == c.kb + k) {
+            c.ppos[k] = (c.kb + k) * n + j[3];
+            c.phit[k] = out[w];
+            if (out[w] != kNoBlk) continue;
+            if (!missed.empty() && missed.back()[0] == j[0] && missed.back()[2] == c.kb + k)
                 missed.back()[2] = c.kb + k + 1;
-            } else {
+            else
                 missed.push_back({j[0], c.kb + k, c.kb + k + 1});
-            }
         }
-        merge_hits(c, pos, blk);
     }
     return SYDELTA_OK;
 }

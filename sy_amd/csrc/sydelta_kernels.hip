@@ -42,16 +42,30 @@ typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
 struct RowPiece {
     uint4 v[4];
 };
+template <bool kAligned = true>
 __device__ __forceinline__ void load_piece(const uint8_t* __restrict__ p, uint32_t slot, uint32_t q, uint32_t lim,
                                            RowPiece& r) {
-    // bytes [0, lim) of the piece are valid (lim <= 1024); the rest reads as zero
+    // bytes [0, lim) of the piece are valid (lim <= 1024, a multiple of 16 here); the
+    // rest reads as zero.  Unaligned pieces: a 4-byte aligned 16-byte load plus one
+    // dword, funnel-shifted (alignbyte) into place.
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
         const uint32_t off = ((slot + 4 * k) << 6) + (q << 4);
         r.v[k] = make_uint4(0, 0, 0, 0);
         if (off < lim) {
-            const u32x4 x = __builtin_nontemporal_load((const u32x4*)(p + off));
-            r.v[k] = make_uint4(x.x, x.y, x.z, x.w);
+            if (kAligned) {
+                const u32x4 x = __builtin_nontemporal_load((const u32x4*)(p + off));
+                r.v[k] = make_uint4(x.x, x.y, x.z, x.w);
+            } else {
+                const uintptr_t u = (uintptr_t)(p + off);
+                const uint32_t sh = (uint32_t)(u & 3);
+                const uint32_t* w = (const uint32_t*)(u & ~(uintptr_t)3);
+                u32x4 x;
+                __builtin_memcpy(&x, w, 16);
+                const uint32_t d4 = sh ? w[4] : 0u;
+                r.v[k] = make_uint4(__builtin_amdgcn_alignbyte(x.y, x.x, sh), __builtin_amdgcn_alignbyte(x.z, x.y, sh),
+                                    __builtin_amdgcn_alignbyte(x.w, x.z, sh), __builtin_amdgcn_alignbyte(d4, x.w, sh));
+            }
         }
     }
 }
@@ -97,6 +111,7 @@ __device__ __forceinline__ void hash_piece(const RowPiece& r, uint32_t slot, uin
 // Hash of the window [base, base + bs) of this lane's row; the result is valid in
 // the row's first lane (lane & 15 == 0).  All four rows of the wave must call it
 // (DPP inside rows only; rows may pass different windows of the same bs).
+template <bool kAligned = true>
 __device__ __forceinline__ void row_hash(const uint8_t* __restrict__ base, uint32_t bs, uint32_t& weak_out,
                                          uint64_t& strong_out) {
     const uint32_t lane = threadIdx.x & 63;
@@ -116,10 +131,10 @@ __device__ __forceinline__ void row_hash(const uint8_t* __restrict__ base, uint3
     uint32_t asum = 0, vsum = 0;
     uint64_t bpos = 0;
     RowPiece cur, nxt;
-    load_piece(base, slot, q, npieces > 1 ? 1024u : bs, cur);
+    load_piece<kAligned>(base, slot, q, npieces > 1 ? 1024u : bs, cur);
     for (uint32_t j = 0; j + 1 < npieces; ++j) {  // full pieces, each followed by a scramble
         const uint32_t nlim = (j + 2 < npieces) ? 1024u : bs - ((j + 1) << 10);
-        load_piece(base + ((j + 1) << 10), slot, q, nlim, nxt);
+        load_piece<kAligned>(base + ((j + 1) << 10), slot, q, nlim, nxt);
         uint64_t c_lo, c_hi;
         hash_piece<false>(cur, slot, q, j << 10, bs, kk0, kk1, 0, 0, k0l, k1l, asum, vsum, bpos, c_lo, c_hi);
         acc_lo = scramble1(acc_lo + c_lo, sk0);
@@ -450,6 +465,7 @@ __global__ __launch_bounds__(256) void k_probe(const uint8_t* __restrict__ base,
 
 // Pass 1, aligned windows (n % 64 == 0, n >= 256, 16-byte aligned): four windows
 // per wave, one per row (row_hash, the signature kernel's layout).
+template <bool kAligned>
 __global__ __launch_bounds__(256) void k_probe_rows(const uint8_t* __restrict__ base,
                                                     const ProbeJob* __restrict__ jobs, uint32_t njobs,
                                                     uint64_t nprobes, uint32_t stride, uint32_t n,
@@ -463,7 +479,7 @@ __global__ __launch_bounds__(256) void k_probe_rows(const uint8_t* __restrict__ 
     const uint64_t k = J.k0 + (wl - J.pfx) * stride;
     uint32_t wk;
     uint64_t st;
-    row_hash(base + J.src + k * n, n, wk, st);
+    row_hash<kAligned>(base + J.src + k * n, n, wk, st);
     if ((lane & 15) == 0 && live) {
         pw[w] = wk;
         pst[w] = st;
@@ -2113,8 +2129,11 @@ hipError_t launch_probe(const uint8_t* d_base, const ProbeJob* d_jobs, uint32_t 
     {
         ProfScope ps(prof, s, stride > 1 ? "k_probe_sample" : "k_probe");
         if (fast)
-            hipLaunchKernelGGL(k_probe_rows, dim3(grid_for((nprobes + 3) / 4 * 64, 256)), dim3(256), 0, s, d_base,
-                               d_jobs, njobs, nprobes, stride, n, d_pw, d_pst);
+            hipLaunchKernelGGL(k_probe_rows<true>, dim3(grid_for((nprobes + 3) / 4 * 64, 256)), dim3(256), 0, s,
+                               d_base, d_jobs, njobs, nprobes, stride, n, d_pw, d_pst);
+        else if (n % 64 == 0 && n >= 256)  // any alignment: funnel-shifted row loads
+            hipLaunchKernelGGL(k_probe_rows<false>, dim3(grid_for((nprobes + 3) / 4 * 64, 256)), dim3(256), 0, s,
+                               d_base, d_jobs, njobs, nprobes, stride, n, d_pw, d_pst);
         else
             hipLaunchKernelGGL(k_probe, dim3(grid_for(nprobes * 64, 256)), dim3(256), 0, s, d_base, d_jobs, njobs,
                                nprobes, stride, n, d_pw, d_pst);
