@@ -261,3 +261,40 @@ def test_batch_1mib_files_c4_shape(gpu, oracle_c):
     out, _ = _batch_device(gpu, pairs, 4096)
     for (src, basis), d in zip(pairs, out):
         assert d.tuples() == _oracle_ops(oracle_c, src, basis, 4096)
+
+
+def test_match_past_4gib_properties(gpu):
+    """A 5 GiB source (positions past 2^32, scan segments past 2^31 positions, a
+    partial last block): one 1-byte insertion at 3 GiB and 1% of 8 KiB blocks edited.
+    The op list tiles the source, apply(delta) rebuilds it bit-exactly on the device,
+    and every block away from an edit is copied."""
+    import torch
+
+    bs = 8192
+    n = (5 << 30) + 1234
+    m = 3 << 30
+    basis = torch.empty(n + 16, dtype=torch.uint8, device="cuda")
+    gpu.synth_fill_range(basis[:n], 0, 0x5E1D0009)
+    src = torch.empty(n + 1 + 16, dtype=torch.uint8, device="cuda")
+    src[:m] = basis[:m]
+    src[m] = 0x5A
+    src[m + 1:n + 1] = basis[m:n]
+    gpu.synth_mutate_blocks(src[:n + 1], src[:n + 1], 0, bs, 0x5E1D000A, 10000)
+    L = n + 1
+    w, s = gpu.signature(basis[:n], bs)
+    idx = gpu.Index(w, s, bs, n - (w.numel() - 1) * bs)
+    d = gpu.match(idx, src, length=L)
+    idx.close()
+    kind = np.asarray(d.kind)
+    a = np.asarray(d.a, dtype=np.uint64)
+    b = np.asarray(d.b, dtype=np.uint64)
+    assert int(b.sum()) == L
+    pos = np.concatenate([[0], np.cumsum(b)[:-1]]).astype(np.uint64)
+    data = kind == 1
+    assert np.array_equal(a[data], pos[data])  # Data ops name their own source bytes
+    assert d.stats["copy_ops"] > 0.97 * (n // bs)
+    assert (pos[~data] > (1 << 32)).any()  # copies found past 4 GiB of positions
+    out = torch.empty(L + 16, dtype=torch.uint8, device="cuda")
+    rebuilt, st = gpu.apply_device(basis[:n], d, src[:L], out=out)
+    assert st["bytes_written"] == L
+    assert torch.equal(rebuilt, src[:L])
