@@ -119,6 +119,17 @@ std::map<std::string, std::pair<double, uint64_t>> g_prof;
 }  // namespace
 
 int sydelta::ensure_device(int device) { return ensure_device_impl(device); }
+int sydelta::host_exception() {
+    try {
+        throw;
+    } catch (const std::bad_alloc&) {
+        return fail(SYDELTA_E_OOM, "out of host memory");
+    } catch (const std::exception& e) {
+        return fail(SYDELTA_E_INVAL, "%s", e.what());
+    } catch (...) {
+        return fail(SYDELTA_E_INVAL, "unexpected host error");
+    }
+}
 hipStream_t sydelta::thread_stream(int device) { return thread_stream_impl(device); }
 
 namespace sydelta {
@@ -198,12 +209,14 @@ extern "C" size_t sydelta_profile_json(char* buf, size_t cap, int reset) {
 // ---------------------------------------------------------------------------
 // small utilities
 // ---------------------------------------------------------------------------
-extern "C" int sydelta_device_count(int* count) {
+extern "C" int sydelta_device_count(int* count) try {
     if (!count) return fail(SYDELTA_E_INVAL, "count is NULL");
     int n = 0;
     if (hipGetDeviceCount(&n) != hipSuccess) n = 0;
     *count = n;
     return SYDELTA_OK;
+} catch (...) {
+    return sydelta::host_exception();
 }
 
 // mod.rs:20-23
@@ -222,7 +235,7 @@ static uint32_t ceil_log2(uint64_t v) {
 // signature
 // ---------------------------------------------------------------------------
 extern "C" int sydelta_signature_device(int device, const uint8_t* d_buf, uint64_t len, uint64_t block_size,
-                                        uint32_t* d_weak, uint64_t* d_strong, void* stream) {
+                                        uint32_t* d_weak, uint64_t* d_strong, void* stream) try {
     if (block_size == 0) return fail(SYDELTA_E_INVAL, "block_size must be > 0");
     if (len && (!d_buf || !d_weak || !d_strong)) return fail(SYDELTA_E_INVAL, "NULL device pointer");
     if (int r = ensure_device(device)) return r;
@@ -231,11 +244,13 @@ extern "C" int sydelta_signature_device(int device, const uint8_t* d_buf, uint64
     HIP_TRY(launch_signature(d_buf, len, block_size, d_weak, d_strong, s, cp.get()));
     if (!stream || cp.get()) HIP_TRY(hipStreamSynchronize(s));
     return SYDELTA_OK;
+} catch (...) {
+    return sydelta::host_exception();
 }
 
 extern "C" int sydelta_signature_batch_device(int device, const uint8_t* d_buf, const uint64_t* off,
                                               const uint64_t* len, uint64_t nfiles, uint64_t block_size,
-                                              uint32_t* d_weak, uint64_t* d_strong, void* stream) {
+                                              uint32_t* d_weak, uint64_t* d_strong, void* stream) try {
     if (block_size == 0) return fail(SYDELTA_E_INVAL, "block_size must be > 0");
     if (nfiles && (!off || !len)) return fail(SYDELTA_E_INVAL, "NULL segment table");
     if (int r = ensure_device(device)) return r;
@@ -296,6 +311,8 @@ extern "C" int sydelta_signature_batch_device(int device, const uint8_t* d_buf, 
     HIP_TRY(e);
     HIP_TRY(hipStreamSynchronize(s));  // the host segment table must outlive the copies
     return SYDELTA_OK;
+} catch (...) {
+    return sydelta::host_exception();
 }
 
 // ---------------------------------------------------------------------------
@@ -416,18 +433,22 @@ static int index_create_impl(int device, const uint32_t* weak, const uint64_t* s
 
 extern "C" int sydelta_index_create(int device, const uint32_t* weak, const uint64_t* strong, uint64_t nblocks,
                                     uint64_t block_size, uint64_t last_size, int arrays_on_device, void* stream,
-                                    sydelta_index** out) {
+                                    sydelta_index** out) try {
     const uint64_t last = nblocks ? last_size : 0;
     return index_create_impl(device, weak, strong, &nblocks, &last, 1, block_size, arrays_on_device, stream, out);
+} catch (...) {
+    return sydelta::host_exception();
 }
 
 extern "C" int sydelta_index_create_batch(int device, const uint32_t* weak, const uint64_t* strong,
                                           const uint64_t* nblocks, const uint64_t* last_size, uint64_t nfiles,
                                           uint64_t block_size, int arrays_on_device, void* stream,
-                                          sydelta_index** out) {
+                                          sydelta_index** out) try {
     if (nfiles && (!nblocks || !last_size)) return fail(SYDELTA_E_INVAL, "NULL file table");
     return index_create_impl(device, weak, strong, nblocks, last_size, nfiles, block_size, arrays_on_device, stream,
                              out);
+} catch (...) {
+    return sydelta::host_exception();
 }
 
 // ---------------------------------------------------------------------------
@@ -483,10 +504,12 @@ extern "C" const uint8_t* sydelta_delta_literal(const sydelta_delta* d, uint64_t
     if (d->ops[i].kind != SYDELTA_OP_DATA || d->lit_off[i] == UINT64_MAX) return nullptr;
     return d->lit.data() + d->lit_off[i];
 }
-extern "C" int sydelta_delta_stats(const sydelta_delta* d, sydelta_match_stats* out) {
+extern "C" int sydelta_delta_stats(const sydelta_delta* d, sydelta_match_stats* out) try {
     if (!d || !out) return fail(SYDELTA_E_INVAL, "NULL argument");
     *out = d->stats;
     return SYDELTA_OK;
+} catch (...) {
+    return sydelta::host_exception();
 }
 // generator.rs:30-55
 extern "C" double sydelta_delta_compression_ratio(const sydelta_delta* d) {
@@ -506,10 +529,12 @@ extern "C" uint64_t sydelta_delta_batch_count(const sydelta_delta_batch* b) { re
 extern "C" const sydelta_delta* sydelta_delta_batch_get(const sydelta_delta_batch* b, uint64_t i) {
     return (b && i < b->d.size()) ? &b->d[i] : nullptr;
 }
-extern "C" int sydelta_delta_batch_stats(const sydelta_delta_batch* b, sydelta_match_stats* out) {
+extern "C" int sydelta_delta_batch_stats(const sydelta_delta_batch* b, sydelta_match_stats* out) try {
     if (!b || !out) return fail(SYDELTA_E_INVAL, "NULL argument");
     *out = b->total;
     return SYDELTA_OK;
+} catch (...) {
+    return sydelta::host_exception();
 }
 extern "C" void sydelta_delta_batch_free(sydelta_delta_batch* b) { delete b; }
 
@@ -694,6 +719,34 @@ double ms_since(std::chrono::steady_clock::time_point t0);
 int walk_threads();
 uint64_t walk_par_min();
 
+// Run task(t) for t in [0, n): t = 0 on the calling thread, the others on std::threads
+// (inline when a thread cannot be started).  No exception leaves: returns false when a
+// task threw (out of memory), so the C entry points can report SYDELTA_E_OOM.
+template <class F>
+bool run_parallel(int n, F&& task) {
+    std::atomic<bool> ok{true};
+    auto guarded = [&](int t) {
+        try {
+            task(t);
+        } catch (...) {
+            ok = false;
+        }
+    };
+    std::vector<std::thread> th;
+    int t = 1;
+    for (; t < n; ++t) {
+        try {
+            th.emplace_back(guarded, t);
+        } catch (...) {
+            break;
+        }
+    }
+    for (int u = t; u < n; ++u) guarded(u);
+    guarded(0);
+    for (auto& x : th) x.join();
+    return ok;
+}
+
 bool phase_probe_on() {
     // "1": probe long miss runs at their phase (opt-in: on the C4 shape the unaligned
     // window probes and the extra hit merges cost more host time than the scan they save)
@@ -801,10 +854,8 @@ int Classifier::probe(int mode) {
     };
     const size_t ns = src.size();
     const int nthr = ns >= 256 ? walk_threads() : 1;
-    std::vector<std::thread> th;
-    for (int t = 1; t < nthr; ++t) th.emplace_back(fill, ns * t / nthr, ns * (t + 1) / nthr);
-    fill(0, ns / nthr);
-    for (auto& x : th) x.join();
+    if (!run_parallel(nthr, [&](int t) { fill(ns * t / nthr, ns * (t + 1) / nthr); }))
+        return fail(SYDELTA_E_OOM, "out of host memory (probe results)");
     return SYDELTA_OK;
 }
 
@@ -946,10 +997,8 @@ int Classifier::scan(const std::vector<std::array<uint64_t, 3>>& ranges) {
             cut.push_back(h);
         }
         cut.push_back(nver);
-        std::vector<std::thread> th;
-        for (int t = 1; t < nthr; ++t) th.emplace_back(merge_range, cut[t], cut[t + 1]);
-        merge_range(cut[0], cut[1]);
-        for (auto& x : th) x.join();
+        if (!run_parallel(nthr, [&](int t) { merge_range(cut[t], cut[t + 1]); }))
+            return fail(SYDELTA_E_OOM, "out of host memory (hit lists)");
     } else {
         merge_range(0, nver);
     }
@@ -1184,12 +1233,8 @@ int Classifier::walk_parallel(size_t i, uint64_t entry, const BasisInfo& bi, boo
         rc[t] = walk_src(c, n, from, st[t + 1], bi, fin, tail_match, part[t], &ex[t], &need[t]);
         tseg[t] = ms_since(ts);
     };
-    {
-        std::vector<std::thread> th;
-        for (int t = 1; t < T; ++t) th.emplace_back(seg, t, st[t]);
-        seg(0, entry);
-        for (auto& x : th) x.join();
-    }
+    if (!run_parallel(T, [&](int t) { seg(t, t ? st[t] : entry); }))
+        return fail(SYDELTA_E_OOM, "out of host memory (op lists)");
     const double t_walk = ms_since(t0);
     if (rc[0]) return 1;
     // chain: segment t's true entry is segment t-1's exit
@@ -1219,16 +1264,10 @@ int Classifier::walk_parallel(size_t i, uint64_t entry, const BasisInfo& bi, boo
     give_ops(std::move(joined));
     const size_t cap0 = ops.capacity();
     ops.resize(at[T]);
-    {
-        std::vector<std::thread> th;
-        auto put = [&](int t) {
-            if (part[t].size() > skip[t])
-                memcpy(ops.data() + at[t], part[t].data() + skip[t], (part[t].size() - skip[t]) * sizeof(sydelta_op));
-        };
-        for (int t = 1; t < T; ++t) th.emplace_back(put, t);
-        put(0);
-        for (auto& x : th) x.join();
-    }
+    run_parallel(T, [&](int t) {
+        if (part[t].size() > skip[t])
+            memcpy(ops.data() + at[t], part[t].data() + skip[t], (part[t].size() - skip[t]) * sizeof(sydelta_op));
+    });
     // merged lengths: the op before each skipped one absorbs it
     for (int t = 1; t < T; ++t)
         if (skip[t]) ops[at[t] - 1].b += part[t][0].b;  // the op before segment t absorbs its first
@@ -1362,10 +1401,7 @@ static int match_impl(sydelta_index* ix, const uint8_t* d_buf, const uint64_t* s
                 }
             }
         };
-        std::vector<std::thread> th;
-        for (int t = 1; t < nthr; ++t) th.emplace_back(worker);
-        worker();
-        for (auto& x : th) x.join();
+        if (!run_parallel(nthr, [&](int) { worker(); })) return fail(SYDELTA_E_OOM, "out of host memory (op lists)");
     }
     const double t_par = ms_since(t0);
     for (uint64_t f = 0; f < nf; ++f) {
@@ -1394,7 +1430,7 @@ static int match_impl(sydelta_index* ix, const uint8_t* d_buf, const uint64_t* s
 }
 
 extern "C" int sydelta_match_device(sydelta_index* idx, const uint8_t* d_src, uint64_t len, void* stream,
-                                    sydelta_delta** out) {
+                                    sydelta_delta** out) try {
     if (!idx || !out) return fail(SYDELTA_E_INVAL, "NULL argument");
     *out = nullptr;
     if (idx->nfiles != 1) return fail(SYDELTA_E_INVAL, "index holds %llu files; use sydelta_match_batch_device",
@@ -1407,11 +1443,13 @@ extern "C" int sydelta_match_device(sydelta_index* idx, const uint8_t* d_src, ui
     if (int r = match_impl(idx, d_src, &off, &len, s, &b)) return r;
     *out = new sydelta_delta(std::move(b.d[0]));
     return SYDELTA_OK;
+} catch (...) {
+    return sydelta::host_exception();
 }
 
 extern "C" int sydelta_match_batch_device(sydelta_index* idx, const uint8_t* d_buf, const uint64_t* src_off,
                                           const uint64_t* src_len, uint64_t nfiles, void* stream,
-                                          sydelta_delta_batch** out) {
+                                          sydelta_delta_batch** out) try {
     if (!idx || !out) return fail(SYDELTA_E_INVAL, "NULL argument");
     *out = nullptr;
     if (nfiles != idx->nfiles) return fail(SYDELTA_E_INVAL, "index holds %llu files, %llu sources given",
@@ -1423,13 +1461,15 @@ extern "C" int sydelta_match_batch_device(sydelta_index* idx, const uint8_t* d_b
     if (int r = match_impl(idx, d_buf, src_off, src_len, s, b.get())) return r;
     *out = b.release();
     return SYDELTA_OK;
+} catch (...) {
+    return sydelta::host_exception();
 }
 
 // ---------------------------------------------------------------------------
 // host-buffer entry points
 // ---------------------------------------------------------------------------
 extern "C" int sydelta_compute_checksums_buf(int device, const uint8_t* buf, uint64_t len, uint64_t block_size,
-                                             sydelta_block_checksum* out, uint64_t cap, uint64_t* n_out) {
+                                             sydelta_block_checksum* out, uint64_t cap, uint64_t* n_out) try {
     if (block_size == 0) return fail(SYDELTA_E_INVAL, "block_size must be > 0");
     if (!n_out) return fail(SYDELTA_E_INVAL, "n_out is NULL");
     const uint64_t nb = len ? (len + block_size - 1) / block_size : 0;  // checksum.rs:36-41
@@ -1465,6 +1505,8 @@ extern "C" int sydelta_compute_checksums_buf(int device, const uint8_t* buf, uin
         out[i].strong = st[i];
     }
     return SYDELTA_OK;
+} catch (...) {
+    return sydelta::host_exception();
 }
 
 // Signatures from the caller must follow compute_checksums' layout (index order,
@@ -1531,8 +1573,10 @@ static int generate_from_host(int device, const uint8_t* src, uint64_t len, cons
 
 extern "C" int sydelta_generate_delta_buf(int device, const uint8_t* src, uint64_t len,
                                           const sydelta_block_checksum* sigs, uint64_t nsigs, uint64_t block_size,
-                                          sydelta_delta** out) {
+                                          sydelta_delta** out) try {
     return generate_from_host(device, src, len, sigs, nsigs, block_size, out);
+} catch (...) {
+    return sydelta::host_exception();
 }
 
 // ---------------------------------------------------------------------------
@@ -1557,7 +1601,7 @@ static int read_file(const char* path, std::vector<uint8_t>& data) {
 
 // checksum.rs:31-80
 extern "C" int sydelta_compute_checksums(const char* path, uint64_t block_size, sydelta_block_checksum** out,
-                                         uint64_t* n) {
+                                         uint64_t* n) try {
     if (!out || !n) return fail(SYDELTA_E_INVAL, "NULL output");
     *out = nullptr;
     *n = 0;
@@ -1576,30 +1620,36 @@ extern "C" int sydelta_compute_checksums(const char* path, uint64_t block_size, 
     *out = v;
     *n = got;
     return SYDELTA_OK;
+} catch (...) {
+    return sydelta::host_exception();
 }
 
 extern "C" void sydelta_checksums_free(sydelta_block_checksum* p) { free(p); }
 
 // generator.rs:242
 extern "C" int sydelta_generate_delta(const char* source_path, const sydelta_block_checksum* sigs, uint64_t nsigs,
-                                      uint64_t block_size, sydelta_delta** out) {
+                                      uint64_t block_size, sydelta_delta** out) try {
     if (!out) return fail(SYDELTA_E_INVAL, "out is NULL");
     *out = nullptr;
     std::vector<uint8_t> data;
     if (int r = read_file(source_path, data)) return r;
     return generate_from_host(-1, data.data(), data.size(), sigs, nsigs, block_size, out);
+} catch (...) {
+    return sydelta::host_exception();
 }
 
 // generator.rs:67 — identical ops to generate_delta for block_size <= 128 KiB
 // (SURVEY.md App. A R10); larger sizes are outside the production domain.
 extern "C" int sydelta_generate_delta_streaming(const char* source_path, const sydelta_block_checksum* sigs,
-                                                uint64_t nsigs, uint64_t block_size, sydelta_delta** out) {
+                                                uint64_t nsigs, uint64_t block_size, sydelta_delta** out) try {
     if (!out) return fail(SYDELTA_E_INVAL, "out is NULL");
     *out = nullptr;
     if (block_size > 128 * 1024)
         return fail(SYDELTA_E_INVAL, "block_size %llu > 131072: streaming semantics diverge (see sydelta.h)",
                     (unsigned long long)block_size);
     return sydelta_generate_delta(source_path, sigs, nsigs, block_size, out);
+} catch (...) {
+    return sydelta::host_exception();
 }
 
 // applier.rs:22-56 — receiver side, host I/O only.
@@ -1609,7 +1659,7 @@ extern "C" int sydelta_generate_delta_streaming(const char* source_path, const s
 // source the delta was generated from).
 extern "C" int sydelta_apply_delta_device(int device, const uint8_t* d_basis, uint64_t basis_len,
                                           const sydelta_delta* d, const uint8_t* d_lit, uint64_t lit_len,
-                                          uint8_t* d_out, uint64_t out_cap, void* stream, sydelta_apply_stats* out) {
+                                          uint8_t* d_out, uint64_t out_cap, void* stream, sydelta_apply_stats* out) try {
     if (!d) return fail(SYDELTA_E_INVAL, "NULL delta");
     if (int r = ensure_device(device)) return r;
     // the piece table is staged in pinned host memory (one per thread, grown on demand)
@@ -1706,10 +1756,12 @@ extern "C" int sydelta_apply_delta_device(int device, const uint8_t* d_basis, ui
         out->bytes_written = pos;
     }
     return SYDELTA_OK;
+} catch (...) {
+    return sydelta::host_exception();
 }
 
 extern "C" int sydelta_apply_delta(const char* old_file, const sydelta_delta* d, const char* new_file,
-                                   sydelta_apply_stats* out) {
+                                   sydelta_apply_stats* out) try {
     if (!d || !old_file || !new_file) return fail(SYDELTA_E_INVAL, "NULL argument");
     if (d->lit_off.size() != d->ops.size())
         return fail(SYDELTA_E_INVAL, "delta has no literal bytes (device-only source)");
@@ -1747,6 +1799,8 @@ extern "C" int sydelta_apply_delta(const char* old_file, const sydelta_delta* d,
         out->bytes_written = written;
     }
     return rc;
+} catch (...) {
+    return sydelta::host_exception();
 }
 
 // rolling.rs:35-45
@@ -1762,7 +1816,7 @@ extern "C" uint32_t sydelta_adler32_hash(const uint8_t* data, uint64_t len) {
 // ---------------------------------------------------------------------------
 // synthetic data (bench)
 // ---------------------------------------------------------------------------
-extern "C" int sydelta_synth_fill(uint8_t* d_buf, uint64_t len, uint64_t seed, void* stream) {
+extern "C" int sydelta_synth_fill(uint8_t* d_buf, uint64_t len, uint64_t seed, void* stream) try {
     if (len && !d_buf) return fail(SYDELTA_E_INVAL, "NULL buffer");
     int dev = 0;
     (void)hipGetDevice(&dev);
@@ -1771,9 +1825,11 @@ extern "C" int sydelta_synth_fill(uint8_t* d_buf, uint64_t len, uint64_t seed, v
     HIP_TRY(launch_synth_fill(d_buf, len, seed, s));
     if (!stream) HIP_TRY(hipStreamSynchronize(s));
     return SYDELTA_OK;
+} catch (...) {
+    return sydelta::host_exception();
 }
 
-extern "C" int sydelta_synth_fill_range(uint8_t* d_buf, uint64_t first, uint64_t len, uint64_t seed, void* stream) {
+extern "C" int sydelta_synth_fill_range(uint8_t* d_buf, uint64_t first, uint64_t len, uint64_t seed, void* stream) try {
     if (len && !d_buf) return fail(SYDELTA_E_INVAL, "NULL buffer");
     if (first % 8) return fail(SYDELTA_E_INVAL, "first must be a multiple of 8");
     int dev = 0;
@@ -1783,10 +1839,12 @@ extern "C" int sydelta_synth_fill_range(uint8_t* d_buf, uint64_t first, uint64_t
     HIP_TRY(launch_synth_fill(d_buf, len, seed, s, first));
     if (!stream) HIP_TRY(hipStreamSynchronize(s));
     return SYDELTA_OK;
+} catch (...) {
+    return sydelta::host_exception();
 }
 
 extern "C" int sydelta_synth_mutate_blocks(uint8_t* d_dst, const uint8_t* d_src, uint64_t first, uint64_t len,
-                                           uint64_t block_size, uint64_t seed, uint32_t rate_ppm, void* stream) {
+                                           uint64_t block_size, uint64_t seed, uint32_t rate_ppm, void* stream) try {
     if (len && (!d_dst || !d_src)) return fail(SYDELTA_E_INVAL, "NULL buffer");
     if (!block_size || first % block_size) return fail(SYDELTA_E_INVAL, "first must be a multiple of block_size");
     int dev = 0;
@@ -1797,10 +1855,12 @@ extern "C" int sydelta_synth_mutate_blocks(uint8_t* d_dst, const uint8_t* d_src,
     HIP_TRY(launch_synth_edit_blocks(d_dst, len, block_size, first, seed, rate_ppm, s));
     if (!stream) HIP_TRY(hipStreamSynchronize(s));
     return SYDELTA_OK;
+} catch (...) {
+    return sydelta::host_exception();
 }
 
 extern "C" int sydelta_synth_mutate(uint8_t* d_dst, const uint8_t* d_src, uint64_t len, uint64_t seed,
-                                    uint32_t rate_ppm, void* stream) {
+                                    uint32_t rate_ppm, void* stream) try {
     if (len && (!d_dst || !d_src)) return fail(SYDELTA_E_INVAL, "NULL buffer");
     int dev = 0;
     (void)hipGetDevice(&dev);
@@ -1809,6 +1869,8 @@ extern "C" int sydelta_synth_mutate(uint8_t* d_dst, const uint8_t* d_src, uint64
     HIP_TRY(launch_synth_mutate(d_dst, d_src, len, seed, rate_ppm, s));
     if (!stream) HIP_TRY(hipStreamSynchronize(s));
     return SYDELTA_OK;
+} catch (...) {
+    return sydelta::host_exception();
 }
 
 // ---------------------------------------------------------------------------
@@ -1829,7 +1891,7 @@ struct sydelta_chunk {
 
 extern "C" int sydelta_chunk_classify(sydelta_index* idx, const uint8_t* d_buf, uint64_t buf_pos, uint64_t buf_len,
                                       uint64_t file_len, uint64_t pos_begin, uint64_t pos_end, void* stream,
-                                      sydelta_chunk** out) {
+                                      sydelta_chunk** out) try {
     if (!idx || !out) return fail(SYDELTA_E_INVAL, "NULL argument");
     *out = nullptr;
     if (idx->nfiles != 1) return fail(SYDELTA_E_INVAL, "chunked match needs a single-file index");
@@ -1882,9 +1944,11 @@ extern "C" int sydelta_chunk_classify(sydelta_index* idx, const uint8_t* d_buf, 
     C.prof = nullptr;
     *out = ch.release();
     return SYDELTA_OK;
+} catch (...) {
+    return sydelta::host_exception();
 }
 
-extern "C" int sydelta_chunk_walk(sydelta_chunk* ch, uint64_t entry, uint64_t* exit_pos, sydelta_delta** out) {
+extern "C" int sydelta_chunk_walk(sydelta_chunk* ch, uint64_t entry, uint64_t* exit_pos, sydelta_delta** out) try {
     if (!ch || !exit_pos || !out) return fail(SYDELTA_E_INVAL, "NULL argument");
     *out = nullptr;
     Classifier& C = ch->C;
@@ -1905,6 +1969,8 @@ extern "C" int sydelta_chunk_walk(sydelta_chunk* ch, uint64_t entry, uint64_t* e
     finish_stats(d.get());
     *out = d.release();
     return SYDELTA_OK;
+} catch (...) {
+    return sydelta::host_exception();
 }
 
 extern "C" void sydelta_chunk_free(sydelta_chunk* ch) {
@@ -1915,7 +1981,7 @@ extern "C" void sydelta_chunk_free(sydelta_chunk* ch) {
 
 // Concatenate src's ops onto dst; a Data op that ends where src's first Data op
 // starts is extended (literal runs stay maximal, generator.rs:186-197, 218-221).
-extern "C" int sydelta_delta_append(sydelta_delta* dst, const sydelta_delta* src) {
+extern "C" int sydelta_delta_append(sydelta_delta* dst, const sydelta_delta* src) try {
     if (!dst || !src) return fail(SYDELTA_E_INVAL, "NULL argument");
     if (!dst->lit_off.empty() || !src->lit_off.empty())
         return fail(SYDELTA_E_INVAL, "append is for device deltas (no host literal copies)");
@@ -1936,6 +2002,8 @@ extern "C" int sydelta_delta_append(sydelta_delta* dst, const sydelta_delta* src
     dst->source_size = std::max(dst->source_size, src->source_size);
     finish_stats(dst);
     return SYDELTA_OK;
+} catch (...) {
+    return sydelta::host_exception();
 }
 
 extern "C" sydelta_delta* sydelta_delta_from_ops(const sydelta_op* ops, uint64_t n, uint64_t source_size,

@@ -46,6 +46,9 @@ struct sydelta_delta {
 namespace sydelta {
 // Record the calling thread's error text (sydelta_last_error) and return code.
 int fail(int code, const char* fmt, ...);
+// For the catch (...) of every int entry point (a function-try-block): no C++
+// exception crosses the C ABI; std::bad_alloc -> SYDELTA_E_OOM, others -> SYDELTA_E_INVAL.
+int host_exception();
 // Make `device` current after its one-time gfx950 check.
 int ensure_device(int device);
 // The calling thread's stream for `device`.

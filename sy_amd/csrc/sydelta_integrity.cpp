@@ -11,7 +11,7 @@
 using namespace sydelta;
 
 extern "C" int sydelta_xxh3_batch_device(int device, const uint8_t* d_buf, uint64_t buf_len, const uint64_t* offs, const uint64_t* lens,
-                                         uint64_t nfiles, void* stream, uint64_t* out) {
+                                         uint64_t nfiles, void* stream, uint64_t* out) try {
     if (!nfiles) return SYDELTA_OK;
     if (!offs || !lens || !out) return fail(SYDELTA_E_INVAL, "NULL offs/lens/out");
     if (nfiles > 0xFFFFFFFFull) return fail(SYDELTA_E_INVAL, "too many files");
@@ -71,9 +71,13 @@ extern "C" int sydelta_xxh3_batch_device(int device, const uint8_t* d_buf, uint6
     HIP_TRY(hipMemcpyAsync(out, d_out, nfiles * 8, hipMemcpyDeviceToHost, s));
     HIP_TRY(hipStreamSynchronize(s));
     return SYDELTA_OK;
+} catch (...) {
+    return sydelta::host_exception();
 }
 
-extern "C" int sydelta_xxh3_device(int device, const uint8_t* d_buf, uint64_t len, void* stream, uint64_t* out) {
+extern "C" int sydelta_xxh3_device(int device, const uint8_t* d_buf, uint64_t len, void* stream, uint64_t* out) try {
     const uint64_t off = 0;
     return sydelta_xxh3_batch_device(device, d_buf, len, &off, &len, 1, stream, out);
+} catch (...) {
+    return sydelta::host_exception();
 }

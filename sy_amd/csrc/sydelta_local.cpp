@@ -26,7 +26,7 @@ struct DevMem {
 // literal_bytes = bytes of changed blocks, bytes_written = source size).
 extern "C" int sydelta_block_compare_device(int device, const uint8_t* d_src, uint64_t src_len, const uint8_t* d_dst,
                                             uint64_t dst_len, uint64_t block_size, uint8_t* d_changed, void* stream,
-                                            sydelta_block_compare_stats* out) {
+                                            sydelta_block_compare_stats* out) try {
     if (!block_size) return fail(SYDELTA_E_INVAL, "block_size must be > 0");
     if (src_len && (!d_src || !d_changed)) return fail(SYDELTA_E_INVAL, "NULL buffer");
     if (dst_len && !d_dst) return fail(SYDELTA_E_INVAL, "NULL destination");
@@ -51,6 +51,8 @@ extern "C" int sydelta_block_compare_device(int device, const uint8_t* d_src, ui
         out->bytes_written = src_len;
     }
     return SYDELTA_OK;
+} catch (...) {
+    return sydelta::host_exception();
 }
 
 // ratio.rs:78-192 on device-resident bytes.  sample_count < 0 -> 20, threshold < 0 ->
@@ -58,7 +60,7 @@ extern "C" int sydelta_block_compare_device(int device, const uint8_t* d_src, ui
 extern "C" int sydelta_estimate_change_ratio_device(int device, const uint8_t* d_src, uint64_t src_len,
                                                     const uint8_t* d_dst, uint64_t dst_len, uint64_t block_size,
                                                     int64_t sample_count, double threshold, void* stream,
-                                                    sydelta_change_ratio* out) {
+                                                    sydelta_change_ratio* out) try {
     if (!out) return fail(SYDELTA_E_INVAL, "NULL result");
     if (!block_size) return fail(SYDELTA_E_INVAL, "block_size must be > 0");
     uint64_t want = sample_count < 0 ? 20 : (uint64_t)sample_count;
@@ -104,4 +106,6 @@ extern "C" int sydelta_estimate_change_ratio_device(int device, const uint8_t* d
         if (sr != dr || hs[i] != hd[i]) ++changed;
     }
     return finish((double)changed / (double)want, want, changed);  // :171-175
+} catch (...) {
+    return sydelta::host_exception();
 }

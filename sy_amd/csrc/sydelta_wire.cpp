@@ -172,7 +172,7 @@ extern "C" uint64_t sydelta_checksums_to_json(const sydelta_block_checksum* sigs
 
 // serde_json::from_str::<Vec<BlockChecksum>>  (ssh.rs:967-973)
 extern "C" int sydelta_checksums_from_json(const char* json, uint64_t len, sydelta_block_checksum** out,
-                                           uint64_t* n_out) {
+                                           uint64_t* n_out) try {
     if (!json || !out || !n_out) return fail(SYDELTA_E_INVAL, "NULL argument");
     *out = nullptr;
     *n_out = 0;
@@ -219,12 +219,14 @@ extern "C" int sydelta_checksums_from_json(const char* json, uint64_t len, sydel
     }
     *n_out = v.size();
     return SYDELTA_OK;
+} catch (...) {
+    return sydelta::host_exception();
 }
 
 // serde_json::to_string(&Delta)  (ssh.rs:1003).  Literal bytes: the delta's own (host
 // entry points), or `lit` indexed by the Data ops' source offsets (device deltas).
 extern "C" int sydelta_delta_to_json(const sydelta_delta* d, const uint8_t* lit, uint64_t lit_len, char* buf,
-                                     uint64_t cap, uint64_t* out_len) {
+                                     uint64_t cap, uint64_t* out_len) try {
     if (!d || !out_len) return fail(SYDELTA_E_INVAL, "NULL argument");
     const bool own = !lit;
     if (own && d->lit_off.size() != d->ops.size())
@@ -288,11 +290,13 @@ extern "C" int sydelta_delta_to_json(const sydelta_delta* d, const uint8_t* lit,
     p = put_u64(p, d->block_size);
     *p++ = '}';
     return (uint64_t)(p - buf) == total ? SYDELTA_OK : fail(SYDELTA_E_KERNEL, "delta JSON length mismatch");
+} catch (...) {
+    return sydelta::host_exception();
 }
 
 // serde_json::from_str::<Delta>  (sy-remote.rs:175): a host delta with its literal bytes,
 // ready for sydelta_apply_delta.
-extern "C" int sydelta_delta_from_json(const char* json, uint64_t len, sydelta_delta** out) {
+extern "C" int sydelta_delta_from_json(const char* json, uint64_t len, sydelta_delta** out) try {
     if (!json || !out) return fail(SYDELTA_E_INVAL, "NULL argument");
     *out = nullptr;
     Reader r{json, json + len, {}, json};
@@ -369,12 +373,14 @@ extern "C" int sydelta_delta_from_json(const char* json, uint64_t len, sydelta_d
     finish_stats(d.get());
     *out = d.release();
     return SYDELTA_OK;
+} catch (...) {
+    return sydelta::host_exception();
 }
 
 // serde_json::to_string(&Delta) on the device (K7): the literal runs (3.6 characters per
 // byte on average) are formatted in HBM; the op table goes up once, pinned.
 extern "C" int sydelta_delta_to_json_device(const sydelta_delta* d, const uint8_t* d_lit, uint64_t lit_len,
-                                            uint8_t* d_out, uint64_t out_cap, uint64_t* out_len, void* stream) {
+                                            uint8_t* d_out, uint64_t out_cap, uint64_t* out_len, void* stream) try {
     if (!d || !out_len) return fail(SYDELTA_E_INVAL, "NULL argument");
     int dev = 0;
     (void)hipGetDevice(&dev);
@@ -462,4 +468,6 @@ extern "C" int sydelta_delta_to_json_device(const sydelta_delta* d, const uint8_
     }
     HIP_TRY(hipStreamSynchronize(s));  // pinned piece table and host strings are reused / go away
     return SYDELTA_OK;
+} catch (...) {
+    return sydelta::host_exception();
 }
