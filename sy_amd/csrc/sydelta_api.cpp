@@ -803,7 +803,16 @@ int Classifier::probe(int mode) {
     if (mode < 0 && total < 4096) return SYDELTA_OK;  // small inputs: one scan is cheaper
     bool fast = n % 64 == 0 && n >= 256;
     for (auto& c : src) fast = fast && ((uintptr_t)(base + c.off) & 15) == 0;
-    auto run = [&](uint32_t stride, std::vector<uint32_t>& out, std::vector<uint64_t>& pfx) -> int {
+    // results land in pinned host memory (per thread, grown on demand): no zero fill and
+    // no staging copy for the D2H of one u32 per probed window
+    struct PinnedU32 {
+        uint32_t* p = nullptr;
+        size_t cap = 0;
+    };
+    static thread_local PinnedU32 pin;  // never freed, like the per-thread streams
+    uint32_t* out = nullptr;
+    uint64_t nout = 0;
+    auto run = [&](uint32_t stride, std::vector<uint64_t>& pfx) -> int {
         std::vector<ProbeJob> jobs;
         pfx.assign(src.size() + 1, 0);
         uint64_t np = 0;
@@ -815,8 +824,16 @@ int Classifier::probe(int mode) {
             np += cnt;
         }
         pfx[src.size()] = np;
-        out.assign(np, kNoBlk);
+        nout = np;
         if (!np) return SYDELTA_OK;
+        if (np > pin.cap) {
+            if (pin.p) (void)hipHostFree(pin.p);
+            pin.p = nullptr;
+            pin.cap = 0;
+            HIP_TRY(hipHostMalloc((void**)&pin.p, np * 5 / 4 * 4, hipHostMallocDefault));
+            pin.cap = np * 5 / 4;
+        }
+        out = pin.p;
         DevBuf jb;
         const size_t jbytes = (jobs.size() * sizeof(ProbeJob) + 255) & ~(size_t)255;
         const size_t obytes = (np * 4 + 255) & ~(size_t)255;
@@ -828,25 +845,24 @@ int Classifier::probe(int mode) {
         HIP_TRY(hipMemcpyAsync(jb.p, jobs.data(), jobs.size() * sizeof(ProbeJob), hipMemcpyHostToDevice, s));
         HIP_TRY(launch_probe(base, (const ProbeJob*)jb.p, (uint32_t)jobs.size(), np, stride, (uint32_t)n, fast,
                              ix->ix, d_pw, d_pst, d_out, s, prof));
-        HIP_TRY(hipMemcpyAsync(out.data(), d_out, np * 4, hipMemcpyDeviceToHost, s));
+        HIP_TRY(hipMemcpyAsync(out, d_out, np * 4, hipMemcpyDeviceToHost, s));
         HIP_TRY(hipStreamSynchronize(s));
         return SYDELTA_OK;
     };
-    std::vector<uint32_t> out;
     std::vector<uint64_t> pfx;
     if (mode < 0) {
         const uint32_t S = 16;
-        if (int r = run(S, out, pfx)) return r;
+        if (int r = run(S, pfx)) return r;
         uint64_t hits = 0;
-        for (uint32_t v : out) hits += v != kNoBlk;
-        if (hits * 8 < out.size()) return SYDELTA_OK;
+        for (uint64_t i = 0; i < nout; ++i) hits += out[i] != kNoBlk;
+        if (hits * 8 < nout) return SYDELTA_OK;
     }
-    if (int r = run(1, out, pfx)) return r;
+    if (int r = run(1, pfx)) return r;
     auto fill = [&](size_t i0, size_t i1) {
         for (size_t i = i0; i < i1; ++i) {
             Src& c = src[i];
             c.probed = true;
-            c.ahit.assign(out.begin() + pfx[i], out.begin() + pfx[i + 1]);
+            c.ahit.assign(out + pfx[i], out + pfx[i + 1]);
             c.scanned.assign(c.nblk, 0);
             c.nahit = 0;
             for (uint32_t v : c.ahit) c.nahit += v != kNoBlk;
