@@ -249,7 +249,8 @@ int sydelta_chunk_classify(sydelta_index *idx, const uint8_t *d_buf, uint64_t bu
 int sydelta_chunk_walk(sydelta_chunk *c, uint64_t entry, uint64_t *exit_pos, sydelta_delta **out);
 void sydelta_chunk_free(sydelta_chunk *c);
 /* A delta holding a copy of n ops (e.g. one received from the sender, to apply on the
- * device); NULL if ops is NULL with n > 0. */
+ * device); NULL if ops is NULL with n > 0 or an op's kind is neither SYDELTA_OP_COPY nor
+ * SYDELTA_OP_DATA (sydelta_last_error says which). */
 sydelta_delta *sydelta_delta_from_ops(const sydelta_op *ops, uint64_t n, uint64_t source_size, uint64_t block_size);
 /* Empty delta (Delta { ops: [], source_size, block_size }) to append chunk deltas to. */
 sydelta_delta *sydelta_delta_new(uint64_t source_size, uint64_t block_size);

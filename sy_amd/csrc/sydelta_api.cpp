@@ -22,6 +22,7 @@
 #include <cmath>
 #include <map>
 #include <memory>
+#include <new>
 #include <mutex>
 #include <thread>
 #include <string>
@@ -389,7 +390,7 @@ static int index_create_impl(int device, const uint32_t* weak, const uint64_t* s
         F.filt_off = fw;
         F.slot_off = sl;
         F.blk_base = fblk[f];
-        F.fwshift = 33 - fwbits;  // 2^(fwbits-1) 64-bit words
+        F.fwshift = 32 - fwbits;  // 2^fwbits 32-bit words
         F.bmask = (1u << bbits) - 1;
         fw += 1ull << fwbits;
         sl += 4ull << bbits;
@@ -402,12 +403,17 @@ static int index_create_impl(int device, const uint32_t* weak, const uint64_t* s
     const size_t sz_weak = al(4 * nb), sz_strong = al(8 * nb), sz_filt = al(4 * fw), sz_t = al(4 * sl);
     const size_t sz_order = al(4 * nb), sz_slot = al(4 * nb), sz_files = al(sizeof(FileIx) * nfiles);
     const size_t sz_fblk = al(8 * (nfiles + 1)), sz_cstrong = al(8 * nb);
-    const size_t total = sz_weak + sz_strong + sz_filt + 4 * sz_t + sz_order + sz_slot + sz_files + sz_fblk + sz_cstrong;
+    // level-1 filter for k_scan_l1: one large file (the BASELINE C3 shape)
+    const bool want_l1 = nfiles == 1 && nblocks > kLdsFilterKeys;
+    const size_t sz_l1 = want_l1 ? al(4 * (size_t)kL1Words) : 0;
+    const size_t total =
+        sz_weak + sz_strong + sz_filt + sz_l1 + 4 * sz_t + sz_order + sz_slot + sz_files + sz_fblk + sz_cstrong;
     HIP_TRY(hipMalloc(&x->d_pool, total));
     uint8_t* p = (uint8_t*)x->d_pool;
     x->d_weak = (uint32_t*)p; p += sz_weak;
     x->d_strong = (uint64_t*)p; p += sz_strong;
     ix.filt = (uint32_t*)p; p += sz_filt;
+    if (want_l1) { ix.l1 = (uint32_t*)p; p += sz_l1; }
     ix.keys = (uint32_t*)p; p += sz_t;
     ix.cnt = (uint32_t*)p; p += sz_t;
     ix.start = (uint32_t*)p; p += sz_t;
@@ -1686,23 +1692,17 @@ extern "C" int sydelta_apply_delta_device(int device, const uint8_t* d_basis, ui
         ~Pinned() { if (p) (void)hipHostFree(p); }
     };
     static thread_local Pinned pin;
-    uint64_t need = 0;
-    constexpr uint64_t kSlice = 64 * 1024;
-    for (const sydelta_op& o : d->ops) need += (o.b + kSlice - 1) / kSlice;
-    if (need > pin.cap) {
-        if (pin.p) { (void)hipHostFree(pin.p); pin.p = nullptr; pin.cap = 0; }
-        const size_t cap = std::max<size_t>(need, 4096) * 5 / 4;
-        HIP_TRY(hipHostMalloc((void**)&pin.p, cap * sizeof(ApplyPiece), hipHostMallocDefault));
-        pin.cap = cap;
-    }
-    ApplyPiece* pieces = pin.p;
     static const bool host_timing = getenv("SYDELTA_HOST_TIMING") != nullptr;
     const auto t0 = std::chrono::steady_clock::now();
-    // validate every op first (the output is not touched on an error)
-    uint64_t pos = 0, literal = 0;
+    constexpr uint64_t kSlice = 64 * 1024;
+    // validate every op first, overflow-checked (a delta parsed from remote JSON may
+    // carry any sizes): the output is not touched and nothing is allocated on an error
+    uint64_t pos = 0, literal = 0, need = 0;
     for (size_t i = 0; i < d->ops.size(); ++i) {
         const sydelta_op& o = d->ops[i];
         const bool cp = o.kind == SYDELTA_OP_COPY;
+        if (o.kind != SYDELTA_OP_COPY && o.kind != SYDELTA_OP_DATA)
+            return fail(SYDELTA_E_INVAL, "op %zu: unknown kind %u", i, (unsigned)o.kind);
         if (cp && (o.a > basis_len || o.b > basis_len - o.a))
             return fail(SYDELTA_E_IO, "op %zu: Copy{offset %llu, size %llu} past the end of the basis (%llu bytes): "
                         "failed to fill whole buffer", i, (unsigned long long)o.a, (unsigned long long)o.b,
@@ -1710,12 +1710,21 @@ extern "C" int sydelta_apply_delta_device(int device, const uint8_t* d_basis, ui
         if (!cp && (o.a > lit_len || o.b > lit_len - o.a))
             return fail(SYDELTA_E_INVAL, "op %zu: Data [%llu, +%llu) outside the literal buffer", i,
                         (unsigned long long)o.a, (unsigned long long)o.b);
-        pos += o.b;
+        if (o.b > out_cap - std::min(pos, out_cap))
+            return fail(SYDELTA_E_INVAL, "output needs more than its capacity of %llu bytes",
+                        (unsigned long long)out_cap);
+        pos += o.b;  // <= out_cap: no overflow
         if (!cp) literal += o.b;
+        need += o.b / kSlice + (o.b % kSlice != 0);
     }
-    if (pos > out_cap) return fail(SYDELTA_E_INVAL, "output needs %llu bytes, capacity %llu",
-                                   (unsigned long long)pos, (unsigned long long)out_cap);
     if (pos && !d_out) return fail(SYDELTA_E_INVAL, "NULL output");
+    if (need > pin.cap) {
+        if (pin.p) { (void)hipHostFree(pin.p); pin.p = nullptr; pin.cap = 0; }
+        const size_t cap = std::max<size_t>(need, 4096) * 5 / 4;
+        HIP_TRY(hipHostMalloc((void**)&pin.p, cap * sizeof(ApplyPiece), hipHostMallocDefault));
+        pin.cap = cap;
+    }
+    ApplyPiece* pieces = pin.p;
     hipStream_t s = stream ? (hipStream_t)stream : thread_stream(device < 0 ? 0 : device);
     CallProf cp;
     if (need) {
@@ -1733,11 +1742,21 @@ extern "C" int sydelta_apply_delta_device(int device, const uint8_t* d_basis, ui
         }
         hipStream_t cstream = cs.first;
         const std::vector<hipEvent_t>& ev = cs.second;
+        // On an error after the first upload was queued: drain both streams before the
+        // table (device) and the pinned staging (host, reused by the next call) go away.
+        struct Drain {
+            hipStream_t a, b;
+            bool armed = false;
+            ~Drain() {
+                if (armed) { (void)hipStreamSynchronize(a); (void)hipStreamSynchronize(b); }
+            }
+        } drain{cstream, s};
         DevBuf pb;
         HIP_TRY(hipMallocAsync(&pb.p, need * sizeof(ApplyPiece), s));
         pb.s = s;
         HIP_TRY(hipEventRecord(ev[0], s));  // the table allocation is ordered before the uploads
         HIP_TRY(hipStreamWaitEvent(cstream, ev[0], 0));
+        drain.armed = true;
         ApplyPiece* dp = (ApplyPiece*)pb.p;
         const size_t per = std::max<size_t>(1, (d->ops.size() + kBatches - 1) / kBatches);
         size_t np = 0, j = 0;
@@ -1747,8 +1766,7 @@ extern "C" int sydelta_apply_delta_device(int device, const uint8_t* d_basis, ui
             const size_t b0 = np;
             for (size_t i = i0; i < i1; ++i) {
                 const sydelta_op& o = d->ops[i];
-                const bool cpy = o.kind == SYDELTA_OP_COPY;
-                const uint32_t cpf = cpy ? 1u : 0u;
+                const uint32_t cpf = o.kind == SYDELTA_OP_COPY ? 1u : 0u;
                 for (uint64_t k = 0; k < o.b; k += kSlice)
                     pieces[np++] = {at + k, o.a + k, (uint32_t)std::min<uint64_t>(kSlice, o.b - k), cpf};
                 at += o.b;
@@ -1762,6 +1780,7 @@ extern "C" int sydelta_apply_delta_device(int device, const uint8_t* d_basis, ui
         }
         const double t_enq = ms_since(t0);
         HIP_TRY(hipStreamSynchronize(s));  // the pinned table is reused by the next call
+        drain.armed = false;
         if (host_timing)
             fprintf(stderr, "sydelta apply: %zu pieces, validate+build+enqueue %.3f ms, total %.3f ms\n", np,
                     t_enq, ms_since(t0));
@@ -2025,7 +2044,13 @@ extern "C" int sydelta_delta_append(sydelta_delta* dst, const sydelta_delta* src
 extern "C" sydelta_delta* sydelta_delta_from_ops(const sydelta_op* ops, uint64_t n, uint64_t source_size,
                                                  uint64_t block_size) {
     if (n && !ops) return nullptr;
-    sydelta_delta* d = new sydelta_delta();
+    for (uint64_t i = 0; i < n; ++i)  // only DeltaOp::Copy / DeltaOp::Data exist (generator.rs:10-15)
+        if (ops[i].kind != SYDELTA_OP_COPY && ops[i].kind != SYDELTA_OP_DATA) {
+            fail(SYDELTA_E_INVAL, "op %llu: unknown kind %u", (unsigned long long)i, (unsigned)ops[i].kind);
+            return nullptr;
+        }
+    sydelta_delta* d = new (std::nothrow) sydelta_delta();
+    if (!d) return nullptr;
     d->source_size = source_size;
     d->block_size = block_size;
     d->ops.assign(ops, ops + n);

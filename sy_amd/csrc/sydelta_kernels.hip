@@ -312,25 +312,41 @@ __global__ __launch_bounds__(256) void k_sig_batch(const uint8_t* __restrict__ b
 // ===========================================================================
 // K3: index (probe structure) over basis weak values
 // ===========================================================================
-// Blocked Bloom filter: 64-bit words, 4 bits per key, all in the key's word.
-// h = fmix32(weak) picks the word (top bits); a second multiply of h gives the
-// four 6-bit bit positions.  At 16 bits per key that is ~0.5 % false passes
-// (a 32-bit word with 3 bits: ~1 %, measured 1.4 % with a 24-bit-multiply hash).
-// Sizing (sydelta_index_create): up to 16 Ki keys the filter is <= 32 KiB and
-// the LDS-staged scan copies it into LDS; above that it stays in HBM/L2 at 16
-// bits per key.  FileIx::filt_off counts 32-bit units; fwshift = 32 - log2(words).
-__device__ __forceinline__ uint32_t filt_hash(uint32_t w) {
-    uint32_t h = w * 0x9E3779B1u;
-    h ^= h >> 16;
-    h *= 0x85EBCA6Bu;
-    h ^= h >> 13;
-    return h;
+// Probe hashes of a weak value w = (B << 16) | A, each two 24-bit multiplies (full
+// rate; a 32-bit multiply is quarter rate and this runs once per scanned position):
+//   q = A*0x9E3779 + B*0x85EBCB  -> the level-1 bit (below) and the three bit
+//                                   positions of the level-2 word (bits 0..14)
+//   r = A*0xC2B2AF + B*0x27D4EB  -> the level-2 word (top bits)
+// Level 2 is a blocked Bloom filter of 32-bit words, 3 bits per key in the key's
+// word, 16 bits per key for large indexes: 1.1 % false passes on Adler values of
+// random 4 KiB blocks (the word from r and the bits from q: taking both from one
+// linear hash correlates them, 1.8 %).  Sizing (sydelta_index_create): up to 16 Ki
+// keys the filter is <= 32 KiB and the LDS-staged scan copies it into LDS; above
+// that it stays in HBM/L2.  FileIx::filt_off counts words; fwshift = 32 - log2(words).
+struct ProbeHash {
+    uint32_t q, r;
+};
+__device__ __forceinline__ ProbeHash probe_hash(uint32_t A, uint32_t B) {
+    const uint32_t q = (uint32_t)__umul24(A, 0x9E3779u) + (uint32_t)__umul24(B, 0x85EBCBu);
+    const uint32_t r = (uint32_t)__umul24(A, 0xC2B2AFu) + (uint32_t)__umul24(B, 0x27D4EBu);
+    return {q, r};
 }
-__device__ __forceinline__ uint64_t filt_mask(uint32_t h) {
-    const uint32_t g = (h ^ (h >> 15)) * 0x2C1B3C6Du;
-    return (1ull << ((g >> 8) & 63)) | (1ull << ((g >> 14) & 63)) | (1ull << ((g >> 20) & 63)) |
-           (1ull << (g >> 26));
+__device__ __forceinline__ ProbeHash probe_hash(uint32_t w) { return probe_hash(w & 0xFFFFu, w >> 16); }
+__device__ __forceinline__ uint32_t filt_mask(uint32_t q) {
+    return (1u << (q & 31)) | (1u << ((q >> 5) & 31)) | (1u << ((q >> 10) & 31));
 }
+__device__ __forceinline__ bool filt_pass(uint32_t word, uint32_t q) {
+    const uint32_t m = filt_mask(q);
+    return (word & m) == m;
+}
+// Level-1 filter of a large single-file index (kL1Words 32-bit words, 0.94 bits per
+// key at 1 Mi keys: 66 % false passes), held in LDS by k_scan_l1 so that only the
+// positions it passes cost a level-2 request to L2 (sydelta_internal.hpp).
+// word = floor((q >> 8) * 30720 / 2^24) (one v_mul_hi_u32_u24), bit = bits 8..12 of q.
+__device__ __forceinline__ uint32_t l1_word(uint32_t q) {
+    return (uint32_t)(((uint64_t)(q >> 8) * (30720ull << 8)) >> 32);  // < kL1Words
+}
+__device__ __forceinline__ uint32_t l1_test(uint32_t word, uint32_t q) { return __builtin_amdgcn_ubfe(word, q >> 8, 1); }
 __device__ __forceinline__ uint32_t bucket_hash(uint32_t w) {
     uint32_t h = w ^ (w >> 15);
     h *= 0x2C1B3C6Du;
@@ -350,13 +366,15 @@ __device__ __forceinline__ uint32_t file_of_block(const uint64_t* __restrict__ f
 
 __global__ void k_idx_insert(const uint32_t* __restrict__ weak, uint64_t n, const uint64_t* __restrict__ fblk,
                              uint32_t nf, const FileIx* __restrict__ files, uint32_t* __restrict__ filt,
-                             uint32_t* __restrict__ keys, uint32_t* __restrict__ cnt, uint32_t* __restrict__ slot_of) {
+                             uint32_t* __restrict__ l1, uint32_t* __restrict__ keys, uint32_t* __restrict__ cnt,
+                             uint32_t* __restrict__ slot_of) {
     const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
     const FileIx F = files[file_of_block(fblk, nf, i)];
     const uint32_t w = weak[i];
-    const uint32_t h = filt_hash(w);
-    atomicOr((unsigned long long*)(filt + F.filt_off) + (h >> F.fwshift), (unsigned long long)filt_mask(h));
+    const ProbeHash h = probe_hash(w);
+    atomicOr(filt + F.filt_off + (h.r >> F.fwshift), filt_mask(h.q));
+    if (l1) atomicOr(l1 + l1_word(h.q), 1u << ((h.q >> 8) & 31));  // single-file index only (l1_test)
     uint32_t b = bucket_hash(w) & F.bmask;
     for (;;) {
         for (uint32_t j = 0; j < 4; ++j) {
@@ -503,8 +521,8 @@ __global__ __launch_bounds__(256) void k_probe_lookup(const ProbeJob* __restrict
     const FileIx F = files[jobs[probe_job(jobs, njobs, w)].file];
     const uint32_t wk = pw[w];
     uint32_t best = kNoBlock;
-    const uint32_t h = filt_hash(wk);
-    if ((filt_mask(h) & ~((const uint64_t*)(filt + F.filt_off))[h >> F.fwshift]) == 0) {
+    const ProbeHash h = probe_hash(wk);
+    if (filt_pass(filt[F.filt_off + (h.r >> F.fwshift)], h.q)) {
         const int64_t slot = table_find(keys + F.slot_off, F.bmask, wk);
         if (slot >= 0) {
             const uint64_t gs = F.slot_off + (uint64_t)slot;
@@ -563,6 +581,7 @@ struct ScanArgs {
     uint32_t nchunks;    // LDS chunk slots per tile (k_scan)
     // probe structures (concatenated over files)
     const uint32_t* filt;
+    const uint32_t* l1;       // k_scan_l1: level-1 filter (kL1Words)
     const uint32_t* keys;
     const uint32_t* start;
     const uint32_t* cnt;
@@ -864,15 +883,16 @@ __global__ __launch_bounds__(kScanThreads) void k_scan(ScanArgs a) {
 #pragma unroll
         for (int hb = 0; hb < 64; hb += kBatch) {
             uint32_t wv[kBatch];
-            uint64_t fw[kBatch];
+            uint32_t fw[kBatch];
             uint32_t fh[kBatch];
 #pragma unroll
             for (int t = 0; t < kBatch; ++t) {
                 const int i = hb + t;
                 const uint32_t am = a_ex % kMod;
                 wv[t] = (bm << 16) | am;
-                fh[t] = filt_hash(wv[t]);
-                fw[t] = ((const uint64_t*)a.filt)[fh[t] >> a.fwshift];
+                const ProbeHash h = probe_hash(am, bm);
+                fh[t] = h.q;
+                fw[t] = a.filt[h.r >> a.fwshift];
                 const uint32_t out = (xo[i >> 2] >> (8 * (i & 3))) & 0xFF;
                 const uint32_t in = (xi[i >> 2] >> (8 * (i & 3))) & 0xFF;
                 a_ex = a_ex + in - out;
@@ -881,8 +901,7 @@ __global__ __launch_bounds__(kScanThreads) void k_scan(ScanArgs a) {
 #pragma unroll
             for (int t = 0; t < kBatch; ++t) {
                 const uint32_t rel = g + hb + t;
-                const uint64_t fmask = filt_mask(fh[t]);
-                const bool pass = ((fw[t] & fmask) == fmask) && rel < npos;
+                const bool pass = filt_pass(fw[t], fh[t]) && rel < npos;
                 const uint64_t mk = __ballot(pass);
                 if (mk) {
                     if (pass) fq[nfq + __popcll(mk & ((1ull << lane) - 1))] = make_uint2(rel0 + rel, wv[t]);
@@ -1231,7 +1250,7 @@ __global__ __launch_bounds__(kT2, kWgPerCu) void k_scan_lds(ScanArgs a, uint32_t
     uint32_t* PV = (uint32_t*)(smem + L.pv);
     uint64_t* PJ = (uint64_t*)(smem + L.pj);
     uint32_t* ntab = (uint32_t*)(smem + L.ntab);
-    uint64_t* lfilt = (uint64_t*)(smem + L.filt);
+    uint32_t* lfilt = (uint32_t*)(smem + L.filt);
     const uint32_t tid = threadIdx.x;
     const uint32_t lane = tid & 63, wid = tid >> 6;
     uint4* wq = (uint4*)(smem + L.q) + (size_t)wid * kWQ2;
@@ -1251,7 +1270,7 @@ __global__ __launch_bounds__(kT2, kWgPerCu) void k_scan_lds(ScanArgs a, uint32_t
     uint32_t nfq = 0;
     uint32_t cur_file = 0xFFFFFFFFu;
     uint32_t fwshift = 0;
-    const uint64_t* gfilt = (const uint64_t*)a.filt;
+    const uint32_t* gfilt = a.filt;
     SegCtx sc;
 
     unsigned long long tm[4] = {0, 0, 0, 0};
@@ -1284,14 +1303,14 @@ __global__ __launch_bounds__(kT2, kWgPerCu) void k_scan_lds(ScanArgs a, uint32_t
             sc.bmask = F.bmask;
             sc.seg_id = si;
             fwshift = F.fwshift;
-            gfilt = (const uint64_t*)(a.filt + F.filt_off);
+            gfilt = a.filt + F.filt_off;
             if (kLdsFilter && S.file != cur_file) {
                 // the previous tile ended with a barrier; phase 1's barrier publishes the copy
                 const uint4* src4 = (const uint4*)gfilt;
                 uint4* dst4 = (uint4*)lfilt;
-                const uint32_t fwords64 = 1u << (32 - fwshift);
+                const uint32_t fwords = 1u << (32 - fwshift);
 #pragma unroll 4
-                for (uint32_t i = tid; i < fwords64 / 2; i += kT2) dst4[i] = src4[i];
+                for (uint32_t i = tid; i < fwords / 4; i += kT2) dst4[i] = src4[i];
             }
             cur_file = S.file;
         }
@@ -1398,16 +1417,15 @@ __global__ __launch_bounds__(kT2, kWgPerCu) void k_scan_lds(ScanArgs a, uint32_t
             uint32_t ct[kB2];
 #pragma unroll
             for (int t = 0; t < kB2; ++t) ct[t] = ntab[(xo[t >> 2] >> (8 * (t & 3))) & 0xFF];
-            uint32_t wv[kB2], fh[kB2];
-            uint64_t fw[kB2];
+            uint32_t wv[kB2], fh[kB2], fw[kB2];
 #pragma unroll
             for (int t = 0; t < kB2; ++t) {
                 const uint32_t out = (xo[t >> 2] >> (8 * (t & 3))) & 0xFF;
                 const uint32_t in = (xi[t >> 2] >> (8 * (t & 3))) & 0xFF;
                 wv[t] = (bm << 16) | am;
-                const uint32_t h = filt_hash(wv[t]);
-                fh[t] = h;
-                fw[t] = kLdsFilter ? lfilt[h >> fwshift] : gfilt[h >> fwshift];
+                const ProbeHash h = probe_hash(am, bm);
+                fh[t] = h.q;
+                fw[t] = kLdsFilter ? lfilt[h.r >> fwshift] : gfilt[h.r >> fwshift];
                 uint32_t u = am + in - out;  // (-255, M+255), wrapped when negative
                 u = min(u, u + kMod);
                 am = min(u, u - kMod);
@@ -1417,7 +1435,7 @@ __global__ __launch_bounds__(kT2, kWgPerCu) void k_scan_lds(ScanArgs a, uint32_t
             }
 #pragma unroll
             for (int t = 0; t < kB2; ++t) {
-                const bool pass = (filt_mask(fh[t]) & ~fw[t]) == 0;
+                const bool pass = filt_pass(fw[t], fh[t]);
                 const uint64_t mk = __ballot(pass);
                 if (mk) {
                     if (pass) fq[nfq + __popcll(mk & ((1ull << lane) - 1))] = make_uint2(qtile | (rel0 + g + t), wv[t]);
@@ -1441,6 +1459,331 @@ __global__ __launch_bounds__(kT2, kWgPerCu) void k_scan_lds(ScanArgs a, uint32_t
     if (lane == 0 && weak_hits) atomicAdd(&a.counters[1], weak_hits);
     if (a.timing && tid == 0)
         for (int k = 0; k < 4; ++k) atomicAdd(&a.counters[4 + k], tm[k]);
+}
+
+// ===========================================================================
+// K2+K4 for a large single-file index: k_scan_l1 (window n <= kMaxN3)
+// ===========================================================================
+// The BASELINE C3 shape: 2^32 window starts against 2^20 basis keys, every one a
+// literal.  Each position must test its weak value against the key set.  With the
+// level-2 filter (2 MiB, 16 bits per key) in L2 that is one random L2 request per
+// position, and the chip serves ~265 G of those per second whatever their width or
+// cache policy (profiles/r02_micro_gather2.txt): >= 16 ms per 4 GiB.  So each
+// workgroup (one per CU) keeps a level-1 filter of 120 KiB in LDS, and only the
+// positions it passes (66 % at 1 Mi keys) cost an L2 request.  Eight waves, two
+// per SIMD (a wave alone on its SIMD issues VALU at half rate), 32 positions per
+// thread, the tile of k_scan_lds:
+//   phase 1  tile bytes [T0, T0 + kTile3 + n) -> LDS rows (64 B, 17-dword
+//            stride), sums of every 32-byte half
+//   phase 2  exclusive prefix of the half sums (S, sum of i*x, sum of h*S_h)
+//   phase 3  thread t's first window [T0 + 32t, +n) in closed form
+//   phase 4  roll 32 positions in batches of 8 (rolling.rs:66-79, both halves kept
+//            reduced with one min3 each); per position probe_hash, the level-1 bit
+//            from LDS, for its passes the level-2 word from L2; level-2 passes are
+//            queued per wave in LDS and drained (exact lookups, XXH3 of weak hits
+//            from the LDS rows, generator.rs:121-155) when a batch might not fit
+//            and at the end of the tile.
+constexpr int kT3 = 512;           // threads per workgroup (8 waves)
+constexpr int kR3 = 32;            // positions per thread = half a 64-byte row
+constexpr int kTile3 = kT3 * kR3;  // 16384 positions per tile
+constexpr int kB3 = 8;             // positions per batch
+constexpr int kFQ3 = 64;           // level-2 passes queued per wave (LDS)
+constexpr int kWQ3 = 32;           // weak hits queued per wave (LDS)
+constexpr uint32_t kMaxN3 = 4096;  // largest window whose tile fits beside the level-1 filter
+static_assert(kTile3 == kTile2, "k_scan_l1 and k_scan_lds share the host's tiling");
+
+struct Lds3 {
+    uint32_t nch, nh;                             // 64-byte rows, 32-byte halves
+    uint32_t ps, pv, pj, ntab, fq, wq, l1, total;  // byte offsets
+};
+__host__ __device__ __forceinline__ Lds3 lds3_layout(uint32_t n) {
+    Lds3 L;
+    L.nch = (kTile3 + n + 63) / 64 + 1;
+    L.nh = 2 * L.nch;
+    uint32_t o = L.nch * kRowDw * 4;
+    o = (o + 15) & ~15u; L.ps = o; o += (L.nh + 1) * 4;
+    L.pv = o; o += (L.nh + 1) * 4;
+    L.pj = o; o += (L.nh + 1) * 4;
+    o = (o + 15) & ~15u; L.ntab = o; o += 256 * 4;
+    L.fq = o; o += (kT3 / 64) * kFQ3 * 8;
+    L.wq = o; o += (kT3 / 64) * kWQ3 * 16;
+    L.l1 = o; o += kL1Words * 4;
+    L.total = o;
+    return L;
+}
+
+// Exact lookups of this wave's queued level-2 passes (all in the current tile), 64 per
+// round (positions at or past the segment end are dropped here); weak hits go to wq
+// and are verified from the LDS rows when wq cannot take another round, and at the end.
+__device__ __forceinline__ void drain_l1(const ScanArgs& a, const uint2* fq, uint32_t nfq, uint4* wq,
+                                         unsigned long long& weak_hits, const uint32_t* rows, uint64_t tile_start,
+                                         const SegCtx& cur) {
+    const uint32_t lane = threadIdx.x & 63;
+    lds_fence();
+    uint32_t nwq = 0;
+    for (uint32_t base = 0; base < nfq; base += 64) {
+        const uint32_t i = base + lane;
+        int64_t slot = -1;
+        uint32_t rp = 0;
+        if (i < nfq) {
+            const uint2 e = fq[i];  // {position in tile, weak}
+            const uint64_t p = tile_start + e.x;
+            if (p < cur.pos_end) slot = table_find(cur.keys, cur.bmask, e.y);
+            rp = (uint32_t)(p - cur.pos_begin);
+        }
+        const bool hit = slot >= 0;
+        const uint64_t m = __ballot(hit);
+        if (!m) continue;
+        const uint32_t cnt = __popcll(m);
+        weak_hits += cnt;
+        if (nwq + cnt > (uint32_t)kWQ3) {
+            lds_fence();
+            verify3<true>(a, wq, nwq, rows, tile_start, &cur);
+            nwq = 0;
+        }
+        const uint32_t rank = __popcll(m & ((1ull << lane) - 1));
+        const uint4 e = make_uint4(cur.seg_id, rp, (uint32_t)cur.slot_off + (uint32_t)slot, 0);
+        if (cnt > (uint32_t)kWQ3) {  // a round of more hits than wq holds (dense data): two halves
+            if (hit && rank < (uint32_t)kWQ3) wq[rank] = e;
+            lds_fence();
+            verify3<true>(a, wq, kWQ3, rows, tile_start, &cur);
+            if (hit && rank >= (uint32_t)kWQ3) wq[rank - kWQ3] = e;
+            nwq = cnt - kWQ3;
+        } else {
+            if (hit) wq[nwq + rank] = e;
+            nwq += cnt;
+        }
+    }
+    lds_fence();
+    verify3<true>(a, wq, nwq, rows, tile_start, &cur);
+    lds_fence();
+}
+
+__global__ __launch_bounds__(kT3, 2) void k_scan_l1(ScanArgs a, uint32_t per) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    const uint32_t n = a.n;
+    const Lds3 L = lds3_layout(n);
+    uint32_t* rows = (uint32_t*)smem;
+    uint32_t* PS = (uint32_t*)(smem + L.ps);
+    uint32_t* PV = (uint32_t*)(smem + L.pv);
+    uint32_t* PJ = (uint32_t*)(smem + L.pj);
+    uint32_t* ntab = (uint32_t*)(smem + L.ntab);
+    const uint32_t* l1 = (const uint32_t*)(smem + L.l1);
+    const uint32_t tid = threadIdx.x;
+    const uint32_t lane = tid & 63, wid = tid >> 6;
+    uint2* fq = (uint2*)(smem + L.fq) + (size_t)wid * kFQ3;
+    uint4* wq = (uint4*)(smem + L.wq) + (size_t)wid * kWQ3;
+    __shared__ uint32_t red_s[kT3 / 64], red_v[kT3 / 64], red_j[kT3 / 64];
+
+    const uint32_t t_begin = blockIdx.x * per;
+    const uint32_t t_end = min(a.ntiles, t_begin + per);
+    if (t_begin >= t_end) return;
+    // level-1 filter and the n*x table, once per workgroup (published by the first
+    // tile's barrier)
+    {
+        const uint4* g = (const uint4*)a.l1;
+        uint4* d = (uint4*)(smem + L.l1);
+#pragma unroll 4
+        for (uint32_t i = tid; i < kL1Words / 4; i += kT3) d[i] = g[i];
+    }
+    for (uint32_t i = tid; i < 256; i += kT3) ntab[i] = kMod - 1 - (a.nm * i) % kMod;
+    const uint32_t nch = L.nch, nh = L.nh;
+    const uint32_t sh = n & 3;
+    const uint32_t rel0 = tid * kR3;
+    const uint32_t orow = (tid >> 1) * kRowDw + 8 * (tid & 1);  // this thread's first out dword
+    const uint32_t din0 = (rel0 + n) >> 2;                      // ... and first in dword
+    unsigned long long passes = 0, weak_hits = 0;
+    uint32_t nfq = 0;
+    SegCtx sc;
+    const uint32_t* gfilt = a.filt;
+    uint32_t fwshift = 0;
+    uint32_t si = 0;
+#pragma unroll 1
+    for (uint32_t tile = t_begin; tile < t_end; ++tile) {
+        if (tile == t_begin || (si + 1 < a.nsegs && a.segs[si + 1].tile_base <= tile)) {
+            uint32_t lo = tile == t_begin ? 0 : si, hi = a.nsegs;
+            while (hi - lo > 1) {
+                const uint32_t mid = (lo + hi) >> 1;
+                if (a.segs[mid].tile_base <= tile) lo = mid; else hi = mid;
+            }
+            si = lo;
+            const ScanSeg S = a.segs[si];
+            const FileIx F = a.files[S.file];
+            sc.base = a.src + S.src;
+            sc.pos_begin = S.pos_begin;
+            sc.pos_end = S.pos_end;
+            sc.keys = a.keys + F.slot_off;
+            sc.slot_off = F.slot_off;
+            sc.bmask = F.bmask;
+            sc.seg_id = si;
+            fwshift = F.fwshift;
+            gfilt = a.filt + F.filt_off;
+        }
+        const uint64_t seg_len = a.segs[si].len;
+        const uint64_t tile_start = sc.pos_begin + (uint64_t)(tile - a.segs[si].tile_base) * kTile3;
+
+        // ---- phase 1: tile bytes -> LDS rows, half sums
+#pragma unroll 1
+        for (uint32_t c = tid; c < nch; c += kT3) {
+            uint32_t x[16];
+            load_chunk_nt(sc.base, seg_len, tile_start + 64ull * c, x);
+            uint32_t S0 = 0, V0 = 0, S1 = 0, V1 = 0;
+#pragma unroll
+            for (int i = 0; i < 8; ++i) {
+                S0 = udot4(x[i], 0x01010101u, S0);
+                V0 = udot4(x[i], offw(i), V0);
+                S1 = udot4(x[i + 8], 0x01010101u, S1);
+                V1 = udot4(x[i + 8], offw(i), V1);
+            }
+#pragma unroll
+            for (int i = 0; i < 16; ++i) rows[c * kRowDw + i] = x[i];
+            PS[2 * c] = S0; PS[2 * c + 1] = S1;
+            PV[2 * c] = V0; PV[2 * c + 1] = V1;
+        }
+        __syncthreads();
+
+        // ---- phase 2: exclusive prefix over the halves (PJ = sum of h * S_h < 2^31)
+        {
+            const uint32_t per_t = (nh + kT3 - 1) / kT3;
+            const uint32_t c_lo = min(nh, tid * per_t), c_hi = min(nh, c_lo + per_t);
+            uint32_t ts = 0, tv = 0, tj = 0;
+            for (uint32_t c = c_lo; c < c_hi; ++c) { ts += PS[c]; tv += PV[c]; tj += c * PS[c]; }
+            uint32_t is = ts, iv = tv, ij = tj;
+#pragma unroll
+            for (int m = 1; m < 64; m <<= 1) {
+                const uint32_t os = (uint32_t)__shfl_up((int)is, m, 64);
+                const uint32_t ov = (uint32_t)__shfl_up((int)iv, m, 64);
+                const uint32_t oj = (uint32_t)__shfl_up((int)ij, m, 64);
+                if (lane >= (uint32_t)m) { is += os; iv += ov; ij += oj; }
+            }
+            if (lane == 63) { red_s[wid] = is; red_v[wid] = iv; red_j[wid] = ij; }
+            __syncthreads();
+            uint32_t bs_ = 0, bv_ = 0, bj_ = 0;
+            for (uint32_t w = 0; w < wid; ++w) { bs_ += red_s[w]; bv_ += red_v[w]; bj_ += red_j[w]; }
+            uint32_t es = bs_ + is - ts, ev = bv_ + iv - tv, ej = bj_ + ij - tj;
+            for (uint32_t c = c_lo; c < c_hi; ++c) {
+                const uint32_t s0 = PS[c], v0 = PV[c];
+                PS[c] = es; PV[c] = ev; PJ[c] = ej;
+                es += s0; ev += v0; ej += c * s0;
+            }
+            if (tid == kT3 - 1) { PS[nh] = es; PV[nh] = ev; PJ[nh] = ej; }
+            __syncthreads();
+        }
+
+        // ---- phase 3: first window of this thread (tile offset 32*tid = half tid)
+        uint32_t am, bm;
+        {
+            const uint32_t c0 = tid, m = n >> 5, rem = n & 31;
+            const uint64_t dS = PS[c0 + m] - PS[c0];
+            const uint64_t dV = PV[c0 + m] - PV[c0];
+            const uint64_t dJ = PJ[c0 + m] - PJ[c0];
+            uint64_t A = dS;
+            uint64_t B = (uint64_t)n * dS - 32ull * (dJ - (uint64_t)c0 * dS) - dV;
+            for (uint32_t r = 0; r < rem; ++r) {
+                const uint32_t b = 32 * (c0 + m) + r;
+                const uint32_t xr = (rows[(b >> 6) * kRowDw + ((b >> 2) & 15)] >> (8 * (b & 3))) & 0xFF;
+                A += xr;
+                B += (uint64_t)(rem - r) * xr;
+            }
+            am = (uint32_t)((1 + A) % kMod);
+            bm = (uint32_t)((n + B) % kMod);
+        }
+
+        // ---- phase 4: roll.  Positions at or past pos_end (last tile of a segment)
+        // are rolled like the others and dropped by drain_l1's bound check.
+#pragma unroll 1
+        for (uint32_t g = 0; g < (uint32_t)kR3; g += kB3) {
+            uint32_t xo[2], xi[2];
+            xo[0] = rows[orow + (g >> 2)];
+            xo[1] = rows[orow + (g >> 2) + 1];
+            {
+                uint32_t dw[3];
+#pragma unroll
+                for (int j = 0; j < 3; ++j) {
+                    const uint32_t d = din0 + (g >> 2) + j;
+                    dw[j] = rows[(d >> 4) * kRowDw + (d & 15)];
+                }
+                xi[0] = __builtin_amdgcn_alignbyte(dw[1], dw[0], sh);
+                xi[1] = __builtin_amdgcn_alignbyte(dw[2], dw[1], sh);
+            }
+            uint32_t ct[kB3];
+#pragma unroll
+            for (int t = 0; t < kB3; ++t) ct[t] = ntab[(xo[t >> 2] >> (8 * (t & 3))) & 0xFF];
+            uint32_t wv[kB3], hq[kB3], ri[kB3], w1[kB3], w2[kB3];
+#pragma unroll
+            for (int t = 0; t < kB3; ++t) {
+                const uint32_t out = (xo[t >> 2] >> (8 * (t & 3))) & 0xFF;
+                const uint32_t in = (xi[t >> 2] >> (8 * (t & 3))) & 0xFF;
+                __builtin_assume(am < kMod);  // lets the 24-bit multiplies take am, bm as they are
+                __builtin_assume(bm < kMod);
+                wv[t] = (bm << 16) | am;
+                const ProbeHash h = probe_hash(am, bm);
+                hq[t] = h.q;
+                ri[t] = h.r >> fwshift;
+                w1[t] = l1[l1_word(h.q)];
+                const uint32_t u = am + in + (kMod - out);  // [M-255, 2M+255)
+                am = min(u, min(u - kMod, u - 2 * kMod));
+                const uint32_t v = bm + am + ct[t];          // [0, 3M)
+                bm = min(v, min(v - kMod, v - 2 * kMod));
+            }
+#pragma unroll
+            for (int t = 0; t < kB3; ++t) {
+                w2[t] = 0;  // level-1 miss: filt_pass(0, q) is false
+                if (l1_test(w1[t], hq[t])) w2[t] = gfilt[ri[t]];
+            }
+            uint32_t pbits = 0;
+#pragma unroll
+            for (int t = 0; t < kB3; ++t) pbits |= (filt_pass(w2[t], hq[t]) ? 1u : 0u) << t;
+            // opaque: the ballots below re-derive the masks instead of holding eight
+            // compare results in SGPRs (which spilled)
+            asm volatile("" : "+v"(pbits));
+            uint32_t tot = 0;
+#pragma unroll
+            for (int t = 0; t < kB3; ++t) tot += __popcll(__ballot((pbits >> t) & 1));
+            if (tot) {
+                if (nfq + tot > (uint32_t)kFQ3) {
+                    passes += nfq;
+                    drain_l1(a, fq, nfq, wq, weak_hits, rows, tile_start, sc);
+                    nfq = 0;
+                }
+                const uint64_t below = (1ull << lane) - 1;
+                if (tot <= (uint32_t)kFQ3) {
+#pragma unroll
+                    for (int t = 0; t < kB3; ++t) {
+                        const uint64_t mk = __ballot((pbits >> t) & 1);  // recomputed: 8 masks held would spill SGPRs
+                        if ((pbits >> t) & 1) fq[nfq + __popcll(mk & below)] = make_uint2(rel0 + g + t, wv[t]);
+                        nfq += __popcll(mk);
+                    }
+                } else {
+                    // degenerate data (more passes in one batch than the queue holds):
+                    // one position at a time
+#pragma unroll 1
+                    for (uint32_t t = 0; t < (uint32_t)kB3; ++t) {
+                        uint32_t w = wv[0];
+#pragma unroll
+                        for (int j = 1; j < kB3; ++j) w = t == (uint32_t)j ? wv[j] : w;
+                        const bool p = (pbits >> t) & 1;
+                        const uint64_t m1 = __ballot(p);
+                        if (nfq + __popcll(m1) > (uint32_t)kFQ3) {
+                            passes += nfq;
+                            drain_l1(a, fq, nfq, wq, weak_hits, rows, tile_start, sc);
+                            nfq = 0;
+                        }
+                        if (p) fq[nfq + __popcll(m1 & below)] = make_uint2(rel0 + g + t, w);
+                        nfq += __popcll(m1);
+                    }
+                }
+            }
+        }
+        if (nfq) {  // the tile's weak hits are verified while its bytes are in LDS
+            passes += nfq;
+            drain_l1(a, fq, nfq, wq, weak_hits, rows, tile_start, sc);
+            nfq = 0;
+        }
+        __syncthreads();  // rows / prefix arrays are rewritten by the next tile
+    }
+    if (lane == 0 && passes) atomicAdd(&a.counters[2], passes);
+    if (lane == 0 && weak_hits) atomicAdd(&a.counters[1], weak_hits);
 }
 
 // Tail rule (generator.rs:156-184): at p* = len - last_size (last_size < n), the
@@ -1467,10 +1810,12 @@ __global__ void k_tail(const uint8_t* __restrict__ buf, const TailJob* __restric
 // K6: apply_delta on the device (applier.rs:22-56 as a gather-copy)
 // ===========================================================================
 // One workgroup per piece (an op, or a <= 64 KiB slice of one).  Thread t writes the
-// aligned 16-byte destination chunks t, t+256, ...; a chunk wholly inside the piece
-// is assembled from two aligned 16-byte source loads with alignbyte (the source
-// misalignment (src - dst) & 15 is uniform per piece); the partial chunks at the two
-// ends of a piece are written byte by byte, so adjacent pieces never race.
+// 16-byte-aligned destination chunks t, t+256, ... (aligned in absolute addresses, so
+// any buffer offsets work); a chunk wholly inside the piece is assembled from two
+// aligned 16-byte source loads with alignbyte (the source address of destination
+// address x is x + delta, uniform per piece, so the misalignment delta & 15 is too);
+// the partial chunks at the two ends of a piece are written byte by byte, so adjacent
+// pieces never race.
 __device__ __forceinline__ uint32_t funnel(uint32_t hi, uint32_t lo, uint32_t r) {
     return __builtin_amdgcn_alignbyte(hi, lo, r);
 }
@@ -1478,16 +1823,14 @@ __device__ __forceinline__ uint32_t funnel(uint32_t hi, uint32_t lo, uint32_t r)
 __global__ __launch_bounds__(256) void k_apply(const ApplyPiece* __restrict__ pieces, const uint8_t* __restrict__ basis,
                                                const uint8_t* __restrict__ lit, uint8_t* __restrict__ out) {
     const ApplyPiece P = pieces[blockIdx.x];
-    const uint8_t* src = (P.from_basis ? basis : lit) + P.src;
-    uint8_t* dst = out + P.dst;
-    const uint64_t d0 = P.dst, d1 = P.dst + P.len;
-    const uint64_t c_first = d0 & ~15ull, c_end = (d1 + 15) & ~15ull;
-    const uint32_t sh = (uint32_t)((P.src - P.dst) & 15);  // source byte of dst byte x is at x + (src - dst)
+    const uintptr_t a0 = (uintptr_t)(out + P.dst), a1 = a0 + P.len;  // absolute destination range
+    const uintptr_t delta = (uintptr_t)((P.from_basis ? basis : lit) + P.src) - a0;  // mod 2^64
+    const uintptr_t c_first = a0 & ~(uintptr_t)15, c_end = (a1 + 15) & ~(uintptr_t)15;
+    const uint32_t sh = (uint32_t)(delta & 15);
     const uint32_t dq = sh >> 2, r = sh & 3;
-    for (uint64_t c = c_first + 16ull * threadIdx.x; c < c_end; c += 16ull * blockDim.x) {
-        if (c >= d0 && c + 16 <= d1) {
-            const uint8_t* s = src + (c - d0);
-            const uint4* sa = (const uint4*)((uintptr_t)s & ~(uintptr_t)15);
+    for (uintptr_t c = c_first + 16ull * threadIdx.x; c < c_end; c += 16ull * blockDim.x) {
+        if (c >= a0 && c + 16 <= a1) {
+            const uint4* sa = (const uint4*)((c + delta) & ~(uintptr_t)15);
             const uint4 A = sa[0];
             uint4 B = make_uint4(0, 0, 0, 0);
             if (sh) B = sa[1];
@@ -1500,10 +1843,10 @@ __global__ __launch_bounds__(256) void k_apply(const ApplyPiece* __restrict__ pi
                 case 2: o = make_uint4(funnel(w[3], w[2], r), funnel(w[4], w[3], r), funnel(w[5], w[4], r), funnel(w[6], w[5], r)); break;
                 default: o = make_uint4(funnel(w[4], w[3], r), funnel(w[5], w[4], r), funnel(w[6], w[5], r), funnel(w[7], w[6], r)); break;
             }
-            *(uint4*)(out + c) = o;
+            *(uint4*)c = o;
         } else {
-            const uint64_t lo = c < d0 ? d0 : c, hi = (c + 16 < d1) ? c + 16 : d1;
-            for (uint64_t x = lo; x < hi; ++x) dst[x - d0] = src[x - d0];
+            const uintptr_t lo = c < a0 ? a0 : c, hi = (c + 16 < a1) ? c + 16 : a1;
+            for (uintptr_t x = lo; x < hi; ++x) *(uint8_t*)x = *(const uint8_t*)(x + delta);
         }
     }
 }
@@ -2015,6 +2358,15 @@ __global__ void k_synth_mutate(uint8_t* __restrict__ dst, const uint8_t* __restr
 // ===========================================================================
 static inline unsigned grid_for(uint64_t threads, unsigned block) { return (unsigned)((threads + block - 1) / block); }
 
+// SYDELTA_SCAN_L1=0 scans large indexes with k_scan_lds instead of k_scan_l1 (A/B runs).
+static bool scan_l1_enabled() {
+    static const bool on = [] {
+        const char* e = getenv("SYDELTA_SCAN_L1");
+        return !(e && e[0] == '0');
+    }();
+    return on;
+}
+
 hipError_t launch_signature(const uint8_t* d_buf, uint64_t len, uint64_t bs, uint32_t* d_weak, uint64_t* d_strong,
                             hipStream_t s, Profiler* prof) {
     if (len == 0) return hipSuccess;
@@ -2081,6 +2433,7 @@ hipError_t launch_index_build(const uint32_t* d_weak, const uint64_t* d_strong, 
                               Profiler* prof) {
     hipError_t e;
     if ((e = hipMemsetAsync(ix.filt, 0, ix.fwords * 4, s))) return e;
+    if (ix.l1 && (e = hipMemsetAsync(ix.l1, 0, kL1Words * 4, s))) return e;
     if ((e = hipMemsetAsync(ix.keys, 0xFF, ix.nslots * 4, s))) return e;
     if ((e = hipMemsetAsync(ix.cnt, 0, ix.nslots * 4, s))) return e;
     const uint64_t n = ix.nblocks;
@@ -2088,7 +2441,7 @@ hipError_t launch_index_build(const uint32_t* d_weak, const uint64_t* d_strong, 
     {
         ProfScope ps(prof, s, "k_idx_insert");
         hipLaunchKernelGGL(k_idx_insert, dim3(grid_for(n, 256)), dim3(256), 0, s, d_weak, n, ix.d_fblk,
-                           (uint32_t)ix.nfiles, ix.d_files, ix.filt, ix.keys, ix.cnt, ix.slot_of);
+                           (uint32_t)ix.nfiles, ix.d_files, ix.filt, ix.l1, ix.keys, ix.cnt, ix.slot_of);
     }
     size_t tmp = 0;
     if ((e = hipcub::DeviceScan::ExclusiveSum(nullptr, tmp, ix.cnt, ix.start, (int)ix.nslots, s))) return e;
@@ -2183,6 +2536,29 @@ hipError_t launch_scan(const uint8_t* d_buf, const ScanSeg* d_segs, uint32_t nse
     a.hit_val = d_hit_val;
     a.out_cap = out_cap;
     a.counters = d_counters;
+    a.l1 = ix.l1;
+    static std::once_flag l1_once;
+    static hipError_t l1_err = hipSuccess;
+    static int l1_cus = 256;
+    const Lds3 L3 = lds3_layout(n);
+    if (ix.l1 && n <= kMaxN3 && scan_l1_enabled()) {
+        std::call_once(l1_once, [] {
+            l1_err = hipFuncSetAttribute((const void*)k_scan_l1, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                         160 * 1024 - 256);
+            int dev = 0, cus = 0;
+            if (hipGetDevice(&dev) == hipSuccess &&
+                hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess && cus > 0)
+                l1_cus = cus;
+        });
+        if (l1_err != hipSuccess) return l1_err;
+        if (L3.total > 160u * 1024 - 256) return hipErrorInvalidValue;
+        // one workgroup per CU (the level-1 filter fills its LDS), contiguous tile ranges
+        const uint32_t grid = (uint32_t)std::min<uint64_t>(ntiles, (uint64_t)l1_cus);
+        const uint32_t per = (ntiles + grid - 1) / grid;
+        ProfScope ps(prof, s, "k_scan_l1");
+        hipLaunchKernelGGL(k_scan_l1, dim3(grid), dim3(kT3), L3.total, s, a, per);
+        return hipGetLastError();
+    }
     const bool lds_filter = ix.max_fwords <= kLdsFilterWordsMax;
     const uint32_t lds_fwords = lds_filter ? std::max<uint32_t>(ix.max_fwords, 4u) : 0u;
     const Lds2 L = lds2_layout(n, lds_fwords);

@@ -13,6 +13,7 @@
 // integers in decimal, no whitespace.  Host writers and parsers for both, and the
 // device writer of a Delta whose literal bytes are in HBM (sydelta_kernels.hip K7:
 // literal runs dominate the text, ~3.6 characters per byte).
+#include <ctype.h>
 #include <errno.h>
 #include <stdio.h>
 #include <string.h>
@@ -103,36 +104,71 @@ struct Reader {
         }
         return true;
     }
-    // skip any JSON value (for unknown keys)
-    bool skip() {
+    // skip one JSON value (an unknown key's), validating it as serde_json's parser would
+    // (its default recursion limit is 128 levels)
+    bool skip(int depth = 0) {
         ws();
         if (p >= e) { err = "unexpected end"; return false; }
+        if (depth > 128) { err = "recursion limit exceeded"; return false; }
         if (*p == '{' || *p == '[') {
-            const char open = *p, close = open == '{' ? '}' : ']';
-            int depth = 0;
-            bool str = false;
-            for (; p < e; ++p) {
-                if (str) {
-                    if (*p == '\\') ++p;
-                    else if (*p == '"') str = false;
-                    continue;
+            const bool obj = *p == '{';
+            ++p;
+            if (eat(obj ? '}' : ']')) return true;
+            do {
+                if (obj) {
+                    ws();
+                    if (p >= e || *p != '"' || !string()) { err = "expected a key at byte " + std::to_string(pos()); return false; }
+                    if (!expect(':')) return false;
                 }
-                if (*p == '"') str = true;
-                else if (*p == open) ++depth;
-                else if (*p == close && --depth == 0) { ++p; return true; }
-            }
-            err = "unterminated value";
-            return false;
+                if (!skip(depth + 1)) return false;
+            } while (eat(','));
+            return expect(obj ? '}' : ']');
         }
-        if (*p == '"') {
-            for (++p; p < e; ++p) {
-                if (*p == '\\') ++p;
-                else if (*p == '"') { ++p; return true; }
-            }
-            err = "unterminated string";
-            return false;
+        if (*p == '"') return string();
+        for (const char* lit : {"true", "false", "null"}) {
+            const size_t l = strlen(lit);
+            if ((size_t)(e - p) >= l && memcmp(p, lit, l) == 0) { p += l; return true; }
         }
-        while (p < e && *p != ',' && *p != '}' && *p != ']') ++p;
+        // number: -?(0|[1-9][0-9]*)(.[0-9]+)?([eE][+-]?[0-9]+)?
+        const char* s = p;
+        auto digits = [&]() { const char* q = p; while (p < e && *p >= '0' && *p <= '9') ++p; return p > q; };
+        if (p < e && *p == '-') ++p;
+        if (p < e && *p == '0') ++p;
+        else if (!digits()) { p = s; err = "expected a value at byte " + std::to_string(pos()); return false; }
+        if (p < e && *p == '.') { ++p; if (!digits()) { err = "bad number at byte " + std::to_string(pos()); return false; } }
+        if (p < e && (*p == 'e' || *p == 'E')) {
+            ++p;
+            if (p < e && (*p == '+' || *p == '-')) ++p;
+            if (!digits()) { err = "bad number at byte " + std::to_string(pos()); return false; }
+        }
+        return true;
+    }
+    // a string at p (escapes checked for shape, control characters rejected)
+    bool string() {
+        ++p;
+        while (p < e) {
+            const unsigned char c = (unsigned char)*p;
+            if (c == '"') { ++p; return true; }
+            if (c < 0x20) { err = "control character in string at byte " + std::to_string(pos()); return false; }
+            if (c == '\\') {
+                if (++p >= e) break;
+                if (*p == 'u') {
+                    for (int i = 0; i < 4; ++i)
+                        if (++p >= e || !isxdigit((unsigned char)*p)) { err = "bad \\u escape"; return false; }
+                } else if (!*p || !strchr("\"\\/bfnrt", *p)) {
+                    err = "bad escape at byte " + std::to_string(pos());
+                    return false;
+                }
+            }
+            ++p;
+        }
+        err = "unterminated string";
+        return false;
+    }
+    // serde's derived Deserialize rejects a repeated field ("duplicate field `x`")
+    bool once(unsigned& seen, unsigned bit, const char* name) {
+        if (seen & bit) { err = std::string("duplicate field `") + name + "`"; return false; }
+        seen |= bit;
         return true;
     }
 };
@@ -191,14 +227,16 @@ extern "C" int sydelta_checksums_from_json(const char* json, uint64_t len, sydel
                     if (!r.key(k)) return bad();
                     uint64_t x = 0;
                     if (k == "index" || k == "offset" || k == "size" || k == "weak" || k == "strong") {
+                        const unsigned bit = k == "index" ? 1 : k == "offset" ? 2 : k == "size" ? 4 : k == "weak" ? 8 : 16;
+                        if (!r.once(seen, bit, k.c_str())) return bad();
                         if (!r.u64(x)) return bad();
-                        if (k == "index") { c.index = x; seen |= 1; }
-                        else if (k == "offset") { c.offset = x; seen |= 2; }
-                        else if (k == "size") { c.size = x; seen |= 4; }
+                        if (k == "index") c.index = x;
+                        else if (k == "offset") c.offset = x;
+                        else if (k == "size") c.size = x;
                         else if (k == "weak") {
                             if (x > 0xFFFFFFFFull) { r.err = "weak out of u32 range"; return bad(); }
-                            c.weak = (uint32_t)x; seen |= 8;
-                        } else { c.strong = x; seen |= 16; }
+                            c.weak = (uint32_t)x;
+                        } else c.strong = x;
                     } else if (!r.skip()) {
                         return bad();
                     }
@@ -309,7 +347,7 @@ extern "C" int sydelta_delta_from_json(const char* json, uint64_t len, sydelta_d
             std::string k;
             if (!r.key(k)) return bad();
             if (k == "ops") {
-                seen |= 1;
+                if (!r.once(seen, 1, "ops")) return bad();
                 if (!r.expect('[')) return bad();
                 if (!r.eat(']')) {
                     do {
@@ -324,8 +362,8 @@ extern "C" int sydelta_delta_from_json(const char* json, uint64_t len, sydelta_d
                                 do {
                                     std::string ck;
                                     if (!r.key(ck)) return bad();
-                                    if (ck == "offset") { if (!r.u64(off)) return bad(); f |= 1; }
-                                    else if (ck == "size") { if (!r.u64(size)) return bad(); f |= 2; }
+                                    if (ck == "offset") { if (!r.once(f, 1, "offset") || !r.u64(off)) return bad(); }
+                                    else if (ck == "size") { if (!r.once(f, 2, "size") || !r.u64(size)) return bad(); }
                                     else if (!r.skip()) return bad();
                                 } while (r.eat(','));
                                 if (!r.expect('}')) return bad();
@@ -356,11 +394,9 @@ extern "C" int sydelta_delta_from_json(const char* json, uint64_t len, sydelta_d
                     if (!r.expect(']')) return bad();
                 }
             } else if (k == "source_size") {
-                if (!r.u64(d->source_size)) return bad();
-                seen |= 2;
+                if (!r.once(seen, 2, "source_size") || !r.u64(d->source_size)) return bad();
             } else if (k == "block_size") {
-                if (!r.u64(d->block_size)) return bad();
-                seen |= 4;
+                if (!r.once(seen, 4, "block_size") || !r.u64(d->block_size)) return bad();
             } else if (!r.skip()) {
                 return bad();
             }

@@ -248,6 +248,38 @@ def test_apply_device_round_trip(bs, gpu, oracle_c):
     assert st["literal_bytes"] == sum(int(b) for k, b in zip(d.kind, d.b) if int(k) == 1)
 
 
+@pytest.mark.parametrize("offs", [(1, 3, 5), (15, 0, 9), (0, 7, 1), (8, 8, 8)])
+def test_apply_device_misaligned_views(offs, gpu, oracle_c):
+    """basis, literal and output buffers that are views at byte
+    offsets (basis[1:], lit[3:], out[5:]) rebuild the source exactly."""
+    import torch
+
+    ob, ol, oo = offs
+    bs = 1000
+    rng = random.Random(sum(offs) + 5)
+    basis = rng.randbytes(300 * bs + 123)
+    src = bytearray(_shift_edits(basis, rng, bs, 6))
+    for _ in range(6):
+        p = rng.randrange(len(src))
+        src[p:p] = rng.randbytes(rng.randint(1, 200 * 1024))  # Data ops longer than a slice
+    src = bytes(src)
+    idx = _index(gpu, basis, bs)
+    d = gpu.match(idx, _to_dev(src), length=len(src))
+    idx.close()
+    assert d.tuples() == _oracle_ops(oracle_c, src, basis, bs)
+    bbuf = torch.zeros(len(basis) + ob + 32, dtype=torch.uint8, device="cuda")
+    bbuf[ob:ob + len(basis)] = torch.frombuffer(bytearray(basis), dtype=torch.uint8).cuda()
+    lbuf = torch.zeros(len(src) + ol + 32, dtype=torch.uint8, device="cuda")
+    lbuf[ol:ol + len(src)] = torch.frombuffer(bytearray(src), dtype=torch.uint8).cuda()
+    obuf = torch.full((len(src) + oo + 32,), 0xEE, dtype=torch.uint8, device="cuda")
+    out, st = gpu.apply_device(bbuf[ob:ob + len(basis)], d, lbuf[ol:ol + len(src)], out=obuf[oo:oo + len(src)])
+    torch.cuda.synchronize()
+    assert st["bytes_written"] == len(src)
+    got = obuf.cpu().numpy()
+    assert bytes(got[oo:oo + len(src)]) == src
+    assert (got[:oo] == 0xEE).all() and (got[oo + len(src):] == 0xEE).all()  # nothing written outside
+
+
 def test_apply_device_rejects_copy_past_end(gpu):
     import torch
     import sy_amd._lib as L

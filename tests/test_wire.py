@@ -89,3 +89,48 @@ def test_delta_json_edge_cases():
         for k, x, y in zip(kind, a, b):
             exp.append({"Copy": {"offset": x, "size": y}} if k == 0 else {"Data": list(lit[x:x + y])})
         assert text.decode() == json.dumps({"ops": exp, "source_size": 17, "block_size": 8}, separators=(",", ":"))
+
+
+_SIG = '"index":0,"offset":0,"size":1,"weak":1,"strong":0'
+
+
+@pytest.mark.parametrize("bad", [
+    '[{' + _SIG + ',"index":0}]',                   # duplicate field (serde: "duplicate field `index`")
+    '[{' + _SIG + ',"weak":2}]',
+    '[{' + _SIG + ',"x":tru}]',                     # unknown key with an invalid value
+    '[{' + _SIG + ',"x":01}]',
+    '[{' + _SIG + ',"x":1.}]',
+    '[{' + _SIG + ',"x":"a\\q"}]',
+    '[{' + _SIG + ',"x":[1,]}]',
+    '[{' + _SIG + ',"x":{"a"}}]',
+    '[{' + _SIG + ',"x":' + '[' * 200 + ']' * 200 + '}]',  # past serde_json's recursion limit
+    '[{' + _SIG + ',"x":"\x01"}]',
+])
+def test_checksums_json_rejects_malformed(bad):
+    import sy_amd._lib as L
+
+    with pytest.raises(L.SyDeltaError):
+        wire.checksums_from_json(bad.encode())
+
+
+@pytest.mark.parametrize("good", [
+    '[{' + _SIG + ',"x":-1.5e+3}]', '[{' + _SIG + ',"x":null,"y":true,"z":[false,{"k":"v\\u00e9"}]}]',
+    '[{' + _SIG + ',"x":0,"x":1}]',  # repeated unknown keys are ignored, as serde does
+])
+def test_checksums_json_accepts_valid_unknown_values(good):
+    assert len(wire.checksums_from_json(good.encode())) == 1
+
+
+@pytest.mark.parametrize("bad", [
+    '{"ops":[],"ops":[],"source_size":0,"block_size":4}',
+    '{"ops":[],"source_size":0,"source_size":1,"block_size":4}',
+    '{"ops":[{"Copy":{"offset":0,"size":1,"size":2}}],"source_size":1,"block_size":4}',
+    '{"ops":[{"Copy":{"offset":0,"offset":0,"size":1}}],"source_size":1,"block_size":4}',
+    '{"ops":[],"source_size":0,"block_size":4,"x":[}',
+    '{"ops":[{"Data":[256]}],"source_size":1,"block_size":4}',
+])
+def test_delta_json_rejects_malformed(bad):
+    import sy_amd._lib as L
+
+    with pytest.raises(L.SyDeltaError):
+        wire.delta_from_json(bad.encode())
