@@ -43,6 +43,15 @@ sys.path.insert(0, ROOT)
 GIB = float(1 << 30)
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
 METRIC = "GiB/s device-resident delta signature+match, 4 KiB blocks; % HBM-read peak"
+# Random 4/8-byte gathers from an L2-resident table, chip-wide, whatever their width or
+# cache policy (profiles/r02_micro_gather2.txt: 262-281 G/s): the ceiling of a scan that
+# sends one request per window start to L2.
+L2_GATHER_PEAK = 265e9
+
+
+def metric_for(bs: int) -> str:
+    """BASELINE.json's metric, with the block size the run actually used."""
+    return METRIC if bs == 4096 else METRIC.replace("4 KiB", f"{bs / 1024:g} KiB")
 
 
 def parse():
@@ -318,6 +327,49 @@ def pmc_traffic(kernel: str, per_launch: int):
     return int(best) if best else None
 
 
+def algo_bytes_per_step(workload: str, n: int, nb_bytes: int, src_bytes: int) -> dict:
+    """Algorithmic HBM bytes per step of each kernel that can dominate a workload.  Per
+    step the signature kernels read the basis once and the scan reads the source once
+    (SURVEY.md section 8(d))."""
+    return {"k_scan": src_bytes, "k_scan_lds": src_bytes, "k_scan_l1": src_bytes,
+            "k_sig_fast": nb_bytes if workload == "c3" else n,
+            "k_sig_batch": n, "k_sig_wave": n, "k_probe": src_bytes,
+            "k_apply": 2 * n,  # apply: every output byte read once and written once
+            "k_json_write": n,  # json: every literal byte read once (text written: ~3.6x)
+            "k_block_cmp": 2 * n,  # local: both files read once
+            "k_xxh_pieces": n}  # xxh3: every file byte read once
+
+
+def roofline(prof: dict, steps: int, algo_step: dict, positions=None):
+    """Roofline of the dominant kernel: algorithmic bytes per launch / its average launch
+    time (HIP events on the launch stream, sydelta_profile).  A kernel launched L times
+    per step gets 1/L of its per-step bytes per launch (the scan is split into segments
+    of 2^31 positions).
+
+    For the scan in global-filter mode (k_scan_lds / k_scan over an index whose Bloom
+    filter lives in L2) the binding resource is not HBM but the L2 request rate: one
+    random filter-word request per window start.  `l2_gather` reports that rate against
+    L2_GATHER_PEAK (the measured chip-wide ceiling of random L2 gathers,
+    profiles/r02_micro_gather2.txt) when the step's scanned positions are known."""
+    dom = max(prof, key=lambda k: prof[k]["ms"]) if prof else None
+    if not dom or dom not in algo_step:
+        return None
+    launches_per_step = prof[dom]["count"] / steps
+    avg_ms = prof[dom]["ms"] / max(1, prof[dom]["count"])
+    per_launch = int(algo_step[dom] / launches_per_step)
+    ach = per_launch / (avg_ms * 1e-3) / 1e9
+    roof = {"bound": "hbm", "achieved": round(ach, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+            "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": pmc_traffic(dom, per_launch),
+            "kernel": dom, "avg_launch_ms": round(avg_ms, 4), "algorithmic_bytes_per_launch": per_launch}
+    if positions and dom in ("k_scan_lds", "k_scan"):
+        req = positions / launches_per_step  # one filter-word request per window start
+        rate = req / (avg_ms * 1e-3)
+        roof["l2_gather"] = {"requests_per_launch": int(req), "achieved": round(rate / 1e9, 2),
+                             "peak": round(L2_GATHER_PEAK / 1e9, 1), "unit": "G requests/s",
+                             "frac": round(rate / L2_GATHER_PEAK, 4)}
+    return roof
+
+
 def main():
     args = parse()
     import numpy as np
@@ -524,27 +576,11 @@ def main():
     value = total_bytes / elapsed / GIB
     ms_per_step = elapsed / args.steps * 1e3
 
-    # roofline of the dominant kernel: algorithmic bytes per launch / avg launch time.
-    # Per step the signature kernels read the basis once and the scan reads the source
-    # once; a kernel launched L times per step gets 1/L of that per launch (the scan is
-    # split into segments of 2^31 positions).
     src_bytes = int(files[3].sum()) if args.workload == "c4" else n
-    algo_step = {"k_scan": src_bytes, "k_scan_lds": src_bytes, "k_sig_fast": nb_bytes if args.workload == "c3" else n,
-                 "k_sig_batch": n, "k_sig_wave": n, "k_probe": src_bytes,
-                 "k_apply": 2 * n,  # apply: every output byte read once and written once
-                 "k_json_write": n,  # json: every literal byte read once (text written: ~3.6x)
-                 "k_block_cmp": 2 * n,  # local: both files read once
-                 "k_xxh_pieces": n}  # xxh3: every file byte read once
-    dom = max(prof, key=lambda k: prof[k]["ms"]) if prof else None
-    roof = None
-    if dom and dom in algo_step:
-        launches_per_step = prof[dom]["count"] / args.steps
-        avg_ms = prof[dom]["ms"] / max(1, prof[dom]["count"])
-        per_launch = int(algo_step[dom] / launches_per_step)
-        ach = per_launch / (avg_ms * 1e-3) / 1e9
-        roof = {"bound": "hbm", "achieved": round(ach, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": pmc_traffic(dom, per_launch),
-                "kernel": dom, "avg_launch_ms": round(avg_ms, 4), "algorithmic_bytes_per_launch": per_launch}
+    algo_step = algo_bytes_per_step(args.workload, n, nb_bytes, src_bytes)
+    stats = (last if isinstance(last, dict) else last.stats) if last is not None else None
+    positions = stats.get("positions") if isinstance(stats, dict) and args.workload == "c3" else None
+    roof = roofline(prof, args.steps, algo_step, positions)
     kernels = {k: {"avg_ms": round(v["ms"] / max(1, v["count"]), 4), "launches": v["count"]} for k, v in prof.items()}
 
     if rank == 0:
@@ -564,7 +600,7 @@ def main():
             hinc = host_inclusive(dev, bs, min(n, 1 << 30), local)
         sig_ms = kernels.get("k_sig_fast", {}).get("avg_ms")
         line = {
-            "metric": METRIC,
+            "metric": metric_for(bs),
             "value": round(value, 3),
             "unit": "GiB/s",
             "n_gpus": world,
@@ -609,7 +645,7 @@ def main():
             "host_inclusive": hinc,
             "kernels": kernels,
             "signature_only_gibps": round(n / (sig_ms * 1e-3) / GIB, 2) if sig_ms else None,
-            "match_stats": (last if isinstance(last, dict) else last.stats) if last is not None else None,
+            "match_stats": stats,
         }
         print(json.dumps(line), flush=True)
     if world > 1:

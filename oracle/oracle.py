@@ -48,27 +48,27 @@ def py_adler32(data: bytes) -> int:
 
 
 class PyAdler32:
-    """struct Adler32, rolling.rs:16-92 (u32 wrap semantics kept)."""
+    """struct Adler32, rolling.rs:16-91 (u32 wrap semantics kept)."""
 
-    def __init__(self, block_size: int):  # :62-68
+    def __init__(self, block_size: int):  # :26-32
         self.a, self.b, self.block_size = 1, 0, block_size
 
-    def update_block(self, block: bytes):  # :84-92
+    def update_block(self, block: bytes):  # :48-56
         self.a, self.b = 1, 0
         for x in block:
             self.a = (self.a + x) % MOD_ADLER
             self.b = (self.b + self.a) % MOD_ADLER
 
-    def roll(self, old: int, new: int):  # :102-115
+    def roll(self, old: int, new: int):  # :66-79
         n = self.block_size & 0xFFFFFFFF
         self.a = ((self.a + MOD_ADLER * 2 - old + new) & 0xFFFFFFFF) % MOD_ADLER
         n_old = ((n * old) & 0xFFFFFFFF) % MOD_ADLER
         self.b = ((self.b + MOD_ADLER * 3 - n_old + self.a - 1) & 0xFFFFFFFF) % MOD_ADLER
 
-    def digest(self) -> int:  # :118-120
+    def digest(self) -> int:  # :82-84
         return (self.b << 16) | self.a
 
-    def reset(self):  # :124-127
+    def reset(self):  # :88-91
         self.a, self.b = 1, 0
 
 

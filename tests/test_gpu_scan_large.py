@@ -1,5 +1,6 @@
-"""GPU parity for large single-file indexes (> 16 Ki basis blocks): the level-1-filter
-scan (k_scan_l1) against the oracle.
+"""GPU parity for large single-file indexes (> 16 Ki basis blocks): both scans of a
+large index -- k_scan_lds in global-filter mode (the default) and the level-1-filter
+scan k_scan_l1 (SYDELTA_SCAN_L1=1) -- against the oracle.
 
 * 96 MiB basis, mixed edits (an all-literal stretch, sparse substitutions, a shift,
   planted unaligned copies, duplicated blocks): bit-exact op list against the C
@@ -20,6 +21,13 @@ import pytest
 from oracle import oracle as O
 
 pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(params=["lds", "l1"])
+def scanner(request, monkeypatch):
+    """The large-index scan kernel (read by launch_scan on every call)."""
+    monkeypatch.setenv("SYDELTA_SCAN_L1", "1" if request.param == "l1" else "0")
+    return request.param
 
 
 def _ops_device(gpu, basis_t, src_t, bs, src_len=None, probe=None):
@@ -77,7 +85,7 @@ def _mixed_source(basis: np.ndarray, bs: int, seed: int) -> np.ndarray:
 
 
 @pytest.mark.parametrize("probe", ["0", "1"])
-def test_large_index_mixed_edits(gpu, oracle_c, probe):
+def test_large_index_mixed_edits(gpu, oracle_c, scanner, probe):
     import torch
 
     bs = 4096
@@ -96,7 +104,7 @@ def test_large_index_mixed_edits(gpu, oracle_c, probe):
     assert d.stats["copy_ops"] > 10000
 
 
-def test_large_index_dense_passes(gpu, oracle_c):
+def test_large_index_dense_passes(gpu, oracle_c, scanner):
     """All-zero and period-3 stretches against a random basis that holds a zero block
     and the three phases of the period-3 block: every window start there is a weak
     hit, so the per-wave pass queue overflows inside one batch (the one position at
@@ -123,7 +131,7 @@ def test_large_index_dense_passes(gpu, oracle_c):
     assert d.tuples() == O.ops_from_arrays(*oracle_c.generate_delta(src, ew, es, ez, bs))
 
 
-def test_config3_full_size_planted(gpu, oracle_c):
+def test_config3_full_size_planted(gpu, oracle_c, scanner):
     """C3 at 4 GiB with a non-trivial expected op list."""
     import torch
 
