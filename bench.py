@@ -85,44 +85,109 @@ def parse():
     return a
 
 
-def cpu_baseline(bs: int):
-    """sy's CPU delta path restated in C (oracle/, 'port'): rayon-style parallel
-    signature on `threads` cores + single-threaded greedy scan, on a bounded sample
-    of the C3 workload; returns GiB/s for the full (sig + match) byte count."""
+def host_cores():
+    """Host threads a CPU baseline may use: the affinity mask (os.sched_getaffinity),
+    capped by the cgroup CPU quota when one is set (the GPU box gives a job a share of
+    a large host: nproc and the mask show every core there).  Returns (threads,
+    affinity count, quota or None)."""
+    aff = len(os.sched_getaffinity(0))
+    quota = None
+    try:
+        q, per = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        if q != "max":
+            quota = max(1, int(int(q) / int(per)))
+    except (OSError, ValueError):
+        pass
+    return (min(aff, quota) if quota else aff), aff, quota
+
+
+def cpu_baseline(basis, src, src_len: int, bs: int, scan_bytes: int = 256 << 20, file_bytes: int = 512 << 20):
+    """sy's CPU delta path restated in C (oracle/, 'port') on the C3 pair itself (host
+    copies of the device inputs): the signature of the WHOLE basis on the host's cores
+    (checksum.rs:31-80, rayon over blocks), then the single-threaded greedy scan
+    (generator.rs:116-221) of the first `scan_bytes` of the source (`src` holds at least
+    that prefix) against that full signature (1 Mi keys at 4 GiB), extrapolated to the
+    whole source of `src_len` bytes.  Variants: the
+    per-block open/seek/read signature of checksum.rs:50-59 on a page-cache-warm file of
+    `file_bytes` of the basis."""
+    import tempfile
+
     import numpy as np
 
     from oracle import oracle as O
 
     C = O.C()
-    threads = int(os.environ.get("SYDELTA_CPU_THREADS", "16"))
-    sig_n, scan_n = 512 << 20, 64 << 20
-    basis = O.synth_bytes(sig_n, 0x5E1D0002)
+    threads, aff, quota = host_cores()
     t0 = time.perf_counter()
     w, s, z = C.compute_checksums(basis, bs, threads=threads)
     t_sig = time.perf_counter() - t0
-    # scan sample: source = basis prefix with 5% byte substitutions, probed against
-    # the signature of that prefix (same per-position work as the full scan)
-    rng = np.random.default_rng(0x5E1D0003)
-    src = basis[:scan_n].copy()
-    m = rng.random(scan_n) < 0.05
-    src[m] ^= rng.integers(1, 256, int(m.sum()), dtype=np.uint8)
-    nb = scan_n // bs
+    scan_n = min(scan_bytes, src.size)
     t0 = time.perf_counter()
-    C.generate_delta(src, w[:nb], s[:nb], z[:nb], bs)
+    C.generate_delta(src[:scan_n], w, s, z, bs)
     t_scan = time.perf_counter() - t0
-    sig_rate = sig_n / t_sig          # bytes/s, `threads` threads
-    scan_rate = scan_n / t_scan       # bytes/s, 1 thread (generator.rs is sequential)
-    full = 4 * GIB
-    t_full = full / sig_rate + full / scan_rate
+    sig_rate = basis.size / t_sig    # bytes/s, `threads` threads
+    scan_rate = scan_n / t_scan      # bytes/s, 1 thread (generator.rs is sequential)
+    t_full = basis.size / sig_rate + src_len / scan_rate
+    # the file-reading signature (open + seek + read per block, each worker its own fd)
+    fb = min(file_bytes, basis.size) // bs * bs
+    file_rate = None
+    with tempfile.NamedTemporaryFile(dir=os.environ.get("TMPDIR", "/tmp"), delete=True) as f:
+        basis[:fb].tofile(f.name)
+        nb = fb // bs
+        fw = np.zeros(max(nb, 1), np.uint32)
+        fs = np.zeros(max(nb, 1), np.uint64)
+        C.L.oracle_compute_checksums_file(f.name.encode(), bs, fw.ctypes.data, fs.ctypes.data, nb, threads)  # warm
+        t0 = time.perf_counter()
+        got = C.L.oracle_compute_checksums_file(f.name.encode(), bs, fw.ctypes.data, fs.ctypes.data, nb, threads)
+        dt = time.perf_counter() - t0
+        if got == nb and np.array_equal(fw[:nb], w[:nb]):
+            file_rate = fb / dt
     return {
-        "value": round(2 * full / t_full / GIB, 5),
+        "value": round((basis.size + src_len) / t_full / GIB, 5),
         "unit": "GiB/s",
         "cores": threads,
+        "affinity_cores": aff,
+        "cgroup_quota_cores": quota,
         "kind": "port",
-        "sample": (f"signature of {sig_n >> 20} MiB on {threads} threads ({sig_rate / GIB:.3f} GiB/s) + "
-                   f"single-thread rolling scan of {scan_n >> 20} MiB with 5% byte edits "
-                   f"({scan_rate / 2**20:.2f} MiB/s); extrapolated to 4 GiB + 4 GiB"),
+        "sample": (f"signature of the whole {basis.size / GIB:g} GiB basis on {threads} threads "
+                   f"({sig_rate / GIB:.3f} GiB/s, {w.size} keys) + single-thread rolling scan of the first "
+                   f"{scan_n >> 20} MiB of the source against it ({scan_rate / 2**20:.2f} MiB/s); "
+                   f"scan extrapolated to the whole source"),
+        "variants": {
+            "signature_file_per_block_read_gibps": round(file_rate / GIB, 3) if file_rate else None,
+            "signature_file_sample_mib": fb >> 20,
+            "signature_in_memory_gibps": round(sig_rate / GIB, 3),
+            "scan_single_thread_mibps": round(scan_rate / 2**20, 2),
+        },
     }
+
+
+def cpu_c4_baseline(basis, new, files, bs: int, workers: int = 10, sample_files: int = 500):
+    """C4 on the host the way sy runs it: up to `workers` file transfers at once
+    (cli.rs:178-180, --parallel default 10), each one compute_checksums of its basis +
+    the sequential scan of its new file (the C oracle, which releases the GIL), over
+    the first `sample_files` files; bytes = basis + new bytes of those files."""
+    from concurrent.futures import ThreadPoolExecutor
+
+    from oracle import oracle as O
+
+    C = O.C()
+    boff, blen, soff, slen = files
+    k = min(sample_files, len(boff))
+    hb = [basis[int(boff[i]):int(boff[i] + blen[i])] for i in range(k)]
+    hn = [new[int(soff[i]):int(soff[i] + slen[i])] for i in range(k)]
+
+    def one(i):
+        w, s, z = C.compute_checksums(hb[i], bs)
+        C.generate_delta(hn[i], w, s, z, bs)
+
+    t0 = time.perf_counter()
+    with ThreadPoolExecutor(workers) as ex:
+        list(ex.map(one, range(k)))
+    dt = time.perf_counter() - t0
+    nbytes = int(blen[:k].sum() + slen[:k].sum())
+    return {"value": round(nbytes / dt / GIB, 4), "unit": "GiB/s", "cores": workers, "kind": "port",
+            "sample": f"{k} file pairs ({nbytes >> 20} MiB) on {workers} concurrent transfers (C oracle)"}
 
 
 def cpu_json_baseline(src_dev, bs: int):
@@ -586,7 +651,11 @@ def main():
     if rank == 0:
         cpu = None
         if world == 1 and not args.no_cpu_baseline and args.workload == "c3":
-            cpu = cpu_baseline(bs)
+            cpu = cpu_baseline(basis[:nb_bytes].cpu().numpy(), new[:min(n, 256 << 20)].cpu().numpy(), n, bs)
+        if world == 1 and not args.no_cpu_baseline and args.workload == "c4":
+            k = min(500, len(files[0]))  # the sampled files' bytes only
+            cpu = cpu_c4_baseline(basis[:int(files[0][k - 1] + files[1][k - 1])].cpu().numpy(),
+                                  new[:int(files[2][k - 1] + files[3][k - 1])].cpu().numpy(), files, bs, sample_files=k)
         if world == 1 and not args.no_cpu_baseline and args.workload == "json":
             cpu = cpu_json_baseline(new, bs)
         if world == 1 and not args.no_cpu_baseline and args.workload == "xxh3":

@@ -33,3 +33,38 @@ def test_roofline_split_launches_and_no_gather():
 def test_metric_names_block_size():
     assert bench.metric_for(4096) == bench.METRIC
     assert "64 KiB" in bench.metric_for(65536)
+
+
+def test_cpu_baselines_run_small():
+    """The CPU baselines on small host inputs: cores from the affinity mask, the scan
+    against the whole signature, the file-reading signature agreeing with the in-memory
+    one, and the C4 worker pool."""
+    import numpy as np
+
+    from oracle import oracle as O
+
+    threads, aff, quota = bench.host_cores()
+    assert 1 <= threads <= aff
+    bs = 4096
+    basis = O.synth_bytes(8 << 20, 0x5E1D0002)
+    src = basis.copy()
+    rng = np.random.default_rng(1)
+    m = rng.random(src.size) < 0.05
+    src[m] ^= 0x5A
+    r = bench.cpu_baseline(basis, src, src.size, bs, scan_bytes=1 << 20, file_bytes=2 << 20)
+    assert r["value"] > 0 and r["cores"] == threads and r["affinity_cores"] == aff
+    assert r["variants"]["signature_file_per_block_read_gibps"] is not None
+    assert "2048 keys" in r["sample"]
+    # C4: three 64 KiB pairs packed at 16-byte-aligned offsets
+    fs = 64 << 10
+    stride = (fs + 1 + 15) & ~15
+    hb = np.zeros(3 * stride, np.uint8)
+    hn = np.zeros(3 * stride, np.uint8)
+    for k in range(3):
+        b = O.synth_bytes(fs, 7 + k)
+        hb[k * stride:k * stride + fs] = b
+        hn[k * stride:k * stride + fs + 1] = np.concatenate([b[:100], [1], b[100:]])
+    offs = np.arange(3, dtype=np.uint64) * stride
+    files = (offs, np.full(3, fs, np.uint64), offs.copy(), np.full(3, fs + 1, np.uint64))
+    c = bench.cpu_c4_baseline(hb, hn, files, bs, workers=2)
+    assert c["value"] > 0 and c["cores"] == 2
