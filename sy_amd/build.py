@@ -14,7 +14,10 @@ ROOT = os.path.dirname(HERE)
 CSRC = os.path.join(HERE, "csrc")
 LIB = os.path.join(HERE, "libsydelta.so")
 SOURCES = ["sydelta_kernels.hip", "sydelta_api.cpp", "sydelta_wire.cpp", "sydelta_local.cpp", "sydelta_integrity.cpp"]
-HEADERS = ["sydelta_device.hpp", "sydelta_internal.hpp", "sydelta_host.hpp", os.path.join("..", "..", "include", "sydelta.h")]
+HEADERS = ["sydelta_device.hpp", "sydelta_internal.hpp", "sydelta_host.hpp", "sydelta_walk.hpp",
+           os.path.join("..", "..", "include", "sydelta.h")]
+# objects stay in build/obj (the host sanitizer test links sydelta_kernels.o)
+OBJDIR = os.path.join(ROOT, "build", "obj")
 ARCH = os.environ.get("SYDELTA_ARCH", "gfx950")
 
 
@@ -31,8 +34,9 @@ def build(force: bool = False, verbose: bool = False) -> str:
     hipcc = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
     objs = []
     jobs = []
+    os.makedirs(OBJDIR, exist_ok=True)
     for src in SOURCES:
-        obj = os.path.join(CSRC, src.rsplit(".", 1)[0] + ".o")
+        obj = os.path.join(OBJDIR, src.rsplit(".", 1)[0] + ".o")
         cmd = [hipcc, f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-Wall", "-Wno-unused-result",
                "-I", os.path.join(ROOT, "include"), "-x", "hip", "-c", os.path.join(CSRC, src), "-o", obj]
         objs.append(obj)
@@ -49,8 +53,6 @@ def build(force: bool = False, verbose: bool = False) -> str:
     if r.returncode != 0:
         raise RuntimeError(f"link failed:\n{r.stdout}")
     os.replace(tmp, LIB)
-    for o in objs:
-        os.remove(o)
     return LIB
 
 

@@ -568,190 +568,19 @@ struct DevBuf {
     DevBuf& operator=(const DevBuf&) = delete;
 };
 
-constexpr uint32_t kNoBlk = 0xFFFFFFFFu;
-constexpr uint64_t kUnknownNone = UINT64_MAX;
-
-// One source being classified: a whole file of a batch, or a chunk of one file.
-struct Src {
-    uint32_t file = 0;          // basis file in the index
-    uint64_t off = 0;           // byte offset of source position 0 from the launch base
-    uint64_t len = 0;           // bytes readable from position 0 (zeros beyond, see load_chunk)
-    uint64_t flen = 0;          // source file length (Delta::source_size)
-    uint64_t p0 = 0, p1 = 0;    // full-window positions to classify, [p0, p1); p0 % n == 0
-    uint64_t kb = 0, nblk = 0;  // blocks kb .. kb+nblk-1 (position k*n) cover [p0, p1)
-    bool probed = false;
-    std::vector<uint32_t> ahit;    // probed: per block, its aligned window's hit or kNoBlk
-    uint64_t nahit = 0;            // aligned windows that hit
-    std::vector<uint8_t> scanned;  // probed: per block, all its window starts were scanned
-    std::vector<uint64_t> hpos;    // hits found by scans, sorted, unique
-    std::vector<uint32_t> hblk;    // their global block indices
-    std::vector<uint64_t> ppos;    // probed: per block, its phase-probed window start or kUnknownNone
-    std::vector<uint32_t> phit;    // ... and that window's hit or kNoBlk
-};
-
-// Merge sorted (pos, blk) lists into c's hits (equal positions carry equal blocks).
-void merge_hits(Src& c, const std::vector<uint64_t>& pos, const std::vector<uint32_t>& blk) {
-    if (pos.empty()) return;
-    if (c.hpos.empty() || pos.front() > c.hpos.back()) {  // later positions: append
-        c.hpos.insert(c.hpos.end(), pos.begin(), pos.end());
-        c.hblk.insert(c.hblk.end(), blk.begin(), blk.end());
-        return;
-    }
-    std::vector<uint64_t> np;
-    std::vector<uint32_t> nb;
-    np.reserve(c.hpos.size() + pos.size());
-    nb.reserve(c.hpos.size() + pos.size());
-    size_t i = 0, j = 0;
-    while (i < c.hpos.size() || j < pos.size()) {
-        if (j == pos.size() || (i < c.hpos.size() && c.hpos[i] < pos[j])) {
-            np.push_back(c.hpos[i]); nb.push_back(c.hblk[i]); ++i;
-        } else if (i == c.hpos.size() || pos[j] < c.hpos[i]) {
-            np.push_back(pos[j]); nb.push_back(blk[j]); ++j;
-        } else {
-            np.push_back(pos[j]); nb.push_back(blk[j]); ++i; ++j;
-        }
-    }
-    c.hpos.swap(np);
-    c.hblk.swap(nb);
-}
-
-// First position of [x, p) whose class is unknown (window starts inside a probed
-// block that was not scanned; its aligned start k*n is known), or kUnknownNone.
-uint64_t first_unknown(const Src& c, uint64_t n, uint64_t x, uint64_t p) {
-    if (!c.probed || x >= p) return kUnknownNone;
-    const uint64_t kend = std::min(c.kb + c.nblk, (p - 1) / n + 1);
-    for (uint64_t k = std::max(c.kb, x / n); k < kend; ++k) {
-        if (c.scanned[k - c.kb]) continue;
-        uint64_t lo = std::max(x, k * n + 1);
-        const uint64_t hi = std::min(p, k * n + n);
-        // a phase-probed window start inside the block is classified too
-        if (lo < hi && !c.ppos.empty() && c.ppos[k - c.kb] == lo) ++lo;
-        if (lo < hi) return lo;
-    }
-    return kUnknownNone;
-}
-
-// The basis file a walk copies from.
-struct BasisInfo {
-    uint64_t blk_base;   // its first global block
-    uint64_t nblocks;
-    uint64_t last_size;  // size of its last block
-};
-
-// Greedy walk (generator.rs:116-221 / 283-379) over c's classified positions from
-// `entry` up to `end` (c.p1, or a split point of a parallel walk).  ops get Data(source offset, len) and Copy(basis offset, size); consecutive
-// Copies are never merged (generator.rs:135-140).  A non-final chunk ends with the
-// literal run up to p1 (continued by the next chunk) and *exit = where the walk left
-// [p0, p1).  A final source (its file ends inside it) applies the tail rule
-// (generator.rs:156-184: only p* = len - last_size can match) and the last literal
-// run.  Returns 1 with *need = the first position whose class is unknown.
-int walk_src(const Src& c, uint64_t n, uint64_t entry, uint64_t end, const BasisInfo& bi, bool final_src,
-             int tail_match, OpVec& ops, uint64_t* exit, uint64_t* need) {
-    const size_t ops0 = ops.size();  // appended to; rolled back on a need
-    {
-        const uint64_t span = c.p1 > c.p0 ? c.p1 - c.p0 : 1;
-        const double frac = end > entry ? double(end - entry) / double(span) : 0.0;
-        ops.reserve(ops0 + (size_t)(2.0 * double(c.hpos.size() + c.nahit) * std::min(1.0, frac)) + 16);
-    }
-    uint64_t x = entry, lit = entry;
-    auto data = [&](uint64_t a, uint64_t b) {
-        if (b > a) ops.push_back({SYDELTA_OP_DATA, 0, a, b - a});
-    };
-    auto copy = [&](uint64_t gblk) {
-        const uint64_t b = gblk - bi.blk_base;
-        ops.push_back({SYDELTA_OP_COPY, 0, b * n, (b + 1 == bi.nblocks) ? bi.last_size : n});
-    };
-    size_t i = std::lower_bound(c.hpos.begin(), c.hpos.end(), x) - c.hpos.begin();
-    const size_t H = c.hpos.size();
-    const uint64_t kend = c.kb + c.nblk;
-    uint64_t ka = c.kb;  // next aligned window that may hit (probed sources)
-    uint64_t kp = c.kb;  // next block whose phase-probed window may hit
-    const bool has_phase = c.probed && !c.ppos.empty();
-    while (x < end) {
-        // next hit at or after x and before end: the next scan hit or the next aligned hit
-        while (i < H && c.hpos[i] < x) ++i;
-        uint64_t p = end;
-        uint32_t pb = kNoBlk;
-        if (i < H && c.hpos[i] < end) { p = c.hpos[i]; pb = c.hblk[i]; }
-        if (c.probed) {
-            if (ka * n < x) ka = (x + n - 1) / n;  // after an aligned Copy x == (ka+1)*n: no division
-            while (ka < kend && ka * n < p && c.ahit[ka - c.kb] == kNoBlk) ++ka;
-            if (ka < kend && ka * n < p) { p = ka * n; pb = c.ahit[ka - c.kb]; }
-            if (has_phase) {  // phase-probed hits (one window per block, inside it)
-                if (kp * n + n <= x) kp = x / n;
-                while (kp < kend && kp * n < p &&
-                       (c.ppos[kp - c.kb] < x || c.ppos[kp - c.kb] == kUnknownNone || c.phit[kp - c.kb] == kNoBlk))
-                    ++kp;
-                if (kp < kend && c.ppos[kp - c.kb] < p && c.ppos[kp - c.kb] >= x && c.phit[kp - c.kb] != kNoBlk) {
-                    p = c.ppos[kp - c.kb];
-                    pb = c.phit[kp - c.kb];
-                }
-            }
-        }
-        const uint64_t u = first_unknown(c, n, x, p);
-        if (u != kUnknownNone) {
-            *need = u;
-            ops.resize(ops0);
-            return 1;
-        }
-        if (pb == kNoBlk) {
-            x = end;
-            break;
-        }
-        data(lit, p);
-        copy(pb);
-        x = p + n;  // generator.rs:144 / :313
-        lit = x;
-    }
-    if (!final_src) {
-        data(lit, end);
-        *exit = std::max(x, end);
-        return 0;
-    }
-    if (tail_match && bi.nblocks) {
-        const uint64_t pstar = c.flen - bi.last_size;
-        if (pstar >= lit) {
-            data(lit, pstar);
-            copy(bi.blk_base + bi.nblocks - 1);
-            lit = c.flen;
-        }
-    }
-    data(lit, c.flen);
-    *exit = c.flen;
-    return 0;
-}
+using walk::BasisInfo;
+using walk::first_unknown;
+using walk::kNoBlk;
+using walk::kUnknownNone;
+using walk::merge_hits;
+using walk::run_parallel;
+using walk::Src;
+using walk::walk_src;
 
 double ms_since(std::chrono::steady_clock::time_point t0);
 int walk_threads();
 uint64_t walk_par_min();
 
-// Run task(t) for t in [0, n): t = 0 on the calling thread, the others on std::threads
-// (inline when a thread cannot be started).  No exception leaves: returns false when a
-// task threw (out of memory), so the C entry points can report SYDELTA_E_OOM.
-template <class F>
-bool run_parallel(int n, F&& task) {
-    std::atomic<bool> ok{true};
-    auto guarded = [&](int t) {
-        try {
-            task(t);
-        } catch (...) {
-            ok = false;
-        }
-    };
-    std::vector<std::thread> th;
-    int t = 1;
-    for (; t < n; ++t) {
-        try {
-            th.emplace_back(guarded, t);
-        } catch (...) {
-            break;
-        }
-    }
-    for (int u = t; u < n; ++u) guarded(u);
-    guarded(0);
-    for (auto& x : th) x.join();
-    return ok;
-}
 
 bool phase_probe_on() {
     // "1": probe long miss runs at their phase (opt-in: on the C4 shape the unaligned
@@ -1226,81 +1055,23 @@ int Classifier::walk_parallel(size_t i, uint64_t entry, const BasisInfo& bi, boo
     const uint64_t nh = c.nahit + c.hpos.size();
     const int T0 = walk_threads();
     if (T0 < 2 || nh < walk_par_min() || c.p1 <= entry || (c.p1 - entry) / n < 2 * (uint64_t)T0) return 2;
-    // split points: multiples of n strictly inside (entry, p1)
-    std::vector<uint64_t> st{entry};
-    for (int t = 1; t < T0; ++t) {
-        const uint64_t q = (entry + (c.p1 - entry) / T0 * t) / n * n;
-        if (q > st.back() && q < c.p1) st.push_back(q);
-    }
-    const int T = (int)st.size();
-    st.push_back(c.p1);
-    std::vector<OpVec> part(T);
-    std::vector<uint64_t> ex(T, 0), need(T, 0);
-    std::vector<int> rc(T, 0);
-    static const bool host_timing = getenv("SYDELTA_HOST_TIMING") != nullptr;
+    const std::vector<uint64_t> st = walk::split_points(c, n, entry, T0);
+    struct Pool {
+        OpVec take(size_t want) { return take_ops(want); }
+        void give(OpVec&& v) { give_ops(std::move(v)); }
+    } pool;
     const auto t0 = std::chrono::steady_clock::now();
-    OpVec joined = take_ops(nh);  // before the segments' arrays, so they do not take it
-    for (int t = 0; t < T; ++t) part[t] = take_ops(2 * nh / T + 64);
-    struct Give {
-        std::vector<OpVec>& v;
-        ~Give() {
-            for (auto& x : v) give_ops(std::move(x));
-        }
-    } give{part};
-    std::vector<double> tseg(T, 0.0);
-    auto seg = [&](int t, uint64_t from) {
-        const auto ts = std::chrono::steady_clock::now();
-        part[t].clear();
-        const bool fin = final_src && t == T - 1;
-        rc[t] = walk_src(c, n, from, st[t + 1], bi, fin, tail_match, part[t], &ex[t], &need[t]);
-        tseg[t] = ms_since(ts);
-    };
-    if (!run_parallel(T, [&](int t) { seg(t, t ? st[t] : entry); }))
-        return fail(SYDELTA_E_OOM, "out of host memory (op lists)");
-    const double t_walk = ms_since(t0);
-    if (rc[0]) return 1;
-    // chain: segment t's true entry is segment t-1's exit
-    for (int t = 1; t < T; ++t) {
-        if (ex[t - 1] != st[t]) seg(t, ex[t - 1]);
-        if (rc[t]) return 1;
-    }
-    // join, merging a Data op that ends where the next segment's first Data op starts
-    std::vector<size_t> at(T + 1, 0), skip(T, 0);
-    bool last_data = false;  // the joined list so far ends with a Data op ending at last_end
-    uint64_t last_end = 0;
-    for (int t = 0; t < T; ++t) {
-        const OpVec& v = part[t];
-        if (!v.empty() && last_data && v[0].kind == SYDELTA_OP_DATA && last_end == v[0].a) {
-            skip[t] = 1;
-            last_end += v[0].b;
-        }
-        at[t + 1] = at[t] + v.size() - skip[t];
-        if (v.size() > skip[t]) {
-            last_data = v.back().kind == SYDELTA_OP_DATA;
-            last_end = v.back().a + v.back().b;
-        }
-    }
-    const double t_chain = ms_since(t0);
-    OpVec& ops = d->ops;
-    ops.swap(joined);
-    give_ops(std::move(joined));
-    const size_t cap0 = ops.capacity();
-    ops.resize(at[T]);
-    run_parallel(T, [&](int t) {
-        if (part[t].size() > skip[t])
-            memcpy(ops.data() + at[t], part[t].data() + skip[t], (part[t].size() - skip[t]) * sizeof(sydelta_op));
-    });
-    // merged lengths: the op before each skipped one absorbs it
-    for (int t = 1; t < T; ++t)
-        if (skip[t]) ops[at[t] - 1].b += part[t][0].b;  // the op before segment t absorbs its first
-    *exit = ex[T - 1];
-    if (host_timing)
+    walk::SplitTiming tm;
+    const int r = walk::walk_split(c, n, st, bi, final_src, tail_match, d->ops, exit, pool,
+                                   [&] { return ms_since(t0); }, &tm);
+    if (r < 0) return fail(SYDELTA_E_OOM, "out of host memory (op lists)");
+    static const bool host_timing = getenv("SYDELTA_HOST_TIMING") != nullptr;
+    if (host_timing && r == 0)
         fprintf(stderr,
                 "sydelta parallel walk: %d segments, walk %.3f ms (segment max %.3f min %.3f), chain %.3f ms, "
-                "join %.3f ms (cap %zu)\n",
-                T, t_walk, *std::max_element(tseg.begin(), tseg.end()), *std::min_element(tseg.begin(), tseg.end()),
-                t_chain - t_walk, ms_since(t0) - t_chain, cap0);
-    return 0;
+                "join %.3f ms\n",
+                (int)st.size() - 1, tm.walk_ms, tm.seg_max_ms, tm.seg_min_ms, tm.chain_ms, tm.join_ms);
+    return r;
 }
 
 void finish_stats_impl(sydelta_delta* d) {

@@ -11,28 +11,8 @@
 
 #include "../../include/sydelta.h"
 #include "sydelta_internal.hpp"
+#include "sydelta_walk.hpp"  // OpVec
 
-// Op arrays grow without zero-filling: resize() default-initialises the POD ops, so a
-// parallel walk can size the joined array and fill it from several threads.
-template <class T>
-struct NoInitAlloc : std::allocator<T> {
-    template <class U>
-    struct rebind {
-        using other = NoInitAlloc<U>;
-    };
-    NoInitAlloc() = default;
-    template <class U>
-    NoInitAlloc(const NoInitAlloc<U>&) {}
-    template <class U>
-    void construct(U* p) noexcept {
-        ::new ((void*)p) U;
-    }
-    template <class U, class... A>
-    void construct(U* p, A&&... a) {
-        ::new ((void*)p) U(std::forward<A>(a)...);
-    }
-};
-using OpVec = std::vector<sydelta_op, NoInitAlloc<sydelta_op>>;
 
 // Delta (generator.rs:19-25): ops plus, for host-data entry points, the literal bytes.
 struct sydelta_delta {
