@@ -310,6 +310,12 @@ typedef struct sydelta_change_ratio {
 int sydelta_estimate_change_ratio_device(int device, const uint8_t *d_src, uint64_t src_len, const uint8_t *d_dst,
                                          uint64_t dst_len, uint64_t block_size, int64_t sample_count,
                                          double threshold, void *stream, sydelta_change_ratio *out);
+/* ratio.rs:78 `estimate_change_ratio(source: &Path, dest: &Path, block_size, sample_count:
+ * Option<usize>, threshold: Option<f64>) -> io::Result<ChangeRatioResult>` on two paths:
+ * the sampled blocks are read from the files and hashed on the current device
+ * (sample_count < 0 / threshold < 0: the defaults).  Open/read failures -> SYDELTA_E_IO. */
+int sydelta_estimate_change_ratio(const char *source_path, const char *dest_path, uint64_t block_size,
+                                  int64_t sample_count, double threshold, sydelta_change_ratio *out);
 
 /* ---------------------------------------------------------------------------
  * Whole-file XXH3-64, bytes already in device memory.

@@ -109,6 +109,8 @@ SIGNATURES = [
     ("sydelta_block_compare_device", _i, [_i, _vp, _u64, _vp, _u64, _u64, _vp, _vp, ctypes.POINTER(BlockCompareStatsC)]),
     ("sydelta_estimate_change_ratio_device", _i, [_i, _vp, _u64, _vp, _u64, _u64, ctypes.c_int64, ctypes.c_double,
                                                   _vp, ctypes.POINTER(ChangeRatioC)]),
+    ("sydelta_estimate_change_ratio", _i, [ctypes.c_char_p, ctypes.c_char_p, _u64, ctypes.c_int64, ctypes.c_double,
+                                           ctypes.POINTER(ChangeRatioC)]),
     ("sydelta_xxh3_device", _i, [_i, _vp, _u64, _vp, _vp]),
     ("sydelta_xxh3_batch_device", _i, [_i, _vp, _u64, _vp, _vp, _u64, _vp, _vp]),
     ("sydelta_set_profiling", None, [_i]),

@@ -13,11 +13,11 @@ Reference functions and where they are mirrored:
 ``generate_delta``     generator.rs:242  ``generate_delta``
 ``apply_delta``        applier.rs:22     ``apply_delta`` (host file I/O)
 ``calculate_block_size`` mod.rs:20       ``calculate_block_size``
+``estimate_change_ratio`` ratio.rs:78    ``estimate_change_ratio`` (sampled blocks hashed
+                                         on the device)
 ``Adler32``            rolling.rs:16     ``Adler32``
 ``BlockChecksum``/``Delta``/``DeltaOp``  dataclasses below
 =======================================  =====================================
-
-``estimate_change_ratio`` (ratio.rs) is out of scope.
 """
 from __future__ import annotations
 
@@ -226,3 +226,29 @@ def apply_delta(old_file, delta: Delta, new_file) -> DeltaStats:
                 literal += len(op.data)
                 written += len(op.data)
     return DeltaStats(len(delta.ops), literal, written)
+
+
+@dataclass(frozen=True)
+class ChangeRatioResult:
+    """ratio.rs:11-27."""
+
+    change_ratio: float
+    blocks_sampled: int
+    blocks_changed: int
+    use_delta: bool
+    threshold: float
+
+    def change_ratio_percent(self) -> str:
+        """ratio.rs:47-50."""
+        return f"{self.change_ratio * 100.0:.1f}%"
+
+
+def estimate_change_ratio(source, dest, block_size: int, sample_count: int | None = None,
+                          threshold: float | None = None) -> ChangeRatioResult:
+    """ratio.rs:78-192: sample evenly spaced blocks of both files and compare their
+    XXH3-64 (computed on the device); I/O errors raise SyDeltaError."""
+    r = _lib.ChangeRatioC()
+    check(lib.sydelta_estimate_change_ratio(_pathb(source), _pathb(dest), block_size,
+                                            -1 if sample_count is None else sample_count,
+                                            -1.0 if threshold is None else threshold, ctypes.byref(r)))
+    return ChangeRatioResult(r.change_ratio, r.blocks_sampled, r.blocks_changed, bool(r.use_delta), r.threshold)

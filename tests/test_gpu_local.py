@@ -102,3 +102,73 @@ def test_block_compare_large_properties(gpu):
     assert torch.equal(got.cpu(), exp)
     assert st["changed_blocks"] == int(exp.sum()) and st["literal_bytes"] == int(exp.sum()) * bs
     assert st["bytes_written"] == n
+
+
+@pytest.mark.parametrize("sample_count,threshold", [(None, None), (5, None), (1, 0.5), (0, None), (1000, 0.1)])
+@pytest.mark.parametrize("case", CASES, ids=lambda c: c[0])
+def test_change_ratio_paths_match_oracle(case, sample_count, threshold, tmp_path):
+    """The path-level estimate_change_ratio (files read on the host, sampled blocks
+    hashed on the device) against the oracle on the same bytes."""
+    from sy_amd import delta
+
+    name, src, dst, bs = case
+    ps, pd = tmp_path / "source.bin", tmp_path / "dest.bin"
+    ps.write_bytes(src)
+    pd.write_bytes(dst)
+    r, sampled, changed, use, thr = O.py_estimate_change_ratio(src, dst, bs, sample_count, threshold)
+    got = delta.estimate_change_ratio(ps, pd, bs, sample_count, threshold)
+    assert (got.change_ratio, got.blocks_sampled, got.blocks_changed, got.use_delta, got.threshold) == \
+        (r, sampled, changed, use, thr)
+
+
+@pytest.mark.parametrize("name", ["same", "all_changed", "partial", "threshold", "size", "small_sample"])
+def test_change_ratio_paths_reference_tests(name, tmp_path):
+    """ratio.rs:199-325, the reference's own tests, through the path API."""
+    from sy_amd import delta
+
+    src = bytearray(b"\x2a" * MiB)
+    dst = bytes(b"\x2a" * MiB)
+    if name == "all_changed":
+        dst = b"\x63" * MiB
+    elif name == "partial":
+        src[:256 * 1024] = b"\x63" * (256 * 1024)
+    elif name == "threshold":
+        src[:800 * 1024] = b"\x63" * (800 * 1024)
+    elif name == "size":
+        src = bytearray(b"\x2a" * (2 * MiB))
+    ps, pd = tmp_path / "source.bin", tmp_path / "dest.bin"
+    ps.write_bytes(bytes(src))
+    pd.write_bytes(dst)
+    r = delta.estimate_change_ratio(ps, pd, BS, 5 if name == "small_sample" else None)
+    if name in ("same", "small_sample"):
+        assert r.blocks_changed == 0 and r.change_ratio == 0.0 and r.use_delta
+        assert r.blocks_sampled == (5 if name == "small_sample" else 16)
+    elif name == "all_changed":
+        assert r.blocks_changed == r.blocks_sampled and r.change_ratio == 1.0 and not r.use_delta
+    elif name == "partial":
+        assert 0 < r.blocks_changed < r.blocks_sampled and 0.0 < r.change_ratio < 1.0 and r.use_delta
+    elif name == "threshold":
+        assert not r.use_delta
+        assert delta.estimate_change_ratio(ps, pd, BS, threshold=0.90).use_delta
+    else:
+        assert not r.use_delta
+
+
+def test_change_ratio_paths_large_sample(tmp_path, gpu):
+    """More samples than one 64 MiB batch: 300 MiB files, 64 KiB blocks, every block
+    sampled, edits in 37 of them."""
+    from sy_amd import delta
+
+    n = 300 * MiB
+    base = O.synth_bytes(n, 21)
+    ed = base.copy()
+    rng = np.random.default_rng(4)
+    blocks = rng.choice(n // BS, 37, replace=False)
+    ed[blocks * BS + 17] ^= 0x11
+    ps, pd = tmp_path / "source.bin", tmp_path / "dest.bin"
+    ed.tofile(ps)
+    base.tofile(pd)
+    r = delta.estimate_change_ratio(ps, pd, BS, sample_count=n // BS)
+    exp = O.py_estimate_change_ratio(ed.tobytes(), base.tobytes(), BS, n // BS)
+    assert (r.change_ratio, r.blocks_sampled, r.blocks_changed, r.use_delta) == exp[:4]
+    assert r.blocks_changed == 37

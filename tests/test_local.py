@@ -92,3 +92,26 @@ def test_block_compare_counts(slen, dlen):
         exp.append(int(s != d))
     assert flags == exp
     assert lit == sum(min(BS, slen - k * BS) for k in range(nb) if flags[k])
+
+
+def test_ratio_paths_host_only_cases(tmp_path):
+    """The path API's cases decided before any device work (ratio.rs:89-121): a missing
+    file is an I/O error, a > 50 % size difference and an empty destination return
+    without sampling."""
+    import sy_amd._lib as L
+    from sy_amd import delta
+
+    ps, pd = tmp_path / "source.bin", tmp_path / "dest.bin"
+    ps.write_bytes(b"\x2a" * (2 * MiB))
+    with pytest.raises(L.SyDeltaError):
+        delta.estimate_change_ratio(ps, tmp_path / "missing.bin", BS)
+    with pytest.raises(L.SyDeltaError):
+        delta.estimate_change_ratio(tmp_path / "missing.bin", ps, BS)
+    pd.write_bytes(b"\x2a" * MiB)
+    r = delta.estimate_change_ratio(ps, pd, BS)  # ratio.rs:292-307
+    assert (r.change_ratio, r.blocks_sampled, r.blocks_changed, r.use_delta) == (1.0, 0, 0, False)
+    assert r.change_ratio_percent() == "100.0%"
+    pd.write_bytes(b"")
+    r = delta.estimate_change_ratio(ps, pd, BS, threshold=0.9)
+    assert (r.change_ratio, r.blocks_sampled, r.use_delta, r.threshold) == (1.0, 0, False, 0.9)
+    assert r == delta.ChangeRatioResult(*O.py_estimate_change_ratio(ps.read_bytes(), b"", BS, threshold=0.9))
