@@ -1,6 +1,9 @@
-"""Device Delta JSON writer (K7) against the host writer (itself checked against
-json.dumps in test_wire.py): bit-identical text for copy-heavy, literal-heavy
-(multi-chunk Data runs) and mixed deltas, including empty Data ops."""
+"""Device Delta JSON writer (K7) against the host writer and against an independent
+writer -- Python's json.dumps with serde's compact separators and the field order of
+generator.rs:10-25 (ssh.rs:1003 serde_json::to_string(&delta)): bit-identical text for
+copy-heavy, literal-heavy (multi-chunk Data runs) and mixed deltas, including empty
+Data ops, and for a text past 2^32 bytes."""
+import json
 import random
 
 import numpy as np
@@ -30,6 +33,14 @@ def _cases():
     yield "copies", [0] * 5000, [i * 8192 for i in range(5000)], [8192] * 5000, src
 
 
+def _dumps(kind, a, b, source_size, bs, src) -> bytes:
+    """serde_json::to_string(&Delta) restated with json.dumps (generator.rs:10-25:
+    DeltaOp::Copy{offset,size} / DeltaOp::Data(Vec<u8>), then source_size, block_size)."""
+    ops = [{"Copy": {"offset": x, "size": y}} if k == 0 else {"Data": list(src[x:x + y])}
+           for k, x, y in zip(kind, a, b)]
+    return json.dumps({"ops": ops, "source_size": source_size, "block_size": bs}, separators=(",", ":")).encode()
+
+
 @pytest.mark.parametrize("case", list(_cases()), ids=lambda c: c[0])
 def test_device_json_equals_host(case, gpu):
     import torch
@@ -42,6 +53,38 @@ def test_device_json_equals_host(case, gpu):
     got = bytes(dev.cpu().numpy())
     assert len(got) == len(host)
     assert got == host
+    assert got == _dumps(kind, a, b, len(src), 4096, src)
+
+
+def test_device_json_past_4gib_against_dumps(gpu):
+    """A 1.25 GiB literal run of a 256-byte period (a permutation of 0..255), then a
+    Copy and a short Data run: > 4 GiB of text.  json.dumps writes one period's text and
+    the ops around the run; the device text is compared with them on the device, the
+    run as a [periods x period-text] view."""
+    import torch
+
+    P, L = 256, 5 << 28
+    perm = np.random.default_rng(17).permutation(P).astype(np.uint8)
+    lit = torch.from_numpy(perm).cuda().repeat(L // P + 1)[:L + 16].contiguous()
+    kind, a, b = [1, 0, 1], [0, 12345, 100], [L, 4096, 5]
+    text = wire.delta_to_json_device(kind, a, b, L + 4096, 4096, lit[:L])
+    torch.cuda.synchronize()
+    period = json.dumps(perm.tolist(), separators=(",", ":"))[1:-1].encode() + b","  # "v0,v1,...,v255,"
+    T = len(period)
+    head = b'{"ops":[{"Data":['
+    rest = json.dumps({"ops": [{"Data": []}, {"Copy": {"offset": 12345, "size": 4096}},
+                               {"Data": perm[100:105].tolist()}], "source_size": L + 4096, "block_size": 4096},
+                      separators=(",", ":")).encode()
+    rest = rest[rest.index(b"]},"):]  # from the first (empty) Data op's "]"
+    nrep = L // P
+    assert text.numel() == len(head) + nrep * T - 1 + len(rest)
+    assert text.numel() > (1 << 32)
+    assert bytes(text[:len(head)].cpu().numpy()) == head
+    body = text[len(head):len(head) + nrep * T].view(nrep, T)
+    row = torch.frombuffer(bytearray(period), dtype=torch.uint8).cuda()
+    assert bool((body[:-1] == row).all())
+    assert bool((body[-1, :T - 1] == row[:T - 1]).all())
+    assert bytes(text[len(head) + nrep * T - 1:].cpu().numpy()) == rest
 
 
 def test_device_json_text_past_4gib(gpu):
