@@ -331,9 +331,13 @@ struct sydelta_index {
     void* d_pool = nullptr;           // one allocation for all index arrays
 };
 
+// Stream-ordered release on the calling thread's library stream (a hipFree would wait
+// for the whole device, i.e. for every other caller's work).  Every entry point that
+// reads an index synchronizes its stream before returning, so no queued work still
+// reads the pool; the memory pool reuses it only in stream order after this point.
 static void index_release(sydelta_index* x) {
     if (!x) return;
-    if (x->d_pool) (void)hipFree(x->d_pool);
+    if (x->d_pool) (void)hipFreeAsync(x->d_pool, thread_stream(x->device));
     delete x;
 }
 
@@ -408,7 +412,7 @@ static int index_create_impl(int device, const uint32_t* weak, const uint64_t* s
     const size_t sz_l1 = want_l1 ? al(4 * (size_t)kL1Words) : 0;
     const size_t total =
         sz_weak + sz_strong + sz_filt + sz_l1 + 4 * sz_t + sz_order + sz_slot + sz_files + sz_fblk + sz_cstrong;
-    HIP_TRY(hipMalloc(&x->d_pool, total));
+    HIP_TRY(hipMallocAsync(&x->d_pool, total, s));  // stream-ordered: no device-wide synchronization
     uint8_t* p = (uint8_t*)x->d_pool;
     x->d_weak = (uint32_t*)p; p += sz_weak;
     x->d_strong = (uint64_t*)p; p += sz_strong;

@@ -7,9 +7,15 @@
 #include <stdint.h>
 #include <string.h>
 
+#include <stdlib.h>
+
 #include <algorithm>
 #include <atomic>
+#include <condition_variable>
+#include <deque>
+#include <functional>
 #include <memory>
+#include <mutex>
 #include <thread>
 #include <utility>
 #include <vector>
@@ -195,32 +201,112 @@ inline int walk_src(const Src& c, uint64_t n, uint64_t entry, uint64_t end, cons
     return 0;
 }
 
-// Run task(t) for t in [0, n): t = 0 on the calling thread, the others on std::threads
-// (inline when a thread cannot be started).  No exception leaves: returns false when a
-// task threw (out of memory), so the C entry points can report SYDELTA_E_OOM.
-template <class F>
-bool run_parallel(int n, F&& task) {
-    std::atomic<bool> ok{true};
-    auto guarded = [&](int t) {
-        try {
-            task(t);
-        } catch (...) {
-            ok = false;
+// Process-wide worker pool shared by every caller's parallel host work (walk
+// segments, probe-result fills): concurrent entry-point calls share its threads
+// instead of each starting its own.  Size: SYDELTA_HOST_THREADS,
+// else the hardware threads capped at 16.  Threads start on first use and are never
+// joined (the pool outlives static destruction).
+class HostPool {
+  public:
+    struct Batch {
+        std::function<void(int)> f;
+        int n = 0;
+        std::atomic<int> next{0}, done{0};
+        std::atomic<bool> ok{true};
+        std::mutex mu;
+        std::condition_variable cv;
+        void work() {
+            for (;;) {
+                const int i = next.fetch_add(1);
+                if (i >= n) return;
+                try {
+                    f(i);
+                } catch (...) {
+                    ok = false;
+                }
+                if (done.fetch_add(1) + 1 == n) {
+                    std::lock_guard<std::mutex> lk(mu);
+                    cv.notify_all();
+                }
+            }
         }
     };
-    std::vector<std::thread> th;
-    int t = 1;
-    for (; t < n; ++t) {
-        try {
-            th.emplace_back(guarded, t);
-        } catch (...) {
-            break;
+    static HostPool& get() {
+        static HostPool* p = new HostPool();  // never destroyed: workers may still wait on it at exit
+        return *p;
+    }
+    int size() const { return nthreads_; }
+    // Run f(0..n): the caller works on the batch too, so a call completes even when
+    // every pool thread is busy with other callers' batches.  False if a task threw.
+    bool run(int n, std::function<void(int)> f) {
+        if (n <= 0) return true;
+        auto b = std::make_shared<Batch>();
+        b->f = std::move(f);
+        b->n = n;
+        const int helpers = std::min(n - 1, nthreads_);
+        if (helpers > 0) {
+            try {
+                start();
+                std::lock_guard<std::mutex> lk(mu_);
+                for (int i = 0; i < helpers; ++i) q_.push_back(b);
+            } catch (...) {  // no threads: the caller runs the whole batch
+            }
+            cv_.notify_all();
+        }
+        b->work();
+        std::unique_lock<std::mutex> lk(b->mu);
+        b->cv.wait(lk, [&] { return b->done.load() == b->n; });
+        return b->ok;
+    }
+
+  private:
+    HostPool() {
+        const char* e = getenv("SYDELTA_HOST_THREADS");
+        const unsigned hw = std::thread::hardware_concurrency();
+        nthreads_ = (e && *e) ? std::max(0, atoi(e)) : (int)std::min(16u, std::max(1u, hw));
+    }
+    void start() {
+        std::call_once(once_, [this] {
+            for (int t = 0; t < nthreads_; ++t) std::thread([this] { loop(); }).detach();
+        });
+    }
+    void loop() {
+        for (;;) {
+            std::shared_ptr<Batch> b;
+            {
+                std::unique_lock<std::mutex> lk(mu_);
+                cv_.wait(lk, [&] { return !q_.empty(); });
+                b = std::move(q_.front());
+                q_.pop_front();
+            }
+            b->work();
         }
     }
-    for (int u = t; u < n; ++u) guarded(u);
-    guarded(0);
-    for (auto& x : th) x.join();
-    return ok;
+    int nthreads_ = 0;
+    std::once_flag once_;
+    std::mutex mu_;
+    std::condition_variable cv_;
+    std::deque<std::shared_ptr<Batch>> q_;
+};
+
+// Run task(t) for t in [0, n) on the shared pool (and the calling thread).  No
+// exception leaves: returns false when a task threw (out of memory), so the C entry
+// points can report SYDELTA_E_OOM.
+template <class F>
+bool run_parallel(int n, F&& task) {
+    if (n == 1) {
+        try {
+            task(0);
+            return true;
+        } catch (...) {
+            return false;
+        }
+    }
+    try {
+        return HostPool::get().run(n, [&](int t) { task(t); });
+    } catch (...) {
+        return false;
+    }
 }
 
 // Split points of a parallel walk of c from `entry`: multiples of n strictly inside

@@ -67,3 +67,22 @@ def test_host_code_under_asan_ubsan():
     assert r.returncode == 0, (r.stdout[-2000:], r.stderr[-6000:])
     assert "host_fuzz ok" in r.stdout
     assert "runtime error" not in r.stderr  # UBSan reports
+
+
+@pytest.mark.timeout(600)
+def test_host_pool_under_tsan():
+    """The shared host pool and the split walk from 10 caller threads at once under
+    ThreadSanitizer (tests/csrc/pool_tsan.cpp): no data race, results equal the serial
+    walk."""
+    if shutil.which("g++") is None:
+        pytest.skip("needs g++")
+    os.makedirs(OUT, exist_ok=True)
+    exe = os.path.join(OUT, "pool_tsan")
+    r = subprocess.run(["g++", "-std=c++17", "-O1", "-g", "-fsanitize=thread", "-I" + os.path.join(ROOT, "include"),
+                        "-I" + CSRC, os.path.join(ROOT, "tests", "csrc", "pool_tsan.cpp"), "-o", exe, "-lpthread"],
+                       capture_output=True, text=True)
+    assert r.returncode == 0, r.stderr[-4000:]
+    env = dict(os.environ, TSAN_OPTIONS="halt_on_error=1:second_deadlock_stack=1", SYDELTA_HOST_THREADS="6")
+    r = subprocess.run([exe], capture_output=True, text=True, env=env, timeout=500)
+    assert r.returncode == 0, (r.stdout[-2000:], r.stderr[-6000:])
+    assert "pool_tsan ok" in r.stdout and "WARNING: ThreadSanitizer" not in r.stderr
