@@ -410,14 +410,18 @@ static int index_create_impl(int device, const uint32_t* weak, const uint64_t* s
     // level-1 filter for k_scan_l1: one large file (the BASELINE C3 shape)
     const bool want_l1 = nfiles == 1 && nblocks > kLdsFilterKeys;
     const size_t sz_l1 = want_l1 ? al(4 * (size_t)kL1Words) : 0;
-    const size_t total =
-        sz_weak + sz_strong + sz_filt + sz_l1 + 4 * sz_t + sz_order + sz_slot + sz_files + sz_fblk + sz_cstrong;
+    const size_t sz_fat = want_l1 ? al(16 * (size_t)sl) : 0;
+    const size_t total = sz_weak + sz_strong + sz_filt + sz_l1 + sz_fat + 4 * sz_t + sz_order + sz_slot + sz_files +
+                         sz_fblk + sz_cstrong;
     HIP_TRY(hipMallocAsync(&x->d_pool, total, s));  // stream-ordered: no device-wide synchronization
     uint8_t* p = (uint8_t*)x->d_pool;
     x->d_weak = (uint32_t*)p; p += sz_weak;
     x->d_strong = (uint64_t*)p; p += sz_strong;
     ix.filt = (uint32_t*)p; p += sz_filt;
-    if (want_l1) { ix.l1 = (uint32_t*)p; p += sz_l1; }
+    if (want_l1) {
+        ix.l1 = (uint32_t*)p; p += sz_l1;
+        ix.fat = (uint4*)p; p += sz_fat;
+    }
     ix.keys = (uint32_t*)p; p += sz_t;
     ix.cnt = (uint32_t*)p; p += sz_t;
     ix.start = (uint32_t*)p; p += sz_t;
@@ -795,9 +799,11 @@ int Classifier::scan(const std::vector<std::array<uint64_t, 3>>& ranges) {
         HIP_TRY(hipMemcpyAsync(counts, d_counts, 128, hipMemcpyDeviceToHost, s));
         HIP_TRY(hipStreamSynchronize(s));
         if (getenv("SYDELTA_PHASE_TIMING"))
-            fprintf(stderr, "sydelta phase cycles (wave 0, summed over workgroups): stage %llu prefix %llu roll %llu flush %llu"
-                            " (lookup %llu verify %llu) passes %llu weak %llu\n",
-                    counts[4], counts[5], counts[6], counts[7], counts[8], counts[9], counts[2], counts[1]);
+            fprintf(stderr, "sydelta phase cycles (wave 0, summed over workgroups): [k_scan_lds: stage prefix roll flush"
+                            " lookup verify; k_scan_l1: stage window roll prefetch drain barrier] %llu %llu %llu %llu"
+                            " %llu %llu l1 passes %llu passes %llu weak %llu positions %llu\n",
+                    counts[4], counts[5], counts[6], counts[7], counts[8], counts[9], counts[3], counts[2], counts[1],
+                    (unsigned long long)tot_pos);
         if (counts[0] <= cap) break;
         want = counts[0];  // dense hits: grow once and rescan
     }

@@ -12,9 +12,9 @@ namespace sydelta {
 constexpr uint32_t kEmptyKey = 0xFFFFFFFFu;  // never a valid weak: A = weak & 0xFFFF <= 65520
 constexpr uint64_t kLdsFilterKeys = 16384;   // index sizes whose Bloom filter (<= 32 KiB) the scan keeps in LDS
 constexpr uint32_t kLdsFilterWordsMax = 8192;
-// Level-1 filter of a large single-file index (k_scan_l1 keeps it in LDS): 30720 words
-// = 120 KiB = 983040 bits, built for indexes of more than kLdsFilterKeys keys.
-constexpr uint32_t kL1Words = 30720;
+// Level-1 filter of a large single-file index (k_scan_l1 keeps it in LDS): 32768 words
+// = 128 KiB = 2^20 bits, built for indexes of more than kLdsFilterKeys keys.
+constexpr uint32_t kL1Words = 32768;
 
 // Verified hits are written as key/value pairs: key = (segment << 32) | position
 // relative to the segment's first position, value = global block index (into the
@@ -46,6 +46,7 @@ struct ScanSeg {
 struct DeviceIndex {
     uint32_t* filt = nullptr;   // blocked Bloom filters (probe_hash/filt_mask), per-file 2^k 32-bit words
     uint32_t* l1 = nullptr;     // level-1 filter (kL1Words), single-file indexes above kLdsFilterKeys keys
+    uint4* fat = nullptr;       // with l1: per slot {key, first candidate | multi, its strong} (k_idx_fat)
     uint32_t* keys = nullptr;   // 4-key buckets of unique weak values, kEmptyKey = free
     uint32_t* cnt = nullptr;    // candidates per slot
     uint32_t* start = nullptr;  // exclusive prefix of cnt (global positions into order)

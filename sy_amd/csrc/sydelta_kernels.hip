@@ -339,14 +339,12 @@ __device__ __forceinline__ bool filt_pass(uint32_t word, uint32_t q) {
     const uint32_t m = filt_mask(q);
     return (word & m) == m;
 }
-// Level-1 filter of a large single-file index (kL1Words 32-bit words, 0.94 bits per
-// key at 1 Mi keys: 66 % false passes), held in LDS by k_scan_l1 so that only the
-// positions it passes cost a level-2 request to L2 (sydelta_internal.hpp).
-// word = floor((q >> 8) * 30720 / 2^24) (one v_mul_hi_u32_u24), bit = bits 8..12 of q.
-__device__ __forceinline__ uint32_t l1_word(uint32_t q) {
-    return (uint32_t)(((uint64_t)(q >> 8) * (30720ull << 8)) >> 32);  // < kL1Words
-}
-__device__ __forceinline__ uint32_t l1_test(uint32_t word, uint32_t q) { return __builtin_amdgcn_ubfe(word, q >> 8, 1); }
+// Level-1 filter of a large single-file index (2^20 bits, one per key: 63 % false
+// passes at 1 Mi keys), held in LDS by k_scan_l1 so that only the positions it passes
+// cost a level-2 request to L2 (sydelta_internal.hpp): word = q[17..31], bit = q[12..16].
+static_assert(kL1Words == 32768, "l1_word takes the top 15 bits of q");
+__device__ __forceinline__ uint32_t l1_word(uint32_t q) { return q >> 17; }
+__device__ __forceinline__ uint32_t l1_test(uint32_t word, uint32_t q) { return __builtin_amdgcn_ubfe(word, q >> 12, 1); }
 __device__ __forceinline__ uint32_t bucket_hash(uint32_t w) {
     uint32_t h = w ^ (w >> 15);
     h *= 0x2C1B3C6Du;
@@ -374,7 +372,7 @@ __global__ void k_idx_insert(const uint32_t* __restrict__ weak, uint64_t n, cons
     const uint32_t w = weak[i];
     const ProbeHash h = probe_hash(w);
     atomicOr(filt + F.filt_off + (h.r >> F.fwshift), filt_mask(h.q));
-    if (l1) atomicOr(l1 + l1_word(h.q), 1u << ((h.q >> 8) & 31));  // single-file index only (l1_test)
+    if (l1) atomicOr(l1 + l1_word(h.q), 1u << ((h.q >> 12) & 31));  // single-file index only (l1_test)
     uint32_t b = bucket_hash(w) & F.bmask;
     for (;;) {
         for (uint32_t j = 0; j < 4; ++j) {
@@ -404,6 +402,26 @@ __global__ void k_idx_cstrong(uint64_t n, const uint32_t* __restrict__ order, co
     const uint64_t j = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (j >= n) return;
     cstrong[j] = strong[order[j]];
+}
+
+// Fat table of a single-file index (k_scan_l1): per slot {key, first candidate in index
+// order (or kMulti | slot when the slot has more than one), that candidate's strong}, so
+// one bucket read answers a lookup (the 4 slots of a bucket are one 64-byte line).
+__global__ void k_idx_fat(uint64_t nslots, const uint32_t* __restrict__ keys, const uint32_t* __restrict__ cnt,
+                          const uint32_t* __restrict__ start, const uint32_t* __restrict__ order,
+                          const uint64_t* __restrict__ cstrong, uint4* __restrict__ fat) {
+    const uint64_t j = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (j >= nslots) return;
+    const uint32_t k = keys[j];
+    uint4 r = make_uint4(k, 0, 0, 0);
+    if (k != kEmptyKey) {
+        const uint32_t s0 = start[j];
+        const uint64_t st = cstrong[s0];
+        r.y = cnt[j] > 1 ? (0x80000000u | (uint32_t)j) : order[s0];
+        r.z = (uint32_t)st;
+        r.w = (uint32_t)(st >> 32);
+    }
+    fat[j] = r;
 }
 
 // Exact lookup: slot of weak value w, or -1.
@@ -582,6 +600,7 @@ struct ScanArgs {
     // probe structures (concatenated over files)
     const uint32_t* filt;
     const uint32_t* l1;       // k_scan_l1: level-1 filter (kL1Words)
+    const uint4* fat;         // k_scan_l1: {key, first candidate | kMulti+slot, strong} per slot
     const uint32_t* keys;
     const uint32_t* start;
     const uint32_t* cnt;
@@ -604,6 +623,10 @@ struct SegCtx {
     uint64_t slot_off;
     uint32_t bmask;
     uint32_t seg_id;
+    // k_scan_l1
+    const uint4* fat;     // this file's fat table (slot_off applied)
+    const uint32_t* filt; // this file's level-2 filter
+    uint32_t fwshift, fwords;
 };
 
 // 64-byte chunk [c0, c0+64) of src, bytes at or beyond len read as 0.  Past the
@@ -1469,20 +1492,23 @@ __global__ __launch_bounds__(kT2, kWgPerCu) void k_scan_lds(ScanArgs a, uint32_t
 // level-2 filter (2 MiB, 16 bits per key) in L2 that is one random L2 request per
 // position, and the chip serves ~265 G of those per second whatever their width or
 // cache policy (profiles/r02_micro_gather2.txt): >= 16 ms per 4 GiB.  So each
-// workgroup (one per CU) keeps a level-1 filter of 120 KiB in LDS, and only the
-// positions it passes (66 % at 1 Mi keys) cost an L2 request.  Eight waves, two
-// per SIMD (a wave alone on its SIMD issues VALU at half rate), 32 positions per
-// thread, the tile of k_scan_lds:
-//   phase 1  tile bytes [T0, T0 + kTile3 + n) -> LDS rows (64 B, 17-dword
-//            stride), sums of every 32-byte half
-//   phase 2  exclusive prefix of the half sums (S, sum of i*x, sum of h*S_h)
-//   phase 3  thread t's first window [T0 + 32t, +n) in closed form
-//   phase 4  roll 32 positions in batches of 8 (rolling.rs:66-79, both halves kept
-//            reduced with one min3 each); per position probe_hash, the level-1 bit
-//            from LDS, for its passes the level-2 word from L2; level-2 passes are
-//            queued per wave in LDS and drained (exact lookups, XXH3 of weak hits
-//            from the LDS rows, generator.rs:121-155) when a batch might not fit
-//            and at the end of the tile.
+// workgroup (one per CU) keeps a level-1 filter of 128 KiB in LDS, and only the
+// positions it passes (63 % at 1 Mi keys) cost an L2 request.  Eight waves, two per
+// SIMD (a wave alone on its SIMD issues VALU at half rate), 32 positions per thread,
+// the tile of k_scan_lds.  Per tile:
+//   stage    the tile's bytes [T0, T0 + kTile3 + n) -> LDS rows (64 B, 17-dword
+//            stride); they were loaded into registers during the previous tile's
+//            drain, so the HBM latency hides behind it
+//   window   each wave computes its threads' first windows [T0 + 32t, +n) in closed
+//            form from 32-byte half sums with wave scans (no workgroup barrier)
+//   roll     32 positions in batches of 8 (rolling.rs:66-79, both halves kept
+//            reduced with one min3 each); per position probe_hash and the level-1
+//            bit from LDS; the level-2 words of the passes are fetched by
+//            bounds-checked buffer loads (a level-1 miss gets an out-of-range offset:
+//            no request, reads 0) one batch ahead of their test
+//   drain    level-2 passes queued per wave in LDS: one bucket read of the fat table
+//            ({key, first candidate, its strong}) per pass, then XXH3 of the weak
+//            hits from the LDS rows (generator.rs:121-155)
 constexpr int kT3 = 512;           // threads per workgroup (8 waves)
 constexpr int kR3 = 32;            // positions per thread = half a 64-byte row
 constexpr int kTile3 = kT3 * kR3;  // 16384 positions per tile
@@ -1490,20 +1516,17 @@ constexpr int kB3 = 8;             // positions per batch
 constexpr int kFQ3 = 64;           // level-2 passes queued per wave (LDS)
 constexpr int kWQ3 = 32;           // weak hits queued per wave (LDS)
 constexpr uint32_t kMaxN3 = 4096;  // largest window whose tile fits beside the level-1 filter
+constexpr uint32_t kMulti = 0x80000000u;  // fat record: more than one candidate (info = slot)
 static_assert(kTile3 == kTile2, "k_scan_l1 and k_scan_lds share the host's tiling");
 
 struct Lds3 {
-    uint32_t nch, nh;                             // 64-byte rows, 32-byte halves
-    uint32_t ps, pv, pj, ntab, fq, wq, l1, total;  // byte offsets
+    uint32_t nch;                         // 64-byte rows
+    uint32_t ntab, fq, wq, l1, total;     // byte offsets
 };
 __host__ __device__ __forceinline__ Lds3 lds3_layout(uint32_t n) {
     Lds3 L;
     L.nch = (kTile3 + n + 63) / 64 + 1;
-    L.nh = 2 * L.nch;
     uint32_t o = L.nch * kRowDw * 4;
-    o = (o + 15) & ~15u; L.ps = o; o += (L.nh + 1) * 4;
-    L.pv = o; o += (L.nh + 1) * 4;
-    L.pj = o; o += (L.nh + 1) * 4;
     o = (o + 15) & ~15u; L.ntab = o; o += 256 * 4;
     L.fq = o; o += (kT3 / 64) * kFQ3 * 8;
     L.wq = o; o += (kT3 / 64) * kWQ3 * 16;
@@ -1512,9 +1535,104 @@ __host__ __device__ __forceinline__ Lds3 lds3_layout(uint32_t n) {
     return L;
 }
 
-// Exact lookups of this wave's queued level-2 passes (all in the current tile), 64 per
-// round (positions at or past the segment end are dropped here); weak hits go to wq
-// and are verified from the LDS rows when wq cannot take another round, and at the end.
+// Fat-table lookup: the bucket of w (4 records, one 64-byte line) in one round trip.
+__device__ __forceinline__ bool fat_find(const uint4* __restrict__ fat, uint32_t bmask, uint32_t w, uint4& rec) {
+    uint32_t b = bucket_hash(w) & bmask;
+    for (;;) {
+        const uint4* B = fat + 4 * (size_t)b;
+        const uint4 e0 = B[0], e1 = B[1], e2 = B[2], e3 = B[3];
+        if (e0.x == w) { rec = e0; return true; }
+        if (e1.x == w) { rec = e1; return true; }
+        if (e2.x == w) { rec = e2; return true; }
+        if (e3.x == w) { rec = e3; return true; }
+        if (e3.x == kEmptyKey) return false;  // buckets fill in order
+        b = (b + 1) & bmask;
+    }
+}
+
+// Verify this wave's weak hits wq[0..nwq) = {position in tile, first candidate |
+// kMulti+slot, strong lo, hi}: XXH3 of the window from the LDS rows (four windows per
+// wave, one per 16-lane row, when n % 64 == 0 and n >= 256), then the first candidate
+// in index order with equal strong (generator.rs:127-133); verified hits to the output.
+__device__ __forceinline__ void verify_l1(const ScanArgs& a, uint4* wq, uint32_t nwq, const uint32_t* rows,
+                                          uint64_t tile_start, const SegCtx& cur) {
+    if (!nwq) return;
+    lds_fence();
+    const uint32_t lane = threadIdx.x & 63;
+    if (a.n % 64 == 0 && a.n >= 256) {
+        const uint32_t row = lane >> 4, rl = lane & 15;
+        RowKeys K;
+        row_keys(K);
+        for (uint32_t t = 0; t < nwq; t += 4) {
+            const uint32_t h = t + row;
+            const bool live = h < nwq;
+            const uint4 e = wq[live ? h : t];
+            uint32_t s0 = 0, cn = 0;
+            if (e.y & kMulti) { s0 = a.start[e.y & ~kMulti]; cn = a.cnt[e.y & ~kMulti]; }  // in flight while hashing
+            const uint64_t st = row_strong_lds(rows, e.x, a.n, K);
+            uint32_t best = 0xFFFFFFFFu;
+            if (!(e.y & kMulti)) {
+                if (st == (((uint64_t)e.w << 32) | e.z)) best = e.y;
+            } else {
+                for (uint32_t b = 0; b < cn; b += 16) {  // in index order, 16 candidates per step
+                    const uint32_t j = b + rl;
+                    const uint64_t m = (__ballot(j < cn && a.cstrong[s0 + j] == st) >> (row << 4)) & 0xFFFFull;
+                    if (m) {
+                        best = a.order[s0 + b + (uint32_t)__builtin_ctzll(m)];
+                        break;
+                    }
+                }
+            }
+            if (live && rl == 0) wq[h].y = best;
+        }
+    } else {
+        for (uint32_t k = 0; k < nwq; ++k) {
+            const uint4 e = wq[k];
+            uint64_t st;
+            if (a.n > 240) {
+                uint32_t wk;
+                wave_hash_src(LdsRowBytes{rows, e.x}, a.n, wk, st);
+            } else {
+                st = 0;
+                if (lane == 0) st = xxh3_short(cur.base + tile_start + e.x, a.n);
+                st = shfl64(st, 0);
+            }
+            uint32_t best = 0xFFFFFFFFu;
+            if (!(e.y & kMulti)) {
+                if (st == (((uint64_t)e.w << 32) | e.z)) best = e.y;
+            } else {
+                best = first_strong_match(a.order, a.cstrong, a.start[e.y & ~kMulti], a.cnt[e.y & ~kMulti], st);
+            }
+            if (lane == 0) wq[k].y = best;
+        }
+    }
+    lds_fence();
+    uint32_t nver = 0;
+    for (uint32_t base = 0; base < nwq; base += 64) {
+        const bool v = base + lane < nwq && wq[base + lane].y != 0xFFFFFFFFu;
+        nver += __popcll(__ballot(v));
+    }
+    if (!nver) return;
+    unsigned long long k0 = 0;
+    if (lane == 0) k0 = atomicAdd(&a.counters[0], (unsigned long long)nver);
+    k0 = shfl64(k0, 0);
+    for (uint32_t base = 0; base < nwq; base += 64) {
+        const uint32_t i = base + lane;
+        const uint4 e = i < nwq ? wq[i] : make_uint4(0, 0xFFFFFFFFu, 0, 0);
+        const bool v = e.y != 0xFFFFFFFFu;
+        const uint64_t m = __ballot(v);
+        const unsigned long long k = k0 + __popcll(m & ((1ull << lane) - 1));
+        if (v && k < a.out_cap) {
+            a.hit_key[k] = ((uint64_t)cur.seg_id << kSegShift) | (uint64_t)(tile_start + e.x - cur.pos_begin);
+            a.hit_val[k] = e.y;
+        }
+        k0 += __popcll(m);
+    }
+}
+
+// Fat-table lookups of this wave's queued level-2 passes (all in the current tile),
+// 64 per round (positions at or past the segment end are dropped here); weak hits go
+// to wq, verified when wq cannot take another round and at the end.
 __device__ __forceinline__ void drain_l1(const ScanArgs& a, const uint2* fq, uint32_t nfq, uint4* wq,
                                          unsigned long long& weak_hits, const uint32_t* rows, uint64_t tile_start,
                                          const SegCtx& cur) {
@@ -1523,30 +1641,27 @@ __device__ __forceinline__ void drain_l1(const ScanArgs& a, const uint2* fq, uin
     uint32_t nwq = 0;
     for (uint32_t base = 0; base < nfq; base += 64) {
         const uint32_t i = base + lane;
-        int64_t slot = -1;
-        uint32_t rp = 0;
+        bool hit = false;
+        uint4 rec = make_uint4(0, 0, 0, 0);
+        uint32_t tp = 0;
         if (i < nfq) {
             const uint2 e = fq[i];  // {position in tile, weak}
-            const uint64_t p = tile_start + e.x;
-            if (p < cur.pos_end) slot = table_find(cur.keys, cur.bmask, e.y);
-            rp = (uint32_t)(p - cur.pos_begin);
+            tp = e.x;
+            if (tile_start + e.x < cur.pos_end) hit = fat_find(cur.fat, cur.bmask, e.y, rec);
         }
-        const bool hit = slot >= 0;
         const uint64_t m = __ballot(hit);
         if (!m) continue;
         const uint32_t cnt = __popcll(m);
         weak_hits += cnt;
         if (nwq + cnt > (uint32_t)kWQ3) {
-            lds_fence();
-            verify3<true>(a, wq, nwq, rows, tile_start, &cur);
+            verify_l1(a, wq, nwq, rows, tile_start, cur);
             nwq = 0;
         }
         const uint32_t rank = __popcll(m & ((1ull << lane) - 1));
-        const uint4 e = make_uint4(cur.seg_id, rp, (uint32_t)cur.slot_off + (uint32_t)slot, 0);
+        const uint4 e = make_uint4(tp, rec.y, rec.z, rec.w);  // a multi-candidate record names its global slot
         if (cnt > (uint32_t)kWQ3) {  // a round of more hits than wq holds (dense data): two halves
             if (hit && rank < (uint32_t)kWQ3) wq[rank] = e;
-            lds_fence();
-            verify3<true>(a, wq, kWQ3, rows, tile_start, &cur);
+            verify_l1(a, wq, kWQ3, rows, tile_start, cur);
             if (hit && rank >= (uint32_t)kWQ3) wq[rank - kWQ3] = e;
             nwq = cnt - kWQ3;
         } else {
@@ -1554,26 +1669,48 @@ __device__ __forceinline__ void drain_l1(const ScanArgs& a, const uint2* fq, uin
             nwq += cnt;
         }
     }
-    lds_fence();
-    verify3<true>(a, wq, nwq, rows, tile_start, &cur);
+    verify_l1(a, wq, nwq, rows, tile_start, cur);
     lds_fence();
 }
+
+// Exclusive wave scan (lane l gets the sum over lanes < l) and the wave total: DPP
+// row_shr steps inside each 16-lane row, then the row totals through SGPRs (no LDS
+// crossbar round trips: the window phase runs three of these per value).
+template <int K>
+__device__ __forceinline__ uint32_t dpp_shr(uint32_t v) {
+    return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x110 + K, 0xF, 0xF, true);  // out of row: 0
+}
+__device__ __forceinline__ uint32_t wave_scan_excl(uint32_t v, uint32_t& total) {
+    uint32_t x = v;
+    x += dpp_shr<1>(x);
+    x += dpp_shr<2>(x);
+    x += dpp_shr<4>(x);
+    x += dpp_shr<8>(x);
+    const uint32_t r0 = __builtin_amdgcn_readlane(x, 15), r1 = __builtin_amdgcn_readlane(x, 31);
+    const uint32_t r2 = __builtin_amdgcn_readlane(x, 47), r3 = __builtin_amdgcn_readlane(x, 63);
+    const uint32_t row = (threadIdx.x & 63) >> 4;
+    const uint32_t off = row == 0 ? 0u : row == 1 ? r0 : row == 2 ? r0 + r1 : r0 + r1 + r2;
+    total = r0 + r1 + r2 + r3;
+    return x + off - v;
+}
+
+// One batch of kB3 positions in flight: the level-2 words (buffer loads issued),
+// probe hashes and weak values, tested one batch later.
+struct L1Batch {
+    uint32_t w2[kB3], hq[kB3], wv[kB3];
+};
 
 __global__ __launch_bounds__(kT3, 2) void k_scan_l1(ScanArgs a, uint32_t per) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     const uint32_t n = a.n;
     const Lds3 L = lds3_layout(n);
     uint32_t* rows = (uint32_t*)smem;
-    uint32_t* PS = (uint32_t*)(smem + L.ps);
-    uint32_t* PV = (uint32_t*)(smem + L.pv);
-    uint32_t* PJ = (uint32_t*)(smem + L.pj);
     uint32_t* ntab = (uint32_t*)(smem + L.ntab);
     const uint32_t* l1 = (const uint32_t*)(smem + L.l1);
     const uint32_t tid = threadIdx.x;
     const uint32_t lane = tid & 63, wid = tid >> 6;
     uint2* fq = (uint2*)(smem + L.fq) + (size_t)wid * kFQ3;
     uint4* wq = (uint4*)(smem + L.wq) + (size_t)wid * kWQ3;
-    __shared__ uint32_t red_s[kT3 / 64], red_v[kT3 / 64], red_j[kT3 / 64];
 
     const uint32_t t_begin = blockIdx.x * per;
     const uint32_t t_end = min(a.ntiles, t_begin + per);
@@ -1587,112 +1724,146 @@ __global__ __launch_bounds__(kT3, 2) void k_scan_l1(ScanArgs a, uint32_t per) {
         for (uint32_t i = tid; i < kL1Words / 4; i += kT3) d[i] = g[i];
     }
     for (uint32_t i = tid; i < 256; i += kT3) ntab[i] = kMod - 1 - (a.nm * i) % kMod;
-    const uint32_t nch = L.nch, nh = L.nh;
+    const uint32_t nch = L.nch;
     const uint32_t sh = n & 3;
     const uint32_t rel0 = tid * kR3;
     const uint32_t orow = (tid >> 1) * kRowDw + 8 * (tid & 1);  // this thread's first out dword
     const uint32_t din0 = (rel0 + n) >> 2;                      // ... and first in dword
+    const uint32_t m32 = n >> 5, rem = n & 31;                  // window = m32 halves + rem bytes
     unsigned long long passes = 0, weak_hits = 0;
     uint32_t nfq = 0;
-    SegCtx sc;
-    const uint32_t* gfilt = a.filt;
-    uint32_t fwshift = 0;
-    uint32_t si = 0;
+    // SYDELTA_PHASE_TIMING: wave 0's s_memtime cycles per phase (stage, window, roll,
+    // drains) into counters[4..8), level-1 passes into counters[3]
+    unsigned long long tm[6] = {0, 0, 0, 0, 0, 0}, l1pass = 0;
+    unsigned long long tprev = a.timing ? __builtin_amdgcn_s_memtime() : 0;
+#define PHASE_MARK3(k)                                                 \
+    if (a.timing) {                                                    \
+        const unsigned long long tnow = __builtin_amdgcn_s_memtime(); \
+        tm[k] += tnow - tprev;                                         \
+        tprev = tnow;                                                  \
+    }
+
+    // segment of a tile (tiles of a launch are laid out segment after segment)
+    auto seg_ctx = [&](uint32_t tile, uint32_t si0, SegCtx& sc, uint32_t& si, uint64_t& tile_start,
+                       uint64_t& seg_len) {
+        uint32_t lo = si0, hi = a.nsegs;
+        while (hi - lo > 1) {
+            const uint32_t mid = (lo + hi) >> 1;
+            if (a.segs[mid].tile_base <= tile) lo = mid; else hi = mid;
+        }
+        si = lo;
+        const ScanSeg S = a.segs[si];
+        const FileIx F = a.files[S.file];
+        sc.base = a.src + S.src;
+        sc.pos_begin = S.pos_begin;
+        sc.pos_end = S.pos_end;
+        sc.keys = a.keys + F.slot_off;
+        sc.fat = a.fat + F.slot_off;
+        sc.slot_off = F.slot_off;
+        sc.bmask = F.bmask;
+        sc.seg_id = si;
+        sc.fwshift = F.fwshift;
+        sc.filt = a.filt + F.filt_off;
+        sc.fwords = 1u << (32 - F.fwshift);
+        tile_start = S.pos_begin + (uint64_t)(tile - S.tile_base) * kTile3;
+        seg_len = S.len;
+    };
+    SegCtx sc, nsc;
+    uint32_t si = 0, nsi = 0;
+    uint64_t tile_start = 0, seg_len = 0, ntile_start = 0, nseg_len = 0;
+    seg_ctx(t_begin, 0, nsc, nsi, ntile_start, nseg_len);
+    // next tile's chunk (thread c stages 64-byte chunk c), loaded ahead
+    uint32_t x[16];
+    if (tid < nch) load_chunk_nt(nsc.base, nseg_len, ntile_start + 64ull * tid, x);
+
 #pragma unroll 1
     for (uint32_t tile = t_begin; tile < t_end; ++tile) {
-        if (tile == t_begin || (si + 1 < a.nsegs && a.segs[si + 1].tile_base <= tile)) {
-            uint32_t lo = tile == t_begin ? 0 : si, hi = a.nsegs;
-            while (hi - lo > 1) {
-                const uint32_t mid = (lo + hi) >> 1;
-                if (a.segs[mid].tile_base <= tile) lo = mid; else hi = mid;
-            }
-            si = lo;
-            const ScanSeg S = a.segs[si];
-            const FileIx F = a.files[S.file];
-            sc.base = a.src + S.src;
-            sc.pos_begin = S.pos_begin;
-            sc.pos_end = S.pos_end;
-            sc.keys = a.keys + F.slot_off;
-            sc.slot_off = F.slot_off;
-            sc.bmask = F.bmask;
-            sc.seg_id = si;
-            fwshift = F.fwshift;
-            gfilt = a.filt + F.filt_off;
-        }
-        const uint64_t seg_len = a.segs[si].len;
-        const uint64_t tile_start = sc.pos_begin + (uint64_t)(tile - a.segs[si].tile_base) * kTile3;
-
-        // ---- phase 1: tile bytes -> LDS rows, half sums
-#pragma unroll 1
-        for (uint32_t c = tid; c < nch; c += kT3) {
-            uint32_t x[16];
-            load_chunk_nt(sc.base, seg_len, tile_start + 64ull * c, x);
-            uint32_t S0 = 0, V0 = 0, S1 = 0, V1 = 0;
+        sc = nsc;
+        si = nsi;
+        tile_start = ntile_start;
+        seg_len = nseg_len;
+        // ---- stage: the prefetched chunk -> LDS rows (the previous tile's barrier
+        // ended every read of the rows)
+        if (tid < nch) {
 #pragma unroll
-            for (int i = 0; i < 8; ++i) {
-                S0 = udot4(x[i], 0x01010101u, S0);
-                V0 = udot4(x[i], offw(i), V0);
-                S1 = udot4(x[i + 8], 0x01010101u, S1);
-                V1 = udot4(x[i + 8], offw(i), V1);
-            }
-#pragma unroll
-            for (int i = 0; i < 16; ++i) rows[c * kRowDw + i] = x[i];
-            PS[2 * c] = S0; PS[2 * c + 1] = S1;
-            PV[2 * c] = V0; PV[2 * c + 1] = V1;
+            for (int i = 0; i < 16; ++i) rows[tid * kRowDw + i] = x[i];
         }
         __syncthreads();
-
-        // ---- phase 2: exclusive prefix over the halves (PJ = sum of h * S_h < 2^31)
-        {
-            const uint32_t per_t = (nh + kT3 - 1) / kT3;
-            const uint32_t c_lo = min(nh, tid * per_t), c_hi = min(nh, c_lo + per_t);
-            uint32_t ts = 0, tv = 0, tj = 0;
-            for (uint32_t c = c_lo; c < c_hi; ++c) { ts += PS[c]; tv += PV[c]; tj += c * PS[c]; }
-            uint32_t is = ts, iv = tv, ij = tj;
-#pragma unroll
-            for (int m = 1; m < 64; m <<= 1) {
-                const uint32_t os = (uint32_t)__shfl_up((int)is, m, 64);
-                const uint32_t ov = (uint32_t)__shfl_up((int)iv, m, 64);
-                const uint32_t oj = (uint32_t)__shfl_up((int)ij, m, 64);
-                if (lane >= (uint32_t)m) { is += os; iv += ov; ij += oj; }
-            }
-            if (lane == 63) { red_s[wid] = is; red_v[wid] = iv; red_j[wid] = ij; }
-            __syncthreads();
-            uint32_t bs_ = 0, bv_ = 0, bj_ = 0;
-            for (uint32_t w = 0; w < wid; ++w) { bs_ += red_s[w]; bv_ += red_v[w]; bj_ += red_j[w]; }
-            uint32_t es = bs_ + is - ts, ev = bv_ + iv - tv, ej = bj_ + ij - tj;
-            for (uint32_t c = c_lo; c < c_hi; ++c) {
-                const uint32_t s0 = PS[c], v0 = PV[c];
-                PS[c] = es; PV[c] = ev; PJ[c] = ej;
-                es += s0; ev += v0; ej += c * s0;
-            }
-            if (tid == kT3 - 1) { PS[nh] = es; PV[nh] = ev; PJ[nh] = ej; }
-            __syncthreads();
+        // next tile's chunk, issued now: its HBM latency hides behind the window phase
+        // (which waits on no vector memory) and the first batches
+        if (tile + 1 < t_end) {
+            if (nsi + 1 < a.nsegs && a.segs[nsi + 1].tile_base <= tile + 1)
+                seg_ctx(tile + 1, nsi, nsc, nsi, ntile_start, nseg_len);  // the next segment
+            else
+                ntile_start = tile_start + kTile3;
+            if (tid < nch) load_chunk_nt(nsc.base, nseg_len, ntile_start + 64ull * tid, x);
         }
+        PHASE_MARK3(0)
 
-        // ---- phase 3: first window of this thread (tile offset 32*tid = half tid)
+        // ---- window: lane l of wave w starts at half t = 64w + l (tile offset 32t);
+        // halves t + 64j, j = 0..2, cover its window [32t, 32t + n) (m32 <= 128)
         uint32_t am, bm;
         {
-            const uint32_t c0 = tid, m = n >> 5, rem = n & 31;
-            const uint64_t dS = PS[c0 + m] - PS[c0];
-            const uint64_t dV = PV[c0 + m] - PV[c0];
-            const uint64_t dJ = PJ[c0 + m] - PJ[c0];
-            uint64_t A = dS;
-            uint64_t B = (uint64_t)n * dS - 32ull * (dJ - (uint64_t)c0 * dS) - dV;
+            uint32_t S[3], V[3], J[3], TS[3], TV[3], TJ[3];
+#pragma unroll
+            for (int j = 0; j < 3; ++j) {
+                const uint32_t h = tid + 64 * j;  // half index in the tile
+                const uint32_t* r = rows + (h >> 1) * kRowDw + 8 * (h & 1);
+                uint32_t s = 0, v = 0;
+#pragma unroll
+                for (int i = 0; i < 8; ++i) {
+                    const uint32_t d = r[i];
+                    s = udot4(d, 0x01010101u, s);
+                    v = udot4(d, offw(i), v);
+                }
+                S[j] = wave_scan_excl(s, TS[j]);
+                V[j] = wave_scan_excl(v, TV[j]);
+                J[j] = wave_scan_excl((uint32_t)(64 * j + lane) * s, TJ[j]);  // half index relative to the wave
+            }
+            // prefix at relative half y = lane + m32 (column jy = y >> 6, lane y & 63)
+            const uint32_t jA = m32 >> 6, ly = (lane + m32) & 63;
+            const bool carry = lane + (m32 & 63) >= 64;
+            auto pre = [&](const uint32_t* E, const uint32_t* T) -> uint32_t {
+                uint32_t base0 = 0, ea = 0, eb = 0, base1 = 0;
+#pragma unroll
+                for (int j = 0; j < 3; ++j) {
+                    // the common n % 2048 == 0 (m32 = 128 halves): the lane's own value
+                    const uint32_t sj = (m32 & 63) == 0 ? E[j] : (uint32_t)__shfl((int)E[j], (int)ly, 64);
+                    if ((uint32_t)j == jA) ea = sj;
+                    if ((uint32_t)j == jA + 1) eb = sj;
+                    if ((uint32_t)j < jA) base0 += T[j];
+                    if ((uint32_t)j < jA + 1) base1 += T[j];
+                }
+                return carry ? base1 + eb : base0 + ea;
+            };
+            const uint64_t dS = pre(S, TS) - S[0];
+            const uint64_t dV = pre(V, TV) - V[0];
+            const uint64_t dJ = pre(J, TJ) - J[0];
+            uint32_t A = (uint32_t)dS;
+            // B = sum_i (n - i) x_{32t+i} = n dS - 32 sum_k (k - l) S_k - dV   (< 2^31 for n <= 4096)
+            uint32_t B = (uint32_t)((uint64_t)n * dS - 32ull * (dJ - (uint64_t)lane * dS) - dV);
             for (uint32_t r = 0; r < rem; ++r) {
-                const uint32_t b = 32 * (c0 + m) + r;
+                const uint32_t b = 32 * (tid + m32) + r;
                 const uint32_t xr = (rows[(b >> 6) * kRowDw + ((b >> 2) & 15)] >> (8 * (b & 3))) & 0xFF;
                 A += xr;
-                B += (uint64_t)(rem - r) * xr;
+                B += (rem - r) * xr;
             }
-            am = (uint32_t)((1 + A) % kMod);
-            bm = (uint32_t)((n + B) % kMod);
+            am = (1 + A) % kMod;
+            bm = (n + B) % kMod;
         }
+        PHASE_MARK3(1)
 
-        // ---- phase 4: roll.  Positions at or past pos_end (last tile of a segment)
-        // are rolled like the others and dropped by drain_l1's bound check.
-#pragma unroll 1
-        for (uint32_t g = 0; g < (uint32_t)kR3; g += kB3) {
+        // ---- roll.  Positions at or past pos_end (last tile of a segment) are rolled
+        // like the others and dropped by drain_l1's bound check.
+        // the descriptor must be uniform (SGPRs): a VGPR one makes every load a waterfall loop
+        const uint64_t fptr = (uint64_t)(uintptr_t)sc.filt;
+        const uint32_t fp_lo = __builtin_amdgcn_readfirstlane((uint32_t)fptr);
+        const uint32_t fp_hi = __builtin_amdgcn_readfirstlane((uint32_t)(fptr >> 32));
+        const __amdgpu_buffer_rsrc_t frsrc = __builtin_amdgcn_make_buffer_rsrc(
+            (void*)(uintptr_t)(((uint64_t)fp_hi << 32) | fp_lo), (short)0,
+            (int)__builtin_amdgcn_readfirstlane(sc.fwords * 4), 0x00020000);
+        const uint32_t fwshift = __builtin_amdgcn_readfirstlane(sc.fwshift);
+        auto compute = [&](uint32_t g, L1Batch& Bt) {
             uint32_t xo[2], xi[2];
             xo[0] = rows[orow + (g >> 2)];
             xo[1] = rows[orow + (g >> 2) + 1];
@@ -1706,20 +1877,19 @@ __global__ __launch_bounds__(kT3, 2) void k_scan_l1(ScanArgs a, uint32_t per) {
                 xi[0] = __builtin_amdgcn_alignbyte(dw[1], dw[0], sh);
                 xi[1] = __builtin_amdgcn_alignbyte(dw[2], dw[1], sh);
             }
-            uint32_t ct[kB3];
+            uint32_t ct[kB3], off[kB3], w1[kB3];
 #pragma unroll
             for (int t = 0; t < kB3; ++t) ct[t] = ntab[(xo[t >> 2] >> (8 * (t & 3))) & 0xFF];
-            uint32_t wv[kB3], hq[kB3], ri[kB3], w1[kB3], w2[kB3];
 #pragma unroll
             for (int t = 0; t < kB3; ++t) {
                 const uint32_t out = (xo[t >> 2] >> (8 * (t & 3))) & 0xFF;
                 const uint32_t in = (xi[t >> 2] >> (8 * (t & 3))) & 0xFF;
                 __builtin_assume(am < kMod);  // lets the 24-bit multiplies take am, bm as they are
                 __builtin_assume(bm < kMod);
-                wv[t] = (bm << 16) | am;
+                Bt.wv[t] = (bm << 16) | am;
                 const ProbeHash h = probe_hash(am, bm);
-                hq[t] = h.q;
-                ri[t] = h.r >> fwshift;
+                Bt.hq[t] = h.q;
+                off[t] = (h.r >> fwshift) * 4;
                 w1[t] = l1[l1_word(h.q)];
                 const uint32_t u = am + in + (kMod - out);  // [M-255, 2M+255)
                 am = min(u, min(u - kMod, u - 2 * kMod));
@@ -1728,62 +1898,99 @@ __global__ __launch_bounds__(kT3, 2) void k_scan_l1(ScanArgs a, uint32_t per) {
             }
 #pragma unroll
             for (int t = 0; t < kB3; ++t) {
-                w2[t] = 0;  // level-1 miss: filt_pass(0, q) is false
-                if (l1_test(w1[t], hq[t])) w2[t] = gfilt[ri[t]];
+                const uint32_t p1 = l1_test(w1[t], Bt.hq[t]);
+                if (a.timing) l1pass += __popcll(__ballot(p1));
+                // a level-1 miss asks for an offset past the buffer: no request, reads 0
+                // (and filt_pass(0, q) is false)
+                Bt.w2[t] = __builtin_amdgcn_raw_buffer_load_b32(frsrc, (int)(p1 ? off[t] : 0xFFFFFFFFu), 0, 0);
             }
+        };
+        // Queue the level-2 passes of batch g's positions still in `todo` (per-wave LDS
+        // queue, positions in order); false when the queue could not take them all
+        // (todo then names the rest).  Never drains: the queue is drained between
+        // pipelines, so no drain code (and its registers) sits inside the hot loop.
+        auto finish = [&](uint32_t g, L1Batch& Bt, uint32_t& todo) -> bool {
             uint32_t pbits = 0;
 #pragma unroll
-            for (int t = 0; t < kB3; ++t) pbits |= (filt_pass(w2[t], hq[t]) ? 1u : 0u) << t;
+            for (int t = 0; t < kB3; ++t) pbits |= (filt_pass(Bt.w2[t], Bt.hq[t]) ? 1u : 0u) << t;
             // opaque: the ballots below re-derive the masks instead of holding eight
             // compare results in SGPRs (which spilled)
             asm volatile("" : "+v"(pbits));
-            uint32_t tot = 0;
+            const uint64_t below = (1ull << lane) - 1;
+            uint32_t need = 0;
 #pragma unroll
-            for (int t = 0; t < kB3; ++t) tot += __popcll(__ballot((pbits >> t) & 1));
-            if (tot) {
-                if (nfq + tot > (uint32_t)kFQ3) {
-                    passes += nfq;
-                    drain_l1(a, fq, nfq, wq, weak_hits, rows, tile_start, sc);
-                    nfq = 0;
-                }
-                const uint64_t below = (1ull << lane) - 1;
-                if (tot <= (uint32_t)kFQ3) {
+            for (int t = 0; t < kB3; ++t)
+                if ((todo >> t) & 1) need += __popcll(__ballot((pbits >> t) & 1));
+            const bool all = nfq + need <= (uint32_t)kFQ3;
+            bool full = false;
 #pragma unroll
-                    for (int t = 0; t < kB3; ++t) {
-                        const uint64_t mk = __ballot((pbits >> t) & 1);  // recomputed: 8 masks held would spill SGPRs
-                        if ((pbits >> t) & 1) fq[nfq + __popcll(mk & below)] = make_uint2(rel0 + g + t, wv[t]);
-                        nfq += __popcll(mk);
-                    }
-                } else {
-                    // degenerate data (more passes in one batch than the queue holds):
-                    // one position at a time
-#pragma unroll 1
-                    for (uint32_t t = 0; t < (uint32_t)kB3; ++t) {
-                        uint32_t w = wv[0];
-#pragma unroll
-                        for (int j = 1; j < kB3; ++j) w = t == (uint32_t)j ? wv[j] : w;
-                        const bool p = (pbits >> t) & 1;
-                        const uint64_t m1 = __ballot(p);
-                        if (nfq + __popcll(m1) > (uint32_t)kFQ3) {
-                            passes += nfq;
-                            drain_l1(a, fq, nfq, wq, weak_hits, rows, tile_start, sc);
-                            nfq = 0;
-                        }
-                        if (p) fq[nfq + __popcll(m1 & below)] = make_uint2(rel0 + g + t, w);
-                        nfq += __popcll(m1);
-                    }
+            for (int t = 0; t < kB3; ++t) {
+                if (!((todo >> t) & 1) || full) continue;
+                const uint64_t mk = __ballot((pbits >> t) & 1);
+                if (!all && nfq + __popcll(mk) > (uint32_t)kFQ3) { full = true; continue; }
+                if ((pbits >> t) & 1) fq[nfq + __popcll(mk & below)] = make_uint2(rel0 + g + t, Bt.wv[t]);
+                nfq += __popcll(mk);
+                todo &= ~(1u << t);
+            }
+            if (all) todo = 0xFFu;
+            return all;
+        };
+        // Pipeline: batch g+8's level-2 loads are in flight while batch g is tested.
+        // A batch the queue cannot take stops it; the queue is drained and the roll
+        // resumes from that batch's saved state (only degenerate data gets there).
+        uint32_t stop = 4, todo = 0xFFu, ra = 0, rb = 0;
+        {
+            L1Batch b0, b1;
+            const uint32_t a0 = am, s0 = bm;
+            compute(0, b0);
+            const uint32_t a1 = am, s1 = bm;
+            compute(8, b1);
+            if (!finish(0, b0, todo)) { stop = 0; ra = a0; rb = s0; }
+            if (stop == 4) {
+                const uint32_t a2 = am, s2 = bm;
+                compute(16, b0);
+                if (!finish(8, b1, todo)) { stop = 1; ra = a1; rb = s1; }
+                if (stop == 4) {
+                    const uint32_t a3 = am, s3 = bm;
+                    compute(24, b1);
+                    if (!finish(16, b0, todo)) { stop = 2; ra = a2; rb = s2; }
+                    if (stop == 4 && !finish(24, b1, todo)) { stop = 3; ra = a3; rb = s3; }
                 }
             }
         }
+        while (stop < 4) {
+            passes += nfq;
+            drain_l1(a, fq, nfq, wq, weak_hits, rows, tile_start, sc);
+            nfq = 0;
+            uint32_t k = stop;
+            stop = 4;
+            am = ra;
+            bm = rb;
+#pragma unroll 1
+            for (; k < 4; ++k) {
+                L1Batch bt;
+                const uint32_t ak = am, sk = bm;
+                compute(8 * k, bt);
+                if (!finish(8 * k, bt, todo)) { stop = k; ra = ak; rb = sk; break; }
+            }
+        }
+        PHASE_MARK3(2)
+        PHASE_MARK3(3)
         if (nfq) {  // the tile's weak hits are verified while its bytes are in LDS
             passes += nfq;
             drain_l1(a, fq, nfq, wq, weak_hits, rows, tile_start, sc);
             nfq = 0;
         }
-        __syncthreads();  // rows / prefix arrays are rewritten by the next tile
+        PHASE_MARK3(4)
+        __syncthreads();  // rows are rewritten by the next tile
+        PHASE_MARK3(5)
     }
+#undef PHASE_MARK3
     if (lane == 0 && passes) atomicAdd(&a.counters[2], passes);
     if (lane == 0 && weak_hits) atomicAdd(&a.counters[1], weak_hits);
+    if (a.timing && lane == 0) atomicAdd(&a.counters[3], l1pass);
+    if (a.timing && tid == 0)
+        for (int k = 0; k < 6; ++k) atomicAdd(&a.counters[4 + k], tm[k]);
 }
 
 // Tail rule (generator.rs:156-184): at p* = len - last_size (last_size < n), the
@@ -2358,13 +2565,12 @@ __global__ void k_synth_mutate(uint8_t* __restrict__ dst, const uint8_t* __restr
 // ===========================================================================
 static inline unsigned grid_for(uint64_t threads, unsigned block) { return (unsigned)((threads + block - 1) / block); }
 
-// Large single-file indexes scan with k_scan_lds (global-filter mode) by default: it
-// measured 19.2 ms per 4 GiB against k_scan_l1's 20.0-20.5 ms ("C3 scan
-// variants").  SYDELTA_SCAN_L1=1 selects k_scan_l1 (read per call: the parity tests run
-// both).
+// Large single-file indexes scan with k_scan_l1 by default: 17.24 ms per 4 GiB against
+// k_scan_lds's 19.2 ms in global-filter mode.  SYDELTA_SCAN_L1=0
+// selects k_scan_lds (read per call: the parity tests run both).
 static bool scan_l1_enabled() {
     const char* e = getenv("SYDELTA_SCAN_L1");
-    return e && e[0] == '1';
+    return !(e && e[0] == '0');
 }
 
 hipError_t launch_signature(const uint8_t* d_buf, uint64_t len, uint64_t bs, uint32_t* d_weak, uint64_t* d_strong,
@@ -2471,6 +2677,10 @@ hipError_t launch_index_build(const uint32_t* d_weak, const uint64_t* d_strong, 
         if (e) return e;
     }
     hipLaunchKernelGGL(k_idx_cstrong, dim3(grid_for(n, 256)), dim3(256), 0, s, n, ix.order, d_strong, ix.cstrong);
+    if ((e = hipGetLastError())) return e;
+    if (ix.fat)
+        hipLaunchKernelGGL(k_idx_fat, dim3(grid_for(ix.nslots, 256)), dim3(256), 0, s, (uint64_t)ix.nslots, ix.keys,
+                           ix.cnt, ix.start, ix.order, ix.cstrong, ix.fat);
     return hipGetLastError();
 }
 
@@ -2537,6 +2747,7 @@ hipError_t launch_scan(const uint8_t* d_buf, const ScanSeg* d_segs, uint32_t nse
     a.out_cap = out_cap;
     a.counters = d_counters;
     a.l1 = ix.l1;
+    a.fat = ix.fat;
     static std::once_flag l1_once;
     static hipError_t l1_err = hipSuccess;
     static int l1_cus = 256;
@@ -2551,7 +2762,7 @@ hipError_t launch_scan(const uint8_t* d_buf, const ScanSeg* d_segs, uint32_t nse
                 l1_cus = cus;
         });
         if (l1_err != hipSuccess) return l1_err;
-        if (L3.total > 160u * 1024 - 256) return hipErrorInvalidValue;
+        if (L3.total > 160u * 1024 - 256 || !ix.fat) return hipErrorInvalidValue;
         // one workgroup per CU (the level-1 filter fills its LDS), contiguous tile ranges
         const uint32_t grid = (uint32_t)std::min<uint64_t>(ntiles, (uint64_t)l1_cus);
         const uint32_t per = (ntiles + grid - 1) / grid;
