@@ -19,6 +19,10 @@ already resident in HBM:
      with one substituted byte; chunk-sharded: each rank signs its 8 GiB of the
      basis, RCCL all-gathers the signature, builds the full index, classifies its
      8 GiB of the source and the walks are chained (sy_amd/shard.py).
+  path: the drop-in path API on page-cache-warm files (host-inclusive): per step
+     sydelta_compute_checksums(basis file) + sydelta_generate_delta_streaming(source
+     file), both streaming their file through pinned double buffers; 1 GiB files,
+     1% of blocks with one substituted byte; value = (basis + source bytes) / time.
 Multi-GPU (torchrun, one rank per GPU): c3 -- every rank processes its own
 independent pair (file-sharded, no data-path collective); c4 -- the files are
 split over ranks; c5 -- chunks of one file.  value = total bytes of all ranks /
@@ -59,7 +63,8 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=2)
-    ap.add_argument("--workload", default="c3", choices=["c3", "c2", "c4", "c5", "apply", "json", "local", "xxh3"])
+    ap.add_argument("--workload", default="c3",
+                    choices=["c3", "c2", "c4", "c5", "apply", "json", "local", "xxh3", "path"])
     ap.add_argument("--size-gib", type=float, default=None,
                     help="bytes per rank: c2/c3 basis and source (default 4), c5 chunk (default 8)")
     ap.add_argument("--block-size", type=int, default=None, help="default 4096 (c5: 8192)")
@@ -75,13 +80,13 @@ def parse():
     ap.add_argument("--no-host-inclusive", action="store_true")
     a = ap.parse_args()
     if a.size_gib is None:
-        a.size_gib = 8.0 if a.workload in ("c5", "apply", "local") else 4.0
+        a.size_gib = 8.0 if a.workload in ("c5", "apply", "local") else 1.0 if a.workload == "path" else 4.0
     if a.files is None:
         a.files = 4096 if a.workload == "xxh3" else 10000
     if a.block_size is None:
         a.block_size = {"c5": 8192, "apply": 8192, "local": 65536}.get(a.workload, 4096)
     if a.edit_ppm is None:
-        a.edit_ppm = 10000 if a.workload in ("c5", "apply", "local") else 50000
+        a.edit_ppm = 10000 if a.workload in ("c5", "apply", "local", "path") else 50000
     return a
 
 
@@ -459,7 +464,7 @@ def main():
 
     nb_bytes = min(n, (args.basis_mib << 20) // bs * bs) if args.basis_mib else n
     basis = None
-    if args.workload != "c4":
+    if args.workload not in ("c4", "path"):
         basis = torch.empty(n, dtype=torch.uint8, device="cuda")
         if args.workload != "c5":
             dev.synth_fill(basis, seed_base)
@@ -532,6 +537,25 @@ def main():
         else:
             gather, bcast = (lambda v: [v]), (lambda v, src: v)
         c5 = dict(file_len=file_len, first=first, p0=p0, p1=p1, gather=gather, bcast=bcast, shard=shard)
+    path_files = None
+    if args.workload == "path":
+        import tempfile
+
+        from oracle import oracle as O
+
+        tmpd = tempfile.mkdtemp(prefix=f"sydelta_bench_r{rank}_", dir=os.environ.get("TMPDIR", "/tmp"))
+        pb, ps = os.path.join(tmpd, "basis"), os.path.join(tmpd, "source")
+        piece = 64 << 20
+        with open(pb, "wb") as fb, open(ps, "wb") as fs:
+            for i in range(0, n, piece):
+                b = O.synth_bytes(min(piece, n - i), 0x5E1D0500 + rank, i)
+                fb.write(b.tobytes())
+                fs.write(O.synth_edit_blocks(b, i, bs, 0x5E1D0501, args.edit_ppm).tobytes())
+        for f in (pb, ps):  # page-cache warm
+            with open(f, "rb") as fh:
+                while fh.read(64 << 20):
+                    pass
+        path_files = (tmpd, pb, ps)
     if args.workload == "c4":
         # BASELINE config 4: files [lo, hi) of --files 1 MiB files go to this rank
         # (equal sizes, so contiguous ranges are the bytes-balanced LPT split).
@@ -544,6 +568,21 @@ def main():
     stream = torch.cuda.current_stream()
 
     def step():
+        if args.workload == "path":
+            sig = ctypes.POINTER(_lib.BlockChecksumC)()
+            nsig = ctypes.c_uint64(0)
+            check(lib.sydelta_compute_checksums(path_files[1].encode(), bs, ctypes.byref(sig), ctypes.byref(nsig)))
+            h = ctypes.c_void_p()
+            try:
+                check(lib.sydelta_generate_delta_streaming(path_files[2].encode(), sig, nsig.value, bs,
+                                                           ctypes.byref(h)))
+                st = _lib.MatchStatsC()
+                check(lib.sydelta_delta_stats(h, ctypes.byref(st)))
+            finally:
+                lib.sydelta_checksums_free(ctypes.cast(sig, ctypes.c_void_p))
+                if h:
+                    lib.sydelta_delta_free(h)
+            return {k: getattr(st, k) for k, _ in _lib.MatchStatsC._fields_}
         if args.workload == "c2":
             dev.signature(basis, bs, stream=stream)
             return None
@@ -635,6 +674,8 @@ def main():
         bytes_per_step = int(xxh_lens.sum())
     elif args.workload == "json":
         bytes_per_step = n  # delta source bytes covered by the text
+    elif args.workload == "path":
+        bytes_per_step = 2 * n  # basis file signed + source file matched
     else:
         bytes_per_step = int(files[1].sum() + files[3].sum())
     total_bytes = bytes_per_step * args.steps * world
@@ -681,7 +722,7 @@ def main():
             "vs_baseline": None,
             "dtype": "u8",
             "data": (f"synthetic (counter-based splitmix64 bytes; one substituted byte in {args.edit_ppm / 1e4:g}% of {bs // 1024} KiB blocks)"
-                     if args.workload in ("c5", "apply", "local") else
+                     if args.workload in ("c5", "apply", "local", "path") else
                      "synthetic (counter-based splitmix64 bytes; Bernoulli byte substitutions)"),
             "config": {
                 "workload": {
@@ -699,6 +740,9 @@ def main():
                     "local": f"local transport: change-ratio sample + block compare of two {n / GIB:.0f} GiB files, "
                              f"bs {bs}, {args.edit_ppm / 1e4:g}% of blocks edited",
                     "json": f"serde_json text of the C3 delta ({n / GIB:.0f} GiB source, one literal run) on the device",
+                    "path": f"path API on page-cache-warm files: compute_checksums({n / GIB:g} GiB basis) + "
+                            f"generate_delta_streaming({n / GIB:g} GiB source, {args.edit_ppm / 1e4:g}% of {bs} B "
+                            f"blocks edited), host-inclusive",
                 }[args.workload],
                 "block_size": bs,
                 "basis_bytes": nb_bytes if args.workload == "c3" else n,
@@ -717,6 +761,10 @@ def main():
             "match_stats": stats,
         }
         print(json.dumps(line), flush=True)
+    if path_files:
+        import shutil
+
+        shutil.rmtree(path_files[0], ignore_errors=True)
     if world > 1:
         dist.destroy_process_group()
 

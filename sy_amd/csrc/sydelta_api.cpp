@@ -13,13 +13,16 @@
 #include <stdarg.h>
 #include <stdio.h>
 #include <string.h>
+#include <fcntl.h>
 #include <sys/stat.h>
+#include <unistd.h>
 
 #include <algorithm>
 #include <array>
 #include <atomic>
 #include <chrono>
 #include <cmath>
+#include <numeric>
 #include <map>
 #include <memory>
 #include <new>
@@ -1402,26 +1405,163 @@ static int read_file(const char* path, std::vector<uint8_t>& data) {
     return SYDELTA_OK;
 }
 
-// checksum.rs:31-80
+// Streamed file input for the path API: a file is read in chunks (64 MiB, a multiple of
+// lcm(block_size, 16); SYDELTA_STREAM_CHUNK overrides the size for tests) through two
+// per-thread pinned buffers.  While the device works on chunk g (H2D, then its kernels),
+// a reader thread fills the other buffer with chunk g+1, so host memory stays at two
+// chunks whatever the file size (plus the output: checksums, ops, literal bytes).
+namespace {
+uint64_t stream_chunk_bytes(uint64_t bs) {
+    uint64_t want = 64ull << 20;
+    if (const char* e = getenv("SYDELTA_STREAM_CHUNK")) {
+        const uint64_t v = strtoull(e, nullptr, 10);
+        if (v) want = v;
+    }
+    const uint64_t unit = bs / std::gcd<uint64_t>(bs, 16) * 16;  // lcm(bs, 16)
+    return std::max<uint64_t>(unit, want / unit * unit);
+}
+
+struct PinnedPair {  // per thread, grown on demand, freed at thread exit
+    uint8_t* p[2] = {nullptr, nullptr};
+    uint64_t cap = 0;
+    ~PinnedPair() { release(); }
+    void release() {
+        for (auto& q : p) {
+            if (q) (void)hipHostFree(q);
+            q = nullptr;
+        }
+        cap = 0;
+    }
+    int ensure(uint64_t bytes) {
+        if (bytes <= cap) return SYDELTA_OK;
+        release();
+        for (auto& q : p) HIP_TRY(hipHostMalloc((void**)&q, bytes, hipHostMallocDefault));
+        cap = bytes;
+        return SYDELTA_OK;
+    }
+};
+thread_local PinnedPair t_stream_pinned;
+
+struct InFile {
+    int fd = -1;
+    uint64_t len = 0;
+    std::string path;
+    ~InFile() {
+        if (fd >= 0) close(fd);
+    }
+    int open_(const char* p) {
+        if (!p) return fail(SYDELTA_E_INVAL, "path is NULL");
+        path = p;
+        fd = open(p, O_RDONLY | O_CLOEXEC);
+        if (fd < 0) return fail(SYDELTA_E_IO, "%s: %s", p, strerror(errno));
+        struct stat stt;
+        if (fstat(fd, &stt) != 0) return fail(SYDELTA_E_IO, "%s: %s", p, strerror(errno));
+        len = (uint64_t)stt.st_size;
+        return SYDELTA_OK;
+    }
+    // exactly [off, off + n) (the file must not shrink meanwhile)
+    int read_at(uint64_t off, uint8_t* dst, uint64_t n) const {
+        uint64_t got = 0;
+        while (got < n) {
+            const ssize_t r = pread(fd, dst + got, (size_t)std::min<uint64_t>(n - got, 1ull << 30), (off_t)(off + got));
+            if (r < 0 && errno == EINTR) continue;
+            if (r < 0) return fail(SYDELTA_E_IO, "%s: %s", path.c_str(), strerror(errno));
+            if (r == 0) return fail(SYDELTA_E_IO, "%s: short read at %llu", path.c_str(), (unsigned long long)(off + got));
+            got += (uint64_t)r;
+        }
+        return SYDELTA_OK;
+    }
+};
+
+// Runs `read` (the next chunk) on a helper thread while the caller runs `work` (the
+// device part of this chunk); inline after `work` when no thread can be started.  A
+// failed read is repeated on the calling thread so that its sydelta_last_error() names
+// the failure.
+template <class R, class W>
+int overlap(bool has_next, R&& read, W&& work) {
+    int rr = SYDELTA_OK;
+    std::thread t;
+    bool threaded = false;
+    if (has_next) {
+        try {
+            t = std::thread([&] { rr = read(); });
+            threaded = true;
+        } catch (...) {
+        }
+    }
+    int wr;
+    try {
+        wr = work();
+    } catch (...) {
+        if (t.joinable()) t.join();
+        throw;
+    }
+    if (t.joinable()) t.join();
+    if (wr) return wr;
+    if (has_next && (!threaded || rr)) rr = read();
+    return rr;
+}
+}  // namespace
+
+// checksum.rs:31-80: every block of the file, read chunk by chunk (the reference opens,
+// seeks and reads each block, :46-59), signed on the device; bounded host memory.
 extern "C" int sydelta_compute_checksums(const char* path, uint64_t block_size, sydelta_block_checksum** out,
                                          uint64_t* n) try {
     if (!out || !n) return fail(SYDELTA_E_INVAL, "NULL output");
     *out = nullptr;
     *n = 0;
-    std::vector<uint8_t> data;
-    if (int r = read_file(path, data)) return r;
-    if (data.empty()) return SYDELTA_OK;  // checksum.rs:36-38
+    InFile f;
+    if (int r = f.open_(path)) return r;
+    const uint64_t L = f.len;
+    if (L == 0) return SYDELTA_OK;  // checksum.rs:36-38
     if (block_size == 0) return fail(SYDELTA_E_INVAL, "block_size must be > 0");
-    const uint64_t nb = (data.size() + block_size - 1) / block_size;
+    const uint64_t nb = (L + block_size - 1) / block_size;
+    if (int r = ensure_device(-1)) return r;
+    hipStream_t s = thread_stream(0);
+    const uint64_t C = std::min<uint64_t>(stream_chunk_bytes(block_size), L);
+    const uint64_t nch = (L + C - 1) / C;
+    PinnedPair& pin = t_stream_pinned;
+    if (int r = pin.ensure(C + 16)) return r;
+    DevBuf db, dw;
+    HIP_TRY(hipMallocAsync(&db.p, C + 16, s));
+    db.s = s;
+    HIP_TRY(hipMallocAsync(&dw.p, nb * 12 + 16, s));
+    dw.s = s;
+    uint32_t* d_w = (uint32_t*)dw.p;
+    uint64_t* d_st = (uint64_t*)(((uintptr_t)(d_w + nb) + 7) & ~(uintptr_t)7);
+    if (int r = f.read_at(0, pin.p[0], std::min(C, L))) return r;
+    CallProf cp;
+    for (uint64_t g = 0; g < nch; ++g) {
+        const uint64_t b0 = g * C, len = std::min(C, L - b0);
+        const uint64_t nb1 = b0 + C < L ? std::min(C, L - b0 - C) : 0;
+        const int r = overlap(
+            g + 1 < nch, [&] { return f.read_at(b0 + C, pin.p[(g + 1) & 1], nb1); },
+            [&]() -> int {
+                HIP_TRY(hipMemcpyAsync(db.p, pin.p[g & 1], len, hipMemcpyHostToDevice, s));
+                HIP_TRY(launch_signature((const uint8_t*)db.p, len, block_size, d_w + b0 / block_size,
+                                         d_st + b0 / block_size, s, cp.get()));
+                HIP_TRY(hipStreamSynchronize(s));  // the device buffer and this pinned buffer are reused
+                return SYDELTA_OK;
+            });
+        if (r) return r;
+    }
+    std::vector<uint32_t> w(nb);
+    std::vector<uint64_t> st(nb);
+    HIP_TRY(hipMemcpyAsync(w.data(), d_w, 4 * nb, hipMemcpyDeviceToHost, s));
+    HIP_TRY(hipMemcpyAsync(st.data(), d_st, 8 * nb, hipMemcpyDeviceToHost, s));
+    HIP_TRY(hipStreamSynchronize(s));
     sydelta_block_checksum* v = (sydelta_block_checksum*)malloc(sizeof(sydelta_block_checksum) * nb);
     if (!v) return fail(SYDELTA_E_OOM, "host allocation failed");
-    uint64_t got = 0;
-    if (int r = sydelta_compute_checksums_buf(-1, data.data(), data.size(), block_size, v, nb, &got)) {
-        free(v);
-        return r;
+    for (uint64_t i = 0; i < nb; ++i) {
+        v[i].index = i;
+        v[i].offset = i * block_size;
+        v[i].size = std::min<uint64_t>(block_size, L - i * block_size);
+        v[i].weak = w[i];
+        v[i].reserved = 0;
+        v[i].strong = st[i];
     }
     *out = v;
-    *n = got;
+    *n = nb;
     return SYDELTA_OK;
 } catch (...) {
     return sydelta::host_exception();
@@ -1441,16 +1581,114 @@ extern "C" int sydelta_generate_delta(const char* source_path, const sydelta_blo
     return sydelta::host_exception();
 }
 
-// generator.rs:67 — identical ops to generate_delta for block_size <= 128 KiB
-// (SURVEY.md App. A R10); larger sizes are outside the production domain.
+// generator.rs:67-228 — identical ops to generate_delta for block_size <= 128 KiB
+// (SURVEY.md App. A R10); larger sizes are outside the production domain.  The source is
+// streamed: chunk g (window starts [g*C, (g+1)*C), its bytes plus the n-1 that the last
+// window needs) is copied from a pinned buffer to the device, classified
+// (sydelta_chunk_classify: aligned probe, scans) and walked from the previous chunk's
+// exit (sydelta_chunk_walk, on-demand scans read the chunk still on the device), and
+// its Data ops take their literal bytes from the pinned chunk; the next chunk is read
+// meanwhile.  The ops equal generate_delta's (the chunk-sharded walk).
 extern "C" int sydelta_generate_delta_streaming(const char* source_path, const sydelta_block_checksum* sigs,
                                                 uint64_t nsigs, uint64_t block_size, sydelta_delta** out) try {
     if (!out) return fail(SYDELTA_E_INVAL, "out is NULL");
     *out = nullptr;
+    if (block_size == 0) return fail(SYDELTA_E_INVAL, "block_size must be > 0");
     if (block_size > 128 * 1024)
         return fail(SYDELTA_E_INVAL, "block_size %llu > 131072: streaming semantics diverge (see sydelta.h)",
                     (unsigned long long)block_size);
-    return sydelta_generate_delta(source_path, sigs, nsigs, block_size, out);
+    if (nsigs && !sigs) return fail(SYDELTA_E_INVAL, "NULL checksums");
+    uint64_t last_size = 0;
+    if (int r = check_sigs(sigs, nsigs, block_size, &last_size)) return r;
+    InFile f;
+    if (int r = f.open_(source_path)) return r;
+    if (int r = ensure_device(-1)) return r;
+    hipStream_t s = thread_stream(0);
+    const uint64_t L = f.len, n = block_size;
+    std::vector<uint32_t> w(nsigs);
+    std::vector<uint64_t> st(nsigs);
+    for (uint64_t i = 0; i < nsigs; ++i) {
+        w[i] = sigs[i].weak;
+        st[i] = sigs[i].strong;
+    }
+    sydelta_index* ixp = nullptr;
+    if (int r = sydelta_index_create(0, w.data(), st.data(), nsigs, n, last_size, 0, s, &ixp)) return r;
+    std::unique_ptr<sydelta_index, void (*)(sydelta_index*)> ix(ixp, sydelta_index_free);
+    std::vector<uint32_t>().swap(w);
+    std::vector<uint64_t>().swap(st);
+    const uint64_t npos = L >= n ? L - n + 1 : 0;
+    const uint64_t C = stream_chunk_bytes(n);
+    const uint64_t nch = npos ? (npos + C - 1) / C : 1;
+    auto chunk_end = [&](uint64_t g) { return g + 1 == nch ? L : std::min(L, (g + 1) * C + n - 1); };
+    const uint64_t cap = std::max<uint64_t>(chunk_end(0), nch > 1 ? chunk_end(nch - 1) - (nch - 1) * C : 0);
+    PinnedPair& pin = t_stream_pinned;
+    if (int r = pin.ensure(cap + 16)) return r;
+    DevBuf db;
+    HIP_TRY(hipMallocAsync(&db.p, cap + 16, s));
+    db.s = s;
+    std::unique_ptr<sydelta_delta> d(new sydelta_delta());
+    d->source_size = L;
+    d->block_size = n;
+    if (L) {
+        if (int r = f.read_at(0, pin.p[0], chunk_end(0))) return r;
+    }
+    uint64_t entry = 0;
+    for (uint64_t g = 0; g < nch; ++g) {
+        const uint64_t b0 = g * C, b1 = chunk_end(g), blen = b1 - b0;
+        const uint8_t* host = pin.p[g & 1];
+        const int r = overlap(
+            g + 1 < nch, [&] { return f.read_at(b0 + C, pin.p[(g + 1) & 1], chunk_end(g + 1) - (b0 + C)); },
+            [&]() -> int {
+                if (blen) HIP_TRY(hipMemcpyAsync(db.p, host, blen, hipMemcpyHostToDevice, s));
+                sydelta_chunk* chp = nullptr;
+                const uint64_t pe = g + 1 == nch ? std::max(npos, b0) : b0 + C;
+                if (int rc = sydelta_chunk_classify(ix.get(), (const uint8_t*)db.p, b0, blen, L, b0, pe, s, &chp))
+                    return rc;
+                std::unique_ptr<sydelta_chunk, void (*)(sydelta_chunk*)> ch(chp, sydelta_chunk_free);
+                sydelta_delta* pp = nullptr;
+                uint64_t exit = 0;
+                if (int rc = sydelta_chunk_walk(ch.get(), entry, &exit, &pp)) return rc;
+                std::unique_ptr<sydelta_delta> part(pp);
+                HIP_TRY(hipStreamSynchronize(s));  // the device buffer and this pinned buffer are reused
+                // append, merging a Data op contiguous with the previous chunk's last one, and
+                // copy every Data op's bytes from this chunk's host buffer
+                size_t j = 0;
+                if (!d->ops.empty() && !part->ops.empty()) {
+                    sydelta_op& a = d->ops.back();
+                    const sydelta_op& b = part->ops.front();
+                    if (a.kind == SYDELTA_OP_DATA && b.kind == SYDELTA_OP_DATA && a.a + a.b == b.a) {
+                        if (b.a < b0 || b.a + b.b > b1)
+                            return fail(SYDELTA_E_INVAL, "internal: literal run outside its chunk");
+                        d->lit.insert(d->lit.end(), host + (b.a - b0), host + (b.a - b0) + b.b);
+                        a.b += b.b;
+                        j = 1;
+                    }
+                }
+                for (; j < part->ops.size(); ++j) {
+                    const sydelta_op& o = part->ops[j];
+                    d->ops.push_back(o);
+                    if (o.kind == SYDELTA_OP_DATA) {
+                        if (o.a < b0 || o.a + o.b > b1)
+                            return fail(SYDELTA_E_INVAL, "internal: literal run [%llu, +%llu) outside chunk [%llu, %llu)",
+                                        (unsigned long long)o.a, (unsigned long long)o.b, (unsigned long long)b0,
+                                        (unsigned long long)b1);
+                        d->lit_off.resize(d->ops.size() - 1, UINT64_MAX);
+                        d->lit_off.push_back(d->lit.size());
+                        d->lit.insert(d->lit.end(), host + (o.a - b0), host + (o.a - b0) + o.b);
+                    }
+                }
+                d->stats.positions += part->stats.positions;
+                d->stats.weak_hits += part->stats.weak_hits;
+                d->stats.verified_hits += part->stats.verified_hits;
+                entry = exit;
+                return SYDELTA_OK;
+            });
+        if (r) return r;
+    }
+    d->lit_off.resize(d->ops.size(), UINT64_MAX);
+    finish_stats(d.get());
+    *out = d.release();
+    return SYDELTA_OK;
 } catch (...) {
     return sydelta::host_exception();
 }
@@ -1712,7 +1950,6 @@ extern "C" int sydelta_chunk_classify(sydelta_index* idx, const uint8_t* d_buf, 
     *out = nullptr;
     if (idx->nfiles != 1) return fail(SYDELTA_E_INVAL, "chunked match needs a single-file index");
     const uint64_t n = idx->bs;
-    if (n > scan_max_window()) return fail(SYDELTA_E_INVAL, "chunked match needs block_size <= %u", scan_max_window());
     const uint64_t npos = file_len >= n ? file_len - n + 1 : 0;
     // a chunk at or past the last window start is empty (it may still own the tail)
     if (pos_begin < npos && pos_begin % n) return fail(SYDELTA_E_INVAL, "pos_begin must be a multiple of block_size");
@@ -1751,7 +1988,9 @@ extern "C" int sydelta_chunk_classify(sydelta_index* idx, const uint8_t* d_buf, 
     ch->final_src = final_src;
     ch->file_len = file_len;
     ch->bi = BasisInfo{0, idx->fblk[1], idx->last_size[0]};
-    if (int r = C.classify(probe_mode_env())) return r;
+    // windows above the LDS scan's limit: every position scanned (k_scan), no probe, as
+    // match_impl does
+    if (int r = C.classify(n > scan_max_window() ? 0 : probe_mode_env())) return r;
     if (final_src) {
         std::vector<int> tf;
         if (int r = tail_flags(C, {0}, tf)) return r;
