@@ -410,7 +410,7 @@ def algo_bytes_per_step(workload: str, n: int, nb_bytes: int, src_bytes: int) ->
             "k_xxh_pieces": n}  # xxh3: every file byte read once
 
 
-def roofline(prof: dict, steps: int, algo_step: dict, positions=None):
+def roofline(prof: dict, steps: int, algo_step: dict, positions=None, keys=None):
     """Roofline of the dominant kernel: algorithmic bytes per launch / its average launch
     time (HIP events on the launch stream, sydelta_profile).  A kernel launched L times
     per step gets 1/L of its per-step bytes per launch (the scan is split into segments
@@ -420,7 +420,12 @@ def roofline(prof: dict, steps: int, algo_step: dict, positions=None):
     filter lives in L2) the binding resource is not HBM but the L2 request rate: one
     random filter-word request per window start.  `l2_gather` reports that rate against
     L2_GATHER_PEAK (the measured chip-wide ceiling of random L2 gathers,
-    profiles/r02_micro_gather2.txt) when the step's scanned positions are known."""
+    profiles/r02_micro_gather2.txt) when the step's scanned positions are known.  For
+    k_scan_l1 only the positions that pass its 2^20-bit level-1 filter in LDS send a
+    request; that fraction is modelled as 1 - exp(-keys / 2^20) (one bit per key) and
+    the entry says so."""
+    import math
+
     dom = max(prof, key=lambda k: prof[k]["ms"]) if prof else None
     if not dom or dom not in algo_step:
         return None
@@ -431,12 +436,16 @@ def roofline(prof: dict, steps: int, algo_step: dict, positions=None):
     roof = {"bound": "hbm", "achieved": round(ach, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
             "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": pmc_traffic(dom, per_launch),
             "kernel": dom, "avg_launch_ms": round(avg_ms, 4), "algorithmic_bytes_per_launch": per_launch}
-    if positions and dom in ("k_scan_lds", "k_scan"):
-        req = positions / launches_per_step  # one filter-word request per window start
+    if positions and (dom in ("k_scan_lds", "k_scan") or (dom == "k_scan_l1" and keys)):
+        per_pos = 1.0 if dom != "k_scan_l1" else 1.0 - math.exp(-keys / float(1 << 20))
+        req = positions * per_pos / launches_per_step  # filter-word requests per launch
         rate = req / (avg_ms * 1e-3)
         roof["l2_gather"] = {"requests_per_launch": int(req), "achieved": round(rate / 1e9, 2),
                              "peak": round(L2_GATHER_PEAK / 1e9, 1), "unit": "G requests/s",
-                             "frac": round(rate / L2_GATHER_PEAK, 4)}
+                             "frac": round(rate / L2_GATHER_PEAK, 4),
+                             "requests_per_position": round(per_pos, 4),
+                             "model": ("one per window start" if dom != "k_scan_l1" else
+                                       "window starts x level-1 pass rate 1-exp(-keys/2^20)")}
     return roof
 
 
@@ -686,7 +695,7 @@ def main():
     algo_step = algo_bytes_per_step(args.workload, n, nb_bytes, src_bytes)
     stats = (last if isinstance(last, dict) else last.stats) if last is not None else None
     positions = stats.get("positions") if isinstance(stats, dict) and args.workload == "c3" else None
-    roof = roofline(prof, args.steps, algo_step, positions)
+    roof = roofline(prof, args.steps, algo_step, positions, keys=nb_bytes // bs if args.workload == "c3" else None)
     kernels = {k: {"avg_ms": round(v["ms"] / max(1, v["count"]), 4), "launches": v["count"]} for k, v in prof.items()}
 
     if rank == 0:

@@ -68,3 +68,17 @@ def test_cpu_baselines_run_small():
     files = (offs, np.full(3, fs, np.uint64), offs.copy(), np.full(3, fs + 1, np.uint64))
     c = bench.cpu_c4_baseline(hb, hn, files, bs, workers=2)
     assert c["value"] > 0 and c["cores"] == 2
+
+
+def test_roofline_scan_l1_modelled_requests():
+    import math
+
+    n = 1 << 32
+    algo = bench.algo_bytes_per_step("c3", n, n, n)
+    r = bench.roofline({"k_scan_l1": {"ms": 172.4, "count": 10}}, 10, algo, positions=n, keys=1 << 20)
+    g = r["l2_gather"]
+    assert abs(g["requests_per_position"] - (1 - math.exp(-1))) < 1e-4
+    assert g["requests_per_launch"] == int(n * (1 - math.exp(-1)))
+    assert "level-1" in g["model"]
+    # without the key count no request rate is claimed
+    assert "l2_gather" not in bench.roofline({"k_scan_l1": {"ms": 172.4, "count": 10}}, 10, algo, positions=n)
