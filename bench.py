@@ -7,6 +7,9 @@ already resident in HBM:
   c3 (default, BASELINE config 3): signature of a 4 GiB basis (bs 4096) + probe-table
      build + greedy rolling match of a 4 GiB source carrying Bernoulli(5%) byte
      substitutions -> op list on the host.  Algorithmic bytes = 4 GiB + 4 GiB.
+  c3b (BASELINE C3's variant): the same 4 GiB basis; the source has one
+     substituted byte in 5% of its 4 KiB blocks and a 1-byte insertion in 1% of them
+     (every insertion shifts what follows: unaligned copies, probe + scans).
   c2 (config 2): signature only over 4 GiB.
   c4 (config 4 shape): batch of 1 MiB files (signature + per-file match).
   apply: apply_delta on the device for the C5-shaped pair of
@@ -64,7 +67,7 @@ def parse():
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--workload", default="c3",
-                    choices=["c3", "c2", "c4", "c5", "apply", "json", "local", "xxh3", "path"])
+                    choices=["c3", "c3b", "c2", "c4", "c5", "apply", "json", "local", "xxh3", "path"])
     ap.add_argument("--size-gib", type=float, default=None,
                     help="bytes per rank: c2/c3 basis and source (default 4), c5 chunk (default 8)")
     ap.add_argument("--block-size", type=int, default=None, help="default 4096 (c5: 8192)")
@@ -402,7 +405,7 @@ def algo_bytes_per_step(workload: str, n: int, nb_bytes: int, src_bytes: int) ->
     step the signature kernels read the basis once and the scan reads the source once
     (SURVEY.md section 8(d))."""
     return {"k_scan": src_bytes, "k_scan_lds": src_bytes, "k_scan_l1": src_bytes,
-            "k_sig_fast": nb_bytes if workload == "c3" else n,
+            "k_sig_fast": nb_bytes if workload in ("c3", "c3b") else n,
             "k_sig_batch": n, "k_sig_wave": n, "k_probe": src_bytes,
             "k_apply": 2 * n,  # apply: every output byte read once and written once
             "k_json_write": n,  # json: every literal byte read once (text written: ~3.6x)
@@ -482,6 +485,23 @@ def main():
     if args.workload in ("c3",):
         new = torch.empty(n, dtype=torch.uint8, device="cuda")
         dev.synth_mutate(new, basis, seed_base + 1, args.edit_ppm)
+    if args.workload == "c3b":
+        import numpy as np
+
+        ed = torch.empty(n, dtype=torch.uint8, device="cuda")
+        dev.synth_mutate_blocks(ed, basis, 0, 4096, seed_base + 1, 50000)
+        rng = np.random.default_rng(seed_base + 2)
+        nblk4 = n // 4096
+        ins = np.sort(rng.choice(nblk4, nblk4 // 100, replace=False)) * 4096 + rng.integers(0, 4096, nblk4 // 100)
+        extra = torch.from_numpy(rng.integers(0, 256, ins.size, dtype=np.uint8)).cuda()
+        cuts = np.concatenate([[0], ins, [n]])
+        parts = []
+        for i in range(ins.size + 1):
+            parts.append(ed[int(cuts[i]):int(cuts[i + 1])])
+            if i < ins.size:
+                parts.append(extra[i:i + 1])
+        new = torch.cat(parts)
+        del ed, parts
     c5 = None
     apply_d = None
     json_d = None
@@ -595,7 +615,7 @@ def main():
         if args.workload == "c2":
             dev.signature(basis, bs, stream=stream)
             return None
-        if args.workload == "c3":
+        if args.workload in ("c3", "c3b"):
             w, s = dev.signature(basis[:nb_bytes], bs, stream=stream)
             idx = dev.Index(w, s, bs, bs, device=local, stream=stream)
             d = dev.match(idx, new, stream=stream)
@@ -671,8 +691,8 @@ def main():
 
     if args.workload == "c2":
         bytes_per_step = n
-    elif args.workload == "c3":
-        bytes_per_step = nb_bytes + n
+    elif args.workload in ("c3", "c3b"):
+        bytes_per_step = nb_bytes + new.numel()
     elif args.workload == "c5":
         bytes_per_step = 2 * n
     elif args.workload == "apply":
@@ -691,17 +711,19 @@ def main():
     value = total_bytes / elapsed / GIB
     ms_per_step = elapsed / args.steps * 1e3
 
-    src_bytes = int(files[3].sum()) if args.workload == "c4" else n
+    src_bytes = int(files[3].sum()) if args.workload == "c4" else new.numel() if args.workload == "c3b" else n
     algo_step = algo_bytes_per_step(args.workload, n, nb_bytes, src_bytes)
     stats = (last if isinstance(last, dict) else last.stats) if last is not None else None
-    positions = stats.get("positions") if isinstance(stats, dict) and args.workload == "c3" else None
-    roof = roofline(prof, args.steps, algo_step, positions, keys=nb_bytes // bs if args.workload == "c3" else None)
+    positions = stats.get("positions") if isinstance(stats, dict) and args.workload in ("c3", "c3b") else None
+    roof = roofline(prof, args.steps, algo_step, positions,
+                    keys=nb_bytes // bs if args.workload in ("c3", "c3b") else None)
     kernels = {k: {"avg_ms": round(v["ms"] / max(1, v["count"]), 4), "launches": v["count"]} for k, v in prof.items()}
 
     if rank == 0:
         cpu = None
-        if world == 1 and not args.no_cpu_baseline and args.workload == "c3":
-            cpu = cpu_baseline(basis[:nb_bytes].cpu().numpy(), new[:min(n, 256 << 20)].cpu().numpy(), n, bs)
+        if world == 1 and not args.no_cpu_baseline and args.workload in ("c3", "c3b"):
+            cpu = cpu_baseline(basis[:nb_bytes].cpu().numpy(), new[:min(new.numel(), 256 << 20)].cpu().numpy(),
+                               new.numel(), bs)
         if world == 1 and not args.no_cpu_baseline and args.workload == "c4":
             k = min(500, len(files[0]))  # the sampled files' bytes only
             cpu = cpu_c4_baseline(basis[:int(files[0][k - 1] + files[1][k - 1])].cpu().numpy(),
@@ -736,6 +758,8 @@ def main():
             "config": {
                 "workload": {
                     "c3": "C3: signature(4 GiB basis) + rolling match(4 GiB source, 5% random byte edits), bs 4096",
+                    "c3b": "C3b: signature(4 GiB basis) + rolling match(4 GiB source: one substituted byte in 5% "
+                           "of 4 KiB blocks, a 1-byte insertion in 1%), bs 4096",
                     "c2": "C2: signature only over 4 GiB, bs 4096",
                     "c4": f"C4: {args.files} x 1 MiB files (1-byte insertion + 16 substitutions each), "
                           f"batched signature + per-file index + batched match, file-sharded over ranks",
@@ -754,7 +778,7 @@ def main():
                             f"blocks edited), host-inclusive",
                 }[args.workload],
                 "block_size": bs,
-                "basis_bytes": nb_bytes if args.workload == "c3" else n,
+                "basis_bytes": nb_bytes if args.workload in ("c3", "c3b") else n,
                 "bytes_per_rank_per_step": bytes_per_step,
                 "parallelism": (f"chunk-sharded x{world} (RCCL all-gather of the signature, chained walks)"
                                 if args.workload == "c5" else
