@@ -9,7 +9,7 @@ mkdir -p "$OUT"
 export TMPDIR=/tmp
 cd "$R"
 step() { local t=$1; shift; echo "== $* (limit ${t}s)" >&2; timeout -k 10 "$t" "$@"; local rc=$?; echo "== rc=$rc" >&2; return $rc; }
-[ -n "${SKIP_TESTS:-}" ] || step 900 python -m pytest tests -m gpu -x -q -p no:cacheprovider > "$OUT/pytest.log" 2>&1 || { tail -30 "$OUT/pytest.log"; exit 1; }
+[ -n "${SKIP_TESTS:-}" ] || step 1100 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread -p no:cacheprovider > "$OUT/pytest.log" 2>&1 || { tail -30 "$OUT/pytest.log"; exit 1; }
 tail -3 "$OUT/pytest.log" 2>/dev/null
 step 600 python bench.py "$@" > "$OUT/bench.json" 2> "$OUT/bench.err" || { cat "$OUT/bench.err" | tail -20; exit 1; }
 cat "$OUT/bench.json"
