@@ -148,6 +148,30 @@ inline int walk_src(const Src& c, uint64_t n, uint64_t entry, uint64_t end, cons
     uint64_t kp = c.kb;  // next block whose phase-probed window may hit
     const bool has_phase = c.probed && !c.ppos.empty();
     while (x < end) {
+        if (c.probed && x == lit && ka < kend && ka * n == x) {
+            // a run of aligned Copies (the rsync case): at an aligned x whose aligned window
+            // hit, that window is the earliest hit (a scan hit at x names the same block,
+            // phase-probed windows lie inside blocks), so copy it and jump a block.  The run
+            // is measured first and written through a pointer (locals: the op stores cannot
+            // alias them).
+            const uint32_t* ah = c.ahit.data() - c.kb;
+            uint64_t k1 = ka;
+            while (k1 < kend && k1 * n < end && ah[k1] != kNoBlk) ++k1;
+            if (k1 > ka) {
+                const uint64_t bb = bi.blk_base, nbb = bi.nblocks, ls = bi.last_size;
+                const size_t o = ops.size();
+                ops.resize(o + (k1 - ka));
+                sydelta_op* w = ops.data() + o;
+                for (uint64_t k = ka; k < k1; ++k) {
+                    const uint64_t g = ah[k] - bb;
+                    *w++ = {SYDELTA_OP_COPY, 0, g * n, g + 1 == nbb ? ls : n};
+                }
+                x = k1 * n;
+                lit = x;
+                ka = k1;
+                if (x >= end) break;
+            }
+        }
         // next hit at or after x and before end: the next scan hit or the next aligned hit
         while (i < H && c.hpos[i] < x) ++i;
         uint64_t p = end;
@@ -353,9 +377,19 @@ int walk_split(const Src& c, uint64_t n, const std::vector<uint64_t>& st, const 
     std::vector<double> tseg(T, 0.0);
     auto seg = [&](int t, uint64_t from) {
         const double ts = clock();
-        part[t].clear();
+        // walk into a vector whose header lives on this thread's stack: the segments'
+        // headers sit side by side in `part`, and every push_back writes its end pointer
+        // (false sharing made 8 concurrent segments ~8x slower than one)
+        OpVec local;
+        local.swap(part[t]);
+        local.clear();
         const bool fin = final_src && t == T - 1;
-        rc[t] = walk_src(c, n, from, st[t + 1], bi, fin, tail_match, part[t], &ex[t], &need[t]);
+        uint64_t e = 0, nd = 0;
+        const int r = walk_src(c, n, from, st[t + 1], bi, fin, tail_match, local, &e, &nd);
+        local.swap(part[t]);
+        rc[t] = r;
+        ex[t] = e;
+        need[t] = nd;
         tseg[t] = clock() - ts;
     };
     if (!run_parallel(T, [&](int t) { seg(t, st[t]); })) return -1;
