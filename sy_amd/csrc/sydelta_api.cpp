@@ -1648,7 +1648,7 @@ extern "C" int sydelta_generate_delta_streaming(const char* source_path, const s
                 sydelta_delta* pp = nullptr;
                 uint64_t exit = 0;
                 if (int rc = sydelta_chunk_walk(ch.get(), entry, &exit, &pp)) return rc;
-                std::unique_ptr<sydelta_delta> part(pp);
+                std::unique_ptr<sydelta_delta, void (*)(sydelta_delta*)> part(pp, sydelta_delta_free);  // recycles its ops
                 HIP_TRY(hipStreamSynchronize(s));  // the device buffer and this pinned buffer are reused
                 // append, merging a Data op contiguous with the previous chunk's last one, and
                 // copy every Data op's bytes from this chunk's host buffer
