@@ -1,0 +1,151 @@
+"""TEST INFRASTRUCTURE: the library's host logic run on the CPU against the host
+emulation of the device layer (tests/csrc/fake_device.cpp), checked against the C
+oracle.  Run by tests/test_host_emulated.py as `python emulated_checks.py <repo> <lib>`;
+loads sy_amd/_lib.py's bindings onto <lib> instead of libsydelta.so (the product
+module is not modified and never loads this library).
+
+Covers what the GPU tests cover for the host side: the streamed path API over many
+chunks (compute_checksums, generate_delta_streaming, bs up to 128 KiB), the in-memory
+generator, tiny and empty files, the probe + on-demand scan walk (SYDELTA_PROBE=1),
+the split walk (SYDELTA_WALK_PAR_MIN=1), the path-level change ratio on ratio.rs's
+cases, and 10 threads calling the path API at once.
+"""
+import os
+import sys
+import tempfile
+import types
+from concurrent.futures import ThreadPoolExecutor
+
+import numpy as np
+
+ROOT, LIB = sys.argv[1], sys.argv[2]
+sys.path.insert(0, ROOT)
+
+# sy_amd._lib with LIB_PATH pointing at the emulation build (exec'd from the source)
+import sy_amd  # noqa: E402
+
+src = open(os.path.join(ROOT, "sy_amd", "_lib.py")).read()
+anchor = 'LIB_PATH = os.path.join(HERE, "libsydelta.so")'
+assert anchor in src
+mod = types.ModuleType("sy_amd._lib")
+mod.__file__ = os.path.join(ROOT, "sy_amd", "_lib.py")
+exec(compile(src.replace(anchor, f"LIB_PATH = {LIB!r}"), mod.__file__, "exec"), mod.__dict__)
+sys.modules["sy_amd._lib"] = mod
+sy_amd._lib = mod
+
+import sy_amd.delta as D  # noqa: E402
+from oracle import oracle as O  # noqa: E402
+
+C = O.C()
+
+
+def tuples(delta):
+    return [("C", op.offset, op.size) if isinstance(op, D.Copy) else ("D", len(op.data)) for op in delta.ops]
+
+
+def expect(src_b, basis_b, bs):
+    w, s, z = C.compute_checksums(basis_b, bs)
+    return [("C", a, b) if k == "C" else ("D", b) for k, a, b in O.ops_from_arrays(*C.generate_delta(src_b, w, s, z, bs))]
+
+
+def case(seed, n, bs):
+    rng = np.random.default_rng(seed)
+    basis = O.synth_bytes(n, 0x5E1D0300 + seed)
+    s = basis.copy()
+    for p in rng.integers(0, n, 25):
+        s[p] ^= 0x33
+    ins = int(rng.integers(n // 3, n // 2))
+    s = np.concatenate([s[:ins], rng.integers(0, 256, 7, dtype=np.uint8), s[ins:]])
+    k = int(rng.integers(0, max(1, n // bs - 1)))
+    s = np.concatenate([s, basis[k * bs:(k + 1) * bs], basis[(n // bs) * bs:]])
+    return basis, s
+
+
+def check_pair(tmp, basis, s, bs, tag):
+    pb, ps, po = os.path.join(tmp, "dest"), os.path.join(tmp, "src"), os.path.join(tmp, "out")
+    basis.tofile(pb)
+    s.tofile(ps)
+    sigs = D.compute_checksums(pb, bs)
+    w, st, z = C.compute_checksums(basis, bs)
+    assert [x.weak for x in sigs] == w.tolist() and [x.strong for x in sigs] == st.tolist(), tag
+    assert [x.size for x in sigs] == z.tolist(), tag
+    exp = expect(s, basis, bs)
+    d = D.generate_delta_streaming(ps, sigs, bs)
+    assert tuples(d) == exp, (tag, "streaming")
+    D.apply_delta(pb, d, po)
+    assert open(po, "rb").read() == s.tobytes(), (tag, "apply")
+    d2 = D.generate_delta(ps, sigs, bs)
+    assert d2 == d, (tag, "in-memory")
+
+
+def main():
+    n_checks = 0
+    with tempfile.TemporaryDirectory() as tmp:
+        for chunk in (1 << 16, 1 << 20):
+            os.environ["SYDELTA_STREAM_CHUNK"] = str(chunk)
+            for bs, n in [(4096, (1 << 20) + 1234), (1007, (1 << 20) + 99), (64, (1 << 18) + 5),
+                          (16384, (1 << 20) + 4321), (131072, (3 << 20) + 17), (512, 300000)]:
+                for probe in ("0", "1", "auto"):
+                    if probe == "auto":
+                        os.environ.pop("SYDELTA_PROBE", None)
+                    else:
+                        os.environ["SYDELTA_PROBE"] = probe
+                    basis, s = case(bs % 97, n, bs)
+                    check_pair(tmp, basis, s, bs, (chunk, bs, n, probe))
+                    n_checks += 1
+        os.environ.pop("SYDELTA_PROBE", None)
+        # tiny and empty files
+        os.environ["SYDELTA_STREAM_CHUNK"] = "65536"
+        for size in (0, 1, 63, 64, 65, 4095, 4096, 4097):
+            b = O.synth_bytes(size, 5)
+            check_pair(tmp, b, b.copy(), 64, ("tiny", size))
+            n_checks += 1
+        # the split walk on every source with hits (probe on: the aligned-run fast path)
+        os.environ["SYDELTA_WALK_PAR_MIN"] = "1"
+        for t in ("2", "3", "8"):
+            os.environ["SYDELTA_WALK_THREADS"] = t
+            os.environ["SYDELTA_PROBE"] = "1"
+            basis, s = case(11, (2 << 20) + 77, 4096)
+            check_pair(tmp, basis, s, 4096, ("split", t))
+            n_checks += 1
+        for k in ("SYDELTA_WALK_PAR_MIN", "SYDELTA_WALK_THREADS", "SYDELTA_PROBE"):
+            os.environ.pop(k, None)
+        # change ratio on paths: ratio.rs's cases against the oracle
+        MiB = 1 << 20
+        for name in ("same", "all", "partial", "threshold", "size"):
+            a = bytearray(b"\x2a" * MiB)
+            b = bytes(b"\x2a" * MiB)
+            if name == "all":
+                b = b"\x63" * MiB
+            elif name == "partial":
+                a[:256 * 1024] = b"\x63" * (256 * 1024)
+            elif name == "threshold":
+                a[:800 * 1024] = b"\x63" * (800 * 1024)
+            elif name == "size":
+                a = bytearray(b"\x2a" * (2 * MiB))
+            ps, pd = os.path.join(tmp, "rs"), os.path.join(tmp, "rd")
+            open(ps, "wb").write(bytes(a))
+            open(pd, "wb").write(b)
+            for sc, thr in ((None, None), (5, None), (1, 0.5), (0, None), (64, 0.9)):
+                r = D.estimate_change_ratio(ps, pd, 64 * 1024, sc, thr)
+                e = O.py_estimate_change_ratio(bytes(a), b, 64 * 1024, sc, thr)
+                assert (r.change_ratio, r.blocks_sampled, r.blocks_changed, r.use_delta, r.threshold) == e, (name, sc)
+                n_checks += 1
+        # 10 threads through the path API at once
+        os.environ["SYDELTA_STREAM_CHUNK"] = str(1 << 18)
+        pairs = [case(200 + k, (1 << 20) + 977 * k, 4096) for k in range(10)]
+
+        def one(k):
+            d = os.path.join(tmp, f"t{k}")
+            os.makedirs(d, exist_ok=True)
+            check_pair(d, pairs[k][0], pairs[k][1], 4096, ("thread", k))
+            return True
+
+        with ThreadPoolExecutor(10) as ex:
+            assert all(ex.map(one, range(10)))
+        n_checks += 10
+    print(f"emulated host checks ok: {n_checks}")
+
+
+if __name__ == "__main__":
+    main()

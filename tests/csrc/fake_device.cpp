@@ -1,0 +1,359 @@
+// fake_device.cpp — TEST INFRASTRUCTURE, never part of libsydelta.  A host emulation
+// of the device layer so that the library's host logic (classification bookkeeping,
+// walks, chunked and streamed path API, batch API, change-ratio sampling) can run on a
+// CPU-only machine: tests/test_host_emulated.py links the C ABI's host translation
+// units against this file instead of libamdhip64 and the gfx950 kernels.
+//
+//   * HIP runtime calls: host memory, synchronous copies, one fake gfx950 device;
+//   * the launch_* entry points of sydelta_internal.hpp: the same contracts computed
+//     with the C oracle's Adler-32 / XXH3-64 (oracle/sydelta_oracle.c) and hash maps —
+//     weak/strong per block, first candidate in index order with equal strong, hits
+//     keyed (segment << 32 | position - pos_begin).
+//
+// It says nothing about the kernels themselves (the GPU tests do); it checks that the
+// host code around them is right.
+#include <hip/hip_runtime_api.h>
+#include <stdint.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include <algorithm>
+#include <map>
+#include <mutex>
+#include <numeric>
+#include <unordered_map>
+#include <vector>
+
+#include "sydelta_internal.hpp"
+
+extern "C" uint32_t oracle_adler32(const uint8_t* data, uint64_t len);
+extern "C" uint64_t oracle_xxh3_64(const uint8_t* in, uint64_t len);
+
+// ---------------------------------------------------------------------------
+// HIP runtime
+// ---------------------------------------------------------------------------
+struct ihipStream_t {
+    int dummy;
+};
+struct ihipEvent_t {
+    int dummy;
+};
+
+extern "C" {
+hipError_t hipGetDeviceCount(int* n) {
+    *n = 1;
+    return hipSuccess;
+}
+hipError_t hipGetDevice(int* d) {
+    *d = 0;
+    return hipSuccess;
+}
+hipError_t hipSetDevice(int d) { return d == 0 ? hipSuccess : hipErrorInvalidDevice; }
+hipError_t hipGetDevicePropertiesR0600(hipDeviceProp_tR0600* p, int d) {
+    if (d != 0) return hipErrorInvalidDevice;
+    memset(p, 0, sizeof(*p));
+    strcpy(p->name, "host emulation");
+    strcpy(p->gcnArchName, "gfx950:sramecc+:xnack-");
+    p->multiProcessorCount = 256;
+    return hipSuccess;
+}
+const char* hipGetErrorString(hipError_t e) { return e == hipSuccess ? "no error" : "emulated HIP error"; }
+hipError_t hipStreamCreateWithFlags(hipStream_t* s, unsigned int) {
+    *s = new ihipStream_t();
+    return hipSuccess;
+}
+hipError_t hipStreamSynchronize(hipStream_t) { return hipSuccess; }
+hipError_t hipStreamWaitEvent(hipStream_t, hipEvent_t, unsigned int) { return hipSuccess; }
+hipError_t hipEventCreate(hipEvent_t* e) {
+    *e = new ihipEvent_t();
+    return hipSuccess;
+}
+hipError_t hipEventCreateWithFlags(hipEvent_t* e, unsigned) { return hipEventCreate(e); }
+hipError_t hipEventRecord(hipEvent_t, hipStream_t) { return hipSuccess; }
+hipError_t hipEventSynchronize(hipEvent_t) { return hipSuccess; }
+hipError_t hipEventElapsedTime(float* ms, hipEvent_t, hipEvent_t) {
+    *ms = 0.f;
+    return hipSuccess;
+}
+hipError_t hipEventDestroy(hipEvent_t e) {
+    delete e;
+    return hipSuccess;
+}
+static void* emu_alloc(size_t n) {
+    void* p = nullptr;
+    if (posix_memalign(&p, 256, n ? n : 1)) return nullptr;
+    return p;
+}
+hipError_t hipMallocAsync(void** p, size_t n, hipStream_t) {
+    *p = emu_alloc(n);
+    return *p ? hipSuccess : hipErrorOutOfMemory;
+}
+hipError_t hipMalloc(void** p, size_t n) { return hipMallocAsync(p, n, nullptr); }
+hipError_t hipFreeAsync(void* p, hipStream_t) {
+    free(p);
+    return hipSuccess;
+}
+hipError_t hipFree(void* p) {
+    free(p);
+    return hipSuccess;
+}
+hipError_t hipHostMalloc(void** p, size_t n, unsigned int) { return hipMallocAsync(p, n, nullptr); }
+hipError_t hipHostFree(void* p) {
+    free(p);
+    return hipSuccess;
+}
+hipError_t hipMemcpyAsync(void* d, const void* s, size_t n, hipMemcpyKind, hipStream_t) {
+    if (n) memmove(d, s, n);
+    return hipSuccess;
+}
+hipError_t hipMemcpy(void* d, const void* s, size_t n, hipMemcpyKind k) { return hipMemcpyAsync(d, s, n, k, nullptr); }
+hipError_t hipMemsetAsync(void* d, int v, size_t n, hipStream_t) {
+    memset(d, v, n);
+    return hipSuccess;
+}
+hipError_t hipGetLastError() { return hipSuccess; }
+}
+
+// ---------------------------------------------------------------------------
+// device layer
+// ---------------------------------------------------------------------------
+namespace sydelta {
+namespace {
+constexpr uint32_t kNone = 0xFFFFFFFFu;
+constexpr uint32_t kMod = 65521;
+
+struct Cand {
+    uint32_t blk;
+    uint64_t strong;
+};
+struct FakeIndex {
+    std::vector<std::unordered_map<uint32_t, std::vector<Cand>>> files;  // weak -> candidates in index order
+};
+std::mutex g_mu;
+std::map<const void*, FakeIndex> g_ix;  // keyed by the index's `keys` array
+
+const FakeIndex& find_ix(const DeviceIndex& ix) {
+    std::lock_guard<std::mutex> lk(g_mu);
+    return g_ix.at(ix.keys);
+}
+
+// first candidate in index order with equal strong (generator.rs:127-133), or kNone
+uint32_t lookup(const FakeIndex& F, uint32_t file, uint32_t weak, const uint8_t* win, uint64_t n, bool* weak_hit) {
+    const auto& m = F.files[file];
+    auto it = m.find(weak);
+    if (it == m.end()) return kNone;
+    if (weak_hit) *weak_hit = true;
+    const uint64_t st = oracle_xxh3_64(win, n);
+    for (const Cand& c : it->second)
+        if (c.strong == st) return c.blk;
+    return kNone;
+}
+
+// classify window starts [p0, p1) of src (len bytes) against file `file`; hits to the output
+void scan_range(const FakeIndex& F, uint32_t file, const uint8_t* src, uint64_t p0, uint64_t p1, uint64_t n,
+                uint64_t key_hi, uint64_t* key, uint32_t* val, uint64_t cap, unsigned long long* counters) {
+    if (p0 >= p1) return;
+    uint64_t a = 1, b = 0;  // Adler of [p0, p0+n)
+    for (uint64_t i = 0; i < n; ++i) {
+        a = (a + src[p0 + i]) % kMod;
+        b = (b + a) % kMod;
+    }
+    for (uint64_t p = p0;; ++p) {
+        bool wh = false;
+        const uint32_t w = (uint32_t)((b << 16) | a);
+        const uint32_t blk = lookup(F, file, w, src + p, n, &wh);
+        if (wh) counters[1]++;
+        if (blk != kNone) {
+            const unsigned long long k = counters[0]++;
+            if (k < cap) {
+                key[k] = key_hi | (p - p0);
+                val[k] = blk;
+            }
+        }
+        if (p + 1 >= p1) break;
+        const uint64_t out = src[p], in = src[p + n];  // rolling.rs:66-79
+        a = (a + 2 * kMod - out + in) % kMod;
+        b = (b + 3 * kMod - (n * out) % kMod + a - 1) % kMod;
+    }
+}
+}  // namespace
+
+hipError_t launch_signature(const uint8_t* d_buf, uint64_t len, uint64_t bs, uint32_t* d_weak, uint64_t* d_strong,
+                            hipStream_t, Profiler*) {
+    const uint64_t nb = (len + bs - 1) / bs;
+    for (uint64_t k = 0; k < nb; ++k) {
+        const uint64_t sz = std::min(bs, len - k * bs);
+        d_weak[k] = oracle_adler32(d_buf + k * bs, sz);
+        d_strong[k] = oracle_xxh3_64(d_buf + k * bs, sz);
+    }
+    return hipSuccess;
+}
+
+hipError_t launch_signature_batch(const uint8_t* d_buf, const uint64_t* d_off, const uint64_t* d_len,
+                                  const uint64_t* d_fblk, uint64_t nfiles, uint64_t bs, uint64_t, uint32_t* d_weak,
+                                  uint64_t* d_strong, hipStream_t s, Profiler* p) {
+    for (uint64_t f = 0; f < nfiles; ++f)
+        launch_signature(d_buf + d_off[f], d_len[f], bs, d_weak + d_fblk[f], d_strong + d_fblk[f], s, p);
+    return hipSuccess;
+}
+
+hipError_t launch_signature_batch_fast(const uint8_t* d_buf, const uint64_t* d_aoff, const uint64_t* d_agb,
+                                       const uint64_t* d_apfx, uint64_t nact, uint64_t, const uint64_t* d_loff,
+                                       const uint64_t* d_llen, const uint64_t* d_lidx, uint64_t npart, uint64_t bs,
+                                       uint32_t* d_weak, uint64_t* d_strong, hipStream_t, Profiler*) {
+    for (uint64_t f = 0; f < nact; ++f)
+        for (uint64_t j = 0; j < d_apfx[f + 1] - d_apfx[f]; ++j) {
+            const uint8_t* b = d_buf + d_aoff[f] + j * bs;
+            d_weak[d_agb[f] + j] = oracle_adler32(b, bs);
+            d_strong[d_agb[f] + j] = oracle_xxh3_64(b, bs);
+        }
+    for (uint64_t i = 0; i < npart; ++i) {
+        d_weak[d_lidx[i]] = oracle_adler32(d_buf + d_loff[i], d_llen[i]);
+        d_strong[d_lidx[i]] = oracle_xxh3_64(d_buf + d_loff[i], d_llen[i]);
+    }
+    return hipSuccess;
+}
+
+hipError_t launch_index_build(const uint32_t* d_weak, const uint64_t* d_strong, DeviceIndex& ix, hipStream_t,
+                              Profiler*) {
+    FakeIndex F;
+    F.files.resize(ix.nfiles);
+    for (uint64_t f = 0; f < ix.nfiles; ++f)
+        for (uint64_t k = ix.d_fblk[f]; k < ix.d_fblk[f + 1]; ++k)
+            F.files[f][d_weak[k]].push_back({(uint32_t)k, d_strong[k]});
+    std::lock_guard<std::mutex> lk(g_mu);
+    g_ix[ix.keys] = std::move(F);
+    return hipSuccess;
+}
+
+uint64_t scan_tile_positions() { return 16384; }
+uint32_t scan_max_window() { return 8192; }
+size_t scan_queue_entries() { return 1024; }
+
+hipError_t launch_scan(const uint8_t* d_buf, const ScanSeg* d_segs, uint32_t nsegs, uint32_t, uint32_t n,
+                       const DeviceIndex& ix, const uint64_t*, uint64_t* d_hit_key, uint32_t* d_hit_val,
+                       uint64_t out_cap, unsigned long long* d_counters, uint2*, size_t, hipStream_t, Profiler*) {
+    const FakeIndex& F = find_ix(ix);
+    for (uint32_t g = 0; g < nsegs; ++g) {
+        const ScanSeg& S = d_segs[g];
+        scan_range(F, S.file, d_buf + S.src, S.pos_begin, S.pos_end, n, (uint64_t)g << kSegShift, d_hit_key, d_hit_val,
+                   out_cap, d_counters);
+    }
+    return hipSuccess;
+}
+
+hipError_t launch_scan_wide(const uint8_t* d_src, uint64_t, uint64_t pos_begin, uint64_t pos_end, uint32_t seg_id,
+                            uint32_t n, const DeviceIndex& ix, const uint64_t*, uint64_t* d_hit_key,
+                            uint32_t* d_hit_val, uint64_t out_cap, unsigned long long* d_counters, hipStream_t,
+                            Profiler*) {
+    scan_range(find_ix(ix), 0, d_src, pos_begin, pos_end, n, (uint64_t)seg_id << kSegShift, d_hit_key, d_hit_val,
+               out_cap, d_counters);
+    return hipSuccess;
+}
+
+hipError_t launch_sort_hits(uint64_t* key, uint32_t* val, uint64_t*, uint32_t*, uint64_t nhits, int, hipStream_t,
+                            uint64_t** key_out, uint32_t** val_out) {
+    std::vector<uint64_t> idx(nhits);
+    std::iota(idx.begin(), idx.end(), 0);
+    std::stable_sort(idx.begin(), idx.end(), [&](uint64_t x, uint64_t y) { return key[x] < key[y]; });
+    std::vector<uint64_t> k2(nhits);
+    std::vector<uint32_t> v2(nhits);
+    for (uint64_t i = 0; i < nhits; ++i) {
+        k2[i] = key[idx[i]];
+        v2[i] = val[idx[i]];
+    }
+    std::copy(k2.begin(), k2.end(), key);
+    std::copy(v2.begin(), v2.end(), val);
+    *key_out = key;
+    *val_out = val;
+    return hipSuccess;
+}
+
+hipError_t launch_probe(const uint8_t* d_base, const ProbeJob* d_jobs, uint32_t njobs, uint64_t nprobes,
+                        uint32_t stride, uint32_t n, bool, const DeviceIndex& ix, uint32_t* d_pw, uint64_t* d_pst,
+                        uint32_t* d_out, hipStream_t, Profiler*) {
+    const FakeIndex& F = find_ix(ix);
+    for (uint32_t j = 0; j < njobs; ++j) {
+        const uint64_t end = j + 1 < njobs ? d_jobs[j + 1].pfx : nprobes;
+        for (uint64_t w = d_jobs[j].pfx; w < end; ++w) {
+            const uint64_t k = d_jobs[j].k0 + (w - d_jobs[j].pfx) * stride;
+            const uint8_t* win = d_base + d_jobs[j].src + k * n;
+            const uint32_t wk = oracle_adler32(win, n);
+            d_pw[w] = wk;
+            d_pst[w] = oracle_xxh3_64(win, n);
+            d_out[w] = lookup(F, d_jobs[j].file, wk, win, n, nullptr);
+        }
+    }
+    return hipSuccess;
+}
+
+hipError_t launch_tail(const uint8_t* d_buf, const TailJob* d_jobs, uint32_t njobs, const uint32_t* d_weak,
+                       const uint64_t* d_strong, int* d_flag, hipStream_t) {
+    for (uint32_t i = 0; i < njobs; ++i) {
+        const uint8_t* p = d_buf + d_jobs[i].src;
+        const uint64_t L = d_jobs[i].last_size, b = d_jobs[i].blk;
+        d_flag[i] = oracle_adler32(p, L) == d_weak[b] && oracle_xxh3_64(p, L) == d_strong[b];
+    }
+    return hipSuccess;
+}
+
+hipError_t launch_apply(const ApplyPiece* d_pieces, uint64_t npieces, const uint8_t* d_basis, const uint8_t* d_lit,
+                        uint8_t* d_out, hipStream_t, Profiler*) {
+    for (uint64_t i = 0; i < npieces; ++i) {
+        const ApplyPiece& p = d_pieces[i];
+        memcpy(d_out + p.dst, (p.from_basis ? d_basis : d_lit) + p.src, p.len);
+    }
+    return hipSuccess;
+}
+
+hipError_t launch_json_len(const JsonPiece*, uint64_t, const uint8_t*, uint64_t*, hipStream_t, Profiler*) {
+    return hipErrorNotSupported;
+}
+hipError_t launch_json_write(const JsonPiece*, uint64_t, const uint8_t*, const uint64_t*, uint64_t, uint8_t*,
+                             hipStream_t, Profiler*) {
+    return hipErrorNotSupported;
+}
+hipError_t launch_exclusive_sum_u64(const uint64_t* d_in, uint64_t* d_out, uint64_t n, hipStream_t) {
+    uint64_t acc = 0;
+    for (uint64_t i = 0; i < n; ++i) {
+        const uint64_t v = d_in[i];
+        d_out[i] = acc;
+        acc += v;
+    }
+    return hipSuccess;
+}
+
+hipError_t launch_block_cmp(const uint8_t* d_src, uint64_t slen, const uint8_t* d_dst, uint64_t dlen, uint64_t bs,
+                            uint8_t* d_changed, hipStream_t, Profiler*) {
+    const uint64_t nb = (slen + bs - 1) / bs;
+    for (uint64_t k = 0; k < nb; ++k) {
+        const uint64_t o = k * bs, sl = std::min(bs, slen - o), dl = dlen > o ? std::min(bs, dlen - o) : 0;
+        d_changed[k] = sl != dl || memcmp(d_src + o, d_dst + o, sl) != 0;
+    }
+    return hipSuccess;
+}
+
+hipError_t launch_hash_blocks(const uint8_t* d_buf, uint64_t len, uint64_t bs, const uint64_t* d_pos, uint32_t count,
+                              uint64_t* d_out, hipStream_t) {
+    for (uint32_t i = 0; i < count; ++i) {
+        const uint64_t o = d_pos[i] * bs;
+        d_out[i] = oracle_xxh3_64(d_buf + o, o < len ? std::min(bs, len - o) : 0);
+    }
+    return hipSuccess;
+}
+
+hipError_t launch_xxh_files(const uint8_t* d_buf, const uint64_t* d_off, const uint64_t* d_len, const uint64_t*,
+                            const uint64_t*, const uint64_t*, uint64_t, const uint32_t*, uint64_t nfiles, uint64_t,
+                            uint64_t*, uint64_t* d_out, hipStream_t, Profiler*) {
+    for (uint64_t f = 0; f < nfiles; ++f) d_out[f] = oracle_xxh3_64(d_buf + d_off[f], d_len[f]);
+    return hipSuccess;
+}
+
+hipError_t launch_synth_fill(uint8_t*, uint64_t, uint64_t, hipStream_t, uint64_t) { return hipErrorNotSupported; }
+hipError_t launch_synth_edit_blocks(uint8_t*, uint64_t, uint64_t, uint64_t, uint64_t, uint32_t, hipStream_t) {
+    return hipErrorNotSupported;
+}
+hipError_t launch_synth_mutate(uint8_t*, const uint8_t*, uint64_t, uint64_t, uint32_t, hipStream_t) {
+    return hipErrorNotSupported;
+}
+}  // namespace sydelta
