@@ -26,7 +26,6 @@
 
 #include "sydelta_internal.hpp"
 
-extern "C" uint32_t oracle_adler32(const uint8_t* data, uint64_t len);
 extern "C" uint64_t oracle_xxh3_64(const uint8_t* in, uint64_t len);
 
 // ---------------------------------------------------------------------------
@@ -117,6 +116,28 @@ hipError_t hipGetLastError() { return hipSuccess; }
 // ---------------------------------------------------------------------------
 // device layer
 // ---------------------------------------------------------------------------
+// Time spent inside the emulated launches, so a host profile can subtract it
+// (tools/host_profile.py): emu_kernel_ms(reset).
+#include <atomic>
+#include <chrono>
+static std::atomic<uint64_t> g_emu_ns{0};
+static thread_local int t_emu_depth = 0;
+struct EmuTimer {  // the outermost launch of a nest counts
+    std::chrono::steady_clock::time_point t0 = std::chrono::steady_clock::now();
+    EmuTimer() { ++t_emu_depth; }
+    ~EmuTimer() {
+        if (--t_emu_depth == 0)
+            g_emu_ns += (uint64_t)std::chrono::duration_cast<std::chrono::nanoseconds>(
+                            std::chrono::steady_clock::now() - t0)
+                            .count();
+    }
+};
+extern "C" double emu_kernel_ms(int reset) {
+    const double ms = g_emu_ns.load() / 1e6;
+    if (reset) g_emu_ns = 0;
+    return ms;
+}
+
 namespace sydelta {
 namespace {
 constexpr uint32_t kNone = 0xFFFFFFFFu;
@@ -128,7 +149,26 @@ struct Cand {
 };
 struct FakeIndex {
     std::vector<std::unordered_map<uint32_t, std::vector<Cand>>> files;  // weak -> candidates in index order
+    std::vector<uint64_t> any;  // 2^26-bit filter over (file, weak): a fast reject before the map
 };
+inline uint64_t any_bit(uint32_t file, uint32_t w) { return ((uint64_t)w * 0x9E3779B97F4A7C15ull + file * 0xC2B2AE3D27D4EB4Full) >> 38; }
+
+// Adler-32 (zlib), the modulus deferred over 5552-byte runs
+uint32_t adler(const uint8_t* p, uint64_t n) {
+    uint64_t a = 1, b = 0;
+    while (n) {
+        const uint64_t k = n < 5552 ? n : 5552;
+        for (uint64_t i = 0; i < k; ++i) {
+            a += p[i];
+            b += a;
+        }
+        a %= kMod;
+        b %= kMod;
+        p += k;
+        n -= k;
+    }
+    return (uint32_t)((b << 16) | a);
+}
 std::mutex g_mu;
 std::map<const void*, FakeIndex> g_ix;  // keyed by the index's `keys` array
 
@@ -139,6 +179,8 @@ const FakeIndex& find_ix(const DeviceIndex& ix) {
 
 // first candidate in index order with equal strong (generator.rs:127-133), or kNone
 uint32_t lookup(const FakeIndex& F, uint32_t file, uint32_t weak, const uint8_t* win, uint64_t n, bool* weak_hit) {
+    const uint64_t bit = any_bit(file, weak);
+    if (!((F.any[bit >> 6] >> (bit & 63)) & 1)) return kNone;
     const auto& m = F.files[file];
     auto it = m.find(weak);
     if (it == m.end()) return kNone;
@@ -180,10 +222,11 @@ void scan_range(const FakeIndex& F, uint32_t file, const uint8_t* src, uint64_t 
 
 hipError_t launch_signature(const uint8_t* d_buf, uint64_t len, uint64_t bs, uint32_t* d_weak, uint64_t* d_strong,
                             hipStream_t, Profiler*) {
+    EmuTimer emu_t;
     const uint64_t nb = (len + bs - 1) / bs;
     for (uint64_t k = 0; k < nb; ++k) {
         const uint64_t sz = std::min(bs, len - k * bs);
-        d_weak[k] = oracle_adler32(d_buf + k * bs, sz);
+        d_weak[k] = adler(d_buf + k * bs, sz);
         d_strong[k] = oracle_xxh3_64(d_buf + k * bs, sz);
     }
     return hipSuccess;
@@ -192,6 +235,7 @@ hipError_t launch_signature(const uint8_t* d_buf, uint64_t len, uint64_t bs, uin
 hipError_t launch_signature_batch(const uint8_t* d_buf, const uint64_t* d_off, const uint64_t* d_len,
                                   const uint64_t* d_fblk, uint64_t nfiles, uint64_t bs, uint64_t, uint32_t* d_weak,
                                   uint64_t* d_strong, hipStream_t s, Profiler* p) {
+    EmuTimer emu_t;
     for (uint64_t f = 0; f < nfiles; ++f)
         launch_signature(d_buf + d_off[f], d_len[f], bs, d_weak + d_fblk[f], d_strong + d_fblk[f], s, p);
     return hipSuccess;
@@ -201,14 +245,15 @@ hipError_t launch_signature_batch_fast(const uint8_t* d_buf, const uint64_t* d_a
                                        const uint64_t* d_apfx, uint64_t nact, uint64_t, const uint64_t* d_loff,
                                        const uint64_t* d_llen, const uint64_t* d_lidx, uint64_t npart, uint64_t bs,
                                        uint32_t* d_weak, uint64_t* d_strong, hipStream_t, Profiler*) {
+    EmuTimer emu_t;
     for (uint64_t f = 0; f < nact; ++f)
         for (uint64_t j = 0; j < d_apfx[f + 1] - d_apfx[f]; ++j) {
             const uint8_t* b = d_buf + d_aoff[f] + j * bs;
-            d_weak[d_agb[f] + j] = oracle_adler32(b, bs);
+            d_weak[d_agb[f] + j] = adler(b, bs);
             d_strong[d_agb[f] + j] = oracle_xxh3_64(b, bs);
         }
     for (uint64_t i = 0; i < npart; ++i) {
-        d_weak[d_lidx[i]] = oracle_adler32(d_buf + d_loff[i], d_llen[i]);
+        d_weak[d_lidx[i]] = adler(d_buf + d_loff[i], d_llen[i]);
         d_strong[d_lidx[i]] = oracle_xxh3_64(d_buf + d_loff[i], d_llen[i]);
     }
     return hipSuccess;
@@ -216,11 +261,16 @@ hipError_t launch_signature_batch_fast(const uint8_t* d_buf, const uint64_t* d_a
 
 hipError_t launch_index_build(const uint32_t* d_weak, const uint64_t* d_strong, DeviceIndex& ix, hipStream_t,
                               Profiler*) {
+    EmuTimer emu_t;
     FakeIndex F;
     F.files.resize(ix.nfiles);
+    F.any.assign((1ull << 26) / 64, 0);
     for (uint64_t f = 0; f < ix.nfiles; ++f)
-        for (uint64_t k = ix.d_fblk[f]; k < ix.d_fblk[f + 1]; ++k)
+        for (uint64_t k = ix.d_fblk[f]; k < ix.d_fblk[f + 1]; ++k) {
             F.files[f][d_weak[k]].push_back({(uint32_t)k, d_strong[k]});
+            const uint64_t bit = any_bit((uint32_t)f, d_weak[k]);
+            F.any[bit >> 6] |= 1ull << (bit & 63);
+        }
     std::lock_guard<std::mutex> lk(g_mu);
     g_ix[ix.keys] = std::move(F);
     return hipSuccess;
@@ -233,6 +283,7 @@ size_t scan_queue_entries() { return 1024; }
 hipError_t launch_scan(const uint8_t* d_buf, const ScanSeg* d_segs, uint32_t nsegs, uint32_t, uint32_t n,
                        const DeviceIndex& ix, const uint64_t*, uint64_t* d_hit_key, uint32_t* d_hit_val,
                        uint64_t out_cap, unsigned long long* d_counters, uint2*, size_t, hipStream_t, Profiler*) {
+    EmuTimer emu_t;
     const FakeIndex& F = find_ix(ix);
     for (uint32_t g = 0; g < nsegs; ++g) {
         const ScanSeg& S = d_segs[g];
@@ -246,6 +297,7 @@ hipError_t launch_scan_wide(const uint8_t* d_src, uint64_t, uint64_t pos_begin, 
                             uint32_t n, const DeviceIndex& ix, const uint64_t*, uint64_t* d_hit_key,
                             uint32_t* d_hit_val, uint64_t out_cap, unsigned long long* d_counters, hipStream_t,
                             Profiler*) {
+    EmuTimer emu_t;
     scan_range(find_ix(ix), 0, d_src, pos_begin, pos_end, n, (uint64_t)seg_id << kSegShift, d_hit_key, d_hit_val,
                out_cap, d_counters);
     return hipSuccess;
@@ -253,6 +305,7 @@ hipError_t launch_scan_wide(const uint8_t* d_src, uint64_t, uint64_t pos_begin, 
 
 hipError_t launch_sort_hits(uint64_t* key, uint32_t* val, uint64_t*, uint32_t*, uint64_t nhits, int, hipStream_t,
                             uint64_t** key_out, uint32_t** val_out) {
+    EmuTimer emu_t;
     std::vector<uint64_t> idx(nhits);
     std::iota(idx.begin(), idx.end(), 0);
     std::stable_sort(idx.begin(), idx.end(), [&](uint64_t x, uint64_t y) { return key[x] < key[y]; });
@@ -272,13 +325,14 @@ hipError_t launch_sort_hits(uint64_t* key, uint32_t* val, uint64_t*, uint32_t*, 
 hipError_t launch_probe(const uint8_t* d_base, const ProbeJob* d_jobs, uint32_t njobs, uint64_t nprobes,
                         uint32_t stride, uint32_t n, bool, const DeviceIndex& ix, uint32_t* d_pw, uint64_t* d_pst,
                         uint32_t* d_out, hipStream_t, Profiler*) {
+    EmuTimer emu_t;
     const FakeIndex& F = find_ix(ix);
     for (uint32_t j = 0; j < njobs; ++j) {
         const uint64_t end = j + 1 < njobs ? d_jobs[j + 1].pfx : nprobes;
         for (uint64_t w = d_jobs[j].pfx; w < end; ++w) {
             const uint64_t k = d_jobs[j].k0 + (w - d_jobs[j].pfx) * stride;
             const uint8_t* win = d_base + d_jobs[j].src + k * n;
-            const uint32_t wk = oracle_adler32(win, n);
+            const uint32_t wk = adler(win, n);
             d_pw[w] = wk;
             d_pst[w] = oracle_xxh3_64(win, n);
             d_out[w] = lookup(F, d_jobs[j].file, wk, win, n, nullptr);
@@ -289,16 +343,18 @@ hipError_t launch_probe(const uint8_t* d_base, const ProbeJob* d_jobs, uint32_t 
 
 hipError_t launch_tail(const uint8_t* d_buf, const TailJob* d_jobs, uint32_t njobs, const uint32_t* d_weak,
                        const uint64_t* d_strong, int* d_flag, hipStream_t) {
+    EmuTimer emu_t;
     for (uint32_t i = 0; i < njobs; ++i) {
         const uint8_t* p = d_buf + d_jobs[i].src;
         const uint64_t L = d_jobs[i].last_size, b = d_jobs[i].blk;
-        d_flag[i] = oracle_adler32(p, L) == d_weak[b] && oracle_xxh3_64(p, L) == d_strong[b];
+        d_flag[i] = adler(p, L) == d_weak[b] && oracle_xxh3_64(p, L) == d_strong[b];
     }
     return hipSuccess;
 }
 
 hipError_t launch_apply(const ApplyPiece* d_pieces, uint64_t npieces, const uint8_t* d_basis, const uint8_t* d_lit,
                         uint8_t* d_out, hipStream_t, Profiler*) {
+    EmuTimer emu_t;
     for (uint64_t i = 0; i < npieces; ++i) {
         const ApplyPiece& p = d_pieces[i];
         memcpy(d_out + p.dst, (p.from_basis ? d_basis : d_lit) + p.src, p.len);
@@ -307,13 +363,16 @@ hipError_t launch_apply(const ApplyPiece* d_pieces, uint64_t npieces, const uint
 }
 
 hipError_t launch_json_len(const JsonPiece*, uint64_t, const uint8_t*, uint64_t*, hipStream_t, Profiler*) {
+    EmuTimer emu_t;
     return hipErrorNotSupported;
 }
 hipError_t launch_json_write(const JsonPiece*, uint64_t, const uint8_t*, const uint64_t*, uint64_t, uint8_t*,
                              hipStream_t, Profiler*) {
+    EmuTimer emu_t;
     return hipErrorNotSupported;
 }
 hipError_t launch_exclusive_sum_u64(const uint64_t* d_in, uint64_t* d_out, uint64_t n, hipStream_t) {
+    EmuTimer emu_t;
     uint64_t acc = 0;
     for (uint64_t i = 0; i < n; ++i) {
         const uint64_t v = d_in[i];
@@ -325,6 +384,7 @@ hipError_t launch_exclusive_sum_u64(const uint64_t* d_in, uint64_t* d_out, uint6
 
 hipError_t launch_block_cmp(const uint8_t* d_src, uint64_t slen, const uint8_t* d_dst, uint64_t dlen, uint64_t bs,
                             uint8_t* d_changed, hipStream_t, Profiler*) {
+    EmuTimer emu_t;
     const uint64_t nb = (slen + bs - 1) / bs;
     for (uint64_t k = 0; k < nb; ++k) {
         const uint64_t o = k * bs, sl = std::min(bs, slen - o), dl = dlen > o ? std::min(bs, dlen - o) : 0;
@@ -335,6 +395,7 @@ hipError_t launch_block_cmp(const uint8_t* d_src, uint64_t slen, const uint8_t* 
 
 hipError_t launch_hash_blocks(const uint8_t* d_buf, uint64_t len, uint64_t bs, const uint64_t* d_pos, uint32_t count,
                               uint64_t* d_out, hipStream_t) {
+    EmuTimer emu_t;
     for (uint32_t i = 0; i < count; ++i) {
         const uint64_t o = d_pos[i] * bs;
         d_out[i] = oracle_xxh3_64(d_buf + o, o < len ? std::min(bs, len - o) : 0);
@@ -345,15 +406,19 @@ hipError_t launch_hash_blocks(const uint8_t* d_buf, uint64_t len, uint64_t bs, c
 hipError_t launch_xxh_files(const uint8_t* d_buf, const uint64_t* d_off, const uint64_t* d_len, const uint64_t*,
                             const uint64_t*, const uint64_t*, uint64_t, const uint32_t*, uint64_t nfiles, uint64_t,
                             uint64_t*, uint64_t* d_out, hipStream_t, Profiler*) {
+    EmuTimer emu_t;
     for (uint64_t f = 0; f < nfiles; ++f) d_out[f] = oracle_xxh3_64(d_buf + d_off[f], d_len[f]);
     return hipSuccess;
 }
 
-hipError_t launch_synth_fill(uint8_t*, uint64_t, uint64_t, hipStream_t, uint64_t) { return hipErrorNotSupported; }
+hipError_t launch_synth_fill(uint8_t*, uint64_t, uint64_t, hipStream_t, uint64_t) {
+    EmuTimer emu_t; return hipErrorNotSupported; }
 hipError_t launch_synth_edit_blocks(uint8_t*, uint64_t, uint64_t, uint64_t, uint64_t, uint32_t, hipStream_t) {
+    EmuTimer emu_t;
     return hipErrorNotSupported;
 }
 hipError_t launch_synth_mutate(uint8_t*, const uint8_t*, uint64_t, uint64_t, uint32_t, hipStream_t) {
+    EmuTimer emu_t;
     return hipErrorNotSupported;
 }
 }  // namespace sydelta
