@@ -8,7 +8,9 @@ Covers what the GPU tests cover for the host side: the streamed path API over ma
 chunks (compute_checksums, generate_delta_streaming, bs up to 128 KiB), the in-memory
 generator, tiny and empty files, the probe + on-demand scan walk (SYDELTA_PROBE=1),
 the split walk (SYDELTA_WALK_PAR_MIN=1), the path-level change ratio on ratio.rs's
-cases, and 10 threads calling the path API at once.
+cases, 10 threads calling the path API at once, the batched device-pointer path (80
+files incl. empty and sub-block ones, threaded walks) and a file matched in 1/2/3/8
+chained chunks.
 """
 import os
 import sys
@@ -144,7 +146,139 @@ def main():
         with ThreadPoolExecutor(10) as ex:
             assert all(ex.map(one, range(10)))
         n_checks += 10
+        n_checks += batch_and_chunk_checks()
     print(f"emulated host checks ok: {n_checks}")
+
+
+def _ops(lib, h):
+    import ctypes
+
+    n = lib.sydelta_delta_num_ops(h)
+    if not n:
+        return []
+    p = lib.sydelta_delta_ops(h)
+    raw = np.frombuffer((ctypes.c_uint8 * (24 * n)).from_address(ctypes.addressof(p.contents)),
+                        dtype=np.dtype([("kind", "<u4"), ("r", "<u4"), ("a", "<u8"), ("b", "<u8")]))
+    return [("C" if int(k) == 0 else "D", int(x), int(y)) for k, x, y in zip(raw["kind"], raw["a"], raw["b"])]
+
+
+def batch_and_chunk_checks():
+    """The device-pointer entry points on host memory: batched signature + index + match
+    (the C4 path, threaded walks at >= 64 files) and a file matched in 1/2/3/8 chained
+    chunks (the C5 path), each against the oracle."""
+    import ctypes
+
+    from sy_amd._lib import check, lib
+
+    vp = lambda a: ctypes.c_void_p(a.ctypes.data)
+    rng = np.random.default_rng(77)
+    n_checks = 0
+    for bs in (1024, 4096):
+        for probe in ("0", "1", "auto"):
+            if probe == "auto":
+                os.environ.pop("SYDELTA_PROBE", None)
+            else:
+                os.environ["SYDELTA_PROBE"] = probe
+            nf = 80
+            bases, srcs = [], []
+            for k in range(nf):
+                size = [0, 100, bs - 1, bs, int(rng.integers(bs, 40 * bs))][k % 5]
+                b = O.synth_bytes(size, 0x600 + k)
+                s2 = b.copy()
+                if size > 10:
+                    p = int(rng.integers(0, size))
+                    s2 = np.concatenate([s2[:p], np.frombuffer(b"Z", np.uint8), s2[p:]])
+                    for q in rng.integers(0, s2.size, 3):
+                        s2[q] ^= 0x11
+                bases.append(b)
+                srcs.append(s2)
+
+            def pack(parts):
+                offs, cur = [], 0
+                for x in parts:
+                    offs.append(cur)
+                    cur += (x.size + 15) // 16 * 16 + 16
+                buf = np.zeros(cur + 16, np.uint8)
+                for o, x in zip(offs, parts):
+                    buf[o:o + x.size] = x
+                return buf, np.array(offs, np.uint64), np.array([x.size for x in parts], np.uint64)
+
+            bbuf, boff, blen = pack(bases)
+            sbuf, soff, slen = pack(srcs)
+            nblk = (blen + bs - 1) // bs
+            tot = int(nblk.sum())
+            w = np.zeros(max(tot, 1), np.uint32)
+            st = np.zeros(max(tot, 1), np.uint64)
+            check(lib.sydelta_signature_batch_device(0, vp(bbuf), vp(boff), vp(blen), nf, bs, vp(w), vp(st), None))
+            fb = np.concatenate([[0], np.cumsum(nblk)]).astype(np.int64)
+            last = np.where(nblk > 0, blen - (nblk - 1) * bs, 0).astype(np.uint64)
+            ix = ctypes.c_void_p()
+            check(lib.sydelta_index_create_batch(0, vp(w), vp(st), vp(nblk.astype(np.uint64)), vp(last), nf, bs, 1,
+                                                 None, ctypes.byref(ix)))
+            bt = ctypes.c_void_p()
+            check(lib.sydelta_match_batch_device(ix, vp(sbuf), vp(soff), vp(slen), nf, None, ctypes.byref(bt)))
+            for k in range(nf):
+                ew, es, ez = C.compute_checksums(bases[k], bs)
+                assert np.array_equal(w[fb[k]:fb[k + 1]], ew) and np.array_equal(st[fb[k]:fb[k + 1]], es), (bs, k)
+                exp = O.ops_from_arrays(*C.generate_delta(srcs[k], ew, es, ez, bs))
+                got = _ops(lib, lib.sydelta_delta_batch_get(bt, k))
+                assert got == exp, ("batch", bs, probe, k)
+                n_checks += 1
+            lib.sydelta_delta_batch_free(bt)
+            lib.sydelta_index_free(ix)
+    os.environ.pop("SYDELTA_PROBE", None)
+    # chunked: one file in 1/2/3/8 chunks, walks chained in order, parts appended
+    for bs in (512, 4096):
+        basis = O.synth_bytes(300 * bs + 77, 0x700)
+        s2 = np.concatenate([basis[:10 * bs], np.frombuffer(b"Q", np.uint8), basis[10 * bs:150 * bs],
+                             basis[200 * bs:]])
+        for q in rng.integers(0, s2.size, 20):
+            s2[q] ^= 0x22
+        L = s2.size
+        sb = np.zeros(L + 32, np.uint8)
+        sb[:L] = s2
+        nb = -(-basis.size // bs)
+        w = np.zeros(nb, np.uint32)
+        st = np.zeros(nb, np.uint64)
+        bb = np.zeros(basis.size + 16, np.uint8)
+        bb[:basis.size] = basis
+        check(lib.sydelta_signature_device(0, vp(bb), basis.size, bs, vp(w), vp(st), None))
+        ix = ctypes.c_void_p()
+        check(lib.sydelta_index_create(0, vp(w), vp(st), nb, bs, basis.size - (nb - 1) * bs, 1, None,
+                                       ctypes.byref(ix)))
+        ew, es, ez = C.compute_checksums(basis, bs)
+        exp = O.ops_from_arrays(*C.generate_delta(s2, ew, es, ez, bs))
+        npos = L - bs + 1
+        nbp = -(-npos // bs)
+        for nch in (1, 2, 3, 8):
+            for probe in ("0", "1"):
+                os.environ["SYDELTA_PROBE"] = probe
+                cuts = sorted(set(int(c) for c in rng.choice(np.arange(1, nbp), nch - 1, replace=False))) if nch > 1 \
+                    else []
+                bounds = [0] + [c * bs for c in cuts] + [npos]
+                acc = lib.sydelta_delta_new(L, bs)
+                entry = 0
+                for g in range(len(bounds) - 1):
+                    p0, p1 = bounds[g], bounds[g + 1]
+                    final = g == len(bounds) - 2
+                    bpos = p0 & ~15
+                    end = L if final else min(L, p1 + bs - 1)
+                    ch = ctypes.c_void_p()
+                    check(lib.sydelta_chunk_classify(ix, ctypes.c_void_p(sb.ctypes.data + bpos), bpos, end - bpos, L,
+                                                     p0, max(p1, L) if final else p1, None, ctypes.byref(ch)))
+                    d = ctypes.c_void_p()
+                    ex = ctypes.c_uint64()
+                    check(lib.sydelta_chunk_walk(ch, entry, ctypes.byref(ex), ctypes.byref(d)))
+                    check(lib.sydelta_delta_append(acc, d))
+                    lib.sydelta_delta_free(d)
+                    lib.sydelta_chunk_free(ch)
+                    entry = ex.value
+                assert _ops(lib, acc) == exp, ("chunks", bs, nch, probe)
+                lib.sydelta_delta_free(acc)
+                n_checks += 1
+        lib.sydelta_index_free(ix)
+    os.environ.pop("SYDELTA_PROBE", None)
+    return n_checks
 
 
 if __name__ == "__main__":
