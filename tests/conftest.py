@@ -11,6 +11,13 @@ if ROOT not in sys.path:
 def pytest_configure(config):
     config.addinivalue_line("markers", "gpu: needs a real MI355X (gfx950) GPU")
     config.addinivalue_line("markers", "slow: long-running parity case")
+    config.addinivalue_line("markers", "late: depends on the box's environment (child processes, GiB of temp "
+                                       "files); runs after everything else so an environment failure under -x "
+                                       "does not hide the parity tests")
+
+
+def pytest_collection_modifyitems(config, items):
+    items.sort(key=lambda it: it.get_closest_marker("late") is not None)  # stable: order otherwise unchanged
 
 
 @pytest.fixture(scope="session")

@@ -20,7 +20,7 @@ import traceback
 import numpy as np
 import pytest
 
-pytestmark = pytest.mark.gpu
+pytestmark = [pytest.mark.gpu, pytest.mark.late]
 
 BS5 = 8192
 CHUNK = 4 << 20  # C5 basis bytes per rank

@@ -102,6 +102,7 @@ print(n.value, lib.sydelta_delta_num_ops(h), st.copy_ops, st.data_ops, st.litera
 """
 
 
+@pytest.mark.late
 def test_streamed_path_bounded_rss(tmp_path, gpu):
     import shutil
 
