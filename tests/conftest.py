@@ -11,9 +11,9 @@ if ROOT not in sys.path:
 def pytest_configure(config):
     config.addinivalue_line("markers", "gpu: needs a real MI355X (gfx950) GPU")
     config.addinivalue_line("markers", "slow: long-running parity case")
-    config.addinivalue_line("markers", "late: depends on the box's environment (child processes, GiB of temp "
-                                       "files); runs after everything else so an environment failure under -x "
-                                       "does not hide the parity tests")
+    config.addinivalue_line("markers", "late: host-side machinery around the kernels (child processes, "
+                                       "concurrent callers, streamed files, GiB of temp files); runs after the "
+                                       "kernel parity tests so that a failure there under -x does not hide them")
 
 
 def pytest_collection_modifyitems(config, items):

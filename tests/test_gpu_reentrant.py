@@ -19,7 +19,7 @@ import pytest
 
 from oracle import oracle as O
 
-pytestmark = pytest.mark.gpu
+pytestmark = [pytest.mark.gpu, pytest.mark.late]
 
 NT = 10
 

@@ -20,7 +20,7 @@ import pytest
 
 from oracle import oracle as O
 
-pytestmark = pytest.mark.gpu
+pytestmark = [pytest.mark.gpu, pytest.mark.late]
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
@@ -102,7 +102,6 @@ print(n.value, lib.sydelta_delta_num_ops(h), st.copy_ops, st.data_ops, st.litera
 """
 
 
-@pytest.mark.late
 def test_streamed_path_bounded_rss(tmp_path, gpu):
     import shutil
 
