@@ -154,6 +154,7 @@ def test_change_ratio_paths_reference_tests(name, tmp_path):
         assert not r.use_delta
 
 
+@pytest.mark.late
 def test_change_ratio_paths_large_sample(tmp_path, gpu):
     """More samples than one 64 MiB batch: 300 MiB files, 64 KiB blocks, every block
     sampled, edits in 37 of them."""
