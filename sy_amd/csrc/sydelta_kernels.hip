@@ -2752,12 +2752,11 @@ hipError_t launch_scan(const uint8_t* d_buf, const ScanSeg* d_segs, uint32_t nse
     static hipError_t l1_err = hipSuccess;
     static int l1_cus = 256;
     const Lds3 L3 = lds3_layout(n);
-    // k_scan_l1 takes the windows its measured and parity-tested configuration covers:
-    // n a multiple of 2048 (whole wave columns of 32-byte halves, the row-parallel
-    // verification) up to kMaxN3, i.e. 2048 and 4096 (the C3 shape).  Other sizes with
-    // a large index go to k_scan_lds (production block sizes for files with more than
+    // k_scan_l1 takes the window size its measured and parity-tested configuration
+    // covers, n = 4096 (the C3 shape; tests/test_gpu_scan_large.py).  Other sizes with a
+    // large index go to k_scan_lds (production block sizes for files with more than
     // 16 Ki blocks are >= 8 KiB anyway: bs = sqrt(file size)).
-    if (ix.l1 && n <= kMaxN3 && n % 2048 == 0 && scan_l1_enabled()) {
+    if (ix.l1 && n == kMaxN3 && scan_l1_enabled()) {
         std::call_once(l1_once, [] {
             l1_err = hipFuncSetAttribute((const void*)k_scan_l1, hipFuncAttributeMaxDynamicSharedMemorySize,
                                          160 * 1024 - 256);
