@@ -411,7 +411,7 @@ static int index_create_impl(int device, const uint32_t* weak, const uint64_t* s
     const size_t sz_order = al(4 * nb), sz_slot = al(4 * nb), sz_files = al(sizeof(FileIx) * nfiles);
     const size_t sz_fblk = al(8 * (nfiles + 1)), sz_cstrong = al(8 * nb);
     // level-1 filter for k_scan_l1: one large file (the BASELINE C3 shape)
-    const bool want_l1 = nfiles == 1 && nblocks > kLdsFilterKeys;
+    const bool want_l1 = nfiles == 1 && nblocks > kLdsFilterKeys && block_size == 4096;  // k_scan_l1's scope
     const size_t sz_l1 = want_l1 ? al(4 * (size_t)kL1Words) : 0;
     const size_t sz_fat = want_l1 ? al(16 * (size_t)sl) : 0;
     const size_t total = sz_weak + sz_strong + sz_filt + sz_l1 + sz_fat + 4 * sz_t + sz_order + sz_slot + sz_files +
