@@ -147,7 +147,41 @@ def main():
             assert all(ex.map(one, range(10)))
         n_checks += 10
         n_checks += batch_and_chunk_checks()
+        n_checks += error_checks(tmp)
     print(f"emulated host checks ok: {n_checks}")
+
+
+def error_checks(tmp):
+    """I/O errors surface as SYDELTA_E_IO with the path in the message, as io::Error
+    would: missing files, a directory, a checksum list not in compute_checksums layout."""
+    from sy_amd._lib import SyDeltaError, SYDELTA_E_IO, SYDELTA_E_INVAL
+
+    n = 0
+    missing = os.path.join(tmp, "no_such_file")
+    for fn in (lambda: D.compute_checksums(missing, 4096),
+               lambda: D.generate_delta_streaming(missing, [], 4096),
+               lambda: D.generate_delta(missing, [], 4096),
+               lambda: D.compute_checksums(tmp, 4096),
+               lambda: D.generate_delta_streaming(tmp, [], 4096)):
+        try:
+            fn()
+        except SyDeltaError as e:
+            assert e.code == SYDELTA_E_IO, e
+            n += 1
+        else:
+            raise AssertionError("no error")
+    p = os.path.join(tmp, "small")
+    O.synth_bytes(10000, 3).tofile(p)
+    sigs = D.compute_checksums(p, 4096)
+    bad = [D.BlockChecksum(s.index, s.offset + 1, s.size, s.weak, s.strong) for s in sigs]
+    try:
+        D.generate_delta_streaming(p, bad, 4096)
+    except SyDeltaError as e:
+        assert e.code == SYDELTA_E_INVAL, e
+        n += 1
+    else:
+        raise AssertionError("layout not checked")
+    return n
 
 
 def _ops(lib, h):
