@@ -94,6 +94,17 @@ int ensure_device_impl(int device) {
             st->msg = std::string("device is ") + prop.gcnArchName + ", libsydelta is built for gfx950 only";
             return;
         }
+        // Scratch (index arrays, hit lists, probe jobs, streamed chunks) comes from the
+        // device's stream-ordered pool.  Its default release threshold is 0: every stream
+        // synchronization hands the freed memory back and the next call maps it again.
+        // Keep up to SYDELTA_POOL_KEEP_MIB (default 4 GiB) reserved across calls.
+        hipMemPool_t pool = nullptr;
+        if (hipDeviceGetDefaultMemPool(&pool, device) == hipSuccess && pool) {
+            uint64_t keep = 4096;
+            if (const char* e = getenv("SYDELTA_POOL_KEEP_MIB")) keep = strtoull(e, nullptr, 10);
+            keep <<= 20;
+            (void)hipMemPoolSetAttribute(pool, hipMemPoolAttrReleaseThreshold, &keep);
+        }
         st->status = SYDELTA_OK;
     });
     if (st->status != SYDELTA_OK) return fail(st->status, "%s", st->msg.c_str());

@@ -78,6 +78,7 @@ hipError_t hipEventDestroy(hipEvent_t e) {
     delete e;
     return hipSuccess;
 }
+static int emu_pool_tag;
 static void* emu_alloc(size_t n) {
     void* p = nullptr;
     if (posix_memalign(&p, 256, n ? n : 1)) return nullptr;
@@ -88,6 +89,12 @@ hipError_t hipMallocAsync(void** p, size_t n, hipStream_t) {
     return *p ? hipSuccess : hipErrorOutOfMemory;
 }
 hipError_t hipMalloc(void** p, size_t n) { return hipMallocAsync(p, n, nullptr); }
+hipError_t hipDeviceGetDefaultMemPool(hipMemPool_t* p, int d) {
+    if (d != 0) return hipErrorInvalidDevice;
+    *p = (hipMemPool_t)&emu_pool_tag;
+    return hipSuccess;
+}
+hipError_t hipMemPoolSetAttribute(hipMemPool_t, hipMemPoolAttr, void*) { return hipSuccess; }
 hipError_t hipFreeAsync(void* p, hipStream_t) {
     free(p);
     return hipSuccess;
