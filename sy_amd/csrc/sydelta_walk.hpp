@@ -148,6 +148,9 @@ inline int walk_src(const Src& c, uint64_t n, uint64_t entry, uint64_t end, cons
     uint64_t kp = c.kb;  // next block whose phase-probed window may hit
     const bool has_phase = c.probed && !c.ppos.empty();
     while (x < end) {
+        // aligned windows before x are behind the walk (after a Copy of block k found
+        // below, x = (k+1)*n: ka catches up here, so the run fast path resumes)
+        if (c.probed && ka * n < x) ka = (x + n - 1) / n;
         if (c.probed && x == lit && ka < kend && ka * n == x) {
             // a run of aligned Copies (the rsync case): at an aligned x whose aligned window
             // hit, that window is the earliest hit (a scan hit at x names the same block,
@@ -178,7 +181,6 @@ inline int walk_src(const Src& c, uint64_t n, uint64_t entry, uint64_t end, cons
         uint32_t pb = kNoBlk;
         if (i < H && c.hpos[i] < end) { p = c.hpos[i]; pb = c.hblk[i]; }
         if (c.probed) {
-            if (ka * n < x) ka = (x + n - 1) / n;  // after an aligned Copy x == (ka+1)*n: no division
             while (ka < kend && ka * n < p && c.ahit[ka - c.kb] == kNoBlk) ++ka;
             if (ka < kend && ka * n < p) { p = ka * n; pb = c.ahit[ka - c.kb]; }
             if (has_phase) {  // phase-probed hits (one window per block, inside it)

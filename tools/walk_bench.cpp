@@ -2,6 +2,7 @@
 // one 8 GiB chunk at bs 8192 = 1 Mi blocks, aligned probe hits on 99 % of them, the 1 %
 // edited blocks scanned (no hit inside).  Not product code; CPU only.
 //   g++ -O3 -std=c++17 -I include -I sy_amd/csrc tools/walk_bench.cpp -o build/walk_bench -lpthread
+#include <algorithm>
 #include <chrono>
 #include <random>
 #include <stdio.h>
@@ -11,13 +12,16 @@
 
 using namespace sydelta::walk;
 
-struct Pool {  // recycles arrays across repetitions, as the library's op pool does
+struct Pool {  // recycles arrays across repetitions, best fit like the library's take_ops
     std::vector<OpVec> v;
     OpVec take(size_t want) {
+        size_t best = v.size();
+        for (size_t i = 0; i < v.size(); ++i)
+            if (v[i].capacity() >= want && (best == v.size() || v[i].capacity() < v[best].capacity())) best = i;
         OpVec o;
-        if (!v.empty()) {
-            o.swap(v.back());
-            v.pop_back();
+        if (best < v.size()) {
+            o.swap(v[best]);
+            v.erase(v.begin() + best);
         }
         o.clear();
         o.reserve(want);
@@ -48,7 +52,9 @@ int main(int argc, char** argv) {
     const BasisInfo bi{0, nblk, n};
     Pool pool;
     OpVec ops, sops;
-    for (int rep = 0; rep < 5; ++rep) {
+    const int reps = argc > 2 ? atoi(argv[2]) : 5;
+    std::vector<double> tser, tsplit;
+    for (int rep = 0; rep < reps; ++rep) {
         ops.clear();
         ops.reserve(2 * nblk);
         uint64_t exit = 0, need = 0;
@@ -69,9 +75,16 @@ int main(int argc, char** argv) {
         bool same = sops.size() == ops.size();
         for (size_t i = 0; same && i < ops.size(); ++i)
             same = ops[i].kind == sops[i].kind && ops[i].a == sops[i].a && ops[i].b == sops[i].b;
-        printf("serial walk %.3f ms (%zu ops, rc %d)  split walk over %d segments %.3f ms (rc %d, %s): walk %.3f "
+        if (rep) { tser.push_back(ms); tsplit.push_back(ms2); }
+        if (reps <= 5) printf("serial walk %.3f ms (%zu ops, rc %d)  split walk over %d segments %.3f ms (rc %d, %s): walk %.3f "
                "(segments %.3f-%.3f) chain %.3f join %.3f\n", ms, ops.size(), r, T, ms2, r2,
                same ? "same ops" : "DIFFERENT", tm.walk_ms, tm.seg_min_ms, tm.seg_max_ms, tm.chain_ms, tm.join_ms);
+    }
+    if (!tser.empty()) {
+        std::sort(tser.begin(), tser.end());
+        std::sort(tsplit.begin(), tsplit.end());
+        printf("median of %zu: serial %.3f ms, split over %d segments %.3f ms\n", tser.size(), tser[tser.size() / 2],
+               T, tsplit[tsplit.size() / 2]);
     }
     return 0;
 }
