@@ -877,7 +877,7 @@ int Classifier::scan(const std::vector<std::array<uint64_t, 3>>& ranges) {
     } else {
         merge_range(0, nver);
     }
-    if (host_timing && src.size() > 1)
+    if (host_timing)
         fprintf(stderr, "sydelta scan: %zu segments, %llu hits: setup+kernel %.3f ms, sort+D2H %.3f ms, merge %.3f ms\n",
                 segs.size(), (unsigned long long)nver, t_kern, t_d2h - t_kern, ms_since(t0) - t_d2h);
     return SYDELTA_OK;

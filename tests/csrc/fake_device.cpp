@@ -18,6 +18,8 @@
 #include <string.h>
 
 #include <algorithm>
+#include <atomic>
+#include <chrono>
 #include <map>
 #include <mutex>
 #include <numeric>
@@ -79,11 +81,28 @@ hipError_t hipEventDestroy(hipEvent_t e) {
     return hipSuccess;
 }
 static int emu_pool_tag;
+// Host profiles (tools/host_profile.py sets EMU_PROFILE=1): copies and memsets count as
+// device time (DMA engines on the GPU), so memmoves a GPU run would not have on the host
+// stay out of the host column.
+static bool emu_profile() {
+    static const bool on = [] { const char* e = getenv("EMU_PROFILE"); return e && e[0] == '1'; }();
+    return on;
+}
 static void* emu_alloc(size_t n) {
     void* p = nullptr;
     if (posix_memalign(&p, 256, n ? n : 1)) return nullptr;
     return p;
 }
+static void emu_free(void* p) { free(p); }
+static void emu_copy_time(uint64_t ns);
+struct EmuCopyTimer {
+    std::chrono::steady_clock::time_point t0 = std::chrono::steady_clock::now();
+    ~EmuCopyTimer() {
+        if (emu_profile())
+            emu_copy_time((uint64_t)std::chrono::duration_cast<std::chrono::nanoseconds>(
+                              std::chrono::steady_clock::now() - t0).count());
+    }
+};
 hipError_t hipMallocAsync(void** p, size_t n, hipStream_t) {
     *p = emu_alloc(n);
     return *p ? hipSuccess : hipErrorOutOfMemory;
@@ -96,24 +115,26 @@ hipError_t hipDeviceGetDefaultMemPool(hipMemPool_t* p, int d) {
 }
 hipError_t hipMemPoolSetAttribute(hipMemPool_t, hipMemPoolAttr, void*) { return hipSuccess; }
 hipError_t hipFreeAsync(void* p, hipStream_t) {
-    free(p);
+    emu_free(p);
     return hipSuccess;
 }
 hipError_t hipFree(void* p) {
-    free(p);
+    emu_free(p);
     return hipSuccess;
 }
 hipError_t hipHostMalloc(void** p, size_t n, unsigned int) { return hipMallocAsync(p, n, nullptr); }
 hipError_t hipHostFree(void* p) {
-    free(p);
+    emu_free(p);
     return hipSuccess;
 }
 hipError_t hipMemcpyAsync(void* d, const void* s, size_t n, hipMemcpyKind, hipStream_t) {
+    EmuCopyTimer t;
     if (n) memmove(d, s, n);
     return hipSuccess;
 }
 hipError_t hipMemcpy(void* d, const void* s, size_t n, hipMemcpyKind k) { return hipMemcpyAsync(d, s, n, k, nullptr); }
 hipError_t hipMemsetAsync(void* d, int v, size_t n, hipStream_t) {
+    EmuCopyTimer t;
     memset(d, v, n);
     return hipSuccess;
 }
@@ -125,10 +146,11 @@ hipError_t hipGetLastError() { return hipSuccess; }
 // ---------------------------------------------------------------------------
 // Time spent inside the emulated launches, so a host profile can subtract it
 // (tools/host_profile.py): emu_kernel_ms(reset).
-#include <atomic>
-#include <chrono>
 static std::atomic<uint64_t> g_emu_ns{0};
 static thread_local int t_emu_depth = 0;
+static void emu_copy_time(uint64_t ns) {
+    if (t_emu_depth == 0) g_emu_ns += ns;  // inside an emulated launch it is counted already
+}
 struct EmuTimer {  // the outermost launch of a nest counts
     std::chrono::steady_clock::time_point t0 = std::chrono::steady_clock::now();
     EmuTimer() { ++t_emu_depth; }

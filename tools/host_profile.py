@@ -23,6 +23,7 @@ sys.path.insert(0, os.path.join(ROOT, "tests"))
 
 
 def load():
+    os.environ.setdefault("EMU_PROFILE", "1")  # copies count as device time (fake_device.cpp)
     import test_host_emulated as T
 
     lib = ctypes.CDLL(T._build())
