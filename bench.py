@@ -79,6 +79,10 @@ def parse():
     ap.add_argument("--files", type=int, default=None,
                     help="c4: total 1 MiB files over all ranks (10000); xxh3: files per rank (4096; 1 = one file of "
                          "--size-gib)")
+    ap.add_argument("--callers", type=int, default=1,
+                    help="c4: split this rank's files over K host threads, each one batched call on its own "
+                         "library stream (sy runs up to 10 transfers at once, cli.rs:178-180), so one call's "
+                         "host work overlaps another's kernels")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-host-inclusive", action="store_true")
     a = ap.parse_args()
@@ -596,6 +600,31 @@ def main():
     torch.cuda.synchronize()
     stream = torch.cuda.current_stream()
 
+    def c4_batch(fs, strm):
+        """One batched call over files fs = (boff, blen, soff, slen); strm None = the
+        calling thread's library stream (each call then synchronizes before returning)."""
+        boff, blen, soff, slen = fs
+        w, s = dev.signature_batch(basis, boff, blen, bs, stream=strm)
+        nblk = (blen + bs - 1) // bs
+        last = blen - (nblk - 1) * bs
+        idx = dev.BatchIndex(w, s, nblk, last, bs, device=local, stream=strm)
+        # the per-file op lists stay in the library's batch (host memory), as the
+        # Rust caller would read them through the accessors
+        res = dev.match_batch_handle(idx, new, soff, slen, stream=strm)
+        idx.close()
+        tot = res.stats
+        res.close()
+        return tot
+
+    c4_pool, c4_groups = None, []
+    if args.workload == "c4" and args.callers > 1:
+        from concurrent.futures import ThreadPoolExecutor
+
+        nf = len(files[0])
+        c4_groups = [shard_range(nf, args.callers, g) for g in range(args.callers)]
+        c4_groups = [g for g in c4_groups if g[1] > g[0]]
+        c4_pool = ThreadPoolExecutor(len(c4_groups))
+
     def step():
         if args.workload == "path":
             sig = ctypes.POINTER(_lib.BlockChecksumC)()
@@ -655,18 +684,10 @@ def main():
             idx.close()
             return d
         # c4: batched signature of all basis files, per-file index, one batched match
-        boff, blen, soff, slen = files
-        w, s = dev.signature_batch(basis, boff, blen, bs, stream=stream)
-        nblk = (blen + bs - 1) // bs
-        last = blen - (nblk - 1) * bs
-        idx = dev.BatchIndex(w, s, nblk, last, bs, device=local, stream=stream)
-        # the per-file op lists stay in the library's batch (host memory), as the
-        # Rust caller would read them through the accessors
-        res = dev.match_batch_handle(idx, new, soff, slen, stream=stream)
-        idx.close()
-        tot = res.stats
-        res.close()
-        return tot
+        if c4_pool is None:
+            return c4_batch(files, stream)
+        parts = list(c4_pool.map(lambda g: c4_batch(tuple(x[g[0]:g[1]] for x in files), None), c4_groups))
+        return {k: sum(p[k] for p in parts) for k in parts[0]}
 
     for _ in range(args.warmup):
         step()
@@ -783,7 +804,8 @@ def main():
                 "parallelism": (f"chunk-sharded x{world} (RCCL all-gather of the signature, chained walks)"
                                 if args.workload == "c5" else
                                 f"file-sharded x{world} (independent pairs per rank, no collective)"),
-                **({"files": args.files, "files_this_rank": len(files[0])} if args.workload == "c4" else {}),
+                **({"files": args.files, "files_this_rank": len(files[0]), "callers_per_rank": max(1, len(c4_groups))}
+                   if args.workload == "c4" else {}),
             },
             "pct_hbm_peak": round(value * GIB / 1e9 / HBM_PEAK_GBS * 100, 2),
             "roofline": roof,
