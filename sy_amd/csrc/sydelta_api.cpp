@@ -628,6 +628,9 @@ struct Classifier {
     uint64_t weak_hits = 0;
     DevBuf q_buf;
     size_t qcap = 0;
+    // probed sources: their runs of blocks whose aligned window missed, [first, end)
+    // local blocks, ascending (set by probe)
+    std::vector<std::vector<std::array<uint64_t, 2>>> miss_runs;
 
     // Aligned probe of every block of every source (mode 1), of none (0), or, in
     // auto mode (-1), when a 1-in-16 sample finds >= 1/8 of its windows hitting.
@@ -715,20 +718,63 @@ int Classifier::probe(int mode) {
         if (hits * 8 < nout) return SYDELTA_OK;
     }
     if (int r = run(1, pfx)) return r;
-    auto fill = [&](size_t i0, size_t i1) {
-        for (size_t i = i0; i < i1; ++i) {
-            Src& c = src[i];
-            c.probed = true;
-            c.ahit.assign(out + pfx[i], out + pfx[i + 1]);
-            c.scanned.assign(c.nblk, 0);
-            c.nahit = 0;
-            for (uint32_t v : c.ahit) c.nahit += v != kNoBlk;
-        }
-    };
+    // Copy the results into the sources and find their miss runs (the blocks classify
+    // scans) in one pass, in pieces of 64 Ki blocks on the host pool: one large source
+    // (C5) is split as well as many small ones (C4).
     const size_t ns = src.size();
-    const int nthr = ns >= 256 ? walk_threads() : 1;
-    if (!run_parallel(nthr, [&](int t) { fill(ns * t / nthr, ns * (t + 1) / nthr); }))
+    constexpr uint64_t kPiece = 1 << 16;
+    struct Piece {
+        size_t si;
+        uint64_t b0, b1;  // local blocks
+    };
+    std::vector<Piece> pieces;
+    for (size_t i = 0; i < ns; ++i) {
+        Src& c = src[i];
+        c.probed = true;
+        c.ahit.resize(c.nblk);
+        c.scanned.assign(c.nblk, 0);
+        for (uint64_t b = 0; b < c.nblk; b += kPiece) pieces.push_back({i, b, std::min(c.nblk, b + kPiece)});
+    }
+    std::vector<std::vector<std::array<uint64_t, 2>>> pruns(pieces.size());
+    auto fill = [&](size_t p) {
+        const Piece& q = pieces[p];
+        const uint32_t* in = out + pfx[q.si];
+        uint32_t* to = src[q.si].ahit.data();
+        memcpy(to + q.b0, in + q.b0, (q.b1 - q.b0) * sizeof(uint32_t));
+        std::vector<std::array<uint64_t, 2>> runs;
+        uint64_t k = q.b0;
+        while (k < q.b1) {
+            // 16 windows at a time while none missed (a loop the compiler vectorizes)
+            if (k + 16 <= q.b1) {
+                bool miss = false;
+                for (int j = 0; j < 16; ++j) miss |= in[k + j] == kNoBlk;
+                if (!miss) { k += 16; continue; }
+            }
+            if (in[k] != kNoBlk) { ++k; continue; }
+            uint64_t e = k + 1;
+            while (e < q.b1 && in[e] == kNoBlk) ++e;
+            runs.push_back({k, e});
+            k = e;
+        }
+        pruns[p].swap(runs);
+    };
+    const size_t np = pieces.size();
+    const int nthr = np > 1 ? std::min<int>(walk_threads(), (int)np) : 1;
+    if (!run_parallel(nthr, [&](int t) { for (size_t p = t; p < np; p += nthr) fill(p); }))
         return fail(SYDELTA_E_OOM, "out of host memory (probe results)");
+    miss_runs.assign(ns, {});
+    for (size_t p = 0; p < np; ++p) {
+        auto& m = miss_runs[pieces[p].si];
+        for (auto& r : pruns[p]) {
+            if (!m.empty() && m.back()[1] == r[0]) m.back()[1] = r[1];  // a run across pieces
+            else m.push_back(r);
+        }
+    }
+    for (size_t i = 0; i < ns; ++i) {
+        uint64_t missed = 0;
+        for (auto& r : miss_runs[i]) missed += r[1] - r[0];
+        src[i].nahit = src[i].nblk - missed;
+    }
     return SYDELTA_OK;
 }
 
@@ -922,18 +968,14 @@ int Classifier::classify(int mode) {
             ranges.push_back({i, c.kb, c.kb + c.nblk});
             continue;
         }
-        uint64_t k = 0;
-        while (k < c.nblk) {
-            if (c.ahit[k] != kNoBlk) { ++k; continue; }
-            uint64_t e = k + 1;
-            while (e < c.nblk && c.ahit[e] == kNoBlk) ++e;
+        for (auto& m : miss_runs[i]) {
+            const uint64_t k = m[0], e = m[1];
             if (e - k >= kPhaseRun && phase_probe_on()) {
                 ranges.push_back({i, c.kb + k, c.kb + k + 2});
                 runs.push_back({i, k, e});
             } else {
                 ranges.push_back({i, c.kb + k, c.kb + e});
             }
-            k = e;
         }
     }
     merge_ranges(ranges, gap_blocks);

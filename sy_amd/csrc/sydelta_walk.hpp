@@ -59,7 +59,7 @@ struct Src {
     uint64_t p0 = 0, p1 = 0;    // full-window positions to classify, [p0, p1); p0 % n == 0
     uint64_t kb = 0, nblk = 0;  // blocks kb .. kb+nblk-1 (position k*n) cover [p0, p1)
     bool probed = false;
-    std::vector<uint32_t> ahit;    // probed: per block, its aligned window's hit or kNoBlk
+    std::vector<uint32_t, NoInitAlloc<uint32_t>> ahit;  // probed: per block, its aligned window's hit or kNoBlk
     uint64_t nahit = 0;            // aligned windows that hit
     std::vector<uint8_t> scanned;  // probed: per block, all its window starts were scanned
     std::vector<uint64_t> hpos;    // hits found by scans, sorted, unique

@@ -112,6 +112,14 @@ def main():
             n_checks += 1
         for k in ("SYDELTA_WALK_PAR_MIN", "SYDELTA_WALK_THREADS", "SYDELTA_PROBE"):
             os.environ.pop(k, None)
+        # probe results split into 64 Ki-block pieces: 160 000 blocks, the miss run after
+        # the insertion crosses piece boundaries
+        os.environ["SYDELTA_STREAM_CHUNK"] = str(16 << 20)
+        os.environ["SYDELTA_PROBE"] = "1"
+        basis, s = case(31, 64 * 160000 + 5, 64)
+        check_pair(tmp, basis, s, 64, ("pieces",))
+        n_checks += 1
+        os.environ.pop("SYDELTA_PROBE", None)
         # change ratio on paths: ratio.rs's cases against the oracle
         MiB = 1 << 20
         for name in ("same", "all", "partial", "threshold", "size"):
