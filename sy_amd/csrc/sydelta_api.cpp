@@ -600,6 +600,7 @@ using walk::Src;
 using walk::walk_src;
 
 double ms_since(std::chrono::steady_clock::time_point t0);
+void finish_stats_impl(sydelta_delta* d);
 int walk_threads();
 uint64_t walk_par_min();
 
@@ -1081,7 +1082,7 @@ int Classifier::walk(size_t i, uint64_t entry, const BasisInfo& bi, bool final_s
         const int r = walk_parallel(i, entry, bi, final_src, tail_match, d, exit);
         if (host_timing && r != 2)
             fprintf(stderr, "sydelta parallel walk: %.3f ms, %zu ops, rc=%d\n", ms_since(t0), ops.size(), r);
-        if (r != 1 && r != 2) return r;  // done, or an error
+        if (r != 1 && r != 2) return r;  // done (stats counted by the join), or an error
     }
     if (ops.empty() && c.nahit + c.hpos.size() >= 4096) ops = take_ops(2 * (c.nahit + c.hpos.size()));
     for (int round = 0;; ++round) {
@@ -1100,6 +1101,7 @@ int Classifier::walk(size_t i, uint64_t entry, const BasisInfo& bi, bool final_s
         else
             { if (int r = scan({{i, k, c.kb + c.nblk}})) return r; }
     }
+    finish_stats_impl(d);
     return SYDELTA_OK;
 }
 
@@ -1128,9 +1130,15 @@ int Classifier::walk_parallel(size_t i, uint64_t entry, const BasisInfo& bi, boo
     } pool;
     const auto t0 = std::chrono::steady_clock::now();
     walk::SplitTiming tm;
+    walk::OpCounts oc;
     const int r = walk::walk_split(c, n, st, bi, final_src, tail_match, d->ops, exit, pool,
-                                   [&] { return ms_since(t0); }, &tm);
+                                   [&] { return ms_since(t0); }, &tm, &oc);
     if (r < 0) return fail(SYDELTA_E_OOM, "out of host memory (op lists)");
+    if (r == 0) {
+        d->stats.copy_ops = oc.copy_ops;
+        d->stats.data_ops = oc.data_ops;
+        d->stats.literal_bytes = oc.literal_bytes;
+    }
     static const bool host_timing = getenv("SYDELTA_HOST_TIMING") != nullptr;
     if (host_timing && r == 0)
         fprintf(stderr,
@@ -1141,15 +1149,35 @@ int Classifier::walk_parallel(size_t i, uint64_t entry, const BasisInfo& bi, boo
 }
 
 void finish_stats_impl(sydelta_delta* d) {
-    d->stats.copy_ops = d->stats.data_ops = d->stats.literal_bytes = 0;
-    for (auto& o : d->ops) {
-        if (o.kind == SYDELTA_OP_COPY) {
-            d->stats.copy_ops++;
-        } else {
-            d->stats.data_ops++;
-            d->stats.literal_bytes += o.b;
+    // one pass over the op array (24 MiB at 1 Mi ops): split over the host pool when large
+    const size_t no = d->ops.size();
+    const int T = no >= (1u << 18) ? walk_threads() : 1;
+    struct Part {
+        uint64_t data = 0, lit = 0;
+        char pad[48];  // one cache line per part
+    };
+    std::vector<Part> part(T);
+    auto count = [&](int t) {
+        const sydelta_op* o = d->ops.data();
+        uint64_t nd = 0, lit = 0;
+        for (size_t i = no * t / T, e = no * (t + 1) / T; i < e; ++i) {
+            const bool data = o[i].kind != SYDELTA_OP_COPY;
+            nd += data;
+            lit += data ? o[i].b : 0;
         }
+        part[t].data = nd;
+        part[t].lit = lit;
+    };
+    if (!run_parallel(T, count)) {  // the pool could not take the batch: count here
+        part.assign(T, Part{});
+        for (int t = 0; t < T; ++t) count(t);
     }
+    d->stats.data_ops = d->stats.literal_bytes = 0;
+    for (auto& p : part) {
+        d->stats.data_ops += p.data;
+        d->stats.literal_bytes += p.lit;
+    }
+    d->stats.copy_ops = no - d->stats.data_ops;
 }
 
 // Tail-rule flags (generator.rs:156-184) of the given sources of c (file f's last
@@ -1268,9 +1296,8 @@ static int match_impl(sydelta_index* ix, const uint8_t* d_buf, const uint64_t* s
         const BasisInfo bi{ix->fblk[f], ix->fblk[f + 1] - ix->fblk[f], ix->last_size[f]};
         uint64_t exit = 0;
         if (!walked[f]) {
-            if (int r = C.walk(f, 0, bi, true, tail[f], d, &exit)) return r;
+            if (int r = C.walk(f, 0, bi, true, tail[f], d, &exit)) return r;  // counts the ops too
             d->stats.verified_hits = C.src[f].hpos.size() + C.src[f].nahit;
-            finish_stats(d);
         }
         b->total.verified_hits += d->stats.verified_hits;
         b->total.copy_ops += d->stats.copy_ops;
@@ -2073,8 +2100,7 @@ extern "C" int sydelta_chunk_walk(sydelta_chunk* ch, uint64_t entry, uint64_t* e
     C.prof = nullptr;
     if (r) return r;
     d->stats.verified_hits = c.hpos.size() + c.nahit;
-    d->stats.weak_hits = C.weak_hits;
-    finish_stats(d.get());
+    d->stats.weak_hits = C.weak_hits;  // op counts: C.walk
     *out = d.release();
     return SYDELTA_OK;
 } catch (...) {

@@ -351,6 +351,11 @@ struct SplitTiming {
     double walk_ms = 0, seg_max_ms = 0, seg_min_ms = 0, chain_ms = 0, join_ms = 0;
 };
 
+// Op counts of a joined list (Delta stats), counted by the join's copy tasks.
+struct OpCounts {
+    uint64_t copy_ops = 0, data_ops = 0, literal_bytes = 0;
+};
+
 // The walk of c from `entry` split at st[1..T) (split_points): every segment walked
 // concurrently from its split point, then chained -- segment t's true entry is segment
 // t-1's exit; a segment entered elsewhere is walked again from there -- and joined,
@@ -360,7 +365,8 @@ struct SplitTiming {
 // unclassified position: the caller walks sequentially) or -1 (out of host memory).
 template <class Pool, class Clock>
 int walk_split(const Src& c, uint64_t n, const std::vector<uint64_t>& st, const BasisInfo& bi, bool final_src,
-               int tail_match, OpVec& ops, uint64_t* exit, Pool& pool, Clock clock, SplitTiming* tm) {
+               int tail_match, OpVec& ops, uint64_t* exit, Pool& pool, Clock clock, SplitTiming* tm,
+               OpCounts* counts = nullptr) {
     const int T = (int)st.size() - 1;
     const uint64_t nh = c.nahit + c.hpos.size();
     std::vector<OpVec> part(T);
@@ -422,15 +428,38 @@ int walk_split(const Src& c, uint64_t n, const std::vector<uint64_t>& st, const 
     ops.swap(joined);
     pool.give(std::move(joined));
     ops.resize(at[T]);
+    struct alignas(64) Cnt {
+        uint64_t data = 0, lit = 0;
+    };
+    std::vector<Cnt> cnt(T);
     if (!run_parallel(T, [&](int t) {
-            if (part[t].size() > skip[t])
-                memcpy(ops.data() + at[t], part[t].data() + skip[t], (part[t].size() - skip[t]) * sizeof(sydelta_op));
+            if (part[t].size() <= skip[t]) return;
+            const sydelta_op* from = part[t].data() + skip[t];
+            const size_t m = part[t].size() - skip[t];
+            memcpy(ops.data() + at[t], from, m * sizeof(sydelta_op));
+            if (!counts) return;
+            uint64_t nd = 0, lit = 0;
+            for (size_t i = 0; i < m; ++i) {
+                const bool d = from[i].kind != SYDELTA_OP_COPY;
+                nd += d;
+                lit += d ? from[i].b : 0;
+            }
+            cnt[t].data = nd;
+            cnt[t].lit = lit;
         }))
         return -1;
     // merged lengths: the op before each skipped one absorbs it (a run of skipped
     // segments adds up in the same op, in order)
     for (int t = 1; t < T; ++t)
         if (skip[t]) ops[at[t] - 1].b += part[t][0].b;
+    if (counts) {  // a merged Data op's bytes stay in the total
+        *counts = OpCounts{};
+        for (int t = 0; t < T; ++t) {
+            counts->data_ops += cnt[t].data;
+            counts->literal_bytes += cnt[t].lit + (skip[t] ? part[t][0].b : 0);
+        }
+        counts->copy_ops = ops.size() - counts->data_ops;
+    }
     *exit = ex[T - 1];
     if (tm) {
         tm->walk_ms = t_walk - t0;

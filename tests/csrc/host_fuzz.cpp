@@ -205,12 +205,19 @@ static void walk_case(int it) {
         OpVec sops;
         uint64_t sexit = 0;
         SplitTiming tm;
+        OpCounts oc;
         const int r = walk_split(c, k.n, st, k.bi, k.final_src, k.tail_match, sops, &sexit, pool,
-                                 [] { return 0.0; }, &tm);
+                                 [] { return 0.0; }, &tm, &oc);
         CHECK(r == 0);
         if (!same(sops, expect) || sexit != rexit) {
             fprintf(stderr, "split walk mismatch it=%d T=%d (%zu segments)\n", it, T, st.size() - 1);
             abort();
+        }
+        {  // the join's op counts equal a direct count of the joined list
+            uint64_t nd = 0, lit = 0;
+            for (auto& o : sops)
+                if (o.kind != SYDELTA_OP_COPY) { ++nd; lit += o.b; }
+            CHECK(oc.data_ops == nd && oc.literal_bytes == lit && oc.copy_ops == sops.size() - nd);
         }
     }
 }
