@@ -408,7 +408,7 @@ def algo_bytes_per_step(workload: str, n: int, nb_bytes: int, src_bytes: int) ->
     """Algorithmic HBM bytes per step of each kernel that can dominate a workload.  Per
     step the signature kernels read the basis once and the scan reads the source once
     (SURVEY.md section 8(d))."""
-    return {"k_scan": src_bytes, "k_scan_lds": src_bytes, "k_scan_l1": src_bytes,
+    return {"k_scan": src_bytes, "k_scan_lds": src_bytes, "k_scan_l1": src_bytes, "k_scan_l1w": src_bytes,
             "k_sig_fast": nb_bytes if workload in ("c3", "c3b") else n,
             "k_sig_batch": n, "k_sig_wave": n, "k_probe": src_bytes,
             "k_apply": 2 * n,  # apply: every output byte read once and written once
@@ -443,16 +443,17 @@ def roofline(prof: dict, steps: int, algo_step: dict, positions=None, keys=None)
     roof = {"bound": "hbm", "achieved": round(ach, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
             "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": pmc_traffic(dom, per_launch),
             "kernel": dom, "avg_launch_ms": round(avg_ms, 4), "algorithmic_bytes_per_launch": per_launch}
-    if positions and (dom in ("k_scan_lds", "k_scan") or (dom == "k_scan_l1" and keys)):
-        per_pos = 1.0 if dom != "k_scan_l1" else 1.0 - math.exp(-keys / float(1 << 20))
+    l1_bits = {"k_scan_l1": 1 << 20, "k_scan_l1w": 28672 * 32}  # level-1 filter bits (one hash)
+    if positions and (dom in ("k_scan_lds", "k_scan") or (dom in l1_bits and keys)):
+        per_pos = 1.0 if dom not in l1_bits else 1.0 - math.exp(-keys / float(l1_bits[dom]))
         req = positions * per_pos / launches_per_step  # filter-word requests per launch
         rate = req / (avg_ms * 1e-3)
         roof["l2_gather"] = {"requests_per_launch": int(req), "achieved": round(rate / 1e9, 2),
                              "peak": round(L2_GATHER_PEAK / 1e9, 1), "unit": "G requests/s",
                              "frac": round(rate / L2_GATHER_PEAK, 4),
                              "requests_per_position": round(per_pos, 4),
-                             "model": ("one per window start" if dom != "k_scan_l1" else
-                                       "window starts x level-1 pass rate 1-exp(-keys/2^20)")}
+                             "model": ("one per window start" if dom not in l1_bits else
+                                       f"window starts x level-1 pass rate 1-exp(-keys/{l1_bits[dom]})")}
     return roof
 
 

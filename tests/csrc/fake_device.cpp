@@ -306,6 +306,10 @@ hipError_t launch_index_build(const uint32_t* d_weak, const uint64_t* d_strong, 
 }
 
 uint64_t scan_tile_positions() { return 16384; }
+int scan_l1_mode() {
+    const char* e = getenv("SYDELTA_SCAN_L1");
+    return (e && e[0] == '0') ? 0 : (e && e[0] == '2') ? 2 : 1;
+}
 uint32_t scan_max_window() { return 8192; }
 size_t scan_queue_entries() { return 1024; }
 
