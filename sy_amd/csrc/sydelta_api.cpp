@@ -632,8 +632,10 @@ struct Classifier {
     DevBuf q_buf;
     size_t qcap = 0;
     // probed sources: their runs of blocks whose aligned window missed, [first, end)
-    // local blocks, ascending (set by probe)
-    std::vector<std::vector<std::array<uint64_t, 2>>> miss_runs;
+    // local blocks, ascending; source i's are miss_runs[miss_off[i] .. miss_off[i+1])
+    // (set by probe)
+    std::vector<std::array<uint64_t, 2>> miss_runs;
+    std::vector<size_t> miss_off;
 
     // Aligned probe of every block of every source (mode 1), of none (0), or, in
     // auto mode (-1), when a 1-in-16 sample finds >= 1/8 of its windows hitting.
@@ -738,44 +740,55 @@ int Classifier::probe(int mode) {
         c.scanned.assign(c.nblk, 0);
         for (uint64_t b = 0; b < c.nblk; b += kPiece) pieces.push_back({i, b, std::min(c.nblk, b + kPiece)});
     }
-    std::vector<std::vector<std::array<uint64_t, 2>>> pruns(pieces.size());
-    auto fill = [&](size_t p) {
-        const Piece& q = pieces[p];
-        const uint32_t* in = out + pfx[q.si];
-        uint32_t* to = src[q.si].ahit.data();
-        memcpy(to + q.b0, in + q.b0, (q.b1 - q.b0) * sizeof(uint32_t));
-        std::vector<std::array<uint64_t, 2>> runs;
-        uint64_t k = q.b0;
-        while (k < q.b1) {
-            // 16 windows at a time while none missed (a loop the compiler vectorizes)
-            if (k + 16 <= q.b1) {
-                bool miss = false;
-                for (int j = 0; j < 16; ++j) miss |= in[k + j] == kNoBlk;
-                if (!miss) { k += 16; continue; }
-            }
-            if (in[k] != kNoBlk) { ++k; continue; }
-            uint64_t e = k + 1;
-            while (e < q.b1 && in[e] == kNoBlk) ++e;
-            runs.push_back({k, e});
-            k = e;
-        }
-        pruns[p].swap(runs);
+    struct Run {
+        size_t si;
+        uint64_t k, e;
     };
     const size_t np = pieces.size();
     const int nthr = np > 1 ? std::min<int>(walk_threads(), (int)np) : 1;
-    if (!run_parallel(nthr, [&](int t) { for (size_t p = t; p < np; p += nthr) fill(p); }))
-        return fail(SYDELTA_E_OOM, "out of host memory (probe results)");
-    miss_runs.assign(ns, {});
-    for (size_t p = 0; p < np; ++p) {
-        auto& m = miss_runs[pieces[p].si];
-        for (auto& r : pruns[p]) {
-            if (!m.empty() && m.back()[1] == r[0]) m.back()[1] = r[1];  // a run across pieces
-            else m.push_back(r);
+    std::vector<std::vector<Run>> truns(nthr);
+    auto fill = [&](int t) {  // pieces [np*t/nthr, np*(t+1)/nthr), in order
+        std::vector<Run> runs;  // on this thread's stack: the vector headers in truns sit side by side
+        for (size_t p = np * t / nthr, pe = np * (t + 1) / nthr; p < pe; ++p) {
+            const Piece& q = pieces[p];
+            const uint32_t* in = out + pfx[q.si];
+            memcpy(src[q.si].ahit.data() + q.b0, in + q.b0, (q.b1 - q.b0) * sizeof(uint32_t));
+            uint64_t k = q.b0;
+            while (k < q.b1) {
+                // 16 windows at a time while none missed (a loop the compiler vectorizes)
+                if (k + 16 <= q.b1) {
+                    bool miss = false;
+                    for (int j = 0; j < 16; ++j) miss |= in[k + j] == kNoBlk;
+                    if (!miss) { k += 16; continue; }
+                }
+                if (in[k] != kNoBlk) { ++k; continue; }
+                uint64_t e = k + 1;
+                while (e < q.b1 && in[e] == kNoBlk) ++e;
+                runs.push_back({q.si, k, e});
+                k = e;
+            }
         }
-    }
+        truns[t].swap(runs);
+    };
+    if (!run_parallel(nthr, fill)) return fail(SYDELTA_E_OOM, "out of host memory (probe results)");
+    // runs in (source, block) order; a run that crosses a piece boundary is joined
+    miss_runs.clear();
+    miss_off.assign(ns + 1, 0);
+    size_t last_si = SIZE_MAX;
+    for (auto& tr : truns)
+        for (const Run& r : tr) {
+            if (r.si == last_si && miss_runs.back()[1] == r.k) {
+                miss_runs.back()[1] = r.e;
+                continue;
+            }
+            miss_runs.push_back({r.k, r.e});
+            ++miss_off[r.si + 1];
+            last_si = r.si;
+        }
+    for (size_t i = 0; i < ns; ++i) miss_off[i + 1] += miss_off[i];
     for (size_t i = 0; i < ns; ++i) {
         uint64_t missed = 0;
-        for (auto& r : miss_runs[i]) missed += r[1] - r[0];
+        for (size_t j = miss_off[i]; j < miss_off[i + 1]; ++j) missed += miss_runs[j][1] - miss_runs[j][0];
         src[i].nahit = src[i].nblk - missed;
     }
     return SYDELTA_OK;
@@ -971,8 +984,8 @@ int Classifier::classify(int mode) {
             ranges.push_back({i, c.kb, c.kb + c.nblk});
             continue;
         }
-        for (auto& m : miss_runs[i]) {
-            const uint64_t k = m[0], e = m[1];
+        for (size_t j = miss_off[i]; j < miss_off[i + 1]; ++j) {
+            const uint64_t k = miss_runs[j][0], e = miss_runs[j][1];
             if (e - k >= kPhaseRun && phase_probe_on()) {
                 ranges.push_back({i, c.kb + k, c.kb + k + 2});
                 runs.push_back({i, k, e});
