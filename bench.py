@@ -83,9 +83,13 @@ def parse():
                     help="c4: split this rank's files over K host threads, each one batched call on its own "
                          "library stream (sy runs up to 10 transfers at once, cli.rs:178-180), so one call's "
                          "host work overlaps another's kernels")
+    ap.add_argument("--device-walk", action="store_true",
+                    help="resolve the greedy walks on the device (K5b, SYDELTA_DEVICE_WALK=1; c4/c5/path)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-host-inclusive", action="store_true")
     a = ap.parse_args()
+    if a.device_walk:
+        os.environ["SYDELTA_DEVICE_WALK"] = "1"
     if a.size_gib is None:
         a.size_gib = 8.0 if a.workload in ("c5", "apply", "local") else 1.0 if a.workload == "path" else 4.0
     if a.files is None:
@@ -807,6 +811,7 @@ def main():
                                 f"file-sharded x{world} (independent pairs per rank, no collective)"),
                 **({"files": args.files, "files_this_rank": len(files[0]), "callers_per_rank": max(1, len(c4_groups))}
                    if args.workload == "c4" else {}),
+                "walk": "device (K5b)" if args.device_walk else "host threads",
             },
             "pct_hbm_peak": round(value * GIB / 1e9 / HBM_PEAK_GBS * 100, 2),
             "roofline": roof,

@@ -338,6 +338,10 @@ void sydelta_set_profiling(int on);
 /* JSON object {"kernel": {"ms": total, "count": n}, ...}; returns bytes written
  * (excluding NUL) or the size needed if cap is too small. Clears with reset. */
 size_t sydelta_profile_json(char *buf, size_t cap, int reset);
+/* Walks resolved on the device (K5b, SYDELTA_DEVICE_WALK=1) and walks it handed back to
+ * the host walk (the path reached a position only an on-demand scan classifies), since
+ * the library was loaded. */
+int sydelta_walk_counters(uint64_t *device_walks, uint64_t *device_fallbacks);
 /* Deterministic synthetic bytes on the device: counter-based splitmix64 of
  * (seed, 8-byte word index), little endian (oracle.synth_bytes). */
 int sydelta_synth_fill(uint8_t *d_buf, uint64_t len, uint64_t seed, void *stream);

@@ -29,6 +29,7 @@
 #include <mutex>
 #include <thread>
 #include <string>
+#include <unordered_set>
 #include <vector>
 
 #include "../../include/sydelta.h"
@@ -489,8 +490,41 @@ extern "C" int sydelta_index_create_batch(int device, const uint32_t* weak, cons
 // fresh array cost more than the walk itself, so freed deltas hand their arrays
 // back for the next walk (bounded: 16 arrays; a parallel walk takes one per segment).
 namespace {
+// Pinned op arrays (walk::op_arena): installed with the device walk, so the D2H of a
+// device-resolved op list is a DMA into the delta's own array.  Released arrays go back
+// to the pool below first; one released at process exit is left to the OS (the HIP
+// runtime may already be gone).
+std::atomic<bool> g_exiting{false};
+std::mutex g_arena_mu;
+std::unordered_set<void*>* g_arena_live = new std::unordered_set<void*>();  // never destroyed
+void* arena_alloc(size_t bytes) {
+    void* p = nullptr;
+    if (g_exiting.load() || hipHostMalloc(&p, bytes, hipHostMallocDefault) != hipSuccess) return nullptr;
+    std::lock_guard<std::mutex> lk(g_arena_mu);
+    g_arena_live->insert(p);
+    return p;
+}
+bool arena_release(void* p) {
+    {
+        std::lock_guard<std::mutex> lk(g_arena_mu);
+        if (!g_arena_live->erase(p)) return false;
+    }
+    if (!g_exiting.load()) (void)hipHostFree(p);
+    return true;
+}
+void install_op_arena() {
+    static std::once_flag once;
+    std::call_once(once, [] {
+        atexit([] { g_exiting = true; });  // runs before the HIP runtime's own teardown
+        ::op_arena().release = arena_release;
+        ::op_arena().alloc = arena_alloc;
+    });
+}
+
+std::atomic<uint64_t> g_device_walks{0}, g_device_walk_fallbacks{0};  // sydelta_walk_counters
+
 std::mutex g_ops_mu;
-std::vector<OpVec> g_ops_pool;
+std::vector<OpVec>& g_ops_pool = *new std::vector<OpVec>();  // never destroyed (arrays may be pinned)
 OpVec take_ops(size_t want) {
     // best fit: the smallest pooled array holding `want`, else the largest one when it
     // holds at least half (it grows once)
@@ -522,6 +556,12 @@ struct sydelta_delta_batch {
     std::vector<sydelta_delta> d;
     sydelta_match_stats total{};
 };
+
+extern "C" int sydelta_walk_counters(uint64_t* device_walks, uint64_t* device_fallbacks) {
+    if (device_walks) *device_walks = g_device_walks.load();
+    if (device_fallbacks) *device_fallbacks = g_device_walk_fallbacks.load();
+    return SYDELTA_OK;
+}
 
 extern "C" uint64_t sydelta_delta_num_ops(const sydelta_delta* d) { return d ? d->ops.size() : 0; }
 extern "C" const sydelta_op* sydelta_delta_ops(const sydelta_delta* d) {
@@ -605,6 +645,8 @@ double ms_since(std::chrono::steady_clock::time_point t0);
 void finish_stats_impl(sydelta_delta* d);
 int walk_threads();
 uint64_t walk_par_min();
+bool device_walk_on();
+uint64_t device_walk_min();
 
 
 bool phase_probe_on() {
@@ -636,6 +678,10 @@ struct Classifier {
     // (set by probe)
     std::vector<std::array<uint64_t, 2>> miss_runs;
     std::vector<size_t> miss_off;
+    // the full probe pass's results on the device: source i's at d_probe_out + probe_pfx[i]
+    DevBuf probe_buf;
+    uint32_t* d_probe_out = nullptr;
+    std::vector<uint64_t> probe_pfx;
 
     // Aligned probe of every block of every source (mode 1), of none (0), or, in
     // auto mode (-1), when a 1-in-16 sample finds >= 1/8 of its windows hitting.
@@ -658,6 +704,11 @@ struct Classifier {
     // 1 (a segment reached an unclassified block: walk sequentially), 2 (too small).
     int walk_parallel(size_t i, uint64_t entry, const BasisInfo& bi, bool final_src, int tail_match,
                       sydelta_delta* d, uint64_t* exit);
+    // The same walk resolved on the device (K5b, sydelta_chain.hpp; SYDELTA_DEVICE_WALK=1).
+    // Returns 0 (done, d->ops and its stats set), 1 (the path reaches an unclassified
+    // position: walk on the host, which scans on demand), 2 (not applicable) or an error.
+    int walk_device(size_t i, uint64_t entry, const BasisInfo& bi, bool final_src, int tail_match,
+                    sydelta_delta* d, uint64_t* exit);
 };
 
 int Classifier::probe(int mode) {
@@ -699,12 +750,16 @@ int Classifier::probe(int mode) {
             pin.cap = np * 5 / 4;
         }
         out = pin.p;
-        DevBuf jb;
+        // the full pass's results stay on the device for the device walk (walk_device)
+        DevBuf local;
+        DevBuf& jb = stride == 1 ? probe_buf : local;
+        if (jb.p) { (void)hipFreeAsync(jb.p, s); jb.p = nullptr; }
         const size_t jbytes = (jobs.size() * sizeof(ProbeJob) + 255) & ~(size_t)255;
         const size_t obytes = (np * 4 + 255) & ~(size_t)255;
         HIP_TRY(hipMallocAsync(&jb.p, jbytes + 2 * obytes + np * 8, s));
         jb.s = s;
         uint32_t* d_out = (uint32_t*)((uint8_t*)jb.p + jbytes);
+        if (stride == 1) d_probe_out = d_out;
         uint32_t* d_pw = (uint32_t*)((uint8_t*)jb.p + jbytes + obytes);
         uint64_t* d_pst = (uint64_t*)((uint8_t*)jb.p + jbytes + 2 * obytes);
         HIP_TRY(hipMemcpyAsync(jb.p, jobs.data(), jobs.size() * sizeof(ProbeJob), hipMemcpyHostToDevice, s));
@@ -723,6 +778,7 @@ int Classifier::probe(int mode) {
         if (hits * 8 < nout) return SYDELTA_OK;
     }
     if (int r = run(1, pfx)) return r;
+    probe_pfx = pfx;
     // Copy the results into the sources and find their miss runs (the blocks classify
     // scans) in one pass, in pieces of 64 Ki blocks on the host pool: one large source
     // (C5) is split as well as many small ones (C4).
@@ -1092,6 +1148,18 @@ int Classifier::walk(size_t i, uint64_t entry, const BasisInfo& bi, bool final_s
     Src& c = src[i];
     OpVec& ops = d->ops;
     static const bool host_timing = getenv("SYDELTA_HOST_TIMING") != nullptr;
+    if (ops.empty() && device_walk_on()) {
+        const auto t0 = std::chrono::steady_clock::now();
+        const int r = walk_device(i, entry, bi, final_src, tail_match, d, exit);
+        if (host_timing && r != 2)
+            fprintf(stderr, "sydelta device walk: %.3f ms, %zu ops, rc=%d\n", ms_since(t0), ops.size(), r);
+        if (r == 0) {
+            g_device_walks.fetch_add(1);
+            return SYDELTA_OK;
+        }
+        if (r != 1 && r != 2) return r;
+        if (r == 1) g_device_walk_fallbacks.fetch_add(1);
+    }
     if (ops.empty()) {
         const auto t0 = std::chrono::steady_clock::now();
         const int r = walk_parallel(i, entry, bi, final_src, tail_match, d, exit);
@@ -1161,6 +1229,141 @@ int Classifier::walk_parallel(size_t i, uint64_t entry, const BasisInfo& bi, boo
                 "join %.3f ms\n",
                 (int)st.size() - 1, tm.walk_ms, tm.seg_max_ms, tm.seg_min_ms, tm.chain_ms, tm.join_ms);
     return r;
+}
+
+// SYDELTA_DEVICE_WALK=1: resolve walks of sources with at least SYDELTA_DEVICE_WALK_MIN
+// hits (default 4096) on the device.  Off by default until measured on hardware.
+bool device_walk_on() {
+    const char* e = getenv("SYDELTA_DEVICE_WALK");  // read per walk, like the other knobs
+    const bool on = e && e[0] == '1';
+    if (on) install_op_arena();
+    return on;
+}
+uint64_t device_walk_min() {
+    const char* e = getenv("SYDELTA_DEVICE_WALK_MIN");
+    return (e && *e) ? strtoull(e, nullptr, 10) : 4096;
+}
+
+int Classifier::walk_device(size_t i, uint64_t entry, const BasisInfo& bi, bool final_src, int tail_match,
+                            sydelta_delta* d, uint64_t* exit) {
+    const Src& c = src[i];
+    if (!c.ppos.empty() || entry >= c.p1 || entry < c.p0) return 2;  // phase probes: host walk
+    if (c.probed && (!d_probe_out || probe_pfx.size() <= i)) return 2;
+    static const bool host_timing = getenv("SYDELTA_HOST_TIMING") != nullptr;
+    const auto t0 = std::chrono::steady_clock::now();
+    // scan hits, minus those at an aligned position whose aligned window hit (the same
+    // hit twice: the merge needs two disjoint lists)
+    const uint64_t* hp = c.hpos.data();
+    const uint32_t* hb = c.hblk.data();
+    std::vector<uint64_t> fp;
+    std::vector<uint32_t> fb;
+    if (c.probed && !c.hpos.empty()) {
+        bool dup = false;
+        for (uint64_t p : c.hpos)
+            if (p % n == 0 && c.ahit[p / n - c.kb] != kNoBlk) { dup = true; break; }
+        if (dup) {
+            fp.reserve(c.hpos.size());
+            fb.reserve(c.hpos.size());
+            for (size_t h = 0; h < c.hpos.size(); ++h) {
+                const uint64_t p = c.hpos[h];
+                if (p % n == 0 && c.ahit[p / n - c.kb] != kNoBlk) continue;
+                fp.push_back(p);
+                fb.push_back(c.hblk[h]);
+            }
+            hp = fp.data();
+            hb = fb.data();
+        }
+    }
+    const uint64_t H = hp == c.hpos.data() ? c.hpos.size() : fp.size();
+    const uint64_t M = (c.probed ? c.nahit : 0) + H;
+    if (M < device_walk_min() || M > (1ull << 25)) return 2;
+    const uint32_t K = chain::chain_levels(M);
+    const uint64_t W = M + 2, nblk = c.probed ? c.nblk : 0, nkw = (nblk + 31) / 32;
+    // one allocation: known | aflag | apfx | hpos | hblk | upos | ublk | jump | on | cnt | off | ops | res
+    auto al = [](uint64_t b) { return (b + 255) & ~(uint64_t)255; };
+    const uint64_t o_known = 0, o_aflag = o_known + al(4 * nkw), o_apfx = o_aflag + al(4 * (nblk + 1));
+    const uint64_t o_hpos = o_apfx + al(4 * (nblk + 1)), o_hblk = o_hpos + al(8 * H), o_upos = o_hblk + al(4 * H);
+    const uint64_t o_ublk = o_upos + al(8 * M), o_jump = o_ublk + al(4 * M), o_on = o_jump + al(4 * W * K);
+    const uint64_t o_cnt = o_on + al(W), o_off = o_cnt + al(4 * (M + 1)), o_ops = o_off + al(4 * (M + 1));
+    const uint64_t o_res = o_ops + al(sizeof(sydelta_op) * 2 * M), total = o_res + al(sizeof(chain::ChainResult));
+    DevBuf buf;
+    HIP_TRY(hipMallocAsync(&buf.p, total, s));
+    buf.s = s;
+    uint8_t* B = (uint8_t*)buf.p;
+    chain::ChainArgs a{};
+    a.n = n;
+    a.p1 = c.p1;
+    a.kb = c.kb;
+    a.nblk = nblk;
+    a.entry = entry;
+    a.probed = c.probed ? 1u : 0u;
+    a.K = K;
+    a.ahit = c.probed ? d_probe_out + probe_pfx[i] : nullptr;
+    a.known = (const uint32_t*)(B + o_known);
+    a.aflag = (uint32_t*)(B + o_aflag);
+    a.apfx = (uint32_t*)(B + o_apfx);
+    a.hpos = (const uint64_t*)(B + o_hpos);
+    a.hblk = (const uint32_t*)(B + o_hblk);
+    a.H = H;
+    a.M = M;
+    a.upos = (uint64_t*)(B + o_upos);
+    a.ublk = (uint32_t*)(B + o_ublk);
+    a.jump = (uint32_t*)(B + o_jump);
+    a.on = B + o_on;
+    a.cnt = (uint32_t*)(B + o_cnt);
+    a.off = (uint32_t*)(B + o_off);
+    a.blk_base = bi.blk_base;
+    a.nblocks = bi.nblocks;
+    a.last_size = bi.last_size;
+    a.ops = (sydelta_op*)(B + o_ops);
+    a.res = (chain::ChainResult*)(B + o_res);
+    std::vector<uint32_t> known;
+    if (c.probed) {  // bit k: block kb+k was scanned
+        known.assign(nkw, 0);
+        const uint8_t* sc = c.scanned.data();
+        for (uint64_t k = 0; k < nblk; ++k) known[k >> 5] |= (uint32_t)(sc[k] != 0) << (k & 31);
+        HIP_TRY(hipMemcpyAsync(B + o_known, known.data(), 4 * nkw, hipMemcpyHostToDevice, s));
+    }
+    if (H) {
+        HIP_TRY(hipMemcpyAsync(B + o_hpos, hp, 8 * H, hipMemcpyHostToDevice, s));
+        HIP_TRY(hipMemcpyAsync(B + o_hblk, hb, 4 * H, hipMemcpyHostToDevice, s));
+    }
+    HIP_TRY(launch_chain(a, s, prof));
+    chain::ChainResult res{};
+    HIP_TRY(hipMemcpyAsync(&res, a.res, sizeof(res), hipMemcpyDeviceToHost, s));
+    HIP_TRY(hipStreamSynchronize(s));
+    const double t_kern = ms_since(t0);
+    if (res.unk) return 1;
+    if (res.bad || res.nops > 2 * M || (res.first < M) != (res.last < M)) {
+        // cannot happen with consistent inputs; the host walk gives the right answer anyway
+        if (host_timing) fprintf(stderr, "sydelta device walk: inconsistent result, host walk\n");
+        return 1;
+    }
+    // [entry, first hit) | the device's ops | the end of the walk (walk::finish_walk)
+    OpVec& ops = d->ops;
+    const bool lead = res.first < M && res.first_pos > entry;
+    if (ops.capacity() < (lead ? 1 : 0) + res.nops + 3) ops = take_ops((lead ? 1 : 0) + res.nops + 3);
+    ops.resize((lead ? 1 : 0) + res.nops);
+    if (lead) ops[0] = sydelta_op{SYDELTA_OP_DATA, 0, entry, res.first_pos - entry};
+    if (res.nops)
+        HIP_TRY(hipMemcpyAsync(ops.data() + (lead ? 1 : 0), a.ops, sizeof(sydelta_op) * res.nops,
+                               hipMemcpyDeviceToHost, s));
+    const uint64_t x = res.first < M ? res.last_pos + n : c.p1;  // no hit: the walk runs to the end
+    const uint64_t lit = res.first < M ? x : entry;
+    const size_t before_end = ops.size();
+    walk::finish_walk(c, n, lit, x, c.p1, bi, final_src, tail_match, ops, exit);
+    HIP_TRY(hipStreamSynchronize(s));
+    // stats: the device counted its Data ops and bytes
+    uint64_t nd = res.data_ops + (lead ? 1 : 0), lb = res.lit_bytes + (lead ? res.first_pos - entry : 0);
+    for (size_t k = before_end; k < ops.size(); ++k)
+        if (ops[k].kind == SYDELTA_OP_DATA) { ++nd; lb += ops[k].b; }
+    d->stats.copy_ops = ops.size() - nd;
+    d->stats.data_ops = nd;
+    d->stats.literal_bytes = lb;
+    if (host_timing)
+        fprintf(stderr, "sydelta device walk: %llu hits (%llu aligned), %u levels: kernels %.3f ms, ops to host %.3f ms\n",
+                (unsigned long long)M, (unsigned long long)(M - H), K, t_kern, ms_since(t0) - t_kern);
+    return 0;
 }
 
 void finish_stats_impl(sydelta_delta* d) {

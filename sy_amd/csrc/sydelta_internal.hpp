@@ -7,6 +7,8 @@
 #include <string>
 #include <vector>
 
+#include "sydelta_chain.hpp"
+
 namespace sydelta {
 
 constexpr uint32_t kEmptyKey = 0xFFFFFFFFu;  // never a valid weak: A = weak & 0xFFFF <= 65520
@@ -135,6 +137,10 @@ struct TailJob {
 };
 hipError_t launch_tail(const uint8_t* d_buf, const TailJob* d_jobs, uint32_t njobs, const uint32_t* d_weak,
                        const uint64_t* d_strong, int* d_flag, hipStream_t s);
+// K5b: the walk of one classified source resolved on the device (sydelta_chain.hpp):
+// merge, successors, pointer-jumping path marking, op emission; a.res receives the
+// totals.  All arrays of a are device memory sized as ChainArgs documents.
+hipError_t launch_chain(const chain::ChainArgs& a, hipStream_t s, Profiler* prof);
 // One slice (<= 64 KiB) of an op for the device apply: out[dst, dst+len) =
 // (from_basis ? basis : lit)[src, src+len).
 struct ApplyPiece {

@@ -2356,6 +2356,60 @@ __global__ void k_tail(const uint8_t* __restrict__ buf, const TailJob* __restric
 }
 
 // ===========================================================================
+// K5b: the greedy walk resolved on the device (sydelta_chain.hpp)
+// ===========================================================================
+// One thread per block / hit / forest node; the bodies live in sydelta_chain.hpp so the
+// host emulation of the device layer runs the same code.  Every kernel is a plain
+// gather/scatter over arrays of a few MiB (HBM- and launch-bound).
+__device__ __forceinline__ uint64_t gtid() { return (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; }
+
+__global__ __launch_bounds__(256) void k_chain_flag(chain::ChainArgs a) {
+    const uint64_t i = gtid();
+    if (i <= a.nblk) chain::chain_flag(a, i);
+}
+__global__ __launch_bounds__(256) void k_chain_place_aligned(chain::ChainArgs a) {
+    const uint64_t i = gtid();
+    if (i < a.nblk) chain::chain_place_aligned(a, i);
+}
+__global__ __launch_bounds__(256) void k_chain_place_scan(chain::ChainArgs a) {
+    const uint64_t i = gtid();
+    if (i < a.H) chain::chain_place_scan(a, i);
+}
+__global__ __launch_bounds__(256) void k_chain_succ(chain::ChainArgs a) {
+    const uint64_t i = gtid();
+    if (i < a.M + 2) chain::chain_succ(a, i);
+}
+__global__ __launch_bounds__(256) void k_chain_lift(chain::ChainArgs a, uint32_t l) {
+    const uint64_t i = gtid();
+    if (i < a.M + 2) chain::chain_lift(a, l, i);
+}
+__global__ void k_chain_entry(chain::ChainArgs a) {
+    if (gtid() == 0) chain::chain_entry(a);
+}
+__global__ __launch_bounds__(256) void k_chain_mark(chain::ChainArgs a, uint32_t l) {
+    const uint64_t i = gtid();
+    if (i < a.M + 2) chain::chain_mark(a, l, i);
+}
+__global__ __launch_bounds__(256) void k_chain_count(chain::ChainArgs a) {
+    const uint64_t i = gtid();
+    if (i < a.M + 1) chain::chain_count(a, i);
+}
+// The ops of the marked hits; per wave one atomic for the Data-op count and bytes.
+__global__ __launch_bounds__(256) void k_chain_emit(chain::ChainArgs a) {
+    const uint64_t i = gtid();
+    const uint64_t lit = i < a.M ? chain::chain_emit(a, i) : 0;
+    const uint64_t nd = wave_sum64(lit ? 1ull : 0ull);
+    const uint64_t nb = wave_sum64(lit);
+    if ((threadIdx.x & 63) == 0 && nd) {
+        atomicAdd((unsigned long long*)&a.res->data_ops, (unsigned long long)nd);
+        atomicAdd((unsigned long long*)&a.res->lit_bytes, (unsigned long long)nb);
+    }
+}
+__global__ void k_chain_finish(chain::ChainArgs a) {
+    if (gtid() == 0) chain::chain_finish(a);
+}
+
+// ===========================================================================
 // K6: apply_delta on the device (applier.rs:22-56 as a gather-copy)
 // ===========================================================================
 // One workgroup per piece (an op, or a <= 64 KiB slice of one).  Thread t writes the
@@ -3235,6 +3289,45 @@ hipError_t launch_sort_hits(uint64_t* key, uint32_t* val, uint64_t* key_tmp, uin
     *key_out = key_tmp;
     *val_out = val_tmp;
     return e;
+}
+
+// u32 exclusive sum of n items (d_in may equal d_out).
+static hipError_t exclusive_sum_u32(const uint32_t* d_in, uint32_t* d_out, uint64_t n, hipStream_t s) {
+    if (!n) return hipSuccess;
+    size_t tmp = 0;
+    hipError_t e;
+    if ((e = hipcub::DeviceScan::ExclusiveSum(nullptr, tmp, d_in, d_out, (int)n, s))) return e;
+    void* d_t = nullptr;
+    if ((e = hipMallocAsync(&d_t, tmp ? tmp : 16, s))) return e;
+    e = hipcub::DeviceScan::ExclusiveSum(d_t, tmp, d_in, d_out, (int)n, s);
+    (void)hipFreeAsync(d_t, s);
+    return e;
+}
+
+hipError_t launch_chain(const chain::ChainArgs& a, hipStream_t s, Profiler* prof) {
+    // u32 node indices, int item counts for hipcub, grids of < 2^31 blocks
+    if (a.M + 2 >= (1ull << 31) || a.nblk + 1 >= (1ull << 31) || a.K == 0 || a.K > 32) return hipErrorInvalidValue;
+    if ((1ull << a.K) <= a.M + 1) return hipErrorInvalidValue;
+    ProfScope ps(prof, s, "k_chain");
+    const uint64_t W = a.M + 2;
+    hipError_t e;
+    if ((e = hipMemsetAsync(a.res, 0, sizeof(chain::ChainResult), s))) return e;
+    if (a.probed) {
+        hipLaunchKernelGGL(k_chain_flag, dim3(grid_for(a.nblk + 1, 256)), dim3(256), 0, s, a);
+        if ((e = exclusive_sum_u32(a.aflag, a.apfx, a.nblk + 1, s))) return e;
+        if (a.nblk) hipLaunchKernelGGL(k_chain_place_aligned, dim3(grid_for(a.nblk, 256)), dim3(256), 0, s, a);
+    }
+    if (a.H) hipLaunchKernelGGL(k_chain_place_scan, dim3(grid_for(a.H, 256)), dim3(256), 0, s, a);
+    hipLaunchKernelGGL(k_chain_succ, dim3(grid_for(W, 256)), dim3(256), 0, s, a);
+    for (uint32_t l = 0; l + 1 < a.K; ++l) hipLaunchKernelGGL(k_chain_lift, dim3(grid_for(W, 256)), dim3(256), 0, s, a, l);
+    if ((e = hipMemsetAsync(a.on, 0, W, s))) return e;
+    hipLaunchKernelGGL(k_chain_entry, dim3(1), dim3(64), 0, s, a);
+    for (uint32_t l = a.K; l-- > 0;) hipLaunchKernelGGL(k_chain_mark, dim3(grid_for(W, 256)), dim3(256), 0, s, a, l);
+    hipLaunchKernelGGL(k_chain_count, dim3(grid_for(a.M + 1, 256)), dim3(256), 0, s, a);
+    if ((e = exclusive_sum_u32(a.cnt, a.off, a.M + 1, s))) return e;
+    if (a.M) hipLaunchKernelGGL(k_chain_emit, dim3(grid_for(a.M, 256)), dim3(256), 0, s, a);
+    hipLaunchKernelGGL(k_chain_finish, dim3(1), dim3(64), 0, s, a);
+    return hipGetLastError();
 }
 
 hipError_t launch_tail(const uint8_t* d_buf, const TailJob* d_jobs, uint32_t njobs, const uint32_t* d_weak,

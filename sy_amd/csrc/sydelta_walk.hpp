@@ -42,7 +42,48 @@ struct NoInitAlloc : std::allocator<T> {
         ::new ((void*)p) U(std::forward<A>(a)...);
     }
 };
-using OpVec = std::vector<sydelta_op, NoInitAlloc<sydelta_op>>;
+// Op arrays of 1 MiB and more may come from a registered arena: sydelta_api.cpp installs
+// pinned host memory when the device walk is on, so a device-resolved op list lands in
+// the delta's own array by DMA.  Without an arena: the heap.
+struct OpArena {
+    void* (*alloc)(size_t bytes) = nullptr;  // nullptr result: use the heap
+    bool (*release)(void* p) = nullptr;      // true if p came from alloc (and is released)
+};
+inline OpArena& op_arena() {
+    static OpArena a;
+    return a;
+}
+constexpr size_t kOpArenaMin = 1u << 20;
+
+template <class T>
+struct OpAlloc {
+    using value_type = T;
+    OpAlloc() = default;
+    template <class U>
+    OpAlloc(const OpAlloc<U>&) {}
+    T* allocate(size_t n) {
+        const OpArena& A = op_arena();
+        if (n * sizeof(T) >= kOpArenaMin && A.alloc)
+            if (void* p = A.alloc(n * sizeof(T))) return (T*)p;
+        return std::allocator<T>().allocate(n);
+    }
+    void deallocate(T* p, size_t n) {
+        const OpArena& A = op_arena();
+        if (n * sizeof(T) >= kOpArenaMin && A.release && A.release(p)) return;
+        std::allocator<T>().deallocate(p, n);
+    }
+    template <class U>
+    void construct(U* p) noexcept {  // no zero fill (as NoInitAlloc)
+        ::new ((void*)p) U;
+    }
+    template <class U, class... A>
+    void construct(U* p, A&&... a) {
+        ::new ((void*)p) U(std::forward<A>(a)...);
+    }
+    friend bool operator==(const OpAlloc&, const OpAlloc&) { return true; }
+    friend bool operator!=(const OpAlloc&, const OpAlloc&) { return false; }
+};
+using OpVec = std::vector<sydelta_op, OpAlloc<sydelta_op>>;
 
 namespace sydelta {
 namespace walk {
@@ -116,6 +157,33 @@ struct BasisInfo {
     uint64_t nblocks;
     uint64_t last_size;  // size of its last block
 };
+
+// The end of a walk that stopped at x (>= end, or no hit left before end) with its
+// literal run open since lit: a non-final chunk ends with that run up to `end` and
+// *exit = max(x, end); a final source applies the tail rule (generator.rs:156-184: only
+// p* = len - last_size can match) and ends with the last literal run.
+inline void finish_walk(const Src& c, uint64_t n, uint64_t lit, uint64_t x, uint64_t end, const BasisInfo& bi,
+                        bool final_src, int tail_match, OpVec& ops, uint64_t* exit) {
+    auto data = [&](uint64_t a, uint64_t b) {
+        if (b > a) ops.push_back({SYDELTA_OP_DATA, 0, a, b - a});
+    };
+    if (!final_src) {
+        data(lit, end);
+        *exit = std::max(x, end);
+        return;
+    }
+    if (tail_match && bi.nblocks) {
+        const uint64_t pstar = c.flen - bi.last_size;
+        if (pstar >= lit) {
+            data(lit, pstar);
+            const uint64_t b = bi.nblocks - 1;
+            ops.push_back({SYDELTA_OP_COPY, 0, b * n, bi.last_size});
+            lit = c.flen;
+        }
+    }
+    data(lit, c.flen);
+    *exit = c.flen;
+}
 
 // Greedy walk (generator.rs:116-221 / 283-379) over c's classified positions from
 // `entry` up to `end` (c.p1, or a split point of a parallel walk).  ops get
@@ -209,21 +277,7 @@ inline int walk_src(const Src& c, uint64_t n, uint64_t entry, uint64_t end, cons
         x = p + n;  // generator.rs:144 / :313
         lit = x;
     }
-    if (!final_src) {
-        data(lit, end);
-        *exit = std::max(x, end);
-        return 0;
-    }
-    if (tail_match && bi.nblocks) {
-        const uint64_t pstar = c.flen - bi.last_size;
-        if (pstar >= lit) {
-            data(lit, pstar);
-            copy(bi.blk_base + bi.nblocks - 1);
-            lit = c.flen;
-        }
-    }
-    data(lit, c.flen);
-    *exit = c.flen;
+    finish_walk(c, n, lit, x, end, bi, final_src, tail_match, ops, exit);
     return 0;
 }
 

@@ -156,7 +156,100 @@ def main():
         n_checks += 10
         n_checks += batch_and_chunk_checks()
         n_checks += error_checks(tmp)
+        n_checks += device_walk_checks(tmp)
     print(f"emulated host checks ok: {n_checks}")
+
+
+def _walk_counters():
+    import ctypes
+
+    from sy_amd._lib import lib
+
+    a, b = ctypes.c_uint64(), ctypes.c_uint64()
+    lib.sydelta_walk_counters(ctypes.byref(a), ctypes.byref(b))
+    return a.value, b.value
+
+
+def device_walk_checks(tmp):
+    """K5b (sydelta_chain.hpp, SYDELTA_DEVICE_WALK=1, every source with a hit): the
+    kernels' per-thread bodies run by the emulated launch_chain, through the path API,
+    the chunked walks and dense/periodic data where walks from different entries never
+    merge; each op list against the oracle.  Also counts that the device walk ran and
+    that a path into an unscanned block was handed back to the host walk."""
+    os.environ["SYDELTA_DEVICE_WALK"] = "1"
+    os.environ["SYDELTA_DEVICE_WALK_MIN"] = "1"
+    n = 0
+    w0, f0 = _walk_counters()
+    try:
+        os.environ["SYDELTA_STREAM_CHUNK"] = str(1 << 20)
+        for bs, size in [(4096, (1 << 20) + 1234), (1007, (1 << 20) + 99), (64, (1 << 18) + 5),
+                         (16384, (2 << 20) + 4321), (512, 300000)]:
+            for probe in ("0", "1", "auto"):
+                if probe == "auto":
+                    os.environ.pop("SYDELTA_PROBE", None)
+                else:
+                    os.environ["SYDELTA_PROBE"] = probe
+                basis, s = case(bs % 89 + 3, size, bs)
+                check_pair(tmp, basis, s, bs, ("device walk", bs, probe))
+                n += 1
+        # dense hits: low-alphabet and periodic data (every window hits; chains from
+        # neighbouring entries stay apart), a zero file, duplicated blocks
+        rng = np.random.default_rng(5)
+        for probe in ("0", "1"):
+            os.environ["SYDELTA_PROBE"] = probe
+            for name, basis, s in _dense_cases(rng):
+                check_pair(tmp, basis, s, 64, ("device walk dense", name, probe))
+                n += 1
+        os.environ.pop("SYDELTA_PROBE", None)
+        # the chunked walks (entries inside blocks) and the batched path
+        n += batch_and_chunk_checks()
+        # shifted data with the probe on: walks that jump into blocks classified only by
+        # their aligned window (on-demand scans through the host walk)
+        os.environ["SYDELTA_PROBE"] = "1"
+        for seed in range(4):
+            basis = O.synth_bytes(400 * 256 + 3, 0x900 + seed)
+            s = basis.copy()
+            r = np.random.default_rng(seed)
+            for p in sorted(r.integers(0, s.size - 300, 6))[::-1]:
+                k = int(r.integers(1, 255))
+                s = np.concatenate([s[:p], basis[p + 40:p + 40 + k], s[p:]])  # copies of nearby unaligned bytes
+            check_pair(tmp, basis, s, 256, ("device walk shifted", seed))
+            n += 1
+    finally:
+        for k in ("SYDELTA_DEVICE_WALK", "SYDELTA_DEVICE_WALK_MIN", "SYDELTA_PROBE"):
+            os.environ.pop(k, None)
+    w1, f1 = _walk_counters()
+    assert w1 - w0 >= 40, ("device walks ran", w1 - w0)
+    print(f"device walks: {w1 - w0}, handed back to the host walk: {f1 - f0}")
+    return n
+
+
+def _dense_cases(rng):
+    period = rng.integers(0, 256, 100, dtype=np.uint8)
+    per = np.tile(period, 3000)
+    yield "periodic", per, np.concatenate([per[:777], per[5:20000], per[3:]])
+    low = rng.integers(0, 2, 120000, dtype=np.uint8)
+    low2 = low.copy()
+    low2[rng.integers(0, low2.size, 50)] ^= 1
+    yield "binary", low, low2
+    z = np.zeros(90000, np.uint8)
+    yield "zeros", z, np.concatenate([z[:5000], np.ones(3, np.uint8), z[:70001]])
+    blk = rng.integers(0, 256, 64, dtype=np.uint8)
+    dup = np.tile(blk, 500)
+    yield "duplicated", dup, np.concatenate([dup[:1000], rng.integers(0, 256, 33, dtype=np.uint8), dup[7:]])
+    # basis blocks A and rot5(A): a run of A's hits at every aligned position and at every
+    # aligned position + 5, so scanned blocks whose aligned window hit hold unaligned hits
+    # too (the merge's ranks); Z = 5 other bytes + A[5:] enters the +5 phase, so paths run
+    # through those unaligned hits
+    A = rng.integers(0, 256, 64, dtype=np.uint8)
+    rot = np.concatenate([A[5:], A[:5]])
+    rnd = lambda k: rng.integers(0, 256, 64 * k, dtype=np.uint8)
+    Z = np.concatenate([rng.integers(0, 256, 5, dtype=np.uint8), A[5:]])
+    basis = np.concatenate([A, rot, rnd(40)])
+    parts = []
+    for k in range(60):
+        parts += [rnd(1), A, A, A] if k % 3 else [rnd(2), Z, A, A, A, rnd(1), A]
+    yield "rotated", basis, np.concatenate(parts + [A[:17]])
 
 
 def error_checks(tmp):

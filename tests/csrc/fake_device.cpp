@@ -404,6 +404,54 @@ hipError_t launch_json_write(const JsonPiece*, uint64_t, const uint8_t*, const u
     EmuTimer emu_t;
     return hipErrorNotSupported;
 }
+// K5b: the kernels' own per-thread bodies (sydelta_chain.hpp) in the launch order of
+// sydelta_kernels.hip's launch_chain, one loop per kernel.  The marking levels run their
+// threads alternately forward and backward: two of the schedules a GPU may produce for
+// a launch whose threads read marks that others of the same launch write.
+hipError_t launch_chain(const chain::ChainArgs& a, hipStream_t, Profiler*) {
+    EmuTimer emu_t;
+    if (a.M + 2 >= (1ull << 31) || a.nblk + 1 >= (1ull << 31) || a.K == 0 || a.K > 32) return hipErrorInvalidValue;
+    if ((1ull << a.K) <= a.M + 1) return hipErrorInvalidValue;
+    const uint64_t W = a.M + 2;
+    memset(a.res, 0, sizeof(chain::ChainResult));
+    auto excl = [](const uint32_t* in, uint32_t* out, uint64_t n) {
+        uint32_t acc = 0;
+        for (uint64_t i = 0; i < n; ++i) {
+            const uint32_t v = in[i];
+            out[i] = acc;
+            acc += v;
+        }
+    };
+    if (a.probed) {
+        for (uint64_t k = 0; k <= a.nblk; ++k) chain::chain_flag(a, k);
+        excl(a.aflag, a.apfx, a.nblk + 1);
+        for (uint64_t k = 0; k < a.nblk; ++k) chain::chain_place_aligned(a, k);
+    }
+    for (uint64_t h = 0; h < a.H; ++h) chain::chain_place_scan(a, h);
+    for (uint64_t i = 0; i < W; ++i) chain::chain_succ(a, i);
+    for (uint32_t l = 0; l + 1 < a.K; ++l)
+        for (uint64_t i = 0; i < W; ++i) chain::chain_lift(a, l, i);
+    memset(a.on, 0, W);
+    chain::chain_entry(a);
+    for (uint32_t l = a.K; l-- > 0;) {
+        if (l & 1)
+            for (uint64_t i = W; i-- > 0;) chain::chain_mark(a, l, i);
+        else
+            for (uint64_t i = 0; i < W; ++i) chain::chain_mark(a, l, i);
+    }
+    for (uint64_t i = 0; i <= a.M; ++i) chain::chain_count(a, i);
+    excl(a.cnt, a.off, a.M + 1);
+    for (uint64_t i = 0; i < a.M; ++i) {
+        const uint64_t lit = chain::chain_emit(a, i);
+        if (lit) {
+            a.res->data_ops += 1;
+            a.res->lit_bytes += lit;
+        }
+    }
+    chain::chain_finish(a);
+    return hipSuccess;
+}
+
 hipError_t launch_exclusive_sum_u64(const uint64_t* d_in, uint64_t* d_out, uint64_t n, hipStream_t) {
     EmuTimer emu_t;
     uint64_t acc = 0;
