@@ -159,8 +159,39 @@ std::vector<hipEvent_t>& event_pool() {
     (void)hipGetDevice(&dev);
     return t_event_pool[dev];
 }
+// Timed launches are resolved when the profile is read (sydelta_profile_json, after the
+// caller synchronized), not at the end of each call: a per-call event wait would add a
+// host round trip, and an idle GPU, to every call of a profiled run.  Resolved events go
+// to a shared free list per device (the resolving thread may not be the recording one).
+std::vector<Profiler::Pending> g_deferred;                  // under g_prof_mu
+std::map<int, std::vector<hipEvent_t>> g_free_events;       // under g_prof_mu
+constexpr size_t kDeferredMax = 1 << 14;                     // beyond: resolve on the spot
+void resolve_locked(std::vector<Profiler::Pending>& v) {
+    for (auto& q : v) {
+        float ms = 0;
+        if (hipEventSynchronize(q.b) == hipSuccess && hipEventElapsedTime(&ms, q.a, q.b) == hipSuccess) {
+            auto& e = g_prof[q.name];
+            e.first += ms;
+            e.second += 1;
+        }
+        auto& fl = g_free_events[q.device];
+        fl.push_back(q.a);
+        fl.push_back(q.b);
+    }
+    v.clear();
+}
 hipEvent_t take_event() {
     auto& pool = event_pool();
+    if (pool.empty()) {
+        int dev = 0;
+        (void)hipGetDevice(&dev);
+        std::lock_guard<std::mutex> lk(g_prof_mu);
+        auto& fl = g_free_events[dev];
+        while (!fl.empty() && pool.size() < 64) {
+            pool.push_back(fl.back());
+            fl.pop_back();
+        }
+    }
     if (!pool.empty()) {
         hipEvent_t e = pool.back();
         pool.pop_back();
@@ -175,27 +206,20 @@ ProfScope::ProfScope(Profiler* p_, hipStream_t s_, const char* n) : p(p_), s(s_)
     a = take_event();
     b = take_event();
     if (!a || !b) { p = nullptr; return; }
+    (void)hipGetDevice(&device);
     (void)hipEventRecord(a, s);
 }
 ProfScope::~ProfScope() {
     if (!p) return;
     (void)hipEventRecord(b, s);
-    p->pending.push_back({name, a, b});
+    p->pending.push_back({name, a, b, device});
 }
 void Profiler::resolve() {
+    if (pending.empty()) return;
     std::lock_guard<std::mutex> lk(g_prof_mu);
-    for (auto& q : pending) {
-        float ms = 0;
-        if (hipEventSynchronize(q.b) == hipSuccess && hipEventElapsedTime(&ms, q.a, q.b) == hipSuccess) {
-            auto& e = g_prof[q.name];
-            e.first += ms;
-            e.second += 1;
-        }
-        auto& pool = event_pool();
-        pool.push_back(q.a);
-        pool.push_back(q.b);
-    }
+    g_deferred.insert(g_deferred.end(), pending.begin(), pending.end());
     pending.clear();
+    if (g_deferred.size() > kDeferredMax) resolve_locked(g_deferred);
 }
 }  // namespace sydelta
 
@@ -207,6 +231,7 @@ extern "C" size_t sydelta_profile_json(char* buf, size_t cap, int reset) {
     std::string s = "{";
     {
         std::lock_guard<std::mutex> lk(g_prof_mu);
+        sydelta::resolve_locked(sydelta::g_deferred);
         bool first = true;
         for (auto& kv : g_prof) {
             char tmp[256];
@@ -258,7 +283,7 @@ extern "C" int sydelta_signature_device(int device, const uint8_t* d_buf, uint64
     hipStream_t s = stream ? (hipStream_t)stream : thread_stream(device < 0 ? 0 : device);
     CallProf cp;
     HIP_TRY(launch_signature(d_buf, len, block_size, d_weak, d_strong, s, cp.get()));
-    if (!stream || cp.get()) HIP_TRY(hipStreamSynchronize(s));
+    if (!stream) HIP_TRY(hipStreamSynchronize(s));
     return SYDELTA_OK;
 } catch (...) {
     return sydelta::host_exception();
@@ -2060,7 +2085,9 @@ extern "C" int sydelta_apply_delta_device(int device, const uint8_t* d_basis, ui
         hipStream_t cstream = cs.first;
         const std::vector<hipEvent_t>& ev = cs.second;
         // On an error after the first upload was queued: drain both streams before the
-        // table (device) and the pinned staging (host, reused by the next call) go away.
+        // table (device) and the pinned staging (host, reused by the next call) go away
+        // (drain is declared after pb, so it runs first).
+        DevBuf pb;
         struct Drain {
             hipStream_t a, b;
             bool armed = false;
@@ -2068,7 +2095,6 @@ extern "C" int sydelta_apply_delta_device(int device, const uint8_t* d_basis, ui
                 if (armed) { (void)hipStreamSynchronize(a); (void)hipStreamSynchronize(b); }
             }
         } drain{cstream, s};
-        DevBuf pb;
         HIP_TRY(hipMallocAsync(&pb.p, need * sizeof(ApplyPiece), s));
         pb.s = s;
         HIP_TRY(hipEventRecord(ev[0], s));  // the table allocation is ordered before the uploads

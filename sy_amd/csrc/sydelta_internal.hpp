@@ -67,15 +67,16 @@ struct DeviceIndex {
 
 // Per-kernel HIP-event timing (enabled by sydelta_set_profiling).
 struct Profiler {
-    struct Pending { std::string name; hipEvent_t a, b; };
+    struct Pending { std::string name; hipEvent_t a, b; int device; };
     std::vector<Pending> pending;
-    void resolve();  // after the stream has been synchronised
+    void resolve();  // hands the call's timed launches over; read by sydelta_profile_json
 };
 struct ProfScope {
     Profiler* p;
     hipStream_t s;
     const char* name;
     hipEvent_t a{}, b{};
+    int device = 0;
     ProfScope(Profiler* p_, hipStream_t s_, const char* n);
     ~ProfScope();
 };
