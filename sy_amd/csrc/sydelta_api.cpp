@@ -166,8 +166,17 @@ std::vector<hipEvent_t>& event_pool() {
 std::vector<Profiler::Pending> g_deferred;                  // under g_prof_mu
 std::map<int, std::vector<hipEvent_t>> g_free_events;       // under g_prof_mu
 constexpr size_t kDeferredMax = 1 << 14;                     // beyond: resolve on the spot
-void resolve_locked(std::vector<Profiler::Pending>& v) {
-    for (auto& q : v) {
+// Resolve the entries of v (all, waiting on their events; or, with only_done, those whose
+// end event has completed, so a long profiled run keeps recycling its events).
+void resolve_locked(std::vector<Profiler::Pending>& v, bool only_done = false) {
+    size_t keep = 0;
+    for (size_t i = 0; i < v.size(); ++i) {
+        Profiler::Pending& q = v[i];
+        if (only_done && hipEventQuery(q.b) != hipSuccess) {
+            if (keep != i) v[keep] = std::move(q);
+            ++keep;
+            continue;
+        }
         float ms = 0;
         if (hipEventSynchronize(q.b) == hipSuccess && hipEventElapsedTime(&ms, q.a, q.b) == hipSuccess) {
             auto& e = g_prof[q.name];
@@ -178,7 +187,7 @@ void resolve_locked(std::vector<Profiler::Pending>& v) {
         fl.push_back(q.a);
         fl.push_back(q.b);
     }
-    v.clear();
+    v.resize(keep);
 }
 hipEvent_t take_event() {
     auto& pool = event_pool();
@@ -219,7 +228,7 @@ void Profiler::resolve() {
     std::lock_guard<std::mutex> lk(g_prof_mu);
     g_deferred.insert(g_deferred.end(), pending.begin(), pending.end());
     pending.clear();
-    if (g_deferred.size() > kDeferredMax) resolve_locked(g_deferred);
+    resolve_locked(g_deferred, g_deferred.size() <= kDeferredMax);
 }
 }  // namespace sydelta
 
