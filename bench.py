@@ -18,6 +18,9 @@ already resident in HBM:
   json: serde_json text of the C3 delta (one 4 GiB literal run,
      ~3.6 characters per byte) written on the device; value = delta source GiB/s;
      cpu_baseline = the same text from libsydelta's host writer on a 256 MiB sample.
+  zstd (ssh.rs:1009-1017): the zstd frame of that JSON text (1 GiB
+     source by default, ~3.6 GiB of text) on the device; value = text GiB/s;
+     cpu_baseline = libzstd level 3 (compress/mod.rs:71-76) on one thread, 64 MiB sample.
   c5 (config 5): ONE file of N x 8 GiB (64 GiB at 8 GPUs), bs 8192, 1% of blocks
      with one substituted byte; chunk-sharded: each rank signs its 8 GiB of the
      basis, RCCL all-gathers the signature, builds the full index, classifies its
@@ -67,7 +70,7 @@ def parse():
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--workload", default="c3",
-                    choices=["c3", "c3b", "c2", "c4", "c5", "apply", "json", "local", "xxh3", "path"])
+                    choices=["c3", "c3b", "c2", "c4", "c5", "apply", "json", "zstd", "local", "xxh3", "path"])
     ap.add_argument("--size-gib", type=float, default=None,
                     help="bytes per rank: c2/c3 basis and source (default 4), c5 chunk (default 8)")
     ap.add_argument("--block-size", type=int, default=None, help="default 4096 (c5: 8192)")
@@ -91,7 +94,7 @@ def parse():
     if a.device_walk:
         os.environ["SYDELTA_DEVICE_WALK"] = "1"
     if a.size_gib is None:
-        a.size_gib = 8.0 if a.workload in ("c5", "apply", "local") else 1.0 if a.workload == "path" else 4.0
+        a.size_gib = 8.0 if a.workload in ("c5", "apply", "local") else 1.0 if a.workload in ("path", "zstd") else 4.0
     if a.files is None:
         a.files = 4096 if a.workload == "xxh3" else 10000
     if a.block_size is None:
@@ -217,6 +220,28 @@ def cpu_json_baseline(src_dev, bs: int):
     dt = time.perf_counter() - t0
     return {"value": round(sample.size / dt / GIB, 4), "unit": "GiB/s", "cores": 1, "kind": "port",
             "sample": f"host writer, one Data op of {sample.size >> 20} MiB ({len(text) >> 20} MiB of text)"}
+
+
+def cpu_zstd_baseline(text_dev, sample_bytes: int = 64 << 20):
+    """zstd level 3 -- what compress/mod.rs:71-76 runs (zstd::Encoder::new(.., 3)) -- with the
+    system libzstd on one thread, on a prefix of the same Delta JSON text."""
+    import ctypes.util
+
+    z = ctypes.CDLL(ctypes.util.find_library("zstd") or "libzstd.so.1")
+    z.ZSTD_compress.restype = ctypes.c_size_t
+    z.ZSTD_compress.argtypes = [ctypes.c_void_p, ctypes.c_size_t, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int]
+    z.ZSTD_compressBound.restype = ctypes.c_size_t
+    z.ZSTD_compressBound.argtypes = [ctypes.c_size_t]
+    z.ZSTD_versionString.restype = ctypes.c_char_p
+    sample = text_dev[:sample_bytes].cpu().numpy()
+    cap = z.ZSTD_compressBound(sample.size)
+    out = np.empty(cap, np.uint8)
+    t0 = time.perf_counter()
+    got = z.ZSTD_compress(out.ctypes.data, cap, sample.ctypes.data, sample.size, 3)
+    dt = time.perf_counter() - t0
+    return {"value": round(sample.size / dt / GIB, 4), "unit": "GiB/s", "cores": 1, "kind": "port",
+            "sample": f"libzstd {z.ZSTD_versionString().decode()} level 3 (compress/mod.rs:71-76) on the first "
+                      f"{sample.size >> 20} MiB of the same text: ratio {got / sample.size:.3f}"}
 
 
 def cpu_xxh3_baseline(buf_dev, offs, lens):
@@ -417,6 +442,7 @@ def algo_bytes_per_step(workload: str, n: int, nb_bytes: int, src_bytes: int) ->
             "k_sig_batch": n, "k_sig_wave": n, "k_probe": src_bytes,
             "k_apply": 2 * n,  # apply: every output byte read once and written once
             "k_json_write": n,  # json: every literal byte read once (text written: ~3.6x)
+            "k_zstd_block": src_bytes,  # zstd: every text byte read once
             "k_block_cmp": 2 * n,  # local: both files read once
             "k_xxh_pieces": n}  # xxh3: every file byte read once
 
@@ -514,7 +540,7 @@ def main():
     c5 = None
     apply_d = None
     json_d = None
-    if args.workload == "json":
+    if args.workload in ("json", "zstd"):
         from sy_amd import wire
 
         dev.synth_fill(basis, seed_base)
@@ -528,6 +554,11 @@ def main():
         json_len = ctypes.c_uint64()
         check(lib.sydelta_delta_to_json_device(json_h, new.data_ptr(), n, None, 0, ctypes.byref(json_len), None))
         json_out = torch.empty(json_len.value + 16, dtype=torch.uint8, device="cuda")
+        zstd_len = json_len.value
+        if args.workload == "zstd":  # the text to compress, written once
+            check(lib.sydelta_delta_to_json_device(json_h, new.data_ptr(), n, json_out.data_ptr(), json_out.numel(),
+                                                   ctypes.byref(json_len), None))
+            zstd_out = torch.empty(int(lib.sydelta_zstd_bound(zstd_len)) + 16, dtype=torch.uint8, device="cuda")
     if args.workload == "apply":
         dev.synth_fill_range(basis, 0, 0x5E1D0005)
         new = torch.empty(n + 16, dtype=torch.uint8, device="cuda")
@@ -669,6 +700,11 @@ def main():
                                                    local_flags.data_ptr(), int(stream.cuda_stream), ctypes.byref(st)))
             return {"changed_blocks": st.changed_blocks, "literal_bytes": st.literal_bytes,
                     "change_ratio": r["change_ratio"], "use_delta": r["use_delta"]}
+        if args.workload == "zstd":
+            got = ctypes.c_uint64()
+            check(lib.sydelta_zstd_compress_device(local, json_out.data_ptr(), zstd_len, zstd_out.data_ptr(),
+                                                   zstd_out.numel(), ctypes.byref(got), int(stream.cuda_stream)))
+            return {"text_bytes": zstd_len, "frame_bytes": got.value, "ratio": round(got.value / zstd_len, 4)}
         if args.workload == "json":
             ln = ctypes.c_uint64()
             check(lib.sydelta_delta_to_json_device(json_h, new.data_ptr(), n, json_out.data_ptr(), json_out.numel(),
@@ -727,6 +763,8 @@ def main():
         bytes_per_step = 2 * n  # both files compared
     elif args.workload == "xxh3":
         bytes_per_step = int(xxh_lens.sum())
+    elif args.workload == "zstd":
+        bytes_per_step = zstd_len  # JSON text compressed
     elif args.workload == "json":
         bytes_per_step = n  # delta source bytes covered by the text
     elif args.workload == "path":
@@ -737,7 +775,8 @@ def main():
     value = total_bytes / elapsed / GIB
     ms_per_step = elapsed / args.steps * 1e3
 
-    src_bytes = int(files[3].sum()) if args.workload == "c4" else new.numel() if args.workload == "c3b" else n
+    src_bytes = (int(files[3].sum()) if args.workload == "c4" else new.numel() if args.workload == "c3b" else
+                 zstd_len if args.workload == "zstd" else n)
     algo_step = algo_bytes_per_step(args.workload, n, nb_bytes, src_bytes)
     stats = (last if isinstance(last, dict) else last.stats) if last is not None else None
     positions = stats.get("positions") if isinstance(stats, dict) and args.workload in ("c3", "c3b") else None
@@ -754,6 +793,8 @@ def main():
             k = min(500, len(files[0]))  # the sampled files' bytes only
             cpu = cpu_c4_baseline(basis[:int(files[0][k - 1] + files[1][k - 1])].cpu().numpy(),
                                   new[:int(files[2][k - 1] + files[3][k - 1])].cpu().numpy(), files, bs, sample_files=k)
+        if world == 1 and not args.no_cpu_baseline and args.workload == "zstd":
+            cpu = cpu_zstd_baseline(json_out[:zstd_len])
         if world == 1 and not args.no_cpu_baseline and args.workload == "json":
             cpu = cpu_json_baseline(new, bs)
         if world == 1 and not args.no_cpu_baseline and args.workload == "xxh3":
@@ -799,6 +840,8 @@ def main():
                     "local": f"local transport: change-ratio sample + block compare of two {n / GIB:.0f} GiB files, "
                              f"bs {bs}, {args.edit_ppm / 1e4:g}% of blocks edited",
                     "json": f"serde_json text of the C3 delta ({n / GIB:.0f} GiB source, one literal run) on the device",
+                    "zstd": f"zstd frame (entropy-only blocks) of the C3 delta's JSON text ({n / GIB:g} GiB source, "
+                            f"one literal run) on the device; value = text bytes/s",
                     "path": f"path API on page-cache-warm files: compute_checksums({n / GIB:g} GiB basis) + "
                             f"generate_delta_streaming({n / GIB:g} GiB source, {args.edit_ppm / 1e4:g}% of {bs} B "
                             f"blocks edited), host-inclusive",

@@ -277,6 +277,16 @@ int sydelta_delta_to_json(const sydelta_delta *d, const uint8_t *lit, uint64_t l
  * Data ops' source offsets) into d_out; *out_len as above (computed on the device). */
 int sydelta_delta_to_json_device(const sydelta_delta *d, const uint8_t *d_lit, uint64_t lit_len, uint8_t *d_out,
                                  uint64_t out_cap, uint64_t *out_len, void *stream);
+/* The zstd frame (RFC 8878) of d_in[0, len) into d_out, on the device: what ssh.rs:1009-1017
+ * sends (compress(delta_json, Compression::Zstd), compress/mod.rs:71-76) and sy-remote
+ * decompresses (sy-remote.rs:160-179) -- typically the text of sydelta_delta_to_json_device.
+ * Entropy-only blocks (Huffman literals, no matches; Raw / RLE where smaller): any zstd
+ * decoder returns the input; the bytes differ from libzstd level 3's.  d_in 16-byte
+ * aligned and readable to the end of its last 16-byte granule; out_cap >=
+ * sydelta_zstd_bound(len); *out_len = frame size. */
+uint64_t sydelta_zstd_bound(uint64_t len);
+int sydelta_zstd_compress_device(int device, const uint8_t *d_in, uint64_t len, uint8_t *d_out, uint64_t out_cap,
+                                 uint64_t *out_len, void *stream);
 /* serde_json::from_str::<Delta> (sy-remote.rs:175): a host delta holding its literal
  * bytes, ready for sydelta_apply_delta. */
 int sydelta_delta_from_json(const char *json, uint64_t len, sydelta_delta **out);

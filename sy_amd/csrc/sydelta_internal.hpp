@@ -8,6 +8,7 @@
 #include <vector>
 
 #include "sydelta_chain.hpp"
+#include "sydelta_zstd.hpp"
 
 namespace sydelta {
 
@@ -168,6 +169,17 @@ hipError_t launch_json_len(const JsonPiece* d_pieces, uint64_t npieces, const ui
 hipError_t launch_json_write(const JsonPiece* d_pieces, uint64_t npieces, const uint8_t* d_lit,
                              const uint64_t* d_off, uint64_t base, uint8_t* d_out, hipStream_t s, Profiler* prof);
 hipError_t launch_exclusive_sum_u64(const uint64_t* d_in, uint64_t* d_out, uint64_t n, hipStream_t s);
+// zstd frame of a text in HBM (sydelta_zstd.hpp).  Blocks [b0, b0 + nb) of d_text (len
+// bytes, 16-byte aligned, readable to the end of its last granule): slot i of d_slots
+// (zstd::kBlockMax bytes each) gets block b0+i's content, d_size[i] its size, d_type[i]
+// its type, d_len64[i] = 3 + size.  Then launch_zstd_frame writes them behind their block
+// headers at d_out + base + d_off[i] (d_off: exclusive prefix of d_len64), and the frame
+// header when b0 == 0.
+hipError_t launch_zstd_blocks(const uint8_t* d_text, uint64_t len, uint64_t b0, uint32_t nb, uint8_t* d_slots,
+                              uint32_t* d_size, uint32_t* d_type, uint64_t* d_len64, hipStream_t s, Profiler* prof);
+hipError_t launch_zstd_frame(const uint8_t* d_text, uint64_t len, uint64_t b0, uint32_t nb, uint64_t nblocks,
+                             const uint8_t* d_slots, const uint32_t* d_size, const uint32_t* d_type, const uint64_t* d_off,
+                             uint64_t base, uint8_t* d_out, hipStream_t s, Profiler* prof);
 // Local path: changed[k] = block k of src differs from block k of dst (k < ceil(slen/bs)).
 hipError_t launch_block_cmp(const uint8_t* d_src, uint64_t slen, const uint8_t* d_dst, uint64_t dlen, uint64_t bs,
                             uint8_t* d_changed, hipStream_t s, Profiler* prof);

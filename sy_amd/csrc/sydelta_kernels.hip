@@ -2410,6 +2410,193 @@ __global__ void k_chain_finish(chain::ChainArgs a) {
 }
 
 // ===========================================================================
+// K7z: zstd frame of a text in HBM (sydelta_zstd.hpp; ssh.rs:1009-1017)
+// ===========================================================================
+// One workgroup per 128 KiB block: a byte histogram (per-wave LDS sub-histograms), the
+// Huffman code by one thread (huf_build, scratch in LDS), then per literal stream a
+// parallel bit scatter: thread t encodes a contiguous run of the stream's symbols, its
+// first bit at the sum of the later runs' bits (the stream is written last symbol
+// first), OR-ing whole 32-bit words into an LDS stream buffer; the stream leaves for the
+// block's slot with its closing 1 bit.  The slot holds the block content; k_zstd_frame
+// then lays the blocks out behind their headers.
+constexpr int kZT = 256;
+constexpr uint32_t kZRun = 144;  // bytes of a stream per thread: 256 runs cover 32 KiB + the 16-byte phase
+static_assert(kZRun * kZT >= zstd::kBlockMax / 4 + 16, "one run per thread covers a stream");
+constexpr uint32_t kZStreamWords = (zstd::kStreamBytesMax + 3) / 4 + 2;
+
+struct ZLds {
+    uint32_t hist[4][256];
+    uint32_t part[kZT];
+    uint32_t words[kZStreamWords];
+    zstd::HufCode code;
+    zstd::HufWork work;
+    uint32_t ssize[4];
+    uint32_t state[4];  // [0] type (0 Raw, 1 RLE, 2 Compressed), [1] write offset in the slot, [2] abort
+};
+
+__global__ __launch_bounds__(kZT) void k_zstd_block(const uint8_t* __restrict__ text, uint64_t len, uint64_t b0,
+                                                    uint8_t* __restrict__ slots, uint32_t* __restrict__ size_out,
+                                                    uint32_t* __restrict__ type_out, uint64_t* __restrict__ len64) {
+    __shared__ ZLds L;
+    const uint32_t tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+    const uint64_t gb = b0 + blockIdx.x;
+    const uint8_t* in = text + gb * zstd::kBlockMax;
+    const uint32_t n = (uint32_t)min<uint64_t>(zstd::kBlockMax, len - gb * zstd::kBlockMax);
+    uint8_t* slot = slots + (uint64_t)blockIdx.x * zstd::kBlockMax;
+    for (uint32_t i = tid; i < 4 * 256; i += kZT) (&L.hist[0][0])[i] = 0;
+    __syncthreads();
+    // histogram, 16 bytes per load (the text is 16-byte aligned and readable to the end
+    // of its last granule); bytes past n are not counted
+    for (uint32_t c = tid; 16 * c < n; c += kZT) {
+        const uint4 v = *(const uint4*)(in + 16 * c);
+        const uint32_t w4[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+        for (int k = 0; k < 16; ++k)
+            if (16 * c + k < n) atomicAdd(&L.hist[wid][(w4[k >> 2] >> (8 * (k & 3))) & 0xFF], 1u);
+    }
+    __syncthreads();
+    for (uint32_t s = tid; s < 256; s += kZT) L.hist[0][s] += L.hist[1][s] + L.hist[2][s] + L.hist[3][s];
+    __syncthreads();
+    const bool four = n > zstd::kSingleStreamMax;
+    const uint32_t hs = four ? 5u : 3u;  // literals header
+    if (tid == 0) {
+        uint32_t distinct = 0, hi = 0;
+        for (uint32_t s = 0; s < 256; ++s)
+            if (L.hist[0][s]) { ++distinct; hi = s; }
+        uint32_t type = 0;
+        if (distinct == 1 && n > 1) type = 1;
+        else if (distinct >= 2 && hi < zstd::kSymbols) type = 2;
+        L.state[0] = type;
+        L.state[2] = 0;
+        if (type == 2) {
+            zstd::huf_build(L.hist[0], L.code, L.work);
+            const uint32_t tsz = zstd::huf_tree_desc(L.code, slot + hs);
+            L.state[1] = hs + tsz + (four ? 6u : 0u);  // the first stream's offset
+        }
+    }
+    __syncthreads();
+    const uint32_t type = L.state[0];
+    if (type == 2) {
+        const uint32_t ns = four ? 4u : 1u;
+        for (uint32_t st = 0; st < ns; ++st) {
+            uint32_t first, count;
+            zstd::stream_range(n, four, st, first, count);
+            const uint32_t nw = (count * zstd::kMaxBits + 1 + 31) / 32 + 1;
+            for (uint32_t i = tid; i < nw; i += kZT) L.words[i] = 0;
+            // thread t's run: the stream's bytes inside [A + kZRun*t, +kZRun), A = first
+            // rounded down to 16, loaded as 9 aligned 16-byte chunks into registers (the
+            // unrolled loops below index them with constants)
+            const uint32_t A = first & ~15u, r0 = A + kZRun * tid, lim = first + count;
+            uint32_t x[kZRun / 4];
+#pragma unroll
+            for (uint32_t j = 0; j < kZRun / 16; ++j) {
+                uint4 v = make_uint4(0, 0, 0, 0);
+                if (r0 + 16 * j < lim) v = *(const uint4*)(in + r0 + 16 * j);
+                x[4 * j] = v.x; x[4 * j + 1] = v.y; x[4 * j + 2] = v.z; x[4 * j + 3] = v.w;
+            }
+            uint32_t bits = 0;
+#pragma unroll
+            for (uint32_t k = 0; k < kZRun; ++k) {
+                const uint32_t p = r0 + k;
+                if (p >= first && p < lim) bits += L.code.len[(x[k >> 2] >> (8 * (k & 3))) & 0xFF];
+            }
+            L.part[tid] = bits;
+            __syncthreads();
+            // bits written before this run: the runs after it (a suffix sum over threads)
+            uint32_t off = 0, total = 0;
+            for (uint32_t t = 0; t < kZT; ++t) {  // LDS broadcast reads, uniform loop
+                const uint32_t pb = L.part[t];
+                total += pb;
+                off += t > tid ? pb : 0u;
+            }
+            // this run, last symbol first, into whole words
+            uint32_t word = off >> 5, fill = off & 31;
+            uint64_t acc = 0;
+#pragma unroll
+            for (uint32_t kk = kZRun; kk-- > 0;) {
+                const uint32_t p = r0 + kk;
+                if (p >= first && p < lim) {
+                    const uint32_t sym = (x[kk >> 2] >> (8 * (kk & 3))) & 0xFF;
+                    acc |= (uint64_t)L.code.code[sym] << fill;
+                    fill += L.code.len[sym];
+                    if (fill >= 32) {
+                        atomicOr(&L.words[word], (uint32_t)acc);
+                        acc >>= 32;
+                        fill -= 32;
+                        ++word;
+                    }
+                }
+            }
+            if (fill) atomicOr(&L.words[word], (uint32_t)acc);
+            __syncthreads();
+            if (tid == 0) atomicOr(&L.words[total >> 5], 1u << (total & 31));  // the closing bit
+            __syncthreads();
+            const uint32_t bytes = total / 8 + 1;
+            const uint32_t o = L.state[1];
+            // a stream that would not fit the block's own size: store the block Raw
+            const bool fits = o + bytes + 1 < n && (four || o + bytes - hs <= zstd::kSingleStreamMax);
+            if (fits) {
+                const uint8_t* wb = (const uint8_t*)L.words;
+                for (uint32_t i = tid; i < bytes; i += kZT) slot[o + i] = wb[i];
+            }
+            __syncthreads();
+            if (tid == 0) {
+                if (!fits) L.state[2] = 1;
+                L.ssize[st] = bytes;
+                L.state[1] = o + bytes;
+            }
+            __syncthreads();
+            if (L.state[2]) break;
+        }
+    }
+    if (tid == 0) {
+        uint32_t t = type, size = 0;
+        if (t == 2 && L.state[2]) t = 0;
+        if (t == 2) {
+            const uint32_t end = L.state[1];  // past the last stream
+            const uint32_t comp = end - hs;
+            zstd::lit_header(slot, four, n, comp);
+            if (four) {
+                const uint32_t tsz = 1 + (L.code.last + 1) / 2;
+                for (uint32_t k = 0; k < 3; ++k) {
+                    slot[hs + tsz + 2 * k] = (uint8_t)L.ssize[k];
+                    slot[hs + tsz + 2 * k + 1] = (uint8_t)(L.ssize[k] >> 8);
+                }
+            }
+            slot[end] = 0;  // Sequences_Section: Number_of_Sequences = 0
+            size = end + 1;
+            if (size >= n) t = 0;
+        }
+        if (t == 1) size = 1;
+        if (t == 0) size = n;
+        type_out[blockIdx.x] = t;
+        size_out[blockIdx.x] = size;
+        len64[blockIdx.x] = 3ull + size;
+    }
+}
+
+// Blocks [b0, b0 + nb) behind their headers at base + off[i]; block 0 of the frame also
+// writes the frame header.  Raw blocks come from the text, RLE blocks are one byte,
+// Compressed blocks come from their slots.
+__global__ __launch_bounds__(kZT) void k_zstd_frame(const uint8_t* __restrict__ text, uint64_t len, uint64_t b0,
+                                                    uint64_t nblocks, const uint8_t* __restrict__ slots,
+                                                    const uint32_t* __restrict__ size_in,
+                                                    const uint32_t* __restrict__ type_in,
+                                                    const uint64_t* __restrict__ off, uint64_t base,
+                                                    uint8_t* __restrict__ out) {
+    const uint64_t gb = b0 + blockIdx.x;
+    const uint32_t t = type_in[blockIdx.x], size = size_in[blockIdx.x];
+    const uint32_t n = (uint32_t)min<uint64_t>(zstd::kBlockMax, len - gb * zstd::kBlockMax);
+    uint8_t* o = out + base + off[blockIdx.x];
+    if (threadIdx.x == 0) {
+        if (gb == 0) zstd::frame_header(out, len);
+        zstd::block_header(o, gb + 1 == nblocks, t, t == 2 ? size : n);
+    }
+    const uint8_t* src = t == 2 ? slots + (uint64_t)blockIdx.x * zstd::kBlockMax : text + gb * zstd::kBlockMax;
+    for (uint32_t i = threadIdx.x; i < size; i += kZT) o[3 + i] = src[i];
+}
+
+// ===========================================================================
 // K6: apply_delta on the device (applier.rs:22-56 as a gather-copy)
 // ===========================================================================
 // One workgroup per piece (an op, or a <= 64 KiB slice of one).  Thread t writes the
@@ -3289,6 +3476,25 @@ hipError_t launch_sort_hits(uint64_t* key, uint32_t* val, uint64_t* key_tmp, uin
     *key_out = key_tmp;
     *val_out = val_tmp;
     return e;
+}
+
+hipError_t launch_zstd_blocks(const uint8_t* d_text, uint64_t len, uint64_t b0, uint32_t nb, uint8_t* d_slots,
+                              uint32_t* d_size, uint32_t* d_type, uint64_t* d_len64, hipStream_t s, Profiler* prof) {
+    if (!nb) return hipSuccess;
+    if (b0 * zstd::kBlockMax >= len) return hipErrorInvalidValue;
+    ProfScope ps(prof, s, "k_zstd_block");
+    hipLaunchKernelGGL(k_zstd_block, dim3(nb), dim3(kZT), 0, s, d_text, len, b0, d_slots, d_size, d_type, d_len64);
+    return hipGetLastError();
+}
+
+hipError_t launch_zstd_frame(const uint8_t* d_text, uint64_t len, uint64_t b0, uint32_t nb, uint64_t nblocks,
+                             const uint8_t* d_slots, const uint32_t* d_size, const uint32_t* d_type, const uint64_t* d_off,
+                             uint64_t base, uint8_t* d_out, hipStream_t s, Profiler* prof) {
+    if (!nb) return hipSuccess;
+    ProfScope ps(prof, s, "k_zstd_frame");
+    hipLaunchKernelGGL(k_zstd_frame, dim3(nb), dim3(kZT), 0, s, d_text, len, b0, nblocks, d_slots, d_size, d_type,
+                       d_off, base, d_out);
+    return hipGetLastError();
 }
 
 // u32 exclusive sum of n items (d_in may equal d_out).

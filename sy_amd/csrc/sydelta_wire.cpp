@@ -507,3 +507,71 @@ extern "C" int sydelta_delta_to_json_device(const sydelta_delta* d, const uint8_
 } catch (...) {
     return sydelta::host_exception();
 }
+
+// ---------------------------------------------------------------------------
+// zstd frame of a text in HBM (ssh.rs:1009-1017: compress(delta_json, Compression::Zstd);
+// sydelta_zstd.hpp).  The text goes through in batches of 8192 blocks (1 GiB): block
+// contents into per-block slots (k_zstd_block), their placement (an exclusive scan of
+// 3 + content), then the frame (k_zstd_frame); scratch is one batch of slots.
+// ---------------------------------------------------------------------------
+extern "C" uint64_t sydelta_zstd_bound(uint64_t len) { return zstd::frame_bound(len); }
+
+extern "C" int sydelta_zstd_compress_device(int device, const uint8_t* d_in, uint64_t len, uint8_t* d_out,
+                                            uint64_t out_cap, uint64_t* out_len, void* stream) try {
+    if (!out_len) return fail(SYDELTA_E_INVAL, "NULL argument");
+    if (len && !d_in) return fail(SYDELTA_E_INVAL, "NULL input");
+    if (len && ((uintptr_t)d_in & 15)) return fail(SYDELTA_E_INVAL, "input must be 16-byte aligned");
+    if (!d_out || out_cap < zstd::frame_bound(len))
+        return fail(SYDELTA_E_INVAL, "output holds %llu bytes, a frame of %llu bytes needs up to %llu",
+                    (unsigned long long)out_cap, (unsigned long long)len,
+                    (unsigned long long)zstd::frame_bound(len));
+    if (int r = ensure_device(device)) return r;
+    hipStream_t s = stream ? (hipStream_t)stream : thread_stream(device < 0 ? 0 : device);
+    if (len == 0) {  // one empty Raw block, the last
+        uint8_t f[zstd::kFrameHeader + 3];
+        zstd::frame_header(f, 0);
+        zstd::block_header(f + zstd::kFrameHeader, true, 0, 0);
+        HIP_TRY(hipMemcpyAsync(d_out, f, sizeof f, hipMemcpyHostToDevice, s));
+        HIP_TRY(hipStreamSynchronize(s));
+        *out_len = sizeof f;
+        return SYDELTA_OK;
+    }
+    const uint64_t nblocks = (len + zstd::kBlockMax - 1) / zstd::kBlockMax;
+    uint64_t kBatch = 8192;  // blocks per batch; SYDELTA_ZSTD_BATCH overrides (tests)
+    if (const char* e = getenv("SYDELTA_ZSTD_BATCH"))
+        if (const uint64_t v = strtoull(e, nullptr, 10)) kBatch = std::min<uint64_t>(v, 1 << 20);
+    const uint64_t nb_max = std::min<uint64_t>(nblocks, kBatch);
+    auto al = [](uint64_t b) { return (b + 255) & ~(uint64_t)255; };
+    const uint64_t o_size = al(nb_max * zstd::kBlockMax), o_type = o_size + al(4 * nb_max);
+    const uint64_t o_len = o_type + al(4 * nb_max), o_off = o_len + al(8 * nb_max), total = o_off + al(8 * nb_max);
+    DevBuf_wire buf;
+    HIP_TRY(hipMallocAsync(&buf.p, total, s));
+    buf.s = s;
+    uint8_t* B = (uint8_t*)buf.p;
+    uint32_t* d_size = (uint32_t*)(B + o_size);
+    uint32_t* d_type = (uint32_t*)(B + o_type);
+    uint64_t* d_len = (uint64_t*)(B + o_len);
+    uint64_t* d_off = (uint64_t*)(B + o_off);
+    CallProf cp;
+    uint64_t pos = zstd::kFrameHeader;
+    for (uint64_t b0 = 0; b0 < nblocks; b0 += kBatch) {
+        const uint32_t nb = (uint32_t)std::min<uint64_t>(kBatch, nblocks - b0);
+        HIP_TRY(launch_zstd_blocks(d_in, len, b0, nb, B, d_size, d_type, d_len, s, cp.get()));
+        HIP_TRY(launch_exclusive_sum_u64(d_len, d_off, nb, s));
+        HIP_TRY(launch_zstd_frame(d_in, len, b0, nb, nblocks, B, d_size, d_type, d_off, pos, d_out, s, cp.get()));
+        uint64_t last[2] = {0, 0};
+        HIP_TRY(hipMemcpyAsync(&last[0], d_off + nb - 1, 8, hipMemcpyDeviceToHost, s));
+        HIP_TRY(hipMemcpyAsync(&last[1], d_len + nb - 1, 8, hipMemcpyDeviceToHost, s));
+        HIP_TRY(hipStreamSynchronize(s));
+        const uint64_t batch = last[0] + last[1];
+        // every block is at most 3 + its own size (Raw), so the frame stays within the bound
+        if (batch > 3ull * nb + std::min<uint64_t>(len - b0 * zstd::kBlockMax, (uint64_t)nb * zstd::kBlockMax))
+            return fail(SYDELTA_E_KERNEL, "zstd: batch at block %llu larger than its bound",
+                        (unsigned long long)b0);
+        pos += batch;
+    }
+    *out_len = pos;
+    return SYDELTA_OK;
+} catch (...) {
+    return sydelta::host_exception();
+}

@@ -181,6 +181,60 @@ __host__ __device__ __forceinline__ void stream_range(uint32_t regen, bool four,
     count = end - first;
 }
 
+// The sequential form of one block (the host emulation of the device layer and the
+// tests' reference encoder): writes the Compressed block content into slot (kBlockMax
+// bytes) and returns its size with *type = 2, or returns n with *type = 0 (store Raw) /
+// 1 with *type = 1 (RLE).  scratch holds 4 * kStreamBytesMax bytes.  k_zstd_block
+// produces the same bytes with a parallel bit scatter.
+__host__ inline uint32_t block_content_seq(const uint8_t* in, uint32_t n, uint8_t* slot, uint8_t* scratch,
+                                           uint32_t* type) {
+    uint32_t h[256] = {0};
+    for (uint32_t i = 0; i < n; ++i) ++h[in[i]];
+    uint32_t distinct = 0, hi = 0;
+    for (uint32_t s = 0; s < 256; ++s)
+        if (h[s]) { ++distinct; hi = s; }
+    *type = 0;
+    if (distinct == 1 && n > 1) { *type = 1; return 1; }
+    if (distinct < 2 || hi >= kSymbols) return n;
+    HufCode c;
+    HufWork wk;
+    huf_build(h, c, wk);
+    const bool four = n > kSingleStreamMax;
+    const uint32_t hs = four ? 5 : 3;
+    const uint32_t tsz = huf_tree_desc(c, slot + hs);
+    uint32_t o = hs + tsz + (four ? 6 : 0);
+    uint32_t ssz[4] = {0, 0, 0, 0};
+    for (uint32_t st = 0; st < (four ? 4u : 1u); ++st) {
+        uint32_t f, cnt;
+        stream_range(n, four, st, f, cnt);
+        // symbols last to first, LSB-first, then the closing 1 bit (BIT_closeCStream)
+        uint8_t* w = scratch + st * kStreamBytesMax;
+        uint32_t bytes = 0, nb = 0;
+        uint64_t acc = 0;
+        for (uint32_t i = cnt; i-- > 0;) {
+            acc |= (uint64_t)c.code[in[f + i]] << nb;
+            nb += c.len[in[f + i]];
+            while (nb >= 8) { w[bytes++] = (uint8_t)acc; acc >>= 8; nb -= 8; }
+        }
+        acc |= 1ull << nb;
+        ++nb;
+        while (nb > 0) { w[bytes++] = (uint8_t)acc; acc >>= 8; nb = nb > 8 ? nb - 8 : 0; }
+        if (o + bytes + 1 >= n || (!four && o + bytes - hs > kSingleStreamMax)) return n;  // not smaller: Raw
+        for (uint32_t i = 0; i < bytes; ++i) slot[o + i] = w[i];
+        o += bytes;
+        ssz[st] = bytes;
+    }
+    lit_header(slot, four, n, o - hs);
+    if (four)
+        for (uint32_t k = 0; k < 3; ++k) {
+            slot[hs + tsz + 2 * k] = (uint8_t)ssz[k];
+            slot[hs + tsz + 2 * k + 1] = (uint8_t)(ssz[k] >> 8);
+        }
+    slot[o] = 0;  // Sequences_Section: Number_of_Sequences = 0
+    *type = 2;
+    return o + 1;
+}
+
 // Bytes of a frame for `len` bytes of content at worst (every block Raw).
 __host__ __device__ __forceinline__ uint64_t frame_bound(uint64_t len) {
     const uint64_t nb = len ? (len + kBlockMax - 1) / kBlockMax : 1;

@@ -92,6 +92,22 @@ def delta_to_json_device(kind, a, b, source_size: int, block_size: int, d_lit, s
         lib.sydelta_delta_free(h)
 
 
+def zstd_compress_device(d_text, stream=None, device: int = 0):
+    """zstd frame (entropy-only blocks) of the bytes of a uint8 device tensor, as a uint8
+    device tensor: the compression ssh.rs:1009-1017 applies to the Delta JSON.  The
+    tensor must start 16-byte aligned (torch allocations and views at offset 0 do)."""
+    import torch
+
+    from .device import _ptr, _stream
+
+    n = d_text.numel()
+    out = torch.empty(int(lib.sydelta_zstd_bound(n)) + 16, dtype=torch.uint8, device=d_text.device)
+    got = ctypes.c_uint64()
+    check(lib.sydelta_zstd_compress_device(device, _ptr(d_text) if n else None, n, _ptr(out), out.numel(),
+                                           ctypes.byref(got), _stream(stream)))
+    return out[:got.value]
+
+
 def delta_from_json(text: bytes):
     """-> (ops as [(kind, len)], literal bytes per Data op, source_size, block_size)."""
     h = ctypes.c_void_p()

@@ -157,7 +157,43 @@ def main():
         n_checks += batch_and_chunk_checks()
         n_checks += error_checks(tmp)
         n_checks += device_walk_checks(tmp)
+        n_checks += zstd_checks()
     print(f"emulated host checks ok: {n_checks}")
+
+
+def zstd_checks():
+    """sydelta_zstd_compress_device's batching and frame assembly (the emulated blocks are
+    sydelta_zstd.hpp's sequential form): frames equal to the test reference encoder's and
+    decoded by the system libzstd, with batches of 1, 3 and 8192 blocks."""
+    import ctypes
+    import json
+    import random
+
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    import test_zstd as Z
+    from sy_amd._lib import check, lib
+
+    if Z._libzstd() is None:
+        return 0
+    rng = random.Random(4)
+    texts = [b"", b"x", b"ab" * 70000, Z.delta_json(rng, 30000, 0.3), bytes(rng.randrange(256) for _ in range(300000))]
+    n = 0
+    for batch in ("1", "3", "8192"):
+        os.environ["SYDELTA_ZSTD_BATCH"] = batch
+        for t in texts:
+            src = np.zeros(len(t) + 16, np.uint8)
+            src[:len(t)] = np.frombuffer(t, np.uint8)
+            cap = int(lib.sydelta_zstd_bound(len(t)))
+            out = np.zeros(cap, np.uint8)
+            got = ctypes.c_uint64()
+            check(lib.sydelta_zstd_compress_device(0, ctypes.c_void_p(src.ctypes.data), len(t),
+                                                   ctypes.c_void_p(out.ctypes.data), cap, ctypes.byref(got), None))
+            frame = out[:got.value].tobytes()
+            assert frame == Z.ref_compress(t), ("zstd", batch, len(t))
+            assert Z.zstd_decode(frame, len(t)) == t
+            n += 1
+    os.environ.pop("SYDELTA_ZSTD_BATCH", None)
+    return n
 
 
 def _walk_counters():

@@ -453,6 +453,39 @@ hipError_t launch_chain(const chain::ChainArgs& a, hipStream_t, Profiler*) {
     return hipSuccess;
 }
 
+// zstd blocks: the sequential form of k_zstd_block (sydelta_zstd.hpp block_content_seq)
+hipError_t launch_zstd_blocks(const uint8_t* d_text, uint64_t len, uint64_t b0, uint32_t nb, uint8_t* d_slots,
+                              uint32_t* d_size, uint32_t* d_type, uint64_t* d_len64, hipStream_t, Profiler*) {
+    EmuTimer emu_t;
+    if (b0 * zstd::kBlockMax >= len) return hipErrorInvalidValue;
+    std::vector<uint8_t> scratch(4 * zstd::kStreamBytesMax);
+    for (uint32_t i = 0; i < nb; ++i) {
+        const uint64_t p = (b0 + i) * zstd::kBlockMax;
+        const uint32_t n = (uint32_t)std::min<uint64_t>(zstd::kBlockMax, len - p);
+        uint32_t type = 0;
+        d_size[i] = zstd::block_content_seq(d_text + p, n, d_slots + (uint64_t)i * zstd::kBlockMax, scratch.data(),
+                                            &type);
+        d_type[i] = type;
+        d_len64[i] = 3ull + d_size[i];
+    }
+    return hipSuccess;
+}
+hipError_t launch_zstd_frame(const uint8_t* d_text, uint64_t len, uint64_t b0, uint32_t nb, uint64_t nblocks,
+                             const uint8_t* d_slots, const uint32_t* d_size, const uint32_t* d_type, const uint64_t* d_off,
+                             uint64_t base, uint8_t* d_out, hipStream_t, Profiler*) {
+    EmuTimer emu_t;
+    for (uint32_t i = 0; i < nb; ++i) {
+        const uint64_t gb = b0 + i;
+        const uint32_t n = (uint32_t)std::min<uint64_t>(zstd::kBlockMax, len - gb * zstd::kBlockMax);
+        uint8_t* o = d_out + base + d_off[i];
+        if (gb == 0) zstd::frame_header(d_out, len);
+        zstd::block_header(o, gb + 1 == nblocks, d_type[i], d_type[i] == 2 ? d_size[i] : n);
+        const uint8_t* src = d_type[i] == 2 ? d_slots + (uint64_t)i * zstd::kBlockMax : d_text + gb * zstd::kBlockMax;
+        memcpy(o + 3, src, d_size[i]);
+    }
+    return hipSuccess;
+}
+
 hipError_t launch_exclusive_sum_u64(const uint64_t* d_in, uint64_t* d_out, uint64_t n, hipStream_t) {
     EmuTimer emu_t;
     uint64_t acc = 0;
