@@ -2438,7 +2438,7 @@ __global__ __launch_bounds__(kZT) void k_zstd_block(const uint8_t* __restrict__ 
                                                     uint8_t* __restrict__ slots, uint32_t* __restrict__ size_out,
                                                     uint32_t* __restrict__ type_out, uint64_t* __restrict__ len64) {
     __shared__ ZLds L;
-    const uint32_t tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+    const uint32_t tid = threadIdx.x, wid = tid >> 6;
     const uint64_t gb = b0 + blockIdx.x;
     const uint8_t* in = text + gb * zstd::kBlockMax;
     const uint32_t n = (uint32_t)min<uint64_t>(zstd::kBlockMax, len - gb * zstd::kBlockMax);
