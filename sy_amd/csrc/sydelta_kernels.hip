@@ -2412,12 +2412,15 @@ __global__ void k_chain_finish(chain::ChainArgs a) {
 // ===========================================================================
 // K7z: zstd frame of a text in HBM (sydelta_zstd.hpp; ssh.rs:1009-1017)
 // ===========================================================================
-// One workgroup per 128 KiB block: a byte histogram (per-wave LDS sub-histograms), the
-// Huffman code by one thread (huf_build, scratch in LDS), then per literal stream a
-// parallel bit scatter: thread t encodes a contiguous run of the stream's symbols, its
-// first bit at the sum of the later runs' bits (the stream is written last symbol
-// first), OR-ing whole 32-bit words into an LDS stream buffer; the stream leaves for the
-// block's slot with its closing 1 bit.  The slot holds the block content; k_zstd_frame
+// One workgroup per 128 KiB block.  Entropy-only content: a byte histogram (per-wave LDS
+// sub-histograms), the Huffman code by one thread (huf_build, scratch in LDS), then per
+// literal stream a parallel bit scatter: thread t encodes a contiguous run of the
+// stream's symbols, its first bit at the sum of the later runs' bits (the stream is
+// written last symbol first), OR-ing whole 32-bit words into an LDS stream buffer; the
+// stream leaves for the block's slot with its closing 1 bit.  Literals + sequences: the
+// '{' distances and every position's best candidate match in parallel, then (when enough
+// positions match) one thread parses, codes the literals and FSE-codes the sequences with
+// the shared sequential functions; the smaller content stays in the slot.  k_zstd_frame
 // then lays the blocks out behind their headers.
 constexpr int kZT = 256;
 constexpr uint32_t kZRun = 144;  // bytes of a stream per thread: 256 runs cover 32 KiB + the 16-byte phase
@@ -2430,20 +2433,27 @@ struct ZLds {
     uint32_t words[kZStreamWords];
     zstd::HufCode code;
     zstd::HufWork work;
+    zstd::FseCT tll, tml, tof;
+    uint32_t gaps[256];
+    uint32_t cand[zstd::kCands];
     uint32_t ssize[4];
-    uint32_t state[4];  // [0] type (0 Raw, 1 RLE, 2 Compressed), [1] write offset in the slot, [2] abort
+    uint32_t state[8];  // [0] type, [1] write offset, [2] abort, [3] entropy-only size, [4] nc, [5] nbest, [6] lz size
 };
 
 __global__ __launch_bounds__(kZT) void k_zstd_block(const uint8_t* __restrict__ text, uint64_t len, uint64_t b0,
-                                                    uint8_t* __restrict__ slots, uint32_t* __restrict__ size_out,
-                                                    uint32_t* __restrict__ type_out, uint64_t* __restrict__ len64) {
+                                                    uint8_t* __restrict__ slots, zstd::SeqScratch* __restrict__ lz,
+                                                    uint32_t* __restrict__ size_out, uint32_t* __restrict__ type_out,
+                                                    uint64_t* __restrict__ len64) {
     __shared__ ZLds L;
     const uint32_t tid = threadIdx.x, wid = tid >> 6;
     const uint64_t gb = b0 + blockIdx.x;
     const uint8_t* in = text + gb * zstd::kBlockMax;
     const uint32_t n = (uint32_t)min<uint64_t>(zstd::kBlockMax, len - gb * zstd::kBlockMax);
     uint8_t* slot = slots + (uint64_t)blockIdx.x * zstd::kBlockMax;
+    zstd::SeqScratch* sc = lz + blockIdx.x;
     for (uint32_t i = tid; i < 4 * 256; i += kZT) (&L.hist[0][0])[i] = 0;
+    for (uint32_t i = tid; i < 256; i += kZT) L.gaps[i] = 0;
+    if (tid == 0) L.state[5] = 0;
     __syncthreads();
     // histogram, 16 bytes per load (the text is 16-byte aligned and readable to the end
     // of its last granule); bytes past n are not counted
@@ -2463,20 +2473,20 @@ __global__ __launch_bounds__(kZT) void k_zstd_block(const uint8_t* __restrict__ 
         uint32_t distinct = 0, hi = 0;
         for (uint32_t s = 0; s < 256; ++s)
             if (L.hist[0][s]) { ++distinct; hi = s; }
-        uint32_t type = 0;
+        uint32_t type = 0;  // Raw until a content smaller than n turns up
         if (distinct == 1 && n > 1) type = 1;
-        else if (distinct >= 2 && hi < zstd::kSymbols) type = 2;
         L.state[0] = type;
-        L.state[2] = 0;
-        if (type == 2) {
+        L.state[2] = (distinct >= 2 && hi < zstd::kSymbols) ? 0u : 1u;  // entropy-only coding possible?
+        L.state[3] = 0xFFFFFFFFu;
+        if (!L.state[2] && type == 0) {
             zstd::huf_build(L.hist[0], L.code, L.work);
             const uint32_t tsz = zstd::huf_tree_desc(L.code, slot + hs);
             L.state[1] = hs + tsz + (four ? 6u : 0u);  // the first stream's offset
         }
     }
     __syncthreads();
-    const uint32_t type = L.state[0];
-    if (type == 2) {
+    const uint32_t rle = L.state[0];
+    if (!rle && !L.state[2]) {
         const uint32_t ns = four ? 4u : 1u;
         for (uint32_t st = 0; st < ns; ++st) {
             uint32_t first, count;
@@ -2533,7 +2543,7 @@ __global__ __launch_bounds__(kZT) void k_zstd_block(const uint8_t* __restrict__ 
             __syncthreads();
             const uint32_t bytes = total / 8 + 1;
             const uint32_t o = L.state[1];
-            // a stream that would not fit the block's own size: store the block Raw
+            // a stream that would not fit the block's own size: no entropy-only content
             const bool fits = o + bytes + 1 < n && (four || o + bytes - hs <= zstd::kSingleStreamMax);
             if (fits) {
                 const uint8_t* wb = (const uint8_t*)L.words;
@@ -2548,14 +2558,9 @@ __global__ __launch_bounds__(kZT) void k_zstd_block(const uint8_t* __restrict__ 
             __syncthreads();
             if (L.state[2]) break;
         }
-    }
-    if (tid == 0) {
-        uint32_t t = type, size = 0;
-        if (t == 2 && L.state[2]) t = 0;
-        if (t == 2) {
-            const uint32_t end = L.state[1];  // past the last stream
-            const uint32_t comp = end - hs;
-            zstd::lit_header(slot, four, n, comp);
+        if (tid == 0 && !L.state[2]) {  // the entropy-only content is complete
+            const uint32_t end = L.state[1];
+            zstd::lit_header(slot, four, n, end - hs);
             if (four) {
                 const uint32_t tsz = 1 + (L.code.last + 1) / 2;
                 for (uint32_t k = 0; k < 3; ++k) {
@@ -2564,11 +2569,58 @@ __global__ __launch_bounds__(kZT) void k_zstd_block(const uint8_t* __restrict__ 
                 }
             }
             slot[end] = 0;  // Sequences_Section: Number_of_Sequences = 0
-            size = end + 1;
-            if (size >= n) t = 0;
+            L.state[3] = end + 1;
         }
-        if (t == 1) size = 1;
-        if (t == 0) size = n;
+    }
+    // literals + sequences
+    if (!rle && n >= 2) {
+        for (uint32_t p = tid; p < n; p += kZT)
+            if (in[p] == '{') {
+                uint32_t seen = 0;  // zstd::gap_count with LDS atomics
+                for (uint32_t d = 1; d < 256 && d <= p && seen < 3; ++d)
+                    if (in[p - d] == '{') {
+                        atomicAdd(&L.gaps[d], 1u);
+                        ++seen;
+                    }
+            }
+        __syncthreads();
+        if (tid == 0) {
+            L.state[4] = zstd::pick_cands(L.gaps, L.cand);
+            int16_t nrm[53];
+            for (uint32_t i = 0; i < 36; ++i) nrm[i] = zstd::ll_norm(i);
+            zstd::fse_build(L.tll, nrm, 36, 6);
+            for (uint32_t i = 0; i < 53; ++i) nrm[i] = zstd::ml_norm(i);
+            zstd::fse_build(L.tml, nrm, 53, 6);
+            for (uint32_t i = 0; i < 29; ++i) nrm[i] = zstd::of_norm(i);
+            zstd::fse_build(L.tof, nrm, 29, 5);
+        }
+        __syncthreads();
+        const uint32_t nc = L.state[4];
+        uint32_t mine = 0;
+        for (uint32_t p = tid; p < n; p += kZT) {
+            const uint32_t b = zstd::best_at(in, n, p, L.cand, nc);
+            sc->best[p] = b;
+            mine += b != 0;
+        }
+        if (mine) atomicAdd(&L.state[5], mine);
+        __syncthreads();
+        if (zstd::lz_worth(L.state[5], n)) {
+            if (tid == 0) {
+                const uint32_t z = zstd::lz_content(in, n, L.cand, sc, L.hist[1], L.code, L.work, L.tll, L.tml, L.tof);
+                L.state[6] = (z && z < L.state[3]) ? z : 0u;
+            }
+            __syncthreads();
+            const uint32_t z = L.state[6];
+            for (uint32_t i = tid; i < z; i += kZT) slot[i] = sc->body[i];
+            if (tid == 0 && z) L.state[3] = z;
+        }
+    }
+    if (tid == 0) {
+        uint32_t t = rle ? 1u : 0u, size = rle ? 1u : n;
+        if (!rle && L.state[3] < n) {
+            t = 2;
+            size = L.state[3];
+        }
         type_out[blockIdx.x] = t;
         size_out[blockIdx.x] = size;
         len64[blockIdx.x] = 3ull + size;
@@ -3479,11 +3531,13 @@ hipError_t launch_sort_hits(uint64_t* key, uint32_t* val, uint64_t* key_tmp, uin
 }
 
 hipError_t launch_zstd_blocks(const uint8_t* d_text, uint64_t len, uint64_t b0, uint32_t nb, uint8_t* d_slots,
-                              uint32_t* d_size, uint32_t* d_type, uint64_t* d_len64, hipStream_t s, Profiler* prof) {
+                              zstd::SeqScratch* d_lz, uint32_t* d_size, uint32_t* d_type, uint64_t* d_len64,
+                              hipStream_t s, Profiler* prof) {
     if (!nb) return hipSuccess;
     if (b0 * zstd::kBlockMax >= len) return hipErrorInvalidValue;
     ProfScope ps(prof, s, "k_zstd_block");
-    hipLaunchKernelGGL(k_zstd_block, dim3(nb), dim3(kZT), 0, s, d_text, len, b0, d_slots, d_size, d_type, d_len64);
+    hipLaunchKernelGGL(k_zstd_block, dim3(nb), dim3(kZT), 0, s, d_text, len, b0, d_slots, d_lz, d_size, d_type,
+                       d_len64);
     return hipGetLastError();
 }
 

@@ -510,7 +510,7 @@ extern "C" int sydelta_delta_to_json_device(const sydelta_delta* d, const uint8_
 
 // ---------------------------------------------------------------------------
 // zstd frame of a text in HBM (ssh.rs:1009-1017: compress(delta_json, Compression::Zstd);
-// sydelta_zstd.hpp).  The text goes through in batches of 8192 blocks (1 GiB): block
+// sydelta_zstd.hpp).  The text goes through in batches of 512 blocks (64 MiB): block
 // contents into per-block slots (k_zstd_block), their placement (an exclusive scan of
 // 3 + content), then the frame (k_zstd_frame); scratch is one batch of slots.
 // ---------------------------------------------------------------------------
@@ -537,17 +537,19 @@ extern "C" int sydelta_zstd_compress_device(int device, const uint8_t* d_in, uin
         return SYDELTA_OK;
     }
     const uint64_t nblocks = (len + zstd::kBlockMax - 1) / zstd::kBlockMax;
-    uint64_t kBatch = 8192;  // blocks per batch; SYDELTA_ZSTD_BATCH overrides (tests)
+    uint64_t kBatch = 512;  // blocks per batch (64 MiB of text, ~0.7 GiB of scratch); SYDELTA_ZSTD_BATCH overrides
     if (const char* e = getenv("SYDELTA_ZSTD_BATCH"))
         if (const uint64_t v = strtoull(e, nullptr, 10)) kBatch = std::min<uint64_t>(v, 1 << 20);
     const uint64_t nb_max = std::min<uint64_t>(nblocks, kBatch);
     auto al = [](uint64_t b) { return (b + 255) & ~(uint64_t)255; };
-    const uint64_t o_size = al(nb_max * zstd::kBlockMax), o_type = o_size + al(4 * nb_max);
+    const uint64_t o_lz = al(nb_max * zstd::kBlockMax), o_size = o_lz + al(nb_max * sizeof(zstd::SeqScratch));
+    const uint64_t o_type = o_size + al(4 * nb_max);
     const uint64_t o_len = o_type + al(4 * nb_max), o_off = o_len + al(8 * nb_max), total = o_off + al(8 * nb_max);
     DevBuf_wire buf;
     HIP_TRY(hipMallocAsync(&buf.p, total, s));
     buf.s = s;
     uint8_t* B = (uint8_t*)buf.p;
+    zstd::SeqScratch* d_lz = (zstd::SeqScratch*)(B + o_lz);
     uint32_t* d_size = (uint32_t*)(B + o_size);
     uint32_t* d_type = (uint32_t*)(B + o_type);
     uint64_t* d_len = (uint64_t*)(B + o_len);
@@ -556,7 +558,7 @@ extern "C" int sydelta_zstd_compress_device(int device, const uint8_t* d_in, uin
     uint64_t pos = zstd::kFrameHeader;
     for (uint64_t b0 = 0; b0 < nblocks; b0 += kBatch) {
         const uint32_t nb = (uint32_t)std::min<uint64_t>(kBatch, nblocks - b0);
-        HIP_TRY(launch_zstd_blocks(d_in, len, b0, nb, B, d_size, d_type, d_len, s, cp.get()));
+        HIP_TRY(launch_zstd_blocks(d_in, len, b0, nb, B, d_lz, d_size, d_type, d_len, s, cp.get()));
         HIP_TRY(launch_exclusive_sum_u64(d_len, d_off, nb, s));
         HIP_TRY(launch_zstd_frame(d_in, len, b0, nb, nblocks, B, d_size, d_type, d_off, pos, d_out, s, cp.get()));
         uint64_t last[2] = {0, 0};

@@ -181,58 +181,418 @@ __host__ __device__ __forceinline__ void stream_range(uint32_t regen, bool four,
     count = end - first;
 }
 
-// The sequential form of one block (the host emulation of the device layer and the
-// tests' reference encoder): writes the Compressed block content into slot (kBlockMax
-// bytes) and returns its size with *type = 2, or returns n with *type = 0 (store Raw) /
-// 1 with *type = 1 (RLE).  scratch holds 4 * kStreamBytesMax bytes.  k_zstd_block
-// produces the same bytes with a parallel bit scatter.
-__host__ inline uint32_t block_content_seq(const uint8_t* in, uint32_t n, uint8_t* slot, uint8_t* scratch,
-                                           uint32_t* type) {
-    uint32_t h[256] = {0};
-    for (uint32_t i = 0; i < n; ++i) ++h[in[i]];
+// ---------------------------------------------------------------------------
+// Sequences (matches): RFC 8878 3.1.1.3.2, predefined FSE tables only
+// ---------------------------------------------------------------------------
+// A Delta's JSON repeats one skeleton per op ({"Copy":{"offset":...,"size":...}}), so the
+// matches that pay are at the distance of the previous op's text.  Candidate distances
+// are the block's most common gaps between consecutive '{' (and 1, runs); each position's
+// best candidate is found independently (the device does all positions at once), a
+// greedy parse takes a match of >= kMinMatch wherever one starts, and the sequences are
+// FSE-coded with the predefined distributions (no table descriptions).  A block whose
+// matches cover less than 1/8 of it stays entropy-only.
+constexpr uint32_t kMinMatch = 4;
+constexpr uint32_t kProbe = 32;     // bytes compared per candidate when ranking them
+constexpr uint32_t kCands = 5;      // candidate distances: 1 and the 4 most common '{' gaps
+constexpr uint32_t kMaxSeq = kBlockMax / kMinMatch;
+
+// RFC 8878 3.1.1.3.2.2: predefined distributions (accuracy logs 6, 6, 5).
+__host__ __device__ __forceinline__ int16_t ll_norm(uint32_t s) {
+    constexpr int16_t t[36] = {4, 3, 2, 2, 2, 2, 2, 2, 2, 2, 2, 2, 2, 1, 1, 1, 2, 2,
+                               2, 2, 2, 2, 2, 2, 2, 3, 2, 1, 1, 1, 1, 1, -1, -1, -1, -1};
+    return t[s];
+}
+__host__ __device__ __forceinline__ int16_t ml_norm(uint32_t s) {
+    constexpr int16_t t[53] = {1, 4, 3, 2, 2, 2, 2, 2, 2, 1, 1, 1, 1, 1, 1, 1, 1, 1,
+                               1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1,
+                               1, 1, 1, 1, 1, 1, 1, 1, 1, 1, -1, -1, -1, -1, -1, -1, -1};
+    return t[s];
+}
+__host__ __device__ __forceinline__ int16_t of_norm(uint32_t s) {
+    constexpr int16_t t[29] = {1, 1, 1, 1, 1, 1, 2, 2, 2, 1, 1, 1, 1, 1, 1,
+                               1, 1, 1, 1, 1, 1, 1, 1, 1, -1, -1, -1, -1, -1};
+    return t[s];
+}
+
+// Literals_Length / Match_Length codes (RFC 8878 3.1.1.3.2.1.1): code, its extra bits.
+__host__ __device__ __forceinline__ void ll_code(uint32_t ll, uint32_t& code, uint32_t& bits) {
+    constexpr uint32_t base[36] = {0,  1,  2,  3,  4,  5,  6,   7,   8,   9,   10,   11,   12,   13,    14,    15,    16,   18,
+                                   20, 22, 24, 28, 32, 40, 48, 64, 128, 256, 512, 1024, 2048, 4096, 8192, 16384, 32768, 65536};
+    constexpr uint8_t nb[36] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 1, 1,
+                                1, 1, 2, 2, 3, 3, 4, 6, 7, 8, 9, 10, 11, 12, 13, 14, 15, 16};
+    uint32_t c = 35;
+    while (base[c] > ll) --c;
+    code = c;
+    bits = nb[c];
+}
+__host__ __device__ __forceinline__ void ml_code(uint32_t ml, uint32_t& code, uint32_t& bits) {
+    constexpr uint32_t base[21] = {35,  37,  39,   41,   43,   47,   51,   59,    67,    83,   99,
+                                   131, 259, 515, 1027, 2051, 4099, 8195, 16387, 32771, 65539};
+    constexpr uint8_t nb[21] = {1, 1, 1, 1, 2, 2, 3, 3, 4, 4, 5, 7, 8, 9, 10, 11, 12, 13, 14, 15, 16};
+    if (ml < 35) { code = ml - 3; bits = 0; return; }
+    uint32_t c = 20;
+    while (base[c] > ml) --c;
+    code = 32 + c;
+    bits = nb[c];
+}
+
+// One FSE compression table built from a normalized distribution (zstd's
+// FSE_buildCTable: symbols spread with step 5/8 table + 3, "less than 1" symbols in the
+// top cells, state table sorted by symbol).
+struct FseCT {
+    uint16_t state[64];     // next-state table (tableSize entries)
+    int32_t delta_nb[53];   // deltaNbBits per symbol
+    int32_t delta_find[53]; // deltaFindState per symbol
+    uint32_t log;
+};
+__host__ __device__ inline void fse_build(FseCT& t, const int16_t* norm, uint32_t nsym, uint32_t log) {
+    const uint32_t size = 1u << log, mask = size - 1, step = (size >> 1) + (size >> 3) + 3;
+    uint8_t sym[64];
+    uint32_t cumul[54];
+    uint32_t high = size - 1;
+    cumul[0] = 0;
+    for (uint32_t u = 1; u <= nsym; ++u) {
+        if (norm[u - 1] == -1) {
+            cumul[u] = cumul[u - 1] + 1;
+            sym[high--] = (uint8_t)(u - 1);
+        } else {
+            cumul[u] = cumul[u - 1] + (uint32_t)norm[u - 1];
+        }
+    }
+    uint32_t pos = 0;
+    for (uint32_t s = 0; s < nsym; ++s)
+        for (int k = 0; k < norm[s]; ++k) {
+            sym[pos] = (uint8_t)s;
+            pos = (pos + step) & mask;
+            while (pos > high) pos = (pos + step) & mask;
+        }
+    for (uint32_t u = 0; u < size; ++u) t.state[cumul[sym[u]]++] = (uint16_t)(size + u);
+    int32_t total = 0;
+    for (uint32_t s = 0; s < nsym; ++s) {
+        const int n = norm[s];
+        if (n == -1 || n == 1) {
+            t.delta_nb[s] = (int32_t)((log << 16) - (1u << log));
+            t.delta_find[s] = total - 1;
+            total += 1;
+        } else {
+            uint32_t hb = 0;
+            while ((2u << hb) <= (uint32_t)(n - 1)) ++hb;  // highbit(n - 1), n >= 2
+            const uint32_t max_out = log - hb;
+            t.delta_nb[s] = (int32_t)((max_out << 16) - ((uint32_t)n << max_out));
+            t.delta_find[s] = total - n;
+            total += n;
+        }
+    }
+    t.log = log;
+}
+
+// Backward bitstream writer (zstd's BIT_CStream): bits LSB-first, whole bytes out.
+struct BitW {
+    uint8_t* p;
+    uint32_t bytes;
+    uint64_t acc;
+    uint32_t nb;
+    __host__ __device__ void add(uint64_t v, uint32_t n) {
+        if (!n) return;
+        acc |= (v & ((1ull << n) - 1)) << nb;
+        nb += n;
+        while (nb >= 8) { p[bytes++] = (uint8_t)acc; acc >>= 8; nb -= 8; }
+    }
+    __host__ __device__ void close() {
+        add(1, 1);
+        if (nb) { p[bytes++] = (uint8_t)acc; acc = 0; nb = 0; }
+    }
+};
+__host__ __device__ __forceinline__ uint32_t fse_init(const FseCT& t, uint32_t s) {
+    const uint32_t nbo = (uint32_t)((t.delta_nb[s] + (1 << 15)) >> 16);
+    const uint32_t v = (nbo << 16) - (uint32_t)t.delta_nb[s];
+    return t.state[(v >> nbo) + t.delta_find[s]];
+}
+__host__ __device__ __forceinline__ void fse_encode(BitW& w, const FseCT& t, uint32_t& st, uint32_t s) {
+    const uint32_t nbo = (uint32_t)((int32_t)st + t.delta_nb[s]) >> 16;
+    w.add(st, nbo);
+    st = t.state[(st >> nbo) + t.delta_find[s]];
+}
+
+struct Seq {
+    uint32_t ll, ml, off;  // literal length, match length (>= kMinMatch), distance
+};
+
+// The three predefined tables (built once on the host; the device builds them in LDS).
+struct FseTables {
+    FseCT ll, ml, of;
+    __host__ static const FseTables& get() {
+        static const FseTables t = [] {
+            FseTables x;
+            int16_t n[53];
+            for (uint32_t i = 0; i < 36; ++i) n[i] = ll_norm(i);
+            fse_build(x.ll, n, 36, 6);
+            for (uint32_t i = 0; i < 53; ++i) n[i] = ml_norm(i);
+            fse_build(x.ml, n, 53, 6);
+            for (uint32_t i = 0; i < 29; ++i) n[i] = of_norm(i);
+            fse_build(x.of, n, 29, 5);
+            return x;
+        }();
+        return t;
+    }
+};
+
+// Sequences_Section of ns sequences into p (predefined tables); returns its size.  Order
+// of zstd's ZSTD_encodeSequences: the last sequence starts the states, then every earlier
+// one from the end: OF, ML, LL state bits, then LL, ML, OF extra bits; states flushed ML,
+// OF, LL (the decoder reads LL, OF, ML first).
+__host__ __device__ inline uint32_t seq_section(const Seq* sq, uint32_t ns, uint8_t* p, const FseCT& tll,
+                                                const FseCT& tml, const FseCT& tof) {
+    uint32_t o = 0;
+    if (ns < 128) {
+        p[o++] = (uint8_t)ns;
+    } else if (ns < 0x7F00) {
+        p[o++] = (uint8_t)((ns >> 8) + 0x80);
+        p[o++] = (uint8_t)ns;
+    } else {
+        p[o++] = 0xFF;
+        p[o++] = (uint8_t)(ns - 0x7F00);
+        p[o++] = (uint8_t)((ns - 0x7F00) >> 8);
+    }
+    if (!ns) return o;
+    p[o++] = 0;  // Symbol_Compression_Modes: LL, OF, ML predefined
+    BitW w{p + o, 0, 0, 0};
+    auto codes = [&](const Seq& q, uint32_t& lc, uint32_t& lb, uint32_t& mc, uint32_t& mb, uint32_t& oc,
+                     uint32_t& ob) {
+        ll_code(q.ll, lc, lb);
+        ml_code(q.ml, mc, mb);
+        ob = q.off + 3;  // Offset_Value: a distance, never a repeat code
+        oc = 0;
+        while ((2u << oc) <= ob) ++oc;
+    };
+    uint32_t lc, lb, mc, mb, oc, ov;
+    codes(sq[ns - 1], lc, lb, mc, mb, oc, ov);
+    uint32_t sml = fse_init(tml, mc), sof = fse_init(tof, oc), sll = fse_init(tll, lc);
+    w.add(sq[ns - 1].ll, lb);
+    w.add(sq[ns - 1].ml - 3, mb);
+    w.add(ov, oc);
+    for (uint32_t i = ns - 1; i-- > 0;) {
+        codes(sq[i], lc, lb, mc, mb, oc, ov);
+        fse_encode(w, tof, sof, oc);
+        fse_encode(w, tml, sml, mc);
+        fse_encode(w, tll, sll, lc);
+        w.add(sq[i].ll, lb);
+        w.add(sq[i].ml - 3, mb);
+        w.add(ov, oc);
+    }
+    w.add(sml, tml.log);
+    w.add(sof, tof.log);
+    w.add(sll, tll.log);
+    w.close();
+    return o + w.bytes;
+}
+
+// Raw_Literals_Block header (1, 2 or 3 bytes by size); returns its size.
+__host__ __device__ __forceinline__ uint32_t raw_lit_header(uint8_t* p, uint32_t n) {
+    if (n < 32) { p[0] = (uint8_t)(n << 3); return 1; }
+    if (n < 4096) { p[0] = (uint8_t)((1u << 2) | ((n & 15) << 4)); p[1] = (uint8_t)(n >> 4); return 2; }
+    p[0] = (uint8_t)((3u << 2) | ((n & 15) << 4)); p[1] = (uint8_t)(n >> 4); p[2] = (uint8_t)(n >> 12);
+    return 3;
+}
+
+// The '{' at p counts its distances (<= 255) to the three '{' before it: a Copy op's
+// text holds two, so its distance to the previous op's is the second or third.
+__host__ __device__ __forceinline__ void gap_count(const uint8_t* in, uint32_t p, uint32_t* gaps) {
+    uint32_t seen = 0;
+    for (uint32_t d = 1; d < 256 && d <= p && seen < 3; ++d)
+        if (in[p - d] == '{') {
+            ++gaps[d];
+            ++seen;
+        }
+}
+
+// Candidate distances of a block: 1, then the most common '{' distances (gap_count),
+// ties to the smaller distance.  Returns the count (<= kCands).
+__host__ __device__ inline uint32_t pick_cands(const uint32_t* gaps, uint32_t* cand) {
+    uint32_t k = 0;
+    cand[k++] = 1;
+    uint32_t used[kCands] = {1, 0, 0, 0, 0};
+    while (k < kCands) {
+        uint32_t best = 0, bc = 0;
+        for (uint32_t g = 2; g < 256; ++g) {
+            bool dup = false;
+            for (uint32_t j = 0; j < k; ++j) dup |= used[j] == g;
+            if (!dup && gaps[g] > bc) { bc = gaps[g]; best = g; }
+        }
+        if (!bc) break;
+        cand[k] = best;
+        used[k] = best;
+        ++k;
+    }
+    return k;
+}
+
+// Best candidate at position p of in[0, n): the longest match (compared up to kProbe
+// bytes) among the candidates, ties to the earlier candidate; 0 when < kMinMatch.
+// Packed as (length << 8) | candidate index.
+__host__ __device__ __forceinline__ uint32_t best_at(const uint8_t* in, uint32_t n, uint32_t p, const uint32_t* cand,
+                                                     uint32_t nc) {
+    uint32_t bl = 0, bi = 0;
+    for (uint32_t c = 0; c < nc; ++c) {
+        const uint32_t d = cand[c];
+        if (d > p) continue;
+        uint32_t l = 0;
+        const uint32_t lim = (n - p) < kProbe ? (n - p) : kProbe;
+        while (l < lim && in[p + l] == in[p + l - d]) ++l;
+        if (l > bl) { bl = l; bi = c; }
+    }
+    return bl >= kMinMatch ? (bl << 8) | bi : 0;
+}
+
+// Greedy parse of a block from the per-position bests: a match wherever one starts
+// (extended past kProbe bytes as far as it goes), a literal otherwise.  Literal bytes
+// are gathered into lit.  Returns the number of sequences; *nlit = literals (including
+// the last ones, after the last sequence); *covered = matched bytes.
+__host__ __device__ inline uint32_t greedy_parse(const uint8_t* in, uint32_t n, const uint32_t* best,
+                                                 const uint32_t* cand, Seq* sq, uint8_t* lit, uint32_t* nlit,
+                                                 uint32_t* covered) {
+    uint32_t p = 0, ls = 0, ns = 0, nl = 0, cov = 0;
+    while (p < n) {
+        const uint32_t b = best[p];
+        if (!b) { lit[nl++] = in[p++]; continue; }
+        const uint32_t d = cand[b & 0xFF];
+        uint32_t l = b >> 8;
+        if (l == kProbe)
+            while (p + l < n && in[p + l] == in[p + l - d]) ++l;
+        sq[ns++] = Seq{p - ls, l, d};
+        cov += l;
+        p += l;
+        ls = p;
+    }
+    *nlit = nl;
+    *covered = cov;
+    return ns;
+}
+
+// Literals section of lit[0, nl): Huffman-coded (4 streams above kSingleStreamMax
+// literals, else 1) when that is possible and smaller than the raw section, else Raw.
+// scratch holds 4 * kStreamBytesMax bytes.  Returns its size (<= nl + 3).
+__host__ __device__ inline uint32_t lit_section_seq(const uint8_t* lit, uint32_t nl, uint8_t* out, uint8_t* scratch,
+                                                    uint32_t* h, HufCode& c, HufWork& wk) {
+    for (uint32_t s = 0; s < 256; ++s) h[s] = 0;
+    for (uint32_t i = 0; i < nl; ++i) ++h[lit[i]];
     uint32_t distinct = 0, hi = 0;
     for (uint32_t s = 0; s < 256; ++s)
         if (h[s]) { ++distinct; hi = s; }
-    *type = 0;
-    if (distinct == 1 && n > 1) { *type = 1; return 1; }
-    if (distinct < 2 || hi >= kSymbols) return n;
-    HufCode c;
-    HufWork wk;
+    auto raw = [&]() -> uint32_t {
+        const uint32_t hs = raw_lit_header(out, nl);
+        for (uint32_t i = 0; i < nl; ++i) out[hs + i] = lit[i];
+        return hs + nl;
+    };
+    const uint32_t raw_size = nl + (nl < 32 ? 1 : nl < 4096 ? 2 : 3);
+    if (distinct < 2 || hi >= kSymbols) return raw();
     huf_build(h, c, wk);
-    const bool four = n > kSingleStreamMax;
+    const bool four = nl > kSingleStreamMax;
     const uint32_t hs = four ? 5 : 3;
-    const uint32_t tsz = huf_tree_desc(c, slot + hs);
+    const uint32_t tsz = huf_tree_desc(c, out + hs);
     uint32_t o = hs + tsz + (four ? 6 : 0);
     uint32_t ssz[4] = {0, 0, 0, 0};
     for (uint32_t st = 0; st < (four ? 4u : 1u); ++st) {
         uint32_t f, cnt;
-        stream_range(n, four, st, f, cnt);
+        stream_range(nl, four, st, f, cnt);
         // symbols last to first, LSB-first, then the closing 1 bit (BIT_closeCStream)
         uint8_t* w = scratch + st * kStreamBytesMax;
         uint32_t bytes = 0, nb = 0;
         uint64_t acc = 0;
         for (uint32_t i = cnt; i-- > 0;) {
-            acc |= (uint64_t)c.code[in[f + i]] << nb;
-            nb += c.len[in[f + i]];
+            acc |= (uint64_t)c.code[lit[f + i]] << nb;
+            nb += c.len[lit[f + i]];
             while (nb >= 8) { w[bytes++] = (uint8_t)acc; acc >>= 8; nb -= 8; }
         }
         acc |= 1ull << nb;
         ++nb;
         while (nb > 0) { w[bytes++] = (uint8_t)acc; acc >>= 8; nb = nb > 8 ? nb - 8 : 0; }
-        if (o + bytes + 1 >= n || (!four && o + bytes - hs > kSingleStreamMax)) return n;  // not smaller: Raw
-        for (uint32_t i = 0; i < bytes; ++i) slot[o + i] = w[i];
+        if (o + bytes >= raw_size || (!four && o + bytes - hs > kSingleStreamMax)) return raw();
+        for (uint32_t i = 0; i < bytes; ++i) out[o + i] = w[i];
         o += bytes;
         ssz[st] = bytes;
     }
-    lit_header(slot, four, n, o - hs);
+    lit_header(out, four, nl, o - hs);
     if (four)
         for (uint32_t k = 0; k < 3; ++k) {
-            slot[hs + tsz + 2 * k] = (uint8_t)ssz[k];
-            slot[hs + tsz + 2 * k + 1] = (uint8_t)(ssz[k] >> 8);
+            out[hs + tsz + 2 * k] = (uint8_t)ssz[k];
+            out[hs + tsz + 2 * k + 1] = (uint8_t)(ssz[k] >> 8);
         }
-    slot[o] = 0;  // Sequences_Section: Number_of_Sequences = 0
+    return o;
+}
+
+// Scratch of the literals + sequences coding of one block: per position bests,
+// sequences, literals, stream bytes, the content (the device keeps one per block in HBM).
+struct SeqScratch {
+    uint32_t best[kBlockMax];
+    Seq seq[kMaxSeq];
+    uint8_t lit[kBlockMax];
+    uint8_t streams[4 * kStreamBytesMax];
+    // a sequence costs at most 57 bits (LL and ML codes + 16 extra bits each, OF code 8 +
+    // 8 extra bits) and covers >= kMinMatch bytes: content <= nl + 7 + 7.2 (n - nl) / 4 < 2n
+    uint8_t body[2 * kBlockMax + 64];
+    uint32_t h[256];       // host only (the device uses its LDS copies)
+    HufCode code;
+    HufWork work;
+};
+
+// The literals + sequences content of a block whose bests are in sc.best: greedy parse,
+// literals section, sequences section into sc.body.  Returns its size, or 0 when the
+// block has no match.  One thread (the device's thread 0) runs it.
+__host__ __device__ inline uint32_t lz_content(const uint8_t* in, uint32_t n, const uint32_t* cand, SeqScratch* sc,
+                                               uint32_t* h, HufCode& c, HufWork& wk, const FseCT& tll,
+                                               const FseCT& tml, const FseCT& tof) {
+    uint32_t nl = 0, cov = 0;
+    const uint32_t ns = greedy_parse(in, n, sc->best, cand, sc->seq, sc->lit, &nl, &cov);
+    if (!ns) return 0;
+    uint32_t z = lit_section_seq(sc->lit, nl, sc->body, sc->streams, h, c, wk);
+    z += seq_section(sc->seq, ns, sc->body + z, tll, tml, tof);
+    return z;
+}
+
+// Whether a block tries literals + sequences: at least 1/32 of its positions have a
+// candidate match (literal-heavy JSON has almost none and stays entropy-only).
+__host__ __device__ __forceinline__ bool lz_worth(uint32_t nbest, uint32_t n) { return (uint64_t)nbest * 32 >= n; }
+
+// The sequential form of one block (the host emulation of the device layer and the
+// tests' reference encoder): writes the Compressed block content into slot (kBlockMax
+// bytes) and returns its size with *type = 2, or returns n with *type = 0 (store Raw) /
+// 1 with *type = 1 (RLE).  A block whose candidate matches cover >= 1/8 of it is coded
+// as literals + sequences, any other as literals only.  k_zstd_block produces the same
+// bytes with parallel histograms, candidate search and bit scatter.
+__host__ inline uint32_t block_content_seq(const uint8_t* in, uint32_t n, uint8_t* slot, SeqScratch& sc,
+                                           uint32_t* type) {
+    uint32_t h[256] = {0};
+    for (uint32_t i = 0; i < n; ++i) ++h[in[i]];
+    uint32_t distinct = 0;
+    for (uint32_t s = 0; s < 256; ++s) distinct += h[s] != 0;
+    *type = 0;
+    if (distinct == 1 && n > 1) { *type = 1; return 1; }
+    if (n < 2) return n;
+    // candidate distances and the greedy parse
+    uint32_t gaps[256] = {0};
+    for (uint32_t p = 0; p < n; ++p)
+        if (in[p] == '{') gap_count(in, p, gaps);
+    uint32_t cand[kCands];
+    const uint32_t nc = pick_cands(gaps, cand);
+    // entropy-only content into slot
+    uint32_t size = lit_section_seq(in, n, slot, sc.streams, sc.h, sc.code, sc.work);
+    slot[size++] = 0;  // Sequences_Section: Number_of_Sequences = 0
+    // literals + sequences when enough positions have a candidate match: the smaller
+    // content wins (ties: entropy-only)
+    uint32_t nbest = 0;
+    for (uint32_t p = 0; p < n; ++p) nbest += (sc.best[p] = best_at(in, n, p, cand, nc)) != 0;
+    if (lz_worth(nbest, n)) {
+        const FseTables& T = FseTables::get();
+        const uint32_t z = lz_content(in, n, cand, &sc, sc.h, sc.code, sc.work, T.ll, T.ml, T.of);
+        if (z && z < size) {
+            for (uint32_t i = 0; i < z; ++i) slot[i] = sc.body[i];
+            size = z;
+        }
+    }
+    if (size >= n) return n;  // not smaller: Raw
     *type = 2;
-    return o + 1;
+    return size;
 }
 
 // Bytes of a frame for `len` bytes of content at worst (every block Raw).

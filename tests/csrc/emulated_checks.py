@@ -164,7 +164,7 @@ def main():
 def zstd_checks():
     """sydelta_zstd_compress_device's batching and frame assembly (the emulated blocks are
     sydelta_zstd.hpp's sequential form): frames equal to the test reference encoder's and
-    decoded by the system libzstd, with batches of 1, 3 and 8192 blocks."""
+    decoded by the system libzstd, with batches of 1, 3 and 512 blocks."""
     import ctypes
     import json
     import random
@@ -178,7 +178,7 @@ def zstd_checks():
     rng = random.Random(4)
     texts = [b"", b"x", b"ab" * 70000, Z.delta_json(rng, 30000, 0.3), bytes(rng.randrange(256) for _ in range(300000))]
     n = 0
-    for batch in ("1", "3", "8192"):
+    for batch in ("1", "3", "512"):
         os.environ["SYDELTA_ZSTD_BATCH"] = batch
         for t in texts:
             src = np.zeros(len(t) + 16, np.uint8)
