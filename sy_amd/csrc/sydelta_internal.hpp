@@ -172,11 +172,12 @@ hipError_t launch_exclusive_sum_u64(const uint64_t* d_in, uint64_t* d_out, uint6
 // zstd frame of a text in HBM (sydelta_zstd.hpp).  Blocks [b0, b0 + nb) of d_text (len
 // bytes, 16-byte aligned, readable to the end of its last granule): slot i of d_slots
 // (zstd::kBlockMax bytes each) gets block b0+i's content, d_size[i] its size, d_type[i]
-// its type, d_len64[i] = 3 + size; d_lz[i] is block i's literals + sequences scratch.  Then launch_zstd_frame writes them behind their block
+// its type, d_len64[i] = 3 + size; d_lz holds nb * zstd::kSeqScratchBytes of literals +
+// sequences scratch (zstd::seq_scratch_at).  Then launch_zstd_frame writes them behind their block
 // headers at d_out + base + d_off[i] (d_off: exclusive prefix of d_len64), and the frame
 // header when b0 == 0.
 hipError_t launch_zstd_blocks(const uint8_t* d_text, uint64_t len, uint64_t b0, uint32_t nb, uint8_t* d_slots,
-                              zstd::SeqScratch* d_lz, uint32_t* d_size, uint32_t* d_type, uint64_t* d_len64,
+                              uint8_t* d_lz, uint32_t* d_size, uint32_t* d_type, uint64_t* d_len64,
                               hipStream_t s, Profiler* prof);
 hipError_t launch_zstd_frame(const uint8_t* d_text, uint64_t len, uint64_t b0, uint32_t nb, uint64_t nblocks,
                              const uint8_t* d_slots, const uint32_t* d_size, const uint32_t* d_type, const uint64_t* d_off,

@@ -2441,7 +2441,7 @@ struct ZLds {
 };
 
 __global__ __launch_bounds__(kZT) void k_zstd_block(const uint8_t* __restrict__ text, uint64_t len, uint64_t b0,
-                                                    uint8_t* __restrict__ slots, zstd::SeqScratch* __restrict__ lz,
+                                                    uint8_t* __restrict__ slots, uint8_t* __restrict__ lz, uint64_t nlz,
                                                     uint32_t* __restrict__ size_out, uint32_t* __restrict__ type_out,
                                                     uint64_t* __restrict__ len64) {
     __shared__ ZLds L;
@@ -2450,7 +2450,7 @@ __global__ __launch_bounds__(kZT) void k_zstd_block(const uint8_t* __restrict__ 
     const uint8_t* in = text + gb * zstd::kBlockMax;
     const uint32_t n = (uint32_t)min<uint64_t>(zstd::kBlockMax, len - gb * zstd::kBlockMax);
     uint8_t* slot = slots + (uint64_t)blockIdx.x * zstd::kBlockMax;
-    zstd::SeqScratch* sc = lz + blockIdx.x;
+    const zstd::SeqScratch sc = zstd::seq_scratch_at(lz, nlz, blockIdx.x);
     for (uint32_t i = tid; i < 4 * 256; i += kZT) (&L.hist[0][0])[i] = 0;
     for (uint32_t i = tid; i < 256; i += kZT) L.gaps[i] = 0;
     if (tid == 0) L.state[5] = 0;
@@ -2599,7 +2599,7 @@ __global__ __launch_bounds__(kZT) void k_zstd_block(const uint8_t* __restrict__ 
         uint32_t mine = 0;
         for (uint32_t p = tid; p < n; p += kZT) {
             const uint32_t b = zstd::best_at(in, n, p, L.cand, nc);
-            sc->best[p] = b;
+            sc.best[p] = b;
             mine += b != 0;
         }
         if (mine) atomicAdd(&L.state[5], mine);
@@ -2611,7 +2611,7 @@ __global__ __launch_bounds__(kZT) void k_zstd_block(const uint8_t* __restrict__ 
             }
             __syncthreads();
             const uint32_t z = L.state[6];
-            for (uint32_t i = tid; i < z; i += kZT) slot[i] = sc->body[i];
+            for (uint32_t i = tid; i < z; i += kZT) slot[i] = sc.body[i];
             if (tid == 0 && z) L.state[3] = z;
         }
     }
@@ -3531,13 +3531,13 @@ hipError_t launch_sort_hits(uint64_t* key, uint32_t* val, uint64_t* key_tmp, uin
 }
 
 hipError_t launch_zstd_blocks(const uint8_t* d_text, uint64_t len, uint64_t b0, uint32_t nb, uint8_t* d_slots,
-                              zstd::SeqScratch* d_lz, uint32_t* d_size, uint32_t* d_type, uint64_t* d_len64,
+                              uint8_t* d_lz, uint32_t* d_size, uint32_t* d_type, uint64_t* d_len64,
                               hipStream_t s, Profiler* prof) {
     if (!nb) return hipSuccess;
     if (b0 * zstd::kBlockMax >= len) return hipErrorInvalidValue;
     ProfScope ps(prof, s, "k_zstd_block");
-    hipLaunchKernelGGL(k_zstd_block, dim3(nb), dim3(kZT), 0, s, d_text, len, b0, d_slots, d_lz, d_size, d_type,
-                       d_len64);
+    hipLaunchKernelGGL(k_zstd_block, dim3(nb), dim3(kZT), 0, s, d_text, len, b0, d_slots, d_lz, (uint64_t)nb, d_size,
+                       d_type, d_len64);
     return hipGetLastError();
 }
 

@@ -542,14 +542,14 @@ extern "C" int sydelta_zstd_compress_device(int device, const uint8_t* d_in, uin
         if (const uint64_t v = strtoull(e, nullptr, 10)) kBatch = std::min<uint64_t>(v, 1 << 20);
     const uint64_t nb_max = std::min<uint64_t>(nblocks, kBatch);
     auto al = [](uint64_t b) { return (b + 255) & ~(uint64_t)255; };
-    const uint64_t o_lz = al(nb_max * zstd::kBlockMax), o_size = o_lz + al(nb_max * sizeof(zstd::SeqScratch));
+    const uint64_t o_lz = al(nb_max * zstd::kBlockMax), o_size = o_lz + al(nb_max * zstd::kSeqScratchBytes);
     const uint64_t o_type = o_size + al(4 * nb_max);
     const uint64_t o_len = o_type + al(4 * nb_max), o_off = o_len + al(8 * nb_max), total = o_off + al(8 * nb_max);
     DevBuf_wire buf;
     HIP_TRY(hipMallocAsync(&buf.p, total, s));
     buf.s = s;
     uint8_t* B = (uint8_t*)buf.p;
-    zstd::SeqScratch* d_lz = (zstd::SeqScratch*)(B + o_lz);
+    uint8_t* d_lz = B + o_lz;
     uint32_t* d_size = (uint32_t*)(B + o_size);
     uint32_t* d_type = (uint32_t*)(B + o_type);
     uint64_t* d_len = (uint64_t*)(B + o_len);

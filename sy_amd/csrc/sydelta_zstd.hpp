@@ -521,32 +521,48 @@ __host__ __device__ inline uint32_t lit_section_seq(const uint8_t* lit, uint32_t
     return o;
 }
 
-// Scratch of the literals + sequences coding of one block: per position bests,
-// sequences, literals, stream bytes, the content (the device keeps one per block in HBM).
+// Scratch of the literals + sequences coding of one block (views of separate arrays, so
+// a CPU build under AddressSanitizer sees each one's bounds): per position bests,
+// sequences, literals, stream bytes, the content.  The device keeps one set per block of
+// a batch in HBM (SeqArrays).
+constexpr uint32_t kBodyBytes = 2 * kBlockMax + 64;  // see lz_content
 struct SeqScratch {
-    uint32_t best[kBlockMax];
-    Seq seq[kMaxSeq];
-    uint8_t lit[kBlockMax];
-    uint8_t streams[4 * kStreamBytesMax];
-    // a sequence costs at most 57 bits (LL and ML codes + 16 extra bits each, OF code 8 +
-    // 8 extra bits) and covers >= kMinMatch bytes: content <= nl + 7 + 7.2 (n - nl) / 4 < 2n
-    uint8_t body[2 * kBlockMax + 64];
-    uint32_t h[256];       // host only (the device uses its LDS copies)
-    HufCode code;
-    HufWork work;
+    uint32_t* best;    // kBlockMax
+    Seq* seq;          // kMaxSeq
+    uint8_t* lit;      // kBlockMax
+    uint8_t* streams;  // 4 * kStreamBytesMax
+    uint8_t* body;     // kBodyBytes
 };
+// Bytes of the arrays of one block's SeqScratch.
+constexpr uint64_t kSeqScratchBytes =
+    4ull * kBlockMax + sizeof(Seq) * (uint64_t)kMaxSeq + kBlockMax + 4ull * kStreamBytesMax + kBodyBytes;
+// Block i's scratch inside one allocation of nb * kSeqScratchBytes (arrays grouped by
+// kind, each 16-byte aligned).
+__host__ __device__ __forceinline__ SeqScratch seq_scratch_at(uint8_t* base, uint64_t nb, uint64_t i) {
+    SeqScratch sc;
+    uint8_t* p = base;
+    sc.best = (uint32_t*)p + i * kBlockMax;                      p += 4ull * kBlockMax * nb;
+    sc.seq = (Seq*)p + i * kMaxSeq;                              p += sizeof(Seq) * (uint64_t)kMaxSeq * nb;
+    sc.lit = p + i * kBlockMax;                                  p += (uint64_t)kBlockMax * nb;
+    sc.streams = p + i * (4ull * kStreamBytesMax);               p += 4ull * kStreamBytesMax * nb;
+    sc.body = p + i * (uint64_t)kBodyBytes;
+    return sc;
+}
 
 // The literals + sequences content of a block whose bests are in sc.best: greedy parse,
 // literals section, sequences section into sc.body.  Returns its size, or 0 when the
 // block has no match.  One thread (the device's thread 0) runs it.
-__host__ __device__ inline uint32_t lz_content(const uint8_t* in, uint32_t n, const uint32_t* cand, SeqScratch* sc,
+// A sequence costs at most 57 bits (LL and ML codes + 16 extra bits each, OF code 8 + 8
+// extra bits) and covers >= kMinMatch bytes, so the content is <= nl + 7 + 7.2 (n - nl) / 4
+// < 2n + 64 = kBodyBytes.
+__host__ __device__ inline uint32_t lz_content(const uint8_t* in, uint32_t n, const uint32_t* cand, const SeqScratch& sc,
                                                uint32_t* h, HufCode& c, HufWork& wk, const FseCT& tll,
                                                const FseCT& tml, const FseCT& tof) {
     uint32_t nl = 0, cov = 0;
-    const uint32_t ns = greedy_parse(in, n, sc->best, cand, sc->seq, sc->lit, &nl, &cov);
+    const uint32_t ns = greedy_parse(in, n, sc.best, cand, sc.seq, sc.lit, &nl, &cov);
     if (!ns) return 0;
-    uint32_t z = lit_section_seq(sc->lit, nl, sc->body, sc->streams, h, c, wk);
-    z += seq_section(sc->seq, ns, sc->body + z, tll, tml, tof);
+    uint32_t z = lit_section_seq(sc.lit, nl, sc.body, sc.streams, h, c, wk);
+    z += seq_section(sc.seq, ns, sc.body + z, tll, tml, tof);
     return z;
 }
 
@@ -560,8 +576,11 @@ __host__ __device__ __forceinline__ bool lz_worth(uint32_t nbest, uint32_t n) { 
 // 1 with *type = 1 (RLE).  A block whose candidate matches cover >= 1/8 of it is coded
 // as literals + sequences, any other as literals only.  k_zstd_block produces the same
 // bytes with parallel histograms, candidate search and bit scatter.
-__host__ inline uint32_t block_content_seq(const uint8_t* in, uint32_t n, uint8_t* slot, SeqScratch& sc,
+__host__ inline uint32_t block_content_seq(const uint8_t* in, uint32_t n, uint8_t* slot, const SeqScratch& sc,
                                            uint32_t* type) {
+    static thread_local uint32_t hh[256];
+    static thread_local HufCode code;
+    static thread_local HufWork work;
     uint32_t h[256] = {0};
     for (uint32_t i = 0; i < n; ++i) ++h[in[i]];
     uint32_t distinct = 0;
@@ -575,18 +594,22 @@ __host__ inline uint32_t block_content_seq(const uint8_t* in, uint32_t n, uint8_
         if (in[p] == '{') gap_count(in, p, gaps);
     uint32_t cand[kCands];
     const uint32_t nc = pick_cands(gaps, cand);
-    // entropy-only content into slot
-    uint32_t size = lit_section_seq(in, n, slot, sc.streams, sc.h, sc.code, sc.work);
-    slot[size++] = 0;  // Sequences_Section: Number_of_Sequences = 0
+    // entropy-only content (built in body: a Raw literals section is n + 3 bytes; only a
+    // content smaller than the block goes to the slot)
+    uint32_t size = lit_section_seq(in, n, sc.body, sc.streams, hh, code, work);
+    sc.body[size++] = 0;  // Sequences_Section: Number_of_Sequences = 0
+    if (size < n)
+        for (uint32_t i = 0; i < size; ++i) slot[i] = sc.body[i];
     // literals + sequences when enough positions have a candidate match: the smaller
     // content wins (ties: entropy-only)
     uint32_t nbest = 0;
     for (uint32_t p = 0; p < n; ++p) nbest += (sc.best[p] = best_at(in, n, p, cand, nc)) != 0;
     if (lz_worth(nbest, n)) {
         const FseTables& T = FseTables::get();
-        const uint32_t z = lz_content(in, n, cand, &sc, sc.h, sc.code, sc.work, T.ll, T.ml, T.of);
+        const uint32_t z = lz_content(in, n, cand, sc, hh, code, work, T.ll, T.ml, T.of);
         if (z && z < size) {
-            for (uint32_t i = 0; i < z; ++i) slot[i] = sc.body[i];
+            if (z < n)
+                for (uint32_t i = 0; i < z; ++i) slot[i] = sc.body[i];
             size = z;
         }
     }

@@ -455,17 +455,16 @@ hipError_t launch_chain(const chain::ChainArgs& a, hipStream_t, Profiler*) {
 
 // zstd blocks: the sequential form of k_zstd_block (sydelta_zstd.hpp block_content_seq)
 hipError_t launch_zstd_blocks(const uint8_t* d_text, uint64_t len, uint64_t b0, uint32_t nb, uint8_t* d_slots,
-                              zstd::SeqScratch* d_lz, uint32_t* d_size, uint32_t* d_type, uint64_t* d_len64,
+                              uint8_t* d_lz, uint32_t* d_size, uint32_t* d_type, uint64_t* d_len64,
                               hipStream_t, Profiler*) {
     EmuTimer emu_t;
     if (b0 * zstd::kBlockMax >= len) return hipErrorInvalidValue;
-    std::vector<zstd::SeqScratch> scratch(1);
-    (void)d_lz;
     for (uint32_t i = 0; i < nb; ++i) {
         const uint64_t p = (b0 + i) * zstd::kBlockMax;
         const uint32_t n = (uint32_t)std::min<uint64_t>(zstd::kBlockMax, len - p);
         uint32_t type = 0;
-        d_size[i] = zstd::block_content_seq(d_text + p, n, d_slots + (uint64_t)i * zstd::kBlockMax, scratch[0], &type);
+        d_size[i] = zstd::block_content_seq(d_text + p, n, d_slots + (uint64_t)i * zstd::kBlockMax,
+                                            zstd::seq_scratch_at(d_lz, nb, i), &type);
         d_type[i] = type;
         d_len64[i] = 3ull + d_size[i];
     }

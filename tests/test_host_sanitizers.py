@@ -12,6 +12,12 @@ from sy_amd.build supplies the launch symbols; no GPU call is made) and runs:
   writer -> parser -> writer round trips (ssh.rs:967-1003, sy-remote.rs:146-175);
 * sydelta_delta_from_ops validation.
 
+tests/csrc/kernel_bodies_fuzz.cpp (test_kernel_bodies_under_asan_ubsan) drives the
+per-thread bodies of the device walk (sydelta_chain.hpp) and the zstd block coder
+(sydelta_zstd.hpp) with every array allocated at its exact size, so an index a GPU
+kernel would take out of its array is a report here, and checks them against walk_src
+and the sequential stream writer.
+
 Any sanitizer report (including leaks) fails the run.
 """
 import os
@@ -86,3 +92,23 @@ def test_host_pool_under_tsan():
     r = subprocess.run([exe], capture_output=True, text=True, env=env, timeout=500)
     assert r.returncode == 0, (r.stdout[-2000:], r.stderr[-6000:])
     assert "pool_tsan ok" in r.stdout and "WARNING: ThreadSanitizer" not in r.stderr
+
+
+@pytest.mark.timeout(900)
+def test_kernel_bodies_under_asan_ubsan():
+    """K5b's chain bodies on 2000 random classified sources (marking threads shuffled)
+    against walk_src, and K7z's block coder plus a thread-by-thread replica of its
+    parallel bit scatter on random texts, all under ASan + UBSan."""
+    if shutil.which("g++") is None or not os.path.exists("/opt/rocm/include/hip/hip_runtime.h"):
+        pytest.skip("needs g++ and the HIP headers")
+    os.makedirs(OUT, exist_ok=True)
+    exe = os.path.join(OUT, "kernel_bodies_fuzz")
+    r = subprocess.run(["g++"] + FLAGS + [os.path.join(ROOT, "tests", "csrc", "kernel_bodies_fuzz.cpp"), "-o", exe,
+                                          "-lpthread"], capture_output=True, text=True)
+    assert r.returncode == 0, r.stderr[-4000:]
+    env = dict(os.environ, ASAN_OPTIONS="detect_leaks=1:abort_on_error=1",
+               UBSAN_OPTIONS="print_stacktrace=1:halt_on_error=1")
+    r = subprocess.run([exe, "2000"], capture_output=True, text=True, env=env, timeout=800)
+    assert r.returncode == 0, (r.stdout[-2000:], r.stderr[-6000:])
+    assert "kernel bodies ok" in r.stdout
+    assert "runtime error" not in r.stderr
