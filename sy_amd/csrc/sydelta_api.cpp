@@ -1312,10 +1312,10 @@ int Classifier::walk_device(size_t i, uint64_t entry, const BasisInfo& bi, bool 
     const uint64_t M = (c.probed ? c.nahit : 0) + H;
     if (M < device_walk_min() || M > (1ull << 25)) return 2;
     const uint32_t K = chain::chain_levels(M);
-    const uint64_t W = M + 2, nblk = c.probed ? c.nblk : 0, nkw = (nblk + 31) / 32;
+    const uint64_t W = M + 2, nblk = c.probed ? c.nblk : 0;
     // one allocation: known | aflag | apfx | hpos | hblk | upos | ublk | jump | on | cnt | off | ops | res
     auto al = [](uint64_t b) { return (b + 255) & ~(uint64_t)255; };
-    const uint64_t o_known = 0, o_aflag = o_known + al(4 * nkw), o_apfx = o_aflag + al(4 * (nblk + 1));
+    const uint64_t o_known = 0, o_aflag = o_known + al(nblk), o_apfx = o_aflag + al(4 * (nblk + 1));
     const uint64_t o_hpos = o_apfx + al(4 * (nblk + 1)), o_hblk = o_hpos + al(8 * H), o_upos = o_hblk + al(4 * H);
     const uint64_t o_ublk = o_upos + al(8 * M), o_jump = o_ublk + al(4 * M), o_on = o_jump + al(4 * W * K);
     const uint64_t o_cnt = o_on + al(W), o_off = o_cnt + al(4 * (M + 1)), o_ops = o_off + al(4 * (M + 1));
@@ -1333,7 +1333,7 @@ int Classifier::walk_device(size_t i, uint64_t entry, const BasisInfo& bi, bool 
     a.probed = c.probed ? 1u : 0u;
     a.K = K;
     a.ahit = c.probed ? d_probe_out + probe_pfx[i] : nullptr;
-    a.known = (const uint32_t*)(B + o_known);
+    a.known = B + o_known;
     a.aflag = (uint32_t*)(B + o_aflag);
     a.apfx = (uint32_t*)(B + o_apfx);
     a.hpos = (const uint64_t*)(B + o_hpos);
@@ -1351,13 +1351,8 @@ int Classifier::walk_device(size_t i, uint64_t entry, const BasisInfo& bi, bool 
     a.last_size = bi.last_size;
     a.ops = (sydelta_op*)(B + o_ops);
     a.res = (chain::ChainResult*)(B + o_res);
-    std::vector<uint32_t> known;
-    if (c.probed) {  // bit k: block kb+k was scanned
-        known.assign(nkw, 0);
-        const uint8_t* sc = c.scanned.data();
-        for (uint64_t k = 0; k < nblk; ++k) known[k >> 5] |= (uint32_t)(sc[k] != 0) << (k & 31);
-        HIP_TRY(hipMemcpyAsync(B + o_known, known.data(), 4 * nkw, hipMemcpyHostToDevice, s));
-    }
+    if (c.probed && nblk)  // per block: all its window starts were scanned
+        HIP_TRY(hipMemcpyAsync(B + o_known, c.scanned.data(), nblk, hipMemcpyHostToDevice, s));
     if (H) {
         HIP_TRY(hipMemcpyAsync(B + o_hpos, hp, 8 * H, hipMemcpyHostToDevice, s));
         HIP_TRY(hipMemcpyAsync(B + o_hblk, hb, 4 * H, hipMemcpyHostToDevice, s));

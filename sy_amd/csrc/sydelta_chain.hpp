@@ -57,7 +57,7 @@ struct ChainArgs {
     uint32_t probed;       // ahit/known/apfx valid
     uint32_t K;            // pointer-jumping levels: 2^K > M + 1
     const uint32_t* ahit;  // per local block: its aligned window's global block or kNoHit
-    const uint32_t* known; // bit k: every window start of local block k was scanned
+    const uint8_t* known;  // per local block: every window start of it was scanned (walk::Src::scanned)
     uint32_t* aflag;       // nblk + 1: aligned-hit flags (scratch)
     uint32_t* apfx;        // nblk + 1: their exclusive prefix
     const uint64_t* hpos;  // scan hits, ascending, none at an aligned position that hit
@@ -77,9 +77,7 @@ struct ChainArgs {
     ChainResult* res;
 };
 
-__host__ __device__ __forceinline__ bool known_block(const ChainArgs& a, uint64_t k) {
-    return (a.known[k >> 5] >> (k & 31)) & 1u;
-}
+__host__ __device__ __forceinline__ bool known_block(const ChainArgs& a, uint64_t k) { return a.known[k] != 0; }
 
 // A position x < p1 the walk may stand on without its class being known: inside a
 // probed block (not its aligned start) none of whose window starts was scanned.  Such a

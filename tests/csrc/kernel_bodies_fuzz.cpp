@@ -105,15 +105,14 @@ static int chain_case(std::mt19937_64& rng, uint64_t* walked_on_device) {
     }
     const uint64_t H = hp.size(), M = (probed ? c.nahit : 0) + H, W = M + 2, nb = probed ? nblk : 0;
     const uint32_t K = chain::chain_levels(M);
-    Arr<uint32_t> ahit(nb), known((nb + 31) / 32), aflag(nb + 1), apfx(nb + 1), ublk(M), hblk(H), jump(K * W),
-        cnt(M + 1), off(M + 1);
+    Arr<uint32_t> ahit(nb), aflag(nb + 1), apfx(nb + 1), ublk(M), hblk(H), jump(K * W), cnt(M + 1), off(M + 1);
+    Arr<uint8_t> known(nb);
     Arr<uint64_t> hpos(H), upos(M);
     Arr<uint8_t> on(W);
     Arr<sydelta_op> ops(2 * M);
     Arr<chain::ChainResult> res(1);
     for (uint64_t k = 0; k < nb; ++k) ahit.get()[k] = c.ahit[k];
-    for (uint64_t w = 0; w < (nb + 31) / 32; ++w) known.get()[w] = 0;
-    for (uint64_t k = 0; k < nb; ++k) known.get()[k >> 5] |= (uint32_t)(c.scanned[k] != 0) << (k & 31);
+    for (uint64_t k = 0; k < nb; ++k) known.get()[k] = c.scanned[k];
     std::copy(hp.begin(), hp.end(), hpos.get());
     std::copy(hb.begin(), hb.end(), hblk.get());
     chain::ChainArgs a{};
