@@ -97,6 +97,24 @@ __host__ __device__ __forceinline__ uint64_t lower_bound_u(const ChainArgs& a, u
     return lo;
 }
 
+// First index >= lo of U with upos >= x (M if none), for x > upos[lo - 1]: a galloping
+// search from lo (a successor is usually the next hit or one close to it, so this reads a
+// line or two where a binary search over U would make ~log2 M dependent reads).
+__host__ __device__ __forceinline__ uint64_t lower_bound_from(const ChainArgs& a, uint64_t lo, uint64_t x) {
+    uint64_t step = 1, hi = lo;
+    while (hi < a.M && a.upos[hi] < x) {
+        lo = hi + 1;
+        hi = lo + step - 1 < a.M ? lo + step - 1 : a.M;
+        step <<= 1;
+    }
+    // upos[lo - 1] < x (or lo is the start) and (hi == M or upos[hi] >= x): binary search [lo, hi)
+    while (lo < hi) {
+        const uint64_t mid = (lo + hi) >> 1;
+        if (a.upos[mid] < x) lo = mid + 1; else hi = mid;
+    }
+    return lo;
+}
+
 // Scan hits strictly before x.
 __host__ __device__ __forceinline__ uint64_t scan_hits_before(const ChainArgs& a, uint64_t x) {
     uint64_t lo = 0, hi = a.H;
@@ -148,7 +166,7 @@ __host__ __device__ __forceinline__ void chain_succ(const ChainArgs& a, uint64_t
     uint32_t s;
     if (x >= a.p1) s = END;
     else if (unknown_at(a, x)) s = UNK;
-    else s = (uint32_t)lower_bound_u(a, x);
+    else s = (uint32_t)lower_bound_from(a, i + 1, x);  // upos[i] < x
     a.jump[i] = s;
 }
 
