@@ -2420,7 +2420,8 @@ __global__ void k_chain_finish(chain::ChainArgs a) {
 // stream leaves for the block's slot with its closing 1 bit.  Literals + sequences: the
 // '{' distances and every position's best candidate match in parallel, then (when enough
 // positions match) one thread parses, codes the literals and FSE-codes the sequences with
-// the shared sequential functions; the smaller content stays in the slot.  k_zstd_frame
+// the shared sequential functions (tables from the block's counts, in HBM scratch); the
+// smaller content stays in the slot.  k_zstd_frame
 // then lays the blocks out behind their headers.
 constexpr int kZT = 256;
 constexpr uint32_t kZRun = 144;  // bytes of a stream per thread: 256 runs cover 32 KiB + the 16-byte phase
@@ -2433,7 +2434,6 @@ struct ZLds {
     uint32_t words[kZStreamWords];
     zstd::HufCode code;
     zstd::HufWork work;
-    zstd::FseCT tll, tml, tof;
     uint32_t gaps[256];
     uint32_t cand[zstd::kCands];
     uint32_t ssize[4];
@@ -2586,13 +2586,6 @@ __global__ __launch_bounds__(kZT) void k_zstd_block(const uint8_t* __restrict__ 
         __syncthreads();
         if (tid == 0) {
             L.state[4] = zstd::pick_cands(L.gaps, L.cand);
-            int16_t nrm[53];
-            for (uint32_t i = 0; i < 36; ++i) nrm[i] = zstd::ll_norm(i);
-            zstd::fse_build(L.tll, nrm, 36, 6);
-            for (uint32_t i = 0; i < 53; ++i) nrm[i] = zstd::ml_norm(i);
-            zstd::fse_build(L.tml, nrm, 53, 6);
-            for (uint32_t i = 0; i < 29; ++i) nrm[i] = zstd::of_norm(i);
-            zstd::fse_build(L.tof, nrm, 29, 5);
         }
         __syncthreads();
         const uint32_t nc = L.state[4];
@@ -2606,7 +2599,7 @@ __global__ __launch_bounds__(kZT) void k_zstd_block(const uint8_t* __restrict__ 
         __syncthreads();
         if (zstd::lz_worth(L.state[5], n)) {
             if (tid == 0) {
-                const uint32_t z = zstd::lz_content(in, n, L.cand, sc, L.hist[1], L.code, L.work, L.tll, L.tml, L.tof);
+                const uint32_t z = zstd::lz_content(in, n, L.cand, sc, L.hist[1], L.code, L.work);
                 L.state[6] = (z && z < L.state[3]) ? z : 0u;
             }
             __syncthreads();

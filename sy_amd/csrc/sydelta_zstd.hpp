@@ -189,30 +189,12 @@ __host__ __device__ __forceinline__ void stream_range(uint32_t regen, bool four,
 // are the block's most common gaps between consecutive '{' (and 1, runs); each position's
 // best candidate is found independently (the device does all positions at once), a
 // greedy parse takes a match of >= kMinMatch wherever one starts, and the sequences are
-// FSE-coded with the predefined distributions (no table descriptions).  A block whose
-// matches cover less than 1/8 of it stays entropy-only.
+// FSE-coded with tables built from the block's own code counts (RLE for a code that
+// never changes).
 constexpr uint32_t kMinMatch = 4;
 constexpr uint32_t kProbe = 32;     // bytes compared per candidate when ranking them
 constexpr uint32_t kCands = 5;      // candidate distances: 1 and the 4 most common '{' gaps
 constexpr uint32_t kMaxSeq = kBlockMax / kMinMatch;
-
-// RFC 8878 3.1.1.3.2.2: predefined distributions (accuracy logs 6, 6, 5).
-__host__ __device__ __forceinline__ int16_t ll_norm(uint32_t s) {
-    constexpr int16_t t[36] = {4, 3, 2, 2, 2, 2, 2, 2, 2, 2, 2, 2, 2, 1, 1, 1, 2, 2,
-                               2, 2, 2, 2, 2, 2, 2, 3, 2, 1, 1, 1, 1, 1, -1, -1, -1, -1};
-    return t[s];
-}
-__host__ __device__ __forceinline__ int16_t ml_norm(uint32_t s) {
-    constexpr int16_t t[53] = {1, 4, 3, 2, 2, 2, 2, 2, 2, 1, 1, 1, 1, 1, 1, 1, 1, 1,
-                               1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1,
-                               1, 1, 1, 1, 1, 1, 1, 1, 1, 1, -1, -1, -1, -1, -1, -1, -1};
-    return t[s];
-}
-__host__ __device__ __forceinline__ int16_t of_norm(uint32_t s) {
-    constexpr int16_t t[29] = {1, 1, 1, 1, 1, 1, 2, 2, 2, 1, 1, 1, 1, 1, 1,
-                               1, 1, 1, 1, 1, 1, 1, 1, 1, -1, -1, -1, -1, -1};
-    return t[s];
-}
 
 // Literals_Length / Match_Length codes (RFC 8878 3.1.1.3.2.1.1): code, its extra bits.
 __host__ __device__ __forceinline__ void ll_code(uint32_t ll, uint32_t& code, uint32_t& bits) {
@@ -240,14 +222,14 @@ __host__ __device__ __forceinline__ void ml_code(uint32_t ml, uint32_t& code, ui
 // FSE_buildCTable: symbols spread with step 5/8 table + 3, "less than 1" symbols in the
 // top cells, state table sorted by symbol).
 struct FseCT {
-    uint16_t state[64];     // next-state table (tableSize entries)
+    uint16_t state[512];    // next-state table (tableSize entries, log <= 9)
     int32_t delta_nb[53];   // deltaNbBits per symbol
     int32_t delta_find[53]; // deltaFindState per symbol
     uint32_t log;
 };
 __host__ __device__ inline void fse_build(FseCT& t, const int16_t* norm, uint32_t nsym, uint32_t log) {
     const uint32_t size = 1u << log, mask = size - 1, step = (size >> 1) + (size >> 3) + 3;
-    uint8_t sym[64];
+    uint8_t sym[512];
     uint32_t cumul[54];
     uint32_t high = size - 1;
     cumul[0] = 0;
@@ -270,7 +252,10 @@ __host__ __device__ inline void fse_build(FseCT& t, const int16_t* norm, uint32_
     int32_t total = 0;
     for (uint32_t s = 0; s < nsym; ++s) {
         const int n = norm[s];
-        if (n == -1 || n == 1) {
+        if (n == 0) {  // absent: never coded (zstd's case 0)
+            t.delta_nb[s] = (int32_t)(((log + 1) << 16) - (1u << log));
+            t.delta_find[s] = 0;
+        } else if (n == -1 || n == 1) {
             t.delta_nb[s] = (int32_t)((log << 16) - (1u << log));
             t.delta_find[s] = total - 1;
             total += 1;
@@ -318,31 +303,147 @@ struct Seq {
     uint32_t ll, ml, off;  // literal length, match length (>= kMinMatch), distance
 };
 
-// The three predefined tables (built once on the host; the device builds them in LDS).
-struct FseTables {
-    FseCT ll, ml, of;
-    __host__ static const FseTables& get() {
-        static const FseTables t = [] {
-            FseTables x;
-            int16_t n[53];
-            for (uint32_t i = 0; i < 36; ++i) n[i] = ll_norm(i);
-            fse_build(x.ll, n, 36, 6);
-            for (uint32_t i = 0; i < 53; ++i) n[i] = ml_norm(i);
-            fse_build(x.ml, n, 53, 6);
-            for (uint32_t i = 0; i < 29; ++i) n[i] = of_norm(i);
-            fse_build(x.of, n, 29, 5);
-            return x;
-        }();
-        return t;
+// Normalized counts of a block's codes (FSE_Compressed mode): table log L in [5, maxlog]
+// with 2^L >= 2 x the distinct codes, every present code >= 1, the rounding error taken
+// from / given to the most frequent codes.  Deterministic (host and device alike).
+__host__ __device__ inline uint32_t fse_normalize(const uint32_t* cnt, uint32_t nsym, uint32_t total, uint32_t maxlog,
+                                                  int16_t* norm) {
+    uint32_t distinct = 0;
+    for (uint32_t s = 0; s < nsym; ++s) distinct += cnt[s] != 0;
+    uint32_t L = 5;
+    while (L < maxlog && ((1u << L) < 2 * distinct || (1u << L) < total)) ++L;
+    const uint32_t size = 1u << L;
+    int32_t sum = 0;
+    for (uint32_t s = 0; s < nsym; ++s) {
+        int32_t v = 0;
+        if (cnt[s]) {
+            v = (int32_t)(((uint64_t)cnt[s] * size) / total);
+            if (v < 1) v = 1;
+        }
+        norm[s] = (int16_t)v;
+        sum += v;
     }
-};
+    // the difference goes to (or comes from) the largest entries, one step at a time
+    while (sum != (int32_t)size) {
+        uint32_t big = 0;
+        for (uint32_t s = 1; s < nsym; ++s)
+            if (norm[s] > norm[big]) big = s;
+        if (sum < (int32_t)size) {
+            norm[big] = (int16_t)(norm[big] + ((int32_t)size - sum));
+            sum = (int32_t)size;
+        } else {
+            const int32_t take = sum - (int32_t)size < norm[big] - 1 ? sum - (int32_t)size : norm[big] - 1;
+            norm[big] = (int16_t)(norm[big] - take);
+            sum -= take;
+            if (take == 0) break;  // cannot happen with 2^L >= 2 x distinct
+        }
+    }
+    return L;
+}
 
-// Sequences_Section of ns sequences into p (predefined tables); returns its size.  Order
-// of zstd's ZSTD_encodeSequences: the last sequence starts the states, then every earlier
-// one from the end: OF, ML, LL state bits, then LL, ML, OF extra bits; states flushed ML,
-// OF, LL (the decoder reads LL, OF, ML first).
-__host__ __device__ inline uint32_t seq_section(const Seq* sq, uint32_t ns, uint8_t* p, const FseCT& tll,
-                                                const FseCT& tml, const FseCT& tof) {
+// FSE table description (RFC 8878 4.1.1; zstd's FSE_writeNCount): accuracy log - 5, then
+// each count + 1 in a variable number of bits, a run of zero counts as 2-bit repeat
+// flags.  Returns its size.
+__host__ __device__ inline uint32_t fse_write_ncount(uint8_t* out, const int16_t* norm, uint32_t nsym, uint32_t L) {
+    uint32_t o = 0;
+    uint32_t bits = (L - 5), nbits = 4;
+    int32_t remaining = (1 << L) + 1, threshold = 1 << L;
+    uint32_t nb = L + 1;
+    uint32_t s = 0;
+    bool prev0 = false;
+    uint32_t last = nsym;  // past the last nonzero count
+    while (last > 0 && norm[last - 1] == 0) --last;
+    auto flush16 = [&]() {
+        if (nbits > 16) {
+            out[o++] = (uint8_t)bits;
+            out[o++] = (uint8_t)(bits >> 8);
+            bits >>= 16;
+            nbits -= 16;
+        }
+    };
+    while (s < last && remaining > 1) {
+        if (prev0) {
+            uint32_t start = s;
+            while (s < last && !norm[s]) ++s;
+            while (s >= start + 24) {
+                start += 24;
+                bits += 0xFFFFu << nbits;
+                out[o++] = (uint8_t)bits;
+                out[o++] = (uint8_t)(bits >> 8);
+                bits >>= 16;
+            }
+            while (s >= start + 3) {
+                start += 3;
+                bits += 3u << nbits;
+                nbits += 2;
+            }
+            bits += (s - start) << nbits;
+            nbits += 2;
+            flush16();
+        }
+        int32_t count = norm[s++];
+        const int32_t mx = (2 * threshold - 1) - remaining;
+        remaining -= count < 0 ? -count : count;
+        count++;
+        if (count >= threshold) count += mx;
+        bits += (uint32_t)count << nbits;
+        nbits += nb;
+        nbits -= count < mx ? 1u : 0u;
+        prev0 = count == 1;
+        while (remaining < threshold) {
+            --nb;
+            threshold >>= 1;
+        }
+        flush16();
+    }
+    out[o++] = (uint8_t)bits;
+    out[o++] = (uint8_t)(bits >> 8);
+    o -= 2;
+    o += (nbits + 7) / 8;
+    return o;
+}
+
+// One code's table for a block: RLE (one distinct code: mode 1, the table is that byte)
+// or FSE_Compressed (mode 2) from the block's counts.  Writes the table description at
+// out, returns its size; *mode, and t for the coder (log 0 for RLE: no state bits).
+__host__ __device__ inline uint32_t seq_table(const uint32_t* cnt, uint32_t nsym, uint32_t total, uint32_t maxlog,
+                                              FseCT& t, uint32_t* mode, uint8_t* out) {
+    uint32_t distinct = 0, only = 0;
+    for (uint32_t s = 0; s < nsym; ++s)
+        if (cnt[s]) { ++distinct; only = s; }
+    if (distinct == 1) {
+        *mode = 1;
+        out[0] = (uint8_t)only;
+        for (uint32_t s = 0; s < nsym; ++s) { t.delta_nb[s] = 0; t.delta_find[s] = 0; }
+        t.state[0] = 0;
+        t.state[1] = 0;
+        t.log = 0;
+        return 1;
+    }
+    int16_t norm[53];
+    const uint32_t L = fse_normalize(cnt, nsym, total, maxlog, norm);
+    fse_build(t, norm, nsym, L);
+    *mode = 2;
+    return fse_write_ncount(out, norm, nsym, L);
+}
+
+// The codes of a sequence.
+__host__ __device__ __forceinline__ void seq_codes(const Seq& q, uint32_t& lc, uint32_t& lb, uint32_t& mc,
+                                                   uint32_t& mb, uint32_t& oc, uint32_t& ov) {
+    ll_code(q.ll, lc, lb);
+    ml_code(q.ml, mc, mb);
+    ov = q.off + 3;  // Offset_Value: a distance, never a repeat code
+    oc = 0;
+    while ((2u << oc) <= ov) ++oc;
+}
+
+// Sequences_Section of ns sequences into p; returns its size.  Tables per block (RLE or
+// FSE_Compressed from the block's code counts; the FseCT arguments are scratch, sized for
+// tables up to log 9).  Order of zstd's ZSTD_encodeSequences: the last sequence starts
+// the states, then every earlier one from the end: OF, ML, LL state bits, then LL, ML, OF
+// extra bits; states flushed ML, OF, LL (the decoder reads LL, OF, ML first).
+__host__ __device__ inline uint32_t seq_section(const Seq* sq, uint32_t ns, uint8_t* p, FseCT& tll, FseCT& tml,
+                                                FseCT& tof) {
     uint32_t o = 0;
     if (ns < 128) {
         p[o++] = (uint8_t)ns;
@@ -355,27 +456,32 @@ __host__ __device__ inline uint32_t seq_section(const Seq* sq, uint32_t ns, uint
         p[o++] = (uint8_t)((ns - 0x7F00) >> 8);
     }
     if (!ns) return o;
-    p[o++] = 0;  // Symbol_Compression_Modes: LL, OF, ML predefined
-    BitW w{p + o, 0, 0, 0};
-    auto codes = [&](const Seq& q, uint32_t& lc, uint32_t& lb, uint32_t& mc, uint32_t& mb, uint32_t& oc,
-                     uint32_t& ob) {
-        ll_code(q.ll, lc, lb);
-        ml_code(q.ml, mc, mb);
-        ob = q.off + 3;  // Offset_Value: a distance, never a repeat code
-        oc = 0;
-        while ((2u << oc) <= ob) ++oc;
-    };
+    uint32_t cll[36] = {0}, cml[53] = {0}, cof[32] = {0};
     uint32_t lc, lb, mc, mb, oc, ov;
-    codes(sq[ns - 1], lc, lb, mc, mb, oc, ov);
-    uint32_t sml = fse_init(tml, mc), sof = fse_init(tof, oc), sll = fse_init(tll, lc);
+    for (uint32_t i = 0; i < ns; ++i) {
+        seq_codes(sq[i], lc, lb, mc, mb, oc, ov);
+        ++cll[lc];
+        ++cml[mc];
+        ++cof[oc];
+    }
+    const uint32_t modes_at = o++;
+    uint32_t mll, mof, mml;
+    o += seq_table(cll, 36, ns, 9, tll, &mll, p + o);
+    o += seq_table(cof, 32, ns, 8, tof, &mof, p + o);
+    o += seq_table(cml, 53, ns, 9, tml, &mml, p + o);
+    p[modes_at] = (uint8_t)((mll << 6) | (mof << 4) | (mml << 2));
+    BitW w{p + o, 0, 0, 0};
+    seq_codes(sq[ns - 1], lc, lb, mc, mb, oc, ov);
+    uint32_t sml = tml.log ? fse_init(tml, mc) : 0, sof = tof.log ? fse_init(tof, oc) : 0;
+    uint32_t sll = tll.log ? fse_init(tll, lc) : 0;
     w.add(sq[ns - 1].ll, lb);
     w.add(sq[ns - 1].ml - 3, mb);
     w.add(ov, oc);
     for (uint32_t i = ns - 1; i-- > 0;) {
-        codes(sq[i], lc, lb, mc, mb, oc, ov);
-        fse_encode(w, tof, sof, oc);
-        fse_encode(w, tml, sml, mc);
-        fse_encode(w, tll, sll, lc);
+        seq_codes(sq[i], lc, lb, mc, mb, oc, ov);
+        if (tof.log) fse_encode(w, tof, sof, oc);
+        if (tml.log) fse_encode(w, tml, sml, mc);
+        if (tll.log) fse_encode(w, tll, sll, lc);
         w.add(sq[i].ll, lb);
         w.add(sq[i].ml - 3, mb);
         w.add(ov, oc);
@@ -532,10 +638,12 @@ struct SeqScratch {
     uint8_t* lit;      // kBlockMax
     uint8_t* streams;  // 4 * kStreamBytesMax
     uint8_t* body;     // kBodyBytes
+    FseCT* fse;        // 3: the LL, ML, OF tables of the block
 };
+constexpr uint64_t kFseBytes = (3 * sizeof(FseCT) + 15) / 16 * 16;
 // Bytes of the arrays of one block's SeqScratch.
 constexpr uint64_t kSeqScratchBytes =
-    4ull * kBlockMax + sizeof(Seq) * (uint64_t)kMaxSeq + kBlockMax + 4ull * kStreamBytesMax + kBodyBytes;
+    4ull * kBlockMax + sizeof(Seq) * (uint64_t)kMaxSeq + kBlockMax + 4ull * kStreamBytesMax + kBodyBytes + kFseBytes;
 // Block i's scratch inside one allocation of nb * kSeqScratchBytes (arrays grouped by
 // kind, each 16-byte aligned).
 __host__ __device__ __forceinline__ SeqScratch seq_scratch_at(uint8_t* base, uint64_t nb, uint64_t i) {
@@ -545,7 +653,8 @@ __host__ __device__ __forceinline__ SeqScratch seq_scratch_at(uint8_t* base, uin
     sc.seq = (Seq*)p + i * kMaxSeq;                              p += sizeof(Seq) * (uint64_t)kMaxSeq * nb;
     sc.lit = p + i * kBlockMax;                                  p += (uint64_t)kBlockMax * nb;
     sc.streams = p + i * (4ull * kStreamBytesMax);               p += 4ull * kStreamBytesMax * nb;
-    sc.body = p + i * (uint64_t)kBodyBytes;
+    sc.body = p + i * (uint64_t)kBodyBytes;                       p += (uint64_t)kBodyBytes * nb;
+    sc.fse = (FseCT*)(p + i * kFseBytes);
     return sc;
 }
 
@@ -556,13 +665,12 @@ __host__ __device__ __forceinline__ SeqScratch seq_scratch_at(uint8_t* base, uin
 // extra bits) and covers >= kMinMatch bytes, so the content is <= nl + 7 + 7.2 (n - nl) / 4
 // < 2n + 64 = kBodyBytes.
 __host__ __device__ inline uint32_t lz_content(const uint8_t* in, uint32_t n, const uint32_t* cand, const SeqScratch& sc,
-                                               uint32_t* h, HufCode& c, HufWork& wk, const FseCT& tll,
-                                               const FseCT& tml, const FseCT& tof) {
+                                               uint32_t* h, HufCode& c, HufWork& wk) {
     uint32_t nl = 0, cov = 0;
     const uint32_t ns = greedy_parse(in, n, sc.best, cand, sc.seq, sc.lit, &nl, &cov);
     if (!ns) return 0;
     uint32_t z = lit_section_seq(sc.lit, nl, sc.body, sc.streams, h, c, wk);
-    z += seq_section(sc.seq, ns, sc.body + z, tll, tml, tof);
+    z += seq_section(sc.seq, ns, sc.body + z, sc.fse[0], sc.fse[1], sc.fse[2]);
     return z;
 }
 
@@ -605,8 +713,7 @@ __host__ inline uint32_t block_content_seq(const uint8_t* in, uint32_t n, uint8_
     uint32_t nbest = 0;
     for (uint32_t p = 0; p < n; ++p) nbest += (sc.best[p] = best_at(in, n, p, cand, nc)) != 0;
     if (lz_worth(nbest, n)) {
-        const FseTables& T = FseTables::get();
-        const uint32_t z = lz_content(in, n, cand, sc, hh, code, work, T.ll, T.ml, T.of);
+        const uint32_t z = lz_content(in, n, cand, sc, hh, code, work);
         if (z && z < size) {
             if (z < n)
                 for (uint32_t i = 0; i < z; ++i) slot[i] = sc.body[i];

@@ -295,7 +295,8 @@ static void zstd_case(std::mt19937_64& rng, uint64_t* blocks, uint64_t* replica_
             body(zstd::kBodyBytes);
         Arr<uint32_t> best(zstd::kBlockMax);
         Arr<zstd::Seq> seq(zstd::kMaxSeq);
-        const zstd::SeqScratch sc{best.get(), seq.get(), lit.get(), streams.get(), body.get()};
+        Arr<zstd::FseCT> fse(3);
+        const zstd::SeqScratch sc{best.get(), seq.get(), lit.get(), streams.get(), body.get(), fse.get()};
         uint32_t type = 9;
         const uint32_t size = zstd::block_content_seq(b, n, slot.get(), sc, &type);
         CHECK(type <= 2);
