@@ -227,6 +227,8 @@ def cpu_zstd_baseline(text_dev, sample_bytes: int = 64 << 20):
     system libzstd on one thread, on a prefix of the same Delta JSON text."""
     import ctypes.util
 
+    import numpy as np
+
     z = ctypes.CDLL(ctypes.util.find_library("zstd") or "libzstd.so.1")
     z.ZSTD_compress.restype = ctypes.c_size_t
     z.ZSTD_compress.argtypes = [ctypes.c_void_p, ctypes.c_size_t, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int]
@@ -840,7 +842,7 @@ def main():
                     "local": f"local transport: change-ratio sample + block compare of two {n / GIB:.0f} GiB files, "
                              f"bs {bs}, {args.edit_ppm / 1e4:g}% of blocks edited",
                     "json": f"serde_json text of the C3 delta ({n / GIB:.0f} GiB source, one literal run) on the device",
-                    "zstd": f"zstd frame (entropy-only blocks) of the C3 delta's JSON text ({n / GIB:g} GiB source, "
+                    "zstd": f"zstd frame (Huffman literals + FSE-coded sequences, 128 KiB blocks) of the C3 delta's JSON text ({n / GIB:g} GiB source, "
                             f"one literal run) on the device; value = text bytes/s",
                     "path": f"path API on page-cache-warm files: compute_checksums({n / GIB:g} GiB basis) + "
                             f"generate_delta_streaming({n / GIB:g} GiB source, {args.edit_ppm / 1e4:g}% of {bs} B "

@@ -14,10 +14,15 @@ def pytest_configure(config):
     config.addinivalue_line("markers", "late: host-side machinery around the kernels (child processes, "
                                        "concurrent callers, streamed files, GiB of temp files); runs after the "
                                        "kernel parity tests so that a failure there under -x does not hide them")
+    config.addinivalue_line("markers", "firstrun: kernels that have not yet run on hardware (written while the "
+                                       "round's GPU access was closed); run last, after the late tests, so that a "
+                                       "fault there under -x cannot hide any test of hardware-validated code")
 
 
 def pytest_collection_modifyitems(config, items):
-    items.sort(key=lambda it: it.get_closest_marker("late") is not None)  # stable: order otherwise unchanged
+    # stable: order otherwise unchanged.  Validated kernels, then host machinery, then
+    # kernels on their first hardware run.
+    items.sort(key=lambda it: (it.get_closest_marker("firstrun") is not None, it.get_closest_marker("late") is not None))
 
 
 @pytest.fixture(scope="session")

@@ -82,3 +82,38 @@ def test_roofline_scan_l1_modelled_requests():
     assert "level-1" in g["model"]
     # without the key count no request rate is claimed
     assert "l2_gather" not in bench.roofline({"k_scan_l1": {"ms": 172.4, "count": 10}}, 10, algo, positions=n)
+
+
+def test_cpu_baselines_other_workloads_small():
+    """The CPU legs of the zstd, json, xxh3, apply and local workloads on small CPU
+    tensors (the bench hands them device tensors; each leg copies to the host first)."""
+    import types
+
+    import numpy as np
+    import torch
+
+    from oracle import oracle as O
+
+    bs = 4096
+    basis = torch.from_numpy(O.synth_bytes(1 << 20, 0x5E1D0005))
+    new = basis.clone()
+    new[5000] ^= 1
+    text = torch.from_numpy(np.frombuffer(b'{"ops":[' + b'{"Copy":{"offset":4096,"size":4096}},' * 4000 + b']}',
+                                          np.uint8).copy())
+    z = bench.cpu_zstd_baseline(text, sample_bytes=64 << 10)
+    assert z["value"] > 0 and "level 3" in z["sample"]
+    j = bench.cpu_json_baseline(new, bs)
+    assert j["value"] > 0 and j["cores"] == 1
+    offs = np.arange(4, dtype=np.uint64) * np.uint64(1 << 18)
+    lens = np.full(4, 1 << 18, np.uint64)
+    x = bench.cpu_xxh3_baseline(basis, offs, lens)
+    assert x["value"] > 0 and x["sample"].startswith("4 file(s)")
+    # a delta rebuilding `new`: blocks 0 and 2.. copied, block 1 literal
+    nb = basis.numel() // bs
+    kind = [0, 1] + [0] * (nb - 2)
+    a = [0, bs] + [k * bs for k in range(2, nb)]
+    d = types.SimpleNamespace(kind=kind, a=a, b=[bs] * nb)
+    ap = bench.cpu_apply_baseline(basis, new, d, sample_bytes=1 << 20)
+    assert ap["value"] > 0 and f"{nb} ops" in ap["sample"]
+    lo = bench.cpu_local_baseline(new, basis, 65536, sample_bytes=1 << 20)
+    assert lo["value"] > 0

@@ -18,7 +18,7 @@ import pytest
 
 from oracle import oracle as O
 
-pytestmark = [pytest.mark.gpu, pytest.mark.late]
+pytestmark = [pytest.mark.gpu, pytest.mark.late, pytest.mark.firstrun]
 
 
 @pytest.fixture

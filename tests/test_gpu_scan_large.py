@@ -1,6 +1,7 @@
 """GPU parity for large single-file indexes (> 16 Ki basis blocks): both scans of a
-large index -- k_scan_lds in global-filter mode (the default) and the level-1-filter
-scan k_scan_l1 (SYDELTA_SCAN_L1=1) -- against the oracle.
+large index -- the level-1-filter scan k_scan_l1 (the default at n = 4096,
+SYDELTA_SCAN_L1=1) and k_scan_lds in global-filter mode (SYDELTA_SCAN_L1=0) -- against
+the oracle.
 
 * 96 MiB basis, mixed edits (an all-literal stretch, sparse substitutions, a shift,
   planted unaligned copies, duplicated blocks): bit-exact op list against the C
