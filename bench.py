@@ -18,6 +18,9 @@ already resident in HBM:
   json: serde_json text of the C3 delta (one 4 GiB literal run,
      ~3.6 characters per byte) written on the device; value = delta source GiB/s;
      cpu_baseline = the same text from libsydelta's host writer on a 256 MiB sample.
+  sigjson (sy-remote.rs:146-147): serde_json text of the C2
+     signature (4 GiB basis, 1 Mi entries) written on the device; value = basis GiB/s
+     covered; cpu_baseline = libsydelta's host writer on the same signature.
   zstd (ssh.rs:1009-1017): the zstd frame of that JSON text (1 GiB
      source by default, ~3.6 GiB of text) on the device; value = text GiB/s;
      cpu_baseline = libzstd level 3 (compress/mod.rs:71-76) on one thread, 64 MiB sample.
@@ -70,7 +73,7 @@ def parse():
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--workload", default="c3",
-                    choices=["c3", "c3b", "c2", "c4", "c5", "apply", "json", "zstd", "local", "xxh3", "path"])
+                    choices=["c3", "c3b", "c2", "c4", "c5", "apply", "json", "sigjson", "zstd", "local", "xxh3", "path"])
     ap.add_argument("--size-gib", type=float, default=None,
                     help="bytes per rank: c2/c3 basis and source (default 4), c5 chunk (default 8)")
     ap.add_argument("--block-size", type=int, default=None, help="default 4096 (c5: 8192)")
@@ -220,6 +223,24 @@ def cpu_json_baseline(src_dev, bs: int):
     dt = time.perf_counter() - t0
     return {"value": round(sample.size / dt / GIB, 4), "unit": "GiB/s", "cores": 1, "kind": "port",
             "sample": f"host writer, one Data op of {sample.size >> 20} MiB ({len(text) >> 20} MiB of text)"}
+
+
+def cpu_sigjson_baseline(w_dev, s_dev, bs: int):
+    """libsydelta's host serde_json writer (sydelta_checksums_to_json, one thread) on the
+    same signature: what sy-remote does after compute_checksums (sy-remote.rs:146-147)."""
+    import numpy as np
+
+    from sy_amd import wire
+
+    w = w_dev.cpu().numpy().view(np.uint32)
+    s = s_dev.cpu().numpy().view(np.uint64)
+    idx = np.arange(w.size, dtype=np.uint64)
+    sig = wire.sig_array(idx, idx * np.uint64(bs), np.full(w.size, bs, np.uint64), w, s)
+    t0 = time.perf_counter()
+    text = wire.checksums_to_json(sig)
+    dt = time.perf_counter() - t0
+    return {"value": round(w.size * bs / dt / GIB, 4), "unit": "GiB/s", "cores": 1, "kind": "port",
+            "sample": f"host writer, {w.size} entries ({len(text) >> 20} MiB of text), basis GiB/s covered"}
 
 
 def cpu_zstd_baseline(text_dev, sample_bytes: int = 64 << 20):
@@ -445,6 +466,7 @@ def algo_bytes_per_step(workload: str, n: int, nb_bytes: int, src_bytes: int) ->
             "k_apply": 2 * n,  # apply: every output byte read once and written once
             "k_json_write": n,  # json: every literal byte read once (text written: ~3.6x)
             "k_zstd_block": src_bytes,  # zstd: every text byte read once
+            "k_sigjson_write": src_bytes,  # sigjson: 12 B per entry read + the text written once
             "k_block_cmp": 2 * n,  # local: both files read once
             "k_xxh_pieces": n}  # xxh3: every file byte read once
 
@@ -561,6 +583,12 @@ def main():
             check(lib.sydelta_delta_to_json_device(json_h, new.data_ptr(), n, json_out.data_ptr(), json_out.numel(),
                                                    ctypes.byref(json_len), None))
             zstd_out = torch.empty(int(lib.sydelta_zstd_bound(zstd_len)) + 16, dtype=torch.uint8, device="cuda")
+    if args.workload == "sigjson":
+        from sy_amd import wire
+
+        sj_w, sj_s = dev.signature(basis, bs)
+        sj_len = int(wire.checksums_to_json_device(sj_w, sj_s, bs, bs).numel())
+        sj_out = torch.empty(sj_len + 16, dtype=torch.uint8, device="cuda")
     if args.workload == "apply":
         dev.synth_fill_range(basis, 0, 0x5E1D0005)
         new = torch.empty(n + 16, dtype=torch.uint8, device="cuda")
@@ -707,6 +735,12 @@ def main():
             check(lib.sydelta_zstd_compress_device(local, json_out.data_ptr(), zstd_len, zstd_out.data_ptr(),
                                                    zstd_out.numel(), ctypes.byref(got), int(stream.cuda_stream)))
             return {"text_bytes": zstd_len, "frame_bytes": got.value, "ratio": round(got.value / zstd_len, 4)}
+        if args.workload == "sigjson":
+            ln = ctypes.c_uint64()
+            check(lib.sydelta_checksums_to_json_device(sj_w.data_ptr(), sj_s.data_ptr(), sj_w.numel(), bs, bs,
+                                                       sj_out.data_ptr(), sj_out.numel(), ctypes.byref(ln),
+                                                       int(stream.cuda_stream)))
+            return {"json_bytes": ln.value, "entries": sj_w.numel()}
         if args.workload == "json":
             ln = ctypes.c_uint64()
             check(lib.sydelta_delta_to_json_device(json_h, new.data_ptr(), n, json_out.data_ptr(), json_out.numel(),
@@ -769,6 +803,8 @@ def main():
         bytes_per_step = zstd_len  # JSON text compressed
     elif args.workload == "json":
         bytes_per_step = n  # delta source bytes covered by the text
+    elif args.workload == "sigjson":
+        bytes_per_step = n  # basis bytes covered by the signature text
     elif args.workload == "path":
         bytes_per_step = 2 * n  # basis file signed + source file matched
     else:
@@ -778,7 +814,8 @@ def main():
     ms_per_step = elapsed / args.steps * 1e3
 
     src_bytes = (int(files[3].sum()) if args.workload == "c4" else new.numel() if args.workload == "c3b" else
-                 zstd_len if args.workload == "zstd" else n)
+                 zstd_len if args.workload == "zstd" else
+                 sj_len + 12 * (n // bs) if args.workload == "sigjson" else n)
     algo_step = algo_bytes_per_step(args.workload, n, nb_bytes, src_bytes)
     stats = (last if isinstance(last, dict) else last.stats) if last is not None else None
     positions = stats.get("positions") if isinstance(stats, dict) and args.workload in ("c3", "c3b") else None
@@ -797,6 +834,8 @@ def main():
                                   new[:int(files[2][k - 1] + files[3][k - 1])].cpu().numpy(), files, bs, sample_files=k)
         if world == 1 and not args.no_cpu_baseline and args.workload == "zstd":
             cpu = cpu_zstd_baseline(json_out[:zstd_len])
+        if world == 1 and not args.no_cpu_baseline and args.workload == "sigjson":
+            cpu = cpu_sigjson_baseline(sj_w, sj_s, bs)
         if world == 1 and not args.no_cpu_baseline and args.workload == "json":
             cpu = cpu_json_baseline(new, bs)
         if world == 1 and not args.no_cpu_baseline and args.workload == "xxh3":
@@ -841,6 +880,8 @@ def main():
                              f"integrity: whole-file XXH3-64 of one {n / GIB:.0f} GiB file"),
                     "local": f"local transport: change-ratio sample + block compare of two {n / GIB:.0f} GiB files, "
                              f"bs {bs}, {args.edit_ppm / 1e4:g}% of blocks edited",
+                    "sigjson": f"serde_json text of the C2 signature ({n / GIB:g} GiB basis, {n // bs} entries) "
+                               f"on the device",
                     "json": f"serde_json text of the C3 delta ({n / GIB:.0f} GiB source, one literal run) on the device",
                     "zstd": f"zstd frame (Huffman literals + FSE-coded sequences, 128 KiB blocks) of the C3 delta's JSON text ({n / GIB:g} GiB source, "
                             f"one literal run) on the device; value = text bytes/s",

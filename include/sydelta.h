@@ -277,10 +277,20 @@ int sydelta_delta_to_json(const sydelta_delta *d, const uint8_t *lit, uint64_t l
  * Data ops' source offsets) into d_out; *out_len as above (computed on the device). */
 int sydelta_delta_to_json_device(const sydelta_delta *d, const uint8_t *d_lit, uint64_t lit_len, uint8_t *d_out,
                                  uint64_t out_cap, uint64_t *out_len, void *stream);
+/* serde_json::to_string(&Vec<BlockChecksum>) of a signature in HBM, written on the device:
+ * the line `sy-remote checksums` prints (sy-remote.rs:146-147) and ssh.rs:967-973 parses,
+ * for the SoA sydelta_signature_device writes (n blocks in index order, block i at offset
+ * i * block_size, size block_size except the last, last_size in (0, block_size]).  Same
+ * text as sydelta_checksums_to_json.  *out_len = text length (computed on the device);
+ * the text is written when d_out holds it (d_out NULL: length only). */
+int sydelta_checksums_to_json_device(const uint32_t *d_weak, const uint64_t *d_strong, uint64_t n,
+                                     uint64_t block_size, uint64_t last_size, uint8_t *d_out, uint64_t out_cap,
+                                     uint64_t *out_len, void *stream);
 /* The zstd frame (RFC 8878) of d_in[0, len) into d_out, on the device: what ssh.rs:1009-1017
  * sends (compress(delta_json, Compression::Zstd), compress/mod.rs:71-76) and sy-remote
  * decompresses (sy-remote.rs:160-179) -- typically the text of sydelta_delta_to_json_device.
- * Entropy-only blocks (Huffman literals, no matches; Raw / RLE where smaller): any zstd
+ * One 128 KiB block per workgroup: Huffman-coded literals alone, or literals + FSE-coded
+ * sequences (matches at the JSON skeleton's distances), Raw / RLE where smaller; any zstd
  * decoder returns the input; the bytes differ from libzstd level 3's.  d_in 16-byte
  * aligned and readable to the end of its last 16-byte granule; out_cap >=
  * sydelta_zstd_bound(len); *out_len = frame size. */

@@ -8,6 +8,7 @@
 #include <vector>
 
 #include "sydelta_chain.hpp"
+#include "sydelta_sigjson.hpp"
 #include "sydelta_zstd.hpp"
 
 namespace sydelta {
@@ -169,6 +170,11 @@ hipError_t launch_json_len(const JsonPiece* d_pieces, uint64_t npieces, const ui
 hipError_t launch_json_write(const JsonPiece* d_pieces, uint64_t npieces, const uint8_t* d_lit,
                              const uint64_t* d_off, uint64_t base, uint8_t* d_out, hipStream_t s, Profiler* prof);
 hipError_t launch_exclusive_sum_u64(const uint64_t* d_in, uint64_t* d_out, uint64_t n, hipStream_t s);
+// Signature JSON (sydelta_sigjson.hpp, K7s): d_tile_len[t] = text length of entries
+// [t * kTile, +kTile); then tile t's text at d_out + d_tile_off[t].
+hipError_t launch_sigjson_len(const sigjson::SigArgs& a, uint64_t* d_tile_len, hipStream_t s, Profiler* prof);
+hipError_t launch_sigjson_write(const sigjson::SigArgs& a, const uint64_t* d_tile_off, uint8_t* d_out, hipStream_t s,
+                                Profiler* prof);
 // zstd frame of a text in HBM (sydelta_zstd.hpp).  Blocks [b0, b0 + nb) of d_text (len
 // bytes, 16-byte aligned, readable to the end of its last granule): slot i of d_slots
 // (zstd::kBlockMax bytes each) gets block b0+i's content, d_size[i] its size, d_type[i]

@@ -2705,6 +2705,36 @@ __device__ __forceinline__ uint32_t json_copy_len(const JsonPiece& P) {
     return (P.flags & kJsonSep ? 1u : 0u) + 28u + dec_digits(P.a) + dec_digits(P.b);  // {"Copy":{"offset":,"size":}}
 }
 
+// K7s: serde_json text of a device-resident signature (sydelta_sigjson.hpp).  Per tile of
+// kTile entries: the summed text length, then the text composed in LDS and stored with
+// 16-byte stores (byte stores on the two edge chunks shared with the neighbours).
+__global__ __launch_bounds__(sigjson::kTile) void k_sigjson_len(sigjson::SigArgs a, uint64_t* __restrict__ tile_len) {
+    typedef hipcub::BlockReduce<uint32_t, sigjson::kTile> Reduce;
+    __shared__ typename Reduce::TempStorage tmp;
+    const uint64_t i = (uint64_t)blockIdx.x * sigjson::kTile + threadIdx.x;
+    const uint32_t len = i < a.n ? sigjson::entry_len(a, i) : 0u;
+    const uint32_t tot = Reduce(tmp).Sum(len);
+    if (threadIdx.x == 0) tile_len[blockIdx.x] = tot;
+}
+
+__global__ __launch_bounds__(sigjson::kTile) void k_sigjson_write(sigjson::SigArgs a,
+                                                                  const uint64_t* __restrict__ tile_off,
+                                                                  uint8_t* __restrict__ out) {
+    typedef hipcub::BlockScan<uint32_t, sigjson::kTile> Scan;
+    __shared__ typename Scan::TempStorage tmp;
+    __shared__ __attribute__((aligned(16))) uint8_t stage[sigjson::kStage];
+    const uint64_t i = (uint64_t)blockIdx.x * sigjson::kTile + threadIdx.x;
+    const uint32_t len = i < a.n ? sigjson::entry_len(a, i) : 0u;
+    uint32_t off = 0, tot = 0;
+    Scan(tmp).ExclusiveSum(len, off, tot);
+    if (i < a.n) sigjson::entry_write(a, i, stage + off);
+    __syncthreads();
+    uint8_t* dst = out + tile_off[blockIdx.x];
+    const uintptr_t c0 = (uintptr_t)dst & ~(uintptr_t)15, c1 = ((uintptr_t)dst + tot + 15) & ~(uintptr_t)15;
+    for (uintptr_t c = c0 + 16ull * threadIdx.x; c < c1; c += 16ull * sigjson::kTile)
+        sigjson::store_chunk(stage, tot, dst, c);
+}
+
 __global__ __launch_bounds__(256) void k_json_len(const JsonPiece* __restrict__ pieces, uint64_t npieces,
                                                   const uint8_t* __restrict__ lit, uint64_t* __restrict__ len) {
     // one wave per piece (lane l sizes literal bytes [64l, 64l + 64) of a Data chunk);
@@ -3625,6 +3655,25 @@ hipError_t launch_json_write(const JsonPiece* d_pieces, uint64_t npieces, const 
     ProfScope ps(prof, s, "k_json_write");
     hipLaunchKernelGGL(k_json_write, dim3((unsigned)npieces), dim3(256), kJsonStage, s, d_pieces, d_lit, d_off, base,
                        d_out);
+    return hipGetLastError();
+}
+
+hipError_t launch_sigjson_len(const sigjson::SigArgs& a, uint64_t* d_tile_len, hipStream_t s, Profiler* prof) {
+    const uint64_t nt = (a.n + sigjson::kTile - 1) / sigjson::kTile;
+    if (!nt) return hipSuccess;
+    if (nt > 0x7FFFFFFFull) return hipErrorInvalidValue;
+    ProfScope ps(prof, s, "k_sigjson_len");
+    hipLaunchKernelGGL(k_sigjson_len, dim3((unsigned)nt), dim3(sigjson::kTile), 0, s, a, d_tile_len);
+    return hipGetLastError();
+}
+
+hipError_t launch_sigjson_write(const sigjson::SigArgs& a, const uint64_t* d_tile_off, uint8_t* d_out, hipStream_t s,
+                                Profiler* prof) {
+    const uint64_t nt = (a.n + sigjson::kTile - 1) / sigjson::kTile;
+    if (!nt) return hipSuccess;
+    if (nt > 0x7FFFFFFFull) return hipErrorInvalidValue;
+    ProfScope ps(prof, s, "k_sigjson_write");
+    hipLaunchKernelGGL(k_sigjson_write, dim3((unsigned)nt), dim3(sigjson::kTile), 0, s, a, d_tile_off, d_out);
     return hipGetLastError();
 }
 

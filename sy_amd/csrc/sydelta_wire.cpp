@@ -509,6 +509,64 @@ extern "C" int sydelta_delta_to_json_device(const sydelta_delta* d, const uint8_
 }
 
 // ---------------------------------------------------------------------------
+// serde_json::to_string(&Vec<BlockChecksum>) of a signature in HBM (sy-remote.rs:146-147;
+// sydelta_sigjson.hpp, K7s): tile lengths on the device, their exclusive scan, the total
+// checked against the bounds the implied fields give, then the text.
+// ---------------------------------------------------------------------------
+extern "C" int sydelta_checksums_to_json_device(const uint32_t* d_weak, const uint64_t* d_strong, uint64_t n,
+                                                uint64_t block_size, uint64_t last_size, uint8_t* d_out,
+                                                uint64_t out_cap, uint64_t* out_len, void* stream) try {
+    if (!out_len) return fail(SYDELTA_E_INVAL, "NULL argument");
+    if (n && (!d_weak || !d_strong)) return fail(SYDELTA_E_INVAL, "NULL signature arrays");
+    if (n && (block_size == 0 || block_size > (1ull << 32) || last_size == 0 || last_size > block_size))
+        return fail(SYDELTA_E_INVAL, "block_size %llu / last_size %llu out of range", (unsigned long long)block_size,
+                    (unsigned long long)last_size);
+    if (n && n - 1 > (UINT64_MAX - last_size) / block_size)
+        return fail(SYDELTA_E_INVAL, "offsets of %llu blocks overflow", (unsigned long long)n);
+    int dev = 0;
+    (void)hipGetDevice(&dev);
+    if (int r = ensure_device(dev)) return r;
+    hipStream_t s = stream ? (hipStream_t)stream : thread_stream(dev);
+    uint64_t lo = 0, hi = 0;
+    sigjson::text_bounds(n, block_size, last_size, lo, hi);
+    if (n == 0) {
+        *out_len = 2;
+        if (d_out && out_cap >= 2) {
+            HIP_TRY(hipMemcpyAsync(d_out, "[]", 2, hipMemcpyHostToDevice, s));
+            HIP_TRY(hipStreamSynchronize(s));
+        }
+        return SYDELTA_OK;
+    }
+    const sigjson::SigArgs a{d_weak, d_strong, n, block_size, last_size};
+    const uint64_t nt = (n + sigjson::kTile - 1) / sigjson::kTile;
+    CallProf cp;
+    DevBuf_wire buf;
+    HIP_TRY(hipMallocAsync(&buf.p, 2 * nt * 8, s));
+    buf.s = s;
+    uint64_t* d_tlen = (uint64_t*)buf.p;
+    uint64_t* d_toff = d_tlen + nt;
+    HIP_TRY(launch_sigjson_len(a, d_tlen, s, cp.get()));
+    HIP_TRY(launch_exclusive_sum_u64(d_tlen, d_toff, nt, s));
+    uint64_t last_off = 0, last_len = 0;
+    HIP_TRY(hipMemcpyAsync(&last_off, d_toff + nt - 1, 8, hipMemcpyDeviceToHost, s));
+    HIP_TRY(hipMemcpyAsync(&last_len, d_tlen + nt - 1, 8, hipMemcpyDeviceToHost, s));
+    HIP_TRY(hipStreamSynchronize(s));
+    const uint64_t total = last_off + last_len;
+    // a total outside the bounds means a sizing fault: never write with it
+    if (total < lo || total > hi)
+        return fail(SYDELTA_E_KERNEL, "signature JSON sizing out of bounds (%llu not in [%llu, %llu])",
+                    (unsigned long long)total, (unsigned long long)lo, (unsigned long long)hi);
+    *out_len = total;
+    if (d_out && out_cap >= total) {
+        HIP_TRY(launch_sigjson_write(a, d_toff, d_out, s, cp.get()));
+        HIP_TRY(hipStreamSynchronize(s));
+    }
+    return SYDELTA_OK;
+} catch (...) {
+    return sydelta::host_exception();
+}
+
+// ---------------------------------------------------------------------------
 // zstd frame of a text in HBM (ssh.rs:1009-1017: compress(delta_json, Compression::Zstd);
 // sydelta_zstd.hpp).  The text goes through in batches of 512 blocks (64 MiB): block
 // contents into per-block slots (k_zstd_block), their placement (an exclusive scan of

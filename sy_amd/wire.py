@@ -92,8 +92,29 @@ def delta_to_json_device(kind, a, b, source_size: int, block_size: int, d_lit, s
         lib.sydelta_delta_free(h)
 
 
+def checksums_to_json_device(d_weak, d_strong, block_size: int, last_size: int, stream=None):
+    """serde_json::to_string(&Vec<BlockChecksum>) of a signature in HBM (the weak/strong
+    tensors of device.signature), written on the device (sy-remote.rs:146-147); returns
+    the text as a uint8 device tensor."""
+    import torch
+
+    from .device import _ptr, _stream
+
+    nb = d_weak.numel()
+    if d_strong.numel() != nb:
+        raise ValueError("weak and strong arrays differ in length")
+    n = ctypes.c_uint64()
+    wp, sp = (_ptr(d_weak), _ptr(d_strong)) if nb else (None, None)
+    check(lib.sydelta_checksums_to_json_device(wp, sp, nb, block_size, last_size, None, 0, ctypes.byref(n),
+                                               _stream(stream)))
+    out = torch.empty(n.value + 16, dtype=torch.uint8, device=d_weak.device)
+    check(lib.sydelta_checksums_to_json_device(wp, sp, nb, block_size, last_size, _ptr(out), out.numel(),
+                                               ctypes.byref(n), _stream(stream)))
+    return out[:n.value]
+
+
 def zstd_compress_device(d_text, stream=None, device: int = 0):
-    """zstd frame (entropy-only blocks) of the bytes of a uint8 device tensor, as a uint8
+    """zstd frame (Huffman literals, FSE-coded sequences) of the bytes of a uint8 device tensor, as a uint8
     device tensor: the compression ssh.rs:1009-1017 applies to the Delta JSON.  The
     tensor must start 16-byte aligned (torch allocations and views at offset 0 do)."""
     import torch

@@ -10,7 +10,7 @@ generator, tiny and empty files, the probe + on-demand scan walk (SYDELTA_PROBE=
 the split walk (SYDELTA_WALK_PAR_MIN=1), the path-level change ratio on ratio.rs's
 cases, 10 threads calling the path API at once, the batched device-pointer path (80
 files incl. empty and sub-block ones, threaded walks) and a file matched in 1/2/3/8
-chained chunks.
+chained chunks, the device zstd and signature-JSON writers' host sides.
 """
 import os
 import sys
@@ -158,6 +158,7 @@ def main():
         n_checks += error_checks(tmp)
         n_checks += device_walk_checks(tmp)
         n_checks += zstd_checks()
+        n_checks += sigjson_checks()
     print(f"emulated host checks ok: {n_checks}")
 
 
@@ -194,6 +195,72 @@ def zstd_checks():
             n += 1
     os.environ.pop("SYDELTA_ZSTD_BATCH", None)
     return n
+
+
+def sigjson_checks():
+    """sydelta_checksums_to_json_device (K7s; the emulated launches run sydelta_sigjson.hpp's
+    per-thread bodies tile by tile): the text equals json.dumps of the same list of dicts
+    with serde's separators and the host writer's, written at every destination alignment
+    without touching a byte outside it; the length query, a too-small buffer (nothing
+    written), the empty signature and the argument checks."""
+    import ctypes
+    import json
+
+    from sy_amd import wire
+    from sy_amd._lib import check, lib
+
+    rng = np.random.default_rng(7)
+    n_checks = 0
+    cases = [(1, 4096, 1), (1, 4096, 4096), (255, 512, 100), (256, 4096, 4096), (257, 8192, 17),
+             (1000, 131072, 65536), (3 * 256 + 5, 1 << 32, 1 << 32), (20000, 4096, 3000)]
+    for n, bs, last in cases:
+        for dist in ("uniform", "extremes"):
+            if dist == "uniform":
+                weak = rng.integers(0, 1 << 32, n, dtype=np.uint64).astype(np.uint32)
+                strong = rng.integers(0, 1 << 64, n, dtype=np.uint64)
+            else:  # 0, 9, 10, max and every digit count
+                wv = np.array([0, 9, 10, 99, 100, 65535, 0xFFFFFFFF], np.uint32)
+                sv = np.array([0, 9, 10, 10**10, 10**19 - 1, 10**19, 0xFFFFFFFFFFFFFFFF], np.uint64)
+                weak, strong = wv[rng.integers(0, wv.size, n)], sv[rng.integers(0, sv.size, n)]
+            sizes = np.full(n, bs, np.uint64)
+            sizes[-1] = last
+            idx = np.arange(n, dtype=np.uint64)
+            ref = json.dumps([{"index": int(i), "offset": int(i) * bs, "size": int(z), "weak": int(w), "strong": int(t)}
+                              for i, z, w, t in zip(idx, sizes, weak, strong)], separators=(",", ":")).encode()
+            assert wire.checksums_to_json(wire.sig_array(idx, idx * np.uint64(bs), sizes, weak, strong)) == ref
+            got = ctypes.c_uint64()
+            check(lib.sydelta_checksums_to_json_device(ctypes.c_void_p(weak.ctypes.data),
+                                                       ctypes.c_void_p(strong.ctypes.data), n, bs, last, None, 0,
+                                                       ctypes.byref(got), None))
+            assert got.value == len(ref), (n, bs, dist, got.value, len(ref))
+            for shift in (0, 1, 7, 15) if n < 5000 else (3,):
+                buf = np.full(len(ref) + 64, 0xEE, np.uint8)
+                # too small by one: nothing written
+                check(lib.sydelta_checksums_to_json_device(ctypes.c_void_p(weak.ctypes.data),
+                                                           ctypes.c_void_p(strong.ctypes.data), n, bs, last,
+                                                           ctypes.c_void_p(buf.ctypes.data + 16 + shift),
+                                                           len(ref) - 1, ctypes.byref(got), None))
+                assert got.value == len(ref) and (buf == 0xEE).all()
+                check(lib.sydelta_checksums_to_json_device(ctypes.c_void_p(weak.ctypes.data),
+                                                           ctypes.c_void_p(strong.ctypes.data), n, bs, last,
+                                                           ctypes.c_void_p(buf.ctypes.data + 16 + shift), len(ref),
+                                                           ctypes.byref(got), None))
+                o = 16 + shift
+                assert buf[o:o + len(ref)].tobytes() == ref, (n, bs, dist, shift)
+                assert (buf[:o] == 0xEE).all() and (buf[o + len(ref):] == 0xEE).all(), (n, bs, dist, shift)
+                n_checks += 1
+    buf = np.zeros(8, np.uint8)
+    got = ctypes.c_uint64()
+    check(lib.sydelta_checksums_to_json_device(None, None, 0, 4096, 0, ctypes.c_void_p(buf.ctypes.data), 8,
+                                               ctypes.byref(got), None))
+    assert got.value == 2 and buf[:2].tobytes() == b"[]"
+    w1, s1 = np.zeros(4, np.uint32), np.zeros(4, np.uint64)
+    for bs, last in ((0, 1), (4096, 0), (4096, 4097), ((1 << 32) + 1, 1)):
+        rc = lib.sydelta_checksums_to_json_device(ctypes.c_void_p(w1.ctypes.data), ctypes.c_void_p(s1.ctypes.data), 4,
+                                                  bs, last, None, 0, ctypes.byref(got), None)
+        assert rc != 0, (bs, last)
+    assert lib.sydelta_checksums_to_json_device(None, None, 4, 4096, 4096, None, 0, ctypes.byref(got), None) != 0
+    return n_checks + 6
 
 
 def _walk_counters():

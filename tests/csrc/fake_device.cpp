@@ -21,6 +21,7 @@
 #include <atomic>
 #include <chrono>
 #include <map>
+#include <memory>
 #include <mutex>
 #include <numeric>
 #include <unordered_map>
@@ -404,6 +405,42 @@ hipError_t launch_json_write(const JsonPiece*, uint64_t, const uint8_t*, const u
                              hipStream_t, Profiler*) {
     EmuTimer emu_t;
     return hipErrorNotSupported;
+}
+// K7s: the kernels' per-thread bodies (sydelta_sigjson.hpp) tile by tile; each tile's
+// text is staged in an array of exactly its length and stored chunk by chunk, the
+// chunks in descending order (one schedule of the workgroup's threads).
+hipError_t launch_sigjson_len(const sigjson::SigArgs& a, uint64_t* d_tile_len, hipStream_t, Profiler*) {
+    EmuTimer emu_t;
+    const uint64_t nt = (a.n + sigjson::kTile - 1) / sigjson::kTile;
+    for (uint64_t t = 0; t < nt; ++t) {
+        uint64_t tot = 0;
+        for (uint64_t i = t * sigjson::kTile; i < std::min<uint64_t>(a.n, (t + 1) * sigjson::kTile); ++i)
+            tot += sigjson::entry_len(a, i);
+        d_tile_len[t] = tot;
+    }
+    return hipSuccess;
+}
+hipError_t launch_sigjson_write(const sigjson::SigArgs& a, const uint64_t* d_tile_off, uint8_t* d_out, hipStream_t,
+                                Profiler*) {
+    EmuTimer emu_t;
+    const uint64_t nt = (a.n + sigjson::kTile - 1) / sigjson::kTile;
+    for (uint64_t t = 0; t < nt; ++t) {
+        const uint64_t i0 = t * sigjson::kTile, i1 = std::min<uint64_t>(a.n, i0 + sigjson::kTile);
+        std::vector<uint32_t> off(i1 - i0 + 1, 0);
+        for (uint64_t i = i0; i < i1; ++i) off[i - i0 + 1] = off[i - i0] + sigjson::entry_len(a, i);
+        const uint32_t tot = off[i1 - i0];
+        std::unique_ptr<uint8_t[]> stage(new uint8_t[tot ? tot : 1]);
+        for (uint64_t i = i0; i < i1; ++i)
+            if (sigjson::entry_write(a, i, stage.get() + off[i - i0]) != off[i - i0 + 1] - off[i - i0])
+                return hipErrorLaunchFailure;
+        uint8_t* dst = d_out + d_tile_off[t];
+        const uintptr_t c0 = (uintptr_t)dst & ~(uintptr_t)15, c1 = ((uintptr_t)dst + tot + 15) & ~(uintptr_t)15;
+        for (uintptr_t c = c1; c > c0;) {
+            c -= 16;
+            sigjson::store_chunk(stage.get(), tot, dst, c);
+        }
+    }
+    return hipSuccess;
 }
 // K5b: the kernels' own per-thread bodies (sydelta_chain.hpp) in the launch order of
 // sydelta_kernels.hip's launch_chain, one loop per kernel.  The marking levels run their

@@ -12,7 +12,11 @@
 //  * the zstd block coder (sydelta_zstd.hpp, K7z): block_content_seq on random texts with
 //    its scratch as separate exact-size arrays; and a thread-by-thread replica of
 //    k_zstd_block's parallel bit scatter (runs of 144 aligned bytes per thread, suffix
-//    sums, OR-ed words) whose streams must equal the sequential writer's bytes.
+//    sums, OR-ed words) whose streams must equal the sequential writer's bytes;
+//  * the signature JSON writer (sydelta_sigjson.hpp, K7s): k_sigjson_write's tiles on
+//    random signatures, each tile's text staged in an array of exactly its length and
+//    stored chunk by chunk (chunks shuffled) into an output of exactly the text's length
+//    at a random alignment; the text equals a printf-built one and the length bounds hold.
 #include <stdint.h>
 #include <stdio.h>
 #include <stdlib.h>
@@ -22,9 +26,11 @@
 #include <memory>
 #include <numeric>
 #include <random>
+#include <string>
 #include <vector>
 
 #include "sydelta_chain.hpp"
+#include "sydelta_sigjson.hpp"
 #include "sydelta_walk.hpp"
 #include "sydelta_zstd.hpp"
 
@@ -330,6 +336,58 @@ static void zstd_case(std::mt19937_64& rng, uint64_t* blocks, uint64_t* replica_
     }
 }
 
+static void sigjson_case(std::mt19937_64& rng, uint64_t* entries) {
+    const uint64_t n = 1 + rng() % 1500;
+    const uint64_t bss[] = {1, 512, 4096, 8192, 131072, 1ull << 32};
+    const uint64_t bs = bss[rng() % 6];
+    const uint64_t last = 1 + rng() % bs;
+    std::unique_ptr<uint32_t[]> weak(new uint32_t[n]);
+    std::unique_ptr<uint64_t[]> strong(new uint64_t[n]);
+    for (uint64_t i = 0; i < n; ++i) {
+        const int k = (int)(rng() % 3);
+        weak[i] = k == 0 ? (uint32_t)rng() : k == 1 ? (uint32_t)(rng() % 100) : 0xFFFFFFFFu;
+        strong[i] = k == 0 ? rng() : k == 1 ? rng() % 1000 : ~0ull;
+    }
+    const sigjson::SigArgs a{weak.get(), strong.get(), n, bs, last};
+    std::string ref = "[";
+    char tmp[256];
+    for (uint64_t i = 0; i < n; ++i) {
+        snprintf(tmp, sizeof tmp, "%s{\"index\":%llu,\"offset\":%llu,\"size\":%llu,\"weak\":%u,\"strong\":%llu}",
+                 i ? "," : "", (unsigned long long)i, (unsigned long long)(i * bs),
+                 (unsigned long long)(i + 1 == n ? last : bs), weak[i], (unsigned long long)strong[i]);
+        ref += tmp;
+    }
+    ref += "]";
+    uint64_t lo = 0, hi = 0;
+    sigjson::text_bounds(n, bs, last, lo, hi);
+    CHECK(ref.size() >= lo && ref.size() <= hi);
+    // the output: exactly the text's length, at a random offset from a 16-byte boundary
+    const size_t shift = rng() % 16;
+    std::unique_ptr<uint8_t[]> raw(new uint8_t[ref.size() + shift]);
+    uint8_t* out = raw.get() + shift;
+    const uint64_t nt = (n + sigjson::kTile - 1) / sigjson::kTile;
+    uint64_t toff = 0;
+    for (uint64_t t = 0; t < nt; ++t) {
+        const uint64_t i0 = t * sigjson::kTile, i1 = std::min<uint64_t>(n, i0 + sigjson::kTile);
+        std::vector<uint32_t> off(i1 - i0 + 1, 0);
+        for (uint64_t i = i0; i < i1; ++i) off[i - i0 + 1] = off[i - i0] + sigjson::entry_len(a, i);
+        const uint32_t tot = off[i1 - i0];
+        CHECK(tot <= sigjson::kStage);
+        std::unique_ptr<uint8_t[]> stage(new uint8_t[tot]);
+        for (uint64_t i = i0; i < i1; ++i) CHECK(sigjson::entry_write(a, i, stage.get() + off[i - i0]) == off[i - i0 + 1] - off[i - i0]);
+        uint8_t* dst = out + toff;
+        const uintptr_t c0 = (uintptr_t)dst & ~(uintptr_t)15, c1 = ((uintptr_t)dst + tot + 15) & ~(uintptr_t)15;
+        std::vector<uintptr_t> cs;
+        for (uintptr_t c = c0; c < c1; c += 16) cs.push_back(c);
+        std::shuffle(cs.begin(), cs.end(), rng);
+        for (uintptr_t c : cs) sigjson::store_chunk(stage.get(), tot, dst, c);
+        toff += tot;
+    }
+    CHECK(toff == ref.size());
+    CHECK(memcmp(out, ref.data(), ref.size()) == 0);
+    *entries += n;
+}
+
 int main(int argc, char** argv) {
     const int iters = argc > 1 ? atoi(argv[1]) : 2000;
     std::mt19937_64 rng(20261017);
@@ -337,10 +395,12 @@ int main(int argc, char** argv) {
     for (int it = 0; it < iters; ++it) cases += chain_case(rng, &walked) >= 0;
     uint64_t blocks = 0, replica = 0;
     for (int it = 0; it < std::max(1, iters / 25); ++it) zstd_case(rng, &blocks, &replica);
+    uint64_t sj = 0;
+    for (int it = 0; it < std::max(1, iters / 10); ++it) sigjson_case(rng, &sj);
     CHECK(walked > (uint64_t)iters / 4);
     printf("kernel bodies ok: %llu chain cases (%llu resolved on the device path), %llu zstd blocks, %llu stream "
-           "replicas\n",
+           "replicas, %llu signature JSON entries\n",
            (unsigned long long)cases, (unsigned long long)walked, (unsigned long long)blocks,
-           (unsigned long long)replica);
+           (unsigned long long)replica, (unsigned long long)sj);
     return 0;
 }

@@ -117,3 +117,7 @@ def test_cpu_baselines_other_workloads_small():
     assert ap["value"] > 0 and f"{nb} ops" in ap["sample"]
     lo = bench.cpu_local_baseline(new, basis, 65536, sample_bytes=1 << 20)
     assert lo["value"] > 0
+    w = torch.from_numpy(np.arange(256, dtype=np.uint32).view(np.int32))
+    s = torch.from_numpy(np.arange(256, dtype=np.uint64).view(np.int64))
+    sj = bench.cpu_sigjson_baseline(w, s, bs)
+    assert sj["value"] > 0 and sj["sample"].startswith("host writer, 256 entries")
