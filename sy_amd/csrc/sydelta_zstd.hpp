@@ -301,7 +301,36 @@ __host__ __device__ __forceinline__ void fse_encode(BitW& w, const FseCT& t, uin
 
 struct Seq {
     uint32_t ll, ml, off;  // literal length, match length (>= kMinMatch), distance
+    uint32_t ov;           // Offset_Value: 1-3 a repeat offset, else off + 3 (rep_code)
 };
+
+// Offset_Value of a match at distance d after ll literals, and the decoder's update of
+// the repeat-offset history (RFC 8878 3.1.1.5; zstd's ZSTD_updateRep).  Blocks are coded
+// independently, so the history a block enters with is unknown to its coder: rep[] holds
+// only what this block's own sequences put there (0 = unknown), and a repeat code is used
+// only for a known entry.  Index r of the repeated offset is Offset_Value - 1, plus 1
+// when ll == 0 (then r = 3 means rep[0] - 1).
+__host__ __device__ __forceinline__ uint32_t rep_code(uint32_t* rep, uint32_t ll, uint32_t d) {
+    const uint32_t ll0 = ll == 0 ? 1u : 0u;
+    uint32_t ov = d + 3;
+    for (uint32_t r = ll0; r < 3 + ll0; ++r) {
+        const uint32_t v = r == 3 ? (rep[0] > 1 ? rep[0] - 1 : 0u) : rep[r];
+        if (v && v == d) {
+            ov = r + 1 - ll0;
+            break;
+        }
+    }
+    if (ov > 3) {
+        rep[2] = rep[1];
+        rep[1] = rep[0];
+        rep[0] = d;
+    } else if (ov - 1 + ll0 > 0) {
+        if (ov - 1 + ll0 >= 2) rep[2] = rep[1];
+        rep[1] = rep[0];
+        rep[0] = d;
+    }
+    return ov;
+}
 
 // Normalized counts of a block's codes (FSE_Compressed mode): table log L in [5, maxlog]
 // with 2^L >= 2 x the distinct codes, every present code >= 1, the rounding error taken
@@ -432,7 +461,7 @@ __host__ __device__ __forceinline__ void seq_codes(const Seq& q, uint32_t& lc, u
                                                    uint32_t& mb, uint32_t& oc, uint32_t& ov) {
     ll_code(q.ll, lc, lb);
     ml_code(q.ml, mc, mb);
-    ov = q.off + 3;  // Offset_Value: a distance, never a repeat code
+    ov = q.ov;
     oc = 0;
     while ((2u << oc) <= ov) ++oc;
 }
@@ -558,14 +587,23 @@ __host__ __device__ inline uint32_t greedy_parse(const uint8_t* in, uint32_t n, 
                                                  const uint32_t* cand, Seq* sq, uint8_t* lit, uint32_t* nlit,
                                                  uint32_t* covered) {
     uint32_t p = 0, ls = 0, ns = 0, nl = 0, cov = 0;
+    uint32_t rep[3] = {0, 0, 0};
     while (p < n) {
         const uint32_t b = best[p];
         if (!b) { lit[nl++] = in[p++]; continue; }
-        const uint32_t d = cand[b & 0xFF];
+        uint32_t d = cand[b & 0xFF];
         uint32_t l = b >> 8;
+        if (rep[0] && rep[0] != d && rep[0] <= p) {  // an equally long match at the repeat distance is cheaper
+            const uint32_t lim = (n - p) < kProbe ? (n - p) : kProbe;
+            uint32_t lr = 0;
+            while (lr < lim && in[p + lr] == in[p + lr - rep[0]]) ++lr;
+            if (lr >= l) d = rep[0];
+        }
         if (l == kProbe)
             while (p + l < n && in[p + l] == in[p + l - d]) ++l;
-        sq[ns++] = Seq{p - ls, l, d};
+        sq[ns] = Seq{p - ls, l, d, 0};
+        sq[ns].ov = rep_code(rep, p - ls, d);
+        ++ns;
         cov += l;
         p += l;
         ls = p;

@@ -13,6 +13,8 @@
 //    its scratch as separate exact-size arrays; and a thread-by-thread replica of
 //    k_zstd_block's parallel bit scatter (runs of 144 aligned bytes per thread, suffix
 //    sums, OR-ed words) whose streams must equal the sequential writer's bytes;
+//  * the zstd repeat-offset coder (rep_code) against a restatement of the decoder's
+//    history rules started from a history the coder does not know;
 //  * the signature JSON writer (sydelta_sigjson.hpp, K7s): k_sigjson_write's tiles on
 //    random signatures, each tile's text staged in an array of exactly its length and
 //    stored chunk by chunk (chunks shuffled) into an output of exactly the text's length
@@ -388,6 +390,35 @@ static void sigjson_case(std::mt19937_64& rng, uint64_t* entries) {
     *entries += n;
 }
 
+// zstd repeat offsets (sydelta_zstd.hpp rep_code): the Offset_Values the coder picks,
+// read back by an independent restatement of the decoder's history rules (RFC 8878
+// 3.1.1.5) that starts from a history the coder does not know, give every distance back.
+static void repcode_case(std::mt19937_64& rng, uint64_t* reps_used) {
+    uint32_t enc[3] = {0, 0, 0};
+    uint32_t h[3] = {1 + (uint32_t)(rng() % 50), 1 + (uint32_t)(rng() % 50), 1 + (uint32_t)(rng() % 50)};
+    const uint32_t pool[6] = {1 + (uint32_t)(rng() % 40), 1 + (uint32_t)(rng() % 40), 2 + (uint32_t)(rng() % 40),
+                              41, 42, 43};
+    for (int i = 0; i < 400; ++i) {
+        const uint32_t ll = rng() % 3 == 0 ? 0 : (uint32_t)(rng() % 20);
+        const uint32_t d = rng() % 4 == 0 ? 1 + (uint32_t)(rng() % 100000) : pool[rng() % 6];
+        const uint32_t ov = zstd::rep_code(enc, ll, d);
+        uint32_t off;
+        if (ov > 3) {
+            off = ov - 3;
+            h[2] = h[1]; h[1] = h[0]; h[0] = off;
+        } else {
+            const uint32_t idx = ov - 1 + (ll == 0 ? 1 : 0);
+            if (idx == 0) off = h[0];
+            else if (idx == 1) { off = h[1]; h[1] = h[0]; h[0] = off; }
+            else if (idx == 2) { off = h[2]; h[2] = h[1]; h[1] = h[0]; h[0] = off; }
+            else { off = h[0] - 1; h[2] = h[1]; h[1] = h[0]; h[0] = off; }
+            ++*reps_used;
+        }
+        CHECK(off == d);
+        CHECK(ov >= 1);
+    }
+}
+
 int main(int argc, char** argv) {
     const int iters = argc > 1 ? atoi(argv[1]) : 2000;
     std::mt19937_64 rng(20261017);
@@ -395,12 +426,15 @@ int main(int argc, char** argv) {
     for (int it = 0; it < iters; ++it) cases += chain_case(rng, &walked) >= 0;
     uint64_t blocks = 0, replica = 0;
     for (int it = 0; it < std::max(1, iters / 25); ++it) zstd_case(rng, &blocks, &replica);
+    uint64_t reps = 0;
+    for (int it = 0; it < std::max(1, iters / 10); ++it) repcode_case(rng, &reps);
+    CHECK(reps > 0);
     uint64_t sj = 0;
     for (int it = 0; it < std::max(1, iters / 10); ++it) sigjson_case(rng, &sj);
     CHECK(walked > (uint64_t)iters / 4);
     printf("kernel bodies ok: %llu chain cases (%llu resolved on the device path), %llu zstd blocks, %llu stream "
-           "replicas, %llu signature JSON entries\n",
+           "replicas, %llu repeat offsets, %llu signature JSON entries\n",
            (unsigned long long)cases, (unsigned long long)walked, (unsigned long long)blocks,
-           (unsigned long long)replica, (unsigned long long)sj);
+           (unsigned long long)replica, (unsigned long long)reps, (unsigned long long)sj);
     return 0;
 }
