@@ -2,7 +2,7 @@
 # Every bench workload once, one JSON line per leg under gpurun_out/<tag>/, each leg
 # under its own time limit; stops at the first failing leg.
 # Usage (from the repo root on the box): bash scripts/bench_legs.sh [tag] [legs...]
-#   default legs: c3 c3b c2 c5 c4 path apply json local xxh3
+#   default legs: c3 c3b c2 c5 c4 path apply json local xxh3 (sigjson and zstd: first hardware runs, named explicitly)
 set -u
 TAG=${1:-legs}; shift || true
 LEGS=${*:-c3 c3b c2 c5 c4 path apply json local xxh3}
