@@ -2418,7 +2418,8 @@ __global__ void k_chain_finish(chain::ChainArgs a) {
 // stream's symbols, its first bit at the sum of the later runs' bits (the stream is
 // written last symbol first), OR-ing whole 32-bit words into an LDS stream buffer; the
 // stream leaves for the block's slot with its closing 1 bit.  Literals + sequences: the
-// '{' distances and every position's best candidate match in parallel, then (when enough
+// '{' distances, the sampled repeat distances and every position's best candidate match in
+// parallel, then (when enough
 // positions match) one thread parses, codes the literals and FSE-codes the sequences with
 // the shared sequential functions (tables from the block's counts, in HBM scratch); the
 // smaller content stays in the slot.  k_zstd_frame
@@ -2435,6 +2436,7 @@ struct ZLds {
     zstd::HufCode code;
     zstd::HufWork work;
     uint32_t gaps[256];
+    uint32_t reps[256];
     uint32_t cand[zstd::kCands];
     uint32_t ssize[4];
     uint32_t state[8];  // [0] type, [1] write offset, [2] abort, [3] entropy-only size, [4] nc, [5] nbest, [6] lz size
@@ -2452,7 +2454,10 @@ __global__ __launch_bounds__(kZT) void k_zstd_block(const uint8_t* __restrict__ 
     uint8_t* slot = slots + (uint64_t)blockIdx.x * zstd::kBlockMax;
     const zstd::SeqScratch sc = zstd::seq_scratch_at(lz, nlz, blockIdx.x);
     for (uint32_t i = tid; i < 4 * 256; i += kZT) (&L.hist[0][0])[i] = 0;
-    for (uint32_t i = tid; i < 256; i += kZT) L.gaps[i] = 0;
+    for (uint32_t i = tid; i < 256; i += kZT) {
+        L.gaps[i] = 0;
+        L.reps[i] = 0;
+    }
     if (tid == 0) L.state[5] = 0;
     __syncthreads();
     // histogram, 16 bytes per load (the text is 16-byte aligned and readable to the end
@@ -2583,9 +2588,11 @@ __global__ __launch_bounds__(kZT) void k_zstd_block(const uint8_t* __restrict__ 
                         ++seen;
                     }
             }
+        for (uint32_t p = zstd::kRepStep * tid; p < n; p += zstd::kRepStep * kZT)
+            if (const uint32_t d = zstd::repeat_dist(in, n, p)) atomicAdd(&L.reps[d], 1u);
         __syncthreads();
         if (tid == 0) {
-            L.state[4] = zstd::pick_cands(L.gaps, L.cand);
+            L.state[4] = zstd::pick_cands(L.gaps, L.reps, L.cand);
         }
         __syncthreads();
         const uint32_t nc = L.state[4];

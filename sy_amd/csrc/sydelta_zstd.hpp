@@ -186,14 +186,20 @@ __host__ __device__ __forceinline__ void stream_range(uint32_t regen, bool four,
 // ---------------------------------------------------------------------------
 // A Delta's JSON repeats one skeleton per op ({"Copy":{"offset":...,"size":...}}), so the
 // matches that pay are at the distance of the previous op's text.  Candidate distances
-// are the block's most common gaps between consecutive '{' (and 1, runs); each position's
+// are 1 (runs), the block's most common gaps between consecutive '{', and its most common
+// short repeat distances (every kRepStep-th position's nearest earlier copy of its next 4
+// bytes within 255: a Data op's repeated numbers, other periodic text); each position's
 // best candidate is found independently (the device does all positions at once), a
 // greedy parse takes a match of >= kMinMatch wherever one starts, and the sequences are
 // FSE-coded with tables built from the block's own code counts (RLE for a code that
 // never changes).
 constexpr uint32_t kMinMatch = 4;
 constexpr uint32_t kProbe = 32;     // bytes compared per candidate when ranking them
-constexpr uint32_t kCands = 5;      // candidate distances: 1 and the 4 most common '{' gaps
+constexpr uint32_t kGapCands = 4;   // most common '{' gaps
+constexpr uint32_t kRepCands = 3;   // most common sampled repeat distances
+constexpr uint32_t kCands = 1 + kGapCands + kRepCands;
+constexpr uint32_t kRepStep = 8;    // positions between repeat-distance samples
+constexpr uint32_t kRepMin = 4;     // samples a repeat distance needs to become a candidate
 constexpr uint32_t kMaxSeq = kBlockMax / kMinMatch;
 
 // Literals_Length / Match_Length codes (RFC 8878 3.1.1.3.2.1.1): code, its extra bits.
@@ -541,23 +547,39 @@ __host__ __device__ __forceinline__ void gap_count(const uint8_t* in, uint32_t p
         }
 }
 
-// Candidate distances of a block: 1, then the most common '{' distances (gap_count),
-// ties to the smaller distance.  Returns the count (<= kCands).
-__host__ __device__ inline uint32_t pick_cands(const uint32_t* gaps, uint32_t* cand) {
+// Repeat distance of position p (sampled every kRepStep positions): the smallest d in
+// [2, 255] with in[p, p+4) == in[p-d, p-d+4), 0 when there is none or the 4 bytes
+// continue a run (distance 1 is always a candidate).
+__host__ __device__ inline uint32_t repeat_dist(const uint8_t* in, uint32_t n, uint32_t p) {
+    if (p < 2 || p + 4 > n) return 0;
+    const uint8_t b0 = in[p], b1 = in[p + 1], b2 = in[p + 2], b3 = in[p + 3];
+    if (in[p - 1] == b0 && b0 == b1 && b1 == b2 && b2 == b3) return 0;
+    const uint32_t lim = p < 255 ? p : 255;
+    for (uint32_t d = 2; d <= lim; ++d)
+        if (in[p - d] == b0 && in[p - d + 1] == b1 && in[p - d + 2] == b2 && in[p - d + 3] == b3) return d;
+    return 0;
+}
+
+// Candidate distances of a block: 1, then the most common '{' distances (gap_count), then
+// the most common sampled repeat distances (repeat_dist) seen >= kRepMin times, each list
+// without the distances already taken, ties to the smaller distance.  Returns the count
+// (<= kCands).
+__host__ __device__ inline uint32_t pick_cands(const uint32_t* gaps, const uint32_t* reps, uint32_t* cand) {
     uint32_t k = 0;
     cand[k++] = 1;
-    uint32_t used[kCands] = {1, 0, 0, 0, 0};
-    while (k < kCands) {
-        uint32_t best = 0, bc = 0;
-        for (uint32_t g = 2; g < 256; ++g) {
-            bool dup = false;
-            for (uint32_t j = 0; j < k; ++j) dup |= used[j] == g;
-            if (!dup && gaps[g] > bc) { bc = gaps[g]; best = g; }
+    for (uint32_t list = 0; list < 2; ++list) {
+        const uint32_t* h = list == 0 ? gaps : reps;
+        const uint32_t want = list == 0 ? kGapCands : kRepCands, floor = list == 0 ? 1u : kRepMin;
+        for (uint32_t taken = 0; taken < want; ++taken) {
+            uint32_t best = 0, bc = 0;
+            for (uint32_t g = 2; g < 256; ++g) {
+                bool dup = false;
+                for (uint32_t j = 0; j < k; ++j) dup |= cand[j] == g;
+                if (!dup && h[g] >= floor && h[g] > bc) { bc = h[g]; best = g; }
+            }
+            if (!bc) break;
+            cand[k++] = best;
         }
-        if (!bc) break;
-        cand[k] = best;
-        used[k] = best;
-        ++k;
     }
     return k;
 }
@@ -735,11 +757,13 @@ __host__ inline uint32_t block_content_seq(const uint8_t* in, uint32_t n, uint8_
     if (distinct == 1 && n > 1) { *type = 1; return 1; }
     if (n < 2) return n;
     // candidate distances and the greedy parse
-    uint32_t gaps[256] = {0};
+    uint32_t gaps[256] = {0}, reps[256] = {0};
     for (uint32_t p = 0; p < n; ++p)
         if (in[p] == '{') gap_count(in, p, gaps);
+    for (uint32_t p = 0; p < n; p += kRepStep)
+        if (const uint32_t d = repeat_dist(in, n, p)) ++reps[d];
     uint32_t cand[kCands];
-    const uint32_t nc = pick_cands(gaps, cand);
+    const uint32_t nc = pick_cands(gaps, reps, cand);
     // entropy-only content (built in body: a Raw literals section is n + 3 bytes; only a
     // content smaller than the block goes to the slot)
     uint32_t size = lit_section_seq(in, n, sc.body, sc.streams, hh, code, work);
