@@ -3,14 +3,14 @@
 // src/compress/mod.rs:71-76: zstd::Encoder level 3; the receiver decompresses with any
 // zstd decoder, sy-remote.rs:160-179).
 //
-// The encoder is entropy-only: each block of <= 128 KiB of text is one Compressed block
-// whose literals are Huffman-coded (4 streams, or 1 below 1 KiB, the weights in direct
-// representation) and which has no sequences; a block Huffman does not shrink is stored
-// Raw, a block of one repeated byte RLE.  The JSON of a Delta is decimal byte lists and
-// keys over ~20 symbols (~3.4 bits per character), so this keeps the frame format and its
-// decoders while the work per block is a histogram, a <= 128-symbol code and one bit
-// scatter.  The bytes differ from libzstd's level 3 (matches, other entropy tables): the
-// contract is decode(frame) == text, checked against libzstd's decoder.
+// Each block of <= 128 KiB of text is one Compressed block, coded two ways and the smaller
+// kept: literals only (Huffman-coded, 4 streams or 1 below 1 KiB, the weights in direct
+// representation; no sequences), or literals + sequences (matches at a handful of
+// candidate distances -- the JSON skeleton's '{' gaps, sampled repeat distances, runs --
+// with block-local repeat offsets and FSE tables from the block's own code counts).  A
+// block neither shrinks is stored Raw, a block of one repeated byte RLE.  The bytes differ
+// from libzstd's level 3: the contract is decode(frame) == text, checked against
+// libzstd's decoder; the ratios are in DESIGN.md section 11.
 //
 // The functions here are the pieces every block needs whoever runs them: the device
 // kernel (sydelta_kernels.hip, k_zstd_block: one workgroup per block, parallel bit
