@@ -2596,12 +2596,24 @@ __global__ __launch_bounds__(kZT) void k_zstd_block(const uint8_t* __restrict__ 
         }
         __syncthreads();
         const uint32_t nc = L.state[4];
-        uint32_t mine = 0;
-        for (uint32_t p = tid; p < n; p += kZT) {
-            const uint32_t b = zstd::best_at(in, n, p, L.cand, nc);
-            sc.best[p] = b;
-            mine += b != 0;
+        for (uint32_t p = tid; p < n; p += kZT) sc.best[p] = zstd::best_at(in, n, p, L.cand, nc);
+        // hash candidates in rounds of kHashRound positions (zstd::hash_look), the table in
+        // the stream words (free after the entropy-only streams); position p stays with
+        // thread p % kZT, so its best is read back by the thread that wrote it
+        static_assert(zstd::kHashRound % kZT == 0 && (1u << zstd::kHashBits) <= kZStreamWords, "hash rounds");
+        uint32_t* tab = L.words;
+        for (uint32_t i = tid; i < (1u << zstd::kHashBits); i += kZT) tab[i] = 0;
+        __syncthreads();
+        for (uint32_t r0 = 0; r0 < n; r0 += zstd::kHashRound) {
+            const uint32_t r1 = min(n, r0 + zstd::kHashRound);
+            for (uint32_t p = r0 + tid; p < r1; p += kZT) zstd::hash_look(in, n, p, tab, sc.best);
+            __syncthreads();
+            for (uint32_t p = r0 + tid; p < r1; p += kZT)
+                if (p + 4 <= n) atomicMax(&tab[zstd::hash4(in, p)], p + 1);  // zstd::hash_put
+            __syncthreads();
         }
+        uint32_t mine = 0;
+        for (uint32_t p = tid; p < n; p += kZT) mine += sc.best[p] != 0;
         if (mine) atomicAdd(&L.state[5], mine);
         __syncthreads();
         if (zstd::lz_worth(L.state[5], n)) {

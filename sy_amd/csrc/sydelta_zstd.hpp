@@ -20,6 +20,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <memory>
+
 namespace sydelta {
 namespace zstd {
 
@@ -586,7 +588,7 @@ __host__ __device__ inline uint32_t pick_cands(const uint32_t* gaps, const uint3
 
 // Best candidate at position p of in[0, n): the longest match (compared up to kProbe
 // bytes) among the candidates, ties to the earlier candidate; 0 when < kMinMatch.
-// Packed as (length << 8) | candidate index.
+// Packed as (length << 24) | distance.
 __host__ __device__ __forceinline__ uint32_t best_at(const uint8_t* in, uint32_t n, uint32_t p, const uint32_t* cand,
                                                      uint32_t nc) {
     uint32_t bl = 0, bi = 0;
@@ -598,7 +600,36 @@ __host__ __device__ __forceinline__ uint32_t best_at(const uint8_t* in, uint32_t
         while (l < lim && in[p + l] == in[p + l - d]) ++l;
         if (l > bl) { bl = l; bi = c; }
     }
-    return bl >= kMinMatch ? (bl << 8) | bi : 0;
+    return bl >= kMinMatch ? (bl << 24) | cand[bi] : 0;
+}
+
+// Hash candidates, for matches at any distance inside the block (a Data op's numbers
+// repeat hundreds of bytes apart): the block in rounds of kHashRound positions; a position
+// looks up the last earlier-round position whose next 4 bytes hash alike (tab: position +
+// 1, 0 empty) and takes that match when it is longer than its best candidate and at least
+// kHashMinNear (distance < kHashNear) or kHashMinFar bytes long (a far offset costs more
+// bits); after the round every position of it is put (the later position wins).  The
+// device runs a round's lookups in parallel, then its puts (atomicMax): the same table.
+constexpr uint32_t kHashBits = 13, kHashRound = 2048, kHashMinNear = 6, kHashMinFar = 8, kHashNear = 4096;
+__host__ __device__ __forceinline__ uint32_t hash4(const uint8_t* in, uint32_t p) {
+    const uint32_t v = (uint32_t)in[p] | ((uint32_t)in[p + 1] << 8) | ((uint32_t)in[p + 2] << 16) | ((uint32_t)in[p + 3] << 24);
+    return (v * 2654435761u) >> (32 - kHashBits);
+}
+__host__ __device__ __forceinline__ void hash_look(const uint8_t* in, uint32_t n, uint32_t p, const uint32_t* tab,
+                                                   uint32_t* best) {
+    if (p + 4 > n) return;
+    const uint32_t e = tab[hash4(in, p)];
+    if (!e) return;
+    const uint32_t q = e - 1, d = p - q;
+    const uint32_t lim = (n - p) < kProbe ? (n - p) : kProbe;
+    uint32_t l = 0;
+    while (l < lim && in[p + l] == in[q + l]) ++l;
+    if (l >= (d < kHashNear ? kHashMinNear : kHashMinFar) && l > (best[p] >> 24)) best[p] = (l << 24) | d;
+}
+__host__ __device__ __forceinline__ void hash_put(const uint8_t* in, uint32_t n, uint32_t p, uint32_t* tab) {
+    if (p + 4 > n) return;
+    uint32_t& e = tab[hash4(in, p)];
+    if (p + 1 > e) e = p + 1;
 }
 
 // Greedy parse of a block from the per-position bests: a match wherever one starts
@@ -613,8 +644,8 @@ __host__ __device__ inline uint32_t greedy_parse(const uint8_t* in, uint32_t n, 
     while (p < n) {
         const uint32_t b = best[p];
         if (!b) { lit[nl++] = in[p++]; continue; }
-        uint32_t d = cand[b & 0xFF];
-        uint32_t l = b >> 8;
+        uint32_t d = b & 0xFFFFFFu;
+        uint32_t l = b >> 24;
         if (rep[0] && rep[0] != d && rep[0] <= p) {  // an equally long match at the repeat distance is cheaper
             const uint32_t lim = (n - p) < kProbe ? (n - p) : kProbe;
             uint32_t lr = 0;
@@ -773,7 +804,16 @@ __host__ inline uint32_t block_content_seq(const uint8_t* in, uint32_t n, uint8_
     // literals + sequences when enough positions have a candidate match: the smaller
     // content wins (ties: entropy-only)
     uint32_t nbest = 0;
-    for (uint32_t p = 0; p < n; ++p) nbest += (sc.best[p] = best_at(in, n, p, cand, nc)) != 0;
+    for (uint32_t p = 0; p < n; ++p) sc.best[p] = best_at(in, n, p, cand, nc);
+    {
+        std::unique_ptr<uint32_t[]> tab(new uint32_t[1u << kHashBits]());
+        for (uint32_t r0 = 0; r0 < n; r0 += kHashRound) {
+            const uint32_t r1 = r0 + kHashRound < n ? r0 + kHashRound : n;
+            for (uint32_t p = r0; p < r1; ++p) hash_look(in, n, p, tab.get(), sc.best);
+            for (uint32_t p = r0; p < r1; ++p) hash_put(in, n, p, tab.get());
+        }
+    }
+    for (uint32_t p = 0; p < n; ++p) nbest += sc.best[p] != 0;
     if (lz_worth(nbest, n)) {
         const uint32_t z = lz_content(in, n, cand, sc, hh, code, work);
         if (z && z < size) {
