@@ -644,6 +644,7 @@ __host__ __device__ inline uint32_t greedy_parse(const uint8_t* in, uint32_t n, 
     while (p < n) {
         const uint32_t b = best[p];
         if (!b) { lit[nl++] = in[p++]; continue; }
+        if (p + 1 < n && (best[p + 1] >> 24) > (b >> 24)) { lit[nl++] = in[p++]; continue; }  // lazy: a longer match next
         uint32_t d = b & 0xFFFFFFu;
         uint32_t l = b >> 24;
         if (rep[0] && rep[0] != d && rep[0] <= p) {  // an equally long match at the repeat distance is cheaper
