@@ -152,3 +152,32 @@ def test_ref_random_texts():
         p = rng.dirichlet(np.full(alpha, float(rng.choice([0.05, 0.5, 5.0]))))
         data = rng.choice(alpha, size=n, p=p).astype(np.uint8).tobytes()
         assert zstd_decode(ref_compress(data), n) == data, it
+
+
+@pytest.mark.skipif(shutil.which("g++") is None or _libzstd() is None, reason="needs g++ and libzstd")
+def test_ref_structured_texts():
+    """Texts built from a few repeated units (some cut short, some behind '{' or closed
+    by '}', runs between them): matches at skeleton gaps, sampled repeat distances and
+    hash distances, back-to-back matches (literal length 0) and repeat offsets in every
+    form -- each frame decoded by libzstd."""
+    rng = random.Random(5)
+    for it in range(120):
+        units = [bytes(rng.randrange(97, 97 + rng.randint(2, 20)) for _ in range(rng.randint(1, 60)))
+                 for _ in range(rng.randint(1, 6))]
+        target = rng.randint(1000, 300000)
+        parts, size = [], 0
+        while size < target:
+            u = rng.choice(units)
+            k = rng.random()
+            if k < 0.3:
+                piece = b"{" + u
+            elif k < 0.5:
+                piece = u[:rng.randint(0, len(u))]
+            elif k < 0.6:
+                piece = bytes([rng.randrange(256)]) * rng.randint(1, 9)
+            else:
+                piece = b"{" + u + b"}"
+            parts.append(piece)
+            size += len(piece)
+        data = b"".join(parts)
+        assert zstd_decode(ref_compress(data), len(data)) == data, it
