@@ -18,9 +18,10 @@ already resident in HBM:
   json: serde_json text of the C3 delta (one 4 GiB literal run,
      ~3.6 characters per byte) written on the device; value = delta source GiB/s;
      cpu_baseline = the same text from libsydelta's host writer on a 256 MiB sample.
-  sigjson (sy-remote.rs:146-147): serde_json text of the C2
-     signature (4 GiB basis, 1 Mi entries) written on the device; value = basis GiB/s
-     covered; cpu_baseline = libsydelta's host writer on the same signature.
+  sigjson (sy-remote.rs:146-147, ssh.rs:967-973): serde_json text of
+     the C2 signature (4 GiB basis, 1 Mi entries) written on the device (the remote's
+     side) and parsed back on the device (the sender's side); value = basis GiB/s
+     covered; cpu_baseline = libsydelta's host writer + host parser on the same signature.
   zstd (ssh.rs:1009-1017): the zstd frame of that JSON text (1 GiB
      source by default, ~3.6 GiB of text) on the device; value = text GiB/s;
      cpu_baseline = libzstd level 3 (compress/mod.rs:71-76) on one thread, 64 MiB sample.
@@ -238,9 +239,12 @@ def cpu_sigjson_baseline(w_dev, s_dev, bs: int):
     sig = wire.sig_array(idx, idx * np.uint64(bs), np.full(w.size, bs, np.uint64), w, s)
     t0 = time.perf_counter()
     text = wire.checksums_to_json(sig)
+    back = wire.checksums_from_json(text)
     dt = time.perf_counter() - t0
+    assert len(back) == w.size
     return {"value": round(w.size * bs / dt / GIB, 4), "unit": "GiB/s", "cores": 1, "kind": "port",
-            "sample": f"host writer, {w.size} entries ({len(text) >> 20} MiB of text), basis GiB/s covered"}
+            "sample": f"host writer + host parser, {w.size} entries ({len(text) >> 20} MiB of text), basis GiB/s "
+                      f"covered"}
 
 
 def cpu_zstd_baseline(text_dev, sample_bytes: int = 64 << 20):
@@ -467,6 +471,7 @@ def algo_bytes_per_step(workload: str, n: int, nb_bytes: int, src_bytes: int) ->
             "k_json_write": n,  # json: every literal byte read once (text written: ~3.6x)
             "k_zstd_block": src_bytes,  # zstd: every text byte read once
             "k_sigjson_write": src_bytes,  # sigjson: 12 B per entry read + the text written once
+            "k_sigparse": src_bytes + 28 * (n // 4096),  # sigjson (bs 4096): the text read once + 40 B per entry written
             "k_block_cmp": 2 * n,  # local: both files read once
             "k_xxh_pieces": n}  # xxh3: every file byte read once
 
@@ -589,6 +594,7 @@ def main():
         sj_w, sj_s = dev.signature(basis, bs)
         sj_len = int(wire.checksums_to_json_device(sj_w, sj_s, bs, bs).numel())
         sj_out = torch.empty(sj_len + 16, dtype=torch.uint8, device="cuda")
+        sj_recs = torch.empty(sj_w.numel() * 40, dtype=torch.uint8, device="cuda")
     if args.workload == "apply":
         dev.synth_fill_range(basis, 0, 0x5E1D0005)
         new = torch.empty(n + 16, dtype=torch.uint8, device="cuda")
@@ -740,7 +746,10 @@ def main():
             check(lib.sydelta_checksums_to_json_device(sj_w.data_ptr(), sj_s.data_ptr(), sj_w.numel(), bs, bs,
                                                        sj_out.data_ptr(), sj_out.numel(), ctypes.byref(ln),
                                                        int(stream.cuda_stream)))
-            return {"json_bytes": ln.value, "entries": sj_w.numel()}
+            got = ctypes.c_uint64()
+            check(lib.sydelta_checksums_from_json_device(sj_out.data_ptr(), ln.value, sj_recs.data_ptr(),
+                                                         sj_w.numel(), ctypes.byref(got), int(stream.cuda_stream)))
+            return {"json_bytes": ln.value, "entries": sj_w.numel(), "parsed": got.value}
         if args.workload == "json":
             ln = ctypes.c_uint64()
             check(lib.sydelta_delta_to_json_device(json_h, new.data_ptr(), n, json_out.data_ptr(), json_out.numel(),
@@ -881,7 +890,7 @@ def main():
                     "local": f"local transport: change-ratio sample + block compare of two {n / GIB:.0f} GiB files, "
                              f"bs {bs}, {args.edit_ppm / 1e4:g}% of blocks edited",
                     "sigjson": f"serde_json text of the C2 signature ({n / GIB:g} GiB basis, {n // bs} entries) "
-                               f"on the device",
+                               f"written and parsed back on the device",
                     "json": f"serde_json text of the C3 delta ({n / GIB:.0f} GiB source, one literal run) on the device",
                     "zstd": f"zstd frame (Huffman literals + FSE-coded sequences, 128 KiB blocks) of the C3 delta's JSON text ({n / GIB:g} GiB source, "
                             f"one literal run) on the device; value = text bytes/s",

@@ -286,6 +286,15 @@ int sydelta_delta_to_json_device(const sydelta_delta *d, const uint8_t *d_lit, u
 int sydelta_checksums_to_json_device(const uint32_t *d_weak, const uint64_t *d_strong, uint64_t n,
                                      uint64_t block_size, uint64_t last_size, uint8_t *d_out, uint64_t out_cap,
                                      uint64_t *out_len, void *stream);
+/* serde_json::from_str::<Vec<BlockChecksum>> (ssh.rs:967-973) on the device, for text in
+ * HBM that is exactly the compact form sy-remote prints (serde_json::to_string: fields in
+ * checksum.rs's order, no whitespace); d_out (device, cap entries; NULL: validate and
+ * count only) receives the entries in order, *n_out their count.  Any other spelling --
+ * including ones serde accepts, such as whitespace or other key orders -- returns
+ * SYDELTA_E_INVAL naming the first byte that breaks the form: parse those with
+ * sydelta_checksums_from_json. */
+int sydelta_checksums_from_json_device(const uint8_t *d_text, uint64_t len, sydelta_block_checksum *d_out,
+                                       uint64_t cap, uint64_t *n_out, void *stream);
 /* The zstd frame (RFC 8878) of d_in[0, len) into d_out, on the device: what ssh.rs:1009-1017
  * sends (compress(delta_json, Compression::Zstd), compress/mod.rs:71-76) and sy-remote
  * decompresses (sy-remote.rs:160-179) -- typically the text of sydelta_delta_to_json_device.

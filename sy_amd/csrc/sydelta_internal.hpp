@@ -175,6 +175,12 @@ hipError_t launch_exclusive_sum_u64(const uint64_t* d_in, uint64_t* d_out, uint6
 hipError_t launch_sigjson_len(const sigjson::SigArgs& a, uint64_t* d_tile_len, hipStream_t s, Profiler* prof);
 hipError_t launch_sigjson_write(const sigjson::SigArgs& a, const uint64_t* d_tile_off, uint8_t* d_out, hipStream_t s,
                                 Profiler* prof);
+// Signature JSON parse (K7p): d_count[c] = '{' in 64-byte chunk c; then with d_rank (its
+// exclusive scan) every entry parsed into d_out[rank] (d_out NULL or rank >= cap: checked
+// only); *d_bad = the first bad position (atomicMin; initialised to UINT64_MAX).
+hipError_t launch_sigparse_count(const uint8_t* d_text, uint64_t len, uint64_t* d_count, hipStream_t s, Profiler* prof);
+hipError_t launch_sigparse(const uint8_t* d_text, uint64_t len, const uint64_t* d_rank, sydelta_block_checksum* d_out,
+                           uint64_t cap, unsigned long long* d_bad, hipStream_t s, Profiler* prof);
 // zstd frame of a text in HBM (sydelta_zstd.hpp).  Blocks [b0, b0 + nb) of d_text (len
 // bytes, 16-byte aligned, readable to the end of its last granule): slot i of d_slots
 // (zstd::kBlockMax bytes each) gets block b0+i's content, d_size[i] its size, d_type[i]

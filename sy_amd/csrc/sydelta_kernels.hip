@@ -2754,6 +2754,22 @@ __global__ __launch_bounds__(sigjson::kTile) void k_sigjson_write(sigjson::SigAr
         sigjson::store_chunk(stage, tot, dst, c);
 }
 
+// K7p: the compact signature text parsed on the device (sydelta_sigjson.hpp chunk_parse).
+__global__ __launch_bounds__(256) void k_sigparse_count(const uint8_t* __restrict__ t, uint64_t len,
+                                                        uint64_t* __restrict__ count) {
+    const uint64_t c = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+    if (c * sigjson::kParseChunk < len) count[c] = sigjson::chunk_entries(t, len, c);
+}
+
+__global__ __launch_bounds__(256) void k_sigparse(const uint8_t* __restrict__ t, uint64_t len,
+                                                  const uint64_t* __restrict__ rank, sydelta_block_checksum* out,
+                                                  uint64_t cap, unsigned long long* bad) {
+    const uint64_t c = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+    if (c * sigjson::kParseChunk >= len) return;
+    const uint64_t b = sigjson::chunk_parse(t, len, c, rank[c], out, cap);
+    if (b != UINT64_MAX) atomicMin(bad, (unsigned long long)b);
+}
+
 __global__ __launch_bounds__(256) void k_json_len(const JsonPiece* __restrict__ pieces, uint64_t npieces,
                                                   const uint8_t* __restrict__ lit, uint64_t* __restrict__ len) {
     // one wave per piece (lane l sizes literal bytes [64l, 64l + 64) of a Data chunk);
@@ -3693,6 +3709,25 @@ hipError_t launch_sigjson_write(const sigjson::SigArgs& a, const uint64_t* d_til
     if (nt > 0x7FFFFFFFull) return hipErrorInvalidValue;
     ProfScope ps(prof, s, "k_sigjson_write");
     hipLaunchKernelGGL(k_sigjson_write, dim3((unsigned)nt), dim3(sigjson::kTile), 0, s, a, d_tile_off, d_out);
+    return hipGetLastError();
+}
+
+hipError_t launch_sigparse_count(const uint8_t* d_text, uint64_t len, uint64_t* d_count, hipStream_t s, Profiler* prof) {
+    const uint64_t nc = (len + sigjson::kParseChunk - 1) / sigjson::kParseChunk;
+    if (!nc) return hipSuccess;
+    if ((nc + 255) / 256 > 0x7FFFFFFFull) return hipErrorInvalidValue;
+    ProfScope ps(prof, s, "k_sigparse_count");
+    hipLaunchKernelGGL(k_sigparse_count, dim3(grid_for(nc, 256)), dim3(256), 0, s, d_text, len, d_count);
+    return hipGetLastError();
+}
+
+hipError_t launch_sigparse(const uint8_t* d_text, uint64_t len, const uint64_t* d_rank, sydelta_block_checksum* d_out,
+                           uint64_t cap, unsigned long long* d_bad, hipStream_t s, Profiler* prof) {
+    const uint64_t nc = (len + sigjson::kParseChunk - 1) / sigjson::kParseChunk;
+    if (!nc) return hipSuccess;
+    if ((nc + 255) / 256 > 0x7FFFFFFFull) return hipErrorInvalidValue;
+    ProfScope ps(prof, s, "k_sigparse");
+    hipLaunchKernelGGL(k_sigparse, dim3(grid_for(nc, 256)), dim3(256), 0, s, d_text, len, d_rank, d_out, cap, d_bad);
     return hipGetLastError();
 }
 

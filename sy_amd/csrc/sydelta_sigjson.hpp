@@ -18,12 +18,24 @@
 // aligned chunks it covers entirely, byte stores on the two edge chunks it shares with
 // its neighbours.
 //
+// The sender's side (ssh.rs:967-973, serde_json::from_str::<Vec<BlockChecksum>>) parses
+// the same text: on the device when it is exactly this compact form (K7p, parse_entry):
+// every '{' starts an entry, so one thread per 64-byte chunk counts its '{', an exclusive
+// scan ranks them, and each '{' is parsed by the thread whose chunk holds it, which also
+// checks the characters around its entry ('[' or "},"  before, ',' + '{' or the final
+// ']' after).  The entries then form one chain from byte 1 to the last, so every byte of
+// the text is checked by some thread.  Any other spelling serde accepts (whitespace,
+// other key orders, unknown keys) is refused with its position and goes to the host
+// parser (sydelta_checksums_from_json).
+//
 // Every function below is the body of one thread (sydelta_kernels.hip); the host
 // emulation of the device layer (tests/csrc/fake_device.cpp) and the sanitizer build
 // (tests/csrc/kernel_bodies_fuzz.cpp) run the same bodies on the CPU.
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+
+#include "../../include/sydelta.h"
 
 namespace sydelta {
 namespace sigjson {
@@ -115,6 +127,80 @@ __host__ __device__ inline void store_chunk(const uint8_t* stage, uint32_t len, 
         return;
     }
     for (uintptr_t x = lo; x < hi; ++x) *(uint8_t*)x = s[x - lo];
+}
+
+// ---- parse (K7p)
+constexpr uint32_t kParseChunk = 64;  // text bytes per thread
+
+// Unsigned decimal at t[p]: digits only, no leading zero unless the number is 0, value <=
+// maxv.  Returns the digits consumed (0: not a number in range).
+__host__ __device__ inline uint32_t get_dec(const uint8_t* t, uint64_t len, uint64_t p, uint64_t maxv, uint64_t& v) {
+    uint64_t x = 0;
+    uint32_t k = 0;
+    while (p + k < len && t[p + k] >= '0' && t[p + k] <= '9') {
+        const uint64_t d = (uint64_t)(t[p + k] - '0');
+        if (x > (maxv - d) / 10) return 0;
+        x = x * 10 + d;
+        ++k;
+    }
+    if (k == 0 || (k > 1 && t[p] == '0')) return 0;
+    v = x;
+    return k;
+}
+
+__host__ __device__ inline bool get_lit(const uint8_t* t, uint64_t len, uint64_t& p, const char* s) {
+    for (uint32_t k = 0; s[k]; ++k, ++p)
+        if (p >= len || t[p] != (uint8_t)s[k]) return false;
+    return true;
+}
+
+// The entry whose '{' is at t[p], in exactly the compact form, with the right characters
+// before and after it; fills r.  False otherwise.
+__host__ __device__ inline bool parse_entry(const uint8_t* t, uint64_t len, uint64_t p, sydelta_block_checksum& r) {
+    if (!(p == 1 ? t[0] == '[' : p >= 2 && t[p - 1] == ',' && t[p - 2] == '}')) return false;
+    uint64_t q = p, v = 0;
+    uint32_t k;
+    if (!get_lit(t, len, q, "{\"index\":") || !(k = get_dec(t, len, q, UINT64_MAX, v))) return false;
+    r.index = v;
+    q += k;
+    if (!get_lit(t, len, q, ",\"offset\":") || !(k = get_dec(t, len, q, UINT64_MAX, v))) return false;
+    r.offset = v;
+    q += k;
+    if (!get_lit(t, len, q, ",\"size\":") || !(k = get_dec(t, len, q, UINT64_MAX, v))) return false;
+    r.size = v;
+    q += k;
+    if (!get_lit(t, len, q, ",\"weak\":") || !(k = get_dec(t, len, q, 0xFFFFFFFFull, v))) return false;
+    r.weak = (uint32_t)v;
+    r.reserved = 0;
+    q += k;
+    if (!get_lit(t, len, q, ",\"strong\":") || !(k = get_dec(t, len, q, UINT64_MAX, v))) return false;
+    r.strong = v;
+    q += k;
+    if (!get_lit(t, len, q, "}")) return false;
+    return q < len && ((t[q] == ',' && q + 1 < len && t[q + 1] == '{') || (t[q] == ']' && q + 1 == len));
+}
+
+// '{' in chunk c of the text.
+__host__ __device__ inline uint32_t chunk_entries(const uint8_t* t, uint64_t len, uint64_t c) {
+    uint32_t m = 0;
+    for (uint64_t p = c * kParseChunk; p < len && p < (c + 1) * kParseChunk; ++p) m += t[p] == '{';
+    return m;
+}
+
+// Chunk c's entries, ranked from rank: parsed into out[rank..] (out NULL or past cap:
+// checked only); returns the first bad position in the chunk or UINT64_MAX.  Chunk 0
+// also checks the head: "[]" or "[{".
+__host__ __device__ inline uint64_t chunk_parse(const uint8_t* t, uint64_t len, uint64_t c, uint64_t rank,
+                                               sydelta_block_checksum* out, uint64_t cap) {
+    if (c == 0 && !(len >= 2 && t[0] == '[' && (len == 2 ? t[1] == ']' : t[1] == '{'))) return 0;
+    for (uint64_t p = c * kParseChunk; p < len && p < (c + 1) * kParseChunk; ++p) {
+        if (t[p] != '{') continue;
+        sydelta_block_checksum r;
+        if (!parse_entry(t, len, p, r)) return p;
+        if (out && rank < cap) out[rank] = r;
+        ++rank;
+    }
+    return UINT64_MAX;
 }
 
 // sum_{i < n} digits(i * m), in O(20): digits(v) = 1 + #{d >= 1 : v >= 10^d}, and

@@ -95,12 +95,17 @@ struct Reader {
     bool u64(uint64_t& v) {
         ws();
         if (p >= e || *p < '0' || *p > '9') { err = "expected an unsigned integer at byte " + std::to_string(pos()); return false; }
+        const char* q = p;
         v = 0;
         while (p < e && *p >= '0' && *p <= '9') {
             const uint64_t d = (uint64_t)(*p - '0');
             if (v > (UINT64_MAX - d) / 10) { err = "integer overflow at byte " + std::to_string(pos()); return false; }
             v = v * 10 + d;
             ++p;
+        }
+        if (p - q > 1 && *q == '0') {  // serde_json: "invalid number" (no leading zeros)
+            err = "invalid number at byte " + std::to_string((size_t)(q - b0));
+            return false;
         }
         return true;
     }
@@ -561,6 +566,46 @@ extern "C" int sydelta_checksums_to_json_device(const uint32_t* d_weak, const ui
         HIP_TRY(launch_sigjson_write(a, d_toff, d_out, s, cp.get()));
         HIP_TRY(hipStreamSynchronize(s));
     }
+    return SYDELTA_OK;
+} catch (...) {
+    return sydelta::host_exception();
+}
+
+// serde_json::from_str::<Vec<BlockChecksum>> (ssh.rs:967-973) of a text in HBM that is
+// exactly the compact form sy-remote prints (sydelta_sigjson.hpp, K7p): '{' per 64-byte
+// chunk, their exclusive scan (the ranks), then every entry parsed and its surroundings
+// checked; the first position that breaks the form is reported and the caller parses
+// the text with sydelta_checksums_from_json instead.
+extern "C" int sydelta_checksums_from_json_device(const uint8_t* d_text, uint64_t len, sydelta_block_checksum* d_out,
+                                                  uint64_t cap, uint64_t* n_out, void* stream) try {
+    if (!n_out) return fail(SYDELTA_E_INVAL, "NULL argument");
+    *n_out = 0;
+    if (len < 2 || !d_text) return fail(SYDELTA_E_INVAL, "checksum JSON: not serde's compact form at byte 0");
+    int dev = 0;
+    (void)hipGetDevice(&dev);
+    if (int r = ensure_device(dev)) return r;
+    hipStream_t s = stream ? (hipStream_t)stream : thread_stream(dev);
+    const uint64_t nc = (len + sigjson::kParseChunk - 1) / sigjson::kParseChunk;
+    CallProf cp;
+    DevBuf_wire buf;
+    HIP_TRY(hipMallocAsync(&buf.p, 2 * nc * 8 + 8, s));
+    buf.s = s;
+    uint64_t* d_cnt = (uint64_t*)buf.p;
+    uint64_t* d_rank = d_cnt + nc;
+    unsigned long long* d_bad = (unsigned long long*)(d_rank + nc);
+    HIP_TRY(hipMemsetAsync(d_bad, 0xFF, 8, s));
+    HIP_TRY(launch_sigparse_count(d_text, len, d_cnt, s, cp.get()));
+    HIP_TRY(launch_exclusive_sum_u64(d_cnt, d_rank, nc, s));
+    HIP_TRY(launch_sigparse(d_text, len, d_rank, d_out, d_out ? cap : 0, d_bad, s, cp.get()));
+    uint64_t tail[3] = {0, 0, 0};
+    HIP_TRY(hipMemcpyAsync(&tail[0], d_rank + nc - 1, 8, hipMemcpyDeviceToHost, s));
+    HIP_TRY(hipMemcpyAsync(&tail[1], d_cnt + nc - 1, 8, hipMemcpyDeviceToHost, s));
+    HIP_TRY(hipMemcpyAsync(&tail[2], d_bad, 8, hipMemcpyDeviceToHost, s));
+    HIP_TRY(hipStreamSynchronize(s));
+    if (tail[2] != UINT64_MAX)
+        return fail(SYDELTA_E_INVAL, "checksum JSON: not serde's compact form at byte %llu",
+                    (unsigned long long)tail[2]);
+    *n_out = tail[0] + tail[1];
     return SYDELTA_OK;
 } catch (...) {
     return sydelta::host_exception();

@@ -113,6 +113,24 @@ def checksums_to_json_device(d_weak, d_strong, block_size: int, last_size: int, 
     return out[:n.value]
 
 
+def checksums_from_json_device(d_text, stream=None):
+    """serde_json::from_str::<Vec<BlockChecksum>> of a compact text in HBM (uint8 device
+    tensor) parsed on the device; returns the entries as a uint8 device tensor of
+    n * 40 bytes (sydelta_block_checksum records) and n.  Raises SyDeltaError for text in
+    any other spelling (parse that with checksums_from_json)."""
+    import torch
+
+    from .device import _ptr, _stream
+
+    n = ctypes.c_uint64()
+    check(lib.sydelta_checksums_from_json_device(_ptr(d_text), d_text.numel(), None, 0, ctypes.byref(n),
+                                                 _stream(stream)))
+    out = torch.empty(max(1, n.value) * _SIG_DTYPE.itemsize, dtype=torch.uint8, device=d_text.device)
+    check(lib.sydelta_checksums_from_json_device(_ptr(d_text), d_text.numel(), _ptr(out), n.value, ctypes.byref(n),
+                                                 _stream(stream)))
+    return out[:n.value * _SIG_DTYPE.itemsize], n.value
+
+
 def zstd_compress_device(d_text, stream=None, device: int = 0):
     """zstd frame (Huffman literals, FSE-coded sequences) of the bytes of a uint8 device tensor, as a uint8
     device tensor: the compression ssh.rs:1009-1017 applies to the Delta JSON.  The

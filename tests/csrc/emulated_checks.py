@@ -260,7 +260,101 @@ def sigjson_checks():
                                                   bs, last, None, 0, ctypes.byref(got), None)
         assert rc != 0, (bs, last)
     assert lib.sydelta_checksums_to_json_device(None, None, 4, 4096, 4096, None, 0, ctypes.byref(got), None) != 0
-    return n_checks + 6
+    return n_checks + 6 + sigparse_checks()
+
+
+def sigparse_checks():
+    """sydelta_checksums_from_json_device (K7p; the emulated launches run
+    sydelta_sigjson.hpp's chunk bodies): serde's compact text of random signatures (tile
+    and chunk edges, extreme values) parses to the entries the host parser gives; the
+    count-only call; a buffer shorter than the count; and the device parser refuses every
+    text outside the compact form -- whitespace, another key order, an unknown key, a
+    missing or duplicated field, leading zeros, out-of-range values, a trailing comma or
+    byte, a truncated text -- while the host parser's verdict on it stays its own."""
+    import ctypes
+    import json
+
+    from sy_amd import wire
+    from sy_amd._lib import SyDeltaError, check, lib
+
+    rng = np.random.default_rng(11)
+    n_checks = 0
+
+    def dev_parse(text: bytes, cap=None):
+        buf = np.frombuffer(text, np.uint8).copy() if text else np.zeros(1, np.uint8)
+        got = ctypes.c_uint64()
+        rc = lib.sydelta_checksums_from_json_device(ctypes.c_void_p(buf.ctypes.data), len(text), None, 0,
+                                                    ctypes.byref(got), None)
+        if rc:
+            return None
+        n = got.value
+        k = n if cap is None else cap
+        out = np.zeros(max(k, 1), wire._SIG_DTYPE)
+        check(lib.sydelta_checksums_from_json_device(ctypes.c_void_p(buf.ctypes.data), len(text),
+                                                     ctypes.c_void_p(out.ctypes.data), k, ctypes.byref(got), None))
+        assert got.value == n
+        return out[:min(k, n)]
+
+    for n in (0, 1, 2, 3, 255, 256, 257, 1000, 5000):
+        idx = np.arange(n, dtype=np.uint64)
+        if n and rng.random() < 0.5:
+            w = np.array([0, 9, 0xFFFFFFFF], np.uint32)[rng.integers(0, 3, n)]
+            st = np.array([0, 10, 0xFFFFFFFFFFFFFFFF], np.uint64)[rng.integers(0, 3, n)]
+        else:
+            w = rng.integers(0, 1 << 32, n, dtype=np.uint64).astype(np.uint32)
+            st = rng.integers(0, 1 << 64, n, dtype=np.uint64)
+        sizes = np.full(n, 4096, np.uint64)
+        if n:
+            sizes[-1] = 17
+        text = wire.checksums_to_json(wire.sig_array(idx, idx * np.uint64(4096), sizes, w, st))
+        host = wire.checksums_from_json(text)
+        dev = dev_parse(text)
+        assert dev is not None and np.array_equal(dev, host), n
+        if n > 3:
+            part = dev_parse(text, cap=3)
+            assert np.array_equal(part, host[:3])
+        n_checks += 1
+    good = b'[{"index":0,"offset":0,"size":4096,"weak":1,"strong":2},{"index":1,"offset":4096,"size":5,"weak":3,"strong":4}]'
+    assert dev_parse(good) is not None
+    bad = [
+        b"", b"[", b"]", b"[}", b"[{]", b"[ ]", b" []", b"[] ", b"[,]",
+        good.replace(b",{", b", {"), good.replace(b'"index":0', b'"index": 0'),
+        good.replace(b'"offset":0,"size":4096', b'"size":4096,"offset":0'),
+        good.replace(b'"strong":2}', b'"strong":2,"x":1}'),
+        good.replace(b',"weak":1', b''), good.replace(b'"weak":1', b'"weak":1,"weak":1'),
+        good.replace(b'"size":5', b'"size":05'), good.replace(b'"weak":3', b'"weak":4294967296'),
+        good.replace(b'"strong":4', b'"strong":18446744073709551616'), good.replace(b'"index":1', b'"index":-1'),
+        good.replace(b'"weak":3', b'"weak":3.0'), good[:-1] + b",]", good + b"\n", good[:-1], good[:-2] + b"]",
+        good.replace(b"},{", b"}{"), good.replace(b"},{", b"},,{"), b"[" + good[1:-1] + b",{}]",
+    ]
+    for t in bad:
+        assert dev_parse(t) is None, t
+        try:
+            host = wire.checksums_from_json(t)
+        except SyDeltaError:
+            host = None
+        ok_json = True
+        try:
+            json.loads(t)
+        except ValueError:
+            ok_json = False
+        if host is not None:  # a spelling serde accepts that is not the compact form
+            assert ok_json, t
+        n_checks += 1
+    # random byte mutations of a valid text: the device accepts only what equals the
+    # host parser's result on a text that re-serializes to itself
+    for it in range(300):
+        b = bytearray(good)
+        for _ in range(int(rng.integers(1, 4))):
+            b[int(rng.integers(0, len(b)))] = int(rng.choice(list(b'0123456789{}[],:"ax ')))
+        t = bytes(b)
+        dev = dev_parse(t)
+        if dev is not None:
+            host = wire.checksums_from_json(t)
+            assert np.array_equal(dev, host), t
+            assert wire.checksums_to_json(host) == t, t
+        n_checks += 1
+    return n_checks
 
 
 def _walk_counters():

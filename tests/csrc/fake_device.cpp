@@ -442,6 +442,23 @@ hipError_t launch_sigjson_write(const sigjson::SigArgs& a, const uint64_t* d_til
     }
     return hipSuccess;
 }
+// K7p: chunk_entries / chunk_parse per chunk (the chunks in descending order).
+hipError_t launch_sigparse_count(const uint8_t* d_text, uint64_t len, uint64_t* d_count, hipStream_t, Profiler*) {
+    EmuTimer emu_t;
+    const uint64_t nc = (len + sigjson::kParseChunk - 1) / sigjson::kParseChunk;
+    for (uint64_t c = 0; c < nc; ++c) d_count[c] = sigjson::chunk_entries(d_text, len, c);
+    return hipSuccess;
+}
+hipError_t launch_sigparse(const uint8_t* d_text, uint64_t len, const uint64_t* d_rank, sydelta_block_checksum* d_out,
+                           uint64_t cap, unsigned long long* d_bad, hipStream_t, Profiler*) {
+    EmuTimer emu_t;
+    const uint64_t nc = (len + sigjson::kParseChunk - 1) / sigjson::kParseChunk;
+    for (uint64_t c = nc; c-- > 0;) {
+        const uint64_t b = sigjson::chunk_parse(d_text, len, c, d_rank[c], d_out, cap);
+        if (b < *d_bad) *d_bad = b;
+    }
+    return hipSuccess;
+}
 // K5b: the kernels' own per-thread bodies (sydelta_chain.hpp) in the launch order of
 // sydelta_kernels.hip's launch_chain, one loop per kernel.  The marking levels run their
 // threads alternately forward and backward: two of the schedules a GPU may produce for

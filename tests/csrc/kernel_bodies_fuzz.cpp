@@ -18,7 +18,9 @@
 //  * the signature JSON writer (sydelta_sigjson.hpp, K7s): k_sigjson_write's tiles on
 //    random signatures, each tile's text staged in an array of exactly its length and
 //    stored chunk by chunk (chunks shuffled) into an output of exactly the text's length
-//    at a random alignment; the text equals a printf-built one and the length bounds hold.
+//    at a random alignment; the text equals a printf-built one and the length bounds hold;
+//  * its parse (K7p): texts in exact-size arrays parse back to their signature, and a
+//    mutated text is refused or is the compact text of what it parses to.
 #include <stdint.h>
 #include <stdio.h>
 #include <stdlib.h>
@@ -419,6 +421,72 @@ static void repcode_case(std::mt19937_64& rng, uint64_t* reps_used) {
     }
 }
 
+// K7p: the parse bodies on texts in arrays of exactly their length (a read past the text
+// is an ASan report): serde's compact text of a random signature parses back to it; a
+// mutated text is either refused or re-serializes to itself (the device accepts the
+// compact form only).
+static std::vector<uint8_t> sig_text(const std::vector<sydelta_block_checksum>& v) {
+    std::string t = "[";
+    char tmp[256];
+    for (size_t i = 0; i < v.size(); ++i) {
+        snprintf(tmp, sizeof tmp, "%s{\"index\":%llu,\"offset\":%llu,\"size\":%llu,\"weak\":%u,\"strong\":%llu}",
+                 i ? "," : "", (unsigned long long)v[i].index, (unsigned long long)v[i].offset,
+                 (unsigned long long)v[i].size, v[i].weak, (unsigned long long)v[i].strong);
+        t += tmp;
+    }
+    t += "]";
+    return std::vector<uint8_t>(t.begin(), t.end());
+}
+static bool parse_all(const std::vector<uint8_t>& text, std::vector<sydelta_block_checksum>& out) {
+    const uint64_t len = text.size();
+    std::unique_ptr<uint8_t[]> t(new uint8_t[len ? len : 1]);
+    if (len) memcpy(t.get(), text.data(), len);
+    const uint64_t nc = (len + sigjson::kParseChunk - 1) / sigjson::kParseChunk;
+    if (len < 2 || !nc) return false;
+    std::vector<uint64_t> rank(nc + 1, 0);
+    for (uint64_t c = 0; c < nc; ++c) rank[c + 1] = rank[c] + sigjson::chunk_entries(t.get(), len, c);
+    std::unique_ptr<sydelta_block_checksum[]> o(new sydelta_block_checksum[rank[nc] ? rank[nc] : 1]);
+    for (uint64_t c = nc; c-- > 0;)
+        if (sigjson::chunk_parse(t.get(), len, c, rank[c], o.get(), rank[nc]) != UINT64_MAX) return false;
+    out.assign(o.get(), o.get() + rank[nc]);
+    return true;
+}
+static void sigparse_case(std::mt19937_64& rng, uint64_t* accepted, uint64_t* refused) {
+    const size_t n = rng() % 300;
+    std::vector<sydelta_block_checksum> v(n);
+    for (size_t i = 0; i < n; ++i) {
+        const int k = (int)(rng() % 3);
+        v[i] = sydelta_block_checksum{i, i * 4096, k ? 4096u : 1 + rng() % 4096, k == 2 ? 0xFFFFFFFFu : (uint32_t)rng(),
+                                      0, k == 1 ? ~0ull : rng() % (k ? 1000 : ~0ull)};
+    }
+    const std::vector<uint8_t> text = sig_text(v);
+    std::vector<sydelta_block_checksum> back;
+    CHECK(parse_all(text, back));
+    CHECK(back.size() == n);
+    for (size_t i = 0; i < n; ++i)
+        CHECK(back[i].index == v[i].index && back[i].offset == v[i].offset && back[i].size == v[i].size &&
+              back[i].weak == v[i].weak && back[i].strong == v[i].strong);
+    static const char alpha[] = "0123456789{}[],:\"az -";
+    for (int m = 0; m < 20; ++m) {
+        std::vector<uint8_t> t = text;
+        const int k = 1 + (int)(rng() % 3);
+        for (int j = 0; j < k; ++j) {
+            const int op = (int)(rng() % 3);
+            const size_t at = t.empty() ? 0 : rng() % t.size();
+            if (op == 0 && !t.empty()) t[at] = (uint8_t)alpha[rng() % (sizeof alpha - 1)];
+            else if (op == 1) t.insert(t.begin() + at, (uint8_t)alpha[rng() % (sizeof alpha - 1)]);
+            else if (!t.empty()) t.erase(t.begin() + at);
+        }
+        std::vector<sydelta_block_checksum> got;
+        if (parse_all(t, got)) {
+            CHECK(sig_text(got) == t);
+            ++*accepted;
+        } else {
+            ++*refused;
+        }
+    }
+}
+
 int main(int argc, char** argv) {
     const int iters = argc > 1 ? atoi(argv[1]) : 2000;
     std::mt19937_64 rng(20261017);
@@ -429,12 +497,16 @@ int main(int argc, char** argv) {
     uint64_t reps = 0;
     for (int it = 0; it < std::max(1, iters / 10); ++it) repcode_case(rng, &reps);
     CHECK(reps > 0);
+    uint64_t acc = 0, ref = 0;
+    for (int it = 0; it < std::max(1, iters / 10); ++it) sigparse_case(rng, &acc, &ref);
+    CHECK(acc > 0 && ref > 0);
     uint64_t sj = 0;
     for (int it = 0; it < std::max(1, iters / 10); ++it) sigjson_case(rng, &sj);
     CHECK(walked > (uint64_t)iters / 4);
     printf("kernel bodies ok: %llu chain cases (%llu resolved on the device path), %llu zstd blocks, %llu stream "
-           "replicas, %llu repeat offsets, %llu signature JSON entries\n",
+           "replicas, %llu repeat offsets, %llu signature JSON entries, %llu/%llu mutated texts accepted/refused\n",
            (unsigned long long)cases, (unsigned long long)walked, (unsigned long long)blocks,
-           (unsigned long long)replica, (unsigned long long)reps, (unsigned long long)sj);
+           (unsigned long long)replica, (unsigned long long)reps, (unsigned long long)sj, (unsigned long long)acc,
+           (unsigned long long)ref);
     return 0;
 }

@@ -1,11 +1,14 @@
-"""Device signature JSON writer (K7s, sydelta_checksums_to_json_device) against an
+"""Device signature JSON writer (K7s, sydelta_checksums_to_json_device) and parser (K7p,
+sydelta_checksums_from_json_device). The writer is checked against an
 independent writer: json.dumps, with serde's compact separators and checksum.rs:9-21's
 field order, of the C oracle's signature of the same bytes. This is the text
 `sy-remote checksums` prints (sy-remote.rs:146-147) and ssh.rs:967-973 parses. The
 cases cover block sizes with a partial and a full last block, and tile edges (255, 256
 and 257 entries). The destination views start at every alignment, with guard bytes
 checked around them. A C2-sized signature (4 GiB basis, 1 Mi entries) is parsed back
-with json.loads and compared field by field.
+with json.loads and compared field by field. The parser is checked on json.dumps's text
+of the oracle's signature (against the oracle and the host parser), on spellings outside
+the compact form (refused), and on the writer's C2 text (round trip on the device).
 
 Marked firstrun: the kernels were written after this round's GPU access closed. The
 CPU suite runs the same per-thread bodies on the emulated device and under
@@ -88,3 +91,50 @@ def test_signature_json_c2_size(gpu):
     assert [e["strong"] for e in sigs] == hs.tolist()
     assert all(e["index"] == i and e["offset"] == i * bs and e["size"] == bs for i, e in enumerate(sigs))
     assert list(sigs[0]) == ["index", "offset", "size", "weak", "strong"]
+
+
+@pytest.mark.parametrize("bs,length", [(4096, 4096 * 257 - 5), (1007, 3 << 20), (64, 1)])
+def test_signature_json_parse_on_device(bs, length, gpu, oracle_c):
+    """K7p: the compact text (as json.dumps writes it) parsed on the device gives the
+    oracle's signature; the host parser agrees; a spelling outside the compact form is
+    refused with its position."""
+    import torch
+
+    from oracle import oracle as O
+    from sy_amd._lib import SyDeltaError
+
+    host = O.synth_bytes(length, 0x5E1D0710 + bs)
+    ew, es, ez = oracle_c.compute_checksums(host, bs)
+    ref = _dumps(ew, es, ez, bs)
+    d = torch.frombuffer(bytearray(ref), dtype=torch.uint8).cuda()
+    recs, n = wire.checksums_from_json_device(d)
+    got = recs.cpu().numpy().view(wire._SIG_DTYPE)
+    assert n == len(ew)
+    assert np.array_equal(got["weak"], ew) and np.array_equal(got["strong"], es)
+    assert np.array_equal(got["size"], ez)
+    assert np.array_equal(got["offset"], np.arange(n, dtype=np.uint64) * np.uint64(bs))
+    assert np.array_equal(got, wire.checksums_from_json(ref))
+    for bad in (ref.replace(b",", b", ", 1), ref[:-1], ref.replace(b'"weak"', b'"Weak"', 1)):
+        with pytest.raises(SyDeltaError, match="compact form at byte"):
+            wire.checksums_from_json_device(torch.frombuffer(bytearray(bad), dtype=torch.uint8).cuda())
+
+
+@pytest.mark.slow
+def test_signature_json_round_trip_on_device_c2(gpu):
+    """C2's signature written on the device (K7s) and parsed back on the device (K7p):
+    every entry equals the signature, with index/offset/size as implied."""
+    import torch
+
+    n, bs = 4 << 30, 4096
+    basis = torch.empty(n, dtype=torch.uint8, device="cuda")
+    gpu.synth_fill(basis, 0x5E1D0002)
+    w, s = gpu.signature(basis, bs)
+    del basis
+    text = wire.checksums_to_json_device(w, s, bs, bs)
+    recs, m = wire.checksums_from_json_device(text)
+    assert m == w.numel() == 1 << 20
+    r = recs.view(torch.int64).view(-1, 5)  # index, offset, size, weak | reserved << 32, strong
+    idx = torch.arange(m, device="cuda", dtype=torch.int64)
+    assert bool((r[:, 0] == idx).all()) and bool((r[:, 1] == idx * bs).all()) and bool((r[:, 2] == bs).all())
+    assert bool(((r[:, 3] & 0xFFFFFFFF) == (w.to(torch.int64) & 0xFFFFFFFF)).all())
+    assert bool((r[:, 4] == s.view(torch.int64)).all())

@@ -38,7 +38,10 @@ def test_checksums_json_parser_accepts_whitespace_and_field_order():
 
 
 @pytest.mark.parametrize("bad", [b"", b"[", b"[{}]", b'[{"index":0,"offset":0,"size":1,"weak":4294967296,"strong":0}]',
-                                 b'[{"index":-1,"offset":0,"size":1,"weak":1,"strong":0}]', b"[] x"])
+                                 b'[{"index":-1,"offset":0,"size":1,"weak":1,"strong":0}]', b"[] x",
+                                 # serde_json: "invalid number" (no leading zeros)
+                                 b'[{"index":0,"offset":0,"size":01,"weak":1,"strong":0}]',
+                                 b'[{"index":00,"offset":0,"size":1,"weak":1,"strong":0}]'])
 def test_checksums_json_rejects(bad):
     import sy_amd._lib as L
 
