@@ -295,6 +295,15 @@ int sydelta_checksums_to_json_device(const uint32_t *d_weak, const uint64_t *d_s
  * sydelta_checksums_from_json. */
 int sydelta_checksums_from_json_device(const uint8_t *d_text, uint64_t len, sydelta_block_checksum *d_out,
                                        uint64_t cap, uint64_t *n_out, void *stream);
+/* serde_json::from_str::<Delta> (sy-remote.rs:175) on the device, for text in HBM in the
+ * compact form the sender writes (serde_json::to_string, ssh.rs:1003).  *lit_len = the
+ * delta's literal bytes; with d_lit (device, lit_cap >= *lit_len) they are written there
+ * in op order, and *out (when not NULL) receives the ops, source_size and block_size,
+ * its Data ops indexing d_lit (op.a = offset of the first byte) as
+ * sydelta_apply_delta_device reads them.  Any other spelling returns SYDELTA_E_INVAL
+ * naming the first byte that breaks the form: parse those with sydelta_delta_from_json. */
+int sydelta_delta_from_json_device(const uint8_t *d_text, uint64_t len, uint8_t *d_lit, uint64_t lit_cap,
+                                   uint64_t *lit_len, sydelta_delta **out, void *stream);
 /* The zstd frame (RFC 8878) of d_in[0, len) into d_out, on the device: what ssh.rs:1009-1017
  * sends (compress(delta_json, Compression::Zstd), compress/mod.rs:71-76) and sy-remote
  * decompresses (sy-remote.rs:160-179) -- typically the text of sydelta_delta_to_json_device.

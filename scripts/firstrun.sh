@@ -1,6 +1,6 @@
 #!/bin/bash
 # First hardware run of the kernels written while round 2's GPU access was closed: their
-# GPU tests (marker firstrun: device walk, signature JSON, zstd), then their bench legs
+# GPU tests (marker firstrun: device walk, signature and Delta JSON parse/write, zstd), then their bench legs
 # (sigjson, zstd, c5 with the device walk), each step under its own limit; stops at the
 # first failure so that a fault ends the call.
 # Usage (from the repo root on the box): bash scripts/firstrun.sh [tag]

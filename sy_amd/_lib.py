@@ -108,6 +108,7 @@ SIGNATURES = [
     ("sydelta_delta_from_json", _i, [_vp, _u64, _pp]),
     ("sydelta_checksums_to_json_device", _i, [_vp, _vp, _u64, _u64, _u64, _vp, _u64, ctypes.POINTER(_u64), _vp]),
     ("sydelta_checksums_from_json_device", _i, [_vp, _u64, _vp, _u64, ctypes.POINTER(_u64), _vp]),
+    ("sydelta_delta_from_json_device", _i, [_vp, _u64, _vp, _u64, ctypes.POINTER(_u64), _pp, _vp]),
     ("sydelta_zstd_bound", _u64, [_u64]),
     ("sydelta_zstd_compress_device", _i, [_i, _vp, _u64, _vp, _u64, ctypes.POINTER(_u64), _vp]),
     ("sydelta_block_compare_device", _i, [_i, _vp, _u64, _vp, _u64, _u64, _vp, _vp, ctypes.POINTER(BlockCompareStatsC)]),

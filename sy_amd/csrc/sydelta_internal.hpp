@@ -9,6 +9,7 @@
 
 #include "sydelta_chain.hpp"
 #include "sydelta_sigjson.hpp"
+#include "sydelta_dparse.hpp"
 #include "sydelta_zstd.hpp"
 
 namespace sydelta {
@@ -181,6 +182,16 @@ hipError_t launch_sigjson_write(const sigjson::SigArgs& a, const uint64_t* d_til
 hipError_t launch_sigparse_count(const uint8_t* d_text, uint64_t len, uint64_t* d_count, hipStream_t s, Profiler* prof);
 hipError_t launch_sigparse(const uint8_t* d_text, uint64_t len, const uint64_t* d_rank, sydelta_block_checksum* d_out,
                            uint64_t cap, unsigned long long* d_bad, hipStream_t s, Profiler* prof);
+// Delta JSON parse (K7d, sydelta_dparse.hpp): per-chunk op / literal starts, op start
+// positions by rank, then ops and literal bytes (d_lit NULL: checked only); *d_bad =
+// the first bad position (atomicMin; initialised to UINT64_MAX).
+hipError_t launch_dparse_count(const dparse::DArgs& a, uint64_t* d_ocnt, uint64_t* d_lcnt, hipStream_t s,
+                               Profiler* prof);
+hipError_t launch_dparse_place(const dparse::DArgs& a, const uint64_t* d_orank, uint64_t* d_pos, hipStream_t s,
+                               Profiler* prof);
+hipError_t launch_dparse(const dparse::DArgs& a, const uint64_t* d_orank, const uint64_t* d_lrank, const uint64_t* d_pos,
+                         uint64_t nops, sydelta_op* d_ops, uint8_t* d_lit, unsigned long long* d_bad, hipStream_t s,
+                         Profiler* prof);
 // zstd frame of a text in HBM (sydelta_zstd.hpp).  Blocks [b0, b0 + nb) of d_text (len
 // bytes, 16-byte aligned, readable to the end of its last granule): slot i of d_slots
 // (zstd::kBlockMax bytes each) gets block b0+i's content, d_size[i] its size, d_type[i]

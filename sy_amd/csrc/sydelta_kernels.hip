@@ -2770,6 +2770,33 @@ __global__ __launch_bounds__(256) void k_sigparse(const uint8_t* __restrict__ t,
     if (b != UINT64_MAX) atomicMin(bad, (unsigned long long)b);
 }
 
+// K7d: the compact Delta JSON parsed on the device (sydelta_dparse.hpp).
+__global__ __launch_bounds__(256) void k_dparse_count(dparse::DArgs a, uint64_t* __restrict__ ocnt,
+                                                      uint64_t* __restrict__ lcnt) {
+    const uint64_t c = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+    if (c >= a.nc) return;
+    uint64_t no, nl;
+    dparse::chunk_count(a, c, no, nl);
+    ocnt[c] = no;
+    lcnt[c] = nl;
+}
+
+__global__ __launch_bounds__(256) void k_dparse_place(dparse::DArgs a, const uint64_t* __restrict__ orank,
+                                                      uint64_t* __restrict__ pos) {
+    const uint64_t c = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+    if (c < a.nc) dparse::chunk_place(a, c, orank[c], pos);
+}
+
+__global__ __launch_bounds__(256) void k_dparse(dparse::DArgs a, const uint64_t* __restrict__ orank,
+                                                const uint64_t* __restrict__ lrank, const uint64_t* __restrict__ pos,
+                                                uint64_t nops, sydelta_op* __restrict__ ops, uint8_t* lit,
+                                                unsigned long long* bad) {
+    const uint64_t c = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+    if (c >= a.nc) return;
+    const uint64_t b = dparse::chunk_parse(a, c, orank, lrank, pos, nops, ops, lit);
+    if (b != dparse::kNoBad) atomicMin(bad, (unsigned long long)b);
+}
+
 __global__ __launch_bounds__(256) void k_json_len(const JsonPiece* __restrict__ pieces, uint64_t npieces,
                                                   const uint8_t* __restrict__ lit, uint64_t* __restrict__ len) {
     // one wave per piece (lane l sizes literal bytes [64l, 64l + 64) of a Data chunk);
@@ -3728,6 +3755,35 @@ hipError_t launch_sigparse(const uint8_t* d_text, uint64_t len, const uint64_t* 
     if ((nc + 255) / 256 > 0x7FFFFFFFull) return hipErrorInvalidValue;
     ProfScope ps(prof, s, "k_sigparse");
     hipLaunchKernelGGL(k_sigparse, dim3(grid_for(nc, 256)), dim3(256), 0, s, d_text, len, d_rank, d_out, cap, d_bad);
+    return hipGetLastError();
+}
+
+hipError_t launch_dparse_count(const dparse::DArgs& a, uint64_t* d_ocnt, uint64_t* d_lcnt, hipStream_t s,
+                               Profiler* prof) {
+    if (!a.nc) return hipSuccess;
+    if ((a.nc + 255) / 256 > 0x7FFFFFFFull) return hipErrorInvalidValue;
+    ProfScope ps(prof, s, "k_dparse_count");
+    hipLaunchKernelGGL(k_dparse_count, dim3(grid_for(a.nc, 256)), dim3(256), 0, s, a, d_ocnt, d_lcnt);
+    return hipGetLastError();
+}
+
+hipError_t launch_dparse_place(const dparse::DArgs& a, const uint64_t* d_orank, uint64_t* d_pos, hipStream_t s,
+                               Profiler* prof) {
+    if (!a.nc) return hipSuccess;
+    if ((a.nc + 255) / 256 > 0x7FFFFFFFull) return hipErrorInvalidValue;
+    ProfScope ps(prof, s, "k_dparse_place");
+    hipLaunchKernelGGL(k_dparse_place, dim3(grid_for(a.nc, 256)), dim3(256), 0, s, a, d_orank, d_pos);
+    return hipGetLastError();
+}
+
+hipError_t launch_dparse(const dparse::DArgs& a, const uint64_t* d_orank, const uint64_t* d_lrank, const uint64_t* d_pos,
+                         uint64_t nops, sydelta_op* d_ops, uint8_t* d_lit, unsigned long long* d_bad, hipStream_t s,
+                         Profiler* prof) {
+    if (!a.nc) return hipSuccess;
+    if ((a.nc + 255) / 256 > 0x7FFFFFFFull) return hipErrorInvalidValue;
+    ProfScope ps(prof, s, "k_dparse");
+    hipLaunchKernelGGL(k_dparse, dim3(grid_for(a.nc, 256)), dim3(256), 0, s, a, d_orank, d_lrank, d_pos, nops, d_ops,
+                       d_lit, d_bad);
     return hipGetLastError();
 }
 

@@ -611,6 +611,124 @@ extern "C" int sydelta_checksums_from_json_device(const uint8_t* d_text, uint64_
     return sydelta::host_exception();
 }
 
+// serde_json::from_str::<Delta> (sy-remote.rs:175) of a text in HBM in the compact form
+// the sender writes (sydelta_dparse.hpp, K7d).  The host checks the head and parses the
+// tail (`],"source_size":N,"block_size":B}`) from two small copies; the device ranks and
+// parses the ops and literal bytes between them.  Data ops of the result index d_lit
+// (op.a = offset of its first literal byte), as sydelta_apply_delta_device reads them.
+namespace {
+// A u64 in serde's compact spelling at t[p, e): digits, no leading zero; returns the
+// digits consumed or 0.
+size_t host_dec(const char* t, size_t p, size_t e, uint64_t& v) {
+    uint64_t x = 0;
+    size_t k = 0;
+    while (p + k < e && t[p + k] >= '0' && t[p + k] <= '9') {
+        const uint64_t d = (uint64_t)(t[p + k] - '0');
+        if (x > (UINT64_MAX - d) / 10) return 0;
+        x = x * 10 + d;
+        ++k;
+    }
+    if (!k || (k > 1 && t[p] == '0')) return 0;
+    v = x;
+    return k;
+}
+}  // namespace
+
+extern "C" int sydelta_delta_from_json_device(const uint8_t* d_text, uint64_t len, uint8_t* d_lit, uint64_t lit_cap,
+                                              uint64_t* lit_len, sydelta_delta** out, void* stream) try {
+    if (!lit_len) return fail(SYDELTA_E_INVAL, "NULL argument");
+    *lit_len = 0;
+    if (out) *out = nullptr;
+    auto bad_at = [](uint64_t p) {
+        return fail(SYDELTA_E_INVAL, "Delta JSON: not serde's compact form at byte %llu", (unsigned long long)p);
+    };
+    static const char kTailKey[] = "],\"source_size\":";
+    // the shortest text: {"ops":[],"source_size":0,"block_size":0}
+    if (!d_text || len < dparse::kHead + (sizeof kTailKey - 1) + 17) return bad_at(0);
+    int dev = 0;
+    (void)hipGetDevice(&dev);
+    if (int r = ensure_device(dev)) return r;
+    hipStream_t s = stream ? (hipStream_t)stream : thread_stream(dev);
+    // head and tail (the tail is < 80 bytes: two u64 and the keys)
+    char head[dparse::kHead], tail[96];
+    const uint64_t tl = std::min<uint64_t>(len - dparse::kHead, sizeof tail);
+    HIP_TRY(hipMemcpyAsync(head, d_text, dparse::kHead, hipMemcpyDeviceToHost, s));
+    HIP_TRY(hipMemcpyAsync(tail, d_text + len - tl, tl, hipMemcpyDeviceToHost, s));
+    HIP_TRY(hipStreamSynchronize(s));
+    if (memcmp(head, "{\"ops\":[", dparse::kHead) != 0) return bad_at(0);
+    size_t at = SIZE_MAX;  // the last "],\"source_size\":" in the tail
+    for (size_t i = 0; i + sizeof kTailKey - 1 <= tl; ++i)
+        if (memcmp(tail + i, kTailKey, sizeof kTailKey - 1) == 0) at = i;
+    if (at == SIZE_MAX) return bad_at(len - tl);
+    uint64_t src_size = 0, blk = 0;
+    size_t q = at + sizeof kTailKey - 1, k;
+    static const char kBs[] = ",\"block_size\":";
+    if (!(k = host_dec(tail, q, tl, src_size))) return bad_at(len - tl + q);
+    q += k;
+    if (tl - q < sizeof kBs - 1 || memcmp(tail + q, kBs, sizeof kBs - 1) != 0) return bad_at(len - tl + q);
+    q += sizeof kBs - 1;
+    if (!(k = host_dec(tail, q, tl, blk))) return bad_at(len - tl + q);
+    q += k;
+    if (!(q + 1 == tl && tail[q] == '}')) return bad_at(len - tl + q);
+    const uint64_t E = len - tl + at;  // the ops array's ']'
+    if (E < dparse::kHead) return bad_at(E);
+    dparse::DArgs a{d_text, E, (E - dparse::kHead + dparse::kChunk - 1) / dparse::kChunk};
+    uint64_t nops = 0, nlit = 0;
+    CallProf cp;
+    DevBuf_wire buf;
+    const uint64_t nc = a.nc;
+    HIP_TRY(hipMallocAsync(&buf.p, (4 * (nc + 1) + 1) * 8, s));
+    buf.s = s;
+    uint64_t* d_ocnt = (uint64_t*)buf.p;
+    uint64_t* d_lcnt = d_ocnt + nc + 1;
+    uint64_t* d_orank = d_lcnt + nc + 1;
+    uint64_t* d_lrank = d_orank + nc + 1;
+    unsigned long long* d_bad = (unsigned long long*)(d_lrank + nc + 1);
+    HIP_TRY(hipMemsetAsync(d_ocnt, 0, 2 * (nc + 1) * 8, s));
+    HIP_TRY(hipMemsetAsync(d_bad, 0xFF, 8, s));
+    if (nc) {
+        HIP_TRY(launch_dparse_count(a, d_ocnt, d_lcnt, s, cp.get()));
+        HIP_TRY(launch_exclusive_sum_u64(d_ocnt, d_orank, nc + 1, s));  // [nc]: the totals
+        HIP_TRY(launch_exclusive_sum_u64(d_lcnt, d_lrank, nc + 1, s));
+        HIP_TRY(hipMemcpyAsync(&nops, d_orank + nc, 8, hipMemcpyDeviceToHost, s));
+        HIP_TRY(hipMemcpyAsync(&nlit, d_lrank + nc, 8, hipMemcpyDeviceToHost, s));
+        HIP_TRY(hipStreamSynchronize(s));
+    }
+    if (nc && nops == 0) return bad_at(dparse::kHead);  // a non-empty ops region starts with an op
+    *lit_len = nlit;
+    if (d_lit && lit_cap < nlit)
+        return fail(SYDELTA_E_INVAL, "literal buffer holds %llu bytes, the delta has %llu",
+                    (unsigned long long)lit_cap, (unsigned long long)nlit);
+    std::unique_ptr<sydelta_delta> d(new sydelta_delta());
+    d->source_size = src_size;
+    d->block_size = blk;
+    if (nops) {
+        DevBuf_wire ob;
+        HIP_TRY(hipMallocAsync(&ob.p, nops * (8 + sizeof(sydelta_op)), s));
+        ob.s = s;
+        uint64_t* d_pos = (uint64_t*)ob.p;
+        sydelta_op* d_ops = (sydelta_op*)(d_pos + nops);
+        HIP_TRY(launch_dparse_place(a, d_orank, d_pos, s, cp.get()));
+        HIP_TRY(launch_dparse(a, d_orank, d_lrank, d_pos, nops, d_ops, d_lit, d_bad, s, cp.get()));
+        uint64_t b = 0;
+        HIP_TRY(hipMemcpyAsync(&b, d_bad, 8, hipMemcpyDeviceToHost, s));
+        if (out) {
+            d->ops.resize(nops);
+            HIP_TRY(hipMemcpyAsync(d->ops.data(), d_ops, nops * sizeof(sydelta_op), hipMemcpyDeviceToHost, s));
+        }
+        HIP_TRY(hipStreamSynchronize(s));
+        if (b != UINT64_MAX) return bad_at(b);
+    }
+    for (const sydelta_op& o : d->ops) {
+        if (o.kind == SYDELTA_OP_COPY) ++d->stats.copy_ops;
+        else { ++d->stats.data_ops; d->stats.literal_bytes += o.b; }
+    }
+    if (out) *out = d.release();
+    return SYDELTA_OK;
+} catch (...) {
+    return sydelta::host_exception();
+}
+
 // ---------------------------------------------------------------------------
 // zstd frame of a text in HBM (ssh.rs:1009-1017: compress(delta_json, Compression::Zstd);
 // sydelta_zstd.hpp).  The text goes through in batches of 512 blocks (64 MiB): block

@@ -131,6 +131,31 @@ def checksums_from_json_device(d_text, stream=None):
     return out[:n.value * _SIG_DTYPE.itemsize], n.value
 
 
+def delta_from_json_device(d_text, stream=None):
+    """serde_json::from_str::<Delta> of a compact Delta JSON text in HBM (uint8 device
+    tensor) parsed on the device: returns (ops as [(kind, a, b)] with Data ops indexing the
+    literal tensor, the literal bytes as a uint8 device tensor, source_size, block_size).
+    Raises SyDeltaError for text in any other spelling (parse that with delta_from_json)."""
+    import torch
+
+    from .device import _ptr, _stream
+
+    n = ctypes.c_uint64()
+    check(lib.sydelta_delta_from_json_device(_ptr(d_text), d_text.numel(), None, 0, ctypes.byref(n), None,
+                                             _stream(stream)))
+    lit = torch.empty(max(1, n.value), dtype=torch.uint8, device=d_text.device)
+    h = ctypes.c_void_p()
+    check(lib.sydelta_delta_from_json_device(_ptr(d_text), d_text.numel(), _ptr(lit), lit.numel(), ctypes.byref(n),
+                                             ctypes.byref(h), _stream(stream)))
+    try:
+        cnt = lib.sydelta_delta_num_ops(h)
+        ops_p = lib.sydelta_delta_ops(h)
+        ops = [(int(ops_p[i].kind), int(ops_p[i].a), int(ops_p[i].b)) for i in range(cnt)]
+        return ops, lit[:n.value], int(lib.sydelta_delta_source_size(h)), int(lib.sydelta_delta_block_size(h))
+    finally:
+        lib.sydelta_delta_free(h)
+
+
 def zstd_compress_device(d_text, stream=None, device: int = 0):
     """zstd frame (Huffman literals, FSE-coded sequences) of the bytes of a uint8 device tensor, as a uint8
     device tensor: the compression ssh.rs:1009-1017 applies to the Delta JSON.  The
@@ -148,7 +173,7 @@ def zstd_compress_device(d_text, stream=None, device: int = 0):
 
 
 def delta_from_json(text: bytes):
-    """-> (ops as [(kind, len)], literal bytes per Data op, source_size, block_size)."""
+    """-> (ops as [("C", offset, size) | ("D", literal bytes)], source_size, block_size)."""
     h = ctypes.c_void_p()
     check(lib.sydelta_delta_from_json(text, len(text), ctypes.byref(h)))
     try:

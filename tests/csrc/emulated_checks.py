@@ -260,7 +260,104 @@ def sigjson_checks():
                                                   bs, last, None, 0, ctypes.byref(got), None)
         assert rc != 0, (bs, last)
     assert lib.sydelta_checksums_to_json_device(None, None, 4, 4096, 4096, None, 0, ctypes.byref(got), None) != 0
-    return n_checks + 6 + sigparse_checks()
+    return n_checks + 6 + sigparse_checks() + dparse_checks()
+
+
+def dparse_checks():
+    """sydelta_delta_from_json_device (K7d; the emulated launches run sydelta_dparse.hpp's
+    chunk bodies): the compact Delta JSON of random deltas (copy-heavy, literal-heavy,
+    empty Data ops, no ops, literal runs across many chunks) parses to the host parser's
+    ops and literal bytes; the length query and a short literal buffer; and every
+    non-compact or malformed spelling is refused while the host parser keeps its own
+    verdict; random mutations are refused or re-serialize to themselves."""
+    import ctypes
+    import json
+    import random
+
+    from sy_amd import wire
+    from sy_amd._lib import SyDeltaError, check, lib
+
+    rng = random.Random(21)
+
+    def dev_parse(text: bytes):
+        buf = np.frombuffer(text, np.uint8).copy() if text else np.zeros(1, np.uint8)
+        n = ctypes.c_uint64()
+        if lib.sydelta_delta_from_json_device(ctypes.c_void_p(buf.ctypes.data), len(text), None, 0, ctypes.byref(n),
+                                              None, None):
+            return None
+        lit = np.zeros(max(1, n.value), np.uint8)
+        if n.value:
+            short = ctypes.c_uint64()
+            assert lib.sydelta_delta_from_json_device(ctypes.c_void_p(buf.ctypes.data), len(text),
+                                                      ctypes.c_void_p(lit.ctypes.data), n.value - 1,
+                                                      ctypes.byref(short), None, None) != 0
+        h = ctypes.c_void_p()
+        check(lib.sydelta_delta_from_json_device(ctypes.c_void_p(buf.ctypes.data), len(text),
+                                                 ctypes.c_void_p(lit.ctypes.data), lit.size, ctypes.byref(n),
+                                                 ctypes.byref(h), None))
+        try:
+            cnt = lib.sydelta_delta_num_ops(h)
+            p = lib.sydelta_delta_ops(h)
+            ops = []
+            for i in range(cnt):
+                if p[i].kind == 0:
+                    ops.append(("C", int(p[i].a), int(p[i].b)))
+                else:
+                    ops.append(("D", lit[p[i].a:p[i].a + p[i].b].tobytes()))
+            return ops, int(lib.sydelta_delta_source_size(h)), int(lib.sydelta_delta_block_size(h))
+        finally:
+            lib.sydelta_delta_free(h)
+
+    def compact(ops, ss, bs):
+        return json.dumps({"ops": [{"Copy": {"offset": o[1], "size": o[2]}} if o[0] == "C" else {"Data": list(o[1])}
+                                   for o in ops], "source_size": ss, "block_size": bs}, separators=(",", ":")).encode()
+
+    def expect(text):
+        d = json.loads(text)
+        ops = [("C", o["Copy"]["offset"], o["Copy"]["size"]) if "Copy" in o else ("D", bytes(o["Data"]))
+               for o in d["ops"]]
+        return ops, d["source_size"], d["block_size"]
+
+    n_checks = 0
+    cases = [([], 0, 4096), ([("D", b"")], 0, 1), ([("C", 0, 4096)], 4096, 4096),
+             ([("D", bytes(range(256)) * 3)], 768, 4096), ([("D", b""), ("C", 2**64 - 1, 2**64 - 1), ("D", b"\x00")], 7, 9)]
+    for it in range(12):
+        ops = []
+        for _ in range(rng.randint(1, 400)):
+            if rng.random() < 0.6:
+                ops.append(("C", rng.randrange(1 << 40), rng.choice([4096, 17, 0])))
+            else:
+                ops.append(("D", bytes(rng.randrange(256) for _ in range(rng.choice([0, 1, 2, 63, 64, 65, 300, 5000])))))
+        cases.append((ops, rng.randrange(1 << 50), rng.choice([512, 4096, 131072])))
+    for ops, ss, bs in cases:
+        text = compact(ops, ss, bs)
+        got = dev_parse(text)
+        assert got == (ops, ss, bs), (len(ops), got if got is None else len(got[0]))
+        assert wire.delta_from_json(text) == got  # the host parser reads the same delta
+        n_checks += 1
+    good = compact([("C", 4096, 4096), ("D", b"\x01\xff"), ("D", b"")], 8192, 4096)
+    assert dev_parse(good) is not None
+    bad = [b"", b"{}", b'{"ops":[]}', good[:-1], good + b" ", b" " + good, good.replace(b",", b", ", 1),
+           good.replace(b'"Copy"', b'"copy"'), good.replace(b'"offset":4096,"size":4096', b'"size":4096,"offset":4096'),
+           good.replace(b"[1,255]", b"[1,256]"), good.replace(b"[1,255]", b"[01,255]"), good.replace(b"[1,255]", b"[1,,255]"),
+           good.replace(b"[1,255]", b"[1,255,]"), good.replace(b"[1,255]", b"[-1,255]"), good.replace(b"},{", b"}{", 1),
+           good.replace(b'"source_size":8192', b'"source_size":08192'), good.replace(b'"block_size":4096}', b'"block_size":4096,"x":1}'),
+           good.replace(b'{"Data":[]}', b'{"Data":[],"x":0}'), good.replace(b'{"ops":[', b'{"ops" :['),
+           good.replace(b"]}]", b"]}}]"), good.replace(b'{"Copy":{"offset":4096,"size":4096}}', b'{"Copy":{"offset":4096,"size":4096},"x":1}')]
+    for t in bad:
+        assert dev_parse(t) is None, t
+        n_checks += 1
+    for it in range(300):
+        b = bytearray(good)
+        for _ in range(rng.randint(1, 3)):
+            b[rng.randrange(len(b))] = rng.choice(b'0123456789{}[],:"aDC ')
+        t = bytes(b)
+        got = dev_parse(t)
+        if got is not None:
+            assert compact(*got) == t, t
+            assert got == expect(t) == wire.delta_from_json(t), t
+        n_checks += 1
+    return n_checks
 
 
 def sigparse_checks():

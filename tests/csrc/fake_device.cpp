@@ -459,6 +459,28 @@ hipError_t launch_sigparse(const uint8_t* d_text, uint64_t len, const uint64_t* 
     }
     return hipSuccess;
 }
+// K7d: sydelta_dparse.hpp's chunk bodies per chunk (parse in descending chunk order).
+hipError_t launch_dparse_count(const dparse::DArgs& a, uint64_t* d_ocnt, uint64_t* d_lcnt, hipStream_t, Profiler*) {
+    EmuTimer emu_t;
+    for (uint64_t c = 0; c < a.nc; ++c) dparse::chunk_count(a, c, d_ocnt[c], d_lcnt[c]);
+    return hipSuccess;
+}
+hipError_t launch_dparse_place(const dparse::DArgs& a, const uint64_t* d_orank, uint64_t* d_pos, hipStream_t,
+                               Profiler*) {
+    EmuTimer emu_t;
+    for (uint64_t c = 0; c < a.nc; ++c) dparse::chunk_place(a, c, d_orank[c], d_pos);
+    return hipSuccess;
+}
+hipError_t launch_dparse(const dparse::DArgs& a, const uint64_t* d_orank, const uint64_t* d_lrank, const uint64_t* d_pos,
+                         uint64_t nops, sydelta_op* d_ops, uint8_t* d_lit, unsigned long long* d_bad, hipStream_t,
+                         Profiler*) {
+    EmuTimer emu_t;
+    for (uint64_t c = a.nc; c-- > 0;) {
+        const uint64_t b = dparse::chunk_parse(a, c, d_orank, d_lrank, d_pos, nops, d_ops, d_lit);
+        if (b < *d_bad) *d_bad = b;
+    }
+    return hipSuccess;
+}
 // K5b: the kernels' own per-thread bodies (sydelta_chain.hpp) in the launch order of
 // sydelta_kernels.hip's launch_chain, one loop per kernel.  The marking levels run their
 // threads alternately forward and backward: two of the schedules a GPU may produce for

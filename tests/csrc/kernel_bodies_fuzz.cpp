@@ -20,7 +20,9 @@
 //    stored chunk by chunk (chunks shuffled) into an output of exactly the text's length
 //    at a random alignment; the text equals a printf-built one and the length bounds hold;
 //  * its parse (K7p): texts in exact-size arrays parse back to their signature, and a
-//    mutated text is refused or is the compact text of what it parses to.
+//    mutated text is refused or is the compact text of what it parses to;
+//  * the Delta JSON parse (sydelta_dparse.hpp, K7d): the same two properties for the ops
+//    region of random deltas' compact text.
 #include <stdint.h>
 #include <stdio.h>
 #include <stdlib.h>
@@ -35,6 +37,7 @@
 
 #include "sydelta_chain.hpp"
 #include "sydelta_sigjson.hpp"
+#include "sydelta_dparse.hpp"
 #include "sydelta_walk.hpp"
 #include "sydelta_zstd.hpp"
 
@@ -487,6 +490,109 @@ static void sigparse_case(std::mt19937_64& rng, uint64_t* accepted, uint64_t* re
     }
 }
 
+// K7d: the Delta JSON parse bodies on texts in arrays of exactly their length; the ops
+// region of a random delta's compact text parses back to it; a mutated text is refused
+// or its ops region is the compact text of what it parses to.
+struct DOp {
+    bool copy;
+    uint64_t o, s;
+    std::vector<uint8_t> lit;
+};
+static std::string dops_text(const std::vector<DOp>& v) {
+    std::string t;
+    char tmp[96];
+    for (size_t i = 0; i < v.size(); ++i) {
+        if (i) t += ",";
+        if (v[i].copy) {
+            snprintf(tmp, sizeof tmp, "{\"Copy\":{\"offset\":%llu,\"size\":%llu}}", (unsigned long long)v[i].o,
+                     (unsigned long long)v[i].s);
+            t += tmp;
+        } else {
+            t += "{\"Data\":[";
+            for (size_t k = 0; k < v[i].lit.size(); ++k) {
+                if (k) t += ",";
+                t += std::to_string((unsigned)v[i].lit[k]);
+            }
+            t += "]}";
+        }
+    }
+    return t;
+}
+// Parse the ops region of text (head, region, tail) with the chunk bodies; false if refused.
+static bool dparse_all(const std::string& text, std::vector<DOp>& out) {
+    const std::string key = "],\"source_size\":";
+    const size_t at = text.rfind(key);
+    if (text.size() < 8 || at == std::string::npos || at < 8 || text.compare(0, 8, "{\"ops\":[") != 0) return false;
+    const uint64_t len = text.size();
+    std::unique_ptr<uint8_t[]> t(new uint8_t[len]);
+    memcpy(t.get(), text.data(), len);
+    const dparse::DArgs a{t.get(), at, (at - 8 + dparse::kChunk - 1) / dparse::kChunk};
+    std::vector<uint64_t> orank(a.nc + 1, 0), lrank(a.nc + 1, 0);
+    for (uint64_t c = 0; c < a.nc; ++c) {
+        uint64_t no, nl;
+        dparse::chunk_count(a, c, no, nl);
+        orank[c + 1] = orank[c] + no;
+        lrank[c + 1] = lrank[c] + nl;
+    }
+    const uint64_t nops = orank[a.nc], nlit = lrank[a.nc];
+    if (a.nc && !nops) return false;
+    std::unique_ptr<uint64_t[]> pos(new uint64_t[nops ? nops : 1]);
+    std::unique_ptr<sydelta_op[]> ops(new sydelta_op[nops ? nops : 1]);
+    std::unique_ptr<uint8_t[]> lit(new uint8_t[nlit ? nlit : 1]);
+    for (uint64_t c = 0; c < a.nc; ++c) dparse::chunk_place(a, c, orank[c], pos.get());
+    for (uint64_t c = a.nc; c-- > 0;)
+        if (dparse::chunk_parse(a, c, orank.data(), lrank.data(), pos.get(), nops, ops.get(), lit.get()) != dparse::kNoBad)
+            return false;
+    out.clear();
+    for (uint64_t i = 0; i < nops; ++i) {
+        DOp d{ops[i].kind == SYDELTA_OP_COPY, ops[i].a, ops[i].b, {}};
+        if (!d.copy) {
+            CHECK(ops[i].a + ops[i].b <= nlit);
+            d.lit.assign(lit.get() + ops[i].a, lit.get() + ops[i].a + ops[i].b);
+        }
+        out.push_back(d);
+    }
+    return true;
+}
+static void dparse_case(std::mt19937_64& rng, uint64_t* accepted, uint64_t* refused) {
+    std::vector<DOp> v(rng() % 40);
+    for (auto& d : v) {
+        d.copy = rng() % 2;
+        d.o = rng() % 3 ? rng() % 100000 : ~0ull;
+        d.s = rng() % 5000;
+        if (!d.copy) {
+            d.lit.resize(rng() % 4 ? rng() % 40 : rng() % 3000);
+            for (auto& b : d.lit) b = (uint8_t)rng();
+        }
+    }
+    const std::string tail = "],\"source_size\":123,\"block_size\":4096}";
+    const std::string text = "{\"ops\":[" + dops_text(v) + tail;
+    std::vector<DOp> back;
+    CHECK(dparse_all(text, back));
+    CHECK(back.size() == v.size());
+    for (size_t i = 0; i < v.size(); ++i)
+        CHECK(back[i].copy == v[i].copy && (v[i].copy ? back[i].o == v[i].o && back[i].s == v[i].s : back[i].lit == v[i].lit));
+    static const char alpha[] = "0123456789{}[],:\"aDC -";
+    for (int m = 0; m < 20; ++m) {
+        std::string t = text;
+        for (int j = 0, k = 1 + (int)(rng() % 3); j < k; ++j) {
+            const int op = (int)(rng() % 3);
+            const size_t at = rng() % t.size();
+            if (op == 0) t[at] = alpha[rng() % (sizeof alpha - 1)];
+            else if (op == 1) t.insert(t.begin() + at, alpha[rng() % (sizeof alpha - 1)]);
+            else if (t.size() > 1) t.erase(t.begin() + at);
+        }
+        std::vector<DOp> got;
+        if (dparse_all(t, got)) {
+            const size_t at = t.rfind("],\"source_size\":");
+            CHECK(t.substr(8, at - 8) == dops_text(got));
+            ++*accepted;
+        } else {
+            ++*refused;
+        }
+    }
+}
+
 int main(int argc, char** argv) {
     const int iters = argc > 1 ? atoi(argv[1]) : 2000;
     std::mt19937_64 rng(20261017);
@@ -500,13 +606,17 @@ int main(int argc, char** argv) {
     uint64_t acc = 0, ref = 0;
     for (int it = 0; it < std::max(1, iters / 10); ++it) sigparse_case(rng, &acc, &ref);
     CHECK(acc > 0 && ref > 0);
+    uint64_t dacc = 0, dref = 0;
+    for (int it = 0; it < std::max(1, iters / 10); ++it) dparse_case(rng, &dacc, &dref);
+    CHECK(dacc > 0 && dref > 0);
     uint64_t sj = 0;
     for (int it = 0; it < std::max(1, iters / 10); ++it) sigjson_case(rng, &sj);
     CHECK(walked > (uint64_t)iters / 4);
     printf("kernel bodies ok: %llu chain cases (%llu resolved on the device path), %llu zstd blocks, %llu stream "
-           "replicas, %llu repeat offsets, %llu signature JSON entries, %llu/%llu mutated texts accepted/refused\n",
+           "replicas, %llu repeat offsets, %llu signature JSON entries, %llu/%llu mutated texts accepted/refused, "
+           "%llu/%llu mutated Delta texts accepted/refused\n",
            (unsigned long long)cases, (unsigned long long)walked, (unsigned long long)blocks,
            (unsigned long long)replica, (unsigned long long)reps, (unsigned long long)sj, (unsigned long long)acc,
-           (unsigned long long)ref);
+           (unsigned long long)ref, (unsigned long long)dacc, (unsigned long long)dref);
     return 0;
 }
