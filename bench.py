@@ -22,6 +22,9 @@ already resident in HBM:
      the C2 signature (4 GiB basis, 1 Mi entries) written on the device (the remote's
      side) and parsed back on the device (the sender's side); value = basis GiB/s
      covered; cpu_baseline = libsydelta's host writer + host parser on the same signature.
+  dparse (sy-remote.rs:175): the receiver's parse of that JSON text
+     on the device (literal bytes into HBM + the op list); value = literal GiB/s;
+     cpu_baseline = libsydelta's host parser on a 256 MiB-literal sample.
   zstd (ssh.rs:1009-1017): the zstd frame of that JSON text (1 GiB
      source by default, ~3.6 GiB of text) on the device; value = text GiB/s;
      cpu_baseline = libzstd level 3 (compress/mod.rs:71-76) on one thread, 64 MiB sample.
@@ -74,7 +77,7 @@ def parse():
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--workload", default="c3",
-                    choices=["c3", "c3b", "c2", "c4", "c5", "apply", "json", "sigjson", "zstd", "local", "xxh3", "path"])
+                    choices=["c3", "c3b", "c2", "c4", "c5", "apply", "json", "dparse", "sigjson", "zstd", "local", "xxh3", "path"])
     ap.add_argument("--size-gib", type=float, default=None,
                     help="bytes per rank: c2/c3 basis and source (default 4), c5 chunk (default 8)")
     ap.add_argument("--block-size", type=int, default=None, help="default 4096 (c5: 8192)")
@@ -245,6 +248,21 @@ def cpu_sigjson_baseline(w_dev, s_dev, bs: int):
     return {"value": round(w.size * bs / dt / GIB, 4), "unit": "GiB/s", "cores": 1, "kind": "port",
             "sample": f"host writer + host parser, {w.size} entries ({len(text) >> 20} MiB of text), basis GiB/s "
                       f"covered"}
+
+
+def cpu_dparse_baseline(src_dev, bs: int):
+    """libsydelta's host serde_json parser (sydelta_delta_from_json, one thread) on the
+    text of one Data op of 256 MiB of the same source (sy-remote.rs:175)."""
+    from sy_amd import wire
+
+    sample = src_dev[:256 << 20].cpu().numpy()
+    text = wire.delta_to_json([1], [0], [sample.size], sample.size, bs, sample)
+    t0 = time.perf_counter()
+    ops, _, _ = wire.delta_from_json(text)
+    dt = time.perf_counter() - t0
+    assert len(ops) == 1 and len(ops[0][1]) == sample.size
+    return {"value": round(sample.size / dt / GIB, 4), "unit": "GiB/s", "cores": 1, "kind": "port",
+            "sample": f"host parser, one Data op of {sample.size >> 20} MiB ({len(text) >> 20} MiB of text)"}
 
 
 def cpu_zstd_baseline(text_dev, sample_bytes: int = 64 << 20):
@@ -470,6 +488,7 @@ def algo_bytes_per_step(workload: str, n: int, nb_bytes: int, src_bytes: int) ->
             "k_apply": 2 * n,  # apply: every output byte read once and written once
             "k_json_write": n,  # json: every literal byte read once (text written: ~3.6x)
             "k_zstd_block": src_bytes,  # zstd: every text byte read once
+            "k_dparse": src_bytes,  # dparse: the text read once + the literal bytes written
             "k_sigjson_write": src_bytes,  # sigjson: 12 B per entry read + the text written once
             "k_sigparse": src_bytes + 28 * (n // 4096),  # sigjson (bs 4096): the text read once + 40 B per entry written
             "k_block_cmp": 2 * n,  # local: both files read once
@@ -569,7 +588,7 @@ def main():
     c5 = None
     apply_d = None
     json_d = None
-    if args.workload in ("json", "zstd"):
+    if args.workload in ("json", "zstd", "dparse"):
         from sy_amd import wire
 
         dev.synth_fill(basis, seed_base)
@@ -584,10 +603,13 @@ def main():
         check(lib.sydelta_delta_to_json_device(json_h, new.data_ptr(), n, None, 0, ctypes.byref(json_len), None))
         json_out = torch.empty(json_len.value + 16, dtype=torch.uint8, device="cuda")
         zstd_len = json_len.value
-        if args.workload == "zstd":  # the text to compress, written once
+        if args.workload in ("zstd", "dparse"):  # the text to compress / parse, written once
             check(lib.sydelta_delta_to_json_device(json_h, new.data_ptr(), n, json_out.data_ptr(), json_out.numel(),
                                                    ctypes.byref(json_len), None))
-            zstd_out = torch.empty(int(lib.sydelta_zstd_bound(zstd_len)) + 16, dtype=torch.uint8, device="cuda")
+            if args.workload == "zstd":
+                zstd_out = torch.empty(int(lib.sydelta_zstd_bound(zstd_len)) + 16, dtype=torch.uint8, device="cuda")
+            else:
+                dp_lit = torch.empty(n + 16, dtype=torch.uint8, device="cuda")
     if args.workload == "sigjson":
         from sy_amd import wire
 
@@ -750,6 +772,14 @@ def main():
             check(lib.sydelta_checksums_from_json_device(sj_out.data_ptr(), ln.value, sj_recs.data_ptr(),
                                                          sj_w.numel(), ctypes.byref(got), int(stream.cuda_stream)))
             return {"json_bytes": ln.value, "entries": sj_w.numel(), "parsed": got.value}
+        if args.workload == "dparse":
+            ln = ctypes.c_uint64()
+            h = ctypes.c_void_p()
+            check(lib.sydelta_delta_from_json_device(json_out.data_ptr(), zstd_len, dp_lit.data_ptr(), dp_lit.numel(),
+                                                     ctypes.byref(ln), ctypes.byref(h), int(stream.cuda_stream)))
+            nops = int(lib.sydelta_delta_num_ops(h))
+            lib.sydelta_delta_free(h)
+            return {"text_bytes": zstd_len, "literal_bytes": ln.value, "ops": nops}
         if args.workload == "json":
             ln = ctypes.c_uint64()
             check(lib.sydelta_delta_to_json_device(json_h, new.data_ptr(), n, json_out.data_ptr(), json_out.numel(),
@@ -810,6 +840,8 @@ def main():
         bytes_per_step = int(xxh_lens.sum())
     elif args.workload == "zstd":
         bytes_per_step = zstd_len  # JSON text compressed
+    elif args.workload == "dparse":
+        bytes_per_step = n  # literal bytes recovered from the text
     elif args.workload == "json":
         bytes_per_step = n  # delta source bytes covered by the text
     elif args.workload == "sigjson":
@@ -823,7 +855,7 @@ def main():
     ms_per_step = elapsed / args.steps * 1e3
 
     src_bytes = (int(files[3].sum()) if args.workload == "c4" else new.numel() if args.workload == "c3b" else
-                 zstd_len if args.workload == "zstd" else
+                 zstd_len if args.workload == "zstd" else zstd_len + n if args.workload == "dparse" else
                  sj_len + 12 * (n // bs) if args.workload == "sigjson" else n)
     algo_step = algo_bytes_per_step(args.workload, n, nb_bytes, src_bytes)
     stats = (last if isinstance(last, dict) else last.stats) if last is not None else None
@@ -845,6 +877,8 @@ def main():
             cpu = cpu_zstd_baseline(json_out[:zstd_len])
         if world == 1 and not args.no_cpu_baseline and args.workload == "sigjson":
             cpu = cpu_sigjson_baseline(sj_w, sj_s, bs)
+        if world == 1 and not args.no_cpu_baseline and args.workload == "dparse":
+            cpu = cpu_dparse_baseline(new, bs)
         if world == 1 and not args.no_cpu_baseline and args.workload == "json":
             cpu = cpu_json_baseline(new, bs)
         if world == 1 and not args.no_cpu_baseline and args.workload == "xxh3":
@@ -891,6 +925,8 @@ def main():
                              f"bs {bs}, {args.edit_ppm / 1e4:g}% of blocks edited",
                     "sigjson": f"serde_json text of the C2 signature ({n / GIB:g} GiB basis, {n // bs} entries) "
                                f"written and parsed back on the device",
+                    "dparse": f"the C3 delta's serde_json text ({n / GIB:g} GiB source, one literal run) parsed on "
+                              f"the device: literal bytes to HBM + the op list",
                     "json": f"serde_json text of the C3 delta ({n / GIB:.0f} GiB source, one literal run) on the device",
                     "zstd": f"zstd frame (Huffman literals + FSE-coded sequences, 128 KiB blocks) of the C3 delta's JSON text ({n / GIB:g} GiB source, "
                             f"one literal run) on the device; value = text bytes/s",

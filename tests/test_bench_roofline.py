@@ -103,6 +103,8 @@ def test_cpu_baselines_other_workloads_small():
     z = bench.cpu_zstd_baseline(text, sample_bytes=64 << 10)
     assert z["value"] > 0 and "level 3" in z["sample"]
     j = bench.cpu_json_baseline(new, bs)
+    dp = bench.cpu_dparse_baseline(new, bs)
+    assert dp["value"] > 0 and dp["sample"].startswith("host parser, one Data op of 1 MiB")
     assert j["value"] > 0 and j["cores"] == 1
     offs = np.arange(4, dtype=np.uint64) * np.uint64(1 << 18)
     lens = np.full(4, 1 << 18, np.uint64)
