@@ -289,7 +289,8 @@ int sydelta_checksums_to_json_device(const uint32_t *d_weak, const uint64_t *d_s
 /* serde_json::from_str::<Vec<BlockChecksum>> (ssh.rs:967-973) on the device, for text in
  * HBM that is exactly the compact form sy-remote prints (serde_json::to_string: fields in
  * checksum.rs's order, no whitespace); d_out (device, cap entries; NULL: validate and
- * count only) receives the entries in order, *n_out their count.  Any other spelling --
+ * count only) receives the entries in order (those past cap are not written), *n_out
+ * their count.  Any other spelling --
  * including ones serde accepts, such as whitespace or other key orders -- returns
  * SYDELTA_E_INVAL naming the first byte that breaks the form: parse those with
  * sydelta_checksums_from_json. */
