@@ -195,7 +195,7 @@ __host__ __device__ __forceinline__ void stream_range(uint32_t regen, bool four,
 // greedy parse takes a match of >= kMinMatch wherever one starts, and the sequences are
 // FSE-coded with tables built from the block's own code counts (RLE for a code that
 // never changes).
-constexpr uint32_t kMinMatch = 4;
+constexpr uint32_t kMinMatch = 6;
 constexpr uint32_t kProbe = 32;     // bytes compared per candidate when ranking them
 constexpr uint32_t kGapCands = 4;   // most common '{' gaps
 constexpr uint32_t kRepCands = 3;   // most common sampled repeat distances
