@@ -189,26 +189,39 @@ struct DevBuf_wire {
 // serde_json::to_string(&Vec<BlockChecksum>)  (sy-remote.rs:147, without println's '\n')
 extern "C" uint64_t sydelta_checksums_to_json(const sydelta_block_checksum* sigs, uint64_t n, char* buf,
                                               uint64_t cap) {
-    std::string o;
-    o.reserve(n * 96 + 2);
-    o.push_back('[');
+    // the exact length first (digit counts), then the text straight into buf: one pass
+    // each, no intermediate string
+    auto digits = [](uint64_t v) {
+        uint64_t d = 1;
+        while (v >= 10) {
+            v /= 10;
+            ++d;
+        }
+        return d;
+    };
+    uint64_t total = 2;  // [ ]
+    for (uint64_t i = 0; i < n; ++i)
+        total += (i ? 1 : 0) + 46 + digits(sigs[i].index) + digits(sigs[i].offset) + digits(sigs[i].size) +
+                 digits(sigs[i].weak) + digits(sigs[i].strong);
+    if (!buf || cap < total) return total;
+    char* p = buf;
+    *p++ = '[';
     for (uint64_t i = 0; i < n; ++i) {
-        if (i) o.push_back(',');
-        put(o, "{\"index\":");
-        put_num(o, sigs[i].index);
-        put(o, ",\"offset\":");
-        put_num(o, sigs[i].offset);
-        put(o, ",\"size\":");
-        put_num(o, sigs[i].size);
-        put(o, ",\"weak\":");
-        put_num(o, sigs[i].weak);
-        put(o, ",\"strong\":");
-        put_num(o, sigs[i].strong);
-        o.push_back('}');
+        if (i) *p++ = ',';
+        memcpy(p, "{\"index\":", 9);
+        p = put_u64(p + 9, sigs[i].index);
+        memcpy(p, ",\"offset\":", 10);
+        p = put_u64(p + 10, sigs[i].offset);
+        memcpy(p, ",\"size\":", 8);
+        p = put_u64(p + 8, sigs[i].size);
+        memcpy(p, ",\"weak\":", 8);
+        p = put_u64(p + 8, sigs[i].weak);
+        memcpy(p, ",\"strong\":", 10);
+        p = put_u64(p + 10, sigs[i].strong);
+        *p++ = '}';
     }
-    o.push_back(']');
-    if (buf && cap >= o.size()) memcpy(buf, o.data(), o.size());
-    return o.size();
+    *p++ = ']';
+    return total;
 }
 
 // serde_json::from_str::<Vec<BlockChecksum>>  (ssh.rs:967-973)

@@ -122,4 +122,4 @@ def test_cpu_baselines_other_workloads_small():
     w = torch.from_numpy(np.arange(256, dtype=np.uint32).view(np.int32))
     s = torch.from_numpy(np.arange(256, dtype=np.uint64).view(np.int64))
     sj = bench.cpu_sigjson_baseline(w, s, bs)
-    assert sj["value"] > 0 and sj["sample"].startswith("host writer + host parser, 256 entries")
+    assert sj["value"] > 0 and sj["sample"].startswith("host writer + host parser (C calls only), 256 entries")
