@@ -131,6 +131,10 @@ def test_checksums_json_accepts_valid_unknown_values(good):
     '{"ops":[{"Copy":{"offset":0,"offset":0,"size":1}}],"source_size":1,"block_size":4}',
     '{"ops":[],"source_size":0,"block_size":4,"x":[}',
     '{"ops":[{"Data":[256]}],"source_size":1,"block_size":4}',
+    # serde_json: "invalid number" (no leading zeros)
+    '{"ops":[{"Data":[01]}],"source_size":1,"block_size":4}',
+    '{"ops":[{"Copy":{"offset":00,"size":1}}],"source_size":1,"block_size":4}',
+    '{"ops":[],"source_size":01,"block_size":4}',
 ])
 def test_delta_json_rejects_malformed(bad):
     import sy_amd._lib as L
