@@ -21,12 +21,21 @@ def norm(name):
     return name.split("(")[0].replace("void ", "").replace("sydelta::", "").split("<")[0].strip()
 
 
-def per_kernel(path):
+def per_kernel(path, counter=None):
     agg = collections.defaultdict(list)
     for r in csv.DictReader(open(path)):
+        if counter is not None and r["Counter_Name"] != counter:
+            continue
         name = norm(r["Kernel_Name"])
         agg[name].append(float(r["Counter_Value"]))
     return {k: sum(v) / len(v) for k, v in agg.items()}
+
+
+def counters(path):
+    names = set()
+    for r in csv.DictReader(open(path)):
+        names.add(r["Counter_Name"])
+    return sorted(names)
 
 
 def main(src, dst, sizes=()):
@@ -42,6 +51,13 @@ def main(src, dst, sizes=()):
         dur[name] = {"calls": int(r["Calls"]), "avg_ms": float(r["AverageNs"]) / 1e6}
     fetch = per_kernel(os.path.join(src, "pmc_fetch", "run_counter_collection.csv"))
     write = per_kernel(os.path.join(src, "pmc_write", "run_counter_collection.csv"))
+    extra = {}  # raw per-launch averages of the other passes (TCC / TCP request counts)
+    for p in ("tcc", "tcp"):
+        f = os.path.join(src, "pmc_" + p, "run_counter_collection.csv")
+        if os.path.exists(f):
+            for c in counters(f):
+                for k, v in per_kernel(f, c).items():
+                    extra.setdefault(k, {})[c] = round(v, 1)
     out = {}
     for k in dur:
         if k.startswith("void rocprim") or k.startswith("__amd"):
@@ -56,6 +72,8 @@ def main(src, dst, sizes=()):
             out[k]["hbm_write_bytes"] = int(w * 1024)
         if f is not None and w is not None:
             out[k]["traffic_bytes"] = out[k]["hbm_read_bytes"] + out[k]["hbm_write_bytes"]
+        if k in extra:
+            out[k]["counters"] = extra[k]
         if k in sizes:
             out[k]["bytes_per_launch"] = int(sizes[k])
             if "traffic_bytes" in out[k]:

@@ -14,8 +14,7 @@ ROOT = os.path.dirname(HERE)
 CSRC = os.path.join(HERE, "csrc")
 LIB = os.path.join(HERE, "libsydelta.so")
 SOURCES = ["sydelta_kernels.hip", "sydelta_api.cpp", "sydelta_wire.cpp", "sydelta_local.cpp", "sydelta_integrity.cpp"]
-HEADERS = ["sydelta_device.hpp", "sydelta_internal.hpp", "sydelta_host.hpp", "sydelta_walk.hpp",
-           os.path.join("..", "..", "include", "sydelta.h")]
+HEADERS = sorted(f for f in os.listdir(CSRC) if f.endswith(".hpp")) + [os.path.join("..", "..", "include", "sydelta.h")]
 # objects stay in build/obj (the host sanitizer test links sydelta_kernels.o)
 OBJDIR = os.path.join(ROOT, "build", "obj")
 ARCH = os.environ.get("SYDELTA_ARCH", "gfx950")

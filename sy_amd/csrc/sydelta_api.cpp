@@ -68,6 +68,8 @@ struct DevState {
 };
 std::mutex g_dev_mu;
 std::map<int, std::unique_ptr<DevState>> g_devs;
+constexpr int kMaxPoolDevices = 64;
+hipMemPool_t g_pools[kMaxPoolDevices] = {};  // written once per device under its call_once
 
 int ensure_device_impl(int device) {
     if (device < 0) device = 0;
@@ -96,16 +98,30 @@ int ensure_device_impl(int device) {
             return;
         }
         // Scratch (index arrays, hit lists, probe jobs, streamed chunks) comes from the
-        // device's stream-ordered pool.  Its default release threshold is 0: every stream
-        // synchronization hands the freed memory back and the next call maps it again.
-        // Keep up to SYDELTA_POOL_KEEP_MIB (default 4 GiB) reserved across calls.
-        hipMemPool_t pool = nullptr;
-        if (hipDeviceGetDefaultMemPool(&pool, device) == hipSuccess && pool) {
-            uint64_t keep = 4096;
-            if (const char* e = getenv("SYDELTA_POOL_KEEP_MIB")) keep = strtoull(e, nullptr, 10);
-            keep <<= 20;
-            (void)hipMemPoolSetAttribute(pool, hipMemPoolAttrReleaseThreshold, &keep);
+        // library's own stream-ordered pool on this device (never the device's default
+        // pool, which other libraries in the process share).  A pool's default release
+        // threshold is 0: every stream synchronization hands the freed memory back and the
+        // next call maps it again, so keep up to SYDELTA_POOL_KEEP_MIB (default 4 GiB)
+        // reserved across calls -- for this library's scratch only.
+        if (device >= kMaxPoolDevices) {
+            st->msg = "device index " + std::to_string(device) + " above the library's limit";
+            return;
         }
+        hipMemPoolProps props{};
+        props.allocType = hipMemAllocationTypePinned;
+        props.handleTypes = hipMemHandleTypeNone;
+        props.location.type = hipMemLocationTypeDevice;
+        props.location.id = device;
+        hipMemPool_t pool = nullptr;
+        if (hipMemPoolCreate(&pool, &props) != hipSuccess || !pool) {
+            st->msg = "hipMemPoolCreate failed on device " + std::to_string(device);
+            return;
+        }
+        uint64_t keep = 4096;
+        if (const char* e = getenv("SYDELTA_POOL_KEEP_MIB")) keep = strtoull(e, nullptr, 10);
+        keep <<= 20;
+        (void)hipMemPoolSetAttribute(pool, hipMemPoolAttrReleaseThreshold, &keep);
+        g_pools[device] = pool;
         st->status = SYDELTA_OK;
     });
     if (st->status != SYDELTA_OK) return fail(st->status, "%s", st->msg.c_str());
@@ -135,6 +151,14 @@ std::map<std::string, std::pair<double, uint64_t>> g_prof;
 }  // namespace
 
 int sydelta::ensure_device(int device) { return ensure_device_impl(device); }
+hipError_t sydelta::dev_malloc_async(void** p, size_t bytes, hipStream_t s) {
+    int d = 0;
+    hipError_t e = hipGetDevice(&d);
+    if (e != hipSuccess) return e;
+    // every entry point runs ensure_device (which sets the device) before allocating
+    if (d < 0 || d >= kMaxPoolDevices || !g_pools[d]) return hipErrorInvalidDevice;
+    return hipMallocFromPoolAsync(p, bytes, g_pools[d], s);
+}
 int sydelta::host_exception() {
     try {
         throw;
@@ -332,7 +356,7 @@ extern "C" int sydelta_signature_batch_device(int device, const uint8_t* d_buf, 
         const uint64_t nact = aoff.size(), npart = loff.size();
         for (auto* v : {&aoff, &agb, &apfx, &loff, &llen, &lidx}) t.insert(t.end(), v->begin(), v->end());
         uint64_t* d_t = nullptr;
-        HIP_TRY(hipMallocAsync((void**)&d_t, 8 * t.size(), s));
+        HIP_TRY(dev_malloc_async((void**)&d_t, 8 * t.size(), s));
         HIP_TRY(hipMemcpyAsync(d_t, t.data(), 8 * t.size(), hipMemcpyHostToDevice, s));
         const uint64_t* p = d_t;
         const uint64_t* d_aoff = p; p += nact;
@@ -350,7 +374,7 @@ extern "C" int sydelta_signature_batch_device(int device, const uint8_t* d_buf, 
         return SYDELTA_OK;
     }
     uint64_t* d_meta = nullptr;
-    HIP_TRY(hipMallocAsync((void**)&d_meta, sizeof(uint64_t) * (3 * nfiles + 1), s));
+    HIP_TRY(dev_malloc_async((void**)&d_meta, sizeof(uint64_t) * (3 * nfiles + 1), s));
     HIP_TRY(hipMemcpyAsync(d_meta, off, 8 * nfiles, hipMemcpyHostToDevice, s));
     HIP_TRY(hipMemcpyAsync(d_meta + nfiles, len, 8 * nfiles, hipMemcpyHostToDevice, s));
     HIP_TRY(hipMemcpyAsync(d_meta + 2 * nfiles, fblk.data(), 8 * (nfiles + 1), hipMemcpyHostToDevice, s));
@@ -463,7 +487,7 @@ static int index_create_impl(int device, const uint32_t* weak, const uint64_t* s
     const size_t sz_fat = want_l1 ? al(16 * (size_t)sl) : 0;
     const size_t total = sz_weak + sz_strong + sz_filt + sz_l1 + sz_fat + 4 * sz_t + sz_order + sz_slot + sz_files +
                          sz_fblk + sz_cstrong;
-    HIP_TRY(hipMallocAsync(&x->d_pool, total, s));  // stream-ordered: no device-wide synchronization
+    HIP_TRY(dev_malloc_async(&x->d_pool, total, s));  // stream-ordered: no device-wide synchronization
     uint8_t* p = (uint8_t*)x->d_pool;
     x->d_weak = (uint32_t*)p; p += sz_weak;
     x->d_strong = (uint64_t*)p; p += sz_strong;
@@ -790,7 +814,7 @@ int Classifier::probe(int mode) {
         if (jb.p) { (void)hipFreeAsync(jb.p, s); jb.p = nullptr; }
         const size_t jbytes = (jobs.size() * sizeof(ProbeJob) + 255) & ~(size_t)255;
         const size_t obytes = (np * 4 + 255) & ~(size_t)255;
-        HIP_TRY(hipMallocAsync(&jb.p, jbytes + 2 * obytes + np * 8, s));
+        HIP_TRY(dev_malloc_async(&jb.p, jbytes + 2 * obytes + np * 8, s));
         jb.s = s;
         uint32_t* d_out = (uint32_t*)((uint8_t*)jb.p + jbytes);
         if (stride == 1) d_probe_out = d_out;
@@ -922,17 +946,17 @@ int Classifier::scan(const std::vector<std::array<uint64_t, 3>>& ranges) {
     if (wide && ix->nfiles != 1) return fail(SYDELTA_E_INVAL, "batched match needs block_size <= %u", scan_max_window());
     unsigned long long* d_counts = nullptr;
     DevBuf cnt_buf;
-    HIP_TRY(hipMallocAsync((void**)&d_counts, 128, s));
+    HIP_TRY(dev_malloc_async((void**)&d_counts, 128, s));
     cnt_buf.p = d_counts;
     cnt_buf.s = s;
     DevBuf seg_buf;
     if (!wide) {
-        HIP_TRY(hipMallocAsync(&seg_buf.p, segs.size() * sizeof(ScanSeg), s));
+        HIP_TRY(dev_malloc_async(&seg_buf.p, segs.size() * sizeof(ScanSeg), s));
         seg_buf.s = s;
         HIP_TRY(hipMemcpyAsync(seg_buf.p, segs.data(), segs.size() * sizeof(ScanSeg), hipMemcpyHostToDevice, s));
         if (!q_buf.p) {
             qcap = scan_queue_entries();
-            HIP_TRY(hipMallocAsync(&q_buf.p, qcap * sizeof(uint2), s));
+            HIP_TRY(dev_malloc_async(&q_buf.p, qcap * sizeof(uint2), s));
             q_buf.s = s;
         }
     }
@@ -946,7 +970,7 @@ int Classifier::scan(const std::vector<std::array<uint64_t, 3>>& ranges) {
             if (hit_buf.p) { (void)hipFreeAsync(hit_buf.p, s); hit_buf.p = nullptr; }
             cap = want;
             // keys [cap] + key scratch [cap] + values [cap] + value scratch [cap]
-            HIP_TRY(hipMallocAsync(&hit_buf.p, cap * 24, s));
+            HIP_TRY(dev_malloc_async(&hit_buf.p, cap * 24, s));
             hit_buf.s = s;
         }
         uint64_t* d_key = (uint64_t*)hit_buf.p;
@@ -1145,7 +1169,7 @@ int Classifier::phase_probe(const std::vector<std::array<uint64_t, 4>>& jobs,
     DevBuf jb;
     const size_t jbytes = (pj.size() * sizeof(ProbeJob) + 255) & ~(size_t)255;
     const size_t obytes = (np * 4 + 255) & ~(size_t)255;
-    HIP_TRY(hipMallocAsync(&jb.p, jbytes + 2 * obytes + np * 8, s));
+    HIP_TRY(dev_malloc_async(&jb.p, jbytes + 2 * obytes + np * 8, s));
     jb.s = s;
     uint32_t* d_out = (uint32_t*)((uint8_t*)jb.p + jbytes);
     uint32_t* d_pw = (uint32_t*)((uint8_t*)jb.p + jbytes + obytes);
@@ -1321,7 +1345,7 @@ int Classifier::walk_device(size_t i, uint64_t entry, const BasisInfo& bi, bool 
     const uint64_t o_cnt = o_on + al(W), o_off = o_cnt + al(4 * (M + 1)), o_ops = o_off + al(4 * (M + 1));
     const uint64_t o_res = o_ops + al(sizeof(sydelta_op) * 2 * M), total = o_res + al(sizeof(chain::ChainResult));
     DevBuf buf;
-    HIP_TRY(hipMallocAsync(&buf.p, total, s));
+    HIP_TRY(dev_malloc_async(&buf.p, total, s));
     buf.s = s;
     uint8_t* B = (uint8_t*)buf.p;
     chain::ChainArgs a{};
@@ -1447,7 +1471,7 @@ int tail_flags(Classifier& C, const std::vector<size_t>& which, std::vector<int>
     std::vector<int> tf(tails.size(), 0);
     DevBuf tail_buf;
     const size_t bytes = (tails.size() * sizeof(TailJob) + 15) & ~(size_t)15;
-    HIP_TRY(hipMallocAsync(&tail_buf.p, bytes + tails.size() * sizeof(int), C.s));
+    HIP_TRY(dev_malloc_async(&tail_buf.p, bytes + tails.size() * sizeof(int), C.s));
     tail_buf.s = C.s;
     int* d_flag = (int*)((uint8_t*)tail_buf.p + bytes);
     HIP_TRY(hipMemcpyAsync(tail_buf.p, tails.data(), tails.size() * sizeof(TailJob), hipMemcpyHostToDevice, C.s));
@@ -1615,10 +1639,10 @@ extern "C" int sydelta_compute_checksums_buf(int device, const uint8_t* buf, uin
     if (device < 0) device = 0;
     hipStream_t s = thread_stream(device);
     uint8_t* d_buf = nullptr;
-    HIP_TRY(hipMallocAsync((void**)&d_buf, (len + 15) & ~15ull, s));
+    HIP_TRY(dev_malloc_async((void**)&d_buf, (len + 15) & ~15ull, s));
     DevBuf b1; b1.p = d_buf; b1.s = s;
     uint32_t* d_w = nullptr;
-    HIP_TRY(hipMallocAsync((void**)&d_w, nb * 12 + 16, s));
+    HIP_TRY(dev_malloc_async((void**)&d_w, nb * 12 + 16, s));
     DevBuf b2; b2.p = d_w; b2.s = s;
     uint64_t* d_st = (uint64_t*)(((uintptr_t)(d_w + nb) + 7) & ~(uintptr_t)7);
     HIP_TRY(hipMemcpyAsync(d_buf, buf, len, hipMemcpyHostToDevice, s));
@@ -1680,7 +1704,7 @@ static int generate_from_host(int device, const uint8_t* src, uint64_t len, cons
     uint8_t* d_src = nullptr;
     DevBuf b;
     if (len) {
-        HIP_TRY(hipMallocAsync((void**)&d_src, (len + 15) & ~15ull, s));
+        HIP_TRY(dev_malloc_async((void**)&d_src, (len + 15) & ~15ull, s));
         b.p = d_src; b.s = s;
         HIP_TRY(hipMemcpyAsync(d_src, src, len, hipMemcpyHostToDevice, s));
     }
@@ -1850,9 +1874,9 @@ extern "C" int sydelta_compute_checksums(const char* path, uint64_t block_size, 
     PinnedPair& pin = t_stream_pinned;
     if (int r = pin.ensure(C + 16)) return r;
     DevBuf db, dw;
-    HIP_TRY(hipMallocAsync(&db.p, C + 16, s));
+    HIP_TRY(dev_malloc_async(&db.p, C + 16, s));
     db.s = s;
-    HIP_TRY(hipMallocAsync(&dw.p, nb * 12 + 16, s));
+    HIP_TRY(dev_malloc_async(&dw.p, nb * 12 + 16, s));
     dw.s = s;
     uint32_t* d_w = (uint32_t*)dw.p;
     uint64_t* d_st = (uint64_t*)(((uintptr_t)(d_w + nb) + 7) & ~(uintptr_t)7);
@@ -1951,7 +1975,7 @@ extern "C" int sydelta_generate_delta_streaming(const char* source_path, const s
     PinnedPair& pin = t_stream_pinned;
     if (int r = pin.ensure(cap + 16)) return r;
     DevBuf db;
-    HIP_TRY(hipMallocAsync(&db.p, cap + 16, s));
+    HIP_TRY(dev_malloc_async(&db.p, cap + 16, s));
     db.s = s;
     std::unique_ptr<sydelta_delta> d(new sydelta_delta());
     d->source_size = L;
@@ -2099,7 +2123,7 @@ extern "C" int sydelta_apply_delta_device(int device, const uint8_t* d_basis, ui
                 if (armed) { (void)hipStreamSynchronize(a); (void)hipStreamSynchronize(b); }
             }
         } drain{cstream, s};
-        HIP_TRY(hipMallocAsync(&pb.p, need * sizeof(ApplyPiece), s));
+        HIP_TRY(dev_malloc_async(&pb.p, need * sizeof(ApplyPiece), s));
         pb.s = s;
         HIP_TRY(hipEventRecord(ev[0], s));  // the table allocation is ordered before the uploads
         HIP_TRY(hipStreamWaitEvent(cstream, ev[0], 0));

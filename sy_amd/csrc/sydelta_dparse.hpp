@@ -94,6 +94,9 @@ __host__ __device__ inline uint64_t chunk_parse(const DArgs& a, uint64_t c, cons
     const uint8_t* t = a.t;
     const uint64_t len = a.e;  // no token of R reads past its ']'
     uint64_t ork = orank[c], lrk = lrank[c];
+    // The chain starts at the first op: a non-empty region must open with one, or the
+    // bytes before the first "},{" would be checked by no thread.
+    if (c == 0 && a.e > kHead && !op_start(t, kHead)) return kHead;
     for (uint64_t p = chunk_lo(a, c); p < chunk_hi(a, c); ++p) {
         if (op_start(t, p)) {
             uint64_t q = p, o = 0, sz = 0;

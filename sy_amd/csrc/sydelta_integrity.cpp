@@ -45,7 +45,7 @@ extern "C" int sydelta_xxh3_batch_device(int device, const uint8_t* d_buf, uint6
     const uint64_t tab = nfiles * 8 * 3 + (nfiles + 1) * 8 + nact * 8 + (nact + 1) * 8 + nfiles * 4;
     const uint64_t bytes = (tab + 255) / 256 * 256 + xxh_chain_records(npieces) * 64;
     void* ws = nullptr;
-    HIP_TRY(hipMallocAsync(&ws, bytes, s));
+    HIP_TRY(dev_malloc_async(&ws, bytes, s));
     struct Free {
         void* p;
         hipStream_t s;

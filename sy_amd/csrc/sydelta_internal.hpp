@@ -14,6 +14,12 @@
 
 namespace sydelta {
 
+// Stream-ordered device scratch from the library's own memory pool (one per device,
+// created by ensure_device), so its release threshold never touches the device's
+// default pool that torch or other libraries in the process may use.  Freed with
+// hipFreeAsync like any pool allocation.
+hipError_t dev_malloc_async(void** p, size_t bytes, hipStream_t s);
+
 constexpr uint32_t kEmptyKey = 0xFFFFFFFFu;  // never a valid weak: A = weak & 0xFFFF <= 65520
 constexpr uint64_t kLdsFilterKeys = 16384;   // index sizes whose Bloom filter (<= 32 KiB) the scan keeps in LDS
 constexpr uint32_t kLdsFilterWordsMax = 8192;

@@ -2619,7 +2619,9 @@ __global__ __launch_bounds__(kZT) void k_zstd_block(const uint8_t* __restrict__ 
         if (zstd::lz_worth(L.state[5], n)) {
             if (tid == 0) {
                 const uint32_t z = zstd::lz_content(in, n, L.cand, sc, L.hist[1], L.code, L.work);
-                L.state[6] = (z && z < L.state[3]) ? z : 0u;
+                // z < n keeps the copy inside this block's slot (the body may reach 2n + 64
+                // when no entropy-only content was possible), as block_content_seq does
+                L.state[6] = (z && z < L.state[3] && z < n) ? z : 0u;
             }
             __syncthreads();
             const uint32_t z = L.state[6];
@@ -3373,7 +3375,7 @@ hipError_t launch_index_build(const uint32_t* d_weak, const uint64_t* d_strong, 
     size_t tmp = 0;
     if ((e = hipcub::DeviceScan::ExclusiveSum(nullptr, tmp, ix.cnt, ix.start, (int)ix.nslots, s))) return e;
     void* d_tmp = nullptr;
-    if ((e = hipMallocAsync(&d_tmp, tmp ? tmp : 16, s))) return e;
+    if ((e = dev_malloc_async(&d_tmp, tmp ? tmp : 16, s))) return e;
     e = hipcub::DeviceScan::ExclusiveSum(d_tmp, tmp, ix.cnt, ix.start, (int)ix.nslots, s);
     (void)hipFreeAsync(d_tmp, s);
     if (e) return e;
@@ -3391,7 +3393,7 @@ hipError_t launch_index_build(const uint32_t* d_weak, const uint64_t* d_strong, 
                                                     end_bit, s)))
             return e;
         void* d_t2 = nullptr;
-        if ((e = hipMallocAsync(&d_t2, tmp2 ? tmp2 : 16, s))) return e;
+        if ((e = dev_malloc_async(&d_t2, tmp2 ? tmp2 : 16, s))) return e;
         e = hipcub::DeviceRadixSort::SortPairs(d_t2, tmp2, ix.slot_of, keys_out, iota, ix.order, (int)n, 0, end_bit,
                                                s);
         (void)hipFreeAsync(d_t2, s);
@@ -3607,7 +3609,7 @@ hipError_t launch_sort_hits(uint64_t* key, uint32_t* val, uint64_t* key_tmp, uin
     if ((e = hipcub::DeviceRadixSort::SortPairs(nullptr, tmp, key, key_tmp, val, val_tmp, (int)nhits, 0, end_bit, s)))
         return e;
     void* d_t = nullptr;
-    if ((e = hipMallocAsync(&d_t, tmp ? tmp : 16, s))) return e;
+    if ((e = dev_malloc_async(&d_t, tmp ? tmp : 16, s))) return e;
     e = hipcub::DeviceRadixSort::SortPairs(d_t, tmp, key, key_tmp, val, val_tmp, (int)nhits, 0, end_bit, s);
     (void)hipFreeAsync(d_t, s);
     *key_out = key_tmp;
@@ -3643,7 +3645,7 @@ static hipError_t exclusive_sum_u32(const uint32_t* d_in, uint32_t* d_out, uint6
     hipError_t e;
     if ((e = hipcub::DeviceScan::ExclusiveSum(nullptr, tmp, d_in, d_out, (int)n, s))) return e;
     void* d_t = nullptr;
-    if ((e = hipMallocAsync(&d_t, tmp ? tmp : 16, s))) return e;
+    if ((e = dev_malloc_async(&d_t, tmp ? tmp : 16, s))) return e;
     e = hipcub::DeviceScan::ExclusiveSum(d_t, tmp, d_in, d_out, (int)n, s);
     (void)hipFreeAsync(d_t, s);
     return e;
@@ -3795,7 +3797,7 @@ hipError_t launch_exclusive_sum_u64(const uint64_t* d_in, uint64_t* d_out, uint6
     hipError_t e;
     if ((e = hipcub::DeviceScan::ExclusiveSum(nullptr, tmp, d_in, d_out, (int)n, s))) return e;
     void* d_t = nullptr;
-    if ((e = hipMallocAsync(&d_t, tmp ? tmp : 16, s))) return e;
+    if ((e = dev_malloc_async(&d_t, tmp ? tmp : 16, s))) return e;
     e = hipcub::DeviceScan::ExclusiveSum(d_t, tmp, d_in, d_out, (int)n, s);
     (void)hipFreeAsync(d_t, s);
     return e;

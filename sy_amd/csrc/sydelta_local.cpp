@@ -98,7 +98,7 @@ extern "C" int sydelta_estimate_change_ratio_device(int device, const uint8_t* d
     if (int r = ensure_device(device)) return r;
     hipStream_t s = stream ? (hipStream_t)stream : thread_stream(device < 0 ? 0 : device);
     DevMem m;
-    HIP_TRY(hipMallocAsync(&m.p, want * 8 * 3, s));
+    HIP_TRY(dev_malloc_async(&m.p, want * 8 * 3, s));
     m.s = s;
     uint64_t* d_pos = (uint64_t*)m.p;
     uint64_t* d_hs = d_pos + want;
@@ -183,7 +183,7 @@ extern "C" int sydelta_estimate_change_ratio(const char* source_path, const char
     const uint64_t per = std::max<uint64_t>(1, std::min<uint64_t>(want, (64ull << 20) / block_size));
     std::vector<uint8_t> host(2 * per * block_size);
     DevMem m;
-    HIP_TRY(hipMallocAsync(&m.p, host.size(), s));
+    HIP_TRY(dev_malloc_async(&m.p, host.size(), s));
     m.s = s;
     uint64_t changed = 0;
     std::vector<uint64_t> offs, lens, hash;

@@ -486,7 +486,7 @@ extern "C" int sydelta_delta_to_json_device(const sydelta_delta* d, const uint8_
     if (np) {
         const size_t pb = (np * sizeof(JsonPiece) + 255) & ~(size_t)255;
         const size_t lb = (np * 8 + 255) & ~(size_t)255;
-        HIP_TRY(hipMallocAsync(&buf.p, pb + lb + np * 8, s));
+        HIP_TRY(dev_malloc_async(&buf.p, pb + lb + np * 8, s));
         buf.s = s;
         JsonPiece* d_pieces = (JsonPiece*)buf.p;
         uint64_t* d_len = (uint64_t*)((uint8_t*)buf.p + pb);
@@ -559,7 +559,7 @@ extern "C" int sydelta_checksums_to_json_device(const uint32_t* d_weak, const ui
     const uint64_t nt = (n + sigjson::kTile - 1) / sigjson::kTile;
     CallProf cp;
     DevBuf_wire buf;
-    HIP_TRY(hipMallocAsync(&buf.p, 2 * nt * 8, s));
+    HIP_TRY(dev_malloc_async(&buf.p, 2 * nt * 8, s));
     buf.s = s;
     uint64_t* d_tlen = (uint64_t*)buf.p;
     uint64_t* d_toff = d_tlen + nt;
@@ -601,7 +601,7 @@ extern "C" int sydelta_checksums_from_json_device(const uint8_t* d_text, uint64_
     const uint64_t nc = (len + sigjson::kParseChunk - 1) / sigjson::kParseChunk;
     CallProf cp;
     DevBuf_wire buf;
-    HIP_TRY(hipMallocAsync(&buf.p, 2 * nc * 8 + 8, s));
+    HIP_TRY(dev_malloc_async(&buf.p, 2 * nc * 8 + 8, s));
     buf.s = s;
     uint64_t* d_cnt = (uint64_t*)buf.p;
     uint64_t* d_rank = d_cnt + nc;
@@ -690,7 +690,7 @@ extern "C" int sydelta_delta_from_json_device(const uint8_t* d_text, uint64_t le
     CallProf cp;
     DevBuf_wire buf;
     const uint64_t nc = a.nc;
-    HIP_TRY(hipMallocAsync(&buf.p, (4 * (nc + 1) + 1) * 8, s));
+    HIP_TRY(dev_malloc_async(&buf.p, (4 * (nc + 1) + 1) * 8, s));
     buf.s = s;
     uint64_t* d_ocnt = (uint64_t*)buf.p;
     uint64_t* d_lcnt = d_ocnt + nc + 1;
@@ -717,7 +717,7 @@ extern "C" int sydelta_delta_from_json_device(const uint8_t* d_text, uint64_t le
     d->block_size = blk;
     if (nops) {
         DevBuf_wire ob;
-        HIP_TRY(hipMallocAsync(&ob.p, nops * (8 + sizeof(sydelta_op)), s));
+        HIP_TRY(dev_malloc_async(&ob.p, nops * (8 + sizeof(sydelta_op)), s));
         ob.s = s;
         uint64_t* d_pos = (uint64_t*)ob.p;
         sydelta_op* d_ops = (sydelta_op*)(d_pos + nops);
@@ -780,7 +780,7 @@ extern "C" int sydelta_zstd_compress_device(int device, const uint8_t* d_in, uin
     const uint64_t o_type = o_size + al(4 * nb_max);
     const uint64_t o_len = o_type + al(4 * nb_max), o_off = o_len + al(8 * nb_max), total = o_off + al(8 * nb_max);
     DevBuf_wire buf;
-    HIP_TRY(hipMallocAsync(&buf.p, total, s));
+    HIP_TRY(dev_malloc_async(&buf.p, total, s));
     buf.s = s;
     uint8_t* B = (uint8_t*)buf.p;
     uint8_t* d_lz = B + o_lz;

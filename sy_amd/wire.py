@@ -156,7 +156,7 @@ def delta_from_json_device(d_text, stream=None):
         lib.sydelta_delta_free(h)
 
 
-def zstd_compress_device(d_text, stream=None, device: int = 0):
+def zstd_compress_device(d_text, stream=None, device: int | None = None):
     """zstd frame (Huffman literals, FSE-coded sequences) of the bytes of a uint8 device tensor, as a uint8
     device tensor: the compression ssh.rs:1009-1017 applies to the Delta JSON.  The
     tensor must start 16-byte aligned (torch allocations and views at offset 0 do)."""
@@ -164,6 +164,8 @@ def zstd_compress_device(d_text, stream=None, device: int = 0):
 
     from .device import _ptr, _stream
 
+    if device is None:
+        device = d_text.device.index or 0
     n = d_text.numel()
     out = torch.empty(int(lib.sydelta_zstd_bound(n)) + 16, dtype=torch.uint8, device=d_text.device)
     got = ctypes.c_uint64()

@@ -343,7 +343,11 @@ def dparse_checks():
            good.replace(b"[1,255]", b"[1,255,]"), good.replace(b"[1,255]", b"[-1,255]"), good.replace(b"},{", b"}{", 1),
            good.replace(b'"source_size":8192', b'"source_size":08192'), good.replace(b'"block_size":4096}', b'"block_size":4096,"x":1}'),
            good.replace(b'{"Data":[]}', b'{"Data":[],"x":0}'), good.replace(b'{"ops":[', b'{"ops" :['),
-           good.replace(b"]}]", b"]}}]"), good.replace(b'{"Copy":{"offset":4096,"size":4096}}', b'{"Copy":{"offset":4096,"size":4096},"x":1}')]
+           good.replace(b"]}]", b"]}}]"), good.replace(b'{"Copy":{"offset":4096,"size":4096}}', b'{"Copy":{"offset":4096,"size":4096},"x":1}'),
+           # junk before the first op (the chain must start at byte 8: ADVICE r02)
+           b'{"ops":[xyz},{"Data":[5]}],"source_size":1,"block_size":1}',
+           b'{"ops":[1},{"Copy":{"offset":0,"size":1}}],"source_size":1,"block_size":1}',
+           good.replace(b'{"ops":[{', b'{"ops":[ {', 1)]
     for t in bad:
         assert dev_parse(t) is None, t
         n_checks += 1

@@ -116,6 +116,15 @@ hipError_t hipDeviceGetDefaultMemPool(hipMemPool_t* p, int d) {
     return hipSuccess;
 }
 hipError_t hipMemPoolSetAttribute(hipMemPool_t, hipMemPoolAttr, void*) { return hipSuccess; }
+hipError_t hipMemPoolCreate(hipMemPool_t* p, const hipMemPoolProps* props) {
+    if (!props || props->location.id != 0) return hipErrorInvalidDevice;
+    *p = (hipMemPool_t)&emu_pool_tag;
+    return hipSuccess;
+}
+hipError_t hipMallocFromPoolAsync(void** p, size_t n, hipMemPool_t pool, hipStream_t s) {
+    if (pool != (hipMemPool_t)&emu_pool_tag) return hipErrorInvalidValue;
+    return hipMallocAsync(p, n, s);
+}
 hipError_t hipFreeAsync(void* p, hipStream_t) {
     emu_free(p);
     return hipSuccess;

@@ -573,8 +573,18 @@ static void dparse_case(std::mt19937_64& rng, uint64_t* accepted, uint64_t* refu
     for (size_t i = 0; i < v.size(); ++i)
         CHECK(back[i].copy == v[i].copy && (v[i].copy ? back[i].o == v[i].o && back[i].s == v[i].s : back[i].lit == v[i].lit));
     static const char alpha[] = "0123456789{}[],:\"aDC -";
-    for (int m = 0; m < 20; ++m) {
+    for (int m = 0; m < 24; ++m) {
         std::string t = text;
+        if (m >= 20 && !v.empty()) {
+            // junk before the first op, ending in "}," so an op start follows it
+            std::string junk = "},";
+            for (int j = (int)(rng() % 4); j > 0; --j) junk.insert(junk.begin(), alpha[rng() % (sizeof alpha - 1)]);
+            t.insert(8, junk);
+            std::vector<DOp> got;
+            CHECK(!dparse_all(t, got));
+            ++*refused;
+            continue;
+        }
         for (int j = 0, k = 1 + (int)(rng() % 3); j < k; ++j) {
             const int op = (int)(rng() % 3);
             const size_t at = rng() % t.size();

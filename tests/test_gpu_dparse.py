@@ -100,6 +100,7 @@ def test_delta_json_refused_spellings(gpu):
 
     good = _compact([("C", 4096, 4096), ("D", b"\x01\xff"), ("D", b"")], 8192, 4096)
     for bad in (good.replace(b",", b", ", 1), good[:-1], good.replace(b"[1,255]", b"[01,255]"),
-                good.replace(b"[1,255]", b"[1,256]"), good.replace(b'"Copy"', b'"copy"')):
+                good.replace(b"[1,255]", b"[1,256]"), good.replace(b'"Copy"', b'"copy"'),
+                b'{"ops":[xyz},{"Data":[5]}],"source_size":1,"block_size":1}'):
         with pytest.raises(SyDeltaError, match="compact form at byte"):
             wire.delta_from_json_device(torch.frombuffer(bytearray(bad), dtype=torch.uint8).cuda())
