@@ -491,11 +491,28 @@ def pmc_traffic(kernel: str, per_launch: int):
     return int(best) if best else None
 
 
+def pmc_counters(kernel: str):
+    """Raw per-launch counters (TCC/TCP request counts) of `kernel` from the newest
+    profiles/*_pmc.json that has them, with that launch's algorithmic bytes."""
+    import glob
+
+    best = None
+    for f in sorted(glob.glob(os.path.join(ROOT, "profiles", "r*_pmc.json"))):
+        try:
+            d = json.load(open(f))
+        except Exception:
+            continue
+        v = d.get("kernels", {}).get(kernel)
+        if v and v.get("counters") and v.get("bytes_per_launch"):
+            best = dict(v["counters"], bytes_per_launch=v["bytes_per_launch"], source=os.path.basename(f))
+    return best
+
+
 def algo_bytes_per_step(workload: str, n: int, nb_bytes: int, src_bytes: int) -> dict:
     """Algorithmic HBM bytes per step of each kernel that can dominate a workload.  Per
     step the signature kernels read the basis once and the scan reads the source once
     (SURVEY.md section 8(d))."""
-    return {"k_scan": src_bytes, "k_scan_lds": src_bytes, "k_scan_l1": src_bytes, "k_scan_l1w": src_bytes,
+    return {"k_scan": src_bytes, "k_scan_lds": src_bytes, "k_scan_l1": src_bytes,
             "k_sig_fast": nb_bytes if workload in ("c3", "c3b") else n,
             "k_sig_batch": n, "k_sig_wave": n, "k_probe": src_bytes,
             "k_apply": 2 * n,  # apply: every output byte read once and written once
@@ -534,7 +551,9 @@ def roofline(prof: dict, steps: int, algo_step: dict, positions=None, keys=None)
     roof = {"bound": "hbm", "achieved": round(ach, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
             "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": pmc_traffic(dom, per_launch),
             "kernel": dom, "avg_launch_ms": round(avg_ms, 4), "algorithmic_bytes_per_launch": per_launch}
-    l1_bits = {"k_scan_l1": 1 << 20, "k_scan_l1w": 28672 * 32}  # level-1 filter bits (one hash)
+    # level-1 filter bits (one hash) per key: with P key partitions (SYDELTA_SCAN_L1=2) the
+    # scan is launched once per partition and each launch's filter holds 1/P of the keys
+    l1_bits = {"k_scan_l1": (1 << 20) * max(1, round(launches_per_step))}
     if positions and (dom in ("k_scan_lds", "k_scan") or (dom in l1_bits and keys)):
         per_pos = 1.0 if dom not in l1_bits else 1.0 - math.exp(-keys / float(l1_bits[dom]))
         req = positions * per_pos / launches_per_step  # filter-word requests per launch
@@ -545,6 +564,17 @@ def roofline(prof: dict, steps: int, algo_step: dict, positions=None, keys=None)
                              "requests_per_position": round(per_pos, 4),
                              "model": ("one per window start" if dom not in l1_bits else
                                        f"window starts x level-1 pass rate 1-exp(-keys/{l1_bits[dom]})")}
+        pc = pmc_counters(dom)
+        if pc and pc.get("TCC_REQ_sum"):
+            # measured: every L2 request of the launch (filter words, staged bytes, table
+            # lookups) per scanned byte, from the rocprofv3 TCC pass of the same command
+            rq = pc["TCC_REQ_sum"] / pc["bytes_per_launch"]
+            roof["l2_gather"]["measured"] = {
+                "tcc_requests_per_position": round(rq, 4),
+                "tcc_hit_rate": round(pc["TCC_HIT_sum"] / max(1.0, pc["TCC_HIT_sum"] + pc["TCC_MISS_sum"]), 4),
+                "tcc_requests_per_s_G": round(rq * per_launch / (avg_ms * 1e-3) / 1e9, 2),
+                "frac": round(rq * per_launch / (avg_ms * 1e-3) / L2_GATHER_PEAK, 4),
+                "source": "profiles/" + pc["source"]}
     return roof
 
 

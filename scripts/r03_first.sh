@@ -30,4 +30,7 @@ pmc tcc TCC_REQ_sum TCC_HIT_sum TCC_MISS_sum || exit 1
 pmc tcp TCP_TCC_READ_REQ_sum TCP_TOTAL_CACHE_ACCESSES_sum || exit 1
 cd "$R"
 python3 scripts/pmc_summary.py "$OUT" "$OUT/c3" k_scan_l1=4294967296 k_sig_fast=4294967296 > "$OUT/pmc_summary.txt" 2>&1; cat "$OUT/pmc_summary.txt"
+step 300 env SYDELTA_SCAN_L1=2 python3 bench.py --no-cpu-baseline --no-host-inclusive --steps 10 --warmup 3 \
+  > "$OUT/bench_c3_p2.json" 2> "$OUT/bench_c3_p2.err" || { tail -20 "$OUT/bench_c3_p2.err"; exit 1; }
+tail -c 1500 "$OUT/bench_c3_p2.json"; echo
 echo "== done"

@@ -482,8 +482,8 @@ static int index_create_impl(int device, const uint32_t* weak, const uint64_t* s
     const size_t sz_fblk = al(8 * (nfiles + 1)), sz_cstrong = al(8 * nb);
     // level-1 filter for k_scan_l1: one large file (the BASELINE C3 shape)
     const bool want_l1 = nfiles == 1 && nblocks > kLdsFilterKeys && block_size == 4096;  // k_scan_l1's scope
-    const uint32_t l1_words = want_l1 ? (scan_l1_mode() == 2 ? kL1WordsW : kL1Words) : 0;
-    const size_t sz_l1 = al(4 * (size_t)l1_words);
+    const uint32_t l1_parts = want_l1 ? (scan_l1_mode() == 2 ? 2u : 1u) : 0u;
+    const size_t sz_l1 = al(4 * (size_t)l1_parts * kL1Words);
     const size_t sz_fat = want_l1 ? al(16 * (size_t)sl) : 0;
     const size_t total = sz_weak + sz_strong + sz_filt + sz_l1 + sz_fat + 4 * sz_t + sz_order + sz_slot + sz_files +
                          sz_fblk + sz_cstrong;
@@ -494,7 +494,7 @@ static int index_create_impl(int device, const uint32_t* weak, const uint64_t* s
     ix.filt = (uint32_t*)p; p += sz_filt;
     if (want_l1) {
         ix.l1 = (uint32_t*)p; p += sz_l1;
-        ix.l1_words = l1_words;
+        ix.l1_parts = l1_parts;
         ix.fat = (uint4*)p; p += sz_fat;
     }
     ix.keys = (uint32_t*)p; p += sz_t;

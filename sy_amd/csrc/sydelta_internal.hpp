@@ -25,8 +25,7 @@ constexpr uint64_t kLdsFilterKeys = 16384;   // index sizes whose Bloom filter (
 constexpr uint32_t kLdsFilterWordsMax = 8192;
 // Level-1 filter of a large single-file index (k_scan_l1 keeps it in LDS): 32768 words
 // = 128 KiB = 2^20 bits, built for indexes of more than kLdsFilterKeys keys.
-constexpr uint32_t kL1Words = 32768;   // k_scan_l1's level-1 filter (128 KiB)
-constexpr uint32_t kL1WordsW = 28672;  // k_scan_l1w's (112 KiB: its wider tile takes the rest of the LDS)
+constexpr uint32_t kL1Words = 32768;   // k_scan_l1's level-1 filter (128 KiB), per key partition
 
 // Verified hits are written as key/value pairs: key = (segment << 32) | position
 // relative to the segment's first position, value = global block index (into the
@@ -58,7 +57,7 @@ struct ScanSeg {
 struct DeviceIndex {
     uint32_t* filt = nullptr;   // blocked Bloom filters (probe_hash/filt_mask), per-file 2^k 32-bit words
     uint32_t* l1 = nullptr;     // level-1 filter, single-file indexes above kLdsFilterKeys keys at bs 4096
-    uint32_t l1_words = 0;      // its size: kL1Words (k_scan_l1) or kL1WordsW (k_scan_l1w)
+    uint32_t l1_parts = 0;      // key partitions: l1 holds l1_parts filters of kL1Words words
     uint4* fat = nullptr;       // with l1: per slot {key, first candidate | multi, its strong} (k_idx_fat)
     uint32_t* keys = nullptr;   // 4-key buckets of unique weak values, kEmptyKey = free
     uint32_t* cnt = nullptr;    // candidates per slot
@@ -100,8 +99,8 @@ hipError_t launch_signature_batch(const uint8_t* d_buf, const uint64_t* d_off, c
 hipError_t launch_index_build(const uint32_t* d_weak, const uint64_t* d_strong, DeviceIndex& ix, hipStream_t s,
                               Profiler* prof);
 uint64_t scan_tile_positions();  // positions per tile of the LDS-staged scan
-// SYDELTA_SCAN_L1: 0 k_scan_lds, 1 (default) k_scan_l1, 2 k_scan_l1w (read per call;
-// the index's level-1 layout is chosen when it is built)
+// SYDELTA_SCAN_L1: 0 k_scan_lds, 1 (default) k_scan_l1, 2 k_scan_l1 over two key
+// partitions (read per call; the index's level-1 layout is chosen when it is built)
 int scan_l1_mode();
 uint32_t scan_max_window();      // largest block size the LDS-staged scan handles
 // Scratch the LDS-staged scan needs: filter-pass queues, scan_queue_entries() uint2

@@ -345,8 +345,13 @@ __device__ __forceinline__ bool filt_pass(uint32_t word, uint32_t q) {
 static_assert(kL1Words == 32768, "l1_word takes the top 15 bits of q");
 __device__ __forceinline__ uint32_t l1_word(uint32_t q) { return q >> 17; }
 __device__ __forceinline__ uint32_t l1_test(uint32_t word, uint32_t q) { return __builtin_amdgcn_ubfe(word, q >> 12, 1); }
-// k_scan_l1w's filter of kL1WordsW words: word = floor(q * kL1WordsW / 2^32), same bit
-__device__ __forceinline__ uint32_t l1w_word(uint32_t q) { return __umulhi(q, kL1WordsW); }
+// Key partitions (SYDELTA_SCAN_L1=2): key w belongs to partition r & 1 (r's low bits
+// take no part in the level-2 word, r >> fwshift, fwshift >= 4), and partition p's keys
+// alone set the bits of level-1 filter p, so each filter holds half the keys at two bits
+// per key.  A scan pass over partition p tests only the positions whose value falls in
+// p: every position is still rolled in every pass, but the level-1 pass rate -- the L2
+// request rate -- drops from 1 - e^(-k/2^20) to 1 - e^(-k/2^21) (0.63 -> 0.39 at 1 Mi keys).
+__device__ __forceinline__ uint32_t l1_part(uint32_t r, uint32_t pmask) { return r & pmask; }
 __device__ __forceinline__ uint32_t bucket_hash(uint32_t w) {
     uint32_t h = w ^ (w >> 15);
     h *= 0x2C1B3C6Du;
@@ -366,7 +371,7 @@ __device__ __forceinline__ uint32_t file_of_block(const uint64_t* __restrict__ f
 
 __global__ void k_idx_insert(const uint32_t* __restrict__ weak, uint64_t n, const uint64_t* __restrict__ fblk,
                              uint32_t nf, const FileIx* __restrict__ files, uint32_t* __restrict__ filt,
-                             uint32_t* __restrict__ l1, uint32_t l1_words, uint32_t* __restrict__ keys,
+                             uint32_t* __restrict__ l1, uint32_t l1_parts, uint32_t* __restrict__ keys,
                              uint32_t* __restrict__ cnt, uint32_t* __restrict__ slot_of) {
     const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
@@ -374,8 +379,8 @@ __global__ void k_idx_insert(const uint32_t* __restrict__ weak, uint64_t n, cons
     const uint32_t w = weak[i];
     const ProbeHash h = probe_hash(w);
     atomicOr(filt + F.filt_off + (h.r >> F.fwshift), filt_mask(h.q));
-    if (l1)  // single-file index only (l1_test); k_scan_l1w's smaller filter: l1w_word
-        atomicOr(l1 + (l1_words == kL1Words ? l1_word(h.q) : l1w_word(h.q)), 1u << ((h.q >> 12) & 31));
+    if (l1)  // single-file index only (l1_test); l1_parts filters of kL1Words words each
+        atomicOr(l1 + (size_t)l1_part(h.r, l1_parts - 1) * kL1Words + l1_word(h.q), 1u << ((h.q >> 12) & 31));
     uint32_t b = bucket_hash(w) & F.bmask;
     for (;;) {
         for (uint32_t j = 0; j < 4; ++j) {
@@ -1703,7 +1708,8 @@ struct L1Batch {
     uint32_t w2[kB3], hq[kB3], wv[kB3];
 };
 
-__global__ __launch_bounds__(kT3, 2) void k_scan_l1(ScanArgs a, uint32_t per) {
+// part / pmask: the key partition this pass tests (pmask 0: one partition, every position)
+__global__ __launch_bounds__(kT3, 2) void k_scan_l1(ScanArgs a, uint32_t per, uint32_t part, uint32_t pmask) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     const uint32_t n = a.n;
     const Lds3 L = lds3_layout(n);
@@ -1721,7 +1727,7 @@ __global__ __launch_bounds__(kT3, 2) void k_scan_l1(ScanArgs a, uint32_t per) {
     // level-1 filter and the n*x table, once per workgroup (published by the first
     // tile's barrier)
     {
-        const uint4* g = (const uint4*)a.l1;
+        const uint4* g = (const uint4*)(a.l1 + (size_t)part * kL1Words);
         uint4* d = (uint4*)(smem + L.l1);
 #pragma unroll 4
         for (uint32_t i = tid; i < kL1Words / 4; i += kT3) d[i] = g[i];
@@ -1867,7 +1873,7 @@ __global__ __launch_bounds__(kT3, 2) void k_scan_l1(ScanArgs a, uint32_t per) {
             (int)__builtin_amdgcn_readfirstlane(sc.fwords * 4), 0x00020000);
         const uint32_t fwshift = __builtin_amdgcn_readfirstlane(sc.fwshift);
         auto compute = [&](uint32_t g, L1Batch& Bt) {
-            uint32_t xo[2], xi[2];
+            uint32_t xo[2], xi[2], pt[kB3];
             xo[0] = rows[orow + (g >> 2)];
             xo[1] = rows[orow + (g >> 2) + 1];
             {
@@ -1893,6 +1899,7 @@ __global__ __launch_bounds__(kT3, 2) void k_scan_l1(ScanArgs a, uint32_t per) {
                 const ProbeHash h = probe_hash(am, bm);
                 Bt.hq[t] = h.q;
                 off[t] = (h.r >> fwshift) * 4;
+                pt[t] = l1_part(h.r, pmask);
                 w1[t] = l1[l1_word(h.q)];
                 const uint32_t u = am + in + (kMod - out);  // [M-255, 2M+255)
                 am = min(u, min(u - kMod, u - 2 * kMod));
@@ -1901,7 +1908,8 @@ __global__ __launch_bounds__(kT3, 2) void k_scan_l1(ScanArgs a, uint32_t per) {
             }
 #pragma unroll
             for (int t = 0; t < kB3; ++t) {
-                const uint32_t p1 = l1_test(w1[t], Bt.hq[t]);
+                // a position of another key partition is tested by that partition's pass
+                const uint32_t p1 = l1_test(w1[t], Bt.hq[t]) & (pt[t] == part ? 1u : 0u);
                 if (a.timing) l1pass += __popcll(__ballot(p1));
                 // a level-1 miss asks for an offset past the buffer: no request, reads 0
                 // (and filt_pass(0, q) is false)
@@ -1989,345 +1997,6 @@ __global__ __launch_bounds__(kT3, 2) void k_scan_l1(ScanArgs a, uint32_t per) {
         PHASE_MARK3(5)
     }
 #undef PHASE_MARK3
-    if (lane == 0 && passes) atomicAdd(&a.counters[2], passes);
-    if (lane == 0 && weak_hits) atomicAdd(&a.counters[1], weak_hits);
-    if (a.timing && lane == 0) atomicAdd(&a.counters[3], l1pass);
-    if (a.timing && tid == 0)
-        for (int k = 0; k < 6; ++k) atomicAdd(&a.counters[4 + k], tm[k]);
-}
-
-// ===========================================================================
-// k_scan_l1w: k_scan_l1 on tiles of 32 Ki positions (SYDELTA_SCAN_L1=2, opt-in)
-// ===========================================================================
-// k_scan_l1 pays per 16 Ki-position tile for work that does not grow with the tile:
-// every lane's closed-form first window, the drain's fat-table round trip and the
-// barrier at which the waves wait for the slowest one (phase cycles per tile, DESIGN.md
-// section 6.1: window 3.9 K, drain 5.8 K, barrier 8.8 K of ~34 K).  Here a tile is two of
-// the host's tiles: 64 positions per thread in eight batches, first windows from 64-byte
-// row sums (two columns of 64 rows per wave), LDS rows of 36 KiB, which leave 112 KiB for
-// the level-1 filter (kL1WordsW: pass rate 1 - e^(-keys/917504), 0.68 at 1 Mi keys, against
-// 0.63 for k_scan_l1's 128 KiB).  A pair of host tiles that is cut by a segment end or by
-// the workgroup's range is scanned as one tile whose second half is dropped by the drain.
-// Same outputs as k_scan_l1 (hit keys, weak/pass counters, phase timings).
-constexpr int kR4 = 64;            // positions per thread = one 64-byte row
-constexpr int kTile4 = kT3 * kR4;  // 32768 positions per tile
-constexpr int kNB4 = kR4 / kB3;    // batches per thread per tile
-static_assert(kTile4 == 2 * kTile2, "a k_scan_l1w tile is two host tiles");
-
-struct Lds4 {
-    uint32_t nch;                        // 64-byte rows
-    uint32_t ntail;                      // rows past the first kT3 (staged 16 bytes per thread)
-    uint32_t ntab, fq, wq, l1, total;    // byte offsets
-};
-__host__ __device__ __forceinline__ Lds4 lds4_layout(uint32_t n) {
-    Lds4 L;
-    L.nch = (kTile4 + n + 63) / 64 + 1;
-    L.ntail = L.nch > (uint32_t)kT3 ? L.nch - kT3 : 0;
-    uint32_t o = L.nch * kRowDw * 4;
-    o = (o + 15) & ~15u; L.ntab = o; o += 256 * 4;
-    L.fq = o; o += (kT3 / 64) * kFQ3 * 8;
-    L.wq = o; o += (kT3 / 64) * kWQ3 * 16;
-    L.l1 = o; o += kL1WordsW * 4;
-    L.total = o;
-    return L;
-}
-
-// 16 bytes at src + c0 (16-byte aligned; bytes at or beyond len read as 0).
-__device__ __forceinline__ void load16_nt(const uint8_t* src, uint64_t len, uint64_t c0, uint32_t x[4]) {
-    if (c0 + 16 <= len) {
-        const uint4* q = (const uint4*)(src + c0);
-        x[0] = __builtin_nontemporal_load(&q->x);
-        x[1] = __builtin_nontemporal_load(&q->y);
-        x[2] = __builtin_nontemporal_load(&q->z);
-        x[3] = __builtin_nontemporal_load(&q->w);
-    } else {
-#pragma unroll
-        for (int i = 0; i < 4; ++i) {
-            uint32_t v = 0;
-            for (int b = 0; b < 4; ++b) {
-                const uint64_t p = c0 + 4 * i + b;
-                if (p < len) v |= (uint32_t)src[p] << (8 * b);
-            }
-            x[i] = v;
-        }
-    }
-}
-
-__global__ __launch_bounds__(kT3, 2) void k_scan_l1w(ScanArgs a, uint32_t per) {
-    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-    const uint32_t n = a.n;
-    const Lds4 L = lds4_layout(n);
-    uint32_t* rows = (uint32_t*)smem;
-    uint32_t* ntab = (uint32_t*)(smem + L.ntab);
-    const uint32_t* l1 = (const uint32_t*)(smem + L.l1);
-    const uint32_t tid = threadIdx.x;
-    const uint32_t lane = tid & 63, wid = tid >> 6;
-    uint2* fq = (uint2*)(smem + L.fq) + (size_t)wid * kFQ3;
-    uint4* wq = (uint4*)(smem + L.wq) + (size_t)wid * kWQ3;
-
-    const uint32_t t_begin = blockIdx.x * per;
-    const uint32_t t_end = min(a.ntiles, t_begin + per);
-    if (t_begin >= t_end) return;
-    {
-        const uint4* g = (const uint4*)a.l1;
-        uint4* d = (uint4*)(smem + L.l1);
-#pragma unroll 4
-        for (uint32_t i = tid; i < kL1WordsW / 4; i += kT3) d[i] = g[i];
-    }
-    for (uint32_t i = tid; i < 256; i += kT3) ntab[i] = kMod - 1 - (a.nm * i) % kMod;
-    const uint32_t ntail4 = 4 * L.ntail;  // threads staging a 16-byte quarter of a tail row
-    const uint32_t rel0 = tid * kR4;
-    const uint32_t orow = tid * kRowDw;          // this thread's out bytes: row tid
-    const uint32_t din0 = (rel0 + n) >> 2;       // ... and its first in dword
-    const uint32_t sh = n & 3;
-    const uint32_t m64 = n >> 6;                 // window = m64 rows (n % 64 == 0, n <= 4096)
-    unsigned long long passes = 0, weak_hits = 0;
-    uint32_t nfq = 0;
-    unsigned long long tm[6] = {0, 0, 0, 0, 0, 0}, l1pass = 0;
-    unsigned long long tprev = a.timing ? __builtin_amdgcn_s_memtime() : 0;
-#define PHASE_MARK4(k)                                                 \
-    if (a.timing) {                                                    \
-        const unsigned long long tnow = __builtin_amdgcn_s_memtime(); \
-        tm[k] += tnow - tprev;                                         \
-        tprev = tnow;                                                  \
-    }
-
-    auto seg_ctx = [&](uint32_t tile, uint32_t si0, SegCtx& sc, uint32_t& si, uint64_t& tile_start,
-                       uint64_t& seg_len) {
-        uint32_t lo = si0, hi = a.nsegs;
-        while (hi - lo > 1) {
-            const uint32_t mid = (lo + hi) >> 1;
-            if (a.segs[mid].tile_base <= tile) lo = mid; else hi = mid;
-        }
-        si = lo;
-        const ScanSeg S = a.segs[si];
-        const FileIx F = a.files[S.file];
-        sc.base = a.src + S.src;
-        sc.pos_begin = S.pos_begin;
-        sc.pos_end = S.pos_end;
-        sc.keys = a.keys + F.slot_off;
-        sc.fat = a.fat + F.slot_off;
-        sc.slot_off = F.slot_off;
-        sc.bmask = F.bmask;
-        sc.seg_id = si;
-        sc.fwshift = F.fwshift;
-        sc.filt = a.filt + F.filt_off;
-        sc.fwords = 1u << (32 - F.fwshift);
-        tile_start = S.pos_begin + (uint64_t)(tile - S.tile_base) * kTile2;
-        seg_len = S.len;
-    };
-    // host tiles this tile covers: 2 when host tile t+1 is in this workgroup's range and
-    // in the same segment as t (segment si)
-    auto span_of = [&](uint32_t t, uint32_t sidx) -> uint32_t {
-        if (t + 1 >= t_end) return 1;
-        if (sidx + 1 < a.nsegs && a.segs[sidx + 1].tile_base <= t + 1) return 1;
-        return 2;
-    };
-    SegCtx sc, nsc;
-    uint32_t si = 0, nsi = 0;
-    uint64_t tile_start = 0, seg_len = 0, ntile_start = 0, nseg_len = 0;
-    seg_ctx(t_begin, 0, nsc, nsi, ntile_start, nseg_len);
-    uint32_t nspan = span_of(t_begin, nsi);
-    // next tile's rows 0..kT3-1 (thread c: row c) and its tail rows (16 bytes per thread)
-    uint32_t x[16], xt[4];
-    load_chunk_nt(nsc.base, nseg_len, ntile_start + 64ull * tid, x);
-    if (tid < ntail4) load16_nt(nsc.base, nseg_len, ntile_start + 64ull * kT3 + 16ull * tid, xt);
-
-    uint32_t tile = t_begin;
-#pragma unroll 1
-    while (tile < t_end) {
-        sc = nsc;
-        si = nsi;
-        tile_start = ntile_start;
-        seg_len = nseg_len;
-        const uint32_t span = nspan;
-        // ---- stage (the previous tile's barrier ended every read of the rows)
-#pragma unroll
-        for (int i = 0; i < 16; ++i) rows[tid * kRowDw + i] = x[i];
-        if (tid < ntail4) {
-#pragma unroll
-            for (int i = 0; i < 4; ++i) rows[(kT3 + (tid >> 2)) * kRowDw + 4 * (tid & 3) + i] = xt[i];
-        }
-        __syncthreads();
-        const uint32_t nt = tile + span;
-        if (nt < t_end) {
-            if (nsi + 1 < a.nsegs && a.segs[nsi + 1].tile_base <= nt)
-                seg_ctx(nt, nsi, nsc, nsi, ntile_start, nseg_len);
-            else
-                ntile_start = tile_start + (uint64_t)span * kTile2;
-            nspan = span_of(nt, nsi);
-            load_chunk_nt(nsc.base, nseg_len, ntile_start + 64ull * tid, x);
-            if (tid < ntail4) load16_nt(nsc.base, nseg_len, ntile_start + 64ull * kT3 + 16ull * tid, xt);
-        }
-        // positions of this tile that belong to it: [tile_start, tile_start + span * kTile2)
-        sc.pos_end = min(sc.pos_end, tile_start + (uint64_t)span * kTile2);
-        PHASE_MARK4(0)
-
-        // ---- window: lane l of wave w starts at row r = 64w + l (tile offset 64r); rows
-        // r + 64j, j = 0..1, cover its window [64r, 64r + n) (m64 <= 64)
-        uint32_t am, bm;
-        {
-            uint32_t S[2], V[2], J[2], TS[2], TV[2], TJ[2];
-#pragma unroll
-            for (int j = 0; j < 2; ++j) {
-                const uint32_t* r = rows + (tid + 64 * j) * kRowDw;
-                uint32_t s = 0, v = 0;
-#pragma unroll
-                for (int i = 0; i < 16; ++i) {
-                    const uint32_t d = r[i];
-                    s = udot4(d, 0x01010101u, s);
-                    v = udot4(d, offw(i), v);
-                }
-                S[j] = wave_scan_excl(s, TS[j]);
-                V[j] = wave_scan_excl(v, TV[j]);
-                J[j] = wave_scan_excl((uint32_t)(64 * j + lane) * s, TJ[j]);  // row index relative to the wave
-            }
-            // prefix at relative row y = lane + m64 (column jy = y >> 6, lane y & 63)
-            const uint32_t jA = m64 >> 6, ly = (lane + m64) & 63;
-            const bool carry = lane + (m64 & 63) >= 64;
-            auto pre = [&](const uint32_t* E, const uint32_t* T) -> uint32_t {
-                uint32_t base0 = 0, ea = 0, eb = 0, base1 = 0;
-#pragma unroll
-                for (int j = 0; j < 2; ++j) {
-                    const uint32_t sj = (m64 & 63) == 0 ? E[j] : (uint32_t)__shfl((int)E[j], (int)ly, 64);
-                    if ((uint32_t)j == jA) ea = sj;
-                    if ((uint32_t)j == jA + 1) eb = sj;
-                    if ((uint32_t)j < jA) base0 += T[j];
-                    if ((uint32_t)j < jA + 1) base1 += T[j];
-                }
-                return carry ? base1 + eb : base0 + ea;
-            };
-            const uint64_t dS = pre(S, TS) - S[0];
-            const uint64_t dV = pre(V, TV) - V[0];
-            const uint64_t dJ = pre(J, TJ) - J[0];
-            const uint32_t A = (uint32_t)dS;
-            // B = sum_i (n - i) x_{64r+i} = n dS - 64 sum_k (k - l) S_k - dV   (< 2^31 for n <= 4096)
-            const uint32_t B = (uint32_t)((uint64_t)n * dS - 64ull * (dJ - (uint64_t)lane * dS) - dV);
-            am = (1 + A) % kMod;
-            bm = (n + B) % kMod;
-        }
-        PHASE_MARK4(1)
-
-        // ---- roll (as k_scan_l1; positions past dc.pos_end are dropped by the drain)
-        const uint64_t fptr = (uint64_t)(uintptr_t)sc.filt;
-        const uint32_t fp_lo = __builtin_amdgcn_readfirstlane((uint32_t)fptr);
-        const uint32_t fp_hi = __builtin_amdgcn_readfirstlane((uint32_t)(fptr >> 32));
-        const __amdgpu_buffer_rsrc_t frsrc = __builtin_amdgcn_make_buffer_rsrc(
-            (void*)(uintptr_t)(((uint64_t)fp_hi << 32) | fp_lo), (short)0,
-            (int)__builtin_amdgcn_readfirstlane(sc.fwords * 4), 0x00020000);
-        const uint32_t fwshift = __builtin_amdgcn_readfirstlane(sc.fwshift);
-        auto compute = [&](uint32_t g, L1Batch& Bt) {
-            uint32_t xo[2], xi[2];
-            xo[0] = rows[orow + (g >> 2)];
-            xo[1] = rows[orow + (g >> 2) + 1];
-            {
-                uint32_t dw[3];
-#pragma unroll
-                for (int j = 0; j < 3; ++j) {
-                    const uint32_t d = din0 + (g >> 2) + j;
-                    dw[j] = rows[(d >> 4) * kRowDw + (d & 15)];
-                }
-                xi[0] = __builtin_amdgcn_alignbyte(dw[1], dw[0], sh);
-                xi[1] = __builtin_amdgcn_alignbyte(dw[2], dw[1], sh);
-            }
-            uint32_t ct[kB3], off[kB3], w1[kB3];
-#pragma unroll
-            for (int t = 0; t < kB3; ++t) ct[t] = ntab[(xo[t >> 2] >> (8 * (t & 3))) & 0xFF];
-#pragma unroll
-            for (int t = 0; t < kB3; ++t) {
-                const uint32_t out = (xo[t >> 2] >> (8 * (t & 3))) & 0xFF;
-                const uint32_t in = (xi[t >> 2] >> (8 * (t & 3))) & 0xFF;
-                __builtin_assume(am < kMod);
-                __builtin_assume(bm < kMod);
-                Bt.wv[t] = (bm << 16) | am;
-                const ProbeHash h = probe_hash(am, bm);
-                Bt.hq[t] = h.q;
-                off[t] = (h.r >> fwshift) * 4;
-                w1[t] = l1[l1w_word(h.q)];
-                const uint32_t u = am + in + (kMod - out);  // [M-255, 2M+255)
-                am = min(u, min(u - kMod, u - 2 * kMod));
-                const uint32_t v = bm + am + ct[t];          // [0, 3M)
-                bm = min(v, min(v - kMod, v - 2 * kMod));
-            }
-#pragma unroll
-            for (int t = 0; t < kB3; ++t) {
-                const uint32_t p1 = l1_test(w1[t], Bt.hq[t]);
-                if (a.timing) l1pass += __popcll(__ballot(p1));
-                // a level-1 miss asks for an offset past the buffer: no request, reads 0
-                Bt.w2[t] = __builtin_amdgcn_raw_buffer_load_b32(frsrc, (int)(p1 ? off[t] : 0xFFFFFFFFu), 0, 0);
-            }
-        };
-        auto finish = [&](uint32_t g, L1Batch& Bt, uint32_t& todo) -> bool {
-            uint32_t pbits = 0;
-#pragma unroll
-            for (int t = 0; t < kB3; ++t) pbits |= (filt_pass(Bt.w2[t], Bt.hq[t]) ? 1u : 0u) << t;
-            asm volatile("" : "+v"(pbits));
-            const uint64_t below = (1ull << lane) - 1;
-            uint32_t need = 0;
-#pragma unroll
-            for (int t = 0; t < kB3; ++t)
-                if ((todo >> t) & 1) need += __popcll(__ballot((pbits >> t) & 1));
-            const bool all = nfq + need <= (uint32_t)kFQ3;
-            bool full = false;
-#pragma unroll
-            for (int t = 0; t < kB3; ++t) {
-                if (!((todo >> t) & 1) || full) continue;
-                const uint64_t mk = __ballot((pbits >> t) & 1);
-                if (!all && nfq + __popcll(mk) > (uint32_t)kFQ3) { full = true; continue; }
-                if ((pbits >> t) & 1) fq[nfq + __popcll(mk & below)] = make_uint2(rel0 + g + t, Bt.wv[t]);
-                nfq += __popcll(mk);
-                todo &= ~(1u << t);
-            }
-            if (all) todo = 0xFFu;
-            return all;
-        };
-        // Pipeline over the thread's 8 batches: batch k+1's level-2 loads are in flight
-        // while batch k is tested; a batch the queue cannot take stops it, the queue is
-        // drained and the roll resumes from that batch's saved state.
-        uint32_t stop = kNB4, todo = 0xFFu, ra = 0, rb = 0;
-        {
-            L1Batch b0, b1;
-            uint32_t sa0 = am, sb0 = bm;
-            compute(0, b0);
-            uint32_t sa1 = am, sb1 = bm;
-            compute(kB3, b1);
-#pragma unroll 1
-            for (uint32_t k = 0; k < (uint32_t)kNB4; k += 2) {
-                if (!finish(kB3 * k, b0, todo)) { stop = k; ra = sa0; rb = sb0; break; }
-                if (k + 2 < (uint32_t)kNB4) { sa0 = am; sb0 = bm; compute(kB3 * (k + 2), b0); }
-                if (!finish(kB3 * (k + 1), b1, todo)) { stop = k + 1; ra = sa1; rb = sb1; break; }
-                if (k + 3 < (uint32_t)kNB4) { sa1 = am; sb1 = bm; compute(kB3 * (k + 3), b1); }
-            }
-        }
-        while (stop < (uint32_t)kNB4) {
-            passes += nfq;
-            drain_l1(a, fq, nfq, wq, weak_hits, rows, tile_start, sc);
-            nfq = 0;
-            uint32_t k = stop;
-            stop = kNB4;
-            am = ra;
-            bm = rb;
-#pragma unroll 1
-            for (; k < (uint32_t)kNB4; ++k) {
-                L1Batch bt;
-                const uint32_t ak = am, sk = bm;
-                compute(kB3 * k, bt);
-                if (!finish(kB3 * k, bt, todo)) { stop = k; ra = ak; rb = sk; break; }
-            }
-        }
-        PHASE_MARK4(2)
-        PHASE_MARK4(3)
-        if (nfq) {
-            passes += nfq;
-            drain_l1(a, fq, nfq, wq, weak_hits, rows, tile_start, sc);
-            nfq = 0;
-        }
-        PHASE_MARK4(4)
-        __syncthreads();  // rows are rewritten by the next tile
-        PHASE_MARK4(5)
-        tile += span;
-    }
-#undef PHASE_MARK4
     if (lane == 0 && passes) atomicAdd(&a.counters[2], passes);
     if (lane == 0 && weak_hits) atomicAdd(&a.counters[1], weak_hits);
     if (a.timing && lane == 0) atomicAdd(&a.counters[3], l1pass);
@@ -3290,6 +2959,8 @@ static inline unsigned grid_for(uint64_t threads, unsigned block) { return (unsi
 // Large single-file indexes scan with k_scan_l1 by default: 17.24 ms per 4 GiB against
 // k_scan_lds's 19.2 ms in global-filter mode.  SYDELTA_SCAN_L1=0
 // selects k_scan_lds (read per call: the parity tests run both).
+// SYDELTA_SCAN_L1=2 builds the level-1 filter in two key partitions and scans once per
+// partition (l1_part).
 int scan_l1_mode() {
     const char* e = getenv("SYDELTA_SCAN_L1");
     return (e && e[0] == '0') ? 0 : (e && e[0] == '2') ? 2 : 1;
@@ -3361,7 +3032,7 @@ hipError_t launch_index_build(const uint32_t* d_weak, const uint64_t* d_strong, 
                               Profiler* prof) {
     hipError_t e;
     if ((e = hipMemsetAsync(ix.filt, 0, ix.fwords * 4, s))) return e;
-    if (ix.l1 && (e = hipMemsetAsync(ix.l1, 0, (size_t)ix.l1_words * 4, s))) return e;
+    if (ix.l1 && (e = hipMemsetAsync(ix.l1, 0, (size_t)ix.l1_parts * kL1Words * 4, s))) return e;
     if ((e = hipMemsetAsync(ix.keys, 0xFF, ix.nslots * 4, s))) return e;
     if ((e = hipMemsetAsync(ix.cnt, 0, ix.nslots * 4, s))) return e;
     const uint64_t n = ix.nblocks;
@@ -3369,7 +3040,7 @@ hipError_t launch_index_build(const uint32_t* d_weak, const uint64_t* d_strong, 
     {
         ProfScope ps(prof, s, "k_idx_insert");
         hipLaunchKernelGGL(k_idx_insert, dim3(grid_for(n, 256)), dim3(256), 0, s, d_weak, n, ix.d_fblk,
-                           (uint32_t)ix.nfiles, ix.d_files, ix.filt, ix.l1, ix.l1_words, ix.keys, ix.cnt,
+                           (uint32_t)ix.nfiles, ix.d_files, ix.filt, ix.l1, ix.l1_parts, ix.keys, ix.cnt,
                            ix.slot_of);
     }
     size_t tmp = 0;
@@ -3443,32 +3114,6 @@ uint64_t scan_tile_positions() { return kTile2; }
 uint32_t scan_max_window() { return kMaxN2; }
 size_t scan_queue_entries() { return (size_t)kWgPerCuMax2 * 256 * (kT2 / 64) * kGFQ; }
 
-// k_scan_l1w (SYDELTA_SCAN_L1=2 when the index was built): one workgroup per CU, an
-// even number of host tiles each so that the tile pairs line up.
-static hipError_t launch_scan_l1w(const ScanArgs& a, uint32_t ntiles, const DeviceIndex& ix, hipStream_t s,
-                                  Profiler* prof) {
-    static std::once_flag once;
-    static hipError_t err = hipSuccess;
-    static int cus = 256;
-    std::call_once(once, [] {
-        err = hipFuncSetAttribute((const void*)k_scan_l1w, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                  160 * 1024 - 256);
-        int dev = 0, c = 0;
-        if (hipGetDevice(&dev) == hipSuccess &&
-            hipDeviceGetAttribute(&c, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess && c > 0)
-            cus = c;
-    });
-    if (err != hipSuccess) return err;
-    const Lds4 L = lds4_layout(a.n);
-    if (L.total > 160u * 1024 - 256 || !ix.fat || a.n % 64 != 0 || a.n > kMaxN3) return hipErrorInvalidValue;
-    uint32_t per = (uint32_t)((ntiles + (uint64_t)cus - 1) / (uint64_t)cus);
-    per += per & 1;
-    const uint32_t grid = (uint32_t)((ntiles + (uint64_t)per - 1) / per);
-    ProfScope ps(prof, s, "k_scan_l1w");
-    hipLaunchKernelGGL(k_scan_l1w, dim3(grid), dim3(kT3), L.total, s, a, per);
-    return hipGetLastError();
-}
-
 hipError_t launch_scan(const uint8_t* d_buf, const ScanSeg* d_segs, uint32_t nsegs, uint32_t ntiles, uint32_t n,
                        const DeviceIndex& ix, const uint64_t* d_strong, uint64_t* d_hit_key, uint32_t* d_hit_val,
                        uint64_t out_cap, unsigned long long* d_counters, uint2* gfq, size_t gfq_cap, hipStream_t s,
@@ -3505,8 +3150,6 @@ hipError_t launch_scan(const uint8_t* d_buf, const ScanSeg* d_segs, uint32_t nse
     // covers, n = 4096 (the C3 shape; tests/test_gpu_scan_large.py).  Other sizes with a
     // large index go to k_scan_lds (production block sizes for files with more than
     // 16 Ki blocks are >= 8 KiB anyway: bs = sqrt(file size)).
-    if (ix.l1 && n == kMaxN3 && scan_l1_mode() != 0 && ix.l1_words == kL1WordsW)
-        return launch_scan_l1w(a, ntiles, ix, s, prof);
     if (ix.l1 && n == kMaxN3 && scan_l1_mode() != 0) {
         std::call_once(l1_once, [] {
             l1_err = hipFuncSetAttribute((const void*)k_scan_l1, hipFuncAttributeMaxDynamicSharedMemorySize,
@@ -3521,9 +3164,13 @@ hipError_t launch_scan(const uint8_t* d_buf, const ScanSeg* d_segs, uint32_t nse
         // one workgroup per CU (the level-1 filter fills its LDS), contiguous tile ranges
         const uint32_t grid = (uint32_t)std::min<uint64_t>(ntiles, (uint64_t)l1_cus);
         const uint32_t per = (ntiles + grid - 1) / grid;
-        ProfScope ps(prof, s, "k_scan_l1");
-        hipLaunchKernelGGL(k_scan_l1, dim3(grid), dim3(kT3), L3.total, s, a, per);
-        return hipGetLastError();
+        // one pass per key partition (the index's level-1 filters), each over every tile
+        for (uint32_t part = 0; part < ix.l1_parts; ++part) {
+            ProfScope ps(prof, s, "k_scan_l1");
+            hipLaunchKernelGGL(k_scan_l1, dim3(grid), dim3(kT3), L3.total, s, a, per, part, ix.l1_parts - 1);
+            if (hipError_t e = hipGetLastError()) return e;
+        }
+        return hipSuccess;
     }
     const bool lds_filter = ix.max_fwords <= kLdsFilterWordsMax;
     const uint32_t lds_fwords = lds_filter ? std::max<uint32_t>(ix.max_fwords, 4u) : 0u;

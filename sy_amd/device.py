@@ -239,23 +239,30 @@ class Chunk:
 def join_deltas(parts, source_size: int, block_size: int) -> DeviceDelta:
     """Concatenate chunk deltas in file order, merging a trailing Data op with the
     next chunk's leading Data op when contiguous (sydelta_delta_append's rule)."""
-    kinds, aa, bb = [], [], []
+    ks, as_, bs_ = [], [], []
     for p in parts:
-        k, a, b = list(p.kind), list(p.a), list(p.b)
-        if kinds and k and kinds[-1] == 1 and k[0] == 1 and int(aa[-1]) + int(bb[-1]) == int(a[0]):
-            bb[-1] = int(bb[-1]) + int(b[0])
-            k, a, b = k[1:], a[1:], b[1:]
-        kinds += k
-        aa += a
-        bb += b
-    kind = np.array(kinds, dtype=np.uint8)
+        k = np.asarray(p.kind, dtype=np.uint8)
+        a = np.array(p.a, dtype=np.uint64)
+        b = np.array(p.b, dtype=np.uint64)
+        if k.size and ks:
+            # the last non-empty part so far
+            j = max(i for i in range(len(ks)) if ks[i].size) if any(x.size for x in ks) else -1
+            if j >= 0 and ks[j][-1] == 1 and k[0] == 1 and int(as_[j][-1]) + int(bs_[j][-1]) == int(a[0]):
+                bs_[j] = bs_[j].copy()
+                bs_[j][-1] += b[0]
+                k, a, b = k[1:], a[1:], b[1:]
+        ks.append(k)
+        as_.append(a)
+        bs_.append(b)
+    kind = np.concatenate(ks) if ks else np.zeros(0, np.uint8)
+    a = np.concatenate(as_) if as_ else np.zeros(0, np.uint64)
+    b = np.concatenate(bs_) if bs_ else np.zeros(0, np.uint64)
     stats = {"positions": sum(p.stats["positions"] for p in parts),
              "weak_hits": sum(p.stats["weak_hits"] for p in parts),
              "verified_hits": sum(p.stats["verified_hits"] for p in parts),
              "copy_ops": int((kind == 0).sum()), "data_ops": int((kind == 1).sum()),
-             "literal_bytes": int(sum(int(y) for x, y in zip(kinds, bb) if x == 1))}
-    return DeviceDelta(kind, np.array(aa, dtype=np.uint64), np.array(bb, dtype=np.uint64), source_size, block_size,
-                       stats)
+             "literal_bytes": int(b[kind == 1].sum())}
+    return DeviceDelta(kind, a, b, source_size, block_size, stats)
 
 
 def synth_fill_range(buf: torch.Tensor, first: int, seed: int, stream=None) -> None:

@@ -1,7 +1,7 @@
-"""GPU parity for large single-file indexes (> 16 Ki basis blocks): both scans of a
+"""GPU parity for large single-file indexes (> 16 Ki basis blocks): every scan of a
 large index -- the level-1-filter scan k_scan_l1 (the default at n = 4096,
-SYDELTA_SCAN_L1=1) and k_scan_lds in global-filter mode (SYDELTA_SCAN_L1=0) -- against
-the oracle.
+SYDELTA_SCAN_L1=1), the same kernel over two key partitions (SYDELTA_SCAN_L1=2) and
+k_scan_lds in global-filter mode (SYDELTA_SCAN_L1=0) -- against the oracle.
 
 * 96 MiB basis, mixed edits (an all-literal stretch, sparse substitutions, a shift,
   planted unaligned copies, duplicated blocks): bit-exact op list against the C
@@ -24,17 +24,14 @@ from oracle import oracle as O
 pytestmark = pytest.mark.gpu
 
 
-# k_scan_l1w (SYDELTA_SCAN_L1=2) joins the parametrization only when
-# SYDELTA_TEST_SCAN_L1W=1: it was written after this round's GPU access closed and has
-# not run on hardware yet.
-_SCANNERS = ["lds", "l1"] + (["l1w"] if os.environ.get("SYDELTA_TEST_SCAN_L1W") == "1" else [])
+_SCANNERS = ["lds", "l1", "l1p2"]
 
 
 @pytest.fixture(params=_SCANNERS)
 def scanner(request, monkeypatch):
     """The large-index scan kernel (SYDELTA_SCAN_L1 is read when the index is built and
     by launch_scan on every call)."""
-    monkeypatch.setenv("SYDELTA_SCAN_L1", {"lds": "0", "l1": "1", "l1w": "2"}[request.param])
+    monkeypatch.setenv("SYDELTA_SCAN_L1", {"lds": "0", "l1": "1", "l1p2": "2"}[request.param])
     return request.param
 
 
