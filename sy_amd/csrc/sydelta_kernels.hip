@@ -1708,7 +1708,10 @@ struct L1Batch {
     uint32_t w2[kB3], hq[kB3], wv[kB3];
 };
 
-// part / pmask: the key partition this pass tests (pmask 0: one partition, every position)
+// part / pmask: the key partition this pass tests (pmask 0: one partition, every position).
+// kTiming: the SYDELTA_PHASE_TIMING instantiation (phase cycles and level-1 passes
+// counted); the production one carries no timing code in its hot loop.
+template <bool kTiming>
 __global__ __launch_bounds__(kT3, 2) void k_scan_l1(ScanArgs a, uint32_t per, uint32_t part, uint32_t pmask) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     const uint32_t n = a.n;
@@ -1744,9 +1747,9 @@ __global__ __launch_bounds__(kT3, 2) void k_scan_l1(ScanArgs a, uint32_t per, ui
     // SYDELTA_PHASE_TIMING: wave 0's s_memtime cycles per phase (stage, window, roll,
     // drains) into counters[4..8), level-1 passes into counters[3]
     unsigned long long tm[6] = {0, 0, 0, 0, 0, 0}, l1pass = 0;
-    unsigned long long tprev = a.timing ? __builtin_amdgcn_s_memtime() : 0;
+    unsigned long long tprev = kTiming ? __builtin_amdgcn_s_memtime() : 0;
 #define PHASE_MARK3(k)                                                 \
-    if (a.timing) {                                                    \
+    if (kTiming) {                                                     \
         const unsigned long long tnow = __builtin_amdgcn_s_memtime(); \
         tm[k] += tnow - tprev;                                         \
         tprev = tnow;                                                  \
@@ -1910,7 +1913,7 @@ __global__ __launch_bounds__(kT3, 2) void k_scan_l1(ScanArgs a, uint32_t per, ui
             for (int t = 0; t < kB3; ++t) {
                 // a position of another key partition is tested by that partition's pass
                 const uint32_t p1 = l1_test(w1[t], Bt.hq[t]) & (pt[t] == part ? 1u : 0u);
-                if (a.timing) l1pass += __popcll(__ballot(p1));
+                if (kTiming) l1pass += __popcll(__ballot(p1));
                 // a level-1 miss asks for an offset past the buffer: no request, reads 0
                 // (and filt_pass(0, q) is false)
                 Bt.w2[t] = __builtin_amdgcn_raw_buffer_load_b32(frsrc, (int)(p1 ? off[t] : 0xFFFFFFFFu), 0, 0);
@@ -1999,8 +2002,8 @@ __global__ __launch_bounds__(kT3, 2) void k_scan_l1(ScanArgs a, uint32_t per, ui
 #undef PHASE_MARK3
     if (lane == 0 && passes) atomicAdd(&a.counters[2], passes);
     if (lane == 0 && weak_hits) atomicAdd(&a.counters[1], weak_hits);
-    if (a.timing && lane == 0) atomicAdd(&a.counters[3], l1pass);
-    if (a.timing && tid == 0)
+    if (kTiming && lane == 0) atomicAdd(&a.counters[3], l1pass);
+    if (kTiming && tid == 0)
         for (int k = 0; k < 6; ++k) atomicAdd(&a.counters[4 + k], tm[k]);
 }
 
@@ -3152,8 +3155,11 @@ hipError_t launch_scan(const uint8_t* d_buf, const ScanSeg* d_segs, uint32_t nse
     // 16 Ki blocks are >= 8 KiB anyway: bs = sqrt(file size)).
     if (ix.l1 && n == kMaxN3 && scan_l1_mode() != 0) {
         std::call_once(l1_once, [] {
-            l1_err = hipFuncSetAttribute((const void*)k_scan_l1, hipFuncAttributeMaxDynamicSharedMemorySize,
+            l1_err = hipFuncSetAttribute((const void*)k_scan_l1<false>, hipFuncAttributeMaxDynamicSharedMemorySize,
                                          160 * 1024 - 256);
+            if (l1_err == hipSuccess)
+                l1_err = hipFuncSetAttribute((const void*)k_scan_l1<true>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                             160 * 1024 - 256);
             int dev = 0, cus = 0;
             if (hipGetDevice(&dev) == hipSuccess &&
                 hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess && cus > 0)
@@ -3167,7 +3173,10 @@ hipError_t launch_scan(const uint8_t* d_buf, const ScanSeg* d_segs, uint32_t nse
         // one pass per key partition (the index's level-1 filters), each over every tile
         for (uint32_t part = 0; part < ix.l1_parts; ++part) {
             ProfScope ps(prof, s, "k_scan_l1");
-            hipLaunchKernelGGL(k_scan_l1, dim3(grid), dim3(kT3), L3.total, s, a, per, part, ix.l1_parts - 1);
+            if (a.timing)
+                hipLaunchKernelGGL(k_scan_l1<true>, dim3(grid), dim3(kT3), L3.total, s, a, per, part, ix.l1_parts - 1);
+            else
+                hipLaunchKernelGGL(k_scan_l1<false>, dim3(grid), dim3(kT3), L3.total, s, a, per, part, ix.l1_parts - 1);
             if (hipError_t e = hipGetLastError()) return e;
         }
         return hipSuccess;
