@@ -7,7 +7,7 @@
 # Usage (from the repo root on the box): bash scripts/r03b.sh [tag] [legs...]
 set -u
 TAG=${1:-r03b}; shift || true
-LEGS=${*:-tests sq legs}
+LEGS=${*:-tests sq wide legs}
 R=${GRAFT_REPO_ROOT:-$(pwd)}
 OUT=$R/gpurun_out/$TAG
 mkdir -p "$OUT"
@@ -59,7 +59,18 @@ json.dump(out, open(sys.argv[1] + '/sq_k_scan_l1.json', 'w'), indent=1)
 print(json.dumps(out))
 PY
   ;;
+wide)
+  # first hardware run of k_scan_w: a parity failure (rc 1) keeps the legs on the old
+  # kernel (SYDELTA_SCAN_WIDE=0); anything else (fault, timeout) ends the call
+  step 600 python3 -u -m pytest tests/test_gpu_scan_wide.py -x -v --timeout 300 --timeout-method thread \
+    -p no:cacheprovider > "$OUT/pytest_wide.log" 2>&1
+  rc=$?
+  tail -6 "$OUT/pytest_wide.log"
+  if [ $rc -eq 1 ]; then export SYDELTA_SCAN_WIDE=0; echo "== k_scan_w parity failed: legs on k_scan" >&2;
+  elif [ $rc -ne 0 ]; then exit 1; fi ;;
 legs)
+  # the old wide kernel, for the A/B
+  SYDELTA_SCAN_WIDE=0 leg c3_bs64k_kscan --block-size 65536 --steps 2 --warmup 1 --no-cpu-baseline --no-host-inclusive || exit 1
   leg c5_host --workload c5 --steps 10 --warmup 3 --no-cpu-baseline || exit 1
   leg c5_dev --workload c5 --steps 10 --warmup 3 --no-cpu-baseline --device-walk || exit 1
   leg c4_host --workload c4 --steps 5 --warmup 2 --no-cpu-baseline || exit 1

@@ -481,9 +481,14 @@ static int index_create_impl(int device, const uint32_t* weak, const uint64_t* s
     const size_t sz_order = al(4 * nb), sz_slot = al(4 * nb), sz_files = al(sizeof(FileIx) * nfiles);
     const size_t sz_fblk = al(8 * (nfiles + 1)), sz_cstrong = al(8 * nb);
     // level-1 filter for k_scan_l1: one large file (the BASELINE C3 shape)
-    const bool want_l1 = nfiles == 1 && nblocks > kLdsFilterKeys && block_size == 4096;  // k_scan_l1's scope
-    const uint32_t l1_parts = want_l1 ? (scan_l1_mode() == 2 ? 2u : 1u) : 0u;
-    const size_t sz_l1 = al(4 * (size_t)l1_parts * kL1Words);
+    const bool want_narrow = nfiles == 1 && nblocks > kLdsFilterKeys && block_size == 4096;  // k_scan_l1's scope
+    // windows above the LDS-staged scans' limit, one file (the production block sizes of
+    // files over 64 MiB, mod.rs:20-23): k_scan_w's level-1 filter and fat table
+    const bool want_wide = nfiles == 1 && block_size > scan_max_window() && scan_wide_mode() != 0;
+    const bool want_l1 = want_narrow || want_wide;
+    const uint32_t l1_parts = want_narrow ? (scan_l1_mode() == 2 ? 2u : 1u) : want_wide ? 1u : 0u;
+    const uint32_t l1_words = want_narrow ? kL1Words : kL1WordsWide;
+    const size_t sz_l1 = al(4 * (size_t)l1_parts * l1_words);
     const size_t sz_fat = want_l1 ? al(16 * (size_t)sl) : 0;
     const size_t total = sz_weak + sz_strong + sz_filt + sz_l1 + sz_fat + 4 * sz_t + sz_order + sz_slot + sz_files +
                          sz_fblk + sz_cstrong;
@@ -495,6 +500,7 @@ static int index_create_impl(int device, const uint32_t* weak, const uint64_t* s
     if (want_l1) {
         ix.l1 = (uint32_t*)p; p += sz_l1;
         ix.l1_parts = l1_parts;
+        ix.l1_wshift = want_narrow ? 17u : 18u;
         ix.fat = (uint4*)p; p += sz_fat;
     }
     ix.keys = (uint32_t*)p; p += sz_t;
@@ -714,6 +720,12 @@ bool phase_probe_on() {
     return e && e[0] == '1';
 }
 
+// The index carries k_scan_w's level-1 filter (one file, window above the LDS-staged
+// scans' limit) and SYDELTA_SCAN_WIDE does not turn it off.
+bool wide_scan(const sydelta_index* x) {
+    return x->ix.l1 && x->ix.l1_wshift == 18 && scan_wide_mode() != 0;
+}
+
 int probe_mode_env() {
     const char* e = getenv("SYDELTA_PROBE");  // "0" never, "1" always, unset/other: auto
     if (e && e[0] == '0') return 0;
@@ -914,7 +926,10 @@ int Classifier::scan(const std::vector<std::array<uint64_t, 3>>& ranges) {
     double t_kern = 0, t_d2h = 0;
     const uint64_t tile = scan_tile_positions();
     const uint64_t seg_max = (1ull << 31) / tile * tile;
-    const bool wide = n > scan_max_window();
+    // windows above the LDS-staged layouts: k_scan_w when the index has its level-1
+    // filter (single file, built with SYDELTA_SCAN_WIDE != 0), else the per-thread k_scan
+    const bool wide_w = n > scan_max_window() && wide_scan(ix);
+    const bool wide = n > scan_max_window() && !wide_w;
     std::vector<ScanSeg> segs;
     std::vector<uint32_t> seg_src;
     uint64_t ntiles = 0, tot_pos = 0;
@@ -1526,7 +1541,7 @@ static int match_impl(sydelta_index* ix, const uint8_t* d_buf, const uint64_t* s
     b->total.positions = tot_pos;
     static const bool host_timing = getenv("SYDELTA_HOST_TIMING") != nullptr;
     const auto t0 = std::chrono::steady_clock::now();
-    const int mode = n > scan_max_window() ? 0 : probe_mode_env();
+    const int mode = n > scan_max_window() && !wide_scan(ix) ? 0 : probe_mode_env();
     if (int r = C.classify(mode)) return r;
     const double t_cls = ms_since(t0);
     std::vector<size_t> all(nf);
@@ -2340,9 +2355,9 @@ extern "C" int sydelta_chunk_classify(sydelta_index* idx, const uint8_t* d_buf, 
     ch->final_src = final_src;
     ch->file_len = file_len;
     ch->bi = BasisInfo{0, idx->fblk[1], idx->last_size[0]};
-    // windows above the LDS scan's limit: every position scanned (k_scan), no probe, as
-    // match_impl does
-    if (int r = C.classify(n > scan_max_window() ? 0 : probe_mode_env())) return r;
+    // windows above the LDS scans' limit without k_scan_w: every position scanned (k_scan,
+    // one launch per range), no probe, as match_impl does
+    if (int r = C.classify(n > scan_max_window() && !wide_scan(idx) ? 0 : probe_mode_env())) return r;
     if (final_src) {
         std::vector<int> tf;
         if (int r = tail_flags(C, {0}, tf)) return r;

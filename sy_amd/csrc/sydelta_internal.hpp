@@ -26,6 +26,9 @@ constexpr uint32_t kLdsFilterWordsMax = 8192;
 // Level-1 filter of a large single-file index (k_scan_l1 keeps it in LDS): 32768 words
 // = 128 KiB = 2^20 bits, built for indexes of more than kLdsFilterKeys keys.
 constexpr uint32_t kL1Words = 32768;   // k_scan_l1's level-1 filter (128 KiB), per key partition
+// Level-1 filter of a single-file index for windows above scan_max_window() (k_scan_w):
+// 16384 words = 64 KiB = 2^19 bits, beside the wide kernel's two staged byte regions.
+constexpr uint32_t kL1WordsWide = 16384;
 
 // Verified hits are written as key/value pairs: key = (segment << 32) | position
 // relative to the segment's first position, value = global block index (into the
@@ -57,7 +60,8 @@ struct ScanSeg {
 struct DeviceIndex {
     uint32_t* filt = nullptr;   // blocked Bloom filters (probe_hash/filt_mask), per-file 2^k 32-bit words
     uint32_t* l1 = nullptr;     // level-1 filter, single-file indexes above kLdsFilterKeys keys at bs 4096
-    uint32_t l1_parts = 0;      // key partitions: l1 holds l1_parts filters of kL1Words words
+    uint32_t l1_parts = 0;      // key partitions: l1 holds l1_parts filters of 2^(32 - l1_wshift) words
+    uint32_t l1_wshift = 17;    // level-1 word of probe hash q: q >> l1_wshift (17: kL1Words, 18: kL1WordsWide)
     uint4* fat = nullptr;       // with l1: per slot {key, first candidate | multi, its strong} (k_idx_fat)
     uint32_t* keys = nullptr;   // 4-key buckets of unique weak values, kEmptyKey = free
     uint32_t* cnt = nullptr;    // candidates per slot
@@ -102,6 +106,9 @@ uint64_t scan_tile_positions();  // positions per tile of the LDS-staged scan
 // SYDELTA_SCAN_L1: 0 k_scan_lds, 1 (default) k_scan_l1, 2 k_scan_l1 over two key
 // partitions (read per call; the index's level-1 layout is chosen when it is built)
 int scan_l1_mode();
+// SYDELTA_SCAN_WIDE=0: windows above scan_max_window() take the per-thread k_scan
+// instead of the LDS-staged k_scan_w (read when the index is built and per call)
+int scan_wide_mode();
 uint32_t scan_max_window();      // largest block size the LDS-staged scan handles
 // Scratch the LDS-staged scan needs: filter-pass queues, scan_queue_entries() uint2
 // entries (2 workgroups per CU on up to 256 CUs; launch_scan checks).

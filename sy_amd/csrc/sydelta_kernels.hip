@@ -371,7 +371,7 @@ __device__ __forceinline__ uint32_t file_of_block(const uint64_t* __restrict__ f
 
 __global__ void k_idx_insert(const uint32_t* __restrict__ weak, uint64_t n, const uint64_t* __restrict__ fblk,
                              uint32_t nf, const FileIx* __restrict__ files, uint32_t* __restrict__ filt,
-                             uint32_t* __restrict__ l1, uint32_t l1_parts, uint32_t* __restrict__ keys,
+                             uint32_t* __restrict__ l1, uint32_t l1_parts, uint32_t l1_wshift, uint32_t* __restrict__ keys,
                              uint32_t* __restrict__ cnt, uint32_t* __restrict__ slot_of) {
     const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
@@ -379,8 +379,9 @@ __global__ void k_idx_insert(const uint32_t* __restrict__ weak, uint64_t n, cons
     const uint32_t w = weak[i];
     const ProbeHash h = probe_hash(w);
     atomicOr(filt + F.filt_off + (h.r >> F.fwshift), filt_mask(h.q));
-    if (l1)  // single-file index only (l1_test); l1_parts filters of kL1Words words each
-        atomicOr(l1 + (size_t)l1_part(h.r, l1_parts - 1) * kL1Words + l1_word(h.q), 1u << ((h.q >> 12) & 31));
+    if (l1)  // single-file index only (l1_test); l1_parts filters of 2^(32 - l1_wshift) words each
+        atomicOr(l1 + ((size_t)l1_part(h.r, l1_parts - 1) << (32 - l1_wshift)) + (h.q >> l1_wshift),
+                 1u << ((h.q >> 12) & 31));
     uint32_t b = bucket_hash(w) & F.bmask;
     for (;;) {
         for (uint32_t j = 0; j < 4; ++j) {
@@ -1562,12 +1563,15 @@ __device__ __forceinline__ bool fat_find(const uint4* __restrict__ fat, uint32_t
 // kMulti+slot, strong lo, hi}: XXH3 of the window from the LDS rows (four windows per
 // wave, one per 16-lane row, when n % 64 == 0 and n >= 256), then the first candidate
 // in index order with equal strong (generator.rs:127-133); verified hits to the output.
+// kWinLds false (k_scan_w): the windows are longer than the staged rows; hash them from
+// global memory.
+template <bool kWinLds = true>
 __device__ __forceinline__ void verify_l1(const ScanArgs& a, uint4* wq, uint32_t nwq, const uint32_t* rows,
                                           uint64_t tile_start, const SegCtx& cur) {
     if (!nwq) return;
     lds_fence();
     const uint32_t lane = threadIdx.x & 63;
-    if (a.n % 64 == 0 && a.n >= 256) {
+    if (kWinLds && a.n % 64 == 0 && a.n >= 256) {
         const uint32_t row = lane >> 4, rl = lane & 15;
         RowKeys K;
         row_keys(K);
@@ -1599,7 +1603,10 @@ __device__ __forceinline__ void verify_l1(const ScanArgs& a, uint4* wq, uint32_t
             uint64_t st;
             if (a.n > 240) {
                 uint32_t wk;
-                wave_hash_src(LdsRowBytes{rows, e.x}, a.n, wk, st);
+                if (kWinLds)
+                    wave_hash_src(LdsRowBytes{rows, e.x}, a.n, wk, st);
+                else
+                    wave_hash_long(cur.base + tile_start + e.x, a.n, wk, st);
             } else {
                 st = 0;
                 if (lane == 0) st = xxh3_short(cur.base + tile_start + e.x, a.n);
@@ -1641,6 +1648,7 @@ __device__ __forceinline__ void verify_l1(const ScanArgs& a, uint4* wq, uint32_t
 // Fat-table lookups of this wave's queued level-2 passes (all in the current tile),
 // 64 per round (positions at or past the segment end are dropped here); weak hits go
 // to wq, verified when wq cannot take another round and at the end.
+template <bool kWinLds = true>
 __device__ __forceinline__ void drain_l1(const ScanArgs& a, const uint2* fq, uint32_t nfq, uint4* wq,
                                          unsigned long long& weak_hits, const uint32_t* rows, uint64_t tile_start,
                                          const SegCtx& cur) {
@@ -1662,14 +1670,14 @@ __device__ __forceinline__ void drain_l1(const ScanArgs& a, const uint2* fq, uin
         const uint32_t cnt = __popcll(m);
         weak_hits += cnt;
         if (nwq + cnt > (uint32_t)kWQ3) {
-            verify_l1(a, wq, nwq, rows, tile_start, cur);
+            verify_l1<kWinLds>(a, wq, nwq, rows, tile_start, cur);
             nwq = 0;
         }
         const uint32_t rank = __popcll(m & ((1ull << lane) - 1));
         const uint4 e = make_uint4(tp, rec.y, rec.z, rec.w);  // a multi-candidate record names its global slot
         if (cnt > (uint32_t)kWQ3) {  // a round of more hits than wq holds (dense data): two halves
             if (hit && rank < (uint32_t)kWQ3) wq[rank] = e;
-            verify_l1(a, wq, kWQ3, rows, tile_start, cur);
+            verify_l1<kWinLds>(a, wq, kWQ3, rows, tile_start, cur);
             if (hit && rank >= (uint32_t)kWQ3) wq[rank - kWQ3] = e;
             nwq = cnt - kWQ3;
         } else {
@@ -1677,7 +1685,7 @@ __device__ __forceinline__ void drain_l1(const ScanArgs& a, const uint2* fq, uin
             nwq += cnt;
         }
     }
-    verify_l1(a, wq, nwq, rows, tile_start, cur);
+    verify_l1<kWinLds>(a, wq, nwq, rows, tile_start, cur);
     lds_fence();
 }
 
@@ -2005,6 +2013,374 @@ __global__ __launch_bounds__(kT3, 2) void k_scan_l1(ScanArgs a, uint32_t per, ui
     if (kTiming && lane == 0) atomicAdd(&a.counters[3], l1pass);
     if (kTiming && tid == 0)
         for (int k = 0; k < 6; ++k) atomicAdd(&a.counters[4 + k], tm[k]);
+}
+
+// ===========================================================================
+// K2+K4 for windows above kMaxN2: k_scan_w
+// ===========================================================================
+// sy's own block size is calculate_block_size(size) = sqrt(size) clamped to [512, 128 Ki]
+// (mod.rs:20-23, called at ssh.rs:951), so every file above 64 MiB is matched with a
+// window longer than the LDS-staged scans' tile.  Such a window does not fit the tile's
+// rows, so a tile of kTileW positions stages two byte regions instead of one: the bytes
+// that leave the tile's windows, [T0, T0 + kTileW) (rows 0..255), and the bytes that
+// enter them, [T0 + n, T0 + n + kTileW) (rows 256..512, staged from the 16-byte granule
+// that holds T0 + n, in-byte j at region offset o_n + j, o_n = n mod 16).  Windows are
+// carried from tile to tile instead of summed: the workgroup keeps (S, B) of the window
+// at T0, S = sum x, B = sum (n - i) x_i, and thread t's first window [T0 + 32t, +n)
+// follows in closed form (rolling.rs:66-79 applied d = 32t times):
+//   S(d) = S0 + In(d) - Out(d)
+//   B(d) = B0 + d S0 - n Out(d) + sum_{j<d} (d - j) in_j - sum_{j<d} (d - j) out_j
+// from prefix sums of the two regions' 32-byte halves (two wave scans each, the waves'
+// totals through LDS).  The window at a segment's first tile (or at the workgroup's
+// first) is summed from global memory.  The roll, the level-1 filter (kL1WordsWide words
+// in LDS, word q >> 18), the level-2 buffer loads and the fat-table drain are k_scan_l1's;
+// weak hits are verified from global memory (wave_hash_long: the window is not in LDS).
+constexpr int kTW = 512;                        // threads per workgroup (8 waves)
+constexpr int kRW = 32;                         // positions per thread = one 32-byte half
+constexpr int kTileW = kTW * kRW;               // 16384 positions per tile
+constexpr int kRowsW = 2 * (kTileW / 64) + 1;   // out rows 0..255, in rows 256..511, row 512: 16 bytes
+static_assert(kTileW == kTile2, "k_scan_w shares the host's tiling");
+
+struct LdsW {
+    uint32_t ntab, fq, wq, wt, red, l1, total;  // byte offsets
+};
+__host__ __device__ __forceinline__ LdsW ldsw_layout() {
+    LdsW L;
+    uint32_t o = kRowsW * kRowDw * 4;
+    o = (o + 15) & ~15u; L.ntab = o; o += 256 * 4;
+    L.fq = o; o += (kTW / 64) * kFQ3 * 8;
+    L.wq = o; o += (kTW / 64) * kWQ3 * 16;
+    L.wt = o; o += (kTW / 64) * 4 * 4;   // per wave: totals of its halves' four sums
+    L.red = o; o += (kTW / 64) * 16;     // per wave: a fresh window's (S, B) partial sums
+    o = (o + 15) & ~15u; L.l1 = o; o += kL1WordsWide * 4;
+    L.total = o;
+    return L;
+}
+
+// Byte sum and weighted sum (weights 0..4k-1) of the first k dwords of x, bytes below
+// `lim` only (lim <= 4k).
+__device__ __forceinline__ void half_sums(const uint32_t* x, int k, uint32_t lim, uint32_t& s, uint32_t& u) {
+    s = 0;
+    u = 0;
+    for (int i = 0; i < k; ++i) {
+        const uint32_t b = 4u * (uint32_t)i;
+        const uint32_t keep = lim >= b + 4 ? 0xFFFFFFFFu : lim <= b ? 0u : (0xFFFFFFFFu >> (8 * (b + 4 - lim)));
+        const uint32_t d = x[i] & keep;
+        s = udot4(d, 0x01010101u, s);
+        u = udot4(d, offw(i), u);
+    }
+}
+
+__global__ __launch_bounds__(kTW, 2) void k_scan_w(ScanArgs a, uint32_t per) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    const uint32_t n = a.n;
+    const LdsW L = ldsw_layout();
+    uint32_t* rows = (uint32_t*)smem;
+    uint32_t* ntab = (uint32_t*)(smem + L.ntab);
+    uint32_t* wt = (uint32_t*)(smem + L.wt);
+    unsigned long long* red = (unsigned long long*)(smem + L.red);
+    const uint32_t* l1 = (const uint32_t*)(smem + L.l1);
+    const uint32_t tid = threadIdx.x;
+    const uint32_t lane = tid & 63, wid = tid >> 6;
+    uint2* fq = (uint2*)(smem + L.fq) + (size_t)wid * kFQ3;
+    uint4* wq = (uint4*)(smem + L.wq) + (size_t)wid * kWQ3;
+
+    const uint32_t t_begin = blockIdx.x * per;
+    const uint32_t t_end = min(a.ntiles, t_begin + per);
+    if (t_begin >= t_end) return;
+    {
+        const uint4* g = (const uint4*)a.l1;
+        uint4* d = (uint4*)(smem + L.l1);
+#pragma unroll 4
+        for (uint32_t i = tid; i < kL1WordsWide / 4; i += kTW) d[i] = g[i];
+    }
+    for (uint32_t i = tid; i < 256; i += kTW) ntab[i] = kMod - 1 - (a.nm * i) % kMod;
+    const uint32_t on = n & 15;                      // in-byte 0 at in-region offset on
+    const uint32_t nal = n - on;                     // in-region start relative to T0
+    const uint32_t sh = n & 3;
+    const uint32_t rel0 = tid * kRW;
+    const uint32_t orow = (tid >> 1) * kRowDw + 8 * (tid & 1);  // this thread's first out dword
+    const uint32_t din0 = (kTileW + on + rel0) >> 2;            // ... and first in dword (rows 256..)
+    const uint32_t nmod = a.nm;
+    unsigned long long passes = 0, weak_hits = 0;
+    uint32_t nfq = 0;
+
+    auto seg_ctx = [&](uint32_t tile, uint32_t si0, SegCtx& sc, uint32_t& si, uint64_t& tile_start,
+                       uint64_t& seg_len) {
+        uint32_t lo = si0, hi = a.nsegs;
+        while (hi - lo > 1) {
+            const uint32_t mid = (lo + hi) >> 1;
+            if (a.segs[mid].tile_base <= tile) lo = mid; else hi = mid;
+        }
+        si = lo;
+        const ScanSeg S = a.segs[si];
+        const FileIx F = a.files[S.file];
+        sc.base = a.src + S.src;
+        sc.pos_begin = S.pos_begin;
+        sc.pos_end = S.pos_end;
+        sc.keys = a.keys + F.slot_off;
+        sc.fat = a.fat + F.slot_off;
+        sc.slot_off = F.slot_off;
+        sc.bmask = F.bmask;
+        sc.seg_id = si;
+        sc.fwshift = F.fwshift;
+        sc.filt = a.filt + F.filt_off;
+        sc.fwords = 1u << (32 - F.fwshift);
+        tile_start = S.pos_begin + (uint64_t)(tile - S.tile_base) * kTileW;
+        seg_len = S.len;
+    };
+    SegCtx sc, nsc;
+    uint32_t si = 0, nsi = 0;
+    uint64_t tile_start = 0, seg_len = 0, ntile_start = 0, nseg_len = 0;
+    seg_ctx(t_begin, 0, nsc, nsi, ntile_start, nseg_len);
+    // rows of the next tile, loaded ahead: thread c stages row c (c < 256: out bytes,
+    // else in bytes); thread 0 also the first 16 bytes of row 512
+    auto row_addr = [&](uint64_t t0, uint32_t c) -> uint64_t {
+        return c < (uint32_t)(kTileW / 64) ? t0 + 64ull * c : t0 + nal + 64ull * (c - kTileW / 64);
+    };
+    uint32_t x[16], xt[4] = {0, 0, 0, 0};
+    load_chunk_nt(nsc.base, nseg_len, row_addr(ntile_start, tid), x);
+    if (tid == 0) {
+        uint32_t y[16];
+        load_chunk_nt(nsc.base, nseg_len, row_addr(ntile_start, kRowsW - 1), y);
+        xt[0] = y[0]; xt[1] = y[1]; xt[2] = y[2]; xt[3] = y[3];
+    }
+    uint32_t S0 = 0, B0 = 0;  // window at tile_start: byte sum (exact) and B mod M
+    bool carried = false;     // (S0, B0) hold the window at this tile's start
+
+#pragma unroll 1
+    for (uint32_t tile = t_begin; tile < t_end; ++tile) {
+        sc = nsc;
+        si = nsi;
+        tile_start = ntile_start;
+        seg_len = nseg_len;
+        // ---- stage (the previous tile's last barrier ended every read of the rows)
+#pragma unroll
+        for (int i = 0; i < 16; ++i) rows[tid * kRowDw + i] = x[i];
+        if (tid == 0) {
+#pragma unroll
+            for (int i = 0; i < 4; ++i) rows[(kRowsW - 1) * kRowDw + i] = xt[i];
+        }
+        // a segment's first tile: its first window from global memory
+        if (!carried) {
+            uint64_t s = 0, b = 0;
+            for (uint32_t gr = tid; 16 * gr < n; gr += kTW) {
+                uint32_t y[16];
+                const uint64_t at = tile_start + 16ull * gr;
+                // 16 bytes at a 16-byte aligned offset (tile starts are), bytes past the
+                // window or the segment's source masked
+                const uint32_t lim = min(16u, n - 16 * gr);
+                load_chunk(sc.base, seg_len, at & ~63ull, y);
+                const uint32_t q = (uint32_t)((at >> 2) & 12);
+                for (int i = 0; i < 4; ++i) {
+                    const uint32_t bb = 4u * (uint32_t)i;
+                    const uint32_t keep = lim >= bb + 4 ? 0xFFFFFFFFu : lim <= bb ? 0u : (0xFFFFFFFFu >> (8 * (bb + 4 - lim)));
+                    const uint32_t d = y[q + i] & keep;
+                    const uint32_t ds = udot4(d, 0x01010101u, 0);
+                    const uint32_t du = udot4(d, offw(i), 0);  // weights bb .. bb+3
+                    s += ds;
+                    b += (uint64_t)(n - 16 * gr) * ds - du;    // sum (n - i) x_i over these bytes
+                }
+            }
+            s = wave_sum64(s);
+            b = wave_sum64(b);
+            if (lane == 0) { red[2 * wid] = s; red[2 * wid + 1] = b; }
+            __syncthreads();
+            uint64_t ts = 0, tb = 0;
+            for (int w = 0; w < kTW / 64; ++w) { ts += red[2 * w]; tb += red[2 * w + 1]; }
+            S0 = (uint32_t)ts;
+            B0 = (uint32_t)(tb % kMod);
+        }
+        __syncthreads();
+        // next tile's rows, issued now: their latency hides behind the window phase and the roll
+        const bool next_same = tile + 1 < t_end && !(nsi + 1 < a.nsegs && a.segs[nsi + 1].tile_base <= tile + 1);
+        if (tile + 1 < t_end) {
+            if (!next_same)
+                seg_ctx(tile + 1, nsi, nsc, nsi, ntile_start, nseg_len);  // the next segment
+            else
+                ntile_start = tile_start + kTileW;
+            load_chunk_nt(nsc.base, nseg_len, row_addr(ntile_start, tid), x);
+            if (tid == 0) {
+                uint32_t y[16];
+                load_chunk_nt(nsc.base, nseg_len, row_addr(ntile_start, kRowsW - 1), y);
+                xt[0] = y[0]; xt[1] = y[1]; xt[2] = y[2]; xt[3] = y[3];
+            }
+        }
+
+        // ---- window: half t of each region
+        uint32_t am, bm;
+        {
+            const uint32_t* ro = rows + orow;
+            const uint32_t* ri = rows + (kTileW / 64 + (tid >> 1)) * kRowDw + 8 * (tid & 1);
+            uint32_t so, uo, si_, ui, ps, pu;
+            half_sums(ro, 8, 32, so, uo);
+            half_sums(ri, 8, 32, si_, ui);
+            half_sums(ri, 4, on, ps, pu);  // the first `on` bytes of the in half
+            const uint32_t wo = (32u * tid * so + uo) % kMod;   // < 2^32: 32*511*8160 + 31*8160
+            const uint32_t wi = (32u * tid * si_ + ui) % kMod;
+            uint32_t Tso, Two, Tsi, Twi;
+            const uint32_t Eso = wave_scan_excl(so, Tso), Ewo = wave_scan_excl(wo, Two);
+            const uint32_t Esi = wave_scan_excl(si_, Tsi), Ewi = wave_scan_excl(wi, Twi);
+            if (lane == 0) { wt[4 * wid] = Tso; wt[4 * wid + 1] = Two; wt[4 * wid + 2] = Tsi; wt[4 * wid + 3] = Twi; }
+            // partial sums of the first `on` bytes of in-region half 0 and of row 512
+            uint32_t ps0, pu0, psT, puT;
+            half_sums(rows + (kTileW / 64) * kRowDw, 4, on, ps0, pu0);
+            half_sums(rows + (kRowsW - 1) * kRowDw, 4, on, psT, puT);
+            __syncthreads();
+            uint32_t Bso = 0, Bwo = 0, Bsi = 0, Bwi = 0, Aso = 0, Awo = 0, Asi = 0, Awi = 0;
+            for (uint32_t w = 0; w < (uint32_t)(kTW / 64); ++w) {
+                const uint4 v = *(const uint4*)(wt + 4 * w);
+                if (w < wid) { Bso += v.x; Bwo += v.y; Bsi += v.z; Bwi += v.w; }
+                Aso += v.x; Awo += v.y; Asi += v.z; Awi += v.w;
+            }
+            // window of position d (d = 32 t here, kTileW for the next tile's carry), from the
+            // region prefixes at half t: out sums Os (exact), Ow (mod M); in-region sums up to
+            // half t, Is (exact), Iw (mod M), and the partials (ps, pu) of the in half's
+            // first `on` bytes
+            auto window = [&](uint32_t d, uint32_t Os, uint32_t Ow, uint32_t Is, uint32_t Iw, uint32_t p_s,
+                              uint32_t p_u, uint32_t& A, uint32_t& B) {
+                const uint32_t Rs = Is + p_s;                                       // in-region bytes [0, on + d)
+                const uint64_t Rw = ((uint64_t)Iw + (uint64_t)d * p_s + p_u) % kMod; // their weighted sum
+                const uint32_t InS = Rs - ps0;                                      // in_j, j < d
+                const uint64_t Rw_d = (Rw + kMod - pu0 % kMod) % kMod;
+                // sum_{j<d} (d - j) in_j = (on + d) InS - (Rw(on + d) - Rw(on)) (mod M)
+                const uint64_t InW = ((uint64_t)(on + d) * InS + kMod - Rw_d) % kMod;
+                // sum_{j<d} (d - j) out_j = d Os - Ow (mod M)
+                const uint64_t OutW = ((uint64_t)d * Os + kMod - Ow % kMod) % kMod;
+                const uint32_t S = S0 + InS - Os;
+                uint64_t b = (uint64_t)B0 + (uint64_t)d * (S0 % kMod) + InW + kMod - OutW;
+                b += (uint64_t)kMod * kMod - (uint64_t)nmod * (Os % kMod);
+                A = S;
+                B = (uint32_t)(b % kMod);
+            };
+            uint32_t Sd, Bd;
+            window(32u * tid, Bso + Eso, (Bwo + Ewo) % kMod, Bsi + Esi, (Bwi + Ewi) % kMod, ps, pu, Sd, Bd);
+            am = (1 + Sd) % kMod;
+            bm = (n + Bd) % kMod;
+            // the next tile's first window, when it continues this segment
+            uint32_t Sn, Bn;
+            window((uint32_t)kTileW, Aso, Awo % kMod, Asi, Awi % kMod, psT, puT, Sn, Bn);
+            carried = next_same;
+            S0 = Sn;
+            B0 = Bn;
+        }
+
+        // ---- roll (k_scan_l1's; positions past pos_end are dropped by the drain)
+        const uint64_t fptr = (uint64_t)(uintptr_t)sc.filt;
+        const uint32_t fp_lo = __builtin_amdgcn_readfirstlane((uint32_t)fptr);
+        const uint32_t fp_hi = __builtin_amdgcn_readfirstlane((uint32_t)(fptr >> 32));
+        const __amdgpu_buffer_rsrc_t frsrc = __builtin_amdgcn_make_buffer_rsrc(
+            (void*)(uintptr_t)(((uint64_t)fp_hi << 32) | fp_lo), (short)0,
+            (int)__builtin_amdgcn_readfirstlane(sc.fwords * 4), 0x00020000);
+        const uint32_t fwshift = __builtin_amdgcn_readfirstlane(sc.fwshift);
+        auto compute = [&](uint32_t g, L1Batch& Bt) {
+            uint32_t xo[2], xi[2];
+            xo[0] = rows[orow + (g >> 2)];
+            xo[1] = rows[orow + (g >> 2) + 1];
+            {
+                uint32_t dw[3];
+#pragma unroll
+                for (int j = 0; j < 3; ++j) {
+                    const uint32_t d = din0 + (g >> 2) + j;
+                    dw[j] = rows[(d >> 4) * kRowDw + (d & 15)];
+                }
+                xi[0] = __builtin_amdgcn_alignbyte(dw[1], dw[0], sh);
+                xi[1] = __builtin_amdgcn_alignbyte(dw[2], dw[1], sh);
+            }
+            uint32_t ct[kB3], off[kB3], w1[kB3];
+#pragma unroll
+            for (int t = 0; t < kB3; ++t) ct[t] = ntab[(xo[t >> 2] >> (8 * (t & 3))) & 0xFF];
+#pragma unroll
+            for (int t = 0; t < kB3; ++t) {
+                const uint32_t out = (xo[t >> 2] >> (8 * (t & 3))) & 0xFF;
+                const uint32_t in = (xi[t >> 2] >> (8 * (t & 3))) & 0xFF;
+                __builtin_assume(am < kMod);
+                __builtin_assume(bm < kMod);
+                Bt.wv[t] = (bm << 16) | am;
+                const ProbeHash h = probe_hash(am, bm);
+                Bt.hq[t] = h.q;
+                off[t] = (h.r >> fwshift) * 4;
+                w1[t] = l1[h.q >> 18];
+                const uint32_t u = am + in + (kMod - out);  // [M-255, 2M+255)
+                am = min(u, min(u - kMod, u - 2 * kMod));
+                const uint32_t v = bm + am + ct[t];          // [0, 3M)
+                bm = min(v, min(v - kMod, v - 2 * kMod));
+            }
+#pragma unroll
+            for (int t = 0; t < kB3; ++t) {
+                const uint32_t p1 = l1_test(w1[t], Bt.hq[t]);
+                Bt.w2[t] = __builtin_amdgcn_raw_buffer_load_b32(frsrc, (int)(p1 ? off[t] : 0xFFFFFFFFu), 0, 0);
+            }
+        };
+        auto finish = [&](uint32_t g, L1Batch& Bt, uint32_t& todo) -> bool {
+            uint32_t pbits = 0;
+#pragma unroll
+            for (int t = 0; t < kB3; ++t) pbits |= (filt_pass(Bt.w2[t], Bt.hq[t]) ? 1u : 0u) << t;
+            asm volatile("" : "+v"(pbits));
+            const uint64_t below = (1ull << lane) - 1;
+            uint32_t need = 0;
+#pragma unroll
+            for (int t = 0; t < kB3; ++t)
+                if ((todo >> t) & 1) need += __popcll(__ballot((pbits >> t) & 1));
+            const bool all = nfq + need <= (uint32_t)kFQ3;
+            bool full = false;
+#pragma unroll
+            for (int t = 0; t < kB3; ++t) {
+                if (!((todo >> t) & 1) || full) continue;
+                const uint64_t mk = __ballot((pbits >> t) & 1);
+                if (!all && nfq + __popcll(mk) > (uint32_t)kFQ3) { full = true; continue; }
+                if ((pbits >> t) & 1) fq[nfq + __popcll(mk & below)] = make_uint2(rel0 + g + t, Bt.wv[t]);
+                nfq += __popcll(mk);
+                todo &= ~(1u << t);
+            }
+            if (all) todo = 0xFFu;
+            return all;
+        };
+        uint32_t stop = 4, todo = 0xFFu, ra = 0, rb = 0;
+        {
+            L1Batch b0, b1;
+            const uint32_t a0 = am, s0 = bm;
+            compute(0, b0);
+            const uint32_t a1 = am, s1 = bm;
+            compute(8, b1);
+            if (!finish(0, b0, todo)) { stop = 0; ra = a0; rb = s0; }
+            if (stop == 4) {
+                const uint32_t a2 = am, s2 = bm;
+                compute(16, b0);
+                if (!finish(8, b1, todo)) { stop = 1; ra = a1; rb = s1; }
+                if (stop == 4) {
+                    const uint32_t a3 = am, s3 = bm;
+                    compute(24, b1);
+                    if (!finish(16, b0, todo)) { stop = 2; ra = a2; rb = s2; }
+                    if (stop == 4 && !finish(24, b1, todo)) { stop = 3; ra = a3; rb = s3; }
+                }
+            }
+        }
+        while (stop < 4) {
+            passes += nfq;
+            drain_l1<false>(a, fq, nfq, wq, weak_hits, rows, tile_start, sc);
+            nfq = 0;
+            uint32_t k = stop;
+            stop = 4;
+            am = ra;
+            bm = rb;
+#pragma unroll 1
+            for (; k < 4; ++k) {
+                L1Batch bt;
+                const uint32_t ak = am, sk = bm;
+                compute(8 * k, bt);
+                if (!finish(8 * k, bt, todo)) { stop = k; ra = ak; rb = sk; break; }
+            }
+        }
+        if (nfq) {
+            passes += nfq;
+            drain_l1<false>(a, fq, nfq, wq, weak_hits, rows, tile_start, sc);
+            nfq = 0;
+        }
+        __syncthreads();  // rows (and wt) are rewritten by the next tile
+    }
+    if (lane == 0 && passes) atomicAdd(&a.counters[2], passes);
+    if (lane == 0 && weak_hits) atomicAdd(&a.counters[1], weak_hits);
 }
 
 // Tail rule (generator.rs:156-184): at p* = len - last_size (last_size < n), the
@@ -2968,6 +3344,10 @@ int scan_l1_mode() {
     const char* e = getenv("SYDELTA_SCAN_L1");
     return (e && e[0] == '0') ? 0 : (e && e[0] == '2') ? 2 : 1;
 }
+int scan_wide_mode() {
+    const char* e = getenv("SYDELTA_SCAN_WIDE");
+    return (e && e[0] == '0') ? 0 : 1;
+}
 
 hipError_t launch_signature(const uint8_t* d_buf, uint64_t len, uint64_t bs, uint32_t* d_weak, uint64_t* d_strong,
                             hipStream_t s, Profiler* prof) {
@@ -3035,7 +3415,7 @@ hipError_t launch_index_build(const uint32_t* d_weak, const uint64_t* d_strong, 
                               Profiler* prof) {
     hipError_t e;
     if ((e = hipMemsetAsync(ix.filt, 0, ix.fwords * 4, s))) return e;
-    if (ix.l1 && (e = hipMemsetAsync(ix.l1, 0, (size_t)ix.l1_parts * kL1Words * 4, s))) return e;
+    if (ix.l1 && (e = hipMemsetAsync(ix.l1, 0, ((size_t)ix.l1_parts << (32 - ix.l1_wshift)) * 4, s))) return e;
     if ((e = hipMemsetAsync(ix.keys, 0xFF, ix.nslots * 4, s))) return e;
     if ((e = hipMemsetAsync(ix.cnt, 0, ix.nslots * 4, s))) return e;
     const uint64_t n = ix.nblocks;
@@ -3043,7 +3423,7 @@ hipError_t launch_index_build(const uint32_t* d_weak, const uint64_t* d_strong, 
     {
         ProfScope ps(prof, s, "k_idx_insert");
         hipLaunchKernelGGL(k_idx_insert, dim3(grid_for(n, 256)), dim3(256), 0, s, d_weak, n, ix.d_fblk,
-                           (uint32_t)ix.nfiles, ix.d_files, ix.filt, ix.l1, ix.l1_parts, ix.keys, ix.cnt,
+                           (uint32_t)ix.nfiles, ix.d_files, ix.filt, ix.l1, ix.l1_parts, ix.l1_wshift, ix.keys, ix.cnt,
                            ix.slot_of);
     }
     size_t tmp = 0;
@@ -3121,7 +3501,8 @@ hipError_t launch_scan(const uint8_t* d_buf, const ScanSeg* d_segs, uint32_t nse
                        const DeviceIndex& ix, const uint64_t* d_strong, uint64_t* d_hit_key, uint32_t* d_hit_val,
                        uint64_t out_cap, unsigned long long* d_counters, uint2* gfq, size_t gfq_cap, hipStream_t s,
                        Profiler* prof) {
-    if (n > kMaxN2 || n == 0) return hipErrorInvalidValue;
+    if (n == 0) return hipErrorInvalidValue;
+    if (n > kMaxN2 && !(ix.l1 && ix.l1_wshift == 18 && ix.fat && ix.nfiles == 1)) return hipErrorInvalidValue;
     if (ntiles == 0) return hipSuccess;
     ScanArgs a{};
     a.src = d_buf;
@@ -3145,6 +3526,28 @@ hipError_t launch_scan(const uint8_t* d_buf, const ScanSeg* d_segs, uint32_t nse
     a.counters = d_counters;
     a.l1 = ix.l1;
     a.fat = ix.fat;
+    if (n > kMaxN2) {  // k_scan_w: windows above the LDS-staged layouts
+        static std::once_flag w_once;
+        static hipError_t w_err = hipSuccess;
+        static int w_cus = 256;
+        std::call_once(w_once, [] {
+            w_err = hipFuncSetAttribute((const void*)k_scan_w, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                        160 * 1024 - 256);
+            int dev = 0, cus = 0;
+            if (hipGetDevice(&dev) == hipSuccess &&
+                hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess && cus > 0)
+                w_cus = cus;
+        });
+        if (w_err != hipSuccess) return w_err;
+        const LdsW LW = ldsw_layout();
+        if (LW.total > 160u * 1024 - 256) return hipErrorInvalidValue;
+        // one workgroup per CU, contiguous tile ranges (a range's windows are carried)
+        const uint32_t grid = (uint32_t)std::min<uint64_t>(ntiles, (uint64_t)w_cus);
+        const uint32_t per = (ntiles + grid - 1) / grid;
+        ProfScope ps(prof, s, "k_scan_w");
+        hipLaunchKernelGGL(k_scan_w, dim3(grid), dim3(kTW), LW.total, s, a, per);
+        return hipGetLastError();
+    }
     static std::once_flag l1_once;
     static hipError_t l1_err = hipSuccess;
     static int l1_cus = 256;
@@ -3153,7 +3556,7 @@ hipError_t launch_scan(const uint8_t* d_buf, const ScanSeg* d_segs, uint32_t nse
     // covers, n = 4096 (the C3 shape; tests/test_gpu_scan_large.py).  Other sizes with a
     // large index go to k_scan_lds (production block sizes for files with more than
     // 16 Ki blocks are >= 8 KiB anyway: bs = sqrt(file size)).
-    if (ix.l1 && n == kMaxN3 && scan_l1_mode() != 0) {
+    if (ix.l1 && ix.l1_wshift == 17 && n == kMaxN3 && scan_l1_mode() != 0) {
         std::call_once(l1_once, [] {
             l1_err = hipFuncSetAttribute((const void*)k_scan_l1<false>, hipFuncAttributeMaxDynamicSharedMemorySize,
                                          160 * 1024 - 256);

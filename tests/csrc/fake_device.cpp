@@ -321,6 +321,10 @@ int scan_l1_mode() {
     const char* e = getenv("SYDELTA_SCAN_L1");
     return (e && e[0] == '0') ? 0 : (e && e[0] == '2') ? 2 : 1;
 }
+int scan_wide_mode() {
+    const char* e = getenv("SYDELTA_SCAN_WIDE");
+    return (e && e[0] == '0') ? 0 : 1;
+}
 uint32_t scan_max_window() { return 8192; }
 size_t scan_queue_entries() { return 1024; }
 
