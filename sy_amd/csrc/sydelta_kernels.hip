@@ -2383,6 +2383,297 @@ __global__ __launch_bounds__(kTW, 2) void k_scan_w(ScanArgs a, uint32_t per) {
     if (lane == 0 && weak_hits) atomicAdd(&a.counters[1], weak_hits);
 }
 
+// ===========================================================================
+// K2+K4, one stripe of positions per thread: k_scan_s (SYDELTA_SCAN_L1=3, opt-in)
+// ===========================================================================
+// k_scan_l1 shares each 16 Ki-position tile between all eight waves of a workgroup:
+// the tile's bytes are staged in LDS once, but every tile costs a window phase, a
+// drain whose fat-table round trip is on the critical path, and a barrier at which
+// the waves wait for the slowest drain.  Measured (round 3): two key-partition passes
+// with a third of the L2 requests each take 15 ms against 17.6 ms for one pass, so the
+// tile structure, not the L2 request rate, bounds it.  Here every thread rolls its own
+// contiguous stripe of positions (a run of kUS-position units, the window carried from
+// unit to unit), reading its bytes straight into registers (16 bytes of the leaving
+// stream and 32 of the entering one per 16 positions, one step ahead): no LDS rows, no
+// barrier after the level-1 filter copy, waves fully independent.
+// Level-2 passes queue per wave in LDS; a full queue is drained at once (fat-table
+// lookups, then XXH3 of the weak hits' windows from global memory, wave_hash_long).
+// Works for any window (the level-1 filter's size comes from the index: l1_wshift).
+constexpr int kTS = 512;                      // threads per workgroup (8 waves, 2 per SIMD)
+constexpr int kUS = 2048;                     // positions per unit
+constexpr int kUnitsPerTile = kTile2 / kUS;   // 8 (host tiles of kTile2 positions)
+constexpr int kFQS = 64;                      // level-2 passes queued per wave
+static_assert(kTile2 % kUS == 0, "units split host tiles");
+
+struct LdsS {
+    uint32_t ntab, fq, l1, total;
+};
+__host__ __device__ __forceinline__ LdsS lds_s_layout(uint32_t l1_words) {
+    LdsS L;
+    uint32_t o = 0;
+    L.ntab = o; o += 256 * 4;
+    L.fq = o; o += (kTS / 64) * kFQS * 16;
+    L.l1 = o; o += l1_words * 4;
+    L.total = o;
+    return L;
+}
+
+// 16 bytes at base + off (off % 16 == 0), zero when the granule starts at or past len.
+__device__ __forceinline__ uint4 ld16_nt(const uint8_t* base, uint64_t len, uint64_t off) {
+    uint4 v = make_uint4(0, 0, 0, 0);
+    if (off < len) {
+        const uint4* q = (const uint4*)(base + off);
+        v.x = __builtin_nontemporal_load(&q->x); v.y = __builtin_nontemporal_load(&q->y);
+        v.z = __builtin_nontemporal_load(&q->z); v.w = __builtin_nontemporal_load(&q->w);
+    }
+    return v;
+}
+
+// Drain this wave's queued level-2 passes {segment, position in segment, weak, -}: one
+// fat-table bucket read per pass (lane i: pass i), then for each weak hit the XXH3 of its
+// window from global memory and the first candidate in index order with equal strong
+// (generator.rs:121-155); verified hits to the output with one reservation per wave.
+__device__ __forceinline__ void drain_s(const ScanArgs& a, const uint4* fq, uint32_t nfq,
+                                        unsigned long long& weak_hits) {
+    const uint32_t lane = threadIdx.x & 63;
+    lds_fence();
+    bool hit = false;
+    uint4 rec = make_uint4(0, 0, 0, 0);
+    uint4 e = make_uint4(0, 0, 0, 0);
+    if (lane < nfq) {
+        e = fq[lane];
+        const ScanSeg S = a.segs[e.x];
+        const FileIx F = a.files[S.file];
+        hit = fat_find(a.fat + F.slot_off, F.bmask, e.z, rec);
+    }
+    uint64_t m = __ballot(hit);
+    weak_hits += __popcll(m);
+    uint32_t best = 0xFFFFFFFFu;
+    while (m) {  // wave-uniform: one window per weak hit
+        const uint32_t h = (uint32_t)__builtin_ctzll(m);
+        m &= m - 1;
+        const uint32_t seg = __builtin_amdgcn_readlane(e.x, h), rel = __builtin_amdgcn_readlane(e.y, h);
+        const uint32_t cand = __builtin_amdgcn_readlane(rec.y, h);
+        const uint64_t cst = ((uint64_t)__builtin_amdgcn_readlane(rec.w, h) << 32) | __builtin_amdgcn_readlane(rec.z, h);
+        const ScanSeg S = a.segs[seg];
+        const uint8_t* win = a.src + S.src + S.pos_begin + rel;
+        uint64_t st;
+        if (a.n > 240) {
+            uint32_t wk;
+            wave_hash_long(win, a.n, wk, st);
+        } else {
+            st = 0;
+            if (lane == 0) st = xxh3_short(win, a.n);
+            st = shfl64(st, 0);
+        }
+        uint32_t b;
+        if (!(cand & kMulti))
+            b = st == cst ? cand : 0xFFFFFFFFu;
+        else
+            b = first_strong_match(a.order, a.cstrong, a.start[cand & ~kMulti], a.cnt[cand & ~kMulti], st);
+        if (lane == h) best = b;
+    }
+    const bool v = best != 0xFFFFFFFFu;
+    const uint64_t mv = __ballot(v);
+    if (!mv) return;
+    unsigned long long k0 = 0;
+    if (lane == 0) k0 = atomicAdd(&a.counters[0], (unsigned long long)__popcll(mv));
+    k0 = shfl64(k0, 0);
+    const unsigned long long k = k0 + __popcll(mv & ((1ull << lane) - 1));
+    if (v && k < a.out_cap) {
+        a.hit_key[k] = ((uint64_t)e.x << kSegShift) | e.y;
+        a.hit_val[k] = best;
+    }
+}
+
+__global__ __launch_bounds__(kTS) void k_scan_s(ScanArgs a, uint64_t per, uint32_t l1_wshift) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    const uint32_t n = a.n;
+    const uint32_t l1_words = 1u << (32 - l1_wshift);
+    const LdsS L = lds_s_layout(l1_words);
+    uint32_t* ntab = (uint32_t*)(smem + L.ntab);
+    uint32_t* l1 = (uint32_t*)(smem + L.l1);
+    const uint32_t tid = threadIdx.x;
+    const uint32_t lane = tid & 63, wid = tid >> 6;
+    uint4* fq = (uint4*)(smem + L.fq) + (size_t)wid * kFQS;
+    {
+        const uint4* g = (const uint4*)a.l1;
+        uint4* d = (uint4*)l1;
+        for (uint32_t i = tid; i < l1_words / 4; i += kTS) d[i] = g[i];
+    }
+    for (uint32_t i = tid; i < 256; i += kTS) ntab[i] = kMod - 1 - (a.nm * i) % kMod;
+    __syncthreads();  // the only barrier: everything after is per wave
+
+    const uint64_t nunits = (uint64_t)a.ntiles * kUnitsPerTile;
+    const uint64_t u0 = ((uint64_t)blockIdx.x * kTS + tid) * per;
+    // the level-2 filter of file 0 (k_scan_s takes single-file indexes: uniform)
+    const FileIx F0 = a.files[0];
+    const uint64_t fptr = (uint64_t)(uintptr_t)(a.filt + F0.filt_off);
+    const uint32_t fp_lo = __builtin_amdgcn_readfirstlane((uint32_t)fptr);
+    const uint32_t fp_hi = __builtin_amdgcn_readfirstlane((uint32_t)(fptr >> 32));
+    const __amdgpu_buffer_rsrc_t frsrc = __builtin_amdgcn_make_buffer_rsrc(
+        (void*)(uintptr_t)(((uint64_t)fp_hi << 32) | fp_lo), (short)0,
+        (int)__builtin_amdgcn_readfirstlane((1u << (32 - F0.fwshift)) * 4), 0x00020000);
+    const uint32_t fwshift = __builtin_amdgcn_readfirstlane(F0.fwshift);
+    const uint32_t ds = (n & 15) >> 2, sh = n & 3;  // in-stream dword shift and byte shift (uniform)
+    unsigned long long passes = 0, weak_hits = 0;
+    uint32_t nfq = 0;
+    uint32_t am = 0, bm = 0;
+    uint32_t cur_seg = 0xFFFFFFFFu, next_base = 0;  // this lane's segment and the next one's first tile
+    bool carried = false;
+    ScanSeg S{};
+
+#pragma unroll 1
+    for (uint64_t k = 0; k < per; ++k) {  // wave-uniform trip count
+        const uint64_t u = u0 + k;
+        bool live = u < nunits;
+        uint64_t pos = 0;
+        uint32_t lim = 0;  // valid positions of this unit for this lane
+        if (live) {
+            const uint32_t tile = (uint32_t)(u / kUnitsPerTile);
+            if (cur_seg == 0xFFFFFFFFu || tile >= next_base) {
+                uint32_t lo = cur_seg == 0xFFFFFFFFu ? 0 : cur_seg, hi = a.nsegs;
+                while (hi - lo > 1) {
+                    const uint32_t mid = (lo + hi) >> 1;
+                    if (a.segs[mid].tile_base <= tile) lo = mid; else hi = mid;
+                }
+                if (lo != cur_seg) carried = false;
+                cur_seg = lo;
+                S = a.segs[lo];
+                next_base = lo + 1 < a.nsegs ? a.segs[lo + 1].tile_base : 0xFFFFFFFFu;
+            }
+            pos = S.pos_begin + (uint64_t)(tile - S.tile_base) * kTile2 + (u % kUnitsPerTile) * kUS;
+            live = pos < S.pos_end;
+            lim = live ? (uint32_t)min<uint64_t>((uint64_t)kUS, S.pos_end - pos) : 0u;
+        }
+        if (!live) carried = false;
+        const uint8_t* base = a.src + S.src;
+        const uint64_t len = S.len;
+        const uint32_t rel0 = live ? (uint32_t)(pos - S.pos_begin) : 0u;
+        // ---- the unit's first window: carried, or summed from global memory
+        if (live && !carried) {
+            uint64_t s = 0, b = 0;
+            for (uint32_t o = 0; o < n; o += 16) {
+                const uint4 v = ld16_nt(base, len, pos + o);
+                const uint32_t x4[4] = {v.x, v.y, v.z, v.w};
+                const uint32_t lim16 = min(16u, n - o);
+#pragma unroll
+                for (int i = 0; i < 4; ++i) {
+                    const uint32_t bb = 4u * (uint32_t)i;
+                    const uint32_t keep = lim16 >= bb + 4 ? 0xFFFFFFFFu : lim16 <= bb ? 0u
+                                          : (0xFFFFFFFFu >> (8 * (bb + 4 - lim16)));
+                    const uint32_t d = x4[i] & keep;
+                    const uint32_t dsum = udot4(d, 0x01010101u, 0);
+                    s += dsum;
+                    b += (uint64_t)(n - o) * dsum - udot4(d, offw(i), 0);
+                }
+            }
+            am = (uint32_t)((1 + s) % kMod);
+            bm = (uint32_t)((n + b) % kMod);
+        }
+        carried = live;
+        // ---- roll kUS positions, 16 per step (one 16-byte load of leaving bytes, two of
+        // entering ones, loaded a step ahead), batches of kB3 with the level-2 loads of the
+        // next batch in flight while a batch is tested
+        const uint64_t ia = (pos + n) & ~15ull;  // entering bytes: from the granule holding pos + n
+        uint4 o = ld16_nt(base, len, pos), i0 = ld16_nt(base, len, ia), i1 = ld16_nt(base, len, ia + 16);
+        uint4 po, qi0, qi1;  // the next step's
+        L1Batch cur, nxt;
+        uint32_t xo[4], xi[4];
+        auto bytes_of_step = [&]() {
+            xo[0] = o.x; xo[1] = o.y; xo[2] = o.z; xo[3] = o.w;
+            const uint32_t d[8] = {i0.x, i0.y, i0.z, i0.w, i1.x, i1.y, i1.z, i1.w};
+            uint32_t w[5];
+            // uniform dword shift: one of four straight-line selections
+            if (ds == 0) { for (int q = 0; q < 5; ++q) w[q] = d[q]; }
+            else if (ds == 1) { for (int q = 0; q < 5; ++q) w[q] = d[q + 1]; }
+            else if (ds == 2) { for (int q = 0; q < 5; ++q) w[q] = d[q + 2]; }
+            else { for (int q = 0; q < 5; ++q) w[q] = d[q + 3]; }
+#pragma unroll
+            for (int q = 0; q < 4; ++q) xi[q] = __builtin_amdgcn_alignbyte(w[q + 1], w[q], sh);
+        };
+        auto compute = [&](uint32_t t0, L1Batch& Bt) {  // positions t0 .. t0+7 of the step
+            uint32_t ct[kB3], off[kB3], w1[kB3];
+#pragma unroll
+            for (int t = 0; t < kB3; ++t) ct[t] = ntab[(xo[(t0 + t) >> 2] >> (8 * ((t0 + t) & 3))) & 0xFF];
+#pragma unroll
+            for (int t = 0; t < kB3; ++t) {
+                const uint32_t out = (xo[(t0 + t) >> 2] >> (8 * ((t0 + t) & 3))) & 0xFF;
+                const uint32_t in = (xi[(t0 + t) >> 2] >> (8 * ((t0 + t) & 3))) & 0xFF;
+                __builtin_assume(am < kMod);
+                __builtin_assume(bm < kMod);
+                Bt.wv[t] = (bm << 16) | am;
+                const ProbeHash h = probe_hash(am, bm);
+                Bt.hq[t] = h.q;
+                off[t] = (h.r >> fwshift) * 4;
+                w1[t] = l1[h.q >> l1_wshift];
+                const uint32_t uu = am + in + (kMod - out);  // [M-255, 2M+255)
+                am = min(uu, min(uu - kMod, uu - 2 * kMod));
+                const uint32_t vv = bm + am + ct[t];          // [0, 3M)
+                bm = min(vv, min(vv - kMod, vv - 2 * kMod));
+            }
+#pragma unroll
+            for (int t = 0; t < kB3; ++t) {
+                const uint32_t p1 = l1_test(w1[t], Bt.hq[t]);
+                Bt.w2[t] = __builtin_amdgcn_raw_buffer_load_b32(frsrc, (int)(p1 ? off[t] : 0xFFFFFFFFu), 0, 0);
+            }
+        };
+        // queue batch Bt (unit positions j0 .. j0+7) while the queue has room; false when
+        // it filled (todo: the positions still to queue)
+        auto finish = [&](uint32_t j0, const L1Batch& Bt, uint32_t& todo) -> bool {
+            uint32_t pbits = 0;
+#pragma unroll
+            for (int t = 0; t < kB3; ++t)
+                pbits |= ((filt_pass(Bt.w2[t], Bt.hq[t]) && j0 + t < lim) ? 1u : 0u) << t;
+            asm volatile("" : "+v"(pbits));
+            const uint64_t below = (1ull << lane) - 1;
+#pragma unroll
+            for (int t = 0; t < kB3; ++t) {
+                if (!((todo >> t) & 1)) continue;
+                const uint64_t mk = __ballot((pbits >> t) & 1);
+                if (nfq + __popcll(mk) > (uint32_t)kFQS) return false;
+                if ((pbits >> t) & 1) fq[nfq + __popcll(mk & below)] = make_uint4(cur_seg, rel0 + j0 + t, Bt.wv[t], 0);
+                nfq += __popcll(mk);
+                passes += __popcll(mk);
+                todo &= ~(1u << t);
+            }
+            return true;
+        };
+        bytes_of_step();
+        compute(0, cur);
+#pragma unroll 1
+        for (uint32_t j = 0; j < (uint32_t)kUS; j += 16) {
+            const bool more = j + 16 < (uint32_t)kUS;
+            if (more) {  // the next step's bytes
+                po = ld16_nt(base, len, pos + j + 16);
+                qi0 = ld16_nt(base, len, ia + j + 16);
+                qi1 = ld16_nt(base, len, ia + j + 32);
+            }
+            compute(kB3, nxt);  // second batch of this step
+            uint32_t todo = 0xFFu;
+            while (!finish(j, cur, todo)) {  // a full queue: drain it and finish the batch
+                drain_s(a, fq, nfq, weak_hits);
+                nfq = 0;
+            }
+            cur = nxt;
+            if (more) {
+                o = po; i0 = qi0; i1 = qi1;
+                bytes_of_step();
+                compute(0, nxt);  // first batch of the next step
+            }
+            todo = 0xFFu;
+            while (!finish(j + kB3, cur, todo)) {
+                drain_s(a, fq, nfq, weak_hits);
+                nfq = 0;
+            }
+            cur = nxt;
+        }
+    }
+    if (nfq) drain_s(a, fq, nfq, weak_hits);
+    if (lane == 0 && passes) atomicAdd(&a.counters[2], passes);
+    if (lane == 0 && weak_hits) atomicAdd(&a.counters[1], weak_hits);
+}
+
 // Tail rule (generator.rs:156-184): at p* = len - last_size (last_size < n), the
 // suffix matches the last basis block iff weak and strong are equal.  One wave per
 // job (file).
@@ -3342,11 +3633,11 @@ static inline unsigned grid_for(uint64_t threads, unsigned block) { return (unsi
 // partition (l1_part).
 int scan_l1_mode() {
     const char* e = getenv("SYDELTA_SCAN_L1");
-    return (e && e[0] == '0') ? 0 : (e && e[0] == '2') ? 2 : 1;
+    return (e && e[0] == '0') ? 0 : (e && e[0] == '2') ? 2 : (e && e[0] == '3') ? 3 : 1;
 }
 int scan_wide_mode() {
     const char* e = getenv("SYDELTA_SCAN_WIDE");
-    return (e && e[0] == '0') ? 0 : 1;
+    return (e && e[0] == '0') ? 0 : (e && e[0] == '2') ? 2 : 1;
 }
 
 hipError_t launch_signature(const uint8_t* d_buf, uint64_t len, uint64_t bs, uint32_t* d_weak, uint64_t* d_strong,
@@ -3526,6 +3817,34 @@ hipError_t launch_scan(const uint8_t* d_buf, const ScanSeg* d_segs, uint32_t nse
     a.counters = d_counters;
     a.l1 = ix.l1;
     a.fat = ix.fat;
+    // k_scan_s (opt-in: SYDELTA_SCAN_L1=3 for the C3 shape, SYDELTA_SCAN_WIDE=2 for wide
+    // windows): one stripe of positions per thread, any window
+    if (ix.l1 && ix.fat && ix.nfiles == 1 && ix.l1_parts == 1 &&
+        ((n == kMaxN3 && ix.l1_wshift == 17 && scan_l1_mode() == 3) || (n > kMaxN2 && scan_wide_mode() == 2))) {
+        static std::once_flag s_once;
+        static hipError_t s_err = hipSuccess;
+        static int s_cus = 256;
+        std::call_once(s_once, [] {
+            s_err = hipFuncSetAttribute((const void*)k_scan_s, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                        160 * 1024 - 256);
+            int dev = 0, cus = 0;
+            if (hipGetDevice(&dev) == hipSuccess &&
+                hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess && cus > 0)
+                s_cus = cus;
+        });
+        if (s_err != hipSuccess) return s_err;
+        const LdsS LS = lds_s_layout(1u << (32 - ix.l1_wshift));
+        if (LS.total > 160u * 1024 - 256) return hipErrorInvalidValue;
+        const uint64_t nunits = (uint64_t)ntiles * kUnitsPerTile;
+        const uint64_t threads = (uint64_t)s_cus * kTS;
+        // few units (an on-demand rescan): fewer workgroups, one unit per thread
+        const uint64_t per = (nunits + threads - 1) / threads;
+        const uint32_t grid = (uint32_t)std::min<uint64_t>((uint64_t)s_cus, (nunits + (uint64_t)kTS * per - 1) /
+                                                                             ((uint64_t)kTS * per));
+        ProfScope ps(prof, s, "k_scan_s");
+        hipLaunchKernelGGL(k_scan_s, dim3(grid), dim3(kTS), LS.total, s, a, per, ix.l1_wshift);
+        return hipGetLastError();
+    }
     if (n > kMaxN2) {  // k_scan_w: windows above the LDS-staged layouts
         static std::once_flag w_once;
         static hipError_t w_err = hipSuccess;

@@ -1,7 +1,8 @@
 """GPU parity of the wide-window scan k_scan_w (windows above 8 KiB: sy's own block
 size calculate_block_size = sqrt(file size) for every file over 64 MiB, mod.rs:20-23)
 against the C restatement of generator.rs, and against the per-thread k_scan it
-replaces (SYDELTA_SCAN_WIDE=0, which also turns the aligned probe off).
+replaces (SYDELTA_SCAN_WIDE=0, which also turns the aligned probe off); every case
+also through the stripe-per-thread k_scan_s (SYDELTA_SCAN_WIDE=2).
 
 * every n mod 16 class that matters (8193, 9999, 16384, 31622, 65536, 131071, 131072):
   random edits (substitutions, insertions, deletions, block moves) over several tiles,
@@ -22,6 +23,15 @@ import pytest
 from oracle import oracle as O
 
 pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(params=[k for k in ["w", "s"] if k in os.environ.get("SYDELTA_TEST_SCANNERS", "w,s").split(",")],
+                autouse=True)
+def wide_kernel(request, monkeypatch):
+    """k_scan_w (default) or the stripe-per-thread k_scan_s (SYDELTA_SCAN_WIDE=2); read
+    when the index is built and per launch."""
+    monkeypatch.setenv("SYDELTA_SCAN_WIDE", {"w": "1", "s": "2"}[request.param])
+    return request.param
 
 WIDE = [8193, 9999, 16384, 31622, 65536, 131071, 131072]
 
