@@ -2454,7 +2454,10 @@ __device__ __forceinline__ void drain_s(const ScanArgs& a, const uint4* fq, uint
         m &= m - 1;
         const uint32_t seg = __builtin_amdgcn_readlane(e.x, h), rel = __builtin_amdgcn_readlane(e.y, h);
         const uint32_t cand = __builtin_amdgcn_readlane(rec.y, h);
-        const uint64_t cst = ((uint64_t)__builtin_amdgcn_readlane(rec.w, h) << 32) | __builtin_amdgcn_readlane(rec.z, h);
+        // readlane returns int: widen through uint32_t, or bit 31 of the low half would
+        // sign-extend over the high half
+        const uint64_t cst = ((uint64_t)(uint32_t)__builtin_amdgcn_readlane(rec.w, h) << 32) |
+                             (uint32_t)__builtin_amdgcn_readlane(rec.z, h);
         const ScanSeg S = a.segs[seg];
         const uint8_t* win = a.src + S.src + S.pos_begin + rel;
         uint64_t st;
