@@ -980,16 +980,7 @@ int Classifier::scan(const std::vector<std::array<uint64_t, 3>>& ranges) {
     uint64_t cap = 0;
     unsigned long long counts[16] = {0};
     DevBuf hit_buf;
-    // k_scan_l1's deferred pass list (SYDELTA_SCAN_DEFER=1): one record per 64 positions;
-    // when a scan lists more (dense data) it is rescanned with verification in the tiles
-    DevBuf pass_buf;
-    uint64_t pass_cap = 0;
-    if (!wide && scan_defer_mode() && ix->ix.l1 && ix->ix.l1_wshift == 17) {
-        pass_cap = std::max<uint64_t>(1 << 16, tot_pos / 64);
-        HIP_TRY(dev_malloc_async(&pass_buf.p, pass_cap * 16, s));
-        pass_buf.s = s;
-    }
-    for (int attempt = 0; attempt < 3; ++attempt) {
+    for (int attempt = 0; attempt < 2; ++attempt) {
         if (want > cap) {
             if (hit_buf.p) { (void)hipFreeAsync(hit_buf.p, s); hit_buf.p = nullptr; }
             cap = want;
@@ -1003,7 +994,7 @@ int Classifier::scan(const std::vector<std::array<uint64_t, 3>>& ranges) {
         if (!wide) {
             HIP_TRY(launch_scan(base, (const ScanSeg*)seg_buf.p, (uint32_t)segs.size(), (uint32_t)ntiles,
                                 (uint32_t)n, ix->ix, ix->d_strong, d_key, d_val, cap, d_counts, (uint2*)q_buf.p, qcap,
-                                s, prof, (uint4*)pass_buf.p, pass_cap));
+                                s, prof));
         } else {
             for (size_t g = 0; g < segs.size(); ++g)
                 HIP_TRY(launch_scan_wide(base + segs[g].src, segs[g].len, segs[g].pos_begin, segs[g].pos_end,
@@ -1018,10 +1009,6 @@ int Classifier::scan(const std::vector<std::array<uint64_t, 3>>& ranges) {
                             " %llu %llu l1 passes %llu passes %llu weak %llu positions %llu\n",
                     counts[4], counts[5], counts[6], counts[7], counts[8], counts[9], counts[3], counts[2], counts[1],
                     (unsigned long long)tot_pos);
-        if (pass_cap && counts[12] > pass_cap) {  // the pass list overflowed: rescan, verifying in the tiles
-            pass_cap = 0;
-            continue;
-        }
         if (counts[0] <= cap) break;
         want = counts[0];  // dense hits: grow once and rescan
     }

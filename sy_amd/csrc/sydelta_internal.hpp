@@ -114,14 +114,10 @@ uint32_t scan_max_window();      // largest block size the LDS-staged scan handl
 // entries (2 workgroups per CU on up to 256 CUs; launch_scan checks).
 size_t scan_queue_entries();
 // Scan all tiles of segs[0..nsegs) (device copy d_segs; block_size n <= scan_max_window()).
-// gpass / gpass_cap: k_scan_l1's deferred pass list (SYDELTA_SCAN_DEFER=1; null: verify
-// in the tile drains).  counters[12] = passes listed (> gpass_cap: the list overflowed and
-// the scan must be redone without it), counters[13] = k_pass_verify's work counter.
 hipError_t launch_scan(const uint8_t* d_buf, const ScanSeg* d_segs, uint32_t nsegs, uint32_t ntiles, uint32_t n,
                        const DeviceIndex& ix, const uint64_t* d_strong, uint64_t* d_hit_key, uint32_t* d_hit_val,
                        uint64_t out_cap, unsigned long long* d_counters, uint2* gfq, size_t gfq_cap, hipStream_t s,
-                       Profiler* prof, uint4* gpass = nullptr, uint64_t gpass_cap = 0);
-bool scan_defer_mode();  // SYDELTA_SCAN_DEFER=1: k_scan_l1 lists its passes for k_pass_verify
+                       Profiler* prof);
 // Fallback for block sizes above scan_max_window(): one segment, file 0 of ix, hits
 // keyed with seg_id.
 hipError_t launch_scan_wide(const uint8_t* d_src, uint64_t len, uint64_t pos_begin, uint64_t pos_end, uint32_t seg_id,

@@ -1716,39 +1716,11 @@ struct L1Batch {
     uint32_t w2[kB3], hq[kB3], wv[kB3];
 };
 
-// Deferred verification (k_scan_l1<_, true>, SYDELTA_SCAN_DEFER): the wave's queued
-// level-2 passes {position in tile, weak} go to a global list of {segment, position in
-// segment, weak, -} records instead of being looked up and verified in the tile's
-// drain; k_pass_verify does both afterwards.  counters[12] counts every pass (also those
-// past `cap`, which the host then rescans without deferral), counters[14] holds cap.
-__device__ __forceinline__ void flush_passes(const ScanArgs& a, const uint2* fq, uint32_t nfq, uint64_t tile_start,
-                                             const SegCtx& cur, uint4* __restrict__ gpass, uint64_t cap) {
-    const uint32_t lane = threadIdx.x & 63;
-    lds_fence();
-    for (uint32_t base = 0; base < nfq; base += 64) {
-        const uint32_t i = base + lane;
-        uint2 e = make_uint2(0, 0);
-        bool v = false;
-        if (i < nfq) {
-            e = fq[i];
-            v = tile_start + e.x < cur.pos_end;  // the last tile's positions past the segment
-        }
-        const uint64_t m = __ballot(v);
-        if (!m) continue;
-        unsigned long long k0 = 0;
-        if (lane == 0) k0 = atomicAdd(&a.counters[12], (unsigned long long)__popcll(m));
-        k0 = shfl64(k0, 0);
-        const unsigned long long k = k0 + __popcll(m & ((1ull << lane) - 1));
-        if (v && k < cap) gpass[k] = make_uint4(cur.seg_id, (uint32_t)(tile_start + e.x - cur.pos_begin), e.y, 0u);
-    }
-}
-
 // part / pmask: the key partition this pass tests (pmask 0: one partition, every position).
 // kTiming: the SYDELTA_PHASE_TIMING instantiation (phase cycles and level-1 passes
 // counted); the production one carries no timing code in its hot loop.
-template <bool kTiming, bool kDefer>
-__global__ __launch_bounds__(kT3, 2) void k_scan_l1(ScanArgs a, uint32_t per, uint32_t part, uint32_t pmask,
-                                                    uint4* __restrict__ gpass, uint64_t gcap) {
+template <bool kTiming>
+__global__ __launch_bounds__(kT3, 2) void k_scan_l1(ScanArgs a, uint32_t per, uint32_t part, uint32_t pmask) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     const uint32_t n = a.n;
     const Lds3 L = lds3_layout(n);
@@ -2010,10 +1982,7 @@ __global__ __launch_bounds__(kT3, 2) void k_scan_l1(ScanArgs a, uint32_t per, ui
         }
         while (stop < 4) {
             passes += nfq;
-            if (kDefer)
-                flush_passes(a, fq, nfq, tile_start, sc, gpass, gcap);
-            else
-                drain_l1(a, fq, nfq, wq, weak_hits, rows, tile_start, sc);
+            drain_l1(a, fq, nfq, wq, weak_hits, rows, tile_start, sc);
             nfq = 0;
             uint32_t k = stop;
             stop = 4;
@@ -2029,12 +1998,9 @@ __global__ __launch_bounds__(kT3, 2) void k_scan_l1(ScanArgs a, uint32_t per, ui
         }
         PHASE_MARK3(2)
         PHASE_MARK3(3)
-        if (nfq) {  // the tile's weak hits are verified while its bytes are in LDS (or deferred)
+        if (nfq) {  // the tile's weak hits are verified while its bytes are in LDS
             passes += nfq;
-            if (kDefer)
-                flush_passes(a, fq, nfq, tile_start, sc, gpass, gcap);
-            else
-                drain_l1(a, fq, nfq, wq, weak_hits, rows, tile_start, sc);
+            drain_l1(a, fq, nfq, wq, weak_hits, rows, tile_start, sc);
             nfq = 0;
         }
         PHASE_MARK3(4)
@@ -2467,21 +2433,15 @@ __device__ __forceinline__ uint4 ld16_nt(const uint8_t* base, uint64_t len, uint
 // fat-table bucket read per pass (lane i: pass i), then for each weak hit the XXH3 of its
 // window from global memory and the first candidate in index order with equal strong
 // (generator.rs:121-155); verified hits to the output with one reservation per wave.
-__device__ __forceinline__ void verify_entries(const ScanArgs& a, uint4 e, bool have,
-                                               unsigned long long& weak_hits);
 __device__ __forceinline__ void drain_s(const ScanArgs& a, const uint4* fq, uint32_t nfq,
                                         unsigned long long& weak_hits) {
     const uint32_t lane = threadIdx.x & 63;
     lds_fence();
-    verify_entries(a, lane < nfq ? fq[lane] : make_uint4(0, 0, 0, 0), lane < nfq, weak_hits);
-}
-// Lane i holds pass record e {segment, position in segment, weak, -} when `have`.
-__device__ __forceinline__ void verify_entries(const ScanArgs& a, uint4 e, bool have,
-                                               unsigned long long& weak_hits) {
-    const uint32_t lane = threadIdx.x & 63;
     bool hit = false;
     uint4 rec = make_uint4(0, 0, 0, 0);
-    if (have) {
+    uint4 e = make_uint4(0, 0, 0, 0);
+    if (lane < nfq) {
+        e = fq[lane];
         const ScanSeg S = a.segs[e.x];
         const FileIx F = a.files[S.file];
         hit = fat_find(a.fat + F.slot_off, F.bmask, e.z, rec);
@@ -2527,23 +2487,6 @@ __device__ __forceinline__ void verify_entries(const ScanArgs& a, uint4 e, bool 
         a.hit_key[k] = ((uint64_t)e.x << kSegShift) | e.y;
         a.hit_val[k] = best;
     }
-}
-
-// Deferred verification of k_scan_l1<_, true>'s pass list: waves take 64 records at a
-// time from a work counter (counters[13]) until min(counters[12], cap) are done.
-__global__ __launch_bounds__(256) void k_pass_verify(ScanArgs a, const uint4* __restrict__ gpass, uint64_t cap) {
-    const uint32_t lane = threadIdx.x & 63;
-    const uint64_t count = min((uint64_t)a.counters[12], cap);
-    unsigned long long weak_hits = 0;
-    for (;;) {
-        unsigned long long b0 = 0;
-        if (lane == 0) b0 = atomicAdd(&a.counters[13], 64ull);
-        b0 = shfl64(b0, 0);
-        if (b0 >= count) break;
-        const bool have = b0 + lane < count;
-        verify_entries(a, have ? gpass[b0 + lane] : make_uint4(0, 0, 0, 0), have, weak_hits);
-    }
-    if (lane == 0 && weak_hits) atomicAdd(&a.counters[1], weak_hits);
 }
 
 __global__ __launch_bounds__(kTS) void k_scan_s(ScanArgs a, uint64_t per, uint32_t l1_wshift) {
@@ -3695,10 +3638,6 @@ int scan_l1_mode() {
     const char* e = getenv("SYDELTA_SCAN_L1");
     return (e && e[0] == '0') ? 0 : (e && e[0] == '2') ? 2 : (e && e[0] == '3') ? 3 : 1;
 }
-bool scan_defer_mode() {
-    const char* e = getenv("SYDELTA_SCAN_DEFER");
-    return e && e[0] == '1';
-}
 int scan_wide_mode() {
     const char* e = getenv("SYDELTA_SCAN_WIDE");
     return (e && e[0] == '0') ? 0 : (e && e[0] == '2') ? 2 : 1;
@@ -3855,7 +3794,7 @@ size_t scan_queue_entries() { return (size_t)kWgPerCuMax2 * 256 * (kT2 / 64) * k
 hipError_t launch_scan(const uint8_t* d_buf, const ScanSeg* d_segs, uint32_t nsegs, uint32_t ntiles, uint32_t n,
                        const DeviceIndex& ix, const uint64_t* d_strong, uint64_t* d_hit_key, uint32_t* d_hit_val,
                        uint64_t out_cap, unsigned long long* d_counters, uint2* gfq, size_t gfq_cap, hipStream_t s,
-                       Profiler* prof, uint4* gpass, uint64_t gpass_cap) {
+                       Profiler* prof) {
     if (n == 0) return hipErrorInvalidValue;
     if (n > kMaxN2 && !(ix.l1 && ix.l1_wshift == 18 && ix.fat && ix.nfiles == 1)) return hipErrorInvalidValue;
     if (ntiles == 0) return hipSuccess;
@@ -3941,11 +3880,11 @@ hipError_t launch_scan(const uint8_t* d_buf, const ScanSeg* d_segs, uint32_t nse
     // 16 Ki blocks are >= 8 KiB anyway: bs = sqrt(file size)).
     if (ix.l1 && ix.l1_wshift == 17 && n == kMaxN3 && scan_l1_mode() != 0) {
         std::call_once(l1_once, [] {
-            const void* fns[4] = {(const void*)k_scan_l1<false, false>, (const void*)k_scan_l1<true, false>,
-                                  (const void*)k_scan_l1<false, true>, (const void*)k_scan_l1<true, true>};
-            for (const void* f : fns)
-                if (l1_err == hipSuccess)
-                    l1_err = hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024 - 256);
+            l1_err = hipFuncSetAttribute((const void*)k_scan_l1<false>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                         160 * 1024 - 256);
+            if (l1_err == hipSuccess)
+                l1_err = hipFuncSetAttribute((const void*)k_scan_l1<true>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                             160 * 1024 - 256);
             int dev = 0, cus = 0;
             if (hipGetDevice(&dev) == hipSuccess &&
                 hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess && cus > 0)
@@ -3956,29 +3895,13 @@ hipError_t launch_scan(const uint8_t* d_buf, const ScanSeg* d_segs, uint32_t nse
         // one workgroup per CU (the level-1 filter fills its LDS), contiguous tile ranges
         const uint32_t grid = (uint32_t)std::min<uint64_t>(ntiles, (uint64_t)l1_cus);
         const uint32_t per = (ntiles + grid - 1) / grid;
-        // deferred verification (SYDELTA_SCAN_DEFER=1): the pass list holds up to one record
-        // per 64 positions; a denser scan overflows it and the host rescans without it
-        const bool defer = scan_defer_mode() && gpass && gpass_cap;
         // one pass per key partition (the index's level-1 filters), each over every tile
         for (uint32_t part = 0; part < ix.l1_parts; ++part) {
             ProfScope ps(prof, s, "k_scan_l1");
-            const uint32_t pm = ix.l1_parts - 1;
-            if (defer) {
-                if (a.timing)
-                    hipLaunchKernelGGL((k_scan_l1<true, true>), dim3(grid), dim3(kT3), L3.total, s, a, per, part, pm, gpass, gpass_cap);
-                else
-                    hipLaunchKernelGGL((k_scan_l1<false, true>), dim3(grid), dim3(kT3), L3.total, s, a, per, part, pm, gpass, gpass_cap);
-            } else {
-                if (a.timing)
-                    hipLaunchKernelGGL((k_scan_l1<true, false>), dim3(grid), dim3(kT3), L3.total, s, a, per, part, pm, nullptr, 0ull);
-                else
-                    hipLaunchKernelGGL((k_scan_l1<false, false>), dim3(grid), dim3(kT3), L3.total, s, a, per, part, pm, nullptr, 0ull);
-            }
-            if (hipError_t e = hipGetLastError()) return e;
-        }
-        if (defer) {
-            ProfScope ps(prof, s, "k_pass_verify");
-            hipLaunchKernelGGL(k_pass_verify, dim3((uint32_t)l1_cus * 8), dim3(256), 0, s, a, (const uint4*)gpass, gpass_cap);
+            if (a.timing)
+                hipLaunchKernelGGL(k_scan_l1<true>, dim3(grid), dim3(kT3), L3.total, s, a, per, part, ix.l1_parts - 1);
+            else
+                hipLaunchKernelGGL(k_scan_l1<false>, dim3(grid), dim3(kT3), L3.total, s, a, per, part, ix.l1_parts - 1);
             if (hipError_t e = hipGetLastError()) return e;
         }
         return hipSuccess;

@@ -321,7 +321,6 @@ int scan_l1_mode() {
     const char* e = getenv("SYDELTA_SCAN_L1");
     return (e && e[0] == '0') ? 0 : (e && e[0] == '2') ? 2 : 1;
 }
-bool scan_defer_mode() { return false; }
 int scan_wide_mode() {
     const char* e = getenv("SYDELTA_SCAN_WIDE");
     return (e && e[0] == '0') ? 0 : 1;
@@ -331,8 +330,7 @@ size_t scan_queue_entries() { return 1024; }
 
 hipError_t launch_scan(const uint8_t* d_buf, const ScanSeg* d_segs, uint32_t nsegs, uint32_t, uint32_t n,
                        const DeviceIndex& ix, const uint64_t*, uint64_t* d_hit_key, uint32_t* d_hit_val,
-                       uint64_t out_cap, unsigned long long* d_counters, uint2*, size_t, hipStream_t, Profiler*,
-                       uint4*, uint64_t) {
+                       uint64_t out_cap, unsigned long long* d_counters, uint2*, size_t, hipStream_t, Profiler*) {
     EmuTimer emu_t;
     const FakeIndex& F = find_ix(ix);
     for (uint32_t g = 0; g < nsegs; ++g) {
