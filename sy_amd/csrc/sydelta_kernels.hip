@@ -593,6 +593,8 @@ struct ScanArgs {
     uint32_t nm;         // n mod M
     uint32_t c0;         // 2M - 1 - (255*nm mod M)    (k_scan)
     uint32_t timing;     // accumulate per-phase s_memtime cycles of wave 0 into counters[4..8)
+    uint32_t ablate;     // SYDELTA_ABLATE (measurement only, wrong results): k_scan_l1 bit 0 skips the
+                         // drains, bit 1 the level-2 loads, bit 2 the window phase
     // k_scan_lds: segment table and per-file probe offsets
     const ScanSeg* segs;
     uint32_t nsegs;
@@ -1822,8 +1824,8 @@ __global__ __launch_bounds__(kT3, 2) void k_scan_l1(ScanArgs a, uint32_t per, ui
 
         // ---- window: lane l of wave w starts at half t = 64w + l (tile offset 32t);
         // halves t + 64j, j = 0..2, cover its window [32t, 32t + n) (m32 <= 128)
-        uint32_t am, bm;
-        {
+        uint32_t am = tid, bm = lane;
+        if (!(a.ablate & 4)) {
             uint32_t S[3], V[3], J[3], TS[3], TV[3], TJ[3];
 #pragma unroll
             for (int j = 0; j < 3; ++j) {
@@ -1924,7 +1926,8 @@ __global__ __launch_bounds__(kT3, 2) void k_scan_l1(ScanArgs a, uint32_t per, ui
                 if (kTiming) l1pass += __popcll(__ballot(p1));
                 // a level-1 miss asks for an offset past the buffer: no request, reads 0
                 // (and filt_pass(0, q) is false)
-                Bt.w2[t] = __builtin_amdgcn_raw_buffer_load_b32(frsrc, (int)(p1 ? off[t] : 0xFFFFFFFFu), 0, 0);
+                Bt.w2[t] = __builtin_amdgcn_raw_buffer_load_b32(frsrc, (int)(p1 && !(a.ablate & 2) ? off[t] : 0xFFFFFFFFu),
+                                                                0, 0);
             }
         };
         // Queue the level-2 passes of batch g's positions still in `todo` (per-wave LDS
@@ -1982,7 +1985,7 @@ __global__ __launch_bounds__(kT3, 2) void k_scan_l1(ScanArgs a, uint32_t per, ui
         }
         while (stop < 4) {
             passes += nfq;
-            drain_l1(a, fq, nfq, wq, weak_hits, rows, tile_start, sc);
+            if (!(a.ablate & 1)) drain_l1(a, fq, nfq, wq, weak_hits, rows, tile_start, sc);
             nfq = 0;
             uint32_t k = stop;
             stop = 4;
@@ -2000,7 +2003,7 @@ __global__ __launch_bounds__(kT3, 2) void k_scan_l1(ScanArgs a, uint32_t per, ui
         PHASE_MARK3(3)
         if (nfq) {  // the tile's weak hits are verified while its bytes are in LDS
             passes += nfq;
-            drain_l1(a, fq, nfq, wq, weak_hits, rows, tile_start, sc);
+            if (!(a.ablate & 1)) drain_l1(a, fq, nfq, wq, weak_hits, rows, tile_start, sc);
             nfq = 0;
         }
         PHASE_MARK3(4)
@@ -3804,6 +3807,8 @@ hipError_t launch_scan(const uint8_t* d_buf, const ScanSeg* d_segs, uint32_t nse
     a.nm = n % kMod;
     static const bool timing = getenv("SYDELTA_PHASE_TIMING") != nullptr;
     a.timing = timing ? 1u : 0u;
+    static const uint32_t ablate = getenv("SYDELTA_ABLATE") ? (uint32_t)strtoul(getenv("SYDELTA_ABLATE"), nullptr, 0) : 0u;
+    a.ablate = ablate;
     a.segs = d_segs;
     a.nsegs = nsegs;
     a.ntiles = ntiles;
