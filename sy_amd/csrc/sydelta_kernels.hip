@@ -339,12 +339,19 @@ __device__ __forceinline__ bool filt_pass(uint32_t word, uint32_t q) {
     const uint32_t m = filt_mask(q);
     return (word & m) == m;
 }
+// filt_pass as 0/1 with three bit extracts (the offset operand takes bits [4:0]): six
+// VALU where the mask form takes nine
+__device__ __forceinline__ uint32_t filt_bit(uint32_t word, uint32_t q) {
+    return __builtin_amdgcn_ubfe(word, q, 1) & __builtin_amdgcn_ubfe(word, q >> 5, 1) &
+           __builtin_amdgcn_ubfe(word, q >> 10, 1);
+}
 // Level-1 filter of a large single-file index (2^20 bits, one per key: 63 % false
 // passes at 1 Mi keys), held in LDS by k_scan_l1 so that only the positions it passes
-// cost a level-2 request to L2 (sydelta_internal.hpp): word = q[17..31], bit = q[12..16].
+// cost a level-2 request to L2 (sydelta_internal.hpp): word = q[17..31], bit = q[0..4]
+// (one bit extract; the level-2 word tests q[0..4] too, but in an unrelated word).
 static_assert(kL1Words == 32768, "l1_word takes the top 15 bits of q");
 __device__ __forceinline__ uint32_t l1_word(uint32_t q) { return q >> 17; }
-__device__ __forceinline__ uint32_t l1_test(uint32_t word, uint32_t q) { return __builtin_amdgcn_ubfe(word, q >> 12, 1); }
+__device__ __forceinline__ uint32_t l1_test(uint32_t word, uint32_t q) { return __builtin_amdgcn_ubfe(word, q, 1); }
 // Key partitions (SYDELTA_SCAN_L1=2): key w belongs to partition r & 1 (r's low bits
 // take no part in the level-2 word, r >> fwshift, fwshift >= 4), and partition p's keys
 // alone set the bits of level-1 filter p, so each filter holds half the keys at two bits
@@ -381,7 +388,7 @@ __global__ void k_idx_insert(const uint32_t* __restrict__ weak, uint64_t n, cons
     atomicOr(filt + F.filt_off + (h.r >> F.fwshift), filt_mask(h.q));
     if (l1)  // single-file index only (l1_test); l1_parts filters of 2^(32 - l1_wshift) words each
         atomicOr(l1 + ((size_t)l1_part(h.r, l1_parts - 1) << (32 - l1_wshift)) + (h.q >> l1_wshift),
-                 1u << ((h.q >> 12) & 31));
+                 1u << (h.q & 31));
     uint32_t b = bucket_hash(w) & F.bmask;
     for (;;) {
         for (uint32_t j = 0; j < 4; ++j) {
@@ -1534,8 +1541,8 @@ struct Lds3 {
     uint32_t nch;                         // 64-byte rows
     uint32_t ntab, fq, wq, l1, total;     // byte offsets
 };
-__host__ __device__ __forceinline__ Lds3 lds3_layout(uint32_t n) {
-    Lds3 L;
+__host__ __device__ constexpr Lds3 lds3_layout(uint32_t n) {
+    Lds3 L{};
     L.nch = (kTile3 + n + 63) / 64 + 1;
     uint32_t o = L.nch * kRowDw * 4;
     o = (o + 15) & ~15u; L.ntab = o; o += 256 * 4;
@@ -1721,11 +1728,13 @@ struct L1Batch {
 // part / pmask: the key partition this pass tests (pmask 0: one partition, every position).
 // kTiming: the SYDELTA_PHASE_TIMING instantiation (phase cycles and level-1 passes
 // counted); the production one carries no timing code in its hot loop.
-template <bool kTiming>
-__global__ __launch_bounds__(kT3, 2) void k_scan_l1(ScanArgs a, uint32_t per, uint32_t part, uint32_t pmask) {
+template <bool kTiming, bool kParts2>
+__global__ __launch_bounds__(kT3, 2) void k_scan_l1(ScanArgs a, uint32_t per, uint32_t part) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     const uint32_t n = a.n;
-    const Lds3 L = lds3_layout(n);
+    // n == kMaxN3 (launch_scan): every LDS offset a compile-time constant, so the level-1
+    // and n*x table reads take their base in the instruction's offset field
+    constexpr Lds3 L = lds3_layout(kMaxN3);
     uint32_t* rows = (uint32_t*)smem;
     uint32_t* ntab = (uint32_t*)(smem + L.ntab);
     const uint32_t* l1 = (const uint32_t*)(smem + L.l1);
@@ -1911,8 +1920,8 @@ __global__ __launch_bounds__(kT3, 2) void k_scan_l1(ScanArgs a, uint32_t per, ui
                 Bt.wv[t] = (bm << 16) | am;
                 const ProbeHash h = probe_hash(am, bm);
                 Bt.hq[t] = h.q;
-                off[t] = (h.r >> fwshift) * 4;
-                pt[t] = l1_part(h.r, pmask);
+                off[t] = h.r >> fwshift;
+                if (kParts2) pt[t] = l1_part(h.r, 1);
                 w1[t] = l1[l1_word(h.q)];
                 const uint32_t u = am + in + (kMod - out);  // [M-255, 2M+255)
                 am = min(u, min(u - kMod, u - 2 * kMod));
@@ -1922,12 +1931,13 @@ __global__ __launch_bounds__(kT3, 2) void k_scan_l1(ScanArgs a, uint32_t per, ui
 #pragma unroll
             for (int t = 0; t < kB3; ++t) {
                 // a position of another key partition is tested by that partition's pass
-                const uint32_t p1 = l1_test(w1[t], Bt.hq[t]) & (pt[t] == part ? 1u : 0u);
+                uint32_t p1 = l1_test(w1[t], Bt.hq[t]);
+                if (kParts2) p1 &= pt[t] == part ? 1u : 0u;
                 if (kTiming) l1pass += __popcll(__ballot(p1));
-                // a level-1 miss asks for an offset past the buffer: no request, reads 0
-                // (and filt_pass(0, q) is false)
-                Bt.w2[t] = __builtin_amdgcn_raw_buffer_load_b32(frsrc, (int)(p1 && !(a.ablate & 2) ? off[t] : 0xFFFFFFFFu),
-                                                                0, 0);
+                if (a.ablate & 2) p1 = 0;
+                // a level-1 miss asks for an offset past the buffer (p1 - 1 = all ones): no
+                // request, reads 0 (and filt_bit(0, q) is 0)
+                Bt.w2[t] = __builtin_amdgcn_raw_buffer_load_b32(frsrc, (int)((off[t] << 2) | (p1 - 1u)), 0, 0);
             }
         };
         // Queue the level-2 passes of batch g's positions still in `todo` (per-wave LDS
@@ -1937,11 +1947,27 @@ __global__ __launch_bounds__(kT3, 2) void k_scan_l1(ScanArgs a, uint32_t per, ui
         auto finish = [&](uint32_t g, L1Batch& Bt, uint32_t& todo) -> bool {
             uint32_t pbits = 0;
 #pragma unroll
-            for (int t = 0; t < kB3; ++t) pbits |= (filt_pass(Bt.w2[t], Bt.hq[t]) ? 1u : 0u) << t;
+            for (int t = 0; t < kB3; ++t) pbits |= filt_bit(Bt.w2[t], Bt.hq[t]) << t;
             // opaque: the ballots below re-derive the masks instead of holding eight
             // compare results in SGPRs (which spilled)
             asm volatile("" : "+v"(pbits));
             const uint64_t below = (1ull << lane) - 1;
+            // the usual case: at most 8 passes in each lane that has one still fit
+            const uint64_t anyp = __ballot((pbits & todo) != 0);
+            if (nfq + 8u * (uint32_t)__popcll(anyp) <= (uint32_t)kFQ3) {
+                if (anyp) {
+#pragma unroll
+                    for (int t = 0; t < kB3; ++t) {
+                        if (!((todo >> t) & 1)) continue;
+                        const uint64_t mk = __ballot((pbits >> t) & 1);
+                        if (!mk) continue;
+                        if ((pbits >> t) & 1) fq[nfq + __popcll(mk & below)] = make_uint2(rel0 + g + t, Bt.wv[t]);
+                        nfq += __popcll(mk);
+                    }
+                }
+                todo = 0xFFu;
+                return true;
+            }
             uint32_t need = 0;
 #pragma unroll
             for (int t = 0; t < kB3; ++t)
@@ -3885,11 +3911,11 @@ hipError_t launch_scan(const uint8_t* d_buf, const ScanSeg* d_segs, uint32_t nse
     // 16 Ki blocks are >= 8 KiB anyway: bs = sqrt(file size)).
     if (ix.l1 && ix.l1_wshift == 17 && n == kMaxN3 && scan_l1_mode() != 0) {
         std::call_once(l1_once, [] {
-            l1_err = hipFuncSetAttribute((const void*)k_scan_l1<false>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                         160 * 1024 - 256);
-            if (l1_err == hipSuccess)
-                l1_err = hipFuncSetAttribute((const void*)k_scan_l1<true>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                             160 * 1024 - 256);
+            const void* fns[4] = {(const void*)k_scan_l1<false, false>, (const void*)k_scan_l1<true, false>,
+                                  (const void*)k_scan_l1<false, true>, (const void*)k_scan_l1<true, true>};
+            for (const void* f : fns)
+                if (l1_err == hipSuccess)
+                    l1_err = hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024 - 256);
             int dev = 0, cus = 0;
             if (hipGetDevice(&dev) == hipSuccess &&
                 hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess && cus > 0)
@@ -3903,10 +3929,14 @@ hipError_t launch_scan(const uint8_t* d_buf, const ScanSeg* d_segs, uint32_t nse
         // one pass per key partition (the index's level-1 filters), each over every tile
         for (uint32_t part = 0; part < ix.l1_parts; ++part) {
             ProfScope ps(prof, s, "k_scan_l1");
-            if (a.timing)
-                hipLaunchKernelGGL(k_scan_l1<true>, dim3(grid), dim3(kT3), L3.total, s, a, per, part, ix.l1_parts - 1);
-            else
-                hipLaunchKernelGGL(k_scan_l1<false>, dim3(grid), dim3(kT3), L3.total, s, a, per, part, ix.l1_parts - 1);
+            const bool p2 = ix.l1_parts == 2;
+            if (a.timing) {
+                if (p2) hipLaunchKernelGGL((k_scan_l1<true, true>), dim3(grid), dim3(kT3), L3.total, s, a, per, part);
+                else hipLaunchKernelGGL((k_scan_l1<true, false>), dim3(grid), dim3(kT3), L3.total, s, a, per, part);
+            } else {
+                if (p2) hipLaunchKernelGGL((k_scan_l1<false, true>), dim3(grid), dim3(kT3), L3.total, s, a, per, part);
+                else hipLaunchKernelGGL((k_scan_l1<false, false>), dim3(grid), dim3(kT3), L3.total, s, a, per, part);
+            }
             if (hipError_t e = hipGetLastError()) return e;
         }
         return hipSuccess;
