@@ -29,6 +29,9 @@ constexpr uint32_t kL1Words = 32768;   // k_scan_l1's level-1 filter (128 KiB), 
 // Level-1 filter of a single-file index for windows above scan_max_window() (k_scan_w):
 // 16384 words = 64 KiB = 2^19 bits, beside the wide kernel's two staged byte regions.
 constexpr uint32_t kL1WordsWide = 16384;
+// k_scan_l2's level-1 filter (SYDELTA_SCAN_L1=4): 28672 words = 112 KiB beside its
+// 32 Ki-position tile, word = l1w2_word(q) (l1_wshift 0 marks it).
+constexpr uint32_t kL1WordsL2 = 28672;
 
 // Verified hits are written as key/value pairs: key = (segment << 32) | position
 // relative to the segment's first position, value = global block index (into the
@@ -61,7 +64,8 @@ struct DeviceIndex {
     uint32_t* filt = nullptr;   // blocked Bloom filters (probe_hash/filt_mask), per-file 2^k 32-bit words
     uint32_t* l1 = nullptr;     // level-1 filter, single-file indexes above kLdsFilterKeys keys at bs 4096
     uint32_t l1_parts = 0;      // key partitions: l1 holds l1_parts filters of 2^(32 - l1_wshift) words
-    uint32_t l1_wshift = 17;    // level-1 word of probe hash q: q >> l1_wshift (17: kL1Words, 18: kL1WordsWide)
+    uint32_t l1_wshift = 17;    // level-1 word of probe hash q: q >> l1_wshift (17: kL1Words, 18: kL1WordsWide;
+                                // 0: kL1WordsL2 words, l1w2_word)
     uint4* fat = nullptr;       // with l1: per slot {key, first candidate | multi, its strong} (k_idx_fat)
     uint32_t* keys = nullptr;   // 4-key buckets of unique weak values, kEmptyKey = free
     uint32_t* cnt = nullptr;    // candidates per slot
@@ -104,7 +108,8 @@ hipError_t launch_index_build(const uint32_t* d_weak, const uint64_t* d_strong, 
                               Profiler* prof);
 uint64_t scan_tile_positions();  // positions per tile of the LDS-staged scan
 // SYDELTA_SCAN_L1: 0 k_scan_lds, 1 (default) k_scan_l1, 2 k_scan_l1 over two key
-// partitions (read per call; the index's level-1 layout is chosen when it is built)
+// partitions, 3 k_scan_s, 4 k_scan_l2 (read per call; the index's level-1 layout is
+// chosen when it is built)
 int scan_l1_mode();
 // SYDELTA_SCAN_WIDE=0: windows above scan_max_window() take the per-thread k_scan
 // instead of the LDS-staged k_scan_w (read when the index is built and per call)

@@ -352,6 +352,11 @@ __device__ __forceinline__ uint32_t filt_bit(uint32_t word, uint32_t q) {
 static_assert(kL1Words == 32768, "l1_word takes the top 15 bits of q");
 __device__ __forceinline__ uint32_t l1_word(uint32_t q) { return q >> 17; }
 __device__ __forceinline__ uint32_t l1_test(uint32_t word, uint32_t q) { return __builtin_amdgcn_ubfe(word, q, 1); }
+// k_scan_l2's level-1 word (kL1WordsL2 words, not a power of two): floor(q * words / 2^32)
+// from the top 24 bits of q, one shift and one v_mul_hi_u32_u24
+__host__ __device__ __forceinline__ uint32_t l1w2_word(uint32_t q) {
+    return (uint32_t)(((uint64_t)(q >> 8) * (kL1WordsL2 << 8)) >> 32);
+}
 // Key partitions (SYDELTA_SCAN_L1=2): key w belongs to partition r & 1 (r's low bits
 // take no part in the level-2 word, r >> fwshift, fwshift >= 4), and partition p's keys
 // alone set the bits of level-1 filter p, so each filter holds half the keys at two bits
@@ -387,7 +392,8 @@ __global__ void k_idx_insert(const uint32_t* __restrict__ weak, uint64_t n, cons
     const ProbeHash h = probe_hash(w);
     atomicOr(filt + F.filt_off + (h.r >> F.fwshift), filt_mask(h.q));
     if (l1)  // single-file index only (l1_test); l1_parts filters of 2^(32 - l1_wshift) words each
-        atomicOr(l1 + ((size_t)l1_part(h.r, l1_parts - 1) << (32 - l1_wshift)) + (h.q >> l1_wshift),
+        atomicOr(l1 + (l1_wshift ? ((size_t)l1_part(h.r, l1_parts - 1) << (32 - l1_wshift)) + (h.q >> l1_wshift)
+                                 : (size_t)l1w2_word(h.q)),
                  1u << (h.q & 31));
     uint32_t b = bucket_hash(w) & F.bmask;
     for (;;) {
@@ -2045,6 +2051,349 @@ __global__ __launch_bounds__(kT3, 2) void k_scan_l1(ScanArgs a, uint32_t per, ui
 }
 
 // ===========================================================================
+// k_scan_l2: k_scan_l1 on tiles of 32 Ki positions (SYDELTA_SCAN_L1=4, opt-in)
+// ===========================================================================
+// Measured on k_scan_l1 (round 3, C3, SYDELTA_ABLATE): of its 16.8 ms, the tile drains
+// (fat-table round trip + verification) take 4.7 ms and the level-2 loads 4.9 ms, while
+// the roll itself runs in ~5.8 ms.  A drain's round trip and the barrier skew come once
+// per tile whatever its length, so here a tile is two of the host's tiles: 64 positions
+// per thread in eight batches, each thread's first window from 64-byte row sums (two
+// columns of 64 rows per wave), 36 KiB of rows.  The level-1 filter shrinks to
+// kL1WordsL2 words (112 KiB, word = the top bits of q scaled by a 24-bit multiply-high),
+// which passes 1 - e^(-keys / 917504) of the positions (0.68 at 1 Mi keys, 0.63 for
+// k_scan_l1's 128 KiB).  A pair of host tiles cut by a segment end or by the workgroup's
+// range is scanned as one tile whose second half the drain drops.
+constexpr int kR4 = 64;            // positions per thread = one 64-byte row
+constexpr int kTile4 = kT3 * kR4;  // 32768 positions per tile
+constexpr int kNB4 = kR4 / kB3;    // batches per thread per tile
+static_assert(kTile4 == 2 * kTile2, "a k_scan_l2 tile is two host tiles");
+
+struct Lds4 {
+    uint32_t nch;                        // 64-byte rows
+    uint32_t ntail;                      // rows past the first kT3 (staged 16 bytes per thread)
+    uint32_t ntab, fq, wq, l1, total;    // byte offsets
+};
+__host__ __device__ constexpr Lds4 lds4_layout(uint32_t n) {
+    Lds4 L{};
+    L.nch = (kTile4 + n + 63) / 64 + 1;
+    L.ntail = L.nch > (uint32_t)kT3 ? L.nch - kT3 : 0;
+    uint32_t o = L.nch * kRowDw * 4;
+    o = (o + 15) & ~15u; L.ntab = o; o += 256 * 4;
+    L.fq = o; o += (kT3 / 64) * kFQ3 * 8;
+    L.wq = o; o += (kT3 / 64) * kWQ3 * 16;
+    L.l1 = o; o += kL1WordsL2 * 4;
+    L.total = o;
+    return L;
+}
+static_assert(lds4_layout(kMaxN3).total <= 160 * 1024 - 256, "k_scan_l2's LDS");
+static_assert(lds4_layout(kMaxN3).l1 < 65536, "the level-1 base fits a ds_read offset");
+
+// 16 bytes at src + c0 (16-byte aligned; bytes at or beyond len read as 0).
+__device__ __forceinline__ void load16_nt(const uint8_t* src, uint64_t len, uint64_t c0, uint32_t x[4]) {
+    if (c0 + 16 <= len) {
+        const uint4* q = (const uint4*)(src + c0);
+        x[0] = __builtin_nontemporal_load(&q->x);
+        x[1] = __builtin_nontemporal_load(&q->y);
+        x[2] = __builtin_nontemporal_load(&q->z);
+        x[3] = __builtin_nontemporal_load(&q->w);
+    } else {
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            uint32_t v = 0;
+            for (int b = 0; b < 4; ++b) {
+                const uint64_t p = c0 + 4 * i + b;
+                if (p < len) v |= (uint32_t)src[p] << (8 * b);
+            }
+            x[i] = v;
+        }
+    }
+}
+
+template <bool kTiming>
+__global__ __launch_bounds__(kT3, 2) void k_scan_l2(ScanArgs a, uint32_t per) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    const uint32_t n = a.n;  // kMaxN3 (launch_scan)
+    constexpr Lds4 L = lds4_layout(kMaxN3);
+    uint32_t* rows = (uint32_t*)smem;
+    uint32_t* ntab = (uint32_t*)(smem + L.ntab);
+    const uint32_t* l1 = (const uint32_t*)(smem + L.l1);
+    const uint32_t tid = threadIdx.x;
+    const uint32_t lane = tid & 63, wid = tid >> 6;
+    uint2* fq = (uint2*)(smem + L.fq) + (size_t)wid * kFQ3;
+    uint4* wq = (uint4*)(smem + L.wq) + (size_t)wid * kWQ3;
+
+    const uint32_t t_begin = blockIdx.x * per;
+    const uint32_t t_end = min(a.ntiles, t_begin + per);
+    if (t_begin >= t_end) return;
+    {
+        const uint4* g = (const uint4*)a.l1;
+        uint4* d = (uint4*)(smem + L.l1);
+#pragma unroll 4
+        for (uint32_t i = tid; i < kL1WordsL2 / 4; i += kT3) d[i] = g[i];
+    }
+    for (uint32_t i = tid; i < 256; i += kT3) ntab[i] = kMod - 1 - (a.nm * i) % kMod;
+    constexpr uint32_t ntail4 = 4 * L.ntail;  // threads staging a 16-byte quarter of a tail row
+    const uint32_t rel0 = tid * kR4;
+    const uint32_t orow = tid * kRowDw;          // this thread's out bytes: row tid
+    const uint32_t din0 = (rel0 + n) >> 2;       // ... and its first in dword
+    const uint32_t sh = n & 3;
+    const uint32_t m64 = n >> 6;                 // window = m64 rows (n = 4096: 64)
+    unsigned long long passes = 0, weak_hits = 0;
+    uint32_t nfq = 0;
+    unsigned long long tm[6] = {0, 0, 0, 0, 0, 0}, l1pass = 0;
+    unsigned long long tprev = kTiming ? __builtin_amdgcn_s_memtime() : 0;
+#define PHASE_MARK4(k)                                                 \
+    if (kTiming) {                                                     \
+        const unsigned long long tnow = __builtin_amdgcn_s_memtime(); \
+        tm[k] += tnow - tprev;                                         \
+        tprev = tnow;                                                  \
+    }
+
+    auto seg_ctx = [&](uint32_t tile, uint32_t si0, SegCtx& sc, uint32_t& si, uint64_t& tile_start,
+                       uint64_t& seg_len) {
+        uint32_t lo = si0, hi = a.nsegs;
+        while (hi - lo > 1) {
+            const uint32_t mid = (lo + hi) >> 1;
+            if (a.segs[mid].tile_base <= tile) lo = mid; else hi = mid;
+        }
+        si = lo;
+        const ScanSeg S = a.segs[si];
+        const FileIx F = a.files[S.file];
+        sc.base = a.src + S.src;
+        sc.pos_begin = S.pos_begin;
+        sc.pos_end = S.pos_end;
+        sc.keys = a.keys + F.slot_off;
+        sc.fat = a.fat + F.slot_off;
+        sc.slot_off = F.slot_off;
+        sc.bmask = F.bmask;
+        sc.seg_id = si;
+        sc.fwshift = F.fwshift;
+        sc.filt = a.filt + F.filt_off;
+        sc.fwords = 1u << (32 - F.fwshift);
+        tile_start = S.pos_begin + (uint64_t)(tile - S.tile_base) * kTile2;
+        seg_len = S.len;
+    };
+    // host tiles this tile covers: 2 when host tile t+1 is in this workgroup's range and
+    // in the same segment as t (segment sidx)
+    auto span_of = [&](uint32_t t, uint32_t sidx) -> uint32_t {
+        if (t + 1 >= t_end) return 1;
+        if (sidx + 1 < a.nsegs && a.segs[sidx + 1].tile_base <= t + 1) return 1;
+        return 2;
+    };
+    SegCtx sc, nsc;
+    uint32_t si = 0, nsi = 0;
+    uint64_t tile_start = 0, seg_len = 0, ntile_start = 0, nseg_len = 0;
+    seg_ctx(t_begin, 0, nsc, nsi, ntile_start, nseg_len);
+    uint32_t nspan = span_of(t_begin, nsi);
+    // next tile's rows 0..kT3-1 (thread c: row c) and its tail rows (16 bytes per thread)
+    uint32_t x[16], xt[4] = {0, 0, 0, 0};
+    load_chunk_nt(nsc.base, nseg_len, ntile_start + 64ull * tid, x);
+    if (tid < ntail4) load16_nt(nsc.base, nseg_len, ntile_start + 64ull * kT3 + 16ull * tid, xt);
+
+    uint32_t tile = t_begin;
+#pragma unroll 1
+    while (tile < t_end) {
+        sc = nsc;
+        si = nsi;
+        tile_start = ntile_start;
+        seg_len = nseg_len;
+        const uint32_t span = nspan;
+        // ---- stage (the previous tile's barrier ended every read of the rows)
+#pragma unroll
+        for (int i = 0; i < 16; ++i) rows[tid * kRowDw + i] = x[i];
+        if (tid < ntail4) {
+#pragma unroll
+            for (int i = 0; i < 4; ++i) rows[(kT3 + (tid >> 2)) * kRowDw + 4 * (tid & 3) + i] = xt[i];
+        }
+        __syncthreads();
+        const uint32_t nt = tile + span;
+        if (nt < t_end) {
+            if (nsi + 1 < a.nsegs && a.segs[nsi + 1].tile_base <= nt)
+                seg_ctx(nt, nsi, nsc, nsi, ntile_start, nseg_len);
+            else
+                ntile_start = tile_start + (uint64_t)span * kTile2;
+            nspan = span_of(nt, nsi);
+            load_chunk_nt(nsc.base, nseg_len, ntile_start + 64ull * tid, x);
+            if (tid < ntail4) load16_nt(nsc.base, nseg_len, ntile_start + 64ull * kT3 + 16ull * tid, xt);
+        }
+        // positions of this tile that belong to it: [tile_start, tile_start + span * kTile2)
+        sc.pos_end = min(sc.pos_end, tile_start + (uint64_t)span * kTile2);
+        PHASE_MARK4(0)
+
+        // ---- window: lane l of wave w starts at row r = 64w + l (tile offset 64r); rows
+        // r + 64j, j = 0..1, cover its window [64r, 64r + n) (m64 = 64)
+        uint32_t am, bm;
+        {
+            uint32_t S[2], V[2], J[2], TS[2], TV[2], TJ[2];
+#pragma unroll
+            for (int j = 0; j < 2; ++j) {
+                const uint32_t* r = rows + (tid + 64 * j) * kRowDw;
+                uint32_t s = 0, v = 0;
+#pragma unroll
+                for (int i = 0; i < 16; ++i) {
+                    const uint32_t d = r[i];
+                    s = udot4(d, 0x01010101u, s);
+                    v = udot4(d, offw(i), v);
+                }
+                S[j] = wave_scan_excl(s, TS[j]);
+                V[j] = wave_scan_excl(v, TV[j]);
+                J[j] = wave_scan_excl((uint32_t)(64 * j + lane) * s, TJ[j]);  // row index relative to the wave
+            }
+            // prefix at relative row lane + m64 = lane + 64: column 1, this lane
+            const uint64_t dS = TS[0] + S[1] - S[0];
+            const uint64_t dV = TV[0] + V[1] - V[0];
+            const uint64_t dJ = TJ[0] + J[1] - J[0];
+            const uint32_t A = (uint32_t)dS;
+            // B = sum_i (n - i) x_{64r+i} = n dS - 64 sum_k (k - l) S_k - dV   (< 2^31 for n <= 4096)
+            const uint32_t B = (uint32_t)((uint64_t)n * dS - 64ull * (dJ - (uint64_t)lane * dS) - dV);
+            am = (1 + A) % kMod;
+            bm = (n + B) % kMod;
+        }
+        PHASE_MARK4(1)
+
+        // ---- roll (k_scan_l1's trimmed roll; positions past sc.pos_end are dropped by the drain)
+        const uint64_t fptr = (uint64_t)(uintptr_t)sc.filt;
+        const uint32_t fp_lo = __builtin_amdgcn_readfirstlane((uint32_t)fptr);
+        const uint32_t fp_hi = __builtin_amdgcn_readfirstlane((uint32_t)(fptr >> 32));
+        const __amdgpu_buffer_rsrc_t frsrc = __builtin_amdgcn_make_buffer_rsrc(
+            (void*)(uintptr_t)(((uint64_t)fp_hi << 32) | fp_lo), (short)0,
+            (int)__builtin_amdgcn_readfirstlane(sc.fwords * 4), 0x00020000);
+        const uint32_t fwshift = __builtin_amdgcn_readfirstlane(sc.fwshift);
+        auto compute = [&](uint32_t g, L1Batch& Bt) {
+            uint32_t xo[2], xi[2];
+            xo[0] = rows[orow + (g >> 2)];
+            xo[1] = rows[orow + (g >> 2) + 1];
+            {
+                uint32_t dw[3];
+#pragma unroll
+                for (int j = 0; j < 3; ++j) {
+                    const uint32_t d = din0 + (g >> 2) + j;
+                    dw[j] = rows[(d >> 4) * kRowDw + (d & 15)];
+                }
+                xi[0] = __builtin_amdgcn_alignbyte(dw[1], dw[0], sh);
+                xi[1] = __builtin_amdgcn_alignbyte(dw[2], dw[1], sh);
+            }
+            uint32_t ct[kB3], off[kB3], w1[kB3];
+#pragma unroll
+            for (int t = 0; t < kB3; ++t) ct[t] = ntab[(xo[t >> 2] >> (8 * (t & 3))) & 0xFF];
+#pragma unroll
+            for (int t = 0; t < kB3; ++t) {
+                const uint32_t out = (xo[t >> 2] >> (8 * (t & 3))) & 0xFF;
+                const uint32_t in = (xi[t >> 2] >> (8 * (t & 3))) & 0xFF;
+                __builtin_assume(am < kMod);
+                __builtin_assume(bm < kMod);
+                Bt.wv[t] = (bm << 16) | am;
+                const ProbeHash h = probe_hash(am, bm);
+                Bt.hq[t] = h.q;
+                off[t] = h.r >> fwshift;
+                w1[t] = l1[l1w2_word(h.q)];
+                const uint32_t u = am + in + (kMod - out);  // [M-255, 2M+255)
+                am = min(u, min(u - kMod, u - 2 * kMod));
+                const uint32_t v = bm + am + ct[t];          // [0, 3M)
+                bm = min(v, min(v - kMod, v - 2 * kMod));
+            }
+#pragma unroll
+            for (int t = 0; t < kB3; ++t) {
+                const uint32_t p1 = l1_test(w1[t], Bt.hq[t]);
+                if (kTiming) l1pass += __popcll(__ballot(p1));
+                // a level-1 miss asks for an offset past the buffer: no request, reads 0
+                Bt.w2[t] = __builtin_amdgcn_raw_buffer_load_b32(frsrc, (int)((off[t] << 2) | (p1 - 1u)), 0, 0);
+            }
+        };
+        auto finish = [&](uint32_t g, L1Batch& Bt, uint32_t& todo) -> bool {
+            uint32_t pbits = 0;
+#pragma unroll
+            for (int t = 0; t < kB3; ++t) pbits |= filt_bit(Bt.w2[t], Bt.hq[t]) << t;
+            asm volatile("" : "+v"(pbits));
+            const uint64_t below = (1ull << lane) - 1;
+            const uint64_t anyp = __ballot((pbits & todo) != 0);
+            if (nfq + 8u * (uint32_t)__popcll(anyp) <= (uint32_t)kFQ3) {
+                if (anyp) {
+#pragma unroll
+                    for (int t = 0; t < kB3; ++t) {
+                        if (!((todo >> t) & 1)) continue;
+                        const uint64_t mk = __ballot((pbits >> t) & 1);
+                        if (!mk) continue;
+                        if ((pbits >> t) & 1) fq[nfq + __popcll(mk & below)] = make_uint2(rel0 + g + t, Bt.wv[t]);
+                        nfq += __popcll(mk);
+                    }
+                }
+                todo = 0xFFu;
+                return true;
+            }
+            uint32_t need = 0;
+#pragma unroll
+            for (int t = 0; t < kB3; ++t)
+                if ((todo >> t) & 1) need += __popcll(__ballot((pbits >> t) & 1));
+            const bool all = nfq + need <= (uint32_t)kFQ3;
+            bool full = false;
+#pragma unroll
+            for (int t = 0; t < kB3; ++t) {
+                if (!((todo >> t) & 1) || full) continue;
+                const uint64_t mk = __ballot((pbits >> t) & 1);
+                if (!all && nfq + __popcll(mk) > (uint32_t)kFQ3) { full = true; continue; }
+                if ((pbits >> t) & 1) fq[nfq + __popcll(mk & below)] = make_uint2(rel0 + g + t, Bt.wv[t]);
+                nfq += __popcll(mk);
+                todo &= ~(1u << t);
+            }
+            if (all) todo = 0xFFu;
+            return all;
+        };
+        // Pipeline over the thread's 8 batches: batch k+1's level-2 loads are in flight
+        // while batch k is tested; a batch the queue cannot take stops it, the queue is
+        // drained and the roll resumes from that batch's saved state.
+        uint32_t stop = kNB4, todo = 0xFFu, ra = 0, rb = 0;
+        {
+            L1Batch b0, b1;
+            uint32_t sa0 = am, sb0 = bm;
+            compute(0, b0);
+            uint32_t sa1 = am, sb1 = bm;
+            compute(kB3, b1);
+#pragma unroll 1
+            for (uint32_t k = 0; k < (uint32_t)kNB4; k += 2) {
+                if (!finish(kB3 * k, b0, todo)) { stop = k; ra = sa0; rb = sb0; break; }
+                if (k + 2 < (uint32_t)kNB4) { sa0 = am; sb0 = bm; compute(kB3 * (k + 2), b0); }
+                if (!finish(kB3 * (k + 1), b1, todo)) { stop = k + 1; ra = sa1; rb = sb1; break; }
+                if (k + 3 < (uint32_t)kNB4) { sa1 = am; sb1 = bm; compute(kB3 * (k + 3), b1); }
+            }
+        }
+        while (stop < (uint32_t)kNB4) {
+            passes += nfq;
+            drain_l1(a, fq, nfq, wq, weak_hits, rows, tile_start, sc);
+            nfq = 0;
+            uint32_t k = stop;
+            stop = kNB4;
+            am = ra;
+            bm = rb;
+#pragma unroll 1
+            for (; k < (uint32_t)kNB4; ++k) {
+                L1Batch bt;
+                const uint32_t ak = am, sk = bm;
+                compute(kB3 * k, bt);
+                if (!finish(kB3 * k, bt, todo)) { stop = k; ra = ak; rb = sk; break; }
+            }
+        }
+        PHASE_MARK4(2)
+        PHASE_MARK4(3)
+        if (nfq) {
+            passes += nfq;
+            drain_l1(a, fq, nfq, wq, weak_hits, rows, tile_start, sc);
+            nfq = 0;
+        }
+        PHASE_MARK4(4)
+        __syncthreads();  // rows are rewritten by the next tile
+        PHASE_MARK4(5)
+        tile += span;
+    }
+#undef PHASE_MARK4
+    if (lane == 0 && passes) atomicAdd(&a.counters[2], passes);
+    if (lane == 0 && weak_hits) atomicAdd(&a.counters[1], weak_hits);
+    if (kTiming && lane == 0) atomicAdd(&a.counters[3], l1pass);
+    if (kTiming && tid == 0)
+        for (int k = 0; k < 6; ++k) atomicAdd(&a.counters[4 + k], tm[k]);
+}
+
+// ===========================================================================
 // K2+K4 for windows above kMaxN2: k_scan_w
 // ===========================================================================
 // sy's own block size is calculate_block_size(size) = sqrt(size) clamped to [512, 128 Ki]
@@ -3665,7 +4014,7 @@ static inline unsigned grid_for(uint64_t threads, unsigned block) { return (unsi
 // partition (l1_part).
 int scan_l1_mode() {
     const char* e = getenv("SYDELTA_SCAN_L1");
-    return (e && e[0] == '0') ? 0 : (e && e[0] == '2') ? 2 : (e && e[0] == '3') ? 3 : 1;
+    return (e && e[0] >= '0' && e[0] <= '4' && e[1] == 0) ? e[0] - '0' : 1;
 }
 int scan_wide_mode() {
     const char* e = getenv("SYDELTA_SCAN_WIDE");
@@ -3738,7 +4087,9 @@ hipError_t launch_index_build(const uint32_t* d_weak, const uint64_t* d_strong, 
                               Profiler* prof) {
     hipError_t e;
     if ((e = hipMemsetAsync(ix.filt, 0, ix.fwords * 4, s))) return e;
-    if (ix.l1 && (e = hipMemsetAsync(ix.l1, 0, ((size_t)ix.l1_parts << (32 - ix.l1_wshift)) * 4, s))) return e;
+    if (ix.l1 && (e = hipMemsetAsync(ix.l1, 0, (ix.l1_wshift ? ((size_t)ix.l1_parts << (32 - ix.l1_wshift))
+                                                              : (size_t)kL1WordsL2) * 4, s)))
+        return e;
     if ((e = hipMemsetAsync(ix.keys, 0xFF, ix.nslots * 4, s))) return e;
     if ((e = hipMemsetAsync(ix.cnt, 0, ix.nslots * 4, s))) return e;
     const uint64_t n = ix.nblocks;
@@ -3909,6 +4260,35 @@ hipError_t launch_scan(const uint8_t* d_buf, const ScanSeg* d_segs, uint32_t nse
     // covers, n = 4096 (the C3 shape; tests/test_gpu_scan_large.py).  Other sizes with a
     // large index go to k_scan_lds (production block sizes for files with more than
     // 16 Ki blocks are >= 8 KiB anyway: bs = sqrt(file size)).
+    if (ix.l1 && ix.l1_wshift == 0 && n == kMaxN3 && scan_l1_mode() == 4) {  // k_scan_l2
+        static std::once_flag l2_once;
+        static hipError_t l2_err = hipSuccess;
+        static int l2_cus = 256;
+        std::call_once(l2_once, [] {
+            l2_err = hipFuncSetAttribute((const void*)k_scan_l2<false>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                         160 * 1024 - 256);
+            if (l2_err == hipSuccess)
+                l2_err = hipFuncSetAttribute((const void*)k_scan_l2<true>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                             160 * 1024 - 256);
+            int dev = 0, cus = 0;
+            if (hipGetDevice(&dev) == hipSuccess &&
+                hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess && cus > 0)
+                l2_cus = cus;
+        });
+        if (l2_err != hipSuccess) return l2_err;
+        if (!ix.fat) return hipErrorInvalidValue;
+        constexpr Lds4 L4 = lds4_layout(kMaxN3);
+        // one workgroup per CU, an even number of host tiles each so that the pairs line up
+        uint32_t per = (uint32_t)((ntiles + (uint64_t)l2_cus - 1) / (uint64_t)l2_cus);
+        per += per & 1;
+        const uint32_t grid = (uint32_t)((ntiles + (uint64_t)per - 1) / per);
+        ProfScope ps(prof, s, "k_scan_l2");
+        if (a.timing)
+            hipLaunchKernelGGL(k_scan_l2<true>, dim3(grid), dim3(kT3), L4.total, s, a, per);
+        else
+            hipLaunchKernelGGL(k_scan_l2<false>, dim3(grid), dim3(kT3), L4.total, s, a, per);
+        return hipGetLastError();
+    }
     if (ix.l1 && ix.l1_wshift == 17 && n == kMaxN3 && scan_l1_mode() != 0) {
         std::call_once(l1_once, [] {
             const void* fns[4] = {(const void*)k_scan_l1<false, false>, (const void*)k_scan_l1<true, false>,

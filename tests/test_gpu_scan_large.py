@@ -26,15 +26,15 @@ pytestmark = pytest.mark.gpu
 
 
 # SYDELTA_TEST_SCANNERS=a,b restricts the parametrization (a first hardware run of one kernel)
-_SCANNERS = [k for k in ["lds", "l1", "l1p2", "s"]
-             if k in os.environ.get("SYDELTA_TEST_SCANNERS", "lds,l1,l1p2,s").split(",")]
+_SCANNERS = [k for k in ["lds", "l1", "l1p2", "s", "l2"]
+             if k in os.environ.get("SYDELTA_TEST_SCANNERS", "lds,l1,l1p2,s,l2").split(",")]
 
 
 @pytest.fixture(params=_SCANNERS)
 def scanner(request, monkeypatch):
     """The large-index scan kernel (SYDELTA_SCAN_L1 is read when the index is built and
     by launch_scan on every call)."""
-    monkeypatch.setenv("SYDELTA_SCAN_L1", {"lds": "0", "l1": "1", "l1p2": "2", "s": "3"}[request.param])
+    monkeypatch.setenv("SYDELTA_SCAN_L1", {"lds": "0", "l1": "1", "l1p2": "2", "s": "3", "l2": "4"}[request.param])
     return request.param
 
 
