@@ -2109,7 +2109,8 @@ __device__ __forceinline__ void load16_nt(const uint8_t* src, uint64_t len, uint
     }
 }
 
-template <bool kTiming>
+// kDepth: batches whose level-2 loads are in flight while one is tested (1 or 2)
+template <bool kTiming, int kDepth>
 __global__ __launch_bounds__(kT3, 2) void k_scan_l2(ScanArgs a, uint32_t per) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     const uint32_t n = a.n;  // kMaxN3 (launch_scan)
@@ -2343,7 +2344,7 @@ __global__ __launch_bounds__(kT3, 2) void k_scan_l2(ScanArgs a, uint32_t per) {
         // while batch k is tested; a batch the queue cannot take stops it, the queue is
         // drained and the roll resumes from that batch's saved state.
         uint32_t stop = kNB4, todo = 0xFFu, ra = 0, rb = 0;
-        {
+        if (kDepth == 1) {
             L1Batch b0, b1;
             uint32_t sa0 = am, sb0 = bm;
             compute(0, b0);
@@ -2355,6 +2356,28 @@ __global__ __launch_bounds__(kT3, 2) void k_scan_l2(ScanArgs a, uint32_t per) {
                 if (k + 2 < (uint32_t)kNB4) { sa0 = am; sb0 = bm; compute(kB3 * (k + 2), b0); }
                 if (!finish(kB3 * (k + 1), b1, todo)) { stop = k + 1; ra = sa1; rb = sb1; break; }
                 if (k + 3 < (uint32_t)kNB4) { sa1 = am; sb1 = bm; compute(kB3 * (k + 3), b1); }
+            }
+        } else {
+            // three batch buffers in fixed roles (batch k in b[k % 3]): batches k+1 and k+2
+            // in flight while k is tested; a rolled loop of three, so finish is inlined
+            // three times and no buffer is moved (a move would wait for its loads)
+            L1Batch b0, b1, b2;
+            uint32_t sa0 = am, sb0 = bm;
+            compute(0, b0);
+            uint32_t sa1 = am, sb1 = bm;
+            compute(kB3, b1);
+            uint32_t sa2 = am, sb2 = bm;
+            compute(2 * kB3, b2);
+#pragma unroll 1
+            for (uint32_t k = 0; k < (uint32_t)kNB4; k += 3) {
+                if (!finish(kB3 * k, b0, todo)) { stop = k; ra = sa0; rb = sb0; break; }
+                if (k + 3 < (uint32_t)kNB4) { sa0 = am; sb0 = bm; compute(kB3 * (k + 3), b0); }
+                if (k + 1 >= (uint32_t)kNB4) break;
+                if (!finish(kB3 * (k + 1), b1, todo)) { stop = k + 1; ra = sa1; rb = sb1; break; }
+                if (k + 4 < (uint32_t)kNB4) { sa1 = am; sb1 = bm; compute(kB3 * (k + 4), b1); }
+                if (k + 2 >= (uint32_t)kNB4) break;
+                if (!finish(kB3 * (k + 2), b2, todo)) { stop = k + 2; ra = sa2; rb = sb2; break; }
+                if (k + 5 < (uint32_t)kNB4) { sa2 = am; sb2 = bm; compute(kB3 * (k + 5), b2); }
             }
         }
         while (stop < (uint32_t)kNB4) {
@@ -4265,11 +4288,11 @@ hipError_t launch_scan(const uint8_t* d_buf, const ScanSeg* d_segs, uint32_t nse
         static hipError_t l2_err = hipSuccess;
         static int l2_cus = 256;
         std::call_once(l2_once, [] {
-            l2_err = hipFuncSetAttribute((const void*)k_scan_l2<false>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                         160 * 1024 - 256);
-            if (l2_err == hipSuccess)
-                l2_err = hipFuncSetAttribute((const void*)k_scan_l2<true>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                             160 * 1024 - 256);
+            const void* fns[4] = {(const void*)k_scan_l2<false, 1>, (const void*)k_scan_l2<true, 1>,
+                                  (const void*)k_scan_l2<false, 2>, (const void*)k_scan_l2<true, 2>};
+            for (const void* f : fns)
+                if (l2_err == hipSuccess)
+                    l2_err = hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024 - 256);
             int dev = 0, cus = 0;
             if (hipGetDevice(&dev) == hipSuccess &&
                 hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess && cus > 0)
@@ -4283,10 +4306,15 @@ hipError_t launch_scan(const uint8_t* d_buf, const ScanSeg* d_segs, uint32_t nse
         per += per & 1;
         const uint32_t grid = (uint32_t)((ntiles + (uint64_t)per - 1) / per);
         ProfScope ps(prof, s, "k_scan_l2");
-        if (a.timing)
-            hipLaunchKernelGGL(k_scan_l2<true>, dim3(grid), dim3(kT3), L4.total, s, a, per);
-        else
-            hipLaunchKernelGGL(k_scan_l2<false>, dim3(grid), dim3(kT3), L4.total, s, a, per);
+        // SYDELTA_SCAN_DEPTH=1|2 (default 2): level-2 loads in flight per batch tested
+        static const int depth = getenv("SYDELTA_SCAN_DEPTH") && getenv("SYDELTA_SCAN_DEPTH")[0] == '1' ? 1 : 2;
+        if (depth == 1) {
+            if (a.timing) hipLaunchKernelGGL((k_scan_l2<true, 1>), dim3(grid), dim3(kT3), L4.total, s, a, per);
+            else hipLaunchKernelGGL((k_scan_l2<false, 1>), dim3(grid), dim3(kT3), L4.total, s, a, per);
+        } else {
+            if (a.timing) hipLaunchKernelGGL((k_scan_l2<true, 2>), dim3(grid), dim3(kT3), L4.total, s, a, per);
+            else hipLaunchKernelGGL((k_scan_l2<false, 2>), dim3(grid), dim3(kT3), L4.total, s, a, per);
+        }
         return hipGetLastError();
     }
     if (ix.l1 && ix.l1_wshift == 17 && n == kMaxN3 && scan_l1_mode() != 0) {
