@@ -2109,8 +2109,10 @@ __device__ __forceinline__ void load16_nt(const uint8_t* src, uint64_t len, uint
     }
 }
 
-// kDepth: batches whose level-2 loads are in flight while one is tested (1 or 2)
-template <bool kTiming, int kDepth>
+// kDepth: batches whose level-2 loads are in flight while one is tested (1 or 2).
+// kMask: a level-1 miss takes its lane out of the level-2 load (exec mask) instead of
+// asking for an offset past the buffer (SYDELTA_SCAN_MASK=1, an A/B of the address path)
+template <bool kTiming, int kDepth, bool kMask = false>
 __global__ __launch_bounds__(kT3, 2) void k_scan_l2(ScanArgs a, uint32_t per) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     const uint32_t n = a.n;  // kMaxN3 (launch_scan)
@@ -2297,8 +2299,14 @@ __global__ __launch_bounds__(kT3, 2) void k_scan_l2(ScanArgs a, uint32_t per) {
             for (int t = 0; t < kB3; ++t) {
                 const uint32_t p1 = l1_test(w1[t], Bt.hq[t]);
                 if (kTiming) l1pass += __popcll(__ballot(p1));
-                // a level-1 miss asks for an offset past the buffer: no request, reads 0
-                Bt.w2[t] = __builtin_amdgcn_raw_buffer_load_b32(frsrc, (int)((off[t] << 2) | (p1 - 1u)), 0, 0);
+                if (kMask) {
+                    uint32_t w2 = 0;
+                    if (p1) w2 = __builtin_amdgcn_raw_buffer_load_b32(frsrc, (int)(off[t] << 2), 0, 0);
+                    Bt.w2[t] = w2;
+                } else {
+                    // a level-1 miss asks for an offset past the buffer: no request, reads 0
+                    Bt.w2[t] = __builtin_amdgcn_raw_buffer_load_b32(frsrc, (int)((off[t] << 2) | (p1 - 1u)), 0, 0);
+                }
             }
         };
         auto finish = [&](uint32_t g, L1Batch& Bt, uint32_t& todo) -> bool {
@@ -4306,9 +4314,16 @@ hipError_t launch_scan(const uint8_t* d_buf, const ScanSeg* d_segs, uint32_t nse
         per += per & 1;
         const uint32_t grid = (uint32_t)((ntiles + (uint64_t)per - 1) / per);
         ProfScope ps(prof, s, "k_scan_l2");
-        // SYDELTA_SCAN_DEPTH=1|2 (default 2): level-2 loads in flight per batch tested
-        static const int depth = getenv("SYDELTA_SCAN_DEPTH") && getenv("SYDELTA_SCAN_DEPTH")[0] == '1' ? 1 : 2;
-        if (depth == 1) {
+        // SYDELTA_SCAN_DEPTH=1|2 (default 1; 2 measured 15.10 vs 14.91 ms): level-2 loads in
+        // flight per batch tested
+        static const int depth = getenv("SYDELTA_SCAN_DEPTH") && getenv("SYDELTA_SCAN_DEPTH")[0] == '2' ? 2 : 1;
+        static const bool mask = getenv("SYDELTA_SCAN_MASK") && getenv("SYDELTA_SCAN_MASK")[0] == '1';
+        if (mask) {
+            static hipError_t me = hipFuncSetAttribute((const void*)k_scan_l2<false, 1, true>,
+                                                       hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024 - 256);
+            if (me != hipSuccess) return me;
+            hipLaunchKernelGGL((k_scan_l2<false, 1, true>), dim3(grid), dim3(kT3), L4.total, s, a, per);
+        } else if (depth == 1) {
             if (a.timing) hipLaunchKernelGGL((k_scan_l2<true, 1>), dim3(grid), dim3(kT3), L4.total, s, a, per);
             else hipLaunchKernelGGL((k_scan_l2<false, 1>), dim3(grid), dim3(kT3), L4.total, s, a, per);
         } else {
