@@ -512,7 +512,8 @@ def algo_bytes_per_step(workload: str, n: int, nb_bytes: int, src_bytes: int) ->
     """Algorithmic HBM bytes per step of each kernel that can dominate a workload.  Per
     step the signature kernels read the basis once and the scan reads the source once
     (SURVEY.md section 8(d))."""
-    return {"k_scan": src_bytes, "k_scan_lds": src_bytes, "k_scan_l1": src_bytes,
+    return {"k_scan": src_bytes, "k_scan_lds": src_bytes, "k_scan_l1": src_bytes, "k_scan_l2": src_bytes,
+            "k_scan_w": src_bytes, "k_scan_s": src_bytes,
             "k_sig_fast": nb_bytes if workload in ("c3", "c3b") else n,
             "k_sig_batch": n, "k_sig_wave": n, "k_probe": src_bytes,
             "k_apply": 2 * n,  # apply: every output byte read once and written once
@@ -536,8 +537,9 @@ def roofline(prof: dict, steps: int, algo_step: dict, positions=None, keys=None)
     random filter-word request per window start.  `l2_gather` reports that rate against
     L2_GATHER_PEAK (the measured chip-wide ceiling of random L2 gathers,
     profiles/r02_micro_gather2.txt) when the step's scanned positions are known.  For
-    k_scan_l1 only the positions that pass its 2^20-bit level-1 filter in LDS send a
-    request; that fraction is modelled as 1 - exp(-keys / 2^20) (one bit per key) and
+    the level-1 scans (k_scan_l1 / k_scan_s: 2^20 bits, k_scan_l2: 28672 words = 917504
+    bits, k_scan_w: 2^19 bits) only the positions that pass the level-1 filter in LDS send
+    a request; that fraction is modelled as 1 - exp(-keys / bits) (one bit per key) and
     the entry says so."""
     import math
 
@@ -553,7 +555,8 @@ def roofline(prof: dict, steps: int, algo_step: dict, positions=None, keys=None)
             "kernel": dom, "avg_launch_ms": round(avg_ms, 4), "algorithmic_bytes_per_launch": per_launch}
     # level-1 filter bits (one hash) per key: with P key partitions (SYDELTA_SCAN_L1=2) the
     # scan is launched once per partition and each launch's filter holds 1/P of the keys
-    l1_bits = {"k_scan_l1": (1 << 20) * max(1, round(launches_per_step))}
+    l1_bits = {"k_scan_l1": (1 << 20) * max(1, round(launches_per_step)), "k_scan_s": 1 << 20,
+               "k_scan_l2": 28672 * 32, "k_scan_w": 1 << 19}
     if positions and (dom in ("k_scan_lds", "k_scan") or (dom in l1_bits and keys)):
         per_pos = 1.0 if dom not in l1_bits else 1.0 - math.exp(-keys / float(l1_bits[dom]))
         req = positions * per_pos / launches_per_step  # filter-word requests per launch

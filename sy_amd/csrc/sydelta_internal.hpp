@@ -107,8 +107,8 @@ hipError_t launch_signature_batch(const uint8_t* d_buf, const uint64_t* d_off, c
 hipError_t launch_index_build(const uint32_t* d_weak, const uint64_t* d_strong, DeviceIndex& ix, hipStream_t s,
                               Profiler* prof);
 uint64_t scan_tile_positions();  // positions per tile of the LDS-staged scan
-// SYDELTA_SCAN_L1: 0 k_scan_lds, 1 (default) k_scan_l1, 2 k_scan_l1 over two key
-// partitions, 3 k_scan_s, 4 k_scan_l2 (read per call; the index's level-1 layout is
+// SYDELTA_SCAN_L1: 0 k_scan_lds, 1 k_scan_l1, 2 k_scan_l1 over two key partitions,
+// 3 k_scan_s, 4 (default) k_scan_l2 (read per call; the index's level-1 layout is
 // chosen when it is built)
 int scan_l1_mode();
 // SYDELTA_SCAN_WIDE=0: windows above scan_max_window() take the per-thread k_scan

@@ -2051,7 +2051,7 @@ __global__ __launch_bounds__(kT3, 2) void k_scan_l1(ScanArgs a, uint32_t per, ui
 }
 
 // ===========================================================================
-// k_scan_l2: k_scan_l1 on tiles of 32 Ki positions (SYDELTA_SCAN_L1=4, opt-in)
+// k_scan_l2: k_scan_l1 on tiles of 32 Ki positions (SYDELTA_SCAN_L1=4, the default)
 // ===========================================================================
 // Measured on k_scan_l1 (round 3, C3, SYDELTA_ABLATE): of its 16.8 ms, the tile drains
 // (fat-table round trip + verification) take 4.7 ms and the level-2 loads 4.9 ms, while
@@ -2109,10 +2109,8 @@ __device__ __forceinline__ void load16_nt(const uint8_t* src, uint64_t len, uint
     }
 }
 
-// kDepth: batches whose level-2 loads are in flight while one is tested (1 or 2).
-// kMask: a level-1 miss takes its lane out of the level-2 load (exec mask) instead of
-// asking for an offset past the buffer (SYDELTA_SCAN_MASK=1, an A/B of the address path)
-template <bool kTiming, int kDepth, bool kMask = false>
+// kDepth: batches whose level-2 loads are in flight while one is tested (1 or 2)
+template <bool kTiming, int kDepth>
 __global__ __launch_bounds__(kT3, 2) void k_scan_l2(ScanArgs a, uint32_t per) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     const uint32_t n = a.n;  // kMaxN3 (launch_scan)
@@ -2299,14 +2297,11 @@ __global__ __launch_bounds__(kT3, 2) void k_scan_l2(ScanArgs a, uint32_t per) {
             for (int t = 0; t < kB3; ++t) {
                 const uint32_t p1 = l1_test(w1[t], Bt.hq[t]);
                 if (kTiming) l1pass += __popcll(__ballot(p1));
-                if (kMask) {
-                    uint32_t w2 = 0;
-                    if (p1) w2 = __builtin_amdgcn_raw_buffer_load_b32(frsrc, (int)(off[t] << 2), 0, 0);
-                    Bt.w2[t] = w2;
-                } else {
-                    // a level-1 miss asks for an offset past the buffer: no request, reads 0
-                    Bt.w2[t] = __builtin_amdgcn_raw_buffer_load_b32(frsrc, (int)((off[t] << 2) | (p1 - 1u)), 0, 0);
-                }
+                // a level-1 miss asks for an offset past the buffer: no request, reads 0
+                // (taking the lane out of the load with the exec mask instead measured the
+                // same: 15.00 vs 14.85 ms, TA busy 1.89e9 vs 1.93e9; the address path is
+                // not the bound)
+                Bt.w2[t] = __builtin_amdgcn_raw_buffer_load_b32(frsrc, (int)((off[t] << 2) | (p1 - 1u)), 0, 0);
             }
         };
         auto finish = [&](uint32_t g, L1Batch& Bt, uint32_t& todo) -> bool {
@@ -4038,14 +4033,14 @@ __global__ void k_synth_mutate(uint8_t* __restrict__ dst, const uint8_t* __restr
 // ===========================================================================
 static inline unsigned grid_for(uint64_t threads, unsigned block) { return (unsigned)((threads + block - 1) / block); }
 
-// Large single-file indexes scan with k_scan_l1 by default: 17.24 ms per 4 GiB against
-// k_scan_lds's 19.2 ms in global-filter mode.  SYDELTA_SCAN_L1=0
-// selects k_scan_lds (read per call: the parity tests run both).
-// SYDELTA_SCAN_L1=2 builds the level-1 filter in two key partitions and scans once per
-// partition (l1_part).
+// Large single-file indexes (block size 4096) scan with k_scan_l2 by default: 14.85-14.91
+// ms per 4 GiB against k_scan_l1's 16.78 ms and k_scan_lds's 19.2 ms in global-filter mode
+// (DESIGN.md section 6).  SYDELTA_SCAN_L1 (read when the index is built and per call: the
+// parity tests run every scanner): 0 k_scan_lds, 1 k_scan_l1, 2 k_scan_l1 over two key
+// partitions (l1_part), 3 k_scan_s, 4 k_scan_l2.
 int scan_l1_mode() {
     const char* e = getenv("SYDELTA_SCAN_L1");
-    return (e && e[0] >= '0' && e[0] <= '4' && e[1] == 0) ? e[0] - '0' : 1;
+    return (e && e[0] >= '0' && e[0] <= '4' && e[1] == 0) ? e[0] - '0' : 4;
 }
 int scan_wide_mode() {
     const char* e = getenv("SYDELTA_SCAN_WIDE");
@@ -4317,13 +4312,7 @@ hipError_t launch_scan(const uint8_t* d_buf, const ScanSeg* d_segs, uint32_t nse
         // SYDELTA_SCAN_DEPTH=1|2 (default 1; 2 measured 15.10 vs 14.91 ms): level-2 loads in
         // flight per batch tested
         static const int depth = getenv("SYDELTA_SCAN_DEPTH") && getenv("SYDELTA_SCAN_DEPTH")[0] == '2' ? 2 : 1;
-        static const bool mask = getenv("SYDELTA_SCAN_MASK") && getenv("SYDELTA_SCAN_MASK")[0] == '1';
-        if (mask) {
-            static hipError_t me = hipFuncSetAttribute((const void*)k_scan_l2<false, 1, true>,
-                                                       hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024 - 256);
-            if (me != hipSuccess) return me;
-            hipLaunchKernelGGL((k_scan_l2<false, 1, true>), dim3(grid), dim3(kT3), L4.total, s, a, per);
-        } else if (depth == 1) {
+        if (depth == 1) {
             if (a.timing) hipLaunchKernelGGL((k_scan_l2<true, 1>), dim3(grid), dim3(kT3), L4.total, s, a, per);
             else hipLaunchKernelGGL((k_scan_l2<false, 1>), dim3(grid), dim3(kT3), L4.total, s, a, per);
         } else {
