@@ -2430,36 +2430,43 @@ __global__ __launch_bounds__(kT3, 2) void k_scan_l2(ScanArgs a, uint32_t per) {
 // enter them, [T0 + n, T0 + n + kTileW) (rows 256..512, staged from the 16-byte granule
 // that holds T0 + n, in-byte j at region offset o_n + j, o_n = n mod 16).  Windows are
 // carried from tile to tile instead of summed: the workgroup keeps (S, B) of the window
-// at T0, S = sum x, B = sum (n - i) x_i, and thread t's first window [T0 + 32t, +n)
-// follows in closed form (rolling.rs:66-79 applied d = 32t times):
+// at T0, S = sum x, B = sum (n - i) x_i, and thread t's first window [T0 + 64t, +n)
+// follows in closed form (rolling.rs:66-79 applied d = 64t times):
 //   S(d) = S0 + In(d) - Out(d)
 //   B(d) = B0 + d S0 - n Out(d) + sum_{j<d} (d - j) in_j - sum_{j<d} (d - j) out_j
-// from prefix sums of the two regions' 32-byte halves (two wave scans each, the waves'
+// from prefix sums of the two regions' 64-byte rows (two wave scans each, the waves'
 // totals through LDS).  The window at a segment's first tile (or at the workgroup's
-// first) is summed from global memory.  The roll, the level-1 filter (kL1WordsWide words
-// in LDS, word q >> 18), the level-2 buffer loads and the fat-table drain are k_scan_l1's;
-// weak hits are verified from global memory (wave_hash_long: the window is not in LDS).
+// first) is summed from global memory.  A tile is two host tiles (32 Ki positions, 64
+// per thread: the window phase, drain round trip and barrier are paid once per 32 Ki
+// positions), as in k_scan_l2, whose trimmed roll and queue fast path it shares; the
+// level-1 filter is kL1WordsWide words in LDS (word q >> 18), the level-2 buffer loads
+// and the fat-table drain are k_scan_l1's; weak hits are verified from global memory
+// (wave_hash_long: the window is not in LDS).  Round 3's first version (16 Ki-position
+// tiles, k_scan_l1's untrimmed roll, 32 VGPRs spilled) took 25.98 ms per 4 GiB at bs
+// 65536 with every position literal.
 constexpr int kTW = 512;                        // threads per workgroup (8 waves)
-constexpr int kRW = 32;                         // positions per thread = one 32-byte half
-constexpr int kTileW = kTW * kRW;               // 16384 positions per tile
-constexpr int kRowsW = 2 * (kTileW / 64) + 1;   // out rows 0..255, in rows 256..511, row 512: 16 bytes
-static_assert(kTileW == kTile2, "k_scan_w shares the host's tiling");
+constexpr int kRW = 64;                         // positions per thread = one 64-byte row
+constexpr int kTileW = kTW * kRW;               // 32768 positions per tile = two host tiles
+constexpr int kRowsW = 2 * kTW + 1;             // out rows 0..511, in rows 512..1023, row 1024: 16 bytes
+constexpr int kNBW = kRW / kB3;                 // batches per thread per tile
+static_assert(kTileW == 2 * kTile2, "a k_scan_w tile is two host tiles");
 
 struct LdsW {
     uint32_t ntab, fq, wq, wt, red, l1, total;  // byte offsets
 };
-__host__ __device__ __forceinline__ LdsW ldsw_layout() {
-    LdsW L;
+__host__ __device__ constexpr LdsW ldsw_layout() {
+    LdsW L{};
     uint32_t o = kRowsW * kRowDw * 4;
     o = (o + 15) & ~15u; L.ntab = o; o += 256 * 4;
     L.fq = o; o += (kTW / 64) * kFQ3 * 8;
     L.wq = o; o += (kTW / 64) * kWQ3 * 16;
-    L.wt = o; o += (kTW / 64) * 4 * 4;   // per wave: totals of its halves' four sums
+    L.wt = o; o += (kTW / 64) * 4 * 4;   // per wave: totals of its rows' four sums
     L.red = o; o += (kTW / 64) * 16;     // per wave: a fresh window's (S, B) partial sums
     o = (o + 15) & ~15u; L.l1 = o; o += kL1WordsWide * 4;
     L.total = o;
     return L;
 }
+static_assert(ldsw_layout().total <= 160 * 1024 - 256, "k_scan_w's LDS");
 
 // Byte sum and weighted sum (weights 0..4k-1) of the first k dwords of x, bytes below
 // `lim` only (lim <= 4k).
@@ -2475,10 +2482,11 @@ __device__ __forceinline__ void half_sums(const uint32_t* x, int k, uint32_t lim
     }
 }
 
+template <bool kTiming>
 __global__ __launch_bounds__(kTW, 2) void k_scan_w(ScanArgs a, uint32_t per) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     const uint32_t n = a.n;
-    const LdsW L = ldsw_layout();
+    constexpr LdsW L = ldsw_layout();
     uint32_t* rows = (uint32_t*)smem;
     uint32_t* ntab = (uint32_t*)(smem + L.ntab);
     uint32_t* wt = (uint32_t*)(smem + L.wt);
@@ -2503,11 +2511,19 @@ __global__ __launch_bounds__(kTW, 2) void k_scan_w(ScanArgs a, uint32_t per) {
     const uint32_t nal = n - on;                     // in-region start relative to T0
     const uint32_t sh = n & 3;
     const uint32_t rel0 = tid * kRW;
-    const uint32_t orow = (tid >> 1) * kRowDw + 8 * (tid & 1);  // this thread's first out dword
-    const uint32_t din0 = (kTileW + on + rel0) >> 2;            // ... and first in dword (rows 256..)
+    const uint32_t orow = tid * kRowDw;              // this thread's out bytes: row tid
+    const uint32_t din0 = (kTileW + on + rel0) >> 2; // ... and its first in dword (rows 512..)
     const uint32_t nmod = a.nm;
     unsigned long long passes = 0, weak_hits = 0;
     uint32_t nfq = 0;
+    unsigned long long tm[6] = {0, 0, 0, 0, 0, 0}, l1pass = 0;
+    unsigned long long tprev = kTiming ? __builtin_amdgcn_s_memtime() : 0;
+#define PHASE_MARKW(k)                                                 \
+    if (kTiming) {                                                     \
+        const unsigned long long tnow = __builtin_amdgcn_s_memtime(); \
+        tm[k] += tnow - tprev;                                         \
+        tprev = tnow;                                                  \
+    }
 
     auto seg_ctx = [&](uint32_t tile, uint32_t si0, SegCtx& sc, uint32_t& si, uint64_t& tile_start,
                        uint64_t& seg_len) {
@@ -2530,56 +2546,62 @@ __global__ __launch_bounds__(kTW, 2) void k_scan_w(ScanArgs a, uint32_t per) {
         sc.fwshift = F.fwshift;
         sc.filt = a.filt + F.filt_off;
         sc.fwords = 1u << (32 - F.fwshift);
-        tile_start = S.pos_begin + (uint64_t)(tile - S.tile_base) * kTileW;
+        tile_start = S.pos_begin + (uint64_t)(tile - S.tile_base) * kTile2;
         seg_len = S.len;
+    };
+    // host tiles this tile covers: 2 when host tile t+1 is in this workgroup's range and
+    // in the same segment as t (segment sidx); a lone host tile ends a segment or the range,
+    // so its window is never carried
+    auto span_of = [&](uint32_t t, uint32_t sidx) -> uint32_t {
+        if (t + 1 >= t_end) return 1;
+        if (sidx + 1 < a.nsegs && a.segs[sidx + 1].tile_base <= t + 1) return 1;
+        return 2;
     };
     SegCtx sc, nsc;
     uint32_t si = 0, nsi = 0;
     uint64_t tile_start = 0, seg_len = 0, ntile_start = 0, nseg_len = 0;
     seg_ctx(t_begin, 0, nsc, nsi, ntile_start, nseg_len);
-    // rows of the next tile, loaded ahead: thread c stages row c (c < 256: out bytes,
-    // else in bytes); thread 0 also the first 16 bytes of row 512
-    auto row_addr = [&](uint64_t t0, uint32_t c) -> uint64_t {
-        return c < (uint32_t)(kTileW / 64) ? t0 + 64ull * c : t0 + nal + 64ull * (c - kTileW / 64);
-    };
-    uint32_t x[16], xt[4] = {0, 0, 0, 0};
-    load_chunk_nt(nsc.base, nseg_len, row_addr(ntile_start, tid), x);
-    if (tid == 0) {
-        uint32_t y[16];
-        load_chunk_nt(nsc.base, nseg_len, row_addr(ntile_start, kRowsW - 1), y);
-        xt[0] = y[0]; xt[1] = y[1]; xt[2] = y[2]; xt[3] = y[3];
-    }
+    uint32_t nspan = span_of(t_begin, nsi);
+    // the next tile's rows, loaded ahead: thread c stages out row c and in row 512 + c,
+    // thread 0 also the 16 bytes of row 1024 (all 16-byte aligned: segment starts and nal are)
+    uint32_t x[16], y[16], xt[4] = {0, 0, 0, 0};
+    load_chunk_nt(nsc.base, nseg_len, ntile_start + 64ull * tid, x);
+    load_chunk_nt(nsc.base, nseg_len, ntile_start + nal + 64ull * tid, y);
+    if (tid == 0) load16_nt(nsc.base, nseg_len, ntile_start + nal + (uint64_t)kTileW, xt);
     uint32_t S0 = 0, B0 = 0;  // window at tile_start: byte sum (exact) and B mod M
     bool carried = false;     // (S0, B0) hold the window at this tile's start
 
+    uint32_t tile = t_begin;
 #pragma unroll 1
-    for (uint32_t tile = t_begin; tile < t_end; ++tile) {
+    while (tile < t_end) {
         sc = nsc;
         si = nsi;
         tile_start = ntile_start;
         seg_len = nseg_len;
+        const uint32_t span = nspan;
         // ---- stage (the previous tile's last barrier ended every read of the rows)
 #pragma unroll
         for (int i = 0; i < 16; ++i) rows[tid * kRowDw + i] = x[i];
+#pragma unroll
+        for (int i = 0; i < 16; ++i) rows[(kTW + tid) * kRowDw + i] = y[i];
         if (tid == 0) {
 #pragma unroll
             for (int i = 0; i < 4; ++i) rows[(kRowsW - 1) * kRowDw + i] = xt[i];
         }
-        // a segment's first tile: its first window from global memory
+        // a segment's (or the range's) first tile: its first window from global memory
         if (!carried) {
             uint64_t s = 0, b = 0;
             for (uint32_t gr = tid; 16 * gr < n; gr += kTW) {
-                uint32_t y[16];
-                const uint64_t at = tile_start + 16ull * gr;
+                uint32_t z[4];
                 // 16 bytes at a 16-byte aligned offset (tile starts are), bytes past the
                 // window or the segment's source masked
                 const uint32_t lim = min(16u, n - 16 * gr);
-                load_chunk(sc.base, seg_len, at & ~63ull, y);
-                const uint32_t q = (uint32_t)((at >> 2) & 12);
+                load16_nt(sc.base, seg_len, tile_start + 16ull * gr, z);
+#pragma unroll
                 for (int i = 0; i < 4; ++i) {
                     const uint32_t bb = 4u * (uint32_t)i;
                     const uint32_t keep = lim >= bb + 4 ? 0xFFFFFFFFu : lim <= bb ? 0u : (0xFFFFFFFFu >> (8 * (bb + 4 - lim)));
-                    const uint32_t d = y[q + i] & keep;
+                    const uint32_t d = z[i] & keep;
                     const uint32_t ds = udot4(d, 0x01010101u, 0);
                     const uint32_t du = udot4(d, offw(i), 0);  // weights bb .. bb+3
                     s += ds;
@@ -2597,50 +2619,55 @@ __global__ __launch_bounds__(kTW, 2) void k_scan_w(ScanArgs a, uint32_t per) {
         }
         __syncthreads();
         // next tile's rows, issued now: their latency hides behind the window phase and the roll
-        const bool next_same = tile + 1 < t_end && !(nsi + 1 < a.nsegs && a.segs[nsi + 1].tile_base <= tile + 1);
-        if (tile + 1 < t_end) {
-            if (!next_same)
-                seg_ctx(tile + 1, nsi, nsc, nsi, ntile_start, nseg_len);  // the next segment
-            else
-                ntile_start = tile_start + kTileW;
-            load_chunk_nt(nsc.base, nseg_len, row_addr(ntile_start, tid), x);
-            if (tid == 0) {
-                uint32_t y[16];
-                load_chunk_nt(nsc.base, nseg_len, row_addr(ntile_start, kRowsW - 1), y);
-                xt[0] = y[0]; xt[1] = y[1]; xt[2] = y[2]; xt[3] = y[3];
+        const uint32_t nt = tile + span;
+        bool next_same = false;
+        if (nt < t_end) {
+            if (nsi + 1 < a.nsegs && a.segs[nsi + 1].tile_base <= nt) {
+                seg_ctx(nt, nsi, nsc, nsi, ntile_start, nseg_len);  // the next segment
+            } else {
+                ntile_start = tile_start + (uint64_t)span * kTile2;
+                next_same = true;  // then span == 2: a lone host tile ends the range or its segment
             }
+            nspan = span_of(nt, nsi);
+            load_chunk_nt(nsc.base, nseg_len, ntile_start + 64ull * tid, x);
+            load_chunk_nt(nsc.base, nseg_len, ntile_start + nal + 64ull * tid, y);
+            if (tid == 0) load16_nt(nsc.base, nseg_len, ntile_start + nal + (uint64_t)kTileW, xt);
         }
+        // positions of this tile that belong to it: [tile_start, tile_start + span * kTile2)
+        sc.pos_end = min(sc.pos_end, tile_start + (uint64_t)span * kTile2);
+        PHASE_MARKW(0)
 
-        // ---- window: half t of each region
+        // ---- window: row t of each region
         uint32_t am, bm;
         {
             const uint32_t* ro = rows + orow;
-            const uint32_t* ri = rows + (kTileW / 64 + (tid >> 1)) * kRowDw + 8 * (tid & 1);
+            const uint32_t* ri = rows + (kTW + tid) * kRowDw;
             uint32_t so, uo, si_, ui, ps, pu;
-            half_sums(ro, 8, 32, so, uo);
-            half_sums(ri, 8, 32, si_, ui);
-            half_sums(ri, 4, on, ps, pu);  // the first `on` bytes of the in half
-            const uint32_t wo = (32u * tid * so + uo) % kMod;   // < 2^32: 32*511*8160 + 31*8160
-            const uint32_t wi = (32u * tid * si_ + ui) % kMod;
+            half_sums(ro, 16, 64, so, uo);
+            half_sums(ri, 16, 64, si_, ui);
+            half_sums(ri, 4, on, ps, pu);  // the first `on` bytes of the in row
+            const uint32_t wo = (64u * tid * so + uo) % kMod;   // < 2^32: 64*511*16320 + 63*16320
+            const uint32_t wi = (64u * tid * si_ + ui) % kMod;
             uint32_t Tso, Two, Tsi, Twi;
             const uint32_t Eso = wave_scan_excl(so, Tso), Ewo = wave_scan_excl(wo, Two);
             const uint32_t Esi = wave_scan_excl(si_, Tsi), Ewi = wave_scan_excl(wi, Twi);
             if (lane == 0) { wt[4 * wid] = Tso; wt[4 * wid + 1] = Two; wt[4 * wid + 2] = Tsi; wt[4 * wid + 3] = Twi; }
-            // partial sums of the first `on` bytes of in-region half 0 and of row 512
+            // partial sums of the first `on` bytes of in row 0 and of row 1024
             uint32_t ps0, pu0, psT, puT;
-            half_sums(rows + (kTileW / 64) * kRowDw, 4, on, ps0, pu0);
+            half_sums(rows + kTW * kRowDw, 4, on, ps0, pu0);
             half_sums(rows + (kRowsW - 1) * kRowDw, 4, on, psT, puT);
             __syncthreads();
             uint32_t Bso = 0, Bwo = 0, Bsi = 0, Bwi = 0, Aso = 0, Awo = 0, Asi = 0, Awi = 0;
+#pragma unroll
             for (uint32_t w = 0; w < (uint32_t)(kTW / 64); ++w) {
                 const uint4 v = *(const uint4*)(wt + 4 * w);
                 if (w < wid) { Bso += v.x; Bwo += v.y; Bsi += v.z; Bwi += v.w; }
                 Aso += v.x; Awo += v.y; Asi += v.z; Awi += v.w;
             }
-            // window of position d (d = 32 t here, kTileW for the next tile's carry), from the
-            // region prefixes at half t: out sums Os (exact), Ow (mod M); in-region sums up to
-            // half t, Is (exact), Iw (mod M), and the partials (ps, pu) of the in half's
-            // first `on` bytes
+            // window of position d (d = 64 t here, kTileW for the next tile's carry), from the
+            // region prefixes at row t: out sums Os (exact), Ow (mod M); in-region sums up to
+            // row t, Is (exact), Iw (mod M), and the partials (ps, pu) of the in row's first
+            // `on` bytes
             auto window = [&](uint32_t d, uint32_t Os, uint32_t Ow, uint32_t Is, uint32_t Iw, uint32_t p_s,
                               uint32_t p_u, uint32_t& A, uint32_t& B) {
                 const uint32_t Rs = Is + p_s;                                       // in-region bytes [0, on + d)
@@ -2658,7 +2685,7 @@ __global__ __launch_bounds__(kTW, 2) void k_scan_w(ScanArgs a, uint32_t per) {
                 B = (uint32_t)(b % kMod);
             };
             uint32_t Sd, Bd;
-            window(32u * tid, Bso + Eso, (Bwo + Ewo) % kMod, Bsi + Esi, (Bwi + Ewi) % kMod, ps, pu, Sd, Bd);
+            window(64u * tid, Bso + Eso, (Bwo + Ewo) % kMod, Bsi + Esi, (Bwi + Ewi) % kMod, ps, pu, Sd, Bd);
             am = (1 + Sd) % kMod;
             bm = (n + Bd) % kMod;
             // the next tile's first window, when it continues this segment
@@ -2668,8 +2695,9 @@ __global__ __launch_bounds__(kTW, 2) void k_scan_w(ScanArgs a, uint32_t per) {
             S0 = Sn;
             B0 = Bn;
         }
+        PHASE_MARKW(1)
 
-        // ---- roll (k_scan_l1's; positions past pos_end are dropped by the drain)
+        // ---- roll (k_scan_l2's; positions past sc.pos_end are dropped by the drain)
         const uint64_t fptr = (uint64_t)(uintptr_t)sc.filt;
         const uint32_t fp_lo = __builtin_amdgcn_readfirstlane((uint32_t)fptr);
         const uint32_t fp_hi = __builtin_amdgcn_readfirstlane((uint32_t)(fptr >> 32));
@@ -2703,7 +2731,7 @@ __global__ __launch_bounds__(kTW, 2) void k_scan_w(ScanArgs a, uint32_t per) {
                 Bt.wv[t] = (bm << 16) | am;
                 const ProbeHash h = probe_hash(am, bm);
                 Bt.hq[t] = h.q;
-                off[t] = (h.r >> fwshift) * 4;
+                off[t] = h.r >> fwshift;
                 w1[t] = l1[h.q >> 18];
                 const uint32_t u = am + in + (kMod - out);  // [M-255, 2M+255)
                 am = min(u, min(u - kMod, u - 2 * kMod));
@@ -2713,15 +2741,32 @@ __global__ __launch_bounds__(kTW, 2) void k_scan_w(ScanArgs a, uint32_t per) {
 #pragma unroll
             for (int t = 0; t < kB3; ++t) {
                 const uint32_t p1 = l1_test(w1[t], Bt.hq[t]);
-                Bt.w2[t] = __builtin_amdgcn_raw_buffer_load_b32(frsrc, (int)(p1 ? off[t] : 0xFFFFFFFFu), 0, 0);
+                if (kTiming) l1pass += __popcll(__ballot(p1));
+                // a level-1 miss asks for an offset past the buffer: no request, reads 0
+                Bt.w2[t] = __builtin_amdgcn_raw_buffer_load_b32(frsrc, (int)((off[t] << 2) | (p1 - 1u)), 0, 0);
             }
         };
         auto finish = [&](uint32_t g, L1Batch& Bt, uint32_t& todo) -> bool {
             uint32_t pbits = 0;
 #pragma unroll
-            for (int t = 0; t < kB3; ++t) pbits |= (filt_pass(Bt.w2[t], Bt.hq[t]) ? 1u : 0u) << t;
+            for (int t = 0; t < kB3; ++t) pbits |= filt_bit(Bt.w2[t], Bt.hq[t]) << t;
             asm volatile("" : "+v"(pbits));
             const uint64_t below = (1ull << lane) - 1;
+            const uint64_t anyp = __ballot((pbits & todo) != 0);
+            if (nfq + 8u * (uint32_t)__popcll(anyp) <= (uint32_t)kFQ3) {
+                if (anyp) {
+#pragma unroll
+                    for (int t = 0; t < kB3; ++t) {
+                        if (!((todo >> t) & 1)) continue;
+                        const uint64_t mk = __ballot((pbits >> t) & 1);
+                        if (!mk) continue;
+                        if ((pbits >> t) & 1) fq[nfq + __popcll(mk & below)] = make_uint2(rel0 + g + t, Bt.wv[t]);
+                        nfq += __popcll(mk);
+                    }
+                }
+                todo = 0xFFu;
+                return true;
+            }
             uint32_t need = 0;
 #pragma unroll
             for (int t = 0; t < kB3; ++t)
@@ -2740,51 +2785,58 @@ __global__ __launch_bounds__(kTW, 2) void k_scan_w(ScanArgs a, uint32_t per) {
             if (all) todo = 0xFFu;
             return all;
         };
-        uint32_t stop = 4, todo = 0xFFu, ra = 0, rb = 0;
+        // Pipeline over the thread's 8 batches: batch k+1's level-2 loads are in flight
+        // while batch k is tested; a batch the queue cannot take stops it, the queue is
+        // drained and the roll resumes from that batch's saved state.
+        uint32_t stop = kNBW, todo = 0xFFu, ra = 0, rb = 0;
         {
             L1Batch b0, b1;
-            const uint32_t a0 = am, s0 = bm;
+            uint32_t sa0 = am, sb0 = bm;
             compute(0, b0);
-            const uint32_t a1 = am, s1 = bm;
-            compute(8, b1);
-            if (!finish(0, b0, todo)) { stop = 0; ra = a0; rb = s0; }
-            if (stop == 4) {
-                const uint32_t a2 = am, s2 = bm;
-                compute(16, b0);
-                if (!finish(8, b1, todo)) { stop = 1; ra = a1; rb = s1; }
-                if (stop == 4) {
-                    const uint32_t a3 = am, s3 = bm;
-                    compute(24, b1);
-                    if (!finish(16, b0, todo)) { stop = 2; ra = a2; rb = s2; }
-                    if (stop == 4 && !finish(24, b1, todo)) { stop = 3; ra = a3; rb = s3; }
-                }
+            uint32_t sa1 = am, sb1 = bm;
+            compute(kB3, b1);
+#pragma unroll 1
+            for (uint32_t k = 0; k < (uint32_t)kNBW; k += 2) {
+                if (!finish(kB3 * k, b0, todo)) { stop = k; ra = sa0; rb = sb0; break; }
+                if (k + 2 < (uint32_t)kNBW) { sa0 = am; sb0 = bm; compute(kB3 * (k + 2), b0); }
+                if (!finish(kB3 * (k + 1), b1, todo)) { stop = k + 1; ra = sa1; rb = sb1; break; }
+                if (k + 3 < (uint32_t)kNBW) { sa1 = am; sb1 = bm; compute(kB3 * (k + 3), b1); }
             }
         }
-        while (stop < 4) {
+        while (stop < (uint32_t)kNBW) {
             passes += nfq;
             drain_l1<false>(a, fq, nfq, wq, weak_hits, rows, tile_start, sc);
             nfq = 0;
             uint32_t k = stop;
-            stop = 4;
+            stop = kNBW;
             am = ra;
             bm = rb;
 #pragma unroll 1
-            for (; k < 4; ++k) {
+            for (; k < (uint32_t)kNBW; ++k) {
                 L1Batch bt;
                 const uint32_t ak = am, sk = bm;
-                compute(8 * k, bt);
-                if (!finish(8 * k, bt, todo)) { stop = k; ra = ak; rb = sk; break; }
+                compute(kB3 * k, bt);
+                if (!finish(kB3 * k, bt, todo)) { stop = k; ra = ak; rb = sk; break; }
             }
         }
+        PHASE_MARKW(2)
+        PHASE_MARKW(3)
         if (nfq) {
             passes += nfq;
             drain_l1<false>(a, fq, nfq, wq, weak_hits, rows, tile_start, sc);
             nfq = 0;
         }
+        PHASE_MARKW(4)
         __syncthreads();  // rows (and wt) are rewritten by the next tile
+        PHASE_MARKW(5)
+        tile += span;
     }
+#undef PHASE_MARKW
     if (lane == 0 && passes) atomicAdd(&a.counters[2], passes);
     if (lane == 0 && weak_hits) atomicAdd(&a.counters[1], weak_hits);
+    if (kTiming && lane == 0) atomicAdd(&a.counters[3], l1pass);
+    if (kTiming && tid == 0)
+        for (int k = 0; k < 6; ++k) atomicAdd(&a.counters[4 + k], tm[k]);
 }
 
 // ===========================================================================
@@ -4261,21 +4313,24 @@ hipError_t launch_scan(const uint8_t* d_buf, const ScanSeg* d_segs, uint32_t nse
         static hipError_t w_err = hipSuccess;
         static int w_cus = 256;
         std::call_once(w_once, [] {
-            w_err = hipFuncSetAttribute((const void*)k_scan_w, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                        160 * 1024 - 256);
+            for (const void* f : {(const void*)k_scan_w<false>, (const void*)k_scan_w<true>})
+                if (w_err == hipSuccess)
+                    w_err = hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024 - 256);
             int dev = 0, cus = 0;
             if (hipGetDevice(&dev) == hipSuccess &&
                 hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess && cus > 0)
                 w_cus = cus;
         });
         if (w_err != hipSuccess) return w_err;
-        const LdsW LW = ldsw_layout();
-        if (LW.total > 160u * 1024 - 256) return hipErrorInvalidValue;
-        // one workgroup per CU, contiguous tile ranges (a range's windows are carried)
-        const uint32_t grid = (uint32_t)std::min<uint64_t>(ntiles, (uint64_t)w_cus);
-        const uint32_t per = (ntiles + grid - 1) / grid;
+        constexpr LdsW LW = ldsw_layout();
+        // one workgroup per CU, contiguous ranges of an even number of host tiles (a range's
+        // windows are carried; the pairs line up)
+        uint32_t per = (uint32_t)((ntiles + (uint64_t)w_cus - 1) / (uint64_t)w_cus);
+        per += per & 1;
+        const uint32_t grid = (uint32_t)((ntiles + (uint64_t)per - 1) / per);
         ProfScope ps(prof, s, "k_scan_w");
-        hipLaunchKernelGGL(k_scan_w, dim3(grid), dim3(kTW), LW.total, s, a, per);
+        if (a.timing) hipLaunchKernelGGL(k_scan_w<true>, dim3(grid), dim3(kTW), LW.total, s, a, per);
+        else hipLaunchKernelGGL(k_scan_w<false>, dim3(grid), dim3(kTW), LW.total, s, a, per);
         return hipGetLastError();
     }
     static std::once_flag l1_once;
