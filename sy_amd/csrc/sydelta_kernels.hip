@@ -636,6 +636,17 @@ struct ScanArgs {
     uint64_t out_cap;
     unsigned long long* counters;  // [0] verified hits, [1] weak hits, [2] filter passes, [4..8) phase cycles
     uint2* gfq;          // k_scan_lds: per-wave filter-pass queues in HBM/L2, kGFQ entries each
+    struct WDef* wdef;   // k_scan_w: weak hits whose verification k_verify_w does (count: counters[10])
+    uint64_t wdef_cap;
+};
+
+// A weak hit of k_scan_w, verified after the scan by k_verify_w.
+struct WDef {
+    uint64_t at;      // byte offset of the window in ScanArgs::src
+    uint64_t key;     // its hit key: (segment << kSegShift) | position - segment start
+    uint32_t cand;    // fat record: first candidate, or kMulti + slot
+    uint32_t pad;
+    uint64_t strong;  // the first candidate's strong hash (single-candidate records)
 };
 
 // The segment a tile belongs to, as the drains see it.
@@ -2444,6 +2455,130 @@ __global__ __launch_bounds__(kT3, 2) void k_scan_l2(ScanArgs a, uint32_t per) {
 // (wave_hash_long: the window is not in LDS).  Round 3's first version (16 Ki-position
 // tiles, k_scan_l1's untrimmed roll, 32 VGPRs spilled) took 25.98 ms per 4 GiB at bs
 // 65536 with every position literal.
+// k_scan_w's drain: fat-table lookups of this wave's queued level-2 passes (as
+// drain_l1); each weak hit is appended to the deferred list (a.wdef) for k_verify_w
+// instead of being hashed here.  A window above 8 KiB is hashed from global memory by
+// one wave at the latency of its dependent loads (tens of microseconds for 64 KiB), and
+// measured at bs 65536 that made the other seven waves wait at the tile's barrier for
+// more than half of the kernel (phase cycles, round 3).  Hits the full list cannot take
+// (dense data) are verified here, as drain_l1 does.
+__device__ __forceinline__ void drain_w(const ScanArgs& a, const uint2* fq, uint32_t nfq, uint4* wq,
+                                        unsigned long long& weak_hits, uint64_t tile_start, const SegCtx& cur) {
+    const uint32_t lane = threadIdx.x & 63;
+    const uint64_t below = (1ull << lane) - 1;
+    lds_fence();
+    uint32_t nwq = 0;
+    for (uint32_t base = 0; base < nfq; base += 64) {
+        const uint32_t i = base + lane;
+        bool hit = false;
+        uint4 rec = make_uint4(0, 0, 0, 0);
+        uint32_t tp = 0;
+        if (i < nfq) {
+            const uint2 e = fq[i];  // {position in tile, weak}
+            tp = e.x;
+            if (tile_start + e.x < cur.pos_end) hit = fat_find(cur.fat, cur.bmask, e.y, rec);
+        }
+        const uint64_t m = __ballot(hit);
+        if (!m) continue;
+        const uint32_t cnt = __popcll(m);
+        weak_hits += cnt;
+        unsigned long long k0 = 0;
+        if (lane == 0) k0 = atomicAdd(&a.counters[10], (unsigned long long)cnt);
+        k0 = shfl64(k0, 0);
+        const uint64_t slot = k0 + __popcll(m & below);
+        const bool deferred = hit && slot < a.wdef_cap;
+        if (deferred) {
+            const uint64_t pos = tile_start + tp;
+            WDef d;
+            d.at = (uint64_t)(cur.base - a.src) + pos;
+            d.key = ((uint64_t)cur.seg_id << kSegShift) | (pos - cur.pos_begin);
+            d.cand = rec.y;
+            d.pad = 0;
+            d.strong = ((uint64_t)rec.w << 32) | rec.z;
+            a.wdef[slot] = d;
+        }
+        const uint64_t mi = __ballot(hit && !deferred);
+        if (!mi) continue;
+        const uint32_t ci = __popcll(mi);
+        const uint32_t rank = __popcll(mi & below);
+        if (nwq + ci > (uint32_t)kWQ3) {
+            verify_l1<false>(a, wq, nwq, nullptr, tile_start, cur);
+            nwq = 0;
+        }
+        const uint4 e = make_uint4(tp, rec.y, rec.z, rec.w);
+        const bool mine = hit && !deferred;
+        if (ci > (uint32_t)kWQ3) {  // more than wq holds: two halves
+            if (mine && rank < (uint32_t)kWQ3) wq[rank] = e;
+            verify_l1<false>(a, wq, kWQ3, nullptr, tile_start, cur);
+            if (mine && rank >= (uint32_t)kWQ3) wq[rank - kWQ3] = e;
+            nwq = ci - kWQ3;
+        } else {
+            if (mine) wq[nwq + rank] = e;
+            nwq += ci;
+        }
+    }
+    verify_l1<false>(a, wq, nwq, nullptr, tile_start, cur);
+    lds_fence();
+}
+
+// The deferred weak hits of a k_scan_w launch (counters[10] of them, at most wdef_cap):
+// XXH3 of each window (four windows per wave, one per 16-lane row, when n % 64 == 0;
+// else one per wave), then the first candidate in index order with equal strong
+// (generator.rs:127-133); verified hits to the output like verify_l1.
+__global__ __launch_bounds__(256) void k_verify_w(ScanArgs a) {
+    const uint32_t lane = threadIdx.x & 63;
+    const uint32_t row = lane >> 4, rl = lane & 15;
+    const uint64_t total = min((uint64_t)a.counters[10], a.wdef_cap);
+    const uint64_t wave = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+    const uint64_t nwaves = ((uint64_t)gridDim.x * blockDim.x) >> 6;
+    const bool rows = a.n % 64 == 0;
+    const uint32_t per = rows ? 4u : 1u;
+    for (uint64_t r0 = wave * per; r0 < total; r0 += nwaves * per) {  // wave-uniform
+        const uint64_t ri = rows ? r0 + row : r0;
+        const bool live = ri < total;
+        const WDef d = a.wdef[live ? ri : r0];
+        uint32_t wk;
+        uint64_t st;
+        uint32_t best = kNoBlock;
+        if (rows) {
+            row_hash<false>(a.src + d.at, a.n, wk, st);  // valid in the row's first lane
+            st = ((uint64_t)(uint32_t)__shfl((int)(uint32_t)(st >> 32), (int)(lane & 48)) << 32) |
+                 (uint32_t)__shfl((int)(uint32_t)st, (int)(lane & 48));
+            if (!(d.cand & kMulti)) {
+                if (st == d.strong) best = d.cand;
+            } else {
+                const uint32_t s0 = a.start[d.cand & ~kMulti], cn = a.cnt[d.cand & ~kMulti];
+                for (uint32_t b = 0; b < cn; b += 16) {  // in index order, 16 candidates per step
+                    const uint32_t j = b + rl;
+                    const uint64_t m = (__ballot(j < cn && a.cstrong[s0 + j] == st) >> (row << 4)) & 0xFFFFull;
+                    if (m) {
+                        best = a.order[s0 + b + (uint32_t)__builtin_ctzll(m)];
+                        break;
+                    }
+                }
+            }
+        } else {
+            wave_hash_long(a.src + d.at, a.n, wk, st);
+            if (!(d.cand & kMulti)) {
+                if (st == d.strong) best = d.cand;
+            } else {
+                best = first_strong_match(a.order, a.cstrong, a.start[d.cand & ~kMulti], a.cnt[d.cand & ~kMulti], st);
+            }
+        }
+        const bool v = live && (rows ? rl == 0 : lane == 0) && best != kNoBlock;
+        const uint64_t m = __ballot(v);
+        if (!m) continue;
+        unsigned long long k0 = 0;
+        if (lane == 0) k0 = atomicAdd(&a.counters[0], (unsigned long long)__popcll(m));
+        k0 = shfl64(k0, 0);
+        const unsigned long long k = k0 + __popcll(m & ((1ull << lane) - 1));
+        if (v && k < a.out_cap) {
+            a.hit_key[k] = d.key;
+            a.hit_val[k] = best;
+        }
+    }
+}
+
 constexpr int kTW = 512;                        // threads per workgroup (8 waves)
 constexpr int kRW = 64;                         // positions per thread = one 64-byte row
 constexpr int kTileW = kTW * kRW;               // 32768 positions per tile = two host tiles
@@ -2805,7 +2940,7 @@ __global__ __launch_bounds__(kTW, 2) void k_scan_w(ScanArgs a, uint32_t per) {
         }
         while (stop < (uint32_t)kNBW) {
             passes += nfq;
-            drain_l1<false>(a, fq, nfq, wq, weak_hits, rows, tile_start, sc);
+            drain_w(a, fq, nfq, wq, weak_hits, tile_start, sc);
             nfq = 0;
             uint32_t k = stop;
             stop = kNBW;
@@ -2823,7 +2958,7 @@ __global__ __launch_bounds__(kTW, 2) void k_scan_w(ScanArgs a, uint32_t per) {
         PHASE_MARKW(3)
         if (nfq) {
             passes += nfq;
-            drain_l1<false>(a, fq, nfq, wq, weak_hits, rows, tile_start, sc);
+            drain_w(a, fq, nfq, wq, weak_hits, tile_start, sc);
             nfq = 0;
         }
         PHASE_MARKW(4)
@@ -4328,10 +4463,26 @@ hipError_t launch_scan(const uint8_t* d_buf, const ScanSeg* d_segs, uint32_t nse
         uint32_t per = (uint32_t)((ntiles + (uint64_t)w_cus - 1) / (uint64_t)w_cus);
         per += per & 1;
         const uint32_t grid = (uint32_t)((ntiles + (uint64_t)per - 1) / per);
-        ProfScope ps(prof, s, "k_scan_w");
-        if (a.timing) hipLaunchKernelGGL(k_scan_w<true>, dim3(grid), dim3(kTW), LW.total, s, a, per);
-        else hipLaunchKernelGGL(k_scan_w<false>, dim3(grid), dim3(kTW), LW.total, s, a, per);
-        return hipGetLastError();
+        // deferred weak hits (counters[10] counts them; the caller zeroes the counters):
+        // room for 2^20 (a shifted 64 GiB file at bs 65536 has 2^20 blocks to find)
+        a.wdef_cap = 1u << 20;
+        void* wdef = nullptr;
+        hipError_t e = dev_malloc_async(&wdef, a.wdef_cap * sizeof(WDef), s);
+        if (e != hipSuccess) return e;
+        a.wdef = (WDef*)wdef;
+        {
+            ProfScope ps(prof, s, "k_scan_w");
+            if (a.timing) hipLaunchKernelGGL(k_scan_w<true>, dim3(grid), dim3(kTW), LW.total, s, a, per);
+            else hipLaunchKernelGGL(k_scan_w<false>, dim3(grid), dim3(kTW), LW.total, s, a, per);
+        }
+        e = hipGetLastError();
+        if (e == hipSuccess) {
+            ProfScope ps(prof, s, "k_verify_w");
+            hipLaunchKernelGGL(k_verify_w, dim3(4 * (uint32_t)w_cus), dim3(256), 0, s, a);
+            e = hipGetLastError();
+        }
+        const hipError_t fe = hipFreeAsync(wdef, s);
+        return e != hipSuccess ? e : fe;
     }
     static std::once_flag l1_once;
     static hipError_t l1_err = hipSuccess;
