@@ -13,6 +13,7 @@ files incl. empty and sub-block ones, threaded walks) and a file matched in 1/2/
 chained chunks, the device zstd and signature-JSON writers' host sides.
 """
 import os
+import subprocess
 import sys
 import tempfile
 import types
@@ -80,6 +81,20 @@ def check_pair(tmp, basis, s, bs, tag):
     assert d2 == d, (tag, "in-memory")
 
 
+PIECES_CHILD = """
+import sys, tempfile
+sys.path.insert(0, sys.argv[3])
+import emulated_checks as E
+n = 0
+with tempfile.TemporaryDirectory() as tmp:
+    for bs, size in [(4096, (3 << 20) + 1234), (1007, (2 << 20) + 99), (131072, (3 << 20) + 17)]:
+        basis, s = E.case(bs % 89, size, bs)
+        E.check_pair(tmp, basis, s, bs, ("pieces", bs))
+        n += 1
+print(n)
+"""
+
+
 def main():
     n_checks = 0
     with tempfile.TemporaryDirectory() as tmp:
@@ -96,6 +111,12 @@ def main():
                     check_pair(tmp, basis, s, bs, (chunk, bs, n, probe))
                     n_checks += 1
         os.environ.pop("SYDELTA_PROBE", None)
+        # chunks read in parallel pieces (the path API's reader splits a chunk over the
+        # host pool; SYDELTA_READ_PIECE is read once per process, so a child runs them)
+        r = subprocess.run([sys.executable, "-c", PIECES_CHILD, ROOT, LIB, os.path.dirname(os.path.abspath(__file__))], env=dict(os.environ, SYDELTA_READ_PIECE="65536",
+                           SYDELTA_STREAM_CHUNK=str(1 << 20)), capture_output=True, text=True, timeout=600)
+        assert r.returncode == 0, r.stdout + r.stderr
+        n_checks += int(r.stdout.split()[-1])
         # tiny and empty files
         os.environ["SYDELTA_STREAM_CHUNK"] = "65536"
         for size in (0, 1, 63, 64, 65, 4095, 4096, 4097):
