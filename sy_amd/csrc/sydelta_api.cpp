@@ -1827,13 +1827,14 @@ struct InFile {
     }
     // exactly [off, off + n) (the file must not shrink meanwhile).  A large read is split
     // into pieces of >= 8 MiB read by the shared host pool: one thread copies from the
-    // page cache at ~12 GB/s (round 3, the path API's 4 GiB leg ran at 11.2 GiB/s behind
-    // it), far below the pinned H2D's 57 GB/s.  A failed piece repeats the whole read on
-    // this thread, so sydelta_last_error() names the failure.
+    // page cache at ~12 GB/s, far below the pinned H2D's 57 GB/s (round 3, the path API's
+    // 4 GiB leg: 12.7 GiB/s with 1 reader, 20.0 with 8, 25.7 with 16 on the box's 16-core
+    // share; profiles/r03n_*).  A failed piece repeats the whole read on this thread, so
+    // sydelta_last_error() names the failure.
     int read_at(uint64_t off, uint8_t* dst, uint64_t n) const {
         static const int kReaders = [] {  // SYDELTA_READ_THREADS: readers per chunk
             const char* e = getenv("SYDELTA_READ_THREADS");
-            return (e && *e) ? std::max(1, atoi(e)) : 8;
+            return (e && *e) ? std::max(1, atoi(e)) : 16;
         }();
         static const uint64_t kPiece = [] {  // SYDELTA_READ_PIECE: smallest piece (tests)
             const char* e = getenv("SYDELTA_READ_PIECE");
