@@ -487,7 +487,8 @@ static int index_create_impl(int device, const uint32_t* weak, const uint64_t* s
     const bool want_wide = nfiles == 1 && block_size > scan_max_window() && scan_wide_mode() != 0;
     const bool want_l1 = want_narrow || want_wide;
     const uint32_t l1_parts = want_narrow ? (scan_l1_mode() == 2 ? 2u : 1u) : want_wide ? 1u : 0u;
-    const uint32_t l1_words = want_narrow ? (scan_l1_mode() == 4 ? kL1WordsL2 : kL1Words) : kL1WordsWide;
+    const uint32_t l1_words = want_narrow ? (scan_l1_mode() == 5 ? kL1WordsR : scan_l1_mode() == 4 ? kL1WordsL2 : kL1Words)
+                                          : kL1WordsWide;
     const size_t sz_l1 = al(4 * (size_t)l1_parts * l1_words);
     const size_t sz_fat = want_l1 ? al(16 * (size_t)sl) : 0;
     const size_t total = sz_weak + sz_strong + sz_filt + sz_l1 + sz_fat + 4 * sz_t + sz_order + sz_slot + sz_files +
@@ -500,7 +501,7 @@ static int index_create_impl(int device, const uint32_t* weak, const uint64_t* s
     if (want_l1) {
         ix.l1 = (uint32_t*)p; p += sz_l1;
         ix.l1_parts = l1_parts;
-        ix.l1_wshift = want_narrow ? (scan_l1_mode() == 4 ? 0u : 17u) : 18u;
+        ix.l1_wshift = want_narrow ? (scan_l1_mode() == 5 ? 1u : scan_l1_mode() == 4 ? 0u : 17u) : 18u;
         ix.fat = (uint4*)p; p += sz_fat;
     }
     ix.keys = (uint32_t*)p; p += sz_t;

@@ -32,6 +32,15 @@ constexpr uint32_t kL1WordsWide = 16384;
 // k_scan_l2's level-1 filter (SYDELTA_SCAN_L1=4): 28672 words = 112 KiB beside its
 // 32 Ki-position tile, word = l1w2_word(q) (l1_wshift 0 marks it).
 constexpr uint32_t kL1WordsL2 = 28672;
+// k_scan_r's level-1 filter (SYDELTA_SCAN_L1=5): 38400 words = 150 KiB, the LDS left
+// when the tile's bytes stay in registers, word = l1r_word(q) (l1_wshift 1 marks it).
+constexpr uint32_t kL1WordsR = 38400;
+// words of a level-1 filter: l1_wshift 0 / 1 mark the scaled-word layouts of k_scan_l2 /
+// k_scan_r, any other value l1_parts power-of-two filters of 2^(32 - l1_wshift) words
+constexpr size_t l1_total_words(uint32_t l1_wshift, uint32_t l1_parts) {
+    return l1_wshift == 0 ? (size_t)kL1WordsL2 : l1_wshift == 1 ? (size_t)kL1WordsR
+                                                                : (size_t)l1_parts << (32 - l1_wshift);
+}
 
 // Verified hits are written as key/value pairs: key = (segment << 32) | position
 // relative to the segment's first position, value = global block index (into the

@@ -357,6 +357,11 @@ __device__ __forceinline__ uint32_t l1_test(uint32_t word, uint32_t q) { return 
 __host__ __device__ __forceinline__ uint32_t l1w2_word(uint32_t q) {
     return (uint32_t)(((uint64_t)(q >> 8) * (kL1WordsL2 << 8)) >> 32);
 }
+// k_scan_r's level-1 word (kL1WordsR words), the same scaling
+static_assert((kL1WordsR << 8) < (1u << 24), "l1r_word's constant is a 24-bit operand");
+__host__ __device__ __forceinline__ uint32_t l1r_word(uint32_t q) {
+    return (uint32_t)(((uint64_t)(q >> 8) * (kL1WordsR << 8)) >> 32);
+}
 // Key partitions (SYDELTA_SCAN_L1=2): key w belongs to partition r & 1 (r's low bits
 // take no part in the level-2 word, r >> fwshift, fwshift >= 4), and partition p's keys
 // alone set the bits of level-1 filter p, so each filter holds half the keys at two bits
@@ -392,8 +397,8 @@ __global__ void k_idx_insert(const uint32_t* __restrict__ weak, uint64_t n, cons
     const ProbeHash h = probe_hash(w);
     atomicOr(filt + F.filt_off + (h.r >> F.fwshift), filt_mask(h.q));
     if (l1)  // single-file index only (l1_test); l1_parts filters of 2^(32 - l1_wshift) words each
-        atomicOr(l1 + (l1_wshift ? ((size_t)l1_part(h.r, l1_parts - 1) << (32 - l1_wshift)) + (h.q >> l1_wshift)
-                                 : (size_t)l1w2_word(h.q)),
+        atomicOr(l1 + (l1_wshift > 1 ? ((size_t)l1_part(h.r, l1_parts - 1) << (32 - l1_wshift)) + (h.q >> l1_wshift)
+                       : l1_wshift == 1 ? (size_t)l1r_word(h.q) : (size_t)l1w2_word(h.q)),
                  1u << (h.q & 31));
     uint32_t b = bucket_hash(w) & F.bmask;
     for (;;) {
@@ -607,7 +612,8 @@ struct ScanArgs {
     uint32_t c0;         // 2M - 1 - (255*nm mod M)    (k_scan)
     uint32_t timing;     // accumulate per-phase s_memtime cycles of wave 0 into counters[4..8)
     uint32_t ablate;     // SYDELTA_ABLATE (measurement only, wrong results): k_scan_l1 bit 0 skips the
-                         // drains, bit 1 the level-2 loads, bit 2 the window phase
+                         // drains, bit 1 the level-2 loads, bit 2 the window phase; drain_l1 bit 3
+                         // skips the verification, bit 4 the fat-table lookups
     // k_scan_lds: segment table and per-file probe offsets
     const ScanSeg* segs;
     uint32_t nsegs;
@@ -638,6 +644,11 @@ struct ScanArgs {
     uint2* gfq;          // k_scan_lds: per-wave filter-pass queues in HBM/L2, kGFQ entries each
     struct WDef* wdef;   // k_scan_w: weak hits whose verification k_verify_w does (count: counters[10])
     uint64_t wdef_cap;
+    // k_scan_r: each wave's level-2 passes {position in run, weak} (rcap per wave) and,
+    // per pair of host tiles, {wave, first record, records of sub-run 0, of sub-run 1}
+    uint2* rrec;
+    uint32_t rcap;
+    uint4* rrun;
 };
 
 // A weak hit of k_scan_w, verified after the scan by k_verify_w.
@@ -1689,12 +1700,13 @@ __device__ __forceinline__ void drain_l1(const ScanArgs& a, const uint2* fq, uin
         if (i < nfq) {
             const uint2 e = fq[i];  // {position in tile, weak}
             tp = e.x;
-            if (tile_start + e.x < cur.pos_end) hit = fat_find(cur.fat, cur.bmask, e.y, rec);
+            if (tile_start + e.x < cur.pos_end && !(a.ablate & 16)) hit = fat_find(cur.fat, cur.bmask, e.y, rec);
         }
         const uint64_t m = __ballot(hit);
         if (!m) continue;
         const uint32_t cnt = __popcll(m);
         weak_hits += cnt;
+        if (a.ablate & 8) continue;
         if (nwq + cnt > (uint32_t)kWQ3) {
             verify_l1<kWinLds>(a, wq, nwq, rows, tile_start, cur);
             nwq = 0;
@@ -2306,7 +2318,8 @@ __global__ __launch_bounds__(kT3, 2) void k_scan_l2(ScanArgs a, uint32_t per) {
             }
 #pragma unroll
             for (int t = 0; t < kB3; ++t) {
-                const uint32_t p1 = l1_test(w1[t], Bt.hq[t]);
+                uint32_t p1 = l1_test(w1[t], Bt.hq[t]);
+                if (kTiming && (a.ablate & 2)) p1 = 0;
                 if (kTiming) l1pass += __popcll(__ballot(p1));
                 // a level-1 miss asks for an offset past the buffer: no request, reads 0
                 // (taking the lane out of the load with the exec mask instead measured the
@@ -2396,7 +2409,7 @@ __global__ __launch_bounds__(kT3, 2) void k_scan_l2(ScanArgs a, uint32_t per) {
         }
         while (stop < (uint32_t)kNB4) {
             passes += nfq;
-            drain_l1(a, fq, nfq, wq, weak_hits, rows, tile_start, sc);
+            if (!(kTiming && (a.ablate & 1))) drain_l1(a, fq, nfq, wq, weak_hits, rows, tile_start, sc);
             nfq = 0;
             uint32_t k = stop;
             stop = kNB4;
@@ -2414,7 +2427,7 @@ __global__ __launch_bounds__(kT3, 2) void k_scan_l2(ScanArgs a, uint32_t per) {
         PHASE_MARK4(3)
         if (nfq) {
             passes += nfq;
-            drain_l1(a, fq, nfq, wq, weak_hits, rows, tile_start, sc);
+            if (!(kTiming && (a.ablate & 1))) drain_l1(a, fq, nfq, wq, weak_hits, rows, tile_start, sc);
             nfq = 0;
         }
         PHASE_MARK4(4)
@@ -2428,6 +2441,493 @@ __global__ __launch_bounds__(kT3, 2) void k_scan_l2(ScanArgs a, uint32_t per) {
     if (kTiming && lane == 0) atomicAdd(&a.counters[3], l1pass);
     if (kTiming && tid == 0)
         for (int k = 0; k < 6; ++k) atomicAdd(&a.counters[4 + k], tm[k]);
+}
+
+// ===========================================================================
+// k_scan_r: the tile's bytes in registers, no workgroup barriers (SYDELTA_SCAN_L1=5)
+// ===========================================================================
+// Measured on k_scan_l2 (round 3, SYDELTA_ABLATE, C3, profiles/r03p_*): of its 14.8 ms,
+// 6.0 ms go away without the level-2 loads (2.9e9 L2 requests, 0.68 per position: the
+// chip's L2 request rate bounds the kernel), 1.6 ms without the verification and 0.85 ms
+// without the fat-table lookups; the roll alone runs in 6.5 ms.  Fewer L2 requests need
+// a larger level-1 filter, and k_scan_l2's LDS is full (36 KiB of staged rows beside the
+// 112 KiB filter).  Here no byte is staged in LDS.  Each wave owns wave tiles of 4096
+// positions: lane l rolls the 64 positions of row l, whose bytes leave the windows (out
+// row [P + 64l, +64)) and enter them (in row [P + n + 64l, +64), n = 4096) from
+// registers.  A wave walks a run of consecutive wave tiles, so tile k's in rows are tile
+// k+1's out rows and each row is loaded once; the next tile's in rows are loaded while
+// the current tile rolls.  First windows come from the two rows' sums by wave scans
+// (k_scan_l2's closed form).  Waves never wait for each other: runs of two host tiles
+// are handed out by an LDS counter.  The LDS holds the level-1 filter (150 KiB, passing
+// 1 - e^(-keys/1228800) of the positions: 0.57 at 1 Mi keys) and ntab.
+// The level-2 passes are not looked up here: each wave appends them to its own region
+// of HBM (no atomics) and records, per pair of host tiles, where they are; k_verify_r
+// then does the fat-table lookups and verifies the weak hits from the run's bytes staged
+// in its LDS.  Measured first with the drains inline (fat lookups and XXH3 of each weak
+// hit's window from global memory, four per wave): 14.43 ms at C3, of which 3.77 ms
+// verification and 0.93 ms lookups, 9.75 ms without both (r03r).  A wave whose region
+// cannot take another wave tile drains that tile inline instead (dense data).
+constexpr int kTR = 512;          // threads per workgroup (8 waves)
+constexpr int kWTR = 4096;        // positions per wave tile (64 per lane)
+constexpr int kNBR = 64 / kB3;    // batches per lane per wave tile
+constexpr uint32_t kRCapR = 24576;  // level-2 pass records per wave (>= 2 wave tiles)
+static_assert(kRCapR >= 2 * kWTR, "a wave's region holds the tile it may drain inline");
+static_assert(kMaxN3 == 4096 && kWTR % kMaxN3 == 0, "k_scan_r: a lane's in row is row l of the next wave tile");
+
+struct LdsR {
+    uint32_t l1, ntab, wq, ctr, total;  // byte offsets
+};
+__host__ __device__ constexpr LdsR ldsr_layout() {
+    LdsR L{};
+    uint32_t o = 0;
+    L.l1 = o; o += kL1WordsR * 4;
+    L.ntab = o; o += 256 * 4;
+    L.wq = o; o += (kTR / 64) * kWQ3 * 16;
+    L.ctr = o; o += 16;
+    L.total = o;
+    return L;
+}
+static_assert(ldsr_layout().total <= 160 * 1024 - 256, "k_scan_r's LDS");
+
+// Verify this wave's weak hits wq[0..nwq) = {position in run, first candidate |
+// kMulti+slot, strong lo, hi}: XXH3 of each window from global memory, four per wave (one
+// per 16-lane row, row_hash), then the first candidate in index order with equal strong
+// (generator.rs:127-133); verified hits to the output (as verify_l1).
+__device__ __forceinline__ void verify_r(const ScanArgs& a, uint4* wq, uint32_t nwq, uint64_t run_start,
+                                         const SegCtx& cur) {
+    if (!nwq) return;
+    lds_fence();
+    const uint32_t lane = threadIdx.x & 63, row = lane >> 4, rl = lane & 15;
+    for (uint32_t t = 0; t < nwq; t += 4) {
+        const uint32_t h = t + row;
+        const bool live = h < nwq;
+        const uint4 e = wq[live ? h : t];
+        uint32_t s0 = 0, cn = 0;
+        if (e.y & kMulti) { s0 = a.start[e.y & ~kMulti]; cn = a.cnt[e.y & ~kMulti]; }  // in flight while hashing
+        uint32_t wk;
+        uint64_t st;
+        row_hash<false>(cur.base + run_start + e.x, a.n, wk, st);  // valid in the row's first lane
+        st = ((uint64_t)(uint32_t)__shfl((int)(uint32_t)(st >> 32), (int)(lane & 48)) << 32) |
+             (uint32_t)__shfl((int)(uint32_t)st, (int)(lane & 48));
+        uint32_t best = kNoBlock;
+        if (!(e.y & kMulti)) {
+            if (st == (((uint64_t)e.w << 32) | e.z)) best = e.y;
+        } else {
+            for (uint32_t b = 0; b < cn; b += 16) {  // in index order, 16 candidates per step
+                const uint32_t j = b + rl;
+                const uint64_t m = (__ballot(j < cn && a.cstrong[s0 + j] == st) >> (row << 4)) & 0xFFFFull;
+                if (m) {
+                    best = a.order[s0 + b + (uint32_t)__builtin_ctzll(m)];
+                    break;
+                }
+            }
+        }
+        if (live && rl == 0) wq[h].y = best;
+    }
+    lds_fence();
+    uint32_t nver = 0;
+    for (uint32_t base = 0; base < nwq; base += 64) {
+        const bool v = base + lane < nwq && wq[base + lane].y != kNoBlock;
+        nver += __popcll(__ballot(v));
+    }
+    if (!nver) return;
+    unsigned long long k0 = 0;
+    if (lane == 0) k0 = atomicAdd(&a.counters[0], (unsigned long long)nver);
+    k0 = shfl64(k0, 0);
+    for (uint32_t base = 0; base < nwq; base += 64) {
+        const uint32_t i = base + lane;
+        const uint4 e = i < nwq ? wq[i] : make_uint4(0, kNoBlock, 0, 0);
+        const bool v = e.y != kNoBlock;
+        const uint64_t m = __ballot(v);
+        const unsigned long long k = k0 + __popcll(m & ((1ull << lane) - 1));
+        if (v && k < a.out_cap) {
+            a.hit_key[k] = ((uint64_t)cur.seg_id << kSegShift) | (uint64_t)(run_start + e.x - cur.pos_begin);
+            a.hit_val[k] = e.y;
+        }
+        k0 += __popcll(m);
+    }
+}
+
+// Inline drain of one wave tile's level-2 pass records (the wave's region is full):
+// fat-table lookups, 64 per round; positions at or past the run's end are dropped; weak
+// hits to wq, verified when wq cannot take another round and at the end (drain_l1's
+// logic), windows from global memory.
+__device__ __forceinline__ void drain_r(const ScanArgs& a, const uint2* recs, uint32_t nfq, uint4* wq,
+                                        unsigned long long& weak_hits, uint64_t run_start, const SegCtx& cur) {
+    const uint32_t lane = threadIdx.x & 63;
+    __threadfence_block();  // this wave's record stores before its loads
+    uint32_t nwq = 0;
+    for (uint32_t base = 0; base < nfq; base += 64) {
+        const uint32_t i = base + lane;
+        bool hit = false;
+        uint4 rec = make_uint4(0, 0, 0, 0);
+        uint32_t tp = 0;
+        if (i < nfq) {
+            const volatile uint2* g = recs + i;  // rewritten by later tiles: not from a stale L1 line
+            uint2 e;
+            e.x = g->x;
+            e.y = g->y;
+            tp = e.x;
+            if (run_start + e.x < cur.pos_end && !(a.ablate & 16)) hit = fat_find(cur.fat, cur.bmask, e.y, rec);
+        }
+        const uint64_t m = __ballot(hit);
+        if (!m) continue;
+        const uint32_t cnt = __popcll(m);
+        weak_hits += cnt;
+        if (a.ablate & 8) continue;
+        if (nwq + cnt > (uint32_t)kWQ3) {
+            verify_r(a, wq, nwq, run_start, cur);
+            nwq = 0;
+        }
+        const uint32_t rank = __popcll(m & ((1ull << lane) - 1));
+        const uint4 e = make_uint4(tp, rec.y, rec.z, rec.w);
+        if (cnt > (uint32_t)kWQ3) {  // a round of more hits than wq holds (dense data): two halves
+            if (hit && rank < (uint32_t)kWQ3) wq[rank] = e;
+            verify_r(a, wq, kWQ3, run_start, cur);
+            if (hit && rank >= (uint32_t)kWQ3) wq[rank - kWQ3] = e;
+            nwq = cnt - kWQ3;
+        } else {
+            if (hit) wq[nwq + rank] = e;
+            nwq += cnt;
+        }
+    }
+    verify_r(a, wq, nwq, run_start, cur);
+    lds_fence();
+}
+
+// kAblate: the SYDELTA_ABLATE instantiation (measurement only): bit 0 skips the drains,
+// bit 1 the level-2 loads; drain bits 3 (verification) and 4 (fat lookups) as drain_l1
+template <bool kAblate>
+__global__ __launch_bounds__(kTR, 2) void k_scan_r(ScanArgs a, uint32_t per) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    constexpr LdsR L = ldsr_layout();
+    const uint32_t n = a.n;  // kMaxN3 (launch_scan)
+    const uint32_t* l1 = (const uint32_t*)(smem + L.l1);
+    uint32_t* ntab = (uint32_t*)(smem + L.ntab);
+    const uint32_t tid = threadIdx.x;
+    const uint32_t lane = tid & 63, wid = tid >> 6;
+    uint4* wq = (uint4*)(smem + L.wq) + (size_t)wid * kWQ3;
+    uint32_t* ctr = (uint32_t*)(smem + L.ctr);
+    const uint32_t gwave = blockIdx.x * (kTR / 64) + wid;
+    uint2* rec = a.rrec + (size_t)gwave * a.rcap;  // this wave's pass records
+
+    const uint32_t t_begin = blockIdx.x * per;
+    const uint32_t t_end = min(a.ntiles, t_begin + per);
+    if (t_begin >= t_end) return;
+    {
+        const uint4* g = (const uint4*)a.l1;
+        uint4* d = (uint4*)(smem + L.l1);
+#pragma unroll 4
+        for (uint32_t i = tid; i < kL1WordsR / 4; i += kTR) d[i] = g[i];
+    }
+    for (uint32_t i = tid; i < 256; i += kTR) ntab[i] = kMod - 1 - (a.nm * i) % kMod;
+    if (tid == 0) *ctr = 0;
+    __syncthreads();  // the only barrier: the waves run independently from here
+
+    unsigned long long passes = 0, weak_hits = 0;
+    uint32_t nrec = 0, si_hint = 0;
+    const uint64_t below = (1ull << lane) - 1;
+#pragma unroll 1
+    for (;;) {
+        uint32_t c = 0;
+        if (lane == 0) c = atomicAdd(ctr, 1u);
+        c = __builtin_amdgcn_readfirstlane(c);
+        const uint32_t t0 = t_begin + 2 * c;
+        if (t0 >= t_end) break;
+        const uint32_t tz = min(t_end, t0 + 2);
+        const uint32_t rec0 = nrec;  // the pair's records start here
+        uint32_t cnt[2] = {0, 0}, nsr = 0;
+#pragma unroll 1
+        for (uint32_t t = t0; t < tz;) {
+            const uint32_t run_rec = nrec;
+            // the run: host tiles t (and t+1 when in the same segment)
+            uint32_t lo = si_hint, hi = a.nsegs;
+            while (hi - lo > 1) {
+                const uint32_t mid = (lo + hi) >> 1;
+                if (a.segs[mid].tile_base <= t) lo = mid; else hi = mid;
+            }
+            const uint32_t si = lo;
+            si_hint = si;
+            const ScanSeg S = a.segs[si];
+            const FileIx F = a.files[S.file];
+            SegCtx sc;
+            sc.base = a.src + S.src;
+            sc.pos_begin = S.pos_begin;
+            sc.keys = a.keys + F.slot_off;
+            sc.fat = a.fat + F.slot_off;
+            sc.slot_off = F.slot_off;
+            sc.bmask = F.bmask;
+            sc.seg_id = si;
+            sc.fwshift = F.fwshift;
+            sc.filt = a.filt + F.filt_off;
+            sc.fwords = 1u << (32 - F.fwshift);
+            const uint32_t span = (t + 1 < tz && !(si + 1 < a.nsegs && a.segs[si + 1].tile_base <= t + 1)) ? 2u : 1u;
+            const uint64_t run_start = S.pos_begin + (uint64_t)(t - S.tile_base) * kTile2;
+            sc.pos_end = min(S.pos_end, run_start + (uint64_t)span * kTile2);
+            const uint64_t seg_len = S.len;
+            const uint32_t nwt = span * (kTile2 / kWTR);  // wave tiles of the run
+            t += span;
+
+            const uint64_t fptr = (uint64_t)(uintptr_t)sc.filt;
+            const uint32_t fp_lo = __builtin_amdgcn_readfirstlane((uint32_t)fptr);
+            const uint32_t fp_hi = __builtin_amdgcn_readfirstlane((uint32_t)(fptr >> 32));
+            const __amdgpu_buffer_rsrc_t frsrc = __builtin_amdgcn_make_buffer_rsrc(
+                (void*)(uintptr_t)(((uint64_t)fp_hi << 32) | fp_lo), (short)0,
+                (int)__builtin_amdgcn_readfirstlane(sc.fwords * 4), 0x00020000);
+            const uint32_t fwshift = __builtin_amdgcn_readfirstlane(sc.fwshift);
+
+            uint32_t xo[16], xi[16], xn[16];
+            load_chunk(sc.base, seg_len, run_start + 64ull * lane, xo);
+            load_chunk(sc.base, seg_len, run_start + n + 64ull * lane, xi);
+#pragma unroll 1
+            for (uint32_t k = 0; k < nwt; ++k) {
+                const uint64_t P = run_start + (uint64_t)k * kWTR;
+                const uint32_t rel0 = k * kWTR + lane * 64;  // position in run of this lane's first window
+                // ---- window: lane l's window [P + 64l, +n) = out rows l..63 + in rows 0..l-1
+                uint32_t am, bm;
+                {
+                    uint32_t Sx[2], Vx[2], Jx[2], TS[2], TV[2], TJ[2];
+#pragma unroll
+                    for (int j = 0; j < 2; ++j) {
+                        uint32_t s = 0, v = 0;
+#pragma unroll
+                        for (int i = 0; i < 16; ++i) {
+                            const uint32_t d = j ? xi[i] : xo[i];
+                            s = udot4(d, 0x01010101u, s);
+                            v = udot4(d, offw(i), v);
+                        }
+                        Sx[j] = wave_scan_excl(s, TS[j]);
+                        Vx[j] = wave_scan_excl(v, TV[j]);
+                        Jx[j] = wave_scan_excl((uint32_t)(64 * j + lane) * s, TJ[j]);
+                    }
+                    const uint64_t dS = TS[0] + Sx[1] - Sx[0];
+                    const uint64_t dV = TV[0] + Vx[1] - Vx[0];
+                    const uint64_t dJ = TJ[0] + Jx[1] - Jx[0];
+                    const uint32_t A = (uint32_t)dS;
+                    const uint32_t B = (uint32_t)((uint64_t)n * dS - 64ull * (dJ - (uint64_t)lane * dS) - dV);
+                    am = (1 + A) % kMod;
+                    bm = (n + B) % kMod;
+                }
+                // ---- roll: k_scan_l2's trimmed roll, bytes from the registers
+                auto compute = [&](const int g, L1Batch& Bt) {
+                    const uint32_t xo0 = xo[g >> 2], xo1 = xo[(g >> 2) + 1];
+                    const uint32_t xi0 = xi[g >> 2], xi1 = xi[(g >> 2) + 1];
+                    uint32_t ct[kB3], off[kB3], w1[kB3];
+#pragma unroll
+                    for (int t2 = 0; t2 < kB3; ++t2) ct[t2] = ntab[((t2 < 4 ? xo0 : xo1) >> (8 * (t2 & 3))) & 0xFF];
+#pragma unroll
+                    for (int t2 = 0; t2 < kB3; ++t2) {
+                        const uint32_t out = ((t2 < 4 ? xo0 : xo1) >> (8 * (t2 & 3))) & 0xFF;
+                        const uint32_t in = ((t2 < 4 ? xi0 : xi1) >> (8 * (t2 & 3))) & 0xFF;
+                        __builtin_assume(am < kMod);
+                        __builtin_assume(bm < kMod);
+                        Bt.wv[t2] = (bm << 16) | am;
+                        const ProbeHash h = probe_hash(am, bm);
+                        Bt.hq[t2] = h.q;
+                        off[t2] = h.r >> fwshift;
+                        w1[t2] = l1[l1r_word(h.q)];
+                        const uint32_t u = am + in + (kMod - out);  // [M-255, 2M+255)
+                        am = min(u, min(u - kMod, u - 2 * kMod));
+                        const uint32_t v = bm + am + ct[t2];          // [0, 3M)
+                        bm = min(v, min(v - kMod, v - 2 * kMod));
+                    }
+#pragma unroll
+                    for (int t2 = 0; t2 < kB3; ++t2) {
+                        uint32_t p1 = l1_test(w1[t2], Bt.hq[t2]);
+                        if (kAblate && (a.ablate & 2)) p1 = 0;
+                        // a level-1 miss asks for an offset past the buffer: no request, reads 0
+                        Bt.w2[t2] = __builtin_amdgcn_raw_buffer_load_b32(frsrc, (int)((off[t2] << 2) | (p1 - 1u)), 0, 0);
+                    }
+                };
+                auto finish = [&](const int g, L1Batch& Bt) {
+                    uint32_t pbits = 0;
+#pragma unroll
+                    for (int t2 = 0; t2 < kB3; ++t2) pbits |= filt_bit(Bt.w2[t2], Bt.hq[t2]) << t2;
+                    asm volatile("" : "+v"(pbits));
+                    if (!__ballot(pbits != 0)) return;
+#pragma unroll
+                    for (int t2 = 0; t2 < kB3; ++t2) {  // appended in position order per batch
+                        const uint64_t mk = __ballot((pbits >> t2) & 1);
+                        if (!mk) continue;
+                        if ((pbits >> t2) & 1) rec[nrec + __popcll(mk & below)] = make_uint2(rel0 + g + t2, Bt.wv[t2]);
+                        nrec += __popcll(mk);
+                    }
+                };
+                // batch b+2's level-2 loads are issued before batch b is tested; the next
+                // wave tile's in rows after batch 4's (so that a wait on batches 0..4's
+                // loads never waits on them, and they land before the tile ends)
+                const uint32_t tile_rec = nrec;
+                L1Batch b0, b1;
+                compute(0, b0);
+                compute(8, b1);
+#pragma unroll
+                for (int bi = 0; bi < kNBR; ++bi) {
+                    L1Batch& Bt = (bi & 1) ? b1 : b0;
+                    finish(kB3 * bi, Bt);
+                    if (bi + 2 < kNBR) compute(kB3 * (bi + 2), Bt);
+                    if (bi == 2 && k + 1 < nwt)
+                        load_chunk(sc.base, seg_len, P + n + kWTR + 64ull * lane, xn);
+                }
+                passes += nrec - tile_rec;
+                // the region must hold the next tile's records (up to kWTR): when it might
+                // not, this tile's records are looked up and verified here instead
+                if (nrec > a.rcap - kWTR) {
+                    if (!(kAblate && (a.ablate & 1)))
+                        drain_r(a, rec + tile_rec, nrec - tile_rec, wq, weak_hits, run_start, sc);
+                    nrec = tile_rec;
+                }
+                if (kAblate && (a.ablate & 1)) nrec = tile_rec;
+#pragma unroll
+                for (int i = 0; i < 16; ++i) {
+                    xo[i] = xi[i];
+                    xi[i] = xn[i];
+                }
+            }
+            cnt[nsr++] = nrec - run_rec;  // the second run of a pair split by a segment end
+        }
+        if (lane == 0) a.rrun[t0 >> 1] = make_uint4(gwave, rec0, cnt[0], cnt[1]);
+    }
+    if (lane == 0 && passes) atomicAdd(&a.counters[2], passes);
+    if (lane == 0 && weak_hits) atomicAdd(&a.counters[1], weak_hits);
+}
+
+// k_verify_r: the level-2 passes k_scan_r recorded for one pair of host tiles (one
+// workgroup per pair): fat-table lookups, kTVR per round, then XXH3 of each weak hit's
+// window from the run's bytes staged in LDS (k_scan_l2's 17-dword rows, four windows per
+// wave, row_strong_lds), the first candidate in index order with equal strong
+// (generator.rs:127-133), verified hits to the output.  43 KiB of LDS: three workgroups
+// per CU, so one workgroup's lookups and staging overlap another's hashing.
+constexpr int kTVR = 256;
+struct LdsVR {
+    uint32_t nch, rows, hits, cnt, total;  // rows; byte offsets
+};
+__host__ __device__ constexpr LdsVR ldsvr_layout() {
+    LdsVR L{};
+    L.nch = (kTile4 + kMaxN3 + 63) / 64 + 1;
+    uint32_t o = 0;
+    L.rows = o; o += L.nch * kRowDw * 4;
+    o = (o + 15) & ~15u;
+    L.hits = o; o += kTVR * 16;
+    L.cnt = o; o += 16;
+    L.total = o;
+    return L;
+}
+
+__global__ __launch_bounds__(kTVR) void k_verify_r(ScanArgs a) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    constexpr LdsVR L = ldsvr_layout();
+    uint32_t* rows = (uint32_t*)(smem + L.rows);
+    uint4* hits = (uint4*)(smem + L.hits);
+    uint32_t* hcnt = (uint32_t*)(smem + L.cnt);
+    const uint32_t tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+    const uint32_t row = lane >> 4, rl = lane & 15;
+    const uint32_t g = blockIdx.x;
+    const uint4 R = a.rrun[g];
+    if (R.z + R.w == 0) return;
+    const uint2* recs = a.rrec + (size_t)R.x * a.rcap + R.y;
+    const uint32_t t0 = 2 * g, tz = min(a.ntiles, t0 + 2);
+    RowKeys K;
+    row_keys(K);
+    unsigned long long weak = 0;
+    uint32_t si = 0, roff = 0, sr = 0;
+#pragma unroll 1
+    for (uint32_t t = t0; t < tz; ++sr) {
+        uint32_t lo = si, hi = a.nsegs;
+        while (hi - lo > 1) {
+            const uint32_t mid = (lo + hi) >> 1;
+            if (a.segs[mid].tile_base <= t) lo = mid; else hi = mid;
+        }
+        si = lo;
+        const ScanSeg S = a.segs[si];
+        const FileIx F = a.files[S.file];
+        const uint8_t* base = a.src + S.src;
+        const uint4* fat = a.fat + F.slot_off;
+        const uint32_t span = (t + 1 < tz && !(si + 1 < a.nsegs && a.segs[si + 1].tile_base <= t + 1)) ? 2u : 1u;
+        const uint64_t run_start = S.pos_begin + (uint64_t)(t - S.tile_base) * kTile2;
+        const uint64_t pos_end = min(S.pos_end, run_start + (uint64_t)span * kTile2);
+        t += span;
+        const uint32_t cnt = sr == 0 ? R.z : R.w;
+        const uint2* rr = recs + roff;
+        roff += cnt;
+        if (!cnt) continue;
+        // the run's bytes [run_start, + span * kTile2 + n) into the rows (past the
+        // segment's end: zeros)
+        const uint32_t nch = (span * kTile2 + a.n + 63) / 64 + 1;
+#pragma unroll 1
+        for (uint32_t r = tid; r < nch; r += kTVR) {
+            uint32_t x[16];
+            load_chunk(base, S.len, run_start + 64ull * r, x);
+#pragma unroll
+            for (int i = 0; i < 16; ++i) rows[r * kRowDw + i] = x[i];
+        }
+#pragma unroll 1
+        for (uint32_t b0 = 0; b0 < cnt; b0 += kTVR) {
+            if (tid == 0) *hcnt = 0;
+            __syncthreads();  // rows staged; the previous round's hits consumed
+            const uint32_t i = b0 + tid;
+            if (i < cnt) {
+                const uint2 e = rr[i];
+                uint4 rec;
+                if (run_start + e.x < pos_end && fat_find(fat, F.bmask, e.y, rec)) {
+                    const uint32_t k = atomicAdd(hcnt, 1u);
+                    hits[k] = make_uint4(e.x, rec.y, rec.z, rec.w);
+                }
+            }
+            __syncthreads();
+            const uint32_t nh = *hcnt;
+            if (tid == 0) weak += nh;
+#pragma unroll 1
+            for (uint32_t h0 = 4 * wid; h0 < nh; h0 += 4 * (kTVR / 64)) {  // wave-uniform
+                const uint32_t h = h0 + row;
+                const bool live = h < nh;
+                const uint4 e = hits[live ? h : h0];
+                uint32_t s0 = 0, cn = 0;
+                if (e.y & kMulti) { s0 = a.start[e.y & ~kMulti]; cn = a.cnt[e.y & ~kMulti]; }
+                const uint64_t st = row_strong_lds(rows, e.x, a.n, K);
+                uint32_t best = kNoBlock;
+                if (!(e.y & kMulti)) {
+                    if (st == (((uint64_t)e.w << 32) | e.z)) best = e.y;
+                } else {
+                    for (uint32_t b = 0; b < cn; b += 16) {  // in index order, 16 candidates per step
+                        const uint32_t j = b + rl;
+                        const uint64_t m = (__ballot(j < cn && a.cstrong[s0 + j] == st) >> (row << 4)) & 0xFFFFull;
+                        if (m) {
+                            best = a.order[s0 + b + (uint32_t)__builtin_ctzll(m)];
+                            break;
+                        }
+                    }
+                }
+                if (live && rl == 0) hits[h].y = best;
+            }
+            __syncthreads();
+            if (wid == 0) {
+                uint32_t nver = 0;
+                for (uint32_t hb = 0; hb < nh; hb += 64) {
+                    const bool v = hb + lane < nh && hits[hb + lane].y != kNoBlock;
+                    nver += __popcll(__ballot(v));
+                }
+                if (nver) {
+                    unsigned long long k0 = 0;
+                    if (lane == 0) k0 = atomicAdd(&a.counters[0], (unsigned long long)nver);
+                    k0 = shfl64(k0, 0);
+                    for (uint32_t hb = 0; hb < nh; hb += 64) {
+                        const uint32_t j = hb + lane;
+                        const uint4 e = j < nh ? hits[j] : make_uint4(0, kNoBlock, 0, 0);
+                        const bool v = e.y != kNoBlock;
+                        const uint64_t m = __ballot(v);
+                        const unsigned long long k = k0 + __popcll(m & ((1ull << lane) - 1));
+                        if (v && k < a.out_cap) {
+                            a.hit_key[k] = ((uint64_t)si << kSegShift) | (uint64_t)(run_start + e.x - S.pos_begin);
+                            a.hit_val[k] = e.y;
+                        }
+                        k0 += __popcll(m);
+                    }
+                }
+            }
+        }
+        __syncthreads();  // the rows are rewritten by the next run
+    }
+    if (tid == 0 && weak) atomicAdd(&a.counters[1], weak);
 }
 
 // ===========================================================================
@@ -2875,7 +3375,8 @@ __global__ __launch_bounds__(kTW, 2) void k_scan_w(ScanArgs a, uint32_t per) {
             }
 #pragma unroll
             for (int t = 0; t < kB3; ++t) {
-                const uint32_t p1 = l1_test(w1[t], Bt.hq[t]);
+                uint32_t p1 = l1_test(w1[t], Bt.hq[t]);
+                if (kTiming && (a.ablate & 2)) p1 = 0;
                 if (kTiming) l1pass += __popcll(__ballot(p1));
                 // a level-1 miss asks for an offset past the buffer: no request, reads 0
                 Bt.w2[t] = __builtin_amdgcn_raw_buffer_load_b32(frsrc, (int)((off[t] << 2) | (p1 - 1u)), 0, 0);
@@ -4227,7 +4728,7 @@ static inline unsigned grid_for(uint64_t threads, unsigned block) { return (unsi
 // partitions (l1_part), 3 k_scan_s, 4 k_scan_l2.
 int scan_l1_mode() {
     const char* e = getenv("SYDELTA_SCAN_L1");
-    return (e && e[0] >= '0' && e[0] <= '4' && e[1] == 0) ? e[0] - '0' : 4;
+    return (e && e[0] >= '0' && e[0] <= '5' && e[1] == 0) ? e[0] - '0' : 4;
 }
 int scan_wide_mode() {
     const char* e = getenv("SYDELTA_SCAN_WIDE");
@@ -4300,9 +4801,7 @@ hipError_t launch_index_build(const uint32_t* d_weak, const uint64_t* d_strong, 
                               Profiler* prof) {
     hipError_t e;
     if ((e = hipMemsetAsync(ix.filt, 0, ix.fwords * 4, s))) return e;
-    if (ix.l1 && (e = hipMemsetAsync(ix.l1, 0, (ix.l1_wshift ? ((size_t)ix.l1_parts << (32 - ix.l1_wshift))
-                                                              : (size_t)kL1WordsL2) * 4, s)))
-        return e;
+    if (ix.l1 && (e = hipMemsetAsync(ix.l1, 0, l1_total_words(ix.l1_wshift, ix.l1_parts) * 4, s))) return e;
     if ((e = hipMemsetAsync(ix.keys, 0xFF, ix.nslots * 4, s))) return e;
     if ((e = hipMemsetAsync(ix.cnt, 0, ix.nslots * 4, s))) return e;
     const uint64_t n = ix.nblocks;
@@ -4492,6 +4991,50 @@ hipError_t launch_scan(const uint8_t* d_buf, const ScanSeg* d_segs, uint32_t nse
     // covers, n = 4096 (the C3 shape; tests/test_gpu_scan_large.py).  Other sizes with a
     // large index go to k_scan_lds (production block sizes for files with more than
     // 16 Ki blocks are >= 8 KiB anyway: bs = sqrt(file size)).
+    if (ix.l1 && ix.l1_wshift == 1 && n == kMaxN3) {  // k_scan_r (an index built with SYDELTA_SCAN_L1=5)
+        static std::once_flag r_once;
+        static hipError_t r_err = hipSuccess;
+        static int r_cus = 256;
+        std::call_once(r_once, [] {
+            for (const void* f : {(const void*)k_scan_r<false>, (const void*)k_scan_r<true>})
+                if (r_err == hipSuccess)
+                    r_err = hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024 - 256);
+            int dev = 0, cus = 0;
+            if (hipGetDevice(&dev) == hipSuccess &&
+                hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess && cus > 0)
+                r_cus = cus;
+        });
+        if (r_err != hipSuccess) return r_err;
+        if (!ix.fat) return hipErrorInvalidValue;
+        constexpr LdsR LR = ldsr_layout();
+        constexpr LdsVR LV = ldsvr_layout();
+        // one workgroup per CU over contiguous host tiles, an even number each (runs are pairs)
+        uint32_t per = (uint32_t)((ntiles + (uint64_t)r_cus - 1) / (uint64_t)r_cus);
+        per += per & 1;
+        const uint32_t grid = (uint32_t)((ntiles + (uint64_t)per - 1) / per);
+        const uint32_t npairs = (uint32_t)((ntiles + 1ull) / 2);
+        // pass records (kRCapR per wave) and the pair table
+        a.rcap = kRCapR;
+        const size_t rec_bytes = ((size_t)grid * (kTR / 64) * kRCapR * sizeof(uint2) + 255) & ~(size_t)255;
+        void* rbuf = nullptr;
+        hipError_t e = dev_malloc_async(&rbuf, rec_bytes + (size_t)npairs * sizeof(uint4), s);
+        if (e != hipSuccess) return e;
+        a.rrec = (uint2*)rbuf;
+        a.rrun = (uint4*)((uint8_t*)rbuf + rec_bytes);
+        {
+            ProfScope ps(prof, s, "k_scan_r");
+            if (a.ablate) hipLaunchKernelGGL(k_scan_r<true>, dim3(grid), dim3(kTR), LR.total, s, a, per);
+            else hipLaunchKernelGGL(k_scan_r<false>, dim3(grid), dim3(kTR), LR.total, s, a, per);
+        }
+        e = hipGetLastError();
+        if (e == hipSuccess && !(a.ablate & 1)) {
+            ProfScope ps(prof, s, "k_verify_r");
+            hipLaunchKernelGGL(k_verify_r, dim3(npairs), dim3(kTVR), LV.total, s, a);
+            e = hipGetLastError();
+        }
+        const hipError_t fe = hipFreeAsync(rbuf, s);
+        return e != hipSuccess ? e : fe;
+    }
     if (ix.l1 && ix.l1_wshift == 0 && n == kMaxN3 && scan_l1_mode() == 4) {  // k_scan_l2
         static std::once_flag l2_once;
         static hipError_t l2_err = hipSuccess;

@@ -1,8 +1,9 @@
 """GPU parity for large single-file indexes (> 16 Ki basis blocks): every scan of a
 large index -- the level-1-filter scan k_scan_l1 (the default at n = 4096,
 SYDELTA_SCAN_L1=1), the same kernel over two key partitions (SYDELTA_SCAN_L1=2), the
-stripe-per-thread k_scan_s (SYDELTA_SCAN_L1=3) and k_scan_lds in global-filter mode
-(SYDELTA_SCAN_L1=0) -- against the oracle.
+stripe-per-thread k_scan_s (SYDELTA_SCAN_L1=3), k_scan_l2 (=4), the register-fed
+k_scan_r (=5) and k_scan_lds in global-filter mode (SYDELTA_SCAN_L1=0) -- against the
+oracle.
 
 * 96 MiB basis, mixed edits (an all-literal stretch, sparse substitutions, a shift,
   planted unaligned copies, duplicated blocks): bit-exact op list against the C
@@ -26,15 +27,15 @@ pytestmark = pytest.mark.gpu
 
 
 # SYDELTA_TEST_SCANNERS=a,b restricts the parametrization (a first hardware run of one kernel)
-_SCANNERS = [k for k in ["lds", "l1", "l1p2", "s", "l2"]
-             if k in os.environ.get("SYDELTA_TEST_SCANNERS", "lds,l1,l1p2,s,l2").split(",")]
+_SCANNERS = [k for k in ["lds", "l1", "l1p2", "s", "l2", "r"]
+             if k in os.environ.get("SYDELTA_TEST_SCANNERS", "lds,l1,l1p2,s,l2,r").split(",")]
 
 
 @pytest.fixture(params=_SCANNERS)
 def scanner(request, monkeypatch):
     """The large-index scan kernel (SYDELTA_SCAN_L1 is read when the index is built and
     by launch_scan on every call)."""
-    monkeypatch.setenv("SYDELTA_SCAN_L1", {"lds": "0", "l1": "1", "l1p2": "2", "s": "3", "l2": "4"}[request.param])
+    monkeypatch.setenv("SYDELTA_SCAN_L1", {"lds": "0", "l1": "1", "l1p2": "2", "s": "3", "l2": "4", "r": "5"}[request.param])
     return request.param
 
 
