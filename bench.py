@@ -513,7 +513,7 @@ def algo_bytes_per_step(workload: str, n: int, nb_bytes: int, src_bytes: int) ->
     step the signature kernels read the basis once and the scan reads the source once
     (SURVEY.md section 8(d))."""
     return {"k_scan": src_bytes, "k_scan_lds": src_bytes, "k_scan_l1": src_bytes, "k_scan_l2": src_bytes,
-            "k_scan_w": src_bytes, "k_scan_s": src_bytes,
+            "k_scan_w": src_bytes, "k_scan_s": src_bytes, "k_scan_r": src_bytes,
             "k_sig_fast": nb_bytes if workload in ("c3", "c3b") else n,
             "k_sig_batch": n, "k_sig_wave": n, "k_probe": src_bytes,
             "k_apply": 2 * n,  # apply: every output byte read once and written once
@@ -538,9 +538,12 @@ def roofline(prof: dict, steps: int, algo_step: dict, positions=None, keys=None)
     L2_GATHER_PEAK (the measured chip-wide ceiling of random L2 gathers,
     profiles/r02_micro_gather2.txt) when the step's scanned positions are known.  For
     the level-1 scans (k_scan_l1 / k_scan_s: 2^20 bits, k_scan_l2: 28672 words = 917504
-    bits, k_scan_w: 2^19 bits) only the positions that pass the level-1 filter in LDS send
-    a request; that fraction is modelled as 1 - exp(-keys / bits) (one bit per key) and
-    the entry says so."""
+    bits, k_scan_r: 38400 words = 1228800 bits, k_scan_w: 2^19 bits) only the positions
+    that pass the level-1 filter in LDS send a request; that fraction is modelled as
+    1 - exp(-keys / bits) (one bit per key) and the entry says so.
+
+    k_scan_r hands its level-2 passes to k_lookup_r and k_verify_r, so `match` adds the
+    three kernels' time: the source bytes per step over the whole match."""
     import math
 
     dom = max(prof, key=lambda k: prof[k]["ms"]) if prof else None
@@ -556,7 +559,7 @@ def roofline(prof: dict, steps: int, algo_step: dict, positions=None, keys=None)
     # level-1 filter bits (one hash) per key: with P key partitions (SYDELTA_SCAN_L1=2) the
     # scan is launched once per partition and each launch's filter holds 1/P of the keys
     l1_bits = {"k_scan_l1": (1 << 20) * max(1, round(launches_per_step)), "k_scan_s": 1 << 20,
-               "k_scan_l2": 28672 * 32, "k_scan_w": 1 << 19}
+               "k_scan_l2": 28672 * 32, "k_scan_w": 1 << 19, "k_scan_r": 38400 * 32}
     if positions and (dom in ("k_scan_lds", "k_scan") or (dom in l1_bits and keys)):
         per_pos = 1.0 if dom not in l1_bits else 1.0 - math.exp(-keys / float(l1_bits[dom]))
         req = positions * per_pos / launches_per_step  # filter-word requests per launch
@@ -578,6 +581,12 @@ def roofline(prof: dict, steps: int, algo_step: dict, positions=None, keys=None)
                 "tcc_requests_per_s_G": round(rq * per_launch / (avg_ms * 1e-3) / 1e9, 2),
                 "frac": round(rq * per_launch / (avg_ms * 1e-3) / L2_GATHER_PEAK, 4),
                 "source": "profiles/" + pc["source"]}
+    parts = [k for k in ("k_scan_r", "k_lookup_r", "k_verify_r") if k in prof]
+    if dom == "k_scan_r" and len(parts) == 3:
+        ms = sum(prof[k]["ms"] for k in parts) / steps  # per step
+        mb = algo_step[dom] / (ms * 1e-3) / 1e9
+        roof["match"] = {"kernels": parts, "ms_per_step": round(ms, 4), "achieved": round(mb, 2),
+                         "unit": "GB/s", "frac": round(mb / HBM_PEAK_GBS, 4)}
     return roof
 
 

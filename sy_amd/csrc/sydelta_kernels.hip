@@ -1596,6 +1596,24 @@ __device__ __forceinline__ bool fat_find(const uint4* __restrict__ fat, uint32_t
     }
 }
 
+// fat_find through the keys-only table: one 16-byte request for the bucket's four keys
+// (ScanArgs::keys, 4 B per slot) and the 16-byte record only on a hit, where
+// fat_find reads the bucket's 64-byte line of records for every lookup.
+__device__ __forceinline__ bool fat_find_k(const uint32_t* __restrict__ keys, const uint4* __restrict__ fat,
+                                           uint32_t bmask, uint32_t w, uint4& rec) {
+    uint32_t b = bucket_hash(w) & bmask;
+    for (;;) {
+        const uint4 k = *(const uint4*)(keys + 4 * (size_t)b);
+        const int j = k.x == w ? 0 : k.y == w ? 1 : k.z == w ? 2 : k.w == w ? 3 : -1;
+        if (j >= 0) {
+            rec = fat[4 * (size_t)b + j];
+            return true;
+        }
+        if (k.w == kEmptyKey) return false;  // buckets fill in order
+        b = (b + 1) & bmask;
+    }
+}
+
 // Verify this wave's weak hits wq[0..nwq) = {position in tile, first candidate |
 // kMulti+slot, strong lo, hi}: XXH3 of the window from the LDS rows (four windows per
 // wave, one per 16-lane row, when n % 64 == 0 and n >= 256), then the first candidate
@@ -2842,6 +2860,7 @@ __global__ __launch_bounds__(kTVR) void k_verify_r(ScanArgs a) {
         const FileIx F = a.files[S.file];
         const uint8_t* base = a.src + S.src;
         const uint4* fat = a.fat + F.slot_off;
+        const uint32_t* fkeys = a.keys + F.slot_off;
         const uint32_t span = (t + 1 < tz && !(si + 1 < a.nsegs && a.segs[si + 1].tile_base <= t + 1)) ? 2u : 1u;
         const uint64_t run_start = S.pos_begin + (uint64_t)(t - S.tile_base) * kTile2;
         const uint64_t pos_end = min(S.pos_end, run_start + (uint64_t)span * kTile2);
@@ -2856,7 +2875,7 @@ __global__ __launch_bounds__(kTVR) void k_verify_r(ScanArgs a) {
 #pragma unroll 1
         for (uint32_t r = tid; r < nch; r += kTVR) {
             uint32_t x[16];
-            load_chunk(base, S.len, run_start + 64ull * r, x);
+            if (!(a.ablate & 32)) load_chunk(base, S.len, run_start + 64ull * r, x);
 #pragma unroll
             for (int i = 0; i < 16; ++i) rows[r * kRowDw + i] = x[i];
         }
@@ -2868,7 +2887,7 @@ __global__ __launch_bounds__(kTVR) void k_verify_r(ScanArgs a) {
             if (i < cnt) {
                 const uint2 e = rr[i];
                 uint4 rec;
-                if (run_start + e.x < pos_end && fat_find(fat, F.bmask, e.y, rec)) {
+                if (run_start + e.x < pos_end && !(a.ablate & 16) && fat_find_k(fkeys, fat, F.bmask, e.y, rec)) {
                     const uint32_t k = atomicAdd(hcnt, 1u);
                     hits[k] = make_uint4(e.x, rec.y, rec.z, rec.w);
                 }
@@ -2877,7 +2896,7 @@ __global__ __launch_bounds__(kTVR) void k_verify_r(ScanArgs a) {
             const uint32_t nh = *hcnt;
             if (tid == 0) weak += nh;
 #pragma unroll 1
-            for (uint32_t h0 = 4 * wid; h0 < nh; h0 += 4 * (kTVR / 64)) {  // wave-uniform
+            for (uint32_t h0 = 4 * wid; h0 < (a.ablate & 8 ? 0u : nh); h0 += 4 * (kTVR / 64)) {  // wave-uniform
                 const uint32_t h = h0 + row;
                 const bool live = h < nh;
                 const uint4 e = hits[live ? h : h0];
@@ -2900,7 +2919,7 @@ __global__ __launch_bounds__(kTVR) void k_verify_r(ScanArgs a) {
                 if (live && rl == 0) hits[h].y = best;
             }
             __syncthreads();
-            if (wid == 0) {
+            if (wid == 0 && !(a.ablate & 8)) {
                 uint32_t nver = 0;
                 for (uint32_t hb = 0; hb < nh; hb += 64) {
                     const bool v = hb + lane < nh && hits[hb + lane].y != kNoBlock;
