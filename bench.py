@@ -542,8 +542,8 @@ def roofline(prof: dict, steps: int, algo_step: dict, positions=None, keys=None)
     that pass the level-1 filter in LDS send a request; that fraction is modelled as
     1 - exp(-keys / bits) (one bit per key) and the entry says so.
 
-    k_scan_r hands its level-2 passes to k_lookup_r and k_verify_r, so `match` adds the
-    three kernels' time: the source bytes per step over the whole match."""
+    k_scan_r hands its level-2 passes to k_verify_r, so `match` adds the two kernels'
+    time: the source bytes per step over the whole match."""
     import math
 
     dom = max(prof, key=lambda k: prof[k]["ms"]) if prof else None
@@ -582,7 +582,7 @@ def roofline(prof: dict, steps: int, algo_step: dict, positions=None, keys=None)
                 "frac": round(rq * per_launch / (avg_ms * 1e-3) / L2_GATHER_PEAK, 4),
                 "source": "profiles/" + pc["source"]}
     parts = [k for k in ("k_scan_r", "k_lookup_r", "k_verify_r") if k in prof]
-    if dom == "k_scan_r" and len(parts) == 3:
+    if dom == "k_scan_r" and "k_verify_r" in parts:
         ms = sum(prof[k]["ms"] for k in parts) / steps  # per step
         mb = algo_step[dom] / (ms * 1e-3) / 1e9
         roof["match"] = {"kernels": parts, "ms_per_step": round(ms, 4), "achieved": round(mb, 2),

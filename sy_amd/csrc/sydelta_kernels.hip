@@ -2815,6 +2815,8 @@ __global__ __launch_bounds__(kTR, 2) void k_scan_r(ScanArgs a, uint32_t per) {
 // wave, row_strong_lds), the first candidate in index order with equal strong
 // (generator.rs:127-133), verified hits to the output.  43 KiB of LDS: three workgroups
 // per CU, so one workgroup's lookups and staging overlap another's hashing.
+// (Measured and rejected: one workgroup per host tile with half the rows, six per CU:
+// 3.48 ms against 2.81 at C3, the pair's records read twice.)
 constexpr int kTVR = 256;
 struct LdsVR {
     uint32_t nch, rows, hits, cnt, total;  // rows; byte offsets
@@ -4740,14 +4742,14 @@ __global__ void k_synth_mutate(uint8_t* __restrict__ dst, const uint8_t* __restr
 // ===========================================================================
 static inline unsigned grid_for(uint64_t threads, unsigned block) { return (unsigned)((threads + block - 1) / block); }
 
-// Large single-file indexes (block size 4096) scan with k_scan_l2 by default: 14.85-14.91
-// ms per 4 GiB against k_scan_l1's 16.78 ms and k_scan_lds's 19.2 ms in global-filter mode
-// (DESIGN.md section 6).  SYDELTA_SCAN_L1 (read when the index is built and per call: the
+// Large single-file indexes (block size 4096) scan with k_scan_r + k_verify_r by default:
+// 9.88 + 2.81 ms per 4 GiB against k_scan_l2's 14.82, k_scan_l1's 16.78 and k_scan_lds's
+// 19.2 ms in global-filter mode.  SYDELTA_SCAN_L1 (read when the index is built and per call: the
 // parity tests run every scanner): 0 k_scan_lds, 1 k_scan_l1, 2 k_scan_l1 over two key
-// partitions (l1_part), 3 k_scan_s, 4 k_scan_l2.
+// partitions (l1_part), 3 k_scan_s, 4 k_scan_l2, 5 k_scan_r + k_verify_r (the default).
 int scan_l1_mode() {
     const char* e = getenv("SYDELTA_SCAN_L1");
-    return (e && e[0] >= '0' && e[0] <= '5' && e[1] == 0) ? e[0] - '0' : 4;
+    return (e && e[0] >= '0' && e[0] <= '5' && e[1] == 0) ? e[0] - '0' : 5;
 }
 int scan_wide_mode() {
     const char* e = getenv("SYDELTA_SCAN_WIDE");

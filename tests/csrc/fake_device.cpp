@@ -319,7 +319,7 @@ hipError_t launch_index_build(const uint32_t* d_weak, const uint64_t* d_strong, 
 uint64_t scan_tile_positions() { return 16384; }
 int scan_l1_mode() {
     const char* e = getenv("SYDELTA_SCAN_L1");
-    return (e && e[0] >= '0' && e[0] <= '5' && e[1] == 0) ? e[0] - '0' : 4;
+    return (e && e[0] >= '0' && e[0] <= '5' && e[1] == 0) ? e[0] - '0' : 5;
 }
 int scan_wide_mode() {
     const char* e = getenv("SYDELTA_SCAN_WIDE");
