@@ -114,6 +114,9 @@ int sydelta_signature_device(int device, const uint8_t *d_buf, uint64_t len, uin
 int sydelta_index_create(int device, const uint32_t *weak, const uint64_t *strong, uint64_t nblocks,
                          uint64_t block_size, uint64_t last_size, int arrays_on_device, void *stream,
                          sydelta_index **out);
+/* The index's device memory is released in the order of the stream it was created on
+ * (a caller stream must outlive the index; NULL: the creating thread's library stream,
+ * which lives as long as the process). */
 void sydelta_index_free(sydelta_index *idx);
 
 /* Rolling match of a device-resident source against the index: the greedy

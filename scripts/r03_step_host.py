@@ -29,9 +29,12 @@ for rep in range(4):
     d = dev.match(idx, new, stream=stream)
     torch.cuda.synchronize()
     t3 = time.perf_counter()
-    idx.close()
     del d
+    t3a = time.perf_counter()
+    idx.close()
+    t3b = time.perf_counter()
     torch.cuda.synchronize()
     t4 = time.perf_counter()
     print(f"rep {rep}: signature {1e3*(t1-t0):.3f} ms, index {1e3*(t2-t1):.3f} ms, match {1e3*(t3-t2):.3f} ms, "
-          f"close {1e3*(t4-t3):.3f} ms, total {1e3*(t4-t0):.3f} ms", flush=True)
+          f"del delta {1e3*(t3a-t3):.3f} ms, index free {1e3*(t3b-t3a):.3f} ms, sync {1e3*(t4-t3b):.3f} ms, "
+          f"total {1e3*(t4-t0):.3f} ms", flush=True)

@@ -23,6 +23,7 @@
 #include <hipcub/hipcub.hpp>
 
 #include <algorithm>
+#include <chrono>
 #include <mutex>
 
 namespace sydelta {
@@ -5037,9 +5038,12 @@ hipError_t launch_scan(const uint8_t* d_buf, const ScanSeg* d_segs, uint32_t nse
         // pass records (kRCapR per wave) and the pair table
         a.rcap = kRCapR;
         const size_t rec_bytes = ((size_t)grid * (kTR / 64) * kRCapR * sizeof(uint2) + 255) & ~(size_t)255;
+        static const bool host_timing = getenv("SYDELTA_HOST_TIMING") != nullptr;
+        const auto th0 = std::chrono::steady_clock::now();
         void* rbuf = nullptr;
         hipError_t e = dev_malloc_async(&rbuf, rec_bytes + (size_t)npairs * sizeof(uint4), s);
         if (e != hipSuccess) return e;
+        const auto th1 = std::chrono::steady_clock::now();
         a.rrec = (uint2*)rbuf;
         a.rrun = (uint4*)((uint8_t*)rbuf + rec_bytes);
         {
@@ -5053,7 +5057,13 @@ hipError_t launch_scan(const uint8_t* d_buf, const ScanSeg* d_segs, uint32_t nse
             hipLaunchKernelGGL(k_verify_r, dim3(npairs), dim3(kTVR), LV.total, s, a);
             e = hipGetLastError();
         }
+        const auto th2 = std::chrono::steady_clock::now();
         const hipError_t fe = hipFreeAsync(rbuf, s);
+        if (host_timing)
+            fprintf(stderr, "sydelta k_scan_r launch: malloc %.3f ms, launches %.3f ms, free %.3f ms\n",
+                    std::chrono::duration<double, std::milli>(th1 - th0).count(),
+                    std::chrono::duration<double, std::milli>(th2 - th1).count(),
+                    std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - th2).count());
         return e != hipSuccess ? e : fe;
     }
     if (ix.l1 && ix.l1_wshift == 0 && n == kMaxN3 && scan_l1_mode() == 4) {  // k_scan_l2
