@@ -2494,7 +2494,7 @@ static_assert(kRCapR >= 2 * kWTR, "a wave's region holds the tile it may drain i
 static_assert(kMaxN3 == 4096 && kWTR % kMaxN3 == 0, "k_scan_r: a lane's in row is row l of the next wave tile");
 
 struct LdsR {
-    uint32_t l1, ntab, wq, ctr, total;  // byte offsets
+    uint32_t l1, ntab, wq, kt, ctr, total;  // byte offsets
 };
 __host__ __device__ constexpr LdsR ldsr_layout() {
     LdsR L{};
@@ -2502,6 +2502,7 @@ __host__ __device__ constexpr LdsR ldsr_layout() {
     L.l1 = o; o += kL1WordsR * 4;
     L.ntab = o; o += 256 * 4;
     L.wq = o; o += (kTR / 64) * kWQ3 * 16;
+    L.kt = o; o += 48 * 8;  // wave_strong_regs' key table (kKtWords)
     L.ctr = o; o += 16;
     L.total = o;
     return L;
@@ -2614,9 +2615,169 @@ __device__ __forceinline__ void drain_r(const ScanArgs& a, const uint2* recs, ui
     lds_fence();
 }
 
+// ---------------------------------------------------------------------------
+// XXH3-64 of a 4096-byte window held in a wave's registers (k_scan_r, inline verification)
+// ---------------------------------------------------------------------------
+// The window starts at wave-tile offset o = 64 lp + c of the rows xo (rows 0..63: lane L
+// holds row L) and xi (rows 64..127: lane L holds row 64 + L).  Lane s takes stripe s:
+// bytes [64 s + c, +64) of rows lp + s and lp + s + 1, gathered with ds_bpermute from the
+// owning lanes (the source register index q + j is uniform: v_movrels), aligned by c & 3.
+// Stripes 0..62 use keys w[(s & 15) + i], stripe 63 -- the last stripe of a 4096-byte
+// input -- the last-stripe keys; the four 16-lane rows are the four 1 KiB blocks, each
+// reduced in its row (reduce-scatter: accumulator (L >> 1) & 7 ends in lane L), blocks
+// 0..2 followed by a scramble, block 3 (stripes 48..62 and the last stripe) not.  Keys,
+// initial accumulators and merge keys come from an LDS table (kt: w[0..23], last[0..7],
+// init[0..7], merge[0..7]).  Every lane returns the hash.
+constexpr int kKtW = 0, kKtLast = 24, kKtInit = 32, kKtMerge = 40, kKtWords = 48;
+typedef uint32_t v16u32 __attribute__((ext_vector_type(16)));
+
+__device__ __forceinline__ uint64_t dpp64_ctrl_shr4(uint64_t v) {
+    return ((uint64_t)dpp32<0x114>((uint32_t)(v >> 32)) << 32) | dpp32<0x114>((uint32_t)v);
+}
+__device__ __forceinline__ uint64_t dpp64_ctrl_shl4(uint64_t v) {
+    return ((uint64_t)dpp32<0x104>((uint32_t)(v >> 32)) << 32) | dpp32<0x104>((uint32_t)v);
+}
+template <int kCtrl>
+__device__ __forceinline__ uint64_t dpp64(uint64_t v) {
+    return ((uint64_t)dpp32<kCtrl>((uint32_t)(v >> 32)) << 32) | dpp32<kCtrl>((uint32_t)v);
+}
+
+__device__ __forceinline__ uint64_t wave_strong_regs(const uint32_t (&xo)[16], const uint32_t (&xi)[16], uint32_t o,
+                                                  const uint64_t* kt) {
+    const uint32_t lane = threadIdx.x & 63;
+    o = __builtin_amdgcn_readfirstlane(o);
+    const uint32_t lp = o >> 6, c = o & 63, q = c >> 2, sh = c & 3;
+    v16u32 S0, S1;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+        S0[r] = lane >= lp ? xo[r] : xi[r];  // global row lp + s for the lane that owns it
+        S1[r] = lane > lp ? xo[r] : xi[r];   // global row lp + s + 1 (row lp + 64: xi of lane lp)
+    }
+    const int addrA = (int)(((lp + lane) & 63) << 2), addrB = (int)(((lp + lane + 1) & 63) << 2);
+    uint32_t raw[17];
+#pragma unroll
+    for (int j = 0; j < 17; ++j) {
+        const uint32_t r = q + j;  // uniform
+        const uint32_t v = r < 16 ? S0[r & 15] : S1[r & 15];
+        raw[j] = (uint32_t)__builtin_amdgcn_ds_bpermute(r < 16 ? addrA : addrB, (int)v);
+    }
+    const uint32_t kb = lane == 63 ? (uint32_t)kKtLast : (lane & 15);
+    uint64_t cc[8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) cc[i] = 0;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+        const uint32_t w0 = __builtin_amdgcn_alignbyte(raw[2 * i + 1], raw[2 * i], sh);
+        const uint32_t w1 = __builtin_amdgcn_alignbyte(raw[2 * i + 2], raw[2 * i + 1], sh);
+        const uint64_t v = (uint64_t)w0 | ((uint64_t)w1 << 32);
+        const uint64_t dk = v ^ kt[kb + i];
+        cc[i ^ 1] += v;
+        cc[i] += mul32x32(dk);
+    }
+    // reduce-scatter inside each 16-lane row: lane L ends with accumulator (L >> 1) & 7
+    uint64_t f;
+    const bool b3 = lane & 8, b2 = lane & 4, b1 = lane & 2;
+    uint64_t d[4], e[2];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        const uint64_t send = b3 ? cc[k] : cc[4 + k], keep = b3 ? cc[4 + k] : cc[k];
+        d[k] = keep + dpp64<kDppRowRor8>(send);  // row_ror:8 = xor 8
+    }
+#pragma unroll
+    for (int k = 0; k < 2; ++k) {
+        const uint64_t send = b2 ? d[k] : d[2 + k], keep = b2 ? d[2 + k] : d[k];
+        // both shifts in every lane, then the select: a DPP inside the conditional would run
+        // with the partner lanes masked off and read 0 from them
+        const uint64_t from_lo = dpp64_ctrl_shr4(send), from_hi = dpp64_ctrl_shl4(send);
+        e[k] = keep + (b2 ? from_lo : from_hi);  // lane L ^ 4
+    }
+    {
+        const uint64_t send = b1 ? e[0] : e[1], keep = b1 ? e[1] : e[0];
+        f = keep + dpp64<kDppQuadXor2>(send);
+    }
+    f += dpp64<kDppQuadXor1>(f);
+    // blocks 1..3 from the rows below; lanes 0..15 carry the chain
+    const uint64_t p1 = shfl64(f, (int)((lane + 16) & 63));
+    const uint64_t p2 = shfl64(f, (int)((lane + 32) & 63));
+    const uint64_t p3 = shfl64(f, (int)((lane + 48) & 63));
+    const uint32_t ai = (lane >> 1) & 7;
+    const uint64_t skey = kt[kKtW + 16 + ai];
+    uint64_t acc = kt[kKtInit + ai] + f;
+    acc = scramble1(acc, skey) + p1;
+    acc = scramble1(acc, skey) + p2;
+    acc = scramble1(acc, skey) + p3;
+    // merge: accumulators 2k, 2k+1 sit in lanes L, L ^ 2 (L % 4 == 0 holds 2k)
+    const uint64_t z = acc ^ kt[kKtMerge + ai];
+    const uint64_t zp = dpp64<kDppQuadXor2>(z);
+    uint64_t m = (lane & 3) == 0 ? fold64(z, zp) : 0ull;
+    m += dpp64<kDppRowRor4>(m);
+    m += dpp64<kDppRowRor8>(m);
+    const uint64_t h = xxh3_aval((uint64_t)4096 * P64_1 + m);
+    return ((uint64_t)__builtin_amdgcn_readlane((int)(uint32_t)(h >> 32), 0) << 32) |
+           (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)h, 0);
+}
+
+// Inline drain of one wave tile's level-2 pass records [0, nr) (just written by this wave
+// to its region): keys-only lookups, 64 per round; each weak hit's window is hashed from
+// the registers (wave_strong_regs, one window at a time for the whole wave), the first
+// candidate in index order with equal strong taken (generator.rs:127-133); verified hits
+// to the output.  tile_rel: the run position of the tile's first window.
+__device__ __forceinline__ void drain_regs(const ScanArgs& a, const uint2* recs, uint32_t nr, uint32_t tile_rel,
+                                           const uint32_t (&xo)[16], const uint32_t (&xi)[16], const uint64_t* kt,
+                                           unsigned long long& weak_hits, uint64_t run_start, const SegCtx& cur) {
+    const uint32_t lane = threadIdx.x & 63;
+    const uint64_t below = (1ull << lane) - 1;
+    __threadfence_block();  // this wave's record stores before its loads
+    for (uint32_t base = 0; base < nr; base += 64) {
+        const uint32_t i = base + lane;
+        bool hit = false;
+        uint4 rec = make_uint4(0, 0, 0, 0);
+        uint32_t pos = 0;
+        if (i < nr) {
+            const volatile uint2* g = recs + i;  // rewritten by later tiles: not from a stale L1 line
+            pos = g->x;
+            const uint32_t w = g->y;
+            if (run_start + pos < cur.pos_end && !(a.ablate & 16)) hit = fat_find_k(cur.keys, cur.fat, cur.bmask, w, rec);
+        }
+        uint64_t m = __ballot(hit);
+        weak_hits += __popcll(m);
+        if (a.ablate & 8) continue;
+        uint32_t best_mine = kNoBlock;
+        while (m) {  // wave-uniform
+            const int h = __builtin_ctzll(m);
+            m &= m - 1;
+            const uint32_t hp = __builtin_amdgcn_readlane((int)pos, h);
+            const uint32_t hy = __builtin_amdgcn_readlane((int)rec.y, h);
+            const uint64_t hs = ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)rec.w, h) << 32) |
+                                (uint32_t)__builtin_amdgcn_readlane((int)rec.z, h);
+            const uint64_t st = wave_strong_regs(xo, xi, hp - tile_rel, kt);
+            uint32_t best = kNoBlock;
+            if (!(hy & kMulti)) {
+                if (st == hs) best = hy;
+            } else {
+                best = first_strong_match(a.order, a.cstrong, a.start[hy & ~kMulti], a.cnt[hy & ~kMulti], st);
+            }
+            if ((int)lane == h) best_mine = best;
+        }
+        const bool v = best_mine != kNoBlock;
+        const uint64_t mv = __ballot(v);
+        if (!mv) continue;
+        unsigned long long k0 = 0;
+        if (lane == 0) k0 = atomicAdd(&a.counters[0], (unsigned long long)__popcll(mv));
+        k0 = shfl64(k0, 0);
+        const unsigned long long k = k0 + __popcll(mv & below);
+        if (v && k < a.out_cap) {
+            a.hit_key[k] = ((uint64_t)cur.seg_id << kSegShift) | (uint64_t)(run_start + pos - cur.pos_begin);
+            a.hit_val[k] = best_mine;
+        }
+    }
+}
+
 // kAblate: the SYDELTA_ABLATE instantiation (measurement only): bit 0 skips the drains,
 // bit 1 the level-2 loads; drain bits 3 (verification) and 4 (fat lookups) as drain_l1
-template <bool kAblate>
+// kInline (SYDELTA_SCAN_R_INLINE=1): each wave tile's passes are looked up and verified at
+// the tile's end (drain_regs: the windows hashed from the registers), no k_verify_r.
+template <bool kAblate, bool kInline>
 __global__ __launch_bounds__(kTR, 2) void k_scan_r(ScanArgs a, uint32_t per) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     constexpr LdsR L = ldsr_layout();
@@ -2640,6 +2801,10 @@ __global__ __launch_bounds__(kTR, 2) void k_scan_r(ScanArgs a, uint32_t per) {
         for (uint32_t i = tid; i < kL1WordsR / 4; i += kTR) d[i] = g[i];
     }
     for (uint32_t i = tid; i < 256; i += kTR) ntab[i] = kMod - 1 - (a.nm * i) % kMod;
+    uint64_t* kt = (uint64_t*)(smem + L.kt);
+    if (kInline && tid < 48)
+        kt[tid] = tid < 24 ? c_tab.w[tid] : tid < 32 ? c_tab.last[tid - 24] : tid < 40 ? c_tab.init[tid - 32]
+                                                                                       : c_tab.merge[tid - 40];
     if (tid == 0) *ctr = 0;
     __syncthreads();  // the only barrier: the waves run independently from here
 
@@ -2788,9 +2953,14 @@ __global__ __launch_bounds__(kTR, 2) void k_scan_r(ScanArgs a, uint32_t per) {
                         load_chunk(sc.base, seg_len, P + n + kWTR + 64ull * lane, xn);
                 }
                 passes += nrec - tile_rec;
+                if (kInline) {
+                    if (nrec > tile_rec && !(kAblate && (a.ablate & 1)))
+                        drain_regs(a, rec + tile_rec, nrec - tile_rec, k * kWTR, xo, xi, kt, weak_hits, run_start, sc);
+                    nrec = tile_rec;
+                }
                 // the region must hold the next tile's records (up to kWTR): when it might
                 // not, this tile's records are looked up and verified here instead
-                if (nrec > a.rcap - kWTR) {
+                if (!kInline && nrec > a.rcap - kWTR) {
                     if (!(kAblate && (a.ablate & 1)))
                         drain_r(a, rec + tile_rec, nrec - tile_rec, wq, weak_hits, run_start, sc);
                     nrec = tile_rec;
@@ -2804,7 +2974,7 @@ __global__ __launch_bounds__(kTR, 2) void k_scan_r(ScanArgs a, uint32_t per) {
             }
             cnt[nsr++] = nrec - run_rec;  // the second run of a pair split by a segment end
         }
-        if (lane == 0) a.rrun[t0 >> 1] = make_uint4(gwave, rec0, cnt[0], cnt[1]);
+        if (!kInline && lane == 0) a.rrun[t0 >> 1] = make_uint4(gwave, rec0, cnt[0], cnt[1]);
     }
     if (lane == 0 && passes) atomicAdd(&a.counters[2], passes);
     if (lane == 0 && weak_hits) atomicAdd(&a.counters[1], weak_hits);
@@ -5018,7 +5188,8 @@ hipError_t launch_scan(const uint8_t* d_buf, const ScanSeg* d_segs, uint32_t nse
         static hipError_t r_err = hipSuccess;
         static int r_cus = 256;
         std::call_once(r_once, [] {
-            for (const void* f : {(const void*)k_scan_r<false>, (const void*)k_scan_r<true>})
+            for (const void* f : {(const void*)k_scan_r<false, false>, (const void*)k_scan_r<true, false>,
+                                  (const void*)k_scan_r<false, true>, (const void*)k_scan_r<true, true>})
                 if (r_err == hipSuccess)
                     r_err = hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024 - 256);
             int dev = 0, cus = 0;
@@ -5030,29 +5201,37 @@ hipError_t launch_scan(const uint8_t* d_buf, const ScanSeg* d_segs, uint32_t nse
         if (!ix.fat) return hipErrorInvalidValue;
         constexpr LdsR LR = ldsr_layout();
         constexpr LdsVR LV = ldsvr_layout();
+        // SYDELTA_SCAN_R_INLINE=0: the passes recorded for k_verify_r (round 3's first form,
+        // 9.91 + 2.81 ms at C3) instead of verified at each wave tile's end (11.18 ms)
+        static const bool inl = !(getenv("SYDELTA_SCAN_R_INLINE") && getenv("SYDELTA_SCAN_R_INLINE")[0] == '0');
         // one workgroup per CU over contiguous host tiles, an even number each (runs are pairs)
         uint32_t per = (uint32_t)((ntiles + (uint64_t)r_cus - 1) / (uint64_t)r_cus);
         per += per & 1;
         const uint32_t grid = (uint32_t)((ntiles + (uint64_t)per - 1) / per);
         const uint32_t npairs = (uint32_t)((ntiles + 1ull) / 2);
-        // pass records (kRCapR per wave) and the pair table
-        a.rcap = kRCapR;
-        const size_t rec_bytes = ((size_t)grid * (kTR / 64) * kRCapR * sizeof(uint2) + 255) & ~(size_t)255;
+        // pass records (kRCapR per wave, and the pair table; inline: one wave tile's)
+        a.rcap = inl ? (uint32_t)kWTR : kRCapR;
+        const size_t rec_bytes = ((size_t)grid * (kTR / 64) * a.rcap * sizeof(uint2) + 255) & ~(size_t)255;
         static const bool host_timing = getenv("SYDELTA_HOST_TIMING") != nullptr;
         const auto th0 = std::chrono::steady_clock::now();
         void* rbuf = nullptr;
-        hipError_t e = dev_malloc_async(&rbuf, rec_bytes + (size_t)npairs * sizeof(uint4), s);
+        hipError_t e = dev_malloc_async(&rbuf, rec_bytes + (inl ? 0 : (size_t)npairs * sizeof(uint4)), s);
         if (e != hipSuccess) return e;
         const auto th1 = std::chrono::steady_clock::now();
         a.rrec = (uint2*)rbuf;
-        a.rrun = (uint4*)((uint8_t*)rbuf + rec_bytes);
+        a.rrun = inl ? nullptr : (uint4*)((uint8_t*)rbuf + rec_bytes);
         {
             ProfScope ps(prof, s, "k_scan_r");
-            if (a.ablate) hipLaunchKernelGGL(k_scan_r<true>, dim3(grid), dim3(kTR), LR.total, s, a, per);
-            else hipLaunchKernelGGL(k_scan_r<false>, dim3(grid), dim3(kTR), LR.total, s, a, per);
+            if (inl) {
+                if (a.ablate) hipLaunchKernelGGL((k_scan_r<true, true>), dim3(grid), dim3(kTR), LR.total, s, a, per);
+                else hipLaunchKernelGGL((k_scan_r<false, true>), dim3(grid), dim3(kTR), LR.total, s, a, per);
+            } else {
+                if (a.ablate) hipLaunchKernelGGL((k_scan_r<true, false>), dim3(grid), dim3(kTR), LR.total, s, a, per);
+                else hipLaunchKernelGGL((k_scan_r<false, false>), dim3(grid), dim3(kTR), LR.total, s, a, per);
+            }
         }
         e = hipGetLastError();
-        if (e == hipSuccess && !(a.ablate & 1)) {
+        if (e == hipSuccess && !(a.ablate & 1) && !inl) {
             ProfScope ps(prof, s, "k_verify_r");
             hipLaunchKernelGGL(k_verify_r, dim3(npairs), dim3(kTVR), LV.total, s, a);
             e = hipGetLastError();
