@@ -420,8 +420,15 @@ static void index_release(sydelta_index* x) {
 
 extern "C" void sydelta_index_free(sydelta_index* idx) {
     if (!idx) return;
+    static const bool host_timing = getenv("SYDELTA_HOST_TIMING") != nullptr;
+    const auto t0 = std::chrono::steady_clock::now();
     (void)hipSetDevice(idx->device);
+    const auto t1 = std::chrono::steady_clock::now();
     index_release(idx);
+    if (host_timing)
+        fprintf(stderr, "sydelta index free: set device %.3f ms, release %.3f ms\n",
+                std::chrono::duration<double, std::milli>(t1 - t0).count(),
+                std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t1).count());
 }
 
 static int index_create_impl(int device, const uint32_t* weak, const uint64_t* strong, const uint64_t* nblk,
@@ -985,18 +992,42 @@ int Classifier::scan(const std::vector<std::array<uint64_t, 3>>& ranges) {
     uint64_t want = std::min<uint64_t>(tot_pos, tot_pos / n * 4 + (1 << 16));
     uint64_t cap = 0;
     unsigned long long counts[16] = {0};
-    DevBuf hit_buf;
+    // The verified-hit buffers (keys [cap] + key scratch [cap] + values [cap] + value
+    // scratch [cap]) stay with the calling thread between calls, grown as needed: freeing
+    // them after the synchronize below -- ~100 MB at C3 -- blocked the host ~0.6 ms per
+    // call (measured, round 3), reusing them costs nothing.  The previous call on this
+    // thread synchronized its stream, so a buffer made on another stream is free to
+    // take over (or to release in this stream's order).  Never freed at thread exit (the
+    // HIP runtime may be gone), like the per-thread streams.
+    struct HitScratch {
+        void* p = nullptr;
+        size_t bytes = 0;
+        int dev = -1;
+    };
+    static thread_local HitScratch hits_tl;
+    int cur_dev = 0;
+    HIP_TRY(hipGetDevice(&cur_dev));
+    if (hits_tl.p && hits_tl.dev != cur_dev) hits_tl = HitScratch();  // another device's: left to that pool
+    struct {
+        void* p = nullptr;
+    } hit_buf;
     for (int attempt = 0; attempt < 2; ++attempt) {
         if (want > cap) {
-            if (hit_buf.p) { (void)hipFreeAsync(hit_buf.p, s); hit_buf.p = nullptr; }
             cap = want;
-            // keys [cap] + key scratch [cap] + values [cap] + value scratch [cap]
-            HIP_TRY(dev_malloc_async(&hit_buf.p, cap * 24, s));
-            hit_buf.s = s;
+            if (hits_tl.bytes < cap * 24) {
+                if (hits_tl.p) (void)hipFreeAsync(hits_tl.p, s);
+                hits_tl = HitScratch();
+                const size_t bytes = cap * 24 + (cap * 24) / 4;  // room to grow by a quarter
+                HIP_TRY(dev_malloc_async(&hits_tl.p, bytes, s));
+                hits_tl.bytes = bytes;
+                hits_tl.dev = cur_dev;
+            }
+            hit_buf.p = hits_tl.p;
         }
         uint64_t* d_key = (uint64_t*)hit_buf.p;
         uint32_t* d_val = (uint32_t*)(d_key + 2 * cap);
         HIP_TRY(hipMemsetAsync(d_counts, 0, 128, s));
+        if (host_timing) fprintf(stderr, "sydelta scan setup: %.3f ms\n", ms_since(t0));
         if (!wide) {
             HIP_TRY(launch_scan(base, (const ScanSeg*)seg_buf.p, (uint32_t)segs.size(), (uint32_t)ntiles,
                                 (uint32_t)n, ix->ix, ix->d_strong, d_key, d_val, cap, d_counts, (uint2*)q_buf.p, qcap,
@@ -1007,8 +1038,10 @@ int Classifier::scan(const std::vector<std::array<uint64_t, 3>>& ranges) {
                                          (uint32_t)g, (uint32_t)n, ix->ix, ix->d_strong, d_key, d_val, cap, d_counts,
                                          s, prof));
         }
+        if (host_timing) fprintf(stderr, "sydelta scan launched: %.3f ms\n", ms_since(t0));
         HIP_TRY(hipMemcpyAsync(counts, d_counts, 128, hipMemcpyDeviceToHost, s));
         HIP_TRY(hipStreamSynchronize(s));
+        if (host_timing) fprintf(stderr, "sydelta scan synchronized: %.3f ms\n", ms_since(t0));
         if (getenv("SYDELTA_PHASE_TIMING"))
             fprintf(stderr, "sydelta phase cycles (wave 0, summed over workgroups): [k_scan_lds: stage prefix roll flush"
                             " lookup verify; k_scan_l1: stage window roll prefetch drain barrier] %llu %llu %llu %llu"
@@ -1598,6 +1631,7 @@ static int match_impl(sydelta_index* ix, const uint8_t* d_buf, const uint64_t* s
     }
     b->total.weak_hits = C.weak_hits;
     if (nf == 1) b->d[0].stats.weak_hits = C.weak_hits;
+    if (host_timing && nf == 1) fprintf(stderr, "sydelta match: %.3f ms before the classifier's release\n", ms_since(t_begin));
     if (host_timing && nf > 1)
         fprintf(stderr,
                 "sydelta match batch: %llu files, setup %.3f ms, classify %.3f ms, tail %.3f ms, threaded walks %.3f "
@@ -1618,8 +1652,11 @@ extern "C" int sydelta_match_device(sydelta_index* idx, const uint8_t* d_src, ui
     hipStream_t s = stream ? (hipStream_t)stream : thread_stream(idx->device);
     sydelta_delta_batch b;
     const uint64_t off = 0;
+    static const bool host_timing = getenv("SYDELTA_HOST_TIMING") != nullptr;
+    const auto t0 = std::chrono::steady_clock::now();
     if (int r = match_impl(idx, d_src, &off, &len, s, &b)) return r;
     *out = new sydelta_delta(std::move(b.d[0]));
+    if (host_timing) fprintf(stderr, "sydelta match_device: %.3f ms (with the classifier's release)\n", ms_since(t0));
     return SYDELTA_OK;
 } catch (...) {
     return sydelta::host_exception();
