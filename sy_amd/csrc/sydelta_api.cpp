@@ -402,20 +402,63 @@ struct sydelta_index {
     uint64_t* d_strong = nullptr;
     DeviceIndex ix;
     void* d_pool = nullptr;           // one allocation for all index arrays
+    size_t pool_bytes = 0;
     hipStream_t stream = nullptr;     // the stream the pool was allocated on
 };
 
-// Stream-ordered release on the stream the index was built on (a hipFree would wait for
-// the whole device, i.e. for every other caller's work; a hipFreeAsync on another stream
-// than the allocation's blocked the host ~0.5 ms per call on the C3 index, on the same
-// stream ~0.3 ms).  Every entry point that reads an index synchronizes its stream before
-// returning, so no queued work still reads the pool; the memory pool reuses it only in
-// stream order after this point.  (Recycling the allocation for the next index instead
-// was measured too: the free's 0.3 ms moved into the next build, no step got faster.)
+// Index memory is kept for the next index: a released index's allocation is held (one
+// per device) and the next index built on the same stream with no more bytes (and no
+// less than half) takes it over, so the usual sequence -- build, match, free, build
+// again (a file after another, bench steps) -- allocates once.  A hipFreeAsync on a stream
+// with no work queued blocked the host 0.3-0.6 ms for these allocations (measured, round
+// 3: C3's 50 MB index, C5's 130 MB one), as for the scan's hit buffers.  Every entry point
+// that reads an index synchronizes its stream before returning, so no queued work still
+// reads a released pool, and a new owner on the same stream uses it in stream order.  A
+// held allocation that does not fit is released in its stream's order (a caller stream
+// must outlive the index, include/sydelta.h).
+namespace {
+struct KeptPool {
+    void* p = nullptr;
+    size_t bytes = 0;
+    hipStream_t s = nullptr;
+};
+std::mutex g_kept_mu;
+KeptPool g_kept[64];
+}  // namespace
+
 static void index_release(sydelta_index* x) {
     if (!x) return;
-    if (x->d_pool) (void)hipFreeAsync(x->d_pool, x->stream ? x->stream : thread_stream(x->device));
+    if (x->d_pool) {
+        KeptPool old;
+        if (x->device >= 0 && x->device < 64) {
+            std::lock_guard<std::mutex> lk(g_kept_mu);
+            old = g_kept[x->device];
+            g_kept[x->device] = {x->d_pool, x->pool_bytes, x->stream};
+        } else {
+            old = {x->d_pool, 0, x->stream};
+        }
+        if (old.p) (void)hipFreeAsync(old.p, old.s ? old.s : thread_stream(x->device));
+    }
     delete x;
+}
+
+// The held allocation of `device` if it was made on stream s and fits `bytes` (else
+// released in its own stream's order).
+static void* take_kept_pool(int device, size_t bytes, hipStream_t s, size_t* got) {
+    if (device < 0 || device >= 64) return nullptr;
+    KeptPool k;
+    {
+        std::lock_guard<std::mutex> lk(g_kept_mu);
+        k = g_kept[device];
+        g_kept[device] = KeptPool();
+    }
+    if (!k.p) return nullptr;
+    if (k.s == s && k.bytes >= bytes && k.bytes <= 2 * bytes + (64u << 20)) {
+        *got = k.bytes;
+        return k.p;
+    }
+    (void)hipFreeAsync(k.p, k.s ? k.s : thread_stream(device));
+    return nullptr;
 }
 
 extern "C" void sydelta_index_free(sydelta_index* idx) {
@@ -504,7 +547,11 @@ static int index_create_impl(int device, const uint32_t* weak, const uint64_t* s
     const size_t sz_fat = want_l1 ? al(16 * (size_t)sl) : 0;
     const size_t total = sz_weak + sz_strong + sz_filt + sz_l1 + sz_fat + 4 * sz_t + sz_order + sz_slot + sz_files +
                          sz_fblk + sz_cstrong;
-    HIP_TRY(dev_malloc_async(&x->d_pool, total, s));  // stream-ordered: no device-wide synchronization
+    x->d_pool = take_kept_pool(device, total, s, &x->pool_bytes);
+    if (!x->d_pool) {
+        HIP_TRY(dev_malloc_async(&x->d_pool, total, s));  // stream-ordered: no device-wide synchronization
+        x->pool_bytes = total;
+    }
     x->stream = s;
     uint8_t* p = (uint8_t*)x->d_pool;
     x->d_weak = (uint32_t*)p; p += sz_weak;
