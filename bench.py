@@ -51,6 +51,7 @@ from __future__ import annotations
 import argparse
 import json
 import os
+import re
 import sys
 import time
 
@@ -473,6 +474,13 @@ def host_inclusive(dev, bs: int, size: int, stream_dev: int):
             "h2d_GBps": round(h2d, 2), "ops": len(d.kind)}
 
 
+def _pmc_order(path: str):
+    """Chronological order of profiles/r<round><tag>_*_pmc.json: round, then the tag as
+    the scripts name them (r03, r03b .. r03z, r03aa ..: shorter tags first)."""
+    m = re.match(r"r(\d+)([a-z]*)_", os.path.basename(path))
+    return (int(m.group(1)), len(m.group(2)), m.group(2)) if m else (0, 0, "")
+
+
 def pmc_traffic(kernel: str, per_launch: int):
     """HBM bytes per launch of `kernel` from the committed rocprofv3 PMC summary of this
     round (profiles/*_pmc.json, written by scripts/pmc_summary.py from FETCH_SIZE and
@@ -480,7 +488,7 @@ def pmc_traffic(kernel: str, per_launch: int):
     import glob
 
     best = None
-    for f in sorted(glob.glob(os.path.join(ROOT, "profiles", "r*_pmc.json"))):
+    for f in sorted(glob.glob(os.path.join(ROOT, "profiles", "r*_pmc.json")), key=_pmc_order):
         try:
             d = json.load(open(f))
         except Exception:
@@ -497,7 +505,7 @@ def pmc_counters(kernel: str):
     import glob
 
     best = None
-    for f in sorted(glob.glob(os.path.join(ROOT, "profiles", "r*_pmc.json"))):
+    for f in sorted(glob.glob(os.path.join(ROOT, "profiles", "r*_pmc.json")), key=_pmc_order):
         try:
             d = json.load(open(f))
         except Exception:
