@@ -839,6 +839,61 @@ struct Classifier {
     // position: walk on the host, which scans on demand), 2 (not applicable) or an error.
     int walk_device(size_t i, uint64_t entry, const BasisInfo& bi, bool final_src, int tail_match,
                     sydelta_delta* d, uint64_t* exit);
+
+    // The first sources' per-block and hit lists are handed to the next classifier on
+    // the same thread (emptied, capacity kept): at C3b's 1 Mi blocks and hits, fresh
+    // lists cost their first-touch page faults and their release ~3 ms (measured, round
+    // 3).  Bounded: kSpareSrcs sources, kSpareBytes in all.
+    static constexpr size_t kSpareSrcs = 2, kSpareBytes = 512ull << 20;
+    static std::vector<Src>& spare() {
+        static thread_local std::vector<Src> v;
+        return v;
+    }
+    template <class V>
+    static size_t cap_bytes(const V& v) {
+        return v.capacity() * sizeof(typename V::value_type);
+    }
+    static size_t src_bytes(const Src& c) {
+        return cap_bytes(c.ahit) + cap_bytes(c.scanned) + cap_bytes(c.hpos) + cap_bytes(c.hblk) +
+               cap_bytes(c.ppos) + cap_bytes(c.phit);
+    }
+    // after src.resize(): take the spare lists
+    void adopt_spare() {
+        auto& sp = spare();
+        for (size_t i = 0; i < src.size() && i < sp.size(); ++i) {
+            src[i].ahit.swap(sp[i].ahit);
+            src[i].scanned.swap(sp[i].scanned);
+            src[i].hpos.swap(sp[i].hpos);
+            src[i].hblk.swap(sp[i].hblk);
+            src[i].ppos.swap(sp[i].ppos);
+            src[i].phit.swap(sp[i].phit);
+        }
+        sp.clear();
+    }
+    ~Classifier() {
+        auto& sp = spare();
+        size_t total = 0;
+        sp.clear();
+        for (size_t i = 0; i < src.size() && sp.size() < kSpareSrcs; ++i) {
+            const size_t b = src_bytes(src[i]);
+            if (total + b > kSpareBytes) break;
+            total += b;
+            sp.emplace_back();
+            Src& k = sp.back();
+            k.ahit.swap(src[i].ahit);
+            k.scanned.swap(src[i].scanned);
+            k.hpos.swap(src[i].hpos);
+            k.hblk.swap(src[i].hblk);
+            k.ppos.swap(src[i].ppos);
+            k.phit.swap(src[i].phit);
+            k.ahit.clear();
+            k.scanned.clear();
+            k.hpos.clear();
+            k.hblk.clear();
+            k.ppos.clear();
+            k.phit.clear();
+        }
+    }
 };
 
 int Classifier::probe(int mode) {
@@ -1111,10 +1166,25 @@ int Classifier::scan(const std::vector<std::array<uint64_t, 3>>& ranges) {
         ProfScope ps(prof, s, "sort_hits");
         HIP_TRY(launch_sort_hits(d_key, d_val, d_key + cap, d_val + cap, nver, end_bit, s, &k_out, &v_out));
     }
-    std::vector<uint64_t> hkey(nver);
-    std::vector<uint32_t> hval(nver);
-    HIP_TRY(hipMemcpyAsync(hkey.data(), k_out, nver * 8, hipMemcpyDeviceToHost, s));
-    HIP_TRY(hipMemcpyAsync(hval.data(), v_out, nver * 4, hipMemcpyDeviceToHost, s));
+    // The sorted hits come back into pinned host memory kept by the calling thread (grown
+    // as needed, never freed, like hits_tl): fresh pageable vectors cost their page faults
+    // plus a staged copy, 2-3 ms for C3b's 1 Mi hits (measured, round 3).
+    struct PinnedHits {
+        uint8_t* p = nullptr;
+        size_t bytes = 0;
+    };
+    static thread_local PinnedHits ph;
+    if (ph.bytes < nver * 12) {
+        if (ph.p) (void)hipHostFree(ph.p);
+        ph = PinnedHits();
+        const size_t bytes = nver * 12 + (nver * 12) / 4;
+        HIP_TRY(hipHostMalloc((void**)&ph.p, bytes, hipHostMallocDefault));
+        ph.bytes = bytes;
+    }
+    const uint64_t* hkey = (const uint64_t*)ph.p;
+    const uint32_t* hval = (const uint32_t*)(ph.p + nver * 8);
+    HIP_TRY(hipMemcpyAsync(ph.p, k_out, nver * 8, hipMemcpyDeviceToHost, s));
+    HIP_TRY(hipMemcpyAsync(ph.p + nver * 8, v_out, nver * 4, hipMemcpyDeviceToHost, s));
     HIP_TRY(hipStreamSynchronize(s));
     t_d2h = ms_since(t0);
     // (segment, position)-sorted; segments are in (source, position) order, so each
@@ -1125,18 +1195,22 @@ int Classifier::scan(const std::vector<std::array<uint64_t, 3>>& ranges) {
         while (h < hend) {
             const uint32_t si = seg_src[hkey[h] >> kSegShift];
             Src& c = src[si];
-            pos.clear();
-            blk.clear();
-            for (; h < hend && seg_src[hkey[h] >> kSegShift] == si; ++h) {
+            size_t e = h;
+            while (e < hend && seg_src[hkey[e] >> kSegShift] == si) ++e;
+            // a source's first hits go straight into its lists (recycled capacity, see
+            // Classifier::~Classifier); later ones are merged
+            const bool direct = c.hpos.empty();
+            std::vector<uint64_t>& P = direct ? c.hpos : pos;
+            std::vector<uint32_t>& B = direct ? c.hblk : blk;
+            P.clear();
+            B.clear();
+            P.reserve(e - h);
+            B.reserve(e - h);
+            for (; h < e; ++h) {
                 const uint64_t p = segs[hkey[h] >> kSegShift].pos_begin + (hkey[h] & 0xFFFFFFFFull);
-                if (p >= c.p0 && p < c.p1) { pos.push_back(p); blk.push_back(hval[h]); }
+                if (p >= c.p0 && p < c.p1) { P.push_back(p); B.push_back(hval[h]); }
             }
-            if (c.hpos.empty()) {
-                c.hpos.swap(pos);
-                c.hblk.swap(blk);
-            } else {
-                merge_hits(c, pos, blk);
-            }
+            if (!direct) merge_hits(c, pos, blk);
         }
     };
     const int nthr = nver >= (1u << 16) ? walk_threads() : 1;
@@ -1603,6 +1677,7 @@ static int match_impl(sydelta_index* ix, const uint8_t* d_buf, const uint64_t* s
     C.prof = cp.get();
     C.n = n;
     C.src.resize(nf);
+    C.adopt_spare();
     uint64_t tot_pos = 0;
     for (uint64_t f = 0; f < nf; ++f) {
         b->d[f].source_size = src_len[f];
@@ -2461,6 +2536,7 @@ extern "C" int sydelta_chunk_classify(sydelta_index* idx, const uint8_t* d_buf, 
     C.prof = cp.get();
     C.n = n;
     C.src.resize(1);
+    C.adopt_spare();
     Src& c = C.src[0];
     c.file = 0;
     c.off = 0;

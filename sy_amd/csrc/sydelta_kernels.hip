@@ -4913,11 +4913,13 @@ __global__ void k_synth_mutate(uint8_t* __restrict__ dst, const uint8_t* __restr
 // ===========================================================================
 static inline unsigned grid_for(uint64_t threads, unsigned block) { return (unsigned)((threads + block - 1) / block); }
 
-// Large single-file indexes (block size 4096) scan with k_scan_r + k_verify_r by default:
-// 9.88 + 2.81 ms per 4 GiB against k_scan_l2's 14.82, k_scan_l1's 16.78 and k_scan_lds's
-// 19.2 ms in global-filter mode.  SYDELTA_SCAN_L1 (read when the index is built and per call: the
-// parity tests run every scanner): 0 k_scan_lds, 1 k_scan_l1, 2 k_scan_l1 over two key
-// partitions (l1_part), 3 k_scan_s, 4 k_scan_l2, 5 k_scan_r + k_verify_r (the default).
+// Large single-file indexes (block size 4096) scan with k_scan_r by default, verifying
+// from registers at each tile's end: 11.17 ms per 4 GiB (9.88 + 2.81 with the separate
+// k_verify_r, SYDELTA_SCAN_R_INLINE=0) against k_scan_l2's 14.82, k_scan_l1's 16.78 and
+// k_scan_lds's 19.2 ms in global-filter mode.  SYDELTA_SCAN_L1
+// (read when the index is built and per call: the parity tests run every scanner):
+// 0 k_scan_lds, 1 k_scan_l1, 2 k_scan_l1 over two key partitions (l1_part), 3 k_scan_s,
+// 4 k_scan_l2, 5 k_scan_r (the default).
 int scan_l1_mode() {
     const char* e = getenv("SYDELTA_SCAN_L1");
     return (e && e[0] >= '0' && e[0] <= '5' && e[1] == 0) ? e[0] - '0' : 5;
