@@ -481,35 +481,41 @@ def _pmc_order(path: str):
     return (int(m.group(1)), len(m.group(2)), m.group(2)) if m else (0, 0, "")
 
 
-def pmc_traffic(kernel: str, per_launch: int):
-    """HBM bytes per launch of `kernel` from the committed rocprofv3 PMC summary of this
-    round (profiles/*_pmc.json, written by scripts/pmc_summary.py from FETCH_SIZE and
-    WRITE_SIZE passes of this same bench command), scaled to this launch's size."""
+def _pmc_files(workload: str, block_size: int):
+    """profiles/*_pmc.json of this workload and block size, oldest first.  A summary
+    records both (scripts/pmc_summary.py workload=.. block_size=..); files without them
+    (round 1-3) or of another workload are never borrowed."""
     import glob
 
-    best = None
+    out = []
     for f in sorted(glob.glob(os.path.join(ROOT, "profiles", "r*_pmc.json")), key=_pmc_order):
         try:
             d = json.load(open(f))
         except Exception:
             continue
-        for k, v in d.get("kernels", {}).items():
-            if k == kernel and "traffic_bytes" in v and v.get("bytes_per_launch"):
-                best = v["traffic_bytes"] * per_launch / v["bytes_per_launch"]
-    return int(best) if best else None
+        if d.get("workload") == workload and d.get("block_size") == block_size:
+            out.append((f, d))
+    return out
 
 
-def pmc_counters(kernel: str):
+def pmc_traffic(kernel: str, per_launch: int, workload: str, block_size: int):
+    """(HBM bytes per launch of `kernel`, source file) from the newest committed rocprofv3
+    PMC summary of the same workload and block size (FETCH_SIZE and WRITE_SIZE passes of
+    this bench command), scaled to this launch's size; (None, None) when there is none."""
+    best, src = None, None
+    for f, d in _pmc_files(workload, block_size):
+        v = d.get("kernels", {}).get(kernel)
+        if v and "traffic_bytes" in v and v.get("bytes_per_launch"):
+            best, src = v["traffic_bytes"] * per_launch / v["bytes_per_launch"], os.path.basename(f)
+    return (int(best), "profiles/" + src) if best else (None, None)
+
+
+def pmc_counters(kernel: str, workload: str, block_size: int):
     """Raw per-launch counters (TCC/TCP request counts) of `kernel` from the newest
-    profiles/*_pmc.json that has them, with that launch's algorithmic bytes."""
-    import glob
-
+    profiles/*_pmc.json of the same workload and block size, with that launch's
+    algorithmic bytes."""
     best = None
-    for f in sorted(glob.glob(os.path.join(ROOT, "profiles", "r*_pmc.json")), key=_pmc_order):
-        try:
-            d = json.load(open(f))
-        except Exception:
-            continue
+    for f, d in _pmc_files(workload, block_size):
         v = d.get("kernels", {}).get(kernel)
         if v and v.get("counters") and v.get("bytes_per_launch"):
             best = dict(v["counters"], bytes_per_launch=v["bytes_per_launch"], source=os.path.basename(f))
@@ -520,8 +526,7 @@ def algo_bytes_per_step(workload: str, n: int, nb_bytes: int, src_bytes: int) ->
     """Algorithmic HBM bytes per step of each kernel that can dominate a workload.  Per
     step the signature kernels read the basis once and the scan reads the source once
     (SURVEY.md section 8(d))."""
-    return {"k_scan": src_bytes, "k_scan_lds": src_bytes, "k_scan_l1": src_bytes, "k_scan_l2": src_bytes,
-            "k_scan_w": src_bytes, "k_scan_s": src_bytes, "k_scan_r": src_bytes,
+    return {"k_scan": src_bytes, "k_scan_lds": src_bytes, "k_scan_w": src_bytes, "k_scan_r": src_bytes,
             "k_sig_fast": nb_bytes if workload in ("c3", "c3b") else n,
             "k_sig_batch": n, "k_sig_wave": n, "k_probe": src_bytes,
             "k_apply": 2 * n,  # apply: every output byte read once and written once
@@ -534,7 +539,7 @@ def algo_bytes_per_step(workload: str, n: int, nb_bytes: int, src_bytes: int) ->
             "k_xxh_pieces": n}  # xxh3: every file byte read once
 
 
-def roofline(prof: dict, steps: int, algo_step: dict, positions=None, keys=None):
+def roofline(prof: dict, steps: int, algo_step: dict, positions=None, keys=None, workload="c3", block_size=4096):
     """Roofline of the dominant kernel: algorithmic bytes per launch / its average launch
     time (HIP events on the launch stream, sydelta_profile).  A kernel launched L times
     per step gets 1/L of its per-step bytes per launch (the scan is split into segments
@@ -550,8 +555,9 @@ def roofline(prof: dict, steps: int, algo_step: dict, positions=None, keys=None)
     that pass the level-1 filter in LDS send a request; that fraction is modelled as
     1 - exp(-keys / bits) (one bit per key) and the entry says so.
 
-    k_scan_r hands its level-2 passes to k_verify_r, so `match` adds the two kernels'
-    time: the source bytes per step over the whole match."""
+    `bound` is "l2" when the L2 request rate binds the kernel (its l2_gather fraction,
+    measured or modelled, exceeds its HBM fraction); achieved / peak / frac stay the HBM
+    figures the metric is quoted in."""
     import math
 
     dom = max(prof, key=lambda k: prof[k]["ms"]) if prof else None
@@ -561,13 +567,12 @@ def roofline(prof: dict, steps: int, algo_step: dict, positions=None, keys=None)
     avg_ms = prof[dom]["ms"] / max(1, prof[dom]["count"])
     per_launch = int(algo_step[dom] / launches_per_step)
     ach = per_launch / (avg_ms * 1e-3) / 1e9
+    traffic, tsrc = pmc_traffic(dom, per_launch, workload, block_size)
     roof = {"bound": "hbm", "achieved": round(ach, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-            "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": pmc_traffic(dom, per_launch),
+            "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": traffic, "traffic_source": tsrc,
             "kernel": dom, "avg_launch_ms": round(avg_ms, 4), "algorithmic_bytes_per_launch": per_launch}
-    # level-1 filter bits (one hash) per key: with P key partitions (SYDELTA_SCAN_L1=2) the
-    # scan is launched once per partition and each launch's filter holds 1/P of the keys
-    l1_bits = {"k_scan_l1": (1 << 20) * max(1, round(launches_per_step)), "k_scan_s": 1 << 20,
-               "k_scan_l2": 28672 * 32, "k_scan_w": 1 << 19, "k_scan_r": 38400 * 32}
+    # level-1 filter bits per key (one hash)
+    l1_bits = {"k_scan_w": 1 << 19, "k_scan_r": 38400 * 32}
     if positions and (dom in ("k_scan_lds", "k_scan") or (dom in l1_bits and keys)):
         per_pos = 1.0 if dom not in l1_bits else 1.0 - math.exp(-keys / float(l1_bits[dom]))
         req = positions * per_pos / launches_per_step  # filter-word requests per launch
@@ -578,7 +583,7 @@ def roofline(prof: dict, steps: int, algo_step: dict, positions=None, keys=None)
                              "requests_per_position": round(per_pos, 4),
                              "model": ("one per window start" if dom not in l1_bits else
                                        f"window starts x level-1 pass rate 1-exp(-keys/{l1_bits[dom]})")}
-        pc = pmc_counters(dom)
+        pc = pmc_counters(dom, workload, block_size)
         if pc and pc.get("TCC_REQ_sum"):
             # measured: every L2 request of the launch (filter words, staged bytes, table
             # lookups) per scanned byte, from the rocprofv3 TCC pass of the same command
@@ -589,12 +594,9 @@ def roofline(prof: dict, steps: int, algo_step: dict, positions=None, keys=None)
                 "tcc_requests_per_s_G": round(rq * per_launch / (avg_ms * 1e-3) / 1e9, 2),
                 "frac": round(rq * per_launch / (avg_ms * 1e-3) / L2_GATHER_PEAK, 4),
                 "source": "profiles/" + pc["source"]}
-    parts = [k for k in ("k_scan_r", "k_lookup_r", "k_verify_r") if k in prof]
-    if dom == "k_scan_r" and "k_verify_r" in parts:
-        ms = sum(prof[k]["ms"] for k in parts) / steps  # per step
-        mb = algo_step[dom] / (ms * 1e-3) / 1e9
-        roof["match"] = {"kernels": parts, "ms_per_step": round(ms, 4), "achieved": round(mb, 2),
-                         "unit": "GB/s", "frac": round(mb / HBM_PEAK_GBS, 4)}
+        lf = roof["l2_gather"].get("measured", roof["l2_gather"])["frac"]
+        if lf > roof["frac"]:
+            roof["bound"] = "l2"
     return roof
 
 
@@ -924,7 +926,8 @@ def main():
     stats = (last if isinstance(last, dict) else last.stats) if last is not None else None
     positions = stats.get("positions") if isinstance(stats, dict) and args.workload in ("c3", "c3b") else None
     roof = roofline(prof, args.steps, algo_step, positions,
-                    keys=nb_bytes // bs if args.workload in ("c3", "c3b") else None)
+                    keys=nb_bytes // bs if args.workload in ("c3", "c3b") else None, workload=args.workload,
+                    block_size=bs)
     kernels = {k: {"avg_ms": round(v["ms"] / max(1, v["count"]), 4), "launches": v["count"]} for k, v in prof.items()}
 
     if rank == 0:

@@ -91,6 +91,26 @@ const char *sydelta_last_error(void);
 /* Number of visible HIP devices (0 without a GPU; never initialises a device). */
 int sydelta_device_count(int *count);
 
+/* Devices of the path-level entry points (sydelta_compute_checksums,
+ * sydelta_generate_delta(_streaming), sydelta_estimate_change_ratio).  sy calls them from
+ * up to --parallel (default 10) spawn_blocking threads at once (sync/mod.rs:672-697,
+ * cli.rs:178-180, ssh.rs:913), and Rust makes no device current: each calling thread is
+ * bound on its first path-level call to the allowed device with the fewest bound threads
+ * (ties round-robin) and keeps it (its stream and buffers live there); a thread's exit
+ * unbinds it.  The device-pointer entry points take their device explicitly. */
+/* Restrict automatic binding to devices[0..n) (n = 0: every visible device); threads
+ * already bound keep their device. */
+int sydelta_set_devices(const int *devices, int n);
+/* Bind the calling thread's path-level calls to `device`, or (-1) let its next call bind
+ * it automatically. */
+int sydelta_set_thread_device(int device);
+/* The device the calling thread's path-level calls use (bound now if it was not). */
+int sydelta_thread_device(int *device);
+/* Release memory the library keeps between calls for reuse: index allocations held per
+ * device (made on library streams) and the calling thread's scan buffers (device and
+ * pinned host memory).  Other threads' buffers stay with them. */
+void sydelta_trim(void);
+
 /* mod.rs:20-23 `calculate_block_size(file_size) -> usize`: sqrt clamped to 512..=131072. */
 uint64_t sydelta_calculate_block_size(uint64_t file_size);
 
@@ -260,6 +280,22 @@ sydelta_delta *sydelta_delta_new(uint64_t source_size, uint64_t block_size);
 /* dst.ops += src.ops, merging dst's trailing Data op with src's leading Data op when
  * they are contiguous (literal runs stay maximal, generator.rs:186-197). */
 int sydelta_delta_append(sydelta_delta *dst, const sydelta_delta *src);
+
+/* The same split inside one process (no reference counterpart; the in-process form of
+ * bench.py's one-process-per-GPU C5): one file chunk-sharded over ndev devices.  Basis
+ * chunk g = d_basis[g][0, basis_len[g]) on devices[g], every chunk but the last a whole
+ * number of blocks; it is signed there, and each device pulls the other chunks' slices of
+ * the signature SoA with peer copies (hipMemcpyPeerAsync, xGMI between MI355X devices of
+ * a node) and builds the whole file's index.  Source chunk g classifies full-window
+ * positions [src_pos[g], src_pos[g+1]) (the last: to the end) on devices[g] from d_src[g],
+ * which holds source bytes [src_pos[g], src_pos[g] + src_buf_len[g]) as
+ * sydelta_chunk_classify requires (src_pos[0] = 0, block-aligned starts; a chunk's buffer
+ * reaches block_size - 1 bytes past its end).  The walks are chained inside the library;
+ * *out equals generate_delta's op list for the whole file (generator.rs:242-379).  A
+ * device may be listed more than once. */
+int sydelta_delta_multi_device(const int *devices, int ndev, const uint8_t *const *d_basis, const uint64_t *basis_len,
+                               const uint8_t *const *d_src, const uint64_t *src_pos, const uint64_t *src_buf_len,
+                               uint64_t src_len, uint64_t block_size, sydelta_delta **out);
 
 /* ---------------------------------------------------------------------------
  * Wire formats: serde_json's compact text of the types sy

@@ -1,13 +1,15 @@
 """Summarise rocprofv3 output of scripts/gpu_check.sh into profiles/.
 
-    python scripts/pmc_summary.py gpurun_out/<tag> profiles/<tag> [kernel=bytes_per_launch ...]
+    python scripts/pmc_summary.py gpurun_out/<tag> profiles/<tag> [workload=c3] [block_size=4096] \
+        [kernel=bytes_per_launch ...]
 
 Writes <dst>_kernel_stats.csv (the --kernel-trace --stats summary, verbatim) and
 <dst>_pmc.json: per kernel, average duration and HBM bytes per launch from the
 FETCH_SIZE / WRITE_SIZE passes, corrected as MI355X_MICROARCH.md §HBM says
 (FETCH_SIZE is in KiB and reports half the bytes of 16-B/lane streaming reads on
 gfx950 -> x1024 x2; WRITE_SIZE in KiB, exact -> x1024).  bench.py reads the
-_pmc.json of the current round to fill roofline.traffic.
+_pmc.json whose workload and block size match its own run to fill roofline.traffic
+(a file without them, or of another workload, is never borrowed).
 """
 import collections
 import csv
@@ -40,6 +42,8 @@ def counters(path):
 
 def main(src, dst, sizes=()):
     sizes = dict(kv.split("=") for kv in sizes)
+    workload = sizes.pop("workload", None)
+    block_size = sizes.pop("block_size", None)
     stats = os.path.join(src, "trace", "run_kernel_stats.csv")
     shutil.copy(stats, dst + "_kernel_stats.csv")
     dur = {}
@@ -78,8 +82,9 @@ def main(src, dst, sizes=()):
             out[k]["bytes_per_launch"] = int(sizes[k])
             if "traffic_bytes" in out[k]:
                 out[k]["traffic_over_algorithmic"] = round(out[k]["traffic_bytes"] / int(sizes[k]), 3)
-    meta = {"source": src, "correction": "FETCH_SIZE KiB x1024 x2 (gfx950 half-count of 16B/lane reads); "
-            "WRITE_SIZE KiB x1024", "kernels": out}
+    meta = {"source": src, "workload": workload, "block_size": int(block_size) if block_size else None,
+            "correction": "FETCH_SIZE KiB x1024 x2 (gfx950 half-count of 16B/lane reads); WRITE_SIZE KiB x1024",
+            "kernels": out}
     json.dump(meta, open(dst + "_pmc.json", "w"), indent=1)
     print(json.dumps(out, indent=1))
 

@@ -63,6 +63,10 @@ SIGNATURES = [
     ("sydelta_abi_version", _i, []),
     ("sydelta_last_error", ctypes.c_char_p, []),
     ("sydelta_device_count", _i, [ctypes.POINTER(_i)]),
+    ("sydelta_set_devices", _i, [ctypes.POINTER(_i), _i]),
+    ("sydelta_set_thread_device", _i, [_i]),
+    ("sydelta_thread_device", _i, [ctypes.POINTER(_i)]),
+    ("sydelta_trim", None, []),
     ("sydelta_calculate_block_size", _u64, [_u64]),
     ("sydelta_signature_device", _i, [_i, _vp, _u64, _u64, _vp, _vp, _vp]),
     ("sydelta_index_create", _i, [_i, _vp, _vp, _u64, _u64, _u64, _i, _vp, _pp]),
@@ -100,6 +104,9 @@ SIGNATURES = [
     ("sydelta_delta_new", _vp, [_u64, _u64]),
     ("sydelta_delta_append", _i, [_vp, _vp]),
     ("sydelta_delta_from_ops", _vp, [_vp, _u64, _u64, _u64]),
+    ("sydelta_delta_multi_device", _i, [ctypes.POINTER(_i), _i, ctypes.POINTER(_vp), ctypes.POINTER(_u64),
+                                        ctypes.POINTER(_vp), ctypes.POINTER(_u64), ctypes.POINTER(_u64), _u64, _u64,
+                                        _pp]),
     ("sydelta_checksums_to_json", _u64, [_vp, _u64, _vp, _u64]),
     ("sydelta_checksums_from_json", _i, [_vp, _u64, ctypes.POINTER(ctypes.POINTER(BlockChecksumC)),
                                          ctypes.POINTER(_u64)]),

@@ -29,6 +29,7 @@
 #include <mutex>
 #include <thread>
 #include <string>
+#include <set>
 #include <unordered_set>
 #include <vector>
 
@@ -293,6 +294,97 @@ extern "C" int sydelta_device_count(int* count) try {
     return sydelta::host_exception();
 }
 
+// ---------------------------------------------------------------------------
+// the device of the path-level entry points
+// ---------------------------------------------------------------------------
+// sy calls compute_checksums / generate_delta(_streaming) from up to --parallel (default
+// 10) spawn_blocking threads at once (sync/mod.rs:672-697, cli.rs:178-180, ssh.rs:913),
+// and Rust cannot make a device current for them.  So each calling thread is bound to a
+// device on its first path-level call -- the allowed device with the fewest bound threads,
+// ties broken round-robin -- and stays there (its stream, pinned buffers and scratch live
+// on that device); a thread's exit unbinds it.  sydelta_set_thread_device binds one
+// explicitly, sydelta_set_devices restricts the automatic choice.
+namespace {
+std::mutex& bind_mu() {
+    static std::mutex* m = new std::mutex();  // never destroyed: thread exits may come after static teardown
+    return *m;
+}
+std::vector<int> g_allowed;  // under bind_mu; empty: every visible device
+std::map<int, int> g_bound;  // under bind_mu; device -> bound threads
+unsigned g_rr = 0;           // under bind_mu
+struct ThreadBinding {
+    int dev = -1;
+    void set(int d) {
+        std::lock_guard<std::mutex> lk(bind_mu());
+        if (dev >= 0 && g_bound[dev] > 0) --g_bound[dev];
+        dev = d;
+        if (dev >= 0) ++g_bound[dev];
+    }
+    ~ThreadBinding() { set(-1); }
+};
+thread_local ThreadBinding t_bind;
+}  // namespace
+
+int sydelta::path_device(int* out) {
+    if (t_bind.dev >= 0) {
+        *out = t_bind.dev;
+        return SYDELTA_OK;
+    }
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess || n <= 0) return fail(SYDELTA_E_NODEV, "no HIP device visible");
+    int best = -1;
+    {
+        std::lock_guard<std::mutex> lk(bind_mu());
+        std::vector<int> cand;
+        for (int d : g_allowed)
+            if (d >= 0 && d < n) cand.push_back(d);
+        if (cand.empty())
+            for (int d = 0; d < n; ++d) cand.push_back(d);
+        const unsigned start = g_rr++;
+        for (size_t k = 0; k < cand.size(); ++k) {
+            const int d = cand[(start + k) % cand.size()];
+            if (best < 0 || g_bound[d] < g_bound[best]) best = d;
+        }
+        ++g_bound[best];
+    }
+    t_bind.dev = best;
+    *out = best;
+    return SYDELTA_OK;
+}
+
+extern "C" int sydelta_set_devices(const int* devices, int n) try {
+    if (n < 0 || (n > 0 && !devices)) return fail(SYDELTA_E_INVAL, "bad device list");
+    int vis = 0;
+    if (hipGetDeviceCount(&vis) != hipSuccess) vis = 0;
+    for (int i = 0; i < n; ++i)
+        if (devices[i] < 0 || devices[i] >= vis)
+            return fail(SYDELTA_E_NODEV, "device %d is not visible (%d devices)", devices[i], vis);
+    std::lock_guard<std::mutex> lk(bind_mu());
+    g_allowed.assign(devices, devices + n);
+    return SYDELTA_OK;
+} catch (...) {
+    return sydelta::host_exception();
+}
+
+extern "C" int sydelta_set_thread_device(int device) try {
+    if (device >= 0) {
+        int vis = 0;
+        if (hipGetDeviceCount(&vis) != hipSuccess || device >= vis)
+            return fail(SYDELTA_E_NODEV, "device %d is not visible", device);
+    }
+    t_bind.set(device < 0 ? -1 : device);
+    return SYDELTA_OK;
+} catch (...) {
+    return sydelta::host_exception();
+}
+
+extern "C" int sydelta_thread_device(int* device) try {
+    if (!device) return fail(SYDELTA_E_INVAL, "device is NULL");
+    return path_device(device);
+} catch (...) {
+    return sydelta::host_exception();
+}
+
 // mod.rs:20-23
 extern "C" uint64_t sydelta_calculate_block_size(uint64_t file_size) {
     uint64_t s = (uint64_t)std::sqrt((double)file_size);
@@ -407,43 +499,60 @@ struct sydelta_index {
 };
 
 // Index memory is kept for the next index: a released index's allocation is held (one
-// per device) and the next index built on the same stream with no more bytes (and no
-// less than half) takes it over, so the usual sequence -- build, match, free, build
-// again (a file after another, bench steps) -- allocates once.  A hipFreeAsync on a stream
-// with no work queued blocked the host 0.3-0.6 ms for these allocations (measured, round
-// 3: C3's 50 MB index, C5's 130 MB one), as for the scan's hit buffers.  Every entry point
-// that reads an index synchronizes its stream before returning, so no queued work still
-// reads a released pool, and a new owner on the same stream uses it in stream order.  A
-// held allocation that does not fit is released in its stream's order (a caller stream
-// must outlive the index, include/sydelta.h).
+// per device) and the next index built with no more bytes (and no less than half) takes
+// it over, so the usual sequence -- build, match, free, build again (a file after
+// another, bench steps) -- allocates once.  A hipFreeAsync on a stream with no work
+// queued blocked the host 0.3-0.6 ms for these allocations (measured, round 3: C3's 50 MB
+// index, C5's 130 MB one), as for the scan's hit buffers.  The held block is homed on a
+// library stream (never destroyed): an index built on a caller stream hands its block
+// over with an event (record on the caller stream, wait on the library stream), so no
+// handle to a caller stream outlives its index; a new owner on another stream waits for
+// the home stream the same way.  No host synchronization on either side.
 namespace {
 struct KeptPool {
     void* p = nullptr;
     size_t bytes = 0;
-    hipStream_t s = nullptr;
+    hipStream_t s = nullptr;  // a library thread stream
 };
 std::mutex g_kept_mu;
 KeptPool g_kept[64];
+// One event per (thread, device) for stream hand-offs (re-recorded freely: a wait takes
+// the record that precedes it); never destroyed, like the thread streams.
+hipEvent_t handoff_event(int device) {
+    static thread_local std::map<int, hipEvent_t> ev;
+    hipEvent_t& e = ev[device];
+    if (!e && hipEventCreateWithFlags(&e, hipEventDisableTiming) != hipSuccess) e = nullptr;
+    return e;
+}
+// Order `to` after the work queued so far on `from` (same device, current).
+hipError_t stream_after(hipStream_t to, hipStream_t from, int device) {
+    if (to == from) return hipSuccess;
+    hipEvent_t e = handoff_event(device);
+    if (!e) return hipErrorOutOfMemory;
+    hipError_t r = hipEventRecord(e, from);
+    return r != hipSuccess ? r : hipStreamWaitEvent(to, e, 0);
+}
 }  // namespace
 
 static void index_release(sydelta_index* x) {
     if (!x) return;
     if (x->d_pool) {
         KeptPool old;
-        if (x->device >= 0 && x->device < 64) {
+        const hipStream_t home = thread_stream(x->device);
+        if (x->device >= 0 && x->device < 64 && home && stream_after(home, x->stream, x->device) == hipSuccess) {
             std::lock_guard<std::mutex> lk(g_kept_mu);
             old = g_kept[x->device];
-            g_kept[x->device] = {x->d_pool, x->pool_bytes, x->stream};
+            g_kept[x->device] = {x->d_pool, x->pool_bytes, home};
         } else {
-            old = {x->d_pool, 0, x->stream};
+            old = {x->d_pool, 0, x->stream};  // released in its own stream's order
         }
-        if (old.p) (void)hipFreeAsync(old.p, old.s ? old.s : thread_stream(x->device));
+        if (old.p) (void)hipFreeAsync(old.p, old.s);
     }
     delete x;
 }
 
-// The held allocation of `device` if it was made on stream s and fits `bytes` (else
-// released in its own stream's order).
+// The held allocation of `device` if it fits `bytes` (ordered after its home stream), else
+// released in its home stream's order.
 static void* take_kept_pool(int device, size_t bytes, hipStream_t s, size_t* got) {
     if (device < 0 || device >= 64) return nullptr;
     KeptPool k;
@@ -453,12 +562,60 @@ static void* take_kept_pool(int device, size_t bytes, hipStream_t s, size_t* got
         g_kept[device] = KeptPool();
     }
     if (!k.p) return nullptr;
-    if (k.s == s && k.bytes >= bytes && k.bytes <= 2 * bytes + (64u << 20)) {
+    if (k.bytes >= bytes && k.bytes <= 2 * bytes + (64u << 20) && stream_after(s, k.s, device) == hipSuccess) {
         *got = k.bytes;
         return k.p;
     }
-    (void)hipFreeAsync(k.p, k.s ? k.s : thread_stream(device));
+    (void)hipFreeAsync(k.p, k.s);
     return nullptr;
+}
+
+// Per-thread scratch of the scan (Classifier::scan): the verified-hit buffers on each
+// device and the pinned host buffer the sorted hits come back into.
+namespace sydelta {
+namespace {
+std::mutex g_scratch_mu;
+struct ThreadScratch {
+    std::map<int, HitScratch> hits;  // per device
+    PinnedHits pinned;
+};
+std::vector<ThreadScratch*> g_scratch;  // every thread's (never destroyed), for sydelta_trim
+ThreadScratch& thread_scratch() {
+    static thread_local ThreadScratch* t = [] {
+        ThreadScratch* x = new ThreadScratch();
+        std::lock_guard<std::mutex> lk(g_scratch_mu);
+        g_scratch.push_back(x);
+        return x;
+    }();
+    return *t;
+}
+}  // namespace
+HitScratch& thread_hit_scratch(int device) { return thread_scratch().hits[device]; }
+PinnedHits& thread_pinned_hits() { return thread_scratch().pinned; }
+}  // namespace sydelta
+
+extern "C" void sydelta_trim(void) {
+    // kept index allocations of every device, released in their (library) streams' order
+    KeptPool kept[64];
+    {
+        std::lock_guard<std::mutex> lk(g_kept_mu);
+        for (int d = 0; d < 64; ++d) {
+            kept[d] = g_kept[d];
+            g_kept[d] = KeptPool();
+        }
+    }
+    for (int d = 0; d < 64; ++d)
+        if (kept[d].p && hipSetDevice(d) == hipSuccess) (void)hipFreeAsync(kept[d].p, kept[d].s);
+    // the calling thread's scan scratch (other threads' stay with them: they may be in a call)
+    ThreadScratch& t = thread_scratch();
+    for (auto& kv : t.hits)
+        if (kv.second.p && hipSetDevice(kv.first) == hipSuccess) {
+            (void)hipFreeAsync(kv.second.p, thread_stream(kv.first));
+            (void)hipStreamSynchronize(thread_stream(kv.first));
+        }
+    t.hits.clear();
+    if (t.pinned.p) (void)hipHostFree(t.pinned.p);
+    t.pinned = PinnedHits();
 }
 
 extern "C" void sydelta_index_free(sydelta_index* idx) {
@@ -534,16 +691,14 @@ static int index_create_impl(int device, const uint32_t* weak, const uint64_t* s
     const size_t sz_weak = al(4 * nb), sz_strong = al(8 * nb), sz_filt = al(4 * fw), sz_t = al(4 * sl);
     const size_t sz_order = al(4 * nb), sz_slot = al(4 * nb), sz_files = al(sizeof(FileIx) * nfiles);
     const size_t sz_fblk = al(8 * (nfiles + 1)), sz_cstrong = al(8 * nb);
-    // level-1 filter for k_scan_l1: one large file (the BASELINE C3 shape)
-    const bool want_narrow = nfiles == 1 && nblocks > kLdsFilterKeys && block_size == 4096;  // k_scan_l1's scope
+    // k_scan_r's level-1 filter: one large file at bs 4096 (the BASELINE C3 shape)
+    const bool want_narrow = nfiles == 1 && nblocks > kLdsFilterKeys && block_size == 4096;
     // windows above the LDS-staged scans' limit, one file (the production block sizes of
     // files over 64 MiB, mod.rs:20-23): k_scan_w's level-1 filter and fat table
     const bool want_wide = nfiles == 1 && block_size > scan_max_window() && scan_wide_mode() != 0;
     const bool want_l1 = want_narrow || want_wide;
-    const uint32_t l1_parts = want_narrow ? (scan_l1_mode() == 2 ? 2u : 1u) : want_wide ? 1u : 0u;
-    const uint32_t l1_words = want_narrow ? (scan_l1_mode() == 5 ? kL1WordsR : scan_l1_mode() == 4 ? kL1WordsL2 : kL1Words)
-                                          : kL1WordsWide;
-    const size_t sz_l1 = al(4 * (size_t)l1_parts * l1_words);
+    const uint32_t l1_wshift = want_narrow ? 1u : 18u;
+    const size_t sz_l1 = want_l1 ? al(4 * l1_total_words(l1_wshift)) : 0;
     const size_t sz_fat = want_l1 ? al(16 * (size_t)sl) : 0;
     const size_t total = sz_weak + sz_strong + sz_filt + sz_l1 + sz_fat + 4 * sz_t + sz_order + sz_slot + sz_files +
                          sz_fblk + sz_cstrong;
@@ -559,8 +714,7 @@ static int index_create_impl(int device, const uint32_t* weak, const uint64_t* s
     ix.filt = (uint32_t*)p; p += sz_filt;
     if (want_l1) {
         ix.l1 = (uint32_t*)p; p += sz_l1;
-        ix.l1_parts = l1_parts;
-        ix.l1_wshift = want_narrow ? (scan_l1_mode() == 5 ? 1u : scan_l1_mode() == 4 ? 0u : 17u) : 18u;
+        ix.l1_wshift = l1_wshift;
         ix.fat = (uint4*)p; p += sz_fat;
     }
     ix.keys = (uint32_t*)p; p += sz_t;
@@ -1099,17 +1253,12 @@ int Classifier::scan(const std::vector<std::array<uint64_t, 3>>& ranges) {
     // them after the synchronize below -- ~100 MB at C3 -- blocked the host ~0.6 ms per
     // call (measured, round 3), reusing them costs nothing.  The previous call on this
     // thread synchronized its stream, so a buffer made on another stream is free to
-    // take over (or to release in this stream's order).  Never freed at thread exit (the
-    // HIP runtime may be gone), like the per-thread streams.
-    struct HitScratch {
-        void* p = nullptr;
-        size_t bytes = 0;
-        int dev = -1;
-    };
-    static thread_local HitScratch hits_tl;
+    // take over (or to release in this stream's order).  One buffer per (thread, device):
+    // a thread that alternates devices keeps each device's.  Released by sydelta_trim;
+    // never freed at thread exit (the HIP runtime may be gone), like the per-thread streams.
     int cur_dev = 0;
     HIP_TRY(hipGetDevice(&cur_dev));
-    if (hits_tl.p && hits_tl.dev != cur_dev) hits_tl = HitScratch();  // another device's: left to that pool
+    HitScratch& hits_tl = thread_hit_scratch(cur_dev);
     struct {
         void* p = nullptr;
     } hit_buf;
@@ -1122,7 +1271,6 @@ int Classifier::scan(const std::vector<std::array<uint64_t, 3>>& ranges) {
                 const size_t bytes = cap * 24 + (cap * 24) / 4;  // room to grow by a quarter
                 HIP_TRY(dev_malloc_async(&hits_tl.p, bytes, s));
                 hits_tl.bytes = bytes;
-                hits_tl.dev = cur_dev;
             }
             hit_buf.p = hits_tl.p;
         }
@@ -1167,13 +1315,10 @@ int Classifier::scan(const std::vector<std::array<uint64_t, 3>>& ranges) {
         HIP_TRY(launch_sort_hits(d_key, d_val, d_key + cap, d_val + cap, nver, end_bit, s, &k_out, &v_out));
     }
     // The sorted hits come back into pinned host memory kept by the calling thread (grown
-    // as needed, never freed, like hits_tl): fresh pageable vectors cost their page faults
-    // plus a staged copy, 2-3 ms for C3b's 1 Mi hits (measured, round 3).
-    struct PinnedHits {
-        uint8_t* p = nullptr;
-        size_t bytes = 0;
-    };
-    static thread_local PinnedHits ph;
+    // as needed; released by sydelta_trim, and after a call that needed more than
+    // kPinnedHitsKeep): fresh pageable vectors cost their page faults plus a staged copy,
+    // 2-3 ms for C3b's 1 Mi hits (measured, round 3).
+    PinnedHits& ph = thread_pinned_hits();
     if (ph.bytes < nver * 12) {
         if (ph.p) (void)hipHostFree(ph.p);
         ph = PinnedHits();
@@ -1227,6 +1372,10 @@ int Classifier::scan(const std::vector<std::array<uint64_t, 3>>& ranges) {
             return fail(SYDELTA_E_OOM, "out of host memory (hit lists)");
     } else {
         merge_range(0, nver);
+    }
+    if (ph.bytes > kPinnedHitsKeep) {  // a dense call's buffer is not kept (hipHostFree synchronizes)
+        (void)hipHostFree(ph.p);
+        ph = PinnedHits();
     }
     if (host_timing)
         fprintf(stderr, "sydelta scan: %zu segments, %llu hits: setup+kernel %.3f ms, sort+D2H %.3f ms, merge %.3f ms\n",
@@ -2076,8 +2225,10 @@ extern "C" int sydelta_compute_checksums(const char* path, uint64_t block_size, 
     if (L == 0) return SYDELTA_OK;  // checksum.rs:36-38
     if (block_size == 0) return fail(SYDELTA_E_INVAL, "block_size must be > 0");
     const uint64_t nb = (L + block_size - 1) / block_size;
-    if (int r = ensure_device(-1)) return r;
-    hipStream_t s = thread_stream(0);
+    int dev = 0;
+    if (int r = path_device(&dev)) return r;
+    if (int r = ensure_device(dev)) return r;
+    hipStream_t s = thread_stream(dev);
     const uint64_t C = std::min<uint64_t>(stream_chunk_bytes(block_size), L);
     const uint64_t nch = (L + C - 1) / C;
     PinnedPair& pin = t_stream_pinned;
@@ -2136,7 +2287,9 @@ extern "C" int sydelta_generate_delta(const char* source_path, const sydelta_blo
     *out = nullptr;
     std::vector<uint8_t> data;
     if (int r = read_file(source_path, data)) return r;
-    return generate_from_host(-1, data.data(), data.size(), sigs, nsigs, block_size, out);
+    int dev = 0;
+    if (int r = path_device(&dev)) return r;
+    return generate_from_host(dev, data.data(), data.size(), sigs, nsigs, block_size, out);
 } catch (...) {
     return sydelta::host_exception();
 }
@@ -2162,8 +2315,10 @@ extern "C" int sydelta_generate_delta_streaming(const char* source_path, const s
     if (int r = check_sigs(sigs, nsigs, block_size, &last_size)) return r;
     InFile f;
     if (int r = f.open_(source_path)) return r;
-    if (int r = ensure_device(-1)) return r;
-    hipStream_t s = thread_stream(0);
+    int dev = 0;
+    if (int r = path_device(&dev)) return r;
+    if (int r = ensure_device(dev)) return r;
+    hipStream_t s = thread_stream(dev);
     const uint64_t L = f.len, n = block_size;
     std::vector<uint32_t> w(nsigs);
     std::vector<uint64_t> st(nsigs);
@@ -2172,7 +2327,7 @@ extern "C" int sydelta_generate_delta_streaming(const char* source_path, const s
         st[i] = sigs[i].strong;
     }
     sydelta_index* ixp = nullptr;
-    if (int r = sydelta_index_create(0, w.data(), st.data(), nsigs, n, last_size, 0, s, &ixp)) return r;
+    if (int r = sydelta_index_create(dev, w.data(), st.data(), nsigs, n, last_size, 0, s, &ixp)) return r;
     std::unique_ptr<sydelta_index, void (*)(sydelta_index*)> ix(ixp, sydelta_index_free);
     std::vector<uint32_t>().swap(w);
     std::vector<uint64_t>().swap(st);
@@ -2644,4 +2799,175 @@ extern "C" sydelta_delta* sydelta_delta_new(uint64_t source_size, uint64_t block
     d->source_size = source_size;
     d->block_size = block_size;
     return d;
+}
+
+// ---------------------------------------------------------------------------
+// One file chunk-sharded over several devices of this process (BASELINE config 5,
+// SURVEY.md §8e): the in-process form of bench.py's one-process-per-GPU C5 step.
+// ---------------------------------------------------------------------------
+// 1. each device signs its basis chunk into its slice of a whole-file signature SoA;
+// 2. every device pulls the other slices with peer copies (hipMemcpyPeerAsync: xGMI
+//    between MI355X devices of one node), so each holds the full signature with global
+//    block indices and the lowest-index rule stays global;
+// 3. each device builds the full index and classifies its source chunk (host-pool
+//    threads, one per chunk: the classification's host waits overlap);
+// 4. the walks run speculatively from each chunk's start, in parallel; a chunk whose
+//    true entry (the previous chunk's exit) differs is walked again, in chunk order
+//    (shard.py walk_chain's rule); the parts are joined with sydelta_delta_append.
+// The result equals generate_delta's op list for the whole file (generator.rs:242-379):
+// classification is a pure function of the position.
+namespace {
+std::mutex g_peer_mu;
+std::set<std::pair<int, int>> g_peer_on;  // under g_peer_mu: (device, peer) with access enabled
+void enable_peer(int dev, int peer) {
+    if (dev == peer) return;
+    std::lock_guard<std::mutex> lk(g_peer_mu);
+    if (!g_peer_on.insert({dev, peer}).second) return;
+    int ok = 0;
+    if (hipDeviceCanAccessPeer(&ok, dev, peer) == hipSuccess && ok && hipSetDevice(dev) == hipSuccess)
+        (void)hipDeviceEnablePeerAccess(peer, 0);  // already enabled / unsupported: the copy still works
+    (void)hipGetLastError();
+}
+}  // namespace
+
+extern "C" int sydelta_delta_multi_device(const int* devices, int ndev, const uint8_t* const* d_basis,
+                                          const uint64_t* basis_len, const uint8_t* const* d_src,
+                                          const uint64_t* src_pos, const uint64_t* src_buf_len, uint64_t src_len,
+                                          uint64_t block_size, sydelta_delta** out) try {
+    if (!out) return fail(SYDELTA_E_INVAL, "out is NULL");
+    *out = nullptr;
+    if (ndev < 1 || !devices || !d_basis || !basis_len || !d_src || !src_pos || !src_buf_len)
+        return fail(SYDELTA_E_INVAL, "NULL argument or no device");
+    const uint64_t n = block_size;
+    if (n == 0) return fail(SYDELTA_E_INVAL, "block_size must be > 0");
+    // basis chunks: every one but the last a whole number of blocks
+    std::vector<uint64_t> nbg(ndev), bofs(ndev + 1, 0);
+    uint64_t L = 0;
+    for (int g = 0; g < ndev; ++g) {
+        if (g + 1 < ndev && basis_len[g] % n)
+            return fail(SYDELTA_E_INVAL, "basis chunk %d: length %llu is not a multiple of block_size", g,
+                        (unsigned long long)basis_len[g]);
+        if (basis_len[g] && !d_basis[g]) return fail(SYDELTA_E_INVAL, "basis chunk %d: NULL buffer", g);
+        nbg[g] = (basis_len[g] + n - 1) / n;
+        bofs[g + 1] = bofs[g] + nbg[g];
+        L += basis_len[g];
+    }
+    const uint64_t nb = bofs[ndev];
+    if (nb >= 0xFFFFFFFFull) return fail(SYDELTA_E_INVAL, "too many blocks");
+    const uint64_t last_size = nb ? L - (nb - 1) * n : 0;
+    // source chunks: block-aligned starts, chunk 0 from position 0
+    if (src_pos[0] != 0) return fail(SYDELTA_E_INVAL, "source chunk 0 must start at position 0");
+    for (int g = 1; g < ndev; ++g)
+        if (src_pos[g] < src_pos[g - 1] || src_pos[g] % n)
+            return fail(SYDELTA_E_INVAL, "source chunk %d: start %llu not ascending / not a multiple of block_size", g,
+                        (unsigned long long)src_pos[g]);
+    for (int g = 0; g < ndev; ++g)
+        if (int r = ensure_device(devices[g])) return r;
+    for (int g = 0; g < ndev; ++g)
+        for (int h = 0; h < ndev; ++h) enable_peer(devices[g], devices[h]);
+    // 1. signatures (the calling thread's stream on each device)
+    std::vector<hipStream_t> s(ndev);
+    std::vector<std::unique_ptr<DevBuf>> sig(ndev);
+    std::vector<uint32_t*> dw(ndev);
+    std::vector<uint64_t*> dst(ndev);
+    std::vector<hipEvent_t> ev(ndev, nullptr);
+    struct EvFree {
+        std::vector<hipEvent_t>& v;
+        ~EvFree() {
+            for (hipEvent_t e : v)
+                if (e) (void)hipEventDestroy(e);
+        }
+    } ev_free{ev};
+    CallProf cp;
+    for (int g = 0; g < ndev; ++g) {
+        HIP_TRY(hipSetDevice(devices[g]));
+        s[g] = thread_stream(devices[g]);
+        sig[g].reset(new DevBuf());
+        HIP_TRY(dev_malloc_async(&sig[g]->p, nb * 12 + 16, s[g]));
+        sig[g]->s = s[g];
+        dw[g] = (uint32_t*)sig[g]->p;
+        dst[g] = (uint64_t*)(((uintptr_t)(dw[g] + nb) + 7) & ~(uintptr_t)7);
+        HIP_TRY(launch_signature(d_basis[g], basis_len[g], n, dw[g] + bofs[g], dst[g] + bofs[g], s[g], cp.get()));
+        HIP_TRY(hipEventCreateWithFlags(&ev[g], hipEventDisableTiming));
+        HIP_TRY(hipEventRecord(ev[g], s[g]));
+    }
+    // 2. gather: device g pulls slice h from device h
+    for (int g = 0; g < ndev; ++g) {
+        HIP_TRY(hipSetDevice(devices[g]));
+        for (int h = 0; h < ndev; ++h) {
+            if (h == g || !nbg[h]) continue;
+            HIP_TRY(hipStreamWaitEvent(s[g], ev[h], 0));
+            if (devices[g] == devices[h]) {
+                HIP_TRY(hipMemcpyAsync(dw[g] + bofs[h], dw[h] + bofs[h], 4 * nbg[h], hipMemcpyDeviceToDevice, s[g]));
+                HIP_TRY(hipMemcpyAsync(dst[g] + bofs[h], dst[h] + bofs[h], 8 * nbg[h], hipMemcpyDeviceToDevice, s[g]));
+            } else {
+                HIP_TRY(hipMemcpyPeerAsync(dw[g] + bofs[h], devices[g], dw[h] + bofs[h], devices[h], 4 * nbg[h], s[g]));
+                HIP_TRY(hipMemcpyPeerAsync(dst[g] + bofs[h], devices[g], dst[h] + bofs[h], devices[h], 8 * nbg[h], s[g]));
+            }
+        }
+    }
+    // every device's gather done before any slice is released or read from another stream
+    for (int g = 0; g < ndev; ++g) {
+        HIP_TRY(hipSetDevice(devices[g]));
+        HIP_TRY(hipStreamSynchronize(s[g]));
+    }
+    // 3. full index per device, then the chunks classified in parallel
+    std::vector<std::unique_ptr<sydelta_index, void (*)(sydelta_index*)>> idx;
+    for (int g = 0; g < ndev; ++g) {
+        sydelta_index* x = nullptr;
+        if (int r = sydelta_index_create(devices[g], dw[g], dst[g], nb, n, nb ? last_size : n, 1, s[g], &x)) return r;
+        idx.emplace_back(x, sydelta_index_free);
+    }
+    for (int g = 0; g < ndev; ++g) {
+        HIP_TRY(hipSetDevice(devices[g]));
+        HIP_TRY(hipStreamSynchronize(s[g]));
+    }
+    std::vector<std::unique_ptr<sydelta_chunk, void (*)(sydelta_chunk*)>> ch;
+    for (int g = 0; g < ndev; ++g) ch.emplace_back(nullptr, sydelta_chunk_free);
+    std::vector<int> rc(ndev, SYDELTA_OK);
+    std::vector<std::string> err(ndev);
+    auto pos_end = [&](int g) { return g + 1 < ndev ? src_pos[g + 1] : std::max<uint64_t>(src_len, src_pos[g]) + 1; };
+    if (!run_parallel(ndev, [&](int g) {
+            sydelta_chunk* c = nullptr;
+            rc[g] = sydelta_chunk_classify(idx[g].get(), d_src[g], src_pos[g], src_buf_len[g], src_len, src_pos[g],
+                                           pos_end(g), nullptr, &c);
+            if (rc[g]) err[g] = sydelta_last_error();
+            ch[g].reset(c);
+        }))
+        return fail(SYDELTA_E_OOM, "out of host memory (chunk tasks)");
+    for (int g = 0; g < ndev; ++g)
+        if (rc[g]) return fail(rc[g], "chunk %d: %s", g, err[g].c_str());
+    // 4. speculative walks, then the chain
+    std::vector<std::unique_ptr<sydelta_delta, void (*)(sydelta_delta*)>> part;
+    for (int g = 0; g < ndev; ++g) part.emplace_back(nullptr, sydelta_delta_free);
+    std::vector<uint64_t> ex(ndev, 0);
+    if (!run_parallel(ndev, [&](int g) {
+            sydelta_delta* d = nullptr;
+            rc[g] = sydelta_chunk_walk(ch[g].get(), src_pos[g], &ex[g], &d);
+            if (rc[g]) err[g] = sydelta_last_error();
+            part[g].reset(d);
+        }))
+        return fail(SYDELTA_E_OOM, "out of host memory (walk tasks)");
+    for (int g = 0; g < ndev; ++g)
+        if (rc[g]) return fail(rc[g], "chunk %d walk: %s", g, err[g].c_str());
+    uint64_t e = 0;
+    for (int g = 0; g < ndev; ++g) {
+        if (e != src_pos[g]) {  // the previous chunk's last Copy reaches into this one
+            sydelta_delta* d = nullptr;
+            if (int r = sydelta_chunk_walk(ch[g].get(), e, &ex[g], &d)) return r;
+            part[g].reset(d);
+        }
+        e = ex[g];
+    }
+    std::unique_ptr<sydelta_delta, void (*)(sydelta_delta*)> joined(sydelta_delta_new(src_len, n), sydelta_delta_free);
+    for (int g = 0; g < ndev; ++g)
+        if (int r = sydelta_delta_append(joined.get(), part[g].get())) return r;
+    joined->source_size = src_len;
+    ch.clear();
+    idx.clear();
+    sig.clear();
+    *out = joined.release();
+    return SYDELTA_OK;
+} catch (...) {
+    return sydelta::host_exception();
 }

@@ -31,10 +31,26 @@ int fail(int code, const char* fmt, ...);
 int host_exception();
 // Make `device` current after its one-time gfx950 check.
 int ensure_device(int device);
+// The device of the calling thread's path-level calls (bound on first use, sticky).
+int path_device(int* out);
 // The calling thread's stream for `device`.
 hipStream_t thread_stream(int device);
 // Recount copy/data ops and literal bytes of d.
 void finish_stats(sydelta_delta* d);
+// Per-thread scan scratch (Classifier::scan): the verified-hit buffers on one device,
+// and the pinned host buffer the sorted hits come back into (not kept above
+// kPinnedHitsKeep).  Released by sydelta_trim.
+struct HitScratch {
+    void* p = nullptr;
+    size_t bytes = 0;
+};
+struct PinnedHits {
+    uint8_t* p = nullptr;
+    size_t bytes = 0;
+};
+constexpr size_t kPinnedHitsKeep = (size_t)256 << 20;
+HitScratch& thread_hit_scratch(int device);
+PinnedHits& thread_pinned_hits();
 // sydelta_set_profiling state; CallProf collects one call's kernel timings.
 bool profiling_on();
 struct CallProf {

@@ -23,23 +23,16 @@ hipError_t dev_malloc_async(void** p, size_t bytes, hipStream_t s);
 constexpr uint32_t kEmptyKey = 0xFFFFFFFFu;  // never a valid weak: A = weak & 0xFFFF <= 65520
 constexpr uint64_t kLdsFilterKeys = 16384;   // index sizes whose Bloom filter (<= 32 KiB) the scan keeps in LDS
 constexpr uint32_t kLdsFilterWordsMax = 8192;
-// Level-1 filter of a large single-file index (k_scan_l1 keeps it in LDS): 32768 words
-// = 128 KiB = 2^20 bits, built for indexes of more than kLdsFilterKeys keys.
-constexpr uint32_t kL1Words = 32768;   // k_scan_l1's level-1 filter (128 KiB), per key partition
 // Level-1 filter of a single-file index for windows above scan_max_window() (k_scan_w):
 // 16384 words = 64 KiB = 2^19 bits, beside the wide kernel's two staged byte regions.
 constexpr uint32_t kL1WordsWide = 16384;
-// k_scan_l2's level-1 filter (SYDELTA_SCAN_L1=4): 28672 words = 112 KiB beside its
-// 32 Ki-position tile, word = l1w2_word(q) (l1_wshift 0 marks it).
-constexpr uint32_t kL1WordsL2 = 28672;
-// k_scan_r's level-1 filter (SYDELTA_SCAN_L1=5): 38400 words = 150 KiB, the LDS left
-// when the tile's bytes stay in registers, word = l1r_word(q) (l1_wshift 1 marks it).
+// k_scan_r's level-1 filter (one large file at n = 4096): 38400 words = 150 KiB, the LDS
+// left when the tile's bytes stay in registers, word = l1r_word(q) (l1_wshift 1 marks it).
 constexpr uint32_t kL1WordsR = 38400;
-// words of a level-1 filter: l1_wshift 0 / 1 mark the scaled-word layouts of k_scan_l2 /
-// k_scan_r, any other value l1_parts power-of-two filters of 2^(32 - l1_wshift) words
-constexpr size_t l1_total_words(uint32_t l1_wshift, uint32_t l1_parts) {
-    return l1_wshift == 0 ? (size_t)kL1WordsL2 : l1_wshift == 1 ? (size_t)kL1WordsR
-                                                                : (size_t)l1_parts << (32 - l1_wshift);
+// words of a level-1 filter: l1_wshift 1 marks k_scan_r's scaled-word layout, any other
+// value a power-of-two filter of 2^(32 - l1_wshift) words (18: k_scan_w's)
+constexpr size_t l1_total_words(uint32_t l1_wshift) {
+    return l1_wshift == 1 ? (size_t)kL1WordsR : (size_t)1 << (32 - l1_wshift);
 }
 
 // Verified hits are written as key/value pairs: key = (segment << 32) | position
@@ -71,10 +64,9 @@ struct ScanSeg {
 // Device-resident probe table over one or more basis signatures (SoA in HBM).
 struct DeviceIndex {
     uint32_t* filt = nullptr;   // blocked Bloom filters (probe_hash/filt_mask), per-file 2^k 32-bit words
-    uint32_t* l1 = nullptr;     // level-1 filter, single-file indexes above kLdsFilterKeys keys at bs 4096
-    uint32_t l1_parts = 0;      // key partitions: l1 holds l1_parts filters of 2^(32 - l1_wshift) words
-    uint32_t l1_wshift = 17;    // level-1 word of probe hash q: q >> l1_wshift (17: kL1Words, 18: kL1WordsWide;
-                                // 0: kL1WordsL2 words, l1w2_word)
+    uint32_t* l1 = nullptr;     // level-1 filter: single-file indexes above kLdsFilterKeys keys at bs 4096
+                                // (k_scan_r) or with windows above scan_max_window() (k_scan_w)
+    uint32_t l1_wshift = 1;     // 1: kL1WordsR words, l1r_word(q); 18: kL1WordsWide words, q >> 18
     uint4* fat = nullptr;       // with l1: per slot {key, first candidate | multi, its strong} (k_idx_fat)
     uint32_t* keys = nullptr;   // 4-key buckets of unique weak values, kEmptyKey = free
     uint32_t* cnt = nullptr;    // candidates per slot
@@ -116,10 +108,6 @@ hipError_t launch_signature_batch(const uint8_t* d_buf, const uint64_t* d_off, c
 hipError_t launch_index_build(const uint32_t* d_weak, const uint64_t* d_strong, DeviceIndex& ix, hipStream_t s,
                               Profiler* prof);
 uint64_t scan_tile_positions();  // positions per tile of the LDS-staged scan
-// SYDELTA_SCAN_L1: 0 k_scan_lds, 1 k_scan_l1, 2 k_scan_l1 over two key partitions,
-// 3 k_scan_s, 4 (default) k_scan_l2 (read per call; the index's level-1 layout is
-// chosen when it is built)
-int scan_l1_mode();
 // SYDELTA_SCAN_WIDE=0: windows above scan_max_window() take the per-thread k_scan
 // instead of the LDS-staged k_scan_w (read when the index is built and per call)
 int scan_wide_mode();

@@ -346,30 +346,16 @@ __device__ __forceinline__ uint32_t filt_bit(uint32_t word, uint32_t q) {
     return __builtin_amdgcn_ubfe(word, q, 1) & __builtin_amdgcn_ubfe(word, q >> 5, 1) &
            __builtin_amdgcn_ubfe(word, q >> 10, 1);
 }
-// Level-1 filter of a large single-file index (2^20 bits, one per key: 63 % false
-// passes at 1 Mi keys), held in LDS by k_scan_l1 so that only the positions it passes
-// cost a level-2 request to L2 (sydelta_internal.hpp): word = q[17..31], bit = q[0..4]
-// (one bit extract; the level-2 word tests q[0..4] too, but in an unrelated word).
-static_assert(kL1Words == 32768, "l1_word takes the top 15 bits of q");
-__device__ __forceinline__ uint32_t l1_word(uint32_t q) { return q >> 17; }
+// Level-1 filters (held in LDS by k_scan_r / k_scan_w so that only the positions they
+// pass cost a level-2 request to L2): one bit per key, bit = q[0..4] (one bit extract;
+// the level-2 word tests q[0..4] too, but in an unrelated word).
 __device__ __forceinline__ uint32_t l1_test(uint32_t word, uint32_t q) { return __builtin_amdgcn_ubfe(word, q, 1); }
-// k_scan_l2's level-1 word (kL1WordsL2 words, not a power of two): floor(q * words / 2^32)
+// k_scan_r's level-1 word (kL1WordsR words, not a power of two): floor(q * words / 2^32)
 // from the top 24 bits of q, one shift and one v_mul_hi_u32_u24
-__host__ __device__ __forceinline__ uint32_t l1w2_word(uint32_t q) {
-    return (uint32_t)(((uint64_t)(q >> 8) * (kL1WordsL2 << 8)) >> 32);
-}
-// k_scan_r's level-1 word (kL1WordsR words), the same scaling
 static_assert((kL1WordsR << 8) < (1u << 24), "l1r_word's constant is a 24-bit operand");
 __host__ __device__ __forceinline__ uint32_t l1r_word(uint32_t q) {
     return (uint32_t)(((uint64_t)(q >> 8) * (kL1WordsR << 8)) >> 32);
 }
-// Key partitions (SYDELTA_SCAN_L1=2): key w belongs to partition r & 1 (r's low bits
-// take no part in the level-2 word, r >> fwshift, fwshift >= 4), and partition p's keys
-// alone set the bits of level-1 filter p, so each filter holds half the keys at two bits
-// per key.  A scan pass over partition p tests only the positions whose value falls in
-// p: every position is still rolled in every pass, but the level-1 pass rate -- the L2
-// request rate -- drops from 1 - e^(-k/2^20) to 1 - e^(-k/2^21) (0.63 -> 0.39 at 1 Mi keys).
-__device__ __forceinline__ uint32_t l1_part(uint32_t r, uint32_t pmask) { return r & pmask; }
 __device__ __forceinline__ uint32_t bucket_hash(uint32_t w) {
     uint32_t h = w ^ (w >> 15);
     h *= 0x2C1B3C6Du;
@@ -389,7 +375,7 @@ __device__ __forceinline__ uint32_t file_of_block(const uint64_t* __restrict__ f
 
 __global__ void k_idx_insert(const uint32_t* __restrict__ weak, uint64_t n, const uint64_t* __restrict__ fblk,
                              uint32_t nf, const FileIx* __restrict__ files, uint32_t* __restrict__ filt,
-                             uint32_t* __restrict__ l1, uint32_t l1_parts, uint32_t l1_wshift, uint32_t* __restrict__ keys,
+                             uint32_t* __restrict__ l1, uint32_t l1_wshift, uint32_t* __restrict__ keys,
                              uint32_t* __restrict__ cnt, uint32_t* __restrict__ slot_of) {
     const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
@@ -397,10 +383,8 @@ __global__ void k_idx_insert(const uint32_t* __restrict__ weak, uint64_t n, cons
     const uint32_t w = weak[i];
     const ProbeHash h = probe_hash(w);
     atomicOr(filt + F.filt_off + (h.r >> F.fwshift), filt_mask(h.q));
-    if (l1)  // single-file index only (l1_test); l1_parts filters of 2^(32 - l1_wshift) words each
-        atomicOr(l1 + (l1_wshift > 1 ? ((size_t)l1_part(h.r, l1_parts - 1) << (32 - l1_wshift)) + (h.q >> l1_wshift)
-                       : l1_wshift == 1 ? (size_t)l1r_word(h.q) : (size_t)l1w2_word(h.q)),
-                 1u << (h.q & 31));
+    if (l1)  // single-file index only (l1_test)
+        atomicOr(l1 + (l1_wshift == 1 ? (size_t)l1r_word(h.q) : (size_t)(h.q >> l1_wshift)), 1u << (h.q & 31));
     uint32_t b = bucket_hash(w) & F.bmask;
     for (;;) {
         for (uint32_t j = 0; j < 4; ++j) {
@@ -630,7 +614,7 @@ struct ScanArgs {
     uint32_t nchunks;    // LDS chunk slots per tile (k_scan)
     // probe structures (concatenated over files)
     const uint32_t* filt;
-    const uint32_t* l1;       // k_scan_l1: level-1 filter (kL1Words)
+    const uint32_t* l1;       // level-1 filter (k_scan_r: kL1WordsR words, k_scan_w: kL1WordsWide)
     const uint4* fat;         // k_scan_l1: {key, first candidate | kMulti+slot, strong} per slot
     const uint32_t* keys;
     const uint32_t* start;
@@ -645,11 +629,8 @@ struct ScanArgs {
     uint2* gfq;          // k_scan_lds: per-wave filter-pass queues in HBM/L2, kGFQ entries each
     struct WDef* wdef;   // k_scan_w: weak hits whose verification k_verify_w does (count: counters[10])
     uint64_t wdef_cap;
-    // k_scan_r: each wave's level-2 passes {position in run, weak} (rcap per wave) and,
-    // per pair of host tiles, {wave, first record, records of sub-run 0, of sub-run 1}
+    // k_scan_r: each wave's level-2 passes of one wave tile {position in run, weak}
     uint2* rrec;
-    uint32_t rcap;
-    uint4* rrun;
 };
 
 // A weak hit of k_scan_w, verified after the scan by k_verify_w.
@@ -1532,55 +1513,23 @@ __global__ __launch_bounds__(kT2, kWgPerCu) void k_scan_lds(ScanArgs a, uint32_t
 }
 
 // ===========================================================================
-// K2+K4 for a large single-file index: k_scan_l1 (window n <= kMaxN3)
+// Shared by the level-1-filter scans (k_scan_r, k_scan_w)
 // ===========================================================================
 // The BASELINE C3 shape: 2^32 window starts against 2^20 basis keys, every one a
 // literal.  Each position must test its weak value against the key set.  With the
 // level-2 filter (2 MiB, 16 bits per key) in L2 that is one random L2 request per
 // position, and the chip serves ~265 G of those per second whatever their width or
 // cache policy (profiles/r02_micro_gather2.txt): >= 16 ms per 4 GiB.  So each
-// workgroup (one per CU) keeps a level-1 filter of 128 KiB in LDS, and only the
-// positions it passes (63 % at 1 Mi keys) cost an L2 request.  Eight waves, two per
-// SIMD (a wave alone on its SIMD issues VALU at half rate), 32 positions per thread,
-// the tile of k_scan_lds.  Per tile:
-//   stage    the tile's bytes [T0, T0 + kTile3 + n) -> LDS rows (64 B, 17-dword
-//            stride); they were loaded into registers during the previous tile's
-//            drain, so the HBM latency hides behind it
-//   window   each wave computes its threads' first windows [T0 + 32t, +n) in closed
-//            form from 32-byte half sums with wave scans (no workgroup barrier)
-//   roll     32 positions in batches of 8 (rolling.rs:66-79, both halves kept
-//            reduced with one min3 each); per position probe_hash and the level-1
-//            bit from LDS; the level-2 words of the passes are fetched by
-//            bounds-checked buffer loads (a level-1 miss gets an out-of-range offset:
-//            no request, reads 0) one batch ahead of their test
-//   drain    level-2 passes queued per wave in LDS: one bucket read of the fat table
-//            ({key, first candidate, its strong}) per pass, then XXH3 of the weak
-//            hits from the LDS rows (generator.rs:121-155)
-constexpr int kT3 = 512;           // threads per workgroup (8 waves)
-constexpr int kR3 = 32;            // positions per thread = half a 64-byte row
-constexpr int kTile3 = kT3 * kR3;  // 16384 positions per tile
+// workgroup keeps a level-1 filter in LDS, and only the positions it passes cost an L2
+// request.  Round 2's k_scan_l1 (128 KiB level-1, tile bytes staged in LDS rows, 16.8
+// ms at C3) and round 3's k_scan_l2 (32 Ki-position tiles, 14.8 ms) and k_scan_s (a
+// stripe per thread, 28.7 ms) were superseded by k_scan_r and removed in round 4; their
+// measurements are in DESIGN.md section 6.
 constexpr int kB3 = 8;             // positions per batch
 constexpr int kFQ3 = 64;           // level-2 passes queued per wave (LDS)
 constexpr int kWQ3 = 32;           // weak hits queued per wave (LDS)
-constexpr uint32_t kMaxN3 = 4096;  // largest window whose tile fits beside the level-1 filter
+constexpr uint32_t kMaxN3 = 4096;  // k_scan_r's window: a wave tile's in rows are the next tile's out rows
 constexpr uint32_t kMulti = 0x80000000u;  // fat record: more than one candidate (info = slot)
-static_assert(kTile3 == kTile2, "k_scan_l1 and k_scan_lds share the host's tiling");
-
-struct Lds3 {
-    uint32_t nch;                         // 64-byte rows
-    uint32_t ntab, fq, wq, l1, total;     // byte offsets
-};
-__host__ __device__ constexpr Lds3 lds3_layout(uint32_t n) {
-    Lds3 L{};
-    L.nch = (kTile3 + n + 63) / 64 + 1;
-    uint32_t o = L.nch * kRowDw * 4;
-    o = (o + 15) & ~15u; L.ntab = o; o += 256 * 4;
-    L.fq = o; o += (kT3 / 64) * kFQ3 * 8;
-    L.wq = o; o += (kT3 / 64) * kWQ3 * 16;
-    L.l1 = o; o += kL1Words * 4;
-    L.total = o;
-    return L;
-}
 
 // Fat-table lookup: the bucket of w (4 records, one 64-byte line) in one round trip.
 __device__ __forceinline__ bool fat_find(const uint4* __restrict__ fat, uint32_t bmask, uint32_t w, uint4& rec) {
@@ -1773,363 +1722,6 @@ struct L1Batch {
     uint32_t w2[kB3], hq[kB3], wv[kB3];
 };
 
-// part / pmask: the key partition this pass tests (pmask 0: one partition, every position).
-// kTiming: the SYDELTA_PHASE_TIMING instantiation (phase cycles and level-1 passes
-// counted); the production one carries no timing code in its hot loop.
-template <bool kTiming, bool kParts2>
-__global__ __launch_bounds__(kT3, 2) void k_scan_l1(ScanArgs a, uint32_t per, uint32_t part) {
-    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-    const uint32_t n = a.n;
-    // n == kMaxN3 (launch_scan): every LDS offset a compile-time constant, so the level-1
-    // and n*x table reads take their base in the instruction's offset field
-    constexpr Lds3 L = lds3_layout(kMaxN3);
-    uint32_t* rows = (uint32_t*)smem;
-    uint32_t* ntab = (uint32_t*)(smem + L.ntab);
-    const uint32_t* l1 = (const uint32_t*)(smem + L.l1);
-    const uint32_t tid = threadIdx.x;
-    const uint32_t lane = tid & 63, wid = tid >> 6;
-    uint2* fq = (uint2*)(smem + L.fq) + (size_t)wid * kFQ3;
-    uint4* wq = (uint4*)(smem + L.wq) + (size_t)wid * kWQ3;
-
-    const uint32_t t_begin = blockIdx.x * per;
-    const uint32_t t_end = min(a.ntiles, t_begin + per);
-    if (t_begin >= t_end) return;
-    // level-1 filter and the n*x table, once per workgroup (published by the first
-    // tile's barrier)
-    {
-        const uint4* g = (const uint4*)(a.l1 + (size_t)part * kL1Words);
-        uint4* d = (uint4*)(smem + L.l1);
-#pragma unroll 4
-        for (uint32_t i = tid; i < kL1Words / 4; i += kT3) d[i] = g[i];
-    }
-    for (uint32_t i = tid; i < 256; i += kT3) ntab[i] = kMod - 1 - (a.nm * i) % kMod;
-    const uint32_t nch = L.nch;
-    const uint32_t sh = n & 3;
-    const uint32_t rel0 = tid * kR3;
-    const uint32_t orow = (tid >> 1) * kRowDw + 8 * (tid & 1);  // this thread's first out dword
-    const uint32_t din0 = (rel0 + n) >> 2;                      // ... and first in dword
-    const uint32_t m32 = n >> 5, rem = n & 31;                  // window = m32 halves + rem bytes
-    unsigned long long passes = 0, weak_hits = 0;
-    uint32_t nfq = 0;
-    // SYDELTA_PHASE_TIMING: wave 0's s_memtime cycles per phase (stage, window, roll,
-    // drains) into counters[4..8), level-1 passes into counters[3]
-    unsigned long long tm[6] = {0, 0, 0, 0, 0, 0}, l1pass = 0;
-    unsigned long long tprev = kTiming ? __builtin_amdgcn_s_memtime() : 0;
-#define PHASE_MARK3(k)                                                 \
-    if (kTiming) {                                                     \
-        const unsigned long long tnow = __builtin_amdgcn_s_memtime(); \
-        tm[k] += tnow - tprev;                                         \
-        tprev = tnow;                                                  \
-    }
-
-    // segment of a tile (tiles of a launch are laid out segment after segment)
-    auto seg_ctx = [&](uint32_t tile, uint32_t si0, SegCtx& sc, uint32_t& si, uint64_t& tile_start,
-                       uint64_t& seg_len) {
-        uint32_t lo = si0, hi = a.nsegs;
-        while (hi - lo > 1) {
-            const uint32_t mid = (lo + hi) >> 1;
-            if (a.segs[mid].tile_base <= tile) lo = mid; else hi = mid;
-        }
-        si = lo;
-        const ScanSeg S = a.segs[si];
-        const FileIx F = a.files[S.file];
-        sc.base = a.src + S.src;
-        sc.pos_begin = S.pos_begin;
-        sc.pos_end = S.pos_end;
-        sc.keys = a.keys + F.slot_off;
-        sc.fat = a.fat + F.slot_off;
-        sc.slot_off = F.slot_off;
-        sc.bmask = F.bmask;
-        sc.seg_id = si;
-        sc.fwshift = F.fwshift;
-        sc.filt = a.filt + F.filt_off;
-        sc.fwords = 1u << (32 - F.fwshift);
-        tile_start = S.pos_begin + (uint64_t)(tile - S.tile_base) * kTile3;
-        seg_len = S.len;
-    };
-    SegCtx sc, nsc;
-    uint32_t si = 0, nsi = 0;
-    uint64_t tile_start = 0, seg_len = 0, ntile_start = 0, nseg_len = 0;
-    seg_ctx(t_begin, 0, nsc, nsi, ntile_start, nseg_len);
-    // next tile's chunk (thread c stages 64-byte chunk c), loaded ahead
-    uint32_t x[16];
-    if (tid < nch) load_chunk_nt(nsc.base, nseg_len, ntile_start + 64ull * tid, x);
-
-#pragma unroll 1
-    for (uint32_t tile = t_begin; tile < t_end; ++tile) {
-        sc = nsc;
-        si = nsi;
-        tile_start = ntile_start;
-        seg_len = nseg_len;
-        // ---- stage: the prefetched chunk -> LDS rows (the previous tile's barrier
-        // ended every read of the rows)
-        if (tid < nch) {
-#pragma unroll
-            for (int i = 0; i < 16; ++i) rows[tid * kRowDw + i] = x[i];
-        }
-        __syncthreads();
-        // next tile's chunk, issued now: its HBM latency hides behind the window phase
-        // (which waits on no vector memory) and the first batches
-        if (tile + 1 < t_end) {
-            if (nsi + 1 < a.nsegs && a.segs[nsi + 1].tile_base <= tile + 1)
-                seg_ctx(tile + 1, nsi, nsc, nsi, ntile_start, nseg_len);  // the next segment
-            else
-                ntile_start = tile_start + kTile3;
-            if (tid < nch) load_chunk_nt(nsc.base, nseg_len, ntile_start + 64ull * tid, x);
-        }
-        PHASE_MARK3(0)
-
-        // ---- window: lane l of wave w starts at half t = 64w + l (tile offset 32t);
-        // halves t + 64j, j = 0..2, cover its window [32t, 32t + n) (m32 <= 128)
-        uint32_t am = tid, bm = lane;
-        if (!(a.ablate & 4)) {
-            uint32_t S[3], V[3], J[3], TS[3], TV[3], TJ[3];
-#pragma unroll
-            for (int j = 0; j < 3; ++j) {
-                const uint32_t h = tid + 64 * j;  // half index in the tile
-                const uint32_t* r = rows + (h >> 1) * kRowDw + 8 * (h & 1);
-                uint32_t s = 0, v = 0;
-#pragma unroll
-                for (int i = 0; i < 8; ++i) {
-                    const uint32_t d = r[i];
-                    s = udot4(d, 0x01010101u, s);
-                    v = udot4(d, offw(i), v);
-                }
-                S[j] = wave_scan_excl(s, TS[j]);
-                V[j] = wave_scan_excl(v, TV[j]);
-                J[j] = wave_scan_excl((uint32_t)(64 * j + lane) * s, TJ[j]);  // half index relative to the wave
-            }
-            // prefix at relative half y = lane + m32 (column jy = y >> 6, lane y & 63)
-            const uint32_t jA = m32 >> 6, ly = (lane + m32) & 63;
-            const bool carry = lane + (m32 & 63) >= 64;
-            auto pre = [&](const uint32_t* E, const uint32_t* T) -> uint32_t {
-                uint32_t base0 = 0, ea = 0, eb = 0, base1 = 0;
-#pragma unroll
-                for (int j = 0; j < 3; ++j) {
-                    // the common n % 2048 == 0 (m32 = 128 halves): the lane's own value
-                    const uint32_t sj = (m32 & 63) == 0 ? E[j] : (uint32_t)__shfl((int)E[j], (int)ly, 64);
-                    if ((uint32_t)j == jA) ea = sj;
-                    if ((uint32_t)j == jA + 1) eb = sj;
-                    if ((uint32_t)j < jA) base0 += T[j];
-                    if ((uint32_t)j < jA + 1) base1 += T[j];
-                }
-                return carry ? base1 + eb : base0 + ea;
-            };
-            const uint64_t dS = pre(S, TS) - S[0];
-            const uint64_t dV = pre(V, TV) - V[0];
-            const uint64_t dJ = pre(J, TJ) - J[0];
-            uint32_t A = (uint32_t)dS;
-            // B = sum_i (n - i) x_{32t+i} = n dS - 32 sum_k (k - l) S_k - dV   (< 2^31 for n <= 4096)
-            uint32_t B = (uint32_t)((uint64_t)n * dS - 32ull * (dJ - (uint64_t)lane * dS) - dV);
-            for (uint32_t r = 0; r < rem; ++r) {
-                const uint32_t b = 32 * (tid + m32) + r;
-                const uint32_t xr = (rows[(b >> 6) * kRowDw + ((b >> 2) & 15)] >> (8 * (b & 3))) & 0xFF;
-                A += xr;
-                B += (rem - r) * xr;
-            }
-            am = (1 + A) % kMod;
-            bm = (n + B) % kMod;
-        }
-        PHASE_MARK3(1)
-
-        // ---- roll.  Positions at or past pos_end (last tile of a segment) are rolled
-        // like the others and dropped by drain_l1's bound check.
-        // the descriptor must be uniform (SGPRs): a VGPR one makes every load a waterfall loop
-        const uint64_t fptr = (uint64_t)(uintptr_t)sc.filt;
-        const uint32_t fp_lo = __builtin_amdgcn_readfirstlane((uint32_t)fptr);
-        const uint32_t fp_hi = __builtin_amdgcn_readfirstlane((uint32_t)(fptr >> 32));
-        const __amdgpu_buffer_rsrc_t frsrc = __builtin_amdgcn_make_buffer_rsrc(
-            (void*)(uintptr_t)(((uint64_t)fp_hi << 32) | fp_lo), (short)0,
-            (int)__builtin_amdgcn_readfirstlane(sc.fwords * 4), 0x00020000);
-        const uint32_t fwshift = __builtin_amdgcn_readfirstlane(sc.fwshift);
-        auto compute = [&](uint32_t g, L1Batch& Bt) {
-            uint32_t xo[2], xi[2], pt[kB3];
-            xo[0] = rows[orow + (g >> 2)];
-            xo[1] = rows[orow + (g >> 2) + 1];
-            {
-                uint32_t dw[3];
-#pragma unroll
-                for (int j = 0; j < 3; ++j) {
-                    const uint32_t d = din0 + (g >> 2) + j;
-                    dw[j] = rows[(d >> 4) * kRowDw + (d & 15)];
-                }
-                xi[0] = __builtin_amdgcn_alignbyte(dw[1], dw[0], sh);
-                xi[1] = __builtin_amdgcn_alignbyte(dw[2], dw[1], sh);
-            }
-            uint32_t ct[kB3], off[kB3], w1[kB3];
-#pragma unroll
-            for (int t = 0; t < kB3; ++t) ct[t] = ntab[(xo[t >> 2] >> (8 * (t & 3))) & 0xFF];
-#pragma unroll
-            for (int t = 0; t < kB3; ++t) {
-                const uint32_t out = (xo[t >> 2] >> (8 * (t & 3))) & 0xFF;
-                const uint32_t in = (xi[t >> 2] >> (8 * (t & 3))) & 0xFF;
-                __builtin_assume(am < kMod);  // lets the 24-bit multiplies take am, bm as they are
-                __builtin_assume(bm < kMod);
-                Bt.wv[t] = (bm << 16) | am;
-                const ProbeHash h = probe_hash(am, bm);
-                Bt.hq[t] = h.q;
-                off[t] = h.r >> fwshift;
-                if (kParts2) pt[t] = l1_part(h.r, 1);
-                w1[t] = l1[l1_word(h.q)];
-                const uint32_t u = am + in + (kMod - out);  // [M-255, 2M+255)
-                am = min(u, min(u - kMod, u - 2 * kMod));
-                const uint32_t v = bm + am + ct[t];          // [0, 3M)
-                bm = min(v, min(v - kMod, v - 2 * kMod));
-            }
-#pragma unroll
-            for (int t = 0; t < kB3; ++t) {
-                // a position of another key partition is tested by that partition's pass
-                uint32_t p1 = l1_test(w1[t], Bt.hq[t]);
-                if (kParts2) p1 &= pt[t] == part ? 1u : 0u;
-                if (kTiming) l1pass += __popcll(__ballot(p1));
-                if (a.ablate & 2) p1 = 0;
-                // a level-1 miss asks for an offset past the buffer (p1 - 1 = all ones): no
-                // request, reads 0 (and filt_bit(0, q) is 0)
-                Bt.w2[t] = __builtin_amdgcn_raw_buffer_load_b32(frsrc, (int)((off[t] << 2) | (p1 - 1u)), 0, 0);
-            }
-        };
-        // Queue the level-2 passes of batch g's positions still in `todo` (per-wave LDS
-        // queue, positions in order); false when the queue could not take them all
-        // (todo then names the rest).  Never drains: the queue is drained between
-        // pipelines, so no drain code (and its registers) sits inside the hot loop.
-        auto finish = [&](uint32_t g, L1Batch& Bt, uint32_t& todo) -> bool {
-            uint32_t pbits = 0;
-#pragma unroll
-            for (int t = 0; t < kB3; ++t) pbits |= filt_bit(Bt.w2[t], Bt.hq[t]) << t;
-            // opaque: the ballots below re-derive the masks instead of holding eight
-            // compare results in SGPRs (which spilled)
-            asm volatile("" : "+v"(pbits));
-            const uint64_t below = (1ull << lane) - 1;
-            // the usual case: at most 8 passes in each lane that has one still fit
-            const uint64_t anyp = __ballot((pbits & todo) != 0);
-            if (nfq + 8u * (uint32_t)__popcll(anyp) <= (uint32_t)kFQ3) {
-                if (anyp) {
-#pragma unroll
-                    for (int t = 0; t < kB3; ++t) {
-                        if (!((todo >> t) & 1)) continue;
-                        const uint64_t mk = __ballot((pbits >> t) & 1);
-                        if (!mk) continue;
-                        if ((pbits >> t) & 1) fq[nfq + __popcll(mk & below)] = make_uint2(rel0 + g + t, Bt.wv[t]);
-                        nfq += __popcll(mk);
-                    }
-                }
-                todo = 0xFFu;
-                return true;
-            }
-            uint32_t need = 0;
-#pragma unroll
-            for (int t = 0; t < kB3; ++t)
-                if ((todo >> t) & 1) need += __popcll(__ballot((pbits >> t) & 1));
-            const bool all = nfq + need <= (uint32_t)kFQ3;
-            bool full = false;
-#pragma unroll
-            for (int t = 0; t < kB3; ++t) {
-                if (!((todo >> t) & 1) || full) continue;
-                const uint64_t mk = __ballot((pbits >> t) & 1);
-                if (!all && nfq + __popcll(mk) > (uint32_t)kFQ3) { full = true; continue; }
-                if ((pbits >> t) & 1) fq[nfq + __popcll(mk & below)] = make_uint2(rel0 + g + t, Bt.wv[t]);
-                nfq += __popcll(mk);
-                todo &= ~(1u << t);
-            }
-            if (all) todo = 0xFFu;
-            return all;
-        };
-        // Pipeline: batch g+8's level-2 loads are in flight while batch g is tested.
-        // A batch the queue cannot take stops it; the queue is drained and the roll
-        // resumes from that batch's saved state (only degenerate data gets there).
-        uint32_t stop = 4, todo = 0xFFu, ra = 0, rb = 0;
-        {
-            L1Batch b0, b1;
-            const uint32_t a0 = am, s0 = bm;
-            compute(0, b0);
-            const uint32_t a1 = am, s1 = bm;
-            compute(8, b1);
-            if (!finish(0, b0, todo)) { stop = 0; ra = a0; rb = s0; }
-            if (stop == 4) {
-                const uint32_t a2 = am, s2 = bm;
-                compute(16, b0);
-                if (!finish(8, b1, todo)) { stop = 1; ra = a1; rb = s1; }
-                if (stop == 4) {
-                    const uint32_t a3 = am, s3 = bm;
-                    compute(24, b1);
-                    if (!finish(16, b0, todo)) { stop = 2; ra = a2; rb = s2; }
-                    if (stop == 4 && !finish(24, b1, todo)) { stop = 3; ra = a3; rb = s3; }
-                }
-            }
-        }
-        while (stop < 4) {
-            passes += nfq;
-            if (!(a.ablate & 1)) drain_l1(a, fq, nfq, wq, weak_hits, rows, tile_start, sc);
-            nfq = 0;
-            uint32_t k = stop;
-            stop = 4;
-            am = ra;
-            bm = rb;
-#pragma unroll 1
-            for (; k < 4; ++k) {
-                L1Batch bt;
-                const uint32_t ak = am, sk = bm;
-                compute(8 * k, bt);
-                if (!finish(8 * k, bt, todo)) { stop = k; ra = ak; rb = sk; break; }
-            }
-        }
-        PHASE_MARK3(2)
-        PHASE_MARK3(3)
-        if (nfq) {  // the tile's weak hits are verified while its bytes are in LDS
-            passes += nfq;
-            if (!(a.ablate & 1)) drain_l1(a, fq, nfq, wq, weak_hits, rows, tile_start, sc);
-            nfq = 0;
-        }
-        PHASE_MARK3(4)
-        __syncthreads();  // rows are rewritten by the next tile
-        PHASE_MARK3(5)
-    }
-#undef PHASE_MARK3
-    if (lane == 0 && passes) atomicAdd(&a.counters[2], passes);
-    if (lane == 0 && weak_hits) atomicAdd(&a.counters[1], weak_hits);
-    if (kTiming && lane == 0) atomicAdd(&a.counters[3], l1pass);
-    if (kTiming && tid == 0)
-        for (int k = 0; k < 6; ++k) atomicAdd(&a.counters[4 + k], tm[k]);
-}
-
-// ===========================================================================
-// k_scan_l2: k_scan_l1 on tiles of 32 Ki positions (SYDELTA_SCAN_L1=4, the default)
-// ===========================================================================
-// Measured on k_scan_l1 (round 3, C3, SYDELTA_ABLATE): of its 16.8 ms, the tile drains
-// (fat-table round trip + verification) take 4.7 ms and the level-2 loads 4.9 ms, while
-// the roll itself runs in ~5.8 ms.  A drain's round trip and the barrier skew come once
-// per tile whatever its length, so here a tile is two of the host's tiles: 64 positions
-// per thread in eight batches, each thread's first window from 64-byte row sums (two
-// columns of 64 rows per wave), 36 KiB of rows.  The level-1 filter shrinks to
-// kL1WordsL2 words (112 KiB, word = the top bits of q scaled by a 24-bit multiply-high),
-// which passes 1 - e^(-keys / 917504) of the positions (0.68 at 1 Mi keys, 0.63 for
-// k_scan_l1's 128 KiB).  A pair of host tiles cut by a segment end or by the workgroup's
-// range is scanned as one tile whose second half the drain drops.
-constexpr int kR4 = 64;            // positions per thread = one 64-byte row
-constexpr int kTile4 = kT3 * kR4;  // 32768 positions per tile
-constexpr int kNB4 = kR4 / kB3;    // batches per thread per tile
-static_assert(kTile4 == 2 * kTile2, "a k_scan_l2 tile is two host tiles");
-
-struct Lds4 {
-    uint32_t nch;                        // 64-byte rows
-    uint32_t ntail;                      // rows past the first kT3 (staged 16 bytes per thread)
-    uint32_t ntab, fq, wq, l1, total;    // byte offsets
-};
-__host__ __device__ constexpr Lds4 lds4_layout(uint32_t n) {
-    Lds4 L{};
-    L.nch = (kTile4 + n + 63) / 64 + 1;
-    L.ntail = L.nch > (uint32_t)kT3 ? L.nch - kT3 : 0;
-    uint32_t o = L.nch * kRowDw * 4;
-    o = (o + 15) & ~15u; L.ntab = o; o += 256 * 4;
-    L.fq = o; o += (kT3 / 64) * kFQ3 * 8;
-    L.wq = o; o += (kT3 / 64) * kWQ3 * 16;
-    L.l1 = o; o += kL1WordsL2 * 4;
-    L.total = o;
-    return L;
-}
-static_assert(lds4_layout(kMaxN3).total <= 160 * 1024 - 256, "k_scan_l2's LDS");
-static_assert(lds4_layout(kMaxN3).l1 < 65536, "the level-1 base fits a ds_read offset");
-
 // 16 bytes at src + c0 (16-byte aligned; bytes at or beyond len read as 0).
 __device__ __forceinline__ void load16_nt(const uint8_t* src, uint64_t len, uint64_t c0, uint32_t x[4]) {
     if (c0 + 16 <= len) {
@@ -2151,317 +1743,6 @@ __device__ __forceinline__ void load16_nt(const uint8_t* src, uint64_t len, uint
     }
 }
 
-// kDepth: batches whose level-2 loads are in flight while one is tested (1 or 2)
-template <bool kTiming, int kDepth>
-__global__ __launch_bounds__(kT3, 2) void k_scan_l2(ScanArgs a, uint32_t per) {
-    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-    const uint32_t n = a.n;  // kMaxN3 (launch_scan)
-    constexpr Lds4 L = lds4_layout(kMaxN3);
-    uint32_t* rows = (uint32_t*)smem;
-    uint32_t* ntab = (uint32_t*)(smem + L.ntab);
-    const uint32_t* l1 = (const uint32_t*)(smem + L.l1);
-    const uint32_t tid = threadIdx.x;
-    const uint32_t lane = tid & 63, wid = tid >> 6;
-    uint2* fq = (uint2*)(smem + L.fq) + (size_t)wid * kFQ3;
-    uint4* wq = (uint4*)(smem + L.wq) + (size_t)wid * kWQ3;
-
-    const uint32_t t_begin = blockIdx.x * per;
-    const uint32_t t_end = min(a.ntiles, t_begin + per);
-    if (t_begin >= t_end) return;
-    {
-        const uint4* g = (const uint4*)a.l1;
-        uint4* d = (uint4*)(smem + L.l1);
-#pragma unroll 4
-        for (uint32_t i = tid; i < kL1WordsL2 / 4; i += kT3) d[i] = g[i];
-    }
-    for (uint32_t i = tid; i < 256; i += kT3) ntab[i] = kMod - 1 - (a.nm * i) % kMod;
-    constexpr uint32_t ntail4 = 4 * L.ntail;  // threads staging a 16-byte quarter of a tail row
-    const uint32_t rel0 = tid * kR4;
-    const uint32_t orow = tid * kRowDw;          // this thread's out bytes: row tid
-    const uint32_t din0 = (rel0 + n) >> 2;       // ... and its first in dword
-    const uint32_t sh = n & 3;
-    const uint32_t m64 = n >> 6;                 // window = m64 rows (n = 4096: 64)
-    unsigned long long passes = 0, weak_hits = 0;
-    uint32_t nfq = 0;
-    unsigned long long tm[6] = {0, 0, 0, 0, 0, 0}, l1pass = 0;
-    unsigned long long tprev = kTiming ? __builtin_amdgcn_s_memtime() : 0;
-#define PHASE_MARK4(k)                                                 \
-    if (kTiming) {                                                     \
-        const unsigned long long tnow = __builtin_amdgcn_s_memtime(); \
-        tm[k] += tnow - tprev;                                         \
-        tprev = tnow;                                                  \
-    }
-
-    auto seg_ctx = [&](uint32_t tile, uint32_t si0, SegCtx& sc, uint32_t& si, uint64_t& tile_start,
-                       uint64_t& seg_len) {
-        uint32_t lo = si0, hi = a.nsegs;
-        while (hi - lo > 1) {
-            const uint32_t mid = (lo + hi) >> 1;
-            if (a.segs[mid].tile_base <= tile) lo = mid; else hi = mid;
-        }
-        si = lo;
-        const ScanSeg S = a.segs[si];
-        const FileIx F = a.files[S.file];
-        sc.base = a.src + S.src;
-        sc.pos_begin = S.pos_begin;
-        sc.pos_end = S.pos_end;
-        sc.keys = a.keys + F.slot_off;
-        sc.fat = a.fat + F.slot_off;
-        sc.slot_off = F.slot_off;
-        sc.bmask = F.bmask;
-        sc.seg_id = si;
-        sc.fwshift = F.fwshift;
-        sc.filt = a.filt + F.filt_off;
-        sc.fwords = 1u << (32 - F.fwshift);
-        tile_start = S.pos_begin + (uint64_t)(tile - S.tile_base) * kTile2;
-        seg_len = S.len;
-    };
-    // host tiles this tile covers: 2 when host tile t+1 is in this workgroup's range and
-    // in the same segment as t (segment sidx)
-    auto span_of = [&](uint32_t t, uint32_t sidx) -> uint32_t {
-        if (t + 1 >= t_end) return 1;
-        if (sidx + 1 < a.nsegs && a.segs[sidx + 1].tile_base <= t + 1) return 1;
-        return 2;
-    };
-    SegCtx sc, nsc;
-    uint32_t si = 0, nsi = 0;
-    uint64_t tile_start = 0, seg_len = 0, ntile_start = 0, nseg_len = 0;
-    seg_ctx(t_begin, 0, nsc, nsi, ntile_start, nseg_len);
-    uint32_t nspan = span_of(t_begin, nsi);
-    // next tile's rows 0..kT3-1 (thread c: row c) and its tail rows (16 bytes per thread)
-    uint32_t x[16], xt[4] = {0, 0, 0, 0};
-    load_chunk_nt(nsc.base, nseg_len, ntile_start + 64ull * tid, x);
-    if (tid < ntail4) load16_nt(nsc.base, nseg_len, ntile_start + 64ull * kT3 + 16ull * tid, xt);
-
-    uint32_t tile = t_begin;
-#pragma unroll 1
-    while (tile < t_end) {
-        sc = nsc;
-        si = nsi;
-        tile_start = ntile_start;
-        seg_len = nseg_len;
-        const uint32_t span = nspan;
-        // ---- stage (the previous tile's barrier ended every read of the rows)
-#pragma unroll
-        for (int i = 0; i < 16; ++i) rows[tid * kRowDw + i] = x[i];
-        if (tid < ntail4) {
-#pragma unroll
-            for (int i = 0; i < 4; ++i) rows[(kT3 + (tid >> 2)) * kRowDw + 4 * (tid & 3) + i] = xt[i];
-        }
-        __syncthreads();
-        const uint32_t nt = tile + span;
-        if (nt < t_end) {
-            if (nsi + 1 < a.nsegs && a.segs[nsi + 1].tile_base <= nt)
-                seg_ctx(nt, nsi, nsc, nsi, ntile_start, nseg_len);
-            else
-                ntile_start = tile_start + (uint64_t)span * kTile2;
-            nspan = span_of(nt, nsi);
-            load_chunk_nt(nsc.base, nseg_len, ntile_start + 64ull * tid, x);
-            if (tid < ntail4) load16_nt(nsc.base, nseg_len, ntile_start + 64ull * kT3 + 16ull * tid, xt);
-        }
-        // positions of this tile that belong to it: [tile_start, tile_start + span * kTile2)
-        sc.pos_end = min(sc.pos_end, tile_start + (uint64_t)span * kTile2);
-        PHASE_MARK4(0)
-
-        // ---- window: lane l of wave w starts at row r = 64w + l (tile offset 64r); rows
-        // r + 64j, j = 0..1, cover its window [64r, 64r + n) (m64 = 64)
-        uint32_t am, bm;
-        {
-            uint32_t S[2], V[2], J[2], TS[2], TV[2], TJ[2];
-#pragma unroll
-            for (int j = 0; j < 2; ++j) {
-                const uint32_t* r = rows + (tid + 64 * j) * kRowDw;
-                uint32_t s = 0, v = 0;
-#pragma unroll
-                for (int i = 0; i < 16; ++i) {
-                    const uint32_t d = r[i];
-                    s = udot4(d, 0x01010101u, s);
-                    v = udot4(d, offw(i), v);
-                }
-                S[j] = wave_scan_excl(s, TS[j]);
-                V[j] = wave_scan_excl(v, TV[j]);
-                J[j] = wave_scan_excl((uint32_t)(64 * j + lane) * s, TJ[j]);  // row index relative to the wave
-            }
-            // prefix at relative row lane + m64 = lane + 64: column 1, this lane
-            const uint64_t dS = TS[0] + S[1] - S[0];
-            const uint64_t dV = TV[0] + V[1] - V[0];
-            const uint64_t dJ = TJ[0] + J[1] - J[0];
-            const uint32_t A = (uint32_t)dS;
-            // B = sum_i (n - i) x_{64r+i} = n dS - 64 sum_k (k - l) S_k - dV   (< 2^31 for n <= 4096)
-            const uint32_t B = (uint32_t)((uint64_t)n * dS - 64ull * (dJ - (uint64_t)lane * dS) - dV);
-            am = (1 + A) % kMod;
-            bm = (n + B) % kMod;
-        }
-        PHASE_MARK4(1)
-
-        // ---- roll (k_scan_l1's trimmed roll; positions past sc.pos_end are dropped by the drain)
-        const uint64_t fptr = (uint64_t)(uintptr_t)sc.filt;
-        const uint32_t fp_lo = __builtin_amdgcn_readfirstlane((uint32_t)fptr);
-        const uint32_t fp_hi = __builtin_amdgcn_readfirstlane((uint32_t)(fptr >> 32));
-        const __amdgpu_buffer_rsrc_t frsrc = __builtin_amdgcn_make_buffer_rsrc(
-            (void*)(uintptr_t)(((uint64_t)fp_hi << 32) | fp_lo), (short)0,
-            (int)__builtin_amdgcn_readfirstlane(sc.fwords * 4), 0x00020000);
-        const uint32_t fwshift = __builtin_amdgcn_readfirstlane(sc.fwshift);
-        auto compute = [&](uint32_t g, L1Batch& Bt) {
-            uint32_t xo[2], xi[2];
-            xo[0] = rows[orow + (g >> 2)];
-            xo[1] = rows[orow + (g >> 2) + 1];
-            {
-                uint32_t dw[3];
-#pragma unroll
-                for (int j = 0; j < 3; ++j) {
-                    const uint32_t d = din0 + (g >> 2) + j;
-                    dw[j] = rows[(d >> 4) * kRowDw + (d & 15)];
-                }
-                xi[0] = __builtin_amdgcn_alignbyte(dw[1], dw[0], sh);
-                xi[1] = __builtin_amdgcn_alignbyte(dw[2], dw[1], sh);
-            }
-            uint32_t ct[kB3], off[kB3], w1[kB3];
-#pragma unroll
-            for (int t = 0; t < kB3; ++t) ct[t] = ntab[(xo[t >> 2] >> (8 * (t & 3))) & 0xFF];
-#pragma unroll
-            for (int t = 0; t < kB3; ++t) {
-                const uint32_t out = (xo[t >> 2] >> (8 * (t & 3))) & 0xFF;
-                const uint32_t in = (xi[t >> 2] >> (8 * (t & 3))) & 0xFF;
-                __builtin_assume(am < kMod);
-                __builtin_assume(bm < kMod);
-                Bt.wv[t] = (bm << 16) | am;
-                const ProbeHash h = probe_hash(am, bm);
-                Bt.hq[t] = h.q;
-                off[t] = h.r >> fwshift;
-                w1[t] = l1[l1w2_word(h.q)];
-                const uint32_t u = am + in + (kMod - out);  // [M-255, 2M+255)
-                am = min(u, min(u - kMod, u - 2 * kMod));
-                const uint32_t v = bm + am + ct[t];          // [0, 3M)
-                bm = min(v, min(v - kMod, v - 2 * kMod));
-            }
-#pragma unroll
-            for (int t = 0; t < kB3; ++t) {
-                uint32_t p1 = l1_test(w1[t], Bt.hq[t]);
-                if (kTiming && (a.ablate & 2)) p1 = 0;
-                if (kTiming) l1pass += __popcll(__ballot(p1));
-                // a level-1 miss asks for an offset past the buffer: no request, reads 0
-                // (taking the lane out of the load with the exec mask instead measured the
-                // same: 15.00 vs 14.85 ms, TA busy 1.89e9 vs 1.93e9; the address path is
-                // not the bound)
-                Bt.w2[t] = __builtin_amdgcn_raw_buffer_load_b32(frsrc, (int)((off[t] << 2) | (p1 - 1u)), 0, 0);
-            }
-        };
-        auto finish = [&](uint32_t g, L1Batch& Bt, uint32_t& todo) -> bool {
-            uint32_t pbits = 0;
-#pragma unroll
-            for (int t = 0; t < kB3; ++t) pbits |= filt_bit(Bt.w2[t], Bt.hq[t]) << t;
-            asm volatile("" : "+v"(pbits));
-            const uint64_t below = (1ull << lane) - 1;
-            const uint64_t anyp = __ballot((pbits & todo) != 0);
-            if (nfq + 8u * (uint32_t)__popcll(anyp) <= (uint32_t)kFQ3) {
-                if (anyp) {
-#pragma unroll
-                    for (int t = 0; t < kB3; ++t) {
-                        if (!((todo >> t) & 1)) continue;
-                        const uint64_t mk = __ballot((pbits >> t) & 1);
-                        if (!mk) continue;
-                        if ((pbits >> t) & 1) fq[nfq + __popcll(mk & below)] = make_uint2(rel0 + g + t, Bt.wv[t]);
-                        nfq += __popcll(mk);
-                    }
-                }
-                todo = 0xFFu;
-                return true;
-            }
-            uint32_t need = 0;
-#pragma unroll
-            for (int t = 0; t < kB3; ++t)
-                if ((todo >> t) & 1) need += __popcll(__ballot((pbits >> t) & 1));
-            const bool all = nfq + need <= (uint32_t)kFQ3;
-            bool full = false;
-#pragma unroll
-            for (int t = 0; t < kB3; ++t) {
-                if (!((todo >> t) & 1) || full) continue;
-                const uint64_t mk = __ballot((pbits >> t) & 1);
-                if (!all && nfq + __popcll(mk) > (uint32_t)kFQ3) { full = true; continue; }
-                if ((pbits >> t) & 1) fq[nfq + __popcll(mk & below)] = make_uint2(rel0 + g + t, Bt.wv[t]);
-                nfq += __popcll(mk);
-                todo &= ~(1u << t);
-            }
-            if (all) todo = 0xFFu;
-            return all;
-        };
-        // Pipeline over the thread's 8 batches: batch k+1's level-2 loads are in flight
-        // while batch k is tested; a batch the queue cannot take stops it, the queue is
-        // drained and the roll resumes from that batch's saved state.
-        uint32_t stop = kNB4, todo = 0xFFu, ra = 0, rb = 0;
-        if (kDepth == 1) {
-            L1Batch b0, b1;
-            uint32_t sa0 = am, sb0 = bm;
-            compute(0, b0);
-            uint32_t sa1 = am, sb1 = bm;
-            compute(kB3, b1);
-#pragma unroll 1
-            for (uint32_t k = 0; k < (uint32_t)kNB4; k += 2) {
-                if (!finish(kB3 * k, b0, todo)) { stop = k; ra = sa0; rb = sb0; break; }
-                if (k + 2 < (uint32_t)kNB4) { sa0 = am; sb0 = bm; compute(kB3 * (k + 2), b0); }
-                if (!finish(kB3 * (k + 1), b1, todo)) { stop = k + 1; ra = sa1; rb = sb1; break; }
-                if (k + 3 < (uint32_t)kNB4) { sa1 = am; sb1 = bm; compute(kB3 * (k + 3), b1); }
-            }
-        } else {
-            // three batch buffers in fixed roles (batch k in b[k % 3]): batches k+1 and k+2
-            // in flight while k is tested; a rolled loop of three, so finish is inlined
-            // three times and no buffer is moved (a move would wait for its loads)
-            L1Batch b0, b1, b2;
-            uint32_t sa0 = am, sb0 = bm;
-            compute(0, b0);
-            uint32_t sa1 = am, sb1 = bm;
-            compute(kB3, b1);
-            uint32_t sa2 = am, sb2 = bm;
-            compute(2 * kB3, b2);
-#pragma unroll 1
-            for (uint32_t k = 0; k < (uint32_t)kNB4; k += 3) {
-                if (!finish(kB3 * k, b0, todo)) { stop = k; ra = sa0; rb = sb0; break; }
-                if (k + 3 < (uint32_t)kNB4) { sa0 = am; sb0 = bm; compute(kB3 * (k + 3), b0); }
-                if (k + 1 >= (uint32_t)kNB4) break;
-                if (!finish(kB3 * (k + 1), b1, todo)) { stop = k + 1; ra = sa1; rb = sb1; break; }
-                if (k + 4 < (uint32_t)kNB4) { sa1 = am; sb1 = bm; compute(kB3 * (k + 4), b1); }
-                if (k + 2 >= (uint32_t)kNB4) break;
-                if (!finish(kB3 * (k + 2), b2, todo)) { stop = k + 2; ra = sa2; rb = sb2; break; }
-                if (k + 5 < (uint32_t)kNB4) { sa2 = am; sb2 = bm; compute(kB3 * (k + 5), b2); }
-            }
-        }
-        while (stop < (uint32_t)kNB4) {
-            passes += nfq;
-            if (!(kTiming && (a.ablate & 1))) drain_l1(a, fq, nfq, wq, weak_hits, rows, tile_start, sc);
-            nfq = 0;
-            uint32_t k = stop;
-            stop = kNB4;
-            am = ra;
-            bm = rb;
-#pragma unroll 1
-            for (; k < (uint32_t)kNB4; ++k) {
-                L1Batch bt;
-                const uint32_t ak = am, sk = bm;
-                compute(kB3 * k, bt);
-                if (!finish(kB3 * k, bt, todo)) { stop = k; ra = ak; rb = sk; break; }
-            }
-        }
-        PHASE_MARK4(2)
-        PHASE_MARK4(3)
-        if (nfq) {
-            passes += nfq;
-            if (!(kTiming && (a.ablate & 1))) drain_l1(a, fq, nfq, wq, weak_hits, rows, tile_start, sc);
-            nfq = 0;
-        }
-        PHASE_MARK4(4)
-        __syncthreads();  // rows are rewritten by the next tile
-        PHASE_MARK4(5)
-        tile += span;
-    }
-#undef PHASE_MARK4
-    if (lane == 0 && passes) atomicAdd(&a.counters[2], passes);
-    if (lane == 0 && weak_hits) atomicAdd(&a.counters[1], weak_hits);
-    if (kTiming && lane == 0) atomicAdd(&a.counters[3], l1pass);
-    if (kTiming && tid == 0)
-        for (int k = 0; k < 6; ++k) atomicAdd(&a.counters[4 + k], tm[k]);
-}
-
 // ===========================================================================
 // k_scan_r: the tile's bytes in registers, no workgroup barriers (SYDELTA_SCAN_L1=5)
 // ===========================================================================
@@ -2479,141 +1760,31 @@ __global__ __launch_bounds__(kT3, 2) void k_scan_l2(ScanArgs a, uint32_t per) {
 // (k_scan_l2's closed form).  Waves never wait for each other: runs of two host tiles
 // are handed out by an LDS counter.  The LDS holds the level-1 filter (150 KiB, passing
 // 1 - e^(-keys/1228800) of the positions: 0.57 at 1 Mi keys) and ntab.
-// The level-2 passes are not looked up here: each wave appends them to its own region
-// of HBM (no atomics) and records, per pair of host tiles, where they are; k_verify_r
-// then does the fat-table lookups and verifies the weak hits from the run's bytes staged
-// in its LDS.  Measured first with the drains inline (fat lookups and XXH3 of each weak
-// hit's window from global memory, four per wave): 14.43 ms at C3, of which 3.77 ms
-// verification and 0.93 ms lookups, 9.75 ms without both (r03r).  A wave whose region
-// cannot take another wave tile drains that tile inline instead (dense data).
+// Each wave appends its level-2 passes of a wave tile to its own region of HBM (no
+// atomics) and, at the tile's end, looks them up (keys-only bucket reads) and verifies
+// the weak hits from its registers (wave_strong_regs).  Round 3 measured the other forms
+// (DESIGN.md section 6.4): the drains inline from global memory 14.43 ms at C3, the
+// records verified by a second kernel from LDS-staged rows 9.88 + 2.81 ms, from the
+// registers 11.17 ms.
 constexpr int kTR = 512;          // threads per workgroup (8 waves)
 constexpr int kWTR = 4096;        // positions per wave tile (64 per lane)
 constexpr int kNBR = 64 / kB3;    // batches per lane per wave tile
-constexpr uint32_t kRCapR = 24576;  // level-2 pass records per wave (>= 2 wave tiles)
-static_assert(kRCapR >= 2 * kWTR, "a wave's region holds the tile it may drain inline");
 static_assert(kMaxN3 == 4096 && kWTR % kMaxN3 == 0, "k_scan_r: a lane's in row is row l of the next wave tile");
 
 struct LdsR {
-    uint32_t l1, ntab, wq, kt, ctr, total;  // byte offsets
+    uint32_t l1, ntab, kt, ctr, total;  // byte offsets
 };
 __host__ __device__ constexpr LdsR ldsr_layout() {
     LdsR L{};
     uint32_t o = 0;
     L.l1 = o; o += kL1WordsR * 4;
     L.ntab = o; o += 256 * 4;
-    L.wq = o; o += (kTR / 64) * kWQ3 * 16;
     L.kt = o; o += 48 * 8;  // wave_strong_regs' key table (kKtWords)
     L.ctr = o; o += 16;
     L.total = o;
     return L;
 }
 static_assert(ldsr_layout().total <= 160 * 1024 - 256, "k_scan_r's LDS");
-
-// Verify this wave's weak hits wq[0..nwq) = {position in run, first candidate |
-// kMulti+slot, strong lo, hi}: XXH3 of each window from global memory, four per wave (one
-// per 16-lane row, row_hash), then the first candidate in index order with equal strong
-// (generator.rs:127-133); verified hits to the output (as verify_l1).
-__device__ __forceinline__ void verify_r(const ScanArgs& a, uint4* wq, uint32_t nwq, uint64_t run_start,
-                                         const SegCtx& cur) {
-    if (!nwq) return;
-    lds_fence();
-    const uint32_t lane = threadIdx.x & 63, row = lane >> 4, rl = lane & 15;
-    for (uint32_t t = 0; t < nwq; t += 4) {
-        const uint32_t h = t + row;
-        const bool live = h < nwq;
-        const uint4 e = wq[live ? h : t];
-        uint32_t s0 = 0, cn = 0;
-        if (e.y & kMulti) { s0 = a.start[e.y & ~kMulti]; cn = a.cnt[e.y & ~kMulti]; }  // in flight while hashing
-        uint32_t wk;
-        uint64_t st;
-        row_hash<false>(cur.base + run_start + e.x, a.n, wk, st);  // valid in the row's first lane
-        st = ((uint64_t)(uint32_t)__shfl((int)(uint32_t)(st >> 32), (int)(lane & 48)) << 32) |
-             (uint32_t)__shfl((int)(uint32_t)st, (int)(lane & 48));
-        uint32_t best = kNoBlock;
-        if (!(e.y & kMulti)) {
-            if (st == (((uint64_t)e.w << 32) | e.z)) best = e.y;
-        } else {
-            for (uint32_t b = 0; b < cn; b += 16) {  // in index order, 16 candidates per step
-                const uint32_t j = b + rl;
-                const uint64_t m = (__ballot(j < cn && a.cstrong[s0 + j] == st) >> (row << 4)) & 0xFFFFull;
-                if (m) {
-                    best = a.order[s0 + b + (uint32_t)__builtin_ctzll(m)];
-                    break;
-                }
-            }
-        }
-        if (live && rl == 0) wq[h].y = best;
-    }
-    lds_fence();
-    uint32_t nver = 0;
-    for (uint32_t base = 0; base < nwq; base += 64) {
-        const bool v = base + lane < nwq && wq[base + lane].y != kNoBlock;
-        nver += __popcll(__ballot(v));
-    }
-    if (!nver) return;
-    unsigned long long k0 = 0;
-    if (lane == 0) k0 = atomicAdd(&a.counters[0], (unsigned long long)nver);
-    k0 = shfl64(k0, 0);
-    for (uint32_t base = 0; base < nwq; base += 64) {
-        const uint32_t i = base + lane;
-        const uint4 e = i < nwq ? wq[i] : make_uint4(0, kNoBlock, 0, 0);
-        const bool v = e.y != kNoBlock;
-        const uint64_t m = __ballot(v);
-        const unsigned long long k = k0 + __popcll(m & ((1ull << lane) - 1));
-        if (v && k < a.out_cap) {
-            a.hit_key[k] = ((uint64_t)cur.seg_id << kSegShift) | (uint64_t)(run_start + e.x - cur.pos_begin);
-            a.hit_val[k] = e.y;
-        }
-        k0 += __popcll(m);
-    }
-}
-
-// Inline drain of one wave tile's level-2 pass records (the wave's region is full):
-// fat-table lookups, 64 per round; positions at or past the run's end are dropped; weak
-// hits to wq, verified when wq cannot take another round and at the end (drain_l1's
-// logic), windows from global memory.
-__device__ __forceinline__ void drain_r(const ScanArgs& a, const uint2* recs, uint32_t nfq, uint4* wq,
-                                        unsigned long long& weak_hits, uint64_t run_start, const SegCtx& cur) {
-    const uint32_t lane = threadIdx.x & 63;
-    __threadfence_block();  // this wave's record stores before its loads
-    uint32_t nwq = 0;
-    for (uint32_t base = 0; base < nfq; base += 64) {
-        const uint32_t i = base + lane;
-        bool hit = false;
-        uint4 rec = make_uint4(0, 0, 0, 0);
-        uint32_t tp = 0;
-        if (i < nfq) {
-            const volatile uint2* g = recs + i;  // rewritten by later tiles: not from a stale L1 line
-            uint2 e;
-            e.x = g->x;
-            e.y = g->y;
-            tp = e.x;
-            if (run_start + e.x < cur.pos_end && !(a.ablate & 16)) hit = fat_find(cur.fat, cur.bmask, e.y, rec);
-        }
-        const uint64_t m = __ballot(hit);
-        if (!m) continue;
-        const uint32_t cnt = __popcll(m);
-        weak_hits += cnt;
-        if (a.ablate & 8) continue;
-        if (nwq + cnt > (uint32_t)kWQ3) {
-            verify_r(a, wq, nwq, run_start, cur);
-            nwq = 0;
-        }
-        const uint32_t rank = __popcll(m & ((1ull << lane) - 1));
-        const uint4 e = make_uint4(tp, rec.y, rec.z, rec.w);
-        if (cnt > (uint32_t)kWQ3) {  // a round of more hits than wq holds (dense data): two halves
-            if (hit && rank < (uint32_t)kWQ3) wq[rank] = e;
-            verify_r(a, wq, kWQ3, run_start, cur);
-            if (hit && rank >= (uint32_t)kWQ3) wq[rank - kWQ3] = e;
-            nwq = cnt - kWQ3;
-        } else {
-            if (hit) wq[nwq + rank] = e;
-            nwq += cnt;
-        }
-    }
-    verify_r(a, wq, nwq, run_start, cur);
-    lds_fence();
-}
 
 // ---------------------------------------------------------------------------
 // XXH3-64 of a 4096-byte window held in a wave's registers (k_scan_r, inline verification)
@@ -2774,10 +1945,10 @@ __device__ __forceinline__ void drain_regs(const ScanArgs& a, const uint2* recs,
 }
 
 // kAblate: the SYDELTA_ABLATE instantiation (measurement only): bit 0 skips the drains,
-// bit 1 the level-2 loads; drain bits 3 (verification) and 4 (fat lookups) as drain_l1
-// kInline (SYDELTA_SCAN_R_INLINE=1): each wave tile's passes are looked up and verified at
-// the tile's end (drain_regs: the windows hashed from the registers), no k_verify_r.
-template <bool kAblate, bool kInline>
+// bit 1 the level-2 loads; drain bits 3 (verification) and 4 (fat lookups) as drain_l1.
+// Each wave tile's passes are looked up and verified at the tile's end (drain_regs: the
+// windows hashed from the registers).
+template <bool kAblate>
 __global__ __launch_bounds__(kTR, 2) void k_scan_r(ScanArgs a, uint32_t per) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     constexpr LdsR L = ldsr_layout();
@@ -2786,10 +1957,9 @@ __global__ __launch_bounds__(kTR, 2) void k_scan_r(ScanArgs a, uint32_t per) {
     uint32_t* ntab = (uint32_t*)(smem + L.ntab);
     const uint32_t tid = threadIdx.x;
     const uint32_t lane = tid & 63, wid = tid >> 6;
-    uint4* wq = (uint4*)(smem + L.wq) + (size_t)wid * kWQ3;
     uint32_t* ctr = (uint32_t*)(smem + L.ctr);
     const uint32_t gwave = blockIdx.x * (kTR / 64) + wid;
-    uint2* rec = a.rrec + (size_t)gwave * a.rcap;  // this wave's pass records
+    uint2* rec = a.rrec + (size_t)gwave * kWTR;  // this wave's pass records (one wave tile)
 
     const uint32_t t_begin = blockIdx.x * per;
     const uint32_t t_end = min(a.ntiles, t_begin + per);
@@ -2802,7 +1972,7 @@ __global__ __launch_bounds__(kTR, 2) void k_scan_r(ScanArgs a, uint32_t per) {
     }
     for (uint32_t i = tid; i < 256; i += kTR) ntab[i] = kMod - 1 - (a.nm * i) % kMod;
     uint64_t* kt = (uint64_t*)(smem + L.kt);
-    if (kInline && tid < 48)
+    if (tid < 48)
         kt[tid] = tid < 24 ? c_tab.w[tid] : tid < 32 ? c_tab.last[tid - 24] : tid < 40 ? c_tab.init[tid - 32]
                                                                                        : c_tab.merge[tid - 40];
     if (tid == 0) *ctr = 0;
@@ -2819,11 +1989,8 @@ __global__ __launch_bounds__(kTR, 2) void k_scan_r(ScanArgs a, uint32_t per) {
         const uint32_t t0 = t_begin + 2 * c;
         if (t0 >= t_end) break;
         const uint32_t tz = min(t_end, t0 + 2);
-        const uint32_t rec0 = nrec;  // the pair's records start here
-        uint32_t cnt[2] = {0, 0}, nsr = 0;
 #pragma unroll 1
         for (uint32_t t = t0; t < tz;) {
-            const uint32_t run_rec = nrec;
             // the run: host tiles t (and t+1 when in the same segment)
             uint32_t lo = si_hint, hi = a.nsegs;
             while (hi - lo > 1) {
@@ -2953,173 +2120,19 @@ __global__ __launch_bounds__(kTR, 2) void k_scan_r(ScanArgs a, uint32_t per) {
                         load_chunk(sc.base, seg_len, P + n + kWTR + 64ull * lane, xn);
                 }
                 passes += nrec - tile_rec;
-                if (kInline) {
-                    if (nrec > tile_rec && !(kAblate && (a.ablate & 1)))
-                        drain_regs(a, rec + tile_rec, nrec - tile_rec, k * kWTR, xo, xi, kt, weak_hits, run_start, sc);
-                    nrec = tile_rec;
-                }
-                // the region must hold the next tile's records (up to kWTR): when it might
-                // not, this tile's records are looked up and verified here instead
-                if (!kInline && nrec > a.rcap - kWTR) {
-                    if (!(kAblate && (a.ablate & 1)))
-                        drain_r(a, rec + tile_rec, nrec - tile_rec, wq, weak_hits, run_start, sc);
-                    nrec = tile_rec;
-                }
-                if (kAblate && (a.ablate & 1)) nrec = tile_rec;
+                if (nrec > tile_rec && !(kAblate && (a.ablate & 1)))
+                    drain_regs(a, rec + tile_rec, nrec - tile_rec, k * kWTR, xo, xi, kt, weak_hits, run_start, sc);
+                nrec = tile_rec;
 #pragma unroll
                 for (int i = 0; i < 16; ++i) {
                     xo[i] = xi[i];
                     xi[i] = xn[i];
                 }
             }
-            cnt[nsr++] = nrec - run_rec;  // the second run of a pair split by a segment end
         }
-        if (!kInline && lane == 0) a.rrun[t0 >> 1] = make_uint4(gwave, rec0, cnt[0], cnt[1]);
     }
     if (lane == 0 && passes) atomicAdd(&a.counters[2], passes);
     if (lane == 0 && weak_hits) atomicAdd(&a.counters[1], weak_hits);
-}
-
-// k_verify_r: the level-2 passes k_scan_r recorded for one pair of host tiles (one
-// workgroup per pair): fat-table lookups, kTVR per round, then XXH3 of each weak hit's
-// window from the run's bytes staged in LDS (k_scan_l2's 17-dword rows, four windows per
-// wave, row_strong_lds), the first candidate in index order with equal strong
-// (generator.rs:127-133), verified hits to the output.  43 KiB of LDS: three workgroups
-// per CU, so one workgroup's lookups and staging overlap another's hashing.
-// (Measured and rejected: one workgroup per host tile with half the rows, six per CU:
-// 3.48 ms against 2.81 at C3, the pair's records read twice.)
-constexpr int kTVR = 256;
-struct LdsVR {
-    uint32_t nch, rows, hits, cnt, total;  // rows; byte offsets
-};
-__host__ __device__ constexpr LdsVR ldsvr_layout() {
-    LdsVR L{};
-    L.nch = (kTile4 + kMaxN3 + 63) / 64 + 1;
-    uint32_t o = 0;
-    L.rows = o; o += L.nch * kRowDw * 4;
-    o = (o + 15) & ~15u;
-    L.hits = o; o += kTVR * 16;
-    L.cnt = o; o += 16;
-    L.total = o;
-    return L;
-}
-
-__global__ __launch_bounds__(kTVR) void k_verify_r(ScanArgs a) {
-    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-    constexpr LdsVR L = ldsvr_layout();
-    uint32_t* rows = (uint32_t*)(smem + L.rows);
-    uint4* hits = (uint4*)(smem + L.hits);
-    uint32_t* hcnt = (uint32_t*)(smem + L.cnt);
-    const uint32_t tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
-    const uint32_t row = lane >> 4, rl = lane & 15;
-    const uint32_t g = blockIdx.x;
-    const uint4 R = a.rrun[g];
-    if (R.z + R.w == 0) return;
-    const uint2* recs = a.rrec + (size_t)R.x * a.rcap + R.y;
-    const uint32_t t0 = 2 * g, tz = min(a.ntiles, t0 + 2);
-    RowKeys K;
-    row_keys(K);
-    unsigned long long weak = 0;
-    uint32_t si = 0, roff = 0, sr = 0;
-#pragma unroll 1
-    for (uint32_t t = t0; t < tz; ++sr) {
-        uint32_t lo = si, hi = a.nsegs;
-        while (hi - lo > 1) {
-            const uint32_t mid = (lo + hi) >> 1;
-            if (a.segs[mid].tile_base <= t) lo = mid; else hi = mid;
-        }
-        si = lo;
-        const ScanSeg S = a.segs[si];
-        const FileIx F = a.files[S.file];
-        const uint8_t* base = a.src + S.src;
-        const uint4* fat = a.fat + F.slot_off;
-        const uint32_t* fkeys = a.keys + F.slot_off;
-        const uint32_t span = (t + 1 < tz && !(si + 1 < a.nsegs && a.segs[si + 1].tile_base <= t + 1)) ? 2u : 1u;
-        const uint64_t run_start = S.pos_begin + (uint64_t)(t - S.tile_base) * kTile2;
-        const uint64_t pos_end = min(S.pos_end, run_start + (uint64_t)span * kTile2);
-        t += span;
-        const uint32_t cnt = sr == 0 ? R.z : R.w;
-        const uint2* rr = recs + roff;
-        roff += cnt;
-        if (!cnt) continue;
-        // the run's bytes [run_start, + span * kTile2 + n) into the rows (past the
-        // segment's end: zeros)
-        const uint32_t nch = (span * kTile2 + a.n + 63) / 64 + 1;
-#pragma unroll 1
-        for (uint32_t r = tid; r < nch; r += kTVR) {
-            uint32_t x[16];
-            if (!(a.ablate & 32)) load_chunk(base, S.len, run_start + 64ull * r, x);
-#pragma unroll
-            for (int i = 0; i < 16; ++i) rows[r * kRowDw + i] = x[i];
-        }
-#pragma unroll 1
-        for (uint32_t b0 = 0; b0 < cnt; b0 += kTVR) {
-            if (tid == 0) *hcnt = 0;
-            __syncthreads();  // rows staged; the previous round's hits consumed
-            const uint32_t i = b0 + tid;
-            if (i < cnt) {
-                const uint2 e = rr[i];
-                uint4 rec;
-                if (run_start + e.x < pos_end && !(a.ablate & 16) && fat_find_k(fkeys, fat, F.bmask, e.y, rec)) {
-                    const uint32_t k = atomicAdd(hcnt, 1u);
-                    hits[k] = make_uint4(e.x, rec.y, rec.z, rec.w);
-                }
-            }
-            __syncthreads();
-            const uint32_t nh = *hcnt;
-            if (tid == 0) weak += nh;
-#pragma unroll 1
-            for (uint32_t h0 = 4 * wid; h0 < (a.ablate & 8 ? 0u : nh); h0 += 4 * (kTVR / 64)) {  // wave-uniform
-                const uint32_t h = h0 + row;
-                const bool live = h < nh;
-                const uint4 e = hits[live ? h : h0];
-                uint32_t s0 = 0, cn = 0;
-                if (e.y & kMulti) { s0 = a.start[e.y & ~kMulti]; cn = a.cnt[e.y & ~kMulti]; }
-                const uint64_t st = row_strong_lds(rows, e.x, a.n, K);
-                uint32_t best = kNoBlock;
-                if (!(e.y & kMulti)) {
-                    if (st == (((uint64_t)e.w << 32) | e.z)) best = e.y;
-                } else {
-                    for (uint32_t b = 0; b < cn; b += 16) {  // in index order, 16 candidates per step
-                        const uint32_t j = b + rl;
-                        const uint64_t m = (__ballot(j < cn && a.cstrong[s0 + j] == st) >> (row << 4)) & 0xFFFFull;
-                        if (m) {
-                            best = a.order[s0 + b + (uint32_t)__builtin_ctzll(m)];
-                            break;
-                        }
-                    }
-                }
-                if (live && rl == 0) hits[h].y = best;
-            }
-            __syncthreads();
-            if (wid == 0 && !(a.ablate & 8)) {
-                uint32_t nver = 0;
-                for (uint32_t hb = 0; hb < nh; hb += 64) {
-                    const bool v = hb + lane < nh && hits[hb + lane].y != kNoBlock;
-                    nver += __popcll(__ballot(v));
-                }
-                if (nver) {
-                    unsigned long long k0 = 0;
-                    if (lane == 0) k0 = atomicAdd(&a.counters[0], (unsigned long long)nver);
-                    k0 = shfl64(k0, 0);
-                    for (uint32_t hb = 0; hb < nh; hb += 64) {
-                        const uint32_t j = hb + lane;
-                        const uint4 e = j < nh ? hits[j] : make_uint4(0, kNoBlock, 0, 0);
-                        const bool v = e.y != kNoBlock;
-                        const uint64_t m = __ballot(v);
-                        const unsigned long long k = k0 + __popcll(m & ((1ull << lane) - 1));
-                        if (v && k < a.out_cap) {
-                            a.hit_key[k] = ((uint64_t)si << kSegShift) | (uint64_t)(run_start + e.x - S.pos_begin);
-                            a.hit_val[k] = e.y;
-                        }
-                        k0 += __popcll(m);
-                    }
-                }
-            }
-        }
-        __syncthreads();  // the rows are rewritten by the next run
-    }
-    if (tid == 0 && weak) atomicAdd(&a.counters[1], weak);
 }
 
 // ===========================================================================
@@ -3665,300 +2678,6 @@ __global__ __launch_bounds__(kTW, 2) void k_scan_w(ScanArgs a, uint32_t per) {
     if (kTiming && lane == 0) atomicAdd(&a.counters[3], l1pass);
     if (kTiming && tid == 0)
         for (int k = 0; k < 6; ++k) atomicAdd(&a.counters[4 + k], tm[k]);
-}
-
-// ===========================================================================
-// K2+K4, one stripe of positions per thread: k_scan_s (SYDELTA_SCAN_L1=3, opt-in)
-// ===========================================================================
-// k_scan_l1 shares each 16 Ki-position tile between all eight waves of a workgroup:
-// the tile's bytes are staged in LDS once, but every tile costs a window phase, a
-// drain whose fat-table round trip is on the critical path, and a barrier at which
-// the waves wait for the slowest drain.  Measured (round 3): two key-partition passes
-// with a third of the L2 requests each take 15 ms against 17.6 ms for one pass, so the
-// tile structure, not the L2 request rate, bounds it.  Here every thread rolls its own
-// contiguous stripe of positions (a run of kUS-position units, the window carried from
-// unit to unit), reading its bytes straight into registers (16 bytes of the leaving
-// stream and 32 of the entering one per 16 positions, one step ahead): no LDS rows, no
-// barrier after the level-1 filter copy, waves fully independent.
-// Level-2 passes queue per wave in LDS; a full queue is drained at once (fat-table
-// lookups, then XXH3 of the weak hits' windows from global memory, wave_hash_long).
-// Works for any window (the level-1 filter's size comes from the index: l1_wshift).
-constexpr int kTS = 512;                      // threads per workgroup (8 waves, 2 per SIMD)
-constexpr int kUS = 2048;                     // positions per unit
-constexpr int kUnitsPerTile = kTile2 / kUS;   // 8 (host tiles of kTile2 positions)
-constexpr int kFQS = 64;                      // level-2 passes queued per wave
-static_assert(kTile2 % kUS == 0, "units split host tiles");
-
-struct LdsS {
-    uint32_t ntab, fq, l1, total;
-};
-__host__ __device__ __forceinline__ LdsS lds_s_layout(uint32_t l1_words) {
-    LdsS L;
-    uint32_t o = 0;
-    L.ntab = o; o += 256 * 4;
-    L.fq = o; o += (kTS / 64) * kFQS * 16;
-    L.l1 = o; o += l1_words * 4;
-    L.total = o;
-    return L;
-}
-
-// 16 bytes at base + off (off % 16 == 0), zero when the granule starts at or past len.
-__device__ __forceinline__ uint4 ld16_nt(const uint8_t* base, uint64_t len, uint64_t off) {
-    uint4 v = make_uint4(0, 0, 0, 0);
-    if (off < len) {
-        const uint4* q = (const uint4*)(base + off);
-        v.x = __builtin_nontemporal_load(&q->x); v.y = __builtin_nontemporal_load(&q->y);
-        v.z = __builtin_nontemporal_load(&q->z); v.w = __builtin_nontemporal_load(&q->w);
-    }
-    return v;
-}
-
-// Drain this wave's queued level-2 passes {segment, position in segment, weak, -}: one
-// fat-table bucket read per pass (lane i: pass i), then for each weak hit the XXH3 of its
-// window from global memory and the first candidate in index order with equal strong
-// (generator.rs:121-155); verified hits to the output with one reservation per wave.
-__device__ __forceinline__ void drain_s(const ScanArgs& a, const uint4* fq, uint32_t nfq,
-                                        unsigned long long& weak_hits) {
-    const uint32_t lane = threadIdx.x & 63;
-    lds_fence();
-    bool hit = false;
-    uint4 rec = make_uint4(0, 0, 0, 0);
-    uint4 e = make_uint4(0, 0, 0, 0);
-    if (lane < nfq) {
-        e = fq[lane];
-        const ScanSeg S = a.segs[e.x];
-        const FileIx F = a.files[S.file];
-        hit = fat_find(a.fat + F.slot_off, F.bmask, e.z, rec);
-    }
-    uint64_t m = __ballot(hit);
-    weak_hits += __popcll(m);
-    uint32_t best = 0xFFFFFFFFu;
-    while (m) {  // wave-uniform: one window per weak hit
-        const uint32_t h = (uint32_t)__builtin_ctzll(m);
-        m &= m - 1;
-        const uint32_t seg = __builtin_amdgcn_readlane(e.x, h), rel = __builtin_amdgcn_readlane(e.y, h);
-        const uint32_t cand = __builtin_amdgcn_readlane(rec.y, h);
-        // readlane returns int: widen through uint32_t, or bit 31 of the low half would
-        // sign-extend over the high half
-        const uint64_t cst = ((uint64_t)(uint32_t)__builtin_amdgcn_readlane(rec.w, h) << 32) |
-                             (uint32_t)__builtin_amdgcn_readlane(rec.z, h);
-        const ScanSeg S = a.segs[seg];
-        const uint8_t* win = a.src + S.src + S.pos_begin + rel;
-        uint64_t st;
-        if (a.n > 240) {
-            uint32_t wk;
-            wave_hash_long(win, a.n, wk, st);
-        } else {
-            st = 0;
-            if (lane == 0) st = xxh3_short(win, a.n);
-            st = shfl64(st, 0);
-        }
-        uint32_t b;
-        if (!(cand & kMulti))
-            b = st == cst ? cand : 0xFFFFFFFFu;
-        else
-            b = first_strong_match(a.order, a.cstrong, a.start[cand & ~kMulti], a.cnt[cand & ~kMulti], st);
-        if (lane == h) best = b;
-    }
-    const bool v = best != 0xFFFFFFFFu;
-    const uint64_t mv = __ballot(v);
-    if (!mv) return;
-    unsigned long long k0 = 0;
-    if (lane == 0) k0 = atomicAdd(&a.counters[0], (unsigned long long)__popcll(mv));
-    k0 = shfl64(k0, 0);
-    const unsigned long long k = k0 + __popcll(mv & ((1ull << lane) - 1));
-    if (v && k < a.out_cap) {
-        a.hit_key[k] = ((uint64_t)e.x << kSegShift) | e.y;
-        a.hit_val[k] = best;
-    }
-}
-
-__global__ __launch_bounds__(kTS) void k_scan_s(ScanArgs a, uint64_t per, uint32_t l1_wshift) {
-    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-    const uint32_t n = a.n;
-    const uint32_t l1_words = 1u << (32 - l1_wshift);
-    const LdsS L = lds_s_layout(l1_words);
-    uint32_t* ntab = (uint32_t*)(smem + L.ntab);
-    uint32_t* l1 = (uint32_t*)(smem + L.l1);
-    const uint32_t tid = threadIdx.x;
-    const uint32_t lane = tid & 63, wid = tid >> 6;
-    uint4* fq = (uint4*)(smem + L.fq) + (size_t)wid * kFQS;
-    {
-        const uint4* g = (const uint4*)a.l1;
-        uint4* d = (uint4*)l1;
-        for (uint32_t i = tid; i < l1_words / 4; i += kTS) d[i] = g[i];
-    }
-    for (uint32_t i = tid; i < 256; i += kTS) ntab[i] = kMod - 1 - (a.nm * i) % kMod;
-    __syncthreads();  // the only barrier: everything after is per wave
-
-    const uint64_t nunits = (uint64_t)a.ntiles * kUnitsPerTile;
-    const uint64_t u0 = ((uint64_t)blockIdx.x * kTS + tid) * per;
-    // the level-2 filter of file 0 (k_scan_s takes single-file indexes: uniform)
-    const FileIx F0 = a.files[0];
-    const uint64_t fptr = (uint64_t)(uintptr_t)(a.filt + F0.filt_off);
-    const uint32_t fp_lo = __builtin_amdgcn_readfirstlane((uint32_t)fptr);
-    const uint32_t fp_hi = __builtin_amdgcn_readfirstlane((uint32_t)(fptr >> 32));
-    const __amdgpu_buffer_rsrc_t frsrc = __builtin_amdgcn_make_buffer_rsrc(
-        (void*)(uintptr_t)(((uint64_t)fp_hi << 32) | fp_lo), (short)0,
-        (int)__builtin_amdgcn_readfirstlane((1u << (32 - F0.fwshift)) * 4), 0x00020000);
-    const uint32_t fwshift = __builtin_amdgcn_readfirstlane(F0.fwshift);
-    const uint32_t ds = (n & 15) >> 2, sh = n & 3;  // in-stream dword shift and byte shift (uniform)
-    unsigned long long passes = 0, weak_hits = 0;
-    uint32_t nfq = 0;
-    uint32_t am = 0, bm = 0;
-    uint32_t cur_seg = 0xFFFFFFFFu, next_base = 0;  // this lane's segment and the next one's first tile
-    bool carried = false;
-    ScanSeg S{};
-
-#pragma unroll 1
-    for (uint64_t k = 0; k < per; ++k) {  // wave-uniform trip count
-        const uint64_t u = u0 + k;
-        bool live = u < nunits;
-        uint64_t pos = 0;
-        uint32_t lim = 0;  // valid positions of this unit for this lane
-        if (live) {
-            const uint32_t tile = (uint32_t)(u / kUnitsPerTile);
-            if (cur_seg == 0xFFFFFFFFu || tile >= next_base) {
-                uint32_t lo = cur_seg == 0xFFFFFFFFu ? 0 : cur_seg, hi = a.nsegs;
-                while (hi - lo > 1) {
-                    const uint32_t mid = (lo + hi) >> 1;
-                    if (a.segs[mid].tile_base <= tile) lo = mid; else hi = mid;
-                }
-                if (lo != cur_seg) carried = false;
-                cur_seg = lo;
-                S = a.segs[lo];
-                next_base = lo + 1 < a.nsegs ? a.segs[lo + 1].tile_base : 0xFFFFFFFFu;
-            }
-            pos = S.pos_begin + (uint64_t)(tile - S.tile_base) * kTile2 + (u % kUnitsPerTile) * kUS;
-            live = pos < S.pos_end;
-            lim = live ? (uint32_t)min<uint64_t>((uint64_t)kUS, S.pos_end - pos) : 0u;
-        }
-        if (!live) carried = false;
-        const uint8_t* base = a.src + S.src;
-        const uint64_t len = S.len;
-        const uint32_t rel0 = live ? (uint32_t)(pos - S.pos_begin) : 0u;
-        // ---- the unit's first window: carried, or summed from global memory
-        if (live && !carried) {
-            uint64_t s = 0, b = 0;
-            for (uint32_t o = 0; o < n; o += 16) {
-                const uint4 v = ld16_nt(base, len, pos + o);
-                const uint32_t x4[4] = {v.x, v.y, v.z, v.w};
-                const uint32_t lim16 = min(16u, n - o);
-#pragma unroll
-                for (int i = 0; i < 4; ++i) {
-                    const uint32_t bb = 4u * (uint32_t)i;
-                    const uint32_t keep = lim16 >= bb + 4 ? 0xFFFFFFFFu : lim16 <= bb ? 0u
-                                          : (0xFFFFFFFFu >> (8 * (bb + 4 - lim16)));
-                    const uint32_t d = x4[i] & keep;
-                    const uint32_t dsum = udot4(d, 0x01010101u, 0);
-                    s += dsum;
-                    b += (uint64_t)(n - o) * dsum - udot4(d, offw(i), 0);
-                }
-            }
-            am = (uint32_t)((1 + s) % kMod);
-            bm = (uint32_t)((n + b) % kMod);
-        }
-        carried = live;
-        // ---- roll kUS positions, 16 per step (one 16-byte load of leaving bytes, two of
-        // entering ones, loaded a step ahead), batches of kB3 with the level-2 loads of the
-        // next batch in flight while a batch is tested
-        const uint64_t ia = (pos + n) & ~15ull;  // entering bytes: from the granule holding pos + n
-        uint4 o = ld16_nt(base, len, pos), i0 = ld16_nt(base, len, ia), i1 = ld16_nt(base, len, ia + 16);
-        uint4 po, qi0, qi1;  // the next step's
-        L1Batch cur, nxt;
-        uint32_t xo[4], xi[4];
-        auto bytes_of_step = [&]() {
-            xo[0] = o.x; xo[1] = o.y; xo[2] = o.z; xo[3] = o.w;
-            const uint32_t d[8] = {i0.x, i0.y, i0.z, i0.w, i1.x, i1.y, i1.z, i1.w};
-            uint32_t w[5];
-            // uniform dword shift: one of four straight-line selections
-            if (ds == 0) { for (int q = 0; q < 5; ++q) w[q] = d[q]; }
-            else if (ds == 1) { for (int q = 0; q < 5; ++q) w[q] = d[q + 1]; }
-            else if (ds == 2) { for (int q = 0; q < 5; ++q) w[q] = d[q + 2]; }
-            else { for (int q = 0; q < 5; ++q) w[q] = d[q + 3]; }
-#pragma unroll
-            for (int q = 0; q < 4; ++q) xi[q] = __builtin_amdgcn_alignbyte(w[q + 1], w[q], sh);
-        };
-        auto compute = [&](uint32_t t0, L1Batch& Bt) {  // positions t0 .. t0+7 of the step
-            uint32_t ct[kB3], off[kB3], w1[kB3];
-#pragma unroll
-            for (int t = 0; t < kB3; ++t) ct[t] = ntab[(xo[(t0 + t) >> 2] >> (8 * ((t0 + t) & 3))) & 0xFF];
-#pragma unroll
-            for (int t = 0; t < kB3; ++t) {
-                const uint32_t out = (xo[(t0 + t) >> 2] >> (8 * ((t0 + t) & 3))) & 0xFF;
-                const uint32_t in = (xi[(t0 + t) >> 2] >> (8 * ((t0 + t) & 3))) & 0xFF;
-                __builtin_assume(am < kMod);
-                __builtin_assume(bm < kMod);
-                Bt.wv[t] = (bm << 16) | am;
-                const ProbeHash h = probe_hash(am, bm);
-                Bt.hq[t] = h.q;
-                off[t] = (h.r >> fwshift) * 4;
-                w1[t] = l1[h.q >> l1_wshift];
-                const uint32_t uu = am + in + (kMod - out);  // [M-255, 2M+255)
-                am = min(uu, min(uu - kMod, uu - 2 * kMod));
-                const uint32_t vv = bm + am + ct[t];          // [0, 3M)
-                bm = min(vv, min(vv - kMod, vv - 2 * kMod));
-            }
-#pragma unroll
-            for (int t = 0; t < kB3; ++t) {
-                const uint32_t p1 = l1_test(w1[t], Bt.hq[t]);
-                Bt.w2[t] = __builtin_amdgcn_raw_buffer_load_b32(frsrc, (int)(p1 ? off[t] : 0xFFFFFFFFu), 0, 0);
-            }
-        };
-        // queue batch Bt (unit positions j0 .. j0+7) while the queue has room; false when
-        // it filled (todo: the positions still to queue)
-        auto finish = [&](uint32_t j0, const L1Batch& Bt, uint32_t& todo) -> bool {
-            uint32_t pbits = 0;
-#pragma unroll
-            for (int t = 0; t < kB3; ++t)
-                pbits |= ((filt_pass(Bt.w2[t], Bt.hq[t]) && j0 + t < lim) ? 1u : 0u) << t;
-            asm volatile("" : "+v"(pbits));
-            const uint64_t below = (1ull << lane) - 1;
-#pragma unroll
-            for (int t = 0; t < kB3; ++t) {
-                if (!((todo >> t) & 1)) continue;
-                const uint64_t mk = __ballot((pbits >> t) & 1);
-                if (nfq + __popcll(mk) > (uint32_t)kFQS) return false;
-                if ((pbits >> t) & 1) fq[nfq + __popcll(mk & below)] = make_uint4(cur_seg, rel0 + j0 + t, Bt.wv[t], 0);
-                nfq += __popcll(mk);
-                passes += __popcll(mk);
-                todo &= ~(1u << t);
-            }
-            return true;
-        };
-        bytes_of_step();
-        compute(0, cur);
-#pragma unroll 1
-        for (uint32_t j = 0; j < (uint32_t)kUS; j += 16) {
-            const bool more = j + 16 < (uint32_t)kUS;
-            if (more) {  // the next step's bytes
-                po = ld16_nt(base, len, pos + j + 16);
-                qi0 = ld16_nt(base, len, ia + j + 16);
-                qi1 = ld16_nt(base, len, ia + j + 32);
-            }
-            compute(kB3, nxt);  // second batch of this step
-            uint32_t todo = 0xFFu;
-            while (!finish(j, cur, todo)) {  // a full queue: drain it and finish the batch
-                drain_s(a, fq, nfq, weak_hits);
-                nfq = 0;
-            }
-            cur = nxt;
-            if (more) {
-                o = po; i0 = qi0; i1 = qi1;
-                bytes_of_step();
-                compute(0, nxt);  // first batch of the next step
-            }
-            todo = 0xFFu;
-            while (!finish(j + kB3, cur, todo)) {
-                drain_s(a, fq, nfq, weak_hits);
-                nfq = 0;
-            }
-            cur = nxt;
-        }
-    }
-    if (nfq) drain_s(a, fq, nfq, weak_hits);
-    if (lane == 0 && passes) atomicAdd(&a.counters[2], passes);
-    if (lane == 0 && weak_hits) atomicAdd(&a.counters[1], weak_hits);
 }
 
 // Tail rule (generator.rs:156-184): at p* = len - last_size (last_size < n), the
@@ -4913,17 +3632,6 @@ __global__ void k_synth_mutate(uint8_t* __restrict__ dst, const uint8_t* __restr
 // ===========================================================================
 static inline unsigned grid_for(uint64_t threads, unsigned block) { return (unsigned)((threads + block - 1) / block); }
 
-// Large single-file indexes (block size 4096) scan with k_scan_r by default, verifying
-// from registers at each tile's end: 11.17 ms per 4 GiB (9.88 + 2.81 with the separate
-// k_verify_r, SYDELTA_SCAN_R_INLINE=0) against k_scan_l2's 14.82, k_scan_l1's 16.78 and
-// k_scan_lds's 19.2 ms in global-filter mode.  SYDELTA_SCAN_L1
-// (read when the index is built and per call: the parity tests run every scanner):
-// 0 k_scan_lds, 1 k_scan_l1, 2 k_scan_l1 over two key partitions (l1_part), 3 k_scan_s,
-// 4 k_scan_l2, 5 k_scan_r (the default).
-int scan_l1_mode() {
-    const char* e = getenv("SYDELTA_SCAN_L1");
-    return (e && e[0] >= '0' && e[0] <= '5' && e[1] == 0) ? e[0] - '0' : 5;
-}
 int scan_wide_mode() {
     const char* e = getenv("SYDELTA_SCAN_WIDE");
     return (e && e[0] == '0') ? 0 : (e && e[0] == '2') ? 2 : 1;
@@ -4995,7 +3703,7 @@ hipError_t launch_index_build(const uint32_t* d_weak, const uint64_t* d_strong, 
                               Profiler* prof) {
     hipError_t e;
     if ((e = hipMemsetAsync(ix.filt, 0, ix.fwords * 4, s))) return e;
-    if (ix.l1 && (e = hipMemsetAsync(ix.l1, 0, l1_total_words(ix.l1_wshift, ix.l1_parts) * 4, s))) return e;
+    if (ix.l1 && (e = hipMemsetAsync(ix.l1, 0, l1_total_words(ix.l1_wshift) * 4, s))) return e;
     if ((e = hipMemsetAsync(ix.keys, 0xFF, ix.nslots * 4, s))) return e;
     if ((e = hipMemsetAsync(ix.cnt, 0, ix.nslots * 4, s))) return e;
     const uint64_t n = ix.nblocks;
@@ -5003,7 +3711,7 @@ hipError_t launch_index_build(const uint32_t* d_weak, const uint64_t* d_strong, 
     {
         ProfScope ps(prof, s, "k_idx_insert");
         hipLaunchKernelGGL(k_idx_insert, dim3(grid_for(n, 256)), dim3(256), 0, s, d_weak, n, ix.d_fblk,
-                           (uint32_t)ix.nfiles, ix.d_files, ix.filt, ix.l1, ix.l1_parts, ix.l1_wshift, ix.keys, ix.cnt,
+                           (uint32_t)ix.nfiles, ix.d_files, ix.filt, ix.l1, ix.l1_wshift, ix.keys, ix.cnt,
                            ix.slot_of);
     }
     size_t tmp = 0;
@@ -5108,34 +3816,6 @@ hipError_t launch_scan(const uint8_t* d_buf, const ScanSeg* d_segs, uint32_t nse
     a.counters = d_counters;
     a.l1 = ix.l1;
     a.fat = ix.fat;
-    // k_scan_s (opt-in: SYDELTA_SCAN_L1=3 for the C3 shape, SYDELTA_SCAN_WIDE=2 for wide
-    // windows): one stripe of positions per thread, any window
-    if (ix.l1 && ix.fat && ix.nfiles == 1 && ix.l1_parts == 1 &&
-        ((n == kMaxN3 && ix.l1_wshift == 17 && scan_l1_mode() == 3) || (n > kMaxN2 && scan_wide_mode() == 2))) {
-        static std::once_flag s_once;
-        static hipError_t s_err = hipSuccess;
-        static int s_cus = 256;
-        std::call_once(s_once, [] {
-            s_err = hipFuncSetAttribute((const void*)k_scan_s, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                        160 * 1024 - 256);
-            int dev = 0, cus = 0;
-            if (hipGetDevice(&dev) == hipSuccess &&
-                hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess && cus > 0)
-                s_cus = cus;
-        });
-        if (s_err != hipSuccess) return s_err;
-        const LdsS LS = lds_s_layout(1u << (32 - ix.l1_wshift));
-        if (LS.total > 160u * 1024 - 256) return hipErrorInvalidValue;
-        const uint64_t nunits = (uint64_t)ntiles * kUnitsPerTile;
-        const uint64_t threads = (uint64_t)s_cus * kTS;
-        // few units (an on-demand rescan): fewer workgroups, one unit per thread
-        const uint64_t per = (nunits + threads - 1) / threads;
-        const uint32_t grid = (uint32_t)std::min<uint64_t>((uint64_t)s_cus, (nunits + (uint64_t)kTS * per - 1) /
-                                                                             ((uint64_t)kTS * per));
-        ProfScope ps(prof, s, "k_scan_s");
-        hipLaunchKernelGGL(k_scan_s, dim3(grid), dim3(kTS), LS.total, s, a, per, ix.l1_wshift);
-        return hipGetLastError();
-    }
     if (n > kMaxN2) {  // k_scan_w: windows above the LDS-staged layouts
         static std::once_flag w_once;
         static hipError_t w_err = hipSuccess;
@@ -5158,7 +3838,13 @@ hipError_t launch_scan(const uint8_t* d_buf, const ScanSeg* d_segs, uint32_t nse
         const uint32_t grid = (uint32_t)((ntiles + (uint64_t)per - 1) / per);
         // deferred weak hits (counters[10] counts them; the caller zeroes the counters):
         // room for 2^20 (a shifted 64 GiB file at bs 65536 has 2^20 blocks to find)
-        a.wdef_cap = 1u << 20;
+        // SYDELTA_WDEF_CAP (tests): a smaller list, so that the inline path past it runs too
+        static const uint64_t wdef_cap = [] {
+            const char* e = getenv("SYDELTA_WDEF_CAP");
+            const uint64_t v = e ? strtoull(e, nullptr, 10) : 0;
+            return v ? std::min<uint64_t>(v, 1u << 20) : (uint64_t)1 << 20;
+        }();
+        a.wdef_cap = wdef_cap;
         void* wdef = nullptr;
         hipError_t e = dev_malloc_async(&wdef, a.wdef_cap * sizeof(WDef), s);
         if (e != hipSuccess) return e;
@@ -5177,21 +3863,13 @@ hipError_t launch_scan(const uint8_t* d_buf, const ScanSeg* d_segs, uint32_t nse
         const hipError_t fe = hipFreeAsync(wdef, s);
         return e != hipSuccess ? e : fe;
     }
-    static std::once_flag l1_once;
-    static hipError_t l1_err = hipSuccess;
-    static int l1_cus = 256;
-    const Lds3 L3 = lds3_layout(n);
-    // k_scan_l1 takes the window size its measured and parity-tested configuration
-    // covers, n = 4096 (the C3 shape; tests/test_gpu_scan_large.py).  Other sizes with a
-    // large index go to k_scan_lds (production block sizes for files with more than
-    // 16 Ki blocks are >= 8 KiB anyway: bs = sqrt(file size)).
-    if (ix.l1 && ix.l1_wshift == 1 && n == kMaxN3) {  // k_scan_r (an index built with SYDELTA_SCAN_L1=5)
+    // k_scan_r: one large file at n = 4096 (the index's level-1 filter is kL1WordsR words)
+    if (ix.l1 && ix.l1_wshift == 1 && n == kMaxN3) {
         static std::once_flag r_once;
         static hipError_t r_err = hipSuccess;
         static int r_cus = 256;
         std::call_once(r_once, [] {
-            for (const void* f : {(const void*)k_scan_r<false, false>, (const void*)k_scan_r<true, false>,
-                                  (const void*)k_scan_r<false, true>, (const void*)k_scan_r<true, true>})
+            for (const void* f : {(const void*)k_scan_r<false>, (const void*)k_scan_r<true>})
                 if (r_err == hipSuccess)
                     r_err = hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024 - 256);
             int dev = 0, cus = 0;
@@ -5202,117 +3880,24 @@ hipError_t launch_scan(const uint8_t* d_buf, const ScanSeg* d_segs, uint32_t nse
         if (r_err != hipSuccess) return r_err;
         if (!ix.fat) return hipErrorInvalidValue;
         constexpr LdsR LR = ldsr_layout();
-        constexpr LdsVR LV = ldsvr_layout();
-        // SYDELTA_SCAN_R_INLINE=0: the passes recorded for k_verify_r (round 3's first form,
-        // 9.91 + 2.81 ms at C3) instead of verified at each wave tile's end (11.18 ms)
-        static const bool inl = !(getenv("SYDELTA_SCAN_R_INLINE") && getenv("SYDELTA_SCAN_R_INLINE")[0] == '0');
         // one workgroup per CU over contiguous host tiles, an even number each (runs are pairs)
         uint32_t per = (uint32_t)((ntiles + (uint64_t)r_cus - 1) / (uint64_t)r_cus);
         per += per & 1;
         const uint32_t grid = (uint32_t)((ntiles + (uint64_t)per - 1) / per);
-        const uint32_t npairs = (uint32_t)((ntiles + 1ull) / 2);
-        // pass records (kRCapR per wave, and the pair table; inline: one wave tile's)
-        a.rcap = inl ? (uint32_t)kWTR : kRCapR;
-        const size_t rec_bytes = ((size_t)grid * (kTR / 64) * a.rcap * sizeof(uint2) + 255) & ~(size_t)255;
-        static const bool host_timing = getenv("SYDELTA_HOST_TIMING") != nullptr;
-        const auto th0 = std::chrono::steady_clock::now();
+        // pass records: one wave tile per wave
+        const size_t rec_bytes = ((size_t)grid * (kTR / 64) * kWTR * sizeof(uint2) + 255) & ~(size_t)255;
         void* rbuf = nullptr;
-        hipError_t e = dev_malloc_async(&rbuf, rec_bytes + (inl ? 0 : (size_t)npairs * sizeof(uint4)), s);
+        hipError_t e = dev_malloc_async(&rbuf, rec_bytes, s);
         if (e != hipSuccess) return e;
-        const auto th1 = std::chrono::steady_clock::now();
         a.rrec = (uint2*)rbuf;
-        a.rrun = inl ? nullptr : (uint4*)((uint8_t*)rbuf + rec_bytes);
         {
             ProfScope ps(prof, s, "k_scan_r");
-            if (inl) {
-                if (a.ablate) hipLaunchKernelGGL((k_scan_r<true, true>), dim3(grid), dim3(kTR), LR.total, s, a, per);
-                else hipLaunchKernelGGL((k_scan_r<false, true>), dim3(grid), dim3(kTR), LR.total, s, a, per);
-            } else {
-                if (a.ablate) hipLaunchKernelGGL((k_scan_r<true, false>), dim3(grid), dim3(kTR), LR.total, s, a, per);
-                else hipLaunchKernelGGL((k_scan_r<false, false>), dim3(grid), dim3(kTR), LR.total, s, a, per);
-            }
+            if (a.ablate) hipLaunchKernelGGL((k_scan_r<true>), dim3(grid), dim3(kTR), LR.total, s, a, per);
+            else hipLaunchKernelGGL((k_scan_r<false>), dim3(grid), dim3(kTR), LR.total, s, a, per);
         }
         e = hipGetLastError();
-        if (e == hipSuccess && !(a.ablate & 1) && !inl) {
-            ProfScope ps(prof, s, "k_verify_r");
-            hipLaunchKernelGGL(k_verify_r, dim3(npairs), dim3(kTVR), LV.total, s, a);
-            e = hipGetLastError();
-        }
-        const auto th2 = std::chrono::steady_clock::now();
         const hipError_t fe = hipFreeAsync(rbuf, s);
-        if (host_timing)
-            fprintf(stderr, "sydelta k_scan_r launch: malloc %.3f ms, launches %.3f ms, free %.3f ms\n",
-                    std::chrono::duration<double, std::milli>(th1 - th0).count(),
-                    std::chrono::duration<double, std::milli>(th2 - th1).count(),
-                    std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - th2).count());
         return e != hipSuccess ? e : fe;
-    }
-    if (ix.l1 && ix.l1_wshift == 0 && n == kMaxN3 && scan_l1_mode() == 4) {  // k_scan_l2
-        static std::once_flag l2_once;
-        static hipError_t l2_err = hipSuccess;
-        static int l2_cus = 256;
-        std::call_once(l2_once, [] {
-            const void* fns[4] = {(const void*)k_scan_l2<false, 1>, (const void*)k_scan_l2<true, 1>,
-                                  (const void*)k_scan_l2<false, 2>, (const void*)k_scan_l2<true, 2>};
-            for (const void* f : fns)
-                if (l2_err == hipSuccess)
-                    l2_err = hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024 - 256);
-            int dev = 0, cus = 0;
-            if (hipGetDevice(&dev) == hipSuccess &&
-                hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess && cus > 0)
-                l2_cus = cus;
-        });
-        if (l2_err != hipSuccess) return l2_err;
-        if (!ix.fat) return hipErrorInvalidValue;
-        constexpr Lds4 L4 = lds4_layout(kMaxN3);
-        // one workgroup per CU, an even number of host tiles each so that the pairs line up
-        uint32_t per = (uint32_t)((ntiles + (uint64_t)l2_cus - 1) / (uint64_t)l2_cus);
-        per += per & 1;
-        const uint32_t grid = (uint32_t)((ntiles + (uint64_t)per - 1) / per);
-        ProfScope ps(prof, s, "k_scan_l2");
-        // SYDELTA_SCAN_DEPTH=1|2 (default 1; 2 measured 15.10 vs 14.91 ms): level-2 loads in
-        // flight per batch tested
-        static const int depth = getenv("SYDELTA_SCAN_DEPTH") && getenv("SYDELTA_SCAN_DEPTH")[0] == '2' ? 2 : 1;
-        if (depth == 1) {
-            if (a.timing) hipLaunchKernelGGL((k_scan_l2<true, 1>), dim3(grid), dim3(kT3), L4.total, s, a, per);
-            else hipLaunchKernelGGL((k_scan_l2<false, 1>), dim3(grid), dim3(kT3), L4.total, s, a, per);
-        } else {
-            if (a.timing) hipLaunchKernelGGL((k_scan_l2<true, 2>), dim3(grid), dim3(kT3), L4.total, s, a, per);
-            else hipLaunchKernelGGL((k_scan_l2<false, 2>), dim3(grid), dim3(kT3), L4.total, s, a, per);
-        }
-        return hipGetLastError();
-    }
-    if (ix.l1 && ix.l1_wshift == 17 && n == kMaxN3 && scan_l1_mode() != 0) {
-        std::call_once(l1_once, [] {
-            const void* fns[4] = {(const void*)k_scan_l1<false, false>, (const void*)k_scan_l1<true, false>,
-                                  (const void*)k_scan_l1<false, true>, (const void*)k_scan_l1<true, true>};
-            for (const void* f : fns)
-                if (l1_err == hipSuccess)
-                    l1_err = hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024 - 256);
-            int dev = 0, cus = 0;
-            if (hipGetDevice(&dev) == hipSuccess &&
-                hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess && cus > 0)
-                l1_cus = cus;
-        });
-        if (l1_err != hipSuccess) return l1_err;
-        if (L3.total > 160u * 1024 - 256 || !ix.fat) return hipErrorInvalidValue;
-        // one workgroup per CU (the level-1 filter fills its LDS), contiguous tile ranges
-        const uint32_t grid = (uint32_t)std::min<uint64_t>(ntiles, (uint64_t)l1_cus);
-        const uint32_t per = (ntiles + grid - 1) / grid;
-        // one pass per key partition (the index's level-1 filters), each over every tile
-        for (uint32_t part = 0; part < ix.l1_parts; ++part) {
-            ProfScope ps(prof, s, "k_scan_l1");
-            const bool p2 = ix.l1_parts == 2;
-            if (a.timing) {
-                if (p2) hipLaunchKernelGGL((k_scan_l1<true, true>), dim3(grid), dim3(kT3), L3.total, s, a, per, part);
-                else hipLaunchKernelGGL((k_scan_l1<true, false>), dim3(grid), dim3(kT3), L3.total, s, a, per, part);
-            } else {
-                if (p2) hipLaunchKernelGGL((k_scan_l1<false, true>), dim3(grid), dim3(kT3), L3.total, s, a, per, part);
-                else hipLaunchKernelGGL((k_scan_l1<false, false>), dim3(grid), dim3(kT3), L3.total, s, a, per, part);
-            }
-            if (hipError_t e = hipGetLastError()) return e;
-        }
-        return hipSuccess;
     }
     const bool lds_filter = ix.max_fwords <= kLdsFilterWordsMax;
     const uint32_t lds_fwords = lds_filter ? std::max<uint32_t>(ix.max_fwords, 4u) : 0u;

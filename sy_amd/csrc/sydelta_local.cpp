@@ -178,8 +178,10 @@ extern "C" int sydelta_estimate_change_ratio(const char* source_path, const char
         *got = n;
         return SYDELTA_OK;
     };
-    if (int r = ensure_device(-1)) return r;
-    hipStream_t s = thread_stream(0);
+    int dev = 0;
+    if (int r = path_device(&dev)) return r;
+    if (int r = ensure_device(dev)) return r;
+    hipStream_t s = thread_stream(dev);
     const uint64_t per = std::max<uint64_t>(1, std::min<uint64_t>(want, (64ull << 20) / block_size));
     std::vector<uint8_t> host(2 * per * block_size);
     DevMem m;

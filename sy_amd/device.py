@@ -265,6 +265,31 @@ def join_deltas(parts, source_size: int, block_size: int) -> DeviceDelta:
     return DeviceDelta(kind, a, b, source_size, block_size, stats)
 
 
+def delta_multi_device(devices, basis_chunks, src_chunks, src_pos, src_len: int, block_size: int) -> DeviceDelta:
+    """One file chunk-sharded over `devices` inside the library (sydelta_delta_multi_device):
+    basis_chunks[g] / src_chunks[g] are uint8 tensors on devices[g]; src_chunks[g] holds
+    source bytes [src_pos[g], src_pos[g] + numel) (its chunk plus the block_size - 1 halo).
+    The library synchronizes every stream it uses; the caller's work that filled the
+    tensors must be complete (torch.cuda.synchronize)."""
+    k = len(devices)
+    VP = ctypes.c_void_p * k
+    U = ctypes.c_uint64 * k
+    h = ctypes.c_void_p()
+    check(lib.sydelta_delta_multi_device((ctypes.c_int * k)(*devices), k,
+                                         VP(*[_ptr(b) if b.numel() else None for b in basis_chunks]),
+                                         U(*[b.numel() for b in basis_chunks]),
+                                         VP(*[_ptr(c) if c.numel() else None for c in src_chunks]), U(*src_pos),
+                                         U(*[c.numel() for c in src_chunks]), src_len, block_size, ctypes.byref(h)))
+    return _device_delta(h, _DeltaHandle(h))
+
+
+def thread_device() -> int:
+    """The device the calling thread's path-level calls are bound to (sydelta_thread_device)."""
+    d = ctypes.c_int(-1)
+    check(lib.sydelta_thread_device(ctypes.byref(d)))
+    return d.value
+
+
 def synth_fill_range(buf: torch.Tensor, first: int, seed: int, stream=None) -> None:
     """Bytes [first, first + numel) of the synth_fill stream (first % 8 == 0)."""
     check(lib.sydelta_synth_fill_range(_ptr(buf), first, buf.numel(), seed & 0xFFFFFFFFFFFFFFFF, _stream(stream)))

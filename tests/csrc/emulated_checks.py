@@ -735,5 +735,133 @@ def batch_and_chunk_checks():
     return n_checks
 
 
+def multi_device_checks():
+    """EMU_DEVICES=4: the path API's per-thread device binding (10 concurrent callers
+    spread over the devices, explicit binding, a restricted device set) and
+    sydelta_delta_multi_device (one file chunk-sharded over devices, the signature
+    gathered by peer copies, the walks chained inside the library) against the oracle."""
+    import ctypes
+    import threading
+
+    from sy_amd._lib import check, lib
+
+    n_checks = 0
+    ndev = ctypes.c_int()
+    check(lib.sydelta_device_count(ctypes.byref(ndev)))
+    assert ndev.value == 4, ndev.value
+    lib.emu_device_sets.restype = ctypes.c_uint64
+    lib.emu_device_sets.argtypes = [ctypes.c_int]
+    sets0 = [lib.emu_device_sets(d) for d in range(4)]
+    # 10 concurrent callers: bound to the least-loaded device, sticky, spread evenly
+    bar = threading.Barrier(10)
+    got = [None] * 10
+
+    def bind(k, out):
+        d = ctypes.c_int(-1)
+        check(lib.sydelta_thread_device(ctypes.byref(d)))
+        d2 = ctypes.c_int(-1)
+        check(lib.sydelta_thread_device(ctypes.byref(d2)))
+        assert d.value == d2.value, "binding is sticky"
+        out[k] = d.value
+        bar.wait()  # every thread stays bound until all have bound
+
+    th = [threading.Thread(target=bind, args=(k, got)) for k in range(10)]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join()
+    cnt = [got.count(d) for d in range(4)]
+    assert sorted(cnt) == [2, 2, 3, 3], cnt
+    n_checks += 1
+    # explicit binding and a restricted set
+    check(lib.sydelta_set_thread_device(2))
+    d = ctypes.c_int(-1)
+    check(lib.sydelta_thread_device(ctypes.byref(d)))
+    assert d.value == 2
+    assert lib.sydelta_set_thread_device(7) != 0  # not visible
+    check(lib.sydelta_set_thread_device(-1))
+    allowed = (ctypes.c_int * 2)(1, 3)
+    check(lib.sydelta_set_devices(allowed, 2))
+    got2 = [None] * 6
+    bar = threading.Barrier(6)
+    th = [threading.Thread(target=bind, args=(k, got2)) for k in range(6)]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join()
+    assert sorted(got2) == [1, 1, 1, 3, 3, 3], got2
+    check(lib.sydelta_set_devices(None, 0))
+    n_checks += 1
+    # the path API from 10 threads, each on its bound device, against the oracle
+    os.environ["SYDELTA_STREAM_CHUNK"] = str(1 << 18)
+    pairs = [case(300 + k, (1 << 20) + 1231 * k, 4096) for k in range(10)]
+    with tempfile.TemporaryDirectory() as tmp:
+        def one(k):
+            dd = os.path.join(tmp, f"m{k}")
+            os.makedirs(dd, exist_ok=True)
+            check_pair(dd, pairs[k][0], pairs[k][1], 4096, ("multi thread", k))
+            return True
+
+        with ThreadPoolExecutor(10) as ex:
+            assert all(ex.map(one, range(10)))
+    n_checks += 10
+    sets1 = [lib.emu_device_sets(d) for d in range(4)]
+    assert all(b > a for a, b in zip(sets0, sets1)), (sets0, sets1)
+    # one file over several devices inside the library
+    rng = np.random.default_rng(91)
+    vpa = lambda arrs: (ctypes.c_void_p * len(arrs))(*[ctypes.c_void_p(x) for x in arrs])
+    u64a = lambda xs: (ctypes.c_uint64 * len(xs))(*[int(x) for x in xs])
+    for bs in (512, 4096):
+        basis = O.synth_bytes(301 * bs + 77, 0x800 + bs)
+        s2 = np.concatenate([basis[:40 * bs + 3], np.frombuffer(b"QQ", np.uint8), basis[40 * bs + 3:170 * bs],
+                             basis[210 * bs:], basis[5 * bs:9 * bs]])
+        for q in rng.integers(0, s2.size, 30):
+            s2[q] ^= 0x44
+        L = s2.size
+        sb = np.zeros(L + 64, np.uint8)
+        sb[:L] = s2
+        bb = np.zeros(basis.size + 64, np.uint8)
+        bb[:basis.size] = basis
+        ew, es, ez = C.compute_checksums(basis, bs)
+        exp = O.ops_from_arrays(*C.generate_delta(s2, ew, es, ez, bs))
+        nbb = -(-basis.size // bs)
+        npos = L - bs + 1
+        for devs in ([0], [0, 1], [0, 1, 2, 3], [3, 3, 1], [2, 0, 1, 3, 2, 0, 1, 3]):
+            k = len(devs)
+            bcut = sorted(int(c) for c in rng.choice(np.arange(1, nbb), k - 1, replace=False)) if k > 1 else []
+            bb_pos = [0] + [c * bs for c in bcut]
+            blen = [(bb_pos[g + 1] if g + 1 < k else basis.size) - bb_pos[g] for g in range(k)]
+            scut = sorted(int(c) for c in rng.choice(np.arange(1, -(-npos // bs)), k - 1, replace=False)) if k > 1 \
+                else []
+            sp = [0] + [c * bs for c in scut]
+            slen = [(min(L, sp[g + 1] + bs - 1) if g + 1 < k else L) - sp[g] for g in range(k)]
+            out = ctypes.c_void_p()
+            for probe in ("0", "1"):
+                os.environ["SYDELTA_PROBE"] = probe
+                check(lib.sydelta_delta_multi_device(
+                    (ctypes.c_int * k)(*devs), k, vpa([bb.ctypes.data + x for x in bb_pos]), u64a(blen),
+                    vpa([sb.ctypes.data + x for x in sp]), u64a(sp), u64a(slen), L, bs, ctypes.byref(out)))
+                assert _ops(lib, out) == exp, ("multi", bs, devs, probe)
+                lib.sydelta_delta_free(out)
+                n_checks += 1
+    os.environ.pop("SYDELTA_PROBE", None)
+    # argument checks: a basis chunk that is not whole blocks, a misaligned source start
+    out = ctypes.c_void_p()
+    basis = O.synth_bytes(10 * 512, 1)
+    rc = lib.sydelta_delta_multi_device((ctypes.c_int * 2)(0, 1), 2, vpa([basis.ctypes.data, basis.ctypes.data + 500]),
+                                        u64a([500, 4620]), vpa([basis.ctypes.data, basis.ctypes.data]), u64a([0, 512]),
+                                        u64a([1023, 4608]), 5120, 512, ctypes.byref(out))
+    assert rc == -3, rc
+    rc = lib.sydelta_delta_multi_device((ctypes.c_int * 2)(0, 1), 2, vpa([basis.ctypes.data, basis.ctypes.data + 512]),
+                                        u64a([512, 4608]), vpa([basis.ctypes.data, basis.ctypes.data]), u64a([0, 100]),
+                                        u64a([1023, 4608]), 5120, 512, ctypes.byref(out))
+    assert rc == -3, rc
+    n_checks += 2
+    print(f"emulated multi-device checks ok: {n_checks}")
+
+
 if __name__ == "__main__":
-    main()
+    if len(sys.argv) > 3 and sys.argv[3] == "multi":
+        multi_device_checks()
+    else:
+        main()

@@ -41,18 +41,41 @@ struct ihipEvent_t {
     int dummy;
 };
 
+// EMU_DEVICES=N (default 1): N emulated gfx950 devices sharing host memory; the current
+// device is per thread, as in HIP.  emu_device_sets counts hipSetDevice calls per device.
+static int emu_devices() {
+    static const int n = [] {
+        const char* e = getenv("EMU_DEVICES");
+        const int v = e ? atoi(e) : 1;
+        return v >= 1 && v <= 64 ? v : 1;
+    }();
+    return n;
+}
+static thread_local int t_cur_dev = 0;
+static std::atomic<uint64_t> g_dev_sets[64];
+extern "C" uint64_t emu_device_sets(int d) { return d >= 0 && d < 64 ? g_dev_sets[d].load() : 0; }
 extern "C" {
 hipError_t hipGetDeviceCount(int* n) {
-    *n = 1;
+    *n = emu_devices();
     return hipSuccess;
 }
 hipError_t hipGetDevice(int* d) {
-    *d = 0;
+    *d = t_cur_dev;
     return hipSuccess;
 }
-hipError_t hipSetDevice(int d) { return d == 0 ? hipSuccess : hipErrorInvalidDevice; }
+hipError_t hipSetDevice(int d) {
+    if (d < 0 || d >= emu_devices()) return hipErrorInvalidDevice;
+    t_cur_dev = d;
+    ++g_dev_sets[d];
+    return hipSuccess;
+}
+hipError_t hipDeviceCanAccessPeer(int* ok, int d, int p) {
+    *ok = d != p && d < emu_devices() && p < emu_devices();
+    return hipSuccess;
+}
+hipError_t hipDeviceEnablePeerAccess(int, unsigned int) { return hipSuccess; }
 hipError_t hipGetDevicePropertiesR0600(hipDeviceProp_tR0600* p, int d) {
-    if (d != 0) return hipErrorInvalidDevice;
+    if (d < 0 || d >= emu_devices()) return hipErrorInvalidDevice;
     memset(p, 0, sizeof(*p));
     strcpy(p->name, "host emulation");
     strcpy(p->gcnArchName, "gfx950:sramecc+:xnack-");
@@ -111,13 +134,13 @@ hipError_t hipMallocAsync(void** p, size_t n, hipStream_t) {
 }
 hipError_t hipMalloc(void** p, size_t n) { return hipMallocAsync(p, n, nullptr); }
 hipError_t hipDeviceGetDefaultMemPool(hipMemPool_t* p, int d) {
-    if (d != 0) return hipErrorInvalidDevice;
+    if (d < 0 || d >= emu_devices()) return hipErrorInvalidDevice;
     *p = (hipMemPool_t)&emu_pool_tag;
     return hipSuccess;
 }
 hipError_t hipMemPoolSetAttribute(hipMemPool_t, hipMemPoolAttr, void*) { return hipSuccess; }
 hipError_t hipMemPoolCreate(hipMemPool_t* p, const hipMemPoolProps* props) {
-    if (!props || props->location.id != 0) return hipErrorInvalidDevice;
+    if (!props || props->location.id < 0 || props->location.id >= emu_devices()) return hipErrorInvalidDevice;
     *p = (hipMemPool_t)&emu_pool_tag;
     return hipSuccess;
 }
@@ -144,6 +167,10 @@ hipError_t hipMemcpyAsync(void* d, const void* s, size_t n, hipMemcpyKind, hipSt
     return hipSuccess;
 }
 hipError_t hipMemcpy(void* d, const void* s, size_t n, hipMemcpyKind k) { return hipMemcpyAsync(d, s, n, k, nullptr); }
+hipError_t hipMemcpyPeerAsync(void* d, int dd, const void* s, int sd, size_t n, hipStream_t st) {
+    if (dd < 0 || dd >= emu_devices() || sd < 0 || sd >= emu_devices()) return hipErrorInvalidDevice;
+    return hipMemcpyAsync(d, s, n, hipMemcpyDeviceToDevice, st);
+}
 hipError_t hipMemsetAsync(void* d, int v, size_t n, hipStream_t) {
     EmuCopyTimer t;
     memset(d, v, n);
@@ -317,10 +344,6 @@ hipError_t launch_index_build(const uint32_t* d_weak, const uint64_t* d_strong, 
 }
 
 uint64_t scan_tile_positions() { return 16384; }
-int scan_l1_mode() {
-    const char* e = getenv("SYDELTA_SCAN_L1");
-    return (e && e[0] >= '0' && e[0] <= '5' && e[1] == 0) ? e[0] - '0' : 5;
-}
 int scan_wide_mode() {
     const char* e = getenv("SYDELTA_SCAN_WIDE");
     return (e && e[0] == '0') ? 0 : 1;

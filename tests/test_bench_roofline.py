@@ -8,7 +8,7 @@ def test_roofline_scan_l2_gather():
     algo = bench.algo_bytes_per_step("c3", n, n, n)
     prof = {"k_scan_lds": {"ms": 192.1, "count": 10}, "k_sig_fast": {"ms": 7.0, "count": 10}}
     r = bench.roofline(prof, 10, algo, positions=n - 4095)
-    assert r["kernel"] == "k_scan_lds" and r["bound"] == "hbm"
+    assert r["kernel"] == "k_scan_lds" and r["bound"] == "l2"  # 84 % of the gather ceiling, 28 % of HBM
     assert r["algorithmic_bytes_per_launch"] == n
     assert abs(r["achieved"] - n / 19.21e-3 / 1e9) < 0.01
     assert abs(r["frac"] - r["achieved"] / bench.HBM_PEAK_GBS) < 1e-4
@@ -70,18 +70,37 @@ def test_cpu_baselines_run_small():
     assert c["value"] > 0 and c["cores"] == 2
 
 
-def test_roofline_scan_l1_modelled_requests():
+def test_roofline_scan_r_modelled_requests():
     import math
 
     n = 1 << 32
+    bits = 38400 * 32
     algo = bench.algo_bytes_per_step("c3", n, n, n)
-    r = bench.roofline({"k_scan_l1": {"ms": 172.4, "count": 10}}, 10, algo, positions=n, keys=1 << 20)
+    r = bench.roofline({"k_scan_r": {"ms": 111.7, "count": 10}}, 10, algo, positions=n, keys=1 << 20)
     g = r["l2_gather"]
-    assert abs(g["requests_per_position"] - (1 - math.exp(-1))) < 1e-4
-    assert g["requests_per_launch"] == int(n * (1 - math.exp(-1)))
+    assert abs(g["requests_per_position"] - (1 - math.exp(-(1 << 20) / bits))) < 1e-4
+    assert g["requests_per_launch"] == int(n * (1 - math.exp(-(1 << 20) / bits)))
     assert "level-1" in g["model"]
+    assert r["bound"] == "l2"  # the request rate, not HBM, binds it
     # without the key count no request rate is claimed
-    assert "l2_gather" not in bench.roofline({"k_scan_l1": {"ms": 172.4, "count": 10}}, 10, algo, positions=n)
+    r2 = bench.roofline({"k_scan_r": {"ms": 111.7, "count": 10}}, 10, algo, positions=n)
+    assert "l2_gather" not in r2 and r2["bound"] == "hbm"
+
+
+def test_pmc_traffic_only_from_the_same_workload(tmp_path, monkeypatch):
+    """PMC bytes are read only from a summary of the same workload and block size; a
+    round-1-3 file (no workload field) or another workload's is never borrowed."""
+    import json
+
+    prof = tmp_path / "profiles"
+    prof.mkdir()
+    monkeypatch.setattr(bench, "ROOT", str(tmp_path))
+    k = {"kernels": {"k_scan_lds": {"traffic_bytes": 2000, "bytes_per_launch": 1000}}}
+    json.dump(k, open(prof / "r03_c3_pmc.json", "w"))
+    json.dump(dict(k, workload="c3", block_size=4096), open(prof / "r04a_c3_pmc.json", "w"))
+    assert bench.pmc_traffic("k_scan_lds", 500, "c4", 4096) == (None, None)
+    assert bench.pmc_traffic("k_scan_lds", 500, "c3", 65536) == (None, None)
+    assert bench.pmc_traffic("k_scan_lds", 500, "c3", 4096) == (1000, "profiles/r04a_c3_pmc.json")
 
 
 def test_cpu_baselines_other_workloads_small():

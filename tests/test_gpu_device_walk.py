@@ -6,8 +6,7 @@ threads.  Every op list must equal the C oracle's, and the library's walk counte
 show the device walk ran (a path that reaches a position only an on-demand scan
 classifies is handed back to the host walk, which the counters show too).
 
-Marked late: the kernels were written after this round's GPU access closed and are
-checked here for the first time on hardware (their per-thread bodies are also run by
+Marked late (green on hardware since round 3; the per-thread bodies are also run by
 the CPU suite's emulated device, tests/test_host_emulated.py)."""
 import ctypes
 import os
@@ -18,7 +17,7 @@ import pytest
 
 from oracle import oracle as O
 
-pytestmark = [pytest.mark.gpu, pytest.mark.late, pytest.mark.firstrun]
+pytestmark = [pytest.mark.gpu, pytest.mark.late]
 
 
 @pytest.fixture

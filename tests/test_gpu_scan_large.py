@@ -1,9 +1,6 @@
-"""GPU parity for large single-file indexes (> 16 Ki basis blocks): every scan of a
-large index -- the level-1-filter scan k_scan_l1 (the default at n = 4096,
-SYDELTA_SCAN_L1=1), the same kernel over two key partitions (SYDELTA_SCAN_L1=2), the
-stripe-per-thread k_scan_s (SYDELTA_SCAN_L1=3), k_scan_l2 (=4), the register-fed
-k_scan_r (=5) and k_scan_lds in global-filter mode (SYDELTA_SCAN_L1=0) -- against the
-oracle.
+"""GPU parity for large single-file indexes (> 16 Ki basis blocks) at bs 4096: the
+register-fed level-1-filter scan k_scan_r against the oracle (round 4 removed the
+superseded large-index kernels; each case runs once).
 
 * 96 MiB basis, mixed edits (an all-literal stretch, sparse substitutions, a shift,
   planted unaligned copies, duplicated blocks): bit-exact op list against the C
@@ -24,19 +21,6 @@ import pytest
 from oracle import oracle as O
 
 pytestmark = pytest.mark.gpu
-
-
-# SYDELTA_TEST_SCANNERS=a,b restricts the parametrization (a first hardware run of one kernel)
-_SCANNERS = [k for k in ["lds", "l1", "l1p2", "s", "l2", "r"]
-             if k in os.environ.get("SYDELTA_TEST_SCANNERS", "lds,l1,l1p2,s,l2,r").split(",")]
-
-
-@pytest.fixture(params=_SCANNERS)
-def scanner(request, monkeypatch):
-    """The large-index scan kernel (SYDELTA_SCAN_L1 is read when the index is built and
-    by launch_scan on every call)."""
-    monkeypatch.setenv("SYDELTA_SCAN_L1", {"lds": "0", "l1": "1", "l1p2": "2", "s": "3", "l2": "4", "r": "5"}[request.param])
-    return request.param
 
 
 def _ops_device(gpu, basis_t, src_t, bs, src_len=None, probe=None):
@@ -94,7 +78,7 @@ def _mixed_source(basis: np.ndarray, bs: int, seed: int) -> np.ndarray:
 
 
 @pytest.mark.parametrize("probe", ["0", "1"])
-def test_large_index_mixed_edits(gpu, oracle_c, scanner, probe):
+def test_large_index_mixed_edits(gpu, oracle_c, probe):
     import torch
 
     bs = 4096
@@ -113,7 +97,7 @@ def test_large_index_mixed_edits(gpu, oracle_c, scanner, probe):
     assert d.stats["copy_ops"] > 10000
 
 
-def test_large_index_dense_passes(gpu, oracle_c, scanner):
+def test_large_index_dense_passes(gpu, oracle_c):
     """All-zero and period-3 stretches against a random basis that holds a zero block
     and the three phases of the period-3 block: every window start there is a weak
     hit, so the per-wave pass queue overflows inside one batch (the one position at
@@ -140,7 +124,7 @@ def test_large_index_dense_passes(gpu, oracle_c, scanner):
     assert d.tuples() == O.ops_from_arrays(*oracle_c.generate_delta(src, ew, es, ez, bs))
 
 
-def test_config3_full_size_planted(gpu, oracle_c, scanner):
+def test_config3_full_size_planted(gpu, oracle_c):
     """C3 at 4 GiB with a non-trivial expected op list."""
     import torch
 

@@ -1,8 +1,9 @@
 """GPU parity of the wide-window scan k_scan_w (windows above 8 KiB: sy's own block
 size calculate_block_size = sqrt(file size) for every file over 64 MiB, mod.rs:20-23)
 against the C restatement of generator.rs, and against the per-thread k_scan it
-replaces (SYDELTA_SCAN_WIDE=0, which also turns the aligned probe off); every case
-also through the stripe-per-thread k_scan_s (SYDELTA_SCAN_WIDE=2).
+replaces (SYDELTA_SCAN_WIDE=0, which also turns the aligned probe off).  The deferred
+weak-hit list of k_verify_w also runs with a cap of 64 entries (SYDELTA_WDEF_CAP), so
+that hits past it are verified inline beside the deferred ones.
 
 * every n mod 16 class that matters (8193, 9999, 16384, 31622, 65536, 131071, 131072):
   random edits (substitutions, insertions, deletions, block moves) over several tiles,
@@ -24,14 +25,6 @@ from oracle import oracle as O
 
 pytestmark = pytest.mark.gpu
 
-
-@pytest.fixture(params=[k for k in ["w", "s"] if k in os.environ.get("SYDELTA_TEST_SCANNERS", "w,s").split(",")],
-                autouse=True)
-def wide_kernel(request, monkeypatch):
-    """k_scan_w (default) or the stripe-per-thread k_scan_s (SYDELTA_SCAN_WIDE=2); read
-    when the index is built and per launch."""
-    monkeypatch.setenv("SYDELTA_SCAN_WIDE", {"w": "1", "s": "2"}[request.param])
-    return request.param
 
 WIDE = [8193, 9999, 16384, 31622, 65536, 131071, 131072]
 
@@ -126,6 +119,49 @@ def test_wide_short_sources(bs, gpu, oracle_c):
                 basis[2 * bs:] + basis[:bs // 2], b""):
         for probe in ("0", "1"):
             assert _device(gpu, src, basis, bs, {"SYDELTA_PROBE": probe}).tuples() == _oracle(oracle_c, src, basis, bs)
+
+
+def test_wide_deferred_list_overflow(gpu, oracle_c):
+    """More weak hits than the deferred list holds: a child process with
+    SYDELTA_WDEF_CAP=64 (read once per process) runs shifted and periodic sources whose
+    hits overflow it, so k_verify_w verifies the first 64 and drain_w the rest inline."""
+    import subprocess
+    import sys
+
+    code = r"""
+import random, sys
+sys.path.insert(0, %r)
+import numpy as np, torch
+import sy_amd.device as gpu
+from oracle import oracle as O
+C = O.C()
+def run(src, basis, bs):
+    def dev(b):
+        t = torch.zeros(len(b) + 16, dtype=torch.uint8, device="cuda")
+        if b: t[:len(b)] = torch.frombuffer(bytearray(b), dtype=torch.uint8).cuda()
+        return t
+    bt = dev(basis)
+    w, s = gpu.signature(bt[:len(basis)], bs)
+    nb = w.numel()
+    idx = gpu.Index(w, s, bs, len(basis) - (nb - 1) * bs)
+    d = gpu.match(idx, dev(src), length=len(src))
+    idx.close()
+    ew, es, ez = C.compute_checksums(basis, bs)
+    assert d.tuples() == O.ops_from_arrays(*C.generate_delta(src, ew, es, ez, bs)), (len(src), bs)
+    return d.stats["verified_hits"]
+rng = random.Random(11)
+bs = 9999
+basis = rng.randbytes(300 * bs + 77)
+nv = run(rng.randbytes(3) + basis, basis, bs)
+assert nv >= 290, nv
+pat = (b"ABC" * 70000)[:200000]
+run(pat[:150000], pat, 9000)
+print("ok", nv)
+""" % (os.path.dirname(os.path.dirname(os.path.abspath(__file__))),)
+    env = dict(os.environ, SYDELTA_WDEF_CAP="64", SYDELTA_PROBE="0")
+    r = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert r.stdout.startswith("ok")
 
 
 @pytest.mark.parametrize("pattern", [b"\x00", b"ABC", b"0123456789" * 7])

@@ -10,8 +10,7 @@ with json.loads and compared field by field. The parser is checked on json.dumps
 of the oracle's signature (against the oracle and the host parser), on spellings outside
 the compact form (refused), and on the writer's C2 text (round trip on the device).
 
-Marked firstrun: the kernels were written after this round's GPU access closed. The
-CPU suite runs the same per-thread bodies on the emulated device and under
+Marked late (green on hardware since round 3). The CPU suite also runs the same per-thread bodies on the emulated device and under
 ASan/UBSan (tests/csrc/emulated_checks.py, kernel_bodies_fuzz.cpp)."""
 import json
 
@@ -20,7 +19,7 @@ import pytest
 
 from sy_amd import wire
 
-pytestmark = [pytest.mark.gpu, pytest.mark.late, pytest.mark.firstrun]
+pytestmark = [pytest.mark.gpu, pytest.mark.late]
 
 
 def _dumps(w, s, z, bs) -> bytes:

