@@ -699,9 +699,16 @@ static int index_create_impl(int device, const uint32_t* weak, const uint64_t* s
     const bool want_l1 = want_narrow || want_wide;
     const uint32_t l1_wshift = want_narrow ? 1u : 18u;
     const size_t sz_l1 = want_l1 ? al(4 * l1_total_words(l1_wshift)) : 0;
+    // k_scan_r's ribbon level-1 (sydelta_internal.hpp): its key lists, counts, overflow list
+    // SYDELTA_L1=bloom|ribbon forces the layout (A/B measurements, parity tests at small sizes)
+    const char* l1e = getenv("SYDELTA_L1");
+    const bool want_rib = want_narrow && (l1e && !strcmp(l1e, "ribbon") ? true
+                                          : l1e && !strcmp(l1e, "bloom") ? false
+                                                                          : nblocks >= kRibMinKeys);
+    const size_t sz_rib = want_rib ? al(4ull * kRibShards * kRibCap) + al(4ull * (kRibShards + 1)) + al(4 * nb) : 0;
     const size_t sz_fat = want_l1 ? al(16 * (size_t)sl) : 0;
     const size_t total = sz_weak + sz_strong + sz_filt + sz_l1 + sz_fat + 4 * sz_t + sz_order + sz_slot + sz_files +
-                         sz_fblk + sz_cstrong;
+                         sz_fblk + sz_cstrong + sz_rib;
     x->d_pool = take_kept_pool(device, total, s, &x->pool_bytes);
     if (!x->d_pool) {
         HIP_TRY(dev_malloc_async(&x->d_pool, total, s));  // stream-ordered: no device-wide synchronization
@@ -715,6 +722,12 @@ static int index_create_impl(int device, const uint32_t* weak, const uint64_t* s
     if (want_l1) {
         ix.l1 = (uint32_t*)p; p += sz_l1;
         ix.l1_wshift = l1_wshift;
+        if (want_rib) {
+            ix.l1_ribbon = 1;
+            ix.rib_keys = (uint32_t*)p; p += al(4ull * kRibShards * kRibCap);
+            ix.rib_cnt = (uint32_t*)p; p += al(4ull * (kRibShards + 1));
+            ix.rib_over = (uint32_t*)p; p += al(4 * nb);
+        }
         ix.fat = (uint4*)p; p += sz_fat;
     }
     ix.keys = (uint32_t*)p; p += sz_t;

@@ -29,6 +29,23 @@ constexpr uint32_t kL1WordsWide = 16384;
 // k_scan_r's level-1 filter (one large file at n = 4096): 38400 words = 150 KiB, the LDS
 // left when the tile's bytes stay in registers, word = l1r_word(q) (l1_wshift 1 marks it).
 constexpr uint32_t kL1WordsR = 38400;
+// k_scan_r's level-1 filter as a homogeneous ribbon (Dillinger & Walzer 2021) of width 32
+// in kRibShards independent shards of kRibBits columns: a key w (probe hashes q, r) lies in
+// shard q >> 22, its equation covers columns [start, start + 32) of that shard (start from
+// r) with coefficients (q ^ rotl(r, 16)) | 1, and the solution z satisfies every key's
+// equation c . z = 0 (mod 2); a position passes when its own window's parity is even.
+// One bit of result: a non-key passes with probability ~1/2 however the bits are spent
+// (0.504 measured on Adler values of 1 Mi random 4 KiB blocks, tools/ribbon_sim.c), against
+// 1 - e^(-keys/1228800) for the one-hash Bloom of the same 150 KiB (0.574 at 1 Mi keys):
+// built when the index has at least kRibMinKeys blocks (the two cross at ~852 K keys).
+// Homogeneous: every system is consistent, so no key set makes the build fail (a shard
+// loaded past its columns only passes more positions).
+constexpr uint32_t kRibShards = 1024;
+constexpr uint32_t kRibBits = 1184;  // columns per shard: 37 words
+constexpr uint32_t kRibWords = kRibShards * kRibBits / 32;  // 37888, + 1 pad word read past the last window
+static_assert(kRibWords + 1 <= kL1WordsR, "the ribbon fits k_scan_r's level-1 LDS area");
+constexpr uint32_t kRibCap = 2048;     // distinct keys listed per shard (mean 1024 at 1 Mi keys); more: overflow list
+constexpr uint64_t kRibMinKeys = 852000;
 // words of a level-1 filter: l1_wshift 1 marks k_scan_r's scaled-word layout, any other
 // value a power-of-two filter of 2^(32 - l1_wshift) words (18: k_scan_w's)
 constexpr size_t l1_total_words(uint32_t l1_wshift) {
@@ -67,6 +84,10 @@ struct DeviceIndex {
     uint32_t* l1 = nullptr;     // level-1 filter: single-file indexes above kLdsFilterKeys keys at bs 4096
                                 // (k_scan_r) or with windows above scan_max_window() (k_scan_w)
     uint32_t l1_wshift = 1;     // 1: kL1WordsR words, l1r_word(q); 18: kL1WordsWide words, q >> 18
+    uint32_t l1_ribbon = 0;     // with l1_wshift 1: the words hold the ribbon (kRibWords), not a Bloom filter
+    uint32_t* rib_keys = nullptr;  // ribbon build: kRibShards lists of kRibCap distinct keys
+    uint32_t* rib_cnt = nullptr;   // kRibShards + 1 counts (the last: the overflow list's)
+    uint32_t* rib_over = nullptr;  // overflow list (capacity nblocks)
     uint4* fat = nullptr;       // with l1: per slot {key, first candidate | multi, its strong} (k_idx_fat)
     uint32_t* keys = nullptr;   // 4-key buckets of unique weak values, kEmptyKey = free
     uint32_t* cnt = nullptr;    // candidates per slot

@@ -373,17 +373,33 @@ __device__ __forceinline__ uint32_t file_of_block(const uint64_t* __restrict__ f
     return lo;
 }
 
+// ---------------------------------------------------------------------------
+// k_scan_r's ribbon level-1 filter (sydelta_internal.hpp)
+// ---------------------------------------------------------------------------
+// A key's equation: shard q >> 22, columns [start, start + 32) of the shard, start =
+// floor((r >> 8) * (kRibBits - 31) / 2^24), coefficients (q ^ rotl(r, 16)) | 1 (bit 0:
+// the column `start`).  The scan tests the same parity over its position's window.
+__host__ __device__ __forceinline__ uint32_t rib_bit(uint32_t q, uint32_t r) {
+    const uint32_t start = (uint32_t)(((uint64_t)(r >> 8) * ((kRibBits - 31) << 8)) >> 32);
+    return (q >> 22) * kRibBits + start;  // global column of the window's first bit
+}
+__host__ __device__ __forceinline__ uint32_t rib_coef(uint32_t q, uint32_t r) {
+    return (q ^ ((r << 16) | (r >> 16))) | 1u;
+}
+static_assert(((kRibBits - 31) << 8) < (1u << 24), "rib_bit's constant is a 24-bit operand");
+
 __global__ void k_idx_insert(const uint32_t* __restrict__ weak, uint64_t n, const uint64_t* __restrict__ fblk,
                              uint32_t nf, const FileIx* __restrict__ files, uint32_t* __restrict__ filt,
                              uint32_t* __restrict__ l1, uint32_t l1_wshift, uint32_t* __restrict__ keys,
-                             uint32_t* __restrict__ cnt, uint32_t* __restrict__ slot_of) {
+                             uint32_t* __restrict__ cnt, uint32_t* __restrict__ slot_of, uint32_t* __restrict__ rib_keys,
+                             uint32_t* __restrict__ rib_cnt, uint32_t* __restrict__ rib_over) {
     const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
     const FileIx F = files[file_of_block(fblk, nf, i)];
     const uint32_t w = weak[i];
     const ProbeHash h = probe_hash(w);
     atomicOr(filt + F.filt_off + (h.r >> F.fwshift), filt_mask(h.q));
-    if (l1)  // single-file index only (l1_test)
+    if (l1 && !rib_cnt)  // single-file index only (l1_test)
         atomicOr(l1 + (l1_wshift == 1 ? (size_t)l1r_word(h.q) : (size_t)(h.q >> l1_wshift)), 1u << (h.q & 31));
     uint32_t b = bucket_hash(w) & F.bmask;
     for (;;) {
@@ -393,10 +409,84 @@ __global__ void k_idx_insert(const uint32_t* __restrict__ weak, uint64_t n, cons
             if (old == kEmptyKey || old == w) {
                 atomicAdd(&cnt[sl], 1u);
                 slot_of[i] = (uint32_t)sl;
+                if (rib_cnt && old == kEmptyKey) {  // a new distinct key: list it in its ribbon shard
+                    const uint32_t sh = h.q >> 22;
+                    const uint32_t rank = atomicAdd(&rib_cnt[sh], 1u);
+                    if (rank < kRibCap) rib_keys[(size_t)sh * kRibCap + rank] = w;
+                    else rib_over[atomicAdd(&rib_cnt[kRibShards], 1u)] = w;  // at most n distinct keys
+                }
                 return;
             }
         }
         b = (b + 1) & F.bmask;
+    }
+}
+
+// Insert equation (start column s, coefficients c with bit 0 set) into a shard's echelon
+// rows (rows[j]: the row whose pivot is column j, bit k = column j + k; 0 = none).  Rows
+// are written once (CAS from 0) and never change, so the lanes of a wave insert their keys
+// concurrently: a lane xors a row it reads (final once set) or claims an empty one; a
+// claim lost to another lane is re-read.  An equation that reduces to 0 is a combination of
+// earlier ones (homogeneous: always consistent).
+__device__ __forceinline__ void rib_insert(uint32_t* rows, uint32_t s, uint32_t c) {
+    for (;;) {
+        uint32_t v = __hip_atomic_load(&rows[s], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        if (!v) {
+            v = atomicCAS(&rows[s], 0u, c);
+            if (!v) return;
+        }
+        c ^= v;
+        if (!c) return;
+        const uint32_t t = __builtin_ctz(c);
+        s += t;
+        c >>= t;
+    }
+}
+
+// Free columns of the back-substitution take pseudo-random bits (any values satisfy the
+// equations; random ones make a non-key's parity a fair coin).
+__device__ __forceinline__ uint32_t rib_free_bit(uint32_t col) {
+    uint32_t h = col * 0x9E3779B9u;
+    h ^= h >> 15;
+    h *= 0x2C1B3C6Du;
+    h ^= h >> 13;
+    return h >> 31;
+}
+
+// One workgroup (one wave) per shard: the shard's listed keys (and the overflow list's
+// keys of this shard) inserted into LDS rows 64 at a time, then back-substitution from the
+// last column to the first -- z[j] = parity(rows[j] >> 1 & z[j+1 .. j+31]) for a pivot
+// column, a free bit otherwise -- carried in a 32-bit window; each finished word of z goes
+// to l1[shard * 37 + word].
+__global__ __launch_bounds__(64) void k_ribbon_build(const uint32_t* __restrict__ rib_keys,
+                                                     const uint32_t* __restrict__ rib_cnt,
+                                                     const uint32_t* __restrict__ rib_over, uint32_t* __restrict__ l1) {
+    __shared__ uint32_t rows[kRibBits];
+    const uint32_t sh = blockIdx.x, lane = threadIdx.x;
+    for (uint32_t i = lane; i < kRibBits; i += 64) rows[i] = 0;
+    __syncthreads();
+    const uint32_t nk = min(rib_cnt[sh], kRibCap);
+    for (uint32_t i = lane; i < nk; i += 64) {
+        const ProbeHash h = probe_hash(rib_keys[(size_t)sh * kRibCap + i]);
+        rib_insert(rows, rib_bit(h.q, h.r) - sh * kRibBits, rib_coef(h.q, h.r));
+    }
+    const uint32_t no = rib_cnt[kRibShards];
+    for (uint32_t i = lane; i < no; i += 64) {
+        const ProbeHash h = probe_hash(rib_over[i]);
+        if ((h.q >> 22) == sh) rib_insert(rows, rib_bit(h.q, h.r) - sh * kRibBits, rib_coef(h.q, h.r));
+    }
+    __syncthreads();
+    uint32_t zwin = 0;  // bit k: z[j + 1 + k] while column j is solved
+    for (int wd = (int)(kRibBits / 32) - 1; wd >= 0; --wd) {
+        const uint32_t rv = lane < 32 ? rows[wd * 32 + lane] : 0u;
+#pragma unroll
+        for (int j = 31; j >= 0; --j) {
+            const uint32_t r = (uint32_t)__builtin_amdgcn_readlane((int)rv, j);
+            const uint32_t col = sh * kRibBits + (uint32_t)(wd * 32 + j);
+            const uint32_t z = r ? (__builtin_popcount((r >> 1) & zwin) & 1u) : rib_free_bit(col);
+            zwin = (zwin << 1) | z;
+        }
+        if (lane == 0) l1[sh * (kRibBits / 32) + wd] = zwin;
     }
 }
 
@@ -1948,7 +2038,9 @@ __device__ __forceinline__ void drain_regs(const ScanArgs& a, const uint2* recs,
 // bit 1 the level-2 loads; drain bits 3 (verification) and 4 (fat lookups) as drain_l1.
 // Each wave tile's passes are looked up and verified at the tile's end (drain_regs: the
 // windows hashed from the registers).
-template <bool kAblate>
+// kRib: the level-1 words hold the ribbon (rib_bit / rib_coef: a position passes when the
+// parity of its coefficients over its window is even), else the one-hash Bloom (l1r_word).
+template <bool kAblate, bool kRib>
 __global__ __launch_bounds__(kTR, 2) void k_scan_r(ScanArgs a, uint32_t per) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     constexpr LdsR L = ldsr_layout();
@@ -2063,7 +2155,7 @@ __global__ __launch_bounds__(kTR, 2) void k_scan_r(ScanArgs a, uint32_t per) {
                 auto compute = [&](const int g, L1Batch& Bt) {
                     const uint32_t xo0 = xo[g >> 2], xo1 = xo[(g >> 2) + 1];
                     const uint32_t xi0 = xi[g >> 2], xi1 = xi[(g >> 2) + 1];
-                    uint32_t ct[kB3], off[kB3], w1[kB3];
+                    uint32_t ct[kB3], rr[kB3], w1[kB3], w1b[kB3], bo[kB3];
 #pragma unroll
                     for (int t2 = 0; t2 < kB3; ++t2) ct[t2] = ntab[((t2 < 4 ? xo0 : xo1) >> (8 * (t2 & 3))) & 0xFF];
 #pragma unroll
@@ -2075,8 +2167,14 @@ __global__ __launch_bounds__(kTR, 2) void k_scan_r(ScanArgs a, uint32_t per) {
                         Bt.wv[t2] = (bm << 16) | am;
                         const ProbeHash h = probe_hash(am, bm);
                         Bt.hq[t2] = h.q;
-                        off[t2] = h.r >> fwshift;
-                        w1[t2] = l1[l1r_word(h.q)];
+                        rr[t2] = h.r;
+                        if (kRib) {  // the window's two words (ds_read2_b32)
+                            bo[t2] = rib_bit(h.q, h.r);
+                            w1[t2] = l1[bo[t2] >> 5];
+                            w1b[t2] = l1[(bo[t2] >> 5) + 1];
+                        } else {
+                            w1[t2] = l1[l1r_word(h.q)];
+                        }
                         const uint32_t u = am + in + (kMod - out);  // [M-255, 2M+255)
                         am = min(u, min(u - kMod, u - 2 * kMod));
                         const uint32_t v = bm + am + ct[t2];          // [0, 3M)
@@ -2084,10 +2182,17 @@ __global__ __launch_bounds__(kTR, 2) void k_scan_r(ScanArgs a, uint32_t per) {
                     }
 #pragma unroll
                     for (int t2 = 0; t2 < kB3; ++t2) {
-                        uint32_t p1 = l1_test(w1[t2], Bt.hq[t2]);
+                        uint32_t p1;
+                        if (kRib) {
+                            const uint32_t win = __builtin_amdgcn_alignbit(w1b[t2], w1[t2], bo[t2]);
+                            p1 = ~__builtin_popcount(win & rib_coef(Bt.hq[t2], rr[t2])) & 1u;
+                        } else {
+                            p1 = l1_test(w1[t2], Bt.hq[t2]);
+                        }
                         if (kAblate && (a.ablate & 2)) p1 = 0;
                         // a level-1 miss asks for an offset past the buffer: no request, reads 0
-                        Bt.w2[t2] = __builtin_amdgcn_raw_buffer_load_b32(frsrc, (int)((off[t2] << 2) | (p1 - 1u)), 0, 0);
+                        Bt.w2[t2] = __builtin_amdgcn_raw_buffer_load_b32(frsrc, (int)(((rr[t2] >> fwshift) << 2) | (p1 - 1u)),
+                                                                         0, 0);
                     }
                 };
                 auto finish = [&](const int g, L1Batch& Bt) {
@@ -3704,6 +3809,7 @@ hipError_t launch_index_build(const uint32_t* d_weak, const uint64_t* d_strong, 
     hipError_t e;
     if ((e = hipMemsetAsync(ix.filt, 0, ix.fwords * 4, s))) return e;
     if (ix.l1 && (e = hipMemsetAsync(ix.l1, 0, l1_total_words(ix.l1_wshift) * 4, s))) return e;
+    if (ix.l1_ribbon && (e = hipMemsetAsync(ix.rib_cnt, 0, 4 * (kRibShards + 1), s))) return e;
     if ((e = hipMemsetAsync(ix.keys, 0xFF, ix.nslots * 4, s))) return e;
     if ((e = hipMemsetAsync(ix.cnt, 0, ix.nslots * 4, s))) return e;
     const uint64_t n = ix.nblocks;
@@ -3712,7 +3818,12 @@ hipError_t launch_index_build(const uint32_t* d_weak, const uint64_t* d_strong, 
         ProfScope ps(prof, s, "k_idx_insert");
         hipLaunchKernelGGL(k_idx_insert, dim3(grid_for(n, 256)), dim3(256), 0, s, d_weak, n, ix.d_fblk,
                            (uint32_t)ix.nfiles, ix.d_files, ix.filt, ix.l1, ix.l1_wshift, ix.keys, ix.cnt,
-                           ix.slot_of);
+                           ix.slot_of, ix.rib_keys, ix.l1_ribbon ? ix.rib_cnt : nullptr, ix.rib_over);
+    }
+    if (ix.l1_ribbon) {
+        ProfScope ps(prof, s, "k_ribbon_build");
+        hipLaunchKernelGGL(k_ribbon_build, dim3(kRibShards), dim3(64), 0, s, ix.rib_keys, ix.rib_cnt, ix.rib_over, ix.l1);
+        if ((e = hipGetLastError())) return e;
     }
     size_t tmp = 0;
     if ((e = hipcub::DeviceScan::ExclusiveSum(nullptr, tmp, ix.cnt, ix.start, (int)ix.nslots, s))) return e;
@@ -3869,7 +3980,8 @@ hipError_t launch_scan(const uint8_t* d_buf, const ScanSeg* d_segs, uint32_t nse
         static hipError_t r_err = hipSuccess;
         static int r_cus = 256;
         std::call_once(r_once, [] {
-            for (const void* f : {(const void*)k_scan_r<false>, (const void*)k_scan_r<true>})
+            for (const void* f : {(const void*)k_scan_r<false, false>, (const void*)k_scan_r<true, false>,
+                                  (const void*)k_scan_r<false, true>, (const void*)k_scan_r<true, true>})
                 if (r_err == hipSuccess)
                     r_err = hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024 - 256);
             int dev = 0, cus = 0;
@@ -3892,8 +4004,13 @@ hipError_t launch_scan(const uint8_t* d_buf, const ScanSeg* d_segs, uint32_t nse
         a.rrec = (uint2*)rbuf;
         {
             ProfScope ps(prof, s, "k_scan_r");
-            if (a.ablate) hipLaunchKernelGGL((k_scan_r<true>), dim3(grid), dim3(kTR), LR.total, s, a, per);
-            else hipLaunchKernelGGL((k_scan_r<false>), dim3(grid), dim3(kTR), LR.total, s, a, per);
+            if (ix.l1_ribbon) {
+                if (a.ablate) hipLaunchKernelGGL((k_scan_r<true, true>), dim3(grid), dim3(kTR), LR.total, s, a, per);
+                else hipLaunchKernelGGL((k_scan_r<false, true>), dim3(grid), dim3(kTR), LR.total, s, a, per);
+            } else {
+                if (a.ablate) hipLaunchKernelGGL((k_scan_r<true, false>), dim3(grid), dim3(kTR), LR.total, s, a, per);
+                else hipLaunchKernelGGL((k_scan_r<false, false>), dim3(grid), dim3(kTR), LR.total, s, a, per);
+            }
         }
         e = hipGetLastError();
         const hipError_t fe = hipFreeAsync(rbuf, s);

@@ -1,6 +1,7 @@
 """GPU parity for large single-file indexes (> 16 Ki basis blocks) at bs 4096: the
 register-fed level-1-filter scan k_scan_r against the oracle (round 4 removed the
-superseded large-index kernels; each case runs once).
+superseded large-index kernels), with both level-1 layouts forced on the smaller cases
+(SYDELTA_L1=bloom|ribbon); the 4 GiB C3 case runs once, with the default (the ribbon).
 
 * 96 MiB basis, mixed edits (an all-literal stretch, sparse substitutions, a shift,
   planted unaligned copies, duplicated blocks): bit-exact op list against the C
@@ -21,6 +22,14 @@ import pytest
 from oracle import oracle as O
 
 pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(params=["bloom", "ribbon"])
+def level1(request, monkeypatch):
+    """k_scan_r's level-1 filter layout (SYDELTA_L1, read when the index is built): the
+    one-hash Bloom or the ribbon (the default from 852 K keys, so C3 uses it)."""
+    monkeypatch.setenv("SYDELTA_L1", request.param)
+    return request.param
 
 
 def _ops_device(gpu, basis_t, src_t, bs, src_len=None, probe=None):
@@ -78,7 +87,7 @@ def _mixed_source(basis: np.ndarray, bs: int, seed: int) -> np.ndarray:
 
 
 @pytest.mark.parametrize("probe", ["0", "1"])
-def test_large_index_mixed_edits(gpu, oracle_c, probe):
+def test_large_index_mixed_edits(gpu, oracle_c, level1, probe):
     import torch
 
     bs = 4096
@@ -97,7 +106,7 @@ def test_large_index_mixed_edits(gpu, oracle_c, probe):
     assert d.stats["copy_ops"] > 10000
 
 
-def test_large_index_dense_passes(gpu, oracle_c):
+def test_large_index_dense_passes(gpu, oracle_c, level1):
     """All-zero and period-3 stretches against a random basis that holds a zero block
     and the three phases of the period-3 block: every window start there is a weak
     hit, so the per-wave pass queue overflows inside one batch (the one position at
