@@ -92,6 +92,10 @@ constexpr uint32_t kNoBlk = 0xFFFFFFFFu;
 constexpr uint64_t kUnknownNone = UINT64_MAX;
 
 // One source being classified: a whole file of a batch, or a chunk of one file.
+// Scan-hit lists: filled by index (Classifier::scan), so no zero fill on resize.
+using HitPos = std::vector<uint64_t, NoInitAlloc<uint64_t>>;
+using HitBlk = std::vector<uint32_t, NoInitAlloc<uint32_t>>;
+
 struct Src {
     uint32_t file = 0;          // basis file in the index
     uint64_t off = 0;           // byte offset of source position 0 from the launch base
@@ -103,22 +107,23 @@ struct Src {
     std::vector<uint32_t, NoInitAlloc<uint32_t>> ahit;  // probed: per block, its aligned window's hit or kNoBlk
     uint64_t nahit = 0;            // aligned windows that hit
     std::vector<uint8_t> scanned;  // probed: per block, all its window starts were scanned
-    std::vector<uint64_t> hpos;    // hits found by scans, sorted, unique
-    std::vector<uint32_t> hblk;    // their global block indices
+    HitPos hpos;                   // hits found by scans, sorted, unique
+    HitBlk hblk;                   // their global block indices
     std::vector<uint64_t> ppos;    // probed: per block, its phase-probed window start or kUnknownNone
     std::vector<uint32_t> phit;    // ... and that window's hit or kNoBlk
 };
 
 // Merge sorted (pos, blk) lists into c's hits (equal positions carry equal blocks).
-inline void merge_hits(Src& c, const std::vector<uint64_t>& pos, const std::vector<uint32_t>& blk) {
+template <class PV = HitPos, class BV = HitBlk>
+inline void merge_hits(Src& c, const PV& pos, const BV& blk) {
     if (pos.empty()) return;
     if (c.hpos.empty() || pos.front() > c.hpos.back()) {  // later positions: append
         c.hpos.insert(c.hpos.end(), pos.begin(), pos.end());
         c.hblk.insert(c.hblk.end(), blk.begin(), blk.end());
         return;
     }
-    std::vector<uint64_t> np;
-    std::vector<uint32_t> nb;
+    HitPos np;
+    HitBlk nb;
     np.reserve(c.hpos.size() + pos.size());
     nb.reserve(c.hpos.size() + pos.size());
     size_t i = 0, j = 0;
@@ -389,12 +394,52 @@ bool run_parallel(int n, F&& task) {
     }
 }
 
-// Split points of a parallel walk of c from `entry`: multiples of n strictly inside
-// (entry, c.p1), at most T0 segments; st.back() == c.p1.
+// No known hit starts in (x - n, x): no Copy can cover x, so every walk that starts
+// before x lands exactly on x (a step is +1, or +n from a hit).  Scan hits, aligned hits
+// of probed blocks and phase-probed hits are consulted; a position only an on-demand
+// scan would classify counts as no hit here (the walk then reports it, and the caller
+// walks sequentially).
+inline bool no_hit_before(const Src& c, uint64_t n, uint64_t x) {
+    const uint64_t lo = x >= n ? x - n + 1 : 0;  // (x - n, x) = [lo, x)
+    if (lo >= x) return true;
+    const auto it = std::lower_bound(c.hpos.begin(), c.hpos.end(), lo);
+    if (it != c.hpos.end() && *it < x) return false;
+    if (c.probed) {
+        for (uint64_t k = lo / n; k * n < x; ++k) {  // the blocks [lo, x) touches (at most two)
+            if (k < c.kb || k >= c.kb + c.nblk) continue;
+            if (k * n >= lo && c.ahit[k - c.kb] != kNoBlk) return false;
+            if (!c.ppos.empty() && c.ppos[k - c.kb] != kUnknownNone && c.ppos[k - c.kb] >= lo &&
+                c.ppos[k - c.kb] < x && c.phit[k - c.kb] != kNoBlk)
+                return false;
+        }
+    }
+    return true;
+}
+
+// Split points of a parallel walk of c from `entry`, at most T0 segments, st.back() ==
+// c.p1.  Each cut is a position the walk is known to land on (no_hit_before), so the
+// segments chain without a re-walk: the ideal cut itself, else the first multiple of n
+// or scan hit after it that qualifies (rsync-shaped sources shifted off the block grid
+// put every Copy at a scan hit, C3b), else the multiple of n (then the chain re-walks
+// the next segment when the walk does not land there).
 inline std::vector<uint64_t> split_points(const Src& c, uint64_t n, uint64_t entry, int T0) {
     std::vector<uint64_t> st{entry};
     for (int t = 1; t < T0; ++t) {
-        const uint64_t q = (entry + (c.p1 - entry) / T0 * t) / n * n;
+        const uint64_t ideal = entry + (c.p1 - entry) / T0 * t;
+        const uint64_t lim = std::min(c.p1, ideal + 64 * n);
+        uint64_t q = ideal / n * n, pick = 0;
+        if (no_hit_before(c, n, ideal)) pick = ideal;
+        auto h = std::lower_bound(c.hpos.begin(), c.hpos.end(), ideal);
+        uint64_t m = (ideal + n - 1) / n * n;
+        for (int tries = 0; !pick && tries < 128; ++tries) {
+            const uint64_t hp = h != c.hpos.end() ? *h : UINT64_MAX;
+            const uint64_t x = std::min(hp, m);
+            if (x >= lim) break;
+            if (no_hit_before(c, n, x)) pick = x;
+            if (x == hp) ++h;
+            if (x == m) m += n;
+        }
+        if (pick) q = pick;
         if (q > st.back() && q < c.p1) st.push_back(q);
     }
     st.push_back(c.p1);
