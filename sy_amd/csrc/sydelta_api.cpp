@@ -691,13 +691,14 @@ static int index_create_impl(int device, const uint32_t* weak, const uint64_t* s
     const size_t sz_weak = al(4 * nb), sz_strong = al(8 * nb), sz_filt = al(4 * fw), sz_t = al(4 * sl);
     const size_t sz_order = al(4 * nb), sz_slot = al(4 * nb), sz_files = al(sizeof(FileIx) * nfiles);
     const size_t sz_fblk = al(8 * (nfiles + 1)), sz_cstrong = al(8 * nb);
-    // k_scan_r's level-1 filter: one large file at bs 4096 (the BASELINE C3 shape)
-    const bool want_narrow = nfiles == 1 && nblocks > kLdsFilterKeys && block_size == 4096;
+    // the level-1 filter of the register-fed scans (k_scan_r at bs 4096, k_scan_g at any
+    // other): one file with more keys than an LDS-resident Bloom filter takes
+    const bool want_narrow = nfiles == 1 && nblocks > kLdsFilterKeys;
     // windows above the LDS-staged scans' limit, one file (the production block sizes of
     // files over 64 MiB, mod.rs:20-23): k_scan_w's level-1 filter and fat table
     const bool want_wide = nfiles == 1 && block_size > scan_max_window() && scan_wide_mode() != 0;
     const bool want_l1 = want_narrow || want_wide;
-    const uint32_t l1_wshift = want_narrow ? 1u : 18u;
+    const uint32_t l1_wshift = 1u;  // kL1WordsR words (k_scan_r / k_scan_g)
     const size_t sz_l1 = want_l1 ? al(4 * l1_total_words(l1_wshift)) : 0;
     // k_scan_r's ribbon level-1 (sydelta_internal.hpp): its key lists, counts, overflow list
     // SYDELTA_L1=bloom|ribbon forces the layout (A/B measurements, parity tests at small sizes)
@@ -952,7 +953,7 @@ bool phase_probe_on() {
 // The index carries k_scan_w's level-1 filter (one file, window above the LDS-staged
 // scans' limit) and SYDELTA_SCAN_WIDE does not turn it off.
 bool wide_scan(const sydelta_index* x) {
-    return x->ix.l1 && x->ix.l1_wshift == 18 && scan_wide_mode() != 0;
+    return x->ix.l1 != nullptr && scan_wide_mode() != 0;
 }
 
 int probe_mode_env() {

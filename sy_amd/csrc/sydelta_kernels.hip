@@ -2040,17 +2040,20 @@ __device__ __forceinline__ void drain_regs(const ScanArgs& a, const uint2* recs,
 // windows hashed from the registers).
 // kRib: the level-1 words hold the ribbon (rib_bit / rib_coef: a position passes when the
 // parity of its coefficients over its window is even), else the one-hash Bloom (l1r_word).
-template <bool kAblate, bool kRib>
-__global__ __launch_bounds__(kTR, 2) void k_scan_r(ScanArgs a, uint32_t per) {
+// kWaves: waves per workgroup (one workgroup per CU: the level-1 filter fills the LDS);
+// 12 = three per SIMD, which caps the kernel at 168 VGPRs.
+template <bool kAblate, bool kRib, int kWaves>
+__global__ __launch_bounds__(kWaves * 64, 1) void k_scan_r(ScanArgs a, uint32_t per) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     constexpr LdsR L = ldsr_layout();
+    constexpr uint32_t kT = kWaves * 64;
     const uint32_t n = a.n;  // kMaxN3 (launch_scan)
     const uint32_t* l1 = (const uint32_t*)(smem + L.l1);
     uint32_t* ntab = (uint32_t*)(smem + L.ntab);
     const uint32_t tid = threadIdx.x;
     const uint32_t lane = tid & 63, wid = tid >> 6;
     uint32_t* ctr = (uint32_t*)(smem + L.ctr);
-    const uint32_t gwave = blockIdx.x * (kTR / 64) + wid;
+    const uint32_t gwave = blockIdx.x * kWaves + wid;
     uint2* rec = a.rrec + (size_t)gwave * kWTR;  // this wave's pass records (one wave tile)
 
     const uint32_t t_begin = blockIdx.x * per;
@@ -2060,9 +2063,9 @@ __global__ __launch_bounds__(kTR, 2) void k_scan_r(ScanArgs a, uint32_t per) {
         const uint4* g = (const uint4*)a.l1;
         uint4* d = (uint4*)(smem + L.l1);
 #pragma unroll 4
-        for (uint32_t i = tid; i < kL1WordsR / 4; i += kTR) d[i] = g[i];
+        for (uint32_t i = tid; i < kL1WordsR / 4; i += kT) d[i] = g[i];
     }
-    for (uint32_t i = tid; i < 256; i += kTR) ntab[i] = kMod - 1 - (a.nm * i) % kMod;
+    for (uint32_t i = tid; i < 256; i += kT) ntab[i] = kMod - 1 - (a.nm * i) % kMod;
     uint64_t* kt = (uint64_t*)(smem + L.kt);
     if (tid < 48)
         kt[tid] = tid < 24 ? c_tab.w[tid] : tid < 32 ? c_tab.last[tid - 24] : tid < 40 ? c_tab.init[tid - 32]
@@ -2241,6 +2244,371 @@ __global__ __launch_bounds__(kTR, 2) void k_scan_r(ScanArgs a, uint32_t per) {
 }
 
 // ===========================================================================
+// k_scan_g: k_scan_r's register-fed roll for any window n (one large file)
+// ===========================================================================
+// k_scan_r needs n = 4096: a wave tile's in rows are then the next tile's out rows, and
+// lane l's first window is out rows l..63 + in rows 0..l-1.  For any other n the out
+// rows [P + 64l, +64) and the in rows [P + n + 64l, +64) are loaded separately (the in
+// rows at any alignment: load64_u), and the first windows follow from the window at the
+// tile's start, (A0, B0), in closed form (rolling.rs:66-79 applied d = 64l times):
+//   A(d) = A0 + In(d) - Out(d)
+//   B(d) = B0 + d (A0 - 1) + sum_{j<d} (d - j) in_j - sum_{j<d} (d - j) out_j - n Out(d)
+// from exclusive wave scans of the rows' sums; (A0, B0) of the next tile is lane 63's
+// window after its 64 rolls.  A run's first window is summed from global memory
+// (window_at).  The level-1 filter (Bloom or ribbon), level-2 loads and the keys-only
+// lookups are k_scan_r's; a weak hit's window is not in the registers, so it goes to the
+// deferred list (WDef) that k_verify_w hashes after the scan (hits the list cannot take
+// are verified inline from global memory).  Replaces k_scan_w (windows above 8 KiB) and
+// k_scan_lds in global-filter mode for single-file indexes.
+
+// 64 bytes at byte offset q of src (any alignment) through 16-byte granule loads and
+// alignbyte; bytes at or beyond len read as 0 (only granules holding a byte of [0, len)
+// are loaded).
+__device__ __forceinline__ void load64_u(const uint8_t* src, uint64_t len, uint64_t q, uint32_t x[16]) {
+    const uint32_t sh = (uint32_t)q & 15u;
+    if (!sh) {
+        load_chunk(src, len, q, x);
+        return;
+    }
+    const uint64_t qa = q - sh;
+    const uint4* g = (const uint4*)(src + qa);
+    uint32_t d[20];
+    if (qa + 80 <= len) {
+#pragma unroll
+        for (int i = 0; i < 5; ++i) {
+            const uint4 v = g[i];
+            d[4 * i] = v.x; d[4 * i + 1] = v.y; d[4 * i + 2] = v.z; d[4 * i + 3] = v.w;
+        }
+    } else {
+#pragma unroll
+        for (int i = 0; i < 5; ++i) {
+            uint4 v = make_uint4(0, 0, 0, 0);
+            if (qa + 16 * i < len) v = g[i];
+            d[4 * i] = v.x; d[4 * i + 1] = v.y; d[4 * i + 2] = v.z; d[4 * i + 3] = v.w;
+        }
+#pragma unroll
+        for (int i = 0; i < 20; ++i) {
+            const uint64_t o = qa + 4 * i;
+            d[i] &= o >= len ? 0u : (o + 4 <= len ? 0xFFFFFFFFu : (0xFFFFFFFFu >> (8 * (o + 4 - len))));
+        }
+    }
+    const uint32_t ds = sh >> 2, bs = sh & 3;
+    uint32_t e[17];
+#pragma unroll
+    for (int i = 0; i < 17; ++i) e[i] = ds == 0 ? d[i] : ds == 1 ? d[i + 1] : ds == 2 ? d[i + 2] : d[i + 3];
+#pragma unroll
+    for (int i = 0; i < 16; ++i) x[i] = __builtin_amdgcn_alignbyte(e[i + 1], e[i], bs);
+}
+
+// Adler-32 state (A, B) of the window [P, P + n) of src (rolling.rs:35-45: A = 1 + sum x,
+// B = n + sum (n - i) x_i, mod M), summed by the whole wave; every lane returns it.
+__device__ __forceinline__ void window_at(const uint8_t* src, uint64_t len, uint64_t P, uint32_t n, uint32_t& am,
+                                          uint32_t& bm) {
+    const uint32_t lane = threadIdx.x & 63;
+    uint64_t s = 0, t = 0;  // sum x, sum i x_i (i from the window start)
+    for (uint32_t c = 64 * lane; c < n; c += 64 * 64) {
+        uint32_t x[16];
+        load64_u(src, len, P + c, x);
+        uint32_t cs = 0, cv = 0;
+#pragma unroll
+        for (int i = 0; i < 16; ++i) {
+            const uint32_t j = c + 4 * i;
+            const uint32_t keep = j >= n ? 0u : (j + 4 <= n ? 0xFFFFFFFFu : (0xFFFFFFFFu >> (8 * (j + 4 - n))));
+            const uint32_t v = x[i] & keep;
+            cs = udot4(v, 0x01010101u, cs);
+            cv = udot4(v, offw(i), cv);
+        }
+        s += cs;
+        t += (uint64_t)c * cs + cv;
+    }
+    s = wave_sum64(s);
+    t = wave_sum64(t);
+    am = (uint32_t)((1 + s) % kMod);
+    bm = (uint32_t)((n + (uint64_t)n * s - t) % kMod);
+}
+
+// Lookups of one wave tile's level-2 pass records (keys-only bucket reads, 64 per round);
+// weak hits go to the deferred list a.wdef (counters[10] counts them) for k_verify_w, or,
+// past its capacity, are verified here from global memory (verify_l1<false>).
+__device__ __forceinline__ void drain_g(const ScanArgs& a, const uint2* recs, uint32_t nr, uint4* wq,
+                                        unsigned long long& weak_hits, uint64_t run_start, const SegCtx& cur) {
+    const uint32_t lane = threadIdx.x & 63;
+    const uint64_t below = (1ull << lane) - 1;
+    __threadfence_block();  // this wave's record stores before its loads
+    uint32_t nwq = 0;
+    for (uint32_t base = 0; base < nr; base += 64) {
+        const uint32_t i = base + lane;
+        bool hit = false;
+        uint4 rec = make_uint4(0, 0, 0, 0);
+        uint32_t pos = 0;
+        if (i < nr) {
+            const volatile uint2* g = recs + i;  // rewritten by later tiles: not from a stale L1 line
+            pos = g->x;
+            const uint32_t w = g->y;
+            if (run_start + pos < cur.pos_end && !(a.ablate & 16)) hit = fat_find_k(cur.keys, cur.fat, cur.bmask, w, rec);
+        }
+        const uint64_t m = __ballot(hit);
+        if (!m) continue;
+        const uint32_t cnt = __popcll(m);
+        weak_hits += cnt;
+        if (a.ablate & 8) continue;
+        unsigned long long k0 = 0;
+        if (lane == 0) k0 = atomicAdd(&a.counters[10], (unsigned long long)cnt);
+        k0 = shfl64(k0, 0);
+        const uint64_t slot = k0 + __popcll(m & below);
+        const bool deferred = hit && slot < a.wdef_cap;
+        if (deferred) {
+            const uint64_t p = run_start + pos;
+            WDef d;
+            d.at = (uint64_t)(cur.base - a.src) + p;
+            d.key = ((uint64_t)cur.seg_id << kSegShift) | (p - cur.pos_begin);
+            d.cand = rec.y;
+            d.pad = 0;
+            d.strong = ((uint64_t)rec.w << 32) | rec.z;
+            a.wdef[slot] = d;
+        }
+        const uint64_t mi = __ballot(hit && !deferred);
+        if (!mi) continue;
+        const uint32_t ci = __popcll(mi);
+        const uint32_t rank = __popcll(mi & below);
+        const uint4 e = make_uint4(pos, rec.y, rec.z, rec.w);
+        const bool mine = hit && !deferred;
+        if (nwq + ci > (uint32_t)kWQ3) {
+            verify_l1<false>(a, wq, nwq, nullptr, run_start, cur);
+            nwq = 0;
+        }
+        if (ci > (uint32_t)kWQ3) {  // more than wq holds: two halves
+            if (mine && rank < (uint32_t)kWQ3) wq[rank] = e;
+            verify_l1<false>(a, wq, kWQ3, nullptr, run_start, cur);
+            if (mine && rank >= (uint32_t)kWQ3) wq[rank - kWQ3] = e;
+            nwq = ci - kWQ3;
+        } else {
+            if (mine) wq[nwq + rank] = e;
+            nwq += ci;
+        }
+    }
+    verify_l1<false>(a, wq, nwq, nullptr, run_start, cur);
+    lds_fence();
+}
+
+struct LdsG {
+    uint32_t l1, ntab, wq, ctr, total;  // byte offsets
+};
+__host__ __device__ constexpr LdsG ldsg_layout() {
+    LdsG L{};
+    uint32_t o = 0;
+    L.l1 = o; o += kL1WordsR * 4;
+    L.ntab = o; o += 256 * 4;
+    L.wq = o; o += (kTR / 64) * kWQ3 * 16;
+    L.ctr = o; o += 16;
+    L.total = o;
+    return L;
+}
+static_assert(ldsg_layout().total <= 160 * 1024 - 256, "k_scan_g's LDS");
+
+// per: host tiles per workgroup (a multiple of rt); rt: host tiles per run (the unit a wave
+// takes from the workgroup's counter, sized so the run's first window, summed from global
+// memory, is a small part of the run's reads).
+template <bool kAblate, bool kRib>
+__global__ __launch_bounds__(kTR, 2) void k_scan_g(ScanArgs a, uint32_t per, uint32_t rt) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    constexpr LdsG L = ldsg_layout();
+    const uint32_t n = a.n;
+    const uint32_t* l1 = (const uint32_t*)(smem + L.l1);
+    uint32_t* ntab = (uint32_t*)(smem + L.ntab);
+    const uint32_t tid = threadIdx.x;
+    const uint32_t lane = tid & 63, wid = tid >> 6;
+    uint4* wq = (uint4*)(smem + L.wq) + (size_t)wid * kWQ3;
+    uint32_t* ctr = (uint32_t*)(smem + L.ctr);
+    const uint32_t gwave = blockIdx.x * (kTR / 64) + wid;
+    uint2* rec = a.rrec + (size_t)gwave * kWTR;  // this wave's pass records (one wave tile)
+
+    const uint32_t t_begin = blockIdx.x * per;
+    const uint32_t t_end = min(a.ntiles, t_begin + per);
+    if (t_begin >= t_end) return;
+    {
+        const uint4* g = (const uint4*)a.l1;
+        uint4* d = (uint4*)(smem + L.l1);
+#pragma unroll 4
+        for (uint32_t i = tid; i < kL1WordsR / 4; i += kTR) d[i] = g[i];
+    }
+    for (uint32_t i = tid; i < 256; i += kTR) ntab[i] = kMod - 1 - (a.nm * i) % kMod;
+    if (tid == 0) *ctr = 0;
+    __syncthreads();  // the only barrier: the waves run independently from here
+
+    unsigned long long passes = 0, weak_hits = 0;
+    uint32_t nrec = 0, si_hint = 0;
+    const uint64_t below = (1ull << lane) - 1;
+#pragma unroll 1
+    for (;;) {
+        uint32_t c = 0;
+        if (lane == 0) c = atomicAdd(ctr, 1u);
+        c = __builtin_amdgcn_readfirstlane(c);
+        const uint32_t t0 = t_begin + rt * c;
+        if (t0 >= t_end) break;
+        const uint32_t tz = min(t_end, t0 + rt);
+#pragma unroll 1
+        for (uint32_t t = t0; t < tz;) {
+            // the part of the run in one segment: host tiles [t, t + span)
+            uint32_t lo = si_hint, hi = a.nsegs;
+            while (hi - lo > 1) {
+                const uint32_t mid = (lo + hi) >> 1;
+                if (a.segs[mid].tile_base <= t) lo = mid; else hi = mid;
+            }
+            const uint32_t si = lo;
+            si_hint = si;
+            const ScanSeg S = a.segs[si];
+            const FileIx F = a.files[S.file];
+            SegCtx sc;
+            sc.base = a.src + S.src;
+            sc.pos_begin = S.pos_begin;
+            sc.keys = a.keys + F.slot_off;
+            sc.fat = a.fat + F.slot_off;
+            sc.slot_off = F.slot_off;
+            sc.bmask = F.bmask;
+            sc.seg_id = si;
+            sc.fwshift = F.fwshift;
+            sc.filt = a.filt + F.filt_off;
+            sc.fwords = 1u << (32 - F.fwshift);
+            const uint32_t seg_tend = si + 1 < a.nsegs ? a.segs[si + 1].tile_base : a.ntiles;
+            const uint32_t span = min(tz, seg_tend) - t;
+            const uint64_t run_start = S.pos_begin + (uint64_t)(t - S.tile_base) * kTile2;
+            sc.pos_end = min(S.pos_end, run_start + (uint64_t)span * kTile2);
+            const uint64_t seg_len = S.len;
+            const uint32_t nwt = (uint32_t)((sc.pos_end - run_start + kWTR - 1) / kWTR);  // wave tiles with positions
+            t += span;
+
+            const uint64_t fptr = (uint64_t)(uintptr_t)sc.filt;
+            const uint32_t fp_lo = __builtin_amdgcn_readfirstlane((uint32_t)fptr);
+            const uint32_t fp_hi = __builtin_amdgcn_readfirstlane((uint32_t)(fptr >> 32));
+            const __amdgpu_buffer_rsrc_t frsrc = __builtin_amdgcn_make_buffer_rsrc(
+                (void*)(uintptr_t)(((uint64_t)fp_hi << 32) | fp_lo), (short)0,
+                (int)__builtin_amdgcn_readfirstlane(sc.fwords * 4), 0x00020000);
+            const uint32_t fwshift = __builtin_amdgcn_readfirstlane(sc.fwshift);
+
+            uint32_t A0, B0;  // the window at the current wave tile's start
+            window_at(sc.base, seg_len, run_start, n, A0, B0);
+            uint32_t xo[16], xi[16], no_[16], ni_[16];
+            load_chunk(sc.base, seg_len, run_start + 64ull * lane, xo);
+            load64_u(sc.base, seg_len, run_start + n + 64ull * lane, xi);
+#pragma unroll 1
+            for (uint32_t k = 0; k < nwt; ++k) {
+                const uint64_t P = run_start + (uint64_t)k * kWTR;
+                const uint32_t rel0 = k * kWTR + lane * 64;  // position in run of this lane's first window
+                // ---- window: lane l's window [P + 64l, +n) from (A0, B0) and the rows before l
+                uint32_t am, bm;
+                {
+                    uint32_t so = 0, vo = 0, si_ = 0, vi = 0;
+#pragma unroll
+                    for (int i = 0; i < 16; ++i) {
+                        so = udot4(xo[i], 0x01010101u, so);
+                        vo = udot4(xo[i], offw(i), vo);
+                        si_ = udot4(xi[i], 0x01010101u, si_);
+                        vi = udot4(xi[i], offw(i), vi);
+                    }
+                    uint32_t tot;
+                    const uint32_t Ox = wave_scan_excl(so, tot), Ix = wave_scan_excl(si_, tot);
+                    const uint32_t ROx = wave_scan_excl(lane * so, tot), RIx = wave_scan_excl(lane * si_, tot);
+                    const uint32_t VOx = wave_scan_excl(vo, tot), VIx = wave_scan_excl(vi, tot);
+                    const uint64_t d = 64ull * lane;
+                    // sum_{j<d} (d - j) x_j over a row stream = 64 (l X - R) - V (every term >= 0)
+                    const uint64_t pin = 64ull * ((uint64_t)lane * Ix - RIx) - VIx;
+                    const uint64_t pout = 64ull * ((uint64_t)lane * Ox - ROx) - VOx;
+                    am = (uint32_t)(((uint64_t)A0 + Ix + 16ull * kMod - Ox) % kMod);
+                    const uint64_t bpos = (uint64_t)B0 + d * (A0 + kMod - 1) + pin;
+                    const uint64_t bneg = (pout + (uint64_t)a.nm * Ox) % kMod;
+                    bm = (uint32_t)((bpos % kMod + kMod - bneg) % kMod);
+                }
+                auto compute = [&](const int g, L1Batch& Bt) {
+                    const uint32_t xo0 = xo[g >> 2], xo1 = xo[(g >> 2) + 1];
+                    const uint32_t xi0 = xi[g >> 2], xi1 = xi[(g >> 2) + 1];
+                    uint32_t ct[kB3], rr[kB3], w1[kB3], w1b[kB3], bo[kB3];
+#pragma unroll
+                    for (int t2 = 0; t2 < kB3; ++t2) ct[t2] = ntab[((t2 < 4 ? xo0 : xo1) >> (8 * (t2 & 3))) & 0xFF];
+#pragma unroll
+                    for (int t2 = 0; t2 < kB3; ++t2) {
+                        const uint32_t out = ((t2 < 4 ? xo0 : xo1) >> (8 * (t2 & 3))) & 0xFF;
+                        const uint32_t in = ((t2 < 4 ? xi0 : xi1) >> (8 * (t2 & 3))) & 0xFF;
+                        __builtin_assume(am < kMod);
+                        __builtin_assume(bm < kMod);
+                        Bt.wv[t2] = (bm << 16) | am;
+                        const ProbeHash h = probe_hash(am, bm);
+                        Bt.hq[t2] = h.q;
+                        rr[t2] = h.r;
+                        if (kRib) {
+                            bo[t2] = rib_bit(h.q, h.r);
+                            w1[t2] = l1[bo[t2] >> 5];
+                            w1b[t2] = l1[(bo[t2] >> 5) + 1];
+                        } else {
+                            w1[t2] = l1[l1r_word(h.q)];
+                        }
+                        const uint32_t u = am + in + (kMod - out);  // [M-255, 2M+255)
+                        am = min(u, min(u - kMod, u - 2 * kMod));
+                        const uint32_t v = bm + am + ct[t2];          // [0, 3M)
+                        bm = min(v, min(v - kMod, v - 2 * kMod));
+                    }
+#pragma unroll
+                    for (int t2 = 0; t2 < kB3; ++t2) {
+                        uint32_t p1;
+                        if (kRib) {
+                            const uint32_t win = __builtin_amdgcn_alignbit(w1b[t2], w1[t2], bo[t2]);
+                            p1 = ~__builtin_popcount(win & rib_coef(Bt.hq[t2], rr[t2])) & 1u;
+                        } else {
+                            p1 = l1_test(w1[t2], Bt.hq[t2]);
+                        }
+                        if (kAblate && (a.ablate & 2)) p1 = 0;
+                        Bt.w2[t2] = __builtin_amdgcn_raw_buffer_load_b32(frsrc, (int)(((rr[t2] >> fwshift) << 2) | (p1 - 1u)),
+                                                                         0, 0);
+                    }
+                };
+                auto finish = [&](const int g, L1Batch& Bt) {
+                    uint32_t pbits = 0;
+#pragma unroll
+                    for (int t2 = 0; t2 < kB3; ++t2) pbits |= filt_bit(Bt.w2[t2], Bt.hq[t2]) << t2;
+                    asm volatile("" : "+v"(pbits));
+                    if (!__ballot(pbits != 0)) return;
+#pragma unroll
+                    for (int t2 = 0; t2 < kB3; ++t2) {
+                        const uint64_t mk = __ballot((pbits >> t2) & 1);
+                        if (!mk) continue;
+                        if ((pbits >> t2) & 1) rec[nrec + __popcll(mk & below)] = make_uint2(rel0 + g + t2, Bt.wv[t2]);
+                        nrec += __popcll(mk);
+                    }
+                };
+                const uint32_t tile_rec = nrec;
+                L1Batch b0, b1;
+                compute(0, b0);
+                compute(8, b1);
+#pragma unroll
+                for (int bi = 0; bi < kNBR; ++bi) {
+                    L1Batch& Bt = (bi & 1) ? b1 : b0;
+                    finish(kB3 * bi, Bt);
+                    if (bi + 2 < kNBR) compute(kB3 * (bi + 2), Bt);
+                    if (bi == 2 && k + 1 < nwt) {
+                        load_chunk(sc.base, seg_len, P + kWTR + 64ull * lane, no_);
+                        load64_u(sc.base, seg_len, P + kWTR + n + 64ull * lane, ni_);
+                    }
+                }
+                // the next tile's first window: lane 63's after its 64 rolls
+                A0 = __builtin_amdgcn_readlane(am, 63);
+                B0 = __builtin_amdgcn_readlane(bm, 63);
+                passes += nrec - tile_rec;
+                if (nrec > tile_rec && !(kAblate && (a.ablate & 1)))
+                    drain_g(a, rec + tile_rec, nrec - tile_rec, wq, weak_hits, run_start, sc);
+                nrec = tile_rec;
+#pragma unroll
+                for (int i = 0; i < 16; ++i) {
+                    xo[i] = no_[i];
+                    xi[i] = ni_[i];
+                }
+            }
+        }
+    }
+    if (lane == 0 && passes) atomicAdd(&a.counters[2], passes);
+    if (lane == 0 && weak_hits) atomicAdd(&a.counters[1], weak_hits);
+}
+
+// ===========================================================================
 // K2+K4 for windows above kMaxN2: k_scan_w
 // ===========================================================================
 // sy's own block size is calculate_block_size(size) = sqrt(size) clamped to [512, 128 Ki]
@@ -2341,7 +2709,7 @@ __global__ __launch_bounds__(256) void k_verify_w(ScanArgs a) {
     const uint64_t total = min((uint64_t)a.counters[10], a.wdef_cap);
     const uint64_t wave = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
     const uint64_t nwaves = ((uint64_t)gridDim.x * blockDim.x) >> 6;
-    const bool rows = a.n % 64 == 0;
+    const bool rows = a.n % 64 == 0 && a.n >= 256;  // row_hash: the long path, whole stripes
     const uint32_t per = rows ? 4u : 1u;
     for (uint64_t r0 = wave * per; r0 < total; r0 += nwaves * per) {  // wave-uniform
         const uint64_t ri = rows ? r0 + row : r0;
@@ -2368,7 +2736,13 @@ __global__ __launch_bounds__(256) void k_verify_w(ScanArgs a) {
                 }
             }
         } else {
-            wave_hash_long(a.src + d.at, a.n, wk, st);
+            if (a.n > 240) {
+                wave_hash_long(a.src + d.at, a.n, wk, st);
+            } else {  // XXH3's short paths (k_scan_g takes any window)
+                st = 0;
+                if (lane == 0) st = xxh3_short(a.src + d.at, a.n);
+                st = shfl64(st, 0);
+            }
             if (!(d.cand & kMulti)) {
                 if (st == d.strong) best = d.cand;
             } else {
@@ -3901,7 +4275,7 @@ hipError_t launch_scan(const uint8_t* d_buf, const ScanSeg* d_segs, uint32_t nse
                        uint64_t out_cap, unsigned long long* d_counters, uint2* gfq, size_t gfq_cap, hipStream_t s,
                        Profiler* prof) {
     if (n == 0) return hipErrorInvalidValue;
-    if (n > kMaxN2 && !(ix.l1 && ix.l1_wshift == 18 && ix.fat && ix.nfiles == 1)) return hipErrorInvalidValue;
+    if (n > kMaxN2 && !(ix.l1 && ix.l1_wshift == 1 && ix.fat && ix.nfiles == 1)) return hipErrorInvalidValue;
     if (ntiles == 0) return hipSuccess;
     ScanArgs a{};
     a.src = d_buf;
@@ -3927,61 +4301,72 @@ hipError_t launch_scan(const uint8_t* d_buf, const ScanSeg* d_segs, uint32_t nse
     a.counters = d_counters;
     a.l1 = ix.l1;
     a.fat = ix.fat;
-    if (n > kMaxN2) {  // k_scan_w: windows above the LDS-staged layouts
-        static std::once_flag w_once;
-        static hipError_t w_err = hipSuccess;
-        static int w_cus = 256;
-        std::call_once(w_once, [] {
-            for (const void* f : {(const void*)k_scan_w<false>, (const void*)k_scan_w<true>})
-                if (w_err == hipSuccess)
-                    w_err = hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024 - 256);
+    // k_scan_g: one file with a level-1 filter (more than kLdsFilterKeys blocks, or windows
+    // above the LDS-staged layouts) at any n but 4096; weak hits verified by k_verify_w
+    if (ix.l1 && ix.l1_wshift == 1 && ix.fat && ix.nfiles == 1 && n != kMaxN3) {
+        static std::once_flag g_once;
+        static hipError_t g_err = hipSuccess;
+        static int g_cus = 256;
+        std::call_once(g_once, [] {
+            for (const void* f : {(const void*)k_scan_g<false, false>, (const void*)k_scan_g<true, false>,
+                                  (const void*)k_scan_g<false, true>, (const void*)k_scan_g<true, true>})
+                if (g_err == hipSuccess)
+                    g_err = hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024 - 256);
             int dev = 0, cus = 0;
             if (hipGetDevice(&dev) == hipSuccess &&
                 hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess && cus > 0)
-                w_cus = cus;
+                g_cus = cus;
         });
-        if (w_err != hipSuccess) return w_err;
-        constexpr LdsW LW = ldsw_layout();
-        // one workgroup per CU, contiguous ranges of an even number of host tiles (a range's
-        // windows are carried; the pairs line up)
-        uint32_t per = (uint32_t)((ntiles + (uint64_t)w_cus - 1) / (uint64_t)w_cus);
-        per += per & 1;
+        if (g_err != hipSuccess) return g_err;
+        constexpr LdsG LG = ldsg_layout();
+        // runs of rt host tiles: the run's first window (n bytes from global memory) <= 1/8 of
+        // its reads; each workgroup a contiguous range of whole runs
+        uint32_t rt = 2;
+        while ((uint64_t)rt * kTile2 < 8ull * n) rt *= 2;
+        uint32_t per = (uint32_t)((ntiles + (uint64_t)g_cus - 1) / (uint64_t)g_cus);
+        per = (per + rt - 1) / rt * rt;
         const uint32_t grid = (uint32_t)((ntiles + (uint64_t)per - 1) / per);
-        // deferred weak hits (counters[10] counts them; the caller zeroes the counters):
-        // room for 2^20 (a shifted 64 GiB file at bs 65536 has 2^20 blocks to find)
-        // SYDELTA_WDEF_CAP (tests): a smaller list, so that the inline path past it runs too
         static const uint64_t wdef_cap = [] {
             const char* e = getenv("SYDELTA_WDEF_CAP");
             const uint64_t v = e ? strtoull(e, nullptr, 10) : 0;
-            return v ? std::min<uint64_t>(v, 1u << 20) : (uint64_t)1 << 20;
+            return v ? std::min<uint64_t>(v, 1u << 22) : (uint64_t)1 << 22;
         }();
         a.wdef_cap = wdef_cap;
-        void* wdef = nullptr;
-        hipError_t e = dev_malloc_async(&wdef, a.wdef_cap * sizeof(WDef), s);
+        const size_t rec_bytes = ((size_t)grid * (kTR / 64) * kWTR * sizeof(uint2) + 255) & ~(size_t)255;
+        void* buf = nullptr;
+        hipError_t e = dev_malloc_async(&buf, rec_bytes + a.wdef_cap * sizeof(WDef), s);
         if (e != hipSuccess) return e;
-        a.wdef = (WDef*)wdef;
+        a.rrec = (uint2*)buf;
+        a.wdef = (WDef*)((uint8_t*)buf + rec_bytes);
         {
-            ProfScope ps(prof, s, "k_scan_w");
-            if (a.timing) hipLaunchKernelGGL(k_scan_w<true>, dim3(grid), dim3(kTW), LW.total, s, a, per);
-            else hipLaunchKernelGGL(k_scan_w<false>, dim3(grid), dim3(kTW), LW.total, s, a, per);
+            ProfScope ps(prof, s, "k_scan_g");
+            if (ix.l1_ribbon) {
+                if (a.ablate) hipLaunchKernelGGL((k_scan_g<true, true>), dim3(grid), dim3(kTR), LG.total, s, a, per, rt);
+                else hipLaunchKernelGGL((k_scan_g<false, true>), dim3(grid), dim3(kTR), LG.total, s, a, per, rt);
+            } else {
+                if (a.ablate) hipLaunchKernelGGL((k_scan_g<true, false>), dim3(grid), dim3(kTR), LG.total, s, a, per, rt);
+                else hipLaunchKernelGGL((k_scan_g<false, false>), dim3(grid), dim3(kTR), LG.total, s, a, per, rt);
+            }
         }
         e = hipGetLastError();
-        if (e == hipSuccess) {
+        if (e == hipSuccess && !(a.ablate & 1)) {
             ProfScope ps(prof, s, "k_verify_w");
-            hipLaunchKernelGGL(k_verify_w, dim3(4 * (uint32_t)w_cus), dim3(256), 0, s, a);
+            hipLaunchKernelGGL(k_verify_w, dim3(4 * (uint32_t)g_cus), dim3(256), 0, s, a);
             e = hipGetLastError();
         }
-        const hipError_t fe = hipFreeAsync(wdef, s);
+        const hipError_t fe = hipFreeAsync(buf, s);
         return e != hipSuccess ? e : fe;
     }
-    // k_scan_r: one large file at n = 4096 (the index's level-1 filter is kL1WordsR words)
+    // k_scan_r: one large file at n = 4096 (SYDELTA_SCAN_R_WAVES=12: three waves per SIMD)
     if (ix.l1 && ix.l1_wshift == 1 && n == kMaxN3) {
         static std::once_flag r_once;
         static hipError_t r_err = hipSuccess;
         static int r_cus = 256;
         std::call_once(r_once, [] {
-            for (const void* f : {(const void*)k_scan_r<false, false>, (const void*)k_scan_r<true, false>,
-                                  (const void*)k_scan_r<false, true>, (const void*)k_scan_r<true, true>})
+            for (const void* f : {(const void*)k_scan_r<false, false, 8>, (const void*)k_scan_r<true, false, 8>,
+                                  (const void*)k_scan_r<false, true, 8>, (const void*)k_scan_r<true, true, 8>,
+                                  (const void*)k_scan_r<false, false, 12>, (const void*)k_scan_r<true, false, 12>,
+                                  (const void*)k_scan_r<false, true, 12>, (const void*)k_scan_r<true, true, 12>})
                 if (r_err == hipSuccess)
                     r_err = hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024 - 256);
             int dev = 0, cus = 0;
@@ -3991,26 +4376,30 @@ hipError_t launch_scan(const uint8_t* d_buf, const ScanSeg* d_segs, uint32_t nse
         });
         if (r_err != hipSuccess) return r_err;
         if (!ix.fat) return hipErrorInvalidValue;
+        static const int waves = getenv("SYDELTA_SCAN_R_WAVES") && atoi(getenv("SYDELTA_SCAN_R_WAVES")) == 12 ? 12 : 8;
         constexpr LdsR LR = ldsr_layout();
         // one workgroup per CU over contiguous host tiles, an even number each (runs are pairs)
         uint32_t per = (uint32_t)((ntiles + (uint64_t)r_cus - 1) / (uint64_t)r_cus);
         per += per & 1;
         const uint32_t grid = (uint32_t)((ntiles + (uint64_t)per - 1) / per);
         // pass records: one wave tile per wave
-        const size_t rec_bytes = ((size_t)grid * (kTR / 64) * kWTR * sizeof(uint2) + 255) & ~(size_t)255;
+        const size_t rec_bytes = ((size_t)grid * waves * kWTR * sizeof(uint2) + 255) & ~(size_t)255;
         void* rbuf = nullptr;
         hipError_t e = dev_malloc_async(&rbuf, rec_bytes, s);
         if (e != hipSuccess) return e;
         a.rrec = (uint2*)rbuf;
         {
             ProfScope ps(prof, s, "k_scan_r");
-            if (ix.l1_ribbon) {
-                if (a.ablate) hipLaunchKernelGGL((k_scan_r<true, true>), dim3(grid), dim3(kTR), LR.total, s, a, per);
-                else hipLaunchKernelGGL((k_scan_r<false, true>), dim3(grid), dim3(kTR), LR.total, s, a, per);
+            const dim3 g(grid), b(64 * waves);
+#define LAUNCH_R(AB, RB, W) hipLaunchKernelGGL((k_scan_r<AB, RB, W>), g, b, LR.total, s, a, per)
+            if (waves == 12) {
+                if (ix.l1_ribbon) { if (a.ablate) LAUNCH_R(true, true, 12); else LAUNCH_R(false, true, 12); }
+                else { if (a.ablate) LAUNCH_R(true, false, 12); else LAUNCH_R(false, false, 12); }
             } else {
-                if (a.ablate) hipLaunchKernelGGL((k_scan_r<true, false>), dim3(grid), dim3(kTR), LR.total, s, a, per);
-                else hipLaunchKernelGGL((k_scan_r<false, false>), dim3(grid), dim3(kTR), LR.total, s, a, per);
+                if (ix.l1_ribbon) { if (a.ablate) LAUNCH_R(true, true, 8); else LAUNCH_R(false, true, 8); }
+                else { if (a.ablate) LAUNCH_R(true, false, 8); else LAUNCH_R(false, false, 8); }
             }
+#undef LAUNCH_R
         }
         e = hipGetLastError();
         const hipError_t fe = hipFreeAsync(rbuf, s);
