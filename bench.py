@@ -527,6 +527,7 @@ def algo_bytes_per_step(workload: str, n: int, nb_bytes: int, src_bytes: int) ->
     step the signature kernels read the basis once and the scan reads the source once
     (SURVEY.md section 8(d))."""
     return {"k_scan": src_bytes, "k_scan_lds": src_bytes, "k_scan_w": src_bytes, "k_scan_r": src_bytes,
+            "k_scan_g": src_bytes,
             "k_sig_fast": nb_bytes if workload in ("c3", "c3b") else n,
             "k_sig_batch": n, "k_sig_wave": n, "k_probe": src_bytes,
             "k_apply": 2 * n,  # apply: every output byte read once and written once
@@ -572,9 +573,13 @@ def roofline(prof: dict, steps: int, algo_step: dict, positions=None, keys=None,
             "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": traffic, "traffic_source": tsrc,
             "kernel": dom, "avg_launch_ms": round(avg_ms, 4), "algorithmic_bytes_per_launch": per_launch}
     # level-1 filter bits per key (one hash)
-    l1_bits = {"k_scan_w": 1 << 19, "k_scan_r": 38400 * 32}
+    l1_bits = {"k_scan_w": 1 << 19, "k_scan_r": 38400 * 32, "k_scan_g": 38400 * 32}
     if positions and (dom in ("k_scan_lds", "k_scan") or (dom in l1_bits and keys)):
-        per_pos = 1.0 if dom not in l1_bits else 1.0 - math.exp(-keys / float(l1_bits[dom]))
+        # the ribbon level-1 (sydelta_internal.hpp: 852000..1100000 keys unless SYDELTA_L1
+        # forces a layout) passes ~1/2 of the positions whatever the key count
+        l1_env = os.environ.get("SYDELTA_L1", "")
+        ribbon = dom in l1_bits and keys and (l1_env == "ribbon" or (l1_env != "bloom" and 852000 <= keys <= 1100000))
+        per_pos = 1.0 if dom not in l1_bits else 0.5 if ribbon else 1.0 - math.exp(-keys / float(l1_bits[dom]))
         req = positions * per_pos / launches_per_step  # filter-word requests per launch
         rate = req / (avg_ms * 1e-3)
         roof["l2_gather"] = {"requests_per_launch": int(req), "achieved": round(rate / 1e9, 2),
@@ -582,6 +587,7 @@ def roofline(prof: dict, steps: int, algo_step: dict, positions=None, keys=None,
                              "frac": round(rate / L2_GATHER_PEAK, 4),
                              "requests_per_position": round(per_pos, 4),
                              "model": ("one per window start" if dom not in l1_bits else
+                                       "window starts x ribbon level-1 pass rate 1/2" if ribbon else
                                        f"window starts x level-1 pass rate 1-exp(-keys/{l1_bits[dom]})")}
         pc = pmc_counters(dom, workload, block_size)
         if pc and pc.get("TCC_REQ_sum"):

@@ -705,7 +705,7 @@ static int index_create_impl(int device, const uint32_t* weak, const uint64_t* s
     const char* l1e = getenv("SYDELTA_L1");
     const bool want_rib = want_narrow && (l1e && !strcmp(l1e, "ribbon") ? true
                                           : l1e && !strcmp(l1e, "bloom") ? false
-                                                                          : nblocks >= kRibMinKeys);
+                                                                          : nblocks >= kRibMinKeys && nblocks <= kRibMaxKeys);
     const size_t sz_rib = want_rib ? al(4ull * kRibShards * kRibCap) + al(4ull * (kRibShards + 1)) + al(4 * nb) : 0;
     const size_t sz_fat = want_l1 ? al(16 * (size_t)sl) : 0;
     const size_t total = sz_weak + sz_strong + sz_filt + sz_l1 + sz_fat + 4 * sz_t + sz_order + sz_slot + sz_files +

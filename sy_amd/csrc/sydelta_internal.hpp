@@ -37,7 +37,7 @@ constexpr uint32_t kL1WordsR = 38400;
 // One bit of result: a non-key passes with probability ~1/2 however the bits are spent
 // (0.504 measured on Adler values of 1 Mi random 4 KiB blocks, tools/ribbon_sim.c), against
 // 1 - e^(-keys/1228800) for the one-hash Bloom of the same 150 KiB (0.574 at 1 Mi keys):
-// built when the index has at least kRibMinKeys blocks (the two cross at ~852 K keys).
+// built when the index has kRibMinKeys..kRibMaxKeys blocks (the two cross at ~852 K keys).
 // Homogeneous: every system is consistent, so no key set makes the build fail (a shard
 // loaded past its columns only passes more positions).
 constexpr uint32_t kRibShards = 1024;
@@ -46,6 +46,9 @@ constexpr uint32_t kRibWords = kRibShards * kRibBits / 32;  // 37888, + 1 pad wo
 static_assert(kRibWords + 1 <= kL1WordsR, "the ribbon fits k_scan_r's level-1 LDS area");
 constexpr uint32_t kRibCap = 2048;     // distinct keys listed per shard (mean 1024 at 1 Mi keys); more: overflow list
 constexpr uint64_t kRibMinKeys = 852000;
+// ... and at most kRibMaxKeys: beyond ~0.95 keys per column a shard's system is full and
+// passes nearly every position (the Bloom's 1 - e^(-keys/1228800) is then lower).
+constexpr uint64_t kRibMaxKeys = 1100000;
 // words of a level-1 filter: l1_wshift 1 marks k_scan_r's scaled-word layout, any other
 // value a power-of-two filter of 2^(32 - l1_wshift) words (18: k_scan_w's)
 constexpr size_t l1_total_words(uint32_t l1_wshift) {

@@ -4357,7 +4357,7 @@ hipError_t launch_scan(const uint8_t* d_buf, const ScanSeg* d_segs, uint32_t nse
         const hipError_t fe = hipFreeAsync(buf, s);
         return e != hipSuccess ? e : fe;
     }
-    // k_scan_r: one large file at n = 4096 (SYDELTA_SCAN_R_WAVES=12: three waves per SIMD)
+    // k_scan_r: one large file at n = 4096 (SYDELTA_SCAN_R_WAVES=8: two waves per SIMD)
     if (ix.l1 && ix.l1_wshift == 1 && n == kMaxN3) {
         static std::once_flag r_once;
         static hipError_t r_err = hipSuccess;
@@ -4376,7 +4376,8 @@ hipError_t launch_scan(const uint8_t* d_buf, const ScanSeg* d_segs, uint32_t nse
         });
         if (r_err != hipSuccess) return r_err;
         if (!ix.fat) return hipErrorInvalidValue;
-        static const int waves = getenv("SYDELTA_SCAN_R_WAVES") && atoi(getenv("SYDELTA_SCAN_R_WAVES")) == 12 ? 12 : 8;
+        // 12 waves (three per SIMD, 168 VGPRs): 9.72 ms at C3 against 10.37 with 8 (round 4)
+        static const int waves = getenv("SYDELTA_SCAN_R_WAVES") && atoi(getenv("SYDELTA_SCAN_R_WAVES")) == 8 ? 8 : 12;
         constexpr LdsR LR = ldsr_layout();
         // one workgroup per CU over contiguous host tiles, an even number each (runs are pairs)
         uint32_t per = (uint32_t)((ntiles + (uint64_t)r_cus - 1) / (uint64_t)r_cus);

@@ -76,11 +76,15 @@ def test_roofline_scan_r_modelled_requests():
     n = 1 << 32
     bits = 38400 * 32
     algo = bench.algo_bytes_per_step("c3", n, n, n)
-    r = bench.roofline({"k_scan_r": {"ms": 111.7, "count": 10}}, 10, algo, positions=n, keys=1 << 20)
+    # 512 Ki keys: the one-hash Bloom level-1
+    r = bench.roofline({"k_scan_r": {"ms": 111.7, "count": 10}}, 10, algo, positions=n, keys=1 << 19)
     g = r["l2_gather"]
-    assert abs(g["requests_per_position"] - (1 - math.exp(-(1 << 20) / bits))) < 1e-4
-    assert g["requests_per_launch"] == int(n * (1 - math.exp(-(1 << 20) / bits)))
+    assert abs(g["requests_per_position"] - (1 - math.exp(-(1 << 19) / bits))) < 1e-4
+    assert g["requests_per_launch"] == int(n * (1 - math.exp(-(1 << 19) / bits)))
     assert "level-1" in g["model"]
+    # 1 Mi keys: the ribbon level-1 passes half of the positions
+    r = bench.roofline({"k_scan_r": {"ms": 111.7, "count": 10}}, 10, algo, positions=n, keys=1 << 20)
+    assert r["l2_gather"]["requests_per_position"] == 0.5 and "ribbon" in r["l2_gather"]["model"]
     assert r["bound"] == "l2"  # the request rate, not HBM, binds it
     # without the key count no request rate is claimed
     r2 = bench.roofline({"k_scan_r": {"ms": 111.7, "count": 10}}, 10, algo, positions=n)
