@@ -23,6 +23,9 @@ hipError_t dev_malloc_async(void** p, size_t bytes, hipStream_t s);
 constexpr uint32_t kEmptyKey = 0xFFFFFFFFu;  // never a valid weak: A = weak & 0xFFFF <= 65520
 constexpr uint64_t kLdsFilterKeys = 16384;   // index sizes whose Bloom filter (<= 32 KiB) the scan keeps in LDS
 constexpr uint32_t kLdsFilterWordsMax = 8192;
+// k_scan_g's small-index mode keeps one file filter per wave in LDS: up to 4096 words
+// (16 KiB; files of up to 4 Ki blocks), eight waves per workgroup.
+constexpr uint32_t kSmallWords = 4096;
 // Level-1 filter of a single-file index for windows above scan_max_window() (k_scan_w):
 // 16384 words = 64 KiB = 2^19 bits, beside the wide kernel's two staged byte regions.
 constexpr uint32_t kL1WordsWide = 16384;

@@ -315,13 +315,13 @@ __global__ __launch_bounds__(256) void k_sig_batch(const uint8_t* __restrict__ b
 // ===========================================================================
 // Probe hashes of a weak value w = (B << 16) | A, each two 24-bit multiplies (full
 // rate; a 32-bit multiply is quarter rate and this runs once per scanned position):
-//   q = A*0x9E3779 + B*0x85EBCB  -> the level-1 bit (below) and the three bit
-//                                   positions of the level-2 word (bits 0..14)
-//   r = A*0xC2B2AF + B*0x27D4EB  -> the level-2 word (top bits)
-// Level 2 is a blocked Bloom filter of 32-bit words, 3 bits per key in the key's
-// word, 16 bits per key for large indexes: 1.1 % false passes on Adler values of
-// random 4 KiB blocks (the word from r and the bits from q: taking both from one
-// linear hash correlates them, 1.8 %).  Sizing (sydelta_index_create): up to 16 Ki
+//   q = A*0x9E3779 + B*0x85EBCB  -> the level-1 bit / ribbon shard and coefficients, and
+//                                   the five bit positions of the level-2 word (bits 0..24)
+//   r = A*0xC2B2AF + B*0x27D4EB  -> the level-2 word (top bits), the ribbon start
+// Level 2 is a blocked Bloom filter of 32-bit words, 5 bits per key in the key's word
+// (3 until round 3: 1.1 % false passes measured on Adler values of random 4 KiB blocks),
+// 16 bits per key for large indexes (the word from r and the bits from q: taking both
+// from one linear hash correlates them, 1.8 %).  Sizing (sydelta_index_create): up to 16 Ki
 // keys the filter is <= 32 KiB and the LDS-staged scan copies it into LDS; above
 // that it stays in HBM/L2.  FileIx::filt_off counts words; fwshift = 32 - log2(words).
 struct ProbeHash {
@@ -333,18 +333,23 @@ __device__ __forceinline__ ProbeHash probe_hash(uint32_t A, uint32_t B) {
     return {q, r};
 }
 __device__ __forceinline__ ProbeHash probe_hash(uint32_t w) { return probe_hash(w & 0xFFFFu, w >> 16); }
+// Five bits per key in its 32-bit word (q's five low 5-bit fields): 0.74 % false passes at
+// 16 bits per key against 1.08 % with three (Poisson keys per word), so a third fewer
+// exact-table lookups behind the scans' filters (round 4; each lookup of a level-2 false
+// pass misses L2 for a table line).
 __device__ __forceinline__ uint32_t filt_mask(uint32_t q) {
-    return (1u << (q & 31)) | (1u << ((q >> 5) & 31)) | (1u << ((q >> 10) & 31));
+    return (1u << (q & 31)) | (1u << ((q >> 5) & 31)) | (1u << ((q >> 10) & 31)) | (1u << ((q >> 15) & 31)) |
+           (1u << ((q >> 20) & 31));
 }
 __device__ __forceinline__ bool filt_pass(uint32_t word, uint32_t q) {
     const uint32_t m = filt_mask(q);
     return (word & m) == m;
 }
-// filt_pass as 0/1 with three bit extracts (the offset operand takes bits [4:0]): six
-// VALU where the mask form takes nine
+// filt_pass as 0/1 with five bit extracts (the offset operand takes bits [4:0])
 __device__ __forceinline__ uint32_t filt_bit(uint32_t word, uint32_t q) {
     return __builtin_amdgcn_ubfe(word, q, 1) & __builtin_amdgcn_ubfe(word, q >> 5, 1) &
-           __builtin_amdgcn_ubfe(word, q >> 10, 1);
+           __builtin_amdgcn_ubfe(word, q >> 10, 1) & __builtin_amdgcn_ubfe(word, q >> 15, 1) &
+           __builtin_amdgcn_ubfe(word, q >> 20, 1);
 }
 // Level-1 filters (held in LDS by k_scan_r / k_scan_w so that only the positions they
 // pass cost a level-2 request to L2): one bit per key, bit = q[0..4] (one bit extract;
@@ -2123,8 +2128,8 @@ __global__ __launch_bounds__(kWaves * 64, 1) void k_scan_r(ScanArgs a, uint32_t 
             const uint32_t fwshift = __builtin_amdgcn_readfirstlane(sc.fwshift);
 
             uint32_t xo[16], xi[16], xn[16];
-            load_chunk(sc.base, seg_len, run_start + 64ull * lane, xo);
-            load_chunk(sc.base, seg_len, run_start + n + 64ull * lane, xi);
+            load_chunk_nt(sc.base, seg_len, run_start + 64ull * lane, xo);  // read once: not kept in L2
+            load_chunk_nt(sc.base, seg_len, run_start + n + 64ull * lane, xi);
 #pragma unroll 1
             for (uint32_t k = 0; k < nwt; ++k) {
                 const uint64_t P = run_start + (uint64_t)k * kWTR;
@@ -2225,7 +2230,7 @@ __global__ __launch_bounds__(kWaves * 64, 1) void k_scan_r(ScanArgs a, uint32_t 
                     finish(kB3 * bi, Bt);
                     if (bi + 2 < kNBR) compute(kB3 * (bi + 2), Bt);
                     if (bi == 2 && k + 1 < nwt)
-                        load_chunk(sc.base, seg_len, P + n + kWTR + 64ull * lane, xn);
+                        load_chunk_nt(sc.base, seg_len, P + n + kWTR + 64ull * lane, xn);
                 }
                 passes += nrec - tile_rec;
                 if (nrec > tile_rec && !(kAblate && (a.ablate & 1)))
@@ -2391,13 +2396,82 @@ __device__ __forceinline__ void drain_g(const ScanArgs& a, const uint2* recs, ui
     lds_fence();
 }
 
+// kSmall's drain: exact-table lookups (table_find; small indexes carry no fat table), 64
+// per round; each weak hit goes to the deferred list as {window, key, kMulti | global
+// slot} (k_verify_w looks its candidates up in index order), or past the list's capacity
+// is verified here from global memory.
+__device__ __forceinline__ void drain_gs(const ScanArgs& a, const uint2* recs, uint32_t nr, uint4* wq,
+                                         unsigned long long& weak_hits, uint64_t run_start, const SegCtx& cur) {
+    const uint32_t lane = threadIdx.x & 63;
+    const uint64_t below = (1ull << lane) - 1;
+    __threadfence_block();  // this wave's record stores before its loads
+    uint32_t nwq = 0;
+    for (uint32_t base = 0; base < nr; base += 64) {
+        const uint32_t i = base + lane;
+        bool hit = false;
+        uint32_t pos = 0, gslot = 0;
+        if (i < nr) {
+            const volatile uint2* g = recs + i;
+            pos = g->x;
+            const uint32_t w = g->y;
+            if (run_start + pos < cur.pos_end && !(a.ablate & 16)) {
+                const int64_t sl = table_find(cur.keys, cur.bmask, w);
+                hit = sl >= 0;
+                gslot = (uint32_t)(cur.slot_off + (uint64_t)(sl < 0 ? 0 : sl));
+            }
+        }
+        const uint64_t m = __ballot(hit);
+        if (!m) continue;
+        const uint32_t cnt = __popcll(m);
+        weak_hits += cnt;
+        if (a.ablate & 8) continue;
+        unsigned long long k0 = 0;
+        if (lane == 0) k0 = atomicAdd(&a.counters[10], (unsigned long long)cnt);
+        k0 = shfl64(k0, 0);
+        const uint64_t slot = k0 + __popcll(m & below);
+        const bool deferred = hit && slot < a.wdef_cap;
+        if (deferred) {
+            const uint64_t p = run_start + pos;
+            WDef d;
+            d.at = (uint64_t)(cur.base - a.src) + p;
+            d.key = ((uint64_t)cur.seg_id << kSegShift) | (p - cur.pos_begin);
+            d.cand = kMulti | gslot;
+            d.pad = 0;
+            d.strong = 0;
+            a.wdef[slot] = d;
+        }
+        const uint64_t mi = __ballot(hit && !deferred);
+        if (!mi) continue;
+        const uint32_t ci = __popcll(mi);
+        const uint32_t rank = __popcll(mi & below);
+        const uint4 e = make_uint4(pos, kMulti | gslot, 0, 0);
+        const bool mine = hit && !deferred;
+        if (nwq + ci > (uint32_t)kWQ3) {
+            verify_l1<false>(a, wq, nwq, nullptr, run_start, cur);
+            nwq = 0;
+        }
+        if (ci > (uint32_t)kWQ3) {
+            if (mine && rank < (uint32_t)kWQ3) wq[rank] = e;
+            verify_l1<false>(a, wq, kWQ3, nullptr, run_start, cur);
+            if (mine && rank >= (uint32_t)kWQ3) wq[rank - kWQ3] = e;
+            nwq = ci - kWQ3;
+        } else {
+            if (mine) wq[nwq + rank] = e;
+            nwq += ci;
+        }
+    }
+    verify_l1<false>(a, wq, nwq, nullptr, run_start, cur);
+    lds_fence();
+}
+
 struct LdsG {
     uint32_t l1, ntab, wq, ctr, total;  // byte offsets
 };
-__host__ __device__ constexpr LdsG ldsg_layout() {
+// small_words: kSmall's per-wave filter slot (the largest file filter of the index), else 0
+__host__ __device__ constexpr LdsG ldsg_layout(uint32_t small_words = 0) {
     LdsG L{};
     uint32_t o = 0;
-    L.l1 = o; o += kL1WordsR * 4;
+    L.l1 = o; o += small_words ? (kTR / 64) * small_words * 4 : kL1WordsR * 4;
     L.ntab = o; o += 256 * 4;
     L.wq = o; o += (kTR / 64) * kWQ3 * 16;
     L.ctr = o; o += 16;
@@ -2409,10 +2483,14 @@ static_assert(ldsg_layout().total <= 160 * 1024 - 256, "k_scan_g's LDS");
 // per: host tiles per workgroup (a multiple of rt); rt: host tiles per run (the unit a wave
 // takes from the workgroup's counter, sized so the run's first window, summed from global
 // memory, is a small part of the run's reads).
-template <bool kAblate, bool kRib>
-__global__ __launch_bounds__(kTR, 2) void k_scan_g(ScanArgs a, uint32_t per, uint32_t rt) {
+// kSmall: small indexes (one or many files, each with its Bloom filter of <= kSmallWords
+// words): no level-1 filter and no level-2 loads; each wave copies the filter of the file
+// it scans into its own LDS slot (small_words words) and tests every position there;
+// passes are looked up in the exact table (drain_gs).  Replaces k_scan_lds for them.
+template <bool kAblate, bool kRib, bool kSmall>
+__global__ __launch_bounds__(kTR, 2) void k_scan_g(ScanArgs a, uint32_t per, uint32_t rt, uint32_t small_words) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-    constexpr LdsG L = ldsg_layout();
+    const LdsG L = ldsg_layout(kSmall ? small_words : 0u);
     const uint32_t n = a.n;
     const uint32_t* l1 = (const uint32_t*)(smem + L.l1);
     uint32_t* ntab = (uint32_t*)(smem + L.ntab);
@@ -2422,11 +2500,12 @@ __global__ __launch_bounds__(kTR, 2) void k_scan_g(ScanArgs a, uint32_t per, uin
     uint32_t* ctr = (uint32_t*)(smem + L.ctr);
     const uint32_t gwave = blockIdx.x * (kTR / 64) + wid;
     uint2* rec = a.rrec + (size_t)gwave * kWTR;  // this wave's pass records (one wave tile)
+    uint32_t* fslot = (uint32_t*)(smem + L.l1) + (size_t)wid * small_words;  // kSmall: this wave's filter
 
     const uint32_t t_begin = blockIdx.x * per;
     const uint32_t t_end = min(a.ntiles, t_begin + per);
     if (t_begin >= t_end) return;
-    {
+    if (!kSmall) {
         const uint4* g = (const uint4*)a.l1;
         uint4* d = (uint4*)(smem + L.l1);
 #pragma unroll 4
@@ -2437,7 +2516,7 @@ __global__ __launch_bounds__(kTR, 2) void k_scan_g(ScanArgs a, uint32_t per, uin
     __syncthreads();  // the only barrier: the waves run independently from here
 
     unsigned long long passes = 0, weak_hits = 0;
-    uint32_t nrec = 0, si_hint = 0;
+    uint32_t nrec = 0, si_hint = 0, slot_file = 0xFFFFFFFFu;
     const uint64_t below = (1ull << lane) - 1;
 #pragma unroll 1
     for (;;) {
@@ -2485,11 +2564,19 @@ __global__ __launch_bounds__(kTR, 2) void k_scan_g(ScanArgs a, uint32_t per, uin
                 (void*)(uintptr_t)(((uint64_t)fp_hi << 32) | fp_lo), (short)0,
                 (int)__builtin_amdgcn_readfirstlane(sc.fwords * 4), 0x00020000);
             const uint32_t fwshift = __builtin_amdgcn_readfirstlane(sc.fwshift);
+            if (kSmall && S.file != slot_file) {  // this file's filter into the wave's slot
+                slot_file = S.file;
+                lds_fence();  // the previous file's words are no longer read
+                const uint4* g = (const uint4*)sc.filt;
+                uint4* d = (uint4*)fslot;
+                for (uint32_t i = lane; i < sc.fwords / 4; i += 64) d[i] = g[i];
+                lds_fence();
+            }
 
             uint32_t A0, B0;  // the window at the current wave tile's start
             window_at(sc.base, seg_len, run_start, n, A0, B0);
             uint32_t xo[16], xi[16], no_[16], ni_[16];
-            load_chunk(sc.base, seg_len, run_start + 64ull * lane, xo);
+            load_chunk_nt(sc.base, seg_len, run_start + 64ull * lane, xo);  // the bytes' last read
             load64_u(sc.base, seg_len, run_start + n + 64ull * lane, xi);
 #pragma unroll 1
             for (uint32_t k = 0; k < nwt; ++k) {
@@ -2535,7 +2622,9 @@ __global__ __launch_bounds__(kTR, 2) void k_scan_g(ScanArgs a, uint32_t per, uin
                         const ProbeHash h = probe_hash(am, bm);
                         Bt.hq[t2] = h.q;
                         rr[t2] = h.r;
-                        if (kRib) {
+                        if (kSmall) {
+                            Bt.w2[t2] = fslot[h.r >> fwshift];  // the file's whole filter, tested in finish
+                        } else if (kRib) {
                             bo[t2] = rib_bit(h.q, h.r);
                             w1[t2] = l1[bo[t2] >> 5];
                             w1b[t2] = l1[(bo[t2] >> 5) + 1];
@@ -2548,7 +2637,7 @@ __global__ __launch_bounds__(kTR, 2) void k_scan_g(ScanArgs a, uint32_t per, uin
                         bm = min(v, min(v - kMod, v - 2 * kMod));
                     }
 #pragma unroll
-                    for (int t2 = 0; t2 < kB3; ++t2) {
+                    for (int t2 = 0; t2 < kB3 && !kSmall; ++t2) {
                         uint32_t p1;
                         if (kRib) {
                             const uint32_t win = __builtin_amdgcn_alignbit(w1b[t2], w1[t2], bo[t2]);
@@ -2585,7 +2674,7 @@ __global__ __launch_bounds__(kTR, 2) void k_scan_g(ScanArgs a, uint32_t per, uin
                     finish(kB3 * bi, Bt);
                     if (bi + 2 < kNBR) compute(kB3 * (bi + 2), Bt);
                     if (bi == 2 && k + 1 < nwt) {
-                        load_chunk(sc.base, seg_len, P + kWTR + 64ull * lane, no_);
+                        load_chunk_nt(sc.base, seg_len, P + kWTR + 64ull * lane, no_);
                         load64_u(sc.base, seg_len, P + kWTR + n + 64ull * lane, ni_);
                     }
                 }
@@ -2593,8 +2682,10 @@ __global__ __launch_bounds__(kTR, 2) void k_scan_g(ScanArgs a, uint32_t per, uin
                 A0 = __builtin_amdgcn_readlane(am, 63);
                 B0 = __builtin_amdgcn_readlane(bm, 63);
                 passes += nrec - tile_rec;
-                if (nrec > tile_rec && !(kAblate && (a.ablate & 1)))
-                    drain_g(a, rec + tile_rec, nrec - tile_rec, wq, weak_hits, run_start, sc);
+                if (nrec > tile_rec && !(kAblate && (a.ablate & 1))) {
+                    if (kSmall) drain_gs(a, rec + tile_rec, nrec - tile_rec, wq, weak_hits, run_start, sc);
+                    else drain_g(a, rec + tile_rec, nrec - tile_rec, wq, weak_hits, run_start, sc);
+                }
                 nrec = tile_rec;
 #pragma unroll
                 for (int i = 0; i < 16; ++i) {
@@ -4302,14 +4393,18 @@ hipError_t launch_scan(const uint8_t* d_buf, const ScanSeg* d_segs, uint32_t nse
     a.l1 = ix.l1;
     a.fat = ix.fat;
     // k_scan_g: one file with a level-1 filter (more than kLdsFilterKeys blocks, or windows
-    // above the LDS-staged layouts) at any n but 4096; weak hits verified by k_verify_w
-    if (ix.l1 && ix.l1_wshift == 1 && ix.fat && ix.nfiles == 1 && n != kMaxN3) {
+    // above the LDS-staged layouts) at any n but 4096, or (kSmall) indexes whose file
+    // filters are <= kSmallWords words at any n <= kMaxN2; weak hits verified by k_verify_w
+    static const bool small_off = getenv("SYDELTA_SCAN_SMALL") && getenv("SYDELTA_SCAN_SMALL")[0] == '0';
+    const bool small = !ix.l1 && ix.max_fwords <= kSmallWords && n <= kMaxN2 && !small_off;
+    if ((ix.l1 && ix.l1_wshift == 1 && ix.fat && ix.nfiles == 1 && n != kMaxN3) || small) {
         static std::once_flag g_once;
         static hipError_t g_err = hipSuccess;
         static int g_cus = 256;
         std::call_once(g_once, [] {
-            for (const void* f : {(const void*)k_scan_g<false, false>, (const void*)k_scan_g<true, false>,
-                                  (const void*)k_scan_g<false, true>, (const void*)k_scan_g<true, true>})
+            for (const void* f : {(const void*)k_scan_g<false, false, false>, (const void*)k_scan_g<true, false, false>,
+                                  (const void*)k_scan_g<false, true, false>, (const void*)k_scan_g<true, true, false>,
+                                  (const void*)k_scan_g<false, false, true>, (const void*)k_scan_g<true, false, true>})
                 if (g_err == hipSuccess)
                     g_err = hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024 - 256);
             int dev = 0, cus = 0;
@@ -4318,7 +4413,8 @@ hipError_t launch_scan(const uint8_t* d_buf, const ScanSeg* d_segs, uint32_t nse
                 g_cus = cus;
         });
         if (g_err != hipSuccess) return g_err;
-        constexpr LdsG LG = ldsg_layout();
+        const uint32_t small_words = small ? std::max<uint32_t>(ix.max_fwords, 64u) : 0u;
+        const LdsG LG = ldsg_layout(small_words);
         // runs of rt host tiles: the run's first window (n bytes from global memory) <= 1/8 of
         // its reads; each workgroup a contiguous range of whole runs
         uint32_t rt = 2;
@@ -4340,13 +4436,12 @@ hipError_t launch_scan(const uint8_t* d_buf, const ScanSeg* d_segs, uint32_t nse
         a.wdef = (WDef*)((uint8_t*)buf + rec_bytes);
         {
             ProfScope ps(prof, s, "k_scan_g");
-            if (ix.l1_ribbon) {
-                if (a.ablate) hipLaunchKernelGGL((k_scan_g<true, true>), dim3(grid), dim3(kTR), LG.total, s, a, per, rt);
-                else hipLaunchKernelGGL((k_scan_g<false, true>), dim3(grid), dim3(kTR), LG.total, s, a, per, rt);
-            } else {
-                if (a.ablate) hipLaunchKernelGGL((k_scan_g<true, false>), dim3(grid), dim3(kTR), LG.total, s, a, per, rt);
-                else hipLaunchKernelGGL((k_scan_g<false, false>), dim3(grid), dim3(kTR), LG.total, s, a, per, rt);
-            }
+            const dim3 gd(grid), bd(kTR);
+#define LAUNCH_G(AB, RB, SM) hipLaunchKernelGGL((k_scan_g<AB, RB, SM>), gd, bd, LG.total, s, a, per, rt, small_words)
+            if (small) { if (a.ablate) LAUNCH_G(true, false, true); else LAUNCH_G(false, false, true); }
+            else if (ix.l1_ribbon) { if (a.ablate) LAUNCH_G(true, true, false); else LAUNCH_G(false, true, false); }
+            else { if (a.ablate) LAUNCH_G(true, false, false); else LAUNCH_G(false, false, false); }
+#undef LAUNCH_G
         }
         e = hipGetLastError();
         if (e == hipSuccess && !(a.ablate & 1)) {
