@@ -695,7 +695,7 @@ static int index_create_impl(int device, const uint32_t* weak, const uint64_t* s
     // other): one file with more keys than an LDS-resident Bloom filter takes
     const bool want_narrow = nfiles == 1 && nblocks > kLdsFilterKeys;
     // windows above the LDS-staged scans' limit, one file (the production block sizes of
-    // files over 64 MiB, mod.rs:20-23): k_scan_w's level-1 filter and fat table
+    // files over 64 MiB, mod.rs:20-23): k_scan_g's level-1 filter and fat table
     const bool want_wide = nfiles == 1 && block_size > scan_max_window() && scan_wide_mode() != 0;
     const bool want_l1 = want_narrow || want_wide;
     const uint32_t l1_wshift = 1u;  // kL1WordsR words (k_scan_r / k_scan_g)
@@ -950,7 +950,7 @@ bool phase_probe_on() {
     return e && e[0] == '1';
 }
 
-// The index carries k_scan_w's level-1 filter (one file, window above the LDS-staged
+// The index carries k_scan_g's level-1 filter (one file, window above the LDS-staged
 // scans' limit) and SYDELTA_SCAN_WIDE does not turn it off.
 bool wide_scan(const sydelta_index* x) {
     return x->ix.l1 != nullptr && scan_wide_mode() != 0;
@@ -1211,7 +1211,7 @@ int Classifier::scan(const std::vector<std::array<uint64_t, 3>>& ranges) {
     double t_kern = 0, t_d2h = 0;
     const uint64_t tile = scan_tile_positions();
     const uint64_t seg_max = (1ull << 31) / tile * tile;
-    // windows above the LDS-staged layouts: k_scan_w when the index has its level-1
+    // windows above the LDS-staged layouts: k_scan_g when the index has its level-1
     // filter (single file, built with SYDELTA_SCAN_WIDE != 0), else the per-thread k_scan
     const bool wide_w = n > scan_max_window() && wide_scan(ix);
     const bool wide = n > scan_max_window() && !wide_w;

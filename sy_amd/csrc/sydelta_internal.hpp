@@ -26,9 +26,6 @@ constexpr uint32_t kLdsFilterWordsMax = 8192;
 // k_scan_g's small-index mode keeps one file filter per wave in LDS: up to 4096 words
 // (16 KiB; files of up to 4 Ki blocks), eight waves per workgroup.
 constexpr uint32_t kSmallWords = 4096;
-// Level-1 filter of a single-file index for windows above scan_max_window() (k_scan_w):
-// 16384 words = 64 KiB = 2^19 bits, beside the wide kernel's two staged byte regions.
-constexpr uint32_t kL1WordsWide = 16384;
 // k_scan_r's level-1 filter (one large file at n = 4096): 38400 words = 150 KiB, the LDS
 // left when the tile's bytes stay in registers, word = l1r_word(q) (l1_wshift 1 marks it).
 constexpr uint32_t kL1WordsR = 38400;
@@ -53,7 +50,7 @@ constexpr uint64_t kRibMinKeys = 852000;
 // passes nearly every position (the Bloom's 1 - e^(-keys/1228800) is then lower).
 constexpr uint64_t kRibMaxKeys = 1100000;
 // words of a level-1 filter: l1_wshift 1 marks k_scan_r's scaled-word layout, any other
-// value a power-of-two filter of 2^(32 - l1_wshift) words (18: k_scan_w's)
+// value a power-of-two filter of 2^(32 - l1_wshift) words
 constexpr size_t l1_total_words(uint32_t l1_wshift) {
     return l1_wshift == 1 ? (size_t)kL1WordsR : (size_t)1 << (32 - l1_wshift);
 }
@@ -88,8 +85,8 @@ struct ScanSeg {
 struct DeviceIndex {
     uint32_t* filt = nullptr;   // blocked Bloom filters (probe_hash/filt_mask), per-file 2^k 32-bit words
     uint32_t* l1 = nullptr;     // level-1 filter: single-file indexes above kLdsFilterKeys keys at bs 4096
-                                // (k_scan_r) or with windows above scan_max_window() (k_scan_w)
-    uint32_t l1_wshift = 1;     // 1: kL1WordsR words, l1r_word(q); 18: kL1WordsWide words, q >> 18
+                                // (k_scan_r, k_scan_g) or with windows above scan_max_window() (k_scan_g)
+    uint32_t l1_wshift = 1;     // 1: kL1WordsR words, l1r_word(q)
     uint32_t l1_ribbon = 0;     // with l1_wshift 1: the words hold the ribbon (kRibWords), not a Bloom filter
     uint32_t* rib_keys = nullptr;  // ribbon build: kRibShards lists of kRibCap distinct keys
     uint32_t* rib_cnt = nullptr;   // kRibShards + 1 counts (the last: the overflow list's)
@@ -136,7 +133,7 @@ hipError_t launch_index_build(const uint32_t* d_weak, const uint64_t* d_strong, 
                               Profiler* prof);
 uint64_t scan_tile_positions();  // positions per tile of the LDS-staged scan
 // SYDELTA_SCAN_WIDE=0: windows above scan_max_window() take the per-thread k_scan
-// instead of the LDS-staged k_scan_w (read when the index is built and per call)
+// instead of the register-fed k_scan_g (read when the index is built and per call)
 int scan_wide_mode();
 uint32_t scan_max_window();      // largest block size the LDS-staged scan handles
 // Scratch the LDS-staged scan needs: filter-pass queues, scan_queue_entries() uint2

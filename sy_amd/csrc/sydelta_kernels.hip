@@ -351,7 +351,7 @@ __device__ __forceinline__ uint32_t filt_bit(uint32_t word, uint32_t q) {
            __builtin_amdgcn_ubfe(word, q >> 10, 1) & __builtin_amdgcn_ubfe(word, q >> 15, 1) &
            __builtin_amdgcn_ubfe(word, q >> 20, 1);
 }
-// Level-1 filters (held in LDS by k_scan_r / k_scan_w so that only the positions they
+// Level-1 filters (held in LDS by k_scan_r / k_scan_g so that only the positions they
 // pass cost a level-2 request to L2): one bit per key, bit = q[0..4] (one bit extract;
 // the level-2 word tests q[0..4] too, but in an unrelated word).
 __device__ __forceinline__ uint32_t l1_test(uint32_t word, uint32_t q) { return __builtin_amdgcn_ubfe(word, q, 1); }
@@ -709,7 +709,7 @@ struct ScanArgs {
     uint32_t nchunks;    // LDS chunk slots per tile (k_scan)
     // probe structures (concatenated over files)
     const uint32_t* filt;
-    const uint32_t* l1;       // level-1 filter (k_scan_r: kL1WordsR words, k_scan_w: kL1WordsWide)
+    const uint32_t* l1;       // level-1 filter (k_scan_r / k_scan_g: kL1WordsR words)
     const uint4* fat;         // k_scan_l1: {key, first candidate | kMulti+slot, strong} per slot
     const uint32_t* keys;
     const uint32_t* start;
@@ -722,13 +722,13 @@ struct ScanArgs {
     uint64_t out_cap;
     unsigned long long* counters;  // [0] verified hits, [1] weak hits, [2] filter passes, [4..8) phase cycles
     uint2* gfq;          // k_scan_lds: per-wave filter-pass queues in HBM/L2, kGFQ entries each
-    struct WDef* wdef;   // k_scan_w: weak hits whose verification k_verify_w does (count: counters[10])
+    struct WDef* wdef;   // k_scan_g: weak hits whose verification k_verify_w does (count: counters[10])
     uint64_t wdef_cap;
     // k_scan_r: each wave's level-2 passes of one wave tile {position in run, weak}
     uint2* rrec;
 };
 
-// A weak hit of k_scan_w, verified after the scan by k_verify_w.
+// A weak hit of k_scan_g, verified after the scan by k_verify_w.
 struct WDef {
     uint64_t at;      // byte offset of the window in ScanArgs::src
     uint64_t key;     // its hit key: (segment << kSegShift) | position - segment start
@@ -1608,7 +1608,7 @@ __global__ __launch_bounds__(kT2, kWgPerCu) void k_scan_lds(ScanArgs a, uint32_t
 }
 
 // ===========================================================================
-// Shared by the level-1-filter scans (k_scan_r, k_scan_w)
+// Shared by the level-1-filter scans (k_scan_r, k_scan_g)
 // ===========================================================================
 // The BASELINE C3 shape: 2^32 window starts against 2^20 basis keys, every one a
 // literal.  Each position must test its weak value against the key set.  With the
@@ -1663,7 +1663,7 @@ __device__ __forceinline__ bool fat_find_k(const uint32_t* __restrict__ keys, co
 // kMulti+slot, strong lo, hi}: XXH3 of the window from the LDS rows (four windows per
 // wave, one per 16-lane row, when n % 64 == 0 and n >= 256), then the first candidate
 // in index order with equal strong (generator.rs:127-133); verified hits to the output.
-// kWinLds false (k_scan_w): the windows are longer than the staged rows; hash them from
+// kWinLds false (k_scan_g): the windows are not in LDS; hash them from
 // global memory.
 template <bool kWinLds = true>
 __device__ __forceinline__ void verify_l1(const ScanArgs& a, uint4* wq, uint32_t nwq, const uint32_t* rows,
@@ -2263,7 +2263,8 @@ __global__ __launch_bounds__(kWaves * 64, 1) void k_scan_r(ScanArgs a, uint32_t 
 // (window_at).  The level-1 filter (Bloom or ribbon), level-2 loads and the keys-only
 // lookups are k_scan_r's; a weak hit's window is not in the registers, so it goes to the
 // deferred list (WDef) that k_verify_w hashes after the scan (hits the list cannot take
-// are verified inline from global memory).  Replaces k_scan_w (windows above 8 KiB) and
+// are verified inline from global memory).  Replaces round 3's k_scan_w (windows above 8 KiB:
+// 8.63 + 1.29 ms per 4 GiB at bs 65536) and
 // k_scan_lds in global-filter mode for single-file indexes.
 
 // 64 bytes at byte offset q of src (any alignment) through 16-byte granule loads and
@@ -2700,97 +2701,9 @@ __global__ __launch_bounds__(kTR, 2) void k_scan_g(ScanArgs a, uint32_t per, uin
 }
 
 // ===========================================================================
-// K2+K4 for windows above kMaxN2: k_scan_w
+// Deferred verification of weak hits (k_scan_g)
 // ===========================================================================
-// sy's own block size is calculate_block_size(size) = sqrt(size) clamped to [512, 128 Ki]
-// (mod.rs:20-23, called at ssh.rs:951), so every file above 64 MiB is matched with a
-// window longer than the LDS-staged scans' tile.  Such a window does not fit the tile's
-// rows, so a tile of kTileW positions stages two byte regions instead of one: the bytes
-// that leave the tile's windows, [T0, T0 + kTileW) (rows 0..255), and the bytes that
-// enter them, [T0 + n, T0 + n + kTileW) (rows 256..512, staged from the 16-byte granule
-// that holds T0 + n, in-byte j at region offset o_n + j, o_n = n mod 16).  Windows are
-// carried from tile to tile instead of summed: the workgroup keeps (S, B) of the window
-// at T0, S = sum x, B = sum (n - i) x_i, and thread t's first window [T0 + 64t, +n)
-// follows in closed form (rolling.rs:66-79 applied d = 64t times):
-//   S(d) = S0 + In(d) - Out(d)
-//   B(d) = B0 + d S0 - n Out(d) + sum_{j<d} (d - j) in_j - sum_{j<d} (d - j) out_j
-// from prefix sums of the two regions' 64-byte rows (two wave scans each, the waves'
-// totals through LDS).  The window at a segment's first tile (or at the workgroup's
-// first) is summed from global memory.  A tile is two host tiles (32 Ki positions, 64
-// per thread: the window phase, drain round trip and barrier are paid once per 32 Ki
-// positions), as in k_scan_l2, whose trimmed roll and queue fast path it shares; the
-// level-1 filter is kL1WordsWide words in LDS (word q >> 18), the level-2 buffer loads
-// and the fat-table drain are k_scan_l1's; weak hits are verified from global memory
-// (wave_hash_long: the window is not in LDS).  Round 3's first version (16 Ki-position
-// tiles, k_scan_l1's untrimmed roll, 32 VGPRs spilled) took 25.98 ms per 4 GiB at bs
-// 65536 with every position literal.
-// k_scan_w's drain: fat-table lookups of this wave's queued level-2 passes (as
-// drain_l1); each weak hit is appended to the deferred list (a.wdef) for k_verify_w
-// instead of being hashed here.  A window above 8 KiB is hashed from global memory by
-// one wave at the latency of its dependent loads (tens of microseconds for 64 KiB), and
-// measured at bs 65536 that made the other seven waves wait at the tile's barrier for
-// more than half of the kernel (phase cycles, round 3).  Hits the full list cannot take
-// (dense data) are verified here, as drain_l1 does.
-__device__ __forceinline__ void drain_w(const ScanArgs& a, const uint2* fq, uint32_t nfq, uint4* wq,
-                                        unsigned long long& weak_hits, uint64_t tile_start, const SegCtx& cur) {
-    const uint32_t lane = threadIdx.x & 63;
-    const uint64_t below = (1ull << lane) - 1;
-    lds_fence();
-    uint32_t nwq = 0;
-    for (uint32_t base = 0; base < nfq; base += 64) {
-        const uint32_t i = base + lane;
-        bool hit = false;
-        uint4 rec = make_uint4(0, 0, 0, 0);
-        uint32_t tp = 0;
-        if (i < nfq) {
-            const uint2 e = fq[i];  // {position in tile, weak}
-            tp = e.x;
-            if (tile_start + e.x < cur.pos_end) hit = fat_find(cur.fat, cur.bmask, e.y, rec);
-        }
-        const uint64_t m = __ballot(hit);
-        if (!m) continue;
-        const uint32_t cnt = __popcll(m);
-        weak_hits += cnt;
-        unsigned long long k0 = 0;
-        if (lane == 0) k0 = atomicAdd(&a.counters[10], (unsigned long long)cnt);
-        k0 = shfl64(k0, 0);
-        const uint64_t slot = k0 + __popcll(m & below);
-        const bool deferred = hit && slot < a.wdef_cap;
-        if (deferred) {
-            const uint64_t pos = tile_start + tp;
-            WDef d;
-            d.at = (uint64_t)(cur.base - a.src) + pos;
-            d.key = ((uint64_t)cur.seg_id << kSegShift) | (pos - cur.pos_begin);
-            d.cand = rec.y;
-            d.pad = 0;
-            d.strong = ((uint64_t)rec.w << 32) | rec.z;
-            a.wdef[slot] = d;
-        }
-        const uint64_t mi = __ballot(hit && !deferred);
-        if (!mi) continue;
-        const uint32_t ci = __popcll(mi);
-        const uint32_t rank = __popcll(mi & below);
-        if (nwq + ci > (uint32_t)kWQ3) {
-            verify_l1<false>(a, wq, nwq, nullptr, tile_start, cur);
-            nwq = 0;
-        }
-        const uint4 e = make_uint4(tp, rec.y, rec.z, rec.w);
-        const bool mine = hit && !deferred;
-        if (ci > (uint32_t)kWQ3) {  // more than wq holds: two halves
-            if (mine && rank < (uint32_t)kWQ3) wq[rank] = e;
-            verify_l1<false>(a, wq, kWQ3, nullptr, tile_start, cur);
-            if (mine && rank >= (uint32_t)kWQ3) wq[rank - kWQ3] = e;
-            nwq = ci - kWQ3;
-        } else {
-            if (mine) wq[nwq + rank] = e;
-            nwq += ci;
-        }
-    }
-    verify_l1<false>(a, wq, nwq, nullptr, tile_start, cur);
-    lds_fence();
-}
-
-// The deferred weak hits of a k_scan_w launch (counters[10] of them, at most wdef_cap):
+// The deferred weak hits of a k_scan_g launch (counters[10] of them, at most wdef_cap):
 // XXH3 of each window (four windows per wave, one per 16-lane row, when n % 64 == 0;
 // else one per wave), then the first candidate in index order with equal strong
 // (generator.rs:127-133); verified hits to the output like verify_l1.
@@ -2852,402 +2765,6 @@ __global__ __launch_bounds__(256) void k_verify_w(ScanArgs a) {
             a.hit_val[k] = best;
         }
     }
-}
-
-constexpr int kTW = 512;                        // threads per workgroup (8 waves)
-constexpr int kRW = 64;                         // positions per thread = one 64-byte row
-constexpr int kTileW = kTW * kRW;               // 32768 positions per tile = two host tiles
-constexpr int kRowsW = 2 * kTW + 1;             // out rows 0..511, in rows 512..1023, row 1024: 16 bytes
-constexpr int kNBW = kRW / kB3;                 // batches per thread per tile
-static_assert(kTileW == 2 * kTile2, "a k_scan_w tile is two host tiles");
-
-struct LdsW {
-    uint32_t ntab, fq, wq, wt, red, l1, total;  // byte offsets
-};
-__host__ __device__ constexpr LdsW ldsw_layout() {
-    LdsW L{};
-    uint32_t o = kRowsW * kRowDw * 4;
-    o = (o + 15) & ~15u; L.ntab = o; o += 256 * 4;
-    L.fq = o; o += (kTW / 64) * kFQ3 * 8;
-    L.wq = o; o += (kTW / 64) * kWQ3 * 16;
-    L.wt = o; o += (kTW / 64) * 4 * 4;   // per wave: totals of its rows' four sums
-    L.red = o; o += (kTW / 64) * 16;     // per wave: a fresh window's (S, B) partial sums
-    o = (o + 15) & ~15u; L.l1 = o; o += kL1WordsWide * 4;
-    L.total = o;
-    return L;
-}
-static_assert(ldsw_layout().total <= 160 * 1024 - 256, "k_scan_w's LDS");
-
-// Byte sum and weighted sum (weights 0..4k-1) of the first k dwords of x, bytes below
-// `lim` only (lim <= 4k).
-__device__ __forceinline__ void half_sums(const uint32_t* x, int k, uint32_t lim, uint32_t& s, uint32_t& u) {
-    s = 0;
-    u = 0;
-    for (int i = 0; i < k; ++i) {
-        const uint32_t b = 4u * (uint32_t)i;
-        const uint32_t keep = lim >= b + 4 ? 0xFFFFFFFFu : lim <= b ? 0u : (0xFFFFFFFFu >> (8 * (b + 4 - lim)));
-        const uint32_t d = x[i] & keep;
-        s = udot4(d, 0x01010101u, s);
-        u = udot4(d, offw(i), u);
-    }
-}
-
-template <bool kTiming>
-__global__ __launch_bounds__(kTW, 2) void k_scan_w(ScanArgs a, uint32_t per) {
-    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-    const uint32_t n = a.n;
-    constexpr LdsW L = ldsw_layout();
-    uint32_t* rows = (uint32_t*)smem;
-    uint32_t* ntab = (uint32_t*)(smem + L.ntab);
-    uint32_t* wt = (uint32_t*)(smem + L.wt);
-    unsigned long long* red = (unsigned long long*)(smem + L.red);
-    const uint32_t* l1 = (const uint32_t*)(smem + L.l1);
-    const uint32_t tid = threadIdx.x;
-    const uint32_t lane = tid & 63, wid = tid >> 6;
-    uint2* fq = (uint2*)(smem + L.fq) + (size_t)wid * kFQ3;
-    uint4* wq = (uint4*)(smem + L.wq) + (size_t)wid * kWQ3;
-
-    const uint32_t t_begin = blockIdx.x * per;
-    const uint32_t t_end = min(a.ntiles, t_begin + per);
-    if (t_begin >= t_end) return;
-    {
-        const uint4* g = (const uint4*)a.l1;
-        uint4* d = (uint4*)(smem + L.l1);
-#pragma unroll 4
-        for (uint32_t i = tid; i < kL1WordsWide / 4; i += kTW) d[i] = g[i];
-    }
-    for (uint32_t i = tid; i < 256; i += kTW) ntab[i] = kMod - 1 - (a.nm * i) % kMod;
-    const uint32_t on = n & 15;                      // in-byte 0 at in-region offset on
-    const uint32_t nal = n - on;                     // in-region start relative to T0
-    const uint32_t sh = n & 3;
-    const uint32_t rel0 = tid * kRW;
-    const uint32_t orow = tid * kRowDw;              // this thread's out bytes: row tid
-    const uint32_t din0 = (kTileW + on + rel0) >> 2; // ... and its first in dword (rows 512..)
-    const uint32_t nmod = a.nm;
-    unsigned long long passes = 0, weak_hits = 0;
-    uint32_t nfq = 0;
-    unsigned long long tm[6] = {0, 0, 0, 0, 0, 0}, l1pass = 0;
-    unsigned long long tprev = kTiming ? __builtin_amdgcn_s_memtime() : 0;
-#define PHASE_MARKW(k)                                                 \
-    if (kTiming) {                                                     \
-        const unsigned long long tnow = __builtin_amdgcn_s_memtime(); \
-        tm[k] += tnow - tprev;                                         \
-        tprev = tnow;                                                  \
-    }
-
-    auto seg_ctx = [&](uint32_t tile, uint32_t si0, SegCtx& sc, uint32_t& si, uint64_t& tile_start,
-                       uint64_t& seg_len) {
-        uint32_t lo = si0, hi = a.nsegs;
-        while (hi - lo > 1) {
-            const uint32_t mid = (lo + hi) >> 1;
-            if (a.segs[mid].tile_base <= tile) lo = mid; else hi = mid;
-        }
-        si = lo;
-        const ScanSeg S = a.segs[si];
-        const FileIx F = a.files[S.file];
-        sc.base = a.src + S.src;
-        sc.pos_begin = S.pos_begin;
-        sc.pos_end = S.pos_end;
-        sc.keys = a.keys + F.slot_off;
-        sc.fat = a.fat + F.slot_off;
-        sc.slot_off = F.slot_off;
-        sc.bmask = F.bmask;
-        sc.seg_id = si;
-        sc.fwshift = F.fwshift;
-        sc.filt = a.filt + F.filt_off;
-        sc.fwords = 1u << (32 - F.fwshift);
-        tile_start = S.pos_begin + (uint64_t)(tile - S.tile_base) * kTile2;
-        seg_len = S.len;
-    };
-    // host tiles this tile covers: 2 when host tile t+1 is in this workgroup's range and
-    // in the same segment as t (segment sidx); a lone host tile ends a segment or the range,
-    // so its window is never carried
-    auto span_of = [&](uint32_t t, uint32_t sidx) -> uint32_t {
-        if (t + 1 >= t_end) return 1;
-        if (sidx + 1 < a.nsegs && a.segs[sidx + 1].tile_base <= t + 1) return 1;
-        return 2;
-    };
-    SegCtx sc, nsc;
-    uint32_t si = 0, nsi = 0;
-    uint64_t tile_start = 0, seg_len = 0, ntile_start = 0, nseg_len = 0;
-    seg_ctx(t_begin, 0, nsc, nsi, ntile_start, nseg_len);
-    uint32_t nspan = span_of(t_begin, nsi);
-    // the next tile's rows, loaded ahead: thread c stages out row c and in row 512 + c,
-    // thread 0 also the 16 bytes of row 1024 (all 16-byte aligned: segment starts and nal are)
-    uint32_t x[16], y[16], xt[4] = {0, 0, 0, 0};
-    load_chunk_nt(nsc.base, nseg_len, ntile_start + 64ull * tid, x);
-    load_chunk_nt(nsc.base, nseg_len, ntile_start + nal + 64ull * tid, y);
-    if (tid == 0) load16_nt(nsc.base, nseg_len, ntile_start + nal + (uint64_t)kTileW, xt);
-    uint32_t S0 = 0, B0 = 0;  // window at tile_start: byte sum (exact) and B mod M
-    bool carried = false;     // (S0, B0) hold the window at this tile's start
-
-    uint32_t tile = t_begin;
-#pragma unroll 1
-    while (tile < t_end) {
-        sc = nsc;
-        si = nsi;
-        tile_start = ntile_start;
-        seg_len = nseg_len;
-        const uint32_t span = nspan;
-        // ---- stage (the previous tile's last barrier ended every read of the rows)
-#pragma unroll
-        for (int i = 0; i < 16; ++i) rows[tid * kRowDw + i] = x[i];
-#pragma unroll
-        for (int i = 0; i < 16; ++i) rows[(kTW + tid) * kRowDw + i] = y[i];
-        if (tid == 0) {
-#pragma unroll
-            for (int i = 0; i < 4; ++i) rows[(kRowsW - 1) * kRowDw + i] = xt[i];
-        }
-        // a segment's (or the range's) first tile: its first window from global memory
-        if (!carried) {
-            uint64_t s = 0, b = 0;
-            for (uint32_t gr = tid; 16 * gr < n; gr += kTW) {
-                uint32_t z[4];
-                // 16 bytes at a 16-byte aligned offset (tile starts are), bytes past the
-                // window or the segment's source masked
-                const uint32_t lim = min(16u, n - 16 * gr);
-                load16_nt(sc.base, seg_len, tile_start + 16ull * gr, z);
-#pragma unroll
-                for (int i = 0; i < 4; ++i) {
-                    const uint32_t bb = 4u * (uint32_t)i;
-                    const uint32_t keep = lim >= bb + 4 ? 0xFFFFFFFFu : lim <= bb ? 0u : (0xFFFFFFFFu >> (8 * (bb + 4 - lim)));
-                    const uint32_t d = z[i] & keep;
-                    const uint32_t ds = udot4(d, 0x01010101u, 0);
-                    const uint32_t du = udot4(d, offw(i), 0);  // weights bb .. bb+3
-                    s += ds;
-                    b += (uint64_t)(n - 16 * gr) * ds - du;    // sum (n - i) x_i over these bytes
-                }
-            }
-            s = wave_sum64(s);
-            b = wave_sum64(b);
-            if (lane == 0) { red[2 * wid] = s; red[2 * wid + 1] = b; }
-            __syncthreads();
-            uint64_t ts = 0, tb = 0;
-            for (int w = 0; w < kTW / 64; ++w) { ts += red[2 * w]; tb += red[2 * w + 1]; }
-            S0 = (uint32_t)ts;
-            B0 = (uint32_t)(tb % kMod);
-        }
-        __syncthreads();
-        // next tile's rows, issued now: their latency hides behind the window phase and the roll
-        const uint32_t nt = tile + span;
-        bool next_same = false;
-        if (nt < t_end) {
-            if (nsi + 1 < a.nsegs && a.segs[nsi + 1].tile_base <= nt) {
-                seg_ctx(nt, nsi, nsc, nsi, ntile_start, nseg_len);  // the next segment
-            } else {
-                ntile_start = tile_start + (uint64_t)span * kTile2;
-                next_same = true;  // then span == 2: a lone host tile ends the range or its segment
-            }
-            nspan = span_of(nt, nsi);
-            load_chunk_nt(nsc.base, nseg_len, ntile_start + 64ull * tid, x);
-            load_chunk_nt(nsc.base, nseg_len, ntile_start + nal + 64ull * tid, y);
-            if (tid == 0) load16_nt(nsc.base, nseg_len, ntile_start + nal + (uint64_t)kTileW, xt);
-        }
-        // positions of this tile that belong to it: [tile_start, tile_start + span * kTile2)
-        sc.pos_end = min(sc.pos_end, tile_start + (uint64_t)span * kTile2);
-        PHASE_MARKW(0)
-
-        // ---- window: row t of each region
-        uint32_t am, bm;
-        {
-            const uint32_t* ro = rows + orow;
-            const uint32_t* ri = rows + (kTW + tid) * kRowDw;
-            uint32_t so, uo, si_, ui, ps, pu;
-            half_sums(ro, 16, 64, so, uo);
-            half_sums(ri, 16, 64, si_, ui);
-            half_sums(ri, 4, on, ps, pu);  // the first `on` bytes of the in row
-            const uint32_t wo = (64u * tid * so + uo) % kMod;   // < 2^32: 64*511*16320 + 63*16320
-            const uint32_t wi = (64u * tid * si_ + ui) % kMod;
-            uint32_t Tso, Two, Tsi, Twi;
-            const uint32_t Eso = wave_scan_excl(so, Tso), Ewo = wave_scan_excl(wo, Two);
-            const uint32_t Esi = wave_scan_excl(si_, Tsi), Ewi = wave_scan_excl(wi, Twi);
-            if (lane == 0) { wt[4 * wid] = Tso; wt[4 * wid + 1] = Two; wt[4 * wid + 2] = Tsi; wt[4 * wid + 3] = Twi; }
-            // partial sums of the first `on` bytes of in row 0 and of row 1024
-            uint32_t ps0, pu0, psT, puT;
-            half_sums(rows + kTW * kRowDw, 4, on, ps0, pu0);
-            half_sums(rows + (kRowsW - 1) * kRowDw, 4, on, psT, puT);
-            __syncthreads();
-            uint32_t Bso = 0, Bwo = 0, Bsi = 0, Bwi = 0, Aso = 0, Awo = 0, Asi = 0, Awi = 0;
-#pragma unroll
-            for (uint32_t w = 0; w < (uint32_t)(kTW / 64); ++w) {
-                const uint4 v = *(const uint4*)(wt + 4 * w);
-                if (w < wid) { Bso += v.x; Bwo += v.y; Bsi += v.z; Bwi += v.w; }
-                Aso += v.x; Awo += v.y; Asi += v.z; Awi += v.w;
-            }
-            // window of position d (d = 64 t here, kTileW for the next tile's carry), from the
-            // region prefixes at row t: out sums Os (exact), Ow (mod M); in-region sums up to
-            // row t, Is (exact), Iw (mod M), and the partials (ps, pu) of the in row's first
-            // `on` bytes
-            auto window = [&](uint32_t d, uint32_t Os, uint32_t Ow, uint32_t Is, uint32_t Iw, uint32_t p_s,
-                              uint32_t p_u, uint32_t& A, uint32_t& B) {
-                const uint32_t Rs = Is + p_s;                                       // in-region bytes [0, on + d)
-                const uint64_t Rw = ((uint64_t)Iw + (uint64_t)d * p_s + p_u) % kMod; // their weighted sum
-                const uint32_t InS = Rs - ps0;                                      // in_j, j < d
-                const uint64_t Rw_d = (Rw + kMod - pu0 % kMod) % kMod;
-                // sum_{j<d} (d - j) in_j = (on + d) InS - (Rw(on + d) - Rw(on)) (mod M)
-                const uint64_t InW = ((uint64_t)(on + d) * InS + kMod - Rw_d) % kMod;
-                // sum_{j<d} (d - j) out_j = d Os - Ow (mod M)
-                const uint64_t OutW = ((uint64_t)d * Os + kMod - Ow % kMod) % kMod;
-                const uint32_t S = S0 + InS - Os;
-                uint64_t b = (uint64_t)B0 + (uint64_t)d * (S0 % kMod) + InW + kMod - OutW;
-                b += (uint64_t)kMod * kMod - (uint64_t)nmod * (Os % kMod);
-                A = S;
-                B = (uint32_t)(b % kMod);
-            };
-            uint32_t Sd, Bd;
-            window(64u * tid, Bso + Eso, (Bwo + Ewo) % kMod, Bsi + Esi, (Bwi + Ewi) % kMod, ps, pu, Sd, Bd);
-            am = (1 + Sd) % kMod;
-            bm = (n + Bd) % kMod;
-            // the next tile's first window, when it continues this segment
-            uint32_t Sn, Bn;
-            window((uint32_t)kTileW, Aso, Awo % kMod, Asi, Awi % kMod, psT, puT, Sn, Bn);
-            carried = next_same;
-            S0 = Sn;
-            B0 = Bn;
-        }
-        PHASE_MARKW(1)
-
-        // ---- roll (k_scan_l2's; positions past sc.pos_end are dropped by the drain)
-        const uint64_t fptr = (uint64_t)(uintptr_t)sc.filt;
-        const uint32_t fp_lo = __builtin_amdgcn_readfirstlane((uint32_t)fptr);
-        const uint32_t fp_hi = __builtin_amdgcn_readfirstlane((uint32_t)(fptr >> 32));
-        const __amdgpu_buffer_rsrc_t frsrc = __builtin_amdgcn_make_buffer_rsrc(
-            (void*)(uintptr_t)(((uint64_t)fp_hi << 32) | fp_lo), (short)0,
-            (int)__builtin_amdgcn_readfirstlane(sc.fwords * 4), 0x00020000);
-        const uint32_t fwshift = __builtin_amdgcn_readfirstlane(sc.fwshift);
-        auto compute = [&](uint32_t g, L1Batch& Bt) {
-            uint32_t xo[2], xi[2];
-            xo[0] = rows[orow + (g >> 2)];
-            xo[1] = rows[orow + (g >> 2) + 1];
-            {
-                uint32_t dw[3];
-#pragma unroll
-                for (int j = 0; j < 3; ++j) {
-                    const uint32_t d = din0 + (g >> 2) + j;
-                    dw[j] = rows[(d >> 4) * kRowDw + (d & 15)];
-                }
-                xi[0] = __builtin_amdgcn_alignbyte(dw[1], dw[0], sh);
-                xi[1] = __builtin_amdgcn_alignbyte(dw[2], dw[1], sh);
-            }
-            uint32_t ct[kB3], off[kB3], w1[kB3];
-#pragma unroll
-            for (int t = 0; t < kB3; ++t) ct[t] = ntab[(xo[t >> 2] >> (8 * (t & 3))) & 0xFF];
-#pragma unroll
-            for (int t = 0; t < kB3; ++t) {
-                const uint32_t out = (xo[t >> 2] >> (8 * (t & 3))) & 0xFF;
-                const uint32_t in = (xi[t >> 2] >> (8 * (t & 3))) & 0xFF;
-                __builtin_assume(am < kMod);
-                __builtin_assume(bm < kMod);
-                Bt.wv[t] = (bm << 16) | am;
-                const ProbeHash h = probe_hash(am, bm);
-                Bt.hq[t] = h.q;
-                off[t] = h.r >> fwshift;
-                w1[t] = l1[h.q >> 18];
-                const uint32_t u = am + in + (kMod - out);  // [M-255, 2M+255)
-                am = min(u, min(u - kMod, u - 2 * kMod));
-                const uint32_t v = bm + am + ct[t];          // [0, 3M)
-                bm = min(v, min(v - kMod, v - 2 * kMod));
-            }
-#pragma unroll
-            for (int t = 0; t < kB3; ++t) {
-                uint32_t p1 = l1_test(w1[t], Bt.hq[t]);
-                if (kTiming && (a.ablate & 2)) p1 = 0;
-                if (kTiming) l1pass += __popcll(__ballot(p1));
-                // a level-1 miss asks for an offset past the buffer: no request, reads 0
-                Bt.w2[t] = __builtin_amdgcn_raw_buffer_load_b32(frsrc, (int)((off[t] << 2) | (p1 - 1u)), 0, 0);
-            }
-        };
-        auto finish = [&](uint32_t g, L1Batch& Bt, uint32_t& todo) -> bool {
-            uint32_t pbits = 0;
-#pragma unroll
-            for (int t = 0; t < kB3; ++t) pbits |= filt_bit(Bt.w2[t], Bt.hq[t]) << t;
-            asm volatile("" : "+v"(pbits));
-            const uint64_t below = (1ull << lane) - 1;
-            const uint64_t anyp = __ballot((pbits & todo) != 0);
-            if (nfq + 8u * (uint32_t)__popcll(anyp) <= (uint32_t)kFQ3) {
-                if (anyp) {
-#pragma unroll
-                    for (int t = 0; t < kB3; ++t) {
-                        if (!((todo >> t) & 1)) continue;
-                        const uint64_t mk = __ballot((pbits >> t) & 1);
-                        if (!mk) continue;
-                        if ((pbits >> t) & 1) fq[nfq + __popcll(mk & below)] = make_uint2(rel0 + g + t, Bt.wv[t]);
-                        nfq += __popcll(mk);
-                    }
-                }
-                todo = 0xFFu;
-                return true;
-            }
-            uint32_t need = 0;
-#pragma unroll
-            for (int t = 0; t < kB3; ++t)
-                if ((todo >> t) & 1) need += __popcll(__ballot((pbits >> t) & 1));
-            const bool all = nfq + need <= (uint32_t)kFQ3;
-            bool full = false;
-#pragma unroll
-            for (int t = 0; t < kB3; ++t) {
-                if (!((todo >> t) & 1) || full) continue;
-                const uint64_t mk = __ballot((pbits >> t) & 1);
-                if (!all && nfq + __popcll(mk) > (uint32_t)kFQ3) { full = true; continue; }
-                if ((pbits >> t) & 1) fq[nfq + __popcll(mk & below)] = make_uint2(rel0 + g + t, Bt.wv[t]);
-                nfq += __popcll(mk);
-                todo &= ~(1u << t);
-            }
-            if (all) todo = 0xFFu;
-            return all;
-        };
-        // Pipeline over the thread's 8 batches: batch k+1's level-2 loads are in flight
-        // while batch k is tested; a batch the queue cannot take stops it, the queue is
-        // drained and the roll resumes from that batch's saved state.
-        uint32_t stop = kNBW, todo = 0xFFu, ra = 0, rb = 0;
-        {
-            L1Batch b0, b1;
-            uint32_t sa0 = am, sb0 = bm;
-            compute(0, b0);
-            uint32_t sa1 = am, sb1 = bm;
-            compute(kB3, b1);
-#pragma unroll 1
-            for (uint32_t k = 0; k < (uint32_t)kNBW; k += 2) {
-                if (!finish(kB3 * k, b0, todo)) { stop = k; ra = sa0; rb = sb0; break; }
-                if (k + 2 < (uint32_t)kNBW) { sa0 = am; sb0 = bm; compute(kB3 * (k + 2), b0); }
-                if (!finish(kB3 * (k + 1), b1, todo)) { stop = k + 1; ra = sa1; rb = sb1; break; }
-                if (k + 3 < (uint32_t)kNBW) { sa1 = am; sb1 = bm; compute(kB3 * (k + 3), b1); }
-            }
-        }
-        while (stop < (uint32_t)kNBW) {
-            passes += nfq;
-            drain_w(a, fq, nfq, wq, weak_hits, tile_start, sc);
-            nfq = 0;
-            uint32_t k = stop;
-            stop = kNBW;
-            am = ra;
-            bm = rb;
-#pragma unroll 1
-            for (; k < (uint32_t)kNBW; ++k) {
-                L1Batch bt;
-                const uint32_t ak = am, sk = bm;
-                compute(kB3 * k, bt);
-                if (!finish(kB3 * k, bt, todo)) { stop = k; ra = ak; rb = sk; break; }
-            }
-        }
-        PHASE_MARKW(2)
-        PHASE_MARKW(3)
-        if (nfq) {
-            passes += nfq;
-            drain_w(a, fq, nfq, wq, weak_hits, tile_start, sc);
-            nfq = 0;
-        }
-        PHASE_MARKW(4)
-        __syncthreads();  // rows (and wt) are rewritten by the next tile
-        PHASE_MARKW(5)
-        tile += span;
-    }
-#undef PHASE_MARKW
-    if (lane == 0 && passes) atomicAdd(&a.counters[2], passes);
-    if (lane == 0 && weak_hits) atomicAdd(&a.counters[1], weak_hits);
-    if (kTiming && lane == 0) atomicAdd(&a.counters[3], l1pass);
-    if (kTiming && tid == 0)
-        for (int k = 0; k < 6; ++k) atomicAdd(&a.counters[4 + k], tm[k]);
 }
 
 // Tail rule (generator.rs:156-184): at p* = len - last_size (last_size < n), the
