@@ -26,6 +26,9 @@ constexpr uint32_t kLdsFilterWordsMax = 8192;
 // k_scan_g's small-index mode keeps one file filter per wave in LDS: up to 4096 words
 // (16 KiB; files of up to 4 Ki blocks), eight waves per workgroup.
 constexpr uint32_t kSmallWords = 4096;
+// k_scan_r's small-index mode (n = 4096, twelve waves): one slot per wave in the level-1
+// area (kL1WordsR words), so up to 3200 words; files of up to 512 blocks (1024 words).
+constexpr uint32_t kSmallWordsR = 2048;
 // k_scan_r's level-1 filter (one large file at n = 4096): 38400 words = 150 KiB, the LDS
 // left when the tile's bytes stay in registers, word = l1r_word(q) (l1_wshift 1 marks it).
 constexpr uint32_t kL1WordsR = 38400;

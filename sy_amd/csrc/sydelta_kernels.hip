@@ -337,9 +337,14 @@ __device__ __forceinline__ ProbeHash probe_hash(uint32_t w) { return probe_hash(
 // 16 bits per key against 1.08 % with three (Poisson keys per word), so a third fewer
 // exact-table lookups behind the scans' filters (round 4; each lookup of a level-2 false
 // pass misses L2 for a table line).
+#ifndef SYDELTA_L2_BITS
+#define SYDELTA_L2_BITS 5
+#endif
+static_assert(SYDELTA_L2_BITS == 3 || SYDELTA_L2_BITS == 5, "level-2 bits per key");
 __device__ __forceinline__ uint32_t filt_mask(uint32_t q) {
-    return (1u << (q & 31)) | (1u << ((q >> 5) & 31)) | (1u << ((q >> 10) & 31)) | (1u << ((q >> 15) & 31)) |
-           (1u << ((q >> 20) & 31));
+    uint32_t m = (1u << (q & 31)) | (1u << ((q >> 5) & 31)) | (1u << ((q >> 10) & 31));
+    if (SYDELTA_L2_BITS == 5) m |= (1u << ((q >> 15) & 31)) | (1u << ((q >> 20) & 31));
+    return m;
 }
 __device__ __forceinline__ bool filt_pass(uint32_t word, uint32_t q) {
     const uint32_t m = filt_mask(q);
@@ -347,9 +352,10 @@ __device__ __forceinline__ bool filt_pass(uint32_t word, uint32_t q) {
 }
 // filt_pass as 0/1 with five bit extracts (the offset operand takes bits [4:0])
 __device__ __forceinline__ uint32_t filt_bit(uint32_t word, uint32_t q) {
-    return __builtin_amdgcn_ubfe(word, q, 1) & __builtin_amdgcn_ubfe(word, q >> 5, 1) &
-           __builtin_amdgcn_ubfe(word, q >> 10, 1) & __builtin_amdgcn_ubfe(word, q >> 15, 1) &
-           __builtin_amdgcn_ubfe(word, q >> 20, 1);
+    uint32_t b = __builtin_amdgcn_ubfe(word, q, 1) & __builtin_amdgcn_ubfe(word, q >> 5, 1) &
+                 __builtin_amdgcn_ubfe(word, q >> 10, 1);
+    if (SYDELTA_L2_BITS == 5) b &= __builtin_amdgcn_ubfe(word, q >> 15, 1) & __builtin_amdgcn_ubfe(word, q >> 20, 1);
+    return b;
 }
 // Level-1 filters (held in LDS by k_scan_r / k_scan_g so that only the positions they
 // pass cost a level-2 request to L2): one bit per key, bit = q[0..4] (one bit extract;
@@ -782,7 +788,11 @@ __device__ __forceinline__ void load_chunk(const uint8_t* src, uint64_t len, uin
 // As load_chunk, with non-temporal loads for the aligned case: the staged tile
 // is read once, so it should not evict the Bloom filter from L2.
 __device__ __forceinline__ void load_chunk_nt(const uint8_t* src, uint64_t len, uint64_t c0, uint32_t x[16]) {
+#ifdef SYDELTA_ROW_TEMPORAL
+    if (false) {
+#else
     if (c0 + 64 <= len) {
+#endif
         const uint4* q = (const uint4*)(src + c0);
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
@@ -1988,6 +1998,9 @@ __device__ __forceinline__ uint64_t wave_strong_regs(const uint32_t (&xo)[16], c
 // the registers (wave_strong_regs, one window at a time for the whole wave), the first
 // candidate in index order with equal strong taken (generator.rs:127-133); verified hits
 // to the output.  tile_rel: the run position of the tile's first window.
+// kSmall: the index has no fat table (small files): the exact table's slot is looked up and
+// its candidates swept in index order (first_strong_match).
+template <bool kSmall = false>
 __device__ __forceinline__ void drain_regs(const ScanArgs& a, const uint2* recs, uint32_t nr, uint32_t tile_rel,
                                            const uint32_t (&xo)[16], const uint32_t (&xi)[16], const uint64_t* kt,
                                            unsigned long long& weak_hits, uint64_t run_start, const SegCtx& cur) {
@@ -2003,7 +2016,15 @@ __device__ __forceinline__ void drain_regs(const ScanArgs& a, const uint2* recs,
             const volatile uint2* g = recs + i;  // rewritten by later tiles: not from a stale L1 line
             pos = g->x;
             const uint32_t w = g->y;
-            if (run_start + pos < cur.pos_end && !(a.ablate & 16)) hit = fat_find_k(cur.keys, cur.fat, cur.bmask, w, rec);
+            if (run_start + pos < cur.pos_end && !(a.ablate & 16)) {
+                if (kSmall) {
+                    const int64_t sl = table_find(cur.keys, cur.bmask, w);
+                    hit = sl >= 0;
+                    rec.y = kMulti | (uint32_t)(cur.slot_off + (uint64_t)(sl < 0 ? 0 : sl));
+                } else {
+                    hit = fat_find_k(cur.keys, cur.fat, cur.bmask, w, rec);
+                }
+            }
         }
         uint64_t m = __ballot(hit);
         weak_hits += __popcll(m);
@@ -2047,8 +2068,12 @@ __device__ __forceinline__ void drain_regs(const ScanArgs& a, const uint2* recs,
 // parity of its coefficients over its window is even), else the one-hash Bloom (l1r_word).
 // kWaves: waves per workgroup (one workgroup per CU: the level-1 filter fills the LDS);
 // 12 = three per SIMD, which caps the kernel at 168 VGPRs.
-template <bool kAblate, bool kRib, int kWaves>
-__global__ __launch_bounds__(kWaves * 64, 1) void k_scan_r(ScanArgs a, uint32_t per) {
+// kSmall: small indexes (each file's Bloom filter <= kSmallWordsR words): no level-1 /
+// level-2; each wave copies the filter of the file it scans into its own LDS slot and
+// tests every position there (k_scan_g's small mode, with the windows verified from the
+// registers).
+template <bool kAblate, bool kRib, int kWaves, bool kSmall = false>
+__global__ __launch_bounds__(kWaves * 64, 1) void k_scan_r(ScanArgs a, uint32_t per, uint32_t small_words) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     constexpr LdsR L = ldsr_layout();
     constexpr uint32_t kT = kWaves * 64;
@@ -2060,11 +2085,13 @@ __global__ __launch_bounds__(kWaves * 64, 1) void k_scan_r(ScanArgs a, uint32_t 
     uint32_t* ctr = (uint32_t*)(smem + L.ctr);
     const uint32_t gwave = blockIdx.x * kWaves + wid;
     uint2* rec = a.rrec + (size_t)gwave * kWTR;  // this wave's pass records (one wave tile)
+    uint32_t* fslot = (uint32_t*)(smem + L.l1) + (size_t)wid * small_words;  // kSmall: this wave's filter
+    uint32_t slot_file = 0xFFFFFFFFu;
 
     const uint32_t t_begin = blockIdx.x * per;
     const uint32_t t_end = min(a.ntiles, t_begin + per);
     if (t_begin >= t_end) return;
-    {
+    if (!kSmall) {
         const uint4* g = (const uint4*)a.l1;
         uint4* d = (uint4*)(smem + L.l1);
 #pragma unroll 4
@@ -2126,6 +2153,14 @@ __global__ __launch_bounds__(kWaves * 64, 1) void k_scan_r(ScanArgs a, uint32_t 
                 (void*)(uintptr_t)(((uint64_t)fp_hi << 32) | fp_lo), (short)0,
                 (int)__builtin_amdgcn_readfirstlane(sc.fwords * 4), 0x00020000);
             const uint32_t fwshift = __builtin_amdgcn_readfirstlane(sc.fwshift);
+            if (kSmall && S.file != slot_file) {  // this file's filter into the wave's slot
+                slot_file = S.file;
+                lds_fence();
+                const uint4* g = (const uint4*)sc.filt;
+                uint4* d = (uint4*)fslot;
+                for (uint32_t i = lane; i < sc.fwords / 4; i += 64) d[i] = g[i];
+                lds_fence();
+            }
 
             uint32_t xo[16], xi[16], xn[16];
             load_chunk_nt(sc.base, seg_len, run_start + 64ull * lane, xo);  // read once: not kept in L2
@@ -2176,7 +2211,9 @@ __global__ __launch_bounds__(kWaves * 64, 1) void k_scan_r(ScanArgs a, uint32_t 
                         const ProbeHash h = probe_hash(am, bm);
                         Bt.hq[t2] = h.q;
                         rr[t2] = h.r;
-                        if (kRib) {  // the window's two words (ds_read2_b32)
+                        if (kSmall) {
+                            Bt.w2[t2] = fslot[h.r >> fwshift];  // the file's whole filter, tested in finish
+                        } else if (kRib) {  // the window's two words (ds_read2_b32)
                             bo[t2] = rib_bit(h.q, h.r);
                             w1[t2] = l1[bo[t2] >> 5];
                             w1b[t2] = l1[(bo[t2] >> 5) + 1];
@@ -2189,7 +2226,7 @@ __global__ __launch_bounds__(kWaves * 64, 1) void k_scan_r(ScanArgs a, uint32_t 
                         bm = min(v, min(v - kMod, v - 2 * kMod));
                     }
 #pragma unroll
-                    for (int t2 = 0; t2 < kB3; ++t2) {
+                    for (int t2 = 0; t2 < kB3 && !kSmall; ++t2) {
                         uint32_t p1;
                         if (kRib) {
                             const uint32_t win = __builtin_amdgcn_alignbit(w1b[t2], w1[t2], bo[t2]);
@@ -2234,7 +2271,7 @@ __global__ __launch_bounds__(kWaves * 64, 1) void k_scan_r(ScanArgs a, uint32_t 
                 }
                 passes += nrec - tile_rec;
                 if (nrec > tile_rec && !(kAblate && (a.ablate & 1)))
-                    drain_regs(a, rec + tile_rec, nrec - tile_rec, k * kWTR, xo, xi, kt, weak_hits, run_start, sc);
+                    drain_regs<kSmall>(a, rec + tile_rec, nrec - tile_rec, k * kWTR, xo, xi, kt, weak_hits, run_start, sc);
                 nrec = tile_rec;
 #pragma unroll
                 for (int i = 0; i < 16; ++i) {
@@ -3914,7 +3951,10 @@ hipError_t launch_scan(const uint8_t* d_buf, const ScanSeg* d_segs, uint32_t nse
     // filters are <= kSmallWords words at any n <= kMaxN2; weak hits verified by k_verify_w
     static const bool small_off = getenv("SYDELTA_SCAN_SMALL") && getenv("SYDELTA_SCAN_SMALL")[0] == '0';
     const bool small = !ix.l1 && ix.max_fwords <= kSmallWords && n <= kMaxN2 && !small_off;
-    if ((ix.l1 && ix.l1_wshift == 1 && ix.fat && ix.nfiles == 1 && n != kMaxN3) || small) {
+    // small indexes at n = 4096 with filters <= kSmallWordsR words: k_scan_r's small mode
+    // (windows verified from the registers, no deferred list)
+    const bool small_r = small && n == kMaxN3 && ix.max_fwords <= kSmallWordsR;
+    if ((ix.l1 && ix.l1_wshift == 1 && ix.fat && ix.nfiles == 1 && n != kMaxN3) || (small && !small_r)) {
         static std::once_flag g_once;
         static hipError_t g_err = hipSuccess;
         static int g_cus = 256;
@@ -3970,7 +4010,7 @@ hipError_t launch_scan(const uint8_t* d_buf, const ScanSeg* d_segs, uint32_t nse
         return e != hipSuccess ? e : fe;
     }
     // k_scan_r: one large file at n = 4096 (SYDELTA_SCAN_R_WAVES=8: two waves per SIMD)
-    if (ix.l1 && ix.l1_wshift == 1 && n == kMaxN3) {
+    if ((ix.l1 && ix.l1_wshift == 1 && n == kMaxN3) || small_r) {
         static std::once_flag r_once;
         static hipError_t r_err = hipSuccess;
         static int r_cus = 256;
@@ -3978,7 +4018,8 @@ hipError_t launch_scan(const uint8_t* d_buf, const ScanSeg* d_segs, uint32_t nse
             for (const void* f : {(const void*)k_scan_r<false, false, 8>, (const void*)k_scan_r<true, false, 8>,
                                   (const void*)k_scan_r<false, true, 8>, (const void*)k_scan_r<true, true, 8>,
                                   (const void*)k_scan_r<false, false, 12>, (const void*)k_scan_r<true, false, 12>,
-                                  (const void*)k_scan_r<false, true, 12>, (const void*)k_scan_r<true, true, 12>})
+                                  (const void*)k_scan_r<false, true, 12>, (const void*)k_scan_r<true, true, 12>,
+                                  (const void*)k_scan_r<false, false, 12, true>, (const void*)k_scan_r<true, false, 12, true>})
                 if (r_err == hipSuccess)
                     r_err = hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024 - 256);
             int dev = 0, cus = 0;
@@ -3987,9 +4028,11 @@ hipError_t launch_scan(const uint8_t* d_buf, const ScanSeg* d_segs, uint32_t nse
                 r_cus = cus;
         });
         if (r_err != hipSuccess) return r_err;
-        if (!ix.fat) return hipErrorInvalidValue;
+        if (!ix.fat && !small_r) return hipErrorInvalidValue;
         // 12 waves (three per SIMD, 168 VGPRs): 9.72 ms at C3 against 10.37 with 8 (round 4)
-        static const int waves = getenv("SYDELTA_SCAN_R_WAVES") && atoi(getenv("SYDELTA_SCAN_R_WAVES")) == 8 ? 8 : 12;
+        static const int waves_env = getenv("SYDELTA_SCAN_R_WAVES") && atoi(getenv("SYDELTA_SCAN_R_WAVES")) == 8 ? 8 : 12;
+        const int waves = small_r ? 12 : waves_env;
+        const uint32_t small_words = small_r ? std::max<uint32_t>(ix.max_fwords, 64u) : 0u;
         constexpr LdsR LR = ldsr_layout();
         // one workgroup per CU over contiguous host tiles, an even number each (runs are pairs)
         uint32_t per = (uint32_t)((ntiles + (uint64_t)r_cus - 1) / (uint64_t)r_cus);
@@ -4004,8 +4047,11 @@ hipError_t launch_scan(const uint8_t* d_buf, const ScanSeg* d_segs, uint32_t nse
         {
             ProfScope ps(prof, s, "k_scan_r");
             const dim3 g(grid), b(64 * waves);
-#define LAUNCH_R(AB, RB, W) hipLaunchKernelGGL((k_scan_r<AB, RB, W>), g, b, LR.total, s, a, per)
-            if (waves == 12) {
+#define LAUNCH_R(AB, RB, W) hipLaunchKernelGGL((k_scan_r<AB, RB, W>), g, b, LR.total, s, a, per, 0u)
+            if (small_r) {
+                if (a.ablate) hipLaunchKernelGGL((k_scan_r<true, false, 12, true>), g, b, LR.total, s, a, per, small_words);
+                else hipLaunchKernelGGL((k_scan_r<false, false, 12, true>), g, b, LR.total, s, a, per, small_words);
+            } else if (waves == 12) {
                 if (ix.l1_ribbon) { if (a.ablate) LAUNCH_R(true, true, 12); else LAUNCH_R(false, true, 12); }
                 else { if (a.ablate) LAUNCH_R(true, false, 12); else LAUNCH_R(false, false, 12); }
             } else {
