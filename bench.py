@@ -551,10 +551,10 @@ def roofline(prof: dict, steps: int, algo_step: dict, positions=None, keys=None,
     random filter-word request per window start.  `l2_gather` reports that rate against
     L2_GATHER_PEAK (the measured chip-wide ceiling of random L2 gathers,
     profiles/r02_micro_gather2.txt) when the step's scanned positions are known.  For
-    the level-1 scans (k_scan_l1 / k_scan_s: 2^20 bits, k_scan_l2: 28672 words = 917504
-    bits, k_scan_r: 38400 words = 1228800 bits, k_scan_w: 2^19 bits) only the positions
-    that pass the level-1 filter in LDS send a request; that fraction is modelled as
-    1 - exp(-keys / bits) (one bit per key) and the entry says so.
+    the level-1 scans (k_scan_r / k_scan_g: 38400 words = 1228800 bits; round 3's k_scan_w:
+    2^19 bits) only the positions that pass the level-1 filter in LDS send a request; that
+    fraction is modelled as 1 - exp(-keys / bits) for the one-hash Bloom and 1/2 for the
+    ribbon, and the entry says so.
 
     `bound` is "l2" when the L2 request rate binds the kernel (its l2_gather fraction,
     measured or modelled, exceeds its HBM fraction); achieved / peak / frac stay the HBM

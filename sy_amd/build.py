@@ -59,7 +59,7 @@ def build(force: bool = False, verbose: bool = False) -> str:
 # host objects into sy_amd/variants/libsydelta_<name>.so (loaded with SYDELTA_LIB_VARIANT).
 VARIANTS = {
     "l2b3": ["-DSYDELTA_L2_BITS=3"],        # level-2 words with three bits per key (rounds 1-3)
-    "rowtemp": ["-DSYDELTA_ROW_TEMPORAL"],  # the register scans' row loads kept in L2
+    "rownt": ["-DSYDELTA_ROW_NONTEMPORAL"],  # the register scans' row loads non-temporal
 }
 
 

@@ -1310,7 +1310,7 @@ int Classifier::scan(const std::vector<std::array<uint64_t, 3>>& ranges) {
         if (host_timing) fprintf(stderr, "sydelta scan synchronized: %.3f ms\n", ms_since(t0));
         if (getenv("SYDELTA_PHASE_TIMING"))
             fprintf(stderr, "sydelta phase cycles (wave 0, summed over workgroups): [k_scan_lds: stage prefix roll flush"
-                            " lookup verify; k_scan_l1: stage window roll prefetch drain barrier] %llu %llu %llu %llu"
+                            " lookup verify] %llu %llu %llu %llu"
                             " %llu %llu l1 passes %llu passes %llu weak %llu positions %llu\n",
                     counts[4], counts[5], counts[6], counts[7], counts[8], counts[9], counts[3], counts[2], counts[1],
                     (unsigned long long)tot_pos);
@@ -2748,7 +2748,7 @@ extern "C" int sydelta_chunk_classify(sydelta_index* idx, const uint8_t* d_buf, 
     ch->final_src = final_src;
     ch->file_len = file_len;
     ch->bi = BasisInfo{0, idx->fblk[1], idx->last_size[0]};
-    // windows above the LDS scans' limit without k_scan_w: every position scanned (k_scan,
+    // windows above the LDS scans' limit without k_scan_g: every position scanned (k_scan,
     // one launch per range), no probe, as match_impl does
     if (int r = C.classify(n > scan_max_window() && !wide_scan(idx) ? 0 : probe_mode_env())) return r;
     if (final_src) {

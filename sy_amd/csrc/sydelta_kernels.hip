@@ -517,7 +517,7 @@ __global__ void k_idx_cstrong(uint64_t n, const uint32_t* __restrict__ order, co
     cstrong[j] = strong[order[j]];
 }
 
-// Fat table of a single-file index (k_scan_l1): per slot {key, first candidate in index
+// Fat table of an index with a level-1 filter (k_scan_r / k_scan_g): per slot {key, first candidate in index
 // order (or kMulti | slot when the slot has more than one), that candidate's strong}, so
 // one bucket read answers a lookup (the 4 slots of a bucket are one 64-byte line).
 __global__ void k_idx_fat(uint64_t nslots, const uint32_t* __restrict__ keys, const uint32_t* __restrict__ cnt,
@@ -697,9 +697,9 @@ struct ScanArgs {
     uint32_t nm;         // n mod M
     uint32_t c0;         // 2M - 1 - (255*nm mod M)    (k_scan)
     uint32_t timing;     // accumulate per-phase s_memtime cycles of wave 0 into counters[4..8)
-    uint32_t ablate;     // SYDELTA_ABLATE (measurement only, wrong results): k_scan_l1 bit 0 skips the
-                         // drains, bit 1 the level-2 loads, bit 2 the window phase; drain_l1 bit 3
-                         // skips the verification, bit 4 the fat-table lookups
+    uint32_t ablate;     // SYDELTA_ABLATE (measurement only, wrong results): k_scan_r / k_scan_g bit 0
+                         // skips the drains, bit 1 the level-2 loads; bit 3 the hashing of weak
+                         // hits, bit 4 the fat-table lookups
     // k_scan_lds: segment table and per-file probe offsets
     const ScanSeg* segs;
     uint32_t nsegs;
@@ -716,7 +716,7 @@ struct ScanArgs {
     // probe structures (concatenated over files)
     const uint32_t* filt;
     const uint32_t* l1;       // level-1 filter (k_scan_r / k_scan_g: kL1WordsR words)
-    const uint4* fat;         // k_scan_l1: {key, first candidate | kMulti+slot, strong} per slot
+    const uint4* fat;         // k_scan_r / k_scan_g: {key, first candidate | kMulti+slot, strong} per slot
     const uint32_t* keys;
     const uint32_t* start;
     const uint32_t* cnt;
@@ -752,7 +752,7 @@ struct SegCtx {
     uint64_t slot_off;
     uint32_t bmask;
     uint32_t seg_id;
-    // k_scan_l1
+    // k_scan_r / k_scan_g
     const uint4* fat;     // this file's fat table (slot_off applied)
     const uint32_t* filt; // this file's level-2 filter
     uint32_t fwshift, fwords;
@@ -785,10 +785,11 @@ __device__ __forceinline__ void load_chunk(const uint8_t* src, uint64_t len, uin
     }
 }
 
-// As load_chunk, with non-temporal loads for the aligned case: the staged tile
-// is read once, so it should not evict the Bloom filter from L2.
+// As load_chunk; built with SYDELTA_ROW_NONTEMPORAL, non-temporal loads for the aligned
+// case (meant to keep the rows from evicting the level-2 filter from L2).  Measured at
+// C3 (profiles/r04h_ab_*): 9.82 ms with them against 9.59 ms without, so they are off.
 __device__ __forceinline__ void load_chunk_nt(const uint8_t* src, uint64_t len, uint64_t c0, uint32_t x[16]) {
-#ifdef SYDELTA_ROW_TEMPORAL
+#ifndef SYDELTA_ROW_NONTEMPORAL
     if (false) {
 #else
     if (c0 + 64 <= len) {
@@ -1849,7 +1850,7 @@ __device__ __forceinline__ void load16_nt(const uint8_t* src, uint64_t len, uint
 }
 
 // ===========================================================================
-// k_scan_r: the tile's bytes in registers, no workgroup barriers (SYDELTA_SCAN_L1=5)
+// k_scan_r: the tile's bytes in registers, no workgroup barriers
 // ===========================================================================
 // Measured on k_scan_l2 (round 3, SYDELTA_ABLATE, C3, profiles/r03p_*): of its 14.8 ms,
 // 6.0 ms go away without the level-2 loads (2.9e9 L2 requests, 0.68 per position: the

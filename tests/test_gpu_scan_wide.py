@@ -1,9 +1,10 @@
-"""GPU parity of the wide-window scan k_scan_w (windows above 8 KiB: sy's own block
+"""GPU parity of the register-fed scan k_scan_g on windows above 8 KiB (sy's own block
 size calculate_block_size = sqrt(file size) for every file over 64 MiB, mod.rs:20-23)
-against the C restatement of generator.rs, and against the per-thread k_scan it
-replaces (SYDELTA_SCAN_WIDE=0, which also turns the aligned probe off).  The deferred
-weak-hit list of k_verify_w also runs with a cap of 64 entries (SYDELTA_WDEF_CAP), so
-that hits past it are verified inline beside the deferred ones.
+against the C restatement of generator.rs, and against the per-thread k_scan
+(SYDELTA_SCAN_WIDE=0, which also turns the aligned probe off).  The deferred weak-hit
+list of k_verify_w also runs with a cap of 64 entries (SYDELTA_WDEF_CAP), so that hits
+past it are verified inline beside the deferred ones.  (Round 3's k_scan_w, which this
+file tested before, was replaced by k_scan_g in round 4.)
 
 * every n mod 16 class that matters (8193, 9999, 16384, 31622, 65536, 131071, 131072):
   random edits (substitutions, insertions, deletions, block moves) over several tiles,
@@ -13,7 +14,7 @@ that hits past it are verified inline beside the deferred ones.
   phase: dense verifications from global memory);
 * a source shorter than a tile, one window long, and empty of full windows;
 * periodic data (every window a weak and strong hit, lowest index wins);
-* the streamed path API at bs 65536 (chunk machinery + k_scan_w).
+* the streamed path API at bs 65536 (chunk machinery + k_scan_g).
 """
 import os
 import random
