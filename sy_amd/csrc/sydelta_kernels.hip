@@ -732,6 +732,10 @@ struct ScanArgs {
     uint64_t wdef_cap;
     // k_scan_r: each wave's level-2 passes of one wave tile {position in run, weak}
     uint2* rrec;
+    // k_scan_r / k_scan_g / k_verify_w: each wave's staged outputs (WaveOut), kHStage
+    // verified hits and kDStage deferred weak hits per wave
+    uint4* hstage;
+    struct WDef* dstage;
 };
 
 // A weak hit of k_scan_g, verified after the scan by k_verify_w.
@@ -1632,29 +1636,12 @@ __global__ __launch_bounds__(kT2, kWgPerCu) void k_scan_lds(ScanArgs a, uint32_t
 // stripe per thread, 28.7 ms) were superseded by k_scan_r and removed in round 4; their
 // measurements are in DESIGN.md section 6.
 constexpr int kB3 = 8;             // positions per batch
-constexpr int kFQ3 = 64;           // level-2 passes queued per wave (LDS)
-constexpr int kWQ3 = 32;           // weak hits queued per wave (LDS)
 constexpr uint32_t kMaxN3 = 4096;  // k_scan_r's window: a wave tile's in rows are the next tile's out rows
 constexpr uint32_t kMulti = 0x80000000u;  // fat record: more than one candidate (info = slot)
 
-// Fat-table lookup: the bucket of w (4 records, one 64-byte line) in one round trip.
-__device__ __forceinline__ bool fat_find(const uint4* __restrict__ fat, uint32_t bmask, uint32_t w, uint4& rec) {
-    uint32_t b = bucket_hash(w) & bmask;
-    for (;;) {
-        const uint4* B = fat + 4 * (size_t)b;
-        const uint4 e0 = B[0], e1 = B[1], e2 = B[2], e3 = B[3];
-        if (e0.x == w) { rec = e0; return true; }
-        if (e1.x == w) { rec = e1; return true; }
-        if (e2.x == w) { rec = e2; return true; }
-        if (e3.x == w) { rec = e3; return true; }
-        if (e3.x == kEmptyKey) return false;  // buckets fill in order
-        b = (b + 1) & bmask;
-    }
-}
-
-// fat_find through the keys-only table: one 16-byte request for the bucket's four keys
-// (ScanArgs::keys, 4 B per slot) and the 16-byte record only on a hit, where
-// fat_find reads the bucket's 64-byte line of records for every lookup.
+// Fat-table lookup through the keys-only table: one 16-byte request for the bucket's four
+// keys (ScanArgs::keys, 4 B per slot) and the 16-byte record only on a hit (reading the
+// bucket's 64-byte line of records for every lookup cost more: round 3).
 __device__ __forceinline__ bool fat_find_k(const uint32_t* __restrict__ keys, const uint4* __restrict__ fat,
                                            uint32_t bmask, uint32_t w, uint4& rec) {
     uint32_t b = bucket_hash(w) & bmask;
@@ -1670,136 +1657,6 @@ __device__ __forceinline__ bool fat_find_k(const uint32_t* __restrict__ keys, co
     }
 }
 
-// Verify this wave's weak hits wq[0..nwq) = {position in tile, first candidate |
-// kMulti+slot, strong lo, hi}: XXH3 of the window from the LDS rows (four windows per
-// wave, one per 16-lane row, when n % 64 == 0 and n >= 256), then the first candidate
-// in index order with equal strong (generator.rs:127-133); verified hits to the output.
-// kWinLds false (k_scan_g): the windows are not in LDS; hash them from
-// global memory.
-template <bool kWinLds = true>
-__device__ __forceinline__ void verify_l1(const ScanArgs& a, uint4* wq, uint32_t nwq, const uint32_t* rows,
-                                          uint64_t tile_start, const SegCtx& cur) {
-    if (!nwq) return;
-    lds_fence();
-    const uint32_t lane = threadIdx.x & 63;
-    if (kWinLds && a.n % 64 == 0 && a.n >= 256) {
-        const uint32_t row = lane >> 4, rl = lane & 15;
-        RowKeys K;
-        row_keys(K);
-        for (uint32_t t = 0; t < nwq; t += 4) {
-            const uint32_t h = t + row;
-            const bool live = h < nwq;
-            const uint4 e = wq[live ? h : t];
-            uint32_t s0 = 0, cn = 0;
-            if (e.y & kMulti) { s0 = a.start[e.y & ~kMulti]; cn = a.cnt[e.y & ~kMulti]; }  // in flight while hashing
-            const uint64_t st = row_strong_lds(rows, e.x, a.n, K);
-            uint32_t best = 0xFFFFFFFFu;
-            if (!(e.y & kMulti)) {
-                if (st == (((uint64_t)e.w << 32) | e.z)) best = e.y;
-            } else {
-                for (uint32_t b = 0; b < cn; b += 16) {  // in index order, 16 candidates per step
-                    const uint32_t j = b + rl;
-                    const uint64_t m = (__ballot(j < cn && a.cstrong[s0 + j] == st) >> (row << 4)) & 0xFFFFull;
-                    if (m) {
-                        best = a.order[s0 + b + (uint32_t)__builtin_ctzll(m)];
-                        break;
-                    }
-                }
-            }
-            if (live && rl == 0) wq[h].y = best;
-        }
-    } else {
-        for (uint32_t k = 0; k < nwq; ++k) {
-            const uint4 e = wq[k];
-            uint64_t st;
-            if (a.n > 240) {
-                uint32_t wk;
-                if (kWinLds)
-                    wave_hash_src(LdsRowBytes{rows, e.x}, a.n, wk, st);
-                else
-                    wave_hash_long(cur.base + tile_start + e.x, a.n, wk, st);
-            } else {
-                st = 0;
-                if (lane == 0) st = xxh3_short(cur.base + tile_start + e.x, a.n);
-                st = shfl64(st, 0);
-            }
-            uint32_t best = 0xFFFFFFFFu;
-            if (!(e.y & kMulti)) {
-                if (st == (((uint64_t)e.w << 32) | e.z)) best = e.y;
-            } else {
-                best = first_strong_match(a.order, a.cstrong, a.start[e.y & ~kMulti], a.cnt[e.y & ~kMulti], st);
-            }
-            if (lane == 0) wq[k].y = best;
-        }
-    }
-    lds_fence();
-    uint32_t nver = 0;
-    for (uint32_t base = 0; base < nwq; base += 64) {
-        const bool v = base + lane < nwq && wq[base + lane].y != 0xFFFFFFFFu;
-        nver += __popcll(__ballot(v));
-    }
-    if (!nver) return;
-    unsigned long long k0 = 0;
-    if (lane == 0) k0 = atomicAdd(&a.counters[0], (unsigned long long)nver);
-    k0 = shfl64(k0, 0);
-    for (uint32_t base = 0; base < nwq; base += 64) {
-        const uint32_t i = base + lane;
-        const uint4 e = i < nwq ? wq[i] : make_uint4(0, 0xFFFFFFFFu, 0, 0);
-        const bool v = e.y != 0xFFFFFFFFu;
-        const uint64_t m = __ballot(v);
-        const unsigned long long k = k0 + __popcll(m & ((1ull << lane) - 1));
-        if (v && k < a.out_cap) {
-            a.hit_key[k] = ((uint64_t)cur.seg_id << kSegShift) | (uint64_t)(tile_start + e.x - cur.pos_begin);
-            a.hit_val[k] = e.y;
-        }
-        k0 += __popcll(m);
-    }
-}
-
-// Fat-table lookups of this wave's queued level-2 passes (all in the current tile),
-// 64 per round (positions at or past the segment end are dropped here); weak hits go
-// to wq, verified when wq cannot take another round and at the end.
-template <bool kWinLds = true>
-__device__ __forceinline__ void drain_l1(const ScanArgs& a, const uint2* fq, uint32_t nfq, uint4* wq,
-                                         unsigned long long& weak_hits, const uint32_t* rows, uint64_t tile_start,
-                                         const SegCtx& cur) {
-    const uint32_t lane = threadIdx.x & 63;
-    lds_fence();
-    uint32_t nwq = 0;
-    for (uint32_t base = 0; base < nfq; base += 64) {
-        const uint32_t i = base + lane;
-        bool hit = false;
-        uint4 rec = make_uint4(0, 0, 0, 0);
-        uint32_t tp = 0;
-        if (i < nfq) {
-            const uint2 e = fq[i];  // {position in tile, weak}
-            tp = e.x;
-            if (tile_start + e.x < cur.pos_end && !(a.ablate & 16)) hit = fat_find(cur.fat, cur.bmask, e.y, rec);
-        }
-        const uint64_t m = __ballot(hit);
-        if (!m) continue;
-        const uint32_t cnt = __popcll(m);
-        weak_hits += cnt;
-        if (a.ablate & 8) continue;
-        if (nwq + cnt > (uint32_t)kWQ3) {
-            verify_l1<kWinLds>(a, wq, nwq, rows, tile_start, cur);
-            nwq = 0;
-        }
-        const uint32_t rank = __popcll(m & ((1ull << lane) - 1));
-        const uint4 e = make_uint4(tp, rec.y, rec.z, rec.w);  // a multi-candidate record names its global slot
-        if (cnt > (uint32_t)kWQ3) {  // a round of more hits than wq holds (dense data): two halves
-            if (hit && rank < (uint32_t)kWQ3) wq[rank] = e;
-            verify_l1<kWinLds>(a, wq, kWQ3, rows, tile_start, cur);
-            if (hit && rank >= (uint32_t)kWQ3) wq[rank - kWQ3] = e;
-            nwq = cnt - kWQ3;
-        } else {
-            if (hit) wq[nwq + rank] = e;
-            nwq += cnt;
-        }
-    }
-    verify_l1<kWinLds>(a, wq, nwq, rows, tile_start, cur);
-    lds_fence();
-}
 
 // Exclusive wave scan (lane l gets the sum over lanes < l) and the wave total: DPP
 // row_shr steps inside each 16-lane row, then the row totals through SGPRs (no LDS
@@ -1994,6 +1851,138 @@ __device__ __forceinline__ uint64_t wave_strong_regs(const uint32_t (&xo)[16], c
            (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)h, 0);
 }
 
+// ---------------------------------------------------------------------------
+// Per-wave staging of appended outputs (WaveOut)
+// ---------------------------------------------------------------------------
+// The register-fed scans and k_verify_w append verified hits (and k_scan_g its deferred
+// weak hits) to lists shared by the whole launch.  Taking list slots with a returning
+// atomicAdd per wave round costs one device-scope atomic on ONE word per round with a
+// hit, and one word serves about 88 of those per microsecond chip-wide
+// (MI355X_MICROARCH.md, dequeue): C3b's 1 M verified hits (one per wave tile) queued
+// behind it, +4.7 ms of k_scan_r (profiles/r04c_c3b_bench.json).  So each wave writes its
+// outputs to its own region (ScanArgs::hstage / dstage, no atomics) and moves them to the
+// shared list with one atomicAdd per flush (a full region, or the wave's end).  The
+// list's order changes, not its contents: the host sorts the hits by key.
+constexpr uint32_t kHStage = 256;  // verified hits staged per wave {key lo, key hi, block, 0}
+constexpr uint32_t kDStage = 64;   // deferred weak hits staged per wave
+
+struct WaveOut {
+    uint4* h;     // this wave's hit region
+    WDef* d;      // this wave's deferred region (k_scan_g)
+    uint32_t nh;  // staged hits (wave-uniform)
+    uint32_t nd;  // staged deferred hits (wave-uniform)
+};
+
+// gwave: the wave's index in the launch (regions are kHStage / kDStage entries apart)
+__device__ __forceinline__ WaveOut wave_out(const ScanArgs& a, uint64_t gwave) {
+    WaveOut o;
+    o.h = a.hstage + gwave * kHStage;
+    o.d = a.dstage ? a.dstage + gwave * kDStage : nullptr;
+    o.nh = 0;
+    o.nd = 0;
+    return o;
+}
+
+// Move the staged hits to the output list [counters[0], +nh) (slots past out_cap are
+// counted, not written: the host grows the list and scans again).
+__device__ __forceinline__ void flush_hits(const ScanArgs& a, WaveOut& o) {
+    if (!o.nh) return;
+    const uint32_t lane = threadIdx.x & 63;
+    __threadfence_block();  // this wave's staging stores before its loads
+    unsigned long long k0 = 0;
+    if (lane == 0) k0 = atomicAdd(&a.counters[0], (unsigned long long)o.nh);
+    k0 = shfl64(k0, 0);
+    for (uint32_t i = lane; i < o.nh; i += 64) {
+        const volatile uint4* g = o.h + i;  // rewritten by later flushes: not from a stale L1 line
+        const uint32_t lo = g->x, hi = g->y, blk = g->z;
+        const unsigned long long k = k0 + i;
+        if (k < a.out_cap) {
+            a.hit_key[k] = ((uint64_t)hi << 32) | lo;
+            a.hit_val[k] = blk;
+        }
+    }
+    o.nh = 0;
+}
+
+// Stage the hits of the lanes with v (key, block): wave-uniform call.
+__device__ __forceinline__ void stage_hits(const ScanArgs& a, WaveOut& o, bool v, uint64_t key, uint32_t blk) {
+    const uint64_t m = __ballot(v);
+    if (!m) return;
+    const uint32_t c = __popcll(m);
+    if (o.nh + c > kHStage) flush_hits(a, o);
+    const uint32_t lane = threadIdx.x & 63;
+    if (v) o.h[o.nh + __popcll(m & ((1ull << lane) - 1))] = make_uint4((uint32_t)key, (uint32_t)(key >> 32), blk, 0);
+    o.nh += c;
+}
+
+// One deferred weak hit verified by the whole wave from global memory (the window at
+// d.at): XXH3 of the window, then the first candidate in index order with equal strong
+// (generator.rs:127-133).  Every lane returns the block or kNoBlock.
+__device__ __forceinline__ uint32_t verify_def(const ScanArgs& a, const WDef& d) {
+    uint64_t st;
+    if (a.n > 240) {
+        uint32_t wk;
+        wave_hash_long(a.src + d.at, a.n, wk, st);
+    } else {  // XXH3's short paths
+        st = 0;
+        if ((threadIdx.x & 63) == 0) st = xxh3_short(a.src + d.at, a.n);
+        st = shfl64(st, 0);
+    }
+    if (!(d.cand & kMulti)) return st == d.strong ? d.cand : kNoBlock;
+    return first_strong_match(a.order, a.cstrong, a.start[d.cand & ~kMulti], a.cnt[d.cand & ~kMulti], st);
+}
+
+// Move the staged deferred weak hits to a.wdef [counters[10], +nd); the ones past
+// wdef_cap are verified here, one window per wave step (their hits staged).
+__device__ __forceinline__ void flush_defs(const ScanArgs& a, WaveOut& o) {
+    if (!o.nd) return;
+    const uint32_t lane = threadIdx.x & 63;
+    __threadfence_block();
+    unsigned long long k0 = 0;
+    if (lane == 0) k0 = atomicAdd(&a.counters[10], (unsigned long long)o.nd);
+    k0 = shfl64(k0, 0);
+    for (uint32_t i = lane; i < o.nd; i += 64) {
+        const unsigned long long k = k0 + i;
+        if (k < a.wdef_cap) {
+            const volatile uint64_t* g = (const volatile uint64_t*)(o.d + i);
+            WDef d;
+            d.at = g[0];
+            d.key = g[1];
+            const uint64_t cp = g[2];
+            d.cand = (uint32_t)cp;
+            d.pad = 0;
+            d.strong = g[3];
+            a.wdef[k] = d;
+        }
+    }
+    if (k0 + o.nd > a.wdef_cap) {  // the list is full: verify the rest here
+        const uint32_t first = k0 >= a.wdef_cap ? 0u : (uint32_t)(a.wdef_cap - k0);
+        for (uint32_t i = first; i < o.nd; ++i) {  // wave-uniform
+            const volatile uint64_t* g = (const volatile uint64_t*)(o.d + i);
+            WDef d;
+            d.at = g[0];
+            d.key = g[1];
+            d.cand = (uint32_t)g[2];
+            d.pad = 0;
+            d.strong = g[3];
+            const uint32_t best = verify_def(a, d);
+            stage_hits(a, o, lane == 0 && best != kNoBlock, d.key, best);
+        }
+    }
+    o.nd = 0;
+}
+
+// Stage the deferred weak hits of the lanes with v: wave-uniform call.
+__device__ __forceinline__ void stage_defs(const ScanArgs& a, WaveOut& o, bool v, const WDef& d) {
+    const uint64_t m = __ballot(v);
+    if (!m) return;
+    const uint32_t c = __popcll(m);
+    if (o.nd + c > kDStage) flush_defs(a, o);
+    const uint32_t lane = threadIdx.x & 63;
+    if (v) o.d[o.nd + __popcll(m & ((1ull << lane) - 1))] = d;
+    o.nd += c;
+}
+
 // Inline drain of one wave tile's level-2 pass records [0, nr) (just written by this wave
 // to its region): keys-only lookups, 64 per round; each weak hit's window is hashed from
 // the registers (wave_strong_regs, one window at a time for the whole wave), the first
@@ -2004,9 +1993,9 @@ __device__ __forceinline__ uint64_t wave_strong_regs(const uint32_t (&xo)[16], c
 template <bool kSmall = false>
 __device__ __forceinline__ void drain_regs(const ScanArgs& a, const uint2* recs, uint32_t nr, uint32_t tile_rel,
                                            const uint32_t (&xo)[16], const uint32_t (&xi)[16], const uint64_t* kt,
-                                           unsigned long long& weak_hits, uint64_t run_start, const SegCtx& cur) {
+                                           unsigned long long& weak_hits, uint64_t run_start, const SegCtx& cur,
+                                           WaveOut& o) {
     const uint32_t lane = threadIdx.x & 63;
-    const uint64_t below = (1ull << lane) - 1;
     __threadfence_block();  // this wave's record stores before its loads
     for (uint32_t base = 0; base < nr; base += 64) {
         const uint32_t i = base + lane;
@@ -2047,17 +2036,8 @@ __device__ __forceinline__ void drain_regs(const ScanArgs& a, const uint2* recs,
             }
             if ((int)lane == h) best_mine = best;
         }
-        const bool v = best_mine != kNoBlock;
-        const uint64_t mv = __ballot(v);
-        if (!mv) continue;
-        unsigned long long k0 = 0;
-        if (lane == 0) k0 = atomicAdd(&a.counters[0], (unsigned long long)__popcll(mv));
-        k0 = shfl64(k0, 0);
-        const unsigned long long k = k0 + __popcll(mv & below);
-        if (v && k < a.out_cap) {
-            a.hit_key[k] = ((uint64_t)cur.seg_id << kSegShift) | (uint64_t)(run_start + pos - cur.pos_begin);
-            a.hit_val[k] = best_mine;
-        }
+        stage_hits(a, o, best_mine != kNoBlock,
+                   ((uint64_t)cur.seg_id << kSegShift) | (uint64_t)(run_start + pos - cur.pos_begin), best_mine);
     }
 }
 
@@ -2088,6 +2068,7 @@ __global__ __launch_bounds__(kWaves * 64, 1) void k_scan_r(ScanArgs a, uint32_t 
     uint2* rec = a.rrec + (size_t)gwave * kWTR;  // this wave's pass records (one wave tile)
     uint32_t* fslot = (uint32_t*)(smem + L.l1) + (size_t)wid * small_words;  // kSmall: this wave's filter
     uint32_t slot_file = 0xFFFFFFFFu;
+    WaveOut wo = wave_out(a, gwave);
 
     const uint32_t t_begin = blockIdx.x * per;
     const uint32_t t_end = min(a.ntiles, t_begin + per);
@@ -2272,7 +2253,8 @@ __global__ __launch_bounds__(kWaves * 64, 1) void k_scan_r(ScanArgs a, uint32_t 
                 }
                 passes += nrec - tile_rec;
                 if (nrec > tile_rec && !(kAblate && (a.ablate & 1)))
-                    drain_regs<kSmall>(a, rec + tile_rec, nrec - tile_rec, k * kWTR, xo, xi, kt, weak_hits, run_start, sc);
+                    drain_regs<kSmall>(a, rec + tile_rec, nrec - tile_rec, k * kWTR, xo, xi, kt, weak_hits, run_start, sc,
+                                       wo);
                 nrec = tile_rec;
 #pragma unroll
                 for (int i = 0; i < 16; ++i) {
@@ -2282,6 +2264,7 @@ __global__ __launch_bounds__(kWaves * 64, 1) void k_scan_r(ScanArgs a, uint32_t 
             }
         }
     }
+    flush_hits(a, wo);
     if (lane == 0 && passes) atomicAdd(&a.counters[2], passes);
     if (lane == 0 && weak_hits) atomicAdd(&a.counters[1], weak_hits);
 }
@@ -2372,14 +2355,12 @@ __device__ __forceinline__ void window_at(const uint8_t* src, uint64_t len, uint
 }
 
 // Lookups of one wave tile's level-2 pass records (keys-only bucket reads, 64 per round);
-// weak hits go to the deferred list a.wdef (counters[10] counts them) for k_verify_w, or,
-// past its capacity, are verified here from global memory (verify_l1<false>).
-__device__ __forceinline__ void drain_g(const ScanArgs& a, const uint2* recs, uint32_t nr, uint4* wq,
-                                        unsigned long long& weak_hits, uint64_t run_start, const SegCtx& cur) {
+// weak hits are staged for the deferred list a.wdef (flush_defs), which k_verify_w hashes
+// after the scan.
+__device__ __forceinline__ void drain_g(const ScanArgs& a, const uint2* recs, uint32_t nr, unsigned long long& weak_hits,
+                                        uint64_t run_start, const SegCtx& cur, WaveOut& o) {
     const uint32_t lane = threadIdx.x & 63;
-    const uint64_t below = (1ull << lane) - 1;
     __threadfence_block();  // this wave's record stores before its loads
-    uint32_t nwq = 0;
     for (uint32_t base = 0; base < nr; base += 64) {
         const uint32_t i = base + lane;
         bool hit = false;
@@ -2393,58 +2374,27 @@ __device__ __forceinline__ void drain_g(const ScanArgs& a, const uint2* recs, ui
         }
         const uint64_t m = __ballot(hit);
         if (!m) continue;
-        const uint32_t cnt = __popcll(m);
-        weak_hits += cnt;
+        weak_hits += __popcll(m);
         if (a.ablate & 8) continue;
-        unsigned long long k0 = 0;
-        if (lane == 0) k0 = atomicAdd(&a.counters[10], (unsigned long long)cnt);
-        k0 = shfl64(k0, 0);
-        const uint64_t slot = k0 + __popcll(m & below);
-        const bool deferred = hit && slot < a.wdef_cap;
-        if (deferred) {
-            const uint64_t p = run_start + pos;
-            WDef d;
-            d.at = (uint64_t)(cur.base - a.src) + p;
-            d.key = ((uint64_t)cur.seg_id << kSegShift) | (p - cur.pos_begin);
-            d.cand = rec.y;
-            d.pad = 0;
-            d.strong = ((uint64_t)rec.w << 32) | rec.z;
-            a.wdef[slot] = d;
-        }
-        const uint64_t mi = __ballot(hit && !deferred);
-        if (!mi) continue;
-        const uint32_t ci = __popcll(mi);
-        const uint32_t rank = __popcll(mi & below);
-        const uint4 e = make_uint4(pos, rec.y, rec.z, rec.w);
-        const bool mine = hit && !deferred;
-        if (nwq + ci > (uint32_t)kWQ3) {
-            verify_l1<false>(a, wq, nwq, nullptr, run_start, cur);
-            nwq = 0;
-        }
-        if (ci > (uint32_t)kWQ3) {  // more than wq holds: two halves
-            if (mine && rank < (uint32_t)kWQ3) wq[rank] = e;
-            verify_l1<false>(a, wq, kWQ3, nullptr, run_start, cur);
-            if (mine && rank >= (uint32_t)kWQ3) wq[rank - kWQ3] = e;
-            nwq = ci - kWQ3;
-        } else {
-            if (mine) wq[nwq + rank] = e;
-            nwq += ci;
-        }
+        const uint64_t p = run_start + pos;
+        WDef d;
+        d.at = (uint64_t)(cur.base - a.src) + p;
+        d.key = ((uint64_t)cur.seg_id << kSegShift) | (p - cur.pos_begin);
+        d.cand = rec.y;
+        d.pad = 0;
+        d.strong = ((uint64_t)rec.w << 32) | rec.z;
+        stage_defs(a, o, hit, d);
     }
-    verify_l1<false>(a, wq, nwq, nullptr, run_start, cur);
-    lds_fence();
 }
 
 // kSmall's drain: exact-table lookups (table_find; small indexes carry no fat table), 64
-// per round; each weak hit goes to the deferred list as {window, key, kMulti | global
-// slot} (k_verify_w looks its candidates up in index order), or past the list's capacity
-// is verified here from global memory.
-__device__ __forceinline__ void drain_gs(const ScanArgs& a, const uint2* recs, uint32_t nr, uint4* wq,
-                                         unsigned long long& weak_hits, uint64_t run_start, const SegCtx& cur) {
+// per round; each weak hit is staged for the deferred list as {window, key, kMulti |
+// global slot} (k_verify_w looks its candidates up in index order).
+__device__ __forceinline__ void drain_gs(const ScanArgs& a, const uint2* recs, uint32_t nr,
+                                         unsigned long long& weak_hits, uint64_t run_start, const SegCtx& cur,
+                                         WaveOut& o) {
     const uint32_t lane = threadIdx.x & 63;
-    const uint64_t below = (1ull << lane) - 1;
     __threadfence_block();  // this wave's record stores before its loads
-    uint32_t nwq = 0;
     for (uint32_t base = 0; base < nr; base += 64) {
         const uint32_t i = base + lane;
         bool hit = false;
@@ -2461,50 +2411,21 @@ __device__ __forceinline__ void drain_gs(const ScanArgs& a, const uint2* recs, u
         }
         const uint64_t m = __ballot(hit);
         if (!m) continue;
-        const uint32_t cnt = __popcll(m);
-        weak_hits += cnt;
+        weak_hits += __popcll(m);
         if (a.ablate & 8) continue;
-        unsigned long long k0 = 0;
-        if (lane == 0) k0 = atomicAdd(&a.counters[10], (unsigned long long)cnt);
-        k0 = shfl64(k0, 0);
-        const uint64_t slot = k0 + __popcll(m & below);
-        const bool deferred = hit && slot < a.wdef_cap;
-        if (deferred) {
-            const uint64_t p = run_start + pos;
-            WDef d;
-            d.at = (uint64_t)(cur.base - a.src) + p;
-            d.key = ((uint64_t)cur.seg_id << kSegShift) | (p - cur.pos_begin);
-            d.cand = kMulti | gslot;
-            d.pad = 0;
-            d.strong = 0;
-            a.wdef[slot] = d;
-        }
-        const uint64_t mi = __ballot(hit && !deferred);
-        if (!mi) continue;
-        const uint32_t ci = __popcll(mi);
-        const uint32_t rank = __popcll(mi & below);
-        const uint4 e = make_uint4(pos, kMulti | gslot, 0, 0);
-        const bool mine = hit && !deferred;
-        if (nwq + ci > (uint32_t)kWQ3) {
-            verify_l1<false>(a, wq, nwq, nullptr, run_start, cur);
-            nwq = 0;
-        }
-        if (ci > (uint32_t)kWQ3) {
-            if (mine && rank < (uint32_t)kWQ3) wq[rank] = e;
-            verify_l1<false>(a, wq, kWQ3, nullptr, run_start, cur);
-            if (mine && rank >= (uint32_t)kWQ3) wq[rank - kWQ3] = e;
-            nwq = ci - kWQ3;
-        } else {
-            if (mine) wq[nwq + rank] = e;
-            nwq += ci;
-        }
+        const uint64_t p = run_start + pos;
+        WDef d;
+        d.at = (uint64_t)(cur.base - a.src) + p;
+        d.key = ((uint64_t)cur.seg_id << kSegShift) | (p - cur.pos_begin);
+        d.cand = kMulti | gslot;
+        d.pad = 0;
+        d.strong = 0;
+        stage_defs(a, o, hit, d);
     }
-    verify_l1<false>(a, wq, nwq, nullptr, run_start, cur);
-    lds_fence();
 }
 
 struct LdsG {
-    uint32_t l1, ntab, wq, ctr, total;  // byte offsets
+    uint32_t l1, ntab, ctr, total;  // byte offsets
 };
 // small_words: kSmall's per-wave filter slot (the largest file filter of the index), else 0
 __host__ __device__ constexpr LdsG ldsg_layout(uint32_t small_words = 0) {
@@ -2512,7 +2433,6 @@ __host__ __device__ constexpr LdsG ldsg_layout(uint32_t small_words = 0) {
     uint32_t o = 0;
     L.l1 = o; o += small_words ? (kTR / 64) * small_words * 4 : kL1WordsR * 4;
     L.ntab = o; o += 256 * 4;
-    L.wq = o; o += (kTR / 64) * kWQ3 * 16;
     L.ctr = o; o += 16;
     L.total = o;
     return L;
@@ -2535,10 +2455,10 @@ __global__ __launch_bounds__(kTR, 2) void k_scan_g(ScanArgs a, uint32_t per, uin
     uint32_t* ntab = (uint32_t*)(smem + L.ntab);
     const uint32_t tid = threadIdx.x;
     const uint32_t lane = tid & 63, wid = tid >> 6;
-    uint4* wq = (uint4*)(smem + L.wq) + (size_t)wid * kWQ3;
     uint32_t* ctr = (uint32_t*)(smem + L.ctr);
     const uint32_t gwave = blockIdx.x * (kTR / 64) + wid;
     uint2* rec = a.rrec + (size_t)gwave * kWTR;  // this wave's pass records (one wave tile)
+    WaveOut wo = wave_out(a, gwave);
     uint32_t* fslot = (uint32_t*)(smem + L.l1) + (size_t)wid * small_words;  // kSmall: this wave's filter
 
     const uint32_t t_begin = blockIdx.x * per;
@@ -2722,8 +2642,8 @@ __global__ __launch_bounds__(kTR, 2) void k_scan_g(ScanArgs a, uint32_t per, uin
                 B0 = __builtin_amdgcn_readlane(bm, 63);
                 passes += nrec - tile_rec;
                 if (nrec > tile_rec && !(kAblate && (a.ablate & 1))) {
-                    if (kSmall) drain_gs(a, rec + tile_rec, nrec - tile_rec, wq, weak_hits, run_start, sc);
-                    else drain_g(a, rec + tile_rec, nrec - tile_rec, wq, weak_hits, run_start, sc);
+                    if (kSmall) drain_gs(a, rec + tile_rec, nrec - tile_rec, weak_hits, run_start, sc, wo);
+                    else drain_g(a, rec + tile_rec, nrec - tile_rec, weak_hits, run_start, sc, wo);
                 }
                 nrec = tile_rec;
 #pragma unroll
@@ -2734,6 +2654,8 @@ __global__ __launch_bounds__(kTR, 2) void k_scan_g(ScanArgs a, uint32_t per, uin
             }
         }
     }
+    flush_defs(a, wo);  // may stage hits (verified past the list's capacity)
+    flush_hits(a, wo);
     if (lane == 0 && passes) atomicAdd(&a.counters[2], passes);
     if (lane == 0 && weak_hits) atomicAdd(&a.counters[1], weak_hits);
 }
@@ -2751,6 +2673,7 @@ __global__ __launch_bounds__(256) void k_verify_w(ScanArgs a) {
     const uint64_t total = min((uint64_t)a.counters[10], a.wdef_cap);
     const uint64_t wave = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
     const uint64_t nwaves = ((uint64_t)gridDim.x * blockDim.x) >> 6;
+    WaveOut wo = wave_out(a, wave);
     const bool rows = a.n % 64 == 0 && a.n >= 256;  // row_hash: the long path, whole stripes
     const uint32_t per = rows ? 4u : 1u;
     for (uint64_t r0 = wave * per; r0 < total; r0 += nwaves * per) {  // wave-uniform
@@ -2791,18 +2714,9 @@ __global__ __launch_bounds__(256) void k_verify_w(ScanArgs a) {
                 best = first_strong_match(a.order, a.cstrong, a.start[d.cand & ~kMulti], a.cnt[d.cand & ~kMulti], st);
             }
         }
-        const bool v = live && (rows ? rl == 0 : lane == 0) && best != kNoBlock;
-        const uint64_t m = __ballot(v);
-        if (!m) continue;
-        unsigned long long k0 = 0;
-        if (lane == 0) k0 = atomicAdd(&a.counters[0], (unsigned long long)__popcll(m));
-        k0 = shfl64(k0, 0);
-        const unsigned long long k = k0 + __popcll(m & ((1ull << lane) - 1));
-        if (v && k < a.out_cap) {
-            a.hit_key[k] = d.key;
-            a.hit_val[k] = best;
-        }
+        stage_hits(a, wo, live && (rows ? rl == 0 : lane == 0) && best != kNoBlock, d.key, best);
     }
+    flush_hits(a, wo);
 }
 
 // Tail rule (generator.rs:156-184): at p* = len - last_size (last_size < n), the
@@ -3986,12 +3900,19 @@ hipError_t launch_scan(const uint8_t* d_buf, const ScanSeg* d_segs, uint32_t nse
             return v ? std::min<uint64_t>(v, 1u << 22) : (uint64_t)1 << 22;
         }();
         a.wdef_cap = wdef_cap;
-        const size_t rec_bytes = ((size_t)grid * (kTR / 64) * kWTR * sizeof(uint2) + 255) & ~(size_t)255;
+        const uint32_t verify_grid = 4 * (uint32_t)g_cus;  // k_verify_w: 4 waves per workgroup
+        const size_t scan_waves = (size_t)grid * (kTR / 64);
+        const size_t stage_waves = std::max(scan_waves, (size_t)verify_grid * 4);
+        const size_t rec_bytes = (scan_waves * kWTR * sizeof(uint2) + 255) & ~(size_t)255;
+        const size_t hst_bytes = stage_waves * kHStage * sizeof(uint4);
+        const size_t dst_bytes = scan_waves * kDStage * sizeof(WDef);
         void* buf = nullptr;
-        hipError_t e = dev_malloc_async(&buf, rec_bytes + a.wdef_cap * sizeof(WDef), s);
+        hipError_t e = dev_malloc_async(&buf, rec_bytes + hst_bytes + dst_bytes + a.wdef_cap * sizeof(WDef), s);
         if (e != hipSuccess) return e;
         a.rrec = (uint2*)buf;
-        a.wdef = (WDef*)((uint8_t*)buf + rec_bytes);
+        a.hstage = (uint4*)((uint8_t*)buf + rec_bytes);
+        a.dstage = (WDef*)((uint8_t*)buf + rec_bytes + hst_bytes);
+        a.wdef = (WDef*)((uint8_t*)buf + rec_bytes + hst_bytes + dst_bytes);
         {
             ProfScope ps(prof, s, "k_scan_g");
             const dim3 gd(grid), bd(kTR);
@@ -4004,7 +3925,7 @@ hipError_t launch_scan(const uint8_t* d_buf, const ScanSeg* d_segs, uint32_t nse
         e = hipGetLastError();
         if (e == hipSuccess && !(a.ablate & 1)) {
             ProfScope ps(prof, s, "k_verify_w");
-            hipLaunchKernelGGL(k_verify_w, dim3(4 * (uint32_t)g_cus), dim3(256), 0, s, a);
+            hipLaunchKernelGGL(k_verify_w, dim3(verify_grid), dim3(256), 0, s, a);
             e = hipGetLastError();
         }
         const hipError_t fe = hipFreeAsync(buf, s);
@@ -4039,12 +3960,13 @@ hipError_t launch_scan(const uint8_t* d_buf, const ScanSeg* d_segs, uint32_t nse
         uint32_t per = (uint32_t)((ntiles + (uint64_t)r_cus - 1) / (uint64_t)r_cus);
         per += per & 1;
         const uint32_t grid = (uint32_t)((ntiles + (uint64_t)per - 1) / per);
-        // pass records: one wave tile per wave
+        // pass records: one wave tile per wave; then each wave's staged hits
         const size_t rec_bytes = ((size_t)grid * waves * kWTR * sizeof(uint2) + 255) & ~(size_t)255;
         void* rbuf = nullptr;
-        hipError_t e = dev_malloc_async(&rbuf, rec_bytes, s);
+        hipError_t e = dev_malloc_async(&rbuf, rec_bytes + (size_t)grid * waves * kHStage * sizeof(uint4), s);
         if (e != hipSuccess) return e;
         a.rrec = (uint2*)rbuf;
+        a.hstage = (uint4*)((uint8_t*)rbuf + rec_bytes);
         {
             ProfScope ps(prof, s, "k_scan_r");
             const dim3 g(grid), b(64 * waves);
