@@ -578,7 +578,9 @@ def roofline(prof: dict, steps: int, algo_step: dict, positions=None, keys=None,
         # the ribbon level-1 (sydelta_internal.hpp: 852000..1100000 keys unless SYDELTA_L1
         # forces a layout) passes ~1/2 of the positions whatever the key count
         l1_env = os.environ.get("SYDELTA_L1", "")
-        ribbon = dom in l1_bits and keys and (l1_env == "ribbon" or (l1_env != "bloom" and 852000 <= keys <= 1100000))
+        # and only a scan of >= 2^31 positions builds it (sydelta_internal.hpp: kRibMinScan)
+        ribbon = dom in l1_bits and keys and (l1_env == "ribbon" or (l1_env != "bloom" and 852000 <= keys <= 1100000
+                                                                     and positions >= 1 << 31))
         per_pos = 1.0 if dom not in l1_bits else 0.5 if ribbon else 1.0 - math.exp(-keys / float(l1_bits[dom]))
         req = positions * per_pos / launches_per_step  # filter-word requests per launch
         rate = req / (avg_ms * 1e-3)

@@ -496,6 +496,14 @@ struct sydelta_index {
     void* d_pool = nullptr;           // one allocation for all index arrays
     size_t pool_bytes = 0;
     hipStream_t stream = nullptr;     // the stream the pool was allocated on
+    // the ribbon level-1 (ix.rib_l1): 0 none, 1 built by the first scan of >= kRibMinScan
+    // positions, 2 by the first scan (SYDELTA_L1=ribbon); built once, on the stream of the
+    // scan that builds it, which records rib_ev for scans on other streams
+    int rib_mode = 0;
+    std::mutex rib_mu;
+    bool rib_built = false;
+    hipStream_t rib_stream = nullptr;
+    hipEvent_t rib_ev = nullptr;
 };
 
 // Index memory is kept for the next index: a released index's allocation is held (one
@@ -536,6 +544,7 @@ hipError_t stream_after(hipStream_t to, hipStream_t from, int device) {
 
 static void index_release(sydelta_index* x) {
     if (!x) return;
+    if (x->rib_ev) (void)hipEventDestroy(x->rib_ev);
     if (x->d_pool) {
         KeptPool old;
         const hipStream_t home = thread_stream(x->device);
@@ -577,6 +586,8 @@ namespace {
 std::mutex g_scratch_mu;
 struct ThreadScratch {
     std::map<int, HitScratch> hits;  // per device
+    std::map<int, DevScratch> scan;  // per device: launch_scan's scratch
+    std::map<int, DevScratch> probe;  // per device: the aligned probe's jobs and results
     PinnedHits pinned;
 };
 std::vector<ThreadScratch*> g_scratch;  // every thread's (never destroyed), for sydelta_trim
@@ -591,6 +602,8 @@ ThreadScratch& thread_scratch() {
 }
 }  // namespace
 HitScratch& thread_hit_scratch(int device) { return thread_scratch().hits[device]; }
+DevScratch& thread_scan_scratch(int device) { return thread_scratch().scan[device]; }
+DevScratch& thread_probe_scratch(int device) { return thread_scratch().probe[device]; }
 PinnedHits& thread_pinned_hits() { return thread_scratch().pinned; }
 }  // namespace sydelta
 
@@ -614,6 +627,14 @@ extern "C" void sydelta_trim(void) {
             (void)hipStreamSynchronize(thread_stream(kv.first));
         }
     t.hits.clear();
+    for (auto* m : {&t.scan, &t.probe}) {
+        for (auto& kv : *m)
+            if (kv.second.p && hipSetDevice(kv.first) == hipSuccess) {
+                (void)hipFreeAsync(kv.second.p, thread_stream(kv.first));
+                (void)hipStreamSynchronize(thread_stream(kv.first));
+            }
+        m->clear();
+    }
     if (t.pinned.p) (void)hipHostFree(t.pinned.p);
     t.pinned = PinnedHits();
 }
@@ -706,7 +727,9 @@ static int index_create_impl(int device, const uint32_t* weak, const uint64_t* s
     const bool want_rib = want_narrow && (l1e && !strcmp(l1e, "ribbon") ? true
                                           : l1e && !strcmp(l1e, "bloom") ? false
                                                                           : nblocks >= kRibMinKeys && nblocks <= kRibMaxKeys);
-    const size_t sz_rib = want_rib ? al(4ull * kRibShards * kRibCap) + al(4ull * (kRibShards + 1)) + al(4 * nb) : 0;
+    const size_t sz_rib = want_rib ? al(4ull * kL1WordsR) + al(4ull * kRibShards * kRibCap) + al(4ull * (kRibShards + 1)) +
+                                         al(4 * nb)
+                                   : 0;
     const size_t sz_fat = want_l1 ? al(16 * (size_t)sl) : 0;
     const size_t total = sz_weak + sz_strong + sz_filt + sz_l1 + sz_fat + 4 * sz_t + sz_order + sz_slot + sz_files +
                          sz_fblk + sz_cstrong + sz_rib;
@@ -723,8 +746,9 @@ static int index_create_impl(int device, const uint32_t* weak, const uint64_t* s
     if (want_l1) {
         ix.l1 = (uint32_t*)p; p += sz_l1;
         ix.l1_wshift = l1_wshift;
-        if (want_rib) {
-            ix.l1_ribbon = 1;
+        if (want_rib) {  // the Bloom stays in l1; the ribbon is built on demand (scan_index)
+            x->rib_mode = l1e && !strcmp(l1e, "ribbon") ? 2 : 1;
+            ix.rib_l1 = (uint32_t*)p; p += al(4ull * kL1WordsR);
             ix.rib_keys = (uint32_t*)p; p += al(4ull * kRibShards * kRibCap);
             ix.rib_cnt = (uint32_t*)p; p += al(4ull * (kRibShards + 1));
             ix.rib_over = (uint32_t*)p; p += al(4 * nb);
@@ -971,8 +995,6 @@ struct Classifier {
     uint64_t n = 0;
     std::vector<Src> src;
     uint64_t weak_hits = 0;
-    DevBuf q_buf;
-    size_t qcap = 0;
     // probed sources: their runs of blocks whose aligned window missed, [first, end)
     // local blocks, ascending; source i's are miss_runs[miss_off[i] .. miss_off[i+1])
     // (set by probe)
@@ -980,6 +1002,9 @@ struct Classifier {
     std::vector<size_t> miss_off;
     // the full probe pass's results on the device: source i's at d_probe_out + probe_pfx[i]
     DevBuf probe_buf;
+    // a transient classifier (one match call) takes its probe buffers from the calling
+    // thread's kept scratch instead (a chunk's outlives other calls on its thread)
+    DevScratch* probe_scratch = nullptr;
     uint32_t* d_probe_out = nullptr;
     std::vector<uint64_t> probe_pfx;
 
@@ -1111,14 +1136,27 @@ int Classifier::probe(int mode) {
         if (jb.p) { (void)hipFreeAsync(jb.p, s); jb.p = nullptr; }
         const size_t jbytes = (jobs.size() * sizeof(ProbeJob) + 255) & ~(size_t)255;
         const size_t obytes = (np * 4 + 255) & ~(size_t)255;
-        HIP_TRY(dev_malloc_async(&jb.p, jbytes + 2 * obytes + np * 8, s));
-        jb.s = s;
-        uint32_t* d_out = (uint32_t*)((uint8_t*)jb.p + jbytes);
+        const size_t need = jbytes + 2 * obytes + np * 8;
+        uint8_t* jp = nullptr;
+        if (probe_scratch) {  // the sample pass's results were read before the full pass reuses it
+            if (probe_scratch->bytes < need) {
+                if (probe_scratch->p) (void)hipFreeAsync(probe_scratch->p, s);
+                *probe_scratch = DevScratch();
+                HIP_TRY(dev_malloc_async(&probe_scratch->p, need + need / 4, s));
+                probe_scratch->bytes = need + need / 4;
+            }
+            jp = (uint8_t*)probe_scratch->p;
+        } else {
+            HIP_TRY(dev_malloc_async(&jb.p, need, s));
+            jb.s = s;
+            jp = (uint8_t*)jb.p;
+        }
+        uint32_t* d_out = (uint32_t*)(jp + jbytes);
         if (stride == 1) d_probe_out = d_out;
-        uint32_t* d_pw = (uint32_t*)((uint8_t*)jb.p + jbytes + obytes);
-        uint64_t* d_pst = (uint64_t*)((uint8_t*)jb.p + jbytes + 2 * obytes);
-        HIP_TRY(hipMemcpyAsync(jb.p, jobs.data(), jobs.size() * sizeof(ProbeJob), hipMemcpyHostToDevice, s));
-        HIP_TRY(launch_probe(base, (const ProbeJob*)jb.p, (uint32_t)jobs.size(), np, stride, (uint32_t)n, fast,
+        uint32_t* d_pw = (uint32_t*)(jp + jbytes + obytes);
+        uint64_t* d_pst = (uint64_t*)(jp + jbytes + 2 * obytes);
+        HIP_TRY(hipMemcpyAsync(jp, jobs.data(), jobs.size() * sizeof(ProbeJob), hipMemcpyHostToDevice, s));
+        HIP_TRY(launch_probe(base, (const ProbeJob*)jp, (uint32_t)jobs.size(), np, stride, (uint32_t)n, fast,
                              ix->ix, d_pw, d_pst, d_out, s, prof));
         HIP_TRY(hipMemcpyAsync(out, d_out, np * 4, hipMemcpyDeviceToHost, s));
         HIP_TRY(hipStreamSynchronize(s));
@@ -1147,8 +1185,10 @@ int Classifier::probe(int mode) {
     for (size_t i = 0; i < ns; ++i) {
         Src& c = src[i];
         c.probed = true;
-        c.ahit.resize(c.nblk);
-        c.scanned.assign(c.nblk, 0);
+        if (c.nblk > kPiece) {  // one piece per source is sized on its pool thread (C4: 10 000 sources)
+            c.ahit.resize(c.nblk);
+            c.scanned.assign(c.nblk, 0);
+        }
         for (uint64_t b = 0; b < c.nblk; b += kPiece) pieces.push_back({i, b, std::min(c.nblk, b + kPiece)});
     }
     struct Run {
@@ -1163,6 +1203,10 @@ int Classifier::probe(int mode) {
         for (size_t p = np * t / nthr, pe = np * (t + 1) / nthr; p < pe; ++p) {
             const Piece& q = pieces[p];
             const uint32_t* in = out + pfx[q.si];
+            if (src[q.si].nblk <= kPiece) {
+                src[q.si].ahit.resize(src[q.si].nblk);
+                src[q.si].scanned.assign(src[q.si].nblk, 0);
+            }
             memcpy(src[q.si].ahit.data() + q.b0, in + q.b0, (q.b1 - q.b0) * sizeof(uint32_t));
             uint64_t k = q.b0;
             while (k < q.b1) {
@@ -1203,6 +1247,30 @@ int Classifier::probe(int mode) {
         src[i].nahit = src[i].nblk - missed;
     }
     return SYDELTA_OK;
+}
+
+// The index a scan of tot_pos positions runs against: with the ribbon level-1 (built here
+// by the first scan that wants it, sydelta_index::rib_mode) or as built (the Bloom).
+static hipError_t scan_index(sydelta_index* x, uint64_t tot_pos, hipStream_t s, Profiler* prof, DeviceIndex& out) {
+    out = x->ix;
+    if (x->rib_mode == 0 || (x->rib_mode == 1 && tot_pos < kRibMinScan)) return hipSuccess;
+    {
+        std::lock_guard<std::mutex> lk(x->rib_mu);
+        if (!x->rib_built) {
+            if (hipError_t e = launch_ribbon_build(x->ix, s, prof)) return e;
+            if (!x->rib_ev) {
+                if (hipError_t e = hipEventCreateWithFlags(&x->rib_ev, hipEventDisableTiming)) return e;
+            }
+            if (hipError_t e = hipEventRecord(x->rib_ev, s)) return e;
+            x->rib_built = true;
+            x->rib_stream = s;
+        } else if (x->rib_stream != s) {
+            if (hipError_t e = hipStreamWaitEvent(s, x->rib_ev, 0)) return e;
+        }
+    }
+    out.l1 = out.rib_l1;
+    out.l1_ribbon = 1;
+    return hipSuccess;
 }
 
 int Classifier::scan(const std::vector<std::array<uint64_t, 3>>& ranges) {
@@ -1253,14 +1321,27 @@ int Classifier::scan(const std::vector<std::array<uint64_t, 3>>& ranges) {
     if (!wide) {
         HIP_TRY(dev_malloc_async(&seg_buf.p, segs.size() * sizeof(ScanSeg), s));
         seg_buf.s = s;
-        HIP_TRY(hipMemcpyAsync(seg_buf.p, segs.data(), segs.size() * sizeof(ScanSeg), hipMemcpyHostToDevice, s));
-        if (!q_buf.p) {
-            qcap = scan_queue_entries();
-            HIP_TRY(dev_malloc_async(&q_buf.p, qcap * sizeof(uint2), s));
-            q_buf.s = s;
+        // through the thread's pinned staging buffer: a pageable H2D of C4's 68 K segments
+        // (2.7 MB) is a staged, host-blocking copy.  The previous call on this thread
+        // synchronized its stream, so the buffer is free.
+        static thread_local std::pair<void*, size_t> seg_pin{nullptr, 0};  // never freed, like the streams
+        const size_t sbytes = segs.size() * sizeof(ScanSeg);
+        if (sbytes > (64u << 10)) {
+            if (seg_pin.second < sbytes) {
+                if (seg_pin.first) (void)hipHostFree(seg_pin.first);
+                seg_pin = {nullptr, 0};
+                HIP_TRY(hipHostMalloc(&seg_pin.first, sbytes + sbytes / 4, hipHostMallocDefault));
+                seg_pin.second = sbytes + sbytes / 4;
+            }
+            memcpy(seg_pin.first, segs.data(), sbytes);
+            HIP_TRY(hipMemcpyAsync(seg_buf.p, seg_pin.first, sbytes, hipMemcpyHostToDevice, s));
+        } else {
+            HIP_TRY(hipMemcpyAsync(seg_buf.p, segs.data(), sbytes, hipMemcpyHostToDevice, s));
         }
     }
     // verified hits: at most one per position; start from ~4 per block of positions
+    DeviceIndex dix;
+    HIP_TRY(scan_index(ix, tot_pos, s, prof, dix));
     uint64_t want = std::min<uint64_t>(tot_pos, tot_pos / n * 4 + (1 << 16));
     uint64_t cap = 0;
     unsigned long long counts[16] = {0};
@@ -1296,8 +1377,8 @@ int Classifier::scan(const std::vector<std::array<uint64_t, 3>>& ranges) {
         if (host_timing) fprintf(stderr, "sydelta scan setup: %.3f ms\n", ms_since(t0));
         if (!wide) {
             HIP_TRY(launch_scan(base, (const ScanSeg*)seg_buf.p, (uint32_t)segs.size(), (uint32_t)ntiles,
-                                (uint32_t)n, ix->ix, ix->d_strong, d_key, d_val, cap, d_counts, (uint2*)q_buf.p, qcap,
-                                s, prof));
+                                (uint32_t)n, dix, ix->d_strong, d_key, d_val, cap, d_counts, nullptr, 0,
+                                s, prof, &thread_scan_scratch(cur_dev)));
         } else {
             for (size_t g = 0; g < segs.size(); ++g)
                 HIP_TRY(launch_scan_wide(base + segs[g].src, segs[g].len, segs[g].pos_begin, segs[g].pos_end,
@@ -1870,6 +1951,11 @@ static int match_impl(sydelta_index* ix, const uint8_t* d_buf, const uint64_t* s
     C.n = n;
     C.src.resize(nf);
     C.adopt_spare();
+    {
+        int cur_dev = 0;
+        HIP_TRY(hipGetDevice(&cur_dev));
+        C.probe_scratch = &thread_probe_scratch(cur_dev);
+    }
     uint64_t tot_pos = 0;
     for (uint64_t f = 0; f < nf; ++f) {
         b->d[f].source_size = src_len[f];

@@ -50,6 +50,8 @@ struct PinnedHits {
 };
 constexpr size_t kPinnedHitsKeep = (size_t)256 << 20;
 HitScratch& thread_hit_scratch(int device);
+DevScratch& thread_scan_scratch(int device);   // launch_scan's kept scratch
+DevScratch& thread_probe_scratch(int device);  // Classifier::probe's (transient classifiers)
 PinnedHits& thread_pinned_hits();
 // sydelta_set_profiling state; CallProf collects one call's kernel timings.
 bool profiling_on();

@@ -40,7 +40,10 @@ constexpr uint32_t kL1WordsR = 38400;
 // One bit of result: a non-key passes with probability ~1/2 however the bits are spent
 // (0.504 measured on Adler values of 1 Mi random 4 KiB blocks, tools/ribbon_sim.c), against
 // 1 - e^(-keys/1228800) for the one-hash Bloom of the same 150 KiB (0.574 at 1 Mi keys):
-// built when the index has kRibMinKeys..kRibMaxKeys blocks (the two cross at ~852 K keys).
+// allocated when the index has kRibMinKeys..kRibMaxKeys blocks (the two cross at ~852 K
+// keys) and built by the first scan of at least kRibMinScan positions (its ~0.35 ms of
+// listing and solving pays back ~0.17 ms per 2^30 positions: C3's whole-file scan builds
+// it, C5's scan of its edited blocks does not).
 // Homogeneous: every system is consistent, so no key set makes the build fail (a shard
 // loaded past its columns only passes more positions).
 constexpr uint32_t kRibShards = 1024;
@@ -52,6 +55,7 @@ constexpr uint64_t kRibMinKeys = 852000;
 // ... and at most kRibMaxKeys: beyond ~0.95 keys per column a shard's system is full and
 // passes nearly every position (the Bloom's 1 - e^(-keys/1228800) is then lower).
 constexpr uint64_t kRibMaxKeys = 1100000;
+constexpr uint64_t kRibMinScan = 1ull << 31;
 // words of a level-1 filter: l1_wshift 1 marks k_scan_r's scaled-word layout, any other
 // value a power-of-two filter of 2^(32 - l1_wshift) words
 constexpr size_t l1_total_words(uint32_t l1_wshift) {
@@ -91,6 +95,9 @@ struct DeviceIndex {
                                 // (k_scan_r, k_scan_g) or with windows above scan_max_window() (k_scan_g)
     uint32_t l1_wshift = 1;     // 1: kL1WordsR words, l1r_word(q)
     uint32_t l1_ribbon = 0;     // with l1_wshift 1: the words hold the ribbon (kRibWords), not a Bloom filter
+    // the ribbon, built on demand (launch_ribbon_build) into rib_l1 (kL1WordsR words); a
+    // scan that uses it gets a copy of the index with l1 = rib_l1, l1_ribbon = 1
+    uint32_t* rib_l1 = nullptr;
     uint32_t* rib_keys = nullptr;  // ribbon build: kRibShards lists of kRibCap distinct keys
     uint32_t* rib_cnt = nullptr;   // kRibShards + 1 counts (the last: the overflow list's)
     uint32_t* rib_over = nullptr;  // overflow list (capacity nblocks)
@@ -134,19 +141,32 @@ hipError_t launch_signature_batch(const uint8_t* d_buf, const uint64_t* d_off, c
 // values (ix.nblocks entries; ix.d_fblk / ix.d_files already on the device).
 hipError_t launch_index_build(const uint32_t* d_weak, const uint64_t* d_strong, DeviceIndex& ix, hipStream_t s,
                               Profiler* prof);
+// The ribbon level-1 of a built single-file index (ix.rib_l1 and its key lists set):
+// its distinct keys listed by shard from the exact table, then each shard solved.
+hipError_t launch_ribbon_build(const DeviceIndex& ix, hipStream_t s, Profiler* prof);
 uint64_t scan_tile_positions();  // positions per tile of the LDS-staged scan
 // SYDELTA_SCAN_WIDE=0: windows above scan_max_window() take the per-thread k_scan
 // instead of the register-fed k_scan_g (read when the index is built and per call)
 int scan_wide_mode();
 uint32_t scan_max_window();      // largest block size the LDS-staged scan handles
 // Scratch the LDS-staged scan needs: filter-pass queues, scan_queue_entries() uint2
-// entries (2 workgroups per CU on up to 256 CUs; launch_scan checks).
+// entries (2 workgroups per CU on up to 256 CUs; launch_scan checks; with no queues
+// given it takes them from its scratch).
 size_t scan_queue_entries();
+// A device buffer kept between calls by its owner (the calling thread), grown on demand
+// in the owner's stream order.
+struct DevScratch {
+    void* p = nullptr;
+    size_t bytes = 0;
+};
 // Scan all tiles of segs[0..nsegs) (device copy d_segs; block_size n <= scan_max_window()).
+// scratch (may be null: allocated and freed per call) holds the register-fed scans' pass
+// records, staged outputs and deferred list; the previous use of it must have completed
+// (the caller synchronized its stream).
 hipError_t launch_scan(const uint8_t* d_buf, const ScanSeg* d_segs, uint32_t nsegs, uint32_t ntiles, uint32_t n,
                        const DeviceIndex& ix, const uint64_t* d_strong, uint64_t* d_hit_key, uint32_t* d_hit_val,
                        uint64_t out_cap, unsigned long long* d_counters, uint2* gfq, size_t gfq_cap, hipStream_t s,
-                       Profiler* prof);
+                       Profiler* prof, DevScratch* scratch = nullptr);
 // Fallback for block sizes above scan_max_window(): one segment, file 0 of ix, hits
 // keyed with seg_id.
 hipError_t launch_scan_wide(const uint8_t* d_src, uint64_t len, uint64_t pos_begin, uint64_t pos_end, uint32_t seg_id,

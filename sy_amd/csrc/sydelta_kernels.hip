@@ -402,15 +402,14 @@ static_assert(((kRibBits - 31) << 8) < (1u << 24), "rib_bit's constant is a 24-b
 __global__ void k_idx_insert(const uint32_t* __restrict__ weak, uint64_t n, const uint64_t* __restrict__ fblk,
                              uint32_t nf, const FileIx* __restrict__ files, uint32_t* __restrict__ filt,
                              uint32_t* __restrict__ l1, uint32_t l1_wshift, uint32_t* __restrict__ keys,
-                             uint32_t* __restrict__ cnt, uint32_t* __restrict__ slot_of, uint32_t* __restrict__ rib_keys,
-                             uint32_t* __restrict__ rib_cnt, uint32_t* __restrict__ rib_over) {
+                             uint32_t* __restrict__ cnt, uint32_t* __restrict__ slot_of) {
     const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
     const FileIx F = files[file_of_block(fblk, nf, i)];
     const uint32_t w = weak[i];
     const ProbeHash h = probe_hash(w);
     atomicOr(filt + F.filt_off + (h.r >> F.fwshift), filt_mask(h.q));
-    if (l1 && !rib_cnt)  // single-file index only (l1_test)
+    if (l1)  // single-file index only (l1_test)
         atomicOr(l1 + (l1_wshift == 1 ? (size_t)l1r_word(h.q) : (size_t)(h.q >> l1_wshift)), 1u << (h.q & 31));
     uint32_t b = bucket_hash(w) & F.bmask;
     for (;;) {
@@ -420,12 +419,6 @@ __global__ void k_idx_insert(const uint32_t* __restrict__ weak, uint64_t n, cons
             if (old == kEmptyKey || old == w) {
                 atomicAdd(&cnt[sl], 1u);
                 slot_of[i] = (uint32_t)sl;
-                if (rib_cnt && old == kEmptyKey) {  // a new distinct key: list it in its ribbon shard
-                    const uint32_t sh = h.q >> 22;
-                    const uint32_t rank = atomicAdd(&rib_cnt[sh], 1u);
-                    if (rank < kRibCap) rib_keys[(size_t)sh * kRibCap + rank] = w;
-                    else rib_over[atomicAdd(&rib_cnt[kRibShards], 1u)] = w;  // at most n distinct keys
-                }
                 return;
             }
         }
@@ -499,6 +492,20 @@ __global__ __launch_bounds__(64) void k_ribbon_build(const uint32_t* __restrict_
         }
         if (lane == 0) l1[sh * (kRibBits / 32) + wd] = zwin;
     }
+}
+
+// The ribbon's key lists: every distinct key of the (single-file) exact table in its
+// shard's list (q >> 22), past kRibCap in the overflow list.
+__global__ void k_ribbon_list(const uint32_t* __restrict__ keys, uint64_t nslots, uint32_t* __restrict__ rib_keys,
+                              uint32_t* __restrict__ rib_cnt, uint32_t* __restrict__ rib_over) {
+    const uint64_t j = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (j >= nslots) return;
+    const uint32_t w = keys[j];
+    if (w == kEmptyKey) return;
+    const uint32_t sh = probe_hash(w).q >> 22;
+    const uint32_t rank = atomicAdd(&rib_cnt[sh], 1u);
+    if (rank < kRibCap) rib_keys[(size_t)sh * kRibCap + rank] = w;
+    else rib_over[atomicAdd(&rib_cnt[kRibShards], 1u)] = w;  // at most nblocks distinct keys
 }
 
 // Candidates grouped by slot in index order: order = block indices stably sorted
@@ -3738,12 +3745,25 @@ hipError_t launch_signature_batch_fast(const uint8_t* d_buf, const uint64_t* d_a
     return hipGetLastError();
 }
 
+hipError_t launch_ribbon_build(const DeviceIndex& ix, hipStream_t s, Profiler* prof) {
+    if (!ix.rib_l1 || !ix.rib_keys || ix.nfiles != 1) return hipErrorInvalidValue;
+    hipError_t e;
+    if ((e = hipMemsetAsync(ix.rib_cnt, 0, 4 * (kRibShards + 1), s))) return e;
+    if ((e = hipMemsetAsync(ix.rib_l1, 0, 4 * (size_t)kL1WordsR, s))) return e;
+    ProfScope ps(prof, s, "k_ribbon_build");  // listing + solving
+    hipLaunchKernelGGL(k_ribbon_list, dim3(grid_for(ix.nslots, 256)), dim3(256), 0, s, ix.keys, (uint64_t)ix.nslots,
+                       ix.rib_keys, ix.rib_cnt, ix.rib_over);
+    if ((e = hipGetLastError())) return e;
+    hipLaunchKernelGGL(k_ribbon_build, dim3(kRibShards), dim3(64), 0, s, ix.rib_keys, ix.rib_cnt, ix.rib_over,
+                       ix.rib_l1);
+    return hipGetLastError();
+}
+
 hipError_t launch_index_build(const uint32_t* d_weak, const uint64_t* d_strong, DeviceIndex& ix, hipStream_t s,
                               Profiler* prof) {
     hipError_t e;
     if ((e = hipMemsetAsync(ix.filt, 0, ix.fwords * 4, s))) return e;
     if (ix.l1 && (e = hipMemsetAsync(ix.l1, 0, l1_total_words(ix.l1_wshift) * 4, s))) return e;
-    if (ix.l1_ribbon && (e = hipMemsetAsync(ix.rib_cnt, 0, 4 * (kRibShards + 1), s))) return e;
     if ((e = hipMemsetAsync(ix.keys, 0xFF, ix.nslots * 4, s))) return e;
     if ((e = hipMemsetAsync(ix.cnt, 0, ix.nslots * 4, s))) return e;
     const uint64_t n = ix.nblocks;
@@ -3752,12 +3772,7 @@ hipError_t launch_index_build(const uint32_t* d_weak, const uint64_t* d_strong, 
         ProfScope ps(prof, s, "k_idx_insert");
         hipLaunchKernelGGL(k_idx_insert, dim3(grid_for(n, 256)), dim3(256), 0, s, d_weak, n, ix.d_fblk,
                            (uint32_t)ix.nfiles, ix.d_files, ix.filt, ix.l1, ix.l1_wshift, ix.keys, ix.cnt,
-                           ix.slot_of, ix.rib_keys, ix.l1_ribbon ? ix.rib_cnt : nullptr, ix.rib_over);
-    }
-    if (ix.l1_ribbon) {
-        ProfScope ps(prof, s, "k_ribbon_build");
-        hipLaunchKernelGGL(k_ribbon_build, dim3(kRibShards), dim3(64), 0, s, ix.rib_keys, ix.rib_cnt, ix.rib_over, ix.l1);
-        if ((e = hipGetLastError())) return e;
+                           ix.slot_of);
     }
     size_t tmp = 0;
     if ((e = hipcub::DeviceScan::ExclusiveSum(nullptr, tmp, ix.cnt, ix.start, (int)ix.nslots, s))) return e;
@@ -3833,8 +3848,24 @@ size_t scan_queue_entries() { return (size_t)kWgPerCuMax2 * 256 * (kT2 / 64) * k
 hipError_t launch_scan(const uint8_t* d_buf, const ScanSeg* d_segs, uint32_t nsegs, uint32_t ntiles, uint32_t n,
                        const DeviceIndex& ix, const uint64_t* d_strong, uint64_t* d_hit_key, uint32_t* d_hit_val,
                        uint64_t out_cap, unsigned long long* d_counters, uint2* gfq, size_t gfq_cap, hipStream_t s,
-                       Profiler* prof) {
+                       Profiler* prof, DevScratch* scratch) {
     if (n == 0) return hipErrorInvalidValue;
+    // the register-fed scans' scratch: the caller's kept buffer (grown here), else one
+    // allocation per call (freeing ~100-200 MB per call blocked the host 0.3-0.6 ms, round 3)
+    auto scratch_get = [&](size_t bytes, void** p) -> hipError_t {
+        if (!scratch) return dev_malloc_async(p, bytes, s);
+        if (scratch->bytes < bytes) {
+            if (scratch->p) (void)hipFreeAsync(scratch->p, s);
+            scratch->p = nullptr;
+            scratch->bytes = 0;
+            const size_t b = bytes + bytes / 4;
+            if (hipError_t e = dev_malloc_async(&scratch->p, b, s)) return e;
+            scratch->bytes = b;
+        }
+        *p = scratch->p;
+        return hipSuccess;
+    };
+    auto scratch_put = [&](void* p) -> hipError_t { return scratch ? hipSuccess : hipFreeAsync(p, s); };
     if (n > kMaxN2 && !(ix.l1 && ix.l1_wshift == 1 && ix.fat && ix.nfiles == 1)) return hipErrorInvalidValue;
     if (ntiles == 0) return hipSuccess;
     ScanArgs a{};
@@ -3894,12 +3925,14 @@ hipError_t launch_scan(const uint8_t* d_buf, const ScanSeg* d_segs, uint32_t nse
         uint32_t per = (uint32_t)((ntiles + (uint64_t)g_cus - 1) / (uint64_t)g_cus);
         per = (per + rt - 1) / rt * rt;
         const uint32_t grid = (uint32_t)((ntiles + (uint64_t)per - 1) / per);
-        static const uint64_t wdef_cap = [] {
+        // the deferred list: one entry per 256 scanned positions, 64 Ki to 4 Mi (weak hits
+        // past it are verified inside the scan); SYDELTA_WDEF_CAP overrides (tests)
+        static const uint64_t wdef_env = [] {
             const char* e = getenv("SYDELTA_WDEF_CAP");
-            const uint64_t v = e ? strtoull(e, nullptr, 10) : 0;
-            return v ? std::min<uint64_t>(v, 1u << 22) : (uint64_t)1 << 22;
+            return e ? std::min<uint64_t>(strtoull(e, nullptr, 10), 1u << 22) : 0;
         }();
-        a.wdef_cap = wdef_cap;
+        a.wdef_cap = wdef_env ? wdef_env
+                              : std::min<uint64_t>(1u << 22, std::max<uint64_t>(1u << 16, (uint64_t)ntiles * kTile2 / 256));
         const uint32_t verify_grid = 4 * (uint32_t)g_cus;  // k_verify_w: 4 waves per workgroup
         const size_t scan_waves = (size_t)grid * (kTR / 64);
         const size_t stage_waves = std::max(scan_waves, (size_t)verify_grid * 4);
@@ -3907,7 +3940,7 @@ hipError_t launch_scan(const uint8_t* d_buf, const ScanSeg* d_segs, uint32_t nse
         const size_t hst_bytes = stage_waves * kHStage * sizeof(uint4);
         const size_t dst_bytes = scan_waves * kDStage * sizeof(WDef);
         void* buf = nullptr;
-        hipError_t e = dev_malloc_async(&buf, rec_bytes + hst_bytes + dst_bytes + a.wdef_cap * sizeof(WDef), s);
+        hipError_t e = scratch_get(rec_bytes + hst_bytes + dst_bytes + a.wdef_cap * sizeof(WDef), &buf);
         if (e != hipSuccess) return e;
         a.rrec = (uint2*)buf;
         a.hstage = (uint4*)((uint8_t*)buf + rec_bytes);
@@ -3928,7 +3961,7 @@ hipError_t launch_scan(const uint8_t* d_buf, const ScanSeg* d_segs, uint32_t nse
             hipLaunchKernelGGL(k_verify_w, dim3(verify_grid), dim3(256), 0, s, a);
             e = hipGetLastError();
         }
-        const hipError_t fe = hipFreeAsync(buf, s);
+        const hipError_t fe = scratch_put(buf);
         return e != hipSuccess ? e : fe;
     }
     // k_scan_r: one large file at n = 4096 (SYDELTA_SCAN_R_WAVES=8: two waves per SIMD)
@@ -3963,7 +3996,7 @@ hipError_t launch_scan(const uint8_t* d_buf, const ScanSeg* d_segs, uint32_t nse
         // pass records: one wave tile per wave; then each wave's staged hits
         const size_t rec_bytes = ((size_t)grid * waves * kWTR * sizeof(uint2) + 255) & ~(size_t)255;
         void* rbuf = nullptr;
-        hipError_t e = dev_malloc_async(&rbuf, rec_bytes + (size_t)grid * waves * kHStage * sizeof(uint4), s);
+        hipError_t e = scratch_get(rec_bytes + (size_t)grid * waves * kHStage * sizeof(uint4), &rbuf);
         if (e != hipSuccess) return e;
         a.rrec = (uint2*)rbuf;
         a.hstage = (uint4*)((uint8_t*)rbuf + rec_bytes);
@@ -3984,7 +4017,7 @@ hipError_t launch_scan(const uint8_t* d_buf, const ScanSeg* d_segs, uint32_t nse
 #undef LAUNCH_R
         }
         e = hipGetLastError();
-        const hipError_t fe = hipFreeAsync(rbuf, s);
+        const hipError_t fe = scratch_put(rbuf);
         return e != hipSuccess ? e : fe;
     }
     const bool lds_filter = ix.max_fwords <= kLdsFilterWordsMax;
@@ -4018,14 +4051,26 @@ hipError_t launch_scan(const uint8_t* d_buf, const ScanSeg* d_segs, uint32_t nse
     const uint32_t grid = (uint32_t)std::min<uint64_t>(ntiles, (uint64_t)num_cus * wg_per_cu);
     const uint32_t per = (ntiles + grid - 1) / grid;
     if (per >= (1u << 18)) return hipErrorInvalidValue;  // queue entries pack (tile - t_begin) in 18 bits
-    if (!gfq || gfq_cap < (size_t)grid * (kT2 / 64) * kGFQ) return hipErrorInvalidValue;
+    // the filter-pass queues: the caller's, else from the scratch
+    const size_t gfq_need = (size_t)grid * (kT2 / 64) * kGFQ;
+    void* qbuf = nullptr;
+    if (!gfq) {
+        if (hipError_t e = scratch_get(gfq_need * sizeof(uint2), &qbuf)) return e;
+        gfq = (uint2*)qbuf;
+        gfq_cap = gfq_need;
+    }
+    if (gfq_cap < gfq_need) return hipErrorInvalidValue;
     a.gfq = gfq;
-    ProfScope ps(prof, s, "k_scan_lds");
-    if (lds_filter)
-        hipLaunchKernelGGL(k_scan_lds<true>, dim3(grid), dim3(kT2), L.total, s, a, per, lds_fwords);
-    else
-        hipLaunchKernelGGL((k_scan_lds<false, 3, true>), dim3(grid), dim3(kT2), L.total, s, a, per, 0u);
-    return hipGetLastError();
+    {
+        ProfScope ps(prof, s, "k_scan_lds");
+        if (lds_filter)
+            hipLaunchKernelGGL(k_scan_lds<true>, dim3(grid), dim3(kT2), L.total, s, a, per, lds_fwords);
+        else
+            hipLaunchKernelGGL((k_scan_lds<false, 3, true>), dim3(grid), dim3(kT2), L.total, s, a, per, 0u);
+    }
+    const hipError_t e = hipGetLastError();
+    const hipError_t fe = qbuf ? scratch_put(qbuf) : hipSuccess;
+    return e != hipSuccess ? e : fe;
 }
 
 hipError_t launch_scan_wide(const uint8_t* d_src, uint64_t len, uint64_t pos_begin, uint64_t pos_end, uint32_t seg_id,

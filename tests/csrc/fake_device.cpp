@@ -326,6 +326,9 @@ hipError_t launch_signature_batch_fast(const uint8_t* d_buf, const uint64_t* d_a
     return hipSuccess;
 }
 
+// the emulated scans test windows against the exact keys, so the level-1 filters are not built
+hipError_t launch_ribbon_build(const DeviceIndex&, hipStream_t, Profiler*) { return hipSuccess; }
+
 hipError_t launch_index_build(const uint32_t* d_weak, const uint64_t* d_strong, DeviceIndex& ix, hipStream_t,
                               Profiler*) {
     EmuTimer emu_t;
@@ -353,7 +356,8 @@ size_t scan_queue_entries() { return 1024; }
 
 hipError_t launch_scan(const uint8_t* d_buf, const ScanSeg* d_segs, uint32_t nsegs, uint32_t, uint32_t n,
                        const DeviceIndex& ix, const uint64_t*, uint64_t* d_hit_key, uint32_t* d_hit_val,
-                       uint64_t out_cap, unsigned long long* d_counters, uint2*, size_t, hipStream_t, Profiler*) {
+                       uint64_t out_cap, unsigned long long* d_counters, uint2*, size_t, hipStream_t, Profiler*,
+                       DevScratch*) {
     EmuTimer emu_t;
     const FakeIndex& F = find_ix(ix);
     for (uint32_t g = 0; g < nsegs; ++g) {
