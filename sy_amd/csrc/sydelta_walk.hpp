@@ -250,6 +250,19 @@ inline int walk_src(const Src& c, uint64_t n, uint64_t entry, uint64_t end, cons
         }
         // next hit at or after x and before end: the next scan hit or the next aligned hit
         while (i < H && c.hpos[i] < x) ++i;
+        if (x == lit && x < end && i < H && c.hpos[i] == x) {
+            // a run of scan-hit Copies (a source shifted off the block grid: C3b, C4): a
+            // hit at x itself is the earliest hit at or after x (an aligned or phase-probed
+            // hit there names the same block), so copy it and jump a block, as below
+            do {
+                copy(c.hblk[i]);
+                x += n;
+                while (++i < H && c.hpos[i] < x) {
+                }
+            } while (x < end && i < H && c.hpos[i] == x);
+            lit = x;
+            continue;
+        }
         uint64_t p = end;
         uint32_t pb = kNoBlk;
         if (i < H && c.hpos[i] < end) { p = c.hpos[i]; pb = c.hblk[i]; }
