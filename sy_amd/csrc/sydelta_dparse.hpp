@@ -43,10 +43,14 @@ struct DArgs {
 };
 
 __host__ __device__ __forceinline__ bool is_digit(uint8_t c) { return c >= '0' && c <= '9'; }
-__host__ __device__ __forceinline__ bool op_start(const uint8_t* t, uint64_t p) {
+// T: the text as a byte pointer, or any type with operator[](uint64_t) -> uint8_t (the
+// kernels read their wave's tile from LDS, LdsText in sydelta_kernels.hip)
+template <class T>
+__host__ __device__ __forceinline__ bool op_start(const T& t, uint64_t p) {
     return t[p] == '{' && (p == kHead || (t[p - 1] == ',' && t[p - 2] == '}'));
 }
-__host__ __device__ __forceinline__ bool lit_start(const uint8_t* t, uint64_t p) {
+template <class T>
+__host__ __device__ __forceinline__ bool lit_start(const T& t, uint64_t p) {
     return is_digit(t[p]) && (t[p - 1] == '[' || t[p - 1] == ',');
 }
 __host__ __device__ __forceinline__ uint64_t chunk_lo(const DArgs& a, uint64_t c) { return kHead + c * kChunk; }
@@ -56,42 +60,52 @@ __host__ __device__ __forceinline__ uint64_t chunk_hi(const DArgs& a, uint64_t c
 }
 
 // Op starts and literal starts in chunk c.
-__host__ __device__ inline void chunk_count(const DArgs& a, uint64_t c, uint64_t& nops, uint64_t& nlit) {
+template <class T>
+__host__ __device__ inline void chunk_count(const DArgs& a, const T& t, uint64_t c, uint64_t& nops, uint64_t& nlit) {
     nops = nlit = 0;
     for (uint64_t p = chunk_lo(a, c); p < chunk_hi(a, c); ++p) {
-        nops += op_start(a.t, p);
-        nlit += lit_start(a.t, p);
+        nops += op_start(t, p);
+        nlit += lit_start(t, p);
     }
+}
+__host__ __device__ inline void chunk_count(const DArgs& a, uint64_t c, uint64_t& nops, uint64_t& nlit) {
+    chunk_count(a, a.t, c, nops, nlit);
 }
 
 // Position of every op start of chunk c, by rank.
-__host__ __device__ inline void chunk_place(const DArgs& a, uint64_t c, uint64_t rank, uint64_t* pos) {
+template <class T>
+__host__ __device__ inline void chunk_place(const DArgs& a, const T& t, uint64_t c, uint64_t rank, uint64_t* pos) {
     for (uint64_t p = chunk_lo(a, c); p < chunk_hi(a, c); ++p)
-        if (op_start(a.t, p)) pos[rank++] = p;
+        if (op_start(t, p)) pos[rank++] = p;
+}
+__host__ __device__ inline void chunk_place(const DArgs& a, uint64_t c, uint64_t rank, uint64_t* pos) {
+    chunk_place(a, a.t, c, rank, pos);
 }
 
 // Literal starts before position x (kHead <= x <= e): the chunk's rank plus a recount.
-__host__ __device__ inline uint64_t lits_before(const DArgs& a, const uint64_t* lrank, uint64_t x) {
+template <class T>
+__host__ __device__ inline uint64_t lits_before(const DArgs& a, const T& t, const uint64_t* lrank, uint64_t x) {
     if (x >= a.e) return lrank[a.nc];  // lrank holds nc + 1 entries: the total last
     const uint64_t c = (x - kHead) / kChunk;
     uint64_t r = lrank[c];
-    for (uint64_t p = chunk_lo(a, c); p < x; ++p) r += lit_start(a.t, p);
+    for (uint64_t p = chunk_lo(a, c); p < x; ++p) r += lit_start(t, p);
     return r;
 }
 
 // What may follow an op ending at q: ',' and the next op's '{', or the region's end.
-__host__ __device__ __forceinline__ bool op_follow(const DArgs& a, uint64_t q) {
-    return q == a.e || (q + 1 < a.e && a.t[q] == ',' && a.t[q + 1] == '{');
+template <class T>
+__host__ __device__ __forceinline__ bool op_follow(const DArgs& a, const T& t, uint64_t q) {
+    return q == a.e || (q + 1 < a.e && t[q] == ',' && t[q + 1] == '{');
 }
 
 // Chunk c's ops and literal bytes.  orank/lrank: exclusive scans (lrank with the total
 // at nc), pos: op starts by rank (nops entries).  Writes ops[rank] (kind, a = literal
 // offset or basis offset, b = size) and lit[rank] (lit NULL: checked only).  Returns the
 // first bad position in the chunk or kNoBad.
-__host__ __device__ inline uint64_t chunk_parse(const DArgs& a, uint64_t c, const uint64_t* orank,
+template <class T>
+__host__ __device__ inline uint64_t chunk_parse(const DArgs& a, const T& t, uint64_t c, const uint64_t* orank,
                                                const uint64_t* lrank, const uint64_t* pos, uint64_t nops,
                                                sydelta_op* ops, uint8_t* lit) {
-    const uint8_t* t = a.t;
     const uint64_t len = a.e;  // no token of R reads past its ']'
     uint64_t ork = orank[c], lrk = lrank[c];
     // The chain starts at the first op: a non-empty region must open with one, or the
@@ -108,7 +122,7 @@ __host__ __device__ inline uint64_t chunk_parse(const DArgs& a, uint64_t c, cons
                 if (!sigjson::get_lit(t, len, q, ",\"size\":") || !(k = sigjson::get_dec(t, len, q, UINT64_MAX, sz)))
                     return p;
                 q += k;
-                if (!sigjson::get_lit(t, len, q, "}}") || !op_follow(a, q)) return p;
+                if (!sigjson::get_lit(t, len, q, "}}") || !op_follow(a, t, q)) return p;
                 op.kind = SYDELTA_OP_COPY;
                 op.a = o;
                 op.b = sz;
@@ -117,15 +131,15 @@ __host__ __device__ inline uint64_t chunk_parse(const DArgs& a, uint64_t c, cons
                 if (!sigjson::get_lit(t, len, q, "{\"Data\":[")) return p;
                 if (q < len && t[q] == ']') {  // empty Data
                     ++q;
-                    if (!sigjson::get_lit(t, len, q, "}") || !op_follow(a, q)) return p;
+                    if (!sigjson::get_lit(t, len, q, "}") || !op_follow(a, t, q)) return p;
                 } else if (!(q < len && is_digit(t[q]))) {
                     return p;  // the first literal (checked by its own thread) must start here
                 }
-                const uint64_t l0 = lits_before(a, lrank, q);
+                const uint64_t l0 = lits_before(a, t, lrank, q);
                 const uint64_t next = ork + 1 < nops ? pos[ork + 1] : a.e;
                 op.kind = SYDELTA_OP_DATA;
                 op.a = l0;
-                op.b = lits_before(a, lrank, next) - l0;
+                op.b = lits_before(a, t, lrank, next) - l0;
             }
             ops[ork++] = op;
         } else if (lit_start(t, p)) {
@@ -136,13 +150,18 @@ __host__ __device__ inline uint64_t chunk_parse(const DArgs& a, uint64_t c, cons
             if (q < len && t[q] == ',') {
                 if (!(q + 1 < len && is_digit(t[q + 1]))) return p;
             } else {
-                if (!sigjson::get_lit(t, len, q, "]}") || !op_follow(a, q)) return p;
+                if (!sigjson::get_lit(t, len, q, "]}") || !op_follow(a, t, q)) return p;
             }
             if (lit) lit[lrk] = (uint8_t)v;
             ++lrk;
         }
     }
     return kNoBad;
+}
+__host__ __device__ inline uint64_t chunk_parse(const DArgs& a, uint64_t c, const uint64_t* orank,
+                                               const uint64_t* lrank, const uint64_t* pos, uint64_t nops,
+                                               sydelta_op* ops, uint8_t* lit) {
+    return chunk_parse(a, a.t, c, orank, lrank, pos, nops, ops, lit);
 }
 
 }  // namespace dparse

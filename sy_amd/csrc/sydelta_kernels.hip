@@ -3163,30 +3163,86 @@ __global__ __launch_bounds__(256) void k_sigparse(const uint8_t* __restrict__ t,
     if (b != UINT64_MAX) atomicMin(bad, (unsigned long long)b);
 }
 
-// K7d: the compact Delta JSON parsed on the device (sydelta_dparse.hpp).
+// K7d: the compact Delta JSON parsed on the device (sydelta_dparse.hpp).  Each wave
+// takes 64 consecutive chunks (4 KiB of text) and first stages them, with 8 bytes before
+// and 136 after, in LDS (64-byte rows padded to 68 bytes, so the 64 lanes reading row l at
+// the same column hit different banks); the per-chunk bodies then read their bytes from
+// there (LdsText) and anything outside the staged span from global memory.  Round 3 ran
+// the same bodies on global memory, one byte load per character per thread with the
+// lanes 64 bytes apart: 113 GB/s of text over the three kernels.
+constexpr uint32_t kDpRow = 68;                          // LDS bytes per staged 64-byte row
+constexpr uint32_t kDpBefore = 8;                        // bytes staged before the wave's first chunk
+constexpr uint32_t kDpSpan = 64 * 64 + kDpBefore + 136;  // staged bytes per wave
+constexpr uint32_t kDpRows = (kDpSpan + 63) / 64;
+
+typedef __attribute__((address_space(3))) uint8_t lds_u8;  // an LDS pointer kept as one
+struct LdsText {
+    const uint8_t* g;   // the text
+    const lds_u8* l;    // the wave's staged rows
+    uint64_t p0, n;     // staged text [p0, p0 + n)
+    __device__ __forceinline__ uint8_t operator[](uint64_t p) const {
+        const uint64_t d = p - p0;
+        return d < n ? l[(d >> 6) * kDpRow + (d & 63)] : g[p];
+    }
+};
+
+// Stage this wave's span (chunks c0 .. c0 + 63) and return its accessor.
+__device__ __forceinline__ LdsText dp_stage(const dparse::DArgs& a, uint64_t c0, uint8_t* rows) {
+    const uint32_t lane = threadIdx.x & 63;
+    const uint64_t p0 = dparse::chunk_lo(a, c0) - kDpBefore;  // >= 0: chunk 0 starts at kHead = 8
+    const uint64_t hi = p0 + kDpSpan < a.e ? p0 + kDpSpan : a.e;
+    const uint32_t n = (uint32_t)(hi - p0);
+    const uint8_t* g = a.t + p0;
+    if (((uintptr_t)g & 3) == 0) {
+        for (uint32_t i = 4 * lane; i < n; i += 256) {
+            if (i + 4 <= n) {
+                *(uint32_t*)(rows + (i >> 6) * kDpRow + (i & 63)) = *(const uint32_t*)(g + i);
+            } else {
+                for (uint32_t j = i; j < n; ++j) rows[(j >> 6) * kDpRow + (j & 63)] = g[j];
+            }
+        }
+    } else {
+        for (uint32_t i = lane; i < n; i += 64) rows[(i >> 6) * kDpRow + (i & 63)] = g[i];
+    }
+    lds_fence();
+    return LdsText{a.t, (const lds_u8*)rows, p0, n};
+}
+
 __global__ __launch_bounds__(256) void k_dparse_count(dparse::DArgs a, uint64_t* __restrict__ ocnt,
                                                       uint64_t* __restrict__ lcnt) {
-    const uint64_t c = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+    __shared__ uint8_t st[4][kDpRows * kDpRow];
+    const uint64_t c0 = ((uint64_t)blockIdx.x * 256 + threadIdx.x) & ~63ull;  // the wave's first chunk
+    if (c0 >= a.nc) return;  // whole waves only
+    const LdsText t = dp_stage(a, c0, st[threadIdx.x >> 6]);
+    const uint64_t c = c0 + (threadIdx.x & 63);
     if (c >= a.nc) return;
     uint64_t no, nl;
-    dparse::chunk_count(a, c, no, nl);
+    dparse::chunk_count(a, t, c, no, nl);
     ocnt[c] = no;
     lcnt[c] = nl;
 }
 
 __global__ __launch_bounds__(256) void k_dparse_place(dparse::DArgs a, const uint64_t* __restrict__ orank,
                                                       uint64_t* __restrict__ pos) {
-    const uint64_t c = (uint64_t)blockIdx.x * 256 + threadIdx.x;
-    if (c < a.nc) dparse::chunk_place(a, c, orank[c], pos);
+    __shared__ uint8_t st[4][kDpRows * kDpRow];
+    const uint64_t c0 = ((uint64_t)blockIdx.x * 256 + threadIdx.x) & ~63ull;
+    if (c0 >= a.nc) return;
+    const LdsText t = dp_stage(a, c0, st[threadIdx.x >> 6]);
+    const uint64_t c = c0 + (threadIdx.x & 63);
+    if (c < a.nc) dparse::chunk_place(a, t, c, orank[c], pos);
 }
 
 __global__ __launch_bounds__(256) void k_dparse(dparse::DArgs a, const uint64_t* __restrict__ orank,
                                                 const uint64_t* __restrict__ lrank, const uint64_t* __restrict__ pos,
                                                 uint64_t nops, sydelta_op* __restrict__ ops, uint8_t* lit,
                                                 unsigned long long* bad) {
-    const uint64_t c = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+    __shared__ uint8_t st[4][kDpRows * kDpRow];
+    const uint64_t c0 = ((uint64_t)blockIdx.x * 256 + threadIdx.x) & ~63ull;
+    if (c0 >= a.nc) return;
+    const LdsText t = dp_stage(a, c0, st[threadIdx.x >> 6]);
+    const uint64_t c = c0 + (threadIdx.x & 63);
     if (c >= a.nc) return;
-    const uint64_t b = dparse::chunk_parse(a, c, orank, lrank, pos, nops, ops, lit);
+    const uint64_t b = dparse::chunk_parse(a, t, c, orank, lrank, pos, nops, ops, lit);
     if (b != dparse::kNoBad) atomicMin(bad, (unsigned long long)b);
 }
 

@@ -134,7 +134,10 @@ constexpr uint32_t kParseChunk = 64;  // text bytes per thread
 
 // Unsigned decimal at t[p]: digits only, no leading zero unless the number is 0, value <=
 // maxv.  Returns the digits consumed (0: not a number in range).
-__host__ __device__ inline uint32_t get_dec(const uint8_t* t, uint64_t len, uint64_t p, uint64_t maxv, uint64_t& v) {
+// T: a byte pointer, or any type with operator[](uint64_t) -> uint8_t (the device parsers'
+// LDS-staged text, sydelta_dparse.hpp LdsText)
+template <class T>
+__host__ __device__ inline uint32_t get_dec(const T& t, uint64_t len, uint64_t p, uint64_t maxv, uint64_t& v) {
     uint64_t x = 0;
     uint32_t k = 0;
     while (p + k < len && t[p + k] >= '0' && t[p + k] <= '9') {
@@ -148,7 +151,8 @@ __host__ __device__ inline uint32_t get_dec(const uint8_t* t, uint64_t len, uint
     return k;
 }
 
-__host__ __device__ inline bool get_lit(const uint8_t* t, uint64_t len, uint64_t& p, const char* s) {
+template <class T>
+__host__ __device__ inline bool get_lit(const T& t, uint64_t len, uint64_t& p, const char* s) {
     for (uint32_t k = 0; s[k]; ++k, ++p)
         if (p >= len || t[p] != (uint8_t)s[k]) return false;
     return true;
