@@ -2831,7 +2831,286 @@ struct ZLds {
     uint32_t cand[zstd::kCands];
     uint32_t ssize[4];
     uint32_t state[8];  // [0] type, [1] write offset, [2] abort, [3] entropy-only size, [4] nc, [5] nbest, [6] lz size
+    uint32_t rank[2][kZT];  // the parallel parse: per thread literals / sequences, then their exclusive scans
+    uint32_t pstate[8];     // [0] literals, [1] sequences, [2] literals section size, [3] raw, [4] write offset
 };
+
+// Bits of symbols src[first, first + count) coded with L.code, written as one literal
+// stream (last symbol first, LSB-first) into L.words with its closing 1 bit by a
+// parallel bit scatter: thread t encodes the run [A + kZRun t, +kZRun) (A = first
+// rounded down to 16; src 16-byte aligned and readable to the end of its last granule),
+// its first bit at the sum of the later runs' bits, OR-ing whole words.  Returns the
+// stream's bits without the closing bit (every thread).
+__device__ uint32_t z_stream_scatter(ZLds& L, const uint8_t* __restrict__ src, uint32_t first, uint32_t count) {
+    const uint32_t tid = threadIdx.x;
+    const uint32_t nw = (count * zstd::kMaxBits + 1 + 31) / 32 + 1;
+    for (uint32_t i = tid; i < nw; i += kZT) L.words[i] = 0;
+    const uint32_t A = first & ~15u, r0 = A + kZRun * tid, lim = first + count;
+    uint32_t x[kZRun / 4];
+#pragma unroll
+    for (uint32_t j = 0; j < kZRun / 16; ++j) {
+        uint4 v = make_uint4(0, 0, 0, 0);
+        if (r0 + 16 * j < lim) v = *(const uint4*)(src + r0 + 16 * j);
+        x[4 * j] = v.x; x[4 * j + 1] = v.y; x[4 * j + 2] = v.z; x[4 * j + 3] = v.w;
+    }
+    uint32_t bits = 0;
+#pragma unroll
+    for (uint32_t k = 0; k < kZRun; ++k) {
+        const uint32_t p = r0 + k;
+        if (p >= first && p < lim) bits += L.code.len[(x[k >> 2] >> (8 * (k & 3))) & 0xFF];
+    }
+    L.part[tid] = bits;
+    __syncthreads();
+    uint32_t off = 0, total = 0;
+    for (uint32_t t = 0; t < kZT; ++t) {  // LDS broadcast reads, uniform loop
+        const uint32_t pb = L.part[t];
+        total += pb;
+        off += t > tid ? pb : 0u;
+    }
+    uint32_t word = off >> 5, fill = off & 31;
+    uint64_t acc = 0;
+#pragma unroll
+    for (uint32_t kk = kZRun; kk-- > 0;) {
+        const uint32_t p = r0 + kk;
+        if (p >= first && p < lim) {
+            const uint32_t sym = (x[kk >> 2] >> (8 * (kk & 3))) & 0xFF;
+            acc |= (uint64_t)L.code.code[sym] << fill;
+            fill += L.code.len[sym];
+            if (fill >= 32) {
+                atomicOr(&L.words[word], (uint32_t)acc);
+                acc >>= 32;
+                fill -= 32;
+                ++word;
+            }
+        }
+    }
+    if (fill) atomicOr(&L.words[word], (uint32_t)acc);
+    __syncthreads();
+    if (tid == 0) atomicOr(&L.words[total >> 5], 1u << (total & 31));  // the closing bit
+    __syncthreads();
+    return total;
+}
+
+// The literals section of lit[0, nl) into out (global), as zstd::lit_section_seq writes
+// it: Huffman-coded with the streams scattered in parallel (z_stream_scatter), or Raw
+// when that is impossible or not smaller.  Returns its size (every thread).
+__device__ uint32_t z_lit_section(ZLds& L, const uint8_t* __restrict__ lit, uint32_t nl, uint8_t* __restrict__ out) {
+    const uint32_t tid = threadIdx.x, wid = tid >> 6;
+    for (uint32_t i = tid; i < 4 * 256; i += kZT) (&L.hist[0][0])[i] = 0;
+    __syncthreads();
+    for (uint32_t c = tid; 16 * c < nl; c += kZT) {
+        const uint4 v = *(const uint4*)(lit + 16 * c);
+        const uint32_t w4[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+        for (int k = 0; k < 16; ++k)
+            if (16 * c + k < nl) atomicAdd(&L.hist[wid][(w4[k >> 2] >> (8 * (k & 3))) & 0xFF], 1u);
+    }
+    __syncthreads();
+    for (uint32_t sy = tid; sy < 256; sy += kZT) L.hist[0][sy] += L.hist[1][sy] + L.hist[2][sy] + L.hist[3][sy];
+    __syncthreads();
+    const bool four = nl > zstd::kSingleStreamMax;
+    const uint32_t hs = four ? 5u : 3u;
+    const uint32_t raw_size = nl + (nl < 32 ? 1u : nl < 4096 ? 2u : 3u);
+    if (tid == 0) {
+        uint32_t distinct = 0, hi = 0;
+        for (uint32_t sy = 0; sy < 256; ++sy)
+            if (L.hist[0][sy]) { ++distinct; hi = sy; }
+        L.pstate[3] = (distinct < 2 || hi >= zstd::kSymbols) ? 1u : 0u;
+        if (!L.pstate[3]) {
+            zstd::huf_build(L.hist[0], L.code, L.work);
+            const uint32_t tsz = zstd::huf_tree_desc(L.code, out + hs);
+            L.pstate[4] = hs + tsz + (four ? 6u : 0u);
+        }
+    }
+    __syncthreads();
+    if (!L.pstate[3]) {
+        for (uint32_t st = 0; st < (four ? 4u : 1u); ++st) {
+            uint32_t first, count;
+            zstd::stream_range(nl, four, st, first, count);
+            const uint32_t total = z_stream_scatter(L, lit, first, count);
+            const uint32_t bytes = total / 8 + 1;
+            const uint32_t o = L.pstate[4];
+            if (o + bytes >= raw_size || (!four && o + bytes - hs > zstd::kSingleStreamMax)) {
+                __syncthreads();
+                if (tid == 0) L.pstate[3] = 1;
+                __syncthreads();
+                break;
+            }
+            const uint8_t* wb = (const uint8_t*)L.words;
+            for (uint32_t i = tid; i < bytes; i += kZT) out[o + i] = wb[i];
+            __syncthreads();
+            if (tid == 0) {
+                L.ssize[st] = bytes;
+                L.pstate[4] = o + bytes;
+            }
+            __syncthreads();
+        }
+    }
+    if (L.pstate[3]) {  // Raw literals
+        const uint32_t rh = nl < 32 ? 1u : nl < 4096 ? 2u : 3u;
+        if (tid == 0) zstd::raw_lit_header(out, nl);
+        for (uint32_t i = tid; i < nl; i += kZT) out[rh + i] = lit[i];
+        __syncthreads();
+        return rh + nl;
+    }
+    const uint32_t o = L.pstate[4];
+    if (tid == 0) {
+        zstd::lit_header(out, four, nl, o - hs);
+        if (four) {
+            const uint32_t tsz = 1 + (L.code.last + 1) / 2;
+            for (uint32_t k = 0; k < 3; ++k) {
+                out[hs + tsz + 2 * k] = (uint8_t)L.ssize[k];
+                out[hs + tsz + 2 * k + 1] = (uint8_t)(L.ssize[k] >> 8);
+            }
+        }
+    }
+    __syncthreads();
+    return o;
+}
+
+// Block-wide exclusive scan of v[0..kZT) in place (LDS); the total is returned to every
+// thread through *tot (LDS).
+__device__ uint32_t z_scan(uint32_t* v, uint32_t* tot) {
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        uint32_t sum = 0;
+        for (uint32_t t = 0; t < kZT; ++t) {
+            const uint32_t x = v[t];
+            v[t] = sum;
+            sum += x;
+        }
+        *tot = sum;
+    }
+    __syncthreads();
+    return *tot;
+}
+
+// The literals + sequences content of a block (zstd::lz_content's bytes) with the parse in
+// parallel.  The parse's path from position 0 is a function of the position alone
+// (zstd::parse_take / match_len), so each thread walks its own 512 positions from their
+// start, marking the positions it steps on in an LDS bitmap (L.words), and thread 0
+// chains the segments: where the true entry of a segment differs from its start, it walks
+// from the entry, clearing the speculative marks it jumps over, until it steps on a marked
+// position (the two walks agree from there on).  The marked positions are the literals
+// and the sequence starts: counted per thread, ranked, gathered (literals into sc.lit,
+// starts into sc.seq).  Wave 0 then runs the repeat history over the sequences in order
+// (zstd::seq_dist compared by the whole wave, rep_code), thread 0 codes them
+// (seq_section) after the literals section (z_lit_section).  Returns its size, 0 when
+// the block has no sequence (every thread).
+__device__ uint32_t z_lz_content(ZLds& L, const uint8_t* __restrict__ in, uint32_t n, const zstd::SeqScratch& sc) {
+    const uint32_t tid = threadIdx.x, lane = tid & 63;
+    constexpr uint32_t kSeg = zstd::kBlockMax / kZT;  // 512 positions per thread
+    static_assert(kSeg % 32 == 0 && zstd::kBlockMax / 32 <= kZStreamWords, "the path bitmap fits the stream words");
+    uint32_t* bm = L.words;
+    const uint32_t s0 = tid * kSeg, s1 = min(n, s0 + kSeg);
+    for (uint32_t w = tid * (kSeg / 32); w < (tid + 1) * (kSeg / 32); ++w) bm[w] = 0;
+    __syncthreads();
+    auto step = [&](uint32_t p) -> uint32_t {
+        return zstd::parse_take(sc.best, n, p) ? p + zstd::match_len(in, n, p, sc.best[p]) : p + 1;
+    };
+    // speculative walk of this thread's segment
+    uint32_t p = s0;
+    {
+        uint32_t cw = s0 >> 5, acc = 0;
+        while (p < s1) {
+            if ((p >> 5) != cw) {
+                bm[cw] = acc;
+                acc = 0;
+                cw = p >> 5;
+            }
+            acc |= 1u << (p & 31);
+            p = step(p);
+        }
+        if (s0 < s1) bm[cw] = acc;
+    }
+    L.part[tid] = s0 < n ? p : s0;  // the segment's exit
+    __syncthreads();
+    if (tid == 0) {
+        auto bit = [&](uint32_t x) { return (bm[x >> 5] >> (x & 31)) & 1u; };
+        auto clear = [&](uint32_t a, uint32_t b) {  // marks in [a, b)
+            for (uint32_t x = a; x < b;) {
+                if ((x & 31) == 0 && x + 32 <= b) { bm[x >> 5] = 0; x += 32; }
+                else { bm[x >> 5] &= ~(1u << (x & 31)); ++x; }
+            }
+        };
+        uint32_t e = L.part[0];
+        for (uint32_t t = 1; t < kZT && t * kSeg < n; ++t) {
+            const uint32_t a = t * kSeg, b = min(n, a + kSeg);
+            if (e == a) { e = L.part[t]; continue; }
+            if (e >= b) { clear(a, b); continue; }  // the path jumps over the whole segment
+            clear(a, e);
+            uint32_t x = e;
+            bool met = false;
+            while (x < b) {
+                if (bit(x)) { met = true; break; }
+                bm[x >> 5] |= 1u << (x & 31);
+                const uint32_t y = step(x);
+                clear(x + 1, min(y, b));
+                x = y;
+            }
+            e = met ? L.part[t] : x;
+        }
+    }
+    __syncthreads();
+    // count this segment's literals and sequence starts
+    uint32_t nlit = 0, nseq = 0;
+    for (uint32_t w = s0 >> 5; 32 * w < s1; ++w) {
+        uint32_t m = bm[w];
+        while (m) {
+            const uint32_t x = 32 * w + (uint32_t)__builtin_ctz(m);
+            m &= m - 1;
+            if (zstd::parse_take(sc.best, n, x)) ++nseq; else ++nlit;
+        }
+    }
+    L.rank[0][tid] = nlit;
+    L.rank[1][tid] = nseq;
+    const uint32_t nl = z_scan(L.rank[0], &L.pstate[0]);
+    const uint32_t ns = z_scan(L.rank[1], &L.pstate[1]);
+    if (ns == 0) return 0;  // uniform
+    // gather: literals into sc.lit, sequence starts into sc.seq as {p, length, best distance}
+    {
+        uint32_t lr = L.rank[0][tid], sr = L.rank[1][tid];
+        for (uint32_t w = s0 >> 5; 32 * w < s1; ++w) {
+            uint32_t m = bm[w];
+            while (m) {
+                const uint32_t x = 32 * w + (uint32_t)__builtin_ctz(m);
+                m &= m - 1;
+                if (zstd::parse_take(sc.best, n, x)) {
+                    const uint32_t b = sc.best[x];
+                    sc.seq[sr++] = zstd::Seq{x, zstd::match_len(in, n, x, b), b & 0xFFFFFFu, 0};
+                } else {
+                    sc.lit[lr++] = in[x];
+                }
+            }
+        }
+    }
+    __threadfence_block();
+    __syncthreads();
+    // the repeat history, in order (wave 0; uniform loop)
+    if (tid < 64) {
+        uint32_t rep[3] = {0, 0, 0}, end = 0;
+        for (uint32_t k = 0; k < ns; ++k) {
+            const zstd::Seq q = sc.seq[k];
+            const uint32_t x = q.ll, l = q.ml, d0 = q.off;
+            uint32_t d = d0;
+            if (rep[0] && rep[0] != d0 && rep[0] <= x) {  // zstd::seq_dist, compared by the wave
+                bool bad = false;
+                for (uint32_t i = lane; i < l; i += 64) bad |= in[x + i] != in[x + i - rep[0]];
+                if (!__ballot(bad)) d = rep[0];
+            }
+            const uint32_t ll = x - end;
+            const uint32_t ov = zstd::rep_code(rep, ll, d);
+            if (lane == 0) sc.seq[k] = zstd::Seq{ll, l, d, ov};
+            end = x + l;
+        }
+    }
+    __threadfence_block();
+    __syncthreads();
+    const uint32_t z = z_lit_section(L, sc.lit, nl, sc.body);
+    if (tid == 0) L.pstate[2] = z + zstd::seq_section(sc.seq, ns, sc.body + z, sc.fse[0], sc.fse[1], sc.fse[2]);
+    __syncthreads();
+    return L.pstate[2];
+}
 
 __global__ __launch_bounds__(kZT) void k_zstd_block(const uint8_t* __restrict__ text, uint64_t len, uint64_t b0,
                                                     uint8_t* __restrict__ slots, uint8_t* __restrict__ lz, uint64_t nlz,
@@ -2887,56 +3166,7 @@ __global__ __launch_bounds__(kZT) void k_zstd_block(const uint8_t* __restrict__ 
         for (uint32_t st = 0; st < ns; ++st) {
             uint32_t first, count;
             zstd::stream_range(n, four, st, first, count);
-            const uint32_t nw = (count * zstd::kMaxBits + 1 + 31) / 32 + 1;
-            for (uint32_t i = tid; i < nw; i += kZT) L.words[i] = 0;
-            // thread t's run: the stream's bytes inside [A + kZRun*t, +kZRun), A = first
-            // rounded down to 16, loaded as 9 aligned 16-byte chunks into registers (the
-            // unrolled loops below index them with constants)
-            const uint32_t A = first & ~15u, r0 = A + kZRun * tid, lim = first + count;
-            uint32_t x[kZRun / 4];
-#pragma unroll
-            for (uint32_t j = 0; j < kZRun / 16; ++j) {
-                uint4 v = make_uint4(0, 0, 0, 0);
-                if (r0 + 16 * j < lim) v = *(const uint4*)(in + r0 + 16 * j);
-                x[4 * j] = v.x; x[4 * j + 1] = v.y; x[4 * j + 2] = v.z; x[4 * j + 3] = v.w;
-            }
-            uint32_t bits = 0;
-#pragma unroll
-            for (uint32_t k = 0; k < kZRun; ++k) {
-                const uint32_t p = r0 + k;
-                if (p >= first && p < lim) bits += L.code.len[(x[k >> 2] >> (8 * (k & 3))) & 0xFF];
-            }
-            L.part[tid] = bits;
-            __syncthreads();
-            // bits written before this run: the runs after it (a suffix sum over threads)
-            uint32_t off = 0, total = 0;
-            for (uint32_t t = 0; t < kZT; ++t) {  // LDS broadcast reads, uniform loop
-                const uint32_t pb = L.part[t];
-                total += pb;
-                off += t > tid ? pb : 0u;
-            }
-            // this run, last symbol first, into whole words
-            uint32_t word = off >> 5, fill = off & 31;
-            uint64_t acc = 0;
-#pragma unroll
-            for (uint32_t kk = kZRun; kk-- > 0;) {
-                const uint32_t p = r0 + kk;
-                if (p >= first && p < lim) {
-                    const uint32_t sym = (x[kk >> 2] >> (8 * (kk & 3))) & 0xFF;
-                    acc |= (uint64_t)L.code.code[sym] << fill;
-                    fill += L.code.len[sym];
-                    if (fill >= 32) {
-                        atomicOr(&L.words[word], (uint32_t)acc);
-                        acc >>= 32;
-                        fill -= 32;
-                        ++word;
-                    }
-                }
-            }
-            if (fill) atomicOr(&L.words[word], (uint32_t)acc);
-            __syncthreads();
-            if (tid == 0) atomicOr(&L.words[total >> 5], 1u << (total & 31));  // the closing bit
-            __syncthreads();
+            const uint32_t total = z_stream_scatter(L, in, first, count);
             const uint32_t bytes = total / 8 + 1;
             const uint32_t o = L.state[1];
             // a stream that would not fit the block's own size: no entropy-only content
@@ -3008,12 +3238,10 @@ __global__ __launch_bounds__(kZT) void k_zstd_block(const uint8_t* __restrict__ 
         if (mine) atomicAdd(&L.state[5], mine);
         __syncthreads();
         if (zstd::lz_worth(L.state[5], n)) {
-            if (tid == 0) {
-                const uint32_t z = zstd::lz_content(in, n, L.cand, sc, L.hist[1], L.code, L.work);
-                // z < n keeps the copy inside this block's slot (the body may reach 2n + 64
-                // when no entropy-only content was possible), as block_content_seq does
-                L.state[6] = (z && z < L.state[3] && z < n) ? z : 0u;
-            }
+            const uint32_t zc = z_lz_content(L, in, n, sc);
+            // zc < n keeps the copy inside this block's slot (the body may reach 2n + 64
+            // when no entropy-only content was possible), as block_content_seq does
+            if (tid == 0) L.state[6] = (zc && zc < L.state[3] && zc < n) ? zc : 0u;
             __syncthreads();
             const uint32_t z = L.state[6];
             for (uint32_t i = tid; i < z; i += kZT) slot[i] = sc.body[i];

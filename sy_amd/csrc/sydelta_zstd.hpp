@@ -632,29 +632,46 @@ __host__ __device__ __forceinline__ void hash_put(const uint8_t* in, uint32_t n,
     if (p + 1 > e) e = p + 1;
 }
 
-// Greedy parse of a block from the per-position bests: a match wherever one starts
-// (extended past kProbe bytes as far as it goes), a literal otherwise.  Literal bytes
-// are gathered into lit.  Returns the number of sequences; *nlit = literals (including
-// the last ones, after the last sequence); *covered = matched bytes.
+// Greedy parse of a block from the per-position bests.  Its path is a function of the
+// position alone (so the device resolves it in parallel, k_zstd_block): at p a match when
+// parse_take (a best starts there and the next position's is not longer: a one-position
+// lazy parse) of match_len bytes (the best, extended past kProbe at its own distance),
+// else one literal.  The distance a sequence codes depends on the repeat history: the
+// repeat distance rep[0] when it matches as far (matches of <= kProbe bytes; seq_dist).
+__host__ __device__ __forceinline__ bool parse_take(const uint32_t* best, uint32_t n, uint32_t p) {
+    const uint32_t b = best[p];
+    return b && !(p + 1 < n && (best[p + 1] >> 24) > (b >> 24));
+}
+__host__ __device__ __forceinline__ uint32_t match_len(const uint8_t* in, uint32_t n, uint32_t p, uint32_t b) {
+    uint32_t l = b >> 24;
+    const uint32_t d = b & 0xFFFFFFu;
+    if (l == kProbe)
+        while (p + l < n && in[p + l] == in[p + l - d]) ++l;
+    return l;
+}
+__host__ __device__ __forceinline__ uint32_t seq_dist(const uint8_t* in, uint32_t p, uint32_t l, uint32_t d0,
+                                                      const uint32_t* rep) {
+    if (rep[0] && rep[0] != d0 && rep[0] <= p) {  // an equally long match at the repeat distance is cheaper
+        uint32_t lr = 0;
+        while (lr < l && in[p + lr] == in[p + lr - rep[0]]) ++lr;
+        if (lr >= l) return rep[0];
+    }
+    return d0;
+}
+
+// The parse, sequentially: literal bytes gathered into lit.  Returns the number of
+// sequences; *nlit = literals (including the last ones, after the last sequence);
+// *covered = matched bytes.
 __host__ __device__ inline uint32_t greedy_parse(const uint8_t* in, uint32_t n, const uint32_t* best,
                                                  const uint32_t* cand, Seq* sq, uint8_t* lit, uint32_t* nlit,
                                                  uint32_t* covered) {
     uint32_t p = 0, ls = 0, ns = 0, nl = 0, cov = 0;
     uint32_t rep[3] = {0, 0, 0};
     while (p < n) {
+        if (!parse_take(best, n, p)) { lit[nl++] = in[p++]; continue; }
         const uint32_t b = best[p];
-        if (!b) { lit[nl++] = in[p++]; continue; }
-        if (p + 1 < n && (best[p + 1] >> 24) > (b >> 24)) { lit[nl++] = in[p++]; continue; }  // lazy: a longer match next
-        uint32_t d = b & 0xFFFFFFu;
-        uint32_t l = b >> 24;
-        if (rep[0] && rep[0] != d && rep[0] <= p) {  // an equally long match at the repeat distance is cheaper
-            const uint32_t lim = (n - p) < kProbe ? (n - p) : kProbe;
-            uint32_t lr = 0;
-            while (lr < lim && in[p + lr] == in[p + lr - rep[0]]) ++lr;
-            if (lr >= l) d = rep[0];
-        }
-        if (l == kProbe)
-            while (p + l < n && in[p + l] == in[p + l - d]) ++l;
+        const uint32_t l = match_len(in, n, p, b);
+        const uint32_t d = seq_dist(in, p, l, b & 0xFFFFFFu, rep);
         sq[ns] = Seq{p - ls, l, d, 0};
         sq[ns].ov = rep_code(rep, p - ls, d);
         ++ns;

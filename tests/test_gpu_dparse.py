@@ -21,7 +21,7 @@ import pytest
 
 from sy_amd import wire
 
-pytestmark = [pytest.mark.gpu, pytest.mark.late]
+pytestmark = [pytest.mark.gpu, pytest.mark.late, pytest.mark.firstrun]
 
 
 def _compact(ops, ss, bs) -> bytes:

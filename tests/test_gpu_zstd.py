@@ -15,7 +15,7 @@ import pytest
 
 import test_zstd as Z
 
-pytestmark = [pytest.mark.gpu, pytest.mark.late]
+pytestmark = [pytest.mark.gpu, pytest.mark.late, pytest.mark.firstrun]
 
 
 def _device(data: bytes):
