@@ -260,6 +260,7 @@ hipError_t launch_dparse(const dparse::DArgs& a, const uint64_t* d_orank, const 
 // sequences scratch (zstd::seq_scratch_at).  Then launch_zstd_frame writes them behind their block
 // headers at d_out + base + d_off[i] (d_off: exclusive prefix of d_len64), and the frame
 // header when b0 == 0.
+hipError_t zstd_phase_ticks(unsigned long long* out);  // SYDELTA_PHASE_TIMING (k_zstd_block)
 hipError_t launch_zstd_blocks(const uint8_t* d_text, uint64_t len, uint64_t b0, uint32_t nb, uint8_t* d_slots,
                               uint8_t* d_lz, uint32_t* d_size, uint32_t* d_type, uint64_t* d_len64,
                               hipStream_t s, Profiler* prof);

@@ -3112,11 +3112,24 @@ __device__ uint32_t z_lz_content(ZLds& L, const uint8_t* __restrict__ in, uint32
     return L.pstate[2];
 }
 
+// SYDELTA_PHASE_TIMING: k_zstd_block's thread 0 adds its phases' wall-clock ticks (100 MHz)
+// here: histogram + code, entropy-only streams, candidate distances, candidate matches,
+// hash rounds, literals + sequences content, the rest.
+__device__ unsigned long long g_zstd_phase[8];
+
 __global__ __launch_bounds__(kZT) void k_zstd_block(const uint8_t* __restrict__ text, uint64_t len, uint64_t b0,
                                                     uint8_t* __restrict__ slots, uint8_t* __restrict__ lz, uint64_t nlz,
                                                     uint32_t* __restrict__ size_out, uint32_t* __restrict__ type_out,
-                                                    uint64_t* __restrict__ len64) {
+                                                    uint64_t* __restrict__ len64, uint32_t timing) {
     __shared__ ZLds L;
+    uint64_t tph = timing ? wall_clock64() : 0;
+    auto phase = [&](int k) {
+        if (timing && threadIdx.x == 0) {
+            const uint64_t t = wall_clock64();
+            atomicAdd(&g_zstd_phase[k], (unsigned long long)(t - tph));
+            tph = t;
+        }
+    };
     const uint32_t tid = threadIdx.x, wid = tid >> 6;
     const uint64_t gb = b0 + blockIdx.x;
     const uint8_t* in = text + gb * zstd::kBlockMax;
@@ -3142,6 +3155,7 @@ __global__ __launch_bounds__(kZT) void k_zstd_block(const uint8_t* __restrict__ 
     __syncthreads();
     for (uint32_t s = tid; s < 256; s += kZT) L.hist[0][s] += L.hist[1][s] + L.hist[2][s] + L.hist[3][s];
     __syncthreads();
+    phase(0);
     const bool four = n > zstd::kSingleStreamMax;
     const uint32_t hs = four ? 5u : 3u;  // literals header
     if (tid == 0) {
@@ -3198,6 +3212,8 @@ __global__ __launch_bounds__(kZT) void k_zstd_block(const uint8_t* __restrict__ 
             L.state[3] = end + 1;
         }
     }
+    __syncthreads();
+    phase(1);
     // literals + sequences
     if (!rle && n >= 2) {
         for (uint32_t p = tid; p < n; p += kZT)
@@ -3217,7 +3233,10 @@ __global__ __launch_bounds__(kZT) void k_zstd_block(const uint8_t* __restrict__ 
         }
         __syncthreads();
         const uint32_t nc = L.state[4];
+        phase(2);
         for (uint32_t p = tid; p < n; p += kZT) sc.best[p] = zstd::best_at(in, n, p, L.cand, nc);
+        __syncthreads();
+        phase(3);
         // hash candidates in rounds of kHashRound positions (zstd::hash_look), the table in
         // the stream words (free after the entropy-only streams); position p stays with
         // thread p % kZT, so its best is read back by the thread that wrote it
@@ -3237,17 +3256,20 @@ __global__ __launch_bounds__(kZT) void k_zstd_block(const uint8_t* __restrict__ 
         for (uint32_t p = tid; p < n; p += kZT) mine += sc.best[p] != 0;
         if (mine) atomicAdd(&L.state[5], mine);
         __syncthreads();
+        phase(4);
         if (zstd::lz_worth(L.state[5], n)) {
             const uint32_t zc = z_lz_content(L, in, n, sc);
             // zc < n keeps the copy inside this block's slot (the body may reach 2n + 64
             // when no entropy-only content was possible), as block_content_seq does
             if (tid == 0) L.state[6] = (zc && zc < L.state[3] && zc < n) ? zc : 0u;
             __syncthreads();
+            phase(5);
             const uint32_t z = L.state[6];
             for (uint32_t i = tid; i < z; i += kZT) slot[i] = sc.body[i];
             if (tid == 0 && z) L.state[3] = z;
         }
     }
+    phase(6);
     if (tid == 0) {
         uint32_t t = rle ? 1u : 0u, size = rle ? 1u : n;
         if (!rle && L.state[3] < n) {
@@ -4413,10 +4435,18 @@ hipError_t launch_zstd_blocks(const uint8_t* d_text, uint64_t len, uint64_t b0, 
                               hipStream_t s, Profiler* prof) {
     if (!nb) return hipSuccess;
     if (b0 * zstd::kBlockMax >= len) return hipErrorInvalidValue;
+    static const bool timing = getenv("SYDELTA_PHASE_TIMING") != nullptr;
     ProfScope ps(prof, s, "k_zstd_block");
     hipLaunchKernelGGL(k_zstd_block, dim3(nb), dim3(kZT), 0, s, d_text, len, b0, d_slots, d_lz, (uint64_t)nb, d_size,
-                       d_type, d_len64);
+                       d_type, d_len64, timing ? 1u : 0u);
     return hipGetLastError();
+}
+
+// SYDELTA_PHASE_TIMING: k_zstd_block's phase ticks so far (8 entries, 100 MHz), then zeroed.
+hipError_t zstd_phase_ticks(unsigned long long* out) {
+    if (hipError_t e = hipMemcpyFromSymbol(out, HIP_SYMBOL(g_zstd_phase), sizeof(unsigned long long) * 8)) return e;
+    unsigned long long z[8] = {0};
+    return hipMemcpyToSymbol(HIP_SYMBOL(g_zstd_phase), z, sizeof z);
 }
 
 hipError_t launch_zstd_frame(const uint8_t* d_text, uint64_t len, uint64_t b0, uint32_t nb, uint64_t nblocks,

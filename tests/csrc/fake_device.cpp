@@ -570,6 +570,11 @@ hipError_t launch_chain(const chain::ChainArgs& a, hipStream_t, Profiler*) {
 }
 
 // zstd blocks: the sequential form of k_zstd_block (sydelta_zstd.hpp block_content_seq)
+hipError_t zstd_phase_ticks(unsigned long long* out) {
+    for (int i = 0; i < 8; ++i) out[i] = 0;
+    return hipSuccess;
+}
+
 hipError_t launch_zstd_blocks(const uint8_t* d_text, uint64_t len, uint64_t b0, uint32_t nb, uint8_t* d_slots,
                               uint8_t* d_lz, uint32_t* d_size, uint32_t* d_type, uint64_t* d_len64,
                               hipStream_t, Profiler*) {
