@@ -100,12 +100,13 @@ __host__ __device__ __forceinline__ bool op_follow(const DArgs& a, const T& t, u
 
 // Chunk c's ops and literal bytes.  orank/lrank: exclusive scans (lrank with the total
 // at nc), pos: op starts by rank (nops entries).  Writes ops[rank] (kind, a = literal
-// offset or basis offset, b = size) and lit[rank] (lit NULL: checked only).  Returns the
-// first bad position in the chunk or kNoBad.
-template <class T>
+// offset or basis offset, b = size) and lit[rank] (lit NULL: checked only; L: a byte
+// pointer, or a type with operator bool and operator[](uint64_t) -> uint8_t&, the kernel's
+// LDS staging).  Returns the first bad position in the chunk or kNoBad.
+template <class T, class L = uint8_t*>
 __host__ __device__ inline uint64_t chunk_parse(const DArgs& a, const T& t, uint64_t c, const uint64_t* orank,
                                                const uint64_t* lrank, const uint64_t* pos, uint64_t nops,
-                                               sydelta_op* ops, uint8_t* lit) {
+                                               sydelta_op* ops, L lit) {
     const uint64_t len = a.e;  // no token of R reads past its ']'
     uint64_t ork = orank[c], lrk = lrank[c];
     // The chain starts at the first op: a non-empty region must open with one, or the
@@ -161,7 +162,7 @@ __host__ __device__ inline uint64_t chunk_parse(const DArgs& a, const T& t, uint
 __host__ __device__ inline uint64_t chunk_parse(const DArgs& a, uint64_t c, const uint64_t* orank,
                                                const uint64_t* lrank, const uint64_t* pos, uint64_t nops,
                                                sydelta_op* ops, uint8_t* lit) {
-    return chunk_parse(a, a.t, c, orank, lrank, pos, nops, ops, lit);
+    return chunk_parse<const uint8_t*, uint8_t*>(a, a.t, c, orank, lrank, pos, nops, ops, lit);
 }
 
 }  // namespace dparse

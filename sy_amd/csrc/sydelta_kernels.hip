@@ -495,17 +495,38 @@ __global__ __launch_bounds__(64) void k_ribbon_build(const uint32_t* __restrict_
 }
 
 // The ribbon's key lists: every distinct key of the (single-file) exact table in its
-// shard's list (q >> 22), past kRibCap in the overflow list.
-__global__ void k_ribbon_list(const uint32_t* __restrict__ keys, uint64_t nslots, uint32_t* __restrict__ rib_keys,
-                              uint32_t* __restrict__ rib_cnt, uint32_t* __restrict__ rib_over) {
-    const uint64_t j = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (j >= nslots) return;
-    const uint32_t w = keys[j];
-    if (w == kEmptyKey) return;
-    const uint32_t sh = probe_hash(w).q >> 22;
-    const uint32_t rank = atomicAdd(&rib_cnt[sh], 1u);
-    if (rank < kRibCap) rib_keys[(size_t)sh * kRibCap + rank] = w;
-    else rib_over[atomicAdd(&rib_cnt[kRibShards], 1u)] = w;  // at most nblocks distinct keys
+// shard's list (q >> 22), past kRibCap in the overflow list.  Each workgroup takes `per`
+// slots: it counts its keys per shard in LDS, reserves each shard's range with one
+// global atomic, then places its keys (one global atomic per key on 1024 counters took
+// 0.25 ms at 1 Mi keys).
+constexpr uint32_t kRibListT = 256;
+__global__ __launch_bounds__(kRibListT) void k_ribbon_list(const uint32_t* __restrict__ keys, uint64_t nslots,
+                                                           uint64_t per, uint32_t* __restrict__ rib_keys,
+                                                           uint32_t* __restrict__ rib_cnt,
+                                                           uint32_t* __restrict__ rib_over) {
+    __shared__ uint32_t cnt[kRibShards], base[kRibShards];
+    const uint32_t tid = threadIdx.x;
+    const uint64_t j0 = (uint64_t)blockIdx.x * per, j1 = min(nslots, j0 + per);
+    for (uint32_t i = tid; i < kRibShards; i += kRibListT) cnt[i] = 0;
+    __syncthreads();
+    for (uint64_t j = j0 + tid; j < j1; j += kRibListT) {
+        const uint32_t w = keys[j];
+        if (w != kEmptyKey) atomicAdd(&cnt[probe_hash(w).q >> 22], 1u);
+    }
+    __syncthreads();
+    for (uint32_t i = tid; i < kRibShards; i += kRibListT) {
+        base[i] = cnt[i] ? atomicAdd(&rib_cnt[i], cnt[i]) : 0u;
+        cnt[i] = 0;
+    }
+    __syncthreads();
+    for (uint64_t j = j0 + tid; j < j1; j += kRibListT) {
+        const uint32_t w = keys[j];
+        if (w == kEmptyKey) continue;
+        const uint32_t sh = probe_hash(w).q >> 22;
+        const uint32_t rank = base[sh] + atomicAdd(&cnt[sh], 1u);
+        if (rank < kRibCap) rib_keys[(size_t)sh * kRibCap + rank] = w;
+        else rib_over[atomicAdd(&rib_cnt[kRibShards], 1u)] = w;  // at most nblocks distinct keys
+    }
 }
 
 // Candidates grouped by slot in index order: order = block indices stably sorted
@@ -3482,18 +3503,64 @@ __global__ __launch_bounds__(256) void k_dparse_place(dparse::DArgs a, const uin
     if (c < a.nc) dparse::chunk_place(a, t, c, orank[c], pos);
 }
 
+// The literal bytes of a wave's chunks are one contiguous range of the output, [lrank[c0],
+// lrank[c0 + 64]) (a 64-byte chunk starts at most 32 literals): the lanes write them into
+// the wave's LDS staging (LdsLit) and the wave stores the range with whole dwords, the
+// partial dwords at its two ends byte by byte (they may be shared with the neighbouring
+// waves' ranges).  Byte stores from 64 lanes 18 bytes apart made the round-3 kernel's
+// literal output the bulk of its time.
+constexpr uint32_t kDpLitMax = 64 * (dparse::kChunk / 2);
+struct LdsLit {
+    __attribute__((address_space(3))) uint8_t* l;
+    uint64_t base;  // output index of l[0]
+    __device__ __forceinline__ explicit operator bool() const { return true; }
+    __device__ __forceinline__ __attribute__((address_space(3))) uint8_t& operator[](uint64_t i) const {
+        return l[i - base];
+    }
+};
+
 __global__ __launch_bounds__(256) void k_dparse(dparse::DArgs a, const uint64_t* __restrict__ orank,
                                                 const uint64_t* __restrict__ lrank, const uint64_t* __restrict__ pos,
                                                 uint64_t nops, sydelta_op* __restrict__ ops, uint8_t* lit,
                                                 unsigned long long* bad) {
     __shared__ uint8_t st[4][kDpRows * kDpRow];
+    __shared__ uint8_t lo[4][kDpLitMax];
+    const uint32_t wid = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const uint64_t c0 = ((uint64_t)blockIdx.x * 256 + threadIdx.x) & ~63ull;
     if (c0 >= a.nc) return;
-    const LdsText t = dp_stage(a, c0, st[threadIdx.x >> 6]);
-    const uint64_t c = c0 + (threadIdx.x & 63);
-    if (c >= a.nc) return;
-    const uint64_t b = dparse::chunk_parse(a, t, c, orank, lrank, pos, nops, ops, lit);
-    if (b != dparse::kNoBad) atomicMin(bad, (unsigned long long)b);
+    const LdsText t = dp_stage(a, c0, st[wid]);
+    const uint64_t c = c0 + lane;
+    const uint64_t l0 = lrank[c0], l1 = lrank[c0 + 64 < a.nc ? c0 + 64 : a.nc];
+    if (c < a.nc) {
+        uint64_t b;
+        if (lit && l1 - l0 <= kDpLitMax)
+            b = dparse::chunk_parse(a, t, c, orank, lrank, pos, nops, ops,
+                                    LdsLit{(__attribute__((address_space(3))) uint8_t*)lo[wid], l0});
+        else
+            b = dparse::chunk_parse(a, t, c, orank, lrank, pos, nops, ops, lit);
+        if (b != dparse::kNoBad) atomicMin(bad, (unsigned long long)b);
+    }
+    if (!lit || l1 - l0 > kDpLitMax || l1 == l0) return;  // wave-uniform
+    lds_fence();
+    // [l0, l1): head bytes up to a dword boundary (of the absolute address), whole dwords,
+    // tail bytes
+    const uint8_t* src = lo[wid];
+    const int64_t ph = (int64_t)((uintptr_t)lit & 3);
+    const uint64_t a0 = (uint64_t)((((int64_t)l0 + ph + 3) & ~3ll) - ph);
+    const int64_t a1s = (((int64_t)l1 + ph) & ~3ll) - ph;
+    const uint64_t a1 = a1s < (int64_t)a0 ? a0 : (uint64_t)a1s;
+    if (a0 >= a1) {
+        for (uint64_t i = l0 + lane; i < l1; i += 64) lit[i] = src[i - l0];
+        return;
+    }
+    if (lane < a0 - l0) lit[l0 + lane] = src[lane];
+    if (lane < l1 - a1) lit[a1 + lane] = src[a1 - l0 + lane];
+    for (uint64_t i = a0 + 4ull * lane; i < a1; i += 256) {
+        const uint64_t k = i - l0;
+        const uint32_t v = (uint32_t)src[k] | ((uint32_t)src[k + 1] << 8) | ((uint32_t)src[k + 2] << 16) |
+                           ((uint32_t)src[k + 3] << 24);
+        *(uint32_t*)(lit + i) = v;
+    }
 }
 
 __global__ __launch_bounds__(256) void k_json_len(const JsonPiece* __restrict__ pieces, uint64_t npieces,
@@ -4057,8 +4124,9 @@ hipError_t launch_ribbon_build(const DeviceIndex& ix, hipStream_t s, Profiler* p
     if ((e = hipMemsetAsync(ix.rib_cnt, 0, 4 * (kRibShards + 1), s))) return e;
     if ((e = hipMemsetAsync(ix.rib_l1, 0, 4 * (size_t)kL1WordsR, s))) return e;
     ProfScope ps(prof, s, "k_ribbon_build");  // listing + solving
-    hipLaunchKernelGGL(k_ribbon_list, dim3(grid_for(ix.nslots, 256)), dim3(256), 0, s, ix.keys, (uint64_t)ix.nslots,
-                       ix.rib_keys, ix.rib_cnt, ix.rib_over);
+    const uint64_t per = std::max<uint64_t>(4096, ((uint64_t)ix.nslots + 127) / 128);  // 128 workgroups
+    hipLaunchKernelGGL(k_ribbon_list, dim3((uint32_t)((ix.nslots + per - 1) / per)), dim3(kRibListT), 0, s, ix.keys,
+                       (uint64_t)ix.nslots, per, ix.rib_keys, ix.rib_cnt, ix.rib_over);
     if ((e = hipGetLastError())) return e;
     hipLaunchKernelGGL(k_ribbon_build, dim3(kRibShards), dim3(64), 0, s, ix.rib_keys, ix.rib_cnt, ix.rib_over,
                        ix.rib_l1);
