@@ -651,13 +651,15 @@ def main():
         ins = np.sort(rng.choice(nblk4, nblk4 // 100, replace=False)) * 4096 + rng.integers(0, 4096, nblk4 // 100)
         extra = torch.from_numpy(rng.integers(0, 256, ins.size, dtype=np.uint8)).cuda()
         cuts = np.concatenate([[0], ins, [n]])
-        parts = []
+        # piece i of the edited basis lands i bytes later (the insertions before it); one
+        # copy per piece and one scatter of the inserted bytes (torch.cat of the 21 K pieces
+        # crashed under rocprofv3's counter collection)
+        new = torch.empty(n + ins.size, dtype=torch.uint8, device="cuda")
         for i in range(ins.size + 1):
-            parts.append(ed[int(cuts[i]):int(cuts[i + 1])])
-            if i < ins.size:
-                parts.append(extra[i:i + 1])
-        new = torch.cat(parts)
-        del ed, parts
+            a0, a1 = int(cuts[i]), int(cuts[i + 1])
+            new[a0 + i:a1 + i].copy_(ed[a0:a1])
+        new[torch.from_numpy(ins + np.arange(ins.size)).cuda()] = extra
+        del ed
     c5 = None
     apply_d = None
     json_d = None

@@ -136,11 +136,12 @@ __host__ __device__ inline uint64_t chunk_parse(const DArgs& a, const T& t, uint
                 } else if (!(q < len && is_digit(t[q]))) {
                     return p;  // the first literal (checked by its own thread) must start here
                 }
-                const uint64_t l0 = lits_before(a, t, lrank, q);
+                // the recounts reach other chunks' text (the next op may be anywhere): a.t
+                const uint64_t l0 = lits_before(a, a.t, lrank, q);
                 const uint64_t next = ork + 1 < nops ? pos[ork + 1] : a.e;
                 op.kind = SYDELTA_OP_DATA;
                 op.a = l0;
-                op.b = lits_before(a, t, lrank, next) - l0;
+                op.b = lits_before(a, a.t, lrank, next) - l0;
             }
             ops[ork++] = op;
         } else if (lit_start(t, p)) {

@@ -2837,6 +2837,20 @@ __global__ void k_chain_finish(chain::ChainArgs a) {
 // smaller content stays in the slot.  k_zstd_frame
 // then lays the blocks out behind their headers.
 constexpr int kZT = 256;
+
+// SYDELTA_PHASE_TIMING: k_zstd_block's thread 0 adds its phases' wall-clock ticks (100 MHz)
+// here: histogram + code, entropy-only streams, candidate distances, candidate matches,
+// hash rounds, literals + sequences content, the rest; inside the content: the segment
+// walks, the chaining, the gather, the repeat history, the literals section, the
+// sequences section.
+__device__ unsigned long long g_zstd_phase[16];
+__device__ __forceinline__ void z_phase(uint32_t timing, uint64_t& tph, int k) {
+    if (timing && threadIdx.x == 0) {
+        const uint64_t t = wall_clock64();
+        atomicAdd(&g_zstd_phase[k], (unsigned long long)(t - tph));
+        tph = t;
+    }
+}
 constexpr uint32_t kZRun = 144;  // bytes of a stream per thread: 256 runs cover 32 KiB + the 16-byte phase
 static_assert(kZRun * kZT >= zstd::kBlockMax / 4 + 16, "one run per thread covers a stream");
 constexpr uint32_t kZStreamWords = (zstd::kStreamBytesMax + 3) / 4 + 2;
@@ -2854,7 +2868,10 @@ struct ZLds {
     uint32_t state[8];  // [0] type, [1] write offset, [2] abort, [3] entropy-only size, [4] nc, [5] nbest, [6] lz size
     uint32_t rank[2][kZT];  // the parallel parse: per thread literals / sequences, then their exclusive scans
     uint32_t pstate[8];     // [0] literals, [1] sequences, [2] literals section size, [3] raw, [4] write offset
+    uint32_t ccnt[36 + 53 + 32];  // the sequences' LL / ML / OF code counts
+    zstd::FseCT fse[3];           // their FSE tables (the coder's state lookups stay in LDS)
 };
+static_assert(sizeof(ZLds) <= 64 * 1024, "k_zstd_block's static LDS");
 
 // Bits of symbols src[first, first + count) coded with L.code, written as one literal
 // stream (last symbol first, LSB-first) into L.words with its closing 1 bit by a
@@ -3018,7 +3035,8 @@ __device__ uint32_t z_scan(uint32_t* v, uint32_t* tot) {
 // (zstd::seq_dist compared by the whole wave, rep_code), thread 0 codes them
 // (seq_section) after the literals section (z_lit_section).  Returns its size, 0 when
 // the block has no sequence (every thread).
-__device__ uint32_t z_lz_content(ZLds& L, const uint8_t* __restrict__ in, uint32_t n, const zstd::SeqScratch& sc) {
+__device__ uint32_t z_lz_content(ZLds& L, const uint8_t* __restrict__ in, uint32_t n, const zstd::SeqScratch& sc,
+                                 uint32_t timing, uint64_t& tph) {
     const uint32_t tid = threadIdx.x, lane = tid & 63;
     constexpr uint32_t kSeg = zstd::kBlockMax / kZT;  // 512 positions per thread
     static_assert(kSeg % 32 == 0 && zstd::kBlockMax / 32 <= kZStreamWords, "the path bitmap fits the stream words");
@@ -3046,6 +3064,7 @@ __device__ uint32_t z_lz_content(ZLds& L, const uint8_t* __restrict__ in, uint32
     }
     L.part[tid] = s0 < n ? p : s0;  // the segment's exit
     __syncthreads();
+    z_phase(timing, tph, 7);
     if (tid == 0) {
         auto bit = [&](uint32_t x) { return (bm[x >> 5] >> (x & 31)) & 1u; };
         auto clear = [&](uint32_t a, uint32_t b) {  // marks in [a, b)
@@ -3073,6 +3092,7 @@ __device__ uint32_t z_lz_content(ZLds& L, const uint8_t* __restrict__ in, uint32
         }
     }
     __syncthreads();
+    z_phase(timing, tph, 8);
     // count this segment's literals and sequence starts
     uint32_t nlit = 0, nseq = 0;
     for (uint32_t w = s0 >> 5; 32 * w < s1; ++w) {
@@ -3107,6 +3127,7 @@ __device__ uint32_t z_lz_content(ZLds& L, const uint8_t* __restrict__ in, uint32
     }
     __threadfence_block();
     __syncthreads();
+    z_phase(timing, tph, 9);
     // the repeat history, in order (wave 0; uniform loop)
     if (tid < 64) {
         uint32_t rep[3] = {0, 0, 0}, end = 0;
@@ -3127,16 +3148,27 @@ __device__ uint32_t z_lz_content(ZLds& L, const uint8_t* __restrict__ in, uint32
     }
     __threadfence_block();
     __syncthreads();
-    const uint32_t z = z_lit_section(L, sc.lit, nl, sc.body);
-    if (tid == 0) L.pstate[2] = z + zstd::seq_section(sc.seq, ns, sc.body + z, sc.fse[0], sc.fse[1], sc.fse[2]);
+    z_phase(timing, tph, 10);
+    // code counts in parallel (LDS atomics)
+    for (uint32_t i = tid; i < 36 + 53 + 32; i += kZT) L.ccnt[i] = 0;
     __syncthreads();
+    for (uint32_t k = tid; k < ns; k += kZT) {
+        uint32_t lc, lb, mc, mb, oc, ov;
+        zstd::seq_codes(sc.seq[k], lc, lb, mc, mb, oc, ov);
+        atomicAdd(&L.ccnt[lc], 1u);
+        atomicAdd(&L.ccnt[36 + mc], 1u);
+        atomicAdd(&L.ccnt[36 + 53 + oc], 1u);
+    }
+    const uint32_t z = z_lit_section(L, sc.lit, nl, sc.body);  // starts with a barrier
+    z_phase(timing, tph, 11);
+    if (tid == 0)
+        L.pstate[2] = z + zstd::seq_section_counted(sc.seq, ns, sc.body + z, L.ccnt, L.ccnt + 36, L.ccnt + 36 + 53,
+                                                    L.fse[0], L.fse[1], L.fse[2]);
+    __syncthreads();
+    z_phase(timing, tph, 12);
     return L.pstate[2];
 }
 
-// SYDELTA_PHASE_TIMING: k_zstd_block's thread 0 adds its phases' wall-clock ticks (100 MHz)
-// here: histogram + code, entropy-only streams, candidate distances, candidate matches,
-// hash rounds, literals + sequences content, the rest.
-__device__ unsigned long long g_zstd_phase[8];
 
 __global__ __launch_bounds__(kZT) void k_zstd_block(const uint8_t* __restrict__ text, uint64_t len, uint64_t b0,
                                                     uint8_t* __restrict__ slots, uint8_t* __restrict__ lz, uint64_t nlz,
@@ -3144,13 +3176,7 @@ __global__ __launch_bounds__(kZT) void k_zstd_block(const uint8_t* __restrict__ 
                                                     uint64_t* __restrict__ len64, uint32_t timing) {
     __shared__ ZLds L;
     uint64_t tph = timing ? wall_clock64() : 0;
-    auto phase = [&](int k) {
-        if (timing && threadIdx.x == 0) {
-            const uint64_t t = wall_clock64();
-            atomicAdd(&g_zstd_phase[k], (unsigned long long)(t - tph));
-            tph = t;
-        }
-    };
+    auto phase = [&](int k) { z_phase(timing, tph, k); };
     const uint32_t tid = threadIdx.x, wid = tid >> 6;
     const uint64_t gb = b0 + blockIdx.x;
     const uint8_t* in = text + gb * zstd::kBlockMax;
@@ -3279,7 +3305,7 @@ __global__ __launch_bounds__(kZT) void k_zstd_block(const uint8_t* __restrict__ 
         __syncthreads();
         phase(4);
         if (zstd::lz_worth(L.state[5], n)) {
-            const uint32_t zc = z_lz_content(L, in, n, sc);
+            const uint32_t zc = z_lz_content(L, in, n, sc, timing, tph);
             // zc < n keeps the copy inside this block's slot (the body may reach 2n + 64
             // when no entropy-only content was possible), as block_content_seq does
             if (tid == 0) L.state[6] = (zc && zc < L.state[3] && zc < n) ? zc : 0u;
@@ -3447,13 +3473,18 @@ constexpr uint32_t kDpSpan = 64 * 64 + kDpBefore + 136;  // staged bytes per wav
 constexpr uint32_t kDpRows = (kDpSpan + 63) / 64;
 
 typedef __attribute__((address_space(3))) uint8_t lds_u8;  // an LDS pointer kept as one
+// The text outside the staged span (not reached by well-formed text: every token and its
+// look-ahead ends inside the 136-byte halo).  Not inlined, so that the compiler cannot
+// turn the accessor's branch into a select that issues this global load for every byte.
+__device__ __noinline__ uint8_t dp_gload(const uint8_t* g, uint64_t p) { return g[p]; }
 struct LdsText {
     const uint8_t* g;   // the text
     const lds_u8* l;    // the wave's staged rows
     uint64_t p0, n;     // staged text [p0, p0 + n)
     __device__ __forceinline__ uint8_t operator[](uint64_t p) const {
         const uint64_t d = p - p0;
-        return d < n ? l[(d >> 6) * kDpRow + (d & 63)] : g[p];
+        if (__builtin_expect(d < n, 1)) return l[(d >> 6) * kDpRow + (d & 63)];
+        return dp_gload(g, p);
     }
 };
 
@@ -4512,8 +4543,8 @@ hipError_t launch_zstd_blocks(const uint8_t* d_text, uint64_t len, uint64_t b0, 
 
 // SYDELTA_PHASE_TIMING: k_zstd_block's phase ticks so far (8 entries, 100 MHz), then zeroed.
 hipError_t zstd_phase_ticks(unsigned long long* out) {
-    if (hipError_t e = hipMemcpyFromSymbol(out, HIP_SYMBOL(g_zstd_phase), sizeof(unsigned long long) * 8)) return e;
-    unsigned long long z[8] = {0};
+    if (hipError_t e = hipMemcpyFromSymbol(out, HIP_SYMBOL(g_zstd_phase), sizeof(unsigned long long) * 16)) return e;
+    unsigned long long z[16] = {0};
     return hipMemcpyToSymbol(HIP_SYMBOL(g_zstd_phase), z, sizeof z);
 }
 

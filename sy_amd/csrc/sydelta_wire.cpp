@@ -808,11 +808,13 @@ extern "C" int sydelta_zstd_compress_device(int device, const uint8_t* d_in, uin
     }
     *out_len = pos;
     if (getenv("SYDELTA_PHASE_TIMING")) {
-        unsigned long long t[8];
+        unsigned long long t[16];
         HIP_TRY(zstd_phase_ticks(t));
         fprintf(stderr, "zstd block phases (ms of block time, summed over blocks): histogram+code %.2f, entropy "
-                "streams %.2f, candidate distances %.2f, candidate matches %.2f, hash rounds %.2f, lz content %.2f, "
-                "rest %.2f\n", t[0] / 1e5, t[1] / 1e5, t[2] / 1e5, t[3] / 1e5, t[4] / 1e5, t[5] / 1e5, t[6] / 1e5);
+                "streams %.2f, candidate distances %.2f, candidate matches %.2f, hash rounds %.2f, lz content %.2f "
+                "(walks %.2f, chain %.2f, gather %.2f, repeats %.2f, literals %.2f, sequences %.2f), rest %.2f\n",
+                t[0] / 1e5, t[1] / 1e5, t[2] / 1e5, t[3] / 1e5, t[4] / 1e5, t[5] / 1e5, t[7] / 1e5, t[8] / 1e5,
+                t[9] / 1e5, t[10] / 1e5, t[11] / 1e5, t[12] / 1e5, t[6] / 1e5);
     }
     return SYDELTA_OK;
 } catch (...) {

@@ -205,25 +205,44 @@ constexpr uint32_t kRepMin = 4;     // samples a repeat distance needs to become
 constexpr uint32_t kMaxSeq = kBlockMax / kMinMatch;
 
 // Literals_Length / Match_Length codes (RFC 8878 3.1.1.3.2.1.1): code, its extra bits.
+// Lengths past the table's irregular start follow the highest set bit (zstd's
+// ZSTD_LLcode / ZSTD_MLcode deltas 19 and 36); the tables are namespace-scope constants
+// (a per-call array initialised in private memory made each code a scratch round trip
+// on the device).
+constexpr uint32_t kLLBase[36] = {0,  1,  2,  3,  4,  5,  6,  7,  8,   9,   10,  11,   12,   13,   14,   15,    16,    18,
+                                  20, 22, 24, 28, 32, 40, 48, 64, 128, 256, 512, 1024, 2048, 4096, 8192, 16384, 32768, 65536};
+constexpr uint8_t kLLBits[36] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 1, 1,
+                                 1, 1, 2, 2, 3, 3, 4, 6, 7, 8, 9, 10, 11, 12, 13, 14, 15, 16};
+constexpr uint32_t kMLBase[21] = {35,  37,  39,  41,   43,   47,   51,   59,    67,    83,    99,
+                                  131, 259, 515, 1027, 2051, 4099, 8195, 16387, 32771, 65539};
+constexpr uint8_t kMLBits[21] = {1, 1, 1, 1, 2, 2, 3, 3, 4, 4, 5, 7, 8, 9, 10, 11, 12, 13, 14, 15, 16};
+__host__ __device__ __forceinline__ uint32_t highbit32(uint32_t v) { return 31u - (uint32_t)__builtin_clz(v); }
 __host__ __device__ __forceinline__ void ll_code(uint32_t ll, uint32_t& code, uint32_t& bits) {
-    constexpr uint32_t base[36] = {0,  1,  2,  3,  4,  5,  6,   7,   8,   9,   10,   11,   12,   13,    14,    15,    16,   18,
-                                   20, 22, 24, 28, 32, 40, 48, 64, 128, 256, 512, 1024, 2048, 4096, 8192, 16384, 32768, 65536};
-    constexpr uint8_t nb[36] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 1, 1,
-                                1, 1, 2, 2, 3, 3, 4, 6, 7, 8, 9, 10, 11, 12, 13, 14, 15, 16};
-    uint32_t c = 35;
-    while (base[c] > ll) --c;
+    if (ll < 16) { code = ll; bits = 0; return; }
+    if (ll >= 64) {  // codes 25..35: [2^h, 2^(h+1)) with h extra bits
+        const uint32_t h = highbit32(ll);
+        code = h < 16 ? h + 19 : 35u;
+        bits = kLLBits[code];
+        return;
+    }
+    uint32_t c = 24;
+    while (kLLBase[c] > ll) --c;
     code = c;
-    bits = nb[c];
+    bits = kLLBits[c];
 }
 __host__ __device__ __forceinline__ void ml_code(uint32_t ml, uint32_t& code, uint32_t& bits) {
-    constexpr uint32_t base[21] = {35,  37,  39,   41,   43,   47,   51,   59,    67,    83,   99,
-                                   131, 259, 515, 1027, 2051, 4099, 8195, 16387, 32771, 65539};
-    constexpr uint8_t nb[21] = {1, 1, 1, 1, 2, 2, 3, 3, 4, 4, 5, 7, 8, 9, 10, 11, 12, 13, 14, 15, 16};
     if (ml < 35) { code = ml - 3; bits = 0; return; }
-    uint32_t c = 20;
-    while (base[c] > ml) --c;
+    if (ml >= 131) {  // codes 43..52: ml - 3 in [2^h, 2^(h+1)) with h extra bits
+        const uint32_t h = highbit32(ml - 3);
+        const uint32_t c = h < 16 ? h + 4 : 20u;  // index into kMLBase (h = 7 -> 11)
+        code = 32 + c;
+        bits = kMLBits[c];
+        return;
+    }
+    uint32_t c = 10;
+    while (kMLBase[c] > ml) --c;
     code = 32 + c;
-    bits = nb[c];
+    bits = kMLBits[c];
 }
 
 // One FSE compression table built from a normalized distribution (zstd's
@@ -470,8 +489,7 @@ __host__ __device__ __forceinline__ void seq_codes(const Seq& q, uint32_t& lc, u
     ll_code(q.ll, lc, lb);
     ml_code(q.ml, mc, mb);
     ov = q.ov;
-    oc = 0;
-    while ((2u << oc) <= ov) ++oc;
+    oc = highbit32(ov);  // ov >= 1
 }
 
 // Sequences_Section of ns sequences into p; returns its size.  Tables per block (RLE or
@@ -479,8 +497,26 @@ __host__ __device__ __forceinline__ void seq_codes(const Seq& q, uint32_t& lc, u
 // tables up to log 9).  Order of zstd's ZSTD_encodeSequences: the last sequence starts
 // the states, then every earlier one from the end: OF, ML, LL state bits, then LL, ML, OF
 // extra bits; states flushed ML, OF, LL (the decoder reads LL, OF, ML first).
-__host__ __device__ inline uint32_t seq_section(const Seq* sq, uint32_t ns, uint8_t* p, FseCT& tll, FseCT& tml,
-                                                FseCT& tof) {
+// The code counts of ns sequences (zeroed first).  The device counts in parallel instead.
+__host__ __device__ inline void seq_counts(const Seq* sq, uint32_t ns, uint32_t* cll, uint32_t* cml, uint32_t* cof) {
+    for (uint32_t i = 0; i < 36; ++i) cll[i] = 0;
+    for (uint32_t i = 0; i < 53; ++i) cml[i] = 0;
+    for (uint32_t i = 0; i < 32; ++i) cof[i] = 0;
+    uint32_t lc, lb, mc, mb, oc, ov;
+    for (uint32_t i = 0; i < ns; ++i) {
+        seq_codes(sq[i], lc, lb, mc, mb, oc, ov);
+        ++cll[lc];
+        ++cml[mc];
+        ++cof[oc];
+    }
+}
+
+// Sequences_Section from the code counts (seq_counts).  The sequences are read last to
+// first, eight at a time (independent loads in flight: a one-thread loop over
+// sequences in HBM otherwise waits a full round trip per sequence).
+__host__ __device__ inline uint32_t seq_section_counted(const Seq* sq, uint32_t ns, uint8_t* p, const uint32_t* cll,
+                                                        const uint32_t* cml, const uint32_t* cof, FseCT& tll,
+                                                        FseCT& tml, FseCT& tof) {
     uint32_t o = 0;
     if (ns < 128) {
         p[o++] = (uint8_t)ns;
@@ -493,14 +529,7 @@ __host__ __device__ inline uint32_t seq_section(const Seq* sq, uint32_t ns, uint
         p[o++] = (uint8_t)((ns - 0x7F00) >> 8);
     }
     if (!ns) return o;
-    uint32_t cll[36] = {0}, cml[53] = {0}, cof[32] = {0};
     uint32_t lc, lb, mc, mb, oc, ov;
-    for (uint32_t i = 0; i < ns; ++i) {
-        seq_codes(sq[i], lc, lb, mc, mb, oc, ov);
-        ++cll[lc];
-        ++cml[mc];
-        ++cof[oc];
-    }
     const uint32_t modes_at = o++;
     uint32_t mll, mof, mml;
     o += seq_table(cll, 36, ns, 9, tll, &mll, p + o);
@@ -514,20 +543,38 @@ __host__ __device__ inline uint32_t seq_section(const Seq* sq, uint32_t ns, uint
     w.add(sq[ns - 1].ll, lb);
     w.add(sq[ns - 1].ml - 3, mb);
     w.add(ov, oc);
-    for (uint32_t i = ns - 1; i-- > 0;) {
-        seq_codes(sq[i], lc, lb, mc, mb, oc, ov);
-        if (tof.log) fse_encode(w, tof, sof, oc);
-        if (tml.log) fse_encode(w, tml, sml, mc);
-        if (tll.log) fse_encode(w, tll, sll, lc);
-        w.add(sq[i].ll, lb);
-        w.add(sq[i].ml - 3, mb);
-        w.add(ov, oc);
+    constexpr uint32_t kAhead = 8;
+    for (uint32_t hi = ns - 1; hi > 0;) {  // sequences [lo, hi), last first
+        const uint32_t lo = hi > kAhead ? hi - kAhead : 0;
+        Seq q[kAhead];
+#pragma unroll
+        for (uint32_t k = 0; k < kAhead; ++k)
+            if (lo + k < hi) q[k] = sq[lo + k];
+#pragma unroll
+        for (uint32_t k = kAhead; k-- > 0;) {
+            if (lo + k >= hi) continue;
+            seq_codes(q[k], lc, lb, mc, mb, oc, ov);
+            if (tof.log) fse_encode(w, tof, sof, oc);
+            if (tml.log) fse_encode(w, tml, sml, mc);
+            if (tll.log) fse_encode(w, tll, sll, lc);
+            w.add(q[k].ll, lb);
+            w.add(q[k].ml - 3, mb);
+            w.add(ov, oc);
+        }
+        hi = lo;
     }
     w.add(sml, tml.log);
     w.add(sof, tof.log);
     w.add(sll, tll.log);
     w.close();
     return o + w.bytes;
+}
+
+__host__ __device__ inline uint32_t seq_section(const Seq* sq, uint32_t ns, uint8_t* p, FseCT& tll, FseCT& tml,
+                                                FseCT& tof) {
+    uint32_t cll[36], cml[53], cof[32];
+    seq_counts(sq, ns, cll, cml, cof);
+    return seq_section_counted(sq, ns, p, cll, cml, cof, tll, tml, tof);
 }
 
 // Raw_Literals_Block header (1, 2 or 3 bytes by size); returns its size.

@@ -571,7 +571,7 @@ hipError_t launch_chain(const chain::ChainArgs& a, hipStream_t, Profiler*) {
 
 // zstd blocks: the sequential form of k_zstd_block (sydelta_zstd.hpp block_content_seq)
 hipError_t zstd_phase_ticks(unsigned long long* out) {
-    for (int i = 0; i < 8; ++i) out[i] = 0;
+    for (int i = 0; i < 16; ++i) out[i] = 0;
     return hipSuccess;
 }
 
