@@ -3488,6 +3488,70 @@ struct LdsText {
     }
 };
 
+// The fast path of the three kernels: a chunk of 64 digits and commas (inside a Data
+// op's literal run: almost all of a literal-heavy delta's text) is classified with SWAR
+// masks from 18 dwords of the staged rows instead of byte by byte.  DpFast.ok: the chunk
+// is such a chunk, every literal starting in it is 1-3 digits without a leading zero,
+// <= 255, followed by ',' and a digit (all checked here, with 8 bytes of look-ahead), so
+// chunk_count / chunk_parse would find exactly these literals and nothing else; any other
+// chunk (ops, the end of a run, a bad byte) takes the bodies.
+struct DpFast {
+    bool ok;
+    uint64_t lits;  // bit i: a literal starts at byte i of the chunk
+    uint32_t x[18]; // the chunk's 64 bytes and 8 bytes of look-ahead
+};
+__device__ __forceinline__ uint32_t dp_bits4(uint32_t m) {  // bit 7 of each byte -> bits 0..3
+    return ((m >> 7) & 1u) | ((m >> 14) & 2u) | ((m >> 21) & 4u) | ((m >> 28) & 8u);
+}
+__device__ __forceinline__ uint32_t dp_digits4(uint32_t x) {
+    const uint32_t t = x ^ 0x30303030u;
+    return dp_bits4(~(((t & 0x7F7F7F7Fu) + 0x76767676u) | t) & 0x80808080u);
+}
+__device__ __forceinline__ uint32_t dp_eq4(uint32_t x, uint32_t pat) {
+    const uint32_t y = x ^ pat;
+    return dp_bits4(~(((y & 0x7F7F7F7Fu) + 0x7F7F7F7Fu) | y) & 0x80808080u);
+}
+__device__ __forceinline__ void dp_fast(const dparse::DArgs& a, const LdsText& t, uint64_t c, DpFast& f) {
+    f.ok = false;
+    f.lits = 0;
+    const uint64_t lo = dparse::chunk_lo(a, c);
+    if (c == 0 || lo + 72 > a.e) return;  // the first chunk, the tail: the bodies
+    const uint32_t d0 = (uint32_t)(lo - t.p0);  // 8 + 64 * lane: dword-aligned, inside one row each
+    if (d0 + 72 > t.n) return;
+    typedef __attribute__((address_space(3))) const uint32_t lds_u32;
+#pragma unroll
+    for (int k = 0; k < 18; ++k) {
+        const uint32_t dd = d0 + 4 * k;
+        f.x[k] = *(lds_u32*)(t.l + (dd >> 6) * kDpRow + (dd & 63));
+    }
+    const uint32_t dp = d0 - 4;
+    const uint32_t prevw = *(lds_u32*)(t.l + (dp >> 6) * kDpRow + (dp & 63));
+    uint64_t D = 0, C = 0;
+#pragma unroll
+    for (int k = 0; k < 16; ++k) {
+        D |= (uint64_t)dp_digits4(f.x[k]) << (4 * k);
+        C |= (uint64_t)dp_eq4(f.x[k], 0x2C2C2C2Cu) << (4 * k);
+    }
+    if ((D | C) != ~0ull) return;
+    const uint32_t DL = dp_digits4(f.x[16]) | (dp_digits4(f.x[17]) << 4);  // look-ahead bytes 64..71
+    const uint32_t CL = dp_eq4(f.x[16], 0x2C2C2C2Cu) | (dp_eq4(f.x[17], 0x2C2C2C2Cu) << 4);
+    const uint32_t pb = prevw >> 24;
+    const uint64_t L = D & ((C << 1) | (uint64_t)(pb == ',' || pb == '['));
+    // digits / commas at i+1, i+2, i+3 (with the look-ahead)
+    const uint64_t D1 = (D >> 1) | ((uint64_t)DL << 63), D2 = (D >> 2) | ((uint64_t)DL << 62),
+                   D3 = (D >> 3) | ((uint64_t)DL << 61), D4 = (D >> 4) | ((uint64_t)DL << 60);
+    const uint64_t C1 = (C >> 1) | ((uint64_t)CL << 63), C2 = (C >> 2) | ((uint64_t)CL << 62),
+                   C3 = (C >> 3) | ((uint64_t)CL << 61);
+    // 1 digit: ',' then a digit; 2: digit, ',', digit; 3: digit, digit, ',', digit; 4+: bad
+    const uint64_t len1 = ~D1, len2 = D1 & ~D2, len3 = D1 & D2 & ~D3;
+    const uint64_t follow = (len1 & C1 & D2) | (len2 & C2 & D3) | (len3 & C3 & D4);
+    if (L & ~follow) return;
+    f.lits = L;
+    f.ok = true;  // values (<= 255, no leading zero) are checked while they are written
+}
+// Byte i of the fast chunk (constant i after unrolling).
+__device__ __forceinline__ uint32_t dp_byte(const DpFast& f, int i) { return (f.x[i >> 2] >> (8 * (i & 3))) & 0xFFu; }
+
 // Stage this wave's span (chunks c0 .. c0 + 63) and return its accessor.
 __device__ __forceinline__ LdsText dp_stage(const dparse::DArgs& a, uint64_t c0, uint8_t* rows) {
     const uint32_t lane = threadIdx.x & 63;
@@ -3519,7 +3583,14 @@ __global__ __launch_bounds__(256) void k_dparse_count(dparse::DArgs a, uint64_t*
     const uint64_t c = c0 + (threadIdx.x & 63);
     if (c >= a.nc) return;
     uint64_t no, nl;
-    dparse::chunk_count(a, t, c, no, nl);
+    DpFast f;
+    dp_fast(a, t, c, f);
+    if (f.ok) {
+        no = 0;
+        nl = __popcll(f.lits);
+    } else {
+        dparse::chunk_count(a, t, c, no, nl);
+    }
     ocnt[c] = no;
     lcnt[c] = nl;
 }
@@ -3531,7 +3602,10 @@ __global__ __launch_bounds__(256) void k_dparse_place(dparse::DArgs a, const uin
     if (c0 >= a.nc) return;
     const LdsText t = dp_stage(a, c0, st[threadIdx.x >> 6]);
     const uint64_t c = c0 + (threadIdx.x & 63);
-    if (c < a.nc) dparse::chunk_place(a, t, c, orank[c], pos);
+    if (c >= a.nc) return;
+    DpFast f;
+    dp_fast(a, t, c, f);
+    if (!f.ok) dparse::chunk_place(a, t, c, orank[c], pos);
 }
 
 // The literal bytes of a wave's chunks are one contiguous range of the output, [lrank[c0],
@@ -3563,13 +3637,36 @@ __global__ __launch_bounds__(256) void k_dparse(dparse::DArgs a, const uint64_t*
     const uint64_t c = c0 + lane;
     const uint64_t l0 = lrank[c0], l1 = lrank[c0 + 64 < a.nc ? c0 + 64 : a.nc];
     if (c < a.nc) {
-        uint64_t b;
-        if (lit && l1 - l0 <= kDpLitMax)
-            b = dparse::chunk_parse(a, t, c, orank, lrank, pos, nops, ops,
-                                    LdsLit{(__attribute__((address_space(3))) uint8_t*)lo[wid], l0});
-        else
-            b = dparse::chunk_parse(a, t, c, orank, lrank, pos, nops, ops, lit);
-        if (b != dparse::kNoBad) atomicMin(bad, (unsigned long long)b);
+        const bool staged = lit && l1 - l0 <= kDpLitMax;
+        DpFast f;
+        dp_fast(a, t, c, f);
+        if (f.ok) {  // each literal's value; a leading zero or a value > 255 sends the chunk to the body
+            const uint64_t r0 = lrank[c];
+            bool good = true;
+#pragma unroll
+            for (int i = 0; i < 64; ++i) {
+                if (!((f.lits >> i) & 1)) continue;
+                const uint32_t b0 = dp_byte(f, i) - '0', b1 = dp_byte(f, i + 1) - '0', b2 = dp_byte(f, i + 2) - '0';
+                const bool two = b1 < 10, three = two && b2 < 10;
+                const uint32_t v = three ? b0 * 100 + b1 * 10 + b2 : two ? b0 * 10 + b1 : b0;
+                good &= v <= 255 && !(two && b0 == 0);
+                const uint64_t r = r0 + __popcll(f.lits & ((1ull << i) - 1));
+                if (lit) {
+                    if (staged) lo[wid][r - l0] = (uint8_t)v;
+                    else lit[r] = (uint8_t)v;
+                }
+            }
+            f.ok = good;
+        }
+        if (!f.ok) {
+            uint64_t b;
+            if (staged)
+                b = dparse::chunk_parse(a, t, c, orank, lrank, pos, nops, ops,
+                                        LdsLit{(__attribute__((address_space(3))) uint8_t*)lo[wid], l0});
+            else
+                b = dparse::chunk_parse(a, t, c, orank, lrank, pos, nops, ops, lit);
+            if (b != dparse::kNoBad) atomicMin(bad, (unsigned long long)b);
+        }
     }
     if (!lit || l1 - l0 > kDpLitMax || l1 == l0) return;  // wave-uniform
     lds_fence();
