@@ -1016,10 +1016,12 @@ uint64_t device_walk_min();
 
 
 bool phase_probe_on() {
-    // "1": probe long miss runs at their phase (opt-in: on the C4 shape the unaligned
-    // window probes and the extra hit merges cost more host time than the scan they save)
+    // probe long miss runs at their phase ("0": off).  Off by default until round 4: on the
+    // C4 shape the host time of the phase probes outweighed the scan they save; with the
+    // host path trimmed the phase probe takes C4 (10 callers) from 19.6 to 17.3 ms/step
+    // (profiles/r04p_c4c10{,ph}_bench.json)
     const char* e = getenv("SYDELTA_PHASE_PROBE");
-    return e && e[0] == '1';
+    return !(e && e[0] == '0');
 }
 
 // The index carries k_scan_g's level-1 filter (one file, window above the LDS-staged

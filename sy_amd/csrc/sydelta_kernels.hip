@@ -2867,11 +2867,20 @@ struct ZLds {
     uint32_t ssize[4];
     uint32_t state[8];  // [0] type, [1] write offset, [2] abort, [3] entropy-only size, [4] nc, [5] nbest, [6] lz size
     uint32_t rank[2][kZT];  // the parallel parse: per thread literals / sequences, then their exclusive scans
-    uint32_t pstate[8];     // [0] literals, [1] sequences, [2] literals section size, [3] raw, [4] write offset
+    uint32_t pstate[12];    // [0] literals, [1] sequences, [2] literals section size, [3] raw, [4] write offset,
+                            // [5] sequences header size, [8..10] the final FSE states (OF, ML, LL)
     uint32_t ccnt[36 + 53 + 32];  // the sequences' LL / ML / OF code counts
     zstd::FseCT fse[3];           // their FSE tables (the coder's state lookups stay in LDS)
 };
 static_assert(sizeof(ZLds) <= 64 * 1024, "k_zstd_block's static LDS");
+
+typedef __attribute__((address_space(3))) uint8_t lds_u8;  // an LDS pointer kept as one
+// Text staged in LDS from block position base (k_zstd_block's candidate-distance rounds).
+struct ZStaged {
+    const lds_u8* l;
+    uint32_t base;
+    __device__ __forceinline__ uint8_t operator[](uint32_t p) const { return l[p - base]; }
+};
 
 // Bits of symbols src[first, first + count) coded with L.code, written as one literal
 // stream (last symbol first, LSB-first) into L.words with its closing 1 bit by a
@@ -3023,6 +3032,121 @@ __device__ uint32_t z_scan(uint32_t* v, uint32_t* tot) {
     return *tot;
 }
 
+// The sequences' bitstream of zstd::seq_section_counted (after its header), in parallel:
+// (1) every sequence's codes; (2) the three FSE state chains (OF, ML, LL: lanes 0-2 of
+// wave 0 in lockstep, one sequence per step, last to first, the codes read 64 at a time),
+// each step's state bits recorded; (3) every sequence's bit count and, by a block-wide
+// suffix sum (the stream holds the last sequence first), its offset; (4) the fields ORed
+// into a zeroed word buffer (sc.streams), the final states and the closing bit after
+// them; (5) the bytes copied out.  Byte-identical to the sequential writer (BitW: bits
+// LSB-first from byte 0).  Returns the stream's bytes (every thread).
+__device__ uint32_t z_seq_bits(ZLds& L, const zstd::SeqScratch& sc, uint32_t ns, uint8_t* __restrict__ out) {
+    const uint32_t tid = threadIdx.x, lane = tid & 63;
+    if (!ns) return 0;  // uniform
+    uint32_t* cw = sc.best;                // packed codes: lc | mc << 6 | oc << 12 | lb << 17 | mb << 22
+    uint32_t* rec = sc.best + ns;          // 3 x ns state records: nbo << 16 | bits (OF, ML, LL)
+    uint32_t* wb = (uint32_t*)sc.streams;  // the bit buffer
+    for (uint32_t k = tid; k < ns; k += kZT) {
+        uint32_t lc, lb, mc, mb, oc, ov;
+        zstd::seq_codes(sc.seq[k], lc, lb, mc, mb, oc, ov);
+        cw[k] = lc | (mc << 6) | (oc << 12) | (lb << 17) | (mb << 22);
+    }
+    __threadfence_block();
+    __syncthreads();
+    if (tid < 64) {
+        const zstd::FseCT& T = lane == 0 ? L.fse[2] : lane == 1 ? L.fse[1] : L.fse[0];  // OF, ML, LL
+        auto code_of = [&](uint32_t w) { return lane == 0 ? (w >> 12) & 31u : lane == 1 ? (w >> 6) & 63u : w & 63u; };
+        const bool on = lane < 3 && T.log != 0;
+        uint32_t st = 0;
+        if (on) st = zstd::fse_init(T, code_of(cw[ns - 1]));
+        for (uint32_t hi = ns - 1; hi > 0;) {  // sequences [lo, hi), last first
+            const uint32_t lo = hi > 64 ? hi - 64 : 0;
+            const uint32_t w = lo + lane < hi ? cw[lo + lane] : 0u;
+            for (uint32_t j = hi - lo; j-- > 0;) {
+                const uint32_t wj = __builtin_amdgcn_readlane(w, j);
+                if (lane < 3) {
+                    uint32_t r = 0;
+                    if (on) {
+                        const uint32_t c = code_of(wj);
+                        const uint32_t nbo = (uint32_t)((int32_t)st + T.delta_nb[c]) >> 16;
+                        r = (nbo << 16) | (st & ((1u << nbo) - 1u));
+                        st = T.state[(st >> nbo) + T.delta_find[c]];
+                    }
+                    rec[lane * ns + lo + j] = r;
+                }
+            }
+            hi = lo;
+        }
+        if (lane < 3) L.pstate[8 + lane] = st;  // final states: OF, ML, LL
+    }
+    __threadfence_block();
+    __syncthreads();
+    // bits per sequence, per thread range [t*per, +per), emitted from the top
+    const uint32_t per = (ns + kZT - 1) / kZT;
+    const uint32_t k0 = min(ns, tid * per), k1 = min(ns, k0 + per);
+    auto bits_of = [&](uint32_t k) -> uint32_t {
+        const uint32_t w = cw[k];
+        uint32_t b = ((w >> 17) & 31u) + ((w >> 22) & 31u) + ((w >> 12) & 31u);
+        if (k + 1 < ns) b += (rec[k] >> 16) + (rec[ns + k] >> 16) + (rec[2 * ns + k] >> 16);
+        return b;
+    };
+    uint32_t mine = 0;
+    for (uint32_t k = k0; k < k1; ++k) mine += bits_of(k);
+    L.part[tid] = mine;
+    __syncthreads();
+    uint32_t off = 0, total = 0;
+    for (uint32_t t = 0; t < kZT; ++t) {  // LDS broadcast reads
+        const uint32_t pb = L.part[t];
+        total += pb;
+        off += t > tid ? pb : 0u;
+    }
+    const uint32_t fb = L.fse[1].log + L.fse[2].log + L.fse[0].log;  // final states ML, OF, LL
+    const uint32_t nw = (total + fb + 1 + 31) / 32 + 1;
+    // <= 57 bits per sequence of >= 6 bytes: ~156 KiB at most; past the buffer the content
+    // is reported too large (the block keeps its entropy-only content)
+    if (nw > zstd::kStreamBytesMax) return 1u << 30;  // uniform
+    for (uint32_t i = tid; i < nw; i += kZT) wb[i] = 0;
+    __threadfence_block();
+    __syncthreads();
+    auto put = [&](uint32_t at, uint32_t v, uint32_t n) {
+        if (!n) return;
+        const uint64_t x = (uint64_t)(v & (n >= 32 ? 0xFFFFFFFFu : (1u << n) - 1u)) << (at & 31);
+        atomicOr(&wb[at >> 5], (uint32_t)x);
+        if (x >> 32) atomicOr(&wb[(at >> 5) + 1], (uint32_t)(x >> 32));
+    };
+    uint32_t at = off;
+    for (uint32_t k = k1; k-- > k0;) {
+        const uint32_t w = cw[k];
+        const zstd::Seq q = sc.seq[k];
+        if (k + 1 < ns) {
+            const uint32_t ro = rec[k], rm = rec[ns + k], rl = rec[2 * ns + k];
+            put(at, ro & 0xFFFFu, ro >> 16); at += ro >> 16;
+            put(at, rm & 0xFFFFu, rm >> 16); at += rm >> 16;
+            put(at, rl & 0xFFFFu, rl >> 16); at += rl >> 16;
+        }
+        const uint32_t lb = (w >> 17) & 31u, mb = (w >> 22) & 31u, oc = (w >> 12) & 31u;
+        put(at, q.ll, lb); at += lb;
+        put(at, q.ml - 3, mb); at += mb;
+        put(at, q.ov, oc); at += oc;
+    }
+    __threadfence_block();
+    __syncthreads();
+    if (tid == 0) {  // the final states (ML, OF, LL) and the closing bit
+        uint32_t a = total;
+        put(a, L.pstate[9], L.fse[1].log); a += L.fse[1].log;
+        put(a, L.pstate[8], L.fse[2].log); a += L.fse[2].log;
+        put(a, L.pstate[10], L.fse[0].log); a += L.fse[0].log;
+        put(a, 1u, 1u);
+    }
+    __threadfence_block();
+    __syncthreads();
+    const uint32_t bytes = (total + fb + 1 + 7) / 8;
+    const uint8_t* src = (const uint8_t*)wb;
+    for (uint32_t i = tid; i < bytes; i += kZT) out[i] = src[i];
+    __syncthreads();
+    return bytes;
+}
+
 // The literals + sequences content of a block (zstd::lz_content's bytes) with the parse in
 // parallel.  The parse's path from position 0 is a function of the position alone
 // (zstd::parse_take / match_len), so each thread walks its own 512 positions from their
@@ -3128,22 +3252,60 @@ __device__ uint32_t z_lz_content(ZLds& L, const uint8_t* __restrict__ in, uint32
     __threadfence_block();
     __syncthreads();
     z_phase(timing, tph, 9);
-    // the repeat history, in order (wave 0; uniform loop)
-    if (tid < 64) {
-        uint32_t rep[3] = {0, 0, 0}, end = 0;
-        for (uint32_t k = 0; k < ns; ++k) {
+    // Whether sequence k also matches at the previous sequence's best distance (the repeat
+    // distance the history usually holds there: after a sequence, rep[0] is the distance it
+    // used), for all k at once; the flags in sc.streams (free on the device path).
+    uint8_t* okp = sc.streams;
+    for (uint32_t k = tid; k < ns; k += kZT) {
+        uint8_t ok = 0;
+        if (k) {
             const zstd::Seq q = sc.seq[k];
-            const uint32_t x = q.ll, l = q.ml, d0 = q.off;
-            uint32_t d = d0;
-            if (rep[0] && rep[0] != d0 && rep[0] <= x) {  // zstd::seq_dist, compared by the wave
-                bool bad = false;
-                for (uint32_t i = lane; i < l; i += 64) bad |= in[x + i] != in[x + i - rep[0]];
-                if (!__ballot(bad)) d = rep[0];
+            const uint32_t d = sc.seq[k - 1].off, x = q.ll, l = q.ml;
+            if (d <= x) {
+                uint32_t i = 0;
+                while (i < l && in[x + i] == in[x + i - d]) ++i;
+                ok = i >= l;
             }
-            const uint32_t ll = x - end;
-            const uint32_t ov = zstd::rep_code(rep, ll, d);
-            if (lane == 0) sc.seq[k] = zstd::Seq{ll, l, d, ov};
-            end = x + l;
+        }
+        okp[k] = ok;
+    }
+    __threadfence_block();
+    __syncthreads();
+    // the repeat history, in order (wave 0): 64 records per coalesced load, then walked
+    // with readlane; a repeat distance other than the previous best is compared by the wave
+    if (tid < 64) {
+        uint32_t rep[3] = {0, 0, 0}, end = 0, prev_d0 = 0;
+        for (uint32_t k0 = 0; k0 < ns; k0 += 64) {
+            const uint32_t m = min(64u, ns - k0);
+            zstd::Seq q{0, 0, 0, 0};
+            uint32_t ok = 0;
+            if (lane < m) {
+                q = sc.seq[k0 + lane];
+                ok = okp[k0 + lane];
+            }
+            uint32_t rll = 0, rd = 0, rov = 0;
+            for (uint32_t j = 0; j < m; ++j) {
+                const uint32_t x = __builtin_amdgcn_readlane(q.ll, j), l = __builtin_amdgcn_readlane(q.ml, j);
+                const uint32_t d0 = __builtin_amdgcn_readlane(q.off, j), okj = __builtin_amdgcn_readlane(ok, j);
+                uint32_t d = d0;
+                if (rep[0] && rep[0] != d0 && rep[0] <= x) {  // zstd::seq_dist
+                    bool good;
+                    if (rep[0] == prev_d0) {
+                        good = okj != 0;
+                    } else {
+                        bool bad = false;
+                        for (uint32_t i = lane; i < l; i += 64) bad |= in[x + i] != in[x + i - rep[0]];
+                        good = !__ballot(bad);
+                    }
+                    if (good) d = rep[0];
+                }
+                const uint32_t ll = x - end;
+                const uint32_t ov = zstd::rep_code(rep, ll, d);
+                if (lane == j) { rll = ll; rd = d; rov = ov; }
+                end = x + l;
+                prev_d0 = d0;
+            }
+            if (lane < m) sc.seq[k0 + lane] = zstd::Seq{rll, q.ml, rd, rov};
         }
     }
     __threadfence_block();
@@ -3161,12 +3323,14 @@ __device__ uint32_t z_lz_content(ZLds& L, const uint8_t* __restrict__ in, uint32
     }
     const uint32_t z = z_lit_section(L, sc.lit, nl, sc.body);  // starts with a barrier
     z_phase(timing, tph, 11);
+    uint8_t* sp = sc.body + z;
     if (tid == 0)
-        L.pstate[2] = z + zstd::seq_section_counted(sc.seq, ns, sc.body + z, L.ccnt, L.ccnt + 36, L.ccnt + 36 + 53,
-                                                    L.fse[0], L.fse[1], L.fse[2]);
+        L.pstate[5] = zstd::seq_section_head(ns, sp, L.ccnt, L.ccnt + 36, L.ccnt + 36 + 53, L.fse[0], L.fse[1], L.fse[2]);
     __syncthreads();
+    const uint32_t ho = L.pstate[5];
+    const uint32_t nb = z_seq_bits(L, sc, ns, sp + ho);
     z_phase(timing, tph, 12);
-    return L.pstate[2];
+    return z + ho + nb;
 }
 
 
@@ -3263,17 +3427,31 @@ __global__ __launch_bounds__(kZT) void k_zstd_block(const uint8_t* __restrict__ 
     phase(1);
     // literals + sequences
     if (!rle && n >= 2) {
-        for (uint32_t p = tid; p < n; p += kZT)
-            if (in[p] == '{') {
-                uint32_t seen = 0;  // zstd::gap_count with LDS atomics
-                for (uint32_t d = 1; d < 256 && d <= p && seen < 3; ++d)
-                    if (in[p - d] == '{') {
-                        atomicAdd(&L.gaps[d], 1u);
-                        ++seen;
-                    }
-            }
-        for (uint32_t p = zstd::kRepStep * tid; p < n; p += zstd::kRepStep * kZT)
-            if (const uint32_t d = zstd::repeat_dist(in, n, p)) atomicAdd(&L.reps[d], 1u);
+        // in rounds of kRepStep * kZT positions, the round's text and the 256 bytes before it
+        // staged in LDS (the stream words: free until the hash rounds): one sampled position
+        // per thread (zstd::repeat_dist) and the '{' gaps (zstd::gap_count, LDS atomics)
+        constexpr uint32_t kRound = zstd::kRepStep * kZT;
+        static_assert(kRound + 256 + 4 <= 4 * kZStreamWords, "a round's text fits the stream words");
+        uint8_t* stg = (uint8_t*)L.words;
+        for (uint32_t r0 = 0; r0 < n; r0 += kRound) {
+            const uint32_t a0 = r0 > 256 ? r0 - 256 : 0u, a1 = min(n, r0 + kRound + 4);
+            __syncthreads();
+            for (uint32_t i = a0 + tid; i < a1; i += kZT) stg[i - a0] = in[i];
+            __syncthreads();
+            const ZStaged tx{(const lds_u8*)stg, a0};
+            for (uint32_t p = r0 + tid; p < min(n, r0 + kRound); p += kZT)
+                if (tx[p] == '{') {
+                    uint32_t seen = 0;
+                    for (uint32_t d = 1; d < 256 && d <= p && seen < 3; ++d)
+                        if (tx[p - d] == '{') {
+                            atomicAdd(&L.gaps[d], 1u);
+                            ++seen;
+                        }
+                }
+            const uint32_t p = r0 + zstd::kRepStep * tid;
+            if (p < n)
+                if (const uint32_t d = zstd::repeat_dist(tx, n, p)) atomicAdd(&L.reps[d], 1u);
+        }
         __syncthreads();
         if (tid == 0) {
             L.state[4] = zstd::pick_cands(L.gaps, L.reps, L.cand);
@@ -3472,7 +3650,6 @@ constexpr uint32_t kDpBefore = 8;                        // bytes staged before 
 constexpr uint32_t kDpSpan = 64 * 64 + kDpBefore + 136;  // staged bytes per wave
 constexpr uint32_t kDpRows = (kDpSpan + 63) / 64;
 
-typedef __attribute__((address_space(3))) uint8_t lds_u8;  // an LDS pointer kept as one
 // The text outside the staged span (not reached by well-formed text: every token and its
 // look-ahead ends inside the 136-byte halo).  Not inlined, so that the compiler cannot
 // turn the accessor's branch into a select that issues this global load for every byte.
@@ -3600,6 +3777,8 @@ __global__ __launch_bounds__(256) void k_dparse_place(dparse::DArgs a, const uin
     __shared__ uint8_t st[4][kDpRows * kDpRow];
     const uint64_t c0 = ((uint64_t)blockIdx.x * 256 + threadIdx.x) & ~63ull;
     if (c0 >= a.nc) return;
+    // a wave whose chunks start no op (a literal run's) has nothing to place: orank has nc + 1 entries
+    if (orank[c0 + 64 < a.nc ? c0 + 64 : a.nc] == orank[c0]) return;  // wave-uniform
     const LdsText t = dp_stage(a, c0, st[threadIdx.x >> 6]);
     const uint64_t c = c0 + (threadIdx.x & 63);
     if (c >= a.nc) return;

@@ -514,9 +514,10 @@ __host__ __device__ inline void seq_counts(const Seq* sq, uint32_t ns, uint32_t*
 // Sequences_Section from the code counts (seq_counts).  The sequences are read last to
 // first, eight at a time (independent loads in flight: a one-thread loop over
 // sequences in HBM otherwise waits a full round trip per sequence).
-__host__ __device__ inline uint32_t seq_section_counted(const Seq* sq, uint32_t ns, uint8_t* p, const uint32_t* cll,
-                                                        const uint32_t* cml, const uint32_t* cof, FseCT& tll,
-                                                        FseCT& tml, FseCT& tof) {
+// The Sequences_Section header: Number_of_Sequences, the modes byte and the three tables
+// (built into tll / tml / tof).  Returns its size.
+__host__ __device__ inline uint32_t seq_section_head(uint32_t ns, uint8_t* p, const uint32_t* cll, const uint32_t* cml,
+                                                     const uint32_t* cof, FseCT& tll, FseCT& tml, FseCT& tof) {
     uint32_t o = 0;
     if (ns < 128) {
         p[o++] = (uint8_t)ns;
@@ -529,13 +530,21 @@ __host__ __device__ inline uint32_t seq_section_counted(const Seq* sq, uint32_t 
         p[o++] = (uint8_t)((ns - 0x7F00) >> 8);
     }
     if (!ns) return o;
-    uint32_t lc, lb, mc, mb, oc, ov;
     const uint32_t modes_at = o++;
     uint32_t mll, mof, mml;
     o += seq_table(cll, 36, ns, 9, tll, &mll, p + o);
     o += seq_table(cof, 32, ns, 8, tof, &mof, p + o);
     o += seq_table(cml, 53, ns, 9, tml, &mml, p + o);
     p[modes_at] = (uint8_t)((mll << 6) | (mof << 4) | (mml << 2));
+    return o;
+}
+
+__host__ __device__ inline uint32_t seq_section_counted(const Seq* sq, uint32_t ns, uint8_t* p, const uint32_t* cll,
+                                                        const uint32_t* cml, const uint32_t* cof, FseCT& tll,
+                                                        FseCT& tml, FseCT& tof) {
+    const uint32_t o = seq_section_head(ns, p, cll, cml, cof, tll, tml, tof);
+    if (!ns) return o;
+    uint32_t lc, lb, mc, mb, oc, ov;
     BitW w{p + o, 0, 0, 0};
     seq_codes(sq[ns - 1], lc, lb, mc, mb, oc, ov);
     uint32_t sml = tml.log ? fse_init(tml, mc) : 0, sof = tof.log ? fse_init(tof, oc) : 0;
@@ -587,7 +596,8 @@ __host__ __device__ __forceinline__ uint32_t raw_lit_header(uint8_t* p, uint32_t
 
 // The '{' at p counts its distances (<= 255) to the three '{' before it: a Copy op's
 // text holds two, so its distance to the previous op's is the second or third.
-__host__ __device__ __forceinline__ void gap_count(const uint8_t* in, uint32_t p, uint32_t* gaps) {
+template <class T>
+__host__ __device__ __forceinline__ void gap_count(const T& in, uint32_t p, uint32_t* gaps) {
     uint32_t seen = 0;
     for (uint32_t d = 1; d < 256 && d <= p && seen < 3; ++d)
         if (in[p - d] == '{') {
@@ -599,7 +609,8 @@ __host__ __device__ __forceinline__ void gap_count(const uint8_t* in, uint32_t p
 // Repeat distance of position p (sampled every kRepStep positions): the smallest d in
 // [2, 255] with in[p, p+4) == in[p-d, p-d+4), 0 when there is none or the 4 bytes
 // continue a run (distance 1 is always a candidate).
-__host__ __device__ inline uint32_t repeat_dist(const uint8_t* in, uint32_t n, uint32_t p) {
+template <class T>
+__host__ __device__ inline uint32_t repeat_dist(const T& in, uint32_t n, uint32_t p) {
     if (p < 2 || p + 4 > n) return 0;
     const uint8_t b0 = in[p], b1 = in[p + 1], b2 = in[p + 2], b3 = in[p + 3];
     if (in[p - 1] == b0 && b0 == b1 && b1 == b2 && b2 == b3) return 0;
