@@ -22,10 +22,13 @@ pytestmark = [pytest.mark.gpu, pytest.mark.late]
 
 @pytest.fixture
 def device_walk():
-    keys = ("SYDELTA_DEVICE_WALK", "SYDELTA_DEVICE_WALK_MIN", "SYDELTA_PROBE")
+    keys = ("SYDELTA_DEVICE_WALK", "SYDELTA_DEVICE_WALK_MIN", "SYDELTA_PROBE", "SYDELTA_PHASE_PROBE")
     old = {k: os.environ.get(k) for k in keys}
     os.environ["SYDELTA_DEVICE_WALK"] = "1"
     os.environ["SYDELTA_DEVICE_WALK_MIN"] = "1"
+    # phase-probed sources are walked on the host (walk_device hands them back); the
+    # phase probe is on by default since round 4
+    os.environ["SYDELTA_PHASE_PROBE"] = "0"
     yield
     for k, v in old.items():
         if v is None:
