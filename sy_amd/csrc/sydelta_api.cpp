@@ -1675,27 +1675,62 @@ int Classifier::phase_probe(const std::vector<std::array<uint64_t, 4>>& jobs,
     HIP_TRY(hipMemcpyAsync(jb.p, pj.data(), pj.size() * sizeof(ProbeJob), hipMemcpyHostToDevice, s));
     HIP_TRY(launch_probe(base, (const ProbeJob*)jb.p, (uint32_t)pj.size(), np, 1, (uint32_t)n, fast, ix->ix, d_pw,
                          d_pst, d_out, s, prof));
-    std::vector<uint32_t> out(np);
-    HIP_TRY(hipMemcpyAsync(out.data(), d_out, np * 4, hipMemcpyDeviceToHost, s));
-    HIP_TRY(hipStreamSynchronize(s));
-    uint64_t w = 0;
-    for (auto& j : jobs) {
-        Src& c = src[j[0]];
-        if (c.ppos.empty()) {
-            c.ppos.assign(c.nblk, kUnknownNone);
-            c.phit.assign(c.nblk, kNoBlk);
-        }
-        for (uint64_t t = 0; t < j[2]; ++t, ++w) {
-            const uint64_t k = j[1] + t;  // local block
-            c.ppos[k] = (c.kb + k) * n + j[3];
-            c.phit[k] = out[w];
-            if (out[w] != kNoBlk) continue;
-            if (!missed.empty() && missed.back()[0] == j[0] && missed.back()[2] == c.kb + k)
-                missed.back()[2] = c.kb + k + 1;
-            else
-                missed.push_back({j[0], c.kb + k, c.kb + k + 1});
-        }
+    // results into the thread's pinned buffer (a pageable D2H of C4's ~1.3 M results is a
+    // staged copy); the previous call on this thread synchronized its stream
+    static thread_local std::pair<uint32_t*, size_t> pin{nullptr, 0};  // never freed, like the streams
+    if (pin.second < np) {
+        if (pin.first) (void)hipHostFree(pin.first);
+        pin = {nullptr, 0};
+        HIP_TRY(hipHostMalloc((void**)&pin.first, (np + np / 4) * 4, hipHostMallocDefault));
+        pin.second = np + np / 4;
     }
+    const uint32_t* out = pin.first;
+    HIP_TRY(hipMemcpyAsync(pin.first, d_out, np * 4, hipMemcpyDeviceToHost, s));
+    HIP_TRY(hipStreamSynchronize(s));
+    // each source's phase arrays sized once, then the jobs filled on the host pool (jobs of
+    // one source cover disjoint blocks), each job's missed blocks in its own list, joined
+    // in job order
+    std::vector<uint64_t> jofs(jobs.size() + 1, 0);
+    for (size_t q = 0; q < jobs.size(); ++q) jofs[q + 1] = jofs[q] + jobs[q][2];
+    std::vector<std::vector<std::array<uint64_t, 3>>> jmiss(jobs.size());
+    const int nthr = jobs.size() >= 64 ? walk_threads() : 1;
+    auto fill = [&](int t) {
+        for (size_t q = jobs.size() * t / nthr; q < jobs.size() * (t + 1) / nthr; ++q) {
+            const auto& j = jobs[q];
+            Src& c = src[j[0]];
+            if (q == 0 || jobs[q - 1][0] != j[0]) {  // the source's first job (jobs are grouped by source)
+                c.ppos.assign(c.nblk, kUnknownNone);
+                c.phit.assign(c.nblk, kNoBlk);
+            }
+        }
+    };
+    if (!run_parallel(nthr, fill)) return fail(SYDELTA_E_OOM, "out of host memory (phase probes)");
+    auto fill2 = [&](int t) {
+        for (size_t q = jobs.size() * t / nthr; q < jobs.size() * (t + 1) / nthr; ++q) {
+            const auto& j = jobs[q];
+            Src& c = src[j[0]];
+            auto& mv = jmiss[q];
+            uint64_t w = jofs[q];
+            for (uint64_t t2 = 0; t2 < j[2]; ++t2, ++w) {
+                const uint64_t k = j[1] + t2;  // local block
+                c.ppos[k] = (c.kb + k) * n + j[3];
+                c.phit[k] = out[w];
+                if (out[w] != kNoBlk) continue;
+                if (!mv.empty() && mv.back()[2] == c.kb + k)
+                    mv.back()[2] = c.kb + k + 1;
+                else
+                    mv.push_back({j[0], c.kb + k, c.kb + k + 1});
+            }
+        }
+    };
+    if (!run_parallel(nthr, fill2)) return fail(SYDELTA_E_OOM, "out of host memory (phase probes)");
+    for (auto& mv : jmiss)
+        for (auto& r : mv) {
+            if (!missed.empty() && missed.back()[0] == r[0] && missed.back()[2] == r[1])
+                missed.back()[2] = r[2];
+            else
+                missed.push_back(r);
+        }
     return SYDELTA_OK;
 }
 

@@ -263,6 +263,21 @@ inline int walk_src(const Src& c, uint64_t n, uint64_t entry, uint64_t end, cons
             lit = x;
             continue;
         }
+        if (has_phase && x == lit && x < end) {
+            // a run of phase-probed Copies (the shifted blocks after an insertion, C4): the
+            // window at x itself is the earliest hit at or after x (an aligned or scan hit
+            // there names the same block), so copy it and jump a block
+            uint64_t k = x / n;
+            if (k >= c.kb && k < kend && c.ppos[k - c.kb] == x && c.phit[k - c.kb] != kNoBlk) {
+                do {
+                    copy(c.phit[k - c.kb]);
+                    x += n;
+                    ++k;
+                } while (x < end && k < kend && c.ppos[k - c.kb] == x && c.phit[k - c.kb] != kNoBlk);
+                lit = x;
+                continue;
+            }
+        }
         uint64_t p = end;
         uint32_t pb = kNoBlk;
         if (i < H && c.hpos[i] < end) { p = c.hpos[i]; pb = c.hblk[i]; }
