@@ -3252,29 +3252,31 @@ __device__ uint32_t z_lz_content(ZLds& L, const uint8_t* __restrict__ in, uint32
     __threadfence_block();
     __syncthreads();
     z_phase(timing, tph, 9);
-    // Whether sequence k also matches at the previous sequence's best distance (the repeat
-    // distance the history usually holds there: after a sequence, rep[0] is the distance it
-    // used), for all k at once; the flags in sc.streams (free on the device path).
+    // After a sequence the history's rep[0] is the distance it used, which is the best
+    // distance of the last sequence that did not take the repeat: one of the few before.
+    // So for every k at once: bit b-1 = sequence k also matches (all its l bytes) at the
+    // best distance of sequence k - b, b = 1..8; the bytes in sc.streams (free on the
+    // device path).
     uint8_t* okp = sc.streams;
     for (uint32_t k = tid; k < ns; k += kZT) {
-        uint8_t ok = 0;
-        if (k) {
-            const zstd::Seq q = sc.seq[k];
-            const uint32_t d = sc.seq[k - 1].off, x = q.ll, l = q.ml;
-            if (d <= x) {
-                uint32_t i = 0;
-                while (i < l && in[x + i] == in[x + i - d]) ++i;
-                ok = i >= l;
-            }
+        uint32_t ok = 0;
+        const zstd::Seq q = sc.seq[k];
+        const uint32_t x = q.ll, l = q.ml;
+        for (uint32_t b = 1; b <= 8 && b <= k; ++b) {
+            const uint32_t d = sc.seq[k - b].off;
+            if (d > x || d == q.off) continue;  // unused: seq_dist needs rep[0] <= x and != the own best
+            uint32_t i = 0;
+            while (i < l && in[x + i] == in[x + i - d]) ++i;
+            ok |= (uint32_t)(i >= l) << (b - 1);
         }
-        okp[k] = ok;
+        okp[k] = (uint8_t)ok;
     }
     __threadfence_block();
     __syncthreads();
     // the repeat history, in order (wave 0): 64 records per coalesced load, then walked
     // with readlane; a repeat distance other than the previous best is compared by the wave
     if (tid < 64) {
-        uint32_t rep[3] = {0, 0, 0}, end = 0, prev_d0 = 0;
+        uint32_t rep[3] = {0, 0, 0}, end = 0, owner = 0;  // rep[0] is the best distance of sequence `owner`
         for (uint32_t k0 = 0; k0 < ns; k0 += 64) {
             const uint32_t m = min(64u, ns - k0);
             zstd::Seq q{0, 0, 0, 0};
@@ -3288,10 +3290,11 @@ __device__ uint32_t z_lz_content(ZLds& L, const uint8_t* __restrict__ in, uint32
                 const uint32_t x = __builtin_amdgcn_readlane(q.ll, j), l = __builtin_amdgcn_readlane(q.ml, j);
                 const uint32_t d0 = __builtin_amdgcn_readlane(q.off, j), okj = __builtin_amdgcn_readlane(ok, j);
                 uint32_t d = d0;
+                const uint32_t k = k0 + j;
                 if (rep[0] && rep[0] != d0 && rep[0] <= x) {  // zstd::seq_dist
                     bool good;
-                    if (rep[0] == prev_d0) {
-                        good = okj != 0;
+                    if (k - owner <= 8) {
+                        good = (okj >> (k - owner - 1)) & 1u;
                     } else {
                         bool bad = false;
                         for (uint32_t i = lane; i < l; i += 64) bad |= in[x + i] != in[x + i - rep[0]];
@@ -3303,7 +3306,7 @@ __device__ uint32_t z_lz_content(ZLds& L, const uint8_t* __restrict__ in, uint32
                 const uint32_t ov = zstd::rep_code(rep, ll, d);
                 if (lane == j) { rll = ll; rd = d; rov = ov; }
                 end = x + l;
-                prev_d0 = d0;
+                if (d == d0) owner = k;
             }
             if (lane < m) sc.seq[k0 + lane] = zstd::Seq{rll, q.ml, rd, rov};
         }

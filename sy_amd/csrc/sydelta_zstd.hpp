@@ -615,8 +615,13 @@ __host__ __device__ inline uint32_t repeat_dist(const T& in, uint32_t n, uint32_
     const uint8_t b0 = in[p], b1 = in[p + 1], b2 = in[p + 2], b3 = in[p + 3];
     if (in[p - 1] == b0 && b0 == b1 && b1 == b2 && b2 == b3) return 0;
     const uint32_t lim = p < 255 ? p : 255;
-    for (uint32_t d = 2; d <= lim; ++d)
-        if (in[p - d] == b0 && in[p - d + 1] == b1 && in[p - d + 2] == b2 && in[p - d + 3] == b3) return d;
+    // the 4 bytes at p - d as one word, slid back a byte per step (one read per distance)
+    const uint32_t v = (uint32_t)b0 | ((uint32_t)b1 << 8) | ((uint32_t)b2 << 16) | ((uint32_t)b3 << 24);
+    uint32_t w = (uint32_t)in[p - 2] | ((uint32_t)in[p - 1] << 8) | ((uint32_t)b0 << 16) | ((uint32_t)b1 << 24);
+    for (uint32_t d = 2; d <= lim; ++d) {
+        if (w == v) return d;
+        if (d < lim) w = (w << 8) | (uint32_t)in[p - d - 1];
+    }
     return 0;
 }
 
