@@ -2856,11 +2856,20 @@ static_assert(kZRun * kZT >= zstd::kBlockMax / 4 + 16, "one run per thread cover
 constexpr uint32_t kZStreamWords = (zstd::kStreamBytesMax + 3) / 4 + 2;
 
 struct ZLds {
-    uint32_t hist[4][256];
+    // The stream words share their space with what is dead whenever they are live: the
+    // histograms and the Huffman build's work area (before a stream's scatter) and the
+    // sequences' FSE tables (built after the literals section is out).  ~51 KB in all:
+    // three workgroups per CU.
+    union {
+        uint32_t words[kZStreamWords];
+        struct {
+            uint32_t hist[4][256];
+            zstd::HufWork work;
+        };
+        zstd::FseCT fse[3];  // the sequences' FSE tables (the coder's state lookups stay in LDS)
+    };
     uint32_t part[kZT];
-    uint32_t words[kZStreamWords];
     zstd::HufCode code;
-    zstd::HufWork work;
     uint32_t gaps[256];
     uint32_t reps[256];
     uint32_t cand[zstd::kCands];
@@ -2870,9 +2879,8 @@ struct ZLds {
     uint32_t pstate[12];    // [0] literals, [1] sequences, [2] literals section size, [3] raw, [4] write offset,
                             // [5] sequences header size, [8..10] the final FSE states (OF, ML, LL)
     uint32_t ccnt[36 + 53 + 32];  // the sequences' LL / ML / OF code counts
-    zstd::FseCT fse[3];           // their FSE tables (the coder's state lookups stay in LDS)
 };
-static_assert(sizeof(ZLds) <= 64 * 1024, "k_zstd_block's static LDS");
+static_assert(sizeof(ZLds) <= 160 * 1024 / 3, "k_zstd_block's static LDS: three workgroups per CU");
 
 typedef __attribute__((address_space(3))) uint8_t lds_u8;  // an LDS pointer kept as one
 // Text staged in LDS from block position base (k_zstd_block's candidate-distance rounds).
@@ -2881,6 +2889,32 @@ struct ZStaged {
     uint32_t base;
     __device__ __forceinline__ uint8_t operator[](uint32_t p) const { return l[p - base]; }
 };
+
+// Block-wide: the sum of v over the threads after this one (returned) and over all of
+// them (*total), by a wave suffix scan and the four wave sums in L.part[0..4).  Starts and
+// ends with a barrier.
+__device__ __forceinline__ uint32_t z_suffix(ZLds& L, uint32_t v, uint32_t& total) {
+    const uint32_t tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+    uint32_t x = v;
+#pragma unroll
+    for (uint32_t o = 1; o < 64; o <<= 1) {
+        const uint32_t y = __shfl_down(x, o);
+        if (lane + o < 64) x += y;
+    }
+    __syncthreads();
+    if (lane == 0) L.part[wid] = x;
+    __syncthreads();
+    uint32_t later = 0, all = 0;
+#pragma unroll
+    for (uint32_t w = 0; w < kZT / 64; ++w) {
+        const uint32_t t = L.part[w];
+        all += t;
+        later += w > wid ? t : 0u;
+    }
+    total = all;
+    __syncthreads();
+    return later + x - v;
+}
 
 // Bits of symbols src[first, first + count) coded with L.code, written as one literal
 // stream (last symbol first, LSB-first) into L.words with its closing 1 bit by a
@@ -2893,41 +2927,45 @@ __device__ uint32_t z_stream_scatter(ZLds& L, const uint8_t* __restrict__ src, u
     const uint32_t nw = (count * zstd::kMaxBits + 1 + 31) / 32 + 1;
     for (uint32_t i = tid; i < nw; i += kZT) L.words[i] = 0;
     const uint32_t A = first & ~15u, r0 = A + kZRun * tid, lim = first + count;
-    uint32_t x[kZRun / 4];
-#pragma unroll
-    for (uint32_t j = 0; j < kZRun / 16; ++j) {
+    // one 16-byte granule at a time (the run held whole in registers, fully unrolled, took
+    // ~250 VGPRs: one workgroup per CU); the second pass reads the granules again (L1/L2)
+    auto granule = [&](uint32_t j) {
         uint4 v = make_uint4(0, 0, 0, 0);
         if (r0 + 16 * j < lim) v = *(const uint4*)(src + r0 + 16 * j);
-        x[4 * j] = v.x; x[4 * j + 1] = v.y; x[4 * j + 2] = v.z; x[4 * j + 3] = v.w;
-    }
+        return v;
+    };
     uint32_t bits = 0;
+#pragma unroll 1
+    for (uint32_t j = 0; j < kZRun / 16; ++j) {
+        const uint4 v = granule(j);
+        const uint32_t w4[4] = {v.x, v.y, v.z, v.w};
 #pragma unroll
-    for (uint32_t k = 0; k < kZRun; ++k) {
-        const uint32_t p = r0 + k;
-        if (p >= first && p < lim) bits += L.code.len[(x[k >> 2] >> (8 * (k & 3))) & 0xFF];
+        for (uint32_t k = 0; k < 16; ++k) {
+            const uint32_t p = r0 + 16 * j + k;
+            if (p >= first && p < lim) bits += L.code.len[(w4[k >> 2] >> (8 * (k & 3))) & 0xFF];
+        }
     }
-    L.part[tid] = bits;
-    __syncthreads();
-    uint32_t off = 0, total = 0;
-    for (uint32_t t = 0; t < kZT; ++t) {  // LDS broadcast reads, uniform loop
-        const uint32_t pb = L.part[t];
-        total += pb;
-        off += t > tid ? pb : 0u;
-    }
+    uint32_t total;
+    const uint32_t off = z_suffix(L, bits, total);
     uint32_t word = off >> 5, fill = off & 31;
     uint64_t acc = 0;
+#pragma unroll 1
+    for (uint32_t j = kZRun / 16; j-- > 0;) {
+        const uint4 v = granule(j);
+        const uint32_t w4[4] = {v.x, v.y, v.z, v.w};
 #pragma unroll
-    for (uint32_t kk = kZRun; kk-- > 0;) {
-        const uint32_t p = r0 + kk;
-        if (p >= first && p < lim) {
-            const uint32_t sym = (x[kk >> 2] >> (8 * (kk & 3))) & 0xFF;
-            acc |= (uint64_t)L.code.code[sym] << fill;
-            fill += L.code.len[sym];
-            if (fill >= 32) {
-                atomicOr(&L.words[word], (uint32_t)acc);
-                acc >>= 32;
-                fill -= 32;
-                ++word;
+        for (uint32_t kk = 16; kk-- > 0;) {
+            const uint32_t p = r0 + 16 * j + kk;
+            if (p >= first && p < lim) {
+                const uint32_t sym = (w4[kk >> 2] >> (8 * (kk & 3))) & 0xFF;
+                acc |= (uint64_t)L.code.code[sym] << fill;
+                fill += L.code.len[sym];
+                if (fill >= 32) {
+                    atomicOr(&L.words[word], (uint32_t)acc);
+                    acc >>= 32;
+                    fill -= 32;
+                    ++word;
+                }
             }
         }
     }
@@ -3061,16 +3099,31 @@ __device__ uint32_t z_seq_bits(ZLds& L, const zstd::SeqScratch& sc, uint32_t ns,
         if (on) st = zstd::fse_init(T, code_of(cw[ns - 1]));
         for (uint32_t hi = ns - 1; hi > 0;) {  // sequences [lo, hi), last first
             const uint32_t lo = hi > 64 ? hi - 64 : 0;
-            const uint32_t w = lo + lane < hi ? cw[lo + lane] : 0u;
+            // each lane looks up its sequence's three code transforms (no dependence on the
+            // states): the chains' steps then wait on one LDS read each, the state table's
+            int32_t nb3[3] = {0, 0, 0}, fd3[3] = {0, 0, 0};
+            if (lo + lane < hi) {
+                const uint32_t w = cw[lo + lane];
+                const uint32_t c3[3] = {(w >> 12) & 31u, (w >> 6) & 63u, w & 63u};  // OF, ML, LL
+#pragma unroll
+                for (int t = 0; t < 3; ++t) {
+                    const zstd::FseCT& U = L.fse[2 - t];
+                    nb3[t] = U.delta_nb[c3[t]];
+                    fd3[t] = U.delta_find[c3[t]];
+                }
+            }
             for (uint32_t j = hi - lo; j-- > 0;) {
-                const uint32_t wj = __builtin_amdgcn_readlane(w, j);
+                const int32_t n0 = __builtin_amdgcn_readlane(nb3[0], j), n1 = __builtin_amdgcn_readlane(nb3[1], j);
+                const int32_t n2 = __builtin_amdgcn_readlane(nb3[2], j), f0 = __builtin_amdgcn_readlane(fd3[0], j);
+                const int32_t f1 = __builtin_amdgcn_readlane(fd3[1], j), f2 = __builtin_amdgcn_readlane(fd3[2], j);
                 if (lane < 3) {
                     uint32_t r = 0;
                     if (on) {
-                        const uint32_t c = code_of(wj);
-                        const uint32_t nbo = (uint32_t)((int32_t)st + T.delta_nb[c]) >> 16;
+                        const int32_t dnb = lane == 0 ? n0 : lane == 1 ? n1 : n2;
+                        const int32_t dfd = lane == 0 ? f0 : lane == 1 ? f1 : f2;
+                        const uint32_t nbo = (uint32_t)((int32_t)st + dnb) >> 16;
                         r = (nbo << 16) | (st & ((1u << nbo) - 1u));
-                        st = T.state[(st >> nbo) + T.delta_find[c]];
+                        st = T.state[(st >> nbo) + dfd];
                     }
                     rec[lane * ns + lo + j] = r;
                 }
@@ -3092,14 +3145,8 @@ __device__ uint32_t z_seq_bits(ZLds& L, const zstd::SeqScratch& sc, uint32_t ns,
     };
     uint32_t mine = 0;
     for (uint32_t k = k0; k < k1; ++k) mine += bits_of(k);
-    L.part[tid] = mine;
-    __syncthreads();
-    uint32_t off = 0, total = 0;
-    for (uint32_t t = 0; t < kZT; ++t) {  // LDS broadcast reads
-        const uint32_t pb = L.part[t];
-        total += pb;
-        off += t > tid ? pb : 0u;
-    }
+    uint32_t total;
+    const uint32_t off = z_suffix(L, mine, total);
     const uint32_t fb = L.fse[1].log + L.fse[2].log + L.fse[0].log;  // final states ML, OF, LL
     const uint32_t nw = (total + fb + 1 + 31) / 32 + 1;
     // <= 57 bits per sequence of >= 6 bytes: ~156 KiB at most; past the buffer the content
@@ -3217,38 +3264,57 @@ __device__ uint32_t z_lz_content(ZLds& L, const uint8_t* __restrict__ in, uint32
     }
     __syncthreads();
     z_phase(timing, tph, 8);
-    // count this segment's literals and sequence starts
+    // The marked positions are the path: a mark followed by a mark is a literal, any other
+    // mark starts a sequence that runs to the next mark (position n counts as marked; a
+    // match is >= kMinMatch bytes).  So the counts are popcounts and a sequence's length
+    // is a bitmap search: no reread of the bests or the text.
+    auto word = [&](uint32_t w) -> uint32_t {
+        return (32 * w < n ? bm[w] : 0u) | ((n >> 5) == w ? 1u << (n & 31) : 0u);
+    };
+    auto lit_mask = [&](uint32_t w, uint32_t m) {  // literals among the marks m of word w
+        return m & ((word(w) >> 1) | (word(w + 1) << 31));
+    };
     uint32_t nlit = 0, nseq = 0;
     for (uint32_t w = s0 >> 5; 32 * w < s1; ++w) {
-        uint32_t m = bm[w];
-        while (m) {
-            const uint32_t x = 32 * w + (uint32_t)__builtin_ctz(m);
-            m &= m - 1;
-            if (zstd::parse_take(sc.best, n, x)) ++nseq; else ++nlit;
-        }
+        const uint32_t m = bm[w], lit = lit_mask(w, m);
+        nlit += __builtin_popcount(lit);
+        nseq += __builtin_popcount(m & ~lit);
     }
     L.rank[0][tid] = nlit;
     L.rank[1][tid] = nseq;
     const uint32_t nl = z_scan(L.rank[0], &L.pstate[0]);
     const uint32_t ns = z_scan(L.rank[1], &L.pstate[1]);
     if (ns == 0) return 0;  // uniform
-    // gather: literals into sc.lit, sequence starts into sc.seq as {p, length, best distance}
+    // gather: literals into sc.lit (the word's 32 text bytes loaded once), sequence starts
+    // into sc.seq as {p, length, -, -}
     {
         uint32_t lr = L.rank[0][tid], sr = L.rank[1][tid];
         for (uint32_t w = s0 >> 5; 32 * w < s1; ++w) {
-            uint32_t m = bm[w];
-            while (m) {
-                const uint32_t x = 32 * w + (uint32_t)__builtin_ctz(m);
-                m &= m - 1;
-                if (zstd::parse_take(sc.best, n, x)) {
-                    const uint32_t b = sc.best[x];
-                    sc.seq[sr++] = zstd::Seq{x, zstd::match_len(in, n, x, b), b & 0xFFFFFFu, 0};
-                } else {
-                    sc.lit[lr++] = in[x];
-                }
+            const uint32_t m = bm[w];
+            if (!m) continue;
+            const uint32_t lit = lit_mask(w, m);
+            uint32_t sq = m & ~lit;
+            if (lit) {  // the text is readable to the end of its last 16-byte granule
+                const uint4 v0 = *(const uint4*)(in + 32 * w);
+                uint4 v1 = make_uint4(0, 0, 0, 0);
+                if (32 * w + 16 < n) v1 = *(const uint4*)(in + 32 * w + 16);
+                const uint32_t t8[8] = {v0.x, v0.y, v0.z, v0.w, v1.x, v1.y, v1.z, v1.w};
+#pragma unroll
+                for (uint32_t k = 0; k < 32; ++k)
+                    if ((lit >> k) & 1u) sc.lit[lr++] = (uint8_t)(t8[k >> 2] >> (8 * (k & 3)));
+            }
+            while (sq) {
+                const uint32_t k = (uint32_t)__builtin_ctz(sq);
+                sq &= sq - 1;
+                uint32_t nw = w, t = word(w) & ~((2u << k) - 1u);  // marks after x
+                while (!t) t = word(++nw);
+                sc.seq[sr++] = zstd::Seq{32 * w + k, 32 * nw + (uint32_t)__builtin_ctz(t) - (32 * w + k), 0, 0};
             }
         }
     }
+    __threadfence_block();
+    __syncthreads();
+    for (uint32_t k = tid; k < ns; k += kZT) sc.seq[k].off = sc.best[sc.seq[k].ll] & 0xFFFFFFu;  // best distances
     __threadfence_block();
     __syncthreads();
     z_phase(timing, tph, 9);
@@ -3265,18 +3331,17 @@ __device__ uint32_t z_lz_content(ZLds& L, const uint8_t* __restrict__ in, uint32
         for (uint32_t b = 1; b <= 8 && b <= k; ++b) {
             const uint32_t d = sc.seq[k - b].off;
             if (d > x || d == q.off) continue;  // unused: seq_dist needs rep[0] <= x and != the own best
-            uint32_t i = 0;
-            while (i < l && in[x + i] == in[x + i - d]) ++i;
-            ok |= (uint32_t)(i >= l) << (b - 1);
+            ok |= (uint32_t)(zstd::common_len(in, x, x - d, l) >= l) << (b - 1);
         }
         okp[k] = (uint8_t)ok;
     }
     __threadfence_block();
     __syncthreads();
+    z_phase(timing, tph, 14);
     // the repeat history, in order (wave 0): 64 records per coalesced load, then walked
     // with readlane; a repeat distance other than the previous best is compared by the wave
     if (tid < 64) {
-        uint32_t rep[3] = {0, 0, 0}, end = 0, owner = 0;  // rep[0] is the best distance of sequence `owner`
+        uint32_t rp0 = 0, rp1 = 0, rp2 = 0, end = 0, owner = 0;  // the history; rp0 is the best distance of sequence `owner`
         for (uint32_t k0 = 0; k0 < ns; k0 += 64) {
             const uint32_t m = min(64u, ns - k0);
             zstd::Seq q{0, 0, 0, 0};
@@ -3291,19 +3356,19 @@ __device__ uint32_t z_lz_content(ZLds& L, const uint8_t* __restrict__ in, uint32
                 const uint32_t d0 = __builtin_amdgcn_readlane(q.off, j), okj = __builtin_amdgcn_readlane(ok, j);
                 uint32_t d = d0;
                 const uint32_t k = k0 + j;
-                if (rep[0] && rep[0] != d0 && rep[0] <= x) {  // zstd::seq_dist
+                if (rp0 && rp0 != d0 && rp0 <= x) {  // zstd::seq_dist
                     bool good;
                     if (k - owner <= 8) {
                         good = (okj >> (k - owner - 1)) & 1u;
                     } else {
                         bool bad = false;
-                        for (uint32_t i = lane; i < l; i += 64) bad |= in[x + i] != in[x + i - rep[0]];
+                        for (uint32_t i = lane; i < l; i += 64) bad |= in[x + i] != in[x + i - rp0];
                         good = !__ballot(bad);
                     }
-                    if (good) d = rep[0];
+                    if (good) d = rp0;
                 }
                 const uint32_t ll = x - end;
-                const uint32_t ov = zstd::rep_code(rep, ll, d);
+                const uint32_t ov = zstd::rep_code3(rp0, rp1, rp2, ll, d);
                 if (lane == j) { rll = ll; rd = d; rov = ov; }
                 end = x + l;
                 if (d == d0) owner = k;
@@ -3330,6 +3395,8 @@ __device__ uint32_t z_lz_content(ZLds& L, const uint8_t* __restrict__ in, uint32
     if (tid == 0)
         L.pstate[5] = zstd::seq_section_head(ns, sp, L.ccnt, L.ccnt + 36, L.ccnt + 36 + 53, L.fse[0], L.fse[1], L.fse[2]);
     __syncthreads();
+    z_phase(timing, tph, 13);
+    if (timing && tid == 0) atomicAdd(&g_zstd_phase[15], (unsigned long long)ns);
     const uint32_t ho = L.pstate[5];
     const uint32_t nb = z_seq_bits(L, sc, ns, sp + ho);
     z_phase(timing, tph, 12);

@@ -744,7 +744,7 @@ extern "C" int sydelta_delta_from_json_device(const uint8_t* d_text, uint64_t le
 
 // ---------------------------------------------------------------------------
 // zstd frame of a text in HBM (ssh.rs:1009-1017: compress(delta_json, Compression::Zstd);
-// sydelta_zstd.hpp).  The text goes through in batches of 512 blocks (64 MiB): block
+// sydelta_zstd.hpp).  The text goes through in batches of 3072 blocks (384 MiB): block
 // contents into per-block slots (k_zstd_block), their placement (an exclusive scan of
 // 3 + content), then the frame (k_zstd_frame); scratch is one batch of slots.
 // ---------------------------------------------------------------------------
@@ -771,7 +771,9 @@ extern "C" int sydelta_zstd_compress_device(int device, const uint8_t* d_in, uin
         return SYDELTA_OK;
     }
     const uint64_t nblocks = (len + zstd::kBlockMax - 1) / zstd::kBlockMax;
-    uint64_t kBatch = 512;  // blocks per batch (64 MiB of text, ~0.7 GiB of scratch); SYDELTA_ZSTD_BATCH overrides
+    // blocks per batch (384 MiB of text, ~4 GiB of scratch): four rounds of the 768 blocks
+    // 256 CUs hold at once (three per CU), so the rounds' stragglers overlap; SYDELTA_ZSTD_BATCH overrides
+    uint64_t kBatch = 3072;
     if (const char* e = getenv("SYDELTA_ZSTD_BATCH"))
         if (const uint64_t v = strtoull(e, nullptr, 10)) kBatch = std::min<uint64_t>(v, 1 << 20);
     const uint64_t nb_max = std::min<uint64_t>(nblocks, kBatch);
@@ -812,9 +814,10 @@ extern "C" int sydelta_zstd_compress_device(int device, const uint8_t* d_in, uin
         HIP_TRY(zstd_phase_ticks(t));
         fprintf(stderr, "zstd block phases (ms of block time, summed over blocks): histogram+code %.2f, entropy "
                 "streams %.2f, candidate distances %.2f, candidate matches %.2f, hash rounds %.2f, lz content %.2f "
-                "(walks %.2f, chain %.2f, gather %.2f, repeats %.2f, literals %.2f, sequences %.2f), rest %.2f\n",
+                "(walks %.2f, chain %.2f, gather %.2f, repeat flags %.2f, repeats %.2f, literals %.2f, sequences "
+                "header %.2f, sequences bits %.2f), rest %.2f; %llu sequences\n",
                 t[0] / 1e5, t[1] / 1e5, t[2] / 1e5, t[3] / 1e5, t[4] / 1e5, t[5] / 1e5, t[7] / 1e5, t[8] / 1e5,
-                t[9] / 1e5, t[10] / 1e5, t[11] / 1e5, t[12] / 1e5, t[6] / 1e5);
+                t[9] / 1e5, t[14] / 1e5, t[10] / 1e5, t[11] / 1e5, t[13] / 1e5, t[12] / 1e5, t[6] / 1e5, t[15]);
     }
     return SYDELTA_OK;
 } catch (...) {

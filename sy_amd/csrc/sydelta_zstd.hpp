@@ -337,26 +337,31 @@ struct Seq {
 // only what this block's own sequences put there (0 = unknown), and a repeat code is used
 // only for a known entry.  Index r of the repeated offset is Offset_Value - 1, plus 1
 // when ll == 0 (then r = 3 means rep[0] - 1).
-__host__ __device__ __forceinline__ uint32_t rep_code(uint32_t* rep, uint32_t ll, uint32_t d) {
+// The history as three scalars (no indexed array: on the device an indexed private array
+// lives in scratch memory, a round trip per access in a loop over every sequence).
+__host__ __device__ __forceinline__ uint32_t rep_code3(uint32_t& r0, uint32_t& r1, uint32_t& r2, uint32_t ll,
+                                                       uint32_t d) {
     const uint32_t ll0 = ll == 0 ? 1u : 0u;
+    const uint32_t c3 = r0 > 1 ? r0 - 1 : 0u;  // candidate r = 3: rep[0] - 1
+    // candidates r = ll0 .. ll0 + 2 in order: (r0, r1, r2) or (r1, r2, r0 - 1)
+    const uint32_t va = ll0 ? r1 : r0, vb = ll0 ? r2 : r1, vc = ll0 ? c3 : r2;
     uint32_t ov = d + 3;
-    for (uint32_t r = ll0; r < 3 + ll0; ++r) {
-        const uint32_t v = r == 3 ? (rep[0] > 1 ? rep[0] - 1 : 0u) : rep[r];
-        if (v && v == d) {
-            ov = r + 1 - ll0;
-            break;
-        }
-    }
+    if (va && va == d) ov = 1;
+    else if (vb && vb == d) ov = 2;
+    else if (vc && vc == d) ov = 3;
     if (ov > 3) {
-        rep[2] = rep[1];
-        rep[1] = rep[0];
-        rep[0] = d;
+        r2 = r1;
+        r1 = r0;
+        r0 = d;
     } else if (ov - 1 + ll0 > 0) {
-        if (ov - 1 + ll0 >= 2) rep[2] = rep[1];
-        rep[1] = rep[0];
-        rep[0] = d;
+        if (ov - 1 + ll0 >= 2) r2 = r1;
+        r1 = r0;
+        r0 = d;
     }
     return ov;
+}
+__host__ __device__ __forceinline__ uint32_t rep_code(uint32_t* rep, uint32_t ll, uint32_t d) {
+    return rep_code3(rep[0], rep[1], rep[2], ll, d);
 }
 
 // Normalized counts of a block's codes (FSE_Compressed mode): table log L in [5, maxlog]
@@ -652,16 +657,49 @@ __host__ __device__ inline uint32_t pick_cands(const uint32_t* gaps, const uint3
 // Best candidate at position p of in[0, n): the longest match (compared up to kProbe
 // bytes) among the candidates, ties to the earlier candidate; 0 when < kMinMatch.
 // Packed as (length << 24) | distance.
+// Four bytes from any address, little-endian (one unaligned dword load on the device).
+__host__ __device__ __forceinline__ uint32_t ld32u(const uint8_t* p) {
+    uint32_t v;
+    __builtin_memcpy(&v, p, 4);
+    return v;
+}
+// How many bytes in[a, a + lim) and in[b, b + lim) share from their start: four at a time.
+__host__ __device__ __forceinline__ uint32_t common_len(const uint8_t* in, uint32_t a, uint32_t b, uint32_t lim) {
+    uint32_t l = 0;
+    for (; l + 4 <= lim; l += 4)
+        if (const uint32_t x = ld32u(in + a + l) ^ ld32u(in + b + l)) return l + ((uint32_t)__builtin_ctz(x) >> 3);
+    while (l < lim && in[a + l] == in[b + l]) ++l;
+    return l;
+}
+// common_len(in, p, q, kProbe) with the kProbe bytes at p already loaded (w): the eight
+// loads at q issued together, no early exit.
+__host__ __device__ __forceinline__ uint32_t probe_len(const uint32_t* w, const uint8_t* in, uint32_t q) {
+    uint32_t l = kProbe;
+#pragma unroll
+    for (uint32_t k = kProbe / 4; k-- > 0;)
+        if (const uint32_t x = w[k] ^ ld32u(in + q + 4 * k)) l = 4 * k + ((uint32_t)__builtin_ctz(x) >> 3);
+    return l;
+}
 __host__ __device__ __forceinline__ uint32_t best_at(const uint8_t* in, uint32_t n, uint32_t p, const uint32_t* cand,
                                                      uint32_t nc) {
     uint32_t bl = 0, bi = 0;
-    for (uint32_t c = 0; c < nc; ++c) {
-        const uint32_t d = cand[c];
-        if (d > p) continue;
-        uint32_t l = 0;
-        const uint32_t lim = (n - p) < kProbe ? (n - p) : kProbe;
-        while (l < lim && in[p + l] == in[p + l - d]) ++l;
-        if (l > bl) { bl = l; bi = c; }
+    if (p + kProbe <= n) {
+        uint32_t w[kProbe / 4];
+#pragma unroll
+        for (uint32_t k = 0; k < kProbe / 4; ++k) w[k] = ld32u(in + p + 4 * k);
+        for (uint32_t c = 0; c < nc; ++c) {
+            const uint32_t d = cand[c];
+            if (d > p) continue;
+            const uint32_t l = probe_len(w, in, p - d);
+            if (l > bl) { bl = l; bi = c; }
+        }
+    } else {
+        for (uint32_t c = 0; c < nc; ++c) {
+            const uint32_t d = cand[c];
+            if (d > p) continue;
+            const uint32_t l = common_len(in, p, p - d, n - p);
+            if (l > bl) { bl = l; bi = c; }
+        }
     }
     return bl >= kMinMatch ? (bl << 24) | cand[bi] : 0;
 }
@@ -685,8 +723,7 @@ __host__ __device__ __forceinline__ void hash_look(const uint8_t* in, uint32_t n
     if (!e) return;
     const uint32_t q = e - 1, d = p - q;
     const uint32_t lim = (n - p) < kProbe ? (n - p) : kProbe;
-    uint32_t l = 0;
-    while (l < lim && in[p + l] == in[q + l]) ++l;
+    const uint32_t l = common_len(in, p, q, lim);
     if (l >= (d < kHashNear ? kHashMinNear : kHashMinFar) && l > (best[p] >> 24)) best[p] = (l << 24) | d;
 }
 __host__ __device__ __forceinline__ void hash_put(const uint8_t* in, uint32_t n, uint32_t p, uint32_t* tab) {
@@ -708,16 +745,13 @@ __host__ __device__ __forceinline__ bool parse_take(const uint32_t* best, uint32
 __host__ __device__ __forceinline__ uint32_t match_len(const uint8_t* in, uint32_t n, uint32_t p, uint32_t b) {
     uint32_t l = b >> 24;
     const uint32_t d = b & 0xFFFFFFu;
-    if (l == kProbe)
-        while (p + l < n && in[p + l] == in[p + l - d]) ++l;
+    if (l == kProbe) l += common_len(in, p + l, p + l - d, n - p - l);
     return l;
 }
 __host__ __device__ __forceinline__ uint32_t seq_dist(const uint8_t* in, uint32_t p, uint32_t l, uint32_t d0,
                                                       const uint32_t* rep) {
     if (rep[0] && rep[0] != d0 && rep[0] <= p) {  // an equally long match at the repeat distance is cheaper
-        uint32_t lr = 0;
-        while (lr < l && in[p + lr] == in[p + lr - rep[0]]) ++lr;
-        if (lr >= l) return rep[0];
+        if (common_len(in, p, p - rep[0], l) >= l) return rep[0];
     }
     return d0;
 }
