@@ -2866,7 +2866,10 @@ struct ZLds {
             uint32_t hist[4][256];
             zstd::HufWork work;
         };
-        zstd::FseCT fse[3];  // the sequences' FSE tables (the coder's state lookups stay in LDS)
+        struct {
+            zstd::FseCT fse[3];  // the sequences' FSE tables (the coder's state lookups stay in LDS)
+            zstd::FseWork fw;    // and their build's work arrays
+        };
     };
     uint32_t part[kZT];
     zstd::HufCode code;
@@ -2883,12 +2886,58 @@ struct ZLds {
 static_assert(sizeof(ZLds) <= 160 * 1024 / 3, "k_zstd_block's static LDS: three workgroups per CU");
 
 typedef __attribute__((address_space(3))) uint8_t lds_u8;  // an LDS pointer kept as one
-// Text staged in LDS from block position base (k_zstd_block's candidate-distance rounds).
-struct ZStaged {
-    const lds_u8* l;
-    uint32_t base;
-    __device__ __forceinline__ uint8_t operator[](uint32_t p) const { return l[p - base]; }
-};
+
+// Whether a word holds a '{' byte (exact: the zero-byte test of w ^ '{'s).
+__device__ __forceinline__ bool z_has_brace(uint32_t w) {
+    const uint32_t x = w ^ 0x7B7B7B7Bu;
+    return ((x - 0x01010101u) & ~x & 0x80808080u) != 0;
+}
+// zstd::gap_count from the text in global memory (L1/L2: the 255 bytes behind p), four
+// bytes a load; the first 259 positions byte by byte.
+__device__ __forceinline__ void z_gap_count(const uint8_t* __restrict__ in, uint32_t p, uint32_t* gaps) {
+    if (p < 259) {
+        zstd::gap_count(in, p, gaps);
+        return;
+    }
+    uint32_t seen = 0;
+    for (uint32_t d0 = 1; d0 < 256 && seen < 3; d0 += 4) {
+        const uint32_t w = zstd::ld32u(in + p - d0 - 3);  // byte 3 is at p - d0
+        if (!z_has_brace(w)) continue;
+        for (int k = 3; k >= 0; --k) {
+            const uint32_t d = d0 + 3 - (uint32_t)k;
+            if (d < 256 && seen < 3 && ((w >> (8 * k)) & 0xFF) == '{') {
+                atomicAdd(&gaps[d], 1u);
+                ++seen;
+            }
+        }
+    }
+}
+// zstd::repeat_dist from the text in global memory.  p is a multiple of 4 (kRepStep), so
+// the 32 distances of a chunk, D0 .. D0 + 31, start at bytes A + 3 .. A + 34 with A =
+// p - D0 - 34 4-byte aligned: ten aligned loads and byte shifts by constants.
+static_assert(zstd::kRepStep % 4 == 0, "repeat samples at 4-byte aligned positions");
+__device__ __forceinline__ uint32_t z_repeat_dist(const uint8_t* __restrict__ in, uint32_t n, uint32_t p) {
+    if (p < 260) return zstd::repeat_dist(in, n, p);
+    if (p + 4 > n) return 0;
+    const uint32_t v = *(const uint32_t*)(in + p);
+    if (in[p - 1] == (v & 0xFF) && v == (v & 0xFF) * 0x01010101u) return 0;  // the 4 bytes continue a run
+    for (uint32_t D0 = 2; D0 < 256; D0 += 32) {
+        const uint32_t* A = (const uint32_t*)(in + (p - D0 - 34));  // the text is 16-byte aligned
+        uint32_t w[10];
+#pragma unroll
+        for (int i = 0; i < 10; ++i) w[i] = A[i];
+        uint32_t hit = 0;
+#pragma unroll
+        for (uint32_t t = 0; t < 32; ++t) {  // start A + 3 + t is distance D0 + 31 - t
+            const uint32_t o = 3 + t;
+            const uint32_t x = (o & 3) ? __builtin_amdgcn_alignbyte(w[(o >> 2) + 1], w[o >> 2], o & 3) : w[o >> 2];
+            hit |= (uint32_t)(x == v) << (31 - t);
+        }
+        if (D0 + 31 > 255) hit &= (1u << (256 - D0)) - 1u;  // distances <= 255
+        if (hit) return D0 + (uint32_t)__builtin_ctz(hit);
+    }
+    return 0;
+}
 
 // Block-wide: the sum of v over the threads after this one (returned) and over all of
 // them (*total), by a wave suffix scan and the four wave sums in L.part[0..4).  Starts and
@@ -3393,7 +3442,8 @@ __device__ uint32_t z_lz_content(ZLds& L, const uint8_t* __restrict__ in, uint32
     z_phase(timing, tph, 11);
     uint8_t* sp = sc.body + z;
     if (tid == 0)
-        L.pstate[5] = zstd::seq_section_head(ns, sp, L.ccnt, L.ccnt + 36, L.ccnt + 36 + 53, L.fse[0], L.fse[1], L.fse[2]);
+        L.pstate[5] = zstd::seq_section_head(ns, sp, L.ccnt, L.ccnt + 36, L.ccnt + 36 + 53, L.fse[0], L.fse[1], L.fse[2],
+                                               L.fw);
     __syncthreads();
     z_phase(timing, tph, 13);
     if (timing && tid == 0) atomicAdd(&g_zstd_phase[15], (unsigned long long)ns);
@@ -3497,31 +3547,23 @@ __global__ __launch_bounds__(kZT) void k_zstd_block(const uint8_t* __restrict__ 
     phase(1);
     // literals + sequences
     if (!rle && n >= 2) {
-        // in rounds of kRepStep * kZT positions, the round's text and the 256 bytes before it
-        // staged in LDS (the stream words: free until the hash rounds): one sampled position
-        // per thread (zstd::repeat_dist) and the '{' gaps (zstd::gap_count, LDS atomics)
-        constexpr uint32_t kRound = zstd::kRepStep * kZT;
-        static_assert(kRound + 256 + 4 <= 4 * kZStreamWords, "a round's text fits the stream words");
-        uint8_t* stg = (uint8_t*)L.words;
-        for (uint32_t r0 = 0; r0 < n; r0 += kRound) {
-            const uint32_t a0 = r0 > 256 ? r0 - 256 : 0u, a1 = min(n, r0 + kRound + 4);
-            __syncthreads();
-            for (uint32_t i = a0 + tid; i < a1; i += kZT) stg[i - a0] = in[i];
-            __syncthreads();
-            const ZStaged tx{(const lds_u8*)stg, a0};
-            for (uint32_t p = r0 + tid; p < min(n, r0 + kRound); p += kZT)
-                if (tx[p] == '{') {
-                    uint32_t seen = 0;
-                    for (uint32_t d = 1; d < 256 && d <= p && seen < 3; ++d)
-                        if (tx[p - d] == '{') {
-                            atomicAdd(&L.gaps[d], 1u);
-                            ++seen;
-                        }
+        // the '{' gaps (zstd::gap_count) and the sampled repeat distances (zstd::repeat_dist)
+        // straight from the text, four bytes a load, counted with LDS atomics
+        for (uint32_t c = tid; 16 * c < n; c += kZT) {
+            const uint4 v = *(const uint4*)(in + 16 * c);
+            const uint32_t w4[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                if (!z_has_brace(w4[q])) continue;
+#pragma unroll
+                for (int k = 0; k < 4; ++k) {
+                    const uint32_t p = 16 * c + 4 * q + k;
+                    if (p < n && ((w4[q] >> (8 * k)) & 0xFF) == '{') z_gap_count(in, p, L.gaps);
                 }
-            const uint32_t p = r0 + zstd::kRepStep * tid;
-            if (p < n)
-                if (const uint32_t d = zstd::repeat_dist(tx, n, p)) atomicAdd(&L.reps[d], 1u);
+            }
         }
+        for (uint32_t p = zstd::kRepStep * tid; p < n; p += zstd::kRepStep * kZT)
+            if (const uint32_t d = z_repeat_dist(in, n, p)) atomicAdd(&L.reps[d], 1u);
         __syncthreads();
         if (tid == 0) {
             L.state[4] = zstd::pick_cands(L.gaps, L.reps, L.cand);

@@ -254,10 +254,17 @@ struct FseCT {
     int32_t delta_find[53]; // deltaFindState per symbol
     uint32_t log;
 };
-__host__ __device__ inline void fse_build(FseCT& t, const int16_t* norm, uint32_t nsym, uint32_t log) {
-    const uint32_t size = 1u << log, mask = size - 1, step = (size >> 1) + (size >> 3) + 3;
+// The table builds' work arrays (the device keeps them in LDS: as a thread's private
+// arrays they live in scratch memory, a round trip per access in the spreading loops).
+struct FseWork {
     uint8_t sym[512];
     uint32_t cumul[54];
+    int16_t norm[53];
+};
+__host__ __device__ inline void fse_build(FseCT& t, const int16_t* norm, uint32_t nsym, uint32_t log, FseWork& fw) {
+    const uint32_t size = 1u << log, mask = size - 1, step = (size >> 1) + (size >> 3) + 3;
+    uint8_t* sym = fw.sym;
+    uint32_t* cumul = fw.cumul;
     uint32_t high = size - 1;
     cumul[0] = 0;
     for (uint32_t u = 1; u <= nsym; ++u) {
@@ -468,7 +475,7 @@ __host__ __device__ inline uint32_t fse_write_ncount(uint8_t* out, const int16_t
 // or FSE_Compressed (mode 2) from the block's counts.  Writes the table description at
 // out, returns its size; *mode, and t for the coder (log 0 for RLE: no state bits).
 __host__ __device__ inline uint32_t seq_table(const uint32_t* cnt, uint32_t nsym, uint32_t total, uint32_t maxlog,
-                                              FseCT& t, uint32_t* mode, uint8_t* out) {
+                                              FseCT& t, uint32_t* mode, uint8_t* out, FseWork& fw) {
     uint32_t distinct = 0, only = 0;
     for (uint32_t s = 0; s < nsym; ++s)
         if (cnt[s]) { ++distinct; only = s; }
@@ -481,9 +488,9 @@ __host__ __device__ inline uint32_t seq_table(const uint32_t* cnt, uint32_t nsym
         t.log = 0;
         return 1;
     }
-    int16_t norm[53];
+    int16_t* norm = fw.norm;
     const uint32_t L = fse_normalize(cnt, nsym, total, maxlog, norm);
-    fse_build(t, norm, nsym, L);
+    fse_build(t, norm, nsym, L, fw);
     *mode = 2;
     return fse_write_ncount(out, norm, nsym, L);
 }
@@ -522,7 +529,8 @@ __host__ __device__ inline void seq_counts(const Seq* sq, uint32_t ns, uint32_t*
 // The Sequences_Section header: Number_of_Sequences, the modes byte and the three tables
 // (built into tll / tml / tof).  Returns its size.
 __host__ __device__ inline uint32_t seq_section_head(uint32_t ns, uint8_t* p, const uint32_t* cll, const uint32_t* cml,
-                                                     const uint32_t* cof, FseCT& tll, FseCT& tml, FseCT& tof) {
+                                                     const uint32_t* cof, FseCT& tll, FseCT& tml, FseCT& tof,
+                                                     FseWork& fw) {
     uint32_t o = 0;
     if (ns < 128) {
         p[o++] = (uint8_t)ns;
@@ -537,9 +545,9 @@ __host__ __device__ inline uint32_t seq_section_head(uint32_t ns, uint8_t* p, co
     if (!ns) return o;
     const uint32_t modes_at = o++;
     uint32_t mll, mof, mml;
-    o += seq_table(cll, 36, ns, 9, tll, &mll, p + o);
-    o += seq_table(cof, 32, ns, 8, tof, &mof, p + o);
-    o += seq_table(cml, 53, ns, 9, tml, &mml, p + o);
+    o += seq_table(cll, 36, ns, 9, tll, &mll, p + o, fw);
+    o += seq_table(cof, 32, ns, 8, tof, &mof, p + o, fw);
+    o += seq_table(cml, 53, ns, 9, tml, &mml, p + o, fw);
     p[modes_at] = (uint8_t)((mll << 6) | (mof << 4) | (mml << 2));
     return o;
 }
@@ -547,7 +555,8 @@ __host__ __device__ inline uint32_t seq_section_head(uint32_t ns, uint8_t* p, co
 __host__ __device__ inline uint32_t seq_section_counted(const Seq* sq, uint32_t ns, uint8_t* p, const uint32_t* cll,
                                                         const uint32_t* cml, const uint32_t* cof, FseCT& tll,
                                                         FseCT& tml, FseCT& tof) {
-    const uint32_t o = seq_section_head(ns, p, cll, cml, cof, tll, tml, tof);
+    FseWork fw;
+    const uint32_t o = seq_section_head(ns, p, cll, cml, cof, tll, tml, tof, fw);
     if (!ns) return o;
     uint32_t lc, lb, mc, mb, oc, ov;
     BitW w{p + o, 0, 0, 0};
@@ -671,12 +680,14 @@ __host__ __device__ __forceinline__ uint32_t common_len(const uint8_t* in, uint3
     while (l < lim && in[a + l] == in[b + l]) ++l;
     return l;
 }
-// common_len(in, p, q, kProbe) with the kProbe bytes at p already loaded (w): the eight
-// loads at q issued together, no early exit.
+// common_len(in, p, q, kProbe) with the kProbe bytes at p already loaded (w): past a
+// first word that matches, the seven other loads at q issued together.
 __host__ __device__ __forceinline__ uint32_t probe_len(const uint32_t* w, const uint8_t* in, uint32_t q) {
+    // the first four bytes alone decide most candidates (below kMinMatch either way)
+    if (const uint32_t x = w[0] ^ ld32u(in + q)) return (uint32_t)__builtin_ctz(x) >> 3;
     uint32_t l = kProbe;
 #pragma unroll
-    for (uint32_t k = kProbe / 4; k-- > 0;)
+    for (uint32_t k = kProbe / 4; k-- > 1;)
         if (const uint32_t x = w[k] ^ ld32u(in + q + 4 * k)) l = 4 * k + ((uint32_t)__builtin_ctz(x) >> 3);
     return l;
 }
