@@ -2971,7 +2971,7 @@ __device__ __forceinline__ uint32_t z_suffix(ZLds& L, uint32_t v, uint32_t& tota
 // rounded down to 16; src 16-byte aligned and readable to the end of its last granule),
 // its first bit at the sum of the later runs' bits, OR-ing whole words.  Returns the
 // stream's bits without the closing bit (every thread).
-__device__ uint32_t z_stream_scatter(ZLds& L, const uint8_t* __restrict__ src, uint32_t first, uint32_t count) {
+__device__ __forceinline__ uint32_t z_stream_scatter(ZLds& L, const uint8_t* __restrict__ src, uint32_t first, uint32_t count) {
     const uint32_t tid = threadIdx.x;
     const uint32_t nw = (count * zstd::kMaxBits + 1 + 31) / 32 + 1;
     for (uint32_t i = tid; i < nw; i += kZT) L.words[i] = 0;
@@ -3028,7 +3028,7 @@ __device__ uint32_t z_stream_scatter(ZLds& L, const uint8_t* __restrict__ src, u
 // The literals section of lit[0, nl) into out (global), as zstd::lit_section_seq writes
 // it: Huffman-coded with the streams scattered in parallel (z_stream_scatter), or Raw
 // when that is impossible or not smaller.  Returns its size (every thread).
-__device__ uint32_t z_lit_section(ZLds& L, const uint8_t* __restrict__ lit, uint32_t nl, uint8_t* __restrict__ out) {
+__device__ __forceinline__ uint32_t z_lit_section(ZLds& L, const uint8_t* __restrict__ lit, uint32_t nl, uint8_t* __restrict__ out) {
     const uint32_t tid = threadIdx.x, wid = tid >> 6;
     for (uint32_t i = tid; i < 4 * 256; i += kZT) (&L.hist[0][0])[i] = 0;
     __syncthreads();
@@ -3127,7 +3127,7 @@ __device__ uint32_t z_scan(uint32_t* v, uint32_t* tot) {
 // into a zeroed word buffer (sc.streams), the final states and the closing bit after
 // them; (5) the bytes copied out.  Byte-identical to the sequential writer (BitW: bits
 // LSB-first from byte 0).  Returns the stream's bytes (every thread).
-__device__ uint32_t z_seq_bits(ZLds& L, const zstd::SeqScratch& sc, uint32_t ns, uint8_t* __restrict__ out) {
+__device__ __forceinline__ uint32_t z_seq_bits(ZLds& L, const zstd::SeqScratch& sc, uint32_t ns, uint8_t* __restrict__ out) {
     const uint32_t tid = threadIdx.x, lane = tid & 63;
     if (!ns) return 0;  // uniform
     uint32_t* cw = sc.best;                // packed codes: lc | mc << 6 | oc << 12 | lb << 17 | mb << 22
@@ -3210,20 +3210,38 @@ __device__ uint32_t z_seq_bits(ZLds& L, const zstd::SeqScratch& sc, uint32_t ns,
         atomicOr(&wb[at >> 5], (uint32_t)x);
         if (x >> 32) atomicOr(&wb[(at >> 5) + 1], (uint32_t)(x >> 32));
     };
-    uint32_t at = off;
-    for (uint32_t k = k1; k-- > k0;) {
-        const uint32_t w = cw[k];
-        const zstd::Seq q = sc.seq[k];
-        if (k + 1 < ns) {
-            const uint32_t ro = rec[k], rm = rec[ns + k], rl = rec[2 * ns + k];
-            put(at, ro & 0xFFFFu, ro >> 16); at += ro >> 16;
-            put(at, rm & 0xFFFFu, rm >> 16); at += rm >> 16;
-            put(at, rl & 0xFFFFu, rl >> 16); at += rl >> 16;
+    {
+        // this thread's bits [off, off + mine) accumulated in a register: the words wholly
+        // inside are stored, the two it may share with its neighbours ORed
+        uint32_t word = off >> 5, fill = off & 31;
+        uint64_t acc = 0;
+        bool first = true;
+        auto emit = [&](uint32_t v, uint32_t nb) {
+            acc |= (uint64_t)(v & ((1u << nb) - 1u)) << fill;  // nb <= 31
+            fill += nb;
+            if (fill >= 32) {
+                if (first) atomicOr(&wb[word], (uint32_t)acc);
+                else wb[word] = (uint32_t)acc;
+                first = false;
+                acc >>= 32;
+                fill -= 32;
+                ++word;
+            }
+        };
+        for (uint32_t k = k1; k-- > k0;) {
+            const uint32_t w = cw[k];
+            const zstd::Seq q = sc.seq[k];
+            if (k + 1 < ns) {
+                const uint32_t ro = rec[k], rm = rec[ns + k], rl = rec[2 * ns + k];
+                emit(ro & 0xFFFFu, ro >> 16);
+                emit(rm & 0xFFFFu, rm >> 16);
+                emit(rl & 0xFFFFu, rl >> 16);
+            }
+            emit(q.ll, (w >> 17) & 31u);
+            emit(q.ml - 3, (w >> 22) & 31u);
+            emit(q.ov, (w >> 12) & 31u);
         }
-        const uint32_t lb = (w >> 17) & 31u, mb = (w >> 22) & 31u, oc = (w >> 12) & 31u;
-        put(at, q.ll, lb); at += lb;
-        put(at, q.ml - 3, mb); at += mb;
-        put(at, q.ov, oc); at += oc;
+        if (fill) atomicOr(&wb[word], (uint32_t)acc);
     }
     __threadfence_block();
     __syncthreads();
@@ -3255,7 +3273,7 @@ __device__ uint32_t z_seq_bits(ZLds& L, const zstd::SeqScratch& sc, uint32_t ns,
 // (zstd::seq_dist compared by the whole wave, rep_code), thread 0 codes them
 // (seq_section) after the literals section (z_lit_section).  Returns its size, 0 when
 // the block has no sequence (every thread).
-__device__ uint32_t z_lz_content(ZLds& L, const uint8_t* __restrict__ in, uint32_t n, const zstd::SeqScratch& sc,
+__device__ __forceinline__ uint32_t z_lz_content(ZLds& L, const uint8_t* __restrict__ in, uint32_t n, const zstd::SeqScratch& sc,
                                  uint32_t timing, uint64_t& tph) {
     const uint32_t tid = threadIdx.x, lane = tid & 63;
     constexpr uint32_t kSeg = zstd::kBlockMax / kZT;  // 512 positions per thread
@@ -3399,30 +3417,34 @@ __device__ uint32_t z_lz_content(ZLds& L, const uint8_t* __restrict__ in, uint32
                 q = sc.seq[k0 + lane];
                 ok = okp[k0 + lane];
             }
-            uint32_t rll = 0, rd = 0, rov = 0;
+            // literal lengths in parallel: a sequence's start less the previous one's end
+            const uint32_t pend = __shfl_up(q.ll + q.ml, 1);
+            const uint32_t llv = q.ll - (lane ? pend : end);
+            end = __builtin_amdgcn_readlane(q.ll + q.ml, m - 1);
+            uint32_t rd = 0, rov = 0;
             for (uint32_t j = 0; j < m; ++j) {
-                const uint32_t x = __builtin_amdgcn_readlane(q.ll, j), l = __builtin_amdgcn_readlane(q.ml, j);
                 const uint32_t d0 = __builtin_amdgcn_readlane(q.off, j), okj = __builtin_amdgcn_readlane(ok, j);
+                const uint32_t ll = __builtin_amdgcn_readlane(llv, j);
                 uint32_t d = d0;
                 const uint32_t k = k0 + j;
-                if (rp0 && rp0 != d0 && rp0 <= x) {  // zstd::seq_dist
+                if (rp0 && rp0 != d0) {  // zstd::seq_dist
                     bool good;
-                    if (k - owner <= 8) {
+                    if (k - owner <= 8) {  // the flags hold rp0 <= x too
                         good = (okj >> (k - owner - 1)) & 1u;
                     } else {
-                        bool bad = false;
-                        for (uint32_t i = lane; i < l; i += 64) bad |= in[x + i] != in[x + i - rp0];
+                        const uint32_t x = __builtin_amdgcn_readlane(q.ll, j), l = __builtin_amdgcn_readlane(q.ml, j);
+                        bool bad = rp0 > x;
+                        if (!bad)
+                            for (uint32_t i = lane; i < l; i += 64) bad |= in[x + i] != in[x + i - rp0];
                         good = !__ballot(bad);
                     }
                     if (good) d = rp0;
                 }
-                const uint32_t ll = x - end;
                 const uint32_t ov = zstd::rep_code3(rp0, rp1, rp2, ll, d);
-                if (lane == j) { rll = ll; rd = d; rov = ov; }
-                end = x + l;
+                if (lane == j) { rd = d; rov = ov; }
                 if (d == d0) owner = k;
             }
-            if (lane < m) sc.seq[k0 + lane] = zstd::Seq{rll, q.ml, rd, rov};
+            if (lane < m) sc.seq[k0 + lane] = zstd::Seq{llv, q.ml, rd, rov};
         }
     }
     __threadfence_block();
@@ -3581,12 +3603,40 @@ __global__ __launch_bounds__(kZT) void k_zstd_block(const uint8_t* __restrict__ 
         uint32_t* tab = L.words;
         for (uint32_t i = tid; i < (1u << zstd::kHashBits); i += kZT) tab[i] = 0;
         __syncthreads();
+        // zstd::hash_look / hash_put, a thread's kPer positions of a round at once (their
+        // loads in flight together; the hashes kept for the puts)
+        constexpr uint32_t kPer = zstd::kHashRound / kZT;
         for (uint32_t r0 = 0; r0 < n; r0 += zstd::kHashRound) {
-            const uint32_t r1 = min(n, r0 + zstd::kHashRound);
-            for (uint32_t p = r0 + tid; p < r1; p += kZT) zstd::hash_look(in, n, p, tab, sc.best);
+            uint32_t h[kPer], wp[kPer], e[kPer];
+#pragma unroll
+            for (uint32_t i = 0; i < kPer; ++i) {
+                const uint32_t p = r0 + tid + i * kZT;
+                wp[i] = p + 4 <= n ? zstd::ld32u(in + p) : 0u;
+                h[i] = p + 4 <= n ? (wp[i] * 2654435761u) >> (32 - zstd::kHashBits) : 0xFFFFFFFFu;  // zstd::hash4
+            }
+#pragma unroll
+            for (uint32_t i = 0; i < kPer; ++i) e[i] = h[i] != 0xFFFFFFFFu ? tab[h[i]] : 0u;
+            uint32_t wq[kPer], bp[kPer];
+#pragma unroll
+            for (uint32_t i = 0; i < kPer; ++i) {
+                const uint32_t p = r0 + tid + i * kZT;
+                wq[i] = e[i] ? zstd::ld32u(in + e[i] - 1) : ~wp[i];
+                bp[i] = e[i] ? sc.best[p] : 0u;
+            }
+#pragma unroll
+            for (uint32_t i = 0; i < kPer; ++i) {
+                if (!e[i]) continue;
+                const uint32_t p = r0 + tid + i * kZT, q = e[i] - 1, d = p - q;
+                const uint32_t lim = min(n - p, zstd::kProbe);
+                const uint32_t x = wp[i] ^ wq[i];
+                const uint32_t l = x ? (uint32_t)__builtin_ctz(x) >> 3 : 4 + zstd::common_len(in, p + 4, q + 4, lim - 4);
+                if (l >= (d < zstd::kHashNear ? zstd::kHashMinNear : zstd::kHashMinFar) && l > (bp[i] >> 24))
+                    sc.best[p] = (l << 24) | d;
+            }
             __syncthreads();
-            for (uint32_t p = r0 + tid; p < r1; p += kZT)
-                if (p + 4 <= n) atomicMax(&tab[zstd::hash4(in, p)], p + 1);  // zstd::hash_put
+#pragma unroll
+            for (uint32_t i = 0; i < kPer; ++i)
+                if (h[i] != 0xFFFFFFFFu) atomicMax(&tab[h[i]], r0 + tid + i * kZT + 1);
             __syncthreads();
         }
         uint32_t mine = 0;

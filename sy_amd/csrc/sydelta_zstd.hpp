@@ -724,8 +724,7 @@ __host__ __device__ __forceinline__ uint32_t best_at(const uint8_t* in, uint32_t
 // device runs a round's lookups in parallel, then its puts (atomicMax): the same table.
 constexpr uint32_t kHashBits = 13, kHashRound = 2048, kHashMinNear = 6, kHashMinFar = 8, kHashNear = 4096;
 __host__ __device__ __forceinline__ uint32_t hash4(const uint8_t* in, uint32_t p) {
-    const uint32_t v = (uint32_t)in[p] | ((uint32_t)in[p + 1] << 8) | ((uint32_t)in[p + 2] << 16) | ((uint32_t)in[p + 3] << 24);
-    return (v * 2654435761u) >> (32 - kHashBits);
+    return (ld32u(in + p) * 2654435761u) >> (32 - kHashBits);  // the 4 bytes little-endian
 }
 __host__ __device__ __forceinline__ void hash_look(const uint8_t* in, uint32_t n, uint32_t p, const uint32_t* tab,
                                                    uint32_t* best) {
