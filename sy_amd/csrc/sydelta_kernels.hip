@@ -2853,15 +2853,18 @@ __device__ __forceinline__ void z_phase(uint32_t timing, uint64_t& tph, int k) {
 }
 constexpr uint32_t kZRun = 144;  // bytes of a stream per thread: 256 runs cover 32 KiB + the 16-byte phase
 static_assert(kZRun * kZT >= zstd::kBlockMax / 4 + 16, "one run per thread covers a stream");
-constexpr uint32_t kZStreamWords = (zstd::kStreamBytesMax + 3) / 4 + 2;
+// The LDS words: the hash rounds' table, then the parse's path bitmap (the literal streams
+// are scattered into the block's global scratch, so the workgroup fits 40 KB of LDS).
+constexpr uint32_t kZWords = (1u << zstd::kHashBits) > zstd::kBlockMax / 32 ? (1u << zstd::kHashBits) : zstd::kBlockMax / 32;
+static_assert((zstd::kStreamBytesMax + 3) / 4 + 2 <= zstd::kStreamBytesMax, "a stream's words fit sc.streams (4 x kStreamBytesMax bytes)");
 
 struct ZLds {
-    // The stream words share their space with what is dead whenever they are live: the
-    // histograms and the Huffman build's work area (before a stream's scatter) and the
-    // sequences' FSE tables (built after the literals section is out).  ~51 KB in all:
-    // three workgroups per CU.
+    // The words (hash table, path bitmap) share their space with what is dead whenever
+    // they are live: the histograms and the Huffman build's work area, the sequences' FSE
+    // tables (built after the literals section is out).  ~38 KB in all: four workgroups
+    // per CU.
     union {
-        uint32_t words[kZStreamWords];
+        uint32_t words[kZWords];
         struct {
             uint32_t hist[4][256];
             zstd::HufWork work;
@@ -2883,7 +2886,7 @@ struct ZLds {
                             // [5] sequences header size, [8..10] the final FSE states (OF, ML, LL)
     uint32_t ccnt[36 + 53 + 32];  // the sequences' LL / ML / OF code counts
 };
-static_assert(sizeof(ZLds) <= 160 * 1024 / 3, "k_zstd_block's static LDS: three workgroups per CU");
+static_assert(sizeof(ZLds) <= 160 * 1024 / 4, "k_zstd_block's static LDS: four workgroups per CU");
 
 typedef __attribute__((address_space(3))) uint8_t lds_u8;  // an LDS pointer kept as one
 
@@ -2966,15 +2969,17 @@ __device__ __forceinline__ uint32_t z_suffix(ZLds& L, uint32_t v, uint32_t& tota
 }
 
 // Bits of symbols src[first, first + count) coded with L.code, written as one literal
-// stream (last symbol first, LSB-first) into L.words with its closing 1 bit by a
-// parallel bit scatter: thread t encodes the run [A + kZRun t, +kZRun) (A = first
-// rounded down to 16; src 16-byte aligned and readable to the end of its last granule),
-// its first bit at the sum of the later runs' bits, OR-ing whole words.  Returns the
-// stream's bits without the closing bit (every thread).
-__device__ __forceinline__ uint32_t z_stream_scatter(ZLds& L, const uint8_t* __restrict__ src, uint32_t first, uint32_t count) {
+// stream (last symbol first, LSB-first) into gw (global, the block's scratch) with its
+// closing 1 bit by a parallel bit scatter: thread t encodes the run [A + kZRun t, +kZRun)
+// (A = first rounded down to 16; src 16-byte aligned and readable to the end of its last
+// granule), its first bit at the sum of the later runs' bits; the words wholly inside
+// its bits are stored, the two it may share ORed.  Returns the stream's bits without the
+// closing bit (every thread).
+__device__ __forceinline__ uint32_t z_stream_scatter(ZLds& L, const uint8_t* __restrict__ src, uint32_t first,
+                                                     uint32_t count, uint32_t* __restrict__ gw) {
     const uint32_t tid = threadIdx.x;
     const uint32_t nw = (count * zstd::kMaxBits + 1 + 31) / 32 + 1;
-    for (uint32_t i = tid; i < nw; i += kZT) L.words[i] = 0;
+    for (uint32_t i = tid; i < nw; i += kZT) gw[i] = 0;
     const uint32_t A = first & ~15u, r0 = A + kZRun * tid, lim = first + count;
     // one 16-byte granule at a time (the run held whole in registers, fully unrolled, took
     // ~250 VGPRs: one workgroup per CU); the second pass reads the granules again (L1/L2)
@@ -2998,6 +3003,7 @@ __device__ __forceinline__ uint32_t z_stream_scatter(ZLds& L, const uint8_t* __r
     const uint32_t off = z_suffix(L, bits, total);
     uint32_t word = off >> 5, fill = off & 31;
     uint64_t acc = 0;
+    bool lead = true;
 #pragma unroll 1
     for (uint32_t j = kZRun / 16; j-- > 0;) {
         const uint4 v = granule(j);
@@ -3010,7 +3016,9 @@ __device__ __forceinline__ uint32_t z_stream_scatter(ZLds& L, const uint8_t* __r
                 acc |= (uint64_t)L.code.code[sym] << fill;
                 fill += L.code.len[sym];
                 if (fill >= 32) {
-                    atomicOr(&L.words[word], (uint32_t)acc);
+                    if (lead) atomicOr(&gw[word], (uint32_t)acc);
+                    else gw[word] = (uint32_t)acc;
+                    lead = false;
                     acc >>= 32;
                     fill -= 32;
                     ++word;
@@ -3018,9 +3026,11 @@ __device__ __forceinline__ uint32_t z_stream_scatter(ZLds& L, const uint8_t* __r
             }
         }
     }
-    if (fill) atomicOr(&L.words[word], (uint32_t)acc);
+    if (fill) atomicOr(&gw[word], (uint32_t)acc);
+    __threadfence_block();
     __syncthreads();
-    if (tid == 0) atomicOr(&L.words[total >> 5], 1u << (total & 31));  // the closing bit
+    if (tid == 0) atomicOr(&gw[total >> 5], 1u << (total & 31));  // the closing bit
+    __threadfence_block();
     __syncthreads();
     return total;
 }
@@ -3028,7 +3038,8 @@ __device__ __forceinline__ uint32_t z_stream_scatter(ZLds& L, const uint8_t* __r
 // The literals section of lit[0, nl) into out (global), as zstd::lit_section_seq writes
 // it: Huffman-coded with the streams scattered in parallel (z_stream_scatter), or Raw
 // when that is impossible or not smaller.  Returns its size (every thread).
-__device__ __forceinline__ uint32_t z_lit_section(ZLds& L, const uint8_t* __restrict__ lit, uint32_t nl, uint8_t* __restrict__ out) {
+__device__ __forceinline__ uint32_t z_lit_section(ZLds& L, const uint8_t* __restrict__ lit, uint32_t nl, uint8_t* __restrict__ out,
+                                                  uint32_t* __restrict__ gw) {
     const uint32_t tid = threadIdx.x, wid = tid >> 6;
     for (uint32_t i = tid; i < 4 * 256; i += kZT) (&L.hist[0][0])[i] = 0;
     __syncthreads();
@@ -3061,7 +3072,7 @@ __device__ __forceinline__ uint32_t z_lit_section(ZLds& L, const uint8_t* __rest
         for (uint32_t st = 0; st < (four ? 4u : 1u); ++st) {
             uint32_t first, count;
             zstd::stream_range(nl, four, st, first, count);
-            const uint32_t total = z_stream_scatter(L, lit, first, count);
+            const uint32_t total = z_stream_scatter(L, lit, first, count, gw);
             const uint32_t bytes = total / 8 + 1;
             const uint32_t o = L.pstate[4];
             if (o + bytes >= raw_size || (!four && o + bytes - hs > zstd::kSingleStreamMax)) {
@@ -3070,7 +3081,7 @@ __device__ __forceinline__ uint32_t z_lit_section(ZLds& L, const uint8_t* __rest
                 __syncthreads();
                 break;
             }
-            const uint8_t* wb = (const uint8_t*)L.words;
+            const uint8_t* wb = (const uint8_t*)gw;
             for (uint32_t i = tid; i < bytes; i += kZT) out[o + i] = wb[i];
             __syncthreads();
             if (tid == 0) {
@@ -3277,7 +3288,7 @@ __device__ __forceinline__ uint32_t z_lz_content(ZLds& L, const uint8_t* __restr
                                  uint32_t timing, uint64_t& tph) {
     const uint32_t tid = threadIdx.x, lane = tid & 63;
     constexpr uint32_t kSeg = zstd::kBlockMax / kZT;  // 512 positions per thread
-    static_assert(kSeg % 32 == 0 && zstd::kBlockMax / 32 <= kZStreamWords, "the path bitmap fits the stream words");
+    static_assert(kSeg % 32 == 0 && zstd::kBlockMax / 32 <= kZWords, "the path bitmap fits the LDS words");
     uint32_t* bm = L.words;
     const uint32_t s0 = tid * kSeg, s1 = min(n, s0 + kSeg);
     for (uint32_t w = tid * (kSeg / 32); w < (tid + 1) * (kSeg / 32); ++w) bm[w] = 0;
@@ -3460,7 +3471,7 @@ __device__ __forceinline__ uint32_t z_lz_content(ZLds& L, const uint8_t* __restr
         atomicAdd(&L.ccnt[36 + mc], 1u);
         atomicAdd(&L.ccnt[36 + 53 + oc], 1u);
     }
-    const uint32_t z = z_lit_section(L, sc.lit, nl, sc.body);  // starts with a barrier
+    const uint32_t z = z_lit_section(L, sc.lit, nl, sc.body, (uint32_t*)sc.streams);  // starts with a barrier
     z_phase(timing, tph, 11);
     uint8_t* sp = sc.body + z;
     if (tid == 0)
@@ -3533,13 +3544,13 @@ __global__ __launch_bounds__(kZT) void k_zstd_block(const uint8_t* __restrict__ 
         for (uint32_t st = 0; st < ns; ++st) {
             uint32_t first, count;
             zstd::stream_range(n, four, st, first, count);
-            const uint32_t total = z_stream_scatter(L, in, first, count);
+            const uint32_t total = z_stream_scatter(L, in, first, count, (uint32_t*)sc.streams);
             const uint32_t bytes = total / 8 + 1;
             const uint32_t o = L.state[1];
             // a stream that would not fit the block's own size: no entropy-only content
             const bool fits = o + bytes + 1 < n && (four || o + bytes - hs <= zstd::kSingleStreamMax);
             if (fits) {
-                const uint8_t* wb = (const uint8_t*)L.words;
+                const uint8_t* wb = sc.streams;
                 for (uint32_t i = tid; i < bytes; i += kZT) slot[o + i] = wb[i];
             }
             __syncthreads();
@@ -3599,7 +3610,7 @@ __global__ __launch_bounds__(kZT) void k_zstd_block(const uint8_t* __restrict__ 
         // hash candidates in rounds of kHashRound positions (zstd::hash_look), the table in
         // the stream words (free after the entropy-only streams); position p stays with
         // thread p % kZT, so its best is read back by the thread that wrote it
-        static_assert(zstd::kHashRound % kZT == 0 && (1u << zstd::kHashBits) <= kZStreamWords, "hash rounds");
+        static_assert(zstd::kHashRound % kZT == 0 && (1u << zstd::kHashBits) <= kZWords, "hash rounds");
         uint32_t* tab = L.words;
         for (uint32_t i = tid; i < (1u << zstd::kHashBits); i += kZT) tab[i] = 0;
         __syncthreads();

@@ -744,7 +744,7 @@ extern "C" int sydelta_delta_from_json_device(const uint8_t* d_text, uint64_t le
 
 // ---------------------------------------------------------------------------
 // zstd frame of a text in HBM (ssh.rs:1009-1017: compress(delta_json, Compression::Zstd);
-// sydelta_zstd.hpp).  The text goes through in batches of 3072 blocks (384 MiB): block
+// sydelta_zstd.hpp).  The text goes through in batches of 4096 blocks (512 MiB): block
 // contents into per-block slots (k_zstd_block), their placement (an exclusive scan of
 // 3 + content), then the frame (k_zstd_frame); scratch is one batch of slots.
 // ---------------------------------------------------------------------------
@@ -771,9 +771,9 @@ extern "C" int sydelta_zstd_compress_device(int device, const uint8_t* d_in, uin
         return SYDELTA_OK;
     }
     const uint64_t nblocks = (len + zstd::kBlockMax - 1) / zstd::kBlockMax;
-    // blocks per batch (384 MiB of text, ~4 GiB of scratch): four rounds of the 768 blocks
-    // 256 CUs hold at once (three per CU), so the rounds' stragglers overlap; SYDELTA_ZSTD_BATCH overrides
-    uint64_t kBatch = 3072;
+    // blocks per batch (512 MiB of text, ~6 GiB of scratch: 1.5 MiB a block): four rounds of the 1024 blocks
+    // 256 CUs hold at once (four per CU), so the rounds' stragglers overlap; SYDELTA_ZSTD_BATCH overrides
+    uint64_t kBatch = 4096;
     if (const char* e = getenv("SYDELTA_ZSTD_BATCH"))
         if (const uint64_t v = strtoull(e, nullptr, 10)) kBatch = std::min<uint64_t>(v, 1 << 20);
     const uint64_t nb_max = std::min<uint64_t>(nblocks, kBatch);
