@@ -3416,10 +3416,19 @@ __device__ __forceinline__ uint32_t z_lz_content(ZLds& L, const uint8_t* __restr
     __threadfence_block();
     __syncthreads();
     z_phase(timing, tph, 14);
-    // the repeat history, in order (wave 0): 64 records per coalesced load, then walked
-    // with readlane; a repeat distance other than the previous best is compared by the wave
+    // The repeat history (wave 0), 64 sequences at a time.  Sequence k takes the repeat
+    // distance when flag j-1 of its record is set, j = k - owner (the last sequence that
+    // coded its own best): per lane that is a map of j in {0 (no history), 1..8, 9 (far)},
+    // and a wave scan of the maps gives every lane its j.  Without a repeat coded after a
+    // zero literal length at the same distance (the one case that puts a value twice in
+    // zstd's history), the history entering a sequence is the three latest distinct
+    // distances before it (move to front), which each lane finds by walking back over the
+    // batch's distances, then the carried history.  A batch with a far j, such a repeat or
+    // a carried history holding a value twice runs the sequential loop instead.
     if (tid < 64) {
+        uint32_t* dl = L.part;  // the batch's distances (free here)
         uint32_t rp0 = 0, rp1 = 0, rp2 = 0, end = 0, owner = 0;  // the history; rp0 is the best distance of sequence `owner`
+        uint32_t prev_off = 0;                                    // the previous batch's best distances
         for (uint32_t k0 = 0; k0 < ns; k0 += 64) {
             const uint32_t m = min(64u, ns - k0);
             zstd::Seq q{0, 0, 0, 0};
@@ -3432,30 +3441,89 @@ __device__ __forceinline__ uint32_t z_lz_content(ZLds& L, const uint8_t* __restr
             const uint32_t pend = __shfl_up(q.ll + q.ml, 1);
             const uint32_t llv = q.ll - (lane ? pend : end);
             end = __builtin_amdgcn_readlane(q.ll + q.ml, m - 1);
-            uint32_t rd = 0, rov = 0;
-            for (uint32_t j = 0; j < m; ++j) {
-                const uint32_t d0 = __builtin_amdgcn_readlane(q.off, j), okj = __builtin_amdgcn_readlane(ok, j);
-                const uint32_t ll = __builtin_amdgcn_readlane(llv, j);
-                uint32_t d = d0;
-                const uint32_t k = k0 + j;
-                if (rp0 && rp0 != d0) {  // zstd::seq_dist
-                    bool good;
-                    if (k - owner <= 8) {  // the flags hold rp0 <= x too
-                        good = (okj >> (k - owner - 1)) & 1u;
-                    } else {
-                        const uint32_t x = __builtin_amdgcn_readlane(q.ll, j), l = __builtin_amdgcn_readlane(q.ml, j);
-                        bool bad = rp0 > x;
-                        if (!bad)
-                            for (uint32_t i = lane; i < l; i += 64) bad |= in[x + i] != in[x + i - rp0];
-                        good = !__ballot(bad);
-                    }
-                    if (good) d = rp0;
-                }
-                const uint32_t ov = zstd::rep_code3(rp0, rp1, rp2, ll, d);
-                if (lane == j) { rd = d; rov = ov; }
-                if (d == d0) owner = k;
+            // (1) j per lane: maps of 10 states x 4 bits, composed by a wave scan
+            const uint32_t jin = k0 == 0 ? 0u : min(k0 - owner, 9u);
+            uint64_t f = 0x9876543210ull;  // identity (lanes past m)
+            if (lane < m) {
+                f = 0x9ull << 36 | 1ull;  // j = 9 stays far, j = 0 -> 1
+#pragma unroll
+                for (uint32_t j = 1; j <= 8; ++j) f |= (uint64_t)(((ok >> (j - 1)) & 1u) ? j + 1 : 1u) << (4 * j);
             }
-            if (lane < m) sc.seq[k0 + lane] = zstd::Seq{llv, q.ml, rd, rov};
+            auto compose = [](uint64_t P, uint64_t Q) {  // P after Q
+                uint64_t r = 0;
+#pragma unroll
+                for (uint32_t j = 0; j < 10; ++j) r |= ((P >> (4 * ((Q >> (4 * j)) & 15))) & 15) << (4 * j);
+                return r;
+            };
+#pragma unroll
+            for (uint32_t o = 1; o < 64; o <<= 1) {
+                const uint64_t Q = __shfl_up(f, o);
+                if (lane >= o) f = compose(f, Q);
+            }
+            const uint64_t E = __shfl_up(f, 1);
+            const uint32_t js = lane ? (uint32_t)(E >> (4 * jin)) & 15u : jin;
+            const bool take = js >= 1 && js <= 8 && ((ok >> (js - 1)) & 1u);
+            const uint32_t a0 = __shfl(q.off, (lane - js) & 63), a1 = __shfl(prev_off, (lane - js) & 63);
+            const uint32_t dv = take ? (lane >= js ? a0 : a1) : q.off;
+            // (2) the history entering each lane
+            dl[lane] = dv;
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+            uint32_t h0 = 0, h1 = 0, h2 = 0, nf = 0;
+            auto add = [&](uint32_t v) {
+                if (!v || nf >= 3 || v == h0 || v == h1) return;
+                if (nf == 0) h0 = v; else if (nf == 1) h1 = v; else h2 = v;
+                ++nf;
+            };
+            for (uint32_t o = 1; o <= 64; ++o) {
+                const bool need = lane < m && nf < 3 && o <= lane;
+                if (!__ballot(need)) break;
+                if (need) add(dl[lane - o]);
+            }
+            add(rp0);
+            add(rp1);
+            add(rp2);
+            const bool carried_ok = !(rp0 && (rp0 == rp1 || rp0 == rp2)) && !(rp1 && rp1 == rp2);
+            const bool bad = lane < m && (js == 9 || (llv == 0 && dv == h0 && h0 != 0));
+            if (carried_ok && !__ballot(bad)) {
+                uint32_t t0 = h0, t1 = h1, t2 = h2;
+                const uint32_t ov = zstd::rep_code3(t0, t1, t2, llv, dv);
+                if (lane < m) sc.seq[k0 + lane] = zstd::Seq{llv, q.ml, dv, ov};
+                rp0 = __builtin_amdgcn_readlane(t0, m - 1);
+                rp1 = __builtin_amdgcn_readlane(t1, m - 1);
+                rp2 = __builtin_amdgcn_readlane(t2, m - 1);
+                const uint32_t jl = __builtin_amdgcn_readlane(js, m - 1);
+                const bool tl = __builtin_amdgcn_readlane((uint32_t)take, m - 1) != 0;
+                owner = k0 + m - (tl ? jl + 1 : 1u);
+            } else {  // the sequential form of the batch
+                uint32_t rd = 0, rov = 0;
+                for (uint32_t j = 0; j < m; ++j) {
+                    const uint32_t d0 = __builtin_amdgcn_readlane(q.off, j), okj = __builtin_amdgcn_readlane(ok, j);
+                    const uint32_t ll = __builtin_amdgcn_readlane(llv, j);
+                    uint32_t d = d0;
+                    const uint32_t k = k0 + j;
+                    if (rp0 && rp0 != d0) {  // zstd::seq_dist
+                        bool good;
+                        if (k - owner <= 8) {  // the flags hold rp0 <= x too
+                            good = (okj >> (k - owner - 1)) & 1u;
+                        } else {
+                            const uint32_t x = __builtin_amdgcn_readlane(q.ll, j), l = __builtin_amdgcn_readlane(q.ml, j);
+                            bool bd = rp0 > x;
+                            if (!bd)
+                                for (uint32_t i = lane; i < l; i += 64) bd |= in[x + i] != in[x + i - rp0];
+                            good = !__ballot(bd);
+                        }
+                        if (good) d = rp0;
+                    }
+                    const uint32_t ov = zstd::rep_code3(rp0, rp1, rp2, ll, d);
+                    if (lane == j) { rd = d; rov = ov; }
+                    if (d == d0) owner = k;
+                }
+                if (lane < m) sc.seq[k0 + lane] = zstd::Seq{llv, q.ml, rd, rov};
+            }
+            prev_off = q.off;
+            __builtin_amdgcn_wave_barrier();  // dl is rewritten by the next batch
         }
     }
     __threadfence_block();

@@ -4,7 +4,7 @@ the frame of every text must equal the sequential host form's byte for byte
 libzstd must decode it to the text.  The texts: Delta JSON written on the device
 (copy-heavy ones take literals + sequences blocks), block-size edges, RLE / Raw blocks,
 skewed symbol counts (codes folded to 11 bits), runs, batches of 1 and 3 blocks, and a
-192 MiB text (three batches of 512 blocks).
+192 MiB text (three batches of 512 blocks, and one batch of the default 4096).
 
 Marked late (runs after the kernel parity tests); green on hardware since round 3."""
 import os
@@ -79,23 +79,44 @@ def test_device_json_then_zstd(gpu):
     assert len(frame) < 0.5 * len(host_text)
 
 
-def test_device_frame_large(gpu):
+@pytest.mark.parametrize("batch", ["512", None])
+def test_device_frame_large(batch, gpu):
     """192 MiB of decimal-list text (3 batches of 512 blocks: first, middle and last batch
-    placement): the frame against the host form (compared on the device) and decoded by
-    libzstd.  The host form encodes ~5 MiB/s on one core, so the size is kept to what
-    checks the batching."""
+    placement; then one batch at the default size): the frame against the host form
+    (compared on the device) and decoded by libzstd.  The host form encodes ~5 MiB/s on
+    one core, so the size is kept to what checks the batching."""
     import torch
 
     from sy_amd import wire
 
-    rng = np.random.default_rng(5)
-    period = (",".join(str(int(x)) for x in rng.integers(0, 256, 50000)) + ",").encode()
+    old = os.environ.get("SYDELTA_ZSTD_BATCH")
+    if batch is None:
+        os.environ.pop("SYDELTA_ZSTD_BATCH", None)
+    else:
+        os.environ["SYDELTA_ZSTD_BATCH"] = batch
+    try:
+        _large_frame(wire, torch)
+    finally:
+        if old is None:
+            os.environ.pop("SYDELTA_ZSTD_BATCH", None)
+        else:
+            os.environ["SYDELTA_ZSTD_BATCH"] = old
+
+
+_LARGE = {}
+
+
+def _large_frame(wire, torch):
     L = 3 << 26
-    reps = L // len(period) + 1
-    per = torch.frombuffer(bytearray(period), dtype=torch.uint8).cuda()
-    text = per.repeat(reps)[:L].contiguous()
+    if not _LARGE:  # the text and its host form, made once for both batch sizes
+        rng = np.random.default_rng(5)
+        period = (",".join(str(int(x)) for x in rng.integers(0, 256, 50000)) + ",").encode()
+        reps = L // len(period) + 1
+        per = torch.frombuffer(bytearray(period), dtype=torch.uint8).cuda()
+        _LARGE["text"] = per.repeat(reps)[:L].contiguous()
+        _LARGE["host"] = Z.ref_compress(bytes(_LARGE["text"].cpu().numpy()))
+        assert Z.zstd_decode(_LARGE["host"], L) == bytes(_LARGE["text"].cpu().numpy())
+    text, host = _LARGE["text"], _LARGE["host"]
     frame = wire.zstd_compress_device(text)
-    host = Z.ref_compress(bytes(text.cpu().numpy()))
     assert frame.numel() == len(host)
     assert bool((frame == torch.frombuffer(bytearray(host), dtype=torch.uint8).cuda()).all())
-    assert Z.zstd_decode(host, L) == bytes(text.cpu().numpy())
