@@ -3288,28 +3288,47 @@ __device__ __forceinline__ uint32_t z_lz_content(ZLds& L, const uint8_t* __restr
                                  uint32_t timing, uint64_t& tph) {
     const uint32_t tid = threadIdx.x, lane = tid & 63;
     constexpr uint32_t kSeg = zstd::kBlockMax / kZT;  // 512 positions per thread
-    static_assert(kSeg % 32 == 0 && zstd::kBlockMax / 32 <= kZWords, "the path bitmap fits the LDS words");
-    uint32_t* bm = L.words;
+    static_assert(kSeg % 32 == 0 && 2 * (zstd::kBlockMax / 32) <= kZWords, "the path and take bitmaps fit the LDS words");
+    uint32_t* bm = L.words;                          // the positions the path steps on
+    uint32_t* tk = L.words + zstd::kBlockMax / 32;   // zstd::parse_take of every position
     const uint32_t s0 = tid * kSeg, s1 = min(n, s0 + kSeg);
     for (uint32_t w = tid * (kSeg / 32); w < (tid + 1) * (kSeg / 32); ++w) bm[w] = 0;
-    __syncthreads();
-    auto step = [&](uint32_t p) -> uint32_t {
-        return zstd::parse_take(sc.best, n, p) ? p + zstd::match_len(in, n, p, sc.best[p]) : p + 1;
-    };
-    // speculative walk of this thread's segment
-    uint32_t p = s0;
-    {
-        uint32_t cw = s0 >> 5, acc = 0;
-        while (p < s1) {
-            if ((p >> 5) != cw) {
-                bm[cw] = acc;
-                acc = 0;
-                cw = p >> 5;
+    {  // the take bitmap, 64 positions per wave step (coalesced bests, one ballot)
+        const uint32_t wid = tid >> 6;
+        for (uint32_t b = 64 * wid; b < zstd::kBlockMax; b += kZT) {
+            const uint32_t q = b + lane;
+            const uint32_t cur = q < n ? sc.best[q] : 0u;
+            uint32_t nxt = __shfl_down(cur, 1);
+            if (lane == 63) nxt = q + 1 < n ? sc.best[q + 1] : 0u;
+            const bool take = cur && !(q + 1 < n && (nxt >> 24) > (cur >> 24));  // zstd::parse_take
+            const uint64_t m = __ballot(take);
+            if (lane == 0) {
+                tk[b >> 5] = (uint32_t)m;
+                tk[(b >> 5) + 1] = (uint32_t)(m >> 32);
             }
-            acc |= 1u << (p & 31);
-            p = step(p);
         }
-        if (s0 < s1) bm[cw] = acc;
+    }
+    __syncthreads();
+    auto take_at = [&](uint32_t x) { return (tk[x >> 5] >> (x & 31)) & 1u; };
+    auto step = [&](uint32_t x) -> uint32_t {
+        return take_at(x) ? x + zstd::match_len(in, n, x, sc.best[x]) : x + 1;
+    };
+    // speculative walk of this thread's segment: a run of literals is skipped to the next
+    // take position through the bitmap, marked whole words at a time
+    uint32_t p = s0;
+    while (p < s1) {
+        uint32_t w = p >> 5, t = tk[w] & (~0u << (p & 31));
+        while (!t && 32 * (w + 1) < s1) t = tk[++w];
+        const uint32_t nt = t ? min(s1, 32 * w + (uint32_t)__builtin_ctz(t)) : s1;  // literals [p, nt)
+        for (uint32_t x = p; x < nt;) {
+            const uint32_t xe = min(nt, (x | 31) + 1);
+            bm[x >> 5] |= (xe - x == 32 ? ~0u : ((1u << (xe - x)) - 1u)) << (x & 31);
+            x = xe;
+        }
+        p = nt;
+        if (p >= s1) break;
+        bm[p >> 5] |= 1u << (p & 31);
+        p += zstd::match_len(in, n, p, sc.best[p]);
     }
     L.part[tid] = s0 < n ? p : s0;  // the segment's exit
     __syncthreads();
