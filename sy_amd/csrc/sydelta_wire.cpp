@@ -776,13 +776,23 @@ extern "C" int sydelta_zstd_compress_device(int device, const uint8_t* d_in, uin
     uint64_t kBatch = 4096;
     if (const char* e = getenv("SYDELTA_ZSTD_BATCH"))
         if (const uint64_t v = strtoull(e, nullptr, 10)) kBatch = std::min<uint64_t>(v, 1 << 20);
-    const uint64_t nb_max = std::min<uint64_t>(nblocks, kBatch);
     auto al = [](uint64_t b) { return (b + 255) & ~(uint64_t)255; };
-    const uint64_t o_lz = al(nb_max * zstd::kBlockMax), o_size = o_lz + al(nb_max * zstd::kSeqScratchBytes);
-    const uint64_t o_type = o_size + al(4 * nb_max);
-    const uint64_t o_len = o_type + al(4 * nb_max), o_off = o_len + al(8 * nb_max), total = o_off + al(8 * nb_max);
+    uint64_t nb_max, o_lz, o_size, o_type, o_len, o_off, total;
     DevBuf_wire buf;
-    HIP_TRY(dev_malloc_async(&buf.p, total, s));
+    for (;;) {  // a device short of memory gets smaller batches (down to 64 blocks)
+        nb_max = std::min<uint64_t>(nblocks, kBatch);
+        o_lz = al(nb_max * zstd::kBlockMax);
+        o_size = o_lz + al(nb_max * zstd::kSeqScratchBytes);
+        o_type = o_size + al(4 * nb_max);
+        o_len = o_type + al(4 * nb_max);
+        o_off = o_len + al(8 * nb_max);
+        total = o_off + al(8 * nb_max);
+        const hipError_t e = dev_malloc_async(&buf.p, total, s);
+        if (e == hipSuccess) break;
+        if (e != hipErrorOutOfMemory || kBatch <= 64) HIP_TRY(e);
+        (void)hipGetLastError();
+        kBatch /= 2;
+    }
     buf.s = s;
     uint8_t* B = (uint8_t*)buf.p;
     uint8_t* d_lz = B + o_lz;

@@ -186,14 +186,15 @@ def main():
 def zstd_checks():
     """sydelta_zstd_compress_device's batching and frame assembly (the emulated blocks are
     sydelta_zstd.hpp's sequential form): frames equal to the test reference encoder's and
-    decoded by the system libzstd, with batches of 1, 3 and 512 blocks."""
+    decoded by the system libzstd, with batches of 1, 3 and 512 blocks, and the default
+    batch halved on a device that refuses its scratch."""
     import ctypes
     import json
     import random
 
     sys.path.insert(0, os.path.join(ROOT, "tests"))
     import test_zstd as Z
-    from sy_amd._lib import check, lib
+    from sy_amd._lib import SYDELTA_E_OOM, check, lib
 
     if Z._libzstd() is None:
         return 0
@@ -215,6 +216,32 @@ def zstd_checks():
             assert Z.zstd_decode(frame, len(t)) == t
             n += 1
     os.environ.pop("SYDELTA_ZSTD_BATCH", None)
+    # a device short of memory: the default batch's scratch is refused, the call halves the
+    # batch until it fits (here 128 of the 201 blocks) and writes the same frame
+    t = (Z.delta_json(rng, 30000, 0.3) * 5)[: 200 * 131072 + 777]
+    src = np.zeros(len(t) + 16, np.uint8)
+    src[:len(t)] = np.frombuffer(t, np.uint8)
+    cap = int(lib.sydelta_zstd_bound(len(t)))
+    out = np.zeros(cap, np.uint8)
+    got = ctypes.c_uint64()
+    os.environ["SYDELTA_EMU_POOL_CAP"] = str(200 << 20)  # < 201 blocks' scratch (~1.5 MiB each), > 128 blocks'
+    try:
+        check(lib.sydelta_zstd_compress_device(0, ctypes.c_void_p(src.ctypes.data), len(t),
+                                               ctypes.c_void_p(out.ctypes.data), cap, ctypes.byref(got), None))
+    finally:
+        os.environ.pop("SYDELTA_EMU_POOL_CAP", None)
+    frame = out[:got.value].tobytes()
+    assert frame == Z.ref_compress(t), ("zstd", "oom fallback", len(t))
+    assert Z.zstd_decode(frame, len(t)) == t
+    # the cap is real: below 64 blocks' scratch the call reports the device as full
+    os.environ["SYDELTA_EMU_POOL_CAP"] = str(50 << 20)
+    try:
+        rc = lib.sydelta_zstd_compress_device(0, ctypes.c_void_p(src.ctypes.data), len(t),
+                                              ctypes.c_void_p(out.ctypes.data), cap, ctypes.byref(got), None)
+    finally:
+        os.environ.pop("SYDELTA_EMU_POOL_CAP", None)
+    assert rc == SYDELTA_E_OOM, rc
+    n += 2
     return n
 
 

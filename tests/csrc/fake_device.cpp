@@ -146,6 +146,9 @@ hipError_t hipMemPoolCreate(hipMemPool_t* p, const hipMemPoolProps* props) {
 }
 hipError_t hipMallocFromPoolAsync(void** p, size_t n, hipMemPool_t pool, hipStream_t s) {
     if (pool != (hipMemPool_t)&emu_pool_tag) return hipErrorInvalidValue;
+    // SYDELTA_EMU_POOL_CAP: pool allocations above that many bytes fail as on a full device
+    if (const char* e = getenv("SYDELTA_EMU_POOL_CAP"))
+        if (n > strtoull(e, nullptr, 10)) return hipErrorOutOfMemory;
     return hipMallocAsync(p, n, s);
 }
 hipError_t hipFreeAsync(void* p, hipStream_t) {
