@@ -3280,9 +3280,10 @@ __device__ __forceinline__ uint32_t z_seq_bits(ZLds& L, const zstd::SeqScratch& 
 // from the entry, clearing the speculative marks it jumps over, until it steps on a marked
 // position (the two walks agree from there on).  The marked positions are the literals
 // and the sequence starts: counted per thread, ranked, gathered (literals into sc.lit,
-// starts into sc.seq).  Wave 0 then runs the repeat history over the sequences in order
-// (zstd::seq_dist compared by the whole wave, rep_code), thread 0 codes them
-// (seq_section) after the literals section (z_lit_section).  Returns its size, 0 when
+// starts into sc.seq).  Wave 0 then resolves the repeat history (zstd::seq_dist,
+// rep_code) 64 sequences at a time by a wave scan, the literals section follows
+// (z_lit_section), then the sequences section: its header by thread 0
+// (seq_section_head), its bitstream in parallel (z_seq_bits).  Returns its size, 0 when
 // the block has no sequence (every thread).
 __device__ __forceinline__ uint32_t z_lz_content(ZLds& L, const uint8_t* __restrict__ in, uint32_t n, const zstd::SeqScratch& sc,
                                  uint32_t timing, uint64_t& tph) {
