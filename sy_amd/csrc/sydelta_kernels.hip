@@ -2881,8 +2881,7 @@ struct ZLds {
     uint32_t cand[zstd::kCands];
     uint32_t ssize[4];
     uint32_t state[8];  // [0] type, [1] write offset, [2] abort, [3] entropy-only size, [4] nc, [5] nbest, [6] lz size
-    uint32_t rank[2][kZT];  // the parallel parse: per thread literals / sequences, then their exclusive scans
-    uint32_t pstate[12];    // [0] literals, [1] sequences, [2] literals section size, [3] raw, [4] write offset,
+    uint32_t pstate[12];    // [2] literals section size, [3] raw, [4] write offset,
                             // [5] sequences header size, [8..10] the final FSE states (OF, ML, LL)
     uint32_t ccnt[36 + 53 + 32];  // the sequences' LL / ML / OF code counts
 };
@@ -3111,23 +3110,6 @@ __device__ __forceinline__ uint32_t z_lit_section(ZLds& L, const uint8_t* __rest
     }
     __syncthreads();
     return o;
-}
-
-// Block-wide exclusive scan of v[0..kZT) in place (LDS); the total is returned to every
-// thread through *tot (LDS).
-__device__ uint32_t z_scan(uint32_t* v, uint32_t* tot) {
-    __syncthreads();
-    if (threadIdx.x == 0) {
-        uint32_t sum = 0;
-        for (uint32_t t = 0; t < kZT; ++t) {
-            const uint32_t x = v[t];
-            v[t] = sum;
-            sum += x;
-        }
-        *tot = sum;
-    }
-    __syncthreads();
-    return *tot;
 }
 
 // The sequences' bitstream of zstd::seq_section_counted (after its header), in parallel:
@@ -3378,15 +3360,14 @@ __device__ __forceinline__ uint32_t z_lz_content(ZLds& L, const uint8_t* __restr
         nlit += __builtin_popcount(lit);
         nseq += __builtin_popcount(m & ~lit);
     }
-    L.rank[0][tid] = nlit;
-    L.rank[1][tid] = nseq;
-    const uint32_t nl = z_scan(L.rank[0], &L.pstate[0]);
-    const uint32_t ns = z_scan(L.rank[1], &L.pstate[1]);
+    uint32_t nl, ns;  // block totals; a thread's ranks are what the earlier threads hold
+    const uint32_t lat = z_suffix(L, nlit, nl), sat = z_suffix(L, nseq, ns);
+    const uint32_t lrank = nl - lat - nlit, srank = ns - sat - nseq;
     if (ns == 0) return 0;  // uniform
     // gather: literals into sc.lit (the word's 32 text bytes loaded once), sequence starts
     // into sc.seq as {p, length, -, -}
     {
-        uint32_t lr = L.rank[0][tid], sr = L.rank[1][tid];
+        uint32_t lr = lrank, sr = srank;
         for (uint32_t w = s0 >> 5; 32 * w < s1; ++w) {
             const uint32_t m = bm[w];
             if (!m) continue;
