@@ -608,13 +608,105 @@ def roofline(prof: dict, steps: int, algo_step: dict, positions=None, keys=None,
     return roof
 
 
+def _free_port() -> int:
+    import socket
+
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def visible_gpus() -> int:
+    """Devices this process may use, counted without initialising the GPU (on this image
+    torch.cuda.device_count() does not start the HIP runtime).  SYDELTA_BENCH_FAKE_GPUS
+    overrides it for the launcher's CPU tests."""
+    fake = os.environ.get("SYDELTA_BENCH_FAKE_GPUS")
+    if fake is not None:
+        return int(fake)
+    import torch
+
+    return torch.cuda.device_count()
+
+
+def launch_ranks(nranks: int, argv) -> int:
+    """`bench.py --gpus N` without a launcher: start N child processes of this script, one
+    per GPU, each with RANK / LOCAL_RANK / WORLD_SIZE / MASTER_ADDR / MASTER_PORT (the
+    torchrun contract) and SYDELTA_HOST_THREADS = max(2, host cores // N) so the ranks'
+    host pools do not oversubscribe the host (sy's transfers share one host too,
+    sync/mod.rs:673-697).  Nothing here touches the GPU and nothing execs: the children
+    are ordinary subprocesses.  Rank 0's stdout (the JSON line) is forwarded to ours,
+    the other ranks' stdout to our stderr.  The first rank to fail ends the job: the
+    others are terminated (they would wait in a collective) and its exit code is ours."""
+    import subprocess
+    import threading
+
+    have = visible_gpus()
+    if have < nranks:
+        print(f"bench.py: --gpus {nranks} asks for {nranks} ranks but {have} GPU(s) are visible", file=sys.stderr)
+        return 2
+    cores = host_cores()[0]
+    port = os.environ.get("MASTER_PORT") or str(_free_port())
+    procs = []
+    for r in range(nranks):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(nranks),
+                   LOCAL_WORLD_SIZE=str(nranks), MASTER_ADDR=os.environ.get("MASTER_ADDR", "127.0.0.1"),
+                   MASTER_PORT=port)
+        env.setdefault("SYDELTA_HOST_THREADS", str(max(2, cores // nranks)))
+        procs.append(subprocess.Popen([sys.executable, "-u", os.path.abspath(__file__)] + list(argv), env=env,
+                                      stdout=subprocess.PIPE, text=True, bufsize=1))
+
+    def pump(p, out):
+        for ln in p.stdout:
+            out.write(ln)
+            out.flush()
+
+    pumps = [threading.Thread(target=pump, args=(p, sys.stdout if r == 0 else sys.stderr), daemon=True)
+             for r, p in enumerate(procs)]
+    for t in pumps:
+        t.start()
+    rc = 0
+    live = set(range(nranks))
+    while live:
+        for r in sorted(live):
+            code = procs[r].poll()
+            if code is None:
+                continue
+            live.discard(r)
+            if code != 0 and rc == 0:
+                rc = code if code > 0 else 128 - code
+                print(f"bench.py: rank {r} exited with {code}; stopping the other ranks", file=sys.stderr)
+                for q in live:
+                    procs[q].terminate()
+        time.sleep(0.05)
+    for p in procs:  # every child has exited; collect and close the pipes
+        p.wait()
+    for t in pumps:
+        t.join(timeout=5)
+    return rc
+
+
 def main():
     args = parse()
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(launch_ranks(args.gpus, sys.argv[1:]))
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    if os.environ.get("SYDELTA_BENCH_STUB"):
+        # launcher test hook (tests/test_bench_launch.py): report the rank environment, no GPU
+        print(json.dumps({k: os.environ.get(k) for k in ("RANK", "LOCAL_RANK", "WORLD_SIZE", "MASTER_ADDR",
+                                                       "MASTER_PORT", "SYDELTA_HOST_THREADS")}), flush=True)
+        fail = os.environ.get("SYDELTA_BENCH_STUB_FAIL_RANK")
+        if fail is not None:
+            if int(fail) == int(os.environ.get("RANK", "0")):
+                time.sleep(0.5)
+                sys.exit(7)
+            time.sleep(60)  # the other ranks would wait in a collective for the failed one
+        return
+    if args.gpus != world:
+        print(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world}; n_gpus reports WORLD_SIZE", file=sys.stderr)
     import numpy as np
     import torch
     import torch.distributed as dist
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     torch.cuda.set_device(local)
