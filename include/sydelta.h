@@ -18,6 +18,14 @@
  *  - Re-entrant: callers are tokio spawn_blocking threads (ssh.rs:913), up to
  *    --parallel (default 10) at once (sync/mod.rs:673).  Device init is
  *    call_once per device; every call uses its own stream and buffers.
+ *  - Devices: every entry point leaves the calling thread's current HIP device
+ *    as it found it (hipGetDevice before == after), whichever devices it worked
+ *    on (`device` arguments, an index's device, the path-level binding below,
+ *    sydelta_trim's and sydelta_delta_multi_device's device switches), on success
+ *    and on every error return.
+ *  - Scratch kept between calls (per thread and device: scan / probe / walk
+ *    buffers and pinned host buffers) is released when the thread exits and by
+ *    sydelta_trim, which frees it for every thread not inside a call.
  *  - Data layout in HBM: byte buffers as given; signatures as SoA
  *    (weak u32[n], strong u64[n]).  Device buffers passed in must be readable
  *    up to the end of the 16-byte granule holding their last byte (true for
@@ -107,8 +115,10 @@ int sydelta_set_thread_device(int device);
 /* The device the calling thread's path-level calls use (bound now if it was not). */
 int sydelta_thread_device(int *device);
 /* Release memory the library keeps between calls for reuse: index allocations held per
- * device (made on library streams) and the calling thread's scan buffers (device and
- * pinned host memory).  Other threads' buffers stay with them. */
+ * device (made on library streams), the recycled op arrays, and the scan / probe / walk
+ * buffers (device and pinned host memory) of the calling thread and of every other thread
+ * that is not inside a call (a thread inside a call keeps its own until it exits or a
+ * later trim). */
 void sydelta_trim(void);
 
 /* mod.rs:20-23 `calculate_block_size(file_size) -> usize`: sqrt clamped to 512..=131072. */

@@ -309,8 +309,9 @@ std::mutex& bind_mu() {
     static std::mutex* m = new std::mutex();  // never destroyed: thread exits may come after static teardown
     return *m;
 }
-std::vector<int> g_allowed;  // under bind_mu; empty: every visible device
-std::map<int, int> g_bound;  // under bind_mu; device -> bound threads
+// heap-allocated and never destroyed, like bind_mu: a bound thread may exit after static teardown
+std::vector<int>& g_allowed = *new std::vector<int>();  // under bind_mu; empty: every visible device
+std::map<int, int>& g_bound = *new std::map<int, int>();  // under bind_mu; device -> bound threads
 unsigned g_rr = 0;           // under bind_mu
 struct ThreadBinding {
     int dev = -1;
@@ -404,7 +405,7 @@ extern "C" int sydelta_signature_device(int device, const uint8_t* d_buf, uint64
                                         uint32_t* d_weak, uint64_t* d_strong, void* stream) try {
     if (block_size == 0) return fail(SYDELTA_E_INVAL, "block_size must be > 0");
     if (len && (!d_buf || !d_weak || !d_strong)) return fail(SYDELTA_E_INVAL, "NULL device pointer");
-    if (int r = ensure_device(device)) return r;
+    SYDELTA_ENTER_DEVICE(device);
     hipStream_t s = stream ? (hipStream_t)stream : thread_stream(device < 0 ? 0 : device);
     CallProf cp;
     HIP_TRY(launch_signature(d_buf, len, block_size, d_weak, d_strong, s, cp.get()));
@@ -419,7 +420,7 @@ extern "C" int sydelta_signature_batch_device(int device, const uint8_t* d_buf, 
                                               uint32_t* d_weak, uint64_t* d_strong, void* stream) try {
     if (block_size == 0) return fail(SYDELTA_E_INVAL, "block_size must be > 0");
     if (nfiles && (!off || !len)) return fail(SYDELTA_E_INVAL, "NULL segment table");
-    if (int r = ensure_device(device)) return r;
+    SYDELTA_ENTER_DEVICE(device);
     hipStream_t s = stream ? (hipStream_t)stream : thread_stream(device < 0 ? 0 : device);
     std::vector<uint64_t> fblk(nfiles + 1, 0);
     for (uint64_t f = 0; f < nfiles; ++f) fblk[f + 1] = fblk[f] + (len[f] + block_size - 1) / block_size;
@@ -581,37 +582,118 @@ static void* take_kept_pool(int device, size_t bytes, hipStream_t s, size_t* got
 
 // Per-thread scratch of the scan (Classifier::scan): the verified-hit buffers on each
 // device and the pinned host buffer the sorted hits come back into.
+// A thread's scratch is released by sydelta_trim (the calling thread's, and every other
+// thread's that is not inside a call: the owner holds `mu` while it uses the buffers) and
+// when the thread exits (sy's spawn_blocking threads come and go; the host pool's
+// workers classify chunks of sydelta_delta_multi_device).  The main thread's is left to
+// the process exit (the HIP runtime may be tearing down by then).
 namespace sydelta {
 namespace {
-std::mutex g_scratch_mu;
 struct ThreadScratch {
+    std::recursive_mutex mu;  // held by the owning thread while a call uses the buffers
     std::map<int, HitScratch> hits;  // per device
     std::map<int, DevScratch> scan;  // per device: launch_scan's scratch
     std::map<int, DevScratch> probe;  // per device: the aligned probe's jobs and results
-    PinnedHits pinned;
+    std::map<int, DevScratch> walk;   // per device: k_walk_files' table and records
+    PinnedHits pinned;     // sorted hits / the file walk's table, counts and records
+    PinnedHits seg_pin;    // Classifier::scan's segment table
+    PinnedHits probe_pin;  // Classifier::probe's results
+    PinnedHits phase_pin;  // Classifier::phase_probe's results
 };
-std::vector<ThreadScratch*> g_scratch;  // every thread's (never destroyed), for sydelta_trim
+std::mutex& scratch_mu() {
+    static std::mutex* m = new std::mutex();  // never destroyed (thread exits after static teardown)
+    return *m;
+}
+std::vector<ThreadScratch*>& all_scratch() {  // under scratch_mu: every live thread's
+    static std::vector<ThreadScratch*>* v = new std::vector<ThreadScratch*>();
+    return *v;
+}
+const std::thread::id g_main_thread = std::this_thread::get_id();  // the thread that loaded the library
+
+// Free t's buffers (t.mu held, t's owner outside any call: its last call synchronized the
+// streams it used, so the buffers are idle).  Device memory goes back to the library's
+// pool in the legacy stream's order.
+void release_scratch(ThreadScratch& t) {
+    DeviceScope keep_device;
+    std::set<int> devs;
+    auto dev_free = [&](int d, void* p) {
+        if (p && hipSetDevice(d) == hipSuccess) {
+            (void)hipFreeAsync(p, nullptr);
+            devs.insert(d);
+        }
+    };
+    for (auto& kv : t.hits) dev_free(kv.first, kv.second.p);
+    t.hits.clear();
+    for (auto* m : {&t.scan, &t.probe, &t.walk}) {
+        for (auto& kv : *m) dev_free(kv.first, kv.second.p);
+        m->clear();
+    }
+    for (int d : devs)
+        if (hipSetDevice(d) == hipSuccess) (void)hipStreamSynchronize(nullptr);
+    for (PinnedHits* h : {&t.pinned, &t.seg_pin, &t.probe_pin, &t.phase_pin}) {
+        if (h->p) (void)hipHostFree(h->p);
+        *h = PinnedHits();
+    }
+}
+
+struct ScratchOwner {  // thread_local: the thread's scratch, released at its exit
+    ThreadScratch* t = nullptr;
+    ~ScratchOwner() {
+        if (!t) return;
+        {
+            std::lock_guard<std::mutex> lk(scratch_mu());
+            auto& v = all_scratch();
+            v.erase(std::remove(v.begin(), v.end(), t), v.end());
+        }
+        if (std::this_thread::get_id() == g_main_thread) return;  // process exit: left to the OS
+        {
+            std::lock_guard<std::recursive_mutex> h(t->mu);
+            release_scratch(*t);
+        }
+        delete t;
+    }
+};
 ThreadScratch& thread_scratch() {
-    static thread_local ThreadScratch* t = [] {
-        ThreadScratch* x = new ThreadScratch();
-        std::lock_guard<std::mutex> lk(g_scratch_mu);
-        g_scratch.push_back(x);
-        return x;
-    }();
-    return *t;
+    static thread_local ScratchOwner own;
+    if (!own.t) {
+        own.t = new ThreadScratch();
+        std::lock_guard<std::mutex> lk(scratch_mu());
+        all_scratch().push_back(own.t);
+    }
+    return *own.t;
 }
 }  // namespace
 HitScratch& thread_hit_scratch(int device) { return thread_scratch().hits[device]; }
 DevScratch& thread_scan_scratch(int device) { return thread_scratch().scan[device]; }
 DevScratch& thread_probe_scratch(int device) { return thread_scratch().probe[device]; }
+DevScratch& thread_walk_scratch(int device) { return thread_scratch().walk[device]; }
 PinnedHits& thread_pinned_hits() { return thread_scratch().pinned; }
+ScratchHold::ScratchHold() : mu(&thread_scratch().mu) { mu->lock(); }
+ScratchHold::~ScratchHold() { mu->unlock(); }
 }  // namespace sydelta
+
+namespace {
+PinnedHits& thread_seg_pin() { return thread_scratch().seg_pin; }
+PinnedHits& thread_probe_pin() { return thread_scratch().probe_pin; }
+PinnedHits& thread_phase_pin() { return thread_scratch().phase_pin; }
+// a pinned host buffer of at least `bytes` (grown by a quarter; the previous call on this
+// thread synchronized the streams that used it)
+int pinned_at_least(PinnedHits& h, size_t bytes) {
+    if (h.bytes >= bytes) return SYDELTA_OK;
+    if (h.p) (void)hipHostFree(h.p);
+    h = PinnedHits();
+    HIP_TRY(hipHostMalloc((void**)&h.p, bytes + bytes / 4, hipHostMallocDefault));
+    h.bytes = bytes + bytes / 4;
+    return SYDELTA_OK;
+}
+}  // namespace
 
 namespace {
 void release_small_ops();  // the recycled per-file op arrays (below)
 }
 
 extern "C" void sydelta_trim(void) {
+    DeviceScope keep_device;  // the frees below switch devices
     release_small_ops();
     // kept index allocations of every device, released in their (library) streams' order
     KeptPool kept[64];
@@ -624,28 +706,18 @@ extern "C" void sydelta_trim(void) {
     }
     for (int d = 0; d < 64; ++d)
         if (kept[d].p && hipSetDevice(d) == hipSuccess) (void)hipFreeAsync(kept[d].p, kept[d].s);
-    // the calling thread's scan scratch (other threads' stay with them: they may be in a call)
-    ThreadScratch& t = thread_scratch();
-    for (auto& kv : t.hits)
-        if (kv.second.p && hipSetDevice(kv.first) == hipSuccess) {
-            (void)hipFreeAsync(kv.second.p, thread_stream(kv.first));
-            (void)hipStreamSynchronize(thread_stream(kv.first));
-        }
-    t.hits.clear();
-    for (auto* m : {&t.scan, &t.probe}) {
-        for (auto& kv : *m)
-            if (kv.second.p && hipSetDevice(kv.first) == hipSuccess) {
-                (void)hipFreeAsync(kv.second.p, thread_stream(kv.first));
-                (void)hipStreamSynchronize(thread_stream(kv.first));
-            }
-        m->clear();
+    // the scan / probe / walk scratch of this thread and of every thread not inside a call
+    (void)thread_scratch();  // registers this thread's
+    std::lock_guard<std::mutex> lk(scratch_mu());
+    for (ThreadScratch* t : all_scratch()) {
+        std::unique_lock<std::recursive_mutex> h(t->mu, std::try_to_lock);
+        if (h.owns_lock()) release_scratch(*t);
     }
-    if (t.pinned.p) (void)hipHostFree(t.pinned.p);
-    t.pinned = PinnedHits();
 }
 
 extern "C" void sydelta_index_free(sydelta_index* idx) {
     if (!idx) return;
+    DeviceScope keep_device;
     static const bool host_timing = getenv("SYDELTA_HOST_TIMING") != nullptr;
     const auto t0 = std::chrono::steady_clock::now();
     (void)hipSetDevice(idx->device);
@@ -673,7 +745,7 @@ static int index_create_impl(int device, const uint32_t* weak, const uint64_t* s
     const uint64_t nblocks = fblk[nfiles];
     if (nblocks && (!weak || !strong)) return fail(SYDELTA_E_INVAL, "NULL signature arrays");
     if (nblocks >= 0xFFFFFFFFull) return fail(SYDELTA_E_INVAL, "too many blocks (%llu)", (unsigned long long)nblocks);
-    if (int r = ensure_device(device)) return r;
+    SYDELTA_ENTER_DEVICE(device);
     if (device < 0) device = 0;
     hipStream_t s = stream ? (hipStream_t)stream : thread_stream(device);
     std::unique_ptr<sydelta_index, void (*)(sydelta_index*)> x(new sydelta_index(), index_release);
@@ -1151,11 +1223,8 @@ int Classifier::probe(int mode) {
     for (auto& c : src) fast = fast && ((uintptr_t)(base + c.off) & 15) == 0;
     // results land in pinned host memory (per thread, grown on demand): no zero fill and
     // no staging copy for the D2H of one u32 per probed window
-    struct PinnedU32 {
-        uint32_t* p = nullptr;
-        size_t cap = 0;
-    };
-    static thread_local PinnedU32 pin;  // never freed, like the per-thread streams
+    ScratchHold hold;
+    PinnedHits& pin = thread_probe_pin();
     uint32_t* out = nullptr;
     uint64_t nout = 0;
     auto run = [&](uint32_t stride, std::vector<uint64_t>& pfx) -> int {
@@ -1172,14 +1241,8 @@ int Classifier::probe(int mode) {
         pfx[src.size()] = np;
         nout = np;
         if (!np) return SYDELTA_OK;
-        if (np > pin.cap) {
-            if (pin.p) (void)hipHostFree(pin.p);
-            pin.p = nullptr;
-            pin.cap = 0;
-            HIP_TRY(hipHostMalloc((void**)&pin.p, np * 5 / 4 * 4, hipHostMallocDefault));
-            pin.cap = np * 5 / 4;
-        }
-        out = pin.p;
+        if (int r = pinned_at_least(pin, np * 4)) return r;
+        out = (uint32_t*)pin.p;
         // the full pass's results stay on the device for the device walk (walk_device)
         DevBuf local;
         DevBuf& jb = stride == 1 ? probe_buf : local;
@@ -1324,6 +1387,7 @@ static hipError_t scan_index(sydelta_index* x, uint64_t tot_pos, hipStream_t s, 
 }
 
 int Classifier::scan(const std::vector<std::array<uint64_t, 3>>& ranges) {
+    ScratchHold hold;
     static const bool host_timing = getenv("SYDELTA_HOST_TIMING") != nullptr;
     const auto t0 = std::chrono::steady_clock::now();
     double t_kern = 0, t_d2h = 0;
@@ -1374,17 +1438,12 @@ int Classifier::scan(const std::vector<std::array<uint64_t, 3>>& ranges) {
         // through the thread's pinned staging buffer: a pageable H2D of C4's 68 K segments
         // (2.7 MB) is a staged, host-blocking copy.  The previous call on this thread
         // synchronized its stream, so the buffer is free.
-        static thread_local std::pair<void*, size_t> seg_pin{nullptr, 0};  // never freed, like the streams
+        PinnedHits& seg_pin = thread_seg_pin();
         const size_t sbytes = segs.size() * sizeof(ScanSeg);
         if (sbytes > (64u << 10)) {
-            if (seg_pin.second < sbytes) {
-                if (seg_pin.first) (void)hipHostFree(seg_pin.first);
-                seg_pin = {nullptr, 0};
-                HIP_TRY(hipHostMalloc(&seg_pin.first, sbytes + sbytes / 4, hipHostMallocDefault));
-                seg_pin.second = sbytes + sbytes / 4;
-            }
-            memcpy(seg_pin.first, segs.data(), sbytes);
-            HIP_TRY(hipMemcpyAsync(seg_buf.p, seg_pin.first, sbytes, hipMemcpyHostToDevice, s));
+            if (int r = pinned_at_least(seg_pin, sbytes)) return r;
+            memcpy(seg_pin.p, segs.data(), sbytes);
+            HIP_TRY(hipMemcpyAsync(seg_buf.p, seg_pin.p, sbytes, hipMemcpyHostToDevice, s));
         } else {
             HIP_TRY(hipMemcpyAsync(seg_buf.p, segs.data(), sbytes, hipMemcpyHostToDevice, s));
         }
@@ -1654,6 +1713,7 @@ int Classifier::classify(int mode) {
 int Classifier::phase_probe(const std::vector<std::array<uint64_t, 4>>& jobs,
                             std::vector<std::array<uint64_t, 3>>& missed) {
     if (jobs.empty()) return SYDELTA_OK;
+    ScratchHold hold;
     std::vector<ProbeJob> pj;
     pj.reserve(jobs.size());
     uint64_t np = 0;
@@ -1677,15 +1737,10 @@ int Classifier::phase_probe(const std::vector<std::array<uint64_t, 4>>& jobs,
                          d_pst, d_out, s, prof));
     // results into the thread's pinned buffer (a pageable D2H of C4's ~1.3 M results is a
     // staged copy); the previous call on this thread synchronized its stream
-    static thread_local std::pair<uint32_t*, size_t> pin{nullptr, 0};  // never freed, like the streams
-    if (pin.second < np) {
-        if (pin.first) (void)hipHostFree(pin.first);
-        pin = {nullptr, 0};
-        HIP_TRY(hipHostMalloc((void**)&pin.first, (np + np / 4) * 4, hipHostMallocDefault));
-        pin.second = np + np / 4;
-    }
-    const uint32_t* out = pin.first;
-    HIP_TRY(hipMemcpyAsync(pin.first, d_out, np * 4, hipMemcpyDeviceToHost, s));
+    PinnedHits& pin = thread_phase_pin();
+    if (int r = pinned_at_least(pin, np * 4)) return r;
+    const uint32_t* out = (const uint32_t*)pin.p;
+    HIP_TRY(hipMemcpyAsync(pin.p, d_out, np * 4, hipMemcpyDeviceToHost, s));
     HIP_TRY(hipStreamSynchronize(s));
     // each source's phase arrays sized once, then the jobs filled on the host pool (jobs of
     // one source cover disjoint blocks), each job's missed blocks in its own list, joined
@@ -2019,10 +2074,193 @@ int tail_flags(Classifier& C, const std::vector<size_t>& which, std::vector<int>
 
 void sydelta::finish_stats(sydelta_delta* d) { finish_stats_impl(d); }
 
+// K10 (k_walk_files): the whole walk of every file on the device, for batches of small
+// files (SYDELTA_FILE_WALK=0 turns it off; =1 takes it for any batch it can serve).
+namespace {
+int file_walk_mode() {
+    const char* e = getenv("SYDELTA_FILE_WALK");
+    return (e && e[0] == '0') ? 0 : (e && e[0] == '1') ? 1 : -1;
+}
+bool file_walk_ok(const sydelta_index* ix, const uint64_t* src_off, const uint64_t* src_len, const uint8_t* d_buf) {
+    const int mode = file_walk_mode();
+    if (mode == 0) return false;
+    const uint64_t n = ix->bs, nf = ix->nfiles;
+    if (ix->ix.l1 || n % 64 != 0 || n < 256 || n > kWalkMaxN || ix->ix.max_fwords > kWalkMaxWords || nf >= (1u << 31))
+        return false;
+    // one workgroup walks a file: many files, none large (auto mode)
+    if (mode < 0 && nf < 64) return false;
+    uint64_t recs = 0;
+    for (uint64_t f = 0; f < nf; ++f) {
+        if (src_len[f] >= (1ull << 32) || (mode < 0 && src_len[f] > (64ull << 20))) return false;
+        if (src_len[f] && (!d_buf || ((uintptr_t)(d_buf + src_off[f]) & 15) != 0)) return false;
+        recs += 2 * (src_len[f] / n) + 4;
+    }
+    return recs < (1ull << 32);
+}
+}  // namespace
+
+// The batched match with the walk on the device: one launch, the file table up, the
+// run-length coded ops down (two D2H: the per-file counts, then the records), expanded
+// into the files' op arrays on the host pool.
+static int match_walk_files(sydelta_index* ix, const uint8_t* d_buf, const uint64_t* src_off, const uint64_t* src_len,
+                            hipStream_t s, Profiler* prof, sydelta_delta_batch* b) {
+    ScratchHold hold;
+    static const bool host_timing = getenv("SYDELTA_HOST_TIMING") != nullptr;
+    const auto t0 = std::chrono::steady_clock::now();
+    const uint64_t n = ix->bs, nf = ix->nfiles;
+    int cur_dev = 0;
+    HIP_TRY(hipGetDevice(&cur_dev));
+    // table: soff | slen | rec_off | last_size (u64 each), then the device outputs
+    PinnedHits& ph = thread_pinned_hits();
+    const size_t tbytes = 32 * nf;
+    const size_t fout_bytes = sizeof(WalkFileOut) * nf;
+    if (ph.bytes < std::max(tbytes, fout_bytes + 16)) {
+        if (ph.p) (void)hipHostFree(ph.p);
+        ph = PinnedHits();
+        const size_t want = std::max(tbytes, fout_bytes + 16) * 5 / 4 + (1 << 20);
+        HIP_TRY(hipHostMalloc((void**)&ph.p, want, hipHostMallocDefault));
+        ph.bytes = want;
+    }
+    uint64_t* T = (uint64_t*)ph.p;
+    uint64_t rec_total = 0;
+    for (uint64_t f = 0; f < nf; ++f) {
+        T[f] = src_off[f];
+        T[nf + f] = src_len[f];
+        T[2 * nf + f] = rec_total;
+        T[3 * nf + f] = ix->last_size[f];
+        rec_total += 2 * (src_len[f] / n) + 4;
+    }
+    auto al = [](size_t v) { return (v + 255) & ~(size_t)255; };
+    const size_t o_tab = 0, o_fout = o_tab + al(tbytes), o_total = o_fout + al(fout_bytes), o_stage = o_total + 256;
+    const size_t o_out = o_stage + al(sizeof(WalkRec) * rec_total), need = o_out + al(sizeof(WalkRec) * rec_total);
+    DevScratch& sc = thread_walk_scratch(cur_dev);
+    if (sc.bytes < need) {
+        if (sc.p) (void)hipFreeAsync(sc.p, s);
+        sc = DevScratch();
+        HIP_TRY(dev_malloc_async(&sc.p, need + need / 4, s));
+        sc.bytes = need + need / 4;
+    }
+    uint8_t* D = (uint8_t*)sc.p;
+    HIP_TRY(hipMemcpyAsync(D + o_tab, T, tbytes, hipMemcpyHostToDevice, s));
+    HIP_TRY(hipMemsetAsync(D + o_total, 0, 8, s));
+    WalkArgs a{};
+    a.base = d_buf;
+    a.soff = (const uint64_t*)(D + o_tab);
+    a.slen = a.soff + nf;
+    a.rec_off = a.soff + 2 * nf;
+    a.last_size = a.soff + 3 * nf;
+    a.nfiles = (uint32_t)nf;
+    a.n = (uint32_t)n;
+    a.nm = (uint32_t)(n % 65521);
+    a.fw_max = std::max<uint32_t>(4, ix->ix.max_fwords);
+    a.files = ix->ix.d_files;
+    a.fblk = ix->ix.d_fblk;
+    a.filt = ix->ix.filt;
+    a.keys = ix->ix.keys;
+    a.start = ix->ix.start;
+    a.cnt = ix->ix.cnt;
+    a.order = ix->ix.order;
+    a.cstrong = ix->ix.cstrong;
+    a.weak = ix->d_weak;
+    a.strong = ix->d_strong;
+    a.stage = (WalkRec*)(D + o_stage);
+    a.out = (WalkRec*)(D + o_out);
+    a.fout = (WalkFileOut*)(D + o_fout);
+    a.total = (unsigned long long*)(D + o_total);
+    HIP_TRY(launch_walk_files(a, s, prof));
+    // the host table in ph is dead once the upload ran: the counts come back over it
+    WalkFileOut* fo = (WalkFileOut*)ph.p;
+    uint64_t* tot = (uint64_t*)(ph.p + fout_bytes);
+    HIP_TRY(hipMemcpyAsync(fo, a.fout, fout_bytes, hipMemcpyDeviceToHost, s));
+    HIP_TRY(hipMemcpyAsync(tot, a.total, 8, hipMemcpyDeviceToHost, s));
+    HIP_TRY(hipStreamSynchronize(s));
+    const double t_kern = ms_since(t0);
+    const uint64_t nrec = *tot;
+    if (nrec > rec_total) return fail(SYDELTA_E_KERNEL, "file walk: %llu records (capacity %llu)",
+                                      (unsigned long long)nrec, (unsigned long long)rec_total);
+    // the counts out of the pinned buffer, the records into it (grown when needed)
+    const std::vector<WalkFileOut> fov(fo, fo + nf);
+    const WalkFileOut* FO = fov.data();
+    const size_t rbytes = sizeof(WalkRec) * nrec;
+    if (ph.bytes < rbytes) {
+        (void)hipHostFree(ph.p);
+        ph = PinnedHits();
+        HIP_TRY(hipHostMalloc((void**)&ph.p, rbytes * 5 / 4, hipHostMallocDefault));
+        ph.bytes = rbytes * 5 / 4;
+    }
+    const WalkRec* R = (const WalkRec*)ph.p;
+    if (nrec) {
+        HIP_TRY(hipMemcpyAsync((void*)R, a.out, rbytes, hipMemcpyDeviceToHost, s));
+        HIP_TRY(hipStreamSynchronize(s));
+    }
+    const double t_d2h = ms_since(t0);
+    // expand each file's records into its op array (recycled arrays: no page faults)
+    const int nthr = nf >= 64 ? walk_threads() : 1;
+    std::atomic<uint64_t> next{0};
+    std::vector<sydelta_match_stats> part(nthr);
+    auto worker = [&](int t) {
+        sydelta_match_stats acc{};
+        for (;;) {
+            const uint64_t f0 = next.fetch_add(64);
+            if (f0 >= nf) break;
+            for (uint64_t f = f0; f < std::min<uint64_t>(nf, f0 + 64); ++f) {
+                const WalkFileOut& o = FO[f];
+                sydelta_delta& d = b->d[f];
+                const uint64_t bb = ix->fblk[f], nbf = ix->fblk[f + 1] - bb, ls = ix->last_size[f];
+                uint64_t nops = 0;
+                for (uint32_t i = 0; i < o.count; ++i) nops += R[o.base + i].kind ? R[o.base + i].kind : 1;
+                d.ops.resize(nops);
+                sydelta_op* w = d.ops.data();
+                uint64_t nd = 0, lb = 0;
+                for (uint32_t i = 0; i < o.count; ++i) {
+                    const WalkRec& r = R[o.base + i];
+                    if (!r.kind) {
+                        *w++ = {SYDELTA_OP_DATA, 0, r.off, r.a};
+                        ++nd;
+                        lb += r.a;
+                        continue;
+                    }
+                    for (uint64_t g = r.a - bb, e = g + r.kind; g < e; ++g)
+                        *w++ = {SYDELTA_OP_COPY, 0, g * n, g + 1 == nbf ? ls : n};
+                }
+                d.stats.copy_ops = nops - nd;
+                d.stats.data_ops = nd;
+                d.stats.literal_bytes = lb;
+                d.stats.weak_hits = o.weak_hits;
+                d.stats.verified_hits = o.hits;
+                acc.copy_ops += d.stats.copy_ops;
+                acc.data_ops += nd;
+                acc.literal_bytes += lb;
+                acc.weak_hits += o.weak_hits;
+                acc.verified_hits += o.hits;
+            }
+        }
+        part[t] = acc;
+    };
+    if (!run_parallel(nthr, worker)) return fail(SYDELTA_E_OOM, "out of host memory (op lists)");
+    for (auto& p : part) {
+        b->total.copy_ops += p.copy_ops;
+        b->total.data_ops += p.data_ops;
+        b->total.literal_bytes += p.literal_bytes;
+        b->total.weak_hits += p.weak_hits;
+        b->total.verified_hits += p.verified_hits;
+    }
+    if (ph.bytes > kPinnedHitsKeep) {
+        (void)hipHostFree(ph.p);
+        ph = PinnedHits();
+    }
+    if (host_timing)
+        fprintf(stderr, "sydelta file walk: %llu files, %llu records: kernel+counts %.3f ms, records D2H %.3f ms, "
+                "expand %.3f ms\n", (unsigned long long)nf, (unsigned long long)nrec, t_kern, t_d2h - t_kern,
+                ms_since(t0) - t_d2h);
+    return SYDELTA_OK;
+}
+
 // Match source f (d_buf[src_off[f] .. +src_len[f])) against file f of the index,
 // for every f; results in b->d[f].
 static int match_impl(sydelta_index* ix, const uint8_t* d_buf, const uint64_t* src_off, const uint64_t* src_len,
                       hipStream_t s, sydelta_delta_batch* b) {
+    ScratchHold hold;  // the probe scratch is used until the walks end
     const auto t_begin = std::chrono::steady_clock::now();
     CallProf cp;
     const uint64_t n = ix->bs;
@@ -2064,6 +2302,7 @@ static int match_impl(sydelta_index* ix, const uint8_t* d_buf, const uint64_t* s
         c.nblk = (c.p1 + n - 1) / n;
     }
     b->total.positions = tot_pos;
+    if (file_walk_ok(ix, src_off, src_len, d_buf)) return match_walk_files(ix, d_buf, src_off, src_len, s, C.prof, b);
     static const bool host_timing = getenv("SYDELTA_HOST_TIMING") != nullptr;
     const auto t0 = std::chrono::steady_clock::now();
     const int mode = n > scan_max_window() && !wide_scan(ix) ? 0 : probe_mode_env();
@@ -2134,7 +2373,7 @@ extern "C" int sydelta_match_device(sydelta_index* idx, const uint8_t* d_src, ui
     if (idx->nfiles != 1) return fail(SYDELTA_E_INVAL, "index holds %llu files; use sydelta_match_batch_device",
                                       (unsigned long long)idx->nfiles);
     if (len && !d_src) return fail(SYDELTA_E_INVAL, "NULL source");
-    if (int r = ensure_device(idx->device)) return r;
+    SYDELTA_ENTER_DEVICE(idx->device);
     hipStream_t s = stream ? (hipStream_t)stream : thread_stream(idx->device);
     sydelta_delta_batch b;
     const uint64_t off = 0;
@@ -2156,7 +2395,7 @@ extern "C" int sydelta_match_batch_device(sydelta_index* idx, const uint8_t* d_b
     if (nfiles != idx->nfiles) return fail(SYDELTA_E_INVAL, "index holds %llu files, %llu sources given",
                                            (unsigned long long)idx->nfiles, (unsigned long long)nfiles);
     if (nfiles && (!src_off || !src_len)) return fail(SYDELTA_E_INVAL, "NULL segment table");
-    if (int r = ensure_device(idx->device)) return r;
+    SYDELTA_ENTER_DEVICE(idx->device);
     hipStream_t s = stream ? (hipStream_t)stream : thread_stream(idx->device);
     std::unique_ptr<sydelta_delta_batch> b(new sydelta_delta_batch());
     if (int r = match_impl(idx, d_buf, src_off, src_len, s, b.get())) return r;
@@ -2179,7 +2418,7 @@ extern "C" int sydelta_compute_checksums_buf(int device, const uint8_t* buf, uin
     if (!buf || !out) return fail(SYDELTA_E_INVAL, "NULL buffer");
     if (cap < nb) return fail(SYDELTA_E_INVAL, "output holds %llu entries, need %llu", (unsigned long long)cap,
                               (unsigned long long)nb);
-    if (int r = ensure_device(device)) return r;
+    SYDELTA_ENTER_DEVICE(device);
     if (device < 0) device = 0;
     hipStream_t s = thread_stream(device);
     uint8_t* d_buf = nullptr;
@@ -2236,7 +2475,7 @@ static int generate_from_host(int device, const uint8_t* src, uint64_t len, cons
     if (len && !src) return fail(SYDELTA_E_INVAL, "NULL source");
     uint64_t last_size = 0;
     if (int r = check_sigs(sigs, nsigs, bs, &last_size)) return r;
-    if (int r = ensure_device(device)) return r;
+    SYDELTA_ENTER_DEVICE(device);
     if (device < 0) device = 0;
     hipStream_t s = thread_stream(device);
     std::vector<uint32_t> w(nsigs);
@@ -2442,7 +2681,7 @@ extern "C" int sydelta_compute_checksums(const char* path, uint64_t block_size, 
     const uint64_t nb = (L + block_size - 1) / block_size;
     int dev = 0;
     if (int r = path_device(&dev)) return r;
-    if (int r = ensure_device(dev)) return r;
+    SYDELTA_ENTER_DEVICE(dev);
     hipStream_t s = thread_stream(dev);
     const uint64_t C = std::min<uint64_t>(stream_chunk_bytes(block_size), L);
     const uint64_t nch = (L + C - 1) / C;
@@ -2532,7 +2771,7 @@ extern "C" int sydelta_generate_delta_streaming(const char* source_path, const s
     if (int r = f.open_(source_path)) return r;
     int dev = 0;
     if (int r = path_device(&dev)) return r;
-    if (int r = ensure_device(dev)) return r;
+    SYDELTA_ENTER_DEVICE(dev);
     hipStream_t s = thread_stream(dev);
     const uint64_t L = f.len, n = block_size;
     std::vector<uint32_t> w(nsigs);
@@ -2632,7 +2871,7 @@ extern "C" int sydelta_apply_delta_device(int device, const uint8_t* d_basis, ui
                                           const sydelta_delta* d, const uint8_t* d_lit, uint64_t lit_len,
                                           uint8_t* d_out, uint64_t out_cap, void* stream, sydelta_apply_stats* out) try {
     if (!d) return fail(SYDELTA_E_INVAL, "NULL delta");
-    if (int r = ensure_device(device)) return r;
+    SYDELTA_ENTER_DEVICE(device);
     // the piece table is staged in pinned host memory (one per thread, grown on demand)
     // so its upload runs at PCIe speed
     struct Pinned {
@@ -2805,7 +3044,7 @@ extern "C" int sydelta_synth_fill(uint8_t* d_buf, uint64_t len, uint64_t seed, v
     if (len && !d_buf) return fail(SYDELTA_E_INVAL, "NULL buffer");
     int dev = 0;
     (void)hipGetDevice(&dev);
-    if (int r = ensure_device(dev)) return r;
+    SYDELTA_ENTER_DEVICE(dev);
     hipStream_t s = stream ? (hipStream_t)stream : thread_stream(dev);
     HIP_TRY(launch_synth_fill(d_buf, len, seed, s));
     if (!stream) HIP_TRY(hipStreamSynchronize(s));
@@ -2819,7 +3058,7 @@ extern "C" int sydelta_synth_fill_range(uint8_t* d_buf, uint64_t first, uint64_t
     if (first % 8) return fail(SYDELTA_E_INVAL, "first must be a multiple of 8");
     int dev = 0;
     (void)hipGetDevice(&dev);
-    if (int r = ensure_device(dev)) return r;
+    SYDELTA_ENTER_DEVICE(dev);
     hipStream_t s = stream ? (hipStream_t)stream : thread_stream(dev);
     HIP_TRY(launch_synth_fill(d_buf, len, seed, s, first));
     if (!stream) HIP_TRY(hipStreamSynchronize(s));
@@ -2834,7 +3073,7 @@ extern "C" int sydelta_synth_mutate_blocks(uint8_t* d_dst, const uint8_t* d_src,
     if (!block_size || first % block_size) return fail(SYDELTA_E_INVAL, "first must be a multiple of block_size");
     int dev = 0;
     (void)hipGetDevice(&dev);
-    if (int r = ensure_device(dev)) return r;
+    SYDELTA_ENTER_DEVICE(dev);
     hipStream_t s = stream ? (hipStream_t)stream : thread_stream(dev);
     if (len && d_dst != d_src) HIP_TRY(hipMemcpyAsync(d_dst, d_src, len, hipMemcpyDeviceToDevice, s));
     HIP_TRY(launch_synth_edit_blocks(d_dst, len, block_size, first, seed, rate_ppm, s));
@@ -2849,7 +3088,7 @@ extern "C" int sydelta_synth_mutate(uint8_t* d_dst, const uint8_t* d_src, uint64
     if (len && (!d_dst || !d_src)) return fail(SYDELTA_E_INVAL, "NULL buffer");
     int dev = 0;
     (void)hipGetDevice(&dev);
-    if (int r = ensure_device(dev)) return r;
+    SYDELTA_ENTER_DEVICE(dev);
     hipStream_t s = stream ? (hipStream_t)stream : thread_stream(dev);
     HIP_TRY(launch_synth_mutate(d_dst, d_src, len, seed, rate_ppm, s));
     if (!stream) HIP_TRY(hipStreamSynchronize(s));
@@ -2895,7 +3134,7 @@ extern "C" int sydelta_chunk_classify(sydelta_index* idx, const uint8_t* d_buf, 
         return fail(SYDELTA_E_INVAL, "buffer ends at %llu, chunk needs bytes up to %llu",
                     (unsigned long long)(buf_pos + buf_len), (unsigned long long)need_end);
     if (buf_len && !d_buf) return fail(SYDELTA_E_INVAL, "NULL buffer");
-    if (int r = ensure_device(idx->device)) return r;
+    SYDELTA_ENTER_DEVICE(idx->device);
     hipStream_t s = stream ? (hipStream_t)stream : thread_stream(idx->device);
     std::unique_ptr<sydelta_chunk> ch(new sydelta_chunk());
     CallProf cp;
@@ -2941,7 +3180,7 @@ extern "C" int sydelta_chunk_walk(sydelta_chunk* ch, uint64_t entry, uint64_t* e
     Classifier& C = ch->C;
     const Src& c = C.src[0];
     if (entry < c.p0) return fail(SYDELTA_E_INVAL, "entry %llu precedes the chunk", (unsigned long long)entry);
-    if (int r = ensure_device(C.ix->device)) return r;
+    SYDELTA_ENTER_DEVICE(C.ix->device);
     CallProf cp;
     C.prof = cp.get();
     std::unique_ptr<sydelta_delta> d(new sydelta_delta());
@@ -2961,6 +3200,7 @@ extern "C" int sydelta_chunk_walk(sydelta_chunk* ch, uint64_t entry, uint64_t* e
 
 extern "C" void sydelta_chunk_free(sydelta_chunk* ch) {
     if (!ch) return;
+    DeviceScope keep_device;
     (void)hipSetDevice(ch->C.ix->device);
     delete ch;
 }
@@ -3036,6 +3276,7 @@ std::mutex g_peer_mu;
 std::set<std::pair<int, int>> g_peer_on;  // under g_peer_mu: (device, peer) with access enabled
 void enable_peer(int dev, int peer) {
     if (dev == peer) return;
+    DeviceScope keep_device;
     std::lock_guard<std::mutex> lk(g_peer_mu);
     if (!g_peer_on.insert({dev, peer}).second) return;
     int ok = 0;
@@ -3049,6 +3290,7 @@ extern "C" int sydelta_delta_multi_device(const int* devices, int ndev, const ui
                                           const uint64_t* basis_len, const uint8_t* const* d_src,
                                           const uint64_t* src_pos, const uint64_t* src_buf_len, uint64_t src_len,
                                           uint64_t block_size, sydelta_delta** out) try {
+    DeviceScope keep_device;  // restored after every hipSetDevice below, on every return
     if (!out) return fail(SYDELTA_E_INVAL, "out is NULL");
     *out = nullptr;
     if (ndev < 1 || !devices || !d_basis || !basis_len || !d_src || !src_pos || !src_buf_len)
@@ -3093,6 +3335,16 @@ extern "C" int sydelta_delta_multi_device(const int* devices, int ndev, const ui
                 if (e) (void)hipEventDestroy(e);
         }
     } ev_free{ev};
+    // on any return (an error below included): every stream's queued copies finish before
+    // the slices in sig are released on their own streams (destroyed before sig)
+    struct SyncAll {
+        const int* dev;
+        const std::vector<hipStream_t>& s;
+        ~SyncAll() {
+            for (size_t g = 0; g < s.size(); ++g)
+                if (s[g] && hipSetDevice(dev[g]) == hipSuccess) (void)hipStreamSynchronize(s[g]);
+        }
+    } sync_all{devices, s};
     CallProf cp;
     for (int g = 0; g < ndev; ++g) {
         HIP_TRY(hipSetDevice(devices[g]));

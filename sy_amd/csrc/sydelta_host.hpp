@@ -31,6 +31,21 @@ int fail(int code, const char* fmt, ...);
 int host_exception();
 // Make `device` current after its one-time gfx950 check.
 int ensure_device(int device);
+// Every entry point leaves the calling thread's current HIP device as it found it
+// (sydelta.h, "Devices"): a guard records it on entry and restores it on every return.
+// Guards nest: an inner one restores what the outer entry made current.
+struct DeviceScope {
+    int dev = -1;
+    DeviceScope() {
+        if (hipGetDevice(&dev) != hipSuccess) dev = -1;
+    }
+    ~DeviceScope() {
+        int now = -1;
+        if (dev >= 0 && hipGetDevice(&now) == hipSuccess && now != dev) (void)hipSetDevice(dev);
+    }
+    DeviceScope(const DeviceScope&) = delete;
+    DeviceScope& operator=(const DeviceScope&) = delete;
+};
 // The device of the calling thread's path-level calls (bound on first use, sticky).
 int path_device(int* out);
 // The calling thread's stream for `device`.
@@ -52,7 +67,17 @@ constexpr size_t kPinnedHitsKeep = (size_t)256 << 20;
 HitScratch& thread_hit_scratch(int device);
 DevScratch& thread_scan_scratch(int device);   // launch_scan's kept scratch
 DevScratch& thread_probe_scratch(int device);  // Classifier::probe's (transient classifiers)
+DevScratch& thread_walk_scratch(int device);   // the file walk's (match_walk_files)
 PinnedHits& thread_pinned_hits();
+// Held (recursively) by the calling thread while it uses its scratch: sydelta_trim on
+// another thread then leaves that scratch alone.
+struct ScratchHold {
+    std::recursive_mutex* mu;
+    ScratchHold();
+    ~ScratchHold();
+    ScratchHold(const ScratchHold&) = delete;
+    ScratchHold& operator=(const ScratchHold&) = delete;
+};
 // sydelta_set_profiling state; CallProf collects one call's kernel timings.
 bool profiling_on();
 struct CallProf {
@@ -62,7 +87,13 @@ struct CallProf {
 };
 }  // namespace sydelta
 
-#define HIP_TRY(expr)                                                                                   \
+// An entry point's device: the caller's current device restored on return (DeviceScope),
+// `dev` made current (ensure_device) or the error returned.
+#define SYDELTA_ENTER_DEVICE(dev)              \
+    ::sydelta::DeviceScope sydelta_dscope_;   \
+    if (int r_ = ::sydelta::ensure_device(dev)) return r_
+
+#define HIP_TRY(expr)                                                                                 \
     do {                                                                                                \
         hipError_t e_ = (expr);                                                                         \
         if (e_ != hipSuccess) {                                                                         \

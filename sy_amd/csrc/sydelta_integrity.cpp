@@ -21,7 +21,7 @@ extern "C" int sydelta_xxh3_batch_device(int device, const uint8_t* d_buf, uint6
         total |= lens[f];
     }
     if (total && !d_buf) return fail(SYDELTA_E_INVAL, "NULL buffer");
-    if (int r = ensure_device(device)) return r;
+    SYDELTA_ENTER_DEVICE(device);
     hipStream_t s = stream ? (hipStream_t)stream : thread_stream(device < 0 ? 0 : device);
     // host tables: block-count prefix and the size order of the chains
     std::vector<uint64_t> pfx(nfiles + 1, 0), nb(nfiles);

@@ -206,6 +206,47 @@ hipError_t launch_tail(const uint8_t* d_buf, const TailJob* d_jobs, uint32_t njo
 // merge, successors, pointer-jumping path marking, op emission; a.res receives the
 // totals.  All arrays of a are device memory sized as ChainArgs documents.
 hipError_t launch_chain(const chain::ChainArgs& a, hipStream_t s, Profiler* prof);
+// K10: the whole greedy walk (generator.rs:116-221) of each of many small files on the
+// device, one workgroup per file (k_walk_files), for batched indexes whose per-file Bloom
+// filters fit LDS (<= kWalkMaxWords words) at block sizes n % 64 == 0, 256 <= n <=
+// kWalkMaxN.  The ops come back run-length coded: a Data op, or a run of Copies of
+// consecutive global basis blocks (each Copy's size follows from its block: the basis
+// file's last block has last_size, every other one n).
+constexpr uint32_t kWalkMaxWords = 4096;
+constexpr uint32_t kWalkMaxN = 8192;
+struct WalkRec {
+    uint32_t kind;  // 0: Data; else the number of Copies in the run
+    uint32_t a;     // Data: length; Copy run: its first global block
+    uint64_t off;   // Data: offset in the source file
+};
+struct WalkFileOut {
+    uint32_t base, count;  // the file's records: out[base, base + count)
+    uint32_t weak_hits;    // windows whose weak value has candidates (examined ones)
+    uint32_t hits;         // windows classified as hits
+};
+struct WalkArgs {
+    const uint8_t* base;         // launch base; file f's source at soff[f], slen[f] bytes
+    const uint64_t* soff;
+    const uint64_t* slen;
+    const uint64_t* rec_off;     // file f's staging region: stage + rec_off[f] (2 * (slen/n) + 4 records)
+    const uint64_t* last_size;   // per file (0: empty signature)
+    uint32_t nfiles, n, nm, fw_max;
+    const FileIx* files;
+    const uint64_t* fblk;
+    const uint32_t* filt;
+    const uint32_t* keys;
+    const uint32_t* start;
+    const uint32_t* cnt;
+    const uint32_t* order;
+    const uint64_t* cstrong;
+    const uint32_t* weak;        // the index's signature copies (the tail rule)
+    const uint64_t* strong;
+    WalkRec* stage;
+    WalkRec* out;                // compacted records of every file
+    WalkFileOut* fout;
+    unsigned long long* total;   // records placed in out (zeroed before the launch)
+};
+hipError_t launch_walk_files(const WalkArgs& a, hipStream_t s, Profiler* prof);
 // One slice (<= 64 KiB) of an op for the device apply: out[dst, dst+len) =
 // (from_basis ? basis : lit)[src, src+len).
 struct ApplyPiece {

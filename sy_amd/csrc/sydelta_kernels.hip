@@ -2822,6 +2822,383 @@ __global__ void k_chain_finish(chain::ChainArgs a) {
 }
 
 // ===========================================================================
+// K10: the greedy walk of many small files, one workgroup per file (C4)
+// ===========================================================================
+// The batched match used to classify on the device in five host-synchronised phases
+// (aligned probe, miss ranges, scans, phase probe, scans of the missed blocks) and walk on
+// host threads.  Here a workgroup walks its file itself (generator.rs:116-221), classifying
+// only the window starts the walk visits:
+//   * the walk at x on the phase grid k*n + phi: the phase windows of the next kWRows
+//     blocks are hashed together, one 16-lane row each (row_hash, the signature kernel's
+//     layout), and looked up (first candidate in index order with equal strong,
+//     generator.rs:121-155); a hit copies and moves x by n, so the walk stays on the grid;
+//   * a miss at x: the window starts (x, x + n) are rolled (rolling.rs:66-79), 16 per
+//     thread from the closed form of their first window (workgroup scans of 16-byte group
+//     sums over the bytes staged in LDS), tested against the file's Bloom filter in LDS and
+//     the exact table; weak hits are hashed 16 at a time in position order and the first
+//     verified one is the walk's next hit (a Copy, then a new phase); without one the walk
+//     continues at x + n, the next phase window.
+// So a copy-heavy file costs one hash per block plus one roll of n positions per edited
+// block, and a shift (an insertion or deletion) one new phase grid.  The ops are written
+// run-length coded (WalkRec) to the file's staging region, then moved to the compact
+// output with one atomic per file.
+constexpr int kWT = 256;                 // threads per workgroup (4 waves, 16 rows)
+constexpr uint32_t kWRows = kWT / 16;    // phase windows hashed per pass
+constexpr uint32_t kWRun = 16;           // window starts per thread per roll pass
+constexpr uint32_t kWSub = kWT * kWRun;  // window starts per roll pass (4096)
+
+struct WalkLds {  // byte offsets of the dynamic LDS
+    uint32_t filt, ntab, stage, small, total;
+};
+__host__ __device__ __forceinline__ WalkLds walk_lds(uint32_t fw, uint32_t n) {
+    WalkLds L{};
+    uint32_t o = 0;
+    L.filt = o; o += 4 * fw;
+    L.ntab = o; o += 1024;
+    L.stage = o; o += (kWSub + n + 64 + 15) & ~15u;  // also the scans' prefix arrays: 12 * (kWT + n/16 + 1) bytes
+    L.small = o; o += 512;
+    L.total = o;
+    return L;
+}
+// small area (u32 words)
+constexpr int kWsR = 0;          // [16] phase-window results
+constexpr int kWsVList = 16;     // [16] weak hits being verified (position - y0)
+constexpr int kWsVRes = 32;      // [16] their blocks
+constexpr int kWsWave = 48;      // [4 waves x 4] wave totals of the scans
+constexpr int kWsMisc = 64;      // [0] tail flag, [1] record base
+
+// Workgroup exclusive scan of up to four u32 values per thread (wave DPP scans + the wave
+// totals through LDS); tot = the workgroup totals.  Barriers inside: every thread calls.
+template <int K>
+__device__ __forceinline__ void wg_scan_excl(uint32_t (&v)[K], uint32_t (&tot)[K], uint32_t* wsum) {
+    const uint32_t lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    uint32_t wt[K];
+#pragma unroll
+    for (int k = 0; k < K; ++k) v[k] = wave_scan_excl(v[k], wt[k]);
+    if (lane == 0) {
+#pragma unroll
+        for (int k = 0; k < K; ++k) wsum[wid * 4 + k] = wt[k];
+    }
+    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < K; ++k) {
+        uint32_t before = 0, all = 0;
+#pragma unroll
+        for (int w = 0; w < kWT / 64; ++w) {
+            const uint32_t x = wsum[w * 4 + k];
+            before += (uint32_t)w < wid ? x : 0u;
+            all += x;
+        }
+        v[k] += before;
+        tot[k] = all;
+    }
+    __syncthreads();  // wsum is reused by the next scan
+}
+
+// 16 bytes at LDS byte offset o (any alignment) as 4 dwords
+__device__ __forceinline__ void lds16_u(const uint8_t* st, uint32_t o, uint32_t (&x)[4]) {
+    const uint32_t* w = (const uint32_t*)(st + (o & ~3u));
+    const uint32_t sh = o & 3;
+    uint32_t d[5];
+#pragma unroll
+    for (int i = 0; i < 5; ++i) d[i] = w[i];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) x[i] = __builtin_amdgcn_alignbyte(d[i + 1], d[i], sh);
+}
+
+// First candidate in index order of file F with weak wk and strong st (generator.rs:127-133),
+// or kNoBlock; one thread.
+__device__ __forceinline__ uint32_t walk_lookup(const WalkArgs& a, const FileIx& F, uint32_t wk, uint64_t st) {
+    const int64_t slot = table_find(a.keys + F.slot_off, F.bmask, wk);
+    if (slot < 0) return kNoBlock;
+    const uint64_t gs = F.slot_off + (uint64_t)slot;
+    const uint32_t s0 = a.start[gs], c = a.cnt[gs];
+    for (uint32_t j = 0; j < c; ++j)
+        if (a.cstrong[s0 + j] == st) return a.order[s0 + j];
+    return kNoBlock;
+}
+
+__global__ __launch_bounds__(kWT) void k_walk_files(WalkArgs a) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    const uint32_t f = blockIdx.x;
+    const uint32_t tid = threadIdx.x, lane = tid & 63, wid = tid >> 6, row = tid >> 4;
+    const uint32_t n = a.n;
+    const FileIx F = a.files[f];
+    const uint32_t fw = 1u << (32 - F.fwshift);
+    const WalkLds L = walk_lds(a.fw_max, n);
+    uint32_t* filt = (uint32_t*)(smem + L.filt);
+    uint32_t* ntab = (uint32_t*)(smem + L.ntab);
+    uint8_t* stage = smem + L.stage;
+    uint32_t* sm = (uint32_t*)(smem + L.small);
+    const uint8_t* src = a.base + a.soff[f];
+    const uint64_t len = a.slen[f];
+    const uint64_t gb0 = a.fblk[f], nbf = a.fblk[f + 1] - gb0, ls = a.last_size[f];
+    const uint64_t p1 = (nbf && len >= n) ? len - n + 1 : 0;  // full-window starts [0, p1)
+
+    {  // the file's Bloom filter, the roll table
+        const uint4* g = (const uint4*)(a.filt + F.filt_off);
+        for (uint32_t i = tid; i < fw / 4; i += kWT) ((uint4*)filt)[i] = g[i];
+        ntab[tid] = kMod - 1 - (a.nm * tid) % kMod;  // kWT == 256 bytes
+    }
+    // the tail rule (generator.rs:156-184): the suffix of the basis's last block's size
+    if (wid == 0) {
+        uint32_t ok = 0;
+        if (nbf && ls < n && len >= ls) {
+            const uint8_t* p = src + (len - ls);
+            uint32_t wk = 0;
+            uint64_t st = 0;
+            if (ls > 240) {
+                wave_hash_long(p, ls, wk, st);
+            } else if (lane == 0) {
+                wk = adler_scalar(p, ls);
+                st = xxh3_short(p, ls);
+            }
+            ok = (wk == a.weak[gb0 + nbf - 1] && st == a.strong[gb0 + nbf - 1]) ? 1u : 0u;
+        }
+        if (lane == 0) sm[kWsMisc] = ok;
+    }
+    __syncthreads();
+
+    // run-length coded output (thread 0 writes; every thread keeps the same state)
+    WalkRec* stg = a.stage + a.rec_off[f];
+    uint32_t nrec = 0, ck = 0, ca = 0;  // the open Copy run: ck Copies from block ca (ck 0: none)
+    auto put = [&](uint32_t kind, uint32_t aa, uint64_t off) {
+        if (tid == 0) stg[nrec] = WalkRec{kind, aa, off};
+        ++nrec;
+    };
+    auto close_run = [&]() {
+        if (ck) put(ck, ca, 0);
+        ck = 0;
+    };
+    auto data = [&](uint64_t lo, uint64_t hi) {
+        if (hi > lo) {
+            close_run();
+            put(0, (uint32_t)(hi - lo), lo);
+        }
+    };
+    auto copy = [&](uint32_t g) {
+        if (ck && g == ca + ck) {
+            ++ck;
+        } else {
+            close_run();
+            ck = 1;
+            ca = g;
+        }
+    };
+    uint32_t weak_hits = 0, hits = 0;
+
+    uint64_t x = 0, lit = 0;
+    uint32_t phi = 0xFFFFFFFFu;
+    uint64_t rk0 = 0, rk1 = 0;  // the results in sm[kWsR] are blocks [rk0, rk1) at phase phi
+#pragma unroll 1
+    while (x < p1) {
+        const uint64_t k = x / n;
+        const uint32_t ph = (uint32_t)(x - k * n);
+        if (ph != phi || k >= rk1) {
+            // ---- phase pass: windows (k + r) n + ph, r < cnt, one per row
+            const uint64_t cnt = min((uint64_t)kWRows, (p1 - x + n - 1) / n);
+            const uint64_t pos = (k + (row < cnt ? row : 0)) * n + ph;
+            uint32_t wk;
+            uint64_t st;
+            if ((ph & 15) == 0)
+                row_hash<true>(src + pos, n, wk, st);
+            else
+                row_hash<false>(src + pos, n, wk, st);
+            __syncthreads();  // every wave has read the previous pass's results
+            if ((tid & 15) == 0 && row < cnt) {
+                uint32_t blk = kNoBlock;
+                const ProbeHash h = probe_hash(wk);
+                if (filt_pass(filt[h.r >> F.fwshift], h.q)) blk = walk_lookup(a, F, wk, st);
+                sm[kWsR + row] = blk;
+            }
+            __syncthreads();
+            phi = ph;
+            rk0 = k;
+            rk1 = k + cnt;
+        }
+        const uint32_t blk = sm[kWsR + (uint32_t)(k - rk0)];
+        if (blk != kNoBlock) {  // generator.rs:135-146
+            ++hits;
+            data(lit, x);
+            copy(blk);
+            x += n;
+            lit = x;
+            continue;
+        }
+        // ---- the window at x misses: roll (x, min(x + n, p1)) for the first hit
+        const uint64_t yend = min(x + n, p1);
+        uint64_t q = yend;
+        uint32_t qb = kNoBlock;
+#pragma unroll 1
+        for (uint64_t y0 = x + 1; y0 < yend && qb == kNoBlock; y0 += kWSub) {
+            const uint64_t y1 = min(y0 + kWSub, yend);
+            const uint64_t g0 = y0 & ~15ull;
+            const uint32_t so = (uint32_t)(y0 - g0);
+            const uint32_t sbytes = (kWSub + n + 64 + 15) & ~15u;
+            __syncthreads();  // the stage (prefix arrays of the last pass) is free
+            for (uint32_t i = tid; i < sbytes / 16; i += kWT) {
+                const uint64_t o = g0 + 16ull * i;
+                uint4 v = make_uint4(0, 0, 0, 0);
+                if (o < len) v = *(const uint4*)(src + o);  // a granule holding a byte of the file
+                if (o + 16 > len && o < len) {  // zero the bytes past the end
+                    const uint32_t keep = (uint32_t)(len - o);
+                    uint32_t w[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+                    for (int j = 0; j < 4; ++j) {
+                        const int kb = (int)keep - 4 * j;
+                        w[j] = kb >= 4 ? w[j] : kb <= 0 ? 0u : (w[j] & ((1u << (8 * kb)) - 1));
+                    }
+                    v = make_uint4(w[0], w[1], w[2], w[3]);
+                }
+                ((uint4*)stage)[i] = v;
+            }
+            __syncthreads();
+            // this thread's bytes: out [y0 + 16t, +16), in [y0 + 16t + n, +16)
+            uint32_t xo[4], xi[4];
+            lds16_u(stage, so + 16 * tid, xo);
+            lds16_u(stage, so + 16 * tid + n, xi);
+            // groups j = 3t .. 3t+2 (bytes [y0 + 16j, +16)) of the G = kWT + n/16 the windows span
+            const uint32_t G = kWT + n / 16;
+            uint32_t gs[3], gv[3];
+#pragma unroll
+            for (int m = 0; m < 3; ++m) {
+                const uint32_t j = 3 * tid + m;
+                gs[m] = gv[m] = 0;
+                if (j < G) {
+                    uint32_t d[4];
+                    lds16_u(stage, so + 16 * j, d);
+#pragma unroll
+                    for (int i = 0; i < 4; ++i) {
+                        gs[m] = udot4(d[i], 0x01010101u, gs[m]);
+                        gv[m] = udot4(d[i], offw(i), gv[m]);
+                    }
+                }
+            }
+            uint32_t sc[3] = {gs[0] + gs[1] + gs[2], gv[0] + gv[1] + gv[2],
+                              (3 * tid) * gs[0] + (3 * tid + 1) * gs[1] + (3 * tid + 2) * gs[2]};
+            uint32_t tot[3];
+            __syncthreads();  // every thread has read the stage: the prefix arrays take it over
+            wg_scan_excl<3>(sc, tot, sm + kWsWave);
+            uint32_t* PS = (uint32_t*)stage;
+            uint32_t* PV = PS + (G + 1);
+            uint32_t* PJ = PV + (G + 1);
+            {
+                uint32_t s = sc[0], v = sc[1], jj = sc[2];
+#pragma unroll
+                for (int m = 0; m < 3; ++m) {
+                    const uint32_t j = 3 * tid + m;
+                    if (j < G) {
+                        PS[j] = s;
+                        PV[j] = v;
+                        PJ[j] = jj;
+                    }
+                    s += gs[m];
+                    v += gv[m];
+                    jj += j * gs[m];
+                }
+                if (tid == 0) {
+                    PS[G] = tot[0];
+                    PV[G] = tot[1];
+                    PJ[G] = tot[2];
+                }
+            }
+            __syncthreads();
+            const uint32_t g = n / 16;
+            const uint64_t S = PS[tid + g] - PS[tid];
+            const uint64_t V = PV[tid + g] - PV[tid];
+            const uint64_t J = PJ[tid + g] - PJ[tid];
+            uint32_t am = (uint32_t)((1 + S) % kMod);
+            uint32_t bm = (uint32_t)(((uint64_t)n + (uint64_t)n * S - (16 * (J - (uint64_t)tid * S) + V)) % kMod);
+            // roll the thread's 16 window starts
+            const uint64_t p0 = y0 + 16ull * tid;
+            uint32_t pm = 0, wv[kWRun];
+#pragma unroll
+            for (int i = 0; i < (int)kWRun; ++i) {
+                wv[i] = (bm << 16) | am;
+                const ProbeHash h = probe_hash(am, bm);
+                const uint32_t pass = (p0 + i < y1) ? filt_bit(filt[h.r >> F.fwshift], h.q) : 0u;
+                pm |= pass << i;
+                const uint32_t out = (xo[i >> 2] >> (8 * (i & 3))) & 0xFF;
+                const uint32_t in = (xi[i >> 2] >> (8 * (i & 3))) & 0xFF;
+                const uint32_t u = am + in + (kMod - out);  // [M-255, 2M+255)
+                am = min(u, min(u - kMod, u - 2 * kMod));
+                const uint32_t v = bm + am + ntab[out];  // [0, 3M)
+                bm = min(v, min(v - kMod, v - 2 * kMod));
+            }
+            // exact-table lookups of the filter passes -> weak hits (generator.rs:121-124)
+            uint32_t hm = 0;
+            while (pm) {
+                const int i = __builtin_ctz(pm);
+                pm &= pm - 1;
+                if (table_find(a.keys + F.slot_off, F.bmask, wv[i]) >= 0) hm |= 1u << i;
+            }
+            uint32_t rk[1] = {(uint32_t)__builtin_popcount(hm)}, ntot[1];
+            wg_scan_excl<1>(rk, ntot, sm + kWsWave);
+            weak_hits += ntot[0];
+            // verify the weak hits 16 at a time in position order (generator.rs:127-133)
+#pragma unroll 1
+            for (uint32_t vb = 0; vb < ntot[0]; vb += kWRows) {
+                {
+                    uint32_t r = rk[0], m = hm;
+                    while (m) {
+                        const int i = __builtin_ctz(m);
+                        m &= m - 1;
+                        if (r >= vb && r < vb + kWRows) sm[kWsVList + (r - vb)] = 16 * tid + (uint32_t)i;
+                        ++r;
+                    }
+                }
+                __syncthreads();
+                const uint32_t nv = min((uint32_t)kWRows, ntot[0] - vb);
+                const uint64_t pos = y0 + sm[kWsVList + (row < nv ? row : 0)];
+                uint32_t wk;
+                uint64_t st;
+                row_hash<false>(src + pos, n, wk, st);
+                if ((tid & 15) == 0 && row < nv) sm[kWsVRes + row] = walk_lookup(a, F, wk, st);
+                __syncthreads();
+                for (uint32_t r = 0; r < nv; ++r) {
+                    const uint32_t b = sm[kWsVRes + r];
+                    if (b != kNoBlock) {
+                        q = y0 + sm[kWsVList + r];
+                        qb = b;
+                        break;
+                    }
+                }
+                __syncthreads();  // vlist / vres are rewritten by the next batch
+                if (qb != kNoBlock) break;
+            }
+        }
+        if (qb != kNoBlock) {
+            ++hits;
+            data(lit, q);
+            copy(qb);
+            x = q + n;
+            lit = x;
+        } else {
+            x = yend;  // the next phase window (or the end of the full windows)
+        }
+    }
+    // the walk's end: the tail rule at p* = len - last_size, then the last literal run
+    if (sm[kWsMisc] && ls <= len && len - ls >= lit) {
+        data(lit, len - ls);
+        copy((uint32_t)(gb0 + nbf - 1));
+        lit = len;
+        ++hits;
+    }
+    data(lit, len);
+    close_run();
+    // move the records to the compact output (one atomic per file)
+    __threadfence_block();
+    if (tid == 0) sm[kWsMisc + 1] = nrec ? (uint32_t)atomicAdd(a.total, (unsigned long long)nrec) : 0u;
+    __syncthreads();
+    const uint32_t base = sm[kWsMisc + 1];
+    for (uint32_t i = tid; i < nrec; i += kWT) {
+        const volatile WalkRec* r = stg + i;
+        a.out[base + i] = WalkRec{r->kind, r->a, r->off};
+    }
+    if (tid == 0) a.fout[f] = WalkFileOut{base, nrec, weak_hits, hits};
+}
+
+// ===========================================================================
 // K7z: zstd frame of a text in HBM (sydelta_zstd.hpp; ssh.rs:1009-1017)
 // ===========================================================================
 // One workgroup per 128 KiB block.  Entropy-only content: a byte histogram (per-wave LDS
@@ -5026,6 +5403,16 @@ hipError_t launch_scan_wide(const uint8_t* d_src, uint64_t len, uint64_t pos_beg
     const uint64_t tiles = (pos_end - pos_begin + kScanTile - 1) / kScanTile;
     ProfScope ps(prof, s, "k_scan");
     hipLaunchKernelGGL(k_scan, dim3((unsigned)tiles), dim3(kScanThreads), lds, s, a);
+    return hipGetLastError();
+}
+
+hipError_t launch_walk_files(const WalkArgs& a, hipStream_t s, Profiler* prof) {
+    if (!a.nfiles) return hipSuccess;
+    if (a.n % 64 != 0 || a.n < 256 || a.n > kWalkMaxN || a.fw_max > kWalkMaxWords || a.fw_max < 4)
+        return hipErrorInvalidValue;
+    const WalkLds L = walk_lds(a.fw_max, a.n);
+    ProfScope ps(prof, s, "k_walk_files");
+    hipLaunchKernelGGL(k_walk_files, dim3(a.nfiles), dim3(kWT), L.total, s, a);
     return hipGetLastError();
 }
 

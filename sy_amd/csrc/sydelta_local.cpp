@@ -35,7 +35,7 @@ extern "C" int sydelta_block_compare_device(int device, const uint8_t* d_src, ui
     if (!block_size) return fail(SYDELTA_E_INVAL, "block_size must be > 0");
     if (src_len && (!d_src || !d_changed)) return fail(SYDELTA_E_INVAL, "NULL buffer");
     if (dst_len && !d_dst) return fail(SYDELTA_E_INVAL, "NULL destination");
-    if (int r = ensure_device(device)) return r;
+    SYDELTA_ENTER_DEVICE(device);
     hipStream_t s = stream ? (hipStream_t)stream : thread_stream(device < 0 ? 0 : device);
     const uint64_t nb = (src_len + block_size - 1) / block_size;
     CallProf cp;
@@ -95,7 +95,7 @@ extern "C" int sydelta_estimate_change_ratio_device(int device, const uint8_t* d
     if (size_diff > 0.5) return finish(std::min(size_diff, 1.0), 0, 0);  // :112-124
     const std::vector<uint64_t> pos = sample_blocks(want, total_blocks);
     if (!want) return finish(0.0, 0, 0);
-    if (int r = ensure_device(device)) return r;
+    SYDELTA_ENTER_DEVICE(device);
     hipStream_t s = stream ? (hipStream_t)stream : thread_stream(device < 0 ? 0 : device);
     DevMem m;
     HIP_TRY(dev_malloc_async(&m.p, want * 8 * 3, s));
@@ -180,7 +180,7 @@ extern "C" int sydelta_estimate_change_ratio(const char* source_path, const char
     };
     int dev = 0;
     if (int r = path_device(&dev)) return r;
-    if (int r = ensure_device(dev)) return r;
+    SYDELTA_ENTER_DEVICE(dev);
     hipStream_t s = thread_stream(dev);
     const uint64_t per = std::max<uint64_t>(1, std::min<uint64_t>(want, (64ull << 20) / block_size));
     std::vector<uint8_t> host(2 * per * block_size);

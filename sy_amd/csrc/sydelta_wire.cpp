@@ -438,7 +438,7 @@ extern "C" int sydelta_delta_to_json_device(const sydelta_delta* d, const uint8_
     if (!d || !out_len) return fail(SYDELTA_E_INVAL, "NULL argument");
     int dev = 0;
     (void)hipGetDevice(&dev);
-    if (int r = ensure_device(dev)) return r;
+    SYDELTA_ENTER_DEVICE(dev);
     hipStream_t s = stream ? (hipStream_t)stream : thread_stream(dev);
     struct Pinned {
         JsonPiece* p = nullptr;
@@ -543,7 +543,7 @@ extern "C" int sydelta_checksums_to_json_device(const uint32_t* d_weak, const ui
         return fail(SYDELTA_E_INVAL, "offsets of %llu blocks overflow", (unsigned long long)n);
     int dev = 0;
     (void)hipGetDevice(&dev);
-    if (int r = ensure_device(dev)) return r;
+    SYDELTA_ENTER_DEVICE(dev);
     hipStream_t s = stream ? (hipStream_t)stream : thread_stream(dev);
     uint64_t lo = 0, hi = 0;
     sigjson::text_bounds(n, block_size, last_size, lo, hi);
@@ -596,7 +596,7 @@ extern "C" int sydelta_checksums_from_json_device(const uint8_t* d_text, uint64_
     if (len < 2 || !d_text) return fail(SYDELTA_E_INVAL, "checksum JSON: not serde's compact form at byte 0");
     int dev = 0;
     (void)hipGetDevice(&dev);
-    if (int r = ensure_device(dev)) return r;
+    SYDELTA_ENTER_DEVICE(dev);
     hipStream_t s = stream ? (hipStream_t)stream : thread_stream(dev);
     const uint64_t nc = (len + sigjson::kParseChunk - 1) / sigjson::kParseChunk;
     CallProf cp;
@@ -660,7 +660,7 @@ extern "C" int sydelta_delta_from_json_device(const uint8_t* d_text, uint64_t le
     if (!d_text || len < dparse::kHead + (sizeof kTailKey - 1) + 17) return bad_at(0);
     int dev = 0;
     (void)hipGetDevice(&dev);
-    if (int r = ensure_device(dev)) return r;
+    SYDELTA_ENTER_DEVICE(dev);
     hipStream_t s = stream ? (hipStream_t)stream : thread_stream(dev);
     // head and tail (the tail is < 80 bytes: two u64 and the keys)
     char head[dparse::kHead], tail[96];
@@ -759,7 +759,7 @@ extern "C" int sydelta_zstd_compress_device(int device, const uint8_t* d_in, uin
         return fail(SYDELTA_E_INVAL, "output holds %llu bytes, a frame of %llu bytes needs up to %llu",
                     (unsigned long long)out_cap, (unsigned long long)len,
                     (unsigned long long)zstd::frame_bound(len));
-    if (int r = ensure_device(device)) return r;
+    SYDELTA_ENTER_DEVICE(device);
     hipStream_t s = stream ? (hipStream_t)stream : thread_stream(device < 0 ? 0 : device);
     if (len == 0) {  // one empty Raw block, the last
         uint8_t f[zstd::kFrameHeader + 3];

@@ -655,11 +655,16 @@ def batch_and_chunk_checks():
     rng = np.random.default_rng(77)
     n_checks = 0
     for bs in (1024, 4096):
-        for probe in ("0", "1", "auto"):
-            if probe == "auto":
+        # "0" / "1" / "auto": the classifier path (SYDELTA_FILE_WALK=0); "walk": the file
+        # walk (K10), which a batch of >= 64 small files takes by default
+        for probe in ("0", "1", "auto", "walk"):
+            os.environ["SYDELTA_FILE_WALK"] = "0"
+            if probe in ("auto", "walk"):
                 os.environ.pop("SYDELTA_PROBE", None)
             else:
                 os.environ["SYDELTA_PROBE"] = probe
+            if probe == "walk":
+                os.environ.pop("SYDELTA_FILE_WALK")
             nf = 80
             bases, srcs = [], []
             for k in range(nf):
@@ -708,6 +713,7 @@ def batch_and_chunk_checks():
             lib.sydelta_delta_batch_free(bt)
             lib.sydelta_index_free(ix)
     os.environ.pop("SYDELTA_PROBE", None)
+    os.environ.pop("SYDELTA_FILE_WALK", None)
     # chunked: one file in 1/2/3/8 chunks, walks chained in order, parts appended
     for bs in (512, 4096):
         basis = O.synth_bytes(300 * bs + 77, 0x700)
@@ -884,7 +890,95 @@ def multi_device_checks():
                                         u64a([1023, 4608]), 5120, 512, ctypes.byref(out))
     assert rc == -3, rc
     n_checks += 2
+    n_checks += device_restore_checks(lib)
     print(f"emulated multi-device checks ok: {n_checks}")
+
+
+def device_restore_checks(lib):
+    """Every entry point leaves the calling thread's current device as it found it
+    (sydelta.h, "Devices"): from each starting device, calls that work on other devices --
+    a device-pointer signature, an index built and freed on another device, the path API on
+    a bound device, sydelta_trim, sydelta_delta_multi_device (success and argument errors)."""
+    import ctypes
+
+    from sy_amd._lib import check
+
+    vpa = lambda arrs: (ctypes.c_void_p * len(arrs))(*[ctypes.c_void_p(x) for x in arrs])
+    u64a = lambda xs: (ctypes.c_uint64 * len(xs))(*[int(x) for x in xs])
+    vp = lambda a: ctypes.c_void_p(a.ctypes.data)
+
+    def cur():
+        d = ctypes.c_int(-1)
+        assert lib.hipGetDevice(ctypes.byref(d)) == 0
+        return d.value
+
+    n = 0
+    bs = 512
+    basis = O.synth_bytes(20 * bs + 7, 0x901)
+    src = basis.copy()
+    src[3000] ^= 1
+    L = src.size
+    with tempfile.TemporaryDirectory() as tmp:
+        pb, ps = os.path.join(tmp, "b"), os.path.join(tmp, "s")
+        basis.tofile(pb)
+        src.tofile(ps)
+        for start in range(4):
+            assert lib.hipSetDevice(start) == 0
+            other = (start + 1) % 4
+            nb = -(-basis.size // bs)
+            w = np.zeros(nb, np.uint32)
+            st = np.zeros(nb, np.uint64)
+            check(lib.sydelta_signature_device(other, vp(basis), basis.size, bs, vp(w), vp(st), None))
+            assert cur() == start, ("signature", start)
+            ix = ctypes.c_void_p()
+            check(lib.sydelta_index_create(other, vp(w), vp(st), nb, bs, basis.size - (nb - 1) * bs, 1, None,
+                                           ctypes.byref(ix)))
+            assert cur() == start, ("index_create", start)
+            out = ctypes.c_void_p()
+            check(lib.sydelta_match_device(ix, vp(src), L, None, ctypes.byref(out)))
+            assert cur() == start, ("match", start)
+            lib.sydelta_delta_free(out)
+            lib.sydelta_index_free(ix)
+            assert cur() == start, ("index_free", start)
+            check(lib.sydelta_set_thread_device(other))
+            from sy_amd._lib import BlockChecksumC
+
+            ck = ctypes.POINTER(BlockChecksumC)()
+            nck = ctypes.c_uint64()
+            check(lib.sydelta_compute_checksums(pb.encode(), bs, ctypes.byref(ck), ctypes.byref(nck)))
+            assert cur() == start, ("compute_checksums", start)
+            h = ctypes.c_void_p()
+            check(lib.sydelta_generate_delta_streaming(ps.encode(), ck, nck.value, bs, ctypes.byref(h)))
+            assert cur() == start, ("generate_delta_streaming", start)
+            lib.sydelta_delta_free(h)
+            lib.sydelta_checksums_free(ctypes.cast(ck, ctypes.c_void_p))
+            check(lib.sydelta_set_thread_device(-1))
+            lib.sydelta_trim()
+            assert cur() == start, ("trim", start)
+            bb = np.zeros(basis.size + 64, np.uint8)
+            bb[:basis.size] = basis
+            sb = np.zeros(L + 64, np.uint8)
+            sb[:L] = src
+            devs = [3, 1, 0, 2]
+            bpos = [0, 5 * bs, 10 * bs, 15 * bs]
+            blen = [5 * bs, 5 * bs, 5 * bs, basis.size - 15 * bs]
+            sp = [0, 4 * bs, 9 * bs, 14 * bs]
+            slen = [min(L, sp[g + 1] + bs - 1) - sp[g] if g < 3 else L - sp[g] for g in range(4)]
+            out = ctypes.c_void_p()
+            check(lib.sydelta_delta_multi_device((ctypes.c_int * 4)(*devs), 4, vpa([bb.ctypes.data + x for x in bpos]),
+                                                 u64a(blen), vpa([sb.ctypes.data + x for x in sp]), u64a(sp),
+                                                 u64a(slen), L, bs, ctypes.byref(out)))
+            assert cur() == start, ("multi_device", start)
+            lib.sydelta_delta_free(out)
+            # an argument error after validation of the devices
+            rc = lib.sydelta_delta_multi_device((ctypes.c_int * 2)(other, start), 2,
+                                                vpa([bb.ctypes.data, bb.ctypes.data + 500]), u64a([500, 4620]),
+                                                vpa([sb.ctypes.data, sb.ctypes.data]), u64a([0, 512]),
+                                                u64a([1023, 4608]), 5120, bs, ctypes.byref(out))
+            assert rc == -3 and cur() == start, ("multi_device error", start)
+            n += 1
+    assert lib.hipSetDevice(0) == 0
+    return n
 
 
 if __name__ == "__main__":

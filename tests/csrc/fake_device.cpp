@@ -572,6 +572,91 @@ hipError_t launch_chain(const chain::ChainArgs& a, hipStream_t, Profiler*) {
     return hipSuccess;
 }
 
+// K10: each file's greedy walk (generator.rs:116-221) with every visited window classified
+// exactly, its ops run-length coded as k_walk_files writes them (WalkRec), files placed in
+// order in the compact output.
+hipError_t launch_walk_files(const WalkArgs& a, hipStream_t, Profiler*) {
+    EmuTimer emu_t;
+    if (a.n % 64 != 0 || a.n < 256 || a.n > kWalkMaxN || a.fw_max > kWalkMaxWords) return hipErrorInvalidValue;
+    DeviceIndex key_ix;
+    key_ix.keys = (uint32_t*)a.keys;
+    const FakeIndex& F = find_ix(key_ix);
+    const uint64_t n = a.n;
+    uint64_t placed = *a.total;
+    for (uint32_t f = 0; f < a.nfiles; ++f) {
+        const uint8_t* src = a.base + a.soff[f];
+        const uint64_t len = a.slen[f], gb0 = a.fblk[f], nbf = a.fblk[f + 1] - gb0, ls = a.last_size[f];
+        const uint64_t p1 = (nbf && len >= n) ? len - n + 1 : 0;
+        std::vector<WalkRec> rec;
+        uint32_t ck = 0, ca = 0, weak_hits = 0, hits = 0;
+        auto close_run = [&] {
+            if (ck) rec.push_back({ck, ca, 0});
+            ck = 0;
+        };
+        auto data = [&](uint64_t lo, uint64_t hi) {
+            if (hi > lo) {
+                close_run();
+                rec.push_back({0, (uint32_t)(hi - lo), lo});
+            }
+        };
+        auto copy = [&](uint32_t g) {
+            if (ck && g == ca + ck) {
+                ++ck;
+            } else {
+                close_run();
+                ck = 1;
+                ca = g;
+            }
+        };
+        uint64_t wa = 0, wb = 0, wpos = UINT64_MAX;  // rolling Adler state of the window at wpos
+        auto classify = [&](uint64_t x) {
+            if (wpos != UINT64_MAX && x == wpos + 1) {
+                const uint64_t out = src[wpos], in = src[wpos + n];
+                wa = (wa + 2 * kMod - out + in) % kMod;
+                wb = (wb + 3 * kMod - (n * out) % kMod + wa - 1) % kMod;
+            } else {
+                const uint32_t w = adler(src + x, n);
+                wa = w & 0xFFFF;
+                wb = w >> 16;
+            }
+            wpos = x;
+            bool wh = false;
+            const uint32_t blk = lookup(F, f, (uint32_t)((wb << 16) | wa), src + x, n, &wh);
+            weak_hits += wh;
+            return blk;
+        };
+        uint64_t x = 0, lit = 0;
+        while (x < p1) {
+            const uint32_t blk = classify(x);
+            if (blk != kNone) {
+                ++hits;
+                data(lit, x);
+                copy(blk);
+                x += n;
+                lit = x;
+            } else {
+                ++x;
+            }
+        }
+        if (nbf && ls < n && len >= ls && len - ls >= lit && adler(src + len - ls, ls) == a.weak[gb0 + nbf - 1] &&
+            oracle_xxh3_64(src + len - ls, ls) == a.strong[gb0 + nbf - 1]) {
+            data(lit, len - ls);
+            copy((uint32_t)(gb0 + nbf - 1));
+            lit = len;
+            ++hits;
+        }
+        data(lit, len);
+        close_run();
+        const uint64_t cap = 2 * (len / n) + 4;
+        if (rec.size() > cap) return hipErrorInvalidValue;  // the kernel's staging region would overflow
+        std::copy(rec.begin(), rec.end(), a.out + placed);
+        a.fout[f] = WalkFileOut{(uint32_t)placed, (uint32_t)rec.size(), weak_hits, hits};
+        placed += rec.size();
+    }
+    *a.total = placed;
+    return hipSuccess;
+}
+
 // zstd blocks: the sequential form of k_zstd_block (sydelta_zstd.hpp block_content_seq)
 hipError_t zstd_phase_ticks(unsigned long long* out) {
     for (int i = 0; i < 16; ++i) out[i] = 0;

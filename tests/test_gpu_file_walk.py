@@ -1,0 +1,170 @@
+"""GPU parity of K10 (k_walk_files): the greedy walk of each file of a batch resolved on
+the device, one workgroup per file (generator.rs:116-221, the tail rule :156-184).
+
+Every case runs through the C ABI with SYDELTA_FILE_WALK=1 (the file walk for any batch
+it can serve) and is compared op for op with the C oracle; the same batches with
+SYDELTA_FILE_WALK=0 (the classifier path) must give the same lists."""
+import random
+
+import numpy as np
+import pytest
+
+from oracle import oracle as O
+
+pytestmark = pytest.mark.gpu
+
+
+def _oracle_ops(oracle_c, src, basis, bs):
+    w, s, z = oracle_c.compute_checksums(basis, bs)
+    return O.ops_from_arrays(*oracle_c.generate_delta(src, w, s, z, bs))
+
+
+def _pack(parts):
+    import torch
+
+    offs, pos = [], 0
+    for p in parts:
+        offs.append(pos)
+        pos += (len(p) + 15) & ~15
+    host = bytearray(pos + 16)
+    for o, p in zip(offs, parts):
+        host[o:o + len(p)] = p
+    buf = torch.frombuffer(host, dtype=torch.uint8).cuda()
+    return buf, np.array(offs, np.uint64), np.array([len(p) for p in parts], np.uint64)
+
+
+def _batch(gpu, pairs, bs, walk, monkeypatch):
+    """Batched signature + index + match of (src, basis) pairs; walk: SYDELTA_FILE_WALK."""
+    monkeypatch.setenv("SYDELTA_FILE_WALK", walk)
+    bbuf, boff, blen = _pack([b for _, b in pairs])
+    sbuf, soff, slen = _pack([s for s, _ in pairs])
+    w, s = gpu.signature_batch(bbuf, boff, blen, bs)
+    nblk = [-(-int(x) // bs) for x in blen]
+    last = [int(x) - (k - 1) * bs if k else 0 for x, k in zip(blen, nblk)]
+    idx = gpu.BatchIndex(w, s, nblk, last, bs)
+    gpu.set_profiling(True)
+    gpu.profile(reset=True)
+    out, tot = gpu.match_batch(idx, sbuf, soff, slen)
+    prof = gpu.profile(reset=True)
+    gpu.set_profiling(False)
+    idx.close()
+    return out, tot, prof
+
+
+def _mutate(data: bytes, rng, nops: int) -> bytes:
+    b = bytearray(data)
+    for _ in range(nops):
+        k = rng.randrange(5)
+        p = rng.randrange(len(b) + 1) if b else 0
+        if k == 0 and b:  # substitution
+            b[min(p, len(b) - 1)] ^= rng.randrange(1, 256)
+        elif k == 1:  # insertion
+            b[p:p] = rng.randbytes(rng.randint(1, 40))
+        elif k == 2 and b:  # deletion
+            del b[p:p + rng.randint(1, 40)]
+        elif k == 3 and len(b) > 64:  # duplication of a run
+            q = rng.randrange(len(b) - 32)
+            b[p:p] = b[q:q + rng.randint(1, 5000)]
+        else:  # block-sized move
+            q = rng.randrange(len(b) + 1)
+            b[p:p] = b[q:q + 4096]
+    return bytes(b)
+
+
+def _cases(rng, bs, nfiles):
+    pairs = []
+    for i in range(nfiles):
+        kind = i % 10
+        if kind == 0:  # empty source
+            basis, src = rng.randbytes(rng.randint(0, 3 * bs)), b""
+        elif kind == 1:  # empty basis: one Data op
+            basis, src = b"", rng.randbytes(rng.randint(1, 3 * bs))
+        elif kind == 2:  # the tail rule: the basis's partial last block at the source's end
+            basis = rng.randbytes(rng.randint(1, 6) * bs + rng.randint(1, bs - 1))
+            src = rng.randbytes(rng.randint(0, bs)) + basis[-(len(basis) % bs):]
+        elif kind == 3:  # a source shorter than a block, equal to the basis
+            basis = rng.randbytes(rng.randint(1, bs - 1))
+            src = basis
+        elif kind == 4:  # periodic data: weak hits at many positions, duplicate keys
+            pat = rng.randbytes(rng.choice([1, 3, 64, 100]))
+            basis = (pat * (40 * bs // len(pat) + 1))[:rng.randint(bs, 40 * bs)]
+            src = _mutate(basis, rng, 4)
+        elif kind == 5:  # zeros with a few bytes set
+            basis = bytearray(rng.randint(bs, 20 * bs))
+            for _ in range(3):
+                basis[rng.randrange(len(basis))] = rng.randrange(256)
+            basis = bytes(basis)
+            src = _mutate(basis, rng, 3)
+        elif kind == 6:  # the C4 edit shape: one inserted byte + 16 substitutions
+            basis = rng.randbytes(rng.randint(8, 64) * bs)
+            s = bytearray(basis)
+            p = rng.randrange(len(s) + 1)
+            s[p:p] = bytes([rng.randrange(256)])
+            for _ in range(16):
+                s[rng.randrange(len(s))] ^= rng.randrange(1, 256)
+            src = bytes(s)
+        elif kind == 7:  # low alphabet
+            basis = bytes(rng.randrange(2) for _ in range(rng.randint(bs, 12 * bs)))
+            src = _mutate(basis, rng, 6)
+        else:  # random edits
+            basis = rng.randbytes(rng.randint(bs, 40 * bs))
+            src = _mutate(basis, rng, 10)
+        pairs.append((src, basis))
+    return pairs
+
+
+@pytest.mark.parametrize("bs", [256, 320, 1024, 4096, 8192])
+def test_file_walk_matches_oracle(gpu, oracle_c, monkeypatch, bs):
+    rng = random.Random(1000 + bs)
+    pairs = _cases(rng, bs, 80)
+    out, tot, prof = _batch(gpu, pairs, bs, "1", monkeypatch)
+    assert "k_walk_files" in prof, prof
+    for i, ((src, basis), d) in enumerate(zip(pairs, out)):
+        assert d.tuples() == _oracle_ops(oracle_c, src, basis, bs), (bs, i)
+        assert d.source_size == len(src) and d.block_size == bs
+    assert tot["copy_ops"] == sum(d.stats["copy_ops"] for d in out)
+    assert tot["literal_bytes"] == sum(d.stats["literal_bytes"] for d in out)
+    # the classifier path gives the same lists
+    out0, _, prof0 = _batch(gpu, pairs, bs, "0", monkeypatch)
+    assert "k_walk_files" not in prof0
+    assert [d.tuples() for d in out0] == [d.tuples() for d in out]
+
+
+def test_file_walk_c4_shape_1mib(gpu, oracle_c, monkeypatch):
+    """BASELINE C4's files (1 MiB, one inserted byte + 16 substitutions), 128 of them,
+    through the default (auto) selection."""
+    rng = random.Random(4404)
+    pairs = []
+    for f in range(128):
+        basis = O.synth_bytes(1 << 20, 0x5E1D0004 + f).tobytes()
+        s = bytearray(basis)
+        p = rng.randrange(len(s) + 1)
+        s[p:p] = bytes([rng.randrange(256)])
+        for _ in range(16):
+            s[rng.randrange(len(s))] ^= rng.randrange(1, 256)
+        pairs.append((bytes(s), basis))
+    monkeypatch.delenv("SYDELTA_FILE_WALK", raising=False)
+    out, _, prof = _batch(gpu, pairs, 4096, "", monkeypatch)
+    assert "k_walk_files" in prof
+    for f, ((src, basis), d) in enumerate(zip(pairs, out)):
+        assert d.tuples() == _oracle_ops(oracle_c, src, basis, 4096), f
+
+
+def test_file_walk_long_literal_runs(gpu, oracle_c, monkeypatch):
+    """Sources with long unmatched runs (several roll passes of 4096 starts between hits
+    at bs 8192), matches at every phase, and blocks repeated so that later candidates in
+    index order share the weak value."""
+    rng = random.Random(77)
+    bs = 8192
+    pairs = []
+    for i in range(16):
+        blocks = [rng.randbytes(bs) for _ in range(12)]
+        basis = b"".join(blocks + blocks[:3])  # duplicate blocks: the lowest index wins
+        src = bytearray()
+        for j in range(10):
+            src += rng.randbytes(rng.randint(0, 3 * bs))  # a literal run
+            src += blocks[rng.randrange(12)]
+        pairs.append((bytes(src), basis))
+    out, _, _ = _batch(gpu, pairs, bs, "1", monkeypatch)
+    for i, ((src, basis), d) in enumerate(zip(pairs, out)):
+        assert d.tuples() == _oracle_ops(oracle_c, src, basis, bs), i

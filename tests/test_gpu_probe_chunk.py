@@ -391,6 +391,7 @@ def test_phase_probe_batch_c4_shape(gpu, oracle_c, monkeypatch):
     import torch
 
     monkeypatch.setenv("SYDELTA_PROBE", "1")
+    monkeypatch.setenv("SYDELTA_FILE_WALK", "0")  # the classifier's phase probe, not K10
     bs = 4096
     rng = random.Random(44)
     bases, news = [], []
