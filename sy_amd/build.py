@@ -13,7 +13,7 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 ROOT = os.path.dirname(HERE)
 CSRC = os.path.join(HERE, "csrc")
 LIB = os.path.join(HERE, "libsydelta.so")
-SOURCES = ["sydelta_kernels.hip", "sydelta_api.cpp", "sydelta_wire.cpp", "sydelta_local.cpp", "sydelta_integrity.cpp"]
+SOURCES = ["sydelta_kernels.hip", "sydelta_filewalk.hip", "sydelta_api.cpp", "sydelta_wire.cpp", "sydelta_local.cpp", "sydelta_integrity.cpp"]
 HEADERS = sorted(f for f in os.listdir(CSRC) if f.endswith(".hpp")) + [os.path.join("..", "..", "include", "sydelta.h")]
 # objects stay in build/obj (the host sanitizer test links sydelta_kernels.o)
 OBJDIR = os.path.join(ROOT, "build", "obj")
@@ -34,11 +34,16 @@ def build(force: bool = False, verbose: bool = False) -> str:
     objs = []
     jobs = []
     os.makedirs(OBJDIR, exist_ok=True)
+    # an object is rebuilt when its source, or any header, is newer (or on --force)
+    t_hdr = max(os.path.getmtime(os.path.join(CSRC, h)) for h in HEADERS)
     for src in SOURCES:
         obj = os.path.join(OBJDIR, src.rsplit(".", 1)[0] + ".o")
+        objs.append(obj)
+        if not force and os.path.exists(obj) and os.path.getmtime(obj) >= max(t_hdr, os.path.getmtime(
+                os.path.join(CSRC, src))):
+            continue
         cmd = [hipcc, f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-Wall", "-Wno-unused-result",
                "-I", os.path.join(ROOT, "include"), "-x", "hip", "-c", os.path.join(CSRC, src), "-o", obj]
-        objs.append(obj)
         jobs.append(subprocess.Popen(cmd, stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True))
     for j in jobs:
         out, _ = j.communicate()

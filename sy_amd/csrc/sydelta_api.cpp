@@ -191,6 +191,12 @@ std::vector<hipEvent_t>& event_pool() {
 std::vector<Profiler::Pending> g_deferred;                  // under g_prof_mu
 std::map<int, std::vector<hipEvent_t>> g_free_events;       // under g_prof_mu
 constexpr size_t kDeferredMax = 1 << 14;                     // beyond: resolve on the spot
+// Each device's timed launches as intervals on one time line (relative to the first
+// launch resolved since the last reset, whose start event is kept as the origin): their
+// union is the time the device spent in timed kernels, which per-launch times overstate
+// when launches of several callers' streams overlap (sydelta_profile_json's "__busy__").
+std::map<int, hipEvent_t> g_origin;                                  // under g_prof_mu
+std::map<int, std::vector<std::pair<double, double>>> g_intervals;   // under g_prof_mu
 // Resolve the entries of v (all, waiting on their events; or, with only_done, those whose
 // end event has completed, so a long profiled run keeps recycling its events).
 void resolve_locked(std::vector<Profiler::Pending>& v, bool only_done = false) {
@@ -203,16 +209,55 @@ void resolve_locked(std::vector<Profiler::Pending>& v, bool only_done = false) {
             continue;
         }
         float ms = 0;
+        bool origin = false;
         if (hipEventSynchronize(q.b) == hipSuccess && hipEventElapsedTime(&ms, q.a, q.b) == hipSuccess) {
             auto& e = g_prof[q.name];
             e.first += ms;
             e.second += 1;
+            hipEvent_t& o = g_origin[q.device];
+            if (!o) {
+                o = q.a;
+                origin = true;
+            }
+            float t0 = 0;
+            if (hipEventElapsedTime(&t0, o, q.a) == hipSuccess) g_intervals[q.device].push_back({t0, t0 + ms});
         }
         auto& fl = g_free_events[q.device];
-        fl.push_back(q.a);
+        if (!origin) fl.push_back(q.a);
         fl.push_back(q.b);
     }
     v.resize(keep);
+}
+// union length and span of the intervals of every device (ms)
+std::pair<double, double> busy_locked(size_t* count) {
+    double busy = 0, span = 0;
+    *count = 0;
+    for (auto& kv : g_intervals) {
+        auto iv = kv.second;
+        *count += iv.size();
+        if (iv.empty()) continue;
+        std::sort(iv.begin(), iv.end());
+        double lo = iv[0].first, hi = iv[0].second, first = lo, last = hi;
+        for (auto& x : iv) {
+            last = std::max(last, x.second);
+            if (x.first > hi) {
+                busy += hi - lo;
+                lo = x.first;
+                hi = x.second;
+            } else {
+                hi = std::max(hi, x.second);
+            }
+        }
+        busy += hi - lo;
+        span += last - first;
+    }
+    return {busy, span};
+}
+void reset_intervals_locked() {
+    for (auto& kv : g_origin)
+        if (kv.second) g_free_events[kv.first].push_back(kv.second);
+    g_origin.clear();
+    g_intervals.clear();
 }
 hipEvent_t take_event() {
     auto& pool = event_pool();
@@ -274,7 +319,18 @@ extern "C" size_t sydelta_profile_json(char* buf, size_t cap, int reset) {
             s += tmp;
             first = false;
         }
-        if (reset) g_prof.clear();
+        size_t nint = 0;
+        const auto bs = sydelta::busy_locked(&nint);
+        if (nint) {  // the union of the timed launches (not a kernel)
+            char tmp[256];
+            snprintf(tmp, sizeof tmp, "%s\"__busy__\": {\"ms\": %.6f, \"count\": %llu, \"span_ms\": %.6f}",
+                     first ? "" : ", ", bs.first, (unsigned long long)nint, bs.second);
+            s += tmp;
+        }
+        if (reset) {
+            g_prof.clear();
+            sydelta::reset_intervals_locked();
+        }
     }
     s += "}";
     if (buf && cap > s.size()) memcpy(buf, s.c_str(), s.size() + 1);
@@ -2131,6 +2187,7 @@ static int match_walk_files(sydelta_index* ix, const uint8_t* d_buf, const uint6
         rec_total += 2 * (src_len[f] / n) + 4;
     }
     auto al = [](size_t v) { return (v + 255) & ~(size_t)255; };
+    // o_total: the record counter (8 B) and SYDELTA_PHASE_TIMING's 16 tick counters
     const size_t o_tab = 0, o_fout = o_tab + al(tbytes), o_total = o_fout + al(fout_bytes), o_stage = o_total + 256;
     const size_t o_out = o_stage + al(sizeof(WalkRec) * rec_total), need = o_out + al(sizeof(WalkRec) * rec_total);
     DevScratch& sc = thread_walk_scratch(cur_dev);
@@ -2142,7 +2199,8 @@ static int match_walk_files(sydelta_index* ix, const uint8_t* d_buf, const uint6
     }
     uint8_t* D = (uint8_t*)sc.p;
     HIP_TRY(hipMemcpyAsync(D + o_tab, T, tbytes, hipMemcpyHostToDevice, s));
-    HIP_TRY(hipMemsetAsync(D + o_total, 0, 8, s));
+    static const bool timing = getenv("SYDELTA_PHASE_TIMING") != nullptr;
+    HIP_TRY(hipMemsetAsync(D + o_total, 0, timing ? 8 + 128 : 8, s));
     WalkArgs a{};
     a.base = d_buf;
     a.soff = (const uint64_t*)(D + o_tab);
@@ -2167,7 +2225,16 @@ static int match_walk_files(sydelta_index* ix, const uint8_t* d_buf, const uint6
     a.out = (WalkRec*)(D + o_out);
     a.fout = (WalkFileOut*)(D + o_fout);
     a.total = (unsigned long long*)(D + o_total);
+    a.ticks = timing ? a.total + 1 : nullptr;
     HIP_TRY(launch_walk_files(a, s, prof));
+    if (timing) {
+        unsigned long long tk[16];
+        HIP_TRY(hipMemcpyAsync(tk, a.ticks, sizeof tk, hipMemcpyDeviceToHost, s));
+        HIP_TRY(hipStreamSynchronize(s));
+        fprintf(stderr, "sydelta file walk phases (thread 0 ticks, 100 MHz, summed over files): setup %llu hash %llu "
+                "lookup %llu stage %llu roll %llu verify %llu out %llu | passes %llu windows %llu rolls %llu "
+                "verify batches %llu\n", tk[0], tk[1], tk[2], tk[3], tk[4], tk[5], tk[6], tk[8], tk[9], tk[10], tk[11]);
+    }
     // the host table in ph is dead once the upload ran: the counts come back over it
     WalkFileOut* fo = (WalkFileOut*)ph.p;
     uint64_t* tot = (uint64_t*)(ph.p + fout_bytes);

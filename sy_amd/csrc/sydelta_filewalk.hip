@@ -1,0 +1,420 @@
+// sydelta_filewalk.hip — K10, the whole greedy walk of each file of a batch on the device
+// (C4's batched small files).  Its own translation unit: the shared device code comes from
+// sydelta_kcommon.hpp.
+#include "sydelta_device.hpp"
+#include "sydelta_internal.hpp"
+
+namespace sydelta {
+
+#include "sydelta_kcommon.hpp"
+
+// ===========================================================================
+// K10: the greedy walk of many small files, one wave per file (C4)
+// ===========================================================================
+// The batched match used to classify on the device in five host-synchronised phases
+// (aligned probe, miss ranges, scans, phase probe, scans of the missed blocks) and walk on
+// host threads.  Here one wave walks its file itself (generator.rs:116-221), classifying
+// only the window starts the walk visits:
+//   * the walk at x on the phase grid k*n + phi: the phase windows of the next blocks are
+//     hashed four at a time, one 16-lane row each (row_hash, the signature kernel's layout),
+//     and looked up one per lane (first candidate in index order with equal strong,
+//     generator.rs:121-155); a hit copies and moves x by n, so the walk stays on the grid;
+//   * a miss at x: the window starts (x, x + n) are rolled (rolling.rs:66-79), 64 per lane
+//     from the closed form of their first window (wave scans of the lanes' 64-byte group
+//     sums), tested against the file's Bloom filter in LDS; the passes are hashed four at
+//     a time in position order and the first verified one is the walk's next hit (a Copy,
+//     then a new phase grid); without one the walk continues at x + n, the next phase window.
+// A copy-heavy file costs one window hash per block plus one roll of n starts per edited
+// block, and a shift (an insertion or deletion) one new phase grid.  A wave per file keeps
+// the walk's steps free of workgroup barriers, and a CU holds as many files as waves (the
+// first form, a workgroup of four waves per file, spent half its time waiting at barriers:
+// 5.28 ms for C4's 10 000 files, `profiles/r05d_*`).  The ops are written run-length coded
+// (WalkRec) to the file's staging region, then moved to the compact output with one atomic
+// per file.
+constexpr uint32_t kWRun = 64;          // window starts per lane per roll pass
+constexpr uint32_t kWSub = 64 * kWRun;  // window starts per roll pass (4096)
+constexpr uint32_t kWMaxPass = 64;      // phase windows per pass at most (one lookup per lane)
+
+struct WalkLds {  // byte offsets of the dynamic LDS (one wave per workgroup)
+    uint32_t filt, ntab, pw, pst, total;
+};
+__host__ __device__ __forceinline__ WalkLds walk_lds(uint32_t fw) {
+    WalkLds L{};
+    uint32_t o = 0;
+    L.filt = o; o += 4 * fw;
+    L.ntab = o; o += 1024;
+    L.pw = o; o += 4 * kWMaxPass;   // a pass's weak values
+    L.pst = o; o += 8 * kWMaxPass;  // ... and strong hashes
+    L.total = o;
+    return L;
+}
+// SYDELTA_PHASE_TIMING (WalkArgs::ticks): wall-clock ticks of each wave, summed
+constexpr int kWtSetup = 0, kWtHash = 1, kWtLookup = 2, kWtStage = 3, kWtRoll = 4, kWtVerify = 5, kWtOut = 6;
+constexpr int kWtPasses = 8, kWtWindows = 9, kWtRolls = 10, kWtVerifies = 11;
+
+// 64 bytes of the file at byte offset off (any alignment) as 16 dwords: four dword-aligned
+// 16-byte loads and one dword, funnel-shifted; near the end (where those dwords could leave
+// the readable granules, sydelta.h) byte by byte, bytes at or past len read as 0.
+__device__ __forceinline__ void load64_any(const uint8_t* src, uint64_t len, uint64_t off, uint32_t (&x)[16]) {
+    const uint64_t a4 = off & ~3ull;
+    const uint32_t sh = (uint32_t)(off & 3);
+    if (a4 + 68 <= ((len + 15) & ~15ull)) {
+        const uint32_t* w = (const uint32_t*)(src + a4);
+        uint32_t d[17];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            u32x4 v;
+            __builtin_memcpy(&v, w + 4 * i, 16);
+            d[4 * i] = v.x;
+            d[4 * i + 1] = v.y;
+            d[4 * i + 2] = v.z;
+            d[4 * i + 3] = v.w;
+        }
+        d[16] = sh ? w[16] : 0u;
+#pragma unroll
+        for (int i = 0; i < 16; ++i) x[i] = __builtin_amdgcn_alignbyte(d[i + 1], d[i], sh);
+        return;
+    }
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+        uint32_t v = 0;
+        for (int j = 0; j < 4; ++j) {
+            const uint64_t p = off + 4 * i + j;
+            if (p < len) v |= (uint32_t)src[p] << (8 * j);
+        }
+        x[i] = v;
+    }
+}
+
+// First candidate in index order of file F with weak wk and strong st (generator.rs:127-133),
+// or kNoBlock; one lane.
+__device__ __forceinline__ uint32_t walk_lookup(const WalkArgs& a, const FileIx& F, uint32_t wk, uint64_t st) {
+    const int64_t slot = table_find(a.keys + F.slot_off, F.bmask, wk);
+    if (slot < 0) return kNoBlock;
+    const uint64_t gs = F.slot_off + (uint64_t)slot;
+    const uint32_t s0 = a.start[gs], c = a.cnt[gs];
+    for (uint32_t j = 0; j < c; ++j)
+        if (a.cstrong[s0 + j] == st) return a.order[s0 + j];
+    return kNoBlock;
+}
+
+// One window per row (row_hash's contract).  Issuing all four pieces' loads of a 4 KiB
+// window at once (one round trip instead of four) took 64 more VGPRs: two waves per SIMD
+// instead of four, and the walk 5.09 ms instead of 3.59 at C4 (`profiles/r05f_*`).
+template <bool kAligned>
+__device__ __forceinline__ void walk_hash(const uint8_t* p, uint32_t n, uint32_t& wk, uint64_t& st) {
+    row_hash<kAligned>(p, n, wk, st);
+}
+
+__device__ __forceinline__ uint32_t rl(uint32_t v, uint32_t lane) {
+    return (uint32_t)__builtin_amdgcn_readlane((int)v, (int)lane);
+}
+
+// The suffix p[0, ls) hashes to (weak, strong): the whole wave calls; every lane returns it.
+__device__ __forceinline__ bool tail_matches(const uint8_t* p, uint64_t ls, uint32_t weak, uint64_t strong) {
+    uint32_t wk = 0;
+    uint64_t st = 0;
+    if (ls > 240) {
+        wave_hash_long(p, ls, wk, st);
+    } else if ((threadIdx.x & 63) == 0) {
+        wk = adler_scalar(p, ls);
+        st = xxh3_short(p, ls);
+    }
+    return __builtin_amdgcn_readlane((int)(wk == weak && st == strong ? 1u : 0u), 0) != 0;
+}
+
+__global__ __launch_bounds__(64) void k_walk_files(WalkArgs a) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    const uint32_t f = blockIdx.x;
+    const uint32_t lane = threadIdx.x, row = lane >> 4;
+    const uint32_t n = a.n;
+    const FileIx F = a.files[f];
+    const uint32_t fw = 1u << (32 - F.fwshift);
+    const WalkLds L = walk_lds(a.fw_max);
+    uint32_t* filt = (uint32_t*)(smem + L.filt);
+    uint32_t* ntab = (uint32_t*)(smem + L.ntab);
+    uint32_t* pw = (uint32_t*)(smem + L.pw);
+    uint64_t* pst = (uint64_t*)(smem + L.pst);
+    uint64_t tlast = a.ticks ? wall_clock64() : 0;
+    auto wtick = [&](int k) {  // SYDELTA_PHASE_TIMING: the wave's time since the last tick into ticks[k]
+        if (a.ticks && lane == 0) {
+            const uint64_t t = wall_clock64();
+            atomicAdd(a.ticks + k, (unsigned long long)(t - tlast));
+            tlast = t;
+        }
+    };
+    auto wcount = [&](int k, uint64_t v) {
+        if (a.ticks && lane == 0) atomicAdd(a.ticks + k, (unsigned long long)v);
+    };
+    const uint8_t* src = a.base + a.soff[f];
+    const uint64_t len = a.slen[f];
+    const uint64_t gb0 = a.fblk[f], nbf = a.fblk[f + 1] - gb0, ls = a.last_size[f];
+    const uint64_t p1 = (nbf && len >= n) ? len - n + 1 : 0;  // full-window starts [0, p1)
+
+    {  // the file's Bloom filter, the roll table
+        const uint4* g = (const uint4*)(a.filt + F.filt_off);
+        for (uint32_t i = lane; i < fw / 4; i += 64) ((uint4*)filt)[i] = g[i];
+        for (uint32_t i = lane; i < 256; i += 64) ntab[i] = kMod - 1 - (a.nm * i) % kMod;
+    }
+    // the tail rule (generator.rs:156-184): the suffix of the basis's last block's size
+    const bool tail_ok = nbf && ls < n && len >= ls &&
+                         tail_matches(src + (len - ls), ls, a.weak[gb0 + nbf - 1], a.strong[gb0 + nbf - 1]);
+    __syncthreads();  // the filter and ntab in LDS
+    wtick(kWtSetup);
+
+    // run-length coded output (lane 0 writes; the state is wave-uniform)
+    WalkRec* stg = a.stage + a.rec_off[f];
+    uint32_t nrec = 0, ck = 0, ca = 0;  // the open Copy run: ck Copies from block ca (ck 0: none)
+    auto put = [&](uint32_t kind, uint32_t aa, uint64_t off) {
+        if (lane == 0) stg[nrec] = WalkRec{kind, aa, off};
+        ++nrec;
+    };
+    auto close_run = [&]() {
+        if (ck) put(ck, ca, 0);
+        ck = 0;
+    };
+    auto data = [&](uint64_t lo, uint64_t hi) {
+        if (hi > lo) {
+            close_run();
+            put(0, (uint32_t)(hi - lo), lo);
+        }
+    };
+    auto copy = [&](uint32_t g) {
+        if (ck && g == ca + ck) {
+            ++ck;
+        } else {
+            close_run();
+            ck = 1;
+            ca = g;
+        }
+    };
+    uint32_t weak_hits = 0, hits = 0;
+
+    uint64_t x = 0, lit = 0;
+    uint32_t phi = 0xFFFFFFFFu;
+    uint64_t rk0 = 0, rk1 = 0;  // lane w holds the result (rres) and weak (rwk) of block rk0 + w at phase phi
+    uint64_t kph = 0;           // the block where the walk took phase phi
+    uint32_t rres = kNoBlock, rwk = 0;
+#pragma unroll 1
+    while (x < p1) {
+        const uint64_t k = x / n;
+        const uint32_t ph = (uint32_t)(x - k * n);
+        if (ph != phi || k >= rk1) {
+            // ---- phase pass: windows (k + w) n + ph, w < cnt, four per row_hash round.  The
+            // passes of one phase grow (4, then twice the blocks walked at this phase, up to
+            // 64): a long run of Copies costs few passes, and a phase change soon after a pass
+            // began wastes little of it.
+            if (ph != phi) kph = k;
+            const uint64_t left = (p1 - x + n - 1) / n;
+            const uint32_t cnt = (uint32_t)min(left, min((uint64_t)kWMaxPass, max((uint64_t)4, 2 * (k - kph))));
+#pragma unroll 1
+            for (uint32_t j = 0; j < cnt; j += 4) {
+                const uint32_t w = j + row;
+                const uint64_t pos = (k + (w < cnt ? w : j)) * n + ph;
+                uint32_t wk;
+                uint64_t st;
+                if ((ph & 15) == 0)
+                    walk_hash<true>(src + pos, n, wk, st);
+                else
+                    walk_hash<false>(src + pos, n, wk, st);
+                if ((lane & 15) == 0 && w < cnt) {
+                    pw[w] = wk;
+                    pst[w] = st;
+                }
+            }
+            wtick(kWtHash);
+            __syncthreads();  // the rows' results to the lanes
+            rres = kNoBlock;
+            rwk = 0;
+            if (lane < cnt) {  // lookups (generator.rs:121-155), one window per lane
+                rwk = pw[lane];
+                const ProbeHash h = probe_hash(rwk);
+                if (filt_pass(filt[h.r >> F.fwshift], h.q)) rres = walk_lookup(a, F, rwk, pst[lane]);
+            }
+            __syncthreads();  // pw / pst are rewritten by the next pass
+            wtick(kWtLookup);
+            wcount(kWtPasses, 1);
+            wcount(kWtWindows, cnt);
+            phi = ph;
+            rk0 = k;
+            rk1 = k + cnt;
+        }
+        const uint32_t blk = rl(rres, (uint32_t)(k - rk0));
+        if (blk != kNoBlock) {  // generator.rs:135-146
+            ++hits;
+            data(lit, x);
+            copy(blk);
+            x += n;
+            lit = x;
+            continue;
+        }
+        // ---- the window at x misses: roll (x, min(x + n, p1)) for the first hit.  A pass
+        // rolls 4096 window starts from the window at its base b = y0 - 1 (the phase window x,
+        // then the previous pass's last start), whose (A, B) it knows: lane l's first start
+        // p = b + d, d = 64 l + 1, follows in closed form (rolling.rs:66-79 applied d times):
+        //   A(p) = A(b) + C(d),  B(p) = B(b) + d (A(b) - 1) + d C(d) - J(d) - n Out(d)  (mod M)
+        // with c_j = in_j - out_j (out_j = byte b + j, in_j = byte b + n + j), C(d) = sum_{j<d} c_j,
+        // J(d) = sum_{j<d} j c_j, Out(d) = sum_{j<d} out_j: exclusive wave scans of the lanes'
+        // 64-byte group sums (as residues mod M), each lane's bytes in registers.
+        const uint64_t yend = min(x + n, p1);
+        uint64_t q = yend;
+        uint32_t qb = kNoBlock;
+        uint32_t wbase = rl(rwk, (uint32_t)(k - rk0));  // weak of the window at b
+#pragma unroll 1
+        for (uint64_t y0 = x + 1; y0 < yend && qb == kNoBlock; y0 += kWSub) {
+            const uint64_t y1 = min(y0 + kWSub, yend);
+            const uint64_t b = y0 - 1;
+            wcount(kWtRolls, 1);
+            uint32_t xo[16], xi[16];  // out [b + 64l, +64), in [b + n + 64l, +64)
+            load64_any(src, len, b + 64ull * lane, xo);
+            load64_any(src, len, b + n + 64ull * lane, xi);
+            uint32_t so = 0, si = 0, vo = 0, vi = 0;
+#pragma unroll
+            for (int i = 0; i < 16; ++i) {
+                so = udot4(xo[i], 0x01010101u, so);
+                si = udot4(xi[i], 0x01010101u, si);
+                vo = udot4(xo[i], offw(i), vo);
+                vi = udot4(xi[i], offw(i), vi);
+            }
+            const uint32_t gc = (si + 2 * kMod - so) % kMod;                                          // sum c
+            const uint32_t gj = (uint32_t)(((uint64_t)(64 * lane) * gc + vi + 16 * kMod - vo) % kMod);  // sum j c
+            uint32_t tt;
+            const uint32_t sC = wave_scan_excl(gc, tt);
+            const uint32_t sJ = wave_scan_excl(gj, tt);
+            const uint32_t sO = wave_scan_excl(so, tt);
+            const uint32_t o0 = xo[0] & 0xFF, i0 = xi[0] & 0xFF;  // byte j = 64 l: the last of the first window's c_j
+            const uint32_t c0 = (i0 + kMod - o0) % kMod;
+            const uint32_t C = (sC % kMod + c0) % kMod;
+            const uint32_t J = (uint32_t)((sJ % kMod + (uint64_t)(64 * lane) * c0) % kMod);
+            const uint32_t Out = (sO + o0) % kMod;
+            const uint64_t d = 64ull * lane + 1;
+            const uint32_t Ab = wbase & 0xFFFFu, Bb = wbase >> 16;
+            uint32_t am = (Ab + C) % kMod;
+            uint32_t bm = (uint32_t)(((uint64_t)Bb + d * ((Ab + kMod - 1) % kMod) % kMod + d * C % kMod + (kMod - J) +
+                                      (kMod - (uint64_t)a.nm * Out % kMod)) % kMod);
+            wtick(kWtStage);
+            // roll the lane's 64 window starts; a start whose weak value passes the Bloom filter
+            // is a candidate
+            const uint64_t p0 = y0 + 64ull * lane;
+            const uint32_t nvalid = p0 >= y1 ? 0u : (uint32_t)min((uint64_t)kWRun, y1 - p0);
+            // the bytes the rolls take out / in: group offsets 1..64 (offset 64 is never used)
+#pragma unroll
+            for (int j = 0; j < 16; ++j) {
+                xo[j] = __builtin_amdgcn_alignbyte(j < 15 ? xo[j + 1] : 0u, xo[j], 1);
+                xi[j] = __builtin_amdgcn_alignbyte(j < 15 ? xi[j + 1] : 0u, xi[j], 1);
+            }
+            uint64_t pm = 0;
+            uint32_t wlast = 0;
+            // four starts per round from the first dword, then the dwords move down one
+            // (a loop, not unrolled: the register arrays keep constant indices)
+#pragma unroll 1
+            for (uint32_t t = 0; t < kWRun / 4; ++t) {
+                const uint32_t wo = xo[0], wi = xi[0];
+#pragma unroll
+                for (int b = 0; b < 4; ++b) {
+                    const uint32_t i = 4 * t + b;
+                    const ProbeHash h = probe_hash(am, bm);
+                    const uint64_t pass = filt_bit(filt[h.r >> F.fwshift], h.q);
+                    pm |= (i < nvalid ? pass : 0ull) << i;
+                    wlast = (bm << 16) | am;
+                    const uint32_t out = (wo >> (8 * b)) & 0xFF;
+                    const uint32_t in = (wi >> (8 * b)) & 0xFF;
+                    const uint32_t u = am + in + (kMod - out);  // [M-255, 2M+255)
+                    am = min(u, min(u - kMod, u - 2 * kMod));
+                    const uint32_t v = bm + am + ntab[out];  // [0, 3M)
+                    bm = min(v, min(v - kMod, v - 2 * kMod));
+                }
+#pragma unroll
+                for (int j = 0; j < 15; ++j) {
+                    xo[j] = xo[j + 1];
+                    xi[j] = xi[j + 1];
+                }
+            }
+            wbase = rl(wlast, 63);  // the next pass's base: lane 63's last start, b + 4096
+            wtick(kWtRoll);
+            // verify the candidates four at a time in position order (generator.rs:121-133);
+            // weak_hits counts the verified windows
+#pragma unroll 1
+            for (;;) {
+                uint32_t cand[4], nc = 0;
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    const uint64_t lm = __ballot(pm != 0);
+                    cand[r] = 0;
+                    if (!lm) continue;
+                    const uint32_t fl = (uint32_t)__builtin_ctzll(lm);
+                    const uint32_t lo = rl((uint32_t)pm, fl), hi = rl((uint32_t)(pm >> 32), fl);
+                    const uint64_t m = ((uint64_t)hi << 32) | lo;
+                    const uint32_t bit = (uint32_t)__builtin_ctzll(m);
+                    cand[r] = 64 * fl + bit;
+                    if (lane == fl) pm &= pm - 1;
+                    ++nc;
+                }
+                if (!nc) break;
+                uint32_t mine = row == 1 ? cand[1] : row == 2 ? cand[2] : row == 3 ? cand[3] : cand[0];
+                if (row >= nc) mine = cand[0];
+                uint32_t wk;
+                uint64_t st;
+                walk_hash<false>(src + y0 + mine, n, wk, st);
+                uint32_t vb = kNoBlock;
+                if ((lane & 15) == 0 && row < nc) vb = walk_lookup(a, F, wk, st);
+                weak_hits += nc;
+                wcount(kWtVerifies, 1);
+                for (uint32_t r = 0; r < nc; ++r) {
+                    const uint32_t bb = rl(vb, 16 * r);
+                    if (bb != kNoBlock) {
+                        q = y0 + cand[r];
+                        qb = bb;
+                        break;
+                    }
+                }
+                if (qb != kNoBlock) break;
+            }
+            wtick(kWtVerify);
+        }
+        if (qb != kNoBlock) {
+            ++hits;
+            data(lit, q);
+            copy(qb);
+            x = q + n;
+            lit = x;
+        } else {
+            x = yend;  // the next phase window (or the end of the full windows)
+        }
+    }
+    // the walk's end: the tail rule at p* = len - last_size, then the last literal run
+    if (tail_ok && ls <= len && len - ls >= lit) {
+        data(lit, len - ls);
+        copy((uint32_t)(gb0 + nbf - 1));
+        lit = len;
+        ++hits;
+    }
+    data(lit, len);
+    close_run();
+    // move the records to the compact output (one atomic per file)
+    __threadfence_block();
+    unsigned long long base = 0;
+    if (lane == 0 && nrec) base = atomicAdd(a.total, (unsigned long long)nrec);
+    base = (uint32_t)rl((uint32_t)base, 0);
+    for (uint32_t i = lane; i < nrec; i += 64) {
+        const volatile WalkRec* r = stg + i;
+        a.out[base + i] = WalkRec{r->kind, r->a, r->off};
+    }
+    if (lane == 0) a.fout[f] = WalkFileOut{(uint32_t)base, nrec, weak_hits, hits};
+    wtick(kWtOut);
+}
+
+// ===========================================================================
+// Launch wrapper
+// ===========================================================================
+hipError_t launch_walk_files(const WalkArgs& a, hipStream_t s, Profiler* prof) {
+    if (!a.nfiles) return hipSuccess;
+    if (a.n % 64 != 0 || a.n < 256 || a.n > kWalkMaxN || a.fw_max > kWalkMaxWords || a.fw_max < 4)
+        return hipErrorInvalidValue;
+    const WalkLds L = walk_lds(a.fw_max);
+    ProfScope ps(prof, s, "k_walk_files");
+    hipLaunchKernelGGL(k_walk_files, dim3(a.nfiles), dim3(64), L.total, s, a);
+    return hipGetLastError();
+}
+
+}  // namespace sydelta

@@ -245,6 +245,7 @@ struct WalkArgs {
     WalkRec* out;                // compacted records of every file
     WalkFileOut* fout;
     unsigned long long* total;   // records placed in out (zeroed before the launch)
+    unsigned long long* ticks;   // SYDELTA_PHASE_TIMING: 16 counters (zeroed), else null
 };
 hipError_t launch_walk_files(const WalkArgs& a, hipStream_t s, Profiler* prof);
 // One slice (<= 64 KiB) of an op for the device apply: out[dst, dst+len) =

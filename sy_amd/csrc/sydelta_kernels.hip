@@ -28,147 +28,12 @@
 
 namespace sydelta {
 
-typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+#include "sydelta_kcommon.hpp"
+
 
 // ===========================================================================
 // K1: signature
 // ===========================================================================
-// Row-per-block form (the production signature kernel): each 16-lane row of a wave
-// hashes its own block, so a 1 KiB piece is reduced inside the row (two DPP
-// rotations) and the accumulate/scramble fold (XXH3 long loop) runs in the row with
-// no cross-row traffic.  Lane (slot, q) of a row takes stripes slot, slot+4,
-// slot+8, slot+12 of each piece (accumulator pair q): a load instruction reads
-// 256 contiguous bytes per row.  The next piece's loads are issued before the
-// current piece is hashed.  bs % 64 == 0, bs >= 256, blocks 16-byte aligned.
-struct RowPiece {
-    uint4 v[4];
-};
-template <bool kAligned = true>
-__device__ __forceinline__ void load_piece(const uint8_t* __restrict__ p, uint32_t slot, uint32_t q, uint32_t lim,
-                                           RowPiece& r) {
-    // bytes [0, lim) of the piece are valid (lim <= 1024, a multiple of 16 here); the
-    // rest reads as zero.  Unaligned pieces: a 4-byte aligned 16-byte load plus one
-    // dword, funnel-shifted (alignbyte) into place.
-#pragma unroll
-    for (int k = 0; k < 4; ++k) {
-        const uint32_t off = ((slot + 4 * k) << 6) + (q << 4);
-        r.v[k] = make_uint4(0, 0, 0, 0);
-        if (off < lim) {
-            if (kAligned) {
-                const u32x4 x = __builtin_nontemporal_load((const u32x4*)(p + off));
-                r.v[k] = make_uint4(x.x, x.y, x.z, x.w);
-            } else {
-                const uintptr_t u = (uintptr_t)(p + off);
-                const uint32_t sh = (uint32_t)(u & 3);
-                const uint32_t* w = (const uint32_t*)(u & ~(uintptr_t)3);
-                u32x4 x;
-                __builtin_memcpy(&x, w, 16);
-                const uint32_t d4 = sh ? w[4] : 0u;
-                r.v[k] = make_uint4(__builtin_amdgcn_alignbyte(x.y, x.x, sh), __builtin_amdgcn_alignbyte(x.z, x.y, sh),
-                                    __builtin_amdgcn_alignbyte(x.w, x.z, sh), __builtin_amdgcn_alignbyte(d4, x.w, sh));
-            }
-        }
-    }
-}
-
-template <bool kLast>
-__device__ __forceinline__ void hash_piece(const RowPiece& r, uint32_t slot, uint32_t q, uint32_t poff, uint32_t bs,
-                                           const uint64_t (&kk0)[4], const uint64_t (&kk1)[4], uint32_t last_k,
-                                           uint32_t last_slot, uint64_t k0l, uint64_t k1l, uint32_t& asum,
-                                           uint32_t& vsum, uint64_t& bpos, uint64_t& c_lo, uint64_t& c_hi) {
-    c_lo = 0;
-    c_hi = 0;
-#pragma unroll
-    for (int k = 0; k < 4; ++k) {
-        const uint4 v = r.v[k];
-        const uint32_t off = poff + ((slot + 4 * k) << 6) + (q << 4);
-        uint32_t s = udot4(v.x, 0x01010101u, 0);
-        s = udot4(v.y, 0x01010101u, s);
-        s = udot4(v.z, 0x01010101u, s);
-        s = udot4(v.w, 0x01010101u, s);
-        uint32_t u = udot4(v.x, 0x03020100u, 0);
-        u = udot4(v.y, 0x07060504u, u);
-        u = udot4(v.z, 0x0B0A0908u, u);
-        u = udot4(v.w, 0x0F0E0D0Cu, u);
-        asum += s;
-        vsum += u;
-        bpos += (uint64_t)(bs - off) * s;  // s == 0 past the end
-        uint64_t k0 = kk0[k], k1 = kk1[k];
-        if (kLast && k == (int)last_k && slot == last_slot) { k0 = k0l; k1 = k1l; }
-        const uint64_t w0 = (uint64_t)v.x | ((uint64_t)v.y << 32);
-        const uint64_t w1 = (uint64_t)v.z | ((uint64_t)v.w << 32);
-        uint64_t p_lo = mul32x32(w0 ^ k0) + w1;
-        uint64_t p_hi = mul32x32(w1 ^ k1) + w0;
-        if (kLast && off >= bs) { p_lo = 0; p_hi = 0; }
-        c_lo += p_lo;
-        c_hi += p_hi;
-    }
-    c_lo = dpp_add64<kDppRowRor4>(c_lo);
-    c_lo = dpp_add64<kDppRowRor8>(c_lo);
-    c_hi = dpp_add64<kDppRowRor4>(c_hi);
-    c_hi = dpp_add64<kDppRowRor8>(c_hi);
-}
-
-// Hash of the window [base, base + bs) of this lane's row; the result is valid in
-// the row's first lane (lane & 15 == 0).  All four rows of the wave must call it
-// (DPP inside rows only; rows may pass different windows of the same bs).
-template <bool kAligned = true>
-__device__ __forceinline__ void row_hash(const uint8_t* __restrict__ base, uint32_t bs, uint32_t& weak_out,
-                                         uint64_t& strong_out) {
-    const uint32_t lane = threadIdx.x & 63;
-    const uint32_t q = lane & 3, slot = (lane >> 2) & 3;
-    const uint32_t npieces = (bs + 1023) >> 10;
-    const uint32_t ls = (bs >> 6) - 1 - ((npieces - 1) << 4);  // last stripe inside the last piece
-    const uint32_t last_k = ls >> 2, last_slot = ls & 3;
-    uint64_t kk0[4], kk1[4];
-#pragma unroll
-    for (int k = 0; k < 4; ++k) {
-        kk0[k] = c_tab.w[slot + 4 * k + 2 * q];
-        kk1[k] = c_tab.w[slot + 4 * k + 2 * q + 1];
-    }
-    const uint64_t k0l = c_tab.last[2 * q], k1l = c_tab.last[2 * q + 1];
-    const uint64_t sk0 = c_tab.w[16 + 2 * q], sk1 = c_tab.w[16 + 2 * q + 1];
-    uint64_t acc_lo = c_tab.init[2 * q], acc_hi = c_tab.init[2 * q + 1];
-    uint32_t asum = 0, vsum = 0;
-    uint64_t bpos = 0;
-    RowPiece cur, nxt;
-    load_piece<kAligned>(base, slot, q, npieces > 1 ? 1024u : bs, cur);
-    for (uint32_t j = 0; j + 1 < npieces; ++j) {  // full pieces, each followed by a scramble
-        const uint32_t nlim = (j + 2 < npieces) ? 1024u : bs - ((j + 1) << 10);
-        load_piece<kAligned>(base + ((j + 1) << 10), slot, q, nlim, nxt);
-        uint64_t c_lo, c_hi;
-        hash_piece<false>(cur, slot, q, j << 10, bs, kk0, kk1, 0, 0, k0l, k1l, asum, vsum, bpos, c_lo, c_hi);
-        acc_lo = scramble1(acc_lo + c_lo, sk0);
-        acc_hi = scramble1(acc_hi + c_hi, sk1);
-        cur = nxt;
-    }
-    {
-        uint64_t c_lo, c_hi;
-        hash_piece<true>(cur, slot, q, (npieces - 1) << 10, bs, kk0, kk1, last_k, last_slot, k0l, k1l, asum, vsum,
-                         bpos, c_lo, c_hi);
-        acc_lo += c_lo;
-        acc_hi += c_hi;
-    }
-    uint64_t f = fold64(acc_lo ^ c_tab.merge[2 * q], acc_hi ^ c_tab.merge[2 * q + 1]);
-    f = sum_quad64(f);
-    // row sums of the Adler partials (16 lanes)
-    asum += dpp32<kDppQuadXor1>(asum);
-    asum += dpp32<kDppQuadXor2>(asum);
-    asum += dpp32<kDppRowRor4>(asum);
-    asum += dpp32<kDppRowRor8>(asum);
-    vsum += dpp32<kDppQuadXor1>(vsum);
-    vsum += dpp32<kDppQuadXor2>(vsum);
-    vsum += dpp32<kDppRowRor4>(vsum);
-    vsum += dpp32<kDppRowRor8>(vsum);
-    bpos = sum_quad64(bpos);
-    bpos = dpp_add64<kDppRowRor4>(bpos);
-    bpos = dpp_add64<kDppRowRor8>(bpos);
-    const uint32_t A = (1u + asum) % kMod;
-    const uint32_t B = (uint32_t)(((uint64_t)bs + bpos - vsum) % kMod);
-    weak_out = (B << 16) | A;
-    strong_out = xxh3_aval((uint64_t)bs * P64_1 + f);
-}
-
 // K1: four blocks per wave, one per row.
 __global__ __launch_bounds__(256) void k_sig_fast(const uint8_t* __restrict__ buf, uint64_t nfull, uint32_t bs,
                                                   uint32_t* __restrict__ weak, uint64_t* __restrict__ strong) {
@@ -313,67 +178,6 @@ __global__ __launch_bounds__(256) void k_sig_batch(const uint8_t* __restrict__ b
 // ===========================================================================
 // K3: index (probe structure) over basis weak values
 // ===========================================================================
-// Probe hashes of a weak value w = (B << 16) | A, each two 24-bit multiplies (full
-// rate; a 32-bit multiply is quarter rate and this runs once per scanned position):
-//   q = A*0x9E3779 + B*0x85EBCB  -> the level-1 bit / ribbon shard and coefficients, and
-//                                   the five bit positions of the level-2 word (bits 0..24)
-//   r = A*0xC2B2AF + B*0x27D4EB  -> the level-2 word (top bits), the ribbon start
-// Level 2 is a blocked Bloom filter of 32-bit words, 5 bits per key in the key's word
-// (3 until round 3: 1.1 % false passes measured on Adler values of random 4 KiB blocks),
-// 16 bits per key for large indexes (the word from r and the bits from q: taking both
-// from one linear hash correlates them, 1.8 %).  Sizing (sydelta_index_create): up to 16 Ki
-// keys the filter is <= 32 KiB and the LDS-staged scan copies it into LDS; above
-// that it stays in HBM/L2.  FileIx::filt_off counts words; fwshift = 32 - log2(words).
-struct ProbeHash {
-    uint32_t q, r;
-};
-__device__ __forceinline__ ProbeHash probe_hash(uint32_t A, uint32_t B) {
-    const uint32_t q = (uint32_t)__umul24(A, 0x9E3779u) + (uint32_t)__umul24(B, 0x85EBCBu);
-    const uint32_t r = (uint32_t)__umul24(A, 0xC2B2AFu) + (uint32_t)__umul24(B, 0x27D4EBu);
-    return {q, r};
-}
-__device__ __forceinline__ ProbeHash probe_hash(uint32_t w) { return probe_hash(w & 0xFFFFu, w >> 16); }
-// Five bits per key in its 32-bit word (q's five low 5-bit fields): 0.74 % false passes at
-// 16 bits per key against 1.08 % with three (Poisson keys per word), so a third fewer
-// exact-table lookups behind the scans' filters (round 4; each lookup of a level-2 false
-// pass misses L2 for a table line).
-#ifndef SYDELTA_L2_BITS
-#define SYDELTA_L2_BITS 5
-#endif
-static_assert(SYDELTA_L2_BITS == 3 || SYDELTA_L2_BITS == 5, "level-2 bits per key");
-__device__ __forceinline__ uint32_t filt_mask(uint32_t q) {
-    uint32_t m = (1u << (q & 31)) | (1u << ((q >> 5) & 31)) | (1u << ((q >> 10) & 31));
-    if (SYDELTA_L2_BITS == 5) m |= (1u << ((q >> 15) & 31)) | (1u << ((q >> 20) & 31));
-    return m;
-}
-__device__ __forceinline__ bool filt_pass(uint32_t word, uint32_t q) {
-    const uint32_t m = filt_mask(q);
-    return (word & m) == m;
-}
-// filt_pass as 0/1 with five bit extracts (the offset operand takes bits [4:0])
-__device__ __forceinline__ uint32_t filt_bit(uint32_t word, uint32_t q) {
-    uint32_t b = __builtin_amdgcn_ubfe(word, q, 1) & __builtin_amdgcn_ubfe(word, q >> 5, 1) &
-                 __builtin_amdgcn_ubfe(word, q >> 10, 1);
-    if (SYDELTA_L2_BITS == 5) b &= __builtin_amdgcn_ubfe(word, q >> 15, 1) & __builtin_amdgcn_ubfe(word, q >> 20, 1);
-    return b;
-}
-// Level-1 filters (held in LDS by k_scan_r / k_scan_g so that only the positions they
-// pass cost a level-2 request to L2): one bit per key, bit = q[0..4] (one bit extract;
-// the level-2 word tests q[0..4] too, but in an unrelated word).
-__device__ __forceinline__ uint32_t l1_test(uint32_t word, uint32_t q) { return __builtin_amdgcn_ubfe(word, q, 1); }
-// k_scan_r's level-1 word (kL1WordsR words, not a power of two): floor(q * words / 2^32)
-// from the top 24 bits of q, one shift and one v_mul_hi_u32_u24
-static_assert((kL1WordsR << 8) < (1u << 24), "l1r_word's constant is a 24-bit operand");
-__host__ __device__ __forceinline__ uint32_t l1r_word(uint32_t q) {
-    return (uint32_t)(((uint64_t)(q >> 8) * (kL1WordsR << 8)) >> 32);
-}
-__device__ __forceinline__ uint32_t bucket_hash(uint32_t w) {
-    uint32_t h = w ^ (w >> 15);
-    h *= 0x2C1B3C6Du;
-    h ^= h >> 12;
-    return h;
-}
-
 // Block i of the concatenated signature -> its file (fblk = block prefix, nf+1 entries).
 __device__ __forceinline__ uint32_t file_of_block(const uint64_t* __restrict__ fblk, uint32_t nf, uint64_t i) {
     uint32_t lo = 0, hi = nf;
@@ -565,20 +369,6 @@ __global__ void k_idx_fat(uint64_t nslots, const uint32_t* __restrict__ keys, co
     fat[j] = r;
 }
 
-// Exact lookup: slot of weak value w, or -1.
-__device__ __forceinline__ int64_t table_find(const uint32_t* __restrict__ keys, uint32_t bmask, uint32_t w) {
-    uint32_t b = bucket_hash(w) & bmask;
-    for (;;) {
-        const uint4 k = *(const uint4*)(keys + 4 * b);
-        if (k.x == w) return 4 * b;
-        if (k.y == w) return 4 * b + 1;
-        if (k.z == w) return 4 * b + 2;
-        if (k.w == w) return 4 * b + 3;
-        if (k.w == kEmptyKey) return -1;  // buckets fill in order: a free last slot ends the chain
-        b = (b + 1) & bmask;
-    }
-}
-
 // Candidates of one slot are stored in index order (launch_index_build sorts them),
 // so generator.rs:127-133's "first candidate whose strong matches" is the first hit
 // of an in-order sweep: 64 candidates per step, stop at the first step with a match.
@@ -606,7 +396,6 @@ __device__ __forceinline__ uint32_t first_strong_match(const uint32_t* __restric
 // generator.rs:121-155), one wave per window, so the host scans only the other
 // blocks' windows (sydelta_api.cpp, Classifier).  out[w] = global block index of
 // the hit, or kNoBlock.
-constexpr uint32_t kNoBlock = 0xFFFFFFFFu;
 
 __device__ __forceinline__ uint32_t probe_job(const ProbeJob* __restrict__ jobs, uint32_t njobs, uint64_t w) {
     uint32_t lo = 0, hi = njobs;
@@ -1685,27 +1474,6 @@ __device__ __forceinline__ bool fat_find_k(const uint32_t* __restrict__ keys, co
     }
 }
 
-
-// Exclusive wave scan (lane l gets the sum over lanes < l) and the wave total: DPP
-// row_shr steps inside each 16-lane row, then the row totals through SGPRs (no LDS
-// crossbar round trips: the window phase runs three of these per value).
-template <int K>
-__device__ __forceinline__ uint32_t dpp_shr(uint32_t v) {
-    return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x110 + K, 0xF, 0xF, true);  // out of row: 0
-}
-__device__ __forceinline__ uint32_t wave_scan_excl(uint32_t v, uint32_t& total) {
-    uint32_t x = v;
-    x += dpp_shr<1>(x);
-    x += dpp_shr<2>(x);
-    x += dpp_shr<4>(x);
-    x += dpp_shr<8>(x);
-    const uint32_t r0 = __builtin_amdgcn_readlane(x, 15), r1 = __builtin_amdgcn_readlane(x, 31);
-    const uint32_t r2 = __builtin_amdgcn_readlane(x, 47), r3 = __builtin_amdgcn_readlane(x, 63);
-    const uint32_t row = (threadIdx.x & 63) >> 4;
-    const uint32_t off = row == 0 ? 0u : row == 1 ? r0 : row == 2 ? r0 + r1 : r0 + r1 + r2;
-    total = r0 + r1 + r2 + r3;
-    return x + off - v;
-}
 
 // One batch of kB3 positions in flight: the level-2 words (buffer loads issued),
 // probe hashes and weak values, tested one batch later.
@@ -2819,383 +2587,6 @@ __global__ __launch_bounds__(256) void k_chain_emit(chain::ChainArgs a) {
 }
 __global__ void k_chain_finish(chain::ChainArgs a) {
     if (gtid() == 0) chain::chain_finish(a);
-}
-
-// ===========================================================================
-// K10: the greedy walk of many small files, one workgroup per file (C4)
-// ===========================================================================
-// The batched match used to classify on the device in five host-synchronised phases
-// (aligned probe, miss ranges, scans, phase probe, scans of the missed blocks) and walk on
-// host threads.  Here a workgroup walks its file itself (generator.rs:116-221), classifying
-// only the window starts the walk visits:
-//   * the walk at x on the phase grid k*n + phi: the phase windows of the next kWRows
-//     blocks are hashed together, one 16-lane row each (row_hash, the signature kernel's
-//     layout), and looked up (first candidate in index order with equal strong,
-//     generator.rs:121-155); a hit copies and moves x by n, so the walk stays on the grid;
-//   * a miss at x: the window starts (x, x + n) are rolled (rolling.rs:66-79), 16 per
-//     thread from the closed form of their first window (workgroup scans of 16-byte group
-//     sums over the bytes staged in LDS), tested against the file's Bloom filter in LDS and
-//     the exact table; weak hits are hashed 16 at a time in position order and the first
-//     verified one is the walk's next hit (a Copy, then a new phase); without one the walk
-//     continues at x + n, the next phase window.
-// So a copy-heavy file costs one hash per block plus one roll of n positions per edited
-// block, and a shift (an insertion or deletion) one new phase grid.  The ops are written
-// run-length coded (WalkRec) to the file's staging region, then moved to the compact
-// output with one atomic per file.
-constexpr int kWT = 256;                 // threads per workgroup (4 waves, 16 rows)
-constexpr uint32_t kWRows = kWT / 16;    // phase windows hashed per pass
-constexpr uint32_t kWRun = 16;           // window starts per thread per roll pass
-constexpr uint32_t kWSub = kWT * kWRun;  // window starts per roll pass (4096)
-
-struct WalkLds {  // byte offsets of the dynamic LDS
-    uint32_t filt, ntab, stage, small, total;
-};
-__host__ __device__ __forceinline__ WalkLds walk_lds(uint32_t fw, uint32_t n) {
-    WalkLds L{};
-    uint32_t o = 0;
-    L.filt = o; o += 4 * fw;
-    L.ntab = o; o += 1024;
-    L.stage = o; o += (kWSub + n + 64 + 15) & ~15u;  // also the scans' prefix arrays: 12 * (kWT + n/16 + 1) bytes
-    L.small = o; o += 512;
-    L.total = o;
-    return L;
-}
-// small area (u32 words)
-constexpr int kWsR = 0;          // [16] phase-window results
-constexpr int kWsVList = 16;     // [16] weak hits being verified (position - y0)
-constexpr int kWsVRes = 32;      // [16] their blocks
-constexpr int kWsWave = 48;      // [4 waves x 4] wave totals of the scans
-constexpr int kWsMisc = 64;      // [0] tail flag, [1] record base
-
-// Workgroup exclusive scan of up to four u32 values per thread (wave DPP scans + the wave
-// totals through LDS); tot = the workgroup totals.  Barriers inside: every thread calls.
-template <int K>
-__device__ __forceinline__ void wg_scan_excl(uint32_t (&v)[K], uint32_t (&tot)[K], uint32_t* wsum) {
-    const uint32_t lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-    uint32_t wt[K];
-#pragma unroll
-    for (int k = 0; k < K; ++k) v[k] = wave_scan_excl(v[k], wt[k]);
-    if (lane == 0) {
-#pragma unroll
-        for (int k = 0; k < K; ++k) wsum[wid * 4 + k] = wt[k];
-    }
-    __syncthreads();
-#pragma unroll
-    for (int k = 0; k < K; ++k) {
-        uint32_t before = 0, all = 0;
-#pragma unroll
-        for (int w = 0; w < kWT / 64; ++w) {
-            const uint32_t x = wsum[w * 4 + k];
-            before += (uint32_t)w < wid ? x : 0u;
-            all += x;
-        }
-        v[k] += before;
-        tot[k] = all;
-    }
-    __syncthreads();  // wsum is reused by the next scan
-}
-
-// 16 bytes at LDS byte offset o (any alignment) as 4 dwords
-__device__ __forceinline__ void lds16_u(const uint8_t* st, uint32_t o, uint32_t (&x)[4]) {
-    const uint32_t* w = (const uint32_t*)(st + (o & ~3u));
-    const uint32_t sh = o & 3;
-    uint32_t d[5];
-#pragma unroll
-    for (int i = 0; i < 5; ++i) d[i] = w[i];
-#pragma unroll
-    for (int i = 0; i < 4; ++i) x[i] = __builtin_amdgcn_alignbyte(d[i + 1], d[i], sh);
-}
-
-// First candidate in index order of file F with weak wk and strong st (generator.rs:127-133),
-// or kNoBlock; one thread.
-__device__ __forceinline__ uint32_t walk_lookup(const WalkArgs& a, const FileIx& F, uint32_t wk, uint64_t st) {
-    const int64_t slot = table_find(a.keys + F.slot_off, F.bmask, wk);
-    if (slot < 0) return kNoBlock;
-    const uint64_t gs = F.slot_off + (uint64_t)slot;
-    const uint32_t s0 = a.start[gs], c = a.cnt[gs];
-    for (uint32_t j = 0; j < c; ++j)
-        if (a.cstrong[s0 + j] == st) return a.order[s0 + j];
-    return kNoBlock;
-}
-
-__global__ __launch_bounds__(kWT) void k_walk_files(WalkArgs a) {
-    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-    const uint32_t f = blockIdx.x;
-    const uint32_t tid = threadIdx.x, lane = tid & 63, wid = tid >> 6, row = tid >> 4;
-    const uint32_t n = a.n;
-    const FileIx F = a.files[f];
-    const uint32_t fw = 1u << (32 - F.fwshift);
-    const WalkLds L = walk_lds(a.fw_max, n);
-    uint32_t* filt = (uint32_t*)(smem + L.filt);
-    uint32_t* ntab = (uint32_t*)(smem + L.ntab);
-    uint8_t* stage = smem + L.stage;
-    uint32_t* sm = (uint32_t*)(smem + L.small);
-    const uint8_t* src = a.base + a.soff[f];
-    const uint64_t len = a.slen[f];
-    const uint64_t gb0 = a.fblk[f], nbf = a.fblk[f + 1] - gb0, ls = a.last_size[f];
-    const uint64_t p1 = (nbf && len >= n) ? len - n + 1 : 0;  // full-window starts [0, p1)
-
-    {  // the file's Bloom filter, the roll table
-        const uint4* g = (const uint4*)(a.filt + F.filt_off);
-        for (uint32_t i = tid; i < fw / 4; i += kWT) ((uint4*)filt)[i] = g[i];
-        ntab[tid] = kMod - 1 - (a.nm * tid) % kMod;  // kWT == 256 bytes
-    }
-    // the tail rule (generator.rs:156-184): the suffix of the basis's last block's size
-    if (wid == 0) {
-        uint32_t ok = 0;
-        if (nbf && ls < n && len >= ls) {
-            const uint8_t* p = src + (len - ls);
-            uint32_t wk = 0;
-            uint64_t st = 0;
-            if (ls > 240) {
-                wave_hash_long(p, ls, wk, st);
-            } else if (lane == 0) {
-                wk = adler_scalar(p, ls);
-                st = xxh3_short(p, ls);
-            }
-            ok = (wk == a.weak[gb0 + nbf - 1] && st == a.strong[gb0 + nbf - 1]) ? 1u : 0u;
-        }
-        if (lane == 0) sm[kWsMisc] = ok;
-    }
-    __syncthreads();
-
-    // run-length coded output (thread 0 writes; every thread keeps the same state)
-    WalkRec* stg = a.stage + a.rec_off[f];
-    uint32_t nrec = 0, ck = 0, ca = 0;  // the open Copy run: ck Copies from block ca (ck 0: none)
-    auto put = [&](uint32_t kind, uint32_t aa, uint64_t off) {
-        if (tid == 0) stg[nrec] = WalkRec{kind, aa, off};
-        ++nrec;
-    };
-    auto close_run = [&]() {
-        if (ck) put(ck, ca, 0);
-        ck = 0;
-    };
-    auto data = [&](uint64_t lo, uint64_t hi) {
-        if (hi > lo) {
-            close_run();
-            put(0, (uint32_t)(hi - lo), lo);
-        }
-    };
-    auto copy = [&](uint32_t g) {
-        if (ck && g == ca + ck) {
-            ++ck;
-        } else {
-            close_run();
-            ck = 1;
-            ca = g;
-        }
-    };
-    uint32_t weak_hits = 0, hits = 0;
-
-    uint64_t x = 0, lit = 0;
-    uint32_t phi = 0xFFFFFFFFu;
-    uint64_t rk0 = 0, rk1 = 0;  // the results in sm[kWsR] are blocks [rk0, rk1) at phase phi
-#pragma unroll 1
-    while (x < p1) {
-        const uint64_t k = x / n;
-        const uint32_t ph = (uint32_t)(x - k * n);
-        if (ph != phi || k >= rk1) {
-            // ---- phase pass: windows (k + r) n + ph, r < cnt, one per row
-            const uint64_t cnt = min((uint64_t)kWRows, (p1 - x + n - 1) / n);
-            const uint64_t pos = (k + (row < cnt ? row : 0)) * n + ph;
-            uint32_t wk;
-            uint64_t st;
-            if ((ph & 15) == 0)
-                row_hash<true>(src + pos, n, wk, st);
-            else
-                row_hash<false>(src + pos, n, wk, st);
-            __syncthreads();  // every wave has read the previous pass's results
-            if ((tid & 15) == 0 && row < cnt) {
-                uint32_t blk = kNoBlock;
-                const ProbeHash h = probe_hash(wk);
-                if (filt_pass(filt[h.r >> F.fwshift], h.q)) blk = walk_lookup(a, F, wk, st);
-                sm[kWsR + row] = blk;
-            }
-            __syncthreads();
-            phi = ph;
-            rk0 = k;
-            rk1 = k + cnt;
-        }
-        const uint32_t blk = sm[kWsR + (uint32_t)(k - rk0)];
-        if (blk != kNoBlock) {  // generator.rs:135-146
-            ++hits;
-            data(lit, x);
-            copy(blk);
-            x += n;
-            lit = x;
-            continue;
-        }
-        // ---- the window at x misses: roll (x, min(x + n, p1)) for the first hit
-        const uint64_t yend = min(x + n, p1);
-        uint64_t q = yend;
-        uint32_t qb = kNoBlock;
-#pragma unroll 1
-        for (uint64_t y0 = x + 1; y0 < yend && qb == kNoBlock; y0 += kWSub) {
-            const uint64_t y1 = min(y0 + kWSub, yend);
-            const uint64_t g0 = y0 & ~15ull;
-            const uint32_t so = (uint32_t)(y0 - g0);
-            const uint32_t sbytes = (kWSub + n + 64 + 15) & ~15u;
-            __syncthreads();  // the stage (prefix arrays of the last pass) is free
-            for (uint32_t i = tid; i < sbytes / 16; i += kWT) {
-                const uint64_t o = g0 + 16ull * i;
-                uint4 v = make_uint4(0, 0, 0, 0);
-                if (o < len) v = *(const uint4*)(src + o);  // a granule holding a byte of the file
-                if (o + 16 > len && o < len) {  // zero the bytes past the end
-                    const uint32_t keep = (uint32_t)(len - o);
-                    uint32_t w[4] = {v.x, v.y, v.z, v.w};
-#pragma unroll
-                    for (int j = 0; j < 4; ++j) {
-                        const int kb = (int)keep - 4 * j;
-                        w[j] = kb >= 4 ? w[j] : kb <= 0 ? 0u : (w[j] & ((1u << (8 * kb)) - 1));
-                    }
-                    v = make_uint4(w[0], w[1], w[2], w[3]);
-                }
-                ((uint4*)stage)[i] = v;
-            }
-            __syncthreads();
-            // this thread's bytes: out [y0 + 16t, +16), in [y0 + 16t + n, +16)
-            uint32_t xo[4], xi[4];
-            lds16_u(stage, so + 16 * tid, xo);
-            lds16_u(stage, so + 16 * tid + n, xi);
-            // groups j = 3t .. 3t+2 (bytes [y0 + 16j, +16)) of the G = kWT + n/16 the windows span
-            const uint32_t G = kWT + n / 16;
-            uint32_t gs[3], gv[3];
-#pragma unroll
-            for (int m = 0; m < 3; ++m) {
-                const uint32_t j = 3 * tid + m;
-                gs[m] = gv[m] = 0;
-                if (j < G) {
-                    uint32_t d[4];
-                    lds16_u(stage, so + 16 * j, d);
-#pragma unroll
-                    for (int i = 0; i < 4; ++i) {
-                        gs[m] = udot4(d[i], 0x01010101u, gs[m]);
-                        gv[m] = udot4(d[i], offw(i), gv[m]);
-                    }
-                }
-            }
-            uint32_t sc[3] = {gs[0] + gs[1] + gs[2], gv[0] + gv[1] + gv[2],
-                              (3 * tid) * gs[0] + (3 * tid + 1) * gs[1] + (3 * tid + 2) * gs[2]};
-            uint32_t tot[3];
-            __syncthreads();  // every thread has read the stage: the prefix arrays take it over
-            wg_scan_excl<3>(sc, tot, sm + kWsWave);
-            uint32_t* PS = (uint32_t*)stage;
-            uint32_t* PV = PS + (G + 1);
-            uint32_t* PJ = PV + (G + 1);
-            {
-                uint32_t s = sc[0], v = sc[1], jj = sc[2];
-#pragma unroll
-                for (int m = 0; m < 3; ++m) {
-                    const uint32_t j = 3 * tid + m;
-                    if (j < G) {
-                        PS[j] = s;
-                        PV[j] = v;
-                        PJ[j] = jj;
-                    }
-                    s += gs[m];
-                    v += gv[m];
-                    jj += j * gs[m];
-                }
-                if (tid == 0) {
-                    PS[G] = tot[0];
-                    PV[G] = tot[1];
-                    PJ[G] = tot[2];
-                }
-            }
-            __syncthreads();
-            const uint32_t g = n / 16;
-            const uint64_t S = PS[tid + g] - PS[tid];
-            const uint64_t V = PV[tid + g] - PV[tid];
-            const uint64_t J = PJ[tid + g] - PJ[tid];
-            uint32_t am = (uint32_t)((1 + S) % kMod);
-            uint32_t bm = (uint32_t)(((uint64_t)n + (uint64_t)n * S - (16 * (J - (uint64_t)tid * S) + V)) % kMod);
-            // roll the thread's 16 window starts
-            const uint64_t p0 = y0 + 16ull * tid;
-            uint32_t pm = 0, wv[kWRun];
-#pragma unroll
-            for (int i = 0; i < (int)kWRun; ++i) {
-                wv[i] = (bm << 16) | am;
-                const ProbeHash h = probe_hash(am, bm);
-                const uint32_t pass = (p0 + i < y1) ? filt_bit(filt[h.r >> F.fwshift], h.q) : 0u;
-                pm |= pass << i;
-                const uint32_t out = (xo[i >> 2] >> (8 * (i & 3))) & 0xFF;
-                const uint32_t in = (xi[i >> 2] >> (8 * (i & 3))) & 0xFF;
-                const uint32_t u = am + in + (kMod - out);  // [M-255, 2M+255)
-                am = min(u, min(u - kMod, u - 2 * kMod));
-                const uint32_t v = bm + am + ntab[out];  // [0, 3M)
-                bm = min(v, min(v - kMod, v - 2 * kMod));
-            }
-            // exact-table lookups of the filter passes -> weak hits (generator.rs:121-124)
-            uint32_t hm = 0;
-            while (pm) {
-                const int i = __builtin_ctz(pm);
-                pm &= pm - 1;
-                if (table_find(a.keys + F.slot_off, F.bmask, wv[i]) >= 0) hm |= 1u << i;
-            }
-            uint32_t rk[1] = {(uint32_t)__builtin_popcount(hm)}, ntot[1];
-            wg_scan_excl<1>(rk, ntot, sm + kWsWave);
-            weak_hits += ntot[0];
-            // verify the weak hits 16 at a time in position order (generator.rs:127-133)
-#pragma unroll 1
-            for (uint32_t vb = 0; vb < ntot[0]; vb += kWRows) {
-                {
-                    uint32_t r = rk[0], m = hm;
-                    while (m) {
-                        const int i = __builtin_ctz(m);
-                        m &= m - 1;
-                        if (r >= vb && r < vb + kWRows) sm[kWsVList + (r - vb)] = 16 * tid + (uint32_t)i;
-                        ++r;
-                    }
-                }
-                __syncthreads();
-                const uint32_t nv = min((uint32_t)kWRows, ntot[0] - vb);
-                const uint64_t pos = y0 + sm[kWsVList + (row < nv ? row : 0)];
-                uint32_t wk;
-                uint64_t st;
-                row_hash<false>(src + pos, n, wk, st);
-                if ((tid & 15) == 0 && row < nv) sm[kWsVRes + row] = walk_lookup(a, F, wk, st);
-                __syncthreads();
-                for (uint32_t r = 0; r < nv; ++r) {
-                    const uint32_t b = sm[kWsVRes + r];
-                    if (b != kNoBlock) {
-                        q = y0 + sm[kWsVList + r];
-                        qb = b;
-                        break;
-                    }
-                }
-                __syncthreads();  // vlist / vres are rewritten by the next batch
-                if (qb != kNoBlock) break;
-            }
-        }
-        if (qb != kNoBlock) {
-            ++hits;
-            data(lit, q);
-            copy(qb);
-            x = q + n;
-            lit = x;
-        } else {
-            x = yend;  // the next phase window (or the end of the full windows)
-        }
-    }
-    // the walk's end: the tail rule at p* = len - last_size, then the last literal run
-    if (sm[kWsMisc] && ls <= len && len - ls >= lit) {
-        data(lit, len - ls);
-        copy((uint32_t)(gb0 + nbf - 1));
-        lit = len;
-        ++hits;
-    }
-    data(lit, len);
-    close_run();
-    // move the records to the compact output (one atomic per file)
-    __threadfence_block();
-    if (tid == 0) sm[kWsMisc + 1] = nrec ? (uint32_t)atomicAdd(a.total, (unsigned long long)nrec) : 0u;
-    __syncthreads();
-    const uint32_t base = sm[kWsMisc + 1];
-    for (uint32_t i = tid; i < nrec; i += kWT) {
-        const volatile WalkRec* r = stg + i;
-        a.out[base + i] = WalkRec{r->kind, r->a, r->off};
-    }
-    if (tid == 0) a.fout[f] = WalkFileOut{base, nrec, weak_hits, hits};
 }
 
 // ===========================================================================
@@ -5403,16 +4794,6 @@ hipError_t launch_scan_wide(const uint8_t* d_src, uint64_t len, uint64_t pos_beg
     const uint64_t tiles = (pos_end - pos_begin + kScanTile - 1) / kScanTile;
     ProfScope ps(prof, s, "k_scan");
     hipLaunchKernelGGL(k_scan, dim3((unsigned)tiles), dim3(kScanThreads), lds, s, a);
-    return hipGetLastError();
-}
-
-hipError_t launch_walk_files(const WalkArgs& a, hipStream_t s, Profiler* prof) {
-    if (!a.nfiles) return hipSuccess;
-    if (a.n % 64 != 0 || a.n < 256 || a.n > kWalkMaxN || a.fw_max > kWalkMaxWords || a.fw_max < 4)
-        return hipErrorInvalidValue;
-    const WalkLds L = walk_lds(a.fw_max, a.n);
-    ProfScope ps(prof, s, "k_walk_files");
-    hipLaunchKernelGGL(k_walk_files, dim3(a.nfiles), dim3(kWT), L.total, s, a);
     return hipGetLastError();
 }
 

@@ -36,21 +36,25 @@ FLAGS = ["-std=c++17", "-O1", "-g", "-fno-omit-frame-pointer", "-fsanitize=addre
          "-I" + os.path.join(ROOT, "include"), "-I" + CSRC]
 
 
-def _kernels_object() -> str:
+KERNEL_SOURCES = ["sydelta_kernels.hip", "sydelta_filewalk.hip"]
+
+
+def _kernels_objects() -> list:
+    """The kernel translation units' objects from sy_amd.build (the launch symbols)."""
     from sy_amd import build as b
 
-    obj = os.path.join(b.OBJDIR, "sydelta_kernels.o")
-    if not os.path.exists(obj) or not os.path.exists(b.LIB) or os.path.getmtime(obj) < os.path.getmtime(
-            os.path.join(CSRC, "sydelta_kernels.hip")):
+    objs = [os.path.join(b.OBJDIR, f.rsplit(".", 1)[0] + ".o") for f in KERNEL_SOURCES]
+    if not os.path.exists(b.LIB) or any(not os.path.exists(o) or os.path.getmtime(o) < os.path.getmtime(
+            os.path.join(CSRC, f)) for o, f in zip(objs, KERNEL_SOURCES)):
         b.build(force=True)
-    return obj
+    return objs
 
 
 @pytest.mark.timeout(900)
 def test_host_code_under_asan_ubsan():
     if shutil.which("g++") is None or not os.path.exists("/opt/rocm/lib/libamdhip64.so"):
         pytest.skip("needs g++ and the ROCm runtime library")
-    kobj = _kernels_object()
+    kobjs = _kernels_objects()
     os.makedirs(OUT, exist_ok=True)
     srcs = [os.path.join(CSRC, f) for f in HOST_SOURCES] + [os.path.join(ROOT, "tests", "csrc", "host_fuzz.cpp")]
 
@@ -64,7 +68,7 @@ def test_host_code_under_asan_ubsan():
         objs = list(ex.map(compile_one, srcs))
     exe = os.path.join(OUT, "host_fuzz")
     r = subprocess.run(["g++", "-fsanitize=address,undefined", "-o", exe] + objs +
-                       [kobj, "-L/opt/rocm/lib", "-lamdhip64", "-Wl,-rpath,/opt/rocm/lib", "-lpthread"],
+                       kobjs + ["-L/opt/rocm/lib", "-lamdhip64", "-Wl,-rpath,/opt/rocm/lib", "-lpthread"],
                        capture_output=True, text=True)
     assert r.returncode == 0, r.stderr[-4000:]
     env = dict(os.environ, ASAN_OPTIONS="detect_leaks=1:abort_on_error=1",
