@@ -1184,7 +1184,10 @@ struct Classifier {
     // thread's kept scratch instead (a chunk's outlives other calls on its thread)
     DevScratch* probe_scratch = nullptr;
     uint32_t* d_probe_out = nullptr;
+    uint32_t* d_probe_pw = nullptr;  // ... and the probed windows' weak values
     std::vector<uint64_t> probe_pfx;
+    // the probe's results stay on the device only (the walk runs there: K10 over a chunk)
+    bool device_only = false;
 
     // Aligned probe of every block of every source (mode 1), of none (0), or, in
     // auto mode (-1), when a 1-in-16 sample finds >= 1/8 of its windows hitting.
@@ -1321,12 +1324,16 @@ int Classifier::probe(int mode) {
             jp = (uint8_t*)jb.p;
         }
         uint32_t* d_out = (uint32_t*)(jp + jbytes);
-        if (stride == 1) d_probe_out = d_out;
         uint32_t* d_pw = (uint32_t*)(jp + jbytes + obytes);
+        if (stride == 1) {
+            d_probe_out = d_out;
+            d_probe_pw = d_pw;
+        }
         uint64_t* d_pst = (uint64_t*)(jp + jbytes + 2 * obytes);
         HIP_TRY(hipMemcpyAsync(jp, jobs.data(), jobs.size() * sizeof(ProbeJob), hipMemcpyHostToDevice, s));
         HIP_TRY(launch_probe(base, (const ProbeJob*)jp, (uint32_t)jobs.size(), np, stride, (uint32_t)n, fast,
                              ix->ix, d_pw, d_pst, d_out, s, prof));
+        if (device_only) return SYDELTA_OK;
         HIP_TRY(hipMemcpyAsync(out, d_out, np * 4, hipMemcpyDeviceToHost, s));
         HIP_TRY(hipStreamSynchronize(s));
         return SYDELTA_OK;
@@ -1341,6 +1348,10 @@ int Classifier::probe(int mode) {
     }
     if (int r = run(1, pfx)) return r;
     probe_pfx = pfx;
+    if (device_only) {
+        for (auto& c : src) c.probed = true;
+        return SYDELTA_OK;
+    }
     // Copy the results into the sources and find their miss runs (the blocks classify
     // scans) in one pass, in pieces of 64 Ki blocks on the host pool: one large source
     // (C5) is split as well as many small ones (C4).
@@ -2155,41 +2166,39 @@ bool file_walk_ok(const sydelta_index* ix, const uint64_t* src_off, const uint64
 }
 }  // namespace
 
-// The batched match with the walk on the device: one launch, the file table up, the
-// run-length coded ops down (two D2H: the per-file counts, then the records), expanded
-// into the files' op arrays on the host pool.
-static int match_walk_files(sydelta_index* ix, const uint8_t* d_buf, const uint64_t* src_off, const uint64_t* src_len,
-                            hipStream_t s, Profiler* prof, sydelta_delta_batch* b) {
+// One launch of K10 over `units`: the unit table up, the per-unit results and the
+// run-length coded records down (two D2H: the counts, then the records).  The records stay
+// in the calling thread's pinned buffer (res.rec) until its next use.
+struct WalkResult {
+    std::vector<WalkFileOut> out;  // per unit
+    const WalkRec* rec = nullptr;  // compact records: unit u's at rec[out[u].base, + out[u].count)
+    uint64_t nrec = 0;
+    double ms_kernel = 0, ms_d2h = 0;
+};
+static int run_walk(sydelta_index* ix, const uint8_t* base, const std::vector<WalkUnit>& units, const uint32_t* ahit,
+                    const uint32_t* apw, bool lds_filter, hipStream_t s, Profiler* prof, WalkResult& res) {
     ScratchHold hold;
-    static const bool host_timing = getenv("SYDELTA_HOST_TIMING") != nullptr;
     const auto t0 = std::chrono::steady_clock::now();
-    const uint64_t n = ix->bs, nf = ix->nfiles;
+    const uint64_t nu = units.size(), nf = ix->nfiles;
+    res.out.clear();
+    res.rec = nullptr;
+    res.nrec = 0;
+    if (!nu) return SYDELTA_OK;
     int cur_dev = 0;
     HIP_TRY(hipGetDevice(&cur_dev));
-    // table: soff | slen | rec_off | last_size (u64 each), then the device outputs
-    PinnedHits& ph = thread_pinned_hits();
-    const size_t tbytes = 32 * nf;
-    const size_t fout_bytes = sizeof(WalkFileOut) * nf;
-    if (ph.bytes < std::max(tbytes, fout_bytes + 16)) {
-        if (ph.p) (void)hipHostFree(ph.p);
-        ph = PinnedHits();
-        const size_t want = std::max(tbytes, fout_bytes + 16) * 5 / 4 + (1 << 20);
-        HIP_TRY(hipHostMalloc((void**)&ph.p, want, hipHostMallocDefault));
-        ph.bytes = want;
-    }
-    uint64_t* T = (uint64_t*)ph.p;
     uint64_t rec_total = 0;
-    for (uint64_t f = 0; f < nf; ++f) {
-        T[f] = src_off[f];
-        T[nf + f] = src_len[f];
-        T[2 * nf + f] = rec_total;
-        T[3 * nf + f] = ix->last_size[f];
-        rec_total += 2 * (src_len[f] / n) + 4;
-    }
+    for (const WalkUnit& u : units) rec_total = std::max(rec_total, u.rec_off + 2 * ((u.end - u.entry) / ix->bs) + 4);
+    // pinned: the unit table and the last sizes up; the counts down (over them, once uploaded)
+    const size_t ubytes = sizeof(WalkUnit) * nu, lbytes = 8 * nf, fout_bytes = sizeof(WalkFileOut) * nu;
+    PinnedHits& ph = thread_pinned_hits();
+    if (int r = pinned_at_least(ph, std::max(ubytes + lbytes, fout_bytes + 16))) return r;
+    memcpy(ph.p, units.data(), ubytes);
+    memcpy(ph.p + ubytes, ix->last_size.data(), lbytes);
     auto al = [](size_t v) { return (v + 255) & ~(size_t)255; };
     // o_total: the record counter (8 B) and SYDELTA_PHASE_TIMING's 16 tick counters
-    const size_t o_tab = 0, o_fout = o_tab + al(tbytes), o_total = o_fout + al(fout_bytes), o_stage = o_total + 256;
-    const size_t o_out = o_stage + al(sizeof(WalkRec) * rec_total), need = o_out + al(sizeof(WalkRec) * rec_total);
+    const size_t o_units = 0, o_last = al(ubytes), o_fout = o_last + al(lbytes), o_total = o_fout + al(fout_bytes);
+    const size_t o_stage = o_total + 256, o_out = o_stage + al(sizeof(WalkRec) * rec_total);
+    const size_t need = o_out + al(sizeof(WalkRec) * rec_total);
     DevScratch& sc = thread_walk_scratch(cur_dev);
     if (sc.bytes < need) {
         if (sc.p) (void)hipFreeAsync(sc.p, s);
@@ -2198,19 +2207,18 @@ static int match_walk_files(sydelta_index* ix, const uint8_t* d_buf, const uint6
         sc.bytes = need + need / 4;
     }
     uint8_t* D = (uint8_t*)sc.p;
-    HIP_TRY(hipMemcpyAsync(D + o_tab, T, tbytes, hipMemcpyHostToDevice, s));
+    HIP_TRY(hipMemcpyAsync(D + o_units, ph.p, ubytes, hipMemcpyHostToDevice, s));
+    HIP_TRY(hipMemcpyAsync(D + o_last, ph.p + ubytes, lbytes, hipMemcpyHostToDevice, s));
     static const bool timing = getenv("SYDELTA_PHASE_TIMING") != nullptr;
     HIP_TRY(hipMemsetAsync(D + o_total, 0, timing ? 8 + 128 : 8, s));
     WalkArgs a{};
-    a.base = d_buf;
-    a.soff = (const uint64_t*)(D + o_tab);
-    a.slen = a.soff + nf;
-    a.rec_off = a.soff + 2 * nf;
-    a.last_size = a.soff + 3 * nf;
-    a.nfiles = (uint32_t)nf;
-    a.n = (uint32_t)n;
-    a.nm = (uint32_t)(n % 65521);
-    a.fw_max = std::max<uint32_t>(4, ix->ix.max_fwords);
+    a.base = base;
+    a.units = (const WalkUnit*)(D + o_units);
+    a.last_size = (const uint64_t*)(D + o_last);
+    a.nunits = (uint32_t)nu;
+    a.n = (uint32_t)ix->bs;
+    a.nm = (uint32_t)(ix->bs % 65521);
+    a.fw_max = lds_filter ? std::max<uint32_t>(4, ix->ix.max_fwords) : 0;
     a.files = ix->ix.d_files;
     a.fblk = ix->ix.d_fblk;
     a.filt = ix->ix.filt;
@@ -2221,6 +2229,8 @@ static int match_walk_files(sydelta_index* ix, const uint8_t* d_buf, const uint6
     a.cstrong = ix->ix.cstrong;
     a.weak = ix->d_weak;
     a.strong = ix->d_strong;
+    a.ahit = ahit;
+    a.apw = apw;
     a.stage = (WalkRec*)(D + o_stage);
     a.out = (WalkRec*)(D + o_out);
     a.fout = (WalkFileOut*)(D + o_fout);
@@ -2231,37 +2241,68 @@ static int match_walk_files(sydelta_index* ix, const uint8_t* d_buf, const uint6
         unsigned long long tk[16];
         HIP_TRY(hipMemcpyAsync(tk, a.ticks, sizeof tk, hipMemcpyDeviceToHost, s));
         HIP_TRY(hipStreamSynchronize(s));
-        fprintf(stderr, "sydelta file walk phases (thread 0 ticks, 100 MHz, summed over files): setup %llu hash %llu "
+        fprintf(stderr, "sydelta file walk phases (wave ticks, 100 MHz, summed over units): setup %llu hash %llu "
                 "lookup %llu stage %llu roll %llu verify %llu out %llu | passes %llu windows %llu rolls %llu "
                 "verify batches %llu\n", tk[0], tk[1], tk[2], tk[3], tk[4], tk[5], tk[6], tk[8], tk[9], tk[10], tk[11]);
     }
-    // the host table in ph is dead once the upload ran: the counts come back over it
-    WalkFileOut* fo = (WalkFileOut*)ph.p;
-    uint64_t* tot = (uint64_t*)(ph.p + fout_bytes);
-    HIP_TRY(hipMemcpyAsync(fo, a.fout, fout_bytes, hipMemcpyDeviceToHost, s));
-    HIP_TRY(hipMemcpyAsync(tot, a.total, 8, hipMemcpyDeviceToHost, s));
+    // the unit table in ph is dead once the upload ran: the counts come back over it
+    HIP_TRY(hipMemcpyAsync(ph.p, a.fout, fout_bytes, hipMemcpyDeviceToHost, s));
+    HIP_TRY(hipMemcpyAsync(ph.p + fout_bytes, a.total, 8, hipMemcpyDeviceToHost, s));
     HIP_TRY(hipStreamSynchronize(s));
-    const double t_kern = ms_since(t0);
-    const uint64_t nrec = *tot;
-    if (nrec > rec_total) return fail(SYDELTA_E_KERNEL, "file walk: %llu records (capacity %llu)",
-                                      (unsigned long long)nrec, (unsigned long long)rec_total);
-    // the counts out of the pinned buffer, the records into it (grown when needed)
-    const std::vector<WalkFileOut> fov(fo, fo + nf);
-    const WalkFileOut* FO = fov.data();
-    const size_t rbytes = sizeof(WalkRec) * nrec;
-    if (ph.bytes < rbytes) {
-        (void)hipHostFree(ph.p);
-        ph = PinnedHits();
-        HIP_TRY(hipHostMalloc((void**)&ph.p, rbytes * 5 / 4, hipHostMallocDefault));
-        ph.bytes = rbytes * 5 / 4;
-    }
-    const WalkRec* R = (const WalkRec*)ph.p;
+    res.ms_kernel = ms_since(t0);
+    const uint64_t nrec = *(const uint64_t*)(ph.p + fout_bytes);
+    if (nrec > rec_total)
+        return fail(SYDELTA_E_KERNEL, "walk: %llu records (capacity %llu)", (unsigned long long)nrec,
+                    (unsigned long long)rec_total);
+    res.out.assign((const WalkFileOut*)ph.p, (const WalkFileOut*)ph.p + nu);
+    if (int r = pinned_at_least(ph, sizeof(WalkRec) * nrec + 16)) return r;
     if (nrec) {
-        HIP_TRY(hipMemcpyAsync((void*)R, a.out, rbytes, hipMemcpyDeviceToHost, s));
+        HIP_TRY(hipMemcpyAsync(ph.p, a.out, sizeof(WalkRec) * nrec, hipMemcpyDeviceToHost, s));
         HIP_TRY(hipStreamSynchronize(s));
     }
-    const double t_d2h = ms_since(t0);
-    // expand each file's records into its op array (recycled arrays: no page faults)
+    res.rec = (const WalkRec*)ph.p;
+    res.nrec = nrec;
+    res.ms_d2h = ms_since(t0) - res.ms_kernel;
+    return SYDELTA_OK;
+}
+
+// The ops of records [r0, r1) into w (Copy sizes from the basis file's blocks); returns the
+// data ops and literal bytes written.
+static inline void expand_records(const WalkRec* r0, const WalkRec* r1, uint64_t n, uint64_t bb, uint64_t nbf,
+                                  uint64_t ls, sydelta_op* w, uint64_t* nd, uint64_t* lb) {
+    for (const WalkRec* r = r0; r < r1; ++r) {
+        if (!r->kind) {
+            *w++ = {SYDELTA_OP_DATA, 0, r->off, r->a};
+            ++*nd;
+            *lb += r->a;
+            continue;
+        }
+        for (uint64_t g = r->a - bb, e = g + r->kind; g < e; ++g) *w++ = {SYDELTA_OP_COPY, 0, g * n, g + 1 == nbf ? ls : n};
+    }
+}
+static inline uint64_t records_ops(const WalkRec* r0, const WalkRec* r1) {
+    uint64_t k = 0;
+    for (const WalkRec* r = r0; r < r1; ++r) k += r->kind ? r->kind : 1;
+    return k;
+}
+
+// The batched match with the walk on the device: one unit per file.
+static int match_walk_files(sydelta_index* ix, const uint8_t* d_buf, const uint64_t* src_off, const uint64_t* src_len,
+                            hipStream_t s, Profiler* prof, sydelta_delta_batch* b) {
+    static const bool host_timing = getenv("SYDELTA_HOST_TIMING") != nullptr;
+    const uint64_t n = ix->bs, nf = ix->nfiles;
+    std::vector<WalkUnit> units(nf);
+    uint64_t rec_off = 0;
+    for (uint64_t f = 0; f < nf; ++f) {
+        const uint64_t len = src_len[f], nbf = ix->fblk[f + 1] - ix->fblk[f];
+        const uint64_t p1 = (nbf && len >= n) ? len - n + 1 : 0;  // an empty signature matches nothing (generator.rs:121)
+        units[f] = WalkUnit{src_off[f], len, 0, p1, p1, rec_off, 0, (uint32_t)f, 1};
+        rec_off += 2 * (p1 / n) + 4;
+    }
+    WalkResult res;
+    if (int r = run_walk(ix, d_buf, units, nullptr, nullptr, true, s, prof, res)) return r;
+    const auto t1 = std::chrono::steady_clock::now();
+    // each file's records into its op array (recycled arrays: no page faults)
     const int nthr = nf >= 64 ? walk_threads() : 1;
     std::atomic<uint64_t> next{0};
     std::vector<sydelta_match_stats> part(nthr);
@@ -2271,25 +2312,14 @@ static int match_walk_files(sydelta_index* ix, const uint8_t* d_buf, const uint6
             const uint64_t f0 = next.fetch_add(64);
             if (f0 >= nf) break;
             for (uint64_t f = f0; f < std::min<uint64_t>(nf, f0 + 64); ++f) {
-                const WalkFileOut& o = FO[f];
+                const WalkFileOut& o = res.out[f];
                 sydelta_delta& d = b->d[f];
-                const uint64_t bb = ix->fblk[f], nbf = ix->fblk[f + 1] - bb, ls = ix->last_size[f];
-                uint64_t nops = 0;
-                for (uint32_t i = 0; i < o.count; ++i) nops += R[o.base + i].kind ? R[o.base + i].kind : 1;
+                const WalkRec* r0 = res.rec + o.base;
+                const uint64_t nops = records_ops(r0, r0 + o.count);
                 d.ops.resize(nops);
-                sydelta_op* w = d.ops.data();
                 uint64_t nd = 0, lb = 0;
-                for (uint32_t i = 0; i < o.count; ++i) {
-                    const WalkRec& r = R[o.base + i];
-                    if (!r.kind) {
-                        *w++ = {SYDELTA_OP_DATA, 0, r.off, r.a};
-                        ++nd;
-                        lb += r.a;
-                        continue;
-                    }
-                    for (uint64_t g = r.a - bb, e = g + r.kind; g < e; ++g)
-                        *w++ = {SYDELTA_OP_COPY, 0, g * n, g + 1 == nbf ? ls : n};
-                }
+                expand_records(r0, r0 + o.count, n, ix->fblk[f], ix->fblk[f + 1] - ix->fblk[f], ix->last_size[f],
+                               d.ops.data(), &nd, &lb);
                 d.stats.copy_ops = nops - nd;
                 d.stats.data_ops = nd;
                 d.stats.literal_bytes = lb;
@@ -2312,14 +2342,15 @@ static int match_walk_files(sydelta_index* ix, const uint8_t* d_buf, const uint6
         b->total.weak_hits += p.weak_hits;
         b->total.verified_hits += p.verified_hits;
     }
+    PinnedHits& ph = thread_pinned_hits();
     if (ph.bytes > kPinnedHitsKeep) {
         (void)hipHostFree(ph.p);
         ph = PinnedHits();
     }
     if (host_timing)
         fprintf(stderr, "sydelta file walk: %llu files, %llu records: kernel+counts %.3f ms, records D2H %.3f ms, "
-                "expand %.3f ms\n", (unsigned long long)nf, (unsigned long long)nrec, t_kern, t_d2h - t_kern,
-                ms_since(t0) - t_d2h);
+                "expand %.3f ms\n", (unsigned long long)nf, (unsigned long long)res.nrec, res.ms_kernel, res.ms_d2h,
+                ms_since(t1));
     return SYDELTA_OK;
 }
 
@@ -3178,7 +3209,144 @@ struct sydelta_chunk {
     int tail_flag = 0;
     uint64_t file_len = 0;
     BasisInfo bi{0, 0, 0};
+    bool dev_walk = false;  // K10 over the chunk's segments (chunk_walk_device)
 };
+
+// K10 over a chunk (C5, and the streamed path API's chunks): the aligned probe's results
+// stay on the device and the walk runs there, one wave per segment of kChunkSegBlocks
+// blocks, each from its segment's start; a segment whose true entry (the previous one's
+// exit) differs is walked again from it (after a Copy that crosses the boundary).
+// SYDELTA_CHUNK_WALK=0, or SYDELTA_PROBE=0, keeps the classifier + host walk.
+namespace {
+constexpr uint64_t kChunkSegBlocks = 128;
+bool chunk_walk_ok(const sydelta_index* idx) {
+    const char* e = getenv("SYDELTA_CHUNK_WALK");
+    if (e && e[0] == '0') return false;
+    const uint64_t n = idx->bs;
+    return idx->nfiles == 1 && n % 64 == 0 && n >= 256 && n <= kWalkMaxN && probe_mode_env() != 0;
+}
+
+int chunk_walk_device(sydelta_chunk* ch, uint64_t entry, uint64_t* exit_pos, sydelta_delta* d) {
+    static const bool host_timing = getenv("SYDELTA_HOST_TIMING") != nullptr;
+    const auto t_begin = std::chrono::steady_clock::now();
+    Classifier& C = ch->C;
+    const Src& c = C.src[0];
+    const uint64_t n = C.n, seg = kChunkSegBlocks * n;
+    // units: the segments of [entry, c.p1), the last one final when the file ends in the chunk
+    auto make_units = [&](uint64_t from, std::vector<WalkUnit>& units) {
+        units.clear();
+        uint64_t rec = 0;
+        const uint64_t lo = std::max(from, c.p0);
+        uint64_t s0 = c.p0 + (lo > c.p0 ? (lo - c.p0) / seg * seg : 0);
+        do {
+            const uint64_t e = std::min(c.p1, s0 + seg), en = std::max(lo, s0);
+            const bool last = e >= c.p1;
+            units.push_back(WalkUnit{0, ch->file_len, en, std::max(e, en), c.p1, rec, c.kb, 0,
+                                     (uint32_t)(last && ch->final_src)});
+            rec += 2 * ((std::max(e, en) - en) / n) + 4;
+            s0 = e;
+        } while (s0 < c.p1);
+    };
+    std::vector<WalkUnit> units;
+    make_units(entry, units);
+    const uint32_t* ahit = c.probed ? C.d_probe_out : nullptr;
+    const uint32_t* apw = c.probed ? C.d_probe_pw : nullptr;
+    WalkResult res;
+    if (int r = run_walk(C.ix, C.base, units, ahit, apw, false, C.s, C.prof, res)) return r;
+    std::vector<WalkFileOut> out = res.out;
+    std::vector<WalkRec> rec(res.rec, res.rec + res.nrec);  // the pinned buffer is reused by re-walks
+    // chain the segments: each must start where the previous one left.  Every segment whose
+    // entry differs from the previous one's exit is walked again from that exit, all of them
+    // in one launch; a re-walk usually leaves where the first walk did (a shifted source
+    // keeps its phase), so this converges in a round or two.
+    std::vector<std::pair<uint64_t, uint64_t>> span(units.size());  // records [first, end) in rec
+    for (size_t u = 0; u < units.size(); ++u) span[u] = {out[u].base, (uint64_t)out[u].base + out[u].count};
+    int rounds = 0;
+    for (;;) {
+        std::vector<size_t> bad;
+        std::vector<WalkUnit> again;
+        uint64_t roff = 0;
+        for (size_t u = 1; u < units.size(); ++u) {
+            const uint64_t ex = out[u - 1].exit;  // inside unit u: a Copy reaches < n bytes past a boundary
+            if (ex == units[u].entry) continue;
+            units[u].entry = ex;
+            units[u].end = std::max(units[u].end, ex);
+            WalkUnit w = units[u];
+            w.rec_off = roff;
+            roff += 2 * ((w.end - w.entry) / n) + 4;
+            again.push_back(w);
+            bad.push_back(u);
+        }
+        if (bad.empty()) break;
+        ++rounds;
+        WalkResult r1;
+        if (int r = run_walk(C.ix, C.base, again, ahit, apw, false, C.s, C.prof, r1)) return r;
+        for (size_t j = 0; j < bad.size(); ++j) {
+            const size_t u = bad[j];
+            span[u] = {rec.size(), rec.size() + r1.out[j].count};
+            rec.insert(rec.end(), r1.rec + r1.out[j].base, r1.rec + r1.out[j].base + r1.out[j].count);
+            out[u] = r1.out[j];
+        }
+    }
+    // the ops: each segment's, a Data op that ends at a segment's end joined with the next
+    // segment's first Data op (literal runs stay maximal, generator.rs:186-197)
+    const size_t nu = units.size();
+    std::vector<uint64_t> first(nu + 1, 0);
+    std::vector<uint8_t> join(nu, 0);  // unit u's first op extends unit u-1's last Data op
+    for (size_t u = 0; u < nu; ++u) {
+        const WalkRec* r0 = rec.data() + span[u].first;
+        const WalkRec* r1 = rec.data() + span[u].second;
+        uint64_t k = records_ops(r0, r1);
+        if (u && r0 < r1 && !r0->kind) {
+            const WalkRec* pl = rec.data() + span[u - 1].second - 1;
+            if (span[u - 1].second > span[u - 1].first && !pl->kind && pl->off + pl->a == r0->off) {
+                join[u] = 1;
+                --k;
+            }
+        }
+        first[u + 1] = first[u] + k;
+    }
+    OpVec& ops = d->ops;
+    if (ops.capacity() < first[nu]) ops = take_ops(first[nu]);
+    ops.resize(first[nu]);
+    std::vector<uint64_t> nd(nu, 0), lb(nu, 0);
+    const uint64_t nbf = C.ix->fblk[1], ls = C.ix->last_size[0];
+    auto fill = [&](size_t u) {
+        const WalkRec* r0 = rec.data() + span[u].first;
+        const WalkRec* r1 = rec.data() + span[u].second;
+        sydelta_op* w = ops.data() + first[u];
+        if (join[u]) {  // this segment's leading literal run belongs to the previous op
+            lb[u] += r0->a;
+            ++r0;
+        }
+        expand_records(r0, r1, n, 0, nbf, ls, w, &nd[u], &lb[u]);
+    };
+    const int nthr = nu >= 64 ? walk_threads() : 1;
+    if (!run_parallel(nthr, [&](int t) {
+            for (size_t u = nu * t / nthr; u < nu * (t + 1) / nthr; ++u) fill(u);
+        }))
+        return fail(SYDELTA_E_OOM, "out of host memory (op lists)");
+    uint64_t data_ops = 0, lit = 0, hits = 0, weak = 0;
+    for (size_t u = 0; u < nu; ++u) {
+        if (join[u]) ops[first[u] - 1].b += rec[span[u].first].a;
+        data_ops += nd[u];
+        lit += lb[u];
+        hits += out[u].hits;
+        weak += out[u].weak_hits;
+    }
+    d->stats.data_ops = data_ops;
+    d->stats.copy_ops = ops.size() - data_ops;
+    d->stats.literal_bytes = lit;
+    d->stats.verified_hits = hits;
+    d->stats.weak_hits = weak;
+    *exit_pos = out[nu - 1].exit;
+    if (host_timing)
+        fprintf(stderr, "sydelta chunk walk: %zu segments, %llu records, %d re-walk rounds: kernel+counts %.3f ms, "
+                "records D2H %.3f ms, %zu ops, all %.3f ms\n", nu, (unsigned long long)res.nrec, rounds, res.ms_kernel,
+                res.ms_d2h, ops.size(), ms_since(t_begin));
+    return SYDELTA_OK;
+}
+}  // namespace
 
 extern "C" int sydelta_chunk_classify(sydelta_index* idx, const uint8_t* d_buf, uint64_t buf_pos, uint64_t buf_len,
                                       uint64_t file_len, uint64_t pos_begin, uint64_t pos_end, void* stream,
@@ -3226,6 +3394,15 @@ extern "C" int sydelta_chunk_classify(sydelta_index* idx, const uint8_t* d_buf, 
     ch->final_src = final_src;
     ch->file_len = file_len;
     ch->bi = BasisInfo{0, idx->fblk[1], idx->last_size[0]};
+    if (chunk_walk_ok(idx)) {  // K10 walks the chunk on the device: only the aligned probe here
+        ch->dev_walk = true;
+        C.device_only = true;
+        if (c.p1 > c.p0)
+            if (int r = C.probe(1)) return r;
+        C.prof = nullptr;
+        *out = ch.release();
+        return SYDELTA_OK;
+    }
     // windows above the LDS scans' limit without k_scan_g: every position scanned (k_scan,
     // one launch per range), no probe, as match_impl does
     if (int r = C.classify(n > scan_max_window() && !wide_scan(idx) ? 0 : probe_mode_env())) return r;
@@ -3254,6 +3431,13 @@ extern "C" int sydelta_chunk_walk(sydelta_chunk* ch, uint64_t entry, uint64_t* e
     d->source_size = ch->file_len;
     d->block_size = C.n;
     d->stats.positions = c.p1 - c.p0;
+    if (ch->dev_walk) {
+        const int r = chunk_walk_device(ch, entry, exit_pos, d.get());
+        C.prof = nullptr;
+        if (r) return r;
+        *out = d.release();
+        return SYDELTA_OK;
+    }
     const int r = C.walk(0, entry, ch->bi, ch->final_src, ch->tail_flag, d.get(), exit_pos);
     C.prof = nullptr;
     if (r) return r;

@@ -123,15 +123,18 @@ __device__ __forceinline__ bool tail_matches(const uint8_t* p, uint64_t ls, uint
     return __builtin_amdgcn_readlane((int)(wk == weak && st == strong ? 1u : 0u), 0) != 0;
 }
 
-__global__ __launch_bounds__(64) void k_walk_files(WalkArgs a) {
+// kLdsFilt: the unit's Bloom filter is copied to LDS (a batch's small files), else read from
+// global memory (L2-resident: a large single-file index, the segments of a chunk).
+template <bool kLdsFilt>
+__global__ __launch_bounds__(64, 4) void k_walk_files(WalkArgs a) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-    const uint32_t f = blockIdx.x;
+    const WalkUnit U = a.units[blockIdx.x];
     const uint32_t lane = threadIdx.x, row = lane >> 4;
     const uint32_t n = a.n;
-    const FileIx F = a.files[f];
+    const FileIx F = a.files[U.file];
     const uint32_t fw = 1u << (32 - F.fwshift);
     const WalkLds L = walk_lds(a.fw_max);
-    uint32_t* filt = (uint32_t*)(smem + L.filt);
+    const uint32_t* filt = kLdsFilt ? (const uint32_t*)(smem + L.filt) : a.filt + F.filt_off;
     uint32_t* ntab = (uint32_t*)(smem + L.ntab);
     uint32_t* pw = (uint32_t*)(smem + L.pw);
     uint64_t* pst = (uint64_t*)(smem + L.pst);
@@ -146,24 +149,25 @@ __global__ __launch_bounds__(64) void k_walk_files(WalkArgs a) {
     auto wcount = [&](int k, uint64_t v) {
         if (a.ticks && lane == 0) atomicAdd(a.ticks + k, (unsigned long long)v);
     };
-    const uint8_t* src = a.base + a.soff[f];
-    const uint64_t len = a.slen[f];
-    const uint64_t gb0 = a.fblk[f], nbf = a.fblk[f + 1] - gb0, ls = a.last_size[f];
-    const uint64_t p1 = (nbf && len >= n) ? len - n + 1 : 0;  // full-window starts [0, p1)
+    const uint8_t* src = a.base + U.src;
+    const uint64_t len = U.len, end = U.end;
+    const uint64_t gb0 = a.fblk[U.file], nbf = a.fblk[U.file + 1] - gb0, ls = a.last_size[U.file];
 
     {  // the file's Bloom filter, the roll table
-        const uint4* g = (const uint4*)(a.filt + F.filt_off);
-        for (uint32_t i = lane; i < fw / 4; i += 64) ((uint4*)filt)[i] = g[i];
+        if (kLdsFilt) {
+            const uint4* g = (const uint4*)(a.filt + F.filt_off);
+            for (uint32_t i = lane; i < fw / 4; i += 64) ((uint4*)(smem + L.filt))[i] = g[i];
+        }
         for (uint32_t i = lane; i < 256; i += 64) ntab[i] = kMod - 1 - (a.nm * i) % kMod;
     }
     // the tail rule (generator.rs:156-184): the suffix of the basis's last block's size
-    const bool tail_ok = nbf && ls < n && len >= ls &&
+    const bool tail_ok = U.final_ && nbf && ls < n && len >= ls &&
                          tail_matches(src + (len - ls), ls, a.weak[gb0 + nbf - 1], a.strong[gb0 + nbf - 1]);
     __syncthreads();  // the filter and ntab in LDS
     wtick(kWtSetup);
 
     // run-length coded output (lane 0 writes; the state is wave-uniform)
-    WalkRec* stg = a.stage + a.rec_off[f];
+    WalkRec* stg = a.stage + U.rec_off;
     uint32_t nrec = 0, ck = 0, ca = 0;  // the open Copy run: ck Copies from block ca (ck 0: none)
     auto put = [&](uint32_t kind, uint32_t aa, uint64_t off) {
         if (lane == 0) stg[nrec] = WalkRec{kind, aa, off};
@@ -190,13 +194,13 @@ __global__ __launch_bounds__(64) void k_walk_files(WalkArgs a) {
     };
     uint32_t weak_hits = 0, hits = 0;
 
-    uint64_t x = 0, lit = 0;
+    uint64_t x = U.entry, lit = U.entry;
     uint32_t phi = 0xFFFFFFFFu;
     uint64_t rk0 = 0, rk1 = 0;  // lane w holds the result (rres) and weak (rwk) of block rk0 + w at phase phi
     uint64_t kph = 0;           // the block where the walk took phase phi
     uint32_t rres = kNoBlock, rwk = 0;
 #pragma unroll 1
-    while (x < p1) {
+    while (x < end) {
         const uint64_t k = x / n;
         const uint32_t ph = (uint32_t)(x - k * n);
         if (ph != phi || k >= rk1) {
@@ -205,8 +209,20 @@ __global__ __launch_bounds__(64) void k_walk_files(WalkArgs a) {
             // 64): a long run of Copies costs few passes, and a phase change soon after a pass
             // began wastes little of it.
             if (ph != phi) kph = k;
-            const uint64_t left = (p1 - x + n - 1) / n;
+            const uint64_t left = (end - x + n - 1) / n;
             const uint32_t cnt = (uint32_t)min(left, min((uint64_t)kWMaxPass, max((uint64_t)4, 2 * (k - kph))));
+            if (ph == 0 && a.ahit) {  // phase 0 with the aligned probe's results: nothing to hash
+                rres = kNoBlock;
+                rwk = 0;
+                if (lane < cnt) {
+                    rres = a.ahit[k + lane - U.kb];
+                    rwk = a.apw[k + lane - U.kb];
+                }
+                phi = ph;
+                rk0 = k;
+                rk1 = k + cnt;
+                goto have_pass;
+            }
 #pragma unroll 1
             for (uint32_t j = 0; j < cnt; j += 4) {
                 const uint32_t w = j + row;
@@ -239,6 +255,7 @@ __global__ __launch_bounds__(64) void k_walk_files(WalkArgs a) {
             rk0 = k;
             rk1 = k + cnt;
         }
+    have_pass:
         const uint32_t blk = rl(rres, (uint32_t)(k - rk0));
         if (blk != kNoBlock) {  // generator.rs:135-146
             ++hits;
@@ -248,7 +265,7 @@ __global__ __launch_bounds__(64) void k_walk_files(WalkArgs a) {
             lit = x;
             continue;
         }
-        // ---- the window at x misses: roll (x, min(x + n, p1)) for the first hit.  A pass
+        // ---- the window at x misses: roll (x, min(x + n, end)) for the first hit.  A pass
         // rolls 4096 window starts from the window at its base b = y0 - 1 (the phase window x,
         // then the previous pass's last start), whose (A, B) it knows: lane l's first start
         // p = b + d, d = 64 l + 1, follows in closed form (rolling.rs:66-79 applied d times):
@@ -256,7 +273,7 @@ __global__ __launch_bounds__(64) void k_walk_files(WalkArgs a) {
         // with c_j = in_j - out_j (out_j = byte b + j, in_j = byte b + n + j), C(d) = sum_{j<d} c_j,
         // J(d) = sum_{j<d} j c_j, Out(d) = sum_{j<d} out_j: exclusive wave scans of the lanes'
         // 64-byte group sums (as residues mod M), each lane's bytes in registers.
-        const uint64_t yend = min(x + n, p1);
+        const uint64_t yend = min(x + n, end);  // later starts are the next unit's
         uint64_t q = yend;
         uint32_t qb = kNoBlock;
         uint32_t wbase = rl(rwk, (uint32_t)(k - rk0));  // weak of the window at b
@@ -305,32 +322,57 @@ __global__ __launch_bounds__(64) void k_walk_files(WalkArgs a) {
             }
             uint64_t pm = 0;
             uint32_t wlast = 0;
-            // four starts per round from the first dword, then the dwords move down one
-            // (a loop, not unrolled: the register arrays keep constant indices)
+            // a global filter (a large index: 16 bits per key, ~0.8 % of starts pass) keeps the
+            // weak values of a lane's first four passes, which are looked up in the exact table
+            // below before anything is hashed (8 KiB per candidate otherwise)
+            uint32_t wp[4] = {0, 0, 0, 0}, wpi[4] = {0, 0, 0, 0}, np = 0;
+            // sixteen starts per round from the first four dwords (their filter words loaded
+            // together: a global filter's reads are L2 round trips), then the dwords move down
+            // four (a loop, not unrolled: the register arrays keep constant indices)
 #pragma unroll 1
-            for (uint32_t t = 0; t < kWRun / 4; ++t) {
-                const uint32_t wo = xo[0], wi = xi[0];
+            for (uint32_t t = 0; t < kWRun / 16; ++t) {
+                uint32_t hq[16], fwv[16], wv[16];
 #pragma unroll
-                for (int b = 0; b < 4; ++b) {
-                    const uint32_t i = 4 * t + b;
+                for (int b = 0; b < 16; ++b) {
                     const ProbeHash h = probe_hash(am, bm);
-                    const uint64_t pass = filt_bit(filt[h.r >> F.fwshift], h.q);
-                    pm |= (i < nvalid ? pass : 0ull) << i;
-                    wlast = (bm << 16) | am;
-                    const uint32_t out = (wo >> (8 * b)) & 0xFF;
-                    const uint32_t in = (wi >> (8 * b)) & 0xFF;
+                    hq[b] = h.q;
+                    fwv[b] = filt[h.r >> F.fwshift];
+                    wv[b] = (bm << 16) | am;
+                    const uint32_t out = (xo[b >> 2] >> (8 * (b & 3))) & 0xFF;
+                    const uint32_t in = (xi[b >> 2] >> (8 * (b & 3))) & 0xFF;
                     const uint32_t u = am + in + (kMod - out);  // [M-255, 2M+255)
                     am = min(u, min(u - kMod, u - 2 * kMod));
                     const uint32_t v = bm + am + ntab[out];  // [0, 3M)
                     bm = min(v, min(v - kMod, v - 2 * kMod));
                 }
+                wlast = wv[15];
 #pragma unroll
-                for (int j = 0; j < 15; ++j) {
-                    xo[j] = xo[j + 1];
-                    xi[j] = xi[j + 1];
+                for (int b = 0; b < 16; ++b) {
+                    const uint32_t i = 16 * t + b;
+                    const uint32_t pass = i < nvalid ? filt_bit(fwv[b], hq[b]) : 0u;
+                    pm |= (uint64_t)pass << i;
+                    if (!kLdsFilt && pass) {
+#pragma unroll
+                        for (int j = 0; j < 4; ++j)
+                            if (np == (uint32_t)j) {
+                                wp[j] = wv[b];
+                                wpi[j] = i;
+                            }
+                        ++np;
+                    }
+                }
+#pragma unroll
+                for (int j = 0; j < 12; ++j) {
+                    xo[j] = xo[j + 4];
+                    xi[j] = xi[j + 4];
                 }
             }
             wbase = rl(wlast, 63);  // the next pass's base: lane 63's last start, b + 4096
+            if (!kLdsFilt) {  // exact-table lookups of the first passes (generator.rs:121-124)
+#pragma unroll
+                for (int j = 0; j < 4; ++j)
+                    if ((uint32_t)j < np && table_find(a.keys + F.slot_off, F.bmask, wp[j]) < 0) pm &= ~(1ull << wpi[j]);
+            }
             wtick(kWtRoll);
             // verify the candidates four at a time in position order (generator.rs:121-133);
             // weak_hits counts the verified windows
@@ -382,14 +424,23 @@ __global__ __launch_bounds__(64) void k_walk_files(WalkArgs a) {
             x = yend;  // the next phase window (or the end of the full windows)
         }
     }
-    // the walk's end: the tail rule at p* = len - last_size, then the last literal run
-    if (tail_ok && ls <= len && len - ls >= lit) {
-        data(lit, len - ls);
-        copy((uint32_t)(gb0 + nbf - 1));
-        lit = len;
-        ++hits;
+    // the walk's end.  A final unit: the tail rule at p* = len - last_size, then the last
+    // literal run; another: the literal run up to end (the next unit continues it; the
+    // host joins the two Data ops) and the exit (> end after a Copy that crosses it).
+    uint64_t exit;
+    if (U.final_) {
+        if (tail_ok && ls <= len && len - ls >= lit) {
+            data(lit, len - ls);
+            copy((uint32_t)(gb0 + nbf - 1));
+            lit = len;
+            ++hits;
+        }
+        data(lit, len);
+        exit = len;
+    } else {
+        data(lit, end);
+        exit = max(x, end);
     }
-    data(lit, len);
     close_run();
     // move the records to the compact output (one atomic per file)
     __threadfence_block();
@@ -400,7 +451,7 @@ __global__ __launch_bounds__(64) void k_walk_files(WalkArgs a) {
         const volatile WalkRec* r = stg + i;
         a.out[base + i] = WalkRec{r->kind, r->a, r->off};
     }
-    if (lane == 0) a.fout[f] = WalkFileOut{(uint32_t)base, nrec, weak_hits, hits};
+    if (lane == 0) a.fout[blockIdx.x] = WalkFileOut{(uint32_t)base, nrec, weak_hits, hits, exit, 0};
     wtick(kWtOut);
 }
 
@@ -408,12 +459,15 @@ __global__ __launch_bounds__(64) void k_walk_files(WalkArgs a) {
 // Launch wrapper
 // ===========================================================================
 hipError_t launch_walk_files(const WalkArgs& a, hipStream_t s, Profiler* prof) {
-    if (!a.nfiles) return hipSuccess;
-    if (a.n % 64 != 0 || a.n < 256 || a.n > kWalkMaxN || a.fw_max > kWalkMaxWords || a.fw_max < 4)
+    if (!a.nunits) return hipSuccess;
+    if (a.n % 64 != 0 || a.n < 256 || a.n > kWalkMaxN || a.fw_max > kWalkMaxWords || (a.fw_max && a.fw_max < 4))
         return hipErrorInvalidValue;
     const WalkLds L = walk_lds(a.fw_max);
     ProfScope ps(prof, s, "k_walk_files");
-    hipLaunchKernelGGL(k_walk_files, dim3(a.nfiles), dim3(64), L.total, s, a);
+    if (a.fw_max)
+        hipLaunchKernelGGL(k_walk_files<true>, dim3(a.nunits), dim3(64), L.total, s, a);
+    else
+        hipLaunchKernelGGL(k_walk_files<false>, dim3(a.nunits), dim3(64), L.total, s, a);
     return hipGetLastError();
 }
 

@@ -206,12 +206,14 @@ hipError_t launch_tail(const uint8_t* d_buf, const TailJob* d_jobs, uint32_t njo
 // merge, successors, pointer-jumping path marking, op emission; a.res receives the
 // totals.  All arrays of a are device memory sized as ChainArgs documents.
 hipError_t launch_chain(const chain::ChainArgs& a, hipStream_t s, Profiler* prof);
-// K10: the whole greedy walk (generator.rs:116-221) of each of many small files on the
-// device, one workgroup per file (k_walk_files), for batched indexes whose per-file Bloom
-// filters fit LDS (<= kWalkMaxWords words) at block sizes n % 64 == 0, 256 <= n <=
-// kWalkMaxN.  The ops come back run-length coded: a Data op, or a run of Copies of
-// consecutive global basis blocks (each Copy's size follows from its block: the basis
-// file's last block has last_size, every other one n).
+// K10: the greedy walk (generator.rs:116-221) on the device, one wave per unit
+// (k_walk_files): a unit is a whole file of a batch (C4's small files) or a segment of a
+// chunk of one file (C5), walked from its entry until it leaves [entry, end).  Block sizes
+// n % 64 == 0, 256 <= n <= kWalkMaxN.  A batch's per-file Bloom filters are copied to LDS
+// (<= kWalkMaxWords words); a large single-file index's filter is read from L2.  The ops
+// come back run-length coded: a Data op, or a run of Copies of consecutive global basis
+// blocks (each Copy's size follows from its block: the basis file's last block has
+// last_size, every other one n).
 constexpr uint32_t kWalkMaxWords = 4096;
 constexpr uint32_t kWalkMaxN = 8192;
 struct WalkRec {
@@ -219,18 +221,30 @@ struct WalkRec {
     uint32_t a;     // Data: length; Copy run: its first global block
     uint64_t off;   // Data: offset in the source file
 };
+struct WalkUnit {
+    uint64_t src;      // byte offset of source position 0 from the launch base
+    uint64_t len;      // source file length (a final unit's tail rule and last literal run)
+    uint64_t entry;    // the first position walked
+    uint64_t end;      // the walk leaves the unit at its first position >= end (<= p1)
+    uint64_t p1;       // full-window starts [0, p1) of the source (0 without a signature)
+    uint64_t rec_off;  // staging region: stage + rec_off (2 * ((end - entry) / n) + 4 records)
+    uint64_t kb;       // with probe results (WalkArgs::ahit): block k's at ahit[k - kb]
+    uint32_t file;     // basis file (FileIx) of the index
+    uint32_t final_;   // 1: the source ends in this unit (tail rule, last literal run to len)
+};
 struct WalkFileOut {
-    uint32_t base, count;  // the file's records: out[base, base + count)
-    uint32_t weak_hits;    // windows whose weak value has candidates (examined ones)
+    uint32_t base, count;  // the unit's records: out[base, base + count)
+    uint32_t weak_hits;    // candidate windows verified (passed the Bloom filter)
     uint32_t hits;         // windows classified as hits
+    uint64_t exit;         // where the walk left the unit (>= end; a final unit: len)
+    uint64_t pad;
 };
 struct WalkArgs {
-    const uint8_t* base;         // launch base; file f's source at soff[f], slen[f] bytes
-    const uint64_t* soff;
-    const uint64_t* slen;
-    const uint64_t* rec_off;     // file f's staging region: stage + rec_off[f] (2 * (slen/n) + 4 records)
-    const uint64_t* last_size;   // per file (0: empty signature)
-    uint32_t nfiles, n, nm, fw_max;
+    const uint8_t* base;         // launch base
+    const WalkUnit* units;
+    const uint64_t* last_size;   // per basis file (0: empty signature)
+    uint32_t nunits, n, nm;
+    uint32_t fw_max;             // LDS filter words (0: the filter is read from global memory)
     const FileIx* files;
     const uint64_t* fblk;
     const uint32_t* filt;
@@ -241,8 +255,10 @@ struct WalkArgs {
     const uint64_t* cstrong;
     const uint32_t* weak;        // the index's signature copies (the tail rule)
     const uint64_t* strong;
+    const uint32_t* ahit;        // optional: the aligned probe's results (block k: its hit or none) ...
+    const uint32_t* apw;         // ... and its windows' weak values
     WalkRec* stage;
-    WalkRec* out;                // compacted records of every file
+    WalkRec* out;                // compacted records of every unit
     WalkFileOut* fout;
     unsigned long long* total;   // records placed in out (zeroed before the launch)
     unsigned long long* ticks;   // SYDELTA_PHASE_TIMING: 16 counters (zeroed), else null

@@ -572,9 +572,10 @@ hipError_t launch_chain(const chain::ChainArgs& a, hipStream_t, Profiler*) {
     return hipSuccess;
 }
 
-// K10: each file's greedy walk (generator.rs:116-221) with every visited window classified
-// exactly, its ops run-length coded as k_walk_files writes them (WalkRec), files placed in
-// order in the compact output.
+// K10: each unit's greedy walk (generator.rs:116-221) from its entry until it leaves
+// [entry, end), every visited window classified exactly, the ops run-length coded as
+// k_walk_files writes them (WalkRec), units placed in order in the compact output.  The
+// aligned probe's results, when given, must agree with the exact classification.
 hipError_t launch_walk_files(const WalkArgs& a, hipStream_t, Profiler*) {
     EmuTimer emu_t;
     if (a.n % 64 != 0 || a.n < 256 || a.n > kWalkMaxN || a.fw_max > kWalkMaxWords) return hipErrorInvalidValue;
@@ -583,10 +584,10 @@ hipError_t launch_walk_files(const WalkArgs& a, hipStream_t, Profiler*) {
     const FakeIndex& F = find_ix(key_ix);
     const uint64_t n = a.n;
     uint64_t placed = *a.total;
-    for (uint32_t f = 0; f < a.nfiles; ++f) {
-        const uint8_t* src = a.base + a.soff[f];
-        const uint64_t len = a.slen[f], gb0 = a.fblk[f], nbf = a.fblk[f + 1] - gb0, ls = a.last_size[f];
-        const uint64_t p1 = (nbf && len >= n) ? len - n + 1 : 0;
+    for (uint32_t u = 0; u < a.nunits; ++u) {
+        const WalkUnit& U = a.units[u];
+        const uint8_t* src = a.base + U.src;
+        const uint64_t len = U.len, gb0 = a.fblk[U.file], nbf = a.fblk[U.file + 1] - gb0, ls = a.last_size[U.file];
         std::vector<WalkRec> rec;
         uint32_t ck = 0, ca = 0, weak_hits = 0, hits = 0;
         auto close_run = [&] {
@@ -609,6 +610,7 @@ hipError_t launch_walk_files(const WalkArgs& a, hipStream_t, Profiler*) {
             }
         };
         uint64_t wa = 0, wb = 0, wpos = UINT64_MAX;  // rolling Adler state of the window at wpos
+        bool probe_ok = true;
         auto classify = [&](uint64_t x) {
             if (wpos != UINT64_MAX && x == wpos + 1) {
                 const uint64_t out = src[wpos], in = src[wpos + n];
@@ -621,12 +623,14 @@ hipError_t launch_walk_files(const WalkArgs& a, hipStream_t, Profiler*) {
             }
             wpos = x;
             bool wh = false;
-            const uint32_t blk = lookup(F, f, (uint32_t)((wb << 16) | wa), src + x, n, &wh);
+            const uint32_t w = (uint32_t)((wb << 16) | wa);
+            const uint32_t blk = lookup(F, U.file, w, src + x, n, &wh);
             weak_hits += wh;
+            if (a.ahit && x % n == 0 && (a.ahit[x / n - U.kb] != blk || a.apw[x / n - U.kb] != w)) probe_ok = false;
             return blk;
         };
-        uint64_t x = 0, lit = 0;
-        while (x < p1) {
+        uint64_t x = U.entry, lit = U.entry;
+        while (x < U.end) {
             const uint32_t blk = classify(x);
             if (blk != kNone) {
                 ++hits;
@@ -638,19 +642,27 @@ hipError_t launch_walk_files(const WalkArgs& a, hipStream_t, Profiler*) {
                 ++x;
             }
         }
-        if (nbf && ls < n && len >= ls && len - ls >= lit && adler(src + len - ls, ls) == a.weak[gb0 + nbf - 1] &&
-            oracle_xxh3_64(src + len - ls, ls) == a.strong[gb0 + nbf - 1]) {
-            data(lit, len - ls);
-            copy((uint32_t)(gb0 + nbf - 1));
-            lit = len;
-            ++hits;
+        if (!probe_ok) return hipErrorInvalidValue;  // the host handed over wrong probe results
+        uint64_t exit;
+        if (U.final_) {
+            if (nbf && ls < n && len >= ls && len - ls >= lit && adler(src + len - ls, ls) == a.weak[gb0 + nbf - 1] &&
+                oracle_xxh3_64(src + len - ls, ls) == a.strong[gb0 + nbf - 1]) {
+                data(lit, len - ls);
+                copy((uint32_t)(gb0 + nbf - 1));
+                lit = len;
+                ++hits;
+            }
+            data(lit, len);
+            exit = len;
+        } else {
+            data(lit, U.end);
+            exit = std::max(x, U.end);
         }
-        data(lit, len);
         close_run();
-        const uint64_t cap = 2 * (len / n) + 4;
+        const uint64_t cap = 2 * ((U.end - U.entry) / n) + 4;
         if (rec.size() > cap) return hipErrorInvalidValue;  // the kernel's staging region would overflow
         std::copy(rec.begin(), rec.end(), a.out + placed);
-        a.fout[f] = WalkFileOut{(uint32_t)placed, (uint32_t)rec.size(), weak_hits, hits};
+        a.fout[u] = WalkFileOut{(uint32_t)placed, (uint32_t)rec.size(), weak_hits, hits, exit, 0};
         placed += rec.size();
     }
     *a.total = placed;

@@ -22,10 +22,14 @@ pytestmark = [pytest.mark.gpu, pytest.mark.late]
 
 @pytest.fixture
 def device_walk():
-    keys = ("SYDELTA_DEVICE_WALK", "SYDELTA_DEVICE_WALK_MIN", "SYDELTA_PROBE", "SYDELTA_PHASE_PROBE")
+    keys = ("SYDELTA_DEVICE_WALK", "SYDELTA_DEVICE_WALK_MIN", "SYDELTA_PROBE", "SYDELTA_PHASE_PROBE",
+            "SYDELTA_CHUNK_WALK", "SYDELTA_FILE_WALK")
     old = {k: os.environ.get(k) for k in keys}
     os.environ["SYDELTA_DEVICE_WALK"] = "1"
     os.environ["SYDELTA_DEVICE_WALK_MIN"] = "1"
+    # K5b resolves the classifier's walks: chunks and batches go through the classifier, not K10
+    os.environ["SYDELTA_CHUNK_WALK"] = "0"
+    os.environ["SYDELTA_FILE_WALK"] = "0"
     # phase-probed sources are walked on the host (walk_device hands them back); the
     # phase probe is on by default since round 4
     os.environ["SYDELTA_PHASE_PROBE"] = "0"

@@ -1,9 +1,10 @@
-"""GPU parity of K10 (k_walk_files): the greedy walk of each file of a batch resolved on
-the device, one workgroup per file (generator.rs:116-221, the tail rule :156-184).
+"""GPU parity of K10 (k_walk_files): the greedy walk resolved on the device, one wave per
+unit (generator.rs:116-221, the tail rule :156-184) -- each file of a batch, or each
+segment of a chunk of one file (walked again from its true entry when the previous
+segment's last Copy crosses into it).
 
-Every case runs through the C ABI with SYDELTA_FILE_WALK=1 (the file walk for any batch
-it can serve) and is compared op for op with the C oracle; the same batches with
-SYDELTA_FILE_WALK=0 (the classifier path) must give the same lists."""
+Every case runs through the C ABI and is compared op for op with the C oracle, and with the
+classifier + host walk on the same inputs (SYDELTA_FILE_WALK=0 / SYDELTA_CHUNK_WALK=0)."""
 import random
 
 import numpy as np
@@ -168,3 +169,72 @@ def test_file_walk_long_literal_runs(gpu, oracle_c, monkeypatch):
     out, _, _ = _batch(gpu, pairs, bs, "1", monkeypatch)
     for i, ((src, basis), d) in enumerate(zip(pairs, out)):
         assert d.tuples() == _oracle_ops(oracle_c, src, basis, bs), i
+
+
+def _to_dev(data: bytes, pad: int = 16):
+    import torch
+
+    t = torch.zeros(len(data) + pad, dtype=torch.uint8, device="cuda")
+    if data:
+        t[:len(data)] = torch.frombuffer(bytearray(data), dtype=torch.uint8).cuda()
+    return t
+
+
+def _chunk_walk(gpu, src: bytes, basis: bytes, bs: int, bounds):
+    """Signature + index of basis, then the chunks [bounds[g], bounds[g+1]) of src
+    classified and walked in order (each from the previous one's exit), joined."""
+    b = _to_dev(basis)
+    w, s = gpu.signature(b[:len(basis)], bs)
+    nb = w.numel()
+    idx = gpu.Index(w, s, bs, (len(basis) - (nb - 1) * bs) if nb else 0)
+    L = len(src)
+    parts, entry, chunks = [], 0, []
+    for g in range(len(bounds) - 1):
+        p0, p1 = bounds[g], bounds[g + 1]
+        final = g == len(bounds) - 2
+        buf_pos = p0 & ~15
+        end = L if final else min(L, p1 + bs - 1)
+        chunks.append(gpu.Chunk(idx, _to_dev(src[buf_pos:end]), buf_pos, L, p0, p1 if not final else max(p1, L)))
+    for c in chunks:
+        d, entry = c.walk(entry)
+        parts.append(d)
+    for c in chunks:
+        c.close()
+    idx.close()
+    return gpu.join_deltas(parts, L, bs)
+
+
+@pytest.mark.parametrize("bs", [256, 4096, 8192])
+@pytest.mark.parametrize("nchunks", [1, 3])
+def test_chunk_walk_segments(gpu, oracle_c, monkeypatch, bs, nchunks):
+    """K10 over a chunk's segments (128 blocks each): an early insertion shifts every later
+    Copy off the block grid, so each segment boundary is crossed and the segments are walked
+    again from the true entries; then a deletion realigns, substitutions and a duplicated
+    run follow.  Equal to the oracle, and to the classifier + host walk."""
+    rng = random.Random(bs + nchunks)
+    nblk = 700
+    basis = rng.randbytes(nblk * bs + rng.randint(1, bs - 1))
+    s = bytearray(basis)
+    s[5 * bs + 7:5 * bs + 7] = b"XY"                      # shifted by 2 from here
+    del s[400 * bs + 3:400 * bs + 5]                        # realigned
+    for _ in range(30):
+        s[rng.randrange(len(s))] ^= rng.randrange(1, 256)
+    q = rng.randrange(len(s) - 3 * bs)
+    s[q:q] = s[q:q + 3 * bs]                                # a duplicated run
+    src = bytes(s)
+    npos = len(src) - bs + 1
+    nb = -(-npos // bs)
+    cuts = sorted(rng.sample(range(1, nb), nchunks - 1))
+    bounds = [0] + [c * bs for c in cuts] + [npos]
+    monkeypatch.delenv("SYDELTA_CHUNK_WALK", raising=False)
+    monkeypatch.delenv("SYDELTA_PROBE", raising=False)
+    gpu.set_profiling(True)
+    gpu.profile(reset=True)
+    d = _chunk_walk(gpu, src, basis, bs, bounds)
+    prof = gpu.profile(reset=True)
+    gpu.set_profiling(False)
+    assert "k_walk_files" in prof
+    exp = _oracle_ops(oracle_c, src, basis, bs)
+    assert d.tuples() == exp
+    monkeypatch.setenv("SYDELTA_CHUNK_WALK", "0")
+    assert _chunk_walk(gpu, src, basis, bs, bounds).tuples() == exp

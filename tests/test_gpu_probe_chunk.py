@@ -16,15 +16,21 @@ from oracle import oracle as O
 pytestmark = pytest.mark.gpu
 
 
-@pytest.fixture(params=["0", "1"], ids=["scan-only", "probe"])
+@pytest.fixture(params=["0", "1", "1c"], ids=["scan-only", "probe", "probe-classifier"])
 def probe_mode(request):
-    old = os.environ.get("SYDELTA_PROBE")
-    os.environ["SYDELTA_PROBE"] = request.param
-    yield request.param
-    if old is None:
-        os.environ.pop("SYDELTA_PROBE", None)
-    else:
-        os.environ["SYDELTA_PROBE"] = old
+    """SYDELTA_PROBE=0: every window scanned.  "1": the aligned probe; chunked matches walk
+    on the device (K10 over segments).  "1c": the probe with chunks classified and walked
+    on the host (SYDELTA_CHUNK_WALK=0)."""
+    old = {k: os.environ.get(k) for k in ("SYDELTA_PROBE", "SYDELTA_CHUNK_WALK")}
+    os.environ["SYDELTA_PROBE"] = request.param[0]
+    if request.param == "1c":
+        os.environ["SYDELTA_CHUNK_WALK"] = "0"
+    yield request.param[0]
+    for k, v in old.items():
+        if v is None:
+            os.environ.pop(k, None)
+        else:
+            os.environ[k] = v
 
 
 def _to_dev(data: bytes, pad: int = 16):
