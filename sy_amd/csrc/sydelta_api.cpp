@@ -20,6 +20,7 @@
 #include <algorithm>
 #include <array>
 #include <atomic>
+#include <immintrin.h>
 #include <chrono>
 #include <cmath>
 #include <numeric>
@@ -139,6 +140,18 @@ hipStream_t thread_stream_impl(int device) {
     // blocking: orders against work on the legacy default stream (torch's default
     // stream), so buffers a caller filled there are complete before our kernels read them
     if (hipStreamCreateWithFlags(&s, hipStreamDefault) != hipSuccess) return nullptr;
+    streams[device] = s;
+    return s;
+}
+
+// A second stream per (thread, device) for work overlapped with the first (the chunk
+// walk's launches beside its probe); ordered by events only, never destroyed.
+hipStream_t thread_aux_stream(int device) {
+    static thread_local std::map<int, hipStream_t> streams;
+    auto it = streams.find(device);
+    if (it != streams.end()) return it->second;
+    hipStream_t s = nullptr;
+    if (hipStreamCreateWithFlags(&s, hipStreamNonBlocking) != hipSuccess) return nullptr;
     streams[device] = s;
     return s;
 }
@@ -561,7 +574,20 @@ struct sydelta_index {
     bool rib_built = false;
     hipStream_t rib_stream = nullptr;
     hipEvent_t rib_ev = nullptr;
+    // An index over device arrays is built on the creating thread's aux stream (its
+    // copies of the arrays stay on the caller's stream): `ready` is recorded after the
+    // build and every use waits for it on its own stream (index_wait), so work the caller
+    // queues meanwhile -- C5's aligned probe of the source -- overlaps the build.
+    hipEvent_t ready = nullptr;
+    PinnedHits stage;  // the file tables' upload (mapped; returned at release)
 };
+
+namespace {
+// Order `s` after the index build (a no-op for an index built synchronously).
+hipError_t index_wait(const sydelta_index* x, hipStream_t s) {
+    return x->ready ? hipStreamWaitEvent(s, x->ready, 0) : hipSuccess;
+}
+}  // namespace
 
 // Index memory is kept for the next index: a released index's allocation is held (one
 // per device) and the next index built with no more bytes (and no less than half) takes
@@ -599,13 +625,94 @@ hipError_t stream_after(hipStream_t to, hipStream_t from, int device) {
 }
 }  // namespace
 
+// Host-mapped pinned buffers of finished chunk walks (the records the walk kernel writes
+// straight into host memory): kept for the next chunk, since pinning tens of MB costs
+// milliseconds.  Released by sydelta_trim.
+namespace {
+std::mutex g_mapped_mu;
+std::vector<PinnedHits> g_mapped;  // at most kMappedKeep
+constexpr size_t kMappedKeep = 4;
+int take_mapped(size_t bytes, PinnedHits& out) {
+    {
+        std::lock_guard<std::mutex> lk(g_mapped_mu);
+        size_t best = g_mapped.size();
+        for (size_t i = 0; i < g_mapped.size(); ++i)
+            if (g_mapped[i].bytes >= bytes && (best == g_mapped.size() || g_mapped[i].bytes < g_mapped[best].bytes))
+                best = i;
+        if (best < g_mapped.size()) {
+            out = g_mapped[best];
+            g_mapped.erase(g_mapped.begin() + best);
+            return SYDELTA_OK;
+        }
+    }
+    out = PinnedHits();
+    const size_t want = bytes + bytes / 4;
+    static const bool nc = getenv("SYDELTA_MAPPED_NC") != nullptr;  // A/B: non-coherent mapping
+    HIP_TRY(hipHostMalloc((void**)&out.p, want,
+                          hipHostMallocMapped | hipHostMallocPortable | (nc ? hipHostMallocNonCoherent : hipHostMallocCoherent)));
+    out.bytes = want;
+    return SYDELTA_OK;
+}
+void give_mapped(PinnedHits h) {  // h idle (its last use was synchronized)
+    if (!h.p) return;
+    PinnedHits drop;
+    {
+        std::lock_guard<std::mutex> lk(g_mapped_mu);
+        g_mapped.push_back(h);
+        if (g_mapped.size() > kMappedKeep) {
+            auto it = std::min_element(g_mapped.begin(), g_mapped.end(),
+                                       [](const PinnedHits& a, const PinnedHits& b) { return a.bytes < b.bytes; });
+            drop = *it;
+            g_mapped.erase(it);
+        }
+    }
+    if (drop.p) (void)hipHostFree(drop.p);
+}
+void release_mapped() {
+    std::vector<PinnedHits> v;
+    {
+        std::lock_guard<std::mutex> lk(g_mapped_mu);
+        v.swap(g_mapped);
+    }
+    for (auto& h : v) (void)hipHostFree(h.p);
+}
+// Events that outlive one call (a chunk's, recorded by classify and waited on by walk),
+// recycled per device: creating events costs runtime signal allocations.
+std::mutex g_ev_mu;
+std::map<int, std::vector<hipEvent_t>> g_ev_free;
+hipEvent_t take_event(int device) {
+    {
+        std::lock_guard<std::mutex> lk(g_ev_mu);
+        auto& v = g_ev_free[device];
+        if (!v.empty()) {
+            hipEvent_t e = v.back();
+            v.pop_back();
+            return e;
+        }
+    }
+    hipEvent_t e = nullptr;
+    if (hipEventCreateWithFlags(&e, hipEventDisableTiming) != hipSuccess) return nullptr;
+    return e;
+}
+void give_event(int device, hipEvent_t e) {
+    if (!e) return;
+    std::lock_guard<std::mutex> lk(g_ev_mu);
+    g_ev_free[device].push_back(e);
+}
+}  // namespace
+
 static void index_release(sydelta_index* x) {
     if (!x) return;
     if (x->rib_ev) (void)hipEventDestroy(x->rib_ev);
+    // the build has uploaded the file tables from `stage` (done long before, as a rule)
+    if (x->ready) (void)hipEventSynchronize(x->ready);
+    give_mapped(x->stage);
+    x->stage = PinnedHits();
     if (x->d_pool) {
         KeptPool old;
         const hipStream_t home = thread_stream(x->device);
-        if (x->device >= 0 && x->device < 64 && home && stream_after(home, x->stream, x->device) == hipSuccess) {
+        if (x->device >= 0 && x->device < 64 && home && stream_after(home, x->stream, x->device) == hipSuccess &&
+            index_wait(x, home) == hipSuccess) {
             std::lock_guard<std::mutex> lk(g_kept_mu);
             old = g_kept[x->device];
             g_kept[x->device] = {x->d_pool, x->pool_bytes, home};
@@ -614,6 +721,7 @@ static void index_release(sydelta_index* x) {
         }
         if (old.p) (void)hipFreeAsync(old.p, old.s);
     }
+    if (x->ready) give_event(x->device, x->ready);
     delete x;
 }
 
@@ -635,6 +743,7 @@ static void* take_kept_pool(int device, size_t bytes, hipStream_t s, size_t* got
     (void)hipFreeAsync(k.p, k.s);
     return nullptr;
 }
+
 
 // Per-thread scratch of the scan (Classifier::scan): the verified-hit buffers on each
 // device and the pinned host buffer the sorted hits come back into.
@@ -762,6 +871,7 @@ extern "C" void sydelta_trim(void) {
     }
     for (int d = 0; d < 64; ++d)
         if (kept[d].p && hipSetDevice(d) == hipSuccess) (void)hipFreeAsync(kept[d].p, kept[d].s);
+    release_mapped();
     // the scan / probe / walk scratch of this thread and of every thread not inside a call
     (void)thread_scratch();  // registers this thread's
     std::lock_guard<std::mutex> lk(scratch_mu());
@@ -901,6 +1011,28 @@ static int index_create_impl(int device, const uint32_t* weak, const uint64_t* s
     if (nblocks) {
         HIP_TRY(hipMemcpyAsync(x->d_weak, weak, 4 * nblocks, kind, s));
         HIP_TRY(hipMemcpyAsync(x->d_strong, strong, 8 * nblocks, kind, s));
+    }
+    // device arrays: built on this thread's aux stream, nothing waited for here
+    // (SYDELTA_INDEX_SYNC=1: on the caller's stream, synchronized, as for host arrays)
+    static const bool index_sync = getenv("SYDELTA_INDEX_SYNC") && getenv("SYDELTA_INDEX_SYNC")[0] == '1';
+    if (arrays_on_device && !index_sync) {
+        const size_t fb = sizeof(FileIx) * nfiles, tb = ((fb + 15) & ~(size_t)15) + 8 * (nfiles + 1);
+        if (int r = take_mapped(tb, x->stage)) return r;
+        memcpy(x->stage.p, ix.files.data(), fb);
+        memcpy(x->stage.p + ((fb + 15) & ~(size_t)15), x->fblk.data(), 8 * (nfiles + 1));
+        HIP_TRY(hipMemcpyAsync(ix.d_files, x->stage.p, fb, hipMemcpyHostToDevice, s));
+        HIP_TRY(hipMemcpyAsync(ix.d_fblk, x->stage.p + ((fb + 15) & ~(size_t)15), 8 * (nfiles + 1),
+                               hipMemcpyHostToDevice, s));
+        const hipStream_t sb = thread_aux_stream(device);
+        if (!sb) return fail(SYDELTA_E_OOM, "no stream for the index build");
+        HIP_TRY(stream_after(sb, s, device));
+        x->ready = take_event(device);
+        if (!x->ready) return fail(SYDELTA_E_OOM, "no event for the index build");
+        CallProf cp;
+        HIP_TRY(launch_index_build(x->d_weak, x->d_strong, ix, sb, cp.get()));
+        HIP_TRY(hipEventRecord(x->ready, sb));
+        *out = x.release();
+        return SYDELTA_OK;
     }
     HIP_TRY(hipMemcpyAsync(ix.d_files, ix.files.data(), sizeof(FileIx) * nfiles, hipMemcpyHostToDevice, s));
     HIP_TRY(hipMemcpyAsync(ix.d_fblk, x->fblk.data(), 8 * (nfiles + 1), hipMemcpyHostToDevice, s));
@@ -1184,10 +1316,7 @@ struct Classifier {
     // thread's kept scratch instead (a chunk's outlives other calls on its thread)
     DevScratch* probe_scratch = nullptr;
     uint32_t* d_probe_out = nullptr;
-    uint32_t* d_probe_pw = nullptr;  // ... and the probed windows' weak values
     std::vector<uint64_t> probe_pfx;
-    // the probe's results stay on the device only (the walk runs there: K10 over a chunk)
-    bool device_only = false;
 
     // Aligned probe of every block of every source (mode 1), of none (0), or, in
     // auto mode (-1), when a 1-in-16 sample finds >= 1/8 of its windows hitting.
@@ -1327,13 +1456,11 @@ int Classifier::probe(int mode) {
         uint32_t* d_pw = (uint32_t*)(jp + jbytes + obytes);
         if (stride == 1) {
             d_probe_out = d_out;
-            d_probe_pw = d_pw;
         }
         uint64_t* d_pst = (uint64_t*)(jp + jbytes + 2 * obytes);
         HIP_TRY(hipMemcpyAsync(jp, jobs.data(), jobs.size() * sizeof(ProbeJob), hipMemcpyHostToDevice, s));
         HIP_TRY(launch_probe(base, (const ProbeJob*)jp, (uint32_t)jobs.size(), np, stride, (uint32_t)n, fast,
                              ix->ix, d_pw, d_pst, d_out, s, prof));
-        if (device_only) return SYDELTA_OK;
         HIP_TRY(hipMemcpyAsync(out, d_out, np * 4, hipMemcpyDeviceToHost, s));
         HIP_TRY(hipStreamSynchronize(s));
         return SYDELTA_OK;
@@ -1348,10 +1475,6 @@ int Classifier::probe(int mode) {
     }
     if (int r = run(1, pfx)) return r;
     probe_pfx = pfx;
-    if (device_only) {
-        for (auto& c : src) c.probed = true;
-        return SYDELTA_OK;
-    }
     // Copy the results into the sources and find their miss runs (the blocks classify
     // scans) in one pass, in pieces of 64 Ki blocks on the host pool: one large source
     // (C5) is split as well as many small ones (C4).
@@ -2361,6 +2484,7 @@ static int match_impl(sydelta_index* ix, const uint8_t* d_buf, const uint64_t* s
     ScratchHold hold;  // the probe scratch is used until the walks end
     const auto t_begin = std::chrono::steady_clock::now();
     CallProf cp;
+    HIP_TRY(index_wait(ix, s));
     const uint64_t n = ix->bs;
     const uint64_t nf = ix->nfiles;
     b->d.assign(nf, sydelta_delta());
@@ -3203,13 +3327,47 @@ extern "C" int sydelta_synth_mutate(uint8_t* d_dst, const uint8_t* d_src, uint64
 // chunk g-1's left (its exit may lie up to n-1 bytes inside chunk g after a Copy),
 // and the op lists concatenate with sydelta_delta_append.  The result equals the
 // single-device op list because classification is a pure function of the position.
+namespace {
+// K10 over a chunk, launched by sydelta_chunk_classify (chunk_pipe_launch): sub-range j's
+// aligned probe on the caller's stream, then its walk on the thread's aux stream after an
+// event, the walk's per-unit results and records written straight into host-mapped
+// memory.  sydelta_chunk_walk waits for the sub-ranges in turn and assembles each one's
+// ops while the later ones still run (chunk_pipe_finish).
+struct ChunkPipe {
+    bool on = false;
+    int device = 0;
+    std::vector<WalkUnit> units;   // from the segment starts
+    std::vector<uint32_t> ub;      // sub-range j: units [ub[j], ub[j+1])
+    std::vector<hipEvent_t> done;  // per sub-range: its walk finished (results readable)
+    void* dmem = nullptr;          // the unit table and the probe's results (device)
+    hipStream_t ds = nullptr;      // dmem's stream (the caller's)
+    PinnedHits pin;                // host-mapped: per-unit results, records, upload staging
+    const WalkFileOut* fout = nullptr;
+    const WalkRec* rec = nullptr;
+    const uint32_t* ahit = nullptr;  // the probe's results (device; NULL: no probe)
+    const uint32_t* apw = nullptr;
+    void release() {  // the chunk's device is current
+        if (!done.empty()) (void)hipEventSynchronize(done.back());  // the aux stream runs in order
+        for (hipEvent_t e : done) give_event(device, e);
+        done.clear();
+        if (dmem) (void)hipFreeAsync(dmem, ds);
+        dmem = nullptr;
+        give_mapped(pin);
+        pin = PinnedHits();
+        on = false;
+    }
+    ~ChunkPipe() { release(); }
+};
+}  // namespace
+
 struct sydelta_chunk {
     Classifier C;
     bool final_src = false;
     int tail_flag = 0;
     uint64_t file_len = 0;
     BasisInfo bi{0, 0, 0};
-    bool dev_walk = false;  // K10 over the chunk's segments (chunk_walk_device)
+    bool dev_walk = false;  // K10 over the chunk's segments (ChunkPipe)
+    ChunkPipe pipe;         // destroyed before C (whose buffers its launches read)
 };
 
 // K10 over a chunk (C5, and the streamed path API's chunks): the aligned probe's results
@@ -3226,124 +3384,335 @@ bool chunk_walk_ok(const sydelta_index* idx) {
     return idx->nfiles == 1 && n % 64 == 0 && n >= 256 && n <= kWalkMaxN && probe_mode_env() != 0;
 }
 
-int chunk_walk_device(sydelta_chunk* ch, uint64_t entry, uint64_t* exit_pos, sydelta_delta* d) {
+// The units of a chunk's walk from `from`: the segments of [from, c.p1), the last one final
+// when the file ends in the chunk.
+void chunk_units(const sydelta_chunk* ch, uint64_t from, std::vector<WalkUnit>& units) {
+    const Src& c = ch->C.src[0];
+    const uint64_t n = ch->C.n, seg = kChunkSegBlocks * n;
+    units.clear();
+    uint64_t rec = 0;
+    const uint64_t lo = std::max(from, c.p0);
+    uint64_t s0 = c.p0 + (lo > c.p0 ? (lo - c.p0) / seg * seg : 0);
+    do {
+        const uint64_t e = std::min(c.p1, s0 + seg), en = std::max(lo, s0);
+        const bool last = e >= c.p1;
+        units.push_back(WalkUnit{0, ch->file_len, en, std::max(e, en), c.p1, rec, c.kb, 0,
+                                 (uint32_t)(last && ch->final_src)});
+        rec += 2 * ((std::max(e, en) - en) / n) + 4;
+        s0 = e;
+    } while (s0 < c.p1);
+}
+
+// Sub-ranges of a chunk's walk: 4 from 2048 segments, 2 from 512 (SYDELTA_CHUNK_PIPE=K)
+int chunk_pipe_parts(size_t nu) {
+    const char* e = getenv("SYDELTA_CHUNK_PIPE");
+    int K = (e && *e) ? std::max(1, atoi(e)) : nu >= 2048 ? 4 : nu >= 512 ? 2 : 1;
+    return (int)std::min<size_t>((size_t)K, nu);
+}
+
+// Launch the walk of ch from `from` (with the aligned probe first: from is c.p0), in
+// sub-ranges pipelined over two streams (ChunkPipe).
+int chunk_pipe_launch(sydelta_chunk* ch, uint64_t from, bool probe) {
     static const bool host_timing = getenv("SYDELTA_HOST_TIMING") != nullptr;
     const auto t_begin = std::chrono::steady_clock::now();
     Classifier& C = ch->C;
     const Src& c = C.src[0];
-    const uint64_t n = C.n, seg = kChunkSegBlocks * n;
-    // units: the segments of [entry, c.p1), the last one final when the file ends in the chunk
-    auto make_units = [&](uint64_t from, std::vector<WalkUnit>& units) {
-        units.clear();
-        uint64_t rec = 0;
-        const uint64_t lo = std::max(from, c.p0);
-        uint64_t s0 = c.p0 + (lo > c.p0 ? (lo - c.p0) / seg * seg : 0);
-        do {
-            const uint64_t e = std::min(c.p1, s0 + seg), en = std::max(lo, s0);
-            const bool last = e >= c.p1;
-            units.push_back(WalkUnit{0, ch->file_len, en, std::max(e, en), c.p1, rec, c.kb, 0,
-                                     (uint32_t)(last && ch->final_src)});
-            rec += 2 * ((std::max(e, en) - en) / n) + 4;
-            s0 = e;
-        } while (s0 < c.p1);
+    ChunkPipe& P = ch->pipe;
+    const uint64_t n = C.n;
+    chunk_units(ch, from, P.units);
+    const size_t nu = P.units.size();
+    uint64_t rec_total = 0;
+    for (const WalkUnit& u : P.units) rec_total = std::max(rec_total, u.rec_off + 2 * ((u.end - u.entry) / n) + 4);
+    if (rec_total >= (1ull << 32)) return fail(SYDELTA_E_INVAL, "chunk too large for one walk");
+    const uint64_t np = probe ? c.nblk : 0;
+    const int K = probe ? chunk_pipe_parts(nu) : 1;
+    P.ub.resize(K + 1);
+    for (int j = 0; j <= K; ++j) P.ub[j] = (uint32_t)(nu * j / K);
+    auto al = [](size_t v) { return (v + 255) & ~(size_t)255; };
+    const size_t o_last = al(sizeof(WalkUnit) * nu), o_total = o_last + 256, o_jobs = o_total + 256;
+    const size_t o_out = o_jobs + al(sizeof(ProbeJob) * K), o_pw = o_out + al(4 * np), o_pst = o_pw + al(4 * np);
+    const size_t o_stage = o_pst + al(8 * np), dneed = o_stage + al(sizeof(WalkRec) * rec_total);
+    const size_t h_rec = al(sizeof(WalkFileOut) * nu), h_units = h_rec + al(sizeof(WalkRec) * rec_total);
+    const size_t h_jobs = h_units + al(sizeof(WalkUnit) * nu), h_last = h_jobs + al(sizeof(ProbeJob) * K);
+    P.on = true;  // release() undoes whatever is set below
+    P.device = C.ix->device;
+    P.ds = C.s;
+    if (int r = take_mapped(h_last + 256, P.pin)) return r;
+    HIP_TRY(dev_malloc_async(&P.dmem, dneed, C.s));
+    uint8_t* H = P.pin.p;
+    uint8_t* D = (uint8_t*)P.dmem;
+    P.fout = (const WalkFileOut*)H;
+    P.rec = (const WalkRec*)(H + h_rec);
+    uint32_t* d_out = (uint32_t*)(D + o_out);
+    uint32_t* d_pw = (uint32_t*)(D + o_pw);
+    uint64_t* d_pst = (uint64_t*)(D + o_pst);
+    P.ahit = probe ? d_out : nullptr;
+    P.apw = probe ? d_pw : nullptr;
+    // the unit table, probe jobs and last size up, from the mapped buffer (it outlives the
+    // copies); the per-unit results cleared (their done marks)
+    memset(H, 0, sizeof(WalkFileOut) * nu);
+    memcpy(H + h_units, P.units.data(), sizeof(WalkUnit) * nu);
+    ProbeJob* jobs = (ProbeJob*)(H + h_jobs);
+    for (int j = 0; j < K; ++j) jobs[j] = ProbeJob{c.off, c.kb + (uint64_t)P.ub[j] * kChunkSegBlocks, 0, 0, 0};
+    *(uint64_t*)(H + h_last) = C.ix->last_size[0];
+    HIP_TRY(hipMemcpyAsync(D, H + h_units, sizeof(WalkUnit) * nu, hipMemcpyHostToDevice, C.s));
+    HIP_TRY(hipMemcpyAsync(D + o_last, H + h_last, 8, hipMemcpyHostToDevice, C.s));
+    if (probe) HIP_TRY(hipMemcpyAsync(D + o_jobs, jobs, sizeof(ProbeJob) * K, hipMemcpyHostToDevice, C.s));
+    HIP_TRY(hipMemsetAsync(D + o_total, 0, 8, C.s));
+    hipStream_t s2 = thread_aux_stream(P.device);
+    hipEvent_t hand = handoff_event(P.device);
+    if (!s2 || !hand) return fail(SYDELTA_E_OOM, "no stream or event for the chunk walk");
+    const bool fast = ((uintptr_t)(C.base + c.off) & 15) == 0;
+    WalkArgs a{};
+    a.base = C.base;
+    a.last_size = (const uint64_t*)(D + o_last);
+    a.n = (uint32_t)n;
+    a.nm = (uint32_t)(n % 65521);
+    a.fw_max = 0;  // the filter from L2 (one file's is too large for LDS)
+    const DeviceIndex& ix = C.ix->ix;
+    a.files = ix.d_files;
+    a.fblk = ix.d_fblk;
+    a.filt = ix.filt;
+    a.keys = ix.keys;
+    a.start = ix.start;
+    a.cnt = ix.cnt;
+    a.order = ix.order;
+    a.cstrong = ix.cstrong;
+    a.weak = C.ix->d_weak;
+    a.strong = C.ix->d_strong;
+    a.ahit = P.ahit;
+    a.apw = P.apw;
+    // records staged on the device, compacted into host memory (read in order by the
+    // assembly: staged there, one unit's per 4 KiB page, they cost a TLB miss each)
+    a.stage = (WalkRec*)(D + o_stage);
+    a.out = (WalkRec*)(H + h_rec);
+    a.total = (unsigned long long*)(D + o_total);  // one counter: the sub-ranges' launches run in order
+    a.ticks = nullptr;
+    a.mark_done = 1;
+    auto probe_part = [&](int j, int phases) -> hipError_t {
+        const uint64_t b0 = (uint64_t)P.ub[j] * kChunkSegBlocks;
+        const uint64_t b1 = std::min<uint64_t>((uint64_t)P.ub[j + 1] * kChunkSegBlocks, np);
+        return launch_probe(C.base, (const ProbeJob*)(D + o_jobs) + j, 1, b1 - b0, 1, (uint32_t)n, fast, ix,
+                            d_pw + b0, d_pst + b0, d_out + b0, C.s, C.prof, phases);
     };
-    std::vector<WalkUnit> units;
-    make_units(entry, units);
-    const uint32_t* ahit = c.probed ? C.d_probe_out : nullptr;
-    const uint32_t* apw = c.probed ? C.d_probe_pw : nullptr;
-    WalkResult res;
-    if (int r = run_walk(C.ix, C.base, units, ahit, apw, false, C.s, C.prof, res)) return r;
-    std::vector<WalkFileOut> out = res.out;
-    std::vector<WalkRec> rec(res.rec, res.rec + res.nrec);  // the pinned buffer is reused by re-walks
-    // chain the segments: each must start where the previous one left.  Every segment whose
-    // entry differs from the previous one's exit is walked again from that exit, all of them
-    // in one launch; a re-walk usually leaves where the first walk did (a shifted source
-    // keeps its phase), so this converges in a round or two.
-    std::vector<std::pair<uint64_t, uint64_t>> span(units.size());  // records [first, end) in rec
-    for (size_t u = 0; u < units.size(); ++u) span[u] = {out[u].base, (uint64_t)out[u].base + out[u].count};
-    int rounds = 0;
-    for (;;) {
-        std::vector<size_t> bad;
-        std::vector<WalkUnit> again;
-        uint64_t roff = 0;
-        for (size_t u = 1; u < units.size(); ++u) {
-            const uint64_t ex = out[u - 1].exit;  // inside unit u: a Copy reaches < n bytes past a boundary
-            if (ex == units[u].entry) continue;
-            units[u].entry = ex;
-            units[u].end = std::max(units[u].end, ex);
-            WalkUnit w = units[u];
-            w.rec_off = roff;
-            roff += 2 * ((w.end - w.entry) / n) + 4;
-            again.push_back(w);
-            bad.push_back(u);
-        }
-        if (bad.empty()) break;
-        ++rounds;
-        WalkResult r1;
-        if (int r = run_walk(C.ix, C.base, again, ahit, apw, false, C.s, C.prof, r1)) return r;
-        for (size_t j = 0; j < bad.size(); ++j) {
-            const size_t u = bad[j];
-            span[u] = {rec.size(), rec.size() + r1.out[j].count};
-            rec.insert(rec.end(), r1.rec + r1.out[j].base, r1.rec + r1.out[j].base + r1.out[j].count);
-            out[u] = r1.out[j];
-        }
+    // the windows hashed first (an index built from device arrays may still be building on
+    // the aux stream: this overlaps it), then per sub-range the lookups and the walk
+    if (probe)
+        for (int j = 0; j < K; ++j) HIP_TRY(probe_part(j, 1));
+    HIP_TRY(index_wait(C.ix, C.s));
+    for (int j = 0; j < K; ++j) {
+        if (probe) HIP_TRY(probe_part(j, 2));
+        HIP_TRY(hipEventRecord(hand, C.s));
+        HIP_TRY(hipStreamWaitEvent(s2, hand, 0));
+        hipEvent_t e = take_event(P.device);
+        if (!e) return fail(SYDELTA_E_OOM, "no event for the chunk walk");
+        P.done.push_back(e);
+        a.units = (const WalkUnit*)D + P.ub[j];
+        a.nunits = P.ub[j + 1] - P.ub[j];
+        a.fout = (WalkFileOut*)P.fout + P.ub[j];
+        HIP_TRY(launch_walk_files(a, s2, C.prof));
+        HIP_TRY(hipEventRecord(e, s2));
     }
-    // the ops: each segment's, a Data op that ends at a segment's end joined with the next
-    // segment's first Data op (literal runs stay maximal, generator.rs:186-197)
+    if (host_timing) fprintf(stderr, "sydelta chunk launch: %zu segments, %d parts: %.3f ms\n", nu, K, ms_since(t_begin));
+    return SYDELTA_OK;
+}
+
+// The chunk's ops from `entry`: the segments in order, each sub-range as soon as its walk
+// finished.  A segment whose entry differs from the previous one's exit (a Copy crossed
+// the boundary) stops the overlap: it and every later one whose entry changed are walked
+// again (in one launch per round; a shifted source keeps its phase, so a round or two),
+// then assembled.  A Data op ending at a segment's end is joined with the next segment's
+// first Data op (literal runs stay maximal, generator.rs:186-197).
+int chunk_pipe_finish(sydelta_chunk* ch, uint64_t entry, uint64_t* exit_pos, sydelta_delta* d) {
+    static const bool host_timing = getenv("SYDELTA_HOST_TIMING") != nullptr;
+    const auto t_begin = std::chrono::steady_clock::now();
+    Classifier& C = ch->C;
+    ChunkPipe& P = ch->pipe;
+    const uint64_t n = C.n;
+    std::vector<WalkUnit> units = P.units;  // re-walks move entries (the launch's stay for a later call)
     const size_t nu = units.size();
-    std::vector<uint64_t> first(nu + 1, 0);
-    std::vector<uint8_t> join(nu, 0);  // unit u's first op extends unit u-1's last Data op
-    for (size_t u = 0; u < nu; ++u) {
-        const WalkRec* r0 = rec.data() + span[u].first;
-        const WalkRec* r1 = rec.data() + span[u].second;
-        uint64_t k = records_ops(r0, r1);
-        if (u && r0 < r1 && !r0->kind) {
-            const WalkRec* pl = rec.data() + span[u - 1].second - 1;
-            if (span[u - 1].second > span[u - 1].first && !pl->kind && pl->off + pl->a == r0->off) {
-                join[u] = 1;
-                --k;
+    size_t u0 = 0;  // the segment holding entry
+    while (u0 + 1 < nu && units[u0].end <= entry) ++u0;
+    uint64_t cap = 0;  // ops per unit: at most a Copy per block, a Data op before each, a tail Copy
+    for (size_t u = u0; u < nu; ++u) cap += 2 * ((units[u].end - units[u].entry) / n) + 8;
+    OpVec& ops = d->ops;
+    if (ops.capacity() < cap) ops = take_ops(cap);
+    ops.resize(cap);
+    const double ms_ops = ms_since(t_begin);
+    double ms_asm = 0;
+    std::vector<WalkFileOut> out(nu);
+    std::vector<std::pair<const WalkRec*, const WalkRec*>> span(nu);
+    std::vector<std::vector<WalkRec>> again_rec;  // re-walked units' records
+    const uint64_t nbf = C.ix->fblk[1], ls = C.ix->last_size[0];
+    uint64_t nops = 0, data_ops = 0, lit = 0, hits = 0, weak = 0;
+    const int pool = walk_threads();
+    double ms_wait = 0;
+    // units [a, b) after ops [0, nops)
+    auto assemble = [&](size_t a, size_t b) -> int {
+        if (b <= a) return SYDELTA_OK;
+        const auto ta = std::chrono::steady_clock::now();
+        std::vector<uint64_t> first(b - a + 1, nops);
+        std::vector<uint8_t> join(b - a, 0);
+        for (size_t u = a; u < b; ++u) {
+            const WalkRec *r0 = span[u].first, *r1 = span[u].second;
+            uint64_t k = records_ops(r0, r1);
+            if (u > u0 && r0 < r1 && !r0->kind && span[u - 1].second > span[u - 1].first) {
+                const WalkRec* pl = span[u - 1].second - 1;
+                if (!pl->kind && pl->off + pl->a == r0->off) {
+                    join[u - a] = 1;
+                    --k;
+                }
+            }
+            first[u - a + 1] = first[u - a] + k;
+            hits += out[u].hits;
+            weak += out[u].weak_hits;
+        }
+        if (first.back() > ops.size())
+            return fail(SYDELTA_E_KERNEL, "chunk walk: %llu ops above the bound %llu", (unsigned long long)first.back(),
+                        (unsigned long long)ops.size());
+        const size_t m = b - a;
+        const int nt = first.back() - nops >= (1u << 15) ? (int)std::min<size_t>(m, (size_t)pool) : 1;
+        std::vector<uint64_t> nd(nt, 0), lb(nt, 0);
+        if (!run_parallel(nt, [&](int t) {
+                for (size_t u = a + m * t / nt; u < a + m * (t + 1) / nt; ++u) {
+                    const WalkRec* r0 = span[u].first + join[u - a];
+                    expand_records(r0, span[u].second, n, 0, nbf, ls, ops.data() + first[u - a], &nd[t], &lb[t]);
+                }
+            }))
+            return fail(SYDELTA_E_OOM, "out of host memory (op lists)");
+        for (int t = 0; t < nt; ++t) {
+            data_ops += nd[t];
+            lit += lb[t];
+        }
+        for (size_t u = a; u < b; ++u)
+            if (join[u - a]) {
+                const uint64_t add = span[u].first->a;
+                ops[first[u - a] - 1].b += add;  // the previous unit's last op
+                lit += add;
+            }
+        nops = first.back();
+        ms_asm += ms_since(ta);
+        return SYDELTA_OK;
+    };
+    // the results of units [a, b) out of the mapped buffer: copied in two block moves
+    // (SYDELTA_CHUNK_COPYREC=0: read in place)
+    static const bool copy_rec = !getenv("SYDELTA_CHUNK_COPYREC") || getenv("SYDELTA_CHUNK_COPYREC")[0] != '0';
+    double ms_take = 0;
+    auto take = [&](size_t a, size_t b) {
+        if (b <= a) return;
+        const auto tt = std::chrono::steady_clock::now();
+        memcpy(out.data() + a, P.fout + a, sizeof(WalkFileOut) * (b - a));
+        const WalkRec* base = P.rec;
+        uint64_t lo = 0;
+        if (copy_rec) {
+            uint64_t hi = 0;
+            lo = UINT64_MAX;
+            for (size_t u = a; u < b; ++u)
+                if (out[u].count) {
+                    lo = std::min<uint64_t>(lo, out[u].base);
+                    hi = std::max<uint64_t>(hi, (uint64_t)out[u].base + out[u].count);
+                }
+            if (hi > lo) {
+                again_rec.emplace_back(P.rec + lo, P.rec + hi);
+                base = again_rec.back().data();
+            } else {
+                lo = 0;
             }
         }
-        first[u + 1] = first[u] + k;
-    }
-    OpVec& ops = d->ops;
-    if (ops.capacity() < first[nu]) ops = take_ops(first[nu]);
-    ops.resize(first[nu]);
-    std::vector<uint64_t> nd(nu, 0), lb(nu, 0);
-    const uint64_t nbf = C.ix->fblk[1], ls = C.ix->last_size[0];
-    auto fill = [&](size_t u) {
-        const WalkRec* r0 = rec.data() + span[u].first;
-        const WalkRec* r1 = rec.data() + span[u].second;
-        sydelta_op* w = ops.data() + first[u];
-        if (join[u]) {  // this segment's leading literal run belongs to the previous op
-            lb[u] += r0->a;
-            ++r0;
+        for (size_t u = a; u < b; ++u) {  // (a unit with no records: an empty span anywhere)
+            const WalkRec* r = out[u].count ? base + (out[u].base - lo) : base;
+            span[u] = {r, r + out[u].count};
         }
-        expand_records(r0, r1, n, 0, nbf, ls, w, &nd[u], &lb[u]);
+        ms_take += ms_since(tt);
     };
-    const int nthr = nu >= 64 ? walk_threads() : 1;
-    if (!run_parallel(nthr, [&](int t) {
-            for (size_t u = nu * t / nthr; u < nu * (t + 1) / nthr; ++u) fill(u);
-        }))
-        return fail(SYDELTA_E_OOM, "out of host memory (op lists)");
-    uint64_t data_ops = 0, lit = 0, hits = 0, weak = 0;
-    for (size_t u = 0; u < nu; ++u) {
-        if (join[u]) ops[first[u] - 1].b += rec[span[u].first].a;
-        data_ops += nd[u];
-        lit += lb[u];
-        hits += out[u].hits;
-        weak += out[u].weak_hits;
+    // Units are assembled as they finish: the kernel marks each unit's results done (after a
+    // system-scope fence), waves finish roughly in unit order, so the first ones' ops are
+    // written while the last ones still walk.  Batches of at least kBatch units, or whatever
+    // is done once the sub-range's event has completed.
+    constexpr size_t kBatch = 1024;
+    const volatile uint64_t* mark = (const volatile uint64_t*)&P.fout[0].pad;
+    auto done_to = [&](size_t u, size_t b) {  // first unit in [u, b) not marked done
+        while (u < b && mark[u * (sizeof(WalkFileOut) / 8)]) ++u;
+        return u;
+    };
+    size_t stop = nu;  // the first unit whose entry is not the previous one's exit
+    for (size_t j = 0; j + 1 < P.ub.size() && stop == nu; ++j) {
+        size_t a = std::max<size_t>(P.ub[j], u0);
+        const size_t b = P.ub[j + 1];
+        auto tw = std::chrono::steady_clock::now();
+        bool all = false;
+        while (a < b && stop == nu) {
+            size_t e = done_to(a, b);
+            if (e < b && e - a < kBatch) {
+                if (!all) {
+                    const hipError_t q = hipEventQuery(P.done[j]);
+                    if (q == hipSuccess) {
+                        all = true;  // every unit of the sub-range is marked
+                        continue;
+                    }
+                    if (q != hipErrorNotReady) HIP_TRY(q);
+                    _mm_pause();
+                    continue;
+                }
+                return fail(SYDELTA_E_KERNEL, "chunk walk: unit %zu not marked done", e);
+            }
+            std::atomic_thread_fence(std::memory_order_acquire);
+            ms_wait += ms_since(tw);
+            take(a, e);
+            size_t c = a;
+            while (c < e && units[c].entry == (c == u0 ? entry : out[c - 1].exit)) ++c;
+            if (int r = assemble(a, c)) return r;
+            if (c < e) stop = c;
+            a = e;
+            tw = std::chrono::steady_clock::now();
+        }
     }
+    int rounds = 0;
+    if (stop < nu) {
+        HIP_TRY(hipEventSynchronize(P.done.back()));
+        size_t t0 = stop + 1;  // the first unit not taken yet: past the batch that held `stop`
+        while (t0 < nu && span[t0].first) ++t0;
+        take(t0, nu);
+        for (;;) {
+            std::vector<size_t> bad;
+            std::vector<WalkUnit> again;
+            uint64_t roff = 0;
+            for (size_t u = stop; u < nu; ++u) {
+                const uint64_t ex = u == u0 ? entry : out[u - 1].exit;  // a Copy reaches < n bytes past a boundary
+                if (ex == units[u].entry) continue;
+                units[u].entry = ex;
+                units[u].end = std::max(units[u].end, ex);
+                WalkUnit w = units[u];
+                w.rec_off = roff;
+                roff += 2 * ((w.end - w.entry) / n) + 4;
+                again.push_back(w);
+                bad.push_back(u);
+            }
+            if (bad.empty()) break;
+            ++rounds;
+            WalkResult r1;
+            if (int r = run_walk(C.ix, C.base, again, P.ahit, P.apw, false, C.s, C.prof, r1)) return r;
+            for (size_t j = 0; j < bad.size(); ++j) {
+                const size_t u = bad[j];
+                const WalkRec* q = r1.rec + r1.out[j].base;
+                again_rec.emplace_back(q, q + r1.out[j].count);
+                span[u] = {again_rec.back().data(), again_rec.back().data() + again_rec.back().size()};
+                out[u] = r1.out[j];
+            }
+        }
+        if (int r = assemble(stop, nu)) return r;
+    }
+    ops.resize(nops);
     d->stats.data_ops = data_ops;
-    d->stats.copy_ops = ops.size() - data_ops;
+    d->stats.copy_ops = nops - data_ops;
     d->stats.literal_bytes = lit;
     d->stats.verified_hits = hits;
     d->stats.weak_hits = weak;
     *exit_pos = out[nu - 1].exit;
     if (host_timing)
-        fprintf(stderr, "sydelta chunk walk: %zu segments, %llu records, %d re-walk rounds: kernel+counts %.3f ms, "
-                "records D2H %.3f ms, %zu ops, all %.3f ms\n", nu, (unsigned long long)res.nrec, rounds, res.ms_kernel,
-                res.ms_d2h, ops.size(), ms_since(t_begin));
+        fprintf(stderr, "sydelta chunk walk: %zu segments in %zu parts, %d re-walk rounds, %llu ops: op array %.3f ms, "
+                "waits %.3f ms, results %.3f ms, assembly %.3f ms, all %.3f ms\n", nu, P.done.size(), rounds,
+                (unsigned long long)nops, ms_ops, ms_wait, ms_take, ms_asm, ms_since(t_begin));
     return SYDELTA_OK;
 }
 }  // namespace
@@ -3394,15 +3763,15 @@ extern "C" int sydelta_chunk_classify(sydelta_index* idx, const uint8_t* d_buf, 
     ch->final_src = final_src;
     ch->file_len = file_len;
     ch->bi = BasisInfo{0, idx->fblk[1], idx->last_size[0]};
-    if (chunk_walk_ok(idx)) {  // K10 walks the chunk on the device: only the aligned probe here
+    if (chunk_walk_ok(idx)) {  // K10 walks the chunk on the device: probe and walk launched here
         ch->dev_walk = true;
-        C.device_only = true;
-        if (c.p1 > c.p0)
-            if (int r = C.probe(1)) return r;
+        if (c.p1 > c.p0)  // (the index is waited for between the probe's hashing and its lookups)
+            if (int r = chunk_pipe_launch(ch.get(), c.p0, true)) return r;
         C.prof = nullptr;
         *out = ch.release();
         return SYDELTA_OK;
     }
+    HIP_TRY(index_wait(idx, s));
     // windows above the LDS scans' limit without k_scan_g: every position scanned (k_scan,
     // one launch per range), no probe, as match_impl does
     if (int r = C.classify(n > scan_max_window() && !wide_scan(idx) ? 0 : probe_mode_env())) return r;
@@ -3432,7 +3801,9 @@ extern "C" int sydelta_chunk_walk(sydelta_chunk* ch, uint64_t entry, uint64_t* e
     d->block_size = C.n;
     d->stats.positions = c.p1 - c.p0;
     if (ch->dev_walk) {
-        const int r = chunk_walk_device(ch, entry, exit_pos, d.get());
+        int r = SYDELTA_OK;
+        if (!ch->pipe.on) r = chunk_pipe_launch(ch, entry, false);  // nothing to probe: launched now
+        if (!r) r = chunk_pipe_finish(ch, entry, exit_pos, d.get());
         C.prof = nullptr;
         if (r) return r;
         *out = d.release();

@@ -442,16 +442,23 @@ __global__ __launch_bounds__(64, 4) void k_walk_files(WalkArgs a) {
         exit = max(x, end);
     }
     close_run();
-    // move the records to the compact output (one atomic per file)
-    __threadfence_block();
-    unsigned long long base = 0;
-    if (lane == 0 && nrec) base = atomicAdd(a.total, (unsigned long long)nrec);
-    base = (uint32_t)rl((uint32_t)base, 0);
-    for (uint32_t i = lane; i < nrec; i += 64) {
-        const volatile WalkRec* r = stg + i;
-        a.out[base + i] = WalkRec{r->kind, r->a, r->off};
+    unsigned long long base = U.rec_off;  // no compact output: the records stay where they were staged
+    if (a.out) {
+        // move the records to the compact output (one atomic per file)
+        __threadfence_block();
+        base = 0;
+        if (lane == 0 && nrec) base = atomicAdd(a.total, (unsigned long long)nrec);
+        base = (uint32_t)rl((uint32_t)base, 0);
+        for (uint32_t i = lane; i < nrec; i += 64) {
+            const volatile WalkRec* r = stg + i;
+            a.out[base + i] = WalkRec{r->kind, r->a, r->off};
+        }
     }
     if (lane == 0) a.fout[blockIdx.x] = WalkFileOut{(uint32_t)base, nrec, weak_hits, hits, exit, 0};
+    if (a.mark_done) {  // the host reads units as they finish (chunk_pipe_finish)
+        __threadfence_system();
+        if (lane == 0) *(volatile uint64_t*)&a.fout[blockIdx.x].pad = 1;
+    }
     wtick(kWtOut);
 }
 

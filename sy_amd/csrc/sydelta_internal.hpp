@@ -190,9 +190,11 @@ struct ProbeJob {
 };
 // fast: n % 64 == 0, n >= 256 and every window 16-byte aligned.
 // Scratch: d_pw[nprobes], d_pst[nprobes] (the windows' weak / strong).
+// phases: 1 hash the windows (d_pw, d_pst), 2 look them up (d_out; the index must be
+// built), 3 both -- split so the hashing can run before the index is ready.
 hipError_t launch_probe(const uint8_t* d_base, const ProbeJob* d_jobs, uint32_t njobs, uint64_t nprobes,
                         uint32_t stride, uint32_t n, bool fast, const DeviceIndex& ix, uint32_t* d_pw,
-                        uint64_t* d_pst, uint32_t* d_out, hipStream_t s, Profiler* prof);
+                        uint64_t* d_pst, uint32_t* d_out, hipStream_t s, Profiler* prof, int phases = 3);
 // Tail rule (generator.rs:156-184) of every listed file: flag[i] = 1 iff the
 // suffix of source i hashes to (weak[blk], strong[blk]) of its last basis block.
 struct TailJob {
@@ -237,7 +239,7 @@ struct WalkFileOut {
     uint32_t weak_hits;    // candidate windows verified (passed the Bloom filter)
     uint32_t hits;         // windows classified as hits
     uint64_t exit;         // where the walk left the unit (>= end; a final unit: len)
-    uint64_t pad;
+    uint64_t pad;          // WalkArgs::mark_done: 1 once the unit's results are complete
 };
 struct WalkArgs {
     const uint8_t* base;         // launch base
@@ -245,6 +247,8 @@ struct WalkArgs {
     const uint64_t* last_size;   // per basis file (0: empty signature)
     uint32_t nunits, n, nm;
     uint32_t fw_max;             // LDS filter words (0: the filter is read from global memory)
+    uint32_t mark_done;          // 1: fout in host memory; each unit's `pad` set to 1 after its
+                                 // results are visible to the host (a system-scope fence first)
     const FileIx* files;
     const uint64_t* fblk;
     const uint32_t* filt;
@@ -257,8 +261,8 @@ struct WalkArgs {
     const uint64_t* strong;
     const uint32_t* ahit;        // optional: the aligned probe's results (block k: its hit or none) ...
     const uint32_t* apw;         // ... and its windows' weak values
-    WalkRec* stage;
-    WalkRec* out;                // compacted records of every unit
+    WalkRec* stage;              // may be host-mapped memory (with out NULL)
+    WalkRec* out;                // compacted records of every unit; NULL: left in stage (base = rec_off)
     WalkFileOut* fout;
     unsigned long long* total;   // records placed in out (zeroed before the launch)
     unsigned long long* ticks;   // SYDELTA_PHASE_TIMING: 16 counters (zeroed), else null

@@ -4502,10 +4502,10 @@ hipError_t launch_index_build(const uint32_t* d_weak, const uint64_t* d_strong, 
 
 hipError_t launch_probe(const uint8_t* d_base, const ProbeJob* d_jobs, uint32_t njobs, uint64_t nprobes,
                         uint32_t stride, uint32_t n, bool fast, const DeviceIndex& ix, uint32_t* d_pw,
-                        uint64_t* d_pst, uint32_t* d_out, hipStream_t s, Profiler* prof) {
+                        uint64_t* d_pst, uint32_t* d_out, hipStream_t s, Profiler* prof, int phases) {
     if (!nprobes) return hipSuccess;
     if (fast && (n % 64 != 0 || n < 256)) return hipErrorInvalidValue;
-    {
+    if (phases & 1) {
         ProfScope ps(prof, s, stride > 1 ? "k_probe_sample" : "k_probe");
         if (fast)
             hipLaunchKernelGGL(k_probe_rows<true>, dim3(grid_for((nprobes + 3) / 4 * 64, 256)), dim3(256), 0, s,
@@ -4518,6 +4518,7 @@ hipError_t launch_probe(const uint8_t* d_base, const ProbeJob* d_jobs, uint32_t 
                                nprobes, stride, n, d_pw, d_pst);
     }
     if (hipError_t e = hipGetLastError()) return e;
+    if (!(phases & 2)) return hipSuccess;
     ProfScope ps(prof, s, "k_probe_lookup");
     hipLaunchKernelGGL(k_probe_lookup, dim3(grid_for(nprobes, 256)), dim3(256), 0, s, d_jobs, njobs, nprobes,
                        ix.d_files, ix.filt, ix.keys, ix.start, ix.cnt, ix.order, ix.cstrong, d_pw, d_pst, d_out);

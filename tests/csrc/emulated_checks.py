@@ -738,8 +738,9 @@ def batch_and_chunk_checks():
         npos = L - bs + 1
         nbp = -(-npos // bs)
         for nch in (1, 2, 3, 8):
-            for probe in ("0", "1"):
-                os.environ["SYDELTA_PROBE"] = probe
+            for probe in ("0", "1", "1p"):  # 1p: the device walk's launches in one sub-range per segment
+                os.environ["SYDELTA_PROBE"] = probe[0]
+                os.environ["SYDELTA_CHUNK_PIPE"] = "3" if probe == "1p" else ""
                 cuts = sorted(set(int(c) for c in rng.choice(np.arange(1, nbp), nch - 1, replace=False))) if nch > 1 \
                     else []
                 bounds = [0] + [c * bs for c in cuts] + [npos]
@@ -765,6 +766,7 @@ def batch_and_chunk_checks():
                 n_checks += 1
         lib.sydelta_index_free(ix)
     os.environ.pop("SYDELTA_PROBE", None)
+    os.environ.pop("SYDELTA_CHUNK_PIPE", None)
     return n_checks
 
 

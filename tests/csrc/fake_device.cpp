@@ -402,18 +402,21 @@ hipError_t launch_sort_hits(uint64_t* key, uint32_t* val, uint64_t*, uint32_t*, 
 
 hipError_t launch_probe(const uint8_t* d_base, const ProbeJob* d_jobs, uint32_t njobs, uint64_t nprobes,
                         uint32_t stride, uint32_t n, bool, const DeviceIndex& ix, uint32_t* d_pw, uint64_t* d_pst,
-                        uint32_t* d_out, hipStream_t, Profiler*) {
+                        uint32_t* d_out, hipStream_t, Profiler*, int phases) {
     EmuTimer emu_t;
-    const FakeIndex& F = find_ix(ix);
     for (uint32_t j = 0; j < njobs; ++j) {
         const uint64_t end = j + 1 < njobs ? d_jobs[j + 1].pfx : nprobes;
         for (uint64_t w = d_jobs[j].pfx; w < end; ++w) {
             const uint64_t k = d_jobs[j].k0 + (w - d_jobs[j].pfx) * stride;
             const uint8_t* win = d_base + d_jobs[j].src + k * n;
-            const uint32_t wk = adler(win, n);
-            d_pw[w] = wk;
-            d_pst[w] = oracle_xxh3_64(win, n);
-            d_out[w] = lookup(F, d_jobs[j].file, wk, win, n, nullptr);
+            if (phases & 1) {
+                d_pw[w] = adler(win, n);
+                d_pst[w] = oracle_xxh3_64(win, n);
+            }
+            if (phases & 2) {
+                if (d_pw[w] != adler(win, n)) return hipErrorInvalidValue;  // looked up before it was hashed
+                d_out[w] = lookup(find_ix(ix), d_jobs[j].file, d_pw[w], win, n, nullptr);
+            }
         }
     }
     return hipSuccess;
@@ -661,11 +664,16 @@ hipError_t launch_walk_files(const WalkArgs& a, hipStream_t, Profiler*) {
         close_run();
         const uint64_t cap = 2 * ((U.end - U.entry) / n) + 4;
         if (rec.size() > cap) return hipErrorInvalidValue;  // the kernel's staging region would overflow
+        if (!a.out) {  // records left in the staging region
+            std::copy(rec.begin(), rec.end(), a.stage + U.rec_off);
+            a.fout[u] = WalkFileOut{(uint32_t)U.rec_off, (uint32_t)rec.size(), weak_hits, hits, exit, a.mark_done};
+            continue;
+        }
         std::copy(rec.begin(), rec.end(), a.out + placed);
-        a.fout[u] = WalkFileOut{(uint32_t)placed, (uint32_t)rec.size(), weak_hits, hits, exit, 0};
+        a.fout[u] = WalkFileOut{(uint32_t)placed, (uint32_t)rec.size(), weak_hits, hits, exit, a.mark_done};
         placed += rec.size();
     }
-    *a.total = placed;
+    if (a.out) *a.total = placed;
     return hipSuccess;
 }
 
