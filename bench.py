@@ -860,7 +860,12 @@ def main():
         basis, new, files = files
         n = int(files[1].sum())  # basis bytes of this rank
     torch.cuda.synchronize()
-    stream = torch.cuda.current_stream()
+    # The step's calls get a stream of their own.  torch's default stream is the legacy
+    # NULL stream (handle 0), which the C ABI reads as "no stream": each call would run on
+    # the library's thread stream and synchronize before returning, so the host could not
+    # queue the next call (the index build, the probe) while the signature kernel runs.
+    stream = torch.cuda.Stream()
+    torch.cuda.set_stream(stream)
 
     def c4_batch(fs, strm):
         """One batched call over files fs = (boff, blen, soff, slen); strm None = the

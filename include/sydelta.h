@@ -284,7 +284,11 @@ int sydelta_chunk_classify(sydelta_index *idx, const uint8_t *d_buf, uint64_t bu
                            sydelta_chunk **out);
 /* Greedy walk from entry (>= pos_begin).  *out: the ops for [entry, *exit_pos); a
  * non-final chunk ends with its literal run up to its last position (continued by
- * the next chunk's leading Data op), a final chunk ends at file_len. */
+ * the next chunk's leading Data op), a final chunk ends at file_len.
+ * With the device walk (bs % 64 == 0, 256..8192; SYDELTA_CHUNK_WALK) classify launches
+ * the probe and the walk from the chunk's segment starts and returns; walk waits for
+ * them and walks again only the segments whose true entry differs.  sydelta_chunk_free
+ * waits for work still running on a chunk that was never walked. */
 int sydelta_chunk_walk(sydelta_chunk *c, uint64_t entry, uint64_t *exit_pos, sydelta_delta **out);
 void sydelta_chunk_free(sydelta_chunk *c);
 /* A delta holding a copy of n ops (e.g. one received from the sender, to apply on the

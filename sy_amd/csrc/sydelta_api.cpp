@@ -2391,16 +2391,33 @@ static int run_walk(sydelta_index* ix, const uint8_t* base, const std::vector<Wa
 
 // The ops of records [r0, r1) into w (Copy sizes from the basis file's blocks); returns the
 // data ops and literal bytes written.
+// kStream: non-temporal stores, for a large op array written once and read later (a chunk's:
+// C5's 24 MiB per call); they skip each destination line's read-for-ownership.  The caller
+// fences (_mm_sfence) before another thread reads the array.
+template <bool kStream>
+static inline void put_op(sydelta_op* w, uint32_t kind, uint64_t a, uint64_t b) {
+    static_assert(sizeof(sydelta_op) == 24, "sydelta_op layout");
+    if (kStream) {
+        long long* q = (long long*)w;
+        _mm_stream_si64(q, (long long)kind);
+        _mm_stream_si64(q + 1, (long long)a);
+        _mm_stream_si64(q + 2, (long long)b);
+    } else {
+        *w = {kind, 0, a, b};
+    }
+}
+template <bool kStream = false>
 static inline void expand_records(const WalkRec* r0, const WalkRec* r1, uint64_t n, uint64_t bb, uint64_t nbf,
                                   uint64_t ls, sydelta_op* w, uint64_t* nd, uint64_t* lb) {
     for (const WalkRec* r = r0; r < r1; ++r) {
         if (!r->kind) {
-            *w++ = {SYDELTA_OP_DATA, 0, r->off, r->a};
+            put_op<kStream>(w++, SYDELTA_OP_DATA, r->off, r->a);
             ++*nd;
             *lb += r->a;
             continue;
         }
-        for (uint64_t g = r->a - bb, e = g + r->kind; g < e; ++g) *w++ = {SYDELTA_OP_COPY, 0, g * n, g + 1 == nbf ? ls : n};
+        for (uint64_t g = r->a - bb, e = g + r->kind; g < e; ++g)
+            put_op<kStream>(w++, SYDELTA_OP_COPY, g * n, g + 1 == nbf ? ls : n);
     }
 }
 static inline uint64_t records_ops(const WalkRec* r0, const WalkRec* r1) {
@@ -3371,12 +3388,20 @@ struct sydelta_chunk {
 };
 
 // K10 over a chunk (C5, and the streamed path API's chunks): the aligned probe's results
-// stay on the device and the walk runs there, one wave per segment of kChunkSegBlocks
+// stay on the device and the walk runs there, one wave per segment of chunk_seg_blocks()
 // blocks, each from its segment's start; a segment whose true entry (the previous one's
 // exit) differs is walked again from it (after a Copy that crosses the boundary).
 // SYDELTA_CHUNK_WALK=0, or SYDELTA_PROBE=0, keeps the classifier + host walk.
 namespace {
-constexpr uint64_t kChunkSegBlocks = 128;
+// blocks per segment (SYDELTA_CHUNK_SEG overrides; a power of two from 8 to 1024)
+uint64_t chunk_seg_blocks() {
+    static const uint64_t v = [] {
+        const char* e = getenv("SYDELTA_CHUNK_SEG");
+        const uint64_t x = (e && *e) ? strtoull(e, nullptr, 10) : 128;
+        return (x >= 8 && x <= 1024 && (x & (x - 1)) == 0) ? x : (uint64_t)128;
+    }();
+    return v;
+}
 bool chunk_walk_ok(const sydelta_index* idx) {
     const char* e = getenv("SYDELTA_CHUNK_WALK");
     if (e && e[0] == '0') return false;
@@ -3388,7 +3413,7 @@ bool chunk_walk_ok(const sydelta_index* idx) {
 // when the file ends in the chunk.
 void chunk_units(const sydelta_chunk* ch, uint64_t from, std::vector<WalkUnit>& units) {
     const Src& c = ch->C.src[0];
-    const uint64_t n = ch->C.n, seg = kChunkSegBlocks * n;
+    const uint64_t n = ch->C.n, seg = chunk_seg_blocks() * n;
     units.clear();
     uint64_t rec = 0;
     const uint64_t lo = std::max(from, c.p0);
@@ -3403,10 +3428,13 @@ void chunk_units(const sydelta_chunk* ch, uint64_t from, std::vector<WalkUnit>& 
     } while (s0 < c.p1);
 }
 
-// Sub-ranges of a chunk's walk: 4 from 2048 segments, 2 from 512 (SYDELTA_CHUNK_PIPE=K)
+// Sub-ranges of a chunk's walk: 2 from 512 segments (SYDELTA_CHUNK_PIPE=K).  At C5 (8192
+// segments) two parts took 4.43-4.51 ms per step, one 4.82-4.88 and four 4.96-5.00: the
+// second part's hashing hides the first part's walk, while each further part adds a walk
+// launch whose last round runs under-filled (`profiles/r05r_*`).
 int chunk_pipe_parts(size_t nu) {
     const char* e = getenv("SYDELTA_CHUNK_PIPE");
-    int K = (e && *e) ? std::max(1, atoi(e)) : nu >= 2048 ? 4 : nu >= 512 ? 2 : 1;
+    int K = (e && *e) ? std::max(1, atoi(e)) : nu >= 512 ? 2 : 1;
     return (int)std::min<size_t>((size_t)K, nu);
 }
 
@@ -3448,12 +3476,10 @@ int chunk_pipe_launch(sydelta_chunk* ch, uint64_t from, bool probe) {
     uint64_t* d_pst = (uint64_t*)(D + o_pst);
     P.ahit = probe ? d_out : nullptr;
     P.apw = probe ? d_pw : nullptr;
-    // the unit table, probe jobs and last size up, from the mapped buffer (it outlives the
-    // copies); the per-unit results cleared (their done marks)
-    memset(H, 0, sizeof(WalkFileOut) * nu);
+    // the unit table, probe jobs and last size up, from the mapped buffer (it outlives the copies)
     memcpy(H + h_units, P.units.data(), sizeof(WalkUnit) * nu);
     ProbeJob* jobs = (ProbeJob*)(H + h_jobs);
-    for (int j = 0; j < K; ++j) jobs[j] = ProbeJob{c.off, c.kb + (uint64_t)P.ub[j] * kChunkSegBlocks, 0, 0, 0};
+    for (int j = 0; j < K; ++j) jobs[j] = ProbeJob{c.off, c.kb + (uint64_t)P.ub[j] * chunk_seg_blocks(), 0, 0, 0};
     *(uint64_t*)(H + h_last) = C.ix->last_size[0];
     HIP_TRY(hipMemcpyAsync(D, H + h_units, sizeof(WalkUnit) * nu, hipMemcpyHostToDevice, C.s));
     HIP_TRY(hipMemcpyAsync(D + o_last, H + h_last, 8, hipMemcpyHostToDevice, C.s));
@@ -3488,19 +3514,18 @@ int chunk_pipe_launch(sydelta_chunk* ch, uint64_t from, bool probe) {
     a.out = (WalkRec*)(H + h_rec);
     a.total = (unsigned long long*)(D + o_total);  // one counter: the sub-ranges' launches run in order
     a.ticks = nullptr;
-    a.mark_done = 1;
     auto probe_part = [&](int j, int phases) -> hipError_t {
-        const uint64_t b0 = (uint64_t)P.ub[j] * kChunkSegBlocks;
-        const uint64_t b1 = std::min<uint64_t>((uint64_t)P.ub[j + 1] * kChunkSegBlocks, np);
+        const uint64_t b0 = (uint64_t)P.ub[j] * chunk_seg_blocks();
+        const uint64_t b1 = std::min<uint64_t>((uint64_t)P.ub[j + 1] * chunk_seg_blocks(), np);
         return launch_probe(C.base, (const ProbeJob*)(D + o_jobs) + j, 1, b1 - b0, 1, (uint32_t)n, fast, ix,
                             d_pw + b0, d_pst + b0, d_out + b0, C.s, C.prof, phases);
     };
-    // the windows hashed first (an index built from device arrays may still be building on
-    // the aux stream: this overlaps it), then per sub-range the lookups and the walk
-    if (probe)
-        for (int j = 0; j < K; ++j) HIP_TRY(probe_part(j, 1));
-    HIP_TRY(index_wait(C.ix, C.s));
+    // per sub-range: its windows hashed, looked up (after the index: one built from device
+    // arrays may still be building on the aux stream, and the first hashing overlaps it), and
+    // walked on the aux stream while the next sub-range is hashed
     for (int j = 0; j < K; ++j) {
+        if (probe) HIP_TRY(probe_part(j, 1));
+        if (j == 0) HIP_TRY(index_wait(C.ix, C.s));
         if (probe) HIP_TRY(probe_part(j, 2));
         HIP_TRY(hipEventRecord(hand, C.s));
         HIP_TRY(hipStreamWaitEvent(s2, hand, 0));
@@ -3545,7 +3570,10 @@ int chunk_pipe_finish(sydelta_chunk* ch, uint64_t entry, uint64_t* exit_pos, syd
     std::vector<std::vector<WalkRec>> again_rec;  // re-walked units' records
     const uint64_t nbf = C.ix->fblk[1], ls = C.ix->last_size[0];
     uint64_t nops = 0, data_ops = 0, lit = 0, hits = 0, weak = 0;
-    const int pool = walk_threads();
+    // assembly threads: SYDELTA_ASM_THREADS, else the host pool and the caller (C5's 1 Mi ops:
+    // 0.46-0.58 ms on 16 + 1 threads, 0.78-0.92 on 8, `profiles/r05s_*`)
+    static const int pool = getenv("SYDELTA_ASM_THREADS") ? std::max(1, atoi(getenv("SYDELTA_ASM_THREADS")))
+                                                            : walk::HostPool::get().size() + 1;
     double ms_wait = 0;
     // units [a, b) after ops [0, nops)
     auto assemble = [&](size_t a, size_t b) -> int {
@@ -3576,8 +3604,10 @@ int chunk_pipe_finish(sydelta_chunk* ch, uint64_t entry, uint64_t* exit_pos, syd
         if (!run_parallel(nt, [&](int t) {
                 for (size_t u = a + m * t / nt; u < a + m * (t + 1) / nt; ++u) {
                     const WalkRec* r0 = span[u].first + join[u - a];
-                    expand_records(r0, span[u].second, n, 0, nbf, ls, ops.data() + first[u - a], &nd[t], &lb[t]);
+                    expand_records<true>(r0, span[u].second, n, 0, nbf, ls, ops.data() + first[u - a], &nd[t],
+                                         &lb[t]);
                 }
+                _mm_sfence();  // the streamed ops visible before the task reports done
             }))
             return fail(SYDELTA_E_OOM, "out of host memory (op lists)");
         for (int t = 0; t < nt; ++t) {
@@ -3625,54 +3655,23 @@ int chunk_pipe_finish(sydelta_chunk* ch, uint64_t entry, uint64_t* exit_pos, syd
         }
         ms_take += ms_since(tt);
     };
-    // Units are assembled as they finish: the kernel marks each unit's results done (after a
-    // system-scope fence), waves finish roughly in unit order, so the first ones' ops are
-    // written while the last ones still walk.  Batches of at least kBatch units, or whatever
-    // is done once the sub-range's event has completed.
-    constexpr size_t kBatch = 1024;
-    const volatile uint64_t* mark = (const volatile uint64_t*)&P.fout[0].pad;
-    auto done_to = [&](size_t u, size_t b) {  // first unit in [u, b) not marked done
-        while (u < b && mark[u * (sizeof(WalkFileOut) / 8)]) ++u;
-        return u;
-    };
     size_t stop = nu;  // the first unit whose entry is not the previous one's exit
     for (size_t j = 0; j + 1 < P.ub.size() && stop == nu; ++j) {
-        size_t a = std::max<size_t>(P.ub[j], u0);
-        const size_t b = P.ub[j + 1];
-        auto tw = std::chrono::steady_clock::now();
-        bool all = false;
-        while (a < b && stop == nu) {
-            size_t e = done_to(a, b);
-            if (e < b && e - a < kBatch) {
-                if (!all) {
-                    const hipError_t q = hipEventQuery(P.done[j]);
-                    if (q == hipSuccess) {
-                        all = true;  // every unit of the sub-range is marked
-                        continue;
-                    }
-                    if (q != hipErrorNotReady) HIP_TRY(q);
-                    _mm_pause();
-                    continue;
-                }
-                return fail(SYDELTA_E_KERNEL, "chunk walk: unit %zu not marked done", e);
-            }
-            std::atomic_thread_fence(std::memory_order_acquire);
-            ms_wait += ms_since(tw);
-            take(a, e);
-            size_t c = a;
-            while (c < e && units[c].entry == (c == u0 ? entry : out[c - 1].exit)) ++c;
-            if (int r = assemble(a, c)) return r;
-            if (c < e) stop = c;
-            a = e;
-            tw = std::chrono::steady_clock::now();
-        }
+        const size_t a = std::max<size_t>(P.ub[j], u0), b = P.ub[j + 1];
+        if (b <= a) continue;
+        const auto tw = std::chrono::steady_clock::now();
+        HIP_TRY(hipEventSynchronize(P.done[j]));
+        ms_wait += ms_since(tw);
+        take(a, b);
+        size_t e = a;
+        while (e < b && units[e].entry == (e == u0 ? entry : out[e - 1].exit)) ++e;
+        if (int r = assemble(a, e)) return r;
+        if (e < b) stop = e;
     }
     int rounds = 0;
     if (stop < nu) {
         HIP_TRY(hipEventSynchronize(P.done.back()));
-        size_t t0 = stop + 1;  // the first unit not taken yet: past the batch that held `stop`
-        while (t0 < nu && span[t0].first) ++t0;
-        take(t0, nu);
+        take(P.ub[std::upper_bound(P.ub.begin(), P.ub.end(), (uint32_t)stop) - P.ub.begin()], nu);  // later sub-ranges
         for (;;) {
             std::vector<size_t> bad;
             std::vector<WalkUnit> again;

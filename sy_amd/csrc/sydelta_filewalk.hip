@@ -455,10 +455,6 @@ __global__ __launch_bounds__(64, 4) void k_walk_files(WalkArgs a) {
         }
     }
     if (lane == 0) a.fout[blockIdx.x] = WalkFileOut{(uint32_t)base, nrec, weak_hits, hits, exit, 0};
-    if (a.mark_done) {  // the host reads units as they finish (chunk_pipe_finish)
-        __threadfence_system();
-        if (lane == 0) *(volatile uint64_t*)&a.fout[blockIdx.x].pad = 1;
-    }
     wtick(kWtOut);
 }
 

@@ -239,7 +239,7 @@ struct WalkFileOut {
     uint32_t weak_hits;    // candidate windows verified (passed the Bloom filter)
     uint32_t hits;         // windows classified as hits
     uint64_t exit;         // where the walk left the unit (>= end; a final unit: len)
-    uint64_t pad;          // WalkArgs::mark_done: 1 once the unit's results are complete
+    uint64_t pad;
 };
 struct WalkArgs {
     const uint8_t* base;         // launch base
@@ -247,8 +247,6 @@ struct WalkArgs {
     const uint64_t* last_size;   // per basis file (0: empty signature)
     uint32_t nunits, n, nm;
     uint32_t fw_max;             // LDS filter words (0: the filter is read from global memory)
-    uint32_t mark_done;          // 1: fout in host memory; each unit's `pad` set to 1 after its
-                                 // results are visible to the host (a system-scope fence first)
     const FileIx* files;
     const uint64_t* fblk;
     const uint32_t* filt;
