@@ -144,8 +144,10 @@ hipStream_t thread_stream_impl(int device) {
     return s;
 }
 
-// A second stream per (thread, device) for work overlapped with the first (the chunk
-// walk's launches beside its probe); ordered by events only, never destroyed.
+// A second stream per (thread, device) for work overlapped with the caller's (the index
+// build, the chunk walk's parts); ordered by events only, never destroyed.  (The walks on
+// low-priority streams, so that the dispatcher would favour the hashing beside them,
+// measured the same: `profiles/r05x_*`.)
 hipStream_t thread_aux_stream(int device) {
     static thread_local std::map<int, hipStream_t> streams;
     auto it = streams.find(device);
@@ -3364,8 +3366,10 @@ struct ChunkPipe {
     const uint32_t* ahit = nullptr;  // the probe's results (device; NULL: no probe)
     const uint32_t* apw = nullptr;
     void release() {  // the chunk's device is current
-        if (!done.empty()) (void)hipEventSynchronize(done.back());  // the aux stream runs in order
-        for (hipEvent_t e : done) give_event(device, e);
+        for (hipEvent_t e : done) {  // the parts' walks
+            (void)hipEventSynchronize(e);
+            give_event(device, e);
+        }
         done.clear();
         if (dmem) (void)hipFreeAsync(dmem, ds);
         dmem = nullptr;
@@ -3527,16 +3531,17 @@ int chunk_pipe_launch(sydelta_chunk* ch, uint64_t from, bool probe) {
         if (probe) HIP_TRY(probe_part(j, 1));
         if (j == 0) HIP_TRY(index_wait(C.ix, C.s));
         if (probe) HIP_TRY(probe_part(j, 2));
+        hipStream_t sw = s2;
         HIP_TRY(hipEventRecord(hand, C.s));
-        HIP_TRY(hipStreamWaitEvent(s2, hand, 0));
+        HIP_TRY(hipStreamWaitEvent(sw, hand, 0));
         hipEvent_t e = take_event(P.device);
         if (!e) return fail(SYDELTA_E_OOM, "no event for the chunk walk");
         P.done.push_back(e);
         a.units = (const WalkUnit*)D + P.ub[j];
         a.nunits = P.ub[j + 1] - P.ub[j];
         a.fout = (WalkFileOut*)P.fout + P.ub[j];
-        HIP_TRY(launch_walk_files(a, s2, C.prof));
-        HIP_TRY(hipEventRecord(e, s2));
+        HIP_TRY(launch_walk_files(a, sw, C.prof));
+        HIP_TRY(hipEventRecord(e, sw));
     }
     if (host_timing) fprintf(stderr, "sydelta chunk launch: %zu segments, %d parts: %.3f ms\n", nu, K, ms_since(t_begin));
     return SYDELTA_OK;
@@ -3670,7 +3675,7 @@ int chunk_pipe_finish(sydelta_chunk* ch, uint64_t entry, uint64_t* exit_pos, syd
     }
     int rounds = 0;
     if (stop < nu) {
-        HIP_TRY(hipEventSynchronize(P.done.back()));
+        for (hipEvent_t e : P.done) HIP_TRY(hipEventSynchronize(e));
         take(P.ub[std::upper_bound(P.ub.begin(), P.ub.end(), (uint32_t)stop) - P.ub.begin()], nu);  // later sub-ranges
         for (;;) {
             std::vector<size_t> bad;

@@ -87,6 +87,12 @@ hipError_t hipStreamCreateWithFlags(hipStream_t* s, unsigned int) {
     *s = new ihipStream_t();
     return hipSuccess;
 }
+hipError_t hipStreamCreateWithPriority(hipStream_t* s, unsigned int f, int) { return hipStreamCreateWithFlags(s, f); }
+hipError_t hipDeviceGetStreamPriorityRange(int* least, int* greatest) {
+    *least = 0;
+    *greatest = -1;
+    return hipSuccess;
+}
 hipError_t hipStreamSynchronize(hipStream_t) { return hipSuccess; }
 hipError_t hipStreamWaitEvent(hipStream_t, hipEvent_t, unsigned int) { return hipSuccess; }
 hipError_t hipEventCreate(hipEvent_t* e) {
@@ -666,11 +672,11 @@ hipError_t launch_walk_files(const WalkArgs& a, hipStream_t, Profiler*) {
         if (rec.size() > cap) return hipErrorInvalidValue;  // the kernel's staging region would overflow
         if (!a.out) {  // records left in the staging region
             std::copy(rec.begin(), rec.end(), a.stage + U.rec_off);
-            a.fout[u] = WalkFileOut{(uint32_t)U.rec_off, (uint32_t)rec.size(), weak_hits, hits, exit, a.mark_done};
+            a.fout[u] = WalkFileOut{(uint32_t)U.rec_off, (uint32_t)rec.size(), weak_hits, hits, exit, 0};
             continue;
         }
         std::copy(rec.begin(), rec.end(), a.out + placed);
-        a.fout[u] = WalkFileOut{(uint32_t)placed, (uint32_t)rec.size(), weak_hits, hits, exit, a.mark_done};
+        a.fout[u] = WalkFileOut{(uint32_t)placed, (uint32_t)rec.size(), weak_hits, hits, exit, 0};
         placed += rec.size();
     }
     if (a.out) *a.total = placed;
