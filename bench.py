@@ -1051,6 +1051,24 @@ def main():
         if args.workload == "c4" and len(c4_groups) > 1:
             roof["per_launch_overlap"] = ("the dominant kernel's launches of several callers overlap: its per-launch "
                                           "figures overstate its time; kernel_busy is the step's roofline")
+    if roof is not None and roof.get("kernel") == "k_scan_r" and positions and args.workload == "c3":
+        # the C3 ceiling: every position tested, a level-1 filter of at most
+        # 1.17 bits per key in LDS passes >= 0.444 of them (information bound), each pass one
+        # L2 request for its level-2 word, + 0.016 for the source rows + 0.008 for the table
+        # lookups; the chip serves ~270 G random L2 requests/s.  The rest of the step as measured.
+        step_ms = elapsed / args.steps * 1e3
+        rest = step_ms - roof["avg_launch_ms"] * (prof["k_scan_r"]["count"] / args.steps)
+        ceil = {}
+        for name, rpp in (("information_bound", 0.468), ("ribbon_as_built", 0.528)):
+            scan = positions * rpp / 270e9 * 1e3
+            st = scan + rest
+            ceil[name] = {"requests_per_position": rpp, "scan_ms": round(scan, 3), "step_ms": round(st, 3),
+                          "value_GiBps": round(bytes_per_step / (st * 1e-3) / GIB, 1),
+                          "hbm_frac": round(bytes_per_step / (st * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)}
+        roof["ceiling"] = dict(ceil, model="L2 request rate 270 G/s x requests per position; the rest of the step "
+                                           "as measured (DESIGN.md §6.6)", value_frac_of_bound=round(
+                                               (bytes_per_step / (step_ms * 1e-3) / GIB) /
+                                               ceil["information_bound"]["value_GiBps"], 4))
     kernels = {k: {"avg_ms": round(v["ms"] / max(1, v["count"]), 4), "launches": v["count"]} for k, v in prof.items()}
 
     if rank == 0:

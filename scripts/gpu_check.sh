@@ -19,5 +19,8 @@ cd /tmp
 step 600 rocprofv3 --kernel-trace --stats -d "$OUT/trace" -o run --output-format csv -- python3 "$R/bench.py" --no-cpu-baseline --no-host-inclusive "$@" > "$OUT/prof.log" 2>&1 || { tail -20 "$OUT/prof.log"; exit 1; }
 step 300 rocprofv3 --pmc FETCH_SIZE --kernel-trace -d "$OUT/pmc_fetch" -o run --output-format csv -- python3 "$R/bench.py" --no-cpu-baseline --no-host-inclusive --steps 2 --warmup 1 "$@" > "$OUT/pmc1.log" 2>&1 || { tail -20 "$OUT/pmc1.log"; exit 1; }
 step 300 rocprofv3 --pmc WRITE_SIZE --kernel-trace -d "$OUT/pmc_write" -o run --output-format csv -- python3 "$R/bench.py" --no-cpu-baseline --no-host-inclusive --steps 2 --warmup 1 "$@" > "$OUT/pmc2.log" 2>&1 || { tail -20 "$OUT/pmc2.log"; exit 1; }
+if [ -n "${TCC:-}" ]; then
+    step 300 rocprofv3 --pmc TCC_REQ_sum TCC_HIT_sum TCC_MISS_sum --kernel-trace -d "$OUT/pmc_tcc" -o run --output-format csv -- python3 "$R/bench.py" --no-cpu-baseline --no-host-inclusive --steps 2 --warmup 1 "$@" > "$OUT/pmc3.log" 2>&1 || { tail -20 "$OUT/pmc3.log"; exit 1; }
+fi
 echo "== done"
 find "$OUT" -name "*.csv" | head -20

@@ -6,8 +6,15 @@
 Writes <dst>_kernel_stats.csv (the --kernel-trace --stats summary, verbatim) and
 <dst>_pmc.json: per kernel, average duration and HBM bytes per launch from the
 FETCH_SIZE / WRITE_SIZE passes, corrected as MI355X_MICROARCH.md §HBM says
-(FETCH_SIZE is in KiB and reports half the bytes of 16-B/lane streaming reads on
-gfx950 -> x1024 x2; WRITE_SIZE in KiB, exact -> x1024).  bench.py reads the
+(FETCH_SIZE is in KiB and counts every L2 -> fabric read request as 64 B; WRITE_SIZE
+in KiB, exact -> x1024).  Read bytes, calibrated per access pattern
+(profiles/r05zb_fetch_calibration.json, tools/micro_fetch_cal.hip): a kernel that streams
+its algorithmic bytes (kernel=bytes below) in whole 128-B lines sends one 128-B request per
+line; every other request it sends is a partial-line miss of 64 B (gathers of filter
+words, table buckets).  So read bytes = 128 x min(requests, bytes/128) + 64 x the rest.
+Without a byte count a kernel's requests are taken as 128-B ones (x2, the streaming
+calibration).  Requests the Infinity Cache serves are counted as well (the counters do not
+separate them), so for IC-resident tables this is traffic beyond L2, an upper bound on HBM.  bench.py reads the
 _pmc.json whose workload and block size match its own run to fill roofline.traffic
 (a file without them, or of another workload, is never borrowed).
 """
@@ -71,7 +78,15 @@ def main(src, dst, sizes=()):
         out[k] = dict(dur[k])
         if f is not None:
             out[k]["fetch_kib_raw"] = round(f, 3)
-            out[k]["hbm_read_bytes"] = int(f * 1024 * 2)
+            req = f * 1024 / 64  # EA read requests (FETCH_SIZE tallies 64 B each)
+            out[k]["read_requests"] = int(req)
+            if k in sizes:
+                full = min(req, int(sizes[k]) / 128)
+                out[k]["full_line_requests"] = int(full)
+                out[k]["partial_line_requests"] = int(req - full)
+                out[k]["hbm_read_bytes"] = int(128 * full + 64 * (req - full))
+            else:
+                out[k]["hbm_read_bytes"] = int(128 * req)
         if w is not None:
             out[k]["hbm_write_bytes"] = int(w * 1024)
         if f is not None and w is not None:
@@ -83,7 +98,9 @@ def main(src, dst, sizes=()):
             if "traffic_bytes" in out[k]:
                 out[k]["traffic_over_algorithmic"] = round(out[k]["traffic_bytes"] / int(sizes[k]), 3)
     meta = {"source": src, "workload": workload, "block_size": int(block_size) if block_size else None,
-            "correction": "FETCH_SIZE KiB x1024 x2 (gfx950 half-count of 16B/lane reads); WRITE_SIZE KiB x1024",
+            "correction": ("FETCH_SIZE KiB x1024 / 64 = read requests; read bytes = 128 x the full-line requests of the "
+                           "kernel's streamed bytes + 64 x the partial-line rest (x2 without a byte count); WRITE_SIZE "
+                           "KiB x1024 (profiles/r05zb_fetch_calibration.json)"),
             "kernels": out}
     json.dump(meta, open(dst + "_pmc.json", "w"), indent=1)
     print(json.dumps(out, indent=1))
