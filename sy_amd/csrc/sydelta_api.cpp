@@ -144,10 +144,23 @@ hipStream_t thread_stream_impl(int device) {
     return s;
 }
 
+// A third and fourth stream per (thread, device): the chunk walk's parts alternate between
+// them, so that a part's walk starts when its lookups are done even while the previous
+// part's still runs.  Ordered by events only, never destroyed.  (Low-priority walk streams,
+// so that the dispatcher would favour the hashing beside them, measured the same:
+// `profiles/r05x_*`.)
+hipStream_t thread_walk_stream(int device, int i) {
+    static thread_local std::map<int, hipStream_t> streams[2];
+    auto it = streams[i].find(device);
+    if (it != streams[i].end()) return it->second;
+    hipStream_t s = nullptr;
+    if (hipStreamCreateWithFlags(&s, hipStreamNonBlocking) != hipSuccess) return nullptr;
+    streams[i][device] = s;
+    return s;
+}
+
 // A second stream per (thread, device) for work overlapped with the caller's (the index
-// build, the chunk walk's parts); ordered by events only, never destroyed.  (The walks on
-// low-priority streams, so that the dispatcher would favour the hashing beside them,
-// measured the same: `profiles/r05x_*`.)
+// build); ordered by events only, never destroyed.
 hipStream_t thread_aux_stream(int device) {
     static thread_local std::map<int, hipStream_t> streams;
     auto it = streams.find(device);
@@ -3460,6 +3473,22 @@ int chunk_pipe_launch(sydelta_chunk* ch, uint64_t from, bool probe) {
     const int K = probe ? chunk_pipe_parts(nu) : 1;
     P.ub.resize(K + 1);
     for (int j = 0; j <= K; ++j) P.ub[j] = (uint32_t)(nu * j / K);
+    if (const char* wv = getenv("SYDELTA_CHUNK_PIPE_W")) {  // A/B: part sizes by weights "w0,w1,..."
+        std::vector<double> wt;
+        for (const char* q = wv; *q;) {
+            wt.push_back(std::max(0.0, strtod(q, nullptr)));
+            while (*q && *q != ',') ++q;
+            if (*q == ',') ++q;
+        }
+        if ((int)wt.size() == K) {
+            double tot = 0, acc = 0;
+            for (double x : wt) tot += x;
+            for (int j = 1; j < K && tot > 0; ++j) {
+                acc += wt[j - 1];
+                P.ub[j] = (uint32_t)std::min<double>((double)nu - (K - j), std::max<double>(P.ub[j - 1] + 1, nu * acc / tot));
+            }
+        }
+    }
     auto al = [](size_t v) { return (v + 255) & ~(size_t)255; };
     const size_t o_last = al(sizeof(WalkUnit) * nu), o_total = o_last + 256, o_jobs = o_total + 256;
     const size_t o_out = o_jobs + al(sizeof(ProbeJob) * K), o_pw = o_out + al(4 * np), o_pst = o_pw + al(4 * np);
@@ -3489,9 +3518,9 @@ int chunk_pipe_launch(sydelta_chunk* ch, uint64_t from, bool probe) {
     HIP_TRY(hipMemcpyAsync(D + o_last, H + h_last, 8, hipMemcpyHostToDevice, C.s));
     if (probe) HIP_TRY(hipMemcpyAsync(D + o_jobs, jobs, sizeof(ProbeJob) * K, hipMemcpyHostToDevice, C.s));
     HIP_TRY(hipMemsetAsync(D + o_total, 0, 8, C.s));
-    hipStream_t s2 = thread_aux_stream(P.device);
+    hipStream_t s2[2] = {thread_walk_stream(P.device, 0), thread_walk_stream(P.device, 1)};
     hipEvent_t hand = handoff_event(P.device);
-    if (!s2 || !hand) return fail(SYDELTA_E_OOM, "no stream or event for the chunk walk");
+    if (!s2[0] || !s2[1] || !hand) return fail(SYDELTA_E_OOM, "no stream or event for the chunk walk");
     const bool fast = ((uintptr_t)(C.base + c.off) & 15) == 0;
     WalkArgs a{};
     a.base = C.base;
@@ -3531,7 +3560,7 @@ int chunk_pipe_launch(sydelta_chunk* ch, uint64_t from, bool probe) {
         if (probe) HIP_TRY(probe_part(j, 1));
         if (j == 0) HIP_TRY(index_wait(C.ix, C.s));
         if (probe) HIP_TRY(probe_part(j, 2));
-        hipStream_t sw = s2;
+        hipStream_t sw = s2[j & 1];
         HIP_TRY(hipEventRecord(hand, C.s));
         HIP_TRY(hipStreamWaitEvent(sw, hand, 0));
         hipEvent_t e = take_event(P.device);
