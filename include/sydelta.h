@@ -144,9 +144,10 @@ int sydelta_signature_device(int device, const uint8_t *d_buf, uint64_t len, uin
  * Host arrays: the index is built when the call returns.  Device arrays: they are
  * copied in `stream`'s order (the caller may overwrite them after that point of the
  * stream) and the call returns without waiting; the table is built on a library
- * stream and every call that uses the index orders its own stream after the build,
- * so work the caller queues meanwhile (the source's upload, its aligned probe)
- * overlaps it.  SYDELTA_INDEX_SYNC=1 builds on `stream` and waits, as for host arrays. */
+ * stream (one file; a batch: on `stream`) and every call that uses the index orders
+ * its own stream after the build, so work the caller queues meanwhile (the source's
+ * upload, its aligned probe) overlaps it.  SYDELTA_INDEX_SYNC=1 builds on `stream` and
+ * waits, as for host arrays. */
 int sydelta_index_create(int device, const uint32_t *weak, const uint64_t *strong, uint64_t nblocks,
                          uint64_t block_size, uint64_t last_size, int arrays_on_device, void *stream,
                          sydelta_index **out);

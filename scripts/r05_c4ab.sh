@@ -1,0 +1,18 @@
+#!/bin/bash
+# Round 5: C4 A/B of the library (current vs the r05g build) on one box, 1 and 10 callers.
+set -euo pipefail
+tag=${1:-r05}
+R=${GRAFT_REPO_ROOT:-$(pwd)}
+out=$R/gpurun_out/$tag
+mkdir -p "$out"
+export TMPDIR=/tmp
+for r in a b; do
+  for v in cur r05g; do
+    if [ $v = cur ]; then unset SYDELTA_LIB_VARIANT; else export SYDELTA_LIB_VARIANT=$v; fi
+    timeout -k 10 300 python -u bench.py --workload c4 --steps 10 --warmup 2 --no-cpu-baseline > "$out/c4_c1_${v}_$r.json" 2> "$out/c4_c1_${v}_$r.err"
+    timeout -k 10 300 python -u bench.py --workload c4 --callers 10 --steps 10 --warmup 2 --no-cpu-baseline \
+        > "$out/c4_c10_${v}_$r.json" 2> "$out/c4_c10_${v}_$r.err"
+  done
+done
+unset SYDELTA_LIB_VARIANT
+echo done

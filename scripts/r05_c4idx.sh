@@ -1,0 +1,19 @@
+#!/bin/bash
+# Round 5: batch index built without a host wait -- parity (file walk, batch tests), C4 shares, 10 callers.
+set -euo pipefail
+tag=${1:-r05}
+R=${GRAFT_REPO_ROOT:-$(pwd)}
+out=$R/gpurun_out/$tag
+mkdir -p "$out"
+export TMPDIR=/tmp
+timeout -k 10 600 python -u -m pytest -x -q --timeout 240 --timeout-method thread tests/test_gpu_file_walk.py \
+    tests/test_gpu_match.py tests/test_gpu_async_index.py tests/test_gpu_reentrant.py > "$out/pytest.log" 2>&1
+for f in 10000 2500 1250; do
+  for v in 0 1; do
+    SYDELTA_INDEX_SYNC=$v timeout -k 10 300 python -u bench.py --workload c4 --files $f --steps 20 --warmup 3 --no-cpu-baseline \
+        > "$out/c4_f${f}_s$v.json" 2> "$out/c4_f${f}_s$v.err"
+  done
+done
+timeout -k 10 300 python -u bench.py --workload c4 --callers 10 --steps 10 --warmup 2 --no-cpu-baseline \
+    > "$out/c4_c10.json" 2> "$out/c4_c10.err"
+echo done

@@ -1027,8 +1027,10 @@ static int index_create_impl(int device, const uint32_t* weak, const uint64_t* s
         HIP_TRY(hipMemcpyAsync(x->d_weak, weak, 4 * nblocks, kind, s));
         HIP_TRY(hipMemcpyAsync(x->d_strong, strong, 8 * nblocks, kind, s));
     }
-    // device arrays: built on this thread's aux stream, nothing waited for here
-    // (SYDELTA_INDEX_SYNC=1: on the caller's stream, synchronized, as for host arrays)
+    // device arrays: nothing waited for here (SYDELTA_INDEX_SYNC=1: on the caller's stream,
+    // synchronized, as for host arrays).  One file is built on this thread's aux stream; a
+    // batch's index, used at once by its match, in the caller's stream order (more streams per
+    // caller share the process's four hardware queues with ten callers' work).
     static const bool index_sync = getenv("SYDELTA_INDEX_SYNC") && getenv("SYDELTA_INDEX_SYNC")[0] == '1';
     if (arrays_on_device && !index_sync) {
         const size_t fb = sizeof(FileIx) * nfiles, tb = ((fb + 15) & ~(size_t)15) + 8 * (nfiles + 1);
@@ -1038,7 +1040,9 @@ static int index_create_impl(int device, const uint32_t* weak, const uint64_t* s
         HIP_TRY(hipMemcpyAsync(ix.d_files, x->stage.p, fb, hipMemcpyHostToDevice, s));
         HIP_TRY(hipMemcpyAsync(ix.d_fblk, x->stage.p + ((fb + 15) & ~(size_t)15), 8 * (nfiles + 1),
                                hipMemcpyHostToDevice, s));
-        const hipStream_t sb = thread_aux_stream(device);
+        // one file: on the aux stream, beside the caller's next work; a batch: in the caller's
+        // stream order, no host wait (its match follows at once on that stream)
+        const hipStream_t sb = nfiles == 1 ? thread_aux_stream(device) : s;
         if (!sb) return fail(SYDELTA_E_OOM, "no stream for the index build");
         HIP_TRY(stream_after(sb, s, device));
         x->ready = take_event(device);
@@ -2442,49 +2446,162 @@ static inline uint64_t records_ops(const WalkRec* r0, const WalkRec* r1) {
 }
 
 // The batched match with the walk on the device: one unit per file.
+// Segments per file of a batched device walk (SYDELTA_FILE_SEGS=G forces G): a wave walks
+// its unit serially, so a batch of fewer files than the chip holds twice (8192 waves at
+// four per SIMD) is cut into segments of at least 32 blocks (8 when forced).  nf counts the
+// files of every batch walking at the time (concurrent callers share the chip).
+std::atomic<uint64_t> g_walking_files{0};
+static uint64_t file_segs(uint64_t nf) {
+    const char* e = getenv("SYDELTA_FILE_SEGS");  // read per call (tests switch it)
+    if (e && *e) return std::max<uint64_t>(1, strtoull(e, nullptr, 10));
+    uint64_t g = 1;
+    while (g < 64 && g * 2 * nf <= 8192) g *= 2;
+    return g;
+}
+
+// The batched match with the walk on the device: one unit per file, or per segment of a
+// file (file_segs).  A segment is walked from its start; where the previous segment's walk
+// left it later (a Copy crossing the boundary), the segment's walk still holds when its
+// leading literal run reaches that exit -- the greedy walk from the exit then classifies the
+// same positions the same way -- and its leading Data op is cut to start there; otherwise
+// the segment is walked again from the exit (rounds, as for a chunk's segments).
 static int match_walk_files(sydelta_index* ix, const uint8_t* d_buf, const uint64_t* src_off, const uint64_t* src_len,
                             hipStream_t s, Profiler* prof, sydelta_delta_batch* b) {
     static const bool host_timing = getenv("SYDELTA_HOST_TIMING") != nullptr;
     const uint64_t n = ix->bs, nf = ix->nfiles;
-    std::vector<WalkUnit> units(nf);
+    struct Walking {  // this batch's files counted while it walks
+        uint64_t k, total;
+        explicit Walking(uint64_t k_) : k(k_), total(g_walking_files.fetch_add(k_) + k_) {}
+        ~Walking() { g_walking_files.fetch_sub(k); }
+    } walking(nf);
+    const uint64_t G = file_segs(walking.total), min_seg = (getenv("SYDELTA_FILE_SEGS") && *getenv("SYDELTA_FILE_SEGS")) ? 8 : 32;
+    std::vector<WalkUnit> units;
+    units.reserve(nf * G);
+    std::vector<uint64_t> fu(nf + 1, 0);  // file f's units: [fu[f], fu[f+1])
     uint64_t rec_off = 0;
     for (uint64_t f = 0; f < nf; ++f) {
+        fu[f] = units.size();
         const uint64_t len = src_len[f], nbf = ix->fblk[f + 1] - ix->fblk[f];
         const uint64_t p1 = (nbf && len >= n) ? len - n + 1 : 0;  // an empty signature matches nothing (generator.rs:121)
-        units[f] = WalkUnit{src_off[f], len, 0, p1, p1, rec_off, 0, (uint32_t)f, 1};
-        rec_off += 2 * (p1 / n) + 4;
+        const uint64_t nb = (p1 + n - 1) / n;
+        const uint64_t segb = G > 1 ? std::max<uint64_t>(min_seg, (nb + G - 1) / G) : std::max<uint64_t>(nb, 1);
+        uint64_t e0 = 0;
+        do {
+            const uint64_t e1 = std::min(p1, e0 + segb * n);
+            units.push_back(WalkUnit{src_off[f], len, e0, e1, p1, rec_off, 0, (uint32_t)f, (uint32_t)(e1 >= p1)});
+            rec_off += 2 * ((e1 - e0) / n) + 4;
+            e0 = e1;
+        } while (e0 < p1);
     }
+    fu[nf] = units.size();
+    const uint64_t nu = units.size();
     WalkResult res;
     if (int r = run_walk(ix, d_buf, units, nullptr, nullptr, true, s, prof, res)) return r;
     const auto t1 = std::chrono::steady_clock::now();
+    std::vector<WalkFileOut>& out = res.out;
+    std::vector<std::pair<const WalkRec*, const WalkRec*>> span(nu);
+    for (uint64_t u = 0; u < nu; ++u) span[u] = {res.rec + out[u].base, res.rec + out[u].base + out[u].count};
+    // chain the segments of each file
+    constexpr uint64_t kNoTrim = UINT64_MAX;
+    std::vector<uint64_t> tstart;  // a segment's leading Data op cut to start here
+    std::vector<std::vector<WalkRec>> kept;  // records that outlive the pinned buffer
+    int rounds = 0;
+    if (nu > nf) {
+        tstart.assign(nu, kNoTrim);
+        for (;;) {
+            std::vector<uint64_t> bad;
+            for (uint64_t f = 0; f < nf; ++f)
+                for (uint64_t u = fu[f] + 1; u < fu[f + 1]; ++u) {
+                    const uint64_t pe = out[u - 1].exit;
+                    tstart[u] = kNoTrim;
+                    if (units[u].entry == pe) continue;
+                    const WalkRec* r0 = span[u].first;
+                    const uint64_t h = (r0 < span[u].second && !r0->kind) ? r0->off + r0->a : units[u].entry;
+                    if (pe > units[u].entry && h >= pe)
+                        tstart[u] = pe;  // the walk from pe meets this one at once
+                    else
+                        bad.push_back(u);
+                }
+            if (bad.empty()) break;
+            ++rounds;
+            if (kept.empty()) {  // the next launch reuses the pinned buffer: keep the records
+                kept.emplace_back(res.rec, res.rec + res.nrec);
+                const WalkRec* base = kept.back().data();
+                for (uint64_t u = 0; u < nu; ++u)
+                    span[u] = {base + (span[u].first - res.rec), base + (span[u].second - res.rec)};
+            }
+            std::vector<WalkUnit> again;
+            uint64_t roff = 0;
+            for (uint64_t u : bad) {
+                units[u].entry = out[u - 1].exit;
+                units[u].end = std::max(units[u].end, units[u].entry);
+                WalkUnit w = units[u];
+                w.rec_off = roff;
+                roff += 2 * ((w.end - w.entry) / n) + 4;
+                again.push_back(w);
+            }
+            WalkResult r1;
+            if (int r = run_walk(ix, d_buf, again, nullptr, nullptr, true, s, prof, r1)) return r;
+            kept.emplace_back(r1.rec, r1.rec + r1.nrec);
+            const WalkRec* base = kept.back().data();
+            for (size_t j = 0; j < bad.size(); ++j) {
+                out[bad[j]] = r1.out[j];
+                span[bad[j]] = {base + r1.out[j].base, base + r1.out[j].base + r1.out[j].count};
+            }
+        }
+    }
     // each file's records into its op array (recycled arrays: no page faults)
     const int nthr = nf >= 64 ? walk_threads() : 1;
     std::atomic<uint64_t> next{0};
     std::vector<sydelta_match_stats> part(nthr);
     auto worker = [&](int t) {
         sydelta_match_stats acc{};
+        std::vector<WalkRec> tmp;
         for (;;) {
             const uint64_t f0 = next.fetch_add(64);
             if (f0 >= nf) break;
             for (uint64_t f = f0; f < std::min<uint64_t>(nf, f0 + 64); ++f) {
-                const WalkFileOut& o = res.out[f];
                 sydelta_delta& d = b->d[f];
-                const WalkRec* r0 = res.rec + o.base;
-                const uint64_t nops = records_ops(r0, r0 + o.count);
+                const WalkRec *r0 = span[fu[f]].first, *r1 = span[fu[f]].second;
+                uint32_t wh = 0, vh = 0;
+                for (uint64_t u = fu[f]; u < fu[f + 1]; ++u) {
+                    wh += out[u].weak_hits;
+                    vh += out[u].hits;
+                }
+                if (fu[f + 1] - fu[f] > 1) {  // the segments' records joined: cut leading runs, merged Data ops
+                    tmp.clear();
+                    for (uint64_t u = fu[f]; u < fu[f + 1]; ++u)
+                        for (const WalkRec* r = span[u].first; r < span[u].second; ++r) {
+                            WalkRec x = *r;
+                            if (r == span[u].first && tstart[u] != kNoTrim) {
+                                const uint64_t h = x.off + x.a;
+                                if (h <= tstart[u]) continue;
+                                x.a = (uint32_t)(h - tstart[u]);
+                                x.off = tstart[u];
+                            }
+                            if (!x.kind && !tmp.empty() && !tmp.back().kind && tmp.back().off + tmp.back().a == x.off)
+                                tmp.back().a += x.a;
+                            else
+                                tmp.push_back(x);
+                        }
+                    r0 = tmp.data();
+                    r1 = tmp.data() + tmp.size();
+                }
+                const uint64_t nops = records_ops(r0, r1);
                 d.ops.resize(nops);
                 uint64_t nd = 0, lb = 0;
-                expand_records(r0, r0 + o.count, n, ix->fblk[f], ix->fblk[f + 1] - ix->fblk[f], ix->last_size[f],
-                               d.ops.data(), &nd, &lb);
+                expand_records(r0, r1, n, ix->fblk[f], ix->fblk[f + 1] - ix->fblk[f], ix->last_size[f], d.ops.data(),
+                               &nd, &lb);
                 d.stats.copy_ops = nops - nd;
                 d.stats.data_ops = nd;
                 d.stats.literal_bytes = lb;
-                d.stats.weak_hits = o.weak_hits;
-                d.stats.verified_hits = o.hits;
+                d.stats.weak_hits = wh;
+                d.stats.verified_hits = vh;
                 acc.copy_ops += d.stats.copy_ops;
                 acc.data_ops += nd;
                 acc.literal_bytes += lb;
-                acc.weak_hits += o.weak_hits;
-                acc.verified_hits += o.hits;
+                acc.weak_hits += wh;
+                acc.verified_hits += vh;
             }
         }
         part[t] = acc;
@@ -2503,9 +2620,9 @@ static int match_walk_files(sydelta_index* ix, const uint8_t* d_buf, const uint6
         ph = PinnedHits();
     }
     if (host_timing)
-        fprintf(stderr, "sydelta file walk: %llu files, %llu records: kernel+counts %.3f ms, records D2H %.3f ms, "
-                "expand %.3f ms\n", (unsigned long long)nf, (unsigned long long)res.nrec, res.ms_kernel, res.ms_d2h,
-                ms_since(t1));
+        fprintf(stderr, "sydelta file walk: %llu files in %llu units, %d re-walk rounds, %llu records: kernel+counts "
+                "%.3f ms, records D2H %.3f ms, expand %.3f ms\n", (unsigned long long)nf, (unsigned long long)nu, rounds,
+                (unsigned long long)res.nrec, res.ms_kernel, res.ms_d2h, ms_since(t1));
     return SYDELTA_OK;
 }
 

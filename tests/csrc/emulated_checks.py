@@ -657,13 +657,14 @@ def batch_and_chunk_checks():
     for bs in (1024, 4096):
         # "0" / "1" / "auto": the classifier path (SYDELTA_FILE_WALK=0); "walk": the file
         # walk (K10), which a batch of >= 64 small files takes by default
-        for probe in ("0", "1", "auto", "walk"):
+        for probe in ("0", "1", "auto", "walk", "walk8"):  # walk8: segments of >= 8 blocks (SYDELTA_FILE_SEGS=8)
             os.environ["SYDELTA_FILE_WALK"] = "0"
-            if probe in ("auto", "walk"):
+            os.environ["SYDELTA_FILE_SEGS"] = "8" if probe == "walk8" else ""
+            if probe in ("auto", "walk", "walk8"):
                 os.environ.pop("SYDELTA_PROBE", None)
             else:
                 os.environ["SYDELTA_PROBE"] = probe
-            if probe == "walk":
+            if probe.startswith("walk"):
                 os.environ.pop("SYDELTA_FILE_WALK")
             nf = 80
             bases, srcs = [], []
@@ -714,6 +715,7 @@ def batch_and_chunk_checks():
             lib.sydelta_index_free(ix)
     os.environ.pop("SYDELTA_PROBE", None)
     os.environ.pop("SYDELTA_FILE_WALK", None)
+    os.environ.pop("SYDELTA_FILE_SEGS", None)
     # chunked: one file in 1/2/3/8 chunks, walks chained in order, parts appended
     for bs in (512, 4096):
         basis = O.synth_bytes(300 * bs + 77, 0x700)

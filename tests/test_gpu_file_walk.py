@@ -238,3 +238,39 @@ def test_chunk_walk_segments(gpu, oracle_c, monkeypatch, bs, nchunks):
     assert d.tuples() == exp
     monkeypatch.setenv("SYDELTA_CHUNK_WALK", "0")
     assert _chunk_walk(gpu, src, basis, bs, bounds).tuples() == exp
+
+
+@pytest.mark.parametrize("bs", [256, 4096])
+@pytest.mark.parametrize("segs", ["2", "5", "16"])
+def test_file_walk_in_segments(gpu, oracle_c, monkeypatch, bs, segs):
+    """Files cut into segments of >= 8 blocks (SYDELTA_FILE_SEGS): each segment walked from its
+    start; a Copy that crosses into the next segment is absorbed by cutting that segment's
+    leading literal run, or the segment is walked again from the exit.  Equal to the oracle."""
+    rng = random.Random(2000 + bs + int(segs))
+    pairs = _cases(rng, bs, 80)
+    monkeypatch.setenv("SYDELTA_FILE_SEGS", segs)
+    out, tot, prof = _batch(gpu, pairs, bs, "1", monkeypatch)
+    assert "k_walk_files" in prof
+    for i, ((src, basis), d) in enumerate(zip(pairs, out)):
+        assert d.tuples() == _oracle_ops(oracle_c, src, basis, bs), (bs, segs, i)
+    assert tot["literal_bytes"] == sum(d.stats["literal_bytes"] for d in out)
+
+
+def test_file_walk_c4_shape_few_files(gpu, oracle_c, monkeypatch):
+    """An 8-GPU rank's share of C4 (few 1 MiB files): the auto mode cuts each file into
+    segments (file_segs); every op list equals the oracle's."""
+    rng = random.Random(4405)
+    pairs = []
+    for f in range(96):
+        basis = O.synth_bytes(1 << 20, 0x5E1D0104 + f).tobytes()
+        s = bytearray(basis)
+        p = rng.randrange(len(s) + 1)
+        s[p:p] = bytes([rng.randrange(256)])
+        for _ in range(16):
+            s[rng.randrange(len(s))] ^= rng.randrange(1, 256)
+        pairs.append((bytes(s), basis))
+    monkeypatch.delenv("SYDELTA_FILE_SEGS", raising=False)
+    out, _, prof = _batch(gpu, pairs, 4096, "", monkeypatch)
+    assert "k_walk_files" in prof
+    for f, ((src, basis), d) in enumerate(zip(pairs, out)):
+        assert d.tuples() == _oracle_ops(oracle_c, src, basis, 4096), f
