@@ -1149,7 +1149,9 @@ def main():
                                 f"file-sharded x{world} (independent pairs per rank, no collective)"),
                 **({"files": args.files, "files_this_rank": len(files[0]), "callers_per_rank": max(1, len(c4_groups))}
                    if args.workload == "c4" else {}),
-                "walk": "device (K5b)" if args.device_walk else "host threads",
+                "walk": ("device (K10 per file / file segment)" if args.workload == "c4" else
+                         "device (K10 per chunk segment, two pipelined parts)" if args.workload == "c5" else
+                         "device (K5b)" if args.device_walk else "host threads"),
             },
             "pct_hbm_peak": round(value * GIB / 1e9 / HBM_PEAK_GBS * 100, 2),
             "roofline": roof,

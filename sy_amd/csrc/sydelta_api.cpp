@@ -645,15 +645,16 @@ hipError_t stream_after(hipStream_t to, hipStream_t from, int device) {
 // milliseconds.  Released by sydelta_trim.
 namespace {
 std::mutex g_mapped_mu;
-std::vector<PinnedHits> g_mapped;  // at most kMappedKeep
-constexpr size_t kMappedKeep = 4;
+std::vector<PinnedHits> g_mapped;  // at most kMappedKeep buffers and kMappedKeepBytes
+constexpr size_t kMappedKeep = 64, kMappedKeepBytes = (size_t)1 << 30;
 int take_mapped(size_t bytes, PinnedHits& out) {
     {
         std::lock_guard<std::mutex> lk(g_mapped_mu);
         size_t best = g_mapped.size();
         for (size_t i = 0; i < g_mapped.size(); ++i)
-            if (g_mapped[i].bytes >= bytes && (best == g_mapped.size() || g_mapped[i].bytes < g_mapped[best].bytes))
-                best = i;
+            if (g_mapped[i].bytes >= bytes && g_mapped[i].bytes <= 4 * bytes + (1u << 20) &&
+                (best == g_mapped.size() || g_mapped[i].bytes < g_mapped[best].bytes))
+                best = i;  // (a small request does not take a chunk walk's large buffer)
         if (best < g_mapped.size()) {
             out = g_mapped[best];
             g_mapped.erase(g_mapped.begin() + best);
@@ -674,7 +675,9 @@ void give_mapped(PinnedHits h) {  // h idle (its last use was synchronized)
     {
         std::lock_guard<std::mutex> lk(g_mapped_mu);
         g_mapped.push_back(h);
-        if (g_mapped.size() > kMappedKeep) {
+        size_t held = 0;
+        for (const PinnedHits& x : g_mapped) held += x.bytes;
+        if (g_mapped.size() > kMappedKeep || held > kMappedKeepBytes) {
             auto it = std::min_element(g_mapped.begin(), g_mapped.end(),
                                        [](const PinnedHits& a, const PinnedHits& b) { return a.bytes < b.bytes; });
             drop = *it;
@@ -2332,14 +2335,16 @@ static int run_walk(sydelta_index* ix, const uint8_t* base, const std::vector<Wa
     for (const WalkUnit& u : units) rec_total = std::max(rec_total, u.rec_off + 2 * ((u.end - u.entry) / ix->bs) + 4);
     // pinned: the unit table and the last sizes up; the counts down (over them, once uploaded)
     const size_t ubytes = sizeof(WalkUnit) * nu, lbytes = 8 * nf, fout_bytes = sizeof(WalkFileOut) * nu;
-    PinnedHits& ph = thread_pinned_hits();
-    if (int r = pinned_at_least(ph, std::max(ubytes + lbytes, fout_bytes + 16))) return r;
-    memcpy(ph.p, units.data(), ubytes);
-    memcpy(ph.p + ubytes, ix->last_size.data(), lbytes);
+    // one upload: the unit table, the last sizes and the zeroed record counter (+ the 16
+    // SYDELTA_PHASE_TIMING tick counters) -- ten concurrent callers' extra copies showed
     auto al = [](size_t v) { return (v + 255) & ~(size_t)255; };
-    // o_total: the record counter (8 B) and SYDELTA_PHASE_TIMING's 16 tick counters
-    const size_t o_units = 0, o_last = al(ubytes), o_fout = o_last + al(lbytes), o_total = o_fout + al(fout_bytes);
-    const size_t o_stage = o_total + 256, o_out = o_stage + al(sizeof(WalkRec) * rec_total);
+    const size_t o_units = 0, o_last = ubytes, o_total = o_last + lbytes, up = o_total + 136;
+    PinnedHits& ph = thread_pinned_hits();
+    if (int r = pinned_at_least(ph, std::max(up, fout_bytes + 16))) return r;
+    memcpy(ph.p, units.data(), ubytes);
+    memcpy(ph.p + o_last, ix->last_size.data(), lbytes);
+    memset(ph.p + o_total, 0, 136);
+    const size_t o_fout = al(up), o_stage = o_fout + al(fout_bytes), o_out = o_stage + al(sizeof(WalkRec) * rec_total);
     const size_t need = o_out + al(sizeof(WalkRec) * rec_total);
     DevScratch& sc = thread_walk_scratch(cur_dev);
     if (sc.bytes < need) {
@@ -2349,10 +2354,8 @@ static int run_walk(sydelta_index* ix, const uint8_t* base, const std::vector<Wa
         sc.bytes = need + need / 4;
     }
     uint8_t* D = (uint8_t*)sc.p;
-    HIP_TRY(hipMemcpyAsync(D + o_units, ph.p, ubytes, hipMemcpyHostToDevice, s));
-    HIP_TRY(hipMemcpyAsync(D + o_last, ph.p + ubytes, lbytes, hipMemcpyHostToDevice, s));
+    HIP_TRY(hipMemcpyAsync(D, ph.p, up, hipMemcpyHostToDevice, s));
     static const bool timing = getenv("SYDELTA_PHASE_TIMING") != nullptr;
-    HIP_TRY(hipMemsetAsync(D + o_total, 0, timing ? 8 + 128 : 8, s));
     WalkArgs a{};
     a.base = base;
     a.units = (const WalkUnit*)(D + o_units);
@@ -2474,7 +2477,17 @@ static int match_walk_files(sydelta_index* ix, const uint8_t* d_buf, const uint6
         explicit Walking(uint64_t k_) : k(k_), total(g_walking_files.fetch_add(k_) + k_) {}
         ~Walking() { g_walking_files.fetch_sub(k); }
     } walking(nf);
-    const uint64_t G = file_segs(walking.total), min_seg = (getenv("SYDELTA_FILE_SEGS") && *getenv("SYDELTA_FILE_SEGS")) ? 8 : 32;
+    // callers come and go between their signature, index and match calls: the peak of the
+    // last second stands for them (a heuristic; races only shift the segment count)
+    static std::atomic<uint64_t> peak{0};
+    static std::atomic<int64_t> peak_ms{0};
+    const int64_t now_ms = std::chrono::duration_cast<std::chrono::milliseconds>(
+                               std::chrono::steady_clock::now().time_since_epoch()).count();
+    if (walking.total >= peak.load() || now_ms - peak_ms.load() > 1000) {
+        peak.store(walking.total);
+        peak_ms.store(now_ms);
+    }
+    const uint64_t G = file_segs(std::max(walking.total, peak.load())), min_seg = (getenv("SYDELTA_FILE_SEGS") && *getenv("SYDELTA_FILE_SEGS")) ? 8 : 32;
     std::vector<WalkUnit> units;
     units.reserve(nf * G);
     std::vector<uint64_t> fu(nf + 1, 0);  // file f's units: [fu[f], fu[f+1])
