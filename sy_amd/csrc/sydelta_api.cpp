@@ -3540,6 +3540,17 @@ struct sydelta_chunk {
 // exit) differs is walked again from it (after a Copy that crosses the boundary).
 // SYDELTA_CHUNK_WALK=0, or SYDELTA_PROBE=0, keeps the classifier + host walk.
 namespace {
+// blocks per segment of the last part of a pipelined chunk (SYDELTA_CHUNK_SEG_LAST, default
+// 64: its waves finish sooner, and the last part's walk ends the pipeline)
+uint64_t chunk_seg_blocks();
+uint64_t chunk_seg_last_blocks() {
+    static const uint64_t v = [] {
+        const char* e = getenv("SYDELTA_CHUNK_SEG_LAST");
+        const uint64_t x = (e && *e) ? strtoull(e, nullptr, 10) : 64;
+        return (x >= 8 && x <= 1024 && (x & (x - 1)) == 0) ? std::min(x, chunk_seg_blocks()) : chunk_seg_blocks();
+    }();
+    return v;
+}
 // blocks per segment (SYDELTA_CHUNK_SEG overrides; a power of two from 8 to 1024)
 uint64_t chunk_seg_blocks() {
     static const uint64_t v = [] {
@@ -3558,11 +3569,12 @@ bool chunk_walk_ok(const sydelta_index* idx) {
 
 // The units of a chunk's walk from `from`: the segments of [from, c.p1), the last one final
 // when the file ends in the chunk.
-void chunk_units(const sydelta_chunk* ch, uint64_t from, std::vector<WalkUnit>& units) {
+// (appended to `units`, segments of seg_blocks blocks from the chunk start's grid;
+// record offsets continue from the last unit's)
+void chunk_units(const sydelta_chunk* ch, uint64_t from, std::vector<WalkUnit>& units, uint64_t seg_blocks = 0) {
     const Src& c = ch->C.src[0];
-    const uint64_t n = ch->C.n, seg = chunk_seg_blocks() * n;
-    units.clear();
-    uint64_t rec = 0;
+    const uint64_t n = ch->C.n, seg = (seg_blocks ? seg_blocks : chunk_seg_blocks()) * n;
+    uint64_t rec = units.empty() ? 0 : units.back().rec_off + 2 * ((units.back().end - units.back().entry) / n) + 4;
     const uint64_t lo = std::max(from, c.p0);
     uint64_t s0 = c.p0 + (lo > c.p0 ? (lo - c.p0) / seg * seg : 0);
     do {
@@ -3594,15 +3606,17 @@ int chunk_pipe_launch(sydelta_chunk* ch, uint64_t from, bool probe) {
     const Src& c = C.src[0];
     ChunkPipe& P = ch->pipe;
     const uint64_t n = C.n;
+    P.units.clear();
     chunk_units(ch, from, P.units);
-    const size_t nu = P.units.size();
-    uint64_t rec_total = 0;
-    for (const WalkUnit& u : P.units) rec_total = std::max(rec_total, u.rec_off + 2 * ((u.end - u.entry) / n) + 4);
-    if (rec_total >= (1ull << 32)) return fail(SYDELTA_E_INVAL, "chunk too large for one walk");
+    size_t nu = P.units.size();
     const uint64_t np = probe ? c.nblk : 0;
     const int K = probe ? chunk_pipe_parts(nu) : 1;
     P.ub.resize(K + 1);
     for (int j = 0; j <= K; ++j) P.ub[j] = (uint32_t)(nu * j / K);
+    // two parts: 70 % / 30 % (the second part's hashing hides the first part's walk, and its
+    // own walk, which ends the pipeline, is the shorter: 4.11-4.12 ms per step at C5 against
+    // 4.26-4.43 for halves, `profiles/r05zs_*`, `r05zt_*`)
+    if (K == 2) P.ub[1] = (uint32_t)std::min<uint64_t>(nu - 1, std::max<uint64_t>(1, nu * 7 / 10));
     if (const char* wv = getenv("SYDELTA_CHUNK_PIPE_W")) {  // A/B: part sizes by weights "w0,w1,..."
         std::vector<double> wt;
         for (const char* q = wv; *q;) {
@@ -3619,6 +3633,18 @@ int chunk_pipe_launch(sydelta_chunk* ch, uint64_t from, bool probe) {
             }
         }
     }
+    // the last part, whose walk ends the pipeline, in shorter segments (its waves finish sooner)
+    const uint64_t seg_last = chunk_seg_last_blocks();
+    if (K >= 2 && seg_last < chunk_seg_blocks()) {
+        const uint64_t split = P.units[P.ub[K - 1]].entry;
+        P.units.resize(P.ub[K - 1]);
+        chunk_units(ch, split, P.units, seg_last);
+        nu = P.units.size();
+        P.ub[K] = (uint32_t)nu;
+    }
+    uint64_t rec_total = 0;
+    for (const WalkUnit& u : P.units) rec_total = std::max(rec_total, u.rec_off + 2 * ((u.end - u.entry) / n) + 4);
+    if (rec_total >= (1ull << 32)) return fail(SYDELTA_E_INVAL, "chunk too large for one walk");
     auto al = [](size_t v) { return (v + 255) & ~(size_t)255; };
     const size_t o_last = al(sizeof(WalkUnit) * nu), o_total = o_last + 256, o_jobs = o_total + 256;
     const size_t o_out = o_jobs + al(sizeof(ProbeJob) * K), o_pw = o_out + al(4 * np), o_pst = o_pw + al(4 * np);
@@ -3642,13 +3668,19 @@ int chunk_pipe_launch(sydelta_chunk* ch, uint64_t from, bool probe) {
     // the unit table, probe jobs and last size up, from the mapped buffer (it outlives the copies)
     memcpy(H + h_units, P.units.data(), sizeof(WalkUnit) * nu);
     ProbeJob* jobs = (ProbeJob*)(H + h_jobs);
-    for (int j = 0; j < K; ++j) jobs[j] = ProbeJob{c.off, c.kb + (uint64_t)P.ub[j] * chunk_seg_blocks(), 0, 0, 0};
+    auto part_block = [&](int j) -> uint64_t {  // part j's first block (relative to the chunk's)
+        return j < K ? (P.units[P.ub[j]].entry - c.p0) / n : np;
+    };
+    for (int j = 0; j < K; ++j) jobs[j] = ProbeJob{c.off, c.kb + part_block(j), 0, 0, 0};
     *(uint64_t*)(H + h_last) = C.ix->last_size[0];
     HIP_TRY(hipMemcpyAsync(D, H + h_units, sizeof(WalkUnit) * nu, hipMemcpyHostToDevice, C.s));
     HIP_TRY(hipMemcpyAsync(D + o_last, H + h_last, 8, hipMemcpyHostToDevice, C.s));
     if (probe) HIP_TRY(hipMemcpyAsync(D + o_jobs, jobs, sizeof(ProbeJob) * K, hipMemcpyHostToDevice, C.s));
     HIP_TRY(hipMemsetAsync(D + o_total, 0, 8, C.s));
-    hipStream_t s2[2] = {thread_walk_stream(P.device, 0), thread_walk_stream(P.device, 1)};
+    // (the second: the aux stream, idle once the index is built; a fifth stream would share
+    // one of the process's four hardware queues with another and serialize behind it)
+    hipStream_t s2[2] = {thread_walk_stream(P.device, 0),
+                         getenv("SYDELTA_WALK_STREAMS2") ? thread_walk_stream(P.device, 1) : thread_aux_stream(P.device)};
     hipEvent_t hand = handoff_event(P.device);
     if (!s2[0] || !s2[1] || !hand) return fail(SYDELTA_E_OOM, "no stream or event for the chunk walk");
     const bool fast = ((uintptr_t)(C.base + c.off) & 15) == 0;
@@ -3678,8 +3710,7 @@ int chunk_pipe_launch(sydelta_chunk* ch, uint64_t from, bool probe) {
     a.total = (unsigned long long*)(D + o_total);  // one counter: the sub-ranges' launches run in order
     a.ticks = nullptr;
     auto probe_part = [&](int j, int phases) -> hipError_t {
-        const uint64_t b0 = (uint64_t)P.ub[j] * chunk_seg_blocks();
-        const uint64_t b1 = std::min<uint64_t>((uint64_t)P.ub[j + 1] * chunk_seg_blocks(), np);
+        const uint64_t b0 = part_block(j), b1 = std::min<uint64_t>(part_block(j + 1), np);
         return launch_probe(C.base, (const ProbeJob*)(D + o_jobs) + j, 1, b1 - b0, 1, (uint32_t)n, fast, ix,
                             d_pw + b0, d_pst + b0, d_out + b0, C.s, C.prof, phases);
     };

@@ -54,8 +54,10 @@ def test_host_logic_on_emulated_device():
     if shutil.which("g++") is None or not os.path.exists("/opt/rocm/include/hip/hip_runtime_api.h"):
         pytest.skip("needs g++ and the HIP headers")
     lib = _build()
+    # SYDELTA_CHUNK_SEG_LAST: the pipelined chunk checks' last part in 16-block segments
     r = subprocess.run([sys.executable, os.path.join(ROOT, "tests", "csrc", "emulated_checks.py"), ROOT, lib],
-                       capture_output=True, text=True, timeout=1100, cwd="/tmp")
+                       capture_output=True, text=True, timeout=1100, cwd="/tmp",
+                       env=dict(os.environ, SYDELTA_CHUNK_SEG_LAST="16"))
     assert r.returncode == 0, (r.stdout[-2000:], r.stderr[-6000:])
     assert "emulated host checks ok" in r.stdout
 
