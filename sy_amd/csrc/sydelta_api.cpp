@@ -640,48 +640,56 @@ hipError_t stream_after(hipStream_t to, hipStream_t from, int device) {
 }
 }  // namespace
 
-// Host-mapped pinned buffers of finished chunk walks (the records the walk kernel writes
-// straight into host memory): kept for the next chunk, since pinning tens of MB costs
-// milliseconds.  Released by sydelta_trim.
+// Pinned host buffers of finished chunk walks and indexes, kept for the next ones (pinning
+// tens of MB costs milliseconds), of two kinds: kMapped, coherent and mapped, which kernels
+// write and the host then reads (a chunk walk's per-unit results and records); kStage,
+// ordinary pinned memory (cached by the CPU) the host fills and the DMA engines read (unit
+// tables, file tables: filling coherent memory, which the CPU does not cache, held a chunk's
+// launch ~0.1 ms, `profiles/r05zs_c5_w70_step_timeline.txt`).  Released by sydelta_trim.
 namespace {
+enum PinKind { kMapped = 0, kStage = 1 };
 std::mutex g_mapped_mu;
-std::vector<PinnedHits> g_mapped;  // at most kMappedKeep buffers and kMappedKeepBytes
+std::vector<PinnedHits> g_mapped[2];  // per kind: at most kMappedKeep buffers and kMappedKeepBytes
 constexpr size_t kMappedKeep = 64, kMappedKeepBytes = (size_t)1 << 30;
-int take_mapped(size_t bytes, PinnedHits& out) {
+int take_mapped(size_t bytes, PinnedHits& out, PinKind kind = kMapped) {
     {
         std::lock_guard<std::mutex> lk(g_mapped_mu);
-        size_t best = g_mapped.size();
-        for (size_t i = 0; i < g_mapped.size(); ++i)
-            if (g_mapped[i].bytes >= bytes && g_mapped[i].bytes <= 4 * bytes + (1u << 20) &&
-                (best == g_mapped.size() || g_mapped[i].bytes < g_mapped[best].bytes))
+        std::vector<PinnedHits>& g = g_mapped[kind];
+        size_t best = g.size();
+        for (size_t i = 0; i < g.size(); ++i)
+            if (g[i].bytes >= bytes && g[i].bytes <= 4 * bytes + (1u << 20) &&
+                (best == g.size() || g[i].bytes < g[best].bytes))
                 best = i;  // (a small request does not take a chunk walk's large buffer)
-        if (best < g_mapped.size()) {
-            out = g_mapped[best];
-            g_mapped.erase(g_mapped.begin() + best);
+        if (best < g.size()) {
+            out = g[best];
+            g.erase(g.begin() + best);
             return SYDELTA_OK;
         }
     }
     out = PinnedHits();
     const size_t want = bytes + bytes / 4;
     static const bool nc = getenv("SYDELTA_MAPPED_NC") != nullptr;  // A/B: non-coherent mapping
-    HIP_TRY(hipHostMalloc((void**)&out.p, want,
-                          hipHostMallocMapped | hipHostMallocPortable | (nc ? hipHostMallocNonCoherent : hipHostMallocCoherent)));
+    const unsigned flags = kind == kStage ? hipHostMallocDefault
+                                          : hipHostMallocMapped | hipHostMallocPortable |
+                                                (nc ? hipHostMallocNonCoherent : hipHostMallocCoherent);
+    HIP_TRY(hipHostMalloc((void**)&out.p, want, flags));
     out.bytes = want;
     return SYDELTA_OK;
 }
-void give_mapped(PinnedHits h) {  // h idle (its last use was synchronized)
+void give_mapped(PinnedHits h, PinKind kind = kMapped) {  // h idle (its last use was synchronized)
     if (!h.p) return;
     PinnedHits drop;
     {
         std::lock_guard<std::mutex> lk(g_mapped_mu);
-        g_mapped.push_back(h);
+        std::vector<PinnedHits>& g = g_mapped[kind];
+        g.push_back(h);
         size_t held = 0;
-        for (const PinnedHits& x : g_mapped) held += x.bytes;
-        if (g_mapped.size() > kMappedKeep || held > kMappedKeepBytes) {
-            auto it = std::min_element(g_mapped.begin(), g_mapped.end(),
+        for (const PinnedHits& x : g) held += x.bytes;
+        if (g.size() > kMappedKeep || held > kMappedKeepBytes) {
+            auto it = std::min_element(g.begin(), g.end(),
                                        [](const PinnedHits& a, const PinnedHits& b) { return a.bytes < b.bytes; });
             drop = *it;
-            g_mapped.erase(it);
+            g.erase(it);
         }
     }
     if (drop.p) (void)hipHostFree(drop.p);
@@ -690,7 +698,10 @@ void release_mapped() {
     std::vector<PinnedHits> v;
     {
         std::lock_guard<std::mutex> lk(g_mapped_mu);
-        v.swap(g_mapped);
+        for (auto& g : g_mapped) {
+            v.insert(v.end(), g.begin(), g.end());
+            g.clear();
+        }
     }
     for (auto& h : v) (void)hipHostFree(h.p);
 }
@@ -724,7 +735,7 @@ static void index_release(sydelta_index* x) {
     if (x->rib_ev) (void)hipEventDestroy(x->rib_ev);
     // the build has uploaded the file tables from `stage` (done long before, as a rule)
     if (x->ready) (void)hipEventSynchronize(x->ready);
-    give_mapped(x->stage);
+    give_mapped(x->stage, kStage);
     x->stage = PinnedHits();
     if (x->d_pool) {
         KeptPool old;
@@ -1037,7 +1048,7 @@ static int index_create_impl(int device, const uint32_t* weak, const uint64_t* s
     static const bool index_sync = getenv("SYDELTA_INDEX_SYNC") && getenv("SYDELTA_INDEX_SYNC")[0] == '1';
     if (arrays_on_device && !index_sync) {
         const size_t fb = sizeof(FileIx) * nfiles, tb = ((fb + 15) & ~(size_t)15) + 8 * (nfiles + 1);
-        if (int r = take_mapped(tb, x->stage)) return r;
+        if (int r = take_mapped(tb, x->stage, kStage)) return r;
         memcpy(x->stage.p, ix.files.data(), fb);
         memcpy(x->stage.p + ((fb + 15) & ~(size_t)15), x->fblk.data(), 8 * (nfiles + 1));
         HIP_TRY(hipMemcpyAsync(ix.d_files, x->stage.p, fb, hipMemcpyHostToDevice, s));
@@ -3503,7 +3514,8 @@ struct ChunkPipe {
     std::vector<hipEvent_t> done;  // per sub-range: its walk finished (results readable)
     void* dmem = nullptr;          // the unit table and the probe's results (device)
     hipStream_t ds = nullptr;      // dmem's stream (the caller's)
-    PinnedHits pin;                // host-mapped: per-unit results, records, upload staging
+    PinnedHits pin;                // host-mapped (kMapped): per-unit results, records
+    PinnedHits stage;              // the uploads' source (kStage)
     const WalkFileOut* fout = nullptr;
     const WalkRec* rec = nullptr;
     const uint32_t* ahit = nullptr;  // the probe's results (device; NULL: no probe)
@@ -3518,6 +3530,8 @@ struct ChunkPipe {
         dmem = nullptr;
         give_mapped(pin);
         pin = PinnedHits();
+        give_mapped(stage, kStage);
+        stage = PinnedHits();
         on = false;
     }
     ~ChunkPipe() { release(); }
@@ -3646,17 +3660,23 @@ int chunk_pipe_launch(sydelta_chunk* ch, uint64_t from, bool probe) {
     for (const WalkUnit& u : P.units) rec_total = std::max(rec_total, u.rec_off + 2 * ((u.end - u.entry) / n) + 4);
     if (rec_total >= (1ull << 32)) return fail(SYDELTA_E_INVAL, "chunk too large for one walk");
     auto al = [](size_t v) { return (v + 255) & ~(size_t)255; };
-    const size_t o_last = al(sizeof(WalkUnit) * nu), o_total = o_last + 256, o_jobs = o_total + 256;
-    const size_t o_out = o_jobs + al(sizeof(ProbeJob) * K), o_pw = o_out + al(4 * np), o_pst = o_pw + al(4 * np);
+    // device: the probe jobs, the last size and the record counter (uploaded first, for the
+    // hashing), the unit table (uploaded once the first hashing is queued), the probe's
+    // results, the staged records; host: the per-unit results and the compacted records
+    // (kMapped), the uploads' source (kStage, same offsets as the device's)
+    const size_t o_jobs = 0, o_last = al(sizeof(ProbeJob) * K), o_total = o_last + 8, o_units = al(o_total + 8);
+    const size_t ubytes = sizeof(WalkUnit) * nu;
+    const size_t o_out = o_units + al(ubytes), o_pw = o_out + al(4 * np), o_pst = o_pw + al(4 * np);
     const size_t o_stage = o_pst + al(8 * np), dneed = o_stage + al(sizeof(WalkRec) * rec_total);
-    const size_t h_rec = al(sizeof(WalkFileOut) * nu), h_units = h_rec + al(sizeof(WalkRec) * rec_total);
-    const size_t h_jobs = h_units + al(sizeof(WalkUnit) * nu), h_last = h_jobs + al(sizeof(ProbeJob) * K);
+    const size_t h_rec = al(sizeof(WalkFileOut) * nu), h_end = h_rec + al(sizeof(WalkRec) * rec_total);
     P.on = true;  // release() undoes whatever is set below
     P.device = C.ix->device;
     P.ds = C.s;
-    if (int r = take_mapped(h_last + 256, P.pin)) return r;
+    if (int r = take_mapped(h_end, P.pin)) return r;
+    if (int r = take_mapped(o_units + ubytes, P.stage, kStage)) return r;
     HIP_TRY(dev_malloc_async(&P.dmem, dneed, C.s));
     uint8_t* H = P.pin.p;
+    uint8_t* S = P.stage.p;
     uint8_t* D = (uint8_t*)P.dmem;
     P.fout = (const WalkFileOut*)H;
     P.rec = (const WalkRec*)(H + h_rec);
@@ -3665,18 +3685,23 @@ int chunk_pipe_launch(sydelta_chunk* ch, uint64_t from, bool probe) {
     uint64_t* d_pst = (uint64_t*)(D + o_pst);
     P.ahit = probe ? d_out : nullptr;
     P.apw = probe ? d_pw : nullptr;
-    // the unit table, probe jobs and last size up, from the mapped buffer (it outlives the copies)
-    memcpy(H + h_units, P.units.data(), sizeof(WalkUnit) * nu);
-    ProbeJob* jobs = (ProbeJob*)(H + h_jobs);
+    // the jobs, the last size and the zeroed counter up (the staging buffer outlives the copies)
+    ProbeJob* jobs = (ProbeJob*)(S + o_jobs);
     auto part_block = [&](int j) -> uint64_t {  // part j's first block (relative to the chunk's)
         return j < K ? (P.units[P.ub[j]].entry - c.p0) / n : np;
     };
     for (int j = 0; j < K; ++j) jobs[j] = ProbeJob{c.off, c.kb + part_block(j), 0, 0, 0};
-    *(uint64_t*)(H + h_last) = C.ix->last_size[0];
-    HIP_TRY(hipMemcpyAsync(D, H + h_units, sizeof(WalkUnit) * nu, hipMemcpyHostToDevice, C.s));
-    HIP_TRY(hipMemcpyAsync(D + o_last, H + h_last, 8, hipMemcpyHostToDevice, C.s));
-    if (probe) HIP_TRY(hipMemcpyAsync(D + o_jobs, jobs, sizeof(ProbeJob) * K, hipMemcpyHostToDevice, C.s));
-    HIP_TRY(hipMemsetAsync(D + o_total, 0, 8, C.s));
+    *(uint64_t*)(S + o_last) = C.ix->last_size[0];
+    *(uint64_t*)(S + o_total) = 0;
+    HIP_TRY(hipMemcpyAsync(D, S, o_total + 8, hipMemcpyHostToDevice, C.s));
+    bool units_up = false;
+    auto upload_units = [&]() -> int {
+        if (units_up) return SYDELTA_OK;
+        units_up = true;
+        memcpy(S + o_units, P.units.data(), ubytes);
+        HIP_TRY(hipMemcpyAsync(D + o_units, S + o_units, ubytes, hipMemcpyHostToDevice, C.s));
+        return SYDELTA_OK;
+    };
     // (the second: the aux stream, idle once the index is built; a fifth stream would share
     // one of the process's four hardware queues with another and serialize behind it)
     hipStream_t s2[2] = {thread_walk_stream(P.device, 0),
@@ -3719,6 +3744,7 @@ int chunk_pipe_launch(sydelta_chunk* ch, uint64_t from, bool probe) {
     // walked on the aux stream while the next sub-range is hashed
     for (int j = 0; j < K; ++j) {
         if (probe) HIP_TRY(probe_part(j, 1));
+        if (int r = upload_units()) return r;  // after the first hashing is queued
         if (j == 0) HIP_TRY(index_wait(C.ix, C.s));
         if (probe) HIP_TRY(probe_part(j, 2));
         hipStream_t sw = s2[j & 1];
@@ -3727,7 +3753,7 @@ int chunk_pipe_launch(sydelta_chunk* ch, uint64_t from, bool probe) {
         hipEvent_t e = take_event(P.device);
         if (!e) return fail(SYDELTA_E_OOM, "no event for the chunk walk");
         P.done.push_back(e);
-        a.units = (const WalkUnit*)D + P.ub[j];
+        a.units = (const WalkUnit*)(D + o_units) + P.ub[j];
         a.nunits = P.ub[j + 1] - P.ub[j];
         a.fout = (WalkFileOut*)P.fout + P.ub[j];
         HIP_TRY(launch_walk_files(a, sw, C.prof));

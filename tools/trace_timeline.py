@@ -17,7 +17,8 @@ def main():
     with open(a.csv) as f:
         for r in csv.DictReader(f):
             name = r.get("Kernel_Name", "")
-            rows.append((int(r["Start_Timestamp"]), int(r["End_Timestamp"]), name.split("(")[0][:60]))
+            rows.append((int(r["Start_Timestamp"]), int(r["End_Timestamp"]),
+                         f"q{r.get('Queue_Id', '?')} s{r.get('Stream_Id', '?')} " + name.split("(")[0][:60]))
     rows.sort()
     starts = [i for i, r in enumerate(rows) if a.first in r[2]]
     i0 = starts[a.step]
