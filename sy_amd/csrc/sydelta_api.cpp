@@ -485,6 +485,11 @@ static uint32_t ceil_log2(uint64_t v) {
 // ---------------------------------------------------------------------------
 // signature
 // ---------------------------------------------------------------------------
+namespace {
+int pinned_at_least(PinnedHits& h, size_t bytes);                              // (below)
+int upload_staged(void* d_dst, const void* src, size_t bytes, hipStream_t s);  // (below)
+}  // namespace
+
 extern "C" int sydelta_signature_device(int device, const uint8_t* d_buf, uint64_t len, uint64_t block_size,
                                         uint32_t* d_weak, uint64_t* d_strong, void* stream) try {
     if (block_size == 0) return fail(SYDELTA_E_INVAL, "block_size must be > 0");
@@ -534,7 +539,10 @@ extern "C" int sydelta_signature_batch_device(int device, const uint8_t* d_buf, 
         for (auto* v : {&aoff, &agb, &apfx, &loff, &llen, &lidx}) t.insert(t.end(), v->begin(), v->end());
         uint64_t* d_t = nullptr;
         HIP_TRY(dev_malloc_async((void**)&d_t, 8 * t.size(), s));
-        HIP_TRY(hipMemcpyAsync(d_t, t.data(), 8 * t.size(), hipMemcpyHostToDevice, s));
+        if (int r = upload_staged(d_t, t.data(), 8 * t.size(), s)) {
+            (void)hipFreeAsync(d_t, s);
+            return r;
+        }
         const uint64_t* p = d_t;
         const uint64_t* d_aoff = p; p += nact;
         const uint64_t* d_agb = p; p += nact;
@@ -547,20 +555,27 @@ extern "C" int sydelta_signature_batch_device(int device, const uint8_t* d_buf, 
                                                    d_lidx, npart, block_size, d_weak, d_strong, s, cp.get());
         (void)hipFreeAsync(d_t, s);
         HIP_TRY(e);
-        HIP_TRY(hipStreamSynchronize(s));  // the host table must outlive the copy
+        if (!stream) HIP_TRY(hipStreamSynchronize(s));  // the library's stream: done on return
         return SYDELTA_OK;
     }
     uint64_t* d_meta = nullptr;
     HIP_TRY(dev_malloc_async((void**)&d_meta, sizeof(uint64_t) * (3 * nfiles + 1), s));
-    HIP_TRY(hipMemcpyAsync(d_meta, off, 8 * nfiles, hipMemcpyHostToDevice, s));
-    HIP_TRY(hipMemcpyAsync(d_meta + nfiles, len, 8 * nfiles, hipMemcpyHostToDevice, s));
-    HIP_TRY(hipMemcpyAsync(d_meta + 2 * nfiles, fblk.data(), 8 * (nfiles + 1), hipMemcpyHostToDevice, s));
+    {
+        std::vector<uint64_t> meta(3 * nfiles + 1);
+        std::copy(off, off + nfiles, meta.begin());
+        std::copy(len, len + nfiles, meta.begin() + nfiles);
+        std::copy(fblk.begin(), fblk.end(), meta.begin() + 2 * nfiles);
+        if (int r = upload_staged(d_meta, meta.data(), 8 * meta.size(), s)) {
+            (void)hipFreeAsync(d_meta, s);
+            return r;
+        }
+    }
     CallProf cp;
     hipError_t e = launch_signature_batch(d_buf, d_meta, d_meta + nfiles, d_meta + 2 * nfiles, nfiles, block_size,
                                           total, d_weak, d_strong, s, cp.get());
     (void)hipFreeAsync(d_meta, s);
     HIP_TRY(e);
-    HIP_TRY(hipStreamSynchronize(s));  // the host segment table must outlive the copies
+    if (!stream) HIP_TRY(hipStreamSynchronize(s));  // the library's stream: done on return
     return SYDELTA_OK;
 } catch (...) {
     return sydelta::host_exception();
@@ -793,6 +808,12 @@ struct ThreadScratch {
     PinnedHits seg_pin;    // Classifier::scan's segment table
     PinnedHits probe_pin;  // Classifier::probe's results
     PinnedHits phase_pin;  // Classifier::phase_probe's results
+    // upload_staged's ring: pinned copies of small host tables, each reused once the copy
+    // that read it (its event) has run
+    PinnedHits up[4];
+    hipEvent_t up_ev[4] = {nullptr, nullptr, nullptr, nullptr};
+    int up_dev[4] = {0, 0, 0, 0};
+    unsigned up_next = 0;
 };
 std::mutex& scratch_mu() {
     static std::mutex* m = new std::mutex();  // never destroyed (thread exits after static teardown)
@@ -827,6 +848,15 @@ void release_scratch(ThreadScratch& t) {
     for (PinnedHits* h : {&t.pinned, &t.seg_pin, &t.probe_pin, &t.phase_pin}) {
         if (h->p) (void)hipHostFree(h->p);
         *h = PinnedHits();
+    }
+    for (int i = 0; i < 4; ++i) {
+        if (t.up_ev[i] && hipSetDevice(t.up_dev[i]) == hipSuccess) {
+            (void)hipEventSynchronize(t.up_ev[i]);
+            (void)hipEventDestroy(t.up_ev[i]);
+        }
+        t.up_ev[i] = nullptr;
+        if (t.up[i].p) (void)hipHostFree(t.up[i].p);
+        t.up[i] = PinnedHits();
     }
 }
 
@@ -870,6 +900,35 @@ namespace {
 PinnedHits& thread_seg_pin() { return thread_scratch().seg_pin; }
 PinnedHits& thread_probe_pin() { return thread_scratch().probe_pin; }
 PinnedHits& thread_phase_pin() { return thread_scratch().phase_pin; }
+// Copy `bytes` of host memory to d_dst in s's order without waiting for the copy: through a
+// slot of the calling thread's pinned ring (a pageable source would have to outlive the
+// copy, i.e. a stream synchronisation).  The current device is the stream's.
+int upload_staged(void* d_dst, const void* src, size_t bytes, hipStream_t s) {
+    if (!bytes) return SYDELTA_OK;
+    ScratchHold hold;
+    ThreadScratch& t = thread_scratch();
+    const unsigned i = t.up_next++ & 3;
+    int dev = 0;
+    HIP_TRY(hipGetDevice(&dev));
+    if (t.up_ev[i]) {
+        HIP_TRY(hipEventSynchronize(t.up_ev[i]));  // the slot's previous copy (long done, as a rule)
+        if (t.up_dev[i] != dev) {
+            DeviceScope keep;
+            (void)hipSetDevice(t.up_dev[i]);
+            (void)hipEventDestroy(t.up_ev[i]);
+            t.up_ev[i] = nullptr;
+        }
+    }
+    if (!t.up_ev[i]) {
+        HIP_TRY(hipEventCreateWithFlags(&t.up_ev[i], hipEventDisableTiming));
+        t.up_dev[i] = dev;
+    }
+    if (int r = pinned_at_least(t.up[i], bytes)) return r;
+    memcpy(t.up[i].p, src, bytes);
+    HIP_TRY(hipMemcpyAsync(d_dst, t.up[i].p, bytes, hipMemcpyHostToDevice, s));
+    HIP_TRY(hipEventRecord(t.up_ev[i], s));
+    return SYDELTA_OK;
+}
 // a pinned host buffer of at least `bytes` (grown by a quarter; the previous call on this
 // thread synchronized the streams that used it)
 int pinned_at_least(PinnedHits& h, size_t bytes) {
@@ -2574,8 +2633,11 @@ static int match_walk_files(sydelta_index* ix, const uint8_t* d_buf, const uint6
             }
         }
     }
-    // each file's records into its op array (recycled arrays: no page faults)
-    const int nthr = nf >= 64 ? walk_threads() : 1;
+    // each file's records into its op array (recycled arrays: no page faults), on the host
+    // pool and the caller (SYDELTA_ASM_THREADS overrides)
+    static const int asm_threads = getenv("SYDELTA_ASM_THREADS") ? std::max(1, atoi(getenv("SYDELTA_ASM_THREADS")))
+                                                                   : walk::HostPool::get().size() + 1;
+    const int nthr = nf >= 64 ? (int)std::min<uint64_t>(asm_threads, (nf + 63) / 64) : 1;
     std::atomic<uint64_t> next{0};
     std::vector<sydelta_match_stats> part(nthr);
     auto worker = [&](int t) {
