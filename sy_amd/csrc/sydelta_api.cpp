@@ -808,6 +808,7 @@ struct ThreadScratch {
     PinnedHits seg_pin;    // Classifier::scan's segment table
     PinnedHits probe_pin;  // Classifier::probe's results
     PinnedHits phase_pin;  // Classifier::phase_probe's results
+    PinnedHits walk_map;   // run_walk's results: coherent, mapped (the walk kernel writes it)
     // upload_staged's ring: pinned copies of small host tables, each reused once the copy
     // that read it (its event) has run
     PinnedHits up[4];
@@ -849,6 +850,8 @@ void release_scratch(ThreadScratch& t) {
         if (h->p) (void)hipHostFree(h->p);
         *h = PinnedHits();
     }
+    if (t.walk_map.p) (void)hipHostFree(t.walk_map.p);
+    t.walk_map = PinnedHits();
     for (int i = 0; i < 4; ++i) {
         if (t.up_ev[i] && hipSetDevice(t.up_dev[i]) == hipSuccess) {
             (void)hipEventSynchronize(t.up_ev[i]);
@@ -900,6 +903,7 @@ namespace {
 PinnedHits& thread_seg_pin() { return thread_scratch().seg_pin; }
 PinnedHits& thread_probe_pin() { return thread_scratch().probe_pin; }
 PinnedHits& thread_phase_pin() { return thread_scratch().phase_pin; }
+PinnedHits& thread_walk_map() { return thread_scratch().walk_map; }
 // Copy `bytes` of host memory to d_dst in s's order without waiting for the copy: through a
 // slot of the calling thread's pinned ring (a pageable source would have to outlive the
 // copy, i.e. a stream synchronisation).  The current device is the stream's.
@@ -2414,8 +2418,22 @@ static int run_walk(sydelta_index* ix, const uint8_t* base, const std::vector<Wa
     memcpy(ph.p, units.data(), ubytes);
     memcpy(ph.p + o_last, ix->last_size.data(), lbytes);
     memset(ph.p + o_total, 0, 136);
-    const size_t o_fout = al(up), o_stage = o_fout + al(fout_bytes), o_out = o_stage + al(sizeof(WalkRec) * rec_total);
-    const size_t need = o_out + al(sizeof(WalkRec) * rec_total);
+    // device: the upload, the staged records; host (coherent, mapped; the thread's, kept): the
+    // per-unit results and the compacted records, which the kernel writes there directly --
+    // one stream synchronisation, no D2H round trips
+    const size_t o_stage = al(up), need = o_stage + al(sizeof(WalkRec) * rec_total);
+    const size_t m_rec = al(fout_bytes), m_need = m_rec + sizeof(WalkRec) * rec_total;
+    PinnedHits& wm = thread_walk_map();
+    if (wm.bytes < m_need) {
+        if (wm.p) {
+            HIP_TRY(hipStreamSynchronize(s));  // (the previous call on this thread synchronized its walk)
+            (void)hipHostFree(wm.p);
+        }
+        wm = PinnedHits();
+        const size_t want = m_need + m_need / 4;
+        HIP_TRY(hipHostMalloc((void**)&wm.p, want, hipHostMallocMapped | hipHostMallocPortable | hipHostMallocCoherent));
+        wm.bytes = want;
+    }
     DevScratch& sc = thread_walk_scratch(cur_dev);
     if (sc.bytes < need) {
         if (sc.p) (void)hipFreeAsync(sc.p, s);
@@ -2446,9 +2464,13 @@ static int run_walk(sydelta_index* ix, const uint8_t* base, const std::vector<Wa
     a.strong = ix->d_strong;
     a.ahit = ahit;
     a.apw = apw;
+    // SYDELTA_WALK_D2H=1 (A/B): results in device memory, copied down in two round trips
+    static const bool d2h = getenv("SYDELTA_WALK_D2H") && getenv("SYDELTA_WALK_D2H")[0] == '1';
+    uint8_t* dres = nullptr;
+    if (d2h) HIP_TRY(dev_malloc_async((void**)&dres, m_need + 256, s));
     a.stage = (WalkRec*)(D + o_stage);
-    a.out = (WalkRec*)(D + o_out);
-    a.fout = (WalkFileOut*)(D + o_fout);
+    a.out = (WalkRec*)((d2h ? dres : wm.p) + m_rec);
+    a.fout = (WalkFileOut*)(d2h ? dres : wm.p);
     a.total = (unsigned long long*)(D + o_total);
     a.ticks = timing ? a.total + 1 : nullptr;
     HIP_TRY(launch_walk_files(a, s, prof));
@@ -2460,22 +2482,26 @@ static int run_walk(sydelta_index* ix, const uint8_t* base, const std::vector<Wa
                 "lookup %llu stage %llu roll %llu verify %llu out %llu | passes %llu windows %llu rolls %llu "
                 "verify batches %llu\n", tk[0], tk[1], tk[2], tk[3], tk[4], tk[5], tk[6], tk[8], tk[9], tk[10], tk[11]);
     }
-    // the unit table in ph is dead once the upload ran: the counts come back over it
-    HIP_TRY(hipMemcpyAsync(ph.p, a.fout, fout_bytes, hipMemcpyDeviceToHost, s));
-    HIP_TRY(hipMemcpyAsync(ph.p + fout_bytes, a.total, 8, hipMemcpyDeviceToHost, s));
+    if (d2h) {
+        HIP_TRY(hipMemcpyAsync(wm.p, dres, fout_bytes, hipMemcpyDeviceToHost, s));
+        HIP_TRY(hipMemcpyAsync(wm.p + fout_bytes, a.total, 8, hipMemcpyDeviceToHost, s));
+        HIP_TRY(hipStreamSynchronize(s));
+        const uint64_t nr = *(const uint64_t*)(wm.p + fout_bytes);
+        if (nr > rec_total) return fail(SYDELTA_E_KERNEL, "walk: record count past the capacity");
+        if (nr) HIP_TRY(hipMemcpyAsync(wm.p + m_rec, dres + m_rec, sizeof(WalkRec) * nr, hipMemcpyDeviceToHost, s));
+        (void)hipFreeAsync(dres, s);
+    }
     HIP_TRY(hipStreamSynchronize(s));
     res.ms_kernel = ms_since(t0);
-    const uint64_t nrec = *(const uint64_t*)(ph.p + fout_bytes);
-    if (nrec > rec_total)
-        return fail(SYDELTA_E_KERNEL, "walk: %llu records (capacity %llu)", (unsigned long long)nrec,
-                    (unsigned long long)rec_total);
-    res.out.assign((const WalkFileOut*)ph.p, (const WalkFileOut*)ph.p + nu);
-    if (int r = pinned_at_least(ph, sizeof(WalkRec) * nrec + 16)) return r;
-    if (nrec) {
-        HIP_TRY(hipMemcpyAsync(ph.p, a.out, sizeof(WalkRec) * nrec, hipMemcpyDeviceToHost, s));
-        HIP_TRY(hipStreamSynchronize(s));
+    res.out.assign((const WalkFileOut*)wm.p, (const WalkFileOut*)wm.p + nu);
+    uint64_t nrec = 0;
+    for (const WalkFileOut& o : res.out) {
+        if ((uint64_t)o.base + o.count > rec_total)
+            return fail(SYDELTA_E_KERNEL, "walk: records [%u, +%u) past the capacity %llu", o.base, o.count,
+                        (unsigned long long)rec_total);
+        nrec += o.count;
     }
-    res.rec = (const WalkRec*)ph.p;
+    res.rec = (const WalkRec*)(wm.p + m_rec);
     res.nrec = nrec;
     res.ms_d2h = ms_since(t0) - res.ms_kernel;
     return SYDELTA_OK;
