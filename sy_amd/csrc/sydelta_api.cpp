@@ -2546,16 +2546,16 @@ static inline uint64_t records_ops(const WalkRec* r0, const WalkRec* r1) {
 
 // The batched match with the walk on the device: one unit per file.
 // Segments per file of a batched device walk (SYDELTA_FILE_SEGS=G forces G): a wave walks
-// its unit serially, so a batch of fewer files than the chip holds twice (8192 waves at
-// four per SIMD) is cut into segments of at least 32 blocks (8 when forced).  nf counts the
-// files of every batch walking at the time (concurrent callers share the chip).
+// its unit serially, so a batch of fewer files than the chip holds at once (4096 waves at
+// four per SIMD) is cut into as many segments as keep every unit in that one round (at
+// least 32 blocks each; 8 when forced).  Measured at 1250 files (`profiles/r05zz7_*`): three
+// segments per file walk in 0.55 ms, four (5000 units, a second round) in 0.65.  nf counts
+// the files of every batch walking at the time (concurrent callers share the chip).
 std::atomic<uint64_t> g_walking_files{0};
 static uint64_t file_segs(uint64_t nf) {
     const char* e = getenv("SYDELTA_FILE_SEGS");  // read per call (tests switch it)
     if (e && *e) return std::max<uint64_t>(1, strtoull(e, nullptr, 10));
-    uint64_t g = 1;
-    while (g < 64 && g * 2 * nf <= 8192) g *= 2;
-    return g;
+    return std::max<uint64_t>(1, std::min<uint64_t>(64, 4096 / std::max<uint64_t>(nf, 1)));
 }
 
 // The batched match with the walk on the device: one unit per file, or per segment of a
