@@ -3642,16 +3642,20 @@ struct sydelta_chunk {
 // exit) differs is walked again from it (after a Copy that crosses the boundary).
 // SYDELTA_CHUNK_WALK=0, or SYDELTA_PROBE=0, keeps the classifier + host walk.
 namespace {
-// blocks per segment of the last part of a pipelined chunk (SYDELTA_CHUNK_SEG_LAST, default
-// 64: its waves finish sooner, and the last part's walk ends the pipeline)
+// blocks per segment of the last part of a pipelined chunk, whose walk ends the pipeline:
+// SYDELTA_CHUNK_SEG_LAST, else as short as keeps the part within ~3300 units (one round of
+// the chip's 4096 wave slots, beside the first part's last waves), at least 32.  At C5 (the
+// last 30 %: 315 K blocks): 96 blocks 4.105-4.112 ms per step, 80: 4.20-4.23, 64 (two
+// rounds): 4.19-4.33, 128: 4.22-4.33 (`profiles/r05zz9_*`).
 uint64_t chunk_seg_blocks();
-uint64_t chunk_seg_last_blocks() {
-    static const uint64_t v = [] {
+uint64_t chunk_seg_last_blocks(uint64_t last_blocks) {
+    static const uint64_t forced = [] {
         const char* e = getenv("SYDELTA_CHUNK_SEG_LAST");
-        const uint64_t x = (e && *e) ? strtoull(e, nullptr, 10) : 64;
-        return (x >= 8 && x <= 1024 && (x & (x - 1)) == 0) ? std::min(x, chunk_seg_blocks()) : chunk_seg_blocks();
+        const uint64_t x = (e && *e) ? strtoull(e, nullptr, 10) : 0;
+        return (x >= 8 && x <= 1024) ? x : (uint64_t)0;
     }();
-    return v;
+    const uint64_t v = forced ? forced : std::max<uint64_t>(32, (last_blocks + 3299) / 3300);
+    return std::min(v, chunk_seg_blocks());
 }
 // blocks per segment (SYDELTA_CHUNK_SEG overrides; a power of two from 8 to 1024)
 uint64_t chunk_seg_blocks() {
@@ -3736,7 +3740,8 @@ int chunk_pipe_launch(sydelta_chunk* ch, uint64_t from, bool probe) {
         }
     }
     // the last part, whose walk ends the pipeline, in shorter segments (its waves finish sooner)
-    const uint64_t seg_last = chunk_seg_last_blocks();
+    const uint64_t seg_last = K >= 2 ? chunk_seg_last_blocks((c.p1 - P.units[P.ub[K - 1]].entry + n - 1) / n)
+                                     : chunk_seg_blocks();
     if (K >= 2 && seg_last < chunk_seg_blocks()) {
         const uint64_t split = P.units[P.ub[K - 1]].entry;
         P.units.resize(P.ub[K - 1]);
