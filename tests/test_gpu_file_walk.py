@@ -274,3 +274,38 @@ def test_file_walk_c4_shape_few_files(gpu, oracle_c, monkeypatch):
     assert "k_walk_files" in prof
     for f, ((src, basis), d) in enumerate(zip(pairs, out)):
         assert d.tuples() == _oracle_ops(oracle_c, src, basis, 4096), f
+
+
+def test_chunk_pipeline_two_parts(gpu, oracle_c, monkeypatch):
+    """A chunk large enough for the two-part pipeline (>= 512 segments: 70 % / 30 %, the last
+    part re-cut into shorter segments, the parts' walks on two streams), with insertions and
+    deletions that shift the data across segment and part boundaries (re-walk rounds), a
+    duplicated run and substitutions: equal to the oracle and to the classifier path."""
+    rng = random.Random(512)
+    bs = 256
+    nblk = 600 * 128  # 600 segments of 128 blocks: 19.2 MB
+    basis = O.synth_bytes(nblk * bs + 77, 0x5E1D0A01).tobytes()
+    s = bytearray(basis)
+    for _ in range(40):  # substitutions
+        s[rng.randrange(len(s))] ^= rng.randrange(1, 256)
+    split = int(600 * 0.7) * 128 * bs  # near the first part's end
+    for p in sorted([3 * bs + 5, split - 7, split + 3 * bs + 1, len(s) - 50 * bs], reverse=True):
+        s[p:p] = rng.randbytes(rng.randint(1, 9))  # each shifts everything after it
+    del s[200 * 128 * bs:200 * 128 * bs + 11]
+    q = rng.randrange(len(s) - 4 * bs)
+    s[q:q] = s[q:q + 4 * bs]
+    src = bytes(s)
+    npos = len(src) - bs + 1
+    monkeypatch.delenv("SYDELTA_CHUNK_WALK", raising=False)
+    monkeypatch.delenv("SYDELTA_PROBE", raising=False)
+    monkeypatch.delenv("SYDELTA_CHUNK_PIPE", raising=False)
+    gpu.set_profiling(True)
+    gpu.profile(reset=True)
+    d = _chunk_walk(gpu, src, basis, bs, [0, npos])
+    prof = gpu.profile(reset=True)
+    gpu.set_profiling(False)
+    assert prof["k_walk_files"]["count"] >= 2, prof  # two parts (and any re-walks)
+    exp = _oracle_ops(oracle_c, src, basis, bs)
+    assert d.tuples() == exp
+    monkeypatch.setenv("SYDELTA_CHUNK_WALK", "0")
+    assert _chunk_walk(gpu, src, basis, bs, [0, npos]).tuples() == exp
