@@ -3608,6 +3608,7 @@ struct ChunkPipe {
     const WalkRec* rec = nullptr;
     const uint32_t* ahit = nullptr;  // the probe's results (device; NULL: no probe)
     const uint32_t* apw = nullptr;
+    unsigned long long* ticks = nullptr;  // SYDELTA_PHASE_TIMING: 16 counters per part (device)
     void release() {  // the chunk's device is current
         for (hipEvent_t e : done) {  // the parts' walks
             (void)hipEventSynchronize(e);
@@ -3693,6 +3694,27 @@ void chunk_units(const sydelta_chunk* ch, uint64_t from, std::vector<WalkUnit>& 
     } while (s0 < c.p1);
 }
 
+// The pre-roll of a chunk's aligned misses before the last part's walk (launch_preroll): one
+// wave per miss rolls it, so that walk, which ends the pipeline, takes each miss's result
+// instead of rolling its misses in turn.  SYDELTA_PREROLL=0: off; 2: before every part's
+// walk.  SYDELTA_PREROLL_WAVES: its grid (4096).
+bool preroll_on() {
+    static const bool v = !getenv("SYDELTA_PREROLL") || getenv("SYDELTA_PREROLL")[0] != '0';
+    return v;
+}
+bool preroll_all() {  // SYDELTA_PREROLL=2: every part's (else the last part's: the others' walks are hidden)
+    static const bool v = getenv("SYDELTA_PREROLL") && getenv("SYDELTA_PREROLL")[0] == '2';
+    return v;
+}
+uint32_t preroll_waves() {
+    static const uint32_t v = [] {
+        const char* e = getenv("SYDELTA_PREROLL_WAVES");
+        const long x = (e && *e) ? atol(e) : 4096;
+        return (uint32_t)std::min(65536L, std::max(1L, x));
+    }();
+    return v;
+}
+
 // Sub-ranges of a chunk's walk: 2 from 512 segments (SYDELTA_CHUNK_PIPE=K).  At C5 (8192
 // segments) two parts took 4.43-4.51 ms per step, one 4.82-4.88 and four 4.96-5.00: the
 // second part's hashing hides the first part's walk, while each further part adds a walk
@@ -3757,10 +3779,17 @@ int chunk_pipe_launch(sydelta_chunk* ch, uint64_t from, bool probe) {
     // hashing), the unit table (uploaded once the first hashing is queued), the probe's
     // results, the staged records; host: the per-unit results and the compacted records
     // (kMapped), the uploads' source (kStage, same offsets as the device's)
-    const size_t o_jobs = 0, o_last = al(sizeof(ProbeJob) * K), o_total = o_last + 8, o_units = al(o_total + 8);
+    // (the pre-roll's: per part a miss counter, zeroed with the record counter; the miss
+    // list and the first hits)
+    const bool preroll = probe && preroll_on() && C.ix->fblk[1] < kPreMark;
+    const size_t o_jobs = 0, o_last = al(sizeof(ProbeJob) * K), o_total = o_last + 8, o_cnt = o_total + 8;
+    static const bool timing = getenv("SYDELTA_PHASE_TIMING") != nullptr;  // per part: 16 tick counters
+    const size_t o_ticks = o_cnt + 8 * K, o_zend = o_ticks + (timing ? 128 * K : 0);
+    const size_t o_units = al(o_zend);
     const size_t ubytes = sizeof(WalkUnit) * nu;
     const size_t o_out = o_units + al(ubytes), o_pw = o_out + al(4 * np), o_pst = o_pw + al(4 * np);
-    const size_t o_stage = o_pst + al(8 * np), dneed = o_stage + al(sizeof(WalkRec) * rec_total);
+    const size_t o_list = o_pst + al(8 * np);
+    const size_t o_stage = o_list + (preroll ? al(4 * np) : 0), dneed = o_stage + al(sizeof(WalkRec) * rec_total);
     const size_t h_rec = al(sizeof(WalkFileOut) * nu), h_end = h_rec + al(sizeof(WalkRec) * rec_total);
     P.on = true;  // release() undoes whatever is set below
     P.device = C.ix->device;
@@ -3785,8 +3814,9 @@ int chunk_pipe_launch(sydelta_chunk* ch, uint64_t from, bool probe) {
     };
     for (int j = 0; j < K; ++j) jobs[j] = ProbeJob{c.off, c.kb + part_block(j), 0, 0, 0};
     *(uint64_t*)(S + o_last) = C.ix->last_size[0];
-    *(uint64_t*)(S + o_total) = 0;
-    HIP_TRY(hipMemcpyAsync(D, S, o_total + 8, hipMemcpyHostToDevice, C.s));
+    memset(S + o_total, 0, o_zend - o_total);
+    HIP_TRY(hipMemcpyAsync(D, S, o_zend, hipMemcpyHostToDevice, C.s));
+    P.ticks = timing ? (unsigned long long*)(D + o_ticks) : nullptr;
     bool units_up = false;
     auto upload_units = [&]() -> int {
         if (units_up) return SYDELTA_OK;
@@ -3849,6 +3879,13 @@ int chunk_pipe_launch(sydelta_chunk* ch, uint64_t from, bool probe) {
         a.units = (const WalkUnit*)(D + o_units) + P.ub[j];
         a.nunits = P.ub[j + 1] - P.ub[j];
         a.fout = (WalkFileOut*)P.fout + P.ub[j];
+        a.ticks = P.ticks ? P.ticks + 16 * j : nullptr;
+        if (preroll && (j == K - 1 || preroll_all())) {
+            const uint64_t b0 = part_block(j), b1 = std::min<uint64_t>(part_block(j + 1), np);
+            HIP_TRY(launch_preroll(a, d_out, d_pw, c.kb, b0, b1, c.p1, ch->file_len,
+                                   (uint32_t*)(D + o_list) + b0, (unsigned long long*)(D + o_cnt) + j, preroll_waves(),
+                                   sw, C.prof));
+        }
         HIP_TRY(launch_walk_files(a, sw, C.prof));
         HIP_TRY(hipEventRecord(e, sw));
     }
@@ -4014,6 +4051,16 @@ int chunk_pipe_finish(sydelta_chunk* ch, uint64_t entry, uint64_t* exit_pos, syd
             }
         }
         if (int r = assemble(stop, nu)) return r;
+    }
+    if (P.ticks) {
+        std::vector<unsigned long long> tk(16 * P.done.size());
+        HIP_TRY(hipMemcpy(tk.data(), P.ticks, 8 * tk.size(), hipMemcpyDeviceToHost));
+        for (size_t j = 0; j < P.done.size(); ++j) {
+            const unsigned long long* t = tk.data() + 16 * j;
+            fprintf(stderr, "sydelta chunk walk part %zu (%u units; wave ticks, 100 MHz, summed): setup %llu hash %llu "
+                    "lookup %llu stage %llu roll %llu verify %llu out %llu | passes %llu windows %llu rolls %llu\n", j,
+                    P.ub[j + 1] - P.ub[j], t[0], t[1], t[2], t[3], t[4], t[5], t[6], t[8], t[9], t[10]);
+        }
     }
     ops.resize(nops);
     d->stats.data_ops = data_ops;

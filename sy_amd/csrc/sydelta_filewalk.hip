@@ -123,6 +123,156 @@ __device__ __forceinline__ bool tail_matches(const uint8_t* p, uint64_t ls, uint
     return __builtin_amdgcn_readlane((int)(wk == weak && st == strong ? 1u : 0u), 0) != 0;
 }
 
+// The first verified hit among the window starts (x, yend), the window at x (weak wbase)
+// missed: its position in q and block in qb (else q = yend, qb = kNoBlock); weak_hits counts
+// the verified windows.  The whole wave calls (k_walk_files at a miss, k_preroll per miss).
+template <bool kLdsFilt, class Tick, class Count>
+__device__ __forceinline__ void walk_roll(const WalkArgs& a, const FileIx& F, const uint32_t* filt,
+                                          const uint32_t* ntab, const uint8_t* src, uint64_t len, uint64_t x,
+                                          uint64_t yend, uint32_t wbase, uint64_t& q, uint32_t& qb,
+                                          uint32_t& weak_hits, Tick&& wtick, Count&& wcount) {
+    const uint32_t lane = threadIdx.x & 63, row = lane >> 4, n = a.n;
+    q = yend;
+    qb = kNoBlock;
+#pragma unroll 1
+    for (uint64_t y0 = x + 1; y0 < yend && qb == kNoBlock; y0 += kWSub) {
+        const uint64_t y1 = min(y0 + kWSub, yend);
+        const uint64_t b = y0 - 1;
+        wcount(kWtRolls, 1);
+        uint32_t xo[16], xi[16];  // out [b + 64l, +64), in [b + n + 64l, +64)
+        load64_any(src, len, b + 64ull * lane, xo);
+        load64_any(src, len, b + n + 64ull * lane, xi);
+        uint32_t so = 0, si = 0, vo = 0, vi = 0;
+#pragma unroll
+        for (int i = 0; i < 16; ++i) {
+            so = udot4(xo[i], 0x01010101u, so);
+            si = udot4(xi[i], 0x01010101u, si);
+            vo = udot4(xo[i], offw(i), vo);
+            vi = udot4(xi[i], offw(i), vi);
+        }
+        const uint32_t gc = (si + 2 * kMod - so) % kMod;                                          // sum c
+        const uint32_t gj = (uint32_t)(((uint64_t)(64 * lane) * gc + vi + 16 * kMod - vo) % kMod);  // sum j c
+        uint32_t tt;
+        const uint32_t sC = wave_scan_excl(gc, tt);
+        const uint32_t sJ = wave_scan_excl(gj, tt);
+        const uint32_t sO = wave_scan_excl(so, tt);
+        const uint32_t o0 = xo[0] & 0xFF, i0 = xi[0] & 0xFF;  // byte j = 64 l: the last of the first window's c_j
+        const uint32_t c0 = (i0 + kMod - o0) % kMod;
+        const uint32_t C = (sC % kMod + c0) % kMod;
+        const uint32_t J = (uint32_t)((sJ % kMod + (uint64_t)(64 * lane) * c0) % kMod);
+        const uint32_t Out = (sO + o0) % kMod;
+        const uint64_t d = 64ull * lane + 1;
+        const uint32_t Ab = wbase & 0xFFFFu, Bb = wbase >> 16;
+        uint32_t am = (Ab + C) % kMod;
+        uint32_t bm = (uint32_t)(((uint64_t)Bb + d * ((Ab + kMod - 1) % kMod) % kMod + d * C % kMod + (kMod - J) +
+                                  (kMod - (uint64_t)a.nm * Out % kMod)) % kMod);
+        wtick(kWtStage);
+        // roll the lane's 64 window starts; a start whose weak value passes the Bloom filter
+        // is a candidate
+        const uint64_t p0 = y0 + 64ull * lane;
+        const uint32_t nvalid = p0 >= y1 ? 0u : (uint32_t)min((uint64_t)kWRun, y1 - p0);
+        // the bytes the rolls take out / in: group offsets 1..64 (offset 64 is never used)
+#pragma unroll
+        for (int j = 0; j < 16; ++j) {
+            xo[j] = __builtin_amdgcn_alignbyte(j < 15 ? xo[j + 1] : 0u, xo[j], 1);
+            xi[j] = __builtin_amdgcn_alignbyte(j < 15 ? xi[j + 1] : 0u, xi[j], 1);
+        }
+        uint64_t pm = 0;
+        uint32_t wlast = 0;
+        // a global filter (a large index: 16 bits per key, ~0.8 % of starts pass) keeps the
+        // weak values of a lane's first four passes, which are looked up in the exact table
+        // below before anything is hashed (8 KiB per candidate otherwise)
+        uint32_t wp[4] = {0, 0, 0, 0}, wpi[4] = {0, 0, 0, 0}, np = 0;
+        // sixteen starts per round from the first four dwords (their filter words loaded
+        // together: a global filter's reads are L2 round trips), then the dwords move down
+        // four (a loop, not unrolled: the register arrays keep constant indices)
+#pragma unroll 1
+        for (uint32_t t = 0; t < kWRun / 16; ++t) {
+            uint32_t hq[16], fwv[16], wv[16];
+#pragma unroll
+            for (int b = 0; b < 16; ++b) {
+                const ProbeHash h = probe_hash(am, bm);
+                hq[b] = h.q;
+                fwv[b] = filt[h.r >> F.fwshift];
+                wv[b] = (bm << 16) | am;
+                const uint32_t out = (xo[b >> 2] >> (8 * (b & 3))) & 0xFF;
+                const uint32_t in = (xi[b >> 2] >> (8 * (b & 3))) & 0xFF;
+                const uint32_t u = am + in + (kMod - out);  // [M-255, 2M+255)
+                am = min(u, min(u - kMod, u - 2 * kMod));
+                const uint32_t v = bm + am + ntab[out];  // [0, 3M)
+                bm = min(v, min(v - kMod, v - 2 * kMod));
+            }
+            wlast = wv[15];
+#pragma unroll
+            for (int b = 0; b < 16; ++b) {
+                const uint32_t i = 16 * t + b;
+                const uint32_t pass = i < nvalid ? filt_bit(fwv[b], hq[b]) : 0u;
+                pm |= (uint64_t)pass << i;
+                if (!kLdsFilt && pass) {
+#pragma unroll
+                    for (int j = 0; j < 4; ++j)
+                        if (np == (uint32_t)j) {
+                            wp[j] = wv[b];
+                            wpi[j] = i;
+                        }
+                    ++np;
+                }
+            }
+#pragma unroll
+            for (int j = 0; j < 12; ++j) {
+                xo[j] = xo[j + 4];
+                xi[j] = xi[j + 4];
+            }
+        }
+        wbase = rl(wlast, 63);  // the next pass's base: lane 63's last start, b + 4096
+        if (!kLdsFilt) {  // exact-table lookups of the first passes (generator.rs:121-124)
+#pragma unroll
+            for (int j = 0; j < 4; ++j)
+                if ((uint32_t)j < np && table_find(a.keys + F.slot_off, F.bmask, wp[j]) < 0) pm &= ~(1ull << wpi[j]);
+        }
+        wtick(kWtRoll);
+        // verify the candidates four at a time in position order (generator.rs:121-133);
+        // weak_hits counts the verified windows
+#pragma unroll 1
+        for (;;) {
+            uint32_t cand[4], nc = 0;
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const uint64_t lm = __ballot(pm != 0);
+                cand[r] = 0;
+                if (!lm) continue;
+                const uint32_t fl = (uint32_t)__builtin_ctzll(lm);
+                const uint32_t lo = rl((uint32_t)pm, fl), hi = rl((uint32_t)(pm >> 32), fl);
+                const uint64_t m = ((uint64_t)hi << 32) | lo;
+                const uint32_t bit = (uint32_t)__builtin_ctzll(m);
+                cand[r] = 64 * fl + bit;
+                if (lane == fl) pm &= pm - 1;
+                ++nc;
+            }
+            if (!nc) break;
+            uint32_t mine = row == 1 ? cand[1] : row == 2 ? cand[2] : row == 3 ? cand[3] : cand[0];
+            if (row >= nc) mine = cand[0];
+            uint32_t wk;
+            uint64_t st;
+            walk_hash<false>(src + y0 + mine, n, wk, st);
+            uint32_t vb = kNoBlock;
+            if ((lane & 15) == 0 && row < nc) vb = walk_lookup(a, F, wk, st);
+            weak_hits += nc;
+            wcount(kWtVerifies, 1);
+            for (uint32_t r = 0; r < nc; ++r) {
+                const uint32_t bb = rl(vb, 16 * r);
+                if (bb != kNoBlock) {
+                    q = y0 + cand[r];
+                    qb = bb;
+                    break;
+                }
+            }
+            if (qb != kNoBlock) break;
+        }
+        wtick(kWtVerify);
+    }
+}
+
 // kLdsFilt: the unit's Bloom filter is copied to LDS (a batch's small files), else read from
 // global memory (L2-resident: a large single-file index, the segments of a chunk).
 template <bool kLdsFilt>
@@ -199,10 +349,25 @@ __global__ __launch_bounds__(64, 4) void k_walk_files(WalkArgs a) {
     uint64_t rk0 = 0, rk1 = 0;  // lane w holds the result (rres) and weak (rwk) of block rk0 + w at phase phi
     uint64_t kph = 0;           // the block where the walk took phase phi
     uint32_t rres = kNoBlock, rwk = 0;
+    // x = k n + ph, kept without a division per block (a 64-bit division by a variable n is a
+    // long instruction sequence, and the walk steps a block at a time)
+    uint64_t k = 0;
+    uint32_t ph = 0;
+    bool resync = true;  // k, ph from x by a division (after a move other than by n)
+    auto move_to = [&](uint64_t nx) {
+        if (nx == x + n)
+            ++k;
+        else
+            resync = true;
+        x = nx;
+    };
 #pragma unroll 1
     while (x < end) {
-        const uint64_t k = x / n;
-        const uint32_t ph = (uint32_t)(x - k * n);
+        if (resync) {
+            k = x / n;
+            ph = (uint32_t)(x - k * n);
+            resync = false;
+        }
         if (ph != phi || k >= rk1) {
             // ---- phase pass: windows (k + w) n + ph, w < cnt, four per row_hash round.  The
             // passes of one phase grow (4, then twice the blocks walked at this phase, up to
@@ -257,11 +422,11 @@ __global__ __launch_bounds__(64, 4) void k_walk_files(WalkArgs a) {
         }
     have_pass:
         const uint32_t blk = rl(rres, (uint32_t)(k - rk0));
-        if (blk != kNoBlock) {  // generator.rs:135-146
+        if (blk < kPreMark) {  // generator.rs:135-146
             ++hits;
             data(lit, x);
             copy(blk);
-            x += n;
+            move_to(x + n);
             lit = x;
             continue;
         }
@@ -276,152 +441,24 @@ __global__ __launch_bounds__(64, 4) void k_walk_files(WalkArgs a) {
         const uint64_t yend = min(x + n, end);  // later starts are the next unit's
         uint64_t q = yend;
         uint32_t qb = kNoBlock;
-        uint32_t wbase = rl(rwk, (uint32_t)(k - rk0));  // weak of the window at b
-#pragma unroll 1
-        for (uint64_t y0 = x + 1; y0 < yend && qb == kNoBlock; y0 += kWSub) {
-            const uint64_t y1 = min(y0 + kWSub, yend);
-            const uint64_t b = y0 - 1;
-            wcount(kWtRolls, 1);
-            uint32_t xo[16], xi[16];  // out [b + 64l, +64), in [b + n + 64l, +64)
-            load64_any(src, len, b + 64ull * lane, xo);
-            load64_any(src, len, b + n + 64ull * lane, xi);
-            uint32_t so = 0, si = 0, vo = 0, vi = 0;
-#pragma unroll
-            for (int i = 0; i < 16; ++i) {
-                so = udot4(xo[i], 0x01010101u, so);
-                si = udot4(xi[i], 0x01010101u, si);
-                vo = udot4(xo[i], offw(i), vo);
-                vi = udot4(xi[i], offw(i), vi);
+        const uint32_t wb = rl(rwk, (uint32_t)(k - rk0));  // weak of the window at x (pre-rolled: the result)
+        if (blk == kNoBlock) {
+            walk_roll<kLdsFilt>(a, F, filt, ntab, src, len, x, yend, wb, q, qb, weak_hits, wtick, wcount);
+        } else {  // pre-rolled (k_preroll): the first hit of (x, min(x + n, p1))
+            weak_hits += wb >> 14;
+            if (blk != kPreNone && x + (wb & 0x3FFFu) < yend) {
+                q = x + (wb & 0x3FFFu);
+                qb = blk & ~kPreMark;
             }
-            const uint32_t gc = (si + 2 * kMod - so) % kMod;                                          // sum c
-            const uint32_t gj = (uint32_t)(((uint64_t)(64 * lane) * gc + vi + 16 * kMod - vo) % kMod);  // sum j c
-            uint32_t tt;
-            const uint32_t sC = wave_scan_excl(gc, tt);
-            const uint32_t sJ = wave_scan_excl(gj, tt);
-            const uint32_t sO = wave_scan_excl(so, tt);
-            const uint32_t o0 = xo[0] & 0xFF, i0 = xi[0] & 0xFF;  // byte j = 64 l: the last of the first window's c_j
-            const uint32_t c0 = (i0 + kMod - o0) % kMod;
-            const uint32_t C = (sC % kMod + c0) % kMod;
-            const uint32_t J = (uint32_t)((sJ % kMod + (uint64_t)(64 * lane) * c0) % kMod);
-            const uint32_t Out = (sO + o0) % kMod;
-            const uint64_t d = 64ull * lane + 1;
-            const uint32_t Ab = wbase & 0xFFFFu, Bb = wbase >> 16;
-            uint32_t am = (Ab + C) % kMod;
-            uint32_t bm = (uint32_t)(((uint64_t)Bb + d * ((Ab + kMod - 1) % kMod) % kMod + d * C % kMod + (kMod - J) +
-                                      (kMod - (uint64_t)a.nm * Out % kMod)) % kMod);
-            wtick(kWtStage);
-            // roll the lane's 64 window starts; a start whose weak value passes the Bloom filter
-            // is a candidate
-            const uint64_t p0 = y0 + 64ull * lane;
-            const uint32_t nvalid = p0 >= y1 ? 0u : (uint32_t)min((uint64_t)kWRun, y1 - p0);
-            // the bytes the rolls take out / in: group offsets 1..64 (offset 64 is never used)
-#pragma unroll
-            for (int j = 0; j < 16; ++j) {
-                xo[j] = __builtin_amdgcn_alignbyte(j < 15 ? xo[j + 1] : 0u, xo[j], 1);
-                xi[j] = __builtin_amdgcn_alignbyte(j < 15 ? xi[j + 1] : 0u, xi[j], 1);
-            }
-            uint64_t pm = 0;
-            uint32_t wlast = 0;
-            // a global filter (a large index: 16 bits per key, ~0.8 % of starts pass) keeps the
-            // weak values of a lane's first four passes, which are looked up in the exact table
-            // below before anything is hashed (8 KiB per candidate otherwise)
-            uint32_t wp[4] = {0, 0, 0, 0}, wpi[4] = {0, 0, 0, 0}, np = 0;
-            // sixteen starts per round from the first four dwords (their filter words loaded
-            // together: a global filter's reads are L2 round trips), then the dwords move down
-            // four (a loop, not unrolled: the register arrays keep constant indices)
-#pragma unroll 1
-            for (uint32_t t = 0; t < kWRun / 16; ++t) {
-                uint32_t hq[16], fwv[16], wv[16];
-#pragma unroll
-                for (int b = 0; b < 16; ++b) {
-                    const ProbeHash h = probe_hash(am, bm);
-                    hq[b] = h.q;
-                    fwv[b] = filt[h.r >> F.fwshift];
-                    wv[b] = (bm << 16) | am;
-                    const uint32_t out = (xo[b >> 2] >> (8 * (b & 3))) & 0xFF;
-                    const uint32_t in = (xi[b >> 2] >> (8 * (b & 3))) & 0xFF;
-                    const uint32_t u = am + in + (kMod - out);  // [M-255, 2M+255)
-                    am = min(u, min(u - kMod, u - 2 * kMod));
-                    const uint32_t v = bm + am + ntab[out];  // [0, 3M)
-                    bm = min(v, min(v - kMod, v - 2 * kMod));
-                }
-                wlast = wv[15];
-#pragma unroll
-                for (int b = 0; b < 16; ++b) {
-                    const uint32_t i = 16 * t + b;
-                    const uint32_t pass = i < nvalid ? filt_bit(fwv[b], hq[b]) : 0u;
-                    pm |= (uint64_t)pass << i;
-                    if (!kLdsFilt && pass) {
-#pragma unroll
-                        for (int j = 0; j < 4; ++j)
-                            if (np == (uint32_t)j) {
-                                wp[j] = wv[b];
-                                wpi[j] = i;
-                            }
-                        ++np;
-                    }
-                }
-#pragma unroll
-                for (int j = 0; j < 12; ++j) {
-                    xo[j] = xo[j + 4];
-                    xi[j] = xi[j + 4];
-                }
-            }
-            wbase = rl(wlast, 63);  // the next pass's base: lane 63's last start, b + 4096
-            if (!kLdsFilt) {  // exact-table lookups of the first passes (generator.rs:121-124)
-#pragma unroll
-                for (int j = 0; j < 4; ++j)
-                    if ((uint32_t)j < np && table_find(a.keys + F.slot_off, F.bmask, wp[j]) < 0) pm &= ~(1ull << wpi[j]);
-            }
-            wtick(kWtRoll);
-            // verify the candidates four at a time in position order (generator.rs:121-133);
-            // weak_hits counts the verified windows
-#pragma unroll 1
-            for (;;) {
-                uint32_t cand[4], nc = 0;
-#pragma unroll
-                for (int r = 0; r < 4; ++r) {
-                    const uint64_t lm = __ballot(pm != 0);
-                    cand[r] = 0;
-                    if (!lm) continue;
-                    const uint32_t fl = (uint32_t)__builtin_ctzll(lm);
-                    const uint32_t lo = rl((uint32_t)pm, fl), hi = rl((uint32_t)(pm >> 32), fl);
-                    const uint64_t m = ((uint64_t)hi << 32) | lo;
-                    const uint32_t bit = (uint32_t)__builtin_ctzll(m);
-                    cand[r] = 64 * fl + bit;
-                    if (lane == fl) pm &= pm - 1;
-                    ++nc;
-                }
-                if (!nc) break;
-                uint32_t mine = row == 1 ? cand[1] : row == 2 ? cand[2] : row == 3 ? cand[3] : cand[0];
-                if (row >= nc) mine = cand[0];
-                uint32_t wk;
-                uint64_t st;
-                walk_hash<false>(src + y0 + mine, n, wk, st);
-                uint32_t vb = kNoBlock;
-                if ((lane & 15) == 0 && row < nc) vb = walk_lookup(a, F, wk, st);
-                weak_hits += nc;
-                wcount(kWtVerifies, 1);
-                for (uint32_t r = 0; r < nc; ++r) {
-                    const uint32_t bb = rl(vb, 16 * r);
-                    if (bb != kNoBlock) {
-                        q = y0 + cand[r];
-                        qb = bb;
-                        break;
-                    }
-                }
-                if (qb != kNoBlock) break;
-            }
-            wtick(kWtVerify);
         }
         if (qb != kNoBlock) {
             ++hits;
             data(lit, q);
             copy(qb);
-            x = q + n;
+            move_to(q + n);
             lit = x;
         } else {
-            x = yend;  // the next phase window (or the end of the full windows)
+            move_to(yend);  // the next phase window (or the end of the full windows)
         }
     }
     // the walk's end.  A final unit: the tail rule at p* = len - last_size, then the last
@@ -459,7 +496,73 @@ __global__ __launch_bounds__(64, 4) void k_walk_files(WalkArgs a) {
 }
 
 // ===========================================================================
-// Launch wrapper
+// K10's pre-roll (a chunk's aligned misses, launch_preroll)
+// ===========================================================================
+// A chunk walk spends most of its time rolling the window starts after each missed aligned
+// block, one wave per segment doing its misses in turn.  The pre-roll does those rolls
+// beforehand, one wave per miss: the walk then reads each miss's result instead.
+// The misses are listed first (one thread per block, a wave-aggregated atomic).
+__global__ __launch_bounds__(1024) void k_miss_list(const uint32_t* ahit, uint64_t b0, uint64_t b1, uint32_t* list,
+                                                    unsigned long long* count) {
+    __shared__ uint32_t wc[64];  // per (wave, quarter): misses, then their list offset
+    __shared__ uint32_t wbase;
+    const uint32_t t = threadIdx.x, lane = t & 63, w = t >> 6;
+    const uint64_t g = b0 + (uint64_t)blockIdx.x * 4096 + t;  // the workgroup's 4096 blocks, 4 per thread
+    uint64_t m[4];
+    bool miss[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        const uint64_t r = g + 1024 * i;
+        miss[i] = r < b1 && ahit[r] == kNoBlock;
+        m[i] = __ballot(miss[i]);
+        if (lane == 0) wc[4 * w + i] = (uint32_t)__popcll(m[i]);
+    }
+    __syncthreads();
+    if (t == 0) {  // one atomic per workgroup
+        uint32_t s = 0;
+        for (int j = 0; j < 64; ++j) {
+            const uint32_t c = wc[j];
+            wc[j] = s;
+            s += c;
+        }
+        wbase = s ? (uint32_t)atomicAdd(count, (unsigned long long)s) : 0u;
+    }
+    __syncthreads();
+    const uint64_t below = (1ull << lane) - 1;
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+        if (miss[i]) list[wbase + wc[4 * w + i] + __popcll(m[i] & below)] = (uint32_t)(g + 1024 * i);
+}
+
+__global__ __launch_bounds__(64, 4) void k_preroll(WalkArgs a, uint32_t* ahit, uint32_t* apw, uint64_t kb,
+                                                   uint64_t pend, uint64_t len, const uint32_t* list,
+                                                   const unsigned long long* count) {
+    __shared__ uint32_t ntab[256];
+    const uint32_t lane = threadIdx.x;
+    const uint64_t m = *count;
+    if (blockIdx.x >= m) return;
+    for (uint32_t i = lane; i < 256; i += 64) ntab[i] = kMod - 1 - (a.nm * i) % kMod;
+    __syncthreads();
+    const FileIx F = a.files[0];
+    const uint32_t* filt = a.filt + F.filt_off;
+    const uint64_t n = a.n;
+#pragma unroll 1
+    for (uint64_t i = blockIdx.x; i < m; i += gridDim.x) {
+        const uint32_t r = list[i];
+        const uint64_t x = (kb + r) * n;
+        uint64_t q;
+        uint32_t qb, wh = 0;
+        walk_roll<false>(a, F, filt, ntab, a.base, len, x, min(x + n, pend), apw[r], q, qb, wh, [](int) {},
+                         [](int, uint64_t) {});
+        if (lane == 0) {  // (the walk's miss at x, with the roll's result: launch_preroll)
+            ahit[r] = qb == kNoBlock ? kPreNone : (qb | kPreMark);
+            apw[r] = (qb == kNoBlock ? 0u : (uint32_t)(q - x)) | (min(wh, 0x3FFFFu) << 14);
+        }
+    }
+}
+
+// ===========================================================================
+// Launch wrappers
 // ===========================================================================
 hipError_t launch_walk_files(const WalkArgs& a, hipStream_t s, Profiler* prof) {
     if (!a.nunits) return hipSuccess;
@@ -471,6 +574,22 @@ hipError_t launch_walk_files(const WalkArgs& a, hipStream_t s, Profiler* prof) {
         hipLaunchKernelGGL(k_walk_files<true>, dim3(a.nunits), dim3(64), L.total, s, a);
     else
         hipLaunchKernelGGL(k_walk_files<false>, dim3(a.nunits), dim3(64), L.total, s, a);
+    return hipGetLastError();
+}
+
+hipError_t launch_preroll(const WalkArgs& a, uint32_t* ahit, uint32_t* apw, uint64_t kb, uint64_t b0, uint64_t b1,
+                          uint64_t pend, uint64_t len, uint32_t* list, unsigned long long* count, uint32_t waves,
+                          hipStream_t s, Profiler* prof) {
+    if (b1 <= b0) return hipSuccess;
+    if (a.n % 64 != 0 || a.n < 256 || a.n > kWalkMaxN || !ahit || !apw || !waves || b1 - b0 >= (1ull << 31))
+        return hipErrorInvalidValue;
+    {
+        ProfScope ps(prof, s, "k_miss_list");
+        hipLaunchKernelGGL(k_miss_list, dim3((unsigned)((b1 - b0 + 4095) / 4096)), dim3(1024), 0, s, ahit, b0, b1, list,
+                           count);
+    }
+    ProfScope ps(prof, s, "k_preroll");
+    hipLaunchKernelGGL(k_preroll, dim3(waves), dim3(64), 0, s, a, ahit, apw, kb, pend, len, list, count);
     return hipGetLastError();
 }
 

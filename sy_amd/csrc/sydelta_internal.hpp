@@ -257,7 +257,8 @@ struct WalkArgs {
     const uint64_t* cstrong;
     const uint32_t* weak;        // the index's signature copies (the tail rule)
     const uint64_t* strong;
-    const uint32_t* ahit;        // optional: the aligned probe's results (block k: its hit or none) ...
+    const uint32_t* ahit;        // optional: the aligned probe's results (block k: its hit or none, or
+                                 // launch_preroll's) ...
     const uint32_t* apw;         // ... and its windows' weak values
     WalkRec* stage;              // may be host-mapped memory (with out NULL)
     WalkRec* out;                // compacted records of every unit; NULL: left in stage (base = rec_off)
@@ -266,6 +267,18 @@ struct WalkArgs {
     unsigned long long* ticks;   // SYDELTA_PHASE_TIMING: 16 counters (zeroed), else null
 };
 hipError_t launch_walk_files(const WalkArgs& a, hipStream_t s, Profiler* prof);
+// K10's pre-roll of a chunk's aligned misses: every block r in [b0, b1) (relative to kb)
+// whose aligned probe missed (ahit[r] == kNoBlock) is rolled: the first verified hit among
+// the window starts (x, min(x + n, pend)), x = (kb + r) n, replaces the probe's results:
+// ahit[r] = its block | kPreMark (kPreNone: none), apw[r] = its offset from x (bits 0-13)
+// | the windows verified << 14.  k_walk_files takes such a miss's result instead of rolling.
+// One wave per miss from a list (list[0, *count): count zeroed before, room for b1 - b0);
+// `waves` waves loop over it.  a: the chunk's K10 arguments (one file; the filter from
+// global memory; block ids below kPreMark).
+constexpr uint32_t kPreMark = 0x80000000u, kPreNone = 0xFFFFFFFEu;
+hipError_t launch_preroll(const WalkArgs& a, uint32_t* ahit, uint32_t* apw, uint64_t kb, uint64_t b0, uint64_t b1,
+                          uint64_t pend, uint64_t len, uint32_t* list, unsigned long long* count, uint32_t waves,
+                          hipStream_t s, Profiler* prof);
 // One slice (<= 64 KiB) of an op for the device apply: out[dst, dst+len) =
 // (from_basis ? basis : lit)[src, src+len).
 struct ApplyPiece {

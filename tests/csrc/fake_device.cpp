@@ -635,12 +635,27 @@ hipError_t launch_walk_files(const WalkArgs& a, hipStream_t, Profiler*) {
             const uint32_t w = (uint32_t)((wb << 16) | wa);
             const uint32_t blk = lookup(F, U.file, w, src + x, n, &wh);
             weak_hits += wh;
-            if (a.ahit && x % n == 0 && (a.ahit[x / n - U.kb] != blk || a.apw[x / n - U.kb] != w)) probe_ok = false;
+            if (a.ahit && x % n == 0) {
+                const uint32_t h = a.ahit[x / n - U.kb];
+                if (h != kNone && h >= kPreMark)  // pre-rolled: a miss here
+                    probe_ok = probe_ok && blk == kNone;
+                else if (h != blk || a.apw[x / n - U.kb] != w)
+                    probe_ok = false;
+            }
             return blk;
         };
         uint64_t x = U.entry, lit = U.entry;
         while (x < U.end) {
             const uint32_t blk = classify(x);
+            if (a.ahit && blk == kNone && x % n == 0 && a.ahit[x / n - U.kb] != kNone) {  // pre-rolled
+                const uint32_t h = a.ahit[x / n - U.kb];
+                if (h != kPreNone) {  // its first hit must be a hit
+                    const uint64_t q = x + (a.apw[x / n - U.kb] & 0x3FFF);
+                    bool wh = false;
+                    if (q <= x || q >= x + n || lookup(F, U.file, adler(src + q, n), src + q, n, &wh) != (h & ~kPreMark))
+                        return hipErrorInvalidValue;
+                }
+            }
             if (blk != kNone) {
                 ++hits;
                 data(lit, x);
@@ -680,6 +695,39 @@ hipError_t launch_walk_files(const WalkArgs& a, hipStream_t, Profiler*) {
         placed += rec.size();
     }
     if (a.out) *a.total = placed;
+    return hipSuccess;
+}
+
+// K10's pre-roll: each missed aligned block's first hit in (x, min(x + n, pend)), exactly
+hipError_t launch_preroll(const WalkArgs& a, uint32_t* ahit, uint32_t* apw, uint64_t kb, uint64_t b0, uint64_t b1,
+                          uint64_t pend, uint64_t len, uint32_t*, unsigned long long*, uint32_t waves, hipStream_t,
+                          Profiler*) {
+    EmuTimer emu_t;
+    if (b1 <= b0) return hipSuccess;
+    if (a.n % 64 != 0 || a.n < 256 || a.n > kWalkMaxN || !ahit || !apw || !waves) return hipErrorInvalidValue;
+    DeviceIndex key_ix;
+    key_ix.keys = (uint32_t*)a.keys;
+    const FakeIndex& F = find_ix(key_ix);
+    const uint64_t n = a.n;
+    for (uint64_t r = b0; r < b1; ++r) {
+        if (ahit[r] != kNone) continue;
+        const uint64_t x = (kb + r) * n, yend = std::min(x + n, pend);
+        if (x + n > len) return hipErrorInvalidValue;  // a probed block is a full window
+        uint32_t h = kPreNone, off = 0, wcnt = 0;
+        for (uint64_t y = x + 1; y < yend; ++y) {
+            bool wh = false;
+            const uint32_t b = lookup(F, 0, adler(a.base + y, n), a.base + y, n, &wh);
+            wcnt += wh;
+            if (b != kNone) {
+                if (b >= kPreMark) return hipErrorInvalidValue;
+                h = b | kPreMark;
+                off = (uint32_t)(y - x);
+                break;
+            }
+        }
+        ahit[r] = h;
+        apw[r] = off | (std::min(wcnt, 0x3FFFFu) << 14);
+    }
     return hipSuccess;
 }
 
