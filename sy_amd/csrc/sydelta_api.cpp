@@ -3706,6 +3706,10 @@ bool preroll_all() {  // SYDELTA_PREROLL=2: every part's (else the last part's: 
     static const bool v = getenv("SYDELTA_PREROLL") && getenv("SYDELTA_PREROLL")[0] == '2';
     return v;
 }
+bool slim_walk() {  // SYDELTA_SLIM_WALK=0: a pre-rolled part walked by the full kernel alone
+    static const bool v = !getenv("SYDELTA_SLIM_WALK") || getenv("SYDELTA_SLIM_WALK")[0] != '0';
+    return v;
+}
 uint32_t preroll_waves() {
     static const uint32_t v = [] {
         const char* e = getenv("SYDELTA_PREROLL_WAVES");
@@ -3885,6 +3889,7 @@ int chunk_pipe_launch(sydelta_chunk* ch, uint64_t from, bool probe) {
             HIP_TRY(launch_preroll(a, d_out, d_pw, c.kb, b0, b1, c.p1, ch->file_len,
                                    (uint32_t*)(D + o_list) + b0, (unsigned long long*)(D + o_cnt) + j, preroll_waves(),
                                    sw, C.prof));
+            if (slim_walk()) HIP_TRY(launch_walk_files(a, sw, C.prof, true));
         }
         HIP_TRY(launch_walk_files(a, sw, C.prof));
         HIP_TRY(hipEventRecord(e, sw));

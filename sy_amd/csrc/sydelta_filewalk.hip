@@ -275,10 +275,16 @@ __device__ __forceinline__ void walk_roll(const WalkArgs& a, const FileIx& F, co
 
 // kLdsFilt: the unit's Bloom filter is copied to LDS (a batch's small files), else read from
 // global memory (L2-resident: a large single-file index, the segments of a chunk).
-template <bool kLdsFilt>
+// kSlim: the walk of a pre-rolled part (launch_preroll), without the roll or the phase-window
+// hashing: a unit that needs either (a phase change after a Copy at an unaligned position, a
+// miss that was not pre-rolled) is left to the full kernel launched after it, which skips the
+// units the slim one finished (marked in the unit table).  The full kernel's registers (the
+// roll's) spill, and its spills cost a scratch round trip per block walked.
+template <bool kLdsFilt, bool kSlim>
 __global__ __launch_bounds__(64, 4) void k_walk_files(WalkArgs a) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     const WalkUnit U = a.units[blockIdx.x];
+    if (!kSlim && (U.final_ & kUnitDone)) return;  // walked by the slim kernel
     const uint32_t lane = threadIdx.x, row = lane >> 4;
     const uint32_t n = a.n;
     const FileIx F = a.files[U.file];
@@ -349,8 +355,10 @@ __global__ __launch_bounds__(64, 4) void k_walk_files(WalkArgs a) {
     uint64_t rk0 = 0, rk1 = 0;  // lane w holds the result (rres) and weak (rwk) of block rk0 + w at phase phi
     uint64_t kph = 0;           // the block where the walk took phase phi
     uint32_t rres = kNoBlock, rwk = 0;
-    // x = k n + ph, kept without a division per block (a 64-bit division by a variable n is a
-    // long instruction sequence, and the walk steps a block at a time)
+    // x = k n + ph: the slim kernel keeps it without a division per block (a 64-bit division by
+    // a variable n is a long instruction sequence, and the walk steps a block at a time); the
+    // full kernel divides at every step, which keeps its registers from spilling (LDS filter)
+    // or spills fewer (global filter: 2 VGPRs against 5)
     uint64_t k = 0;
     uint32_t ph = 0;
     bool resync = true;  // k, ph from x by a division (after a move other than by n)
@@ -363,10 +371,11 @@ __global__ __launch_bounds__(64, 4) void k_walk_files(WalkArgs a) {
     };
 #pragma unroll 1
     while (x < end) {
-        if (resync) {
+        if (resync || !kSlim) {
             k = x / n;
             ph = (uint32_t)(x - k * n);
             resync = false;
+            if (kSlim && ph != 0) return;  // a new phase grid: the full kernel's
         }
         if (ph != phi || k >= rk1) {
             // ---- phase pass: windows (k + w) n + ph, w < cnt, four per row_hash round.  The
@@ -376,7 +385,7 @@ __global__ __launch_bounds__(64, 4) void k_walk_files(WalkArgs a) {
             if (ph != phi) kph = k;
             const uint64_t left = (end - x + n - 1) / n;
             const uint32_t cnt = (uint32_t)min(left, min((uint64_t)kWMaxPass, max((uint64_t)4, 2 * (k - kph))));
-            if (ph == 0 && a.ahit) {  // phase 0 with the aligned probe's results: nothing to hash
+            if (kSlim || (ph == 0 && a.ahit)) {  // phase 0 with the aligned probe's results: nothing to hash
                 rres = kNoBlock;
                 rwk = 0;
                 if (lane < cnt) {
@@ -442,7 +451,8 @@ __global__ __launch_bounds__(64, 4) void k_walk_files(WalkArgs a) {
         uint64_t q = yend;
         uint32_t qb = kNoBlock;
         const uint32_t wb = rl(rwk, (uint32_t)(k - rk0));  // weak of the window at x (pre-rolled: the result)
-        if (blk == kNoBlock) {
+        if (kLdsFilt || blk == kNoBlock) {  // (a batch's walks, kLdsFilt, are never pre-rolled)
+            if (kSlim) return;  // not pre-rolled: the full kernel's
             walk_roll<kLdsFilt>(a, F, filt, ntab, src, len, x, yend, wb, q, qb, weak_hits, wtick, wcount);
         } else {  // pre-rolled (k_preroll): the first hit of (x, min(x + n, p1))
             weak_hits += wb >> 14;
@@ -492,6 +502,7 @@ __global__ __launch_bounds__(64, 4) void k_walk_files(WalkArgs a) {
         }
     }
     if (lane == 0) a.fout[blockIdx.x] = WalkFileOut{(uint32_t)base, nrec, weak_hits, hits, exit, 0};
+    if (kSlim && lane == 0) const_cast<WalkUnit*>(a.units)[blockIdx.x].final_ = U.final_ | kUnitDone;
     wtick(kWtOut);
 }
 
@@ -564,16 +575,19 @@ __global__ __launch_bounds__(64, 4) void k_preroll(WalkArgs a, uint32_t* ahit, u
 // ===========================================================================
 // Launch wrappers
 // ===========================================================================
-hipError_t launch_walk_files(const WalkArgs& a, hipStream_t s, Profiler* prof) {
+hipError_t launch_walk_files(const WalkArgs& a, hipStream_t s, Profiler* prof, bool slim) {
     if (!a.nunits) return hipSuccess;
-    if (a.n % 64 != 0 || a.n < 256 || a.n > kWalkMaxN || a.fw_max > kWalkMaxWords || (a.fw_max && a.fw_max < 4))
+    if (a.n % 64 != 0 || a.n < 256 || a.n > kWalkMaxN || a.fw_max > kWalkMaxWords || (a.fw_max && a.fw_max < 4) ||
+        (slim && (a.fw_max || !a.ahit)))
         return hipErrorInvalidValue;
     const WalkLds L = walk_lds(a.fw_max);
-    ProfScope ps(prof, s, "k_walk_files");
+    ProfScope ps(prof, s, slim ? "k_walk_files_slim" : "k_walk_files");
     if (a.fw_max)
-        hipLaunchKernelGGL(k_walk_files<true>, dim3(a.nunits), dim3(64), L.total, s, a);
+        hipLaunchKernelGGL((k_walk_files<true, false>), dim3(a.nunits), dim3(64), L.total, s, a);
+    else if (slim)
+        hipLaunchKernelGGL((k_walk_files<false, true>), dim3(a.nunits), dim3(64), L.total, s, a);
     else
-        hipLaunchKernelGGL(k_walk_files<false>, dim3(a.nunits), dim3(64), L.total, s, a);
+        hipLaunchKernelGGL((k_walk_files<false, false>), dim3(a.nunits), dim3(64), L.total, s, a);
     return hipGetLastError();
 }
 

@@ -266,7 +266,12 @@ struct WalkArgs {
     unsigned long long* total;   // records placed in out (zeroed before the launch)
     unsigned long long* ticks;   // SYDELTA_PHASE_TIMING: 16 counters (zeroed), else null
 };
-hipError_t launch_walk_files(const WalkArgs& a, hipStream_t s, Profiler* prof);
+// slim: the walk of units whose aligned misses were pre-rolled (launch_preroll; a.ahit set,
+// the filter in global memory), for the units whose walk stays on the aligned grid; it marks
+// them done (kUnitDone in WalkUnit::final_, the unit table written), and a full launch after it
+// walks the others.  The unit table must not be reused for another slim launch.
+constexpr uint32_t kUnitDone = 2;
+hipError_t launch_walk_files(const WalkArgs& a, hipStream_t s, Profiler* prof, bool slim = false);
 // K10's pre-roll of a chunk's aligned misses: every block r in [b0, b1) (relative to kb)
 // whose aligned probe missed (ahit[r] == kNoBlock) is rolled: the first verified hit among
 // the window starts (x, min(x + n, pend)), x = (kb + r) n, replaces the probe's results:

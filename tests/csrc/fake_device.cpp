@@ -585,8 +585,9 @@ hipError_t launch_chain(const chain::ChainArgs& a, hipStream_t, Profiler*) {
 // [entry, end), every visited window classified exactly, the ops run-length coded as
 // k_walk_files writes them (WalkRec), units placed in order in the compact output.  The
 // aligned probe's results, when given, must agree with the exact classification.
-hipError_t launch_walk_files(const WalkArgs& a, hipStream_t, Profiler*) {
+hipError_t launch_walk_files(const WalkArgs& a, hipStream_t, Profiler*, bool slim) {
     EmuTimer emu_t;
+    if (slim) return a.ahit && !a.fw_max ? hipSuccess : hipErrorInvalidValue;  // the full launch after it walks every unit
     if (a.n % 64 != 0 || a.n < 256 || a.n > kWalkMaxN || a.fw_max > kWalkMaxWords) return hipErrorInvalidValue;
     DeviceIndex key_ix;
     key_ix.keys = (uint32_t*)a.keys;
