@@ -98,6 +98,12 @@ def parse():
                     help="resolve the greedy walks on the device (K5b, SYDELTA_DEVICE_WALK=1; c4/c5/path)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-host-inclusive", action="store_true")
+    ap.add_argument("--no-legs", action="store_true",
+                    help="c3: skip the C4 and C5 legs that follow the headline (their objects in the line)")
+    ap.add_argument("--proxy-world", type=int, default=0,
+                    help="c5 on one GPU: time rank --proxy-rank of a W-rank job (the other ranks' signatures "
+                         "precomputed and concatenated in place of the all-gather; index over all W chunks' keys)")
+    ap.add_argument("--proxy-rank", type=int, default=0)
     a = ap.parse_args()
     if a.device_walk:
         os.environ["SYDELTA_DEVICE_WALK"] = "1"
@@ -686,6 +692,172 @@ def launch_ranks(nranks: int, argv) -> int:
     return rc
 
 
+C4_FILES = 10000  # BASELINE config 4
+
+
+def time_steps(step, steps: int, warmup: int, world: int):
+    """W untimed steps, then exactly K timed ones bracketed by a barrier + synchronize on
+    both sides; the max over ranks.  Returns (seconds, the last step's result)."""
+    import torch
+    import torch.distributed as dist
+
+    for _ in range(warmup):
+        step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    last = None
+    for _ in range(steps):
+        last = step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    el = time.perf_counter() - t0
+    if world > 1:
+        el = max_over_ranks(el, "cuda")
+    return el, last
+
+
+def c4_step(dev, basis, new, files, bs: int, device: int, strm):
+    """One batched call over files = (boff, blen, soff, slen): batched signature, per-file
+    index, batched match (K10 walks every file on the device); strm None = the calling
+    thread's library stream (the call then synchronizes before returning)."""
+    boff, blen, soff, slen = files
+    w, s = dev.signature_batch(basis, boff, blen, bs, stream=strm)
+    nblk = (blen + bs - 1) // bs
+    last = blen - (nblk - 1) * bs
+    idx = dev.BatchIndex(w, s, nblk, last, bs, device=device, stream=strm)
+    # the per-file op lists stay in the library's batch (host memory), as the Rust caller
+    # would read them through the accessors
+    res = dev.match_batch_handle(idx, new, soff, slen, stream=strm)
+    idx.close()
+    tot = res.stats
+    res.close()
+    return tot
+
+
+def c5_setup(dev, n: int, bs: int, edit_ppm: int, world: int, rank: int):
+    """BASELINE config 5: one file of world * n bytes; rank owns basis bytes [rank n,
+    (rank+1) n) and window starts [rank n, (rank+1) n) of the source (+ the next bs-1 bytes
+    as halo).  Counter-based generators give every rank the same bytes for the same file
+    offsets."""
+    import torch
+
+    from sy_amd import shard
+
+    file_len = world * n
+    first = rank * n
+    basis = torch.empty(n, dtype=torch.uint8, device="cuda")
+    dev.synth_fill_range(basis, first, 0x5E1D0005)
+    p0, p1 = shard.chunk_bounds(file_len, bs, world, rank)
+    buf_end = file_len if rank == world - 1 else min(file_len, p1 + bs - 1)
+    new = torch.empty((buf_end - first + 15) // 16 * 16, dtype=torch.uint8, device="cuda")
+    src_view = new[:buf_end - first]
+    dev.synth_fill_range(src_view, first, 0x5E1D0005)
+    dev.synth_mutate_blocks(src_view, src_view, first, bs, 0x5E1D0006, edit_ppm)
+    return dict(basis=basis, new=new, file_len=file_len, first=first, p0=p0, p1=p1)
+
+
+def c5_proxy_signature(dev, c5: dict, n: int, bs: int, world: int, rank: int):
+    """The whole file's signature SoA of a `world`-rank C5 job as rank `rank` would hold it
+    after the all-gather: every other rank's chunk generated and signed here (untimed) into
+    its slot; rank's own slot is written by each timed step."""
+    import torch
+
+    nb = n // bs
+    W = torch.empty(world * nb, dtype=torch.int32, device="cuda")
+    S = torch.empty(world * nb, dtype=torch.int64, device="cuda")
+    tmp = c5["basis"]
+    for g in range(world):
+        if g == rank:
+            continue
+        dev.synth_fill_range(tmp, g * n, 0x5E1D0005)
+        w, s = dev.signature(tmp, bs)
+        W[g * nb:(g + 1) * nb].copy_(w.view(torch.int32))
+        S[g * nb:(g + 1) * nb].copy_(s.view(torch.int64))
+    dev.synth_fill_range(tmp, rank * n, 0x5E1D0005)  # the rank's own basis chunk again
+    torch.cuda.synchronize()
+    return W, S
+
+
+def run_legs(args, dev, world: int, rank: int, device: int, stream) -> dict:
+    """The north star's multi-GPU configs beside the C3 headline, so the driver's
+    `--gpus N` run measures them (BASELINE.json configs 4 and 5):
+      c4: this rank's shard_range of 10 000 x 1 MiB file pairs (no collective; strong
+          scaling: the total is fixed, each rank's share shrinks with N);
+      c5: one 8 GiB chunk per rank of one N x 8 GiB file, bs 8192, 1 % edited blocks:
+          signature, RCCL all-gather of the signature SoA, the full index, the chunk's
+          walk chained over ranks (weak scaling); the all-gather also timed alone.
+    Same steps / warmup as the headline, barrier-bracketed, max over ranks; no CPU
+    baseline (the c4 / c5 workloads report theirs at N=1)."""
+    import torch
+    import torch.distributed as dist
+
+    out = {}
+    # ---- C4
+    lo, hi = shard_range(C4_FILES, world, rank)
+    basis, new, files = c4_files(dev, basis_bytes=1 << 20, nfiles=hi - lo, first=lo)
+    torch.cuda.synchronize()
+    el, last = time_steps(lambda: c4_step(dev, basis, new, files, 4096, device, stream), args.steps, args.warmup,
+                          world)
+    total = C4_FILES * ((1 << 20) + (1 << 20) + 1)  # basis + source bytes of all ranks' files per step
+    out["c4"] = {"workload": "C4: 10000 x 1 MiB files (1-byte insertion + 16 substitutions each), bs 4096, "
+                             "file-sharded (no collective)",
+                 "value": round(total * args.steps / el / GIB, 3), "unit": "GiB/s", "scaling": "strong",
+                 "ms_per_step": round(el / args.steps * 1e3, 4), "files": C4_FILES, "files_this_rank": hi - lo,
+                 "bytes_this_rank_per_step": int(files[1].sum() + files[3].sum()),
+                 "copy_ops_this_rank": int(last["copy_ops"]), "literal_bytes_this_rank": int(last["literal_bytes"])}
+    del basis, new, files, last
+    torch.cuda.empty_cache()
+    # ---- C5
+    n5, bs5, ppm5 = 8 << 30, 8192, 10000
+    c5 = c5_setup(dev, n5, bs5, ppm5, world, rank)
+    from sy_amd import shard
+
+    gather, bcast = shard.torch_collectives(dist, "cuda") if world > 1 else ((lambda v: [v]), (lambda v, src: v))
+    nb = n5 // bs5
+    W = torch.empty(world * nb, dtype=torch.int32, device="cuda") if world > 1 else None
+    S = torch.empty(world * nb, dtype=torch.int64, device="cuda") if world > 1 else None
+
+    def c5_step():
+        w, s = dev.signature(c5["basis"], bs5, stream=stream)
+        if world > 1:  # the one exchange step: RCCL all-gather of the signature SoA
+            dist.all_gather_into_tensor(W, w.view(torch.int32))
+            dist.all_gather_into_tensor(S, s.view(torch.int64))
+            w, s = W.view(w.dtype), S.view(s.dtype)
+        idx = dev.Index(w, s, bs5, bs5, device=device, stream=stream)
+        ch = dev.Chunk(idx, c5["new"], c5["first"], c5["file_len"], c5["p0"], c5["p1"], stream=stream)
+        d, _ = shard.walk_chain(ch, rank, world, c5["p0"], gather, bcast)
+        ch.close()
+        idx.close()
+        return d.stats
+
+    el, st = time_steps(c5_step, args.steps, args.warmup, world)
+    ag_ms = 0.0
+    if world > 1:
+        w0, s0 = dev.signature(c5["basis"], bs5)
+        torch.cuda.synchronize()
+
+        def ag():
+            dist.all_gather_into_tensor(W, w0.view(torch.int32))
+            dist.all_gather_into_tensor(S, s0.view(torch.int64))
+
+        ag_el, _ = time_steps(ag, args.steps, 1, world)
+        ag_ms = ag_el / args.steps * 1e3
+    out["c5"] = {"workload": f"C5: one {world * n5 / GIB:.0f} GiB file, bs {bs5}, 1% of blocks with one substituted "
+                             f"byte; signature + RCCL all-gather + index + chunk walk, chunk-sharded",
+                 "value": round(world * 2 * n5 * args.steps / el / GIB, 3), "unit": "GiB/s", "scaling": "weak",
+                 "ms_per_step": round(el / args.steps * 1e3, 4), "bytes_per_rank_per_step": 2 * n5,
+                 "allgather_ms": round(ag_ms, 4),
+                 "allgather_bytes_per_rank": 12 * nb * world if world > 1 else 0,
+                 "copy_ops_this_rank": int(st["copy_ops"]), "literal_bytes_this_rank": int(st["literal_bytes"])}
+    del c5, W, S
+    torch.cuda.empty_cache()
+    return out
+
+
 def main():
     args = parse()
     if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
@@ -811,27 +983,21 @@ def main():
             fsz = n // args.files
             xxh_offs = np.arange(args.files, dtype=np.uint64) * np.uint64(fsz)
             xxh_lens = np.full(args.files, fsz, dtype=np.uint64)
+    proxy = args.workload == "c5" and args.proxy_world > 1 and world == 1
     if args.workload == "c5":
-        # BASELINE config 5: one file of world * n bytes; this rank owns basis bytes
-        # [rank*n, (rank+1)*n) and window starts [rank*n, (rank+1)*n) of the source
-        # (+ the next bs-1 bytes as halo).  Counter-based generators give every rank
-        # the same bytes for the same file offsets.
         from sy_amd import shard
 
-        file_len = world * n
-        first = rank * n
-        dev.synth_fill_range(basis, first, 0x5E1D0005)
-        p0, p1 = shard.chunk_bounds(file_len, bs, world, rank)
-        buf_end = file_len if rank == world - 1 else min(file_len, p1 + bs - 1)
-        new = torch.empty((buf_end - first + 15) // 16 * 16, dtype=torch.uint8, device="cuda")
-        src_view = new[:buf_end - first]
-        dev.synth_fill_range(src_view, first, 0x5E1D0005)
-        dev.synth_mutate_blocks(src_view, src_view, first, bs, 0x5E1D0006, args.edit_ppm)
+        del basis
+        cw, cr = (args.proxy_world, args.proxy_rank) if proxy else (world, rank)
+        c5 = c5_setup(dev, n, bs, args.edit_ppm, cw, cr)
+        basis, new = c5["basis"], c5["new"]
         if world > 1:
             gather, bcast = shard.torch_collectives(dist, "cuda")
         else:
             gather, bcast = (lambda v: [v]), (lambda v, src: v)
-        c5 = dict(file_len=file_len, first=first, p0=p0, p1=p1, gather=gather, bcast=bcast, shard=shard)
+        c5.update(gather=gather, bcast=bcast, shard=shard, world=cw, rank=cr)
+        if proxy:  # rank cr of a cw-rank job: the others' signatures in place of the all-gather
+            c5["W"], c5["S"] = c5_proxy_signature(dev, c5, n, bs, cw, cr)
     path_files = None
     if args.workload == "path":
         import tempfile
@@ -868,20 +1034,7 @@ def main():
     torch.cuda.set_stream(stream)
 
     def c4_batch(fs, strm):
-        """One batched call over files fs = (boff, blen, soff, slen); strm None = the
-        calling thread's library stream (each call then synchronizes before returning)."""
-        boff, blen, soff, slen = fs
-        w, s = dev.signature_batch(basis, boff, blen, bs, stream=strm)
-        nblk = (blen + bs - 1) // bs
-        last = blen - (nblk - 1) * bs
-        idx = dev.BatchIndex(w, s, nblk, last, bs, device=local, stream=strm)
-        # the per-file op lists stay in the library's batch (host memory), as the
-        # Rust caller would read them through the accessors
-        res = dev.match_batch_handle(idx, new, soff, slen, stream=strm)
-        idx.close()
-        tot = res.stats
-        res.close()
-        return tot
+        return c4_step(dev, basis, new, fs, bs, local, strm)
 
     c4_pool, c4_groups = None, []
     if args.workload == "c4" and args.callers > 1:
@@ -960,6 +1113,11 @@ def main():
             return {"json_bytes": ln.value, "ops": len(json_d.kind)}
         if args.workload == "c5":
             w, s = dev.signature(basis, bs, stream=stream)
+            if proxy:  # this rank's slot of the whole signature (the all-gather's result, untimed)
+                nb = w.numel()
+                c5["W"][cr * nb:(cr + 1) * nb].copy_(w.view(torch.int32))
+                c5["S"][cr * nb:(cr + 1) * nb].copy_(s.view(torch.int64))
+                w, s = c5["W"].view(w.dtype), c5["S"].view(s.dtype)
             if world > 1:  # the one exchange step: RCCL all-gather of the signature SoA
                 W = torch.empty(world * w.numel(), dtype=w.dtype, device="cuda")
                 S = torch.empty(world * s.numel(), dtype=s.dtype, device="cuda")
@@ -968,7 +1126,10 @@ def main():
                 w, s = W, S
             idx = dev.Index(w, s, bs, bs, device=local, stream=stream)
             ch = dev.Chunk(idx, new, c5["first"], c5["file_len"], c5["p0"], c5["p1"], stream=stream)
-            d, entry = c5["shard"].walk_chain(ch, rank, world, c5["p0"], c5["gather"], c5["bcast"])
+            if proxy:
+                d, _ = ch.walk(c5["p0"])  # (its chain entry is its start: block-aligned copies)
+            else:
+                d, entry = c5["shard"].walk_chain(ch, rank, world, c5["p0"], c5["gather"], c5["bcast"])
             ch.close()
             idx.close()
             return d
@@ -1071,11 +1232,24 @@ def main():
                                                ceil["information_bound"]["value_GiBps"], 4))
     kernels = {k: {"avg_ms": round(v["ms"] / max(1, v["count"]), 4), "launches": v["count"]} for k, v in prof.items()}
 
+    legs = None
+    if args.workload == "c3" and not args.no_legs:
+        # the headline's buffers go first (the legs need ~20 GiB for C4, ~17 GiB for C5)
+        cpu_src = None
+        if rank == 0 and world == 1 and not args.no_cpu_baseline:
+            cpu_src = (basis[:nb_bytes].cpu().numpy(), new[:min(new.numel(), 256 << 20)].cpu().numpy(), new.numel())
+        basis = new = last = None
+        torch.cuda.empty_cache()
+        legs = run_legs(args, dev, world, rank, local, stream)
+
     if rank == 0:
         cpu = None
         if world == 1 and not args.no_cpu_baseline and args.workload in ("c3", "c3b"):
-            cpu = cpu_baseline(basis[:nb_bytes].cpu().numpy(), new[:min(new.numel(), 256 << 20)].cpu().numpy(),
-                               new.numel(), bs)
+            if legs is not None:
+                cpu = cpu_baseline(*cpu_src, bs)
+            else:
+                cpu = cpu_baseline(basis[:nb_bytes].cpu().numpy(), new[:min(new.numel(), 256 << 20)].cpu().numpy(),
+                                   new.numel(), bs)
         if world == 1 and not args.no_cpu_baseline and args.workload == "c4":
             k = min(500, len(files[0]))  # the sampled files' bytes only
             cpu = cpu_c4_baseline(basis[:int(files[0][k - 1] + files[1][k - 1])].cpu().numpy(),
@@ -1095,7 +1269,7 @@ def main():
         if world == 1 and not args.no_cpu_baseline and args.workload == "local":
             cpu = cpu_local_baseline(new, basis, bs)
         hinc = None
-        if world == 1 and not args.no_host_inclusive and args.workload == "c3":
+        if world == 1 and not args.no_host_inclusive and args.workload == "c3" and not proxy:
             hinc = host_inclusive(dev, bs, min(n, 1 << 30), local)
         sig_ms = kernels.get("k_sig_fast", {}).get("avg_ms")
         line = {
@@ -1121,8 +1295,14 @@ def main():
                     "c2": "C2: signature only over 4 GiB, bs 4096",
                     "c4": f"C4: {args.files} x 1 MiB files (1-byte insertion + 16 substitutions each), "
                           f"batched signature + per-file index + batched match, file-sharded over ranks",
-                    "c5": f"C5: one {world * n / GIB:.0f} GiB file, bs {bs}, {args.edit_ppm / 1e4:g}% of blocks with "
-                          f"one substituted byte; signature + all-gather + index + chunk match, chunk-sharded",
+                    "c5": (f"C5 rank proxy: rank {args.proxy_rank} of a {args.proxy_world}-rank job on one GPU -- its "
+                           f"{n / GIB:.0f} GiB chunk of one {args.proxy_world * n / GIB:.0f} GiB file, bs {bs}, "
+                           f"{args.edit_ppm / 1e4:g}% of blocks with one substituted byte: signature of its chunk + "
+                           f"index over the whole file's {args.proxy_world * (n // bs)} keys (the other ranks' "
+                           f"signatures precomputed in place of the all-gather, untimed) + its chunk's walk; value = "
+                           f"this rank's bytes / its step time" if proxy else
+                           f"C5: one {world * n / GIB:.0f} GiB file, bs {bs}, {args.edit_ppm / 1e4:g}% of blocks with "
+                           f"one substituted byte; signature + all-gather + index + chunk match, chunk-sharded"),
                     "apply": f"apply_delta on the device: {n / GIB:.0f} GiB reconstructed from a bs {bs} delta "
                              f"({args.edit_ppm / 1e4:g}% of blocks edited), per rank",
                     "xxh3": (f"integrity: whole-file XXH3-64 of {args.files} x {n // max(1, args.files) >> 20} MiB "
@@ -1157,6 +1337,9 @@ def main():
             "roofline": roof,
             "cpu_baseline": cpu,
             "host_inclusive": hinc,
+            **({"cpu_baseline_note": "rank 0 at N=1 only: a world > 1 run reports no CPU baseline and no "
+                                     "host-inclusive rate"} if world > 1 else {}),
+            **(legs or {}),
             "kernels": kernels,
             "signature_only_gibps": round(n / (sig_ms * 1e-3) / GIB, 2) if sig_ms else None,
             "match_stats": stats,

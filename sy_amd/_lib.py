@@ -10,10 +10,6 @@ import os
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(HERE, "libsydelta.so")
-# SYDELTA_LIB_VARIANT=<name>: an A/B build of the same sources with other compile-time
-# choices (python -m sy_amd.build --variant <name>; measurement only)
-if os.environ.get("SYDELTA_LIB_VARIANT"):
-    LIB_PATH = os.path.join(HERE, "variants", "libsydelta_%s.so" % os.environ["SYDELTA_LIB_VARIANT"])
 
 SYDELTA_OK = 0
 SYDELTA_E_NODEV = -1

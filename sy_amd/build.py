@@ -60,37 +60,5 @@ def build(force: bool = False, verbose: bool = False) -> str:
     return LIB
 
 
-# A/B builds (measurement only): the kernels TU with extra defines, linked with the same
-# host objects into sy_amd/variants/libsydelta_<name>.so (loaded with SYDELTA_LIB_VARIANT).
-VARIANTS = {
-    "l2b3": ["-DSYDELTA_L2_BITS=3"],        # level-2 words with three bits per key (rounds 1-3)
-    "rownt": ["-DSYDELTA_ROW_NONTEMPORAL"],  # the register scans' row loads non-temporal
-}
-
-
-def build_variant(name: str) -> str:
-    build()
-    hipcc = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
-    out_dir = os.path.join(HERE, "variants")
-    os.makedirs(out_dir, exist_ok=True)
-    obj = os.path.join(OBJDIR, f"sydelta_kernels_{name}.o")
-    cmd = [hipcc, f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-Wall", "-Wno-unused-result",
-           "-I", os.path.join(ROOT, "include")] + VARIANTS[name] + ["-x", "hip", "-c",
-                                                                    os.path.join(CSRC, SOURCES[0]), "-o", obj]
-    r = subprocess.run(cmd, stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True)
-    if r.returncode != 0:
-        raise RuntimeError(f"hipcc failed:\n{r.stdout}")
-    objs = [obj] + [os.path.join(OBJDIR, f.rsplit(".", 1)[0] + ".o") for f in SOURCES[1:]]
-    lib = os.path.join(out_dir, f"libsydelta_{name}.so")
-    r = subprocess.run([hipcc, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", lib] + objs,
-                       stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True)
-    if r.returncode != 0:
-        raise RuntimeError(f"link failed:\n{r.stdout}")
-    return lib
-
-
 if __name__ == "__main__":
-    if "--variant" in sys.argv:
-        print(build_variant(sys.argv[sys.argv.index("--variant") + 1]))
-    else:
-        print(build(force="--force" in sys.argv, verbose=True))
+    print(build(force="--force" in sys.argv, verbose=True))

@@ -72,6 +72,9 @@ std::mutex g_dev_mu;
 std::map<int, std::unique_ptr<DevState>> g_devs;
 constexpr int kMaxPoolDevices = 64;
 hipMemPool_t g_pools[kMaxPoolDevices] = {};  // written once per device under its call_once
+// K10's wave slots per device: CUs x 4 SIMDs x 4 waves (k_walk_files' __launch_bounds__(64, 4));
+// 4096 on MI355X's 256 CUs (written under the device's call_once, like g_pools)
+uint32_t g_wave_slots[kMaxPoolDevices] = {};
 
 int ensure_device_impl(int device) {
     if (device < 0) device = 0;
@@ -124,6 +127,7 @@ int ensure_device_impl(int device) {
         keep <<= 20;
         (void)hipMemPoolSetAttribute(pool, hipMemPoolAttrReleaseThreshold, &keep);
         g_pools[device] = pool;
+        g_wave_slots[device] = (uint32_t)std::max(64, prop.multiProcessorCount * 16);
         st->status = SYDELTA_OK;
     });
     if (st->status != SYDELTA_OK) return fail(st->status, "%s", st->msg.c_str());
@@ -200,6 +204,9 @@ int sydelta::host_exception() {
     }
 }
 hipStream_t sydelta::thread_stream(int device) { return thread_stream_impl(device); }
+uint32_t sydelta::wave_slots(int device) {
+    return device >= 0 && device < kMaxPoolDevices && g_wave_slots[device] ? g_wave_slots[device] : 4096u;
+}
 
 namespace sydelta {
 // Timing events are recycled: creating and destroying HIP events per launch costs
@@ -610,12 +617,30 @@ struct sydelta_index {
     // queues meanwhile -- C5's aligned probe of the source -- overlaps the build.
     hipEvent_t ready = nullptr;
     PinnedHits stage;  // the file tables' upload (mapped; returned at release)
+    uint64_t max_nblk = 0;  // the most blocks of any file
+    // A batch whose walks are self-indexed (K10 builds each file's filter and table in LDS from
+    // the signature, sydelta_filewalk.hip) defers its filters and tables until a match takes
+    // another path (index_full): a C4 step then has no index build at all.
+    bool deferred = false;
+    std::mutex build_mu;
 };
 
 namespace {
 // Order `s` after the index build (a no-op for an index built synchronously).
 hipError_t index_wait(const sydelta_index* x, hipStream_t s) {
     return x->ready ? hipStreamWaitEvent(s, x->ready, 0) : hipSuccess;
+}
+// A deferred index's filters and tables, built on `s` (after its copies) for a match that needs
+// them; later users order themselves after the build through `ready`.
+int index_full(sydelta_index* x, hipStream_t s) {
+    std::lock_guard<std::mutex> lk(x->build_mu);
+    if (!x->deferred) return SYDELTA_OK;
+    HIP_TRY(index_wait(x, s));
+    CallProf cp;
+    HIP_TRY(launch_index_build(x->d_weak, x->d_strong, x->ix, s, cp.get()));
+    if (x->ready) HIP_TRY(hipEventRecord(x->ready, s));
+    x->deferred = false;
+    return SYDELTA_OK;
 }
 }  // namespace
 
@@ -683,10 +708,8 @@ int take_mapped(size_t bytes, PinnedHits& out, PinKind kind = kMapped) {
     }
     out = PinnedHits();
     const size_t want = bytes + bytes / 4;
-    static const bool nc = getenv("SYDELTA_MAPPED_NC") != nullptr;  // A/B: non-coherent mapping
     const unsigned flags = kind == kStage ? hipHostMallocDefault
-                                          : hipHostMallocMapped | hipHostMallocPortable |
-                                                (nc ? hipHostMallocNonCoherent : hipHostMallocCoherent);
+                                          : hipHostMallocMapped | hipHostMallocPortable | hipHostMallocCoherent;
     HIP_TRY(hipHostMalloc((void**)&out.p, want, flags));
     out.bytes = want;
     return SYDELTA_OK;
@@ -995,10 +1018,12 @@ static int index_create_impl(int device, const uint32_t* weak, const uint64_t* s
     if (block_size == 0) return fail(SYDELTA_E_INVAL, "block_size must be > 0");
     if (nfiles == 0 || nfiles >= 0xFFFFFFFFull) return fail(SYDELTA_E_INVAL, "bad file count %llu", (unsigned long long)nfiles);
     std::vector<uint64_t> fblk(nfiles + 1, 0);
+    uint64_t max_nblk = 0;
     for (uint64_t f = 0; f < nfiles; ++f) {
         if (nblk[f] && (last[f] == 0 || last[f] > block_size))
             return fail(SYDELTA_E_INVAL, "file %llu: last_size must be in [1, block_size]", (unsigned long long)f);
         fblk[f + 1] = fblk[f] + nblk[f];
+        max_nblk = std::max(max_nblk, nblk[f]);
     }
     const uint64_t nblocks = fblk[nfiles];
     if (nblocks && (!weak || !strong)) return fail(SYDELTA_E_INVAL, "NULL signature arrays");
@@ -1011,6 +1036,7 @@ static int index_create_impl(int device, const uint32_t* weak, const uint64_t* s
     x->bs = block_size;
     x->nfiles = nfiles;
     x->fblk = fblk;
+    x->max_nblk = max_nblk;
     x->last_size.resize(nfiles);
     DeviceIndex& ix = x->ix;
     ix.nfiles = nfiles;
@@ -1104,12 +1130,10 @@ static int index_create_impl(int device, const uint32_t* weak, const uint64_t* s
         HIP_TRY(hipMemcpyAsync(x->d_weak, weak, 4 * nblocks, kind, s));
         HIP_TRY(hipMemcpyAsync(x->d_strong, strong, 8 * nblocks, kind, s));
     }
-    // device arrays: nothing waited for here (SYDELTA_INDEX_SYNC=1: on the caller's stream,
-    // synchronized, as for host arrays).  One file is built on this thread's aux stream; a
+    // device arrays: nothing waited for here.  One file is built on this thread's aux stream; a
     // batch's index, used at once by its match, in the caller's stream order (more streams per
     // caller share the process's four hardware queues with ten callers' work).
-    static const bool index_sync = getenv("SYDELTA_INDEX_SYNC") && getenv("SYDELTA_INDEX_SYNC")[0] == '1';
-    if (arrays_on_device && !index_sync) {
+    if (arrays_on_device) {
         const size_t fb = sizeof(FileIx) * nfiles, tb = ((fb + 15) & ~(size_t)15) + 8 * (nfiles + 1);
         if (int r = take_mapped(tb, x->stage, kStage)) return r;
         memcpy(x->stage.p, ix.files.data(), fb);
@@ -1124,8 +1148,14 @@ static int index_create_impl(int device, const uint32_t* weak, const uint64_t* s
         HIP_TRY(stream_after(sb, s, device));
         x->ready = take_event(device);
         if (!x->ready) return fail(SYDELTA_E_OOM, "no event for the index build");
-        CallProf cp;
-        HIP_TRY(launch_index_build(x->d_weak, x->d_strong, ix, sb, cp.get()));
+        // a batch of small files whose walks self-index (file_walk_ok's index conditions): the
+        // build waits for a match that takes another path (index_full)
+        x->deferred = nfiles >= 2 && block_size % 64 == 0 && block_size >= 256 && block_size <= kWalkMaxN &&
+                      max_nblk <= kSelfIxMaxBlocks && !ix.l1;
+        if (!x->deferred) {
+            CallProf cp;
+            HIP_TRY(launch_index_build(x->d_weak, x->d_strong, ix, sb, cp.get()));
+        }
         HIP_TRY(hipEventRecord(x->ready, sb));
         *out = x.release();
         return SYDELTA_OK;
@@ -2371,7 +2401,7 @@ bool file_walk_ok(const sydelta_index* ix, const uint64_t* src_off, const uint64
     const int mode = file_walk_mode();
     if (mode == 0) return false;
     const uint64_t n = ix->bs, nf = ix->nfiles;
-    if (ix->ix.l1 || n % 64 != 0 || n < 256 || n > kWalkMaxN || ix->ix.max_fwords > kWalkMaxWords || nf >= (1u << 31))
+    if (ix->ix.l1 || n % 64 != 0 || n < 256 || n > kWalkMaxN || ix->max_nblk > kSelfIxMaxBlocks || nf >= (1u << 31))
         return false;
     // one workgroup walks a file: many files, none large (auto mode)
     if (mode < 0 && nf < 64) return false;
@@ -2451,7 +2481,7 @@ static int run_walk(sydelta_index* ix, const uint8_t* base, const std::vector<Wa
     a.nunits = (uint32_t)nu;
     a.n = (uint32_t)ix->bs;
     a.nm = (uint32_t)(ix->bs % 65521);
-    a.fw_max = lds_filter ? std::max<uint32_t>(4, ix->ix.max_fwords) : 0;
+    a.self_nb = lds_filter ? (uint32_t)std::max<uint64_t>(1, ix->max_nblk) : 0u;
     a.files = ix->ix.d_files;
     a.fblk = ix->ix.d_fblk;
     a.filt = ix->ix.filt;
@@ -2464,13 +2494,9 @@ static int run_walk(sydelta_index* ix, const uint8_t* base, const std::vector<Wa
     a.strong = ix->d_strong;
     a.ahit = ahit;
     a.apw = apw;
-    // SYDELTA_WALK_D2H=1 (A/B): results in device memory, copied down in two round trips
-    static const bool d2h = getenv("SYDELTA_WALK_D2H") && getenv("SYDELTA_WALK_D2H")[0] == '1';
-    uint8_t* dres = nullptr;
-    if (d2h) HIP_TRY(dev_malloc_async((void**)&dres, m_need + 256, s));
     a.stage = (WalkRec*)(D + o_stage);
-    a.out = (WalkRec*)((d2h ? dres : wm.p) + m_rec);
-    a.fout = (WalkFileOut*)(d2h ? dres : wm.p);
+    a.out = (WalkRec*)(wm.p + m_rec);
+    a.fout = (WalkFileOut*)wm.p;
     a.total = (unsigned long long*)(D + o_total);
     a.ticks = timing ? a.total + 1 : nullptr;
     HIP_TRY(launch_walk_files(a, s, prof));
@@ -2481,15 +2507,6 @@ static int run_walk(sydelta_index* ix, const uint8_t* base, const std::vector<Wa
         fprintf(stderr, "sydelta file walk phases (wave ticks, 100 MHz, summed over units): setup %llu hash %llu "
                 "lookup %llu stage %llu roll %llu verify %llu out %llu | passes %llu windows %llu rolls %llu "
                 "verify batches %llu\n", tk[0], tk[1], tk[2], tk[3], tk[4], tk[5], tk[6], tk[8], tk[9], tk[10], tk[11]);
-    }
-    if (d2h) {
-        HIP_TRY(hipMemcpyAsync(wm.p, dres, fout_bytes, hipMemcpyDeviceToHost, s));
-        HIP_TRY(hipMemcpyAsync(wm.p + fout_bytes, a.total, 8, hipMemcpyDeviceToHost, s));
-        HIP_TRY(hipStreamSynchronize(s));
-        const uint64_t nr = *(const uint64_t*)(wm.p + fout_bytes);
-        if (nr > rec_total) return fail(SYDELTA_E_KERNEL, "walk: record count past the capacity");
-        if (nr) HIP_TRY(hipMemcpyAsync(wm.p + m_rec, dres + m_rec, sizeof(WalkRec) * nr, hipMemcpyDeviceToHost, s));
-        (void)hipFreeAsync(dres, s);
     }
     HIP_TRY(hipStreamSynchronize(s));
     res.ms_kernel = ms_since(t0);
@@ -2552,10 +2569,10 @@ static inline uint64_t records_ops(const WalkRec* r0, const WalkRec* r1) {
 // segments per file walk in 0.55 ms, four (5000 units, a second round) in 0.65.  nf counts
 // the files of every batch walking at the time (concurrent callers share the chip).
 std::atomic<uint64_t> g_walking_files{0};
-static uint64_t file_segs(uint64_t nf) {
+static uint64_t file_segs(uint64_t nf, int device) {
     const char* e = getenv("SYDELTA_FILE_SEGS");  // read per call (tests switch it)
     if (e && *e) return std::max<uint64_t>(1, strtoull(e, nullptr, 10));
-    return std::max<uint64_t>(1, std::min<uint64_t>(64, 4096 / std::max<uint64_t>(nf, 1)));
+    return std::max<uint64_t>(1, std::min<uint64_t>(64, wave_slots(device) / std::max<uint64_t>(nf, 1)));
 }
 
 // The batched match with the walk on the device: one unit per file, or per segment of a
@@ -2583,7 +2600,7 @@ static int match_walk_files(sydelta_index* ix, const uint8_t* d_buf, const uint6
         peak.store(walking.total);
         peak_ms.store(now_ms);
     }
-    const uint64_t G = file_segs(std::max(walking.total, peak.load())), min_seg = (getenv("SYDELTA_FILE_SEGS") && *getenv("SYDELTA_FILE_SEGS")) ? 8 : 32;
+    const uint64_t G = file_segs(std::max(walking.total, peak.load()), ix->device), min_seg = (getenv("SYDELTA_FILE_SEGS") && *getenv("SYDELTA_FILE_SEGS")) ? 8 : 32;
     std::vector<WalkUnit> units;
     units.reserve(nf * G);
     std::vector<uint64_t> fu(nf + 1, 0);  // file f's units: [fu[f], fu[f+1])
@@ -2740,8 +2757,9 @@ static int match_walk_files(sydelta_index* ix, const uint8_t* d_buf, const uint6
 
 // Match source f (d_buf[src_off[f] .. +src_len[f])) against file f of the index,
 // for every f; results in b->d[f].
+// mode: the classifier's probe mode (-2: SYDELTA_PROBE's, probe_mode_env)
 static int match_impl(sydelta_index* ix, const uint8_t* d_buf, const uint64_t* src_off, const uint64_t* src_len,
-                      hipStream_t s, sydelta_delta_batch* b) {
+                      hipStream_t s, sydelta_delta_batch* b, int mode_hint = -2) {
     ScratchHold hold;  // the probe scratch is used until the walks end
     const auto t_begin = std::chrono::steady_clock::now();
     CallProf cp;
@@ -2786,9 +2804,10 @@ static int match_impl(sydelta_index* ix, const uint8_t* d_buf, const uint64_t* s
     }
     b->total.positions = tot_pos;
     if (file_walk_ok(ix, src_off, src_len, d_buf)) return match_walk_files(ix, d_buf, src_off, src_len, s, C.prof, b);
+    if (int r = index_full(ix, s)) return r;  // the classifier's probes and scans read the tables
     static const bool host_timing = getenv("SYDELTA_HOST_TIMING") != nullptr;
     const auto t0 = std::chrono::steady_clock::now();
-    const int mode = n > scan_max_window() && !wide_scan(ix) ? 0 : probe_mode_env();
+    const int mode = n > scan_max_window() && !wide_scan(ix) ? 0 : mode_hint != -2 ? mode_hint : probe_mode_env();
     if (int r = C.classify(mode)) return r;
     const double t_cls = ms_since(t0);
     std::vector<size_t> all(nf);
@@ -2849,6 +2868,87 @@ static int match_impl(sydelta_index* ix, const uint8_t* d_buf, const uint64_t* s
     return SYDELTA_OK;
 }
 
+namespace {
+bool chunk_walk_ok(const sydelta_index* idx);  // (below)
+
+// Is a single source copy-heavy, so that K10 walks it (as one chunk, sydelta_chunk_classify)
+// instead of the classifier scanning every window start (k_scan_r: a literal-heavy source such
+// as C3)?  Yes when 1/8 or more of a 1-in-16 sample of its aligned windows hit (the
+// classifier's own probe rule), or -- a shifted source, where insertions put every later window
+// off the block grid (C3b) -- when 1/4 or more of 256 consecutive blocks mid-file find a hit
+// among their window starts (the walk's roll, k_preroll, on each missed block).  The index
+// must be built (the caller waited for it).
+int copy_heavy(sydelta_index* ix, const uint8_t* d_src, uint64_t len, hipStream_t s, Profiler* prof, bool* heavy) {
+    *heavy = false;
+    const uint64_t n = ix->bs, npos = len - n + 1, nblk = (npos + n - 1) / n;
+    const uint32_t S = 16;
+    const uint64_t np1 = (nblk + S - 1) / S, np2 = std::min<uint64_t>(256, nblk), r0 = (nblk - np2) / 2;
+    ScratchHold hold;
+    int cur = 0;
+    HIP_TRY(hipGetDevice(&cur));
+    DevScratch& sc = thread_probe_scratch(cur);
+    auto al = [](size_t v) { return (v + 255) & ~(size_t)255; };
+    const size_t o_jobs = 0, o_out1 = 256, o_pw1 = o_out1 + al(4 * np1), o_pst1 = o_pw1 + al(4 * np1);
+    const size_t o_out2 = o_pst1 + al(8 * np1), o_pw2 = o_out2 + al(4 * np2), o_pst2 = o_pw2 + al(4 * np2);
+    const size_t o_list = o_pst2 + al(8 * np2), o_cnt = o_list + al(4 * np2), need = o_cnt + 256;
+    if (sc.bytes < need) {
+        if (sc.p) (void)hipFreeAsync(sc.p, s);
+        sc = DevScratch();
+        HIP_TRY(dev_malloc_async(&sc.p, need + need / 4, s));
+        sc.bytes = need + need / 4;
+    }
+    uint8_t* D = (uint8_t*)sc.p;
+    PinnedHits& pin = thread_probe_pin();
+    if (int r = pinned_at_least(pin, std::max<size_t>(4 * np1, 4 * np2) + 256)) return r;
+    ProbeJob* jobs = (ProbeJob*)(pin.p + al(std::max<size_t>(4 * np1, 4 * np2)));  // the uploads' staging
+    jobs[0] = ProbeJob{0, 0, 0, 0, 0};
+    jobs[1] = ProbeJob{0, r0, 0, 0, 0};
+    HIP_TRY(hipMemcpyAsync(D + o_jobs, jobs, 2 * sizeof(ProbeJob), hipMemcpyHostToDevice, s));
+    HIP_TRY(hipMemsetAsync(D + o_cnt, 0, 8, s));
+    const bool fast = ((uintptr_t)d_src & 15) == 0;
+    HIP_TRY(launch_probe(d_src, (const ProbeJob*)(D + o_jobs), 1, np1, S, (uint32_t)n, fast, ix->ix,
+                         (uint32_t*)(D + o_pw1), (uint64_t*)(D + o_pst1), (uint32_t*)(D + o_out1), s, prof));
+    uint32_t* h = (uint32_t*)pin.p;
+    HIP_TRY(hipMemcpyAsync(h, D + o_out1, 4 * np1, hipMemcpyDeviceToHost, s));
+    HIP_TRY(hipStreamSynchronize(s));
+    uint64_t hits = 0;
+    for (uint64_t i = 0; i < np1; ++i) hits += h[i] != kNoBlk;
+    if (hits * 8 >= np1) {
+        *heavy = true;
+        return SYDELTA_OK;
+    }
+    // the shifted sample: 256 consecutive aligned windows, each miss rolled for its first hit
+    uint32_t* d_out2 = (uint32_t*)(D + o_out2);
+    uint32_t* d_pw2 = (uint32_t*)(D + o_pw2);
+    HIP_TRY(launch_probe(d_src, (const ProbeJob*)(D + o_jobs) + 1, 1, np2, 1, (uint32_t)n, fast, ix->ix, d_pw2,
+                         (uint64_t*)(D + o_pst2), d_out2, s, prof));
+    const DeviceIndex& di = ix->ix;
+    WalkArgs a{};
+    a.base = d_src;
+    a.n = (uint32_t)n;
+    a.nm = (uint32_t)(n % 65521);
+    a.files = di.d_files;
+    a.fblk = di.d_fblk;
+    a.filt = di.filt;
+    a.keys = di.keys;
+    a.start = di.start;
+    a.cnt = di.cnt;
+    a.order = di.order;
+    a.cstrong = di.cstrong;
+    a.weak = ix->d_weak;
+    a.strong = ix->d_strong;
+    if (ix->fblk[1] < kPreMark)
+        HIP_TRY(launch_preroll(a, d_out2, d_pw2, r0, 0, np2, npos, len, (uint32_t*)(D + o_list),
+                               (unsigned long long*)(D + o_cnt), (uint32_t)np2, np2, s, prof));
+    HIP_TRY(hipMemcpyAsync(h, d_out2, 4 * np2, hipMemcpyDeviceToHost, s));
+    HIP_TRY(hipStreamSynchronize(s));
+    hits = 0;
+    for (uint64_t i = 0; i < np2; ++i) hits += h[i] != kNoBlk && h[i] != kPreNone;
+    *heavy = hits * 4 >= np2;
+    return SYDELTA_OK;
+}
+}  // namespace
+
 extern "C" int sydelta_match_device(sydelta_index* idx, const uint8_t* d_src, uint64_t len, void* stream,
                                     sydelta_delta** out) try {
     if (!idx || !out) return fail(SYDELTA_E_INVAL, "NULL argument");
@@ -2862,7 +2962,29 @@ extern "C" int sydelta_match_device(sydelta_index* idx, const uint8_t* d_src, ui
     const uint64_t off = 0;
     static const bool host_timing = getenv("SYDELTA_HOST_TIMING") != nullptr;
     const auto t0 = std::chrono::steady_clock::now();
-    if (int r = match_impl(idx, d_src, &off, &len, s, &b)) return r;
+    int mode = -2;
+    // a copy-heavy source is walked by K10 as one chunk (generator.rs:116-221 on the device);
+    // a literal-heavy one by the classifier, whose probe sample would say the same (mode 0)
+    if (chunk_walk_ok(idx) && probe_mode_env() < 0 && len >= idx->bs && idx->fblk[1] > 0 &&
+        ((uintptr_t)d_src & 15) == 0) {
+        HIP_TRY(index_wait(idx, s));
+        bool heavy = false;
+        {
+            CallProf cp;
+            if (int r = copy_heavy(idx, d_src, len, s, cp.get(), &heavy)) return r;
+        }
+        if (heavy) {
+            sydelta_chunk* ch = nullptr;
+            if (int r = sydelta_chunk_classify(idx, d_src, 0, len, len, 0, len, s, &ch)) return r;
+            uint64_t exit = 0;
+            const int r = sydelta_chunk_walk(ch, 0, &exit, out);
+            sydelta_chunk_free(ch);
+            if (host_timing) fprintf(stderr, "sydelta match_device (K10): %.3f ms\n", ms_since(t0));
+            return r;
+        }
+        mode = 0;
+    }
+    if (int r = match_impl(idx, d_src, &off, &len, s, &b, mode)) return r;
     *out = new sydelta_delta(std::move(b.d[0]));
     if (host_timing) fprintf(stderr, "sydelta match_device: %.3f ms (with the classifier's release)\n", ms_since(t0));
     return SYDELTA_OK;
@@ -3649,23 +3771,19 @@ namespace {
 // last 30 %: 315 K blocks): 96 blocks 4.105-4.112 ms per step, 80: 4.20-4.23, 64 (two
 // rounds): 4.19-4.33, 128: 4.22-4.33 (`profiles/r05zz9_*`).
 uint64_t chunk_seg_blocks();
-uint64_t chunk_seg_last_blocks(uint64_t last_blocks) {
-    static const uint64_t forced = [] {
-        const char* e = getenv("SYDELTA_CHUNK_SEG_LAST");
-        const uint64_t x = (e && *e) ? strtoull(e, nullptr, 10) : 0;
-        return (x >= 8 && x <= 1024) ? x : (uint64_t)0;
-    }();
-    const uint64_t v = forced ? forced : std::max<uint64_t>(32, (last_blocks + 3299) / 3300);
+uint64_t chunk_seg_last_blocks(uint64_t last_blocks, int device) {
+    const char* e = getenv("SYDELTA_CHUNK_SEG_LAST");  // (knobs are read per call: tests switch them)
+    const uint64_t x = (e && *e) ? strtoull(e, nullptr, 10) : 0;
+    const uint64_t forced = (x >= 8 && x <= 1024) ? x : 0;
+    const uint64_t round = std::max<uint64_t>(1, wave_slots(device) * 4 / 5);  // 3276 units at 4096 slots
+    const uint64_t v = forced ? forced : std::max<uint64_t>(32, (last_blocks + round - 1) / round);
     return std::min(v, chunk_seg_blocks());
 }
 // blocks per segment (SYDELTA_CHUNK_SEG overrides; a power of two from 8 to 1024)
 uint64_t chunk_seg_blocks() {
-    static const uint64_t v = [] {
-        const char* e = getenv("SYDELTA_CHUNK_SEG");
-        const uint64_t x = (e && *e) ? strtoull(e, nullptr, 10) : 128;
-        return (x >= 8 && x <= 1024 && (x & (x - 1)) == 0) ? x : (uint64_t)128;
-    }();
-    return v;
+    const char* e = getenv("SYDELTA_CHUNK_SEG");
+    const uint64_t x = (e && *e) ? strtoull(e, nullptr, 10) : 128;
+    return (x >= 8 && x <= 1024 && (x & (x - 1)) == 0) ? x : (uint64_t)128;
 }
 bool chunk_walk_ok(const sydelta_index* idx) {
     const char* e = getenv("SYDELTA_CHUNK_WALK");
@@ -3687,7 +3805,9 @@ void chunk_units(const sydelta_chunk* ch, uint64_t from, std::vector<WalkUnit>& 
     do {
         const uint64_t e = std::min(c.p1, s0 + seg), en = std::max(lo, s0);
         const bool last = e >= c.p1;
-        units.push_back(WalkUnit{0, ch->file_len, en, std::max(e, en), c.p1, rec, c.kb, 0,
+        // len: the readable end of the chunk's buffer (c.len), which bounds the walk's loads; the
+        // final unit's is the file's length (its tail rule and last literal run need it)
+        units.push_back(WalkUnit{0, c.len, en, std::max(e, en), c.p1, rec, c.kb, 0,
                                  (uint32_t)(last && ch->final_src)});
         rec += 2 * ((std::max(e, en) - en) / n) + 4;
         s0 = e;
@@ -3697,26 +3817,18 @@ void chunk_units(const sydelta_chunk* ch, uint64_t from, std::vector<WalkUnit>& 
 // The pre-roll of a chunk's aligned misses before the last part's walk (launch_preroll): one
 // wave per miss rolls it, so that walk, which ends the pipeline, takes each miss's result
 // instead of rolling its misses in turn.  SYDELTA_PREROLL=0: off; 2: before every part's
-// walk.  SYDELTA_PREROLL_WAVES: its grid (4096).
+// walk.  Its grid: the device's wave slots.
 bool preroll_on() {
-    static const bool v = !getenv("SYDELTA_PREROLL") || getenv("SYDELTA_PREROLL")[0] != '0';
-    return v;
+    const char* e = getenv("SYDELTA_PREROLL");
+    return !e || e[0] != '0';
 }
 bool preroll_all() {  // SYDELTA_PREROLL=2: every part's (else the last part's: the others' walks are hidden)
-    static const bool v = getenv("SYDELTA_PREROLL") && getenv("SYDELTA_PREROLL")[0] == '2';
-    return v;
+    const char* e = getenv("SYDELTA_PREROLL");
+    return e && e[0] == '2';
 }
 bool slim_walk() {  // SYDELTA_SLIM_WALK=0: a pre-rolled part walked by the full kernel alone
-    static const bool v = !getenv("SYDELTA_SLIM_WALK") || getenv("SYDELTA_SLIM_WALK")[0] != '0';
-    return v;
-}
-uint32_t preroll_waves() {
-    static const uint32_t v = [] {
-        const char* e = getenv("SYDELTA_PREROLL_WAVES");
-        const long x = (e && *e) ? atol(e) : 4096;
-        return (uint32_t)std::min(65536L, std::max(1L, x));
-    }();
-    return v;
+    const char* e = getenv("SYDELTA_SLIM_WALK");
+    return !e || e[0] != '0';
 }
 
 // Sub-ranges of a chunk's walk: 2 from 512 segments (SYDELTA_CHUNK_PIPE=K).  At C5 (8192
@@ -3749,24 +3861,8 @@ int chunk_pipe_launch(sydelta_chunk* ch, uint64_t from, bool probe) {
     // own walk, which ends the pipeline, is the shorter: 4.11-4.12 ms per step at C5 against
     // 4.26-4.43 for halves, `profiles/r05zs_*`, `r05zt_*`)
     if (K == 2) P.ub[1] = (uint32_t)std::min<uint64_t>(nu - 1, std::max<uint64_t>(1, nu * 7 / 10));
-    if (const char* wv = getenv("SYDELTA_CHUNK_PIPE_W")) {  // A/B: part sizes by weights "w0,w1,..."
-        std::vector<double> wt;
-        for (const char* q = wv; *q;) {
-            wt.push_back(std::max(0.0, strtod(q, nullptr)));
-            while (*q && *q != ',') ++q;
-            if (*q == ',') ++q;
-        }
-        if ((int)wt.size() == K) {
-            double tot = 0, acc = 0;
-            for (double x : wt) tot += x;
-            for (int j = 1; j < K && tot > 0; ++j) {
-                acc += wt[j - 1];
-                P.ub[j] = (uint32_t)std::min<double>((double)nu - (K - j), std::max<double>(P.ub[j - 1] + 1, nu * acc / tot));
-            }
-        }
-    }
     // the last part, whose walk ends the pipeline, in shorter segments (its waves finish sooner)
-    const uint64_t seg_last = K >= 2 ? chunk_seg_last_blocks((c.p1 - P.units[P.ub[K - 1]].entry + n - 1) / n)
+    const uint64_t seg_last = K >= 2 ? chunk_seg_last_blocks((c.p1 - P.units[P.ub[K - 1]].entry + n - 1) / n, C.ix->device)
                                      : chunk_seg_blocks();
     if (K >= 2 && seg_last < chunk_seg_blocks()) {
         const uint64_t split = P.units[P.ub[K - 1]].entry;
@@ -3831,8 +3927,7 @@ int chunk_pipe_launch(sydelta_chunk* ch, uint64_t from, bool probe) {
     };
     // (the second: the aux stream, idle once the index is built; a fifth stream would share
     // one of the process's four hardware queues with another and serialize behind it)
-    hipStream_t s2[2] = {thread_walk_stream(P.device, 0),
-                         getenv("SYDELTA_WALK_STREAMS2") ? thread_walk_stream(P.device, 1) : thread_aux_stream(P.device)};
+    hipStream_t s2[2] = {thread_walk_stream(P.device, 0), thread_aux_stream(P.device)};
     hipEvent_t hand = handoff_event(P.device);
     if (!s2[0] || !s2[1] || !hand) return fail(SYDELTA_E_OOM, "no stream or event for the chunk walk");
     const bool fast = ((uintptr_t)(C.base + c.off) & 15) == 0;
@@ -3841,7 +3936,7 @@ int chunk_pipe_launch(sydelta_chunk* ch, uint64_t from, bool probe) {
     a.last_size = (const uint64_t*)(D + o_last);
     a.n = (uint32_t)n;
     a.nm = (uint32_t)(n % 65521);
-    a.fw_max = 0;  // the filter from L2 (one file's is too large for LDS)
+    a.self_nb = 0;  // the index's filter and tables from L2 (one file's are too large for LDS)
     const DeviceIndex& ix = C.ix->ix;
     a.files = ix.d_files;
     a.fblk = ix.d_fblk;
@@ -3859,7 +3954,11 @@ int chunk_pipe_launch(sydelta_chunk* ch, uint64_t from, bool probe) {
     // assembly: staged there, one unit's per 4 KiB page, they cost a TLB miss each)
     a.stage = (WalkRec*)(D + o_stage);
     a.out = (WalkRec*)(H + h_rec);
-    a.total = (unsigned long long*)(D + o_total);  // one counter: the sub-ranges' launches run in order
+    // one record counter for every part: the parts' walks run on two streams at once, and the
+    // device-scope atomics give each unit a disjoint range of out; take() copies a part's
+    // [lo, hi) only after that part's walk finished (ranges of a part still walking may lie
+    // inside it, but are never read from the copy)
+    a.total = (unsigned long long*)(D + o_total);
     a.ticks = nullptr;
     auto probe_part = [&](int j, int phases) -> hipError_t {
         const uint64_t b0 = part_block(j), b1 = std::min<uint64_t>(part_block(j + 1), np);
@@ -3886,8 +3985,9 @@ int chunk_pipe_launch(sydelta_chunk* ch, uint64_t from, bool probe) {
         a.ticks = P.ticks ? P.ticks + 16 * j : nullptr;
         if (preroll && (j == K - 1 || preroll_all())) {
             const uint64_t b0 = part_block(j), b1 = std::min<uint64_t>(part_block(j + 1), np);
-            HIP_TRY(launch_preroll(a, d_out, d_pw, c.kb, b0, b1, c.p1, ch->file_len,
-                                   (uint32_t*)(D + o_list) + b0, (unsigned long long*)(D + o_cnt) + j, preroll_waves(),
+            HIP_TRY(launch_preroll(a, d_out, d_pw, c.kb, b0, b1, c.p1, c.len,
+                                   (uint32_t*)(D + o_list) + b0, (unsigned long long*)(D + o_cnt) + j, wave_slots(P.device),
+                                   std::max<uint64_t>(64, (b1 - b0) / 16),
                                    sw, C.prof));
             if (slim_walk()) HIP_TRY(launch_walk_files(a, sw, C.prof, true));
         }
@@ -3907,6 +4007,9 @@ int chunk_pipe_launch(sydelta_chunk* ch, uint64_t from, bool probe) {
 int chunk_pipe_finish(sydelta_chunk* ch, uint64_t entry, uint64_t* exit_pos, sydelta_delta* d) {
     static const bool host_timing = getenv("SYDELTA_HOST_TIMING") != nullptr;
     const auto t_begin = std::chrono::steady_clock::now();
+    // the re-walks' records (run_walk's WalkResult) live in this thread's walk scratch until
+    // they are copied out below: sydelta_trim must not release it in between
+    ScratchHold hold;
     Classifier& C = ch->C;
     ChunkPipe& P = ch->pipe;
     const uint64_t n = C.n;
@@ -3981,35 +4084,50 @@ int chunk_pipe_finish(sydelta_chunk* ch, uint64_t entry, uint64_t* exit_pos, syd
         return SYDELTA_OK;
     };
     // the results of units [a, b) out of the mapped buffer: copied in two block moves
-    // (SYDELTA_CHUNK_COPYREC=0: read in place)
-    static const bool copy_rec = !getenv("SYDELTA_CHUNK_COPYREC") || getenv("SYDELTA_CHUNK_COPYREC")[0] != '0';
     double ms_take = 0;
     auto take = [&](size_t a, size_t b) {
         if (b <= a) return;
         const auto tt = std::chrono::steady_clock::now();
         memcpy(out.data() + a, P.fout + a, sizeof(WalkFileOut) * (b - a));
         const WalkRec* base = P.rec;
-        uint64_t lo = 0;
-        if (copy_rec) {
-            uint64_t hi = 0;
-            lo = UINT64_MAX;
-            for (size_t u = a; u < b; ++u)
-                if (out[u].count) {
-                    lo = std::min<uint64_t>(lo, out[u].base);
-                    hi = std::max<uint64_t>(hi, (uint64_t)out[u].base + out[u].count);
-                }
-            if (hi > lo) {
-                again_rec.emplace_back(P.rec + lo, P.rec + hi);
-                base = again_rec.back().data();
-            } else {
-                lo = 0;
+        uint64_t lo = UINT64_MAX, hi = 0;
+        for (size_t u = a; u < b; ++u)
+            if (out[u].count) {
+                lo = std::min<uint64_t>(lo, out[u].base);
+                hi = std::max<uint64_t>(hi, (uint64_t)out[u].base + out[u].count);
             }
+        if (hi > lo) {
+            again_rec.emplace_back(P.rec + lo, P.rec + hi);
+            base = again_rec.back().data();
+        } else {
+            lo = 0;
         }
         for (size_t u = a; u < b; ++u) {  // (a unit with no records: an empty span anywhere)
             const WalkRec* r = out[u].count ? base + (out[u].base - lo) : base;
             span[u] = {r, r + out[u].count};
         }
         ms_take += ms_since(tt);
+    };
+    // Unit u's walk holds from pe, the true entry (the previous unit's exit, or `entry`), when
+    // it started there, or earlier with a leading literal run that reaches pe: the greedy walk
+    // from pe then classifies the same positions the same way (a shifted source's segments,
+    // whose previous Copy crosses the boundary by the shift) -- its leading Data op is cut to
+    // start at pe (dropped when it ends there).  Otherwise it is walked again from pe.
+    auto joins = [&](size_t u, uint64_t pe) -> bool {
+        if (units[u].entry == pe) return true;
+        const WalkRec* r0 = span[u].first;
+        if (pe < units[u].entry || r0 >= span[u].second || r0->kind || r0->off != units[u].entry ||
+            r0->off + r0->a < pe)
+            return false;
+        WalkRec* w = const_cast<WalkRec*>(r0);  // (our copy of the unit's records, take())
+        if (w->off + w->a == pe) {
+            ++span[u].first;
+        } else {
+            w->a = (uint32_t)(w->off + w->a - pe);
+            w->off = pe;
+        }
+        units[u].entry = pe;
+        return true;
     };
     size_t stop = nu;  // the first unit whose entry is not the previous one's exit
     for (size_t j = 0; j + 1 < P.ub.size() && stop == nu; ++j) {
@@ -4020,7 +4138,7 @@ int chunk_pipe_finish(sydelta_chunk* ch, uint64_t entry, uint64_t* exit_pos, syd
         ms_wait += ms_since(tw);
         take(a, b);
         size_t e = a;
-        while (e < b && units[e].entry == (e == u0 ? entry : out[e - 1].exit)) ++e;
+        while (e < b && joins(e, e == u0 ? entry : out[e - 1].exit)) ++e;
         if (int r = assemble(a, e)) return r;
         if (e < b) stop = e;
     }
@@ -4034,7 +4152,7 @@ int chunk_pipe_finish(sydelta_chunk* ch, uint64_t entry, uint64_t* exit_pos, syd
             uint64_t roff = 0;
             for (size_t u = stop; u < nu; ++u) {
                 const uint64_t ex = u == u0 ? entry : out[u - 1].exit;  // a Copy reaches < n bytes past a boundary
-                if (ex == units[u].entry) continue;
+                if (joins(u, ex)) continue;
                 units[u].entry = ex;
                 units[u].end = std::max(units[u].end, ex);
                 WalkUnit w = units[u];

@@ -35,16 +35,27 @@ constexpr uint32_t kWRun = 64;          // window starts per lane per roll pass
 constexpr uint32_t kWSub = 64 * kWRun;  // window starts per roll pass (4096)
 constexpr uint32_t kWMaxPass = 64;      // phase windows per pass at most (one lookup per lane)
 
+// A self-indexed unit's Bloom filter and exact table: 2^k >= 2 nb words / slots each (at least
+// 64): 64 bits per key, five of them set in one word (probe_hash / filt_mask, ~1e-5 false
+// passes), and the table at load <= 1/2.
+__host__ __device__ __forceinline__ uint32_t self_bits(uint32_t nb) {
+    uint32_t k = 6;
+    while ((1u << k) < 2 * nb) ++k;
+    return k;
+}
 struct WalkLds {  // byte offsets of the dynamic LDS (one wave per workgroup)
-    uint32_t filt, ntab, pw, pst, total;
+    uint32_t filt, ntab, pw, pst, tab, lw, total;
 };
-__host__ __device__ __forceinline__ WalkLds walk_lds(uint32_t fw) {
+__host__ __device__ __forceinline__ WalkLds walk_lds(uint32_t self_nb) {
     WalkLds L{};
     uint32_t o = 0;
-    L.filt = o; o += 4 * fw;
+    const uint32_t fw = self_nb ? 1u << self_bits(self_nb) : 0u;
+    L.filt = o; o += 4 * fw;        // self-indexed: the file's Bloom filter
     L.ntab = o; o += 1024;
     L.pw = o; o += 4 * kWMaxPass;   // a pass's weak values
     L.pst = o; o += 8 * kWMaxPass;  // ... and strong hashes
+    L.tab = o; o += 4 * fw;         // self-indexed: slot -> first block (in index order) of its weak value
+    L.lw = o; o += 4 * ((self_nb + 3) & ~3u);  // ... and the file's weak values
     L.total = o;
     return L;
 }
@@ -98,6 +109,26 @@ __device__ __forceinline__ uint32_t walk_lookup(const WalkArgs& a, const FileIx&
     return kNoBlock;
 }
 
+// The same from a self-indexed unit's LDS table (tab: linear probing by bucket_hash, each slot
+// the lowest block of its weak value; lw: the file's weak values): the first block in index
+// order with weak wk and strong st (sg: the file's strong hashes, global) -- the slot's block,
+// or, when its strong differs (a weak collision), the next block with both (generator.rs:76-81,
+// 127-133); one lane.
+__device__ __forceinline__ uint32_t self_lookup(const uint32_t* tab, const uint32_t* lw, uint32_t tmask,
+                                                const uint64_t* sg, uint32_t nbf, uint64_t gb0, uint32_t wk,
+                                                uint64_t st) {
+    uint32_t s = bucket_hash(wk) & tmask, e;
+    for (;;) {
+        e = tab[s];
+        if (e == kNoBlock) return kNoBlock;
+        if (lw[e] == wk) break;
+        s = (s + 1) & tmask;
+    }
+    for (uint32_t j = e; j < nbf; ++j)
+        if (lw[j] == wk && sg[j] == st) return (uint32_t)(gb0 + j);
+    return kNoBlock;
+}
+
 // One window per row (row_hash's contract).  Issuing all four pieces' loads of a 4 KiB
 // window at once (one round trip instead of four) took 64 more VGPRs: two waves per SIMD
 // instead of four, and the walk 5.09 ms instead of 3.59 at C4 (`profiles/r05f_*`).
@@ -126,11 +157,11 @@ __device__ __forceinline__ bool tail_matches(const uint8_t* p, uint64_t ls, uint
 // The first verified hit among the window starts (x, yend), the window at x (weak wbase)
 // missed: its position in q and block in qb (else q = yend, qb = kNoBlock); weak_hits counts
 // the verified windows.  The whole wave calls (k_walk_files at a miss, k_preroll per miss).
-template <bool kLdsFilt, class Tick, class Count>
+template <bool kLdsFilt, class Look, class Tick, class Count>
 __device__ __forceinline__ void walk_roll(const WalkArgs& a, const FileIx& F, const uint32_t* filt,
                                           const uint32_t* ntab, const uint8_t* src, uint64_t len, uint64_t x,
                                           uint64_t yend, uint32_t wbase, uint64_t& q, uint32_t& qb,
-                                          uint32_t& weak_hits, Tick&& wtick, Count&& wcount) {
+                                          uint32_t& weak_hits, Look&& look, Tick&& wtick, Count&& wcount) {
     const uint32_t lane = threadIdx.x & 63, row = lane >> 4, n = a.n;
     q = yend;
     qb = kNoBlock;
@@ -256,7 +287,7 @@ __device__ __forceinline__ void walk_roll(const WalkArgs& a, const FileIx& F, co
             uint64_t st;
             walk_hash<false>(src + y0 + mine, n, wk, st);
             uint32_t vb = kNoBlock;
-            if ((lane & 15) == 0 && row < nc) vb = walk_lookup(a, F, wk, st);
+            if ((lane & 15) == 0 && row < nc) vb = look(wk, st);
             weak_hits += nc;
             wcount(kWtVerifies, 1);
             for (uint32_t r = 0; r < nc; ++r) {
@@ -273,8 +304,10 @@ __device__ __forceinline__ void walk_roll(const WalkArgs& a, const FileIx& F, co
     }
 }
 
-// kLdsFilt: the unit's Bloom filter is copied to LDS (a batch's small files), else read from
-// global memory (L2-resident: a large single-file index, the segments of a chunk).
+// kLdsFilt: the unit is self-indexed -- its file's Bloom filter and exact candidate table are
+// built in LDS from the file's signature (a batch's small files: no index build, no global
+// lookups); else the index's filter and tables are read from global memory (L2-resident: a
+// large single-file index, the segments of a chunk).
 // kSlim: the walk of a pre-rolled part (launch_preroll), without the roll or the phase-window
 // hashing: a unit that needs either (a phase change after a Copy at an unaligned position, a
 // miss that was not pre-rolled) is left to the full kernel launched after it, which skips the
@@ -287,10 +320,20 @@ __global__ __launch_bounds__(64, 4) void k_walk_files(WalkArgs a) {
     if (!kSlim && (U.final_ & kUnitDone)) return;  // walked by the slim kernel
     const uint32_t lane = threadIdx.x, row = lane >> 4;
     const uint32_t n = a.n;
-    const FileIx F = a.files[U.file];
-    const uint32_t fw = 1u << (32 - F.fwshift);
-    const WalkLds L = walk_lds(a.fw_max);
+    const uint64_t gb0 = a.fblk[U.file], nbf = a.fblk[U.file + 1] - gb0, ls = a.last_size[U.file];
+    const uint32_t sbits = kLdsFilt ? self_bits((uint32_t)nbf) : 0u;
+    const FileIx F = kLdsFilt ? FileIx{0, 0, gb0, 32 - sbits, 0} : a.files[U.file];
+    const WalkLds L = walk_lds(a.self_nb);
     const uint32_t* filt = kLdsFilt ? (const uint32_t*)(smem + L.filt) : a.filt + F.filt_off;
+    uint32_t* tab = (uint32_t*)(smem + L.tab);
+    uint32_t* lw = (uint32_t*)(smem + L.lw);
+    const uint32_t tmask = (1u << sbits) - 1;
+    auto look = [&](uint32_t wk, uint64_t st) -> uint32_t {
+        if constexpr (kLdsFilt)
+            return self_lookup(tab, lw, tmask, a.strong + gb0, (uint32_t)nbf, gb0, wk, st);
+        else
+            return walk_lookup(a, F, wk, st);
+    };
     uint32_t* ntab = (uint32_t*)(smem + L.ntab);
     uint32_t* pw = (uint32_t*)(smem + L.pw);
     uint64_t* pst = (uint64_t*)(smem + L.pst);
@@ -307,12 +350,37 @@ __global__ __launch_bounds__(64, 4) void k_walk_files(WalkArgs a) {
     };
     const uint8_t* src = a.base + U.src;
     const uint64_t len = U.len, end = U.end;
-    const uint64_t gb0 = a.fblk[U.file], nbf = a.fblk[U.file + 1] - gb0, ls = a.last_size[U.file];
 
-    {  // the file's Bloom filter, the roll table
-        if (kLdsFilt) {
-            const uint4* g = (const uint4*)(a.filt + F.filt_off);
-            for (uint32_t i = lane; i < fw / 4; i += 64) ((uint4*)(smem + L.filt))[i] = g[i];
+    {  // self-indexed: the file's Bloom filter and candidate table; the roll table
+        if constexpr (kLdsFilt) {
+            uint32_t* fl = (uint32_t*)(smem + L.filt);
+            const uint32_t fw = 1u << sbits;
+            for (uint32_t i = lane; i < fw; i += 64) {
+                fl[i] = 0;
+                tab[i] = kNoBlock;
+            }
+            for (uint32_t i = lane; i < nbf; i += 64) lw[i] = a.weak[gb0 + i];
+            __syncthreads();
+            // each key: its filter bits, then its slot (linear probing; the lowest block of a weak
+            // value keeps the slot, so candidates are found in index order)
+            for (uint32_t i = lane; i < nbf; i += 64) {
+                const uint32_t w = lw[i];
+                const ProbeHash h = probe_hash(w);
+                atomicOr(fl + (h.r >> F.fwshift), filt_mask(h.q));
+                uint32_t sl = bucket_hash(w) & tmask;
+                for (;;) {
+                    uint32_t e = tab[sl];
+                    if (e == kNoBlock) {
+                        e = atomicCAS(tab + sl, kNoBlock, i);
+                        if (e == kNoBlock) break;
+                    }
+                    if (lw[e] == w) {
+                        atomicMin(tab + sl, i);
+                        break;
+                    }
+                    sl = (sl + 1) & tmask;
+                }
+            }
         }
         for (uint32_t i = lane; i < 256; i += 64) ntab[i] = kMod - 1 - (a.nm * i) % kMod;
     }
@@ -419,7 +487,7 @@ __global__ __launch_bounds__(64, 4) void k_walk_files(WalkArgs a) {
             if (lane < cnt) {  // lookups (generator.rs:121-155), one window per lane
                 rwk = pw[lane];
                 const ProbeHash h = probe_hash(rwk);
-                if (filt_pass(filt[h.r >> F.fwshift], h.q)) rres = walk_lookup(a, F, rwk, pst[lane]);
+                if (filt_pass(filt[h.r >> F.fwshift], h.q)) rres = look(rwk, pst[lane]);
             }
             __syncthreads();  // pw / pst are rewritten by the next pass
             wtick(kWtLookup);
@@ -453,7 +521,7 @@ __global__ __launch_bounds__(64, 4) void k_walk_files(WalkArgs a) {
         const uint32_t wb = rl(rwk, (uint32_t)(k - rk0));  // weak of the window at x (pre-rolled: the result)
         if (kLdsFilt || blk == kNoBlock) {  // (a batch's walks, kLdsFilt, are never pre-rolled)
             if (kSlim) return;  // not pre-rolled: the full kernel's
-            walk_roll<kLdsFilt>(a, F, filt, ntab, src, len, x, yend, wb, q, qb, weak_hits, wtick, wcount);
+            walk_roll<kLdsFilt>(a, F, filt, ntab, src, len, x, yend, wb, q, qb, weak_hits, look, wtick, wcount);
         } else {  // pre-rolled (k_preroll): the first hit of (x, min(x + n, p1))
             weak_hits += wb >> 14;
             if (blk != kPreNone && x + (wb & 0x3FFFu) < yend) {
@@ -547,11 +615,13 @@ __global__ __launch_bounds__(1024) void k_miss_list(const uint32_t* ahit, uint64
 
 __global__ __launch_bounds__(64, 4) void k_preroll(WalkArgs a, uint32_t* ahit, uint32_t* apw, uint64_t kb,
                                                    uint64_t pend, uint64_t len, const uint32_t* list,
-                                                   const unsigned long long* count) {
+                                                   const unsigned long long* count, uint64_t max_miss) {
     __shared__ uint32_t ntab[256];
     const uint32_t lane = threadIdx.x;
     const uint64_t m = *count;
-    if (blockIdx.x >= m) return;
+    // more misses than max_miss (a shifted source: every aligned window misses, and the walk
+    // visits few of them): none is pre-rolled, the walk rolls the ones it meets
+    if (blockIdx.x >= m || m > max_miss) return;
     for (uint32_t i = lane; i < 256; i += 64) ntab[i] = kMod - 1 - (a.nm * i) % kMod;
     __syncthreads();
     const FileIx F = a.files[0];
@@ -563,7 +633,8 @@ __global__ __launch_bounds__(64, 4) void k_preroll(WalkArgs a, uint32_t* ahit, u
         const uint64_t x = (kb + r) * n;
         uint64_t q;
         uint32_t qb, wh = 0;
-        walk_roll<false>(a, F, filt, ntab, a.base, len, x, min(x + n, pend), apw[r], q, qb, wh, [](int) {},
+        walk_roll<false>(a, F, filt, ntab, a.base, len, x, min(x + n, pend), apw[r], q, qb, wh,
+                         [&](uint32_t wk, uint64_t st) { return walk_lookup(a, F, wk, st); }, [](int) {},
                          [](int, uint64_t) {});
         if (lane == 0) {  // (the walk's miss at x, with the roll's result: launch_preroll)
             ahit[r] = qb == kNoBlock ? kPreNone : (qb | kPreMark);
@@ -577,12 +648,11 @@ __global__ __launch_bounds__(64, 4) void k_preroll(WalkArgs a, uint32_t* ahit, u
 // ===========================================================================
 hipError_t launch_walk_files(const WalkArgs& a, hipStream_t s, Profiler* prof, bool slim) {
     if (!a.nunits) return hipSuccess;
-    if (a.n % 64 != 0 || a.n < 256 || a.n > kWalkMaxN || a.fw_max > kWalkMaxWords || (a.fw_max && a.fw_max < 4) ||
-        (slim && (a.fw_max || !a.ahit)))
+    if (a.n % 64 != 0 || a.n < 256 || a.n > kWalkMaxN || a.self_nb > kSelfIxMaxBlocks || (slim && (a.self_nb || !a.ahit)))
         return hipErrorInvalidValue;
-    const WalkLds L = walk_lds(a.fw_max);
+    const WalkLds L = walk_lds(a.self_nb);
     ProfScope ps(prof, s, slim ? "k_walk_files_slim" : "k_walk_files");
-    if (a.fw_max)
+    if (a.self_nb)
         hipLaunchKernelGGL((k_walk_files<true, false>), dim3(a.nunits), dim3(64), L.total, s, a);
     else if (slim)
         hipLaunchKernelGGL((k_walk_files<false, true>), dim3(a.nunits), dim3(64), L.total, s, a);
@@ -593,7 +663,7 @@ hipError_t launch_walk_files(const WalkArgs& a, hipStream_t s, Profiler* prof, b
 
 hipError_t launch_preroll(const WalkArgs& a, uint32_t* ahit, uint32_t* apw, uint64_t kb, uint64_t b0, uint64_t b1,
                           uint64_t pend, uint64_t len, uint32_t* list, unsigned long long* count, uint32_t waves,
-                          hipStream_t s, Profiler* prof) {
+                          uint64_t max_miss, hipStream_t s, Profiler* prof) {
     if (b1 <= b0) return hipSuccess;
     if (a.n % 64 != 0 || a.n < 256 || a.n > kWalkMaxN || !ahit || !apw || !waves || b1 - b0 >= (1ull << 31))
         return hipErrorInvalidValue;
@@ -603,7 +673,7 @@ hipError_t launch_preroll(const WalkArgs& a, uint32_t* ahit, uint32_t* apw, uint
                            count);
     }
     ProfScope ps(prof, s, "k_preroll");
-    hipLaunchKernelGGL(k_preroll, dim3(waves), dim3(64), 0, s, a, ahit, apw, kb, pend, len, list, count);
+    hipLaunchKernelGGL(k_preroll, dim3(waves), dim3(64), 0, s, a, ahit, apw, kb, pend, len, list, count, max_miss);
     return hipGetLastError();
 }
 

@@ -50,6 +50,8 @@ struct DeviceScope {
 int path_device(int* out);
 // The calling thread's stream for `device`.
 hipStream_t thread_stream(int device);
+// K10 wave slots of a device (CUs x 16: four waves per SIMD), from its properties at first use
+uint32_t wave_slots(int device);
 // Recount copy/data ops and literal bytes of d.
 void finish_stats(sydelta_delta* d);
 // Per-thread scan scratch (Classifier::scan): the verified-hit buffers on one device,

@@ -211,12 +211,14 @@ hipError_t launch_chain(const chain::ChainArgs& a, hipStream_t s, Profiler* prof
 // K10: the greedy walk (generator.rs:116-221) on the device, one wave per unit
 // (k_walk_files): a unit is a whole file of a batch (C4's small files) or a segment of a
 // chunk of one file (C5), walked from its entry until it leaves [entry, end).  Block sizes
-// n % 64 == 0, 256 <= n <= kWalkMaxN.  A batch's per-file Bloom filters are copied to LDS
-// (<= kWalkMaxWords words); a large single-file index's filter is read from L2.  The ops
+// n % 64 == 0, 256 <= n <= kWalkMaxN.  A batch's walks are self-indexed: each unit builds its
+// file's Bloom filter and exact candidate table in LDS from the file's signature (files of at
+// most kSelfIxMaxBlocks blocks; the batch index's tables are not needed); a large single-file
+// index's filter and tables are read from L2.  The ops
 // come back run-length coded: a Data op, or a run of Copies of consecutive global basis
 // blocks (each Copy's size follows from its block: the basis file's last block has
 // last_size, every other one n).
-constexpr uint32_t kWalkMaxWords = 4096;
+constexpr uint32_t kSelfIxMaxBlocks = 1024;
 constexpr uint32_t kWalkMaxN = 8192;
 struct WalkRec {
     uint32_t kind;  // 0: Data; else the number of Copies in the run
@@ -246,7 +248,8 @@ struct WalkArgs {
     const WalkUnit* units;
     const uint64_t* last_size;   // per basis file (0: empty signature)
     uint32_t nunits, n, nm;
-    uint32_t fw_max;             // LDS filter words (0: the filter is read from global memory)
+    uint32_t self_nb;            // self-indexed: the most blocks of any unit's file (<= kSelfIxMaxBlocks);
+                                 // 0: the index's filter and tables are read from global memory
     const FileIx* files;
     const uint64_t* fblk;
     const uint32_t* filt;
@@ -281,9 +284,10 @@ hipError_t launch_walk_files(const WalkArgs& a, hipStream_t s, Profiler* prof, b
 // `waves` waves loop over it.  a: the chunk's K10 arguments (one file; the filter from
 // global memory; block ids below kPreMark).
 constexpr uint32_t kPreMark = 0x80000000u, kPreNone = 0xFFFFFFFEu;
+// More than max_miss misses (a shifted source): nothing is pre-rolled (the walk rolls what it meets).
 hipError_t launch_preroll(const WalkArgs& a, uint32_t* ahit, uint32_t* apw, uint64_t kb, uint64_t b0, uint64_t b1,
                           uint64_t pend, uint64_t len, uint32_t* list, unsigned long long* count, uint32_t waves,
-                          hipStream_t s, Profiler* prof);
+                          uint64_t max_miss, hipStream_t s, Profiler* prof);
 // One slice (<= 64 KiB) of an op for the device apply: out[dst, dst+len) =
 // (from_basis ? basis : lit)[src, src+len).
 struct ApplyPiece {

@@ -166,14 +166,9 @@ __device__ __forceinline__ ProbeHash probe_hash(uint32_t w) { return probe_hash(
 // 16 bits per key against 1.08 % with three (Poisson keys per word), so a third fewer
 // exact-table lookups behind the scans' filters (round 4; each lookup of a level-2 false
 // pass misses L2 for a table line).
-#ifndef SYDELTA_L2_BITS
-#define SYDELTA_L2_BITS 5
-#endif
-static_assert(SYDELTA_L2_BITS == 3 || SYDELTA_L2_BITS == 5, "level-2 bits per key");
 __device__ __forceinline__ uint32_t filt_mask(uint32_t q) {
-    uint32_t m = (1u << (q & 31)) | (1u << ((q >> 5) & 31)) | (1u << ((q >> 10) & 31));
-    if (SYDELTA_L2_BITS == 5) m |= (1u << ((q >> 15) & 31)) | (1u << ((q >> 20) & 31));
-    return m;
+    return (1u << (q & 31)) | (1u << ((q >> 5) & 31)) | (1u << ((q >> 10) & 31)) | (1u << ((q >> 15) & 31)) |
+           (1u << ((q >> 20) & 31));
 }
 __device__ __forceinline__ bool filt_pass(uint32_t word, uint32_t q) {
     const uint32_t m = filt_mask(q);
@@ -181,10 +176,9 @@ __device__ __forceinline__ bool filt_pass(uint32_t word, uint32_t q) {
 }
 // filt_pass as 0/1 with five bit extracts (the offset operand takes bits [4:0])
 __device__ __forceinline__ uint32_t filt_bit(uint32_t word, uint32_t q) {
-    uint32_t b = __builtin_amdgcn_ubfe(word, q, 1) & __builtin_amdgcn_ubfe(word, q >> 5, 1) &
-                 __builtin_amdgcn_ubfe(word, q >> 10, 1);
-    if (SYDELTA_L2_BITS == 5) b &= __builtin_amdgcn_ubfe(word, q >> 15, 1) & __builtin_amdgcn_ubfe(word, q >> 20, 1);
-    return b;
+    return __builtin_amdgcn_ubfe(word, q, 1) & __builtin_amdgcn_ubfe(word, q >> 5, 1) &
+           __builtin_amdgcn_ubfe(word, q >> 10, 1) & __builtin_amdgcn_ubfe(word, q >> 15, 1) &
+           __builtin_amdgcn_ubfe(word, q >> 20, 1);
 }
 // Level-1 filters (held in LDS by k_scan_r / k_scan_g so that only the positions they
 // pass cost a level-2 request to L2): one bit per key, bit = q[0..4] (one bit extract;

@@ -606,26 +606,11 @@ __device__ __forceinline__ void load_chunk(const uint8_t* src, uint64_t len, uin
     }
 }
 
-// As load_chunk; built with SYDELTA_ROW_NONTEMPORAL, non-temporal loads for the aligned
-// case (meant to keep the rows from evicting the level-2 filter from L2).  Measured at
-// C3 (profiles/r04h_ab_*): 9.82 ms with them against 9.59 ms without, so they are off.
+// The register scans' row loads.  Non-temporal loads (meant to keep the rows from evicting
+// the level-2 filter from L2) measured 9.82 ms at C3 against 9.59 ms with plain ones
+// (profiles/r04h_ab_*), so the rows are loaded as any chunk.
 __device__ __forceinline__ void load_chunk_nt(const uint8_t* src, uint64_t len, uint64_t c0, uint32_t x[16]) {
-#ifndef SYDELTA_ROW_NONTEMPORAL
-    if (false) {
-#else
-    if (c0 + 64 <= len) {
-#endif
-        const uint4* q = (const uint4*)(src + c0);
-#pragma unroll
-        for (int i = 0; i < 4; ++i) {
-            uint4 v;
-            v.x = __builtin_nontemporal_load(&q[i].x); v.y = __builtin_nontemporal_load(&q[i].y);
-            v.z = __builtin_nontemporal_load(&q[i].z); v.w = __builtin_nontemporal_load(&q[i].w);
-            x[4 * i] = v.x; x[4 * i + 1] = v.y; x[4 * i + 2] = v.z; x[4 * i + 3] = v.w;
-        }
-    } else {
-        load_chunk(src, len, c0, x);
-    }
+    load_chunk(src, len, c0, x);
 }
 
 // 64 bytes starting at an arbitrary address q (dword-granular loads + alignbyte);

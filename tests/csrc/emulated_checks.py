@@ -743,7 +743,6 @@ def batch_and_chunk_checks():
             for probe in ("0", "1", "1p"):  # 1p: the device walk's launches in one sub-range per segment
                 os.environ["SYDELTA_PROBE"] = probe[0]
                 os.environ["SYDELTA_CHUNK_PIPE"] = "3" if probe == "1p" else ""
-                os.environ["SYDELTA_CHUNK_PIPE_W"] = "1,3,1" if probe == "1p" else ""
                 cuts = sorted(set(int(c) for c in rng.choice(np.arange(1, nbp), nch - 1, replace=False))) if nch > 1 \
                     else []
                 bounds = [0] + [c * bs for c in cuts] + [npos]
@@ -770,7 +769,6 @@ def batch_and_chunk_checks():
         lib.sydelta_index_free(ix)
     os.environ.pop("SYDELTA_PROBE", None)
     os.environ.pop("SYDELTA_CHUNK_PIPE", None)
-    os.environ.pop("SYDELTA_CHUNK_PIPE_W", None)
     return n_checks
 
 

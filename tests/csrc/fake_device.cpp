@@ -587,11 +587,26 @@ hipError_t launch_chain(const chain::ChainArgs& a, hipStream_t, Profiler*) {
 // aligned probe's results, when given, must agree with the exact classification.
 hipError_t launch_walk_files(const WalkArgs& a, hipStream_t, Profiler*, bool slim) {
     EmuTimer emu_t;
-    if (slim) return a.ahit && !a.fw_max ? hipSuccess : hipErrorInvalidValue;  // the full launch after it walks every unit
-    if (a.n % 64 != 0 || a.n < 256 || a.n > kWalkMaxN || a.fw_max > kWalkMaxWords) return hipErrorInvalidValue;
+    if (slim) return a.ahit && !a.self_nb ? hipSuccess : hipErrorInvalidValue;  // the full launch after it walks every unit
+    if (a.n % 64 != 0 || a.n < 256 || a.n > kWalkMaxN || a.self_nb > kSelfIxMaxBlocks) return hipErrorInvalidValue;
+    FakeIndex self;  // self-indexed (a batch's walks): the units' files' candidates from the signature
+    if (a.self_nb) {
+        uint32_t nfl = 0;
+        for (uint32_t u = 0; u < a.nunits; ++u) nfl = std::max(nfl, a.units[u].file + 1);
+        self.files.resize(nfl);
+        self.any.assign((1ull << 26) / 64, 0);
+        for (uint32_t f = 0; f < nfl; ++f) {
+            if (a.fblk[f + 1] - a.fblk[f] > a.self_nb) return hipErrorInvalidValue;  // the kernel's LDS would overflow
+            for (uint64_t k = a.fblk[f]; k < a.fblk[f + 1]; ++k) {
+                self.files[f][a.weak[k]].push_back({(uint32_t)k, a.strong[k]});
+                const uint64_t bit = any_bit(f, a.weak[k]);
+                self.any[bit >> 6] |= 1ull << (bit & 63);
+            }
+        }
+    }
     DeviceIndex key_ix;
     key_ix.keys = (uint32_t*)a.keys;
-    const FakeIndex& F = find_ix(key_ix);
+    const FakeIndex& F = a.self_nb ? self : find_ix(key_ix);
     const uint64_t n = a.n;
     uint64_t placed = *a.total;
     for (uint32_t u = 0; u < a.nunits; ++u) {
@@ -701,11 +716,14 @@ hipError_t launch_walk_files(const WalkArgs& a, hipStream_t, Profiler*, bool sli
 
 // K10's pre-roll: each missed aligned block's first hit in (x, min(x + n, pend)), exactly
 hipError_t launch_preroll(const WalkArgs& a, uint32_t* ahit, uint32_t* apw, uint64_t kb, uint64_t b0, uint64_t b1,
-                          uint64_t pend, uint64_t len, uint32_t*, unsigned long long*, uint32_t waves, hipStream_t,
-                          Profiler*) {
+                          uint64_t pend, uint64_t len, uint32_t*, unsigned long long*, uint32_t waves,
+                          uint64_t max_miss, hipStream_t, Profiler*) {
     EmuTimer emu_t;
     if (b1 <= b0) return hipSuccess;
     if (a.n % 64 != 0 || a.n < 256 || a.n > kWalkMaxN || !ahit || !apw || !waves) return hipErrorInvalidValue;
+    uint64_t misses = 0;
+    for (uint64_t r = b0; r < b1; ++r) misses += ahit[r] == kNone;
+    if (misses > max_miss) return hipSuccess;  // nothing pre-rolled (the walk rolls what it meets)
     DeviceIndex key_ix;
     key_ix.keys = (uint32_t*)a.keys;
     const FakeIndex& F = find_ix(key_ix);

@@ -276,11 +276,20 @@ def test_file_walk_c4_shape_few_files(gpu, oracle_c, monkeypatch):
         assert d.tuples() == _oracle_ops(oracle_c, src, basis, 4096), f
 
 
-def test_chunk_pipeline_two_parts(gpu, oracle_c, monkeypatch):
+# (SYDELTA_PREROLL, SYDELTA_SLIM_WALK, SYDELTA_CHUNK_SEG, SYDELTA_CHUNK_SEG_LAST): every
+# output-affecting setting of the chunk pipeline, read per call
+PIPE_KNOBS = [("1", "1", "", ""), ("0", "1", "", ""), ("1", "0", "", ""), ("2", "1", "", ""), ("2", "0", "", ""),
+              ("1", "1", "64", "8"), ("0", "1", "1024", "")]
+
+
+@pytest.mark.parametrize("preroll,slim,seg,seg_last", PIPE_KNOBS)
+def test_chunk_pipeline_two_parts(gpu, oracle_c, monkeypatch, preroll, slim, seg, seg_last):
     """A chunk large enough for the two-part pipeline (>= 512 segments: 70 % / 30 %, the last
     part re-cut into shorter segments, the parts' walks on two streams), with insertions and
     deletions that shift the data across segment and part boundaries (re-walk rounds), a
-    duplicated run and substitutions: equal to the oracle and to the classifier path."""
+    duplicated run and substitutions: equal to the oracle and to the classifier path, under
+    every pre-roll / slim-walk / segment-size setting, each of which must launch the kernels
+    it names."""
     rng = random.Random(512)
     bs = 256
     nblk = 600 * 128  # 600 segments of 128 blocks: 19.2 MB
@@ -299,13 +308,83 @@ def test_chunk_pipeline_two_parts(gpu, oracle_c, monkeypatch):
     monkeypatch.delenv("SYDELTA_CHUNK_WALK", raising=False)
     monkeypatch.delenv("SYDELTA_PROBE", raising=False)
     monkeypatch.delenv("SYDELTA_CHUNK_PIPE", raising=False)
+    for k, v in (("SYDELTA_PREROLL", preroll), ("SYDELTA_SLIM_WALK", slim), ("SYDELTA_CHUNK_SEG", seg),
+                 ("SYDELTA_CHUNK_SEG_LAST", seg_last)):
+        monkeypatch.setenv(k, v)
     gpu.set_profiling(True)
     gpu.profile(reset=True)
     d = _chunk_walk(gpu, src, basis, bs, [0, npos])
     prof = gpu.profile(reset=True)
     gpu.set_profiling(False)
     assert prof["k_walk_files"]["count"] >= 2, prof  # two parts (and any re-walks)
+    nparts_pre = {"0": 0, "1": 1, "2": 2}[preroll]
+    assert prof.get("k_preroll", {}).get("count", 0) == nparts_pre, prof
+    assert prof.get("k_walk_files_slim", {}).get("count", 0) == (nparts_pre if slim == "1" else 0), prof
     exp = _oracle_ops(oracle_c, src, basis, bs)
     assert d.tuples() == exp
-    monkeypatch.setenv("SYDELTA_CHUNK_WALK", "0")
-    assert _chunk_walk(gpu, src, basis, bs, [0, npos]).tuples() == exp
+    if preroll == "1" and slim == "1" and not seg:
+        monkeypatch.setenv("SYDELTA_CHUNK_WALK", "0")
+        assert _chunk_walk(gpu, src, basis, bs, [0, npos]).tuples() == exp
+
+
+@pytest.mark.late
+def test_chunk_exact_buffers(gpu, oracle_c):
+    """Non-final chunks whose source buffers end exactly where sydelta.h lets them (the last
+    window byte, min(file_len, p1 + n - 1), in its 16-byte granule) at the END of a raw
+    hipMalloc: the walk's and the pre-roll's loads must stay inside (they were
+    bounded by the file length, ~4 KiB past a non-final chunk's buffer).  Three chunks at bs
+    256 with shifted data (misses everywhere, rolls near each chunk's end), joined: equal to
+    the oracle."""
+    import ctypes
+
+    import torch
+
+    from sy_amd._lib import check, lib
+
+    hip = ctypes.CDLL("libamdhip64.so")
+    rng = random.Random(9090)
+    bs = 256
+    basis = rng.randbytes(3000 * bs + 77)
+    s = bytearray(basis)
+    for p in sorted(rng.sample(range(len(s)), 60), reverse=True):
+        s[p:p] = bytes([rng.randrange(256)])  # insertions: every block after them is off the grid
+    src = bytes(s)
+    L = len(src)
+    npos = L - bs + 1
+    b = _to_dev(basis)
+    w, st = gpu.signature(b[:len(basis)], bs)
+    nb = w.numel()
+    idx = gpu.Index(w, st, bs, len(basis) - (nb - 1) * bs)
+    torch.cuda.synchronize()
+    bounds = [0, 1000 * bs, 2100 * bs, npos]
+    ptrs, parts, entry = [], [], 0
+    try:
+        for g in range(3):
+            p0, p1 = bounds[g], bounds[g + 1]
+            final = g == 2
+            bpos = p0 & ~15
+            end = L if final else min(L, p1 + bs - 1)
+            blen = end - bpos
+            alloc = (((blen + 15) & ~15) + 4095) & ~4095
+            raw = ctypes.c_void_p()
+            assert hip.hipMalloc(ctypes.byref(raw), ctypes.c_size_t(alloc)) == 0
+            ptrs.append(raw)
+            dptr = raw.value + alloc - ((blen + 15) & ~15)  # the buffer's granules end the allocation
+            host = np.frombuffer(src[bpos:end], np.uint8)
+            assert hip.hipMemcpy(ctypes.c_void_p(dptr), host.ctypes.data_as(ctypes.c_void_p), ctypes.c_size_t(blen),
+                                 1) == 0
+            ch = ctypes.c_void_p()
+            check(lib.sydelta_chunk_classify(idx.h, ctypes.c_void_p(dptr), bpos, blen, L, p0, max(p1, L) if final else p1,
+                                             None, ctypes.byref(ch)))
+            dh = ctypes.c_void_p()
+            ex = ctypes.c_uint64()
+            check(lib.sydelta_chunk_walk(ch, entry, ctypes.byref(ex), ctypes.byref(dh)))
+            lib.sydelta_chunk_free(ch)
+            parts.append(gpu._device_delta(dh, gpu._DeltaHandle(dh)))
+            entry = int(ex.value)
+        assert torch.cuda.synchronize() is None
+        assert gpu.join_deltas(parts, L, bs).tuples() == _oracle_ops(oracle_c, src, basis, bs)
+    finally:
+        idx.close()
+        for p in ptrs:
+            hip.hipFree(p)

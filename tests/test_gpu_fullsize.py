@@ -5,14 +5,17 @@ both in HBM), through the same C ABI calls the bench makes.
   substitutions (bench.c4_files), one batched signature + index + match.  For every
   file: the ops tile the source, Data ops name their own source bytes, Copy ops name
   whole basis blocks, and apply_delta on the device rebuilds the source bit-exactly.
-  For 200 files spread over the batch (including the last ones, whose batch offsets
-  lie past 2^32) the op list equals the C oracle's (generator.rs:242-379).
+  Every file's op list equals the C oracle's (generator.rs:242-379), the oracle run on the
+  host's cores (the last files' batch offsets lie past 2^32).
 * C5: one 64 GiB file, bs 8192, 1 % of blocks with one substituted byte, matched as 8
   block-aligned chunks (shard.chunk_bounds) classified against the whole signature
   and walked in a chain (each chunk from the previous chunk's exit,
   generator.rs:116-221); the joined op list tiles the file, apply_delta rebuilds it
-  (compared on the device in 4 GiB pieces), and the 7 chunk-boundary neighbourhoods
-  are re-derived by the C oracle from an op start before each boundary.
+  (compared on the device in 4 GiB pieces), the whole 8 Mi-op list equals the analytic one
+  (each edited block's bytes a literal run -- consecutive ones one Data op -- every other
+  block a Copy of itself: random 8 KiB blocks share no weak+strong pair and no window
+  straddling an edited block matches), and the 7 chunk-boundary neighbourhoods are
+  re-derived by the C oracle from an op start before each boundary.
 """
 import numpy as np
 import pytest
@@ -72,15 +75,24 @@ def test_c4_full_batch(gpu, oracle_c):
         rebuilt, st = gpu.apply_device(basis[int(boff[f]):int(boff[f]) + fsz], d, src_f, out=out)
         assert st["bytes_written"] == fsz + 1
         assert torch.equal(rebuilt, src_f), f
-    # oracle op lists for 200 files spread over the batch, the last 20 included
-    pick = sorted(set(np.linspace(0, nfiles - 21, 180).astype(int).tolist() + list(range(nfiles - 20, nfiles))))
-    assert len(pick) == 200
-    for f in pick:
-        bh = basis[int(boff[f]):int(boff[f]) + fsz].cpu().numpy().tobytes()
-        sh = new[int(soff[f]):int(soff[f]) + fsz + 1].cpu().numpy().tobytes()
+    # every file's op list against the C oracle, on the host's cores (the oracle's calls
+    # release the GIL)
+    from concurrent.futures import ThreadPoolExecutor
+
+    import bench as B
+
+    hb = basis.cpu().numpy()
+    hn = new.cpu().numpy()
+
+    def one(f):
+        bh = hb[int(boff[f]):int(boff[f]) + fsz]
+        sh = hn[int(soff[f]):int(soff[f]) + fsz + 1]
         wk, st, sz = oracle_c.compute_checksums(bh, bs)
-        kind, a, b = oracle_c.generate_delta(sh, wk, st, sz, bs)
-        assert deltas[f].tuples() == O.ops_from_arrays(kind, a, b), f
+        return O.ops_from_arrays(*oracle_c.generate_delta(sh, wk, st, sz, bs))
+
+    with ThreadPoolExecutor(max(2, B.host_cores()[0])) as ex:
+        for f, exp in enumerate(ex.map(one, range(nfiles), chunksize=64)):
+            assert deltas[f].tuples() == exp, f
 
 
 def test_c5_full_chained_chunks(gpu, oracle_c):
@@ -128,6 +140,13 @@ def test_c5_full_chained_chunks(gpu, oracle_c):
     pos = _check_tiling(joined.kind, joined.a, joined.b, L, bs, L)
     nblocks = L // bs
     assert joined.stats["copy_ops"] > 0.985 * nblocks
+    # the analytic op list (synth_mutate_blocks' edited-block set, tests/analytic_ops.py)
+    from tests.analytic_ops import block_edit_ops, edited_blocks
+
+    exp_kind, exp_a, exp_b = block_edit_ops(edited_blocks(nblocks, 0x5E1D0006, 10000), bs)
+    assert np.array_equal(np.asarray(joined.kind, dtype=np.uint8), exp_kind)
+    assert np.array_equal(np.asarray(joined.a, dtype=np.uint64), exp_a)
+    assert np.array_equal(np.asarray(joined.b, dtype=np.uint64), exp_b)
     out = torch.empty(L + 16, dtype=torch.uint8, device="cuda")
     rebuilt, st = gpu.apply_device(basis[:L], joined, src[:L], out=out)
     assert st["bytes_written"] == L
