@@ -4572,7 +4572,7 @@ hipError_t launch_scan(const uint8_t* d_buf, const ScanSeg* d_segs, uint32_t nse
     // k_scan_g: one file with a level-1 filter (more than kLdsFilterKeys blocks, or windows
     // above the LDS-staged layouts) at any n but 4096, or (kSmall) indexes whose file
     // filters are <= kSmallWords words at any n <= kMaxN2; weak hits verified by k_verify_w
-    static const bool small_off = getenv("SYDELTA_SCAN_SMALL") && getenv("SYDELTA_SCAN_SMALL")[0] == '0';
+    const bool small_off = getenv("SYDELTA_SCAN_SMALL") && getenv("SYDELTA_SCAN_SMALL")[0] == '0';  // (per call)
     const bool small = !ix.l1 && ix.max_fwords <= kSmallWords && n <= kMaxN2 && !small_off;
     // small indexes at n = 4096 with filters <= kSmallWordsR words: k_scan_r's small mode
     // (windows verified from the registers, no deferred list)
@@ -4604,10 +4604,8 @@ hipError_t launch_scan(const uint8_t* d_buf, const ScanSeg* d_segs, uint32_t nse
         const uint32_t grid = (uint32_t)((ntiles + (uint64_t)per - 1) / per);
         // the deferred list: one entry per 256 scanned positions, 64 Ki to 4 Mi (weak hits
         // past it are verified inside the scan); SYDELTA_WDEF_CAP overrides (tests)
-        static const uint64_t wdef_env = [] {
-            const char* e = getenv("SYDELTA_WDEF_CAP");
-            return e ? std::min<uint64_t>(strtoull(e, nullptr, 10), 1u << 22) : 0;
-        }();
+        const char* we = getenv("SYDELTA_WDEF_CAP");  // (per call)
+        const uint64_t wdef_env = we ? std::min<uint64_t>(strtoull(we, nullptr, 10), 1u << 22) : 0;
         a.wdef_cap = wdef_env ? wdef_env
                               : std::min<uint64_t>(1u << 22, std::max<uint64_t>(1u << 16, (uint64_t)ntiles * kTile2 / 256));
         const uint32_t verify_grid = 4 * (uint32_t)g_cus;  // k_verify_w: 4 waves per workgroup
@@ -4641,15 +4639,13 @@ hipError_t launch_scan(const uint8_t* d_buf, const ScanSeg* d_segs, uint32_t nse
         const hipError_t fe = scratch_put(buf);
         return e != hipSuccess ? e : fe;
     }
-    // k_scan_r: one large file at n = 4096 (SYDELTA_SCAN_R_WAVES=8: two waves per SIMD)
+    // k_scan_r: one large file at n = 4096
     if ((ix.l1 && ix.l1_wshift == 1 && n == kMaxN3) || small_r) {
         static std::once_flag r_once;
         static hipError_t r_err = hipSuccess;
         static int r_cus = 256;
         std::call_once(r_once, [] {
-            for (const void* f : {(const void*)k_scan_r<false, false, 8>, (const void*)k_scan_r<true, false, 8>,
-                                  (const void*)k_scan_r<false, true, 8>, (const void*)k_scan_r<true, true, 8>,
-                                  (const void*)k_scan_r<false, false, 12>, (const void*)k_scan_r<true, false, 12>,
+            for (const void* f : {(const void*)k_scan_r<false, false, 12>, (const void*)k_scan_r<true, false, 12>,
                                   (const void*)k_scan_r<false, true, 12>, (const void*)k_scan_r<true, true, 12>,
                                   (const void*)k_scan_r<false, false, 12, true>, (const void*)k_scan_r<true, false, 12, true>})
                 if (r_err == hipSuccess)
@@ -4662,8 +4658,7 @@ hipError_t launch_scan(const uint8_t* d_buf, const ScanSeg* d_segs, uint32_t nse
         if (r_err != hipSuccess) return r_err;
         if (!ix.fat && !small_r) return hipErrorInvalidValue;
         // 12 waves (three per SIMD, 168 VGPRs): 9.72 ms at C3 against 10.37 with 8 (round 4)
-        static const int waves_env = getenv("SYDELTA_SCAN_R_WAVES") && atoi(getenv("SYDELTA_SCAN_R_WAVES")) == 8 ? 8 : 12;
-        const int waves = small_r ? 12 : waves_env;
+        const int waves = 12;
         const uint32_t small_words = small_r ? std::max<uint32_t>(ix.max_fwords, 64u) : 0u;
         constexpr LdsR LR = ldsr_layout();
         // one workgroup per CU over contiguous host tiles, an even number each (runs are pairs)
@@ -4684,12 +4679,9 @@ hipError_t launch_scan(const uint8_t* d_buf, const ScanSeg* d_segs, uint32_t nse
             if (small_r) {
                 if (a.ablate) hipLaunchKernelGGL((k_scan_r<true, false, 12, true>), g, b, LR.total, s, a, per, small_words);
                 else hipLaunchKernelGGL((k_scan_r<false, false, 12, true>), g, b, LR.total, s, a, per, small_words);
-            } else if (waves == 12) {
+            } else {
                 if (ix.l1_ribbon) { if (a.ablate) LAUNCH_R(true, true, 12); else LAUNCH_R(false, true, 12); }
                 else { if (a.ablate) LAUNCH_R(true, false, 12); else LAUNCH_R(false, false, 12); }
-            } else {
-                if (ix.l1_ribbon) { if (a.ablate) LAUNCH_R(true, true, 8); else LAUNCH_R(false, true, 8); }
-                else { if (a.ablate) LAUNCH_R(true, false, 8); else LAUNCH_R(false, false, 8); }
             }
 #undef LAUNCH_R
         }

@@ -316,8 +316,10 @@ def test_chunk_pipeline_two_parts(gpu, oracle_c, monkeypatch, preroll, slim, seg
     d = _chunk_walk(gpu, src, basis, bs, [0, npos])
     prof = gpu.profile(reset=True)
     gpu.set_profiling(False)
-    assert prof["k_walk_files"]["count"] >= 2, prof  # two parts (and any re-walks)
-    nparts_pre = {"0": 0, "1": 1, "2": 2}[preroll]
+    nseg = -(-(npos // bs + 1) // int(seg or 128))
+    parts = 2 if nseg >= 512 else 1  # (chunk_pipe_parts)
+    assert prof["k_walk_files"]["count"] >= parts, prof  # the parts (and any re-walks)
+    nparts_pre = {"0": 0, "1": 1, "2": parts}[preroll]
     assert prof.get("k_preroll", {}).get("count", 0) == nparts_pre, prof
     assert prof.get("k_walk_files_slim", {}).get("count", 0) == (nparts_pre if slim == "1" else 0), prof
     exp = _oracle_ops(oracle_c, src, basis, bs)
