@@ -623,6 +623,13 @@ struct sydelta_index {
     // another path (index_full): a C4 step then has no index build at all.
     bool deferred = false;
     std::mutex build_mu;
+    // A single-file index's scan extras (the level-1 filter, the fat table) are filled by the
+    // first scan that runs against it (scan_index): the chunk walk and the aligned probe read
+    // only the Bloom filter and the exact table (C5: 1-8 Mi keys).  extras_ev orders scans on
+    // other streams after them.
+    bool extras_deferred = false;
+    hipEvent_t extras_ev = nullptr;
+    hipStream_t extras_stream = nullptr;
 };
 
 namespace {
@@ -771,6 +778,7 @@ void give_event(int device, hipEvent_t e) {
 static void index_release(sydelta_index* x) {
     if (!x) return;
     if (x->rib_ev) (void)hipEventDestroy(x->rib_ev);
+    if (x->extras_ev) (void)hipEventDestroy(x->extras_ev);
     // the build has uploaded the file tables from `stage` (done long before, as a rule)
     if (x->ready) (void)hipEventSynchronize(x->ready);
     give_mapped(x->stage, kStage);
@@ -1152,9 +1160,10 @@ static int index_create_impl(int device, const uint32_t* weak, const uint64_t* s
         // build waits for a match that takes another path (index_full)
         x->deferred = nfiles >= 2 && block_size % 64 == 0 && block_size >= 256 && block_size <= kWalkMaxN &&
                       max_nblk <= kSelfIxMaxBlocks && !ix.l1;
+        x->extras_deferred = nfiles == 1 && ix.l1 != nullptr;
         if (!x->deferred) {
             CallProf cp;
-            HIP_TRY(launch_index_build(x->d_weak, x->d_strong, ix, sb, cp.get()));
+            HIP_TRY(launch_index_build(x->d_weak, x->d_strong, ix, sb, cp.get(), !x->extras_deferred));
         }
         HIP_TRY(hipEventRecord(x->ready, sb));
         *out = x.release();
@@ -1263,6 +1272,8 @@ void give_ops(OpVec&& v) {
 // the walks that fill them, and their release as much again (tools/walk_bench_c4.cpp,
 // 10 000 C4 files on 8 threads in this container: walks 14 ms with fresh arrays, 5.3 ms
 // with recycled ones, and 14 ms to free the fresh ones).  At most kSmallPoolBytes held.
+struct OpSlab;
+OpSlab* slab_of(const void* q);  // (below)
 std::mutex g_small_mu;
 std::vector<OpVec>* g_small_pool = new std::vector<OpVec>();  // never destroyed (exit order)
 size_t g_small_bytes = 0;
@@ -1271,7 +1282,7 @@ void give_small_ops(std::vector<sydelta_delta>& d) {
     std::lock_guard<std::mutex> lk(g_small_mu);
     for (auto& x : d) {
         const size_t c = x.ops.capacity() * sizeof(sydelta_op);
-        if (!c || c >= kOpArenaMin) continue;
+        if (!c || c >= kOpArenaMin || slab_of(x.ops.data())) continue;  // (a slab's arrays go back to it)
         if (g_small_bytes + c > kSmallPoolBytes) break;
         g_small_bytes += c;
         g_small_pool->push_back(std::move(x.ops));
@@ -1294,6 +1305,90 @@ void take_small_ops(std::vector<sydelta_delta>& d) {
         g_small_bytes -= x.ops.capacity() * sizeof(sydelta_op);
         x.ops.clear();
     }
+}
+
+// Op slabs (OpSlabHooks, sydelta_walk.hpp): when the device expands a batch's op lists
+// (k_walk_expand), every file's op array is reserved from one pinned, host-mapped slab that
+// the kernel writes into.  A slab counts its live arrays (+1 while the batch reserves from it)
+// and is reused once they are all gone; slabs are kept for the process (at most kMaxSlabs:
+// ten concurrent callers take one each), so a released array never races with a free.
+struct OpSlab {
+    uint8_t* p = nullptr;
+    size_t bytes = 0;
+    std::atomic<int64_t> live{0};
+};
+constexpr int kMaxSlabs = 32;
+std::atomic<OpSlab*> g_slab_tab[kMaxSlabs];
+std::mutex g_slab_mu;
+thread_local OpSlab* t_slab = nullptr;  // the slab this thread reserves from
+thread_local size_t t_slab_used = 0;
+void* slab_take(size_t bytes) {
+    OpSlab* sl = t_slab;
+    if (!sl || t_slab_used + bytes > sl->bytes) return nullptr;
+    void* q = sl->p + t_slab_used;
+    t_slab_used += bytes;  // (multiples of 24 bytes: every array stays 8-byte aligned)
+    sl->live.fetch_add(1);
+    return q;
+}
+OpSlab* slab_of(const void* q) {
+    for (int i = 0; i < kMaxSlabs; ++i) {
+        OpSlab* sl = g_slab_tab[i].load(std::memory_order_acquire);
+        if (sl && (const uint8_t*)q >= sl->p && (const uint8_t*)q < sl->p + sl->bytes) return sl;
+    }
+    return nullptr;
+}
+bool slab_give(void* q) {
+    OpSlab* sl = slab_of(q);
+    if (!sl) return false;
+    sl->live.fetch_sub(1);
+    return true;
+}
+// A slab of at least `bytes` for this thread's reservations (nullptr: none to be had, the host
+// expands); slab_close ends them.
+OpSlab* slab_open(size_t bytes) {
+    static std::once_flag once;
+    std::call_once(once, [] {
+        op_slab().take = slab_take;
+        op_slab().give = slab_give;
+    });
+    std::lock_guard<std::mutex> lk(g_slab_mu);
+    OpSlab* best = nullptr;
+    int freei = -1;
+    for (int i = 0; i < kMaxSlabs; ++i) {
+        OpSlab* sl = g_slab_tab[i].load(std::memory_order_acquire);
+        if (!sl) {
+            if (freei < 0) freei = i;
+            continue;
+        }
+        if (sl->live.load() == 0 && sl->bytes >= bytes && (!best || sl->bytes < best->bytes)) best = sl;
+    }
+    if (best) {
+        int64_t z = 0;
+        if (!best->live.compare_exchange_strong(z, 1)) best = nullptr;  // (taken back by a late release? no: live 0 stays 0)
+    }
+    if (!best) {
+        if (freei < 0) return nullptr;
+        size_t want = (size_t)1 << 20;
+        while (want < bytes) want <<= 1;  // powers of two: reuse across batch sizes
+        OpSlab* sl = new OpSlab();
+        if (hipHostMalloc((void**)&sl->p, want, hipHostMallocMapped | hipHostMallocPortable | hipHostMallocCoherent) !=
+            hipSuccess) {
+            delete sl;
+            return nullptr;
+        }
+        sl->bytes = want;
+        sl->live.store(1);
+        g_slab_tab[freei].store(sl, std::memory_order_release);
+        best = sl;
+    }
+    t_slab = best;
+    t_slab_used = 0;
+    return best;
+}
+void slab_close(OpSlab* sl) {
+    t_slab = nullptr;
+    t_slab_used = 0;
+    if (sl) sl->live.fetch_sub(1);
 }
 }  // namespace
 
@@ -1682,6 +1777,19 @@ int Classifier::probe(int mode) {
 // by the first scan that wants it, sydelta_index::rib_mode) or as built (the Bloom).
 static hipError_t scan_index(sydelta_index* x, uint64_t tot_pos, hipStream_t s, Profiler* prof, DeviceIndex& out) {
     out = x->ix;
+    {  // the scan extras, filled by the first scan (sydelta_index::extras_deferred)
+        std::lock_guard<std::mutex> lk(x->build_mu);
+        if (x->extras_deferred) {
+            if (hipError_t e = launch_index_extras(x->d_weak, x->ix, s, prof)) return e;
+            if (!x->extras_ev)
+                if (hipError_t e = hipEventCreateWithFlags(&x->extras_ev, hipEventDisableTiming)) return e;
+            if (hipError_t e = hipEventRecord(x->extras_ev, s)) return e;
+            x->extras_deferred = false;
+            x->extras_stream = s;
+        } else if (x->extras_ev && x->extras_stream != s) {
+            if (hipError_t e = hipStreamWaitEvent(s, x->extras_ev, 0)) return e;
+        }
+    }
     if (x->rib_mode == 0 || (x->rib_mode == 1 && tot_pos < kRibMinScan)) return hipSuccess;
     {
         std::lock_guard<std::mutex> lk(x->rib_mu);
@@ -2422,16 +2530,26 @@ struct WalkResult {
     std::vector<WalkFileOut> out;  // per unit
     const WalkRec* rec = nullptr;  // compact records: unit u's at rec[out[u].base, + out[u].count)
     uint64_t nrec = 0;
+    const ExpandOut* xres = nullptr;  // with an ExpandReq: per file (the thread's mapped buffer)
     double ms_kernel = 0, ms_d2h = 0;
 };
+// The op lists expanded on the device after the walk (k_walk_expand): file f's units
+// [fu[f], fu[f + 1]), its ops at ops + op_off[f] (host-mapped, capacity to op_off[f + 1]).
+struct ExpandReq {
+    const uint32_t* fu;
+    const uint64_t* op_off;
+    sydelta_op* ops;
+};
 static int run_walk(sydelta_index* ix, const uint8_t* base, const std::vector<WalkUnit>& units, const uint32_t* ahit,
-                    const uint32_t* apw, bool lds_filter, hipStream_t s, Profiler* prof, WalkResult& res) {
+                    const uint32_t* apw, bool lds_filter, hipStream_t s, Profiler* prof, WalkResult& res,
+                    const ExpandReq* ex = nullptr) {
     ScratchHold hold;
     const auto t0 = std::chrono::steady_clock::now();
     const uint64_t nu = units.size(), nf = ix->nfiles;
     res.out.clear();
     res.rec = nullptr;
     res.nrec = 0;
+    res.xres = nullptr;
     if (!nu) return SYDELTA_OK;
     int cur_dev = 0;
     HIP_TRY(hipGetDevice(&cur_dev));
@@ -2442,17 +2560,25 @@ static int run_walk(sydelta_index* ix, const uint8_t* base, const std::vector<Wa
     // one upload: the unit table, the last sizes and the zeroed record counter (+ the 16
     // SYDELTA_PHASE_TIMING tick counters) -- ten concurrent callers' extra copies showed
     auto al = [](size_t v) { return (v + 255) & ~(size_t)255; };
-    const size_t o_units = 0, o_last = ubytes, o_total = o_last + lbytes, up = o_total + 136;
+    const size_t o_units = 0, o_last = ubytes, o_total = o_last + lbytes, o_fu = al(o_total + 136);
+    const size_t o_opoff = o_fu + al(4 * (nf + 1)), up = ex ? o_opoff + 8 * (nf + 1) : o_total + 136;
     PinnedHits& ph = thread_pinned_hits();
     if (int r = pinned_at_least(ph, std::max(up, fout_bytes + 16))) return r;
     memcpy(ph.p, units.data(), ubytes);
     memcpy(ph.p + o_last, ix->last_size.data(), lbytes);
     memset(ph.p + o_total, 0, 136);
-    // device: the upload, the staged records; host (coherent, mapped; the thread's, kept): the
-    // per-unit results and the compacted records, which the kernel writes there directly --
-    // one stream synchronisation, no D2H round trips
-    const size_t o_stage = al(up), need = o_stage + al(sizeof(WalkRec) * rec_total);
-    const size_t m_rec = al(fout_bytes), m_need = m_rec + sizeof(WalkRec) * rec_total;
+    if (ex) {
+        memcpy(ph.p + o_fu, ex->fu, 4 * (nf + 1));
+        memcpy(ph.p + o_opoff, ex->op_off, 8 * (nf + 1));
+    }
+    // device: the upload, the staged records (+ the per-unit results' device copy for the
+    // expansion); host (coherent, mapped; the thread's, kept): the per-unit results and the
+    // compacted records, which the kernel writes there directly -- one stream synchronisation,
+    // no D2H round trips (+ the expansion's per-file results)
+    const size_t o_stage = al(up), o_fdev = o_stage + al(sizeof(WalkRec) * rec_total);
+    const size_t need = o_fdev + (ex ? al(fout_bytes) : 0);
+    const size_t m_rec = al(fout_bytes), m_res = al(m_rec + sizeof(WalkRec) * rec_total);
+    const size_t m_need = m_res + (ex ? sizeof(ExpandOut) * nf : 0);
     PinnedHits& wm = thread_walk_map();
     if (wm.bytes < m_need) {
         if (wm.p) {
@@ -2499,7 +2625,24 @@ static int run_walk(sydelta_index* ix, const uint8_t* base, const std::vector<Wa
     a.fout = (WalkFileOut*)wm.p;
     a.total = (unsigned long long*)(D + o_total);
     a.ticks = timing ? a.total + 1 : nullptr;
+    a.fout_dev = ex ? (WalkFileOut*)(D + o_fdev) : nullptr;
     HIP_TRY(launch_walk_files(a, s, prof));
+    if (ex) {
+        ExpandArgs xa{};
+        xa.units = a.units;
+        xa.fout = a.fout_dev;
+        xa.stage = a.stage;
+        xa.fu = (const uint32_t*)(D + o_fu);
+        xa.fblk = ix->ix.d_fblk;
+        xa.last_size = a.last_size;
+        xa.op_off = (const uint64_t*)(D + o_opoff);
+        xa.ops = ex->ops;
+        xa.res = (ExpandOut*)(wm.p + m_res);
+        xa.nf = (uint32_t)nf;
+        xa.n = (uint32_t)ix->bs;
+        HIP_TRY(launch_walk_expand(xa, s, prof));
+        res.xres = xa.res;
+    }
     if (timing) {
         unsigned long long tk[16];
         HIP_TRY(hipMemcpyAsync(tk, a.ticks, sizeof tk, hipMemcpyDeviceToHost, s));
@@ -2621,9 +2764,68 @@ static int match_walk_files(sydelta_index* ix, const uint8_t* d_buf, const uint6
     }
     fu[nf] = units.size();
     const uint64_t nu = units.size();
+    // the op lists: expanded on the device into op arrays reserved from a pinned host-mapped
+    // slab (k_walk_expand) when the host has few threads for them (SYDELTA_DEVICE_EXPAND=0|1
+    // forces it off / on; per call), else on the host below
+    static const int asm_threads = getenv("SYDELTA_ASM_THREADS") ? std::max(1, atoi(getenv("SYDELTA_ASM_THREADS")))
+                                                                   : walk::HostPool::get().size() + 1;
+    const char* dxe = getenv("SYDELTA_DEVICE_EXPAND");
+    const bool dexp = (dxe && *dxe) ? dxe[0] == '1' : asm_threads <= 4;
+    std::vector<uint64_t> op_off;
+    std::vector<uint32_t> fu32;
+    ExpandReq req{};
+    bool expand_dev = false;
+    if (dexp) {
+        op_off.assign(nf + 1, 0);
+        fu32.resize(nf + 1);
+        for (uint64_t f = 0; f < nf; ++f) {
+            uint64_t cap = 0;  // ops per unit: a Copy per block, a Data op before each, the tail's two
+            for (uint64_t u = fu[f]; u < fu[f + 1]; ++u) cap += 2 * ((units[u].end - units[u].entry) / n) + 8;
+            op_off[f + 1] = op_off[f] + cap;
+            fu32[f] = (uint32_t)fu[f];
+        }
+        fu32[nf] = (uint32_t)fu[nf];
+        if (OpSlab* slab = slab_open(op_off[nf] * sizeof(sydelta_op))) {
+            expand_dev = true;
+            for (uint64_t f = 0; f < nf; ++f) {
+                OpVec v;
+                v.reserve(op_off[f + 1] - op_off[f]);  // (from the slab, in file order)
+                expand_dev = expand_dev && (uint8_t*)v.data() == slab->p + op_off[f] * sizeof(sydelta_op);
+                b->d[f].ops.swap(v);
+            }
+            req = ExpandReq{fu32.data(), op_off.data(), (sydelta_op*)slab->p};
+            slab_close(slab);
+        }
+    }
+    if (!expand_dev) take_small_ops(b->d);  // recycled per-file op arrays
     WalkResult res;
-    if (int r = run_walk(ix, d_buf, units, nullptr, nullptr, true, s, prof, res)) return r;
+    if (int r = run_walk(ix, d_buf, units, nullptr, nullptr, true, s, prof, res, expand_dev ? &req : nullptr)) return r;
     const auto t1 = std::chrono::steady_clock::now();
+    if (res.xres) {  // every file expanded on the device (a file that needs a re-walk: the host path below)
+        bool all = true;
+        for (uint64_t f = 0; f < nf && all; ++f) all = !res.xres[f].bad;
+        if (all) {
+            for (uint64_t f = 0; f < nf; ++f) {
+                const ExpandOut& x = res.xres[f];
+                sydelta_delta& d = b->d[f];
+                d.ops.resize(x.nops);  // (written by the device; no initialisation)
+                d.stats.copy_ops = x.nops - x.data_ops;
+                d.stats.data_ops = x.data_ops;
+                d.stats.literal_bytes = x.lit;
+                d.stats.weak_hits = x.weak_hits;
+                d.stats.verified_hits = x.hits;
+                b->total.copy_ops += d.stats.copy_ops;
+                b->total.data_ops += x.data_ops;
+                b->total.literal_bytes += x.lit;
+                b->total.weak_hits += x.weak_hits;
+                b->total.verified_hits += x.hits;
+            }
+            if (host_timing)
+                fprintf(stderr, "sydelta file walk: %llu files in %llu units, ops expanded on the device: kernels %.3f ms, "
+                        "results %.3f ms\n", (unsigned long long)nf, (unsigned long long)nu, res.ms_kernel, ms_since(t1));
+            return SYDELTA_OK;
+        }
+    }
     std::vector<WalkFileOut>& out = res.out;
     std::vector<std::pair<const WalkRec*, const WalkRec*>> span(nu);
     for (uint64_t u = 0; u < nu; ++u) span[u] = {res.rec + out[u].base, res.rec + out[u].base + out[u].count};
@@ -2678,8 +2880,6 @@ static int match_walk_files(sydelta_index* ix, const uint8_t* d_buf, const uint6
     }
     // each file's records into its op array (recycled arrays: no page faults), on the host
     // pool and the caller (SYDELTA_ASM_THREADS overrides)
-    static const int asm_threads = getenv("SYDELTA_ASM_THREADS") ? std::max(1, atoi(getenv("SYDELTA_ASM_THREADS")))
-                                                                   : walk::HostPool::get().size() + 1;
     const int nthr = nf >= 64 ? (int)std::min<uint64_t>(asm_threads, (nf + 63) / 64) : 1;
     std::atomic<uint64_t> next{0};
     std::vector<sydelta_match_stats> part(nthr);
@@ -2767,7 +2967,6 @@ static int match_impl(sydelta_index* ix, const uint8_t* d_buf, const uint64_t* s
     const uint64_t n = ix->bs;
     const uint64_t nf = ix->nfiles;
     b->d.assign(nf, sydelta_delta());
-    if (nf >= 64) take_small_ops(b->d);  // recycled per-file op arrays
     Classifier C;
     C.ix = ix;
     C.base = d_buf;
@@ -2805,6 +3004,7 @@ static int match_impl(sydelta_index* ix, const uint8_t* d_buf, const uint64_t* s
     b->total.positions = tot_pos;
     if (file_walk_ok(ix, src_off, src_len, d_buf)) return match_walk_files(ix, d_buf, src_off, src_len, s, C.prof, b);
     if (int r = index_full(ix, s)) return r;  // the classifier's probes and scans read the tables
+    if (nf >= 64) take_small_ops(b->d);       // recycled per-file op arrays
     static const bool host_timing = getenv("SYDELTA_HOST_TIMING") != nullptr;
     const auto t0 = std::chrono::steady_clock::now();
     const int mode = n > scan_max_window() && !wide_scan(ix) ? 0 : mode_hint != -2 ? mode_hint : probe_mode_env();
@@ -2963,6 +3163,23 @@ extern "C" int sydelta_match_device(sydelta_index* idx, const uint8_t* d_src, ui
     static const bool host_timing = getenv("SYDELTA_HOST_TIMING") != nullptr;
     const auto t0 = std::chrono::steady_clock::now();
     int mode = -2;
+    // the ribbon level-1 a whole-file scan of this many positions takes (scan_index), built now
+    // from the signature's weak values -- beside the index's own build on the aux stream --
+    // instead of from its exact table after it (SYDELTA_EARLY_RIBBON=0: after, as in round 5)
+    const uint64_t npos_all = len >= idx->bs ? len - idx->bs + 1 : 0;
+    const char* er = getenv("SYDELTA_EARLY_RIBBON");
+    if ((!er || er[0] != '0') && s == idx->stream && idx->nfiles == 1 &&
+        (idx->rib_mode == 2 || (idx->rib_mode == 1 && npos_all >= kRibMinScan))) {
+        std::lock_guard<std::mutex> lk(idx->rib_mu);
+        if (!idx->rib_built) {
+            CallProf cp;
+            HIP_TRY(launch_ribbon_build(idx->ix, s, cp.get(), idx->d_weak, idx->fblk[1]));
+            if (!idx->rib_ev) HIP_TRY(hipEventCreateWithFlags(&idx->rib_ev, hipEventDisableTiming));
+            HIP_TRY(hipEventRecord(idx->rib_ev, s));
+            idx->rib_built = true;
+            idx->rib_stream = s;
+        }
+    }
     // a copy-heavy source is walked by K10 as one chunk (generator.rs:116-221 on the device);
     // a literal-heavy one by the classifier, whose probe sample would say the same (mode 0)
     if (chunk_walk_ok(idx) && probe_mode_env() < 0 && len >= idx->bs && idx->fblk[1] > 0 &&

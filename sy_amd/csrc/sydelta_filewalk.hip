@@ -569,7 +569,10 @@ __global__ __launch_bounds__(64, 4) void k_walk_files(WalkArgs a) {
             a.out[base + i] = WalkRec{r->kind, r->a, r->off};
         }
     }
-    if (lane == 0) a.fout[blockIdx.x] = WalkFileOut{(uint32_t)base, nrec, weak_hits, hits, exit, 0};
+    if (lane == 0) {
+        a.fout[blockIdx.x] = WalkFileOut{(uint32_t)base, nrec, weak_hits, hits, exit, 0};
+        if (a.fout_dev) a.fout_dev[blockIdx.x] = WalkFileOut{(uint32_t)base, nrec, weak_hits, hits, exit, 0};
+    }
     if (kSlim && lane == 0) const_cast<WalkUnit*>(a.units)[blockIdx.x].final_ = U.final_ | kUnitDone;
     wtick(kWtOut);
 }
@@ -644,8 +647,156 @@ __global__ __launch_bounds__(64, 4) void k_preroll(WalkArgs a, uint32_t* ahit, u
 }
 
 // ===========================================================================
+// K10's op lists expanded on the device (launch_walk_expand)
+// ===========================================================================
+// One wave per file.  The file's units' records are gathered into LDS in unit order; lane 0
+// chains them (the walk from the previous unit's exit: a unit that started there, or earlier
+// with a leading literal run reaching it, which is cut there) and merges a Data op ending at
+// a unit's end with the next unit's first one; then every lane takes ops i = lane, lane + 64,
+// ...: the record holding op i (a binary search of the records' op prefix) gives it -- a Data
+// op, or Copy (g - gb0) n of block g of a copy run, sized n or the basis's last size.  The ops
+// go to host-mapped memory as three 8-byte stores per lane (24-byte stride).
+__global__ __launch_bounds__(64) void k_walk_expand(ExpandArgs a) {
+    __shared__ WalkRec rec[kExpandRecs];
+    __shared__ uint32_t pre[kExpandRecs];  // inclusive op prefix over the merged records
+    __shared__ uint32_t ustart[65];
+    __shared__ uint32_t s_m, s_bad;
+    const uint32_t f = blockIdx.x, lane = threadIdx.x;
+    const uint32_t u0 = a.fu[f], u1 = a.fu[f + 1], nu = u1 - u0;
+    ExpandOut* res = a.res + f;
+    // gather the units' staged records
+    uint32_t total = 0;
+    bool over = nu > 64;
+    for (uint32_t k = 0; k < nu && !over; ++k) {
+        const uint32_t c = a.fout[u0 + k].count;
+        if (total + c > kExpandRecs) {
+            over = true;
+            break;
+        }
+        const WalkRec* src = a.stage + a.units[u0 + k].rec_off;
+        for (uint32_t i = lane; i < c; i += 64) rec[total + i] = src[i];
+        if (lane == 0) ustart[k] = total;
+        total += c;
+    }
+    if (over) {
+        if (lane == 0) *res = ExpandOut{0, 0, 0, 0, 0, 1, 0};
+        return;
+    }
+    if (lane == 0) ustart[nu] = total;
+    __syncthreads();
+    uint32_t wh = 0, vh = 0;  // (every lane's partial sums of the units' counters)
+    for (uint32_t k = lane; k < nu; k += 64) {
+        wh += a.fout[u0 + k].weak_hits;
+        vh += a.fout[u0 + k].hits;
+    }
+    if (lane == 0) {  // chain and merge in place (the output index never passes the input's)
+        uint32_t m = 0, bad = 0;
+        for (uint32_t k = 0; k < nu && !bad; ++k) {
+            uint32_t r0 = ustart[k];
+            const uint32_t r1 = ustart[k + 1];
+            if (k > 0) {
+                const uint64_t pe = a.fout[u0 + k - 1].exit, entry = a.units[u0 + k].entry;
+                if (entry != pe) {
+                    if (pe > entry && r0 < r1 && rec[r0].kind == 0 && rec[r0].off == entry &&
+                        rec[r0].off + rec[r0].a >= pe) {
+                        const uint64_t h = rec[r0].off + rec[r0].a;
+                        if (h == pe) {
+                            ++r0;
+                        } else {
+                            rec[r0].a = (uint32_t)(h - pe);
+                            rec[r0].off = pe;
+                        }
+                    } else {
+                        bad = 1;
+                    }
+                }
+            }
+            for (uint32_t r = r0; r < r1 && !bad; ++r) {
+                const WalkRec x = rec[r];
+                if (!x.kind && m && !rec[m - 1].kind && rec[m - 1].off + rec[m - 1].a == x.off)
+                    rec[m - 1].a += x.a;
+                else
+                    rec[m++] = x;
+            }
+        }
+        s_m = m;
+        s_bad = bad;
+    }
+    __syncthreads();
+    const uint32_t m = s_m;
+    if (s_bad) {
+        if (lane == 0) *res = ExpandOut{0, 0, 0, 0, 0, 1, 0};
+        return;
+    }
+    // op counts: an inclusive prefix over the records, 64 at a time
+    uint32_t carry = 0, nd = 0;
+    uint64_t lit = 0;
+    for (uint32_t b = 0; b < m; b += 64) {
+        const uint32_t i = b + lane;
+        const WalkRec x = i < m ? rec[i] : WalkRec{1, 0, 0};
+        const uint32_t c = i < m ? (x.kind ? x.kind : 1u) : 0u;
+        if (i < m && !x.kind) {
+            ++nd;
+            lit += x.a;
+        }
+        uint32_t tot;
+        const uint32_t ex = wave_scan_excl(c, tot);
+        if (i < m) pre[i] = carry + ex + c;
+        carry += tot;
+    }
+    __syncthreads();
+    const uint64_t T = carry;
+    const uint64_t gb0 = a.fblk[f], nbf = a.fblk[f + 1] - gb0, ls = a.last_size[f];
+    if (T > a.op_off[f + 1] - a.op_off[f]) {  // (cannot happen: the host sizes by the units' bound)
+        if (lane == 0) *res = ExpandOut{0, 0, 0, 0, 0, 1, 0};
+        return;
+    }
+    uint64_t* w = (uint64_t*)(a.ops + a.op_off[f]);
+    uint32_t r = 0;  // the record of this lane's op (ops ascend: search from the last one)
+    for (uint32_t i = lane; i < (uint32_t)T; i += 64) {
+        uint32_t lo = r, hi = m - 1;
+        while (lo < hi) {  // the first record whose prefix passes i
+            const uint32_t mid = (lo + hi) >> 1;
+            if (pre[mid] > i) hi = mid; else lo = mid + 1;
+        }
+        r = lo;
+        const WalkRec x = rec[r];
+        uint64_t k, oa, ob;
+        if (!x.kind) {
+            k = SYDELTA_OP_DATA;
+            oa = x.off;
+            ob = x.a;
+        } else {
+            const uint64_t g = (uint64_t)x.a - gb0 + (i - (pre[r] - x.kind));
+            k = SYDELTA_OP_COPY;
+            oa = g * a.n;
+            ob = g + 1 == nbf ? ls : (uint64_t)a.n;
+        }
+        w[3 * (uint64_t)i] = k;
+        w[3 * (uint64_t)i + 1] = oa;
+        w[3 * (uint64_t)i + 2] = ob;
+    }
+    // the file's counts
+    uint32_t nd_t = nd;
+    for (int o = 32; o; o >>= 1) {
+        nd_t += __shfl_xor(nd_t, o);
+        lit += __shfl_xor(lit, o);
+        wh += __shfl_xor(wh, o);
+        vh += __shfl_xor(vh, o);
+    }
+    if (lane == 0) *res = ExpandOut{T, nd_t, lit, wh, vh, 0, 0};
+}
+
+// ===========================================================================
 // Launch wrappers
 // ===========================================================================
+hipError_t launch_walk_expand(const ExpandArgs& a, hipStream_t s, Profiler* prof) {
+    if (!a.nf) return hipSuccess;
+    ProfScope ps(prof, s, "k_walk_expand");
+    hipLaunchKernelGGL(k_walk_expand, dim3(a.nf), dim3(64), 0, s, a);
+    return hipGetLastError();
+}
+
 hipError_t launch_walk_files(const WalkArgs& a, hipStream_t s, Profiler* prof, bool slim) {
     if (!a.nunits) return hipSuccess;
     if (a.n % 64 != 0 || a.n < 256 || a.n > kWalkMaxN || a.self_nb > kSelfIxMaxBlocks || (slim && (a.self_nb || !a.ahit)))

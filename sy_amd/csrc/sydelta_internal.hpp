@@ -139,11 +139,19 @@ hipError_t launch_signature_batch(const uint8_t* d_buf, const uint64_t* d_off, c
                                   uint32_t* d_weak, uint64_t* d_strong, hipStream_t s, Profiler* prof);
 // Build filters + exact tables of every file of ix from the concatenated weak
 // values (ix.nblocks entries; ix.d_fblk / ix.d_files already on the device).
+// extras = false leaves the scans' level-1 filter and fat table (ix.l1, ix.fat) unfilled:
+// launch_index_extras fills them when a scan first needs them (the chunk walk and the aligned
+// probe read only the Bloom filter and the exact table).
 hipError_t launch_index_build(const uint32_t* d_weak, const uint64_t* d_strong, DeviceIndex& ix, hipStream_t s,
-                              Profiler* prof);
+                              Profiler* prof, bool extras = true);
+hipError_t launch_index_extras(const uint32_t* d_weak, const DeviceIndex& ix, hipStream_t s, Profiler* prof);
 // The ribbon level-1 of a built single-file index (ix.rib_l1 and its key lists set):
 // its distinct keys listed by shard from the exact table, then each shard solved.
-hipError_t launch_ribbon_build(const DeviceIndex& ix, hipStream_t s, Profiler* prof);
+// keys: the keys to list (nkeys of them, duplicates allowed: a duplicate's equation reduces to 0),
+// by default the exact table's (ix.keys, ix.nslots); the signature's weak values (never
+// kEmptyKey: an Adler digest's low half is below 65521) let it start before the table is built.
+hipError_t launch_ribbon_build(const DeviceIndex& ix, hipStream_t s, Profiler* prof, const uint32_t* keys = nullptr,
+                               uint64_t nkeys = 0);
 uint64_t scan_tile_positions();  // positions per tile of the LDS-staged scan
 // SYDELTA_SCAN_WIDE=0: windows above scan_max_window() take the per-thread k_scan
 // instead of the register-fed k_scan_g (read when the index is built and per call)
@@ -266,9 +274,36 @@ struct WalkArgs {
     WalkRec* stage;              // may be host-mapped memory (with out NULL)
     WalkRec* out;                // compacted records of every unit; NULL: left in stage (base = rec_off)
     WalkFileOut* fout;
+    WalkFileOut* fout_dev;       // optional: a device copy of fout (launch_walk_expand reads it)
     unsigned long long* total;   // records placed in out (zeroed before the launch)
     unsigned long long* ticks;   // SYDELTA_PHASE_TIMING: 16 counters (zeroed), else null
 };
+// The op lists of a batch's walk expanded on the device (k_walk_expand): one wave per file
+// joins its units' staged records (a Data op ending at a unit's end merged with the next
+// unit's first; a unit entered past its start cut at the previous unit's exit when its
+// leading literal run reaches it -- match_walk_files' rules), then writes every op
+// (sydelta_op, generator.rs:10-15: a Copy per block of a copy run) at ops + op_off[f], in
+// host-mapped memory.  A file whose units do not chain that way (it needs a re-walk), whose
+// records exceed kExpandRecs or whose ops exceed op_off[f + 1] - op_off[f] gets bad = 1 and no
+// ops.
+constexpr uint32_t kExpandRecs = 1536;
+struct ExpandOut {
+    uint64_t nops, data_ops, lit;
+    uint32_t weak_hits, hits, bad, pad;
+};
+struct ExpandArgs {
+    const WalkUnit* units;       // the walk's unit table (device)
+    const WalkFileOut* fout;     // its per-unit results (device copy)
+    const WalkRec* stage;        // its staged records (unit u's at stage + units[u].rec_off)
+    const uint32_t* fu;          // nf + 1: file f's units [fu[f], fu[f + 1])
+    const uint64_t* fblk;        // the index's block prefix
+    const uint64_t* last_size;   // per file
+    const uint64_t* op_off;      // nf + 1: file f's ops at ops + op_off[f], capacity to op_off[f + 1]
+    sydelta_op* ops;
+    ExpandOut* res;              // per file
+    uint32_t nf, n;
+};
+hipError_t launch_walk_expand(const ExpandArgs& a, hipStream_t s, Profiler* prof);
 // slim: the walk of units whose aligned misses were pre-rolled (launch_preroll; a.ahit set,
 // the filter in global memory), for the units whose walk stays on the aligned grid; it marks
 // them done (kUnitDone in WalkUnit::final_, the unit table written), and a full launch after it

@@ -4420,26 +4420,53 @@ hipError_t launch_signature_batch_fast(const uint8_t* d_buf, const uint64_t* d_a
     return hipGetLastError();
 }
 
-hipError_t launch_ribbon_build(const DeviceIndex& ix, hipStream_t s, Profiler* prof) {
+hipError_t launch_ribbon_build(const DeviceIndex& ix, hipStream_t s, Profiler* prof, const uint32_t* keys,
+                               uint64_t nkeys) {
     if (!ix.rib_l1 || !ix.rib_keys || ix.nfiles != 1) return hipErrorInvalidValue;
+    if (!keys) {  // the exact table's slots (kEmptyKey: free)
+        keys = ix.keys;
+        nkeys = ix.nslots;
+    }
     hipError_t e;
     if ((e = hipMemsetAsync(ix.rib_cnt, 0, 4 * (kRibShards + 1), s))) return e;
     if ((e = hipMemsetAsync(ix.rib_l1, 0, 4 * (size_t)kL1WordsR, s))) return e;
     ProfScope ps(prof, s, "k_ribbon_build");  // listing + solving
-    const uint64_t per = std::max<uint64_t>(4096, ((uint64_t)ix.nslots + 127) / 128);  // 128 workgroups
-    hipLaunchKernelGGL(k_ribbon_list, dim3((uint32_t)((ix.nslots + per - 1) / per)), dim3(kRibListT), 0, s, ix.keys,
-                       (uint64_t)ix.nslots, per, ix.rib_keys, ix.rib_cnt, ix.rib_over);
+    const uint64_t per = std::max<uint64_t>(4096, (nkeys + 127) / 128);  // 128 workgroups
+    hipLaunchKernelGGL(k_ribbon_list, dim3((uint32_t)((nkeys + per - 1) / per)), dim3(kRibListT), 0, s, keys, nkeys,
+                       per, ix.rib_keys, ix.rib_cnt, ix.rib_over);
     if ((e = hipGetLastError())) return e;
     hipLaunchKernelGGL(k_ribbon_build, dim3(kRibShards), dim3(64), 0, s, ix.rib_keys, ix.rib_cnt, ix.rib_over,
                        ix.rib_l1);
     return hipGetLastError();
 }
 
+// The level-1 filter's bits (as k_idx_insert sets them), for an index built without its extras
+__global__ void k_idx_l1(const uint32_t* __restrict__ weak, uint64_t n, uint32_t* __restrict__ l1, uint32_t l1_wshift) {
+    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const ProbeHash h = probe_hash(weak[i]);
+    atomicOr(l1 + (l1_wshift == 1 ? (size_t)l1r_word(h.q) : (size_t)(h.q >> l1_wshift)), 1u << (h.q & 31));
+}
+
+hipError_t launch_index_extras(const uint32_t* d_weak, const DeviceIndex& ix, hipStream_t s, Profiler* prof) {
+    hipError_t e;
+    if (!ix.l1 || !ix.nblocks) return hipSuccess;
+    ProfScope ps(prof, s, "k_idx_extras");
+    if ((e = hipMemsetAsync(ix.l1, 0, l1_total_words(ix.l1_wshift) * 4, s))) return e;
+    hipLaunchKernelGGL(k_idx_l1, dim3(grid_for(ix.nblocks, 256)), dim3(256), 0, s, d_weak, ix.nblocks, ix.l1,
+                       ix.l1_wshift);
+    if ((e = hipGetLastError())) return e;
+    if (ix.fat)
+        hipLaunchKernelGGL(k_idx_fat, dim3(grid_for(ix.nslots, 256)), dim3(256), 0, s, (uint64_t)ix.nslots, ix.keys,
+                           ix.cnt, ix.start, ix.order, ix.cstrong, ix.fat);
+    return hipGetLastError();
+}
+
 hipError_t launch_index_build(const uint32_t* d_weak, const uint64_t* d_strong, DeviceIndex& ix, hipStream_t s,
-                              Profiler* prof) {
+                              Profiler* prof, bool extras) {
     hipError_t e;
     if ((e = hipMemsetAsync(ix.filt, 0, ix.fwords * 4, s))) return e;
-    if (ix.l1 && (e = hipMemsetAsync(ix.l1, 0, l1_total_words(ix.l1_wshift) * 4, s))) return e;
+    if (extras && ix.l1 && (e = hipMemsetAsync(ix.l1, 0, l1_total_words(ix.l1_wshift) * 4, s))) return e;
     if ((e = hipMemsetAsync(ix.keys, 0xFF, ix.nslots * 4, s))) return e;
     if ((e = hipMemsetAsync(ix.cnt, 0, ix.nslots * 4, s))) return e;
     const uint64_t n = ix.nblocks;
@@ -4447,8 +4474,8 @@ hipError_t launch_index_build(const uint32_t* d_weak, const uint64_t* d_strong, 
     {
         ProfScope ps(prof, s, "k_idx_insert");
         hipLaunchKernelGGL(k_idx_insert, dim3(grid_for(n, 256)), dim3(256), 0, s, d_weak, n, ix.d_fblk,
-                           (uint32_t)ix.nfiles, ix.d_files, ix.filt, ix.l1, ix.l1_wshift, ix.keys, ix.cnt,
-                           ix.slot_of);
+                           (uint32_t)ix.nfiles, ix.d_files, ix.filt, extras ? ix.l1 : nullptr, ix.l1_wshift, ix.keys,
+                           ix.cnt, ix.slot_of);
     }
     size_t tmp = 0;
     if ((e = hipcub::DeviceScan::ExclusiveSum(nullptr, tmp, ix.cnt, ix.start, (int)ix.nslots, s))) return e;
@@ -4479,7 +4506,7 @@ hipError_t launch_index_build(const uint32_t* d_weak, const uint64_t* d_strong, 
     }
     hipLaunchKernelGGL(k_idx_cstrong, dim3(grid_for(n, 256)), dim3(256), 0, s, n, ix.order, d_strong, ix.cstrong);
     if ((e = hipGetLastError())) return e;
-    if (ix.fat)
+    if (extras && ix.fat)
         hipLaunchKernelGGL(k_idx_fat, dim3(grid_for(ix.nslots, 256)), dim3(256), 0, s, (uint64_t)ix.nslots, ix.keys,
                            ix.cnt, ix.start, ix.order, ix.cstrong, ix.fat);
     return hipGetLastError();

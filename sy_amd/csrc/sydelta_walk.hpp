@@ -54,6 +54,17 @@ inline OpArena& op_arena() {
     return a;
 }
 constexpr size_t kOpArenaMin = 1u << 20;
+// Op slabs: a batch whose op lists the device expands (sydelta_api.cpp) reserves every file's
+// op array from one pinned, host-mapped slab.  While the calling thread has a slab open,
+// allocate() takes from it; deallocate() recognises slab memory and counts it off.
+struct OpSlabHooks {
+    void* (*take)(size_t bytes) = nullptr;  // from the calling thread's open slab, else nullptr
+    bool (*give)(void* p) = nullptr;        // true if p lies in a slab (then counted off)
+};
+inline OpSlabHooks& op_slab() {
+    static OpSlabHooks h;
+    return h;
+}
 
 template <class T>
 struct OpAlloc {
@@ -62,12 +73,17 @@ struct OpAlloc {
     template <class U>
     OpAlloc(const OpAlloc<U>&) {}
     T* allocate(size_t n) {
+        const OpSlabHooks& S = op_slab();
+        if (S.take)
+            if (void* p = S.take(n * sizeof(T))) return (T*)p;
         const OpArena& A = op_arena();
         if (n * sizeof(T) >= kOpArenaMin && A.alloc)
             if (void* p = A.alloc(n * sizeof(T))) return (T*)p;
         return std::allocator<T>().allocate(n);
     }
     void deallocate(T* p, size_t n) {
+        const OpSlabHooks& S = op_slab();
+        if (S.give && S.give(p)) return;
         const OpArena& A = op_arena();
         if (n * sizeof(T) >= kOpArenaMin && A.release && A.release(p)) return;
         std::allocator<T>().deallocate(p, n);

@@ -657,10 +657,13 @@ def batch_and_chunk_checks():
     for bs in (1024, 4096):
         # "0" / "1" / "auto": the classifier path (SYDELTA_FILE_WALK=0); "walk": the file
         # walk (K10), which a batch of >= 64 small files takes by default
-        for probe in ("0", "1", "auto", "walk", "walk8"):  # walk8: segments of >= 8 blocks (SYDELTA_FILE_SEGS=8)
+        # walk8: segments of >= 8 blocks (SYDELTA_FILE_SEGS=8); *dx: the op lists expanded on the
+        # device (SYDELTA_DEVICE_EXPAND=1, k_walk_expand), else on the host
+        for probe in ("0", "1", "auto", "walk", "walk8", "walkdx", "walk8dx"):
             os.environ["SYDELTA_FILE_WALK"] = "0"
-            os.environ["SYDELTA_FILE_SEGS"] = "8" if probe == "walk8" else ""
-            if probe in ("auto", "walk", "walk8"):
+            os.environ["SYDELTA_FILE_SEGS"] = "8" if probe.startswith("walk8") else ""
+            os.environ["SYDELTA_DEVICE_EXPAND"] = "1" if probe.endswith("dx") else "0"
+            if probe in ("auto", "walk", "walk8", "walkdx", "walk8dx"):
                 os.environ.pop("SYDELTA_PROBE", None)
             else:
                 os.environ["SYDELTA_PROBE"] = probe
@@ -703,7 +706,10 @@ def batch_and_chunk_checks():
             check(lib.sydelta_index_create_batch(0, vp(w), vp(st), vp(nblk.astype(np.uint64)), vp(last), nf, bs, 1,
                                                  None, ctypes.byref(ix)))
             bt = ctypes.c_void_p()
+            lib.emu_expand_files.restype = ctypes.c_uint64
+            ex0 = lib.emu_expand_files()
             check(lib.sydelta_match_batch_device(ix, vp(sbuf), vp(soff), vp(slen), nf, None, ctypes.byref(bt)))
+            assert (lib.emu_expand_files() > ex0) == probe.endswith("dx"), (bs, probe)  # the expansion's path
             for k in range(nf):
                 ew, es, ez = C.compute_checksums(bases[k], bs)
                 assert np.array_equal(w[fb[k]:fb[k + 1]], ew) and np.array_equal(st[fb[k]:fb[k + 1]], es), (bs, k)
@@ -716,6 +722,7 @@ def batch_and_chunk_checks():
     os.environ.pop("SYDELTA_PROBE", None)
     os.environ.pop("SYDELTA_FILE_WALK", None)
     os.environ.pop("SYDELTA_FILE_SEGS", None)
+    os.environ.pop("SYDELTA_DEVICE_EXPAND", None)
     # chunked: one file in 1/2/3/8 chunks, walks chained in order, parts appended
     for bs in (512, 4096):
         basis = O.synth_bytes(300 * bs + 77, 0x700)

@@ -336,10 +336,11 @@ hipError_t launch_signature_batch_fast(const uint8_t* d_buf, const uint64_t* d_a
 }
 
 // the emulated scans test windows against the exact keys, so the level-1 filters are not built
-hipError_t launch_ribbon_build(const DeviceIndex&, hipStream_t, Profiler*) { return hipSuccess; }
+hipError_t launch_ribbon_build(const DeviceIndex&, hipStream_t, Profiler*, const uint32_t*, uint64_t) { return hipSuccess; }
 
+hipError_t launch_index_extras(const uint32_t*, const DeviceIndex&, hipStream_t, Profiler*) { return hipSuccess; }
 hipError_t launch_index_build(const uint32_t* d_weak, const uint64_t* d_strong, DeviceIndex& ix, hipStream_t,
-                              Profiler*) {
+                              Profiler*, bool) {
     EmuTimer emu_t;
     FakeIndex F;
     F.files.resize(ix.nfiles);
@@ -701,16 +702,87 @@ hipError_t launch_walk_files(const WalkArgs& a, hipStream_t, Profiler*, bool sli
         close_run();
         const uint64_t cap = 2 * ((U.end - U.entry) / n) + 4;
         if (rec.size() > cap) return hipErrorInvalidValue;  // the kernel's staging region would overflow
+        std::copy(rec.begin(), rec.end(), a.stage + U.rec_off);  // (the kernel stages every unit's records)
         if (!a.out) {  // records left in the staging region
-            std::copy(rec.begin(), rec.end(), a.stage + U.rec_off);
             a.fout[u] = WalkFileOut{(uint32_t)U.rec_off, (uint32_t)rec.size(), weak_hits, hits, exit, 0};
+            if (a.fout_dev) a.fout_dev[u] = a.fout[u];
             continue;
         }
         std::copy(rec.begin(), rec.end(), a.out + placed);
         a.fout[u] = WalkFileOut{(uint32_t)placed, (uint32_t)rec.size(), weak_hits, hits, exit, 0};
+        if (a.fout_dev) a.fout_dev[u] = a.fout[u];
         placed += rec.size();
     }
     if (a.out) *a.total = placed;
+    return hipSuccess;
+}
+
+// k_walk_expand: each file's units' staged records chained (a unit entered past its start cut
+// at the previous exit when its leading literal run reaches it, else the file is bad), Data
+// ops joined across units, expanded into ops at ops + op_off[f]
+std::atomic<uint64_t> g_expand_files{0};  // files through launch_walk_expand (emu_expand_files)
+hipError_t launch_walk_expand(const ExpandArgs& a, hipStream_t, Profiler*) {
+    EmuTimer emu_t;
+    g_expand_files += a.nf;
+    for (uint32_t f = 0; f < a.nf; ++f) {
+        std::vector<WalkRec> m;
+        bool bad = false;
+        uint32_t wh = 0, vh = 0;
+        for (uint32_t u = a.fu[f]; u < a.fu[f + 1] && !bad; ++u) {
+            const WalkFileOut& o = a.fout[u];
+            wh += o.weak_hits;
+            vh += o.hits;
+            const WalkRec* r0 = a.stage + a.units[u].rec_off;
+            const WalkRec* r1 = r0 + o.count;
+            std::vector<WalkRec> rs(r0, r1);
+            size_t k0 = 0;
+            if (u > a.fu[f]) {
+                const uint64_t pe = a.fout[u - 1].exit, entry = a.units[u].entry;
+                if (entry != pe) {
+                    if (pe > entry && !rs.empty() && rs[0].kind == 0 && rs[0].off == entry && rs[0].off + rs[0].a >= pe) {
+                        const uint64_t h = rs[0].off + rs[0].a;
+                        if (h == pe) {
+                            k0 = 1;
+                        } else {
+                            rs[0].a = (uint32_t)(h - pe);
+                            rs[0].off = pe;
+                        }
+                    } else {
+                        bad = true;
+                    }
+                }
+            }
+            for (size_t k = k0; k < rs.size() && !bad; ++k) {
+                if (!rs[k].kind && !m.empty() && !m.back().kind && m.back().off + m.back().a == rs[k].off)
+                    m.back().a += rs[k].a;
+                else
+                    m.push_back(rs[k]);
+            }
+        }
+        uint64_t nops = 0, nd = 0, lit = 0;
+        for (const WalkRec& x : m) {
+            nops += x.kind ? x.kind : 1;
+            if (!x.kind) {
+                ++nd;
+                lit += x.a;
+            }
+        }
+        if (bad || m.size() > kExpandRecs || nops > a.op_off[f + 1] - a.op_off[f]) {
+            a.res[f] = ExpandOut{0, 0, 0, 0, 0, 1, 0};
+            continue;
+        }
+        const uint64_t gb0 = a.fblk[f], nbf = a.fblk[f + 1] - gb0, ls = a.last_size[f];
+        sydelta_op* w = a.ops + a.op_off[f];
+        for (const WalkRec& x : m) {
+            if (!x.kind) {
+                *w++ = sydelta_op{SYDELTA_OP_DATA, 0, x.off, x.a};
+                continue;
+            }
+            for (uint64_t g = x.a - gb0, e = g + x.kind; g < e; ++g)
+                *w++ = sydelta_op{SYDELTA_OP_COPY, 0, g * a.n, g + 1 == nbf ? ls : (uint64_t)a.n};
+        }
+        a.res[f] = ExpandOut{nops, nd, lit, wh, vh, 0, 0};
+    }
     return hipSuccess;
 }
 
@@ -839,3 +911,6 @@ hipError_t launch_synth_mutate(uint8_t*, const uint8_t*, uint64_t, uint64_t, uin
     return hipErrorNotSupported;
 }
 }  // namespace sydelta
+
+// the files the emulated k_walk_expand saw (emulated_checks asserts the device-expand path ran)
+extern "C" uint64_t emu_expand_files() { return sydelta::g_expand_files.load(); }

@@ -34,9 +34,11 @@ def _pack(parts):
     return buf, np.array(offs, np.uint64), np.array([len(p) for p in parts], np.uint64)
 
 
-def _batch(gpu, pairs, bs, walk, monkeypatch):
-    """Batched signature + index + match of (src, basis) pairs; walk: SYDELTA_FILE_WALK."""
+def _batch(gpu, pairs, bs, walk, monkeypatch, dx=""):
+    """Batched signature + index + match of (src, basis) pairs; walk: SYDELTA_FILE_WALK; dx:
+    SYDELTA_DEVICE_EXPAND (the op lists expanded by k_walk_expand or on the host)."""
     monkeypatch.setenv("SYDELTA_FILE_WALK", walk)
+    monkeypatch.setenv("SYDELTA_DEVICE_EXPAND", dx)
     bbuf, boff, blen = _pack([b for _, b in pairs])
     sbuf, soff, slen = _pack([s for s, _ in pairs])
     w, s = gpu.signature_batch(bbuf, boff, blen, bs)
@@ -114,12 +116,14 @@ def _cases(rng, bs, nfiles):
     return pairs
 
 
+@pytest.mark.parametrize("dx", ["0", "1"])
 @pytest.mark.parametrize("bs", [256, 320, 1024, 4096, 8192])
-def test_file_walk_matches_oracle(gpu, oracle_c, monkeypatch, bs):
+def test_file_walk_matches_oracle(gpu, oracle_c, monkeypatch, bs, dx):
     rng = random.Random(1000 + bs)
     pairs = _cases(rng, bs, 80)
-    out, tot, prof = _batch(gpu, pairs, bs, "1", monkeypatch)
+    out, tot, prof = _batch(gpu, pairs, bs, "1", monkeypatch, dx)
     assert "k_walk_files" in prof, prof
+    assert ("k_walk_expand" in prof) == (dx == "1") or bs % 64, prof
     for i, ((src, basis), d) in enumerate(zip(pairs, out)):
         assert d.tuples() == _oracle_ops(oracle_c, src, basis, bs), (bs, i)
         assert d.source_size == len(src) and d.block_size == bs
@@ -240,16 +244,17 @@ def test_chunk_walk_segments(gpu, oracle_c, monkeypatch, bs, nchunks):
     assert _chunk_walk(gpu, src, basis, bs, bounds).tuples() == exp
 
 
+@pytest.mark.parametrize("dx", ["0", "1"])
 @pytest.mark.parametrize("bs", [256, 4096])
 @pytest.mark.parametrize("segs", ["2", "5", "16"])
-def test_file_walk_in_segments(gpu, oracle_c, monkeypatch, bs, segs):
+def test_file_walk_in_segments(gpu, oracle_c, monkeypatch, bs, segs, dx):
     """Files cut into segments of >= 8 blocks (SYDELTA_FILE_SEGS): each segment walked from its
     start; a Copy that crosses into the next segment is absorbed by cutting that segment's
     leading literal run, or the segment is walked again from the exit.  Equal to the oracle."""
     rng = random.Random(2000 + bs + int(segs))
     pairs = _cases(rng, bs, 80)
     monkeypatch.setenv("SYDELTA_FILE_SEGS", segs)
-    out, tot, prof = _batch(gpu, pairs, bs, "1", monkeypatch)
+    out, tot, prof = _batch(gpu, pairs, bs, "1", monkeypatch, dx)
     assert "k_walk_files" in prof
     for i, ((src, basis), d) in enumerate(zip(pairs, out)):
         assert d.tuples() == _oracle_ops(oracle_c, src, basis, bs), (bs, segs, i)
@@ -270,10 +275,11 @@ def test_file_walk_c4_shape_few_files(gpu, oracle_c, monkeypatch):
             s[rng.randrange(len(s))] ^= rng.randrange(1, 256)
         pairs.append((bytes(s), basis))
     monkeypatch.delenv("SYDELTA_FILE_SEGS", raising=False)
-    out, _, prof = _batch(gpu, pairs, 4096, "", monkeypatch)
-    assert "k_walk_files" in prof
-    for f, ((src, basis), d) in enumerate(zip(pairs, out)):
-        assert d.tuples() == _oracle_ops(oracle_c, src, basis, 4096), f
+    for dx in ("0", "1"):
+        out, _, prof = _batch(gpu, pairs, 4096, "", monkeypatch, dx)
+        assert "k_walk_files" in prof
+        for f, ((src, basis), d) in enumerate(zip(pairs, out)):
+            assert d.tuples() == _oracle_ops(oracle_c, src, basis, 4096), (dx, f)
 
 
 # (SYDELTA_PREROLL, SYDELTA_SLIM_WALK, SYDELTA_CHUNK_SEG, SYDELTA_CHUNK_SEG_LAST): every
