@@ -94,6 +94,10 @@ def parse():
                     help="c4: split this rank's files over K host threads, each one batched call on its own "
                          "library stream (sy runs up to 10 transfers at once, cli.rs:178-180), so one call's "
                          "host work overlaps another's kernels")
+    ap.add_argument("--c4-calls", default="pairs", choices=["pairs", "three"],
+                    help="c4 (and the c4 leg): one sydelta_delta_pairs_device call per batch (signature + match, "
+                         "the signature of the second half beside the walks of the first, no index), or the three "
+                         "calls signature_batch + index_create_batch + match_batch")
     ap.add_argument("--device-walk", action="store_true",
                     help="resolve the greedy walks on the device (K5b, SYDELTA_DEVICE_WALK=1; c4/c5/path)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -720,11 +724,17 @@ def time_steps(step, steps: int, warmup: int, world: int):
     return el, last
 
 
-def c4_step(dev, basis, new, files, bs: int, device: int, strm):
-    """One batched call over files = (boff, blen, soff, slen): batched signature, per-file
-    index, batched match (K10 walks every file on the device); strm None = the calling
-    thread's library stream (the call then synchronizes before returning)."""
+def c4_step(dev, basis, new, files, bs: int, device: int, strm, calls: str = "pairs"):
+    """One batch of files = (boff, blen, soff, slen): the signature of every basis and the match
+    of every source (K10 walks every file on the device) -- one sydelta_delta_pairs_device call
+    (calls "pairs"), or batched signature, per-file index and batched match (three calls); strm
+    None = the calling thread's library stream (the call then synchronizes before returning)."""
     boff, blen, soff, slen = files
+    if calls == "pairs":
+        res = dev.delta_pairs_handle(basis, boff, blen, new, soff, slen, bs, stream=strm)
+        tot = res.stats
+        res.close()
+        return tot
     w, s = dev.signature_batch(basis, boff, blen, bs, stream=strm)
     nblk = (blen + bs - 1) // bs
     last = blen - (nblk - 1) * bs
@@ -782,6 +792,29 @@ def c5_proxy_signature(dev, c5: dict, n: int, bs: int, world: int, rank: int):
     return W, S
 
 
+def c4_leg(args, world: int, el: float, files_this_rank: int, bytes_this_rank: int, last: dict) -> dict:
+    """The line's "c4" object: the job's aggregate over all ranks' files (el = max over ranks)."""
+    total = C4_FILES * ((1 << 20) + (1 << 20) + 1)  # basis + source bytes of all ranks' files per step
+    return {"workload": "C4: 10000 x 1 MiB files (1-byte insertion + 16 substitutions each), bs 4096, file-sharded "
+                        "(no collective); " + ("one signature+match call per batch" if args.c4_calls == "pairs"
+                                               else "three calls"),
+            "value": round(total * args.steps / el / GIB, 3), "unit": "GiB/s", "scaling": "strong",
+            "ms_per_step": round(el / args.steps * 1e3, 4), "files": C4_FILES, "files_this_rank": files_this_rank,
+            "bytes_this_rank_per_step": bytes_this_rank,
+            "copy_ops_this_rank": int(last["copy_ops"]), "literal_bytes_this_rank": int(last["literal_bytes"])}
+
+
+def c5_leg(args, world: int, el: float, ag_ms: float, st: dict) -> dict:
+    """The line's "c5" object: one 8 GiB chunk per rank (el = max over ranks)."""
+    n5, bs5 = 8 << 30, 8192
+    return {"workload": f"C5: one {world * n5 / GIB:.0f} GiB file, bs {bs5}, 1% of blocks with one substituted byte; "
+                        f"signature + RCCL all-gather + index + chunk walk, chunk-sharded",
+            "value": round(world * 2 * n5 * args.steps / el / GIB, 3), "unit": "GiB/s", "scaling": "weak",
+            "ms_per_step": round(el / args.steps * 1e3, 4), "bytes_per_rank_per_step": 2 * n5,
+            "allgather_ms": round(ag_ms, 4), "allgather_bytes_per_rank": 12 * (n5 // bs5) * world if world > 1 else 0,
+            "copy_ops_this_rank": int(st["copy_ops"]), "literal_bytes_this_rank": int(st["literal_bytes"])}
+
+
 def run_legs(args, dev, world: int, rank: int, device: int, stream) -> dict:
     """The north star's multi-GPU configs beside the C3 headline, so the driver's
     `--gpus N` run measures them (BASELINE.json configs 4 and 5):
@@ -800,15 +833,9 @@ def run_legs(args, dev, world: int, rank: int, device: int, stream) -> dict:
     lo, hi = shard_range(C4_FILES, world, rank)
     basis, new, files = c4_files(dev, basis_bytes=1 << 20, nfiles=hi - lo, first=lo)
     torch.cuda.synchronize()
-    el, last = time_steps(lambda: c4_step(dev, basis, new, files, 4096, device, stream), args.steps, args.warmup,
-                          world)
-    total = C4_FILES * ((1 << 20) + (1 << 20) + 1)  # basis + source bytes of all ranks' files per step
-    out["c4"] = {"workload": "C4: 10000 x 1 MiB files (1-byte insertion + 16 substitutions each), bs 4096, "
-                             "file-sharded (no collective)",
-                 "value": round(total * args.steps / el / GIB, 3), "unit": "GiB/s", "scaling": "strong",
-                 "ms_per_step": round(el / args.steps * 1e3, 4), "files": C4_FILES, "files_this_rank": hi - lo,
-                 "bytes_this_rank_per_step": int(files[1].sum() + files[3].sum()),
-                 "copy_ops_this_rank": int(last["copy_ops"]), "literal_bytes_this_rank": int(last["literal_bytes"])}
+    el, last = time_steps(lambda: c4_step(dev, basis, new, files, 4096, device, stream, args.c4_calls), args.steps,
+                          args.warmup, world)
+    out["c4"] = c4_leg(args, world, el, hi - lo, int(files[1].sum() + files[3].sum()), last)
     del basis, new, files, last
     torch.cuda.empty_cache()
     # ---- C5
@@ -846,13 +873,7 @@ def run_legs(args, dev, world: int, rank: int, device: int, stream) -> dict:
 
         ag_el, _ = time_steps(ag, args.steps, 1, world)
         ag_ms = ag_el / args.steps * 1e3
-    out["c5"] = {"workload": f"C5: one {world * n5 / GIB:.0f} GiB file, bs {bs5}, 1% of blocks with one substituted "
-                             f"byte; signature + RCCL all-gather + index + chunk walk, chunk-sharded",
-                 "value": round(world * 2 * n5 * args.steps / el / GIB, 3), "unit": "GiB/s", "scaling": "weak",
-                 "ms_per_step": round(el / args.steps * 1e3, 4), "bytes_per_rank_per_step": 2 * n5,
-                 "allgather_ms": round(ag_ms, 4),
-                 "allgather_bytes_per_rank": 12 * nb * world if world > 1 else 0,
-                 "copy_ops_this_rank": int(st["copy_ops"]), "literal_bytes_this_rank": int(st["literal_bytes"])}
+    out["c5"] = c5_leg(args, world, el, ag_ms, st)
     del c5, W, S
     torch.cuda.empty_cache()
     return out
@@ -867,6 +888,13 @@ def main():
         # launcher test hook (tests/test_bench_launch.py): report the rank environment, no GPU
         print(json.dumps({k: os.environ.get(k) for k in ("RANK", "LOCAL_RANK", "WORLD_SIZE", "MASTER_ADDR",
                                                        "MASTER_PORT", "SYDELTA_HOST_THREADS")}), flush=True)
+        if os.environ.get("SYDELTA_BENCH_STUB_LEGS") and int(os.environ.get("RANK", "0")) == 0:
+            # the legs' objects as rank 0 builds them (fixed timings: 2 ms C4, 5 ms C5 per step)
+            st = {"copy_ops": 1, "literal_bytes": 2}
+            lo, hi = shard_range(C4_FILES, world, 0)
+            print(json.dumps({"metric": METRIC, "n_gpus": world,
+                              "c4": c4_leg(args, world, 2e-3 * args.steps, hi - lo, 0, st),
+                              "c5": c5_leg(args, world, 5e-3 * args.steps, 0.1, st)}), flush=True)
         fail = os.environ.get("SYDELTA_BENCH_STUB_FAIL_RANK")
         if fail is not None:
             if int(fail) == int(os.environ.get("RANK", "0")):
@@ -1034,7 +1062,7 @@ def main():
     torch.cuda.set_stream(stream)
 
     def c4_batch(fs, strm):
-        return c4_step(dev, basis, new, fs, bs, local, strm)
+        return c4_step(dev, basis, new, fs, bs, local, strm, args.c4_calls)
 
     c4_pool, c4_groups = None, []
     if args.workload == "c4" and args.callers > 1:
@@ -1294,7 +1322,9 @@ def main():
                            "of 4 KiB blocks, a 1-byte insertion in 1%), bs 4096",
                     "c2": "C2: signature only over 4 GiB, bs 4096",
                     "c4": f"C4: {args.files} x 1 MiB files (1-byte insertion + 16 substitutions each), "
-                          f"batched signature + per-file index + batched match, file-sharded over ranks",
+                          + ("signature + match of every pair in one call (sydelta_delta_pairs_device)"
+                             if args.c4_calls == "pairs" else "batched signature + per-file index + batched match")
+                          + ", file-sharded over ranks",
                     "c5": (f"C5 rank proxy: rank {args.proxy_rank} of a {args.proxy_world}-rank job on one GPU -- its "
                            f"{n / GIB:.0f} GiB chunk of one {args.proxy_world * n / GIB:.0f} GiB file, bs {bs}, "
                            f"{args.edit_ppm / 1e4:g}% of blocks with one substituted byte: signature of its chunk + "

@@ -146,8 +146,7 @@ int sydelta_signature_device(int device, const uint8_t *d_buf, uint64_t len, uin
  * stream) and the call returns without waiting; the table is built on a library
  * stream (one file; a batch: on `stream`) and every call that uses the index orders
  * its own stream after the build, so work the caller queues meanwhile (the source's
- * upload, its aligned probe) overlaps it.  SYDELTA_INDEX_SYNC=1 builds on `stream` and
- * waits, as for host arrays. */
+ * upload, its aligned probe) overlaps it. */
 int sydelta_index_create(int device, const uint32_t *weak, const uint64_t *strong, uint64_t nblocks,
                          uint64_t block_size, uint64_t last_size, int arrays_on_device, void *stream,
                          sydelta_index **out);
@@ -252,6 +251,17 @@ int sydelta_index_create_batch(int device, const uint32_t *weak, const uint64_t 
  * delta sy's generate_delta would return for that pair. */
 int sydelta_match_batch_device(sydelta_index *idx, const uint8_t *d_buf, const uint64_t *src_off,
                                const uint64_t *src_len, uint64_t nfiles, void *stream, sydelta_delta_batch **out);
+/* Signature + match of many independent (basis, source) pairs in one call: for each pair,
+ * compute_checksums of the basis (checksum.rs:31-80) then generate_delta of the source against
+ * it (generator.rs:242-379), as the three calls above would do.  The files are taken in two
+ * groups whose signatures and walks overlap, and no index is built (each walk builds its
+ * file's candidate map in on-chip memory).  Needs block_size % 64 == 0 in [256, 8192], bases
+ * of at most 1024 blocks and 16-byte aligned files (else SYDELTA_E_INVAL: use the three
+ * calls). */
+int sydelta_delta_pairs_device(int device, const uint8_t *d_basis, const uint64_t *basis_off,
+                               const uint64_t *basis_len, const uint8_t *d_src, const uint64_t *src_off,
+                               const uint64_t *src_len, uint64_t nfiles, uint64_t block_size, void *stream,
+                               sydelta_delta_batch **out);
 uint64_t sydelta_delta_batch_count(const sydelta_delta_batch *b);
 /* Borrowed pointer, valid until sydelta_delta_batch_free. */
 const sydelta_delta *sydelta_delta_batch_get(const sydelta_delta_batch *b, uint64_t i);
@@ -441,6 +451,10 @@ size_t sydelta_profile_json(char *buf, size_t cap, int reset);
  * the host walk (the path reached a position only an on-demand scan classifies), since
  * the library was loaded. */
 int sydelta_walk_counters(uint64_t *device_walks, uint64_t *device_fallbacks);
+/* Files of batched matches whose op lists the device expanded (K10, each file's last walk
+ * unit; the host had few threads for them or SYDELTA_DEVICE_EXPAND=1), and batches whose
+ * expansion went back to the host (a file needed a re-walk), since the library was loaded. */
+int sydelta_expand_counters(uint64_t *device_files, uint64_t *host_batches);
 /* Deterministic synthetic bytes on the device: counter-based splitmix64 of
  * (seed, 8-byte word index), little endian (oracle.synth_bytes). */
 int sydelta_synth_fill(uint8_t *d_buf, uint64_t len, uint64_t seed, void *stream);

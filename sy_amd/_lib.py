@@ -94,6 +94,7 @@ SIGNATURES = [
     ("sydelta_signature_batch_device", _i, [_i, _vp, _vp, _vp, _u64, _u64, _vp, _vp, _vp]),
     ("sydelta_index_create_batch", _i, [_i, _vp, _vp, _vp, _vp, _u64, _u64, _i, _vp, _pp]),
     ("sydelta_match_batch_device", _i, [_vp, _vp, _vp, _vp, _u64, _vp, _pp]),
+    ("sydelta_delta_pairs_device", _i, [_i, _vp, _vp, _vp, _vp, _vp, _vp, _u64, _u64, _vp, _pp]),
     ("sydelta_delta_batch_count", _u64, [_vp]),
     ("sydelta_delta_batch_get", _vp, [_vp, _u64]),
     ("sydelta_delta_batch_stats", _i, [_vp, ctypes.POINTER(MatchStatsC)]),
@@ -128,6 +129,7 @@ SIGNATURES = [
     ("sydelta_set_profiling", None, [_i]),
     ("sydelta_profile_json", ctypes.c_size_t, [ctypes.c_char_p, ctypes.c_size_t, _i]),
     ("sydelta_walk_counters", _i, [ctypes.POINTER(_u64), ctypes.POINTER(_u64)]),
+    ("sydelta_expand_counters", _i, [ctypes.POINTER(_u64), ctypes.POINTER(_u64)]),
     ("sydelta_synth_fill", _i, [_vp, _u64, _u64, _vp]),
     ("sydelta_synth_mutate", _i, [_vp, _vp, _u64, _u64, _u32, _vp]),
     ("sydelta_synth_fill_range", _i, [_vp, _u64, _u64, _u64, _vp]),

@@ -126,6 +126,13 @@ int ensure_device_impl(int device) {
         if (const char* e = getenv("SYDELTA_POOL_KEEP_MIB")) keep = strtoull(e, nullptr, 10);
         keep <<= 20;
         (void)hipMemPoolSetAttribute(pool, hipMemPoolAttrReleaseThreshold, &keep);
+        // No opportunistic reuse across streams: a block freed on one stream (a kernel's
+        // argument table, freed right after its launch) was handed to an allocation on another
+        // stream while the kernel still read it (the pairs call's two signature groups, measured:
+        // files of the first group signed from the second group's table).  Reuse across streams
+        // then follows event dependencies only.
+        int no_opportunistic = 0;
+        (void)hipMemPoolSetAttribute(pool, hipMemPoolReuseAllowOpportunistic, &no_opportunistic);
         g_pools[device] = pool;
         g_wave_slots[device] = (uint32_t)std::max(64, prop.multiProcessorCount * 16);
         st->status = SYDELTA_OK;
@@ -1238,6 +1245,7 @@ void install_op_arena() {
 }
 
 std::atomic<uint64_t> g_device_walks{0}, g_device_walk_fallbacks{0};  // sydelta_walk_counters
+std::atomic<uint64_t> g_expand_files{0}, g_expand_host{0};               // sydelta_expand_counters
 
 std::mutex g_ops_mu;
 std::vector<OpVec>& g_ops_pool = *new std::vector<OpVec>();  // never destroyed (arrays may be pinned)
@@ -1308,7 +1316,7 @@ void take_small_ops(std::vector<sydelta_delta>& d) {
 }
 
 // Op slabs (OpSlabHooks, sydelta_walk.hpp): when the device expands a batch's op lists
-// (k_walk_expand), every file's op array is reserved from one pinned, host-mapped slab that
+// (WalkArgs::x), every file's op array is reserved from one pinned, host-mapped slab that
 // the kernel writes into.  A slab counts its live arrays (+1 while the batch reserves from it)
 // and is reused once they are all gone; slabs are kept for the process (at most kMaxSlabs:
 // ten concurrent callers take one each), so a released array never races with a free.
@@ -1397,6 +1405,12 @@ struct sydelta_delta_batch {
     std::vector<sydelta_delta> d;
     sydelta_match_stats total{};
 };
+
+extern "C" int sydelta_expand_counters(uint64_t* device_files, uint64_t* host_batches) {
+    if (device_files) *device_files = g_expand_files.load();
+    if (host_batches) *host_batches = g_expand_host.load();
+    return SYDELTA_OK;
+}
 
 extern "C" int sydelta_walk_counters(uint64_t* device_walks, uint64_t* device_fallbacks) {
     if (device_walks) *device_walks = g_device_walks.load();
@@ -2533,16 +2547,24 @@ struct WalkResult {
     const ExpandOut* xres = nullptr;  // with an ExpandReq: per file (the thread's mapped buffer)
     double ms_kernel = 0, ms_d2h = 0;
 };
-// The op lists expanded on the device after the walk (k_walk_expand): file f's units
+// The op lists expanded on the device by the walk (WalkArgs::x): file f's units
 // [fu[f], fu[f + 1]), its ops at ops + op_off[f] (host-mapped, capacity to op_off[f + 1]).
 struct ExpandReq {
     const uint32_t* fu;
     const uint64_t* op_off;
     sydelta_op* ops;
 };
+// Groups of a batch walked by separate launches (sydelta_delta_pairs_device): group g's units
+// [ub[g], ub[g + 1]) start once ev[g] (its files' signature) has passed, odd groups on s2, so a
+// group's walk runs beside the next group's signature.
+struct WalkGroups {
+    std::vector<uint64_t> ub;
+    std::vector<hipEvent_t> ev;
+    hipStream_t s2 = nullptr;
+};
 static int run_walk(sydelta_index* ix, const uint8_t* base, const std::vector<WalkUnit>& units, const uint32_t* ahit,
                     const uint32_t* apw, bool lds_filter, hipStream_t s, Profiler* prof, WalkResult& res,
-                    const ExpandReq* ex = nullptr) {
+                    const ExpandReq* ex = nullptr, const WalkGroups* groups = nullptr) {
     ScratchHold hold;
     const auto t0 = std::chrono::steady_clock::now();
     const uint64_t nu = units.size(), nf = ix->nfiles;
@@ -2561,7 +2583,8 @@ static int run_walk(sydelta_index* ix, const uint8_t* base, const std::vector<Wa
     // SYDELTA_PHASE_TIMING tick counters) -- ten concurrent callers' extra copies showed
     auto al = [](size_t v) { return (v + 255) & ~(size_t)255; };
     const size_t o_units = 0, o_last = ubytes, o_total = o_last + lbytes, o_fu = al(o_total + 136);
-    const size_t o_opoff = o_fu + al(4 * (nf + 1)), up = ex ? o_opoff + 8 * (nf + 1) : o_total + 136;
+    const size_t o_opoff = o_fu + al(4 * (nf + 1)), o_xdone = o_opoff + al(8 * (nf + 1));
+    const size_t up = ex ? o_xdone + 4 * nf : o_total + 136;
     PinnedHits& ph = thread_pinned_hits();
     if (int r = pinned_at_least(ph, std::max(up, fout_bytes + 16))) return r;
     memcpy(ph.p, units.data(), ubytes);
@@ -2570,6 +2593,7 @@ static int run_walk(sydelta_index* ix, const uint8_t* base, const std::vector<Wa
     if (ex) {
         memcpy(ph.p + o_fu, ex->fu, 4 * (nf + 1));
         memcpy(ph.p + o_opoff, ex->op_off, 8 * (nf + 1));
+        memset(ph.p + o_xdone, 0, 4 * nf);  // the per-file unit counters
     }
     // device: the upload, the staged records (+ the per-unit results' device copy for the
     // expansion); host (coherent, mapped; the thread's, kept): the per-unit results and the
@@ -2626,9 +2650,8 @@ static int run_walk(sydelta_index* ix, const uint8_t* base, const std::vector<Wa
     a.total = (unsigned long long*)(D + o_total);
     a.ticks = timing ? a.total + 1 : nullptr;
     a.fout_dev = ex ? (WalkFileOut*)(D + o_fdev) : nullptr;
-    HIP_TRY(launch_walk_files(a, s, prof));
-    if (ex) {
-        ExpandArgs xa{};
+    if (ex) {  // the op lists expanded by each file's last unit (k_walk_files, expand_file)
+        ExpandArgs& xa = a.x;
         xa.units = a.units;
         xa.fout = a.fout_dev;
         xa.stage = a.stage;
@@ -2640,8 +2663,31 @@ static int run_walk(sydelta_index* ix, const uint8_t* base, const std::vector<Wa
         xa.res = (ExpandOut*)(wm.p + m_res);
         xa.nf = (uint32_t)nf;
         xa.n = (uint32_t)ix->bs;
-        HIP_TRY(launch_walk_expand(xa, s, prof));
+        a.xdone = (uint32_t*)(D + o_xdone);
         res.xres = xa.res;
+    }
+    if (groups && groups->ub.size() > 2) {
+        hipEvent_t up = take_event(cur_dev), back = take_event(cur_dev);
+        if (!up || !back) return fail(SYDELTA_E_OOM, "no event for the grouped walk");
+        HIP_TRY(hipEventRecord(up, s));  // the upload, before the other stream's launches
+        for (size_t g = 0; g + 1 < groups->ub.size(); ++g) {
+            const hipStream_t sg = (g & 1) ? groups->s2 : s;
+            if (sg != s) HIP_TRY(hipStreamWaitEvent(sg, up, 0));
+            HIP_TRY(hipStreamWaitEvent(sg, groups->ev[g], 0));
+            WalkArgs ag = a;  // (a.x stays global: the expansion indexes units and files globally)
+            ag.units = a.units + groups->ub[g];
+            ag.nunits = (uint32_t)(groups->ub[g + 1] - groups->ub[g]);
+            ag.fout = a.fout + groups->ub[g];
+            ag.fout_dev = a.fout_dev ? a.fout_dev + groups->ub[g] : nullptr;
+            HIP_TRY(launch_walk_files(ag, sg, prof));
+        }
+        HIP_TRY(hipEventRecord(back, groups->s2));
+        HIP_TRY(hipStreamWaitEvent(s, back, 0));
+        HIP_TRY(hipStreamSynchronize(s));
+        give_event(cur_dev, up);
+        give_event(cur_dev, back);
+    } else {
+        HIP_TRY(launch_walk_files(a, s, prof));
     }
     if (timing) {
         unsigned long long tk[16];
@@ -2724,8 +2770,11 @@ static uint64_t file_segs(uint64_t nf, int device) {
 // leading literal run reaches that exit -- the greedy walk from the exit then classifies the
 // same positions the same way -- and its leading Data op is cut to start there; otherwise
 // the segment is walked again from the exit (rounds, as for a chunk's segments).
+// split/ev/s2: the pairs entry point's groups (files [split[g], split[g + 1]) after event ev[g])
 static int match_walk_files(sydelta_index* ix, const uint8_t* d_buf, const uint64_t* src_off, const uint64_t* src_len,
-                            hipStream_t s, Profiler* prof, sydelta_delta_batch* b) {
+                            hipStream_t s, Profiler* prof, sydelta_delta_batch* b,
+                            const std::vector<uint64_t>* split = nullptr, const std::vector<hipEvent_t>* gev = nullptr,
+                            hipStream_t s2 = nullptr) {
     static const bool host_timing = getenv("SYDELTA_HOST_TIMING") != nullptr;
     const uint64_t n = ix->bs, nf = ix->nfiles;
     struct Walking {  // this batch's files counted while it walks
@@ -2765,7 +2814,7 @@ static int match_walk_files(sydelta_index* ix, const uint8_t* d_buf, const uint6
     fu[nf] = units.size();
     const uint64_t nu = units.size();
     // the op lists: expanded on the device into op arrays reserved from a pinned host-mapped
-    // slab (k_walk_expand) when the host has few threads for them (SYDELTA_DEVICE_EXPAND=0|1
+    // slab (each file's last unit of the walk kernel) when the host has few threads for them (SYDELTA_DEVICE_EXPAND=0|1
     // forces it off / on; per call), else on the host below
     static const int asm_threads = getenv("SYDELTA_ASM_THREADS") ? std::max(1, atoi(getenv("SYDELTA_ASM_THREADS")))
                                                                    : walk::HostPool::get().size() + 1;
@@ -2798,12 +2847,21 @@ static int match_walk_files(sydelta_index* ix, const uint8_t* d_buf, const uint6
         }
     }
     if (!expand_dev) take_small_ops(b->d);  // recycled per-file op arrays
+    WalkGroups groups;
+    if (split) {
+        for (uint64_t f : *split) groups.ub.push_back(fu[f]);
+        groups.ev = *gev;
+        groups.s2 = s2;
+    }
     WalkResult res;
-    if (int r = run_walk(ix, d_buf, units, nullptr, nullptr, true, s, prof, res, expand_dev ? &req : nullptr)) return r;
+    if (int r = run_walk(ix, d_buf, units, nullptr, nullptr, true, s, prof, res, expand_dev ? &req : nullptr,
+                         split ? &groups : nullptr))
+        return r;
     const auto t1 = std::chrono::steady_clock::now();
     if (res.xres) {  // every file expanded on the device (a file that needs a re-walk: the host path below)
         bool all = true;
         for (uint64_t f = 0; f < nf && all; ++f) all = !res.xres[f].bad;
+        (all ? g_expand_files : g_expand_host) += all ? nf : 1;
         if (all) {
             for (uint64_t f = 0; f < nf; ++f) {
                 const ExpandOut& x = res.xres[f];
@@ -3221,6 +3279,116 @@ extern "C" int sydelta_match_batch_device(sydelta_index* idx, const uint8_t* d_b
     hipStream_t s = stream ? (hipStream_t)stream : thread_stream(idx->device);
     std::unique_ptr<sydelta_delta_batch> b(new sydelta_delta_batch());
     if (int r = match_impl(idx, d_buf, src_off, src_len, s, b.get())) return r;
+    *out = b.release();
+    return SYDELTA_OK;
+} catch (...) {
+    return sydelta::host_exception();
+}
+
+// Signature + match of many (basis, source) pairs in one call (the C4 shape): the files in two
+// groups, the first's signature and walks on `stream`, the second's on the thread's aux stream,
+// so the first group's walks run beside the second group's signature; no index is built (the
+// walks self-index each file from the signature, sydelta_filewalk.hip).
+extern "C" int sydelta_delta_pairs_device(int device, const uint8_t* d_basis, const uint64_t* basis_off,
+                                          const uint64_t* basis_len, const uint8_t* d_src, const uint64_t* src_off,
+                                          const uint64_t* src_len, uint64_t nfiles, uint64_t block_size, void* stream,
+                                          sydelta_delta_batch** out) try {
+    if (!out) return fail(SYDELTA_E_INVAL, "out is NULL");
+    *out = nullptr;
+    if (!nfiles || nfiles >= (1ull << 31)) return fail(SYDELTA_E_INVAL, "bad file count %llu", (unsigned long long)nfiles);
+    if (!basis_off || !basis_len || !src_off || !src_len) return fail(SYDELTA_E_INVAL, "NULL segment table");
+    const uint64_t n = block_size;
+    if (n % 64 != 0 || n < 256 || n > kWalkMaxN)
+        return fail(SYDELTA_E_INVAL, "block_size %llu: the pairs call needs a multiple of 64 in [256, %u]",
+                    (unsigned long long)n, kWalkMaxN);
+    std::vector<uint64_t> fblk(nfiles + 1, 0), last(nfiles, 0);
+    uint64_t max_nblk = 0, recs = 0;
+    for (uint64_t f = 0; f < nfiles; ++f) {
+        const uint64_t nb = (basis_len[f] + n - 1) / n;
+        if (nb > kSelfIxMaxBlocks)
+            return fail(SYDELTA_E_INVAL, "basis %llu has %llu blocks (at most %u)", (unsigned long long)f,
+                        (unsigned long long)nb, kSelfIxMaxBlocks);
+        if (basis_len[f] && (!d_basis || ((uintptr_t)(d_basis + basis_off[f]) & 15)))
+            return fail(SYDELTA_E_INVAL, "basis %llu must start 16-byte aligned", (unsigned long long)f);
+        if (src_len[f] && (!d_src || ((uintptr_t)(d_src + src_off[f]) & 15)))
+            return fail(SYDELTA_E_INVAL, "source %llu must start 16-byte aligned", (unsigned long long)f);
+        if (src_len[f] >= (1ull << 32)) return fail(SYDELTA_E_INVAL, "source %llu too large", (unsigned long long)f);
+        fblk[f + 1] = fblk[f] + nb;
+        last[f] = nb ? basis_len[f] - (nb - 1) * n : 0;
+        max_nblk = std::max(max_nblk, nb);
+        recs += 2 * (src_len[f] / n) + 4;
+    }
+    if (recs >= (1ull << 32) || fblk[nfiles] >= 0xFFFFFFFFull) return fail(SYDELTA_E_INVAL, "batch too large");
+    SYDELTA_ENTER_DEVICE(device);
+    if (device < 0) device = 0;
+    hipStream_t s = stream ? (hipStream_t)stream : thread_stream(device);
+    hipStream_t s2 = thread_aux_stream(device);
+    if (!s2) return fail(SYDELTA_E_OOM, "no stream for the pairs call");
+    const uint64_t nb = std::max<uint64_t>(1, fblk[nfiles]);
+    auto al = [](size_t v) { return (v + 255) & ~(size_t)255; };
+    const size_t o_weak = 0, o_strong = al(4 * nb), o_fblk = o_strong + al(8 * nb), need = o_fblk + 8 * (nfiles + 1);
+    uint8_t* D = nullptr;
+    HIP_TRY(dev_malloc_async((void**)&D, need, s));
+    struct Free {  // the arrays, in s's order (the walks on s2 are joined to s before returning)
+        uint8_t* p;
+        hipStream_t s;
+        ~Free() { (void)hipFreeAsync(p, s); }
+    } free_d{D, s};
+    if (int r = upload_staged(D + o_fblk, fblk.data(), 8 * (nfiles + 1), s)) return r;
+    // groups: two halves of a batch of >= 128 files (each half still fills the chip's wave
+    // slots with its segments)
+    const uint64_t G = nfiles >= 128 ? 2 : 1;
+    std::vector<uint64_t> split(G + 1);
+    for (uint64_t g = 0; g <= G; ++g) split[g] = nfiles * g / G;
+    std::vector<hipEvent_t> ev(G, nullptr);
+    struct Events {
+        std::vector<hipEvent_t>& v;
+        int dev;
+        ~Events() {
+            for (hipEvent_t e : v)
+                if (e) give_event(dev, e);
+        }
+    } ev_back{ev, device};
+    hipEvent_t ready = take_event(device);  // the arrays allocated (s2 orders itself after it)
+    if (!ready) return fail(SYDELTA_E_OOM, "no event for the pairs call");
+    ev_back.v.push_back(ready);
+    HIP_TRY(hipEventRecord(ready, s));
+    for (uint64_t g = 0; g < G; ++g) {
+        const uint64_t f0 = split[g], f1 = split[g + 1];
+        const hipStream_t sg = (g & 1) ? s2 : s;  // (run_walk launches group g's walks on the same stream)
+        if (sg != s) HIP_TRY(hipStreamWaitEvent(sg, ready, 0));
+        if (int r = sydelta_signature_batch_device(device, d_basis, basis_off + f0, basis_len + f0, f1 - f0, n,
+                                                   (uint32_t*)(D + o_weak) + fblk[f0],
+                                                   (uint64_t*)(D + o_strong) + fblk[f0], sg))
+            return r;
+        ev[g] = take_event(device);
+        if (!ev[g]) return fail(SYDELTA_E_OOM, "no event for the pairs call");
+        HIP_TRY(hipEventRecord(ev[g], sg));
+    }
+    // the walks' view of the signature: no tables (each walk self-indexes its file)
+    sydelta_index X;
+    X.device = device;
+    X.bs = n;
+    X.nfiles = nfiles;
+    X.fblk = fblk;
+    X.last_size = last;
+    X.d_weak = (uint32_t*)(D + o_weak);
+    X.d_strong = (uint64_t*)(D + o_strong);
+    X.ix.d_fblk = (uint64_t*)(D + o_fblk);
+    X.ix.nfiles = nfiles;
+    X.ix.nblocks = fblk[nfiles];
+    X.max_nblk = max_nblk;
+    X.deferred = true;
+    std::unique_ptr<sydelta_delta_batch> b(new sydelta_delta_batch());
+    b->d.assign(nfiles, sydelta_delta());
+    for (uint64_t f = 0; f < nfiles; ++f) {
+        b->d[f].source_size = src_len[f];
+        b->d[f].block_size = n;
+        b->d[f].stats.positions = src_len[f] >= n ? src_len[f] - n + 1 : 0;
+        b->total.positions += b->d[f].stats.positions;
+    }
+    CallProf cp;
+    if (int r = match_walk_files(&X, d_src, src_off, src_len, s, cp.get(), b.get(), &split, &ev, s2)) return r;
     *out = b.release();
     return SYDELTA_OK;
 } catch (...) {

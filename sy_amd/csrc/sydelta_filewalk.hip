@@ -313,6 +313,7 @@ __device__ __forceinline__ void walk_roll(const WalkArgs& a, const FileIx& F, co
 // miss that was not pre-rolled) is left to the full kernel launched after it, which skips the
 // units the slim one finished (marked in the unit table).  The full kernel's registers (the
 // roll's) spill, and its spills cost a scratch round trip per block walked.
+__device__ void expand_file(const ExpandArgs& a, uint32_t f, unsigned char* lds, uint32_t lds_bytes);
 template <bool kLdsFilt, bool kSlim>
 __global__ __launch_bounds__(64, 4) void k_walk_files(WalkArgs a) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
@@ -574,6 +575,18 @@ __global__ __launch_bounds__(64, 4) void k_walk_files(WalkArgs a) {
         if (a.fout_dev) a.fout_dev[blockIdx.x] = WalkFileOut{(uint32_t)base, nrec, weak_hits, hits, exit, 0};
     }
     if (kSlim && lane == 0) const_cast<WalkUnit*>(a.units)[blockIdx.x].final_ = U.final_ | kUnitDone;
+    if constexpr (kLdsFilt) {
+        if (a.x.ops) {  // the op lists on the device: the file's last unit to finish expands them
+            __threadfence();  // this unit's records and results before its count
+            uint32_t last = 0;
+            if (lane == 0) last = atomicAdd(a.xdone + U.file, 1u) + 1 == a.x.fu[U.file + 1] - a.x.fu[U.file];
+            if (rl(last, 0)) {
+                __threadfence();  // the other units' records and results after their counts
+                __syncthreads();  // (the walk's LDS is free)
+                expand_file(a.x, U.file, smem, L.total);
+            }
+        }
+    }
     wtick(kWtOut);
 }
 
@@ -647,21 +660,25 @@ __global__ __launch_bounds__(64, 4) void k_preroll(WalkArgs a, uint32_t* ahit, u
 }
 
 // ===========================================================================
-// K10's op lists expanded on the device (launch_walk_expand)
+// K10's op lists expanded on the device (WalkArgs::x)
 // ===========================================================================
-// One wave per file.  The file's units' records are gathered into LDS in unit order; lane 0
+// The last unit of a file to finish its walk (a per-file counter) expands the file's op list,
+// so the expansion's writes to host memory overlap the other files' walks.  The file's units'
+// records are gathered into the wave's LDS (free once its walk is done) in unit order; lane 0
 // chains them (the walk from the previous unit's exit: a unit that started there, or earlier
-// with a leading literal run reaching it, which is cut there) and merges a Data op ending at
-// a unit's end with the next unit's first one; then every lane takes ops i = lane, lane + 64,
-// ...: the record holding op i (a binary search of the records' op prefix) gives it -- a Data
-// op, or Copy (g - gb0) n of block g of a copy run, sized n or the basis's last size.  The ops
-// go to host-mapped memory as three 8-byte stores per lane (24-byte stride).
-__global__ __launch_bounds__(64) void k_walk_expand(ExpandArgs a) {
-    __shared__ WalkRec rec[kExpandRecs];
-    __shared__ uint32_t pre[kExpandRecs];  // inclusive op prefix over the merged records
-    __shared__ uint32_t ustart[65];
-    __shared__ uint32_t s_m, s_bad;
-    const uint32_t f = blockIdx.x, lane = threadIdx.x;
+// with a leading literal run reaching it, which is cut there) and merges a Data op ending at a
+// unit's end with the next unit's first one; then every lane takes ops i = lane, lane + 64, ...:
+// the record holding op i (a binary search of the records' op prefix) gives it -- a Data op, or
+// Copy (g - gb0) n of block g of a copy run, sized n or the basis's last size.  The ops go to
+// host-mapped memory as three 8-byte stores per lane (24-byte stride).  cap: records the LDS
+// holds; a file with more (or more than 64 units, or units that do not chain) gets bad = 1.
+__device__ void expand_file(const ExpandArgs& a, uint32_t f, unsigned char* lds, uint32_t lds_bytes) {
+    const uint32_t lane = threadIdx.x & 63;
+    uint32_t* ustart = (uint32_t*)lds;  // 65 entries, then s_m, s_bad
+    uint32_t* sv = ustart + 65;
+    WalkRec* rec = (WalkRec*)(lds + 272);
+    const uint32_t cap = (lds_bytes - 272) / (sizeof(WalkRec) + 4);
+    uint32_t* pre = (uint32_t*)(rec + cap);  // inclusive op prefix over the merged records
     const uint32_t u0 = a.fu[f], u1 = a.fu[f + 1], nu = u1 - u0;
     ExpandOut* res = a.res + f;
     // gather the units' staged records
@@ -669,7 +686,7 @@ __global__ __launch_bounds__(64) void k_walk_expand(ExpandArgs a) {
     bool over = nu > 64;
     for (uint32_t k = 0; k < nu && !over; ++k) {
         const uint32_t c = a.fout[u0 + k].count;
-        if (total + c > kExpandRecs) {
+        if (total + c > cap) {
             over = true;
             break;
         }
@@ -719,12 +736,12 @@ __global__ __launch_bounds__(64) void k_walk_expand(ExpandArgs a) {
                     rec[m++] = x;
             }
         }
-        s_m = m;
-        s_bad = bad;
+        sv[0] = m;
+        sv[1] = bad;
     }
     __syncthreads();
-    const uint32_t m = s_m;
-    if (s_bad) {
+    const uint32_t m = sv[0];
+    if (sv[1]) {
         if (lane == 0) *res = ExpandOut{0, 0, 0, 0, 0, 1, 0};
         return;
     }
@@ -790,12 +807,6 @@ __global__ __launch_bounds__(64) void k_walk_expand(ExpandArgs a) {
 // ===========================================================================
 // Launch wrappers
 // ===========================================================================
-hipError_t launch_walk_expand(const ExpandArgs& a, hipStream_t s, Profiler* prof) {
-    if (!a.nf) return hipSuccess;
-    ProfScope ps(prof, s, "k_walk_expand");
-    hipLaunchKernelGGL(k_walk_expand, dim3(a.nf), dim3(64), 0, s, a);
-    return hipGetLastError();
-}
 
 hipError_t launch_walk_files(const WalkArgs& a, hipStream_t s, Profiler* prof, bool slim) {
     if (!a.nunits) return hipSuccess;

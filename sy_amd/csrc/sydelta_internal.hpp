@@ -251,6 +251,30 @@ struct WalkFileOut {
     uint64_t exit;         // where the walk left the unit (>= end; a final unit: len)
     uint64_t pad;
 };
+// The op lists of a batch's walk expanded on the device (WalkArgs::x, k_walk_files): the
+// last unit of each file to finish joins the file's units' staged records (a Data op ending at a unit's end merged with the next
+// unit's first; a unit entered past its start cut at the previous unit's exit when its
+// leading literal run reaches it -- match_walk_files' rules), then writes every op
+// (sydelta_op, generator.rs:10-15: a Copy per block of a copy run) at ops + op_off[f], in
+// host-mapped memory.  A file whose units do not chain that way (it needs a re-walk), whose
+// records exceed the wave's LDS or whose ops exceed op_off[f + 1] - op_off[f] gets bad = 1 and
+// no ops.
+struct ExpandOut {
+    uint64_t nops, data_ops, lit;
+    uint32_t weak_hits, hits, bad, pad;
+};
+struct ExpandArgs {
+    const WalkUnit* units;       // the walk's unit table (device)
+    const WalkFileOut* fout;     // its per-unit results (device copy)
+    const WalkRec* stage;        // its staged records (unit u's at stage + units[u].rec_off)
+    const uint32_t* fu;          // nf + 1: file f's units [fu[f], fu[f + 1])
+    const uint64_t* fblk;        // the index's block prefix
+    const uint64_t* last_size;   // per file
+    const uint64_t* op_off;      // nf + 1: file f's ops at ops + op_off[f], capacity to op_off[f + 1]
+    sydelta_op* ops;
+    ExpandOut* res;              // per file
+    uint32_t nf, n;
+};
 struct WalkArgs {
     const uint8_t* base;         // launch base
     const WalkUnit* units;
@@ -274,36 +298,12 @@ struct WalkArgs {
     WalkRec* stage;              // may be host-mapped memory (with out NULL)
     WalkRec* out;                // compacted records of every unit; NULL: left in stage (base = rec_off)
     WalkFileOut* fout;
-    WalkFileOut* fout_dev;       // optional: a device copy of fout (launch_walk_expand reads it)
+    WalkFileOut* fout_dev;       // optional: a device copy of fout (the expansion reads it)
     unsigned long long* total;   // records placed in out (zeroed before the launch)
     unsigned long long* ticks;   // SYDELTA_PHASE_TIMING: 16 counters (zeroed), else null
+    ExpandArgs x;                // self-indexed batches: x.ops set -> the op lists expanded on the device
+    uint32_t* xdone;             // ... with per-file unit counters (zeroed)
 };
-// The op lists of a batch's walk expanded on the device (k_walk_expand): one wave per file
-// joins its units' staged records (a Data op ending at a unit's end merged with the next
-// unit's first; a unit entered past its start cut at the previous unit's exit when its
-// leading literal run reaches it -- match_walk_files' rules), then writes every op
-// (sydelta_op, generator.rs:10-15: a Copy per block of a copy run) at ops + op_off[f], in
-// host-mapped memory.  A file whose units do not chain that way (it needs a re-walk), whose
-// records exceed kExpandRecs or whose ops exceed op_off[f + 1] - op_off[f] gets bad = 1 and no
-// ops.
-constexpr uint32_t kExpandRecs = 1536;
-struct ExpandOut {
-    uint64_t nops, data_ops, lit;
-    uint32_t weak_hits, hits, bad, pad;
-};
-struct ExpandArgs {
-    const WalkUnit* units;       // the walk's unit table (device)
-    const WalkFileOut* fout;     // its per-unit results (device copy)
-    const WalkRec* stage;        // its staged records (unit u's at stage + units[u].rec_off)
-    const uint32_t* fu;          // nf + 1: file f's units [fu[f], fu[f + 1])
-    const uint64_t* fblk;        // the index's block prefix
-    const uint64_t* last_size;   // per file
-    const uint64_t* op_off;      // nf + 1: file f's ops at ops + op_off[f], capacity to op_off[f + 1]
-    sydelta_op* ops;
-    ExpandOut* res;              // per file
-    uint32_t nf, n;
-};
-hipError_t launch_walk_expand(const ExpandArgs& a, hipStream_t s, Profiler* prof);
 // slim: the walk of units whose aligned misses were pre-rolled (launch_preroll; a.ahit set,
 // the filter in global memory), for the units whose walk stays on the aligned grid; it marks
 // them done (kUnitDone in WalkUnit::final_, the unit table written), and a full launch after it

@@ -220,8 +220,7 @@ __global__ void k_idx_insert(const uint32_t* __restrict__ weak, uint64_t n, cons
         for (uint32_t j = 0; j < 4; ++j) {
             const uint64_t sl = F.slot_off + 4ull * b + j;
             const uint32_t old = atomicCAS(&keys[sl], kEmptyKey, w);
-            if (old == kEmptyKey || old == w) {
-                atomicAdd(&cnt[sl], 1u);
+            if (old == kEmptyKey || old == w) {  // (the slot's count and start: k_idx_runs, after the sort)
                 slot_of[i] = (uint32_t)sl;
                 return;
             }
@@ -331,6 +330,23 @@ __global__ __launch_bounds__(kRibListT) void k_ribbon_list(const uint32_t* __res
         if (rank < kRibCap) rib_keys[(size_t)sh * kRibCap + rank] = w;
         else rib_over[atomicAdd(&rib_cnt[kRibShards], 1u)] = w;  // at most nblocks distinct keys
     }
+}
+
+// A slot's candidates from the sorted (slot, block) pairs: the run of a slot starts at start
+// (its first entry's position) and has cnt entries (set by its last entry); only slots that
+// hold a key are ever read.  Replaces an atomic count per key and a scan over every slot.
+__global__ void k_idx_runs(const uint32_t* __restrict__ sorted, uint64_t n, uint32_t* __restrict__ start) {
+    const uint64_t j = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (j >= n) return;
+    const uint32_t sl = sorted[j];
+    if (j == 0 || sorted[j - 1] != sl) start[sl] = (uint32_t)j;
+}
+__global__ void k_idx_counts(const uint32_t* __restrict__ sorted, uint64_t n, const uint32_t* __restrict__ start,
+                             uint32_t* __restrict__ cnt) {
+    const uint64_t j = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (j >= n) return;
+    const uint32_t sl = sorted[j];
+    if (j + 1 == n || sorted[j + 1] != sl) cnt[sl] = (uint32_t)(j + 1 - start[sl]);
 }
 
 // Candidates grouped by slot in index order: order = block indices stably sorted
@@ -4468,7 +4484,6 @@ hipError_t launch_index_build(const uint32_t* d_weak, const uint64_t* d_strong, 
     if ((e = hipMemsetAsync(ix.filt, 0, ix.fwords * 4, s))) return e;
     if (extras && ix.l1 && (e = hipMemsetAsync(ix.l1, 0, l1_total_words(ix.l1_wshift) * 4, s))) return e;
     if ((e = hipMemsetAsync(ix.keys, 0xFF, ix.nslots * 4, s))) return e;
-    if ((e = hipMemsetAsync(ix.cnt, 0, ix.nslots * 4, s))) return e;
     const uint64_t n = ix.nblocks;
     if (n == 0) return hipSuccess;
     {
@@ -4477,13 +4492,6 @@ hipError_t launch_index_build(const uint32_t* d_weak, const uint64_t* d_strong, 
                            (uint32_t)ix.nfiles, ix.d_files, ix.filt, extras ? ix.l1 : nullptr, ix.l1_wshift, ix.keys,
                            ix.cnt, ix.slot_of);
     }
-    size_t tmp = 0;
-    if ((e = hipcub::DeviceScan::ExclusiveSum(nullptr, tmp, ix.cnt, ix.start, (int)ix.nslots, s))) return e;
-    void* d_tmp = nullptr;
-    if ((e = dev_malloc_async(&d_tmp, tmp ? tmp : 16, s))) return e;
-    e = hipcub::DeviceScan::ExclusiveSum(d_tmp, tmp, ix.cnt, ix.start, (int)ix.nslots, s);
-    (void)hipFreeAsync(d_tmp, s);
-    if (e) return e;
     {
         // order = block indices stably sorted by slot (keys slot_of, scratch: fill / cstrong)
         ProfScope ps(prof, s, "k_idx_order");
@@ -4503,6 +4511,9 @@ hipError_t launch_index_build(const uint32_t* d_weak, const uint64_t* d_strong, 
                                                s);
         (void)hipFreeAsync(d_t2, s);
         if (e) return e;
+        hipLaunchKernelGGL(k_idx_runs, dim3(grid_for(n, 256)), dim3(256), 0, s, keys_out, n, ix.start);
+        hipLaunchKernelGGL(k_idx_counts, dim3(grid_for(n, 256)), dim3(256), 0, s, keys_out, n, ix.start, ix.cnt);
+        if ((e = hipGetLastError())) return e;
     }
     hipLaunchKernelGGL(k_idx_cstrong, dim3(grid_for(n, 256)), dim3(256), 0, s, n, ix.order, d_strong, ix.cstrong);
     if ((e = hipGetLastError())) return e;

@@ -187,6 +187,27 @@ def match_batch_handle(index: BatchIndex, buf: torch.Tensor, offs, lens, stream=
     return DeltaBatch(h)
 
 
+def delta_pairs_handle(basis: torch.Tensor, boffs, blens, src: torch.Tensor, soffs, slens, block_size: int,
+                       stream=None) -> DeltaBatch:
+    """Signature + match of every (basis f, source f) pair in one call (sydelta_delta_pairs_device);
+    results left in the library (DeltaBatch)."""
+    arrs = [np.ascontiguousarray(x, dtype=np.uint64) for x in (boffs, blens, soffs, slens)]
+    h = ctypes.c_void_p()
+    check(lib.sydelta_delta_pairs_device(basis.device.index or 0, _ptr(basis), arrs[0].ctypes.data, arrs[1].ctypes.data,
+                                         _ptr(src), arrs[2].ctypes.data, arrs[3].ctypes.data, len(arrs[3]), block_size,
+                                         _stream(stream), ctypes.byref(h)))
+    return DeltaBatch(h)
+
+
+def delta_pairs(basis: torch.Tensor, boffs, blens, src: torch.Tensor, soffs, slens, block_size: int, stream=None):
+    """(list of DeviceDelta, batch totals) of delta_pairs_handle."""
+    b = delta_pairs_handle(basis, boffs, blens, src, soffs, slens, block_size, stream)
+    try:
+        return b.deltas(), b.stats
+    finally:
+        b.close()
+
+
 def match_batch(index: BatchIndex, buf: torch.Tensor, offs, lens, stream=None):
     """Batched rolling match: source f = buf[offs[f] : offs[f]+lens[f]] against basis f.
     Returns (list of DeviceDelta, batch totals)."""

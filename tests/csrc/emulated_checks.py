@@ -719,6 +719,19 @@ def batch_and_chunk_checks():
                 n_checks += 1
             lib.sydelta_delta_batch_free(bt)
             lib.sydelta_index_free(ix)
+            if probe.startswith("walk"):  # the same pairs through the one-call form (two groups from 128 files)
+                for reps in (1, 2):
+                    pb, pbo, pbl = pack(bases * reps)
+                    ps_, pso, psl = pack(srcs * reps)
+                    bt = ctypes.c_void_p()
+                    check(lib.sydelta_delta_pairs_device(0, vp(pb), vp(pbo), vp(pbl), vp(ps_), vp(pso), vp(psl),
+                                                         nf * reps, bs, None, ctypes.byref(bt)))
+                    for k in range(nf * reps):
+                        ew, es, ez = C.compute_checksums(bases[k % nf], bs)
+                        exp = O.ops_from_arrays(*C.generate_delta(srcs[k % nf], ew, es, ez, bs))
+                        assert _ops(lib, lib.sydelta_delta_batch_get(bt, k)) == exp, ("pairs", bs, probe, reps, k)
+                        n_checks += 1
+                    lib.sydelta_delta_batch_free(bt)
     os.environ.pop("SYDELTA_PROBE", None)
     os.environ.pop("SYDELTA_FILE_WALK", None)
     os.environ.pop("SYDELTA_FILE_SEGS", None)

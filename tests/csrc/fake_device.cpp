@@ -586,6 +586,7 @@ hipError_t launch_chain(const chain::ChainArgs& a, hipStream_t, Profiler*) {
 // [entry, end), every visited window classified exactly, the ops run-length coded as
 // k_walk_files writes them (WalkRec), units placed in order in the compact output.  The
 // aligned probe's results, when given, must agree with the exact classification.
+void walk_expand(const ExpandArgs& a, uint64_t u_lo, uint64_t u_hi);  // (below)
 hipError_t launch_walk_files(const WalkArgs& a, hipStream_t, Profiler*, bool slim) {
     EmuTimer emu_t;
     if (slim) return a.ahit && !a.self_nb ? hipSuccess : hipErrorInvalidValue;  // the full launch after it walks every unit
@@ -714,17 +715,21 @@ hipError_t launch_walk_files(const WalkArgs& a, hipStream_t, Profiler*, bool sli
         placed += rec.size();
     }
     if (a.out) *a.total = placed;
+    if (a.x.ops) {  // (the kernel: each file's last unit to finish) the files whose units were all in this launch
+        const uint64_t u_lo = (uint64_t)(a.units - a.x.units);
+        walk_expand(a.x, u_lo, u_lo + a.nunits);
+    }
     return hipSuccess;
 }
 
 // k_walk_expand: each file's units' staged records chained (a unit entered past its start cut
 // at the previous exit when its leading literal run reaches it, else the file is bad), Data
 // ops joined across units, expanded into ops at ops + op_off[f]
-std::atomic<uint64_t> g_expand_files{0};  // files through launch_walk_expand (emu_expand_files)
-hipError_t launch_walk_expand(const ExpandArgs& a, hipStream_t, Profiler*) {
-    EmuTimer emu_t;
-    g_expand_files += a.nf;
+std::atomic<uint64_t> g_expand_files{0};  // files expanded (emu_expand_files)
+void walk_expand(const ExpandArgs& a, uint64_t u_lo, uint64_t u_hi) {
     for (uint32_t f = 0; f < a.nf; ++f) {
+        if (a.fu[f] < u_lo || a.fu[f + 1] > u_hi) continue;
+        ++g_expand_files;
         std::vector<WalkRec> m;
         bool bad = false;
         uint32_t wh = 0, vh = 0;
@@ -767,7 +772,7 @@ hipError_t launch_walk_expand(const ExpandArgs& a, hipStream_t, Profiler*) {
                 lit += x.a;
             }
         }
-        if (bad || m.size() > kExpandRecs || nops > a.op_off[f + 1] - a.op_off[f]) {
+        if (bad || nops > a.op_off[f + 1] - a.op_off[f]) {
             a.res[f] = ExpandOut{0, 0, 0, 0, 0, 1, 0};
             continue;
         }
@@ -783,7 +788,6 @@ hipError_t launch_walk_expand(const ExpandArgs& a, hipStream_t, Profiler*) {
         }
         a.res[f] = ExpandOut{nops, nd, lit, wh, vh, 0, 0};
     }
-    return hipSuccess;
 }
 
 // K10's pre-roll: each missed aligned block's first hit in (x, min(x + n, pend)), exactly

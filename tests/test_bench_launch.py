@@ -73,3 +73,23 @@ def test_one_gpu_and_torchrun_run_in_process():
     p = run(2, {"WORLD_SIZE": "2", "RANK": "1", "LOCAL_RANK": "1"})
     assert p.returncode == 0
     assert json.loads(p.stdout)["RANK"] == "1"
+
+
+@pytest.mark.parametrize("n", [2, 4])
+def test_launcher_forwards_rank0_legs(n):
+    """The C4 / C5 legs ride on rank 0's line (stub: the legs' objects built by bench.c4_leg /
+    c5_leg with fixed timings): forwarded to the launcher's stdout once, aggregated over all
+    N ranks (C4: the 10 000 files' bytes per max-rank step; C5: N chunks of 2 x 8 GiB)."""
+    p = run(n, {"SYDELTA_BENCH_STUB_LEGS": "1"}, args=("--steps", "4"))
+    assert p.returncode == 0, p.stderr
+    lines = [json.loads(ln) for ln in p.stdout.splitlines() if ln.startswith("{") and '"c4"' in ln]
+    assert len(lines) == 1
+    d = lines[0]
+    assert d["n_gpus"] == n
+    c4, c5 = d["c4"], d["c5"]
+    assert c4["files"] == 10000 and c4["files_this_rank"] == bench.shard_range(10000, n, 0)[1]
+    assert c4["ms_per_step"] == 2.0 and c4["scaling"] == "strong"
+    assert abs(c4["value"] - 10000 * ((1 << 21) + 1) / 2e-3 / 2**30) < 1e-2
+    assert c5["ms_per_step"] == 5.0 and c5["scaling"] == "weak"
+    assert abs(c5["value"] - n * 2 * (8 << 30) / 5e-3 / 2**30) < 1e-2
+    assert c5["allgather_bytes_per_rank"] == 12 * (1 << 20) * n

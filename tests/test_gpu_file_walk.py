@@ -54,6 +54,17 @@ def _batch(gpu, pairs, bs, walk, monkeypatch, dx=""):
     return out, tot, prof
 
 
+def _expanded():
+    """Files whose op lists the device expanded so far (sydelta_expand_counters)."""
+    import ctypes
+
+    from sy_amd._lib import lib
+
+    f, h = ctypes.c_uint64(), ctypes.c_uint64()
+    lib.sydelta_expand_counters(ctypes.byref(f), ctypes.byref(h))
+    return f.value, h.value
+
+
 def _mutate(data: bytes, rng, nops: int) -> bytes:
     b = bytearray(data)
     for _ in range(nops):
@@ -121,9 +132,12 @@ def _cases(rng, bs, nfiles):
 def test_file_walk_matches_oracle(gpu, oracle_c, monkeypatch, bs, dx):
     rng = random.Random(1000 + bs)
     pairs = _cases(rng, bs, 80)
+    x0 = _expanded()
     out, tot, prof = _batch(gpu, pairs, bs, "1", monkeypatch, dx)
     assert "k_walk_files" in prof, prof
-    assert ("k_walk_expand" in prof) == (dx == "1") or bs % 64, prof
+    x1 = _expanded()
+    # dx 1: the device expanded every file, or (a file needed a re-walk) the host took the batch
+    assert (x1[0] - x0[0], x1[1] - x0[1]) in (((len(pairs), 0), (0, 1)) if dx == "1" else ((0, 0),)), (x0, x1)
     for i, ((src, basis), d) in enumerate(zip(pairs, out)):
         assert d.tuples() == _oracle_ops(oracle_c, src, basis, bs), (bs, i)
         assert d.source_size == len(src) and d.block_size == bs
@@ -276,8 +290,10 @@ def test_file_walk_c4_shape_few_files(gpu, oracle_c, monkeypatch):
         pairs.append((bytes(s), basis))
     monkeypatch.delenv("SYDELTA_FILE_SEGS", raising=False)
     for dx in ("0", "1"):
+        x0 = _expanded()
         out, _, prof = _batch(gpu, pairs, 4096, "", monkeypatch, dx)
         assert "k_walk_files" in prof
+        assert _expanded()[0] - x0[0] == (len(pairs) if dx == "1" else 0)  # the C4 shape: no re-walks
         for f, ((src, basis), d) in enumerate(zip(pairs, out)):
             assert d.tuples() == _oracle_ops(oracle_c, src, basis, 4096), (dx, f)
 
@@ -396,3 +412,67 @@ def test_chunk_exact_buffers(gpu, oracle_c):
         idx.close()
         for p in ptrs:
             hip.hipFree(p)
+
+
+@pytest.mark.parametrize("dx", ["0", "1"])
+@pytest.mark.parametrize("bs,nfiles", [(256, 80), (4096, 130), (1024, 200)])
+def test_delta_pairs_matches_oracle(gpu, oracle_c, monkeypatch, bs, nfiles, dx):
+    """sydelta_delta_pairs_device: signature + match of every pair in one call (two groups of
+    files from 128 on, the second's signature beside the first's walks; no index): every op
+    list equals the oracle's, and the three-call form's."""
+    rng = random.Random(3000 + bs + nfiles)
+    pairs = _cases(rng, bs, nfiles)
+    monkeypatch.setenv("SYDELTA_DEVICE_EXPAND", dx)
+    bbuf, boff, blen = _pack([b for _, b in pairs])
+    sbuf, soff, slen = _pack([s for s, _ in pairs])
+    gpu.set_profiling(True)
+    gpu.profile(reset=True)
+    out, tot = gpu.delta_pairs(bbuf, boff, blen, sbuf, soff, slen, bs)
+    prof = gpu.profile(reset=True)
+    gpu.set_profiling(False)
+    assert prof["k_walk_files"]["count"] >= (2 if nfiles >= 128 else 1), prof
+    assert "k_idx_insert" not in prof, prof
+    for i, ((src, basis), d) in enumerate(zip(pairs, out)):
+        assert d.tuples() == _oracle_ops(oracle_c, src, basis, bs), (bs, i)
+        assert d.source_size == len(src) and d.block_size == bs
+    assert tot["copy_ops"] == sum(d.stats["copy_ops"] for d in out)
+    assert tot["literal_bytes"] == sum(d.stats["literal_bytes"] for d in out)
+
+
+def test_delta_pairs_refuses(gpu):
+    """The one-call form's limits: block sizes K10 does not take, bases above 1024 blocks."""
+    import torch
+
+    from sy_amd._lib import SyDeltaError
+
+    buf = torch.zeros(1 << 20, dtype=torch.uint8, device="cuda")
+    with pytest.raises(SyDeltaError):
+        gpu.delta_pairs(buf, [0], [4096], buf, [0], [4096], 320 + 1)
+    with pytest.raises(SyDeltaError):
+        gpu.delta_pairs(buf, [0], [1025 * 256], buf, [0], [4096], 256)
+
+
+@pytest.mark.parametrize("nfiles", [130, 1250])
+def test_delta_pairs_c4_shape_on_stream(gpu, nfiles):
+    """The bench's C4 step through the one-call form, repeated on a torch stream of its own:
+    every file's op list equals the three-call form's (signature_batch + index + match_batch)."""
+    import torch
+
+    import bench
+
+    basis, new, (boff, blen, soff, slen) = bench.c4_files(gpu, basis_bytes=1 << 20, nfiles=nfiles, first=77)
+    torch.cuda.synchronize()
+    w, s = gpu.signature_batch(basis, boff, blen, 4096)
+    nblk = (blen + 4095) // 4096
+    idx = gpu.BatchIndex(w, s, nblk, blen - (nblk - 1) * 4096, 4096)
+    ref, _ = gpu.match_batch(idx, new, soff, slen)
+    idx.close()
+    exp = [d.tuples() for d in ref]
+    stream = torch.cuda.Stream()
+    for rep in range(3):
+        with torch.cuda.stream(stream):
+            b = gpu.delta_pairs_handle(basis, boff, blen, new, soff, slen, 4096, stream=stream)
+        got = [d.tuples() for d in b.deltas()]
+        b.close()
+        bad = [f for f in range(nfiles) if got[f] != exp[f]]
+        assert not bad, (rep, len(bad), bad[:10])
