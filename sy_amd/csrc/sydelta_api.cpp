@@ -126,13 +126,6 @@ int ensure_device_impl(int device) {
         if (const char* e = getenv("SYDELTA_POOL_KEEP_MIB")) keep = strtoull(e, nullptr, 10);
         keep <<= 20;
         (void)hipMemPoolSetAttribute(pool, hipMemPoolAttrReleaseThreshold, &keep);
-        // No opportunistic reuse across streams: a block freed on one stream (a kernel's
-        // argument table, freed right after its launch) was handed to an allocation on another
-        // stream while the kernel still read it (the pairs call's two signature groups, measured:
-        // files of the first group signed from the second group's table).  Reuse across streams
-        // then follows event dependencies only.
-        int no_opportunistic = 0;
-        (void)hipMemPoolSetAttribute(pool, hipMemPoolReuseAllowOpportunistic, &no_opportunistic);
         g_pools[device] = pool;
         g_wave_slots[device] = (uint32_t)std::max(64, prop.multiProcessorCount * 16);
         st->status = SYDELTA_OK;
@@ -518,6 +511,50 @@ extern "C" int sydelta_signature_device(int device, const uint8_t* d_buf, uint64
     return sydelta::host_exception();
 }
 
+namespace {
+// The batched signature kernel's table for files [0, nfiles) (block_size % 64 == 0, files
+// 16-byte aligned): aoff | agb | apfx (nact + 1) | loff | llen | lidx, appended to t; agb /
+// lidx count blocks from gb0.
+struct SigTable {
+    size_t at;  // the table's first entry in t
+    uint64_t nact, nfull, npart;
+};
+SigTable sig_batch_table(const uint64_t* off, const uint64_t* len, uint64_t nfiles, uint64_t block_size, uint64_t gb0,
+                         std::vector<uint64_t>& t) {
+    std::vector<uint64_t> aoff, agb, apfx{0}, loff, llen, lidx;
+    uint64_t gb = gb0;
+    for (uint64_t f = 0; f < nfiles; ++f) {
+        const uint64_t nfull = len[f] / block_size;
+        if (nfull) {
+            aoff.push_back(off[f]);
+            agb.push_back(gb);
+            apfx.push_back(apfx.back() + nfull);
+        }
+        if (len[f] % block_size) {
+            loff.push_back(off[f] + nfull * block_size);
+            llen.push_back(len[f] % block_size);
+            lidx.push_back(gb + nfull);
+        }
+        gb += (len[f] + block_size - 1) / block_size;
+    }
+    SigTable r{t.size(), aoff.size(), apfx.back(), loff.size()};
+    for (auto* v : {&aoff, &agb, &apfx, &loff, &llen, &lidx}) t.insert(t.end(), v->begin(), v->end());
+    return r;
+}
+hipError_t launch_sig_table(const uint8_t* d_buf, const uint64_t* d_t, const SigTable& T, uint64_t block_size,
+                            uint32_t* d_weak, uint64_t* d_strong, hipStream_t s, Profiler* prof) {
+    const uint64_t* p = d_t + T.at;
+    const uint64_t* d_aoff = p; p += T.nact;
+    const uint64_t* d_agb = p; p += T.nact;
+    const uint64_t* d_apfx = p; p += T.nact + 1;
+    const uint64_t* d_loff = p; p += T.npart;
+    const uint64_t* d_llen = p; p += T.npart;
+    const uint64_t* d_lidx = p;
+    return launch_signature_batch_fast(d_buf, d_aoff, d_agb, d_apfx, T.nact, T.nfull, d_loff, d_llen, d_lidx, T.npart,
+                                       block_size, d_weak, d_strong, s, prof);
+}
+}  // namespace
+
 extern "C" int sydelta_signature_batch_device(int device, const uint8_t* d_buf, const uint64_t* off,
                                               const uint64_t* len, uint64_t nfiles, uint64_t block_size,
                                               uint32_t* d_weak, uint64_t* d_strong, void* stream) try {
@@ -532,41 +569,17 @@ extern "C" int sydelta_signature_batch_device(int device, const uint8_t* d_buf, 
     bool fast = block_size % 64 == 0 && block_size >= 256 && block_size <= (1ull << 31);
     for (uint64_t f = 0; f < nfiles && fast; ++f) fast = !len[f] || ((uintptr_t)(d_buf + off[f]) & 15) == 0;
     if (fast) {
-        // one table: aoff | agb | apfx (nact + 1) | loff | llen | lidx
         std::vector<uint64_t> t;
         t.reserve(6 * nfiles + 1);
-        std::vector<uint64_t> aoff, agb, apfx{0}, loff, llen, lidx;
-        for (uint64_t f = 0; f < nfiles; ++f) {
-            const uint64_t nfull = len[f] / block_size;
-            if (nfull) {
-                aoff.push_back(off[f]);
-                agb.push_back(fblk[f]);
-                apfx.push_back(apfx.back() + nfull);
-            }
-            if (len[f] % block_size) {
-                loff.push_back(off[f] + nfull * block_size);
-                llen.push_back(len[f] % block_size);
-                lidx.push_back(fblk[f] + nfull);
-            }
-        }
-        const uint64_t nact = aoff.size(), npart = loff.size();
-        for (auto* v : {&aoff, &agb, &apfx, &loff, &llen, &lidx}) t.insert(t.end(), v->begin(), v->end());
+        const SigTable T = sig_batch_table(off, len, nfiles, block_size, 0, t);
         uint64_t* d_t = nullptr;
         HIP_TRY(dev_malloc_async((void**)&d_t, 8 * t.size(), s));
         if (int r = upload_staged(d_t, t.data(), 8 * t.size(), s)) {
             (void)hipFreeAsync(d_t, s);
             return r;
         }
-        const uint64_t* p = d_t;
-        const uint64_t* d_aoff = p; p += nact;
-        const uint64_t* d_agb = p; p += nact;
-        const uint64_t* d_apfx = p; p += nact + 1;
-        const uint64_t* d_loff = p; p += npart;
-        const uint64_t* d_llen = p; p += npart;
-        const uint64_t* d_lidx = p;
         CallProf cp;
-        hipError_t e = launch_signature_batch_fast(d_buf, d_aoff, d_agb, d_apfx, nact, apfx.back(), d_loff, d_llen,
-                                                   d_lidx, npart, block_size, d_weak, d_strong, s, cp.get());
+        hipError_t e = launch_sig_table(d_buf, d_t, T, block_size, d_weak, d_strong, s, cp.get());
         (void)hipFreeAsync(d_t, s);
         HIP_TRY(e);
         if (!stream) HIP_TRY(hipStreamSynchronize(s));  // the library's stream: done on return
@@ -3325,21 +3338,29 @@ extern "C" int sydelta_delta_pairs_device(int device, const uint8_t* d_basis, co
     hipStream_t s2 = thread_aux_stream(device);
     if (!s2) return fail(SYDELTA_E_OOM, "no stream for the pairs call");
     const uint64_t nb = std::max<uint64_t>(1, fblk[nfiles]);
+    const uint64_t G = nfiles >= 128 ? 2 : 1;
+    std::vector<uint64_t> split(G + 1);
+    for (uint64_t g = 0; g <= G; ++g) split[g] = nfiles * g / G;
+    // one upload: the file table, then each group's signature table (the kernels' arguments
+    // live in this call's own allocation: none is freed while a kernel on the other stream runs)
+    std::vector<uint64_t> up(fblk.begin(), fblk.end());
+    std::vector<SigTable> tabs;
+    for (uint64_t g = 0; g < G; ++g)
+        tabs.push_back(sig_batch_table(basis_off + split[g], basis_len + split[g], split[g + 1] - split[g], n,
+                                       fblk[split[g]], up));
     auto al = [](size_t v) { return (v + 255) & ~(size_t)255; };
-    const size_t o_weak = 0, o_strong = al(4 * nb), o_fblk = o_strong + al(8 * nb), need = o_fblk + 8 * (nfiles + 1);
+    const size_t o_weak = 0, o_strong = al(4 * nb), o_fblk = o_strong + al(8 * nb), need = o_fblk + 8 * up.size();
     uint8_t* D = nullptr;
+    CallProf cp;
     HIP_TRY(dev_malloc_async((void**)&D, need, s));
     struct Free {  // the arrays, in s's order (the walks on s2 are joined to s before returning)
         uint8_t* p;
         hipStream_t s;
         ~Free() { (void)hipFreeAsync(p, s); }
     } free_d{D, s};
-    if (int r = upload_staged(D + o_fblk, fblk.data(), 8 * (nfiles + 1), s)) return r;
+    if (int r = upload_staged(D + o_fblk, up.data(), 8 * up.size(), s)) return r;
     // groups: two halves of a batch of >= 128 files (each half still fills the chip's wave
     // slots with its segments)
-    const uint64_t G = nfiles >= 128 ? 2 : 1;
-    std::vector<uint64_t> split(G + 1);
-    for (uint64_t g = 0; g <= G; ++g) split[g] = nfiles * g / G;
     std::vector<hipEvent_t> ev(G, nullptr);
     struct Events {
         std::vector<hipEvent_t>& v;
@@ -3354,13 +3375,11 @@ extern "C" int sydelta_delta_pairs_device(int device, const uint8_t* d_basis, co
     ev_back.v.push_back(ready);
     HIP_TRY(hipEventRecord(ready, s));
     for (uint64_t g = 0; g < G; ++g) {
-        const uint64_t f0 = split[g], f1 = split[g + 1];
         const hipStream_t sg = (g & 1) ? s2 : s;  // (run_walk launches group g's walks on the same stream)
         if (sg != s) HIP_TRY(hipStreamWaitEvent(sg, ready, 0));
-        if (int r = sydelta_signature_batch_device(device, d_basis, basis_off + f0, basis_len + f0, f1 - f0, n,
-                                                   (uint32_t*)(D + o_weak) + fblk[f0],
-                                                   (uint64_t*)(D + o_strong) + fblk[f0], sg))
-            return r;
+        if (tabs[g].nfull || tabs[g].npart)
+            HIP_TRY(launch_sig_table(d_basis, (const uint64_t*)(D + o_fblk), tabs[g], n, (uint32_t*)(D + o_weak),
+                                     (uint64_t*)(D + o_strong), sg, cp.get()));
         ev[g] = take_event(device);
         if (!ev[g]) return fail(SYDELTA_E_OOM, "no event for the pairs call");
         HIP_TRY(hipEventRecord(ev[g], sg));
@@ -3387,7 +3406,6 @@ extern "C" int sydelta_delta_pairs_device(int device, const uint8_t* d_basis, co
         b->d[f].stats.positions = src_len[f] >= n ? src_len[f] - n + 1 : 0;
         b->total.positions += b->d[f].stats.positions;
     }
-    CallProf cp;
     if (int r = match_walk_files(&X, d_src, src_off, src_len, s, cp.get(), b.get(), &split, &ev, s2)) return r;
     *out = b.release();
     return SYDELTA_OK;
