@@ -153,8 +153,22 @@ hipStream_t thread_stream_impl(int device) {
 // part's still runs.  Ordered by events only, never destroyed.  (Low-priority walk streams,
 // so that the dispatcher would favour the hashing beside them, measured the same:
 // `profiles/r05x_*`.)
+// Threads expanding walk records into op arrays (SYDELTA_ASM_THREADS, per call; default the
+// host pool and the caller)
+int asm_threads_env() {
+    const char* e = getenv("SYDELTA_ASM_THREADS");
+    return (e && *e) ? std::max(1, atoi(e)) : (int)walk::HostPool::get().size() + 1;
+}
+
+// Where a one-file index's ribbon level-1 starts (read per call): 2 at index creation, 1 at
+// the match call, 0 after the index (by the first scan)
+int early_ribbon_mode() {
+    const char* e = getenv("SYDELTA_EARLY_RIBBON");
+    return e && (e[0] == '0' || e[0] == '1') ? e[0] - '0' : 2;
+}
+
 hipStream_t thread_walk_stream(int device, int i) {
-    static thread_local std::map<int, hipStream_t> streams[2];
+    static thread_local std::map<int, hipStream_t> streams[3];  // [2]: the ribbon started at index creation
     auto it = streams[i].find(device);
     if (it != streams[i].end()) return it->second;
     hipStream_t s = nullptr;
@@ -797,6 +811,11 @@ void give_event(int device, hipEvent_t e) {
 
 static void index_release(sydelta_index* x) {
     if (!x) return;
+    // tables built on other streams (a ribbon started at creation may never have been used):
+    // the pool's release below follows x->stream
+    if (x->rib_ev && x->rib_stream && x->rib_stream != x->stream) (void)hipStreamWaitEvent(x->stream, x->rib_ev, 0);
+    if (x->extras_ev && x->extras_stream && x->extras_stream != x->stream)
+        (void)hipStreamWaitEvent(x->stream, x->extras_ev, 0);
     if (x->rib_ev) (void)hipEventDestroy(x->rib_ev);
     if (x->extras_ev) (void)hipEventDestroy(x->extras_ev);
     // the build has uploaded the file tables from `stage` (done long before, as a rule)
@@ -1181,6 +1200,22 @@ static int index_create_impl(int device, const uint32_t* weak, const uint64_t* s
         x->deferred = nfiles >= 2 && block_size % 64 == 0 && block_size >= 256 && block_size <= kWalkMaxN &&
                       max_nblk <= kSelfIxMaxBlocks && !ix.l1;
         x->extras_deferred = nfiles == 1 && ix.l1 != nullptr;
+        // the ribbon level-1 of a whole-file scan as large as the basis (scan_index), from the
+        // signature's weak values on a stream of its own: beside the index build, before the
+        // match call is made (SYDELTA_EARLY_RIBBON: 2 here, 1 at the match call, 0 after the
+        // index, as in round 5).  A match that never scans has spent ~0.2 ms of a few CUs.
+        if (nfiles == 1 && nblocks && early_ribbon_mode() == 2 &&
+            (x->rib_mode == 2 || (x->rib_mode == 1 && nblocks * block_size >= kRibMinScan))) {
+            const hipStream_t sr = thread_walk_stream(device, 2);
+            if (!sr) return fail(SYDELTA_E_OOM, "no stream for the ribbon");
+            HIP_TRY(stream_after(sr, s, device));
+            CallProf cp;
+            HIP_TRY(launch_ribbon_build(ix, sr, cp.get(), x->d_weak, nblocks));
+            HIP_TRY(hipEventCreateWithFlags(&x->rib_ev, hipEventDisableTiming));
+            HIP_TRY(hipEventRecord(x->rib_ev, sr));
+            x->rib_built = true;
+            x->rib_stream = sr;
+        }
         if (!x->deferred) {
             CallProf cp;
             HIP_TRY(launch_index_build(x->d_weak, x->d_strong, ix, sb, cp.get(), !x->extras_deferred));
@@ -2829,8 +2864,7 @@ static int match_walk_files(sydelta_index* ix, const uint8_t* d_buf, const uint6
     // the op lists: expanded on the device into op arrays reserved from a pinned host-mapped
     // slab (each file's last unit of the walk kernel) when the host has few threads for them (SYDELTA_DEVICE_EXPAND=0|1
     // forces it off / on; per call), else on the host below
-    static const int asm_threads = getenv("SYDELTA_ASM_THREADS") ? std::max(1, atoi(getenv("SYDELTA_ASM_THREADS")))
-                                                                   : walk::HostPool::get().size() + 1;
+    const int asm_threads = asm_threads_env();
     const char* dxe = getenv("SYDELTA_DEVICE_EXPAND");
     const bool dexp = (dxe && *dxe) ? dxe[0] == '1' : asm_threads <= 4;
     std::vector<uint64_t> op_off;
@@ -3238,8 +3272,7 @@ extern "C" int sydelta_match_device(sydelta_index* idx, const uint8_t* d_src, ui
     // from the signature's weak values -- beside the index's own build on the aux stream --
     // instead of from its exact table after it (SYDELTA_EARLY_RIBBON=0: after, as in round 5)
     const uint64_t npos_all = len >= idx->bs ? len - idx->bs + 1 : 0;
-    const char* er = getenv("SYDELTA_EARLY_RIBBON");
-    if ((!er || er[0] != '0') && s == idx->stream && idx->nfiles == 1 &&
+    if (early_ribbon_mode() == 1 && s == idx->stream && idx->nfiles == 1 &&
         (idx->rib_mode == 2 || (idx->rib_mode == 1 && npos_all >= kRibMinScan))) {
         std::lock_guard<std::mutex> lk(idx->rib_mu);
         if (!idx->rib_built) {
@@ -3608,11 +3641,11 @@ struct InFile {
     // share; profiles/r03n_*).  A failed piece repeats the whole read on this thread, so
     // sydelta_last_error() names the failure.
     int read_at(uint64_t off, uint8_t* dst, uint64_t n) const {
-        static const int kReaders = [] {  // SYDELTA_READ_THREADS: readers per chunk
+        const int kReaders = [] {  // SYDELTA_READ_THREADS: readers per chunk (per call)
             const char* e = getenv("SYDELTA_READ_THREADS");
             return (e && *e) ? std::max(1, atoi(e)) : 16;
         }();
-        static const uint64_t kPiece = [] {  // SYDELTA_READ_PIECE: smallest piece (tests)
+        const uint64_t kPiece = [] {  // SYDELTA_READ_PIECE: smallest piece (tests)
             const char* e = getenv("SYDELTA_READ_PIECE");
             const uint64_t v = (e && *e) ? strtoull(e, nullptr, 10) : 0;
             return v ? v : 8ull << 20;
@@ -4434,8 +4467,7 @@ int chunk_pipe_finish(sydelta_chunk* ch, uint64_t entry, uint64_t* exit_pos, syd
     uint64_t nops = 0, data_ops = 0, lit = 0, hits = 0, weak = 0;
     // assembly threads: SYDELTA_ASM_THREADS, else the host pool and the caller (C5's 1 Mi ops:
     // 0.46-0.58 ms on 16 + 1 threads, 0.78-0.92 on 8, `profiles/r05s_*`)
-    static const int pool = getenv("SYDELTA_ASM_THREADS") ? std::max(1, atoi(getenv("SYDELTA_ASM_THREADS")))
-                                                            : walk::HostPool::get().size() + 1;
+    const int pool = asm_threads_env();
     double ms_wait = 0;
     // units [a, b) after ops [0, nops)
     auto assemble = [&](size_t a, size_t b) -> int {

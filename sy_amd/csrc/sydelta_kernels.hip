@@ -530,7 +530,6 @@ struct ScanArgs {
     uint32_t nm;         // n mod M
     uint32_t c0;         // 2M - 1 - (255*nm mod M)    (k_scan)
     uint32_t timing;     // accumulate per-phase s_memtime cycles of wave 0 into counters[4..8)
-    uint32_t ablate;     // SYDELTA_ABLATE (measurement only, wrong results): k_scan_r / k_scan_g bit 0
                          // skips the drains, bit 1 the level-2 loads; bit 3 the hashing of weak
                          // hits, bit 4 the fat-table lookups
     // k_scan_lds: segment table and per-file probe offsets
@@ -1803,7 +1802,7 @@ __device__ __forceinline__ void drain_regs(const ScanArgs& a, const uint2* recs,
             const volatile uint2* g = recs + i;  // rewritten by later tiles: not from a stale L1 line
             pos = g->x;
             const uint32_t w = g->y;
-            if (run_start + pos < cur.pos_end && !(a.ablate & 16)) {
+            if (run_start + pos < cur.pos_end) {
                 if (kSmall) {
                     const int64_t sl = table_find(cur.keys, cur.bmask, w);
                     hit = sl >= 0;
@@ -1815,7 +1814,6 @@ __device__ __forceinline__ void drain_regs(const ScanArgs& a, const uint2* recs,
         }
         uint64_t m = __ballot(hit);
         weak_hits += __popcll(m);
-        if (a.ablate & 8) continue;
         uint32_t best_mine = kNoBlock;
         while (m) {  // wave-uniform
             const int h = __builtin_ctzll(m);
@@ -1838,8 +1836,6 @@ __device__ __forceinline__ void drain_regs(const ScanArgs& a, const uint2* recs,
     }
 }
 
-// kAblate: the SYDELTA_ABLATE instantiation (measurement only): bit 0 skips the drains,
-// bit 1 the level-2 loads; drain bits 3 (verification) and 4 (fat lookups) as drain_l1.
 // Each wave tile's passes are looked up and verified at the tile's end (drain_regs: the
 // windows hashed from the registers).
 // kRib: the level-1 words hold the ribbon (rib_bit / rib_coef: a position passes when the
@@ -1850,7 +1846,7 @@ __device__ __forceinline__ void drain_regs(const ScanArgs& a, const uint2* recs,
 // level-2; each wave copies the filter of the file it scans into its own LDS slot and
 // tests every position there (k_scan_g's small mode, with the windows verified from the
 // registers).
-template <bool kAblate, bool kRib, int kWaves, bool kSmall = false>
+template <bool kRib, int kWaves, bool kSmall = false>
 __global__ __launch_bounds__(kWaves * 64, 1) void k_scan_r(ScanArgs a, uint32_t per, uint32_t small_words) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     constexpr LdsR L = ldsr_layout();
@@ -2013,7 +2009,6 @@ __global__ __launch_bounds__(kWaves * 64, 1) void k_scan_r(ScanArgs a, uint32_t 
                         } else {
                             p1 = l1_test(w1[t2], Bt.hq[t2]);
                         }
-                        if (kAblate && (a.ablate & 2)) p1 = 0;
                         // a level-1 miss asks for an offset past the buffer: no request, reads 0
                         Bt.w2[t2] = __builtin_amdgcn_raw_buffer_load_b32(frsrc, (int)(((rr[t2] >> fwshift) << 2) | (p1 - 1u)),
                                                                          0, 0);
@@ -2049,7 +2044,7 @@ __global__ __launch_bounds__(kWaves * 64, 1) void k_scan_r(ScanArgs a, uint32_t 
                         load_chunk_nt(sc.base, seg_len, P + n + kWTR + 64ull * lane, xn);
                 }
                 passes += nrec - tile_rec;
-                if (nrec > tile_rec && !(kAblate && (a.ablate & 1)))
+                if (nrec > tile_rec)
                     drain_regs<kSmall>(a, rec + tile_rec, nrec - tile_rec, k * kWTR, xo, xi, kt, weak_hits, run_start, sc,
                                        wo);
                 nrec = tile_rec;
@@ -2167,12 +2162,11 @@ __device__ __forceinline__ void drain_g(const ScanArgs& a, const uint2* recs, ui
             const volatile uint2* g = recs + i;  // rewritten by later tiles: not from a stale L1 line
             pos = g->x;
             const uint32_t w = g->y;
-            if (run_start + pos < cur.pos_end && !(a.ablate & 16)) hit = fat_find_k(cur.keys, cur.fat, cur.bmask, w, rec);
+            if (run_start + pos < cur.pos_end) hit = fat_find_k(cur.keys, cur.fat, cur.bmask, w, rec);
         }
         const uint64_t m = __ballot(hit);
         if (!m) continue;
         weak_hits += __popcll(m);
-        if (a.ablate & 8) continue;
         const uint64_t p = run_start + pos;
         WDef d;
         d.at = (uint64_t)(cur.base - a.src) + p;
@@ -2200,7 +2194,7 @@ __device__ __forceinline__ void drain_gs(const ScanArgs& a, const uint2* recs, u
             const volatile uint2* g = recs + i;
             pos = g->x;
             const uint32_t w = g->y;
-            if (run_start + pos < cur.pos_end && !(a.ablate & 16)) {
+            if (run_start + pos < cur.pos_end) {
                 const int64_t sl = table_find(cur.keys, cur.bmask, w);
                 hit = sl >= 0;
                 gslot = (uint32_t)(cur.slot_off + (uint64_t)(sl < 0 ? 0 : sl));
@@ -2209,7 +2203,6 @@ __device__ __forceinline__ void drain_gs(const ScanArgs& a, const uint2* recs, u
         const uint64_t m = __ballot(hit);
         if (!m) continue;
         weak_hits += __popcll(m);
-        if (a.ablate & 8) continue;
         const uint64_t p = run_start + pos;
         WDef d;
         d.at = (uint64_t)(cur.base - a.src) + p;
@@ -2243,7 +2236,7 @@ static_assert(ldsg_layout().total <= 160 * 1024 - 256, "k_scan_g's LDS");
 // words): no level-1 filter and no level-2 loads; each wave copies the filter of the file
 // it scans into its own LDS slot (small_words words) and tests every position there;
 // passes are looked up in the exact table (drain_gs).  Replaces k_scan_lds for them.
-template <bool kAblate, bool kRib, bool kSmall>
+template <bool kRib, bool kSmall>
 __global__ __launch_bounds__(kTR, 2) void k_scan_g(ScanArgs a, uint32_t per, uint32_t rt, uint32_t small_words) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     const LdsG L = ldsg_layout(kSmall ? small_words : 0u);
@@ -2401,7 +2394,6 @@ __global__ __launch_bounds__(kTR, 2) void k_scan_g(ScanArgs a, uint32_t per, uin
                         } else {
                             p1 = l1_test(w1[t2], Bt.hq[t2]);
                         }
-                        if (kAblate && (a.ablate & 2)) p1 = 0;
                         Bt.w2[t2] = __builtin_amdgcn_raw_buffer_load_b32(frsrc, (int)(((rr[t2] >> fwshift) << 2) | (p1 - 1u)),
                                                                          0, 0);
                     }
@@ -2438,7 +2430,7 @@ __global__ __launch_bounds__(kTR, 2) void k_scan_g(ScanArgs a, uint32_t per, uin
                 A0 = __builtin_amdgcn_readlane(am, 63);
                 B0 = __builtin_amdgcn_readlane(bm, 63);
                 passes += nrec - tile_rec;
-                if (nrec > tile_rec && !(kAblate && (a.ablate & 1))) {
+                if (nrec > tile_rec) {
                     if (kSmall) drain_gs(a, rec + tile_rec, nrec - tile_rec, weak_hits, run_start, sc, wo);
                     else drain_g(a, rec + tile_rec, nrec - tile_rec, weak_hits, run_start, sc, wo);
                 }
@@ -4589,8 +4581,6 @@ hipError_t launch_scan(const uint8_t* d_buf, const ScanSeg* d_segs, uint32_t nse
     a.nm = n % kMod;
     static const bool timing = getenv("SYDELTA_PHASE_TIMING") != nullptr;
     a.timing = timing ? 1u : 0u;
-    static const uint32_t ablate = getenv("SYDELTA_ABLATE") ? (uint32_t)strtoul(getenv("SYDELTA_ABLATE"), nullptr, 0) : 0u;
-    a.ablate = ablate;
     a.segs = d_segs;
     a.nsegs = nsegs;
     a.ntiles = ntiles;
@@ -4620,9 +4610,8 @@ hipError_t launch_scan(const uint8_t* d_buf, const ScanSeg* d_segs, uint32_t nse
         static hipError_t g_err = hipSuccess;
         static int g_cus = 256;
         std::call_once(g_once, [] {
-            for (const void* f : {(const void*)k_scan_g<false, false, false>, (const void*)k_scan_g<true, false, false>,
-                                  (const void*)k_scan_g<false, true, false>, (const void*)k_scan_g<true, true, false>,
-                                  (const void*)k_scan_g<false, false, true>, (const void*)k_scan_g<true, false, true>})
+            for (const void* f : {(const void*)k_scan_g<false, false>, (const void*)k_scan_g<true, false>,
+                                  (const void*)k_scan_g<false, true>})
                 if (g_err == hipSuccess)
                     g_err = hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024 - 256);
             int dev = 0, cus = 0;
@@ -4662,14 +4651,14 @@ hipError_t launch_scan(const uint8_t* d_buf, const ScanSeg* d_segs, uint32_t nse
         {
             ProfScope ps(prof, s, "k_scan_g");
             const dim3 gd(grid), bd(kTR);
-#define LAUNCH_G(AB, RB, SM) hipLaunchKernelGGL((k_scan_g<AB, RB, SM>), gd, bd, LG.total, s, a, per, rt, small_words)
-            if (small) { if (a.ablate) LAUNCH_G(true, false, true); else LAUNCH_G(false, false, true); }
-            else if (ix.l1_ribbon) { if (a.ablate) LAUNCH_G(true, true, false); else LAUNCH_G(false, true, false); }
-            else { if (a.ablate) LAUNCH_G(true, false, false); else LAUNCH_G(false, false, false); }
+#define LAUNCH_G(RB, SM) hipLaunchKernelGGL((k_scan_g<RB, SM>), gd, bd, LG.total, s, a, per, rt, small_words)
+            if (small) LAUNCH_G(false, true);
+            else if (ix.l1_ribbon) LAUNCH_G(true, false);
+            else LAUNCH_G(false, false);
 #undef LAUNCH_G
         }
         e = hipGetLastError();
-        if (e == hipSuccess && !(a.ablate & 1)) {
+        if (e == hipSuccess) {
             ProfScope ps(prof, s, "k_verify_w");
             hipLaunchKernelGGL(k_verify_w, dim3(verify_grid), dim3(256), 0, s, a);
             e = hipGetLastError();
@@ -4683,9 +4672,8 @@ hipError_t launch_scan(const uint8_t* d_buf, const ScanSeg* d_segs, uint32_t nse
         static hipError_t r_err = hipSuccess;
         static int r_cus = 256;
         std::call_once(r_once, [] {
-            for (const void* f : {(const void*)k_scan_r<false, false, 12>, (const void*)k_scan_r<true, false, 12>,
-                                  (const void*)k_scan_r<false, true, 12>, (const void*)k_scan_r<true, true, 12>,
-                                  (const void*)k_scan_r<false, false, 12, true>, (const void*)k_scan_r<true, false, 12, true>})
+            for (const void* f : {(const void*)k_scan_r<false, 12>, (const void*)k_scan_r<true, 12>,
+                                  (const void*)k_scan_r<false, 12, true>})
                 if (r_err == hipSuccess)
                     r_err = hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024 - 256);
             int dev = 0, cus = 0;
@@ -4713,14 +4701,13 @@ hipError_t launch_scan(const uint8_t* d_buf, const ScanSeg* d_segs, uint32_t nse
         {
             ProfScope ps(prof, s, "k_scan_r");
             const dim3 g(grid), b(64 * waves);
-#define LAUNCH_R(AB, RB, W) hipLaunchKernelGGL((k_scan_r<AB, RB, W>), g, b, LR.total, s, a, per, 0u)
-            if (small_r) {
-                if (a.ablate) hipLaunchKernelGGL((k_scan_r<true, false, 12, true>), g, b, LR.total, s, a, per, small_words);
-                else hipLaunchKernelGGL((k_scan_r<false, false, 12, true>), g, b, LR.total, s, a, per, small_words);
-            } else {
-                if (ix.l1_ribbon) { if (a.ablate) LAUNCH_R(true, true, 12); else LAUNCH_R(false, true, 12); }
-                else { if (a.ablate) LAUNCH_R(true, false, 12); else LAUNCH_R(false, false, 12); }
-            }
+#define LAUNCH_R(RB, W) hipLaunchKernelGGL((k_scan_r<RB, W>), g, b, LR.total, s, a, per, 0u)
+            if (small_r)
+                hipLaunchKernelGGL((k_scan_r<false, 12, true>), g, b, LR.total, s, a, per, small_words);
+            else if (ix.l1_ribbon)
+                LAUNCH_R(true, 12);
+            else
+                LAUNCH_R(false, 12);
 #undef LAUNCH_R
         }
         e = hipGetLastError();

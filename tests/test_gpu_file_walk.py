@@ -149,6 +149,22 @@ def test_file_walk_matches_oracle(gpu, oracle_c, monkeypatch, bs, dx):
     assert [d.tuples() for d in out0] == [d.tuples() for d in out]
 
 
+@pytest.mark.parametrize("asm", ["1", "4", "5", "16"])
+def test_file_walk_asm_threads(gpu, oracle_c, monkeypatch, asm):
+    """SYDELTA_ASM_THREADS (per call): the expansion's host threads, and with
+    SYDELTA_DEVICE_EXPAND unset the choice it implies (<= 4: the walk kernel expands)."""
+    monkeypatch.setenv("SYDELTA_ASM_THREADS", asm)
+    bs = 1024
+    pairs = _cases(random.Random(77), bs, 80)
+    x0 = _expanded()
+    out, _, _ = _batch(gpu, pairs, bs, "1", monkeypatch)
+    x1 = _expanded()
+    dev = int(asm) <= 4
+    assert (x1[0] - x0[0], x1[1] - x0[1]) in (((len(pairs), 0), (0, 1)) if dev else ((0, 0),)), (asm, x0, x1)
+    for i, ((src, basis), d) in enumerate(zip(pairs, out)):
+        assert d.tuples() == _oracle_ops(oracle_c, src, basis, bs), (asm, i)
+
+
 def test_file_walk_c4_shape_1mib(gpu, oracle_c, monkeypatch):
     """BASELINE C4's files (1 MiB, one inserted byte + 16 substitutions), 128 of them,
     through the default (auto) selection."""

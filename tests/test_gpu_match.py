@@ -122,6 +122,39 @@ def test_random_medium_edits(bs, gpu, oracle_c):
     assert O.py_apply_delta(basis, src, d.tuples()) == src
 
 
+@pytest.mark.parametrize("small", ["0", "1"])
+@pytest.mark.parametrize("bs", [1024, 4096])
+def test_scan_small_index_modes(bs, small, gpu, oracle_c, monkeypatch):
+    """SYDELTA_SCAN_SMALL (per call): a small index scanned by k_scan_lds (0) or by the
+    register-fed scans' small mode (k_scan_r at bs 4096, k_scan_g elsewhere); every
+    position scanned (SYDELTA_PROBE=0)."""
+    monkeypatch.setenv("SYDELTA_SCAN_SMALL", small)
+    monkeypatch.setenv("SYDELTA_PROBE", "0")
+    rng = random.Random(bs + int(small))
+    basis = rng.randbytes(rng.randint(1 << 20, 2 << 20))
+    src = bytearray(basis)
+    for _ in range(30):
+        op, p = rng.randint(0, 2), rng.randrange(len(src))
+        if op == 0:
+            src[p] ^= 0x3C
+        elif op == 1:
+            src[p:p] = rng.randbytes(rng.randint(1, 200))
+        else:
+            q = rng.randrange(len(src))
+            src[p:p] = src[q:q + rng.randint(1, 2 * bs)]
+    src = bytes(src)
+    gpu.set_profiling(True)
+    gpu.profile(reset=True)
+    try:
+        d = _device_ops(gpu, src, basis, bs)
+        prof = gpu.profile(reset=True)
+    finally:
+        gpu.set_profiling(False)
+    want = "k_scan_lds" if small == "0" else ("k_scan_r" if bs == 4096 else "k_scan_g")
+    assert want in prof, prof
+    assert d.tuples() == _oracle_ops(oracle_c, src, basis, bs)
+
+
 @pytest.mark.parametrize("pattern", [b"\x00", b"ABC", b"ABCD", b"0123456789" * 7])
 def test_degenerate_repetitive_data(pattern, gpu, oracle_c):
     """All-zero / periodic data: every window matches (dense hits, the chain

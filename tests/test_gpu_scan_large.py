@@ -1,7 +1,8 @@
 """GPU parity for large single-file indexes (> 16 Ki basis blocks) at bs 4096: the
 register-fed level-1-filter scan k_scan_r against the oracle (round 4 removed the
 superseded large-index kernels), with both level-1 layouts forced on the smaller cases
-(SYDELTA_L1=bloom|ribbon); the 4 GiB C3 case runs once, with the default (the ribbon).
+(SYDELTA_L1=bloom|ribbon); the 4 GiB C3 case runs with the default (the ribbon),
+started at each of its three points (SYDELTA_EARLY_RIBBON).
 
 * 96 MiB basis, mixed edits (an all-literal stretch, sparse substitutions, a shift,
   planted unaligned copies, duplicated blocks): bit-exact op list against the C
@@ -133,9 +134,14 @@ def test_large_index_dense_passes(gpu, oracle_c, level1):
     assert d.tuples() == O.ops_from_arrays(*oracle_c.generate_delta(src, ew, es, ez, bs))
 
 
-def test_config3_full_size_planted(gpu, oracle_c):
-    """C3 at 4 GiB with a non-trivial expected op list."""
+@pytest.mark.parametrize("early", ["0", "1", "2"])
+def test_config3_full_size_planted(gpu, oracle_c, monkeypatch, early):
+    """C3 at 4 GiB with a non-trivial expected op list; the ribbon
+    level-1 started at index creation (SYDELTA_EARLY_RIBBON=2, the default), at the match
+    call (1) or by the first scan (0)."""
     import torch
+
+    monkeypatch.setenv("SYDELTA_EARLY_RIBBON", early)
 
     bs = 4096
     n = (4 << 30) - 1000  # partial last basis block of 3096 bytes

@@ -66,6 +66,29 @@ def test_streamed_path_api_matches_oracle(bs, n, chunk, tmp_path, monkeypatch, o
     assert delta == D.generate_delta(ps, sigs, bs)
 
 
+@pytest.mark.parametrize("readers", ["1", "3", "16"])
+def test_streamed_read_pieces(readers, tmp_path, monkeypatch, oracle_c, gpu):
+    """SYDELTA_READ_THREADS (per call): each streamed chunk read in that many pieces by the
+    host pool (SYDELTA_READ_PIECE lowers the smallest piece so a 1 MiB chunk splits)."""
+    import sy_amd.delta as D
+
+    monkeypatch.setenv("SYDELTA_STREAM_CHUNK", str(1 << 20))
+    monkeypatch.setenv("SYDELTA_READ_THREADS", readers)
+    monkeypatch.setenv("SYDELTA_READ_PIECE", "65536")
+    bs = 4096
+    basis, src = _case(int(readers), (3 << 20) + 777, bs)
+    pb, ps = tmp_path / "dest", tmp_path / "src"
+    basis.tofile(pb)
+    src.tofile(ps)
+    sigs = D.compute_checksums(pb, bs)
+    w, s, z = oracle_c.compute_checksums(basis, bs)
+    assert [x.weak for x in sigs] == w.tolist() and [x.strong for x in sigs] == s.tolist()
+    delta = D.generate_delta_streaming(ps, sigs, bs)
+    exp = O.ops_from_arrays(*oracle_c.generate_delta(src, w, s, z, bs))
+    got = [("C", op.offset, op.size) if isinstance(op, D.Copy) else ("D", len(op.data)) for op in delta.ops]
+    assert got == [("C", a, b) if k == "C" else ("D", b) for k, a, b in exp]
+
+
 @pytest.mark.parametrize("size", [0, 1, 4095, 4096, 4097])
 def test_streamed_small_and_empty_files(size, tmp_path, monkeypatch, oracle_c, gpu):
     import sy_amd.delta as D
