@@ -215,13 +215,20 @@ __global__ void k_idx_insert(const uint32_t* __restrict__ weak, uint64_t n, cons
     atomicOr(filt + F.filt_off + (h.r >> F.fwshift), filt_mask(h.q));
     if (l1)  // single-file index only (l1_test)
         atomicOr(l1 + (l1_wshift == 1 ? (size_t)l1r_word(h.q) : (size_t)(h.q >> l1_wshift)), 1u << (h.q & 31));
+    // The bucket's four slots are read first (one 16-byte load) and only a slot read empty is
+    // claimed: a slot goes from empty to its key once during the build, so a key read is
+    // final, and an empty read that is stale loses its CAS and moves on.  (One CAS per key
+    // instead of one per slot tried before the free one.)
     uint32_t b = bucket_hash(w) & F.bmask;
     for (;;) {
+        const uint64_t s0 = F.slot_off + 4ull * b;
+        const uint4 v = *(const uint4*)(keys + s0);
+        const uint32_t cur[4] = {v.x, v.y, v.z, v.w};
         for (uint32_t j = 0; j < 4; ++j) {
-            const uint64_t sl = F.slot_off + 4ull * b + j;
-            const uint32_t old = atomicCAS(&keys[sl], kEmptyKey, w);
+            uint32_t old = cur[j];
+            if (old == kEmptyKey) old = atomicCAS(&keys[s0 + j], kEmptyKey, w);
             if (old == kEmptyKey || old == w) {  // (the slot's count and start: k_idx_runs, after the sort)
-                slot_of[i] = (uint32_t)sl;
+                slot_of[i] = (uint32_t)(s0 + j);
                 return;
             }
         }
