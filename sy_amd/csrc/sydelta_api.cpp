@@ -1295,6 +1295,8 @@ void install_op_arena() {
 std::atomic<uint64_t> g_device_walks{0}, g_device_walk_fallbacks{0};  // sydelta_walk_counters
 std::atomic<uint64_t> g_expand_files{0}, g_expand_host{0};               // sydelta_expand_counters
 
+struct OpSlab;
+OpSlab* slab_of(const void* q);  // (below)
 std::mutex g_ops_mu;
 std::vector<OpVec>& g_ops_pool = *new std::vector<OpVec>();  // never destroyed (arrays may be pinned)
 OpVec take_ops(size_t want) {
@@ -1317,7 +1319,7 @@ OpVec take_ops(size_t want) {
     return v;
 }
 void give_ops(OpVec&& v) {
-    if (v.capacity() < 4096) return;
+    if (v.capacity() < 4096 || slab_of(v.data())) return;  // (a slab's array goes back to its slab)
     std::lock_guard<std::mutex> lk(g_ops_mu);
     if (g_ops_pool.size() < 16) g_ops_pool.push_back(std::move(v));
 }
@@ -1328,8 +1330,6 @@ void give_ops(OpVec&& v) {
 // the walks that fill them, and their release as much again (tools/walk_bench_c4.cpp,
 // 10 000 C4 files on 8 threads in this container: walks 14 ms with fresh arrays, 5.3 ms
 // with recycled ones, and 14 ms to free the fresh ones).  At most kSmallPoolBytes held.
-struct OpSlab;
-OpSlab* slab_of(const void* q);  // (below)
 std::mutex g_small_mu;
 std::vector<OpVec>* g_small_pool = new std::vector<OpVec>();  // never destroyed (exit order)
 size_t g_small_bytes = 0;
@@ -4164,6 +4164,8 @@ struct ChunkPipe {
     PinnedHits stage;              // the uploads' source (kStage)
     const WalkFileOut* fout = nullptr;
     const WalkRec* rec = nullptr;
+    const WalkUnit* d_units = nullptr;  // the unit table and the staged records (device), for
+    const WalkRec* d_stage = nullptr;   // the ops written on the device (launch_chunk_write)
     const uint32_t* ahit = nullptr;  // the probe's results (device; NULL: no probe)
     const uint32_t* apw = nullptr;
     unsigned long long* ticks = nullptr;  // SYDELTA_PHASE_TIMING: 16 counters per part (device)
@@ -4338,6 +4340,8 @@ int chunk_pipe_launch(sydelta_chunk* ch, uint64_t from, bool probe) {
     uint8_t* D = (uint8_t*)P.dmem;
     P.fout = (const WalkFileOut*)H;
     P.rec = (const WalkRec*)(H + h_rec);
+    P.d_units = (const WalkUnit*)(D + o_units);
+    P.d_stage = (const WalkRec*)(D + o_stage);
     uint32_t* d_out = (uint32_t*)(D + o_out);
     uint32_t* d_pw = (uint32_t*)(D + o_pw);
     uint64_t* d_pst = (uint64_t*)(D + o_pst);
@@ -4456,8 +4460,45 @@ int chunk_pipe_finish(sydelta_chunk* ch, uint64_t entry, uint64_t* exit_pos, syd
     uint64_t cap = 0;  // ops per unit: at most a Copy per block, a Data op before each, a tail Copy
     for (size_t u = u0; u < nu; ++u) cap += 2 * ((units[u].end - units[u].entry) / n) + 8;
     OpVec& ops = d->ops;
-    if (ops.capacity() < cap) ops = take_ops(cap);
+    // the ops written on the device (launch_chunk_write) into an op array reserved from a
+    // pinned host-mapped slab, when the host has few threads for them (SYDELTA_DEVICE_EXPAND,
+    // as for batches): the host only chains the units and plans each one's ops
+    const char* dxe = getenv("SYDELTA_DEVICE_EXPAND");
+    const bool want_dev = P.d_units && P.d_stage && ((dxe && *dxe) ? dxe[0] == '1' : asm_threads_env() <= 4);
+    bool cdev = false;
+    if (want_dev) {
+        if (OpSlab* slab = slab_open(cap * sizeof(sydelta_op))) {
+            OpVec v;
+            v.reserve(cap);
+            cdev = (uint8_t*)v.data() == slab->p;
+            slab_close(slab);
+            if (cdev) ops.swap(v);
+        }
+    }
+    if (!cdev && ops.capacity() < cap) ops = take_ops(cap);
     ops.resize(cap);
+    CxPlan* plan_h = nullptr;  // per unit (staging), and its device copy
+    CxPlan* plan_d = nullptr;
+    PinnedHits plan_pin;
+    struct PlanFree {
+        CxPlan*& d;
+        PinnedHits& h;
+        hipStream_t s;
+        ~PlanFree() {
+            if (d) (void)hipFreeAsync(d, s);
+            give_mapped(h, kStage);
+        }
+    } plan_free{plan_d, plan_pin, C.s};
+    if (cdev) {
+        if (int r = take_mapped(sizeof(CxPlan) * nu, plan_pin, kStage)) return r;
+        HIP_TRY(dev_malloc_async((void**)&plan_d, sizeof(CxPlan) * nu, C.s));
+        plan_h = (CxPlan*)plan_pin.p;
+    }
+    bool dev_pending = false;  // device writes queued on C.s
+    std::vector<std::pair<uint64_t, uint64_t>> patches;  // (op, bytes) added once the device's writes are done
+    std::vector<const WalkRec*> orig(nu, nullptr);  // each unit's first record in the host copy
+    std::vector<uint8_t> cut(nu, 0);  // its first record cut (joins)
+    size_t owner = SIZE_MAX;           // the unit holding the last op planned so far
     const double ms_ops = ms_since(t_begin);
     double ms_asm = 0;
     std::vector<WalkFileOut> out(nu);
@@ -4540,6 +4581,7 @@ int chunk_pipe_finish(sydelta_chunk* ch, uint64_t entry, uint64_t* exit_pos, syd
         for (size_t u = a; u < b; ++u) {  // (a unit with no records: an empty span anywhere)
             const WalkRec* r = out[u].count ? base + (out[u].base - lo) : base;
             span[u] = {r, r + out[u].count};
+            orig[u] = r;
         }
         ms_take += ms_since(tt);
     };
@@ -4560,9 +4602,73 @@ int chunk_pipe_finish(sydelta_chunk* ch, uint64_t entry, uint64_t* exit_pos, syd
         } else {
             w->a = (uint32_t)(w->off + w->a - pe);
             w->off = pe;
+            cut[u] = 1;
         }
         units[u].entry = pe;
         return true;
+    };
+    // units [a, b) planned (the host's assemble rules, same counts) and written on the device
+    auto plan_part = [&](size_t a, size_t b) -> int {
+        if (b <= a) return SYDELTA_OK;
+        const auto ta = std::chrono::steady_clock::now();
+        for (size_t u = a; u < b; ++u) {
+            const WalkRec *r0 = span[u].first, *r1 = span[u].second;
+            uint64_t k = 0, nd = 0, lb = 0;
+            for (const WalkRec* r = r0; r < r1; ++r) {
+                if (r->kind) {
+                    k += r->kind;
+                } else {
+                    ++k;
+                    ++nd;
+                    lb += r->a;
+                }
+            }
+            bool join = false;
+            if (u > u0 && r0 < r1 && !r0->kind && span[u - 1].second > span[u - 1].first) {
+                const WalkRec* pl = span[u - 1].second - 1;
+                join = !pl->kind && pl->off + pl->a == r0->off;
+            }
+            CxPlan& pu = plan_h[u];
+            const uint32_t s0 = (uint32_t)(r0 - orig[u]);
+            pu = CxPlan{nops, 0, 0, 0, out[u].count, s0 + (join ? 1u : 0u), 0};
+            if (!join && cut[u] && s0 == 0 && r0 < r1) {
+                pu.flags = 1;
+                pu.r0_off = r0->off;
+                pu.r0_a = r0->a;
+            }
+            if (join) {  // into the last op so far (a Data op): its unit's, or a patch after the writes
+                --k;
+                --nd;
+                if (owner != SIZE_MAX && owner >= a)
+                    plan_h[owner].ext += r0->a;
+                else
+                    patches.emplace_back(nops - 1, (uint64_t)r0->a);
+            }
+            data_ops += nd;
+            lit += lb;
+            hits += out[u].hits;
+            weak += out[u].weak_hits;
+            nops += k;
+            if (k) owner = u;
+        }
+        if (nops > ops.size())
+            return fail(SYDELTA_E_KERNEL, "chunk walk: %llu ops above the bound %llu", (unsigned long long)nops,
+                        (unsigned long long)ops.size());
+        HIP_TRY(hipMemcpyAsync(plan_d + a, plan_h + a, sizeof(CxPlan) * (b - a), hipMemcpyHostToDevice, C.s));
+        HIP_TRY(launch_chunk_write(P.d_units + a, P.d_stage, plan_d + a, (uint32_t)(b - a), (uint32_t)n, nbf, ls,
+                                   ops.data(), C.s, C.prof));
+        dev_pending = true;
+        ms_asm += ms_since(ta);
+        return SYDELTA_OK;
+    };
+    // the device's writes done, then the joins into ops they wrote
+    auto dev_finish = [&]() -> int {
+        if (!dev_pending) return SYDELTA_OK;
+        dev_pending = false;
+        HIP_TRY(hipStreamSynchronize(C.s));
+        for (const auto& pt : patches) ops[pt.first].b += pt.second;
+        patches.clear();
+        return SYDELTA_OK;
     };
     size_t stop = nu;  // the first unit whose entry is not the previous one's exit
     for (size_t j = 0; j + 1 < P.ub.size() && stop == nu; ++j) {
@@ -4574,11 +4680,12 @@ int chunk_pipe_finish(sydelta_chunk* ch, uint64_t entry, uint64_t* exit_pos, syd
         take(a, b);
         size_t e = a;
         while (e < b && joins(e, e == u0 ? entry : out[e - 1].exit)) ++e;
-        if (int r = assemble(a, e)) return r;
+        if (int r = cdev ? plan_part(a, e) : assemble(a, e)) return r;
         if (e < b) stop = e;
     }
     int rounds = 0;
     if (stop < nu) {
+        if (int r = dev_finish()) return r;  // (the host's assembly below may join into the device's last op)
         for (hipEvent_t e : P.done) HIP_TRY(hipEventSynchronize(e));
         take(P.ub[std::upper_bound(P.ub.begin(), P.ub.end(), (uint32_t)stop) - P.ub.begin()], nu);  // later sub-ranges
         for (;;) {
@@ -4610,6 +4717,7 @@ int chunk_pipe_finish(sydelta_chunk* ch, uint64_t entry, uint64_t* exit_pos, syd
         }
         if (int r = assemble(stop, nu)) return r;
     }
+    if (int r = dev_finish()) return r;
     if (P.ticks) {
         std::vector<unsigned long long> tk(16 * P.done.size());
         HIP_TRY(hipMemcpy(tk.data(), P.ticks, 8 * tk.size(), hipMemcpyDeviceToHost));
@@ -4628,9 +4736,10 @@ int chunk_pipe_finish(sydelta_chunk* ch, uint64_t entry, uint64_t* exit_pos, syd
     d->stats.weak_hits = weak;
     *exit_pos = out[nu - 1].exit;
     if (host_timing)
-        fprintf(stderr, "sydelta chunk walk: %zu segments in %zu parts, %d re-walk rounds, %llu ops: op array %.3f ms, "
+        fprintf(stderr, "sydelta chunk walk: %zu segments in %zu parts, %d re-walk rounds, %llu ops%s: op array %.3f ms, "
                 "waits %.3f ms, results %.3f ms, assembly %.3f ms, all %.3f ms\n", nu, P.done.size(), rounds,
-                (unsigned long long)nops, ms_ops, ms_wait, ms_take, ms_asm, ms_since(t_begin));
+                (unsigned long long)nops, cdev ? " (written on the device)" : "", ms_ops, ms_wait, ms_take, ms_asm,
+                ms_since(t_begin));
     return SYDELTA_OK;
 }
 }  // namespace

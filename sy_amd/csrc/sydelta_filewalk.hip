@@ -805,6 +805,66 @@ __device__ void expand_file(const ExpandArgs& a, uint32_t f, unsigned char* lds,
 }
 
 // ===========================================================================
+// A chunk's ops written on the device (launch_chunk_write)
+// ===========================================================================
+// One wave per unit: its effective records 64 at a time (the plan's cut first record, the
+// extension of its last one), an inclusive op prefix in LDS, then ops j = lane, lane + 64, ...
+// of those records (the record holding op j by binary search), three 8-byte stores each.
+__global__ __launch_bounds__(64) void k_chunk_write(const WalkUnit* __restrict__ units, const WalkRec* __restrict__ stage,
+                                                    const CxPlan* __restrict__ plan, uint32_t n, uint64_t nbf, uint64_t ls,
+                                                    uint64_t* __restrict__ ops) {
+    __shared__ WalkRec rec[64];
+    __shared__ uint32_t pre[64];
+    const uint32_t lane = threadIdx.x;
+    const CxPlan P = plan[blockIdx.x];
+    const WalkRec* src = stage + units[blockIdx.x].rec_off;
+    uint64_t o = P.first;
+    for (uint32_t b = P.skip; b < P.cnt; b += 64) {
+        const uint32_t i = b + lane;
+        WalkRec x{1, 0, 0};
+        uint32_t c = 0;
+        if (i < P.cnt) {
+            x = src[i];
+            if (i == P.skip && (P.flags & 1)) {
+                x.off = P.r0_off;
+                x.a = P.r0_a;
+            }
+            c = x.kind ? x.kind : 1u;
+        }
+        uint32_t tot;
+        const uint32_t ex = wave_scan_excl(c, tot);
+        rec[lane] = x;
+        pre[lane] = ex + c;  // (lanes past the records: the total)
+        __syncthreads();
+        for (uint32_t j = lane; j < tot; j += 64) {
+            uint32_t lo = 0, hi = 63;
+            while (lo < hi) {  // the first record whose prefix passes j
+                const uint32_t mid = (lo + hi) >> 1;
+                if (pre[mid] > j) hi = mid; else lo = mid + 1;
+            }
+            const WalkRec y = rec[lo];
+            uint64_t kd, oa, ob;
+            if (!y.kind) {
+                kd = SYDELTA_OP_DATA;
+                oa = y.off;
+                ob = (uint64_t)y.a + (b + lo + 1 == P.cnt ? P.ext : 0ull);
+            } else {
+                const uint64_t g = (uint64_t)y.a + (j - (pre[lo] - y.kind));
+                kd = SYDELTA_OP_COPY;
+                oa = g * n;
+                ob = g + 1 == nbf ? ls : (uint64_t)n;
+            }
+            uint64_t* w = ops + 3 * (o + j);
+            w[0] = kd;
+            w[1] = oa;
+            w[2] = ob;
+        }
+        o += tot;
+        __syncthreads();
+    }
+}
+
+// ===========================================================================
 // Launch wrappers
 // ===========================================================================
 
@@ -820,6 +880,15 @@ hipError_t launch_walk_files(const WalkArgs& a, hipStream_t s, Profiler* prof, b
         hipLaunchKernelGGL((k_walk_files<false, true>), dim3(a.nunits), dim3(64), L.total, s, a);
     else
         hipLaunchKernelGGL((k_walk_files<false, false>), dim3(a.nunits), dim3(64), L.total, s, a);
+    return hipGetLastError();
+}
+
+hipError_t launch_chunk_write(const WalkUnit* units, const WalkRec* stage, const CxPlan* plan, uint32_t nunits,
+                              uint32_t n, uint64_t nbf, uint64_t ls, sydelta_op* ops, hipStream_t s, Profiler* prof) {
+    if (!nunits) return hipSuccess;
+    if (!units || !stage || !plan || !ops || !n) return hipErrorInvalidValue;
+    ProfScope ps(prof, s, "k_chunk_write");
+    hipLaunchKernelGGL(k_chunk_write, dim3(nunits), dim3(64), 0, s, units, stage, plan, n, nbf, ls, (uint64_t*)ops);
     return hipGetLastError();
 }
 

@@ -310,6 +310,22 @@ struct WalkArgs {
 // walks the others.  The unit table must not be reused for another slim launch.
 constexpr uint32_t kUnitDone = 2;
 hipError_t launch_walk_files(const WalkArgs& a, hipStream_t s, Profiler* prof, bool slim = false);
+// A chunk's op list written on the device (chunk_pipe_finish with SYDELTA_DEVICE_EXPAND): the
+// host chains the units of a part from its copy of their records (a leading literal run cut at
+// the previous unit's exit, a Data op merged into the previous one) and hands each unit a plan;
+// one wave per unit writes the unit's ops from its staged records (generator.rs:10-15's ops: a
+// Copy per block of a copy run) into `ops` (host memory the device can write).
+struct CxPlan {
+    uint64_t first;   // the unit's first op (index into ops)
+    uint64_t ext;     // bytes added to the unit's last op (a Data op: later units' leading Data)
+    uint64_t r0_off;  // flags & 1: record `skip` cut to start here ...
+    uint32_t r0_a;    // ... with this length
+    uint32_t cnt;     // the unit's staged records
+    uint32_t skip;    // leading records not written (cut away, or merged into the previous op)
+    uint32_t flags;
+};
+hipError_t launch_chunk_write(const WalkUnit* units, const WalkRec* stage, const CxPlan* plan, uint32_t nunits,
+                              uint32_t n, uint64_t nbf, uint64_t ls, sydelta_op* ops, hipStream_t s, Profiler* prof);
 // K10's pre-roll of a chunk's aligned misses: every block r in [b0, b1) (relative to kb)
 // whose aligned probe missed (ahit[r] == kNoBlock) is rolled: the first verified hit among
 // the window starts (x, min(x + n, pend)), x = (kb + r) n, replaces the probe's results:

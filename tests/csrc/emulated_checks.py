@@ -759,10 +759,15 @@ def batch_and_chunk_checks():
         exp = O.ops_from_arrays(*C.generate_delta(s2, ew, es, ez, bs))
         npos = L - bs + 1
         nbp = -(-npos // bs)
+        lib.emu_chunk_units.restype = ctypes.c_uint64
         for nch in (1, 2, 3, 8):
-            for probe in ("0", "1", "1p"):  # 1p: the device walk's launches in one sub-range per segment
+            # 1p: the device walk's launches in one sub-range per segment; ...dx: the ops written
+            # by the emulated k_chunk_write (SYDELTA_DEVICE_EXPAND=1)
+            for probe in ("0", "1", "1p", "1dx", "1pdx"):
                 os.environ["SYDELTA_PROBE"] = probe[0]
-                os.environ["SYDELTA_CHUNK_PIPE"] = "3" if probe == "1p" else ""
+                os.environ["SYDELTA_CHUNK_PIPE"] = "3" if probe.startswith("1p") else ""
+                os.environ["SYDELTA_DEVICE_EXPAND"] = "1" if probe.endswith("dx") else "0"
+                cu0 = lib.emu_chunk_units()
                 cuts = sorted(set(int(c) for c in rng.choice(np.arange(1, nbp), nch - 1, replace=False))) if nch > 1 \
                     else []
                 bounds = [0] + [c * bs for c in cuts] + [npos]
@@ -784,11 +789,14 @@ def batch_and_chunk_checks():
                     lib.sydelta_chunk_free(ch)
                     entry = ex.value
                 assert _ops(lib, acc) == exp, ("chunks", bs, nch, probe)
+                if probe != "0":  # the path the ops took
+                    assert (lib.emu_chunk_units() > cu0) == probe.endswith("dx"), ("chunk writes", bs, nch, probe)
                 lib.sydelta_delta_free(acc)
                 n_checks += 1
         lib.sydelta_index_free(ix)
     os.environ.pop("SYDELTA_PROBE", None)
     os.environ.pop("SYDELTA_CHUNK_PIPE", None)
+    os.environ.pop("SYDELTA_DEVICE_EXPAND", None)
     return n_checks
 
 

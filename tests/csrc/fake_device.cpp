@@ -790,6 +790,36 @@ void walk_expand(const ExpandArgs& a, uint64_t u_lo, uint64_t u_hi) {
     }
 }
 
+// k_chunk_write: each unit's records from the plan's `skip`, the cut first record and the
+// last one's extension applied, written as ops from plan.first
+std::atomic<uint64_t> g_chunk_units{0};  // units written (emu_chunk_units)
+hipError_t launch_chunk_write(const WalkUnit* units, const WalkRec* stage, const CxPlan* plan, uint32_t nunits,
+                              uint32_t n, uint64_t nbf, uint64_t ls, sydelta_op* ops, hipStream_t, Profiler*) {
+    EmuTimer emu_t;
+    if (!nunits) return hipSuccess;
+    if (!units || !stage || !plan || !ops || !n) return hipErrorInvalidValue;
+    for (uint32_t u = 0; u < nunits; ++u) {
+        const CxPlan& P = plan[u];
+        const WalkRec* src = stage + units[u].rec_off;
+        sydelta_op* w = ops + P.first;
+        for (uint32_t i = P.skip; i < P.cnt; ++i) {
+            WalkRec x = src[i];
+            if (i == P.skip && (P.flags & 1)) {
+                x.off = P.r0_off;
+                x.a = P.r0_a;
+            }
+            if (!x.kind) {
+                *w++ = sydelta_op{SYDELTA_OP_DATA, 0, x.off, (uint64_t)x.a + (i + 1 == P.cnt ? P.ext : 0)};
+                continue;
+            }
+            for (uint64_t g = x.a, e = g + x.kind; g < e; ++g)
+                *w++ = sydelta_op{SYDELTA_OP_COPY, 0, g * n, g + 1 == nbf ? ls : (uint64_t)n};
+        }
+        ++g_chunk_units;
+    }
+    return hipSuccess;
+}
+
 // K10's pre-roll: each missed aligned block's first hit in (x, min(x + n, pend)), exactly
 hipError_t launch_preroll(const WalkArgs& a, uint32_t* ahit, uint32_t* apw, uint64_t kb, uint64_t b0, uint64_t b1,
                           uint64_t pend, uint64_t len, uint32_t*, unsigned long long*, uint32_t waves,
@@ -918,3 +948,5 @@ hipError_t launch_synth_mutate(uint8_t*, const uint8_t*, uint64_t, uint64_t, uin
 
 // the files the emulated k_walk_expand saw (emulated_checks asserts the device-expand path ran)
 extern "C" uint64_t emu_expand_files() { return sydelta::g_expand_files.load(); }
+// the units the emulated k_chunk_write wrote (emulated_checks asserts the chunk path ran)
+extern "C" uint64_t emu_chunk_units() { return sydelta::g_chunk_units.load(); }

@@ -238,13 +238,15 @@ def _chunk_walk(gpu, src: bytes, basis: bytes, bs: int, bounds):
     return gpu.join_deltas(parts, L, bs)
 
 
+@pytest.mark.parametrize("dx", ["0", "1"])
 @pytest.mark.parametrize("bs", [256, 4096, 8192])
 @pytest.mark.parametrize("nchunks", [1, 3])
-def test_chunk_walk_segments(gpu, oracle_c, monkeypatch, bs, nchunks):
+def test_chunk_walk_segments(gpu, oracle_c, monkeypatch, bs, nchunks, dx):
     """K10 over a chunk's segments (128 blocks each): an early insertion shifts every later
     Copy off the block grid, so each segment boundary is crossed and the segments are walked
     again from the true entries; then a deletion realigns, substitutions and a duplicated
-    run follow.  Equal to the oracle, and to the classifier + host walk."""
+    run follow.  Equal to the oracle, and to the classifier + host walk; the ops written on the
+    host or (dx 1, SYDELTA_DEVICE_EXPAND) by k_chunk_write."""
     rng = random.Random(bs + nchunks)
     nblk = 700
     basis = rng.randbytes(nblk * bs + rng.randint(1, bs - 1))
@@ -262,12 +264,14 @@ def test_chunk_walk_segments(gpu, oracle_c, monkeypatch, bs, nchunks):
     bounds = [0] + [c * bs for c in cuts] + [npos]
     monkeypatch.delenv("SYDELTA_CHUNK_WALK", raising=False)
     monkeypatch.delenv("SYDELTA_PROBE", raising=False)
+    monkeypatch.setenv("SYDELTA_DEVICE_EXPAND", dx)
     gpu.set_profiling(True)
     gpu.profile(reset=True)
     d = _chunk_walk(gpu, src, basis, bs, bounds)
     prof = gpu.profile(reset=True)
     gpu.set_profiling(False)
     assert "k_walk_files" in prof
+    assert ("k_chunk_write" in prof) == (dx == "1"), prof
     exp = _oracle_ops(oracle_c, src, basis, bs)
     assert d.tuples() == exp
     monkeypatch.setenv("SYDELTA_CHUNK_WALK", "0")
@@ -320,14 +324,16 @@ PIPE_KNOBS = [("1", "1", "", ""), ("0", "1", "", ""), ("1", "0", "", ""), ("2", 
               ("1", "1", "64", "8"), ("0", "1", "1024", "")]
 
 
+@pytest.mark.parametrize("dx", ["0", "1"])
 @pytest.mark.parametrize("preroll,slim,seg,seg_last", PIPE_KNOBS)
-def test_chunk_pipeline_two_parts(gpu, oracle_c, monkeypatch, preroll, slim, seg, seg_last):
+def test_chunk_pipeline_two_parts(gpu, oracle_c, monkeypatch, preroll, slim, seg, seg_last, dx):
     """A chunk large enough for the two-part pipeline (>= 512 segments: 70 % / 30 %, the last
     part re-cut into shorter segments, the parts' walks on two streams), with insertions and
     deletions that shift the data across segment and part boundaries (re-walk rounds), a
     duplicated run and substitutions: equal to the oracle and to the classifier path, under
     every pre-roll / slim-walk / segment-size setting, each of which must launch the kernels
-    it names."""
+    it names; the ops written on the host or (dx 1) by k_chunk_write, the re-walked units'
+    by the host after it."""
     rng = random.Random(512)
     bs = 256
     nblk = 600 * 128  # 600 segments of 128 blocks: 19.2 MB
@@ -347,7 +353,7 @@ def test_chunk_pipeline_two_parts(gpu, oracle_c, monkeypatch, preroll, slim, seg
     monkeypatch.delenv("SYDELTA_PROBE", raising=False)
     monkeypatch.delenv("SYDELTA_CHUNK_PIPE", raising=False)
     for k, v in (("SYDELTA_PREROLL", preroll), ("SYDELTA_SLIM_WALK", slim), ("SYDELTA_CHUNK_SEG", seg),
-                 ("SYDELTA_CHUNK_SEG_LAST", seg_last)):
+                 ("SYDELTA_CHUNK_SEG_LAST", seg_last), ("SYDELTA_DEVICE_EXPAND", dx)):
         monkeypatch.setenv(k, v)
     gpu.set_profiling(True)
     gpu.profile(reset=True)
@@ -360,9 +366,10 @@ def test_chunk_pipeline_two_parts(gpu, oracle_c, monkeypatch, preroll, slim, seg
     nparts_pre = {"0": 0, "1": 1, "2": parts}[preroll]
     assert prof.get("k_preroll", {}).get("count", 0) == nparts_pre, prof
     assert prof.get("k_walk_files_slim", {}).get("count", 0) == (nparts_pre if slim == "1" else 0), prof
+    assert ("k_chunk_write" in prof) == (dx == "1"), prof
     exp = _oracle_ops(oracle_c, src, basis, bs)
     assert d.tuples() == exp
-    if preroll == "1" and slim == "1" and not seg:
+    if preroll == "1" and slim == "1" and not seg and dx == "0":
         monkeypatch.setenv("SYDELTA_CHUNK_WALK", "0")
         assert _chunk_walk(gpu, src, basis, bs, [0, npos]).tuples() == exp
 
