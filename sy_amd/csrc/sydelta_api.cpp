@@ -3203,9 +3203,12 @@ int copy_heavy(sydelta_index* ix, const uint8_t* d_src, uint64_t len, hipStream_
         sc.bytes = need + need / 4;
     }
     uint8_t* D = (uint8_t*)sc.p;
+    // both samples' results come back after one synchronization: h1 | h2 | the jobs' staging
     PinnedHits& pin = thread_probe_pin();
-    if (int r = pinned_at_least(pin, std::max<size_t>(4 * np1, 4 * np2) + 256)) return r;
-    ProbeJob* jobs = (ProbeJob*)(pin.p + al(std::max<size_t>(4 * np1, 4 * np2)));  // the uploads' staging
+    if (int r = pinned_at_least(pin, al(4 * np1) + al(4 * np2) + 256)) return r;
+    uint32_t* h1 = (uint32_t*)pin.p;
+    uint32_t* h2 = (uint32_t*)(pin.p + al(4 * np1));
+    ProbeJob* jobs = (ProbeJob*)(pin.p + al(4 * np1) + al(4 * np2));
     jobs[0] = ProbeJob{0, 0, 0, 0, 0};
     jobs[1] = ProbeJob{0, r0, 0, 0, 0};
     HIP_TRY(hipMemcpyAsync(D + o_jobs, jobs, 2 * sizeof(ProbeJob), hipMemcpyHostToDevice, s));
@@ -3213,16 +3216,9 @@ int copy_heavy(sydelta_index* ix, const uint8_t* d_src, uint64_t len, hipStream_
     const bool fast = ((uintptr_t)d_src & 15) == 0;
     HIP_TRY(launch_probe(d_src, (const ProbeJob*)(D + o_jobs), 1, np1, S, (uint32_t)n, fast, ix->ix,
                          (uint32_t*)(D + o_pw1), (uint64_t*)(D + o_pst1), (uint32_t*)(D + o_out1), s, prof));
-    uint32_t* h = (uint32_t*)pin.p;
-    HIP_TRY(hipMemcpyAsync(h, D + o_out1, 4 * np1, hipMemcpyDeviceToHost, s));
-    HIP_TRY(hipStreamSynchronize(s));
-    uint64_t hits = 0;
-    for (uint64_t i = 0; i < np1; ++i) hits += h[i] != kNoBlk;
-    if (hits * 8 >= np1) {
-        *heavy = true;
-        return SYDELTA_OK;
-    }
+    HIP_TRY(hipMemcpyAsync(h1, D + o_out1, 4 * np1, hipMemcpyDeviceToHost, s));
     // the shifted sample: 256 consecutive aligned windows, each miss rolled for its first hit
+    // (queued with the first: one round trip for both)
     uint32_t* d_out2 = (uint32_t*)(D + o_out2);
     uint32_t* d_pw2 = (uint32_t*)(D + o_pw2);
     HIP_TRY(launch_probe(d_src, (const ProbeJob*)(D + o_jobs) + 1, 1, np2, 1, (uint32_t)n, fast, ix->ix, d_pw2,
@@ -3245,10 +3241,16 @@ int copy_heavy(sydelta_index* ix, const uint8_t* d_src, uint64_t len, hipStream_
     if (ix->fblk[1] < kPreMark)
         HIP_TRY(launch_preroll(a, d_out2, d_pw2, r0, 0, np2, npos, len, (uint32_t*)(D + o_list),
                                (unsigned long long*)(D + o_cnt), (uint32_t)np2, np2, s, prof));
-    HIP_TRY(hipMemcpyAsync(h, d_out2, 4 * np2, hipMemcpyDeviceToHost, s));
+    HIP_TRY(hipMemcpyAsync(h2, d_out2, 4 * np2, hipMemcpyDeviceToHost, s));
     HIP_TRY(hipStreamSynchronize(s));
+    uint64_t hits = 0;
+    for (uint64_t i = 0; i < np1; ++i) hits += h1[i] != kNoBlk;
+    if (hits * 8 >= np1) {
+        *heavy = true;
+        return SYDELTA_OK;
+    }
     hits = 0;
-    for (uint64_t i = 0; i < np2; ++i) hits += h[i] != kNoBlk && h[i] != kPreNone;
+    for (uint64_t i = 0; i < np2; ++i) hits += h2[i] != kNoBlk && h2[i] != kPreNone;
     *heavy = hits * 4 >= np2;
     return SYDELTA_OK;
 }
@@ -3282,6 +3284,24 @@ extern "C" int sydelta_match_device(sydelta_index* idx, const uint8_t* d_src, ui
             HIP_TRY(hipEventRecord(idx->rib_ev, s));
             idx->rib_built = true;
             idx->rib_stream = s;
+        }
+    }
+    // the scan's extras (level-1 Bloom, fat table: scan_index) on the ribbon's stream, beside
+    // the copy-heavy sample below, so that a literal-heavy source's scan finds them built (a
+    // copy-heavy one has spent ~0.06 ms of a few CUs)
+    if (idx->nfiles == 1 && s == idx->stream && npos_all) {
+        std::lock_guard<std::mutex> lk(idx->build_mu);
+        if (idx->extras_deferred && !idx->deferred) {
+            const hipStream_t sx = thread_walk_stream(idx->device, 2);
+            if (sx) {
+                HIP_TRY(index_wait(idx, sx));
+                CallProf cp;
+                HIP_TRY(launch_index_extras(idx->d_weak, idx->ix, sx, cp.get()));
+                if (!idx->extras_ev) HIP_TRY(hipEventCreateWithFlags(&idx->extras_ev, hipEventDisableTiming));
+                HIP_TRY(hipEventRecord(idx->extras_ev, sx));
+                idx->extras_deferred = false;
+                idx->extras_stream = sx;
+            }
         }
     }
     // a copy-heavy source is walked by K10 as one chunk (generator.rs:116-221 on the device);
