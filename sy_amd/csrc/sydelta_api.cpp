@@ -1200,9 +1200,14 @@ static int index_create_impl(int device, const uint32_t* weak, const uint64_t* s
         x->deferred = nfiles >= 2 && block_size % 64 == 0 && block_size >= 256 && block_size <= kWalkMaxN &&
                       max_nblk <= kSelfIxMaxBlocks && !ix.l1;
         x->extras_deferred = nfiles == 1 && ix.l1 != nullptr;
+        if (!x->deferred) {
+            CallProf cp;
+            HIP_TRY(launch_index_build(x->d_weak, x->d_strong, ix, sb, cp.get(), !x->extras_deferred));
+        }
+        HIP_TRY(hipEventRecord(x->ready, sb));
         // the ribbon level-1 of a whole-file scan as large as the basis (scan_index), from the
-        // signature's weak values on a stream of its own: beside the index build, before the
-        // match call is made (SYDELTA_EARLY_RIBBON: 2 here, 1 at the match call, 0 after the
+        // signature's weak values on a stream of its own: beside the index build (queued after
+        // it, the first to be needed), before the match call is made (SYDELTA_EARLY_RIBBON: 2 here, 1 at the match call, 0 after the
         // index, as in round 5).  A match that never scans has spent ~0.2 ms of a few CUs.
         if (nfiles == 1 && nblocks && early_ribbon_mode() == 2 &&
             (x->rib_mode == 2 || (x->rib_mode == 1 && nblocks * block_size >= kRibMinScan))) {
@@ -1216,11 +1221,6 @@ static int index_create_impl(int device, const uint32_t* weak, const uint64_t* s
             x->rib_built = true;
             x->rib_stream = sr;
         }
-        if (!x->deferred) {
-            CallProf cp;
-            HIP_TRY(launch_index_build(x->d_weak, x->d_strong, ix, sb, cp.get(), !x->extras_deferred));
-        }
-        HIP_TRY(hipEventRecord(x->ready, sb));
         *out = x.release();
         return SYDELTA_OK;
     }
