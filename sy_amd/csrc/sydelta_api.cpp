@@ -816,8 +816,8 @@ static void index_release(sydelta_index* x) {
     if (x->rib_ev && x->rib_stream && x->rib_stream != x->stream) (void)hipStreamWaitEvent(x->stream, x->rib_ev, 0);
     if (x->extras_ev && x->extras_stream && x->extras_stream != x->stream)
         (void)hipStreamWaitEvent(x->stream, x->extras_ev, 0);
-    if (x->rib_ev) (void)hipEventDestroy(x->rib_ev);
-    if (x->extras_ev) (void)hipEventDestroy(x->extras_ev);
+    give_event(x->device, x->rib_ev);  // (pooled: a wait queued on an event holds its record)
+    give_event(x->device, x->extras_ev);
     // the build has uploaded the file tables from `stage` (done long before, as a rule)
     if (x->ready) (void)hipEventSynchronize(x->ready);
     give_mapped(x->stage, kStage);
@@ -1216,7 +1216,7 @@ static int index_create_impl(int device, const uint32_t* weak, const uint64_t* s
             HIP_TRY(stream_after(sr, s, device));
             CallProf cp;
             HIP_TRY(launch_ribbon_build(ix, sr, cp.get(), x->d_weak, nblocks));
-            HIP_TRY(hipEventCreateWithFlags(&x->rib_ev, hipEventDisableTiming));
+            if (!(x->rib_ev = take_event(device))) return fail(SYDELTA_E_OOM, "no event for the ribbon");
             HIP_TRY(hipEventRecord(x->rib_ev, sr));
             x->rib_built = true;
             x->rib_stream = sr;
@@ -1236,8 +1236,14 @@ static int index_create_impl(int device, const uint32_t* weak, const uint64_t* s
 extern "C" int sydelta_index_create(int device, const uint32_t* weak, const uint64_t* strong, uint64_t nblocks,
                                     uint64_t block_size, uint64_t last_size, int arrays_on_device, void* stream,
                                     sydelta_index** out) try {
+    static const bool host_timing = getenv("SYDELTA_HOST_TIMING") != nullptr;
+    const auto t0 = std::chrono::steady_clock::now();
     const uint64_t last = nblocks ? last_size : 0;
-    return index_create_impl(device, weak, strong, &nblocks, &last, 1, block_size, arrays_on_device, stream, out);
+    const int r = index_create_impl(device, weak, strong, &nblocks, &last, 1, block_size, arrays_on_device, stream, out);
+    if (host_timing)
+        fprintf(stderr, "sydelta index create: %.3f ms (host)\n",
+                std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count());
+    return r;
 } catch (...) {
     return sydelta::host_exception();
 }
@@ -1844,7 +1850,7 @@ static hipError_t scan_index(sydelta_index* x, uint64_t tot_pos, hipStream_t s, 
         if (x->extras_deferred) {
             if (hipError_t e = launch_index_extras(x->d_weak, x->ix, s, prof)) return e;
             if (!x->extras_ev)
-                if (hipError_t e = hipEventCreateWithFlags(&x->extras_ev, hipEventDisableTiming)) return e;
+                if (!(x->extras_ev = take_event(x->device))) return hipErrorOutOfMemory;
             if (hipError_t e = hipEventRecord(x->extras_ev, s)) return e;
             x->extras_deferred = false;
             x->extras_stream = s;
@@ -1858,7 +1864,7 @@ static hipError_t scan_index(sydelta_index* x, uint64_t tot_pos, hipStream_t s, 
         if (!x->rib_built) {
             if (hipError_t e = launch_ribbon_build(x->ix, s, prof)) return e;
             if (!x->rib_ev) {
-                if (hipError_t e = hipEventCreateWithFlags(&x->rib_ev, hipEventDisableTiming)) return e;
+                if (!(x->rib_ev = take_event(x->device))) return hipErrorOutOfMemory;
             }
             if (hipError_t e = hipEventRecord(x->rib_ev, s)) return e;
             x->rib_built = true;
@@ -3280,7 +3286,7 @@ extern "C" int sydelta_match_device(sydelta_index* idx, const uint8_t* d_src, ui
         if (!idx->rib_built) {
             CallProf cp;
             HIP_TRY(launch_ribbon_build(idx->ix, s, cp.get(), idx->d_weak, idx->fblk[1]));
-            if (!idx->rib_ev) HIP_TRY(hipEventCreateWithFlags(&idx->rib_ev, hipEventDisableTiming));
+            if (!idx->rib_ev && !(idx->rib_ev = take_event(idx->device))) return fail(SYDELTA_E_OOM, "no event");
             HIP_TRY(hipEventRecord(idx->rib_ev, s));
             idx->rib_built = true;
             idx->rib_stream = s;
@@ -3297,7 +3303,8 @@ extern "C" int sydelta_match_device(sydelta_index* idx, const uint8_t* d_src, ui
                 HIP_TRY(index_wait(idx, sx));
                 CallProf cp;
                 HIP_TRY(launch_index_extras(idx->d_weak, idx->ix, sx, cp.get()));
-                if (!idx->extras_ev) HIP_TRY(hipEventCreateWithFlags(&idx->extras_ev, hipEventDisableTiming));
+                if (!idx->extras_ev && !(idx->extras_ev = take_event(idx->device)))
+                    return fail(SYDELTA_E_OOM, "no event");
                 HIP_TRY(hipEventRecord(idx->extras_ev, sx));
                 idx->extras_deferred = false;
                 idx->extras_stream = sx;
