@@ -4488,10 +4488,15 @@ int chunk_pipe_finish(sydelta_chunk* ch, uint64_t entry, uint64_t* exit_pos, syd
     for (size_t u = u0; u < nu; ++u) cap += 2 * ((units[u].end - units[u].entry) / n) + 8;
     OpVec& ops = d->ops;
     // the ops written on the device (launch_chunk_write) into an op array reserved from a
-    // pinned host-mapped slab, when the host has few threads for them (SYDELTA_DEVICE_EXPAND,
-    // as for batches): the host only chains the units and plans each one's ops
+    // pinned host-mapped slab: every part's when the host has few threads for them
+    // (SYDELTA_DEVICE_EXPAND, as for batches; the host only chains the units and plans each
+    // one's ops), else the last part's -- the pipeline's tail; the others' assembly on the
+    // host hides behind the next part's walk
     const char* dxe = getenv("SYDELTA_DEVICE_EXPAND");
-    const bool want_dev = P.d_units && P.d_stage && ((dxe && *dxe) ? dxe[0] == '1' : asm_threads_env() <= 4);
+    const bool dev_set = dxe && *dxe;
+    const bool dev_all = dev_set ? dxe[0] == '1' : asm_threads_env() <= 4;
+    const bool dev_last = !dev_set && !dev_all && P.ub.size() > 2;
+    const bool want_dev = P.d_units && P.d_stage && (dev_all || dev_last);
     bool cdev = false;
     if (want_dev) {
         if (OpSlab* slab = slab_open(cap * sizeof(sydelta_op))) {
@@ -4707,7 +4712,8 @@ int chunk_pipe_finish(sydelta_chunk* ch, uint64_t entry, uint64_t* exit_pos, syd
         take(a, b);
         size_t e = a;
         while (e < b && joins(e, e == u0 ? entry : out[e - 1].exit)) ++e;
-        if (int r = cdev ? plan_part(a, e) : assemble(a, e)) return r;
+        const bool part_dev = cdev && (dev_all || j + 2 == P.ub.size());
+        if (int r = part_dev ? plan_part(a, e) : assemble(a, e)) return r;
         if (e < b) stop = e;
     }
     int rounds = 0;

@@ -762,11 +762,12 @@ def batch_and_chunk_checks():
         lib.emu_chunk_units.restype = ctypes.c_uint64
         for nch in (1, 2, 3, 8):
             # 1p: the device walk's launches in one sub-range per segment; ...dx: the ops written
-            # by the emulated k_chunk_write (SYDELTA_DEVICE_EXPAND=1)
-            for probe in ("0", "1", "1p", "1dx", "1pdx"):
+            # by the emulated k_chunk_write (SYDELTA_DEVICE_EXPAND=1); 1pa: the default with this
+            # host's threads (> 4): the last part's ops written by it, the others' on the host
+            for probe in ("0", "1", "1p", "1dx", "1pdx", "1pa"):
                 os.environ["SYDELTA_PROBE"] = probe[0]
                 os.environ["SYDELTA_CHUNK_PIPE"] = "3" if probe.startswith("1p") else ""
-                os.environ["SYDELTA_DEVICE_EXPAND"] = "1" if probe.endswith("dx") else "0"
+                os.environ["SYDELTA_DEVICE_EXPAND"] = "" if probe == "1pa" else "1" if probe.endswith("dx") else "0"
                 cu0 = lib.emu_chunk_units()
                 cuts = sorted(set(int(c) for c in rng.choice(np.arange(1, nbp), nch - 1, replace=False))) if nch > 1 \
                     else []
@@ -789,7 +790,7 @@ def batch_and_chunk_checks():
                     lib.sydelta_chunk_free(ch)
                     entry = ex.value
                 assert _ops(lib, acc) == exp, ("chunks", bs, nch, probe)
-                if probe != "0":  # the path the ops took
+                if probe not in ("0", "1pa"):  # the path the ops took (1pa: as the re-walks leave it)
                     assert (lib.emu_chunk_units() > cu0) == probe.endswith("dx"), ("chunk writes", bs, nch, probe)
                 lib.sydelta_delta_free(acc)
                 n_checks += 1
