@@ -4487,15 +4487,16 @@ int chunk_pipe_finish(sydelta_chunk* ch, uint64_t entry, uint64_t* exit_pos, syd
     uint64_t cap = 0;  // ops per unit: at most a Copy per block, a Data op before each, a tail Copy
     for (size_t u = u0; u < nu; ++u) cap += 2 * ((units[u].end - units[u].entry) / n) + 8;
     OpVec& ops = d->ops;
-    // the ops written on the device (launch_chunk_write) into an op array reserved from a
-    // pinned host-mapped slab: every part's when the host has few threads for them
-    // (SYDELTA_DEVICE_EXPAND, as for batches; the host only chains the units and plans each
-    // one's ops), else the last part's -- the pipeline's tail; the others' assembly on the
-    // host hides behind the next part's walk
+    // the last part's ops -- the pipeline's tail -- written on the device (launch_chunk_write:
+    // the host only chains the units and plans each one's ops) into an op array reserved from
+    // a pinned host-mapped slab; the other parts' assembled on the host behind the next part's
+    // walk.  Writing every part on the device (SYDELTA_DEVICE_EXPAND=1) lets part 1's PCIe
+    // writes slow part 2's pre-roll: the N = 8 proxy rank at 2 host threads 7.05-7.13 ms
+    // against 6.83-6.84 (`profiles/r06z_*`); 0: every part on the host.
     const char* dxe = getenv("SYDELTA_DEVICE_EXPAND");
     const bool dev_set = dxe && *dxe;
-    const bool dev_all = dev_set ? dxe[0] == '1' : asm_threads_env() <= 4;
-    const bool dev_last = !dev_set && !dev_all && P.ub.size() > 2;
+    const bool dev_all = dev_set && dxe[0] == '1';
+    const bool dev_last = (!dev_set || dxe[0] == '2') && P.ub.size() > 2;
     const bool want_dev = P.d_units && P.d_stage && (dev_all || dev_last);
     bool cdev = false;
     if (want_dev) {
